@@ -1,0 +1,308 @@
+"""FFModel: graph builder + training lifecycle.
+
+Public API follows the reference (C++ ``include/model.h:291-517``, Python
+``python/flexflow/core/flexflow_cbinding.py:564-875``): layer builders return output Tensors,
+``compile(optimizer, loss_type, metrics)`` picks the parallelization strategy (imported
+``.pb``, MCMC search over the MI355X simulator, or data parallel), ``init_layers()`` builds the
+per-rank executor, and the training loop is ``forward(); zero_gradients(); backward(); update()``.
+Unlike the reference, a strategy found by search is *applied* to the run (caveat C6) and
+``--strategy`` is accepted as an alias of ``--import`` (caveat C12).
+"""
+from __future__ import annotations
+
+import sys
+from typing import Dict, List
+
+import numpy as np
+import torch
+
+from flexmi.core.config import FFConfig
+from flexmi.core.loss_metrics import Loss, Metrics
+from flexmi.core.optimizers import AdamOptimizer, Optimizer, SGDOptimizer
+from flexmi.core.tensor import Parameter, Tensor
+from flexmi.core.types import (ActiMode, AggrMode, DataType, LossType, MetricsType, OperatorType,
+                               PoolType)
+from flexmi.ops.conv import BatchNorm, Conv2D, Pool2D
+from flexmi.ops.elementwise import ElementBinary, ElementUnary
+from flexmi.ops.embedding import Embedding
+from flexmi.ops.linear import Linear
+from flexmi.ops.nn_ops import BatchMatmul, DotInteraction, Dropout, Softmax
+from flexmi.ops.tensor_ops import Concat, Flat, Reshape, Reverse, Split, Transpose
+from flexmi.parallel.comm import Comm
+from flexmi.parallel.layout import ParallelConfig
+
+
+class FFModel:
+    def __init__(self, ffconfig: FFConfig = None):
+        self.config = ffconfig or FFConfig()
+        self.layers = []
+        self.input_tensors: List[Tensor] = []
+        self.parameters: List[Parameter] = []
+        self.optimizer: Optimizer = None
+        self.loss_op = None
+        self.metrics_op = None
+        self.label_tensor: Tensor = None
+        self.executor = None
+        self.strategies: Dict[str, ParallelConfig] = {}
+        self._seed = self.config.seed * 1000003 + 12345
+        self._tracing_id = 200
+        self.comm = Comm()
+        self.search_result = None
+
+    def _next_seed(self):
+        self._seed = (self._seed * 1103515245 + 12345) & 0x7FFFFFFF
+        return self._seed
+
+    # ------------------------------------------------------------------ tensors
+    def create_tensor(self, dims, data_type=DataType.DT_FLOAT, create_grad=True, name=None):
+        t = Tensor(dims, data_type, None, 0, create_grad, self, name)
+        self.input_tensors.append(t)
+        return t
+
+    def create_constant(self, dims, value, data_type=DataType.DT_FLOAT):
+        t = self.create_tensor(dims, data_type, False)
+        t.constant_value = value
+        return t
+
+    def _add(self, op):
+        op.layer_id = len(self.layers)
+        self.layers.append(op)
+        self.parameters.extend(op.weights)
+        return op
+
+    def add_layer(self, op_type, name):
+        return None
+
+    # ------------------------------------------------------------------ builders
+    def exp(self, x, name=None):
+        return self._add(ElementUnary(self, OperatorType.OP_EXP, x, name)).outputs[0]
+
+    def relu(self, x, name=None):
+        return self._add(ElementUnary(self, OperatorType.OP_RELU, x, name)).outputs[0]
+
+    def sigmoid(self, x, name=None):
+        return self._add(ElementUnary(self, OperatorType.OP_SIGMOID, x, name)).outputs[0]
+
+    def tanh(self, x, name=None):
+        return self._add(ElementUnary(self, OperatorType.OP_TANH, x, name)).outputs[0]
+
+    def elu(self, x, name=None):
+        return self._add(ElementUnary(self, OperatorType.OP_ELU, x, name)).outputs[0]
+
+    def add(self, x, y, name=None):
+        return self._add(ElementBinary(self, OperatorType.OP_EW_ADD, x, y, name)).outputs[0]
+
+    def subtract(self, x, y, name=None):
+        return self._add(ElementBinary(self, OperatorType.OP_EW_SUB, x, y, name)).outputs[0]
+
+    def multiply(self, x, y, name=None):
+        return self._add(ElementBinary(self, OperatorType.OP_EW_MUL, x, y, name)).outputs[0]
+
+    def divide(self, x, y, name=None):
+        return self._add(ElementBinary(self, OperatorType.OP_EW_DIV, x, y, name)).outputs[0]
+
+    def conv2d(self, input, out_channels, kernel_h, kernel_w, stride_h, stride_w, padding_h, padding_w,
+               activation=ActiMode.AC_MODE_NONE, use_bias=True, shared_op=None, kernel_initializer=None,
+               bias_initializer=None, name=None, groups=1):
+        op = Conv2D(self, input, out_channels, kernel_h, kernel_w, stride_h, stride_w, padding_h, padding_w,
+                    activation, use_bias, kernel_initializer, bias_initializer, name, groups)
+        self._share(op, shared_op)
+        return self._add(op).outputs[0]
+
+    def embedding(self, input, num_entries, out_dim, aggr=AggrMode.AGGR_MODE_SUM, shared_op=None,
+                  kernel_initializer=None, name=None):
+        op = Embedding(self, input, num_entries, out_dim, aggr, kernel_initializer, name)
+        self._share(op, shared_op)
+        return self._add(op).outputs[0]
+
+    def pool2d(self, input, kernel_h, kernel_w, stride_h, stride_w, padding_h, padding_w,
+               pool_type=PoolType.POOL_MAX, activation=ActiMode.AC_MODE_NONE, name=None):
+        return self._add(Pool2D(self, input, kernel_h, kernel_w, stride_h, stride_w, padding_h, padding_w,
+                                pool_type, activation, name)).outputs[0]
+
+    def batch_norm(self, input, relu=True, name=None):
+        return self._add(BatchNorm(self, input, relu, name)).outputs[0]
+
+    def batch_matmul(self, A, B, name=None):
+        return self._add(BatchMatmul(self, A, B, name)).outputs[0]
+
+    def dense(self, input, out_dim, activation=ActiMode.AC_MODE_NONE, use_bias=True, shared_op=None,
+              kernel_initializer=None, bias_initializer=None, name=None):
+        op = Linear(self, input, out_dim, activation, use_bias, kernel_initializer, bias_initializer, name)
+        self._share(op, shared_op)
+        return self._add(op).outputs[0]
+
+    def concat(self, tensors, axis, name=None):
+        return self._add(Concat(self, tensors, axis, name)).outputs[0]
+
+    def split(self, input, sizes, axis, name=None):
+        return list(self._add(Split(self, input, sizes, axis, name)).outputs)
+
+    def flat(self, input, name=None):
+        return self._add(Flat(self, input, name)).outputs[0]
+
+    def softmax(self, input, name=None):
+        return self._add(Softmax(self, input, name)).outputs[0]
+
+    def reshape(self, input, shape, name=None):
+        return self._add(Reshape(self, input, shape, name)).outputs[0]
+
+    def transpose(self, input, perm, name=None):
+        return self._add(Transpose(self, input, perm, name)).outputs[0]
+
+    def reverse(self, input, axis, name=None):
+        return self._add(Reverse(self, input, axis, name)).outputs[0]
+
+    def dropout(self, input, rate, seed=0, name=None):
+        return self._add(Dropout(self, input, rate, seed, name)).outputs[0]
+
+    def dot_interaction(self, bottom, embs, self_interaction=False, name=None):
+        """DLRM ``dot`` feature interaction (fixes reference caveat C3)."""
+        return self._add(DotInteraction(self, bottom, embs, 16, self_interaction, name)).outputs[0]
+
+    def _share(self, op, shared_op):
+        if shared_op is not None:
+            raise NotImplementedError("weight sharing between ops is not supported yet")
+
+    # ------------------------------------------------------------------ lifecycle
+    def set_sgd_optimizer(self, optimizer):
+        self.optimizer = optimizer
+        optimizer.model = self
+
+    def set_adam_optimizer(self, optimizer):
+        self.optimizer = optimizer
+        optimizer.model = self
+
+    def compile(self, optimizer=None, loss_type=None, metrics=None, comp_mode=None):
+        """``FFModel::compile`` (``src/runtime/model.cc:995-1080``)."""
+        if optimizer is not None:
+            self.optimizer = optimizer
+            optimizer.model = self
+        if self.optimizer is None:
+            self.optimizer = SGDOptimizer(self, self.config.learningRate)
+        self.loss_type = LossType(loss_type) if loss_type is not None else LossType.LOSS_MEAN_SQUARED_ERROR_AVG_REDUCE
+        self.loss_op = Loss(self.loss_type)
+        self.metrics_op = Metrics(self.loss_type, metrics or [])
+        # ---- strategy --------------------------------------------------------
+        from flexmi.parallel import strategy as S
+        cfg = self.config
+        path = cfg.import_strategy_file or cfg.strategy_file
+        if path:
+            self.strategies = S.resolve_reference_names(self, S.load_strategies_from_file(path))
+        elif cfg.search_budget > 0:
+            from flexmi.parallel.search import optimize
+            self.search_result = optimize(self, cfg.search_budget, cfg.search_alpha,
+                                          num_devices=max(cfg.world_size, cfg.workersPerNode * cfg.numNodes))
+            self.strategies = dict(self.search_result.best)
+            if cfg.export_strategy_file and cfg.rank == 0:
+                S.save_strategies_to_file(cfg.export_strategy_file, self.strategies)
+        # ---- label tensor (model.cc:1051-1076) -------------------------------
+        final = self.layers[-1].outputs[0]
+        if self.loss_type == LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY:
+            self.label_tensor = Tensor((final.dims[0], 1), DataType.DT_INT32, model=self, name="label")
+        else:
+            self.label_tensor = Tensor(final.dims, DataType.DT_FLOAT, model=self, name="label")
+        return self
+
+    def init_layers(self):
+        """``FFModel::init_layers``: build the per-rank executor (allocation + weight init)."""
+        if self.executor is None:
+            from flexmi.runtime.executor import Executor
+            self.executor = Executor(self, self.strategies, self.comm, self.optimizer, self.loss_type,
+                                     self.metrics_op, self.label_tensor)
+        return self.executor
+
+    def _ex(self):
+        if self.executor is None:
+            self.init_layers()
+        return self.executor
+
+    def forward(self):
+        self._ex().forward()
+
+    def backward(self):
+        self._ex().backward()
+
+    def update(self):
+        self._ex().update()
+
+    def zero_gradients(self):
+        self._ex().zero_gradients()
+
+    def compute_metrics(self):
+        self._ex().compute_metrics()
+
+    def reset_metrics(self):
+        self._ex().reset_metrics()
+
+    def prefetch(self):
+        return None
+
+    def get_perf_metrics(self):
+        return self._ex().perf_metrics()
+
+    def train(self, dataloaders, epochs=1, batch_size=None):
+        """``flexflow_cbinding.py:789-807``."""
+        num_samples = dataloaders[0].get_num_samples()
+        bs = self.config.get_batch_size()
+        ex = self._ex()
+        ex.training = True
+        for epoch in range(epochs):
+            for d in dataloaders:
+                d.reset()
+            self.reset_metrics()
+            for _ in range(int(num_samples // bs)):
+                for d in dataloaders:
+                    d.next_batch(self)
+                self.forward()
+                self.zero_gradients()
+                self.backward()
+                self.update()
+
+    def eval(self, dataloaders):
+        num_samples = dataloaders[0].get_num_samples()
+        bs = self.config.get_batch_size()
+        ex = self._ex()
+        ex.training = False
+        for d in dataloaders:
+            d.reset()
+        self.reset_metrics()
+        for _ in range(int(num_samples // bs)):
+            for d in dataloaders:
+                d.next_batch(self)
+            self.forward()
+            self.compute_metrics()
+        ex.training = True
+
+    # ------------------------------------------------------------------ introspection
+    def get_layers(self):
+        return {i: l for i, l in enumerate(self.layers)}
+
+    def print_layers(self, id=-1):
+        for i, l in enumerate(self.layers):
+            if id == -1 or id == i:
+                ins = ", ".join(str(list(t.dims)) for t in l.inputs)
+                outs = ", ".join(str(list(t.dims)) for t in l.outputs)
+                print(f"layer[{i}] {type(l).__name__} name={l.name} inputs=[{ins}] outputs=[{outs}] "
+                      f"weights={[list(w.dims) for w in l.weights]}")
+
+    def get_layer_by_id(self, layer_id):
+        return self.layers[layer_id]
+
+    def get_layer_by_name(self, layer_name):
+        for l in self.layers:
+            if l.name == layer_name:
+                return l
+        raise KeyError(layer_name)
+
+    def get_tensor_by_id(self, id):
+        return self.parameters[id]
+
+    def get_parameter_by_id(self, id):
+        return self.parameters[id]
+
+    def get_label_tensor(self):
+        return self.label_tensor
+
+    def get_output_tensor(self):
+        return self.layers[-1].outputs[0]

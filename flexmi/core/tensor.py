@@ -1,0 +1,119 @@
+"""Logical tensors and parameters of the model graph.
+
+``struct Tensor`` / ``struct Parameter`` of the reference (``include/model.h:181-231``)
+held Legion regions; here a Tensor is a graph handle and the executor owns the per-rank
+shard buffers (plain HIP allocations through PyTorch-ROCm).  The host-view API
+(``inline_map`` / ``get_array`` / ``attach_numpy_array`` / ``set_weights`` ...) keeps the
+reference's semantics: mapping gathers the full logical tensor to
+the host, unmapping scatters it back to every shard/replica.
+"""
+from __future__ import annotations
+
+import itertools
+
+import numpy as np
+import torch
+
+from .types import DataType, to_torch_dtype
+
+_guid = itertools.count(1000)
+
+
+class Tensor:
+    def __init__(self, dims, data_type=DataType.DT_FLOAT, owner_op=None, owner_idx=0,
+                 create_grad=True, model=None, name=None):
+        self.dims = tuple(int(d) for d in dims)
+        self.data_type = DataType(data_type)
+        self.owner_op = owner_op
+        self.owner_idx = owner_idx
+        self.create_grad = create_grad
+        self.model = model
+        self.guid = next(_guid)
+        self.name = name or f"tensor_{self.guid}"
+        self._mapped = None
+
+    # reference attribute spellings -------------------------------------
+    @property
+    def num_dims(self):
+        return len(self.dims)
+
+    @property
+    def adim(self):
+        """Reference-internal (reversed) dims, ``src/runtime/model.cc:492-495``."""
+        return tuple(reversed(self.dims))
+
+    def volume(self):
+        v = 1
+        for d in self.dims:
+            v *= d
+        return v
+
+    @property
+    def torch_dtype(self):
+        return to_torch_dtype(self.data_type)
+
+    def __repr__(self):
+        return f"Tensor({self.name}, dims={list(self.dims)}, {self.data_type.name})"
+
+    # host-view API -----------------------------------------------------
+    def _executor(self, ffmodel=None):
+        m = ffmodel if ffmodel is not None else self.model
+        ex = getattr(m, "executor", None)
+        assert ex is not None, "model is not compiled/initialised"
+        return ex
+
+    def inline_map(self, ffconfig=None):
+        self._mapped = self._executor().gather_to_host(self)
+        return self._mapped
+
+    def inline_unmap(self, ffconfig=None):
+        if self._mapped is not None:
+            self._executor().scatter_from_host(self, self._mapped)
+        self._mapped = None
+
+    def is_mapped(self):
+        return self._mapped is not None
+
+    def get_array(self, ffconfig=None, data_type=None):
+        if self._mapped is None:
+            self.inline_map(ffconfig)
+        return self._mapped
+
+    def get_flat_array(self, ffconfig=None, data_type=None):
+        return self.get_array(ffconfig, data_type).reshape(-1)
+
+    def attach_numpy_array(self, ffconfig, np_array):
+        """Zero-copy attach of a host array (``src/runtime/model.cc:73-86``)."""
+        arr = np.ascontiguousarray(np_array)
+        assert tuple(arr.shape) == self.dims or arr.size == self.volume(), (arr.shape, self.dims)
+        self._attached = torch.from_numpy(arr.reshape(self.dims))
+        return self._attached
+
+    def detach_numpy_array(self, ffconfig=None):
+        # the loaders keep their own reference; dropping ours mirrors detach_raw_ptr
+        pass
+
+    def get_owner_op(self):
+        return self.owner_op
+
+
+class Parameter(Tensor):
+    """Weight tensor of an op (``include/model.h:219-231``)."""
+
+    def __init__(self, dims, data_type=DataType.DT_FLOAT, owner_op=None, owner_idx=0,
+                 model=None, name=None, initializer=None, sync_type=None):
+        super().__init__(dims, data_type, owner_op, owner_idx, True, model, name)
+        self.initializer = initializer
+        self.pcname = name
+
+    def set_weights(self, ffmodel, np_array):
+        arr = np.asarray(np_array, dtype=np.float32)
+        assert arr.size == self.volume(), (arr.shape, self.dims)
+        self._executor(ffmodel).set_param_full(self, torch.from_numpy(arr.reshape(self.dims).copy()))
+        return True
+
+    def get_weights(self, ffmodel=None):
+        return self._executor(ffmodel).get_param_full(self).numpy()
+
+    def __repr__(self):
+        return f"Parameter({self.name}, dims={list(self.dims)})"

@@ -1,0 +1,8 @@
+"""Operators (graph semantics + parallel layouts + local compute) and HIP kernel bindings."""
+from .base import Op, OpCtx  # noqa
+from .linear import Linear  # noqa
+from .embedding import Embedding  # noqa
+from .elementwise import ElementUnary, ElementBinary  # noqa
+from .tensor_ops import Concat, Split, Flat, Reshape, Transpose, Reverse  # noqa
+from .nn_ops import Softmax, Dropout, BatchMatmul, DotInteraction  # noqa
+from .conv import Conv2D, Pool2D, BatchNorm  # noqa

@@ -1,0 +1,116 @@
+"""Embedding bag (``OP_EMBEDDING``).
+
+Reference: ``src/ops/embedding.cu`` -- lookup ``out[b,:] = Σ_j W[idx[b,j],:]`` (``:173-197``),
+backward = atomicAdd of the output grad into a dense ``W_grad`` (``:199-224``), partitions
+allow only the sample dim or whole-table placement (``:108-135``).  AVG divided inside the bag
+loop (bug, ``:187-195``); here AVG divides once.
+
+MI355X: ``csrc/kernels/embedding.hip`` -- a wave gathers whole rows with 16-B loads and writes
+bf16 activations; the backward never materialises a dense gradient for SGD: indices are radix
+sorted, duplicate rows are summed once per unique row and the rows are updated in place
+(fused sparse SGD).  SOAP: sample split, **column (parameter) split** of the table and
+whole-table placement (``dims=[1,1]``, device k) -- a 100 M-row table fits one MI355X's HBM.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from flexmi.core.initializers import UniformInitializer
+from flexmi.core.types import AggrMode, DataType, OperatorType
+from flexmi.parallel.layout import Layout
+
+from .base import Op, OpCtx, store
+from . import _kernels as K
+
+
+class Embedding(Op):
+    op_type = OperatorType.OP_EMBEDDING
+    name_prefix = "Embed"
+
+    def __init__(self, model, input, num_entries, out_dim, aggr=AggrMode.AGGR_MODE_SUM,
+                 kernel_initializer=None, name=None):
+        super().__init__(model, [input], name)
+        self.num_entries = int(num_entries)
+        self.out_dim = int(out_dim)
+        self.aggr = AggrMode(aggr)
+        if self.name is None:
+            self.name = self.auto_name(f"{num_entries}x{out_dim}")
+        if kernel_initializer is None:
+            r = math.sqrt(1.0 / self.num_entries)
+            kernel_initializer = UniformInitializer(model._next_seed() if model else 0, -r, r)
+        self._add_weight((self.num_entries, self.out_dim), kernel_initializer, "weight")
+        self._finish([(input.dims[0], self.out_dim)])
+        # set by the executor when a fused sparse optimizer applies to this table
+        self.sparse_sgd = False
+
+    def splittable_dims(self):
+        return {0, 1}
+
+    def input_layouts(self, pc):
+        out = Layout.from_pc(self.outputs[0].dims, pc)
+        n, c = out.degrees
+        holders = [tuple(out.holders[i * c + j][0] for j in range(c)) for i in range(n)]
+        return [Layout(self.inputs[0].dims, (n, 1), holders)]
+
+    def weight_layouts(self, pc):
+        out = Layout.from_pc(self.outputs[0].dims, pc)
+        n, c = out.degrees
+        holders = [tuple(out.holders[i * c + j][0] for i in range(n)) for j in range(c)]
+        return [Layout(self.weights[0].dims, (1, c), holders)]
+
+    def needs_input_grad(self, i):
+        return False
+
+    # ---------------------------------------------------------- compute
+    def forward(self, ctx: OpCtx):
+        idx = ctx.inputs[0]
+        w = ctx.weights[0]
+        out = ctx.outputs[0]
+        if ctx.hip:
+            K.embedding_forward(idx, w, out, int(self.aggr))
+        else:
+            bag = idx.shape[1]
+            rows = w.index_select(0, idx.reshape(-1).long()).view(idx.shape[0], bag, -1)
+            r = rows.sum(1)
+            if self.aggr == AggrMode.AGGR_MODE_AVG:
+                r = r / bag
+            out.copy_(r)
+
+    def backward(self, ctx: OpCtx):
+        idx = ctx.inputs[0]
+        dy = ctx.out_grads[0]
+        if self.sparse_sgd:
+            # fused sparse SGD (no dense grad): W[idx] -= lr * dy  (duplicates summed first)
+            if ctx.hip:
+                K.embedding_backward_sgd(idx, dy, ctx.weights[0], ctx.lr, int(self.aggr), ctx.workspace)
+            else:
+                g = dy.float()
+                if self.aggr == AggrMode.AGGR_MODE_AVG:
+                    g = g / idx.shape[1]
+                bag = idx.shape[1]
+                flat = idx.reshape(-1).long()
+                gg = g.repeat_interleave(bag, dim=0)
+                upd = torch.zeros_like(ctx.weights[0])
+                upd.index_add_(0, flat, gg)
+                ctx.weights[0].sub_(ctx.lr.to(upd.dtype) * upd)
+            return
+        dw = ctx.weight_grads[0]
+        if ctx.hip:
+            K.embedding_backward_dense(idx, dy, dw, int(self.aggr))
+        else:
+            g = dy.float()
+            if self.aggr == AggrMode.AGGR_MODE_AVG:
+                g = g / idx.shape[1]
+            bag = idx.shape[1]
+            dw.zero_()
+            dw.index_add_(0, idx.reshape(-1).long(), g.repeat_interleave(bag, dim=0))
+
+    def flops(self, in_shapes, out_shapes):
+        return float(in_shapes[0][0] * in_shapes[0][1] * out_shapes[0][1])
+
+    def bytes_moved(self, in_shapes, out_shapes, elem=2):
+        b, bag = in_shapes[0]
+        d = out_shapes[0][1]
+        return float(b * bag * d * 4 + b * d * elem + b * bag * 8)

@@ -1,0 +1,108 @@
+"""Communication backend: RCCL (torch.distributed ``nccl`` backend on ROCm) over xGMI, or gloo
+on CPU for tests.
+
+The reference had no explicit collectives -- Legion/Realm DMA moved every byte implied by region
+dependences.  flexmi makes each call site an explicit collective:
+
+  * reshard (embedding exchange X3/X4, channel-parallel gather/reduce X5, generic repartition
+    X6, spatial halos) -> ONE ``all_to_all_single`` per plan step, pieces packed per peer;
+  * DP weight-gradient sync (X1/X2) -> bucketed async ``all_reduce`` on contiguous slices of
+    the flat gradient buffer, launched as soon as a bucket's gradients are final (overlapped
+    with the rest of backward: RCCL runs on its own HIP stream);
+  * metrics fold (X8) -> one tiny ``all_reduce``.
+
+Communicators for rank subsets (ops placed on a device subset, channel groups) are created
+once at plan time, in the same order on every rank.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+
+class Comm:
+    def __init__(self, rank=None, world=None, device=None):
+        self.initialized = dist.is_available() and dist.is_initialized()
+        self.rank = dist.get_rank() if self.initialized else 0
+        self.world = dist.get_world_size() if self.initialized else 1
+        if rank is not None:
+            assert rank == self.rank
+        self.device = device
+        self._groups: Dict[tuple, object] = {}
+        self.backend = dist.get_backend() if self.initialized else "none"
+        self.bytes_sent = 0
+        self.calls = 0
+
+    # ------------------------------------------------------------------ groups
+    def group_for(self, ranks: Sequence[int]):
+        """Return a process group for ``ranks``.  MUST be called collectively (same order on
+        every rank) -- the plan compiler walks the graph deterministically."""
+        key = tuple(sorted(set(ranks)))
+        if len(key) == self.world:
+            return None  # world group
+        if key not in self._groups:
+            self._groups[key] = dist.new_group(list(key)) if self.initialized else None
+        return self._groups[key]
+
+    # ------------------------------------------------------------------ collectives
+    def all_to_all(self, send: List[Optional[torch.Tensor]], recv_numel: List[int], dtype, device):
+        """Exchange one flat chunk per peer.  ``send[p]`` is the 1-D chunk for rank p (or None),
+        ``recv_numel[p]`` the number of elements expected from p.  Returns per-peer chunks."""
+        W = self.world
+        if W == 1:
+            return [send[0] if send[0] is not None else torch.empty(0, dtype=dtype, device=device)]
+        in_sizes = [0 if s is None else s.numel() for s in send]
+        parts = [s.reshape(-1).to(dtype) for s in send if s is not None and s.numel() > 0]
+        inp = torch.cat(parts) if parts else torch.empty(0, dtype=dtype, device=device)
+        out = torch.empty(sum(recv_numel), dtype=dtype, device=device)
+        dist.all_to_all_single(out, inp, list(recv_numel), in_sizes)
+        self.calls += 1
+        self.bytes_sent += inp.numel() * inp.element_size()
+        return list(torch.split(out, list(recv_numel)))
+
+    def all_reduce_async(self, t: torch.Tensor, ranks=None):
+        if self.world == 1:
+            return None
+        g = self.group_for(ranks) if ranks is not None else None
+        self.calls += 1
+        return dist.all_reduce(t, group=g, async_op=True)
+
+    def all_reduce(self, t: torch.Tensor, ranks=None):
+        w = self.all_reduce_async(t, ranks)
+        if w is not None:
+            w.wait()
+        return t
+
+    def broadcast(self, t: torch.Tensor, src: int):
+        if self.world > 1:
+            dist.broadcast(t, src)
+        return t
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier()
+
+
+def init_distributed(backend=None, timeout_s=600):
+    """Initialise torch.distributed from the torchrun environment (RANK/WORLD_SIZE/MASTER_*).
+    On MI355X the ``nccl`` backend is RCCL over xGMI; ``gloo`` otherwise."""
+    if dist.is_available() and dist.is_initialized():
+        return Comm()
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws <= 1:
+        return Comm()
+    import datetime
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    kw = {}
+    if backend == "nccl":
+        kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
+    dist.init_process_group(backend, timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return Comm()
