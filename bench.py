@@ -1,0 +1,176 @@
+#!/usr/bin/env python3
+"""flexmi headline benchmark: DLRM training throughput (samples/s) on N MI355X GPUs.
+
+Metric/config from BASELINE.json: "samples/sec DLRM (MLPerf-like) at 1/2/4/8 MI355X" on the
+DLRM MLPerf-like configuration (13 dense + 26 sparse features, Criteo-Terabyte table sizes with
+max-ind-range 40M = 187.8 M rows x 128 fp32 = 96 GB of tables, dot interaction, bottom MLP
+13-512-256-128, top MLP 479-1024-1024-512-256-1, BCE loss, SGD), synthetic data of that shape and
+random-init weights (no dataset/network).  Weak scaling: per-GPU batch fixed (default 8192, i.e.
+the MLPerf global batch 65536 at 8 GPUs); tables are placed whole on GPUs (table-wise model
+parallelism) and the MLPs are data parallel (RCCL all-to-all + bucketed all-reduce).
+
+    python bench.py --gpus N --steps K --warmup W          (N>1 under torch.distributed.run)
+
+Timed region: W untimed steps, then EXACTLY K full training steps (forward, backward, all
+collectives, SGD update of every parameter incl. the sparse embedding rows) bracketed by a
+barrier + device synchronize on both sides; the max over ranks is reported.  Prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "samples/sec DLRM (MLPerf-like) at 1/2/4/8 MI355X; SOAP speedup vs pure DP"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="mlperf", choices=["mlperf", "run_random", "criteo_kaggle", "tiny"])
+    ap.add_argument("--batch-per-gpu", type=int, default=8192)
+    ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture of the step")
+    ap.add_argument("--strategy", default="table", choices=["table", "dp"],
+                    help="table: table-wise embedding placement + DP MLPs (default); dp: pure data parallel")
+    ap.add_argument("--profile", action="store_true")
+    ap.add_argument("--table-scale", type=float, default=1.0, help="debug only: shrink tables (invalid for reporting)")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    from flexmi.parallel.comm import init_distributed
+    comm = init_distributed()
+    rank, world = comm.rank, comm.world
+    if world != a.gpus and rank == 0:
+        print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if torch.cuda.is_available():
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    from flexmi.core import FFConfig, FFModel, SGDOptimizer, LossType, MetricsType
+    from flexmi.models.dlrm import DLRMConfig, build_dlrm, dlrm_strategy, SyntheticDLRMData
+
+    dcfg = DLRMConfig.preset(a.config)
+    if a.table_scale != 1.0:
+        dcfg.embedding_size = [max(2, int(r * a.table_scale)) for r in dcfg.embedding_size]
+    cfg = FFConfig()
+    cfg.batchSize = a.batch_per_gpu * world
+    cfg.profiling = a.profile
+    model = FFModel(cfg)
+    dense_in, sparse, out = build_dlrm(model, dcfg)
+    strategies = {}
+    if world > 1 and a.strategy == "table":
+        strategies = dlrm_strategy(model, world)
+    model.strategies = strategies
+    loss = LossType.LOSS_BINARY_CROSSENTROPY if dcfg.loss == "bce" else LossType.LOSS_MEAN_SQUARED_ERROR_AVG_REDUCE
+    model.compile(SGDOptimizer(model, 0.01), loss, [MetricsType.METRICS_ACCURACY, MetricsType.METRICS_MEAN_SQUARED_ERROR])
+    model.strategies = strategies
+    t0 = time.time()
+    ex = model.init_layers()
+    torch.cuda.synchronize()
+    t_init = time.time() - t0
+    data = SyntheticDLRMData(model, dense_in, sparse, dcfg, num_batches=4, seed=rank)
+
+    use_graph = (not a.no_graph) and world == 1 and torch.cuda.is_available()
+    graphs = None
+
+    def step_eager():
+        data.next_batch()
+        ex.train_step()
+
+    if use_graph:
+        # warm the allocator/kernels, then capture one graph per pooled batch (input copy inside)
+        for _ in range(2):
+            step_eager()
+        torch.cuda.synchronize()
+        graphs = []
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        for k in range(data.nb):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s):
+                    data.i = k
+                    step_eager()
+            graphs.append(g)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        gi = [0]
+
+        def step():
+            graphs[gi[0] % len(graphs)].replay()
+            gi[0] += 1
+    else:
+        step = step_eager
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    ms = el * 1e3 / a.steps
+    gb = cfg.batchSize
+    sps = gb * a.steps / el
+    met = model.get_perf_metrics()
+    if rank == 0:
+        rec = {
+            "metric": METRIC,
+            "value": round(sps, 1),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic",
+            "config": {
+                "model": f"DLRM {dcfg.name} ({'MLPerf-like: 13 dense + 26 sparse, Criteo-TB tables (187.8M rows x 128, fp32), dot interaction' if dcfg.name == 'mlperf' else dcfg.name})",
+                "global_batch": gb,
+                "seq_len": 1,
+                "parallelism": (f"dp{world}" if world == 1 or a.strategy == "dp" else f"table-wise-emb{world}+dp{world}-mlp"),
+                "tables_rows": sum(dcfg.embedding_size),
+                "embedding_dim": dcfg.sparse_feature_size,
+                "mlp_bot": dcfg.mlp_bot,
+                "mlp_top": dcfg.mlp_top,
+                "interaction": dcfg.arch_interaction_op,
+                "hip_graph": bool(use_graph),
+                "init_s": round(t_init, 2),
+                "loss": round(met.get_loss(), 5),
+                "table_scale": a.table_scale,
+            },
+        }
+        print(f"ELAPSED TIME = {el:.4f}s, THROUGHPUT = {sps:.2f} samples/s", file=sys.stderr)
+        if a.profile:
+            ex.timer.print_summary(file=sys.stderr)
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

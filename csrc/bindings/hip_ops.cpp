@@ -1,0 +1,246 @@
+// pybind11 bindings of the flexmi HIP kernels (module flexmi._C).
+// Kernels live in csrc/kernels/*.hip behind extern "C" launchers (compiled with hipcc for gfx950
+// only, no torch headers); this file only unpacks torch tensors into raw pointers and launches on
+// PyTorch's current HIP stream, so kernels compose with torch's caching allocator, RCCL streams
+// and hipGraph capture.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <vector>
+
+extern "C" {
+int fm_gemm(const void* A, long lda, long sA, int a_kcontig, const void* B, long ldb, long sB, int b_kcontig, void* C,
+            long ldc, long sC, int c_fp32, const float* bias, int M, int N, int K, int batch, float alpha, int beta,
+            int act, float* ws, long ws_bytes, int ksplit_req, hipStream_t stream);
+void fm_init_fill(float* out, long rows, long cols, long r0, long c0, long ldg, int kind, unsigned seed, float a, float b,
+                  hipStream_t s);
+void fm_embedding_fwd(const void* idx, int idx64, const float* W, void* out, int out_bf16, long B, int bag, int D, long ldo,
+                      float scale, hipStream_t s);
+void fm_embedding_bwd(const void* idx, int idx64, const void* dy, int dy_bf16, float* W, const float* lr, long B, int bag,
+                      int rows, int D, long ldg, float scale, hipStream_t s);
+void fm_dot_interaction_fwd(const void* const* z, int F, long ldz, void* out, long ldo, long B, int D, int W, int self,
+                            hipStream_t s);
+void fm_dot_interaction_bwd(const void* const* z, int F, long ldz, const void* dout, long ldo, void* const* dz, long lddz,
+                            unsigned acc_mask, long B, int D, int self, hipStream_t s);
+void fm_sgd_update(float* W, const float* G, float* V, unsigned short* Wc, const float* lr, long n, float wd, float mom,
+                   int nesterov, hipStream_t s);
+void fm_adam_update(float* W, const float* G, float* M, float* V, unsigned short* Wc, long n, float alpha_t, float b1,
+                    float b2, float wd, float eps, hipStream_t s);
+void fm_cast_bf16(const float* src, unsigned short* dst, long n, hipStream_t s);
+void fm_loss_fwd_bwd(const void* logits, int logits_bf16, const void* labels, void* grad, int grad_bf16, long B, int C,
+                     int loss_type, float scale, float* acc, int mask, hipStream_t s);
+void fm_unary_forward(int code, const void* x, void* y, long n, int bf16, hipStream_t s);
+void fm_unary_backward(int code, const void* x, const void* y, const void* dy, void* dx, long n, int acc, int bf16,
+                       hipStream_t s);
+void fm_binary_forward(int code, const void* a, const void* b, void* y, long n, int bf16, hipStream_t s);
+void fm_binary_backward(int code, const void* a, const void* b, const void* dy, void* da, void* db, long n, int acca,
+                        int accb, int bf16, hipStream_t s);
+void fm_act_bwd_bias(const void* y, const void* dy, void* dpre, float* db, long B, int N, int act, hipStream_t s);
+void fm_multi_copy2d(int n, const void* const* src, void* const* dst, const long* rows, const long* cols, const long* lds,
+                     const long* ldd, int add_mask, int elem_bytes, hipStream_t s);
+void fm_permute_nd(const void* x, void* y, int nd, const long* out_dims, const long* in_strides_perm, int acc, int bf16,
+                   hipStream_t s);
+void fm_reverse_axis(const void* x, void* y, long outer, long len, long inner, int acc, int bf16, hipStream_t s);
+void fm_softmax_fwd(const void* x, void* y, long rows, int C, int bf16, hipStream_t s);
+void fm_dropout_apply(const void* x, void* y, long n, float rate, unsigned seed, unsigned step, int acc, int bf16,
+                      hipStream_t s);
+}
+
+namespace {
+
+hipStream_t cur() { return at::hip::getCurrentHIPStream().stream(); }
+
+const void* cptr(const c10::optional<torch::Tensor>& t) { return (t.has_value() && t->defined()) ? t->data_ptr() : nullptr; }
+void* mptr(const c10::optional<torch::Tensor>& t) { return (t.has_value() && t->defined()) ? t->data_ptr() : nullptr; }
+
+void check_cuda(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a HIP device tensor");
+}
+
+int is_bf16(const torch::Tensor& t) { return t.scalar_type() == torch::kBFloat16 ? 1 : 0; }
+
+// ----------------------------------------------------------------------------- GEMM
+int gemm(torch::Tensor A, int64_t lda, int64_t sA, bool a_kcontig, torch::Tensor B, int64_t ldb, int64_t sB, bool b_kcontig,
+         torch::Tensor C, int64_t ldc, int64_t sC, c10::optional<torch::Tensor> bias, int64_t M, int64_t N, int64_t K,
+         int64_t batch, double alpha, bool beta, int64_t act, c10::optional<torch::Tensor> ws, int64_t ksplit) {
+  check_cuda(A, "A");
+  check_cuda(B, "B");
+  check_cuda(C, "C");
+  TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "gemm operands must be bf16");
+  TORCH_CHECK(C.scalar_type() == torch::kBFloat16 || C.scalar_type() == torch::kFloat32, "gemm output bf16/fp32");
+  // extent checks (the kernel trusts these): last element of each operand must be inside the storage
+  auto lastA = a_kcontig ? (M - 1) * lda + (K - 1) : (K - 1) * lda + (M - 1);
+  auto lastB = b_kcontig ? (N - 1) * ldb + (K - 1) : (K - 1) * ldb + (N - 1);
+  if (K > 0) {
+    TORCH_CHECK(lastA + (batch - 1) * sA < A.numel(), "gemm: A too small");
+    TORCH_CHECK(lastB + (batch - 1) * sB < B.numel(), "gemm: B too small");
+  }
+  TORCH_CHECK((M - 1) * ldc + (N - 1) + (batch - 1) * sC < C.numel(), "gemm: C too small");
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == torch::kFloat32 && bias->numel() >= N, "bias must be fp32 [N]");
+  }
+  float* w = nullptr;
+  long wsb = 0;
+  if (ws.has_value() && ws->defined()) {
+    w = ws->data_ptr<float>();
+    wsb = ws->numel() * 4;
+  }
+  return fm_gemm(A.data_ptr(), lda, sA, a_kcontig, B.data_ptr(), ldb, sB, b_kcontig, C.data_ptr(), ldc, sC,
+                 C.scalar_type() == torch::kFloat32, bias.has_value() && bias->defined() ? bias->data_ptr<float>() : nullptr,
+                 (int)M, (int)N, (int)K, (int)batch, (float)alpha, beta ? 1 : 0, (int)act, w, wsb, (int)ksplit, cur());
+}
+
+void init_fill(torch::Tensor out, int64_t rows, int64_t cols, int64_t r0, int64_t c0, int64_t ldg, int64_t kind, int64_t seed,
+               double a, double b) {
+  check_cuda(out, "out");
+  TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.is_contiguous(), "init_fill: fp32 contiguous");
+  TORCH_CHECK(out.numel() == rows * cols, "init_fill: shape mismatch");
+  fm_init_fill(out.data_ptr<float>(), rows, cols, r0, c0, ldg, (int)kind, (unsigned)seed, (float)a, (float)b, cur());
+}
+
+void embedding_fwd(torch::Tensor idx, torch::Tensor W, torch::Tensor out, int64_t ldo, double scale) {
+  check_cuda(idx, "idx");
+  check_cuda(W, "W");
+  check_cuda(out, "out");
+  TORCH_CHECK(W.scalar_type() == torch::kFloat32 && W.is_contiguous(), "table must be fp32 contiguous");
+  TORCH_CHECK(idx.dim() == 2 && idx.is_contiguous(), "idx [B, bag] contiguous");
+  long B = idx.size(0);
+  int bag = idx.size(1);
+  int D = W.size(1);
+  TORCH_CHECK(out.numel() >= (B - 1) * ldo + D, "embedding out too small");
+  fm_embedding_fwd(idx.data_ptr(), idx.scalar_type() == torch::kInt64, W.data_ptr<float>(), out.data_ptr(), is_bf16(out), B,
+                   bag, D, ldo, (float)scale, cur());
+}
+
+void embedding_bwd(torch::Tensor idx, torch::Tensor dy, int64_t ldg, torch::Tensor W, c10::optional<torch::Tensor> lr,
+                   double scale) {
+  check_cuda(idx, "idx");
+  check_cuda(dy, "dy");
+  check_cuda(W, "W");
+  TORCH_CHECK(W.scalar_type() == torch::kFloat32 && W.is_contiguous(), "table must be fp32 contiguous");
+  long B = idx.size(0);
+  int bag = idx.size(1);
+  fm_embedding_bwd(idx.data_ptr(), idx.scalar_type() == torch::kInt64, dy.data_ptr(), is_bf16(dy), W.data_ptr<float>(),
+                   lr.has_value() && lr->defined() ? lr->data_ptr<float>() : nullptr, B, bag, (int)W.size(0),
+                   (int)W.size(1), ldg, (float)scale, cur());
+}
+
+void dot_fwd(std::vector<torch::Tensor> zs, int64_t ldz, torch::Tensor out, int64_t ldo, int64_t D, int64_t W, bool self) {
+  TORCH_CHECK(zs.size() >= 1 && zs.size() <= 32, "dot interaction: 1..32 features");
+  std::vector<const void*> p;
+  long B = out.size(0);
+  for (auto& z : zs) {
+    check_cuda(z, "z");
+    TORCH_CHECK(z.scalar_type() == torch::kBFloat16, "dot interaction inputs must be bf16");
+    TORCH_CHECK(z.numel() >= (B - 1) * ldz + D, "dot input too small");
+    p.push_back(z.data_ptr());
+  }
+  TORCH_CHECK(D % 16 == 0 && W % 8 == 0 && ldz % 8 == 0 && ldo % 8 == 0, "dot interaction: D%16, W%8, ld%8");
+  fm_dot_interaction_fwd(p.data(), (int)p.size(), ldz, out.data_ptr(), ldo, B, (int)D, (int)W, self ? 1 : 0, cur());
+}
+
+void dot_bwd(std::vector<torch::Tensor> zs, int64_t ldz, torch::Tensor dout, int64_t ldo,
+             std::vector<c10::optional<torch::Tensor>> dzs, int64_t lddz, int64_t acc_mask, int64_t D, bool self) {
+  std::vector<const void*> p;
+  std::vector<void*> g;
+  for (auto& z : zs) p.push_back(z.data_ptr());
+  for (auto& d : dzs) g.push_back(mptr(d));
+  TORCH_CHECK(D % 8 == 0 && D <= 256, "dot interaction backward: D % 8 == 0, D <= 256");
+  fm_dot_interaction_bwd(p.data(), (int)p.size(), ldz, dout.data_ptr(), ldo, g.data(), lddz, (unsigned)acc_mask,
+                         dout.size(0), (int)D, self ? 1 : 0, cur());
+}
+
+void sgd(torch::Tensor W, torch::Tensor G, c10::optional<torch::Tensor> V, c10::optional<torch::Tensor> Wc, torch::Tensor lr,
+         double wd, double mom, bool nesterov) {
+  TORCH_CHECK(W.numel() == G.numel(), "sgd: size mismatch");
+  fm_sgd_update(W.data_ptr<float>(), G.data_ptr<float>(), (float*)mptr(V), (unsigned short*)mptr(Wc), lr.data_ptr<float>(),
+                W.numel(), (float)wd, (float)mom, nesterov ? 1 : 0, cur());
+}
+
+void adam(torch::Tensor W, torch::Tensor G, torch::Tensor M, torch::Tensor V, c10::optional<torch::Tensor> Wc, double alpha_t,
+          double b1, double b2, double wd, double eps) {
+  fm_adam_update(W.data_ptr<float>(), G.data_ptr<float>(), M.data_ptr<float>(), V.data_ptr<float>(), (unsigned short*)mptr(Wc),
+                 W.numel(), (float)alpha_t, (float)b1, (float)b2, (float)wd, (float)eps, cur());
+}
+
+void cast_bf16(torch::Tensor src, torch::Tensor dst) { fm_cast_bf16(src.data_ptr<float>(), (unsigned short*)dst.data_ptr(), src.numel(), cur()); }
+
+void loss(int64_t loss_type, torch::Tensor logits, torch::Tensor labels, c10::optional<torch::Tensor> grad, double scale,
+          torch::Tensor acc, int64_t mask) {
+  long B = logits.size(0);
+  int C = (int)(logits.numel() / std::max<long>(1, B));
+  int gb = (grad.has_value() && grad->defined()) ? is_bf16(*grad) : 0;
+  fm_loss_fwd_bwd(logits.data_ptr(), is_bf16(logits), labels.data_ptr(), mptr(grad), gb, B, C, (int)loss_type, (float)scale,
+                  acc.data_ptr<float>(), (int)mask, cur());
+}
+
+void unary_fwd(int64_t code, torch::Tensor x, torch::Tensor y) { fm_unary_forward((int)code, x.data_ptr(), y.data_ptr(), x.numel(), is_bf16(x), cur()); }
+void unary_bwd(int64_t code, torch::Tensor x, torch::Tensor y, torch::Tensor dy, torch::Tensor dx, bool acc) {
+  fm_unary_backward((int)code, x.data_ptr(), y.data_ptr(), dy.data_ptr(), dx.data_ptr(), x.numel(), acc, is_bf16(x), cur());
+}
+void binary_fwd(int64_t code, torch::Tensor a, torch::Tensor b, torch::Tensor y) {
+  fm_binary_forward((int)code, a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), is_bf16(a), cur());
+}
+void binary_bwd(int64_t code, torch::Tensor a, torch::Tensor b, torch::Tensor dy, c10::optional<torch::Tensor> da,
+                c10::optional<torch::Tensor> db, bool acca, bool accb) {
+  fm_binary_backward((int)code, a.data_ptr(), b.data_ptr(), dy.data_ptr(), mptr(da), mptr(db), a.numel(), acca, accb, is_bf16(a),
+                     cur());
+}
+void act_bwd_bias(torch::Tensor y, torch::Tensor dy, c10::optional<torch::Tensor> dpre, c10::optional<torch::Tensor> db,
+                  int64_t B, int64_t N, int64_t act) {
+  TORCH_CHECK(y.scalar_type() == torch::kBFloat16 && dy.scalar_type() == torch::kBFloat16, "act_bwd_bias: bf16");
+  fm_act_bwd_bias(y.data_ptr(), dy.data_ptr(), mptr(dpre), (float*)mptr(db), B, (int)N, (int)act, cur());
+}
+void multi_copy(std::vector<torch::Tensor> src, std::vector<int64_t> src_off, std::vector<torch::Tensor> dst,
+                std::vector<int64_t> dst_off, std::vector<int64_t> rows, std::vector<int64_t> cols, std::vector<int64_t> lds,
+                std::vector<int64_t> ldd, int64_t add_mask) {
+  int n = (int)src.size();
+  std::vector<const void*> s(n);
+  std::vector<void*> d(n);
+  std::vector<long> r(n), c(n), a(n), b(n);
+  int eb = src.empty() ? 4 : (int)src[0].element_size();
+  for (int i = 0; i < n; ++i) {
+    s[i] = (const char*)src[i].data_ptr() + src_off[i] * eb;
+    d[i] = (char*)dst[i].data_ptr() + dst_off[i] * eb;
+    r[i] = rows[i]; c[i] = cols[i]; a[i] = lds[i]; b[i] = ldd[i];
+  }
+  fm_multi_copy2d(n, s.data(), d.data(), r.data(), c.data(), a.data(), b.data(), (int)add_mask, eb, cur());
+}
+void permute(torch::Tensor x, torch::Tensor y, std::vector<int64_t> out_dims, std::vector<int64_t> in_strides, bool acc) {
+  std::vector<long> od(out_dims.begin(), out_dims.end()), is(in_strides.begin(), in_strides.end());
+  TORCH_CHECK(od.size() <= 6, "permute: <= 6 dims");
+  fm_permute_nd(x.data_ptr(), y.data_ptr(), (int)od.size(), od.data(), is.data(), acc, is_bf16(x), cur());
+}
+void reverse(torch::Tensor x, torch::Tensor y, int64_t outer, int64_t len, int64_t inner, bool acc) {
+  fm_reverse_axis(x.data_ptr(), y.data_ptr(), outer, len, inner, acc, is_bf16(x), cur());
+}
+void softmax(torch::Tensor x, torch::Tensor y, int64_t rows, int64_t C) { fm_softmax_fwd(x.data_ptr(), y.data_ptr(), rows, (int)C, is_bf16(x), cur()); }
+void dropout(torch::Tensor x, torch::Tensor y, double rate, int64_t seed, int64_t step, bool acc) {
+  fm_dropout_apply(x.data_ptr(), y.data_ptr(), x.numel(), (float)rate, (unsigned)seed, (unsigned)step, acc, is_bf16(x), cur());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "flexmi HIP/CDNA4 kernels (gfx950)";
+  m.def("gemm", &gemm);
+  m.def("init_fill", &init_fill);
+  m.def("embedding_fwd", &embedding_fwd);
+  m.def("embedding_bwd", &embedding_bwd);
+  m.def("dot_fwd", &dot_fwd);
+  m.def("dot_bwd", &dot_bwd);
+  m.def("sgd", &sgd);
+  m.def("adam", &adam);
+  m.def("cast_bf16", &cast_bf16);
+  m.def("loss", &loss);
+  m.def("unary_fwd", &unary_fwd);
+  m.def("unary_bwd", &unary_bwd);
+  m.def("binary_fwd", &binary_fwd);
+  m.def("binary_bwd", &binary_bwd);
+  m.def("act_bwd_bias", &act_bwd_bias);
+  m.def("multi_copy", &multi_copy);
+  m.def("permute", &permute);
+  m.def("reverse", &reverse);
+  m.def("softmax", &softmax);
+  m.def("dropout", &dropout);
+  m.attr("arch") = "gfx950";
+}

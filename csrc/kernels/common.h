@@ -1,0 +1,78 @@
+// Common helpers for flexmi CDNA4 (gfx950) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define FM_HOST_DEVICE __host__ __device__ __forceinline__
+#define FM_DEVICE __device__ __forceinline__
+
+typedef short bf16x4_t __attribute__((ext_vector_type(4)));
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8v_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+// bf16 <-> f32 (round-to-nearest-even via the compiler's cast: keeps NaNs, emits v_cvt_pk_bf16_f32)
+FM_DEVICE float bf2f(unsigned short v) { return __uint_as_float(((unsigned)v) << 16); }
+FM_DEVICE unsigned short f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return *reinterpret_cast<unsigned short*>(&b);
+}
+
+// element loads/stores generic over float / bf16 storage
+template <typename T> FM_DEVICE float ld(const T* p);
+template <> FM_DEVICE float ld<float>(const float* p) { return *p; }
+template <> FM_DEVICE float ld<unsigned short>(const unsigned short* p) { return bf2f(*p); }
+template <typename T> FM_DEVICE void st(T* p, float v);
+template <> FM_DEVICE void st<float>(float* p, float v) { *p = v; }
+template <> FM_DEVICE void st<unsigned short>(unsigned short* p, float v) { *p = f2bf(v); }
+
+// activations (ActiMode values of include/ffconst.h)
+enum { ACT_NONE = 10, ACT_RELU = 11, ACT_SIGMOID = 12, ACT_TANH = 13 };
+
+FM_DEVICE float act_fwd(int act, float x) {
+  if (act == ACT_RELU) return x > 0.f ? x : 0.f;
+  if (act == ACT_SIGMOID) return 1.f / (1.f + __expf(-x));
+  if (act == ACT_TANH) return tanhf(x);
+  return x;
+}
+// derivative expressed through the activation OUTPUT y
+FM_DEVICE float act_bwd(int act, float y, float dy) {
+  if (act == ACT_RELU) return y > 0.f ? dy : 0.f;
+  if (act == ACT_SIGMOID) return dy * y * (1.f - y);
+  if (act == ACT_TANH) return dy * (1.f - y * y);
+  return dy;
+}
+
+FM_DEVICE float wave_reduce_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+FM_DEVICE float wave_reduce_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// grid sizing for memory-bound kernels: ~8 blocks per CU on 256 CUs, grid-stride beyond
+static inline int fm_grid(long long n, int block = 256, int cap = 2048) {
+  long long g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+// order this wave's LDS writes before its later LDS reads (cross-lane) -- compiler + hw fence
+#define FM_WAVE_LDS_SYNC() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+
+#define FM_CHECK(x)                                                                   \
+  do {                                                                                \
+    hipError_t e__ = (x);                                                             \
+    if (e__ != hipSuccess) {                                                          \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e__), __FILE__, __LINE__); \
+    }                                                                                 \
+  } while (0)

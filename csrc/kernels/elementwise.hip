@@ -1,0 +1,317 @@
+// Element-wise, data-movement and normalisation kernels:
+//   unary fwd/bwd      (src/ops/element_unary.cu: cuDNN activations + exp kernel :283-404)
+//   binary fwd/bwd     (src/ops/element_binary.cu: cuDNN OpTensor; DIV asserted there, C9 -- works here)
+//   act-bwd + bias-grad column reduction for Linear (src/ops/linear.cu:583-627 reluBackward /
+//                       sigmoid_backward + cublasSgemv db) fused in one pass
+//   multi-copy         (concat/split fwd+bwd: copy_with_stride / add_with_stride, cuda_helper.cu:70-104;
+//                       all pieces of an op in ONE launch from a descriptor table)
+//   permute / reverse  (transpose.cu:135-159, reverse.cu:126-144)
+//   softmax            (softmax.cu cuDNN softmax; wave per row)
+//   dropout            (dropout.cu cuDNN; counter-based mask regenerated in backward: no mask buffer)
+// Storage type T is bf16 (unsigned short) or fp32, selected at launch.
+#include "common.h"
+
+namespace {
+
+// ---------------------------------------------------------------- unary
+FM_DEVICE float un_f(int code, float x) {
+  switch (code) {
+    case 0: return x > 0.f ? x : 0.f;
+    case 1: return 1.f / (1.f + __expf(-x));
+    case 2: return tanhf(x);
+    case 3: return x > 0.f ? x : (__expf(x) - 1.f);
+    default: return __expf(x);
+  }
+}
+FM_DEVICE float un_b(int code, float x, float y, float dy) {
+  switch (code) {
+    case 0: return x > 0.f ? dy : 0.f;
+    case 1: return dy * y * (1.f - y);
+    case 2: return dy * (1.f - y * y);
+    case 3: return x > 0.f ? dy : dy * (y + 1.f);
+    default: return dy * y;
+  }
+}
+
+template <typename T>
+__global__ void fm_unary_fwd(int code, const T* __restrict__ x, T* __restrict__ y, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    st<T>(y + i, un_f(code, ld<T>(x + i)));
+}
+template <typename T>
+__global__ void fm_unary_bwd(int code, const T* __restrict__ x, const T* __restrict__ y, const T* __restrict__ dy,
+                             T* __restrict__ dx, long n, int acc) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float g = un_b(code, ld<T>(x + i), ld<T>(y + i), ld<T>(dy + i));
+    if (acc) g += ld<T>(dx + i);
+    st<T>(dx + i, g);
+  }
+}
+
+// ---------------------------------------------------------------- binary
+template <typename T>
+__global__ void fm_binary_fwd(int code, const T* __restrict__ a, const T* __restrict__ b, T* __restrict__ y, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float u = ld<T>(a + i), v = ld<T>(b + i);
+    float r = code == 0 ? u + v : code == 1 ? u - v : code == 2 ? u * v : u / v;
+    st<T>(y + i, r);
+  }
+}
+template <typename T>
+__global__ void fm_binary_bwd(int code, const T* __restrict__ a, const T* __restrict__ b, const T* __restrict__ dy,
+                              T* __restrict__ da, T* __restrict__ db, long n, int acca, int accb) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float g = ld<T>(dy + i);
+    float u = ld<T>(a + i), v = ld<T>(b + i);
+    float ga, gb;
+    if (code == 0) { ga = g; gb = g; }
+    else if (code == 1) { ga = g; gb = -g; }
+    else if (code == 2) { ga = g * v; gb = g * u; }
+    else { ga = g / v; gb = -g * u / (v * v); }
+    if (da) st<T>(da + i, ga + (acca ? ld<T>(da + i) : 0.f));
+    if (db) st<T>(db + i, gb + (accb ? ld<T>(db + i) : 0.f));
+  }
+}
+
+// ---------------------------------------------------------------- act bwd + bias grad
+// dpre[b][n] = act'(y) * dy ; db[n] += sum_b dpre[b][n]   (4 columns per thread, 64 rows per block-row)
+template <int ROWS>
+__global__ void fm_act_bwd_colsum(const unsigned short* __restrict__ y, const unsigned short* __restrict__ dy,
+                                  unsigned short* __restrict__ dpre, float* __restrict__ db, long B, int N, int act) {
+  const int c4 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const long r0 = (long)blockIdx.y * ROWS;
+  if (c4 >= N) return;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  const bool vec = (N % 4 == 0);
+  for (long r = r0; r < min(B, r0 + ROWS); ++r) {
+    const long o = r * N + c4;
+    if (vec) {
+      bf16x4_t yy = *reinterpret_cast<const bf16x4_t*>(y + o);
+      bf16x4_t gg = *reinterpret_cast<const bf16x4_t*>(dy + o);
+      float g0 = act_bwd(act, bf2f(yy[0]), bf2f(gg[0]));
+      float g1 = act_bwd(act, bf2f(yy[1]), bf2f(gg[1]));
+      float g2 = act_bwd(act, bf2f(yy[2]), bf2f(gg[2]));
+      float g3 = act_bwd(act, bf2f(yy[3]), bf2f(gg[3]));
+      if (dpre) {
+        bf16x4_t out;
+        out[0] = (short)f2bf(g0); out[1] = (short)f2bf(g1); out[2] = (short)f2bf(g2); out[3] = (short)f2bf(g3);
+        *reinterpret_cast<bf16x4_t*>(dpre + o) = out;
+      }
+      s0 += g0; s1 += g1; s2 += g2; s3 += g3;
+    } else {
+      for (int j = 0; j < 4 && c4 + j < N; ++j) {
+        float g = act_bwd(act, bf2f(y[o + j]), bf2f(dy[o + j]));
+        if (dpre) dpre[o + j] = f2bf(g);
+        (j == 0 ? s0 : j == 1 ? s1 : j == 2 ? s2 : s3) += g;
+      }
+    }
+  }
+  if (db) {
+    atomicAdd(db + c4, s0);
+    if (c4 + 1 < N) atomicAdd(db + c4 + 1, s1);
+    if (c4 + 2 < N) atomicAdd(db + c4 + 2, s2);
+    if (c4 + 3 < N) atomicAdd(db + c4 + 3, s3);
+  }
+}
+
+// ---------------------------------------------------------------- multi 2-D copy
+struct CopyDesc {
+  const void* src;
+  void* dst;
+  long rows, cols, lds, ldd;
+};
+constexpr int MAXC = 16;
+struct CopyTab {
+  CopyDesc d[MAXC];
+  int n;
+  int add;  // bitmask: accumulate into dst
+};
+
+template <typename T>
+__global__ void fm_multi_copy(CopyTab t) {
+  const CopyDesc& d = t.d[blockIdx.y];
+  const int add = (t.add >> blockIdx.y) & 1;
+  const long total = d.rows * d.cols;
+  const T* s = reinterpret_cast<const T*>(d.src);
+  T* o = reinterpret_cast<T*>(d.dst);
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    long r = e / d.cols, c = e % d.cols;
+    float v = ld<T>(s + r * d.lds + c);
+    if (add) v += ld<T>(o + r * d.ldd + c);
+    st<T>(o + r * d.ldd + c, v);
+  }
+}
+
+// ---------------------------------------------------------------- permute (N-D <= 6)
+struct PermArgs {
+  long out_dims[6];
+  long in_strides_perm[6];  // stride in the input of output dim i
+  int nd;
+  int acc;
+};
+template <typename T>
+__global__ void fm_permute(const T* __restrict__ x, T* __restrict__ y, long n, PermArgs a) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    long rem = e, off = 0;
+    for (int i = a.nd - 1; i >= 0; --i) {
+      long c = rem % a.out_dims[i];
+      rem /= a.out_dims[i];
+      off += c * a.in_strides_perm[i];
+    }
+    float v = ld<T>(x + off);
+    if (a.acc) v += ld<T>(y + e);
+    st<T>(y + e, v);
+  }
+}
+
+template <typename T>
+__global__ void fm_reverse(const T* __restrict__ x, T* __restrict__ y, long outer, long len, long inner, int acc) {
+  const long n = outer * len * inner;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    long i = e % inner, t = e / inner;
+    long l = t % len, o = t / len;
+    float v = ld<T>(x + (o * len + (len - 1 - l)) * inner + i);
+    if (acc) v += ld<T>(y + e);
+    st<T>(y + e, v);
+  }
+}
+
+// ---------------------------------------------------------------- softmax (wave per row)
+template <typename T>
+__global__ void fm_softmax(const T* __restrict__ x, T* __restrict__ y, long rows, int C) {
+  const int lane = threadIdx.x & 63;
+  const long waves = (long)gridDim.x * (blockDim.x >> 6);
+  for (long r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < rows; r += waves) {
+    const T* xr = x + r * C;
+    float m = -3.4e38f;
+    for (int c = lane; c < C; c += 64) m = fmaxf(m, ld<T>(xr + c));
+    m = wave_reduce_max(m);
+    float s = 0.f;
+    for (int c = lane; c < C; c += 64) s += __expf(ld<T>(xr + c) - m);
+    s = wave_reduce_sum(s);
+    const float inv = 1.f / s;
+    for (int c = lane; c < C; c += 64) st<T>(y + r * C + c, __expf(ld<T>(xr + c) - m) * inv);
+  }
+}
+
+// ---------------------------------------------------------------- dropout (counter-based mask)
+FM_DEVICE unsigned mix32(unsigned x) {
+  x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
+  return x;
+}
+template <typename T>
+__global__ void fm_dropout(const T* __restrict__ x, T* __restrict__ y, long n, float rate, unsigned seed, unsigned step,
+                           int acc) {
+  const float keep = 1.f / (1.f - rate);
+  const unsigned thr = (unsigned)(rate * 4294967295.0);
+  const unsigned s2 = mix32(seed ^ mix32(step + 0x9E3779B9u));
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    unsigned h = mix32((unsigned)e ^ mix32(s2 ^ (unsigned)(e >> 32)));
+    float v = (h >= thr) ? ld<T>(x + e) * keep : 0.f;
+    if (acc) v += ld<T>(y + e);
+    st<T>(y + e, v);
+  }
+}
+
+}  // namespace
+
+#define FM_DISPATCH_T(bf16, KERNEL, ...)                                   \
+  do {                                                                      \
+    if (bf16) hipLaunchKernelGGL((KERNEL<unsigned short>), __VA_ARGS__);    \
+    else hipLaunchKernelGGL((KERNEL<float>), __VA_ARGS__);                  \
+  } while (0)
+
+extern "C" void fm_unary_forward(int code, const void* x, void* y, long n, int bf16, hipStream_t s) {
+  if (n <= 0) return;
+  if (bf16) hipLaunchKernelGGL((fm_unary_fwd<unsigned short>), dim3(fm_grid(n)), dim3(256), 0, s, code, (const unsigned short*)x, (unsigned short*)y, n);
+  else hipLaunchKernelGGL((fm_unary_fwd<float>), dim3(fm_grid(n)), dim3(256), 0, s, code, (const float*)x, (float*)y, n);
+}
+
+extern "C" void fm_unary_backward(int code, const void* x, const void* y, const void* dy, void* dx, long n, int acc, int bf16,
+                                  hipStream_t s) {
+  if (n <= 0) return;
+  if (bf16) hipLaunchKernelGGL((fm_unary_bwd<unsigned short>), dim3(fm_grid(n)), dim3(256), 0, s, code, (const unsigned short*)x,
+                               (const unsigned short*)y, (const unsigned short*)dy, (unsigned short*)dx, n, acc);
+  else hipLaunchKernelGGL((fm_unary_bwd<float>), dim3(fm_grid(n)), dim3(256), 0, s, code, (const float*)x, (const float*)y,
+                          (const float*)dy, (float*)dx, n, acc);
+}
+
+extern "C" void fm_binary_forward(int code, const void* a, const void* b, void* y, long n, int bf16, hipStream_t s) {
+  if (n <= 0) return;
+  if (bf16) hipLaunchKernelGGL((fm_binary_fwd<unsigned short>), dim3(fm_grid(n)), dim3(256), 0, s, code, (const unsigned short*)a,
+                               (const unsigned short*)b, (unsigned short*)y, n);
+  else hipLaunchKernelGGL((fm_binary_fwd<float>), dim3(fm_grid(n)), dim3(256), 0, s, code, (const float*)a, (const float*)b, (float*)y, n);
+}
+
+extern "C" void fm_binary_backward(int code, const void* a, const void* b, const void* dy, void* da, void* db, long n, int acca,
+                                   int accb, int bf16, hipStream_t s) {
+  if (n <= 0) return;
+  if (bf16) hipLaunchKernelGGL((fm_binary_bwd<unsigned short>), dim3(fm_grid(n)), dim3(256), 0, s, code, (const unsigned short*)a,
+                               (const unsigned short*)b, (const unsigned short*)dy, (unsigned short*)da, (unsigned short*)db, n, acca, accb);
+  else hipLaunchKernelGGL((fm_binary_bwd<float>), dim3(fm_grid(n)), dim3(256), 0, s, code, (const float*)a, (const float*)b,
+                          (const float*)dy, (float*)da, (float*)db, n, acca, accb);
+}
+
+extern "C" void fm_act_bwd_bias(const void* y, const void* dy, void* dpre, float* db, long B, int N, int act, hipStream_t s) {
+  if (B <= 0 || N <= 0) return;
+  constexpr int ROWS = 64;
+  int threads = 256;
+  dim3 grid((unsigned)((N + 4 * threads - 1) / (4 * threads)), (unsigned)((B + ROWS - 1) / ROWS));
+  hipLaunchKernelGGL((fm_act_bwd_colsum<ROWS>), grid, dim3(threads), 0, s, (const unsigned short*)y,
+                     (const unsigned short*)dy, (unsigned short*)dpre, db, B, N, act);
+}
+
+extern "C" void fm_multi_copy2d(int n, const void* const* src, void* const* dst, const long* rows, const long* cols,
+                                const long* lds, const long* ldd, int add_mask, int elem_bytes, hipStream_t s) {
+  for (int base = 0; base < n; base += MAXC) {
+    CopyTab t;
+    int m = std::min(MAXC, n - base);
+    long maxe = 1;
+    for (int i = 0; i < m; ++i) {
+      t.d[i] = CopyDesc{src[base + i], dst[base + i], rows[base + i], cols[base + i], lds[base + i], ldd[base + i]};
+      maxe = std::max(maxe, rows[base + i] * cols[base + i]);
+    }
+    t.n = m;
+    t.add = (add_mask >> base) & ((1 << m) - 1);
+    dim3 grid(fm_grid(maxe, 256, 1024), m);
+    if (elem_bytes == 2) hipLaunchKernelGGL((fm_multi_copy<unsigned short>), grid, dim3(256), 0, s, t);
+    else hipLaunchKernelGGL((fm_multi_copy<float>), grid, dim3(256), 0, s, t);
+  }
+}
+
+extern "C" void fm_permute_nd(const void* x, void* y, int nd, const long* out_dims, const long* in_strides_perm, int acc,
+                              int bf16, hipStream_t s) {
+  PermArgs a;
+  long n = 1;
+  for (int i = 0; i < nd; ++i) {
+    a.out_dims[i] = out_dims[i];
+    a.in_strides_perm[i] = in_strides_perm[i];
+    n *= out_dims[i];
+  }
+  a.nd = nd;
+  a.acc = acc;
+  if (n <= 0) return;
+  if (bf16) hipLaunchKernelGGL((fm_permute<unsigned short>), dim3(fm_grid(n)), dim3(256), 0, s, (const unsigned short*)x, (unsigned short*)y, n, a);
+  else hipLaunchKernelGGL((fm_permute<float>), dim3(fm_grid(n)), dim3(256), 0, s, (const float*)x, (float*)y, n, a);
+}
+
+extern "C" void fm_reverse_axis(const void* x, void* y, long outer, long len, long inner, int acc, int bf16, hipStream_t s) {
+  long n = outer * len * inner;
+  if (n <= 0) return;
+  if (bf16) hipLaunchKernelGGL((fm_reverse<unsigned short>), dim3(fm_grid(n)), dim3(256), 0, s, (const unsigned short*)x, (unsigned short*)y, outer, len, inner, acc);
+  else hipLaunchKernelGGL((fm_reverse<float>), dim3(fm_grid(n)), dim3(256), 0, s, (const float*)x, (float*)y, outer, len, inner, acc);
+}
+
+extern "C" void fm_softmax_fwd(const void* x, void* y, long rows, int C, int bf16, hipStream_t s) {
+  if (rows <= 0) return;
+  dim3 g((unsigned)std::min<long>((rows + 3) / 4, 4096));
+  if (bf16) hipLaunchKernelGGL((fm_softmax<unsigned short>), g, dim3(256), 0, s, (const unsigned short*)x, (unsigned short*)y, rows, C);
+  else hipLaunchKernelGGL((fm_softmax<float>), g, dim3(256), 0, s, (const float*)x, (float*)y, rows, C);
+}
+
+extern "C" void fm_dropout_apply(const void* x, void* y, long n, float rate, unsigned seed, unsigned step, int acc, int bf16,
+                                 hipStream_t s) {
+  if (n <= 0) return;
+  if (bf16) hipLaunchKernelGGL((fm_dropout<unsigned short>), dim3(fm_grid(n)), dim3(256), 0, s, (const unsigned short*)x, (unsigned short*)y, n, rate, seed, step, acc);
+  else hipLaunchKernelGGL((fm_dropout<float>), dim3(fm_grid(n)), dim3(256), 0, s, (const float*)x, (float*)y, n, rate, seed, step, acc);
+}

@@ -1,0 +1,160 @@
+// DLRM dot feature interaction on MFMA (absent in the reference: caveat C3; the closest reference
+// path is the DotCompressor test model built from concat/reshape/transpose/batch_matmul,
+// src/ops/tests/test_harness.py:96-186, i.e. cuBLAS strided-batched GEMMs + copies).
+//
+// Forward, one wave per sample b:  Z = [x; e_1; ..; e_{F-1}] (F <= 32 rows of D bf16)
+//   G = Z Z^T with v_mfma_f32_32x32x16_bf16: the A and B fragments of a Gram matrix are the SAME
+//   register (lane l holds Z[l&31][k0 + 8(l>>5) .. +7]), D/16 MFMAs per sample;
+//   out[b] = [x | strictly-lower(G) | 0-pad] assembled in LDS and written with 16-B stores.
+// Backward: S = dG + dG^T built in LDS from dOut's packed triangle; dZ = S Z with the same MFMA
+//   (A = S rows via ds_read_b128, B = Z columns via the transposing ds_read_b64_tr_b16);
+//   dZ_0 += dOut[:, :D].  Inputs/grads are pointer tables, so it also reads/writes concat slices.
+#include "common.h"
+
+namespace {
+
+constexpr int MAXF = 32;
+struct PtrTab {
+  const unsigned short* p[MAXF];
+};
+struct MPtrTab {
+  unsigned short* p[MAXF];
+};
+
+typedef __attribute__((address_space(3))) bf16x4_t lds_v4_t;
+
+FM_DEVICE int pair_pos(int i, int j, int self) { return self ? (i * (i + 1) / 2 + j) : (i * (i - 1) / 2 + j); }
+
+__global__ void __launch_bounds__(256) fm_dot_fwd(PtrTab Z, long ldz, unsigned short* __restrict__ out, long ldo,
+                                                 long B, int F, int D, int W, int self) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  unsigned short* row = reinterpret_cast<unsigned short*>(smem) + wave * W;
+  const int waves_total = gridDim.x * (blockDim.x >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  for (long b = blockIdx.x * (blockDim.x >> 6) + wave; b < B; b += waves_total) {
+    f32x16_t acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    const unsigned short* zr = (r < F) ? (Z.p[r] + b * ldz) : nullptr;
+    for (int k0 = 0; k0 < D; k0 += 16) {
+      bf16x8_t f;
+      if (zr) f = *reinterpret_cast<const bf16x8_t*>(zr + k0 + 8 * h);
+      else f = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<bf16x8v_t*>(&f), *reinterpret_cast<bf16x8v_t*>(&f),
+                                                    acc, 0, 0, 0);
+    }
+    // stage x and the padding
+    for (int c = lane; c < D; c += 64) row[c] = Z.p[0][b * ldz + c];
+    const int npairs = self ? F * (F + 1) / 2 : F * (F - 1) / 2;
+    for (int c = D + npairs + lane; c < W; c += 64) row[c] = 0;
+    // scatter the lower triangle: lane holds G[i][j], j = lane&31, i = (q&3) + 8(q>>2) + 4h
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      int i = (q & 3) + 8 * (q >> 2) + 4 * h;
+      int j = r;
+      if (i < F && (self ? j <= i : j < i)) row[D + pair_pos(i, j, self)] = f2bf(acc[q]);
+    }
+    FM_WAVE_LDS_SYNC();
+    // coalesced write of the assembled row
+    unsigned short* o = out + b * ldo;
+    for (int c = lane * 8; c < W; c += 64 * 8) *reinterpret_cast<u32x4_t*>(o + c) = *reinterpret_cast<const u32x4_t*>(row + c);
+    FM_WAVE_LDS_SYNC();
+  }
+}
+
+__global__ void __launch_bounds__(256) fm_dot_bwd(PtrTab Z, long ldz, const unsigned short* __restrict__ dout, long ldo,
+                                                 MPtrTab dZ, long lddz, unsigned acc_mask, long B, int F, int D,
+                                                 int self) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int Dp = (D + 31) & ~31;  // LDS image padded to whole 32-column MFMA tiles
+  const int zbytes = 32 * Dp * 2;
+  char* base = smem + wave * (zbytes + 32 * 32 * 2);
+  unsigned short* zs = reinterpret_cast<unsigned short*>(base);            // [32][D]
+  unsigned short* ss = reinterpret_cast<unsigned short*>(base + zbytes);   // [32][32]
+  const int waves_total = gridDim.x * (blockDim.x >> 6);
+  const int chunks_per_row = Dp / 8;
+  for (long b = blockIdx.x * (blockDim.x >> 6) + wave; b < B; b += waves_total) {
+    // stage Z (rows >= F zero)
+    for (int c = lane; c < 32 * chunks_per_row; c += 64) {
+      int i = c / chunks_per_row, k = (c % chunks_per_row) * 8;
+      u32x4_t v = {0u, 0u, 0u, 0u};
+      if (i < F && k < D) v = *reinterpret_cast<const u32x4_t*>(Z.p[i] + b * ldz + k);
+      *reinterpret_cast<u32x4_t*>(zs + i * Dp + k) = v;
+    }
+    // build S = dG + dG^T (bf16) from the packed triangle
+    const unsigned short* dp = dout + b * ldo + D;
+    for (int e = lane; e < 32 * 32; e += 64) {
+      int i = e >> 5, j = e & 31;
+      float v = 0.f;
+      if (i < F && j < F) {
+        if (i > j) v = bf2f(dp[pair_pos(i, j, self)]);
+        else if (j > i) v = bf2f(dp[pair_pos(j, i, self)]);
+        else if (self) v = 2.f * bf2f(dp[pair_pos(i, i, self)]);
+      }
+      ss[e] = f2bf(v);
+    }
+    FM_WAVE_LDS_SYNC();
+    const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+    for (int nt = 0; nt < Dp / 32; ++nt) {
+      f32x16_t acc;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) acc[t] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(ss + (lane & 31) * 32 + 16 * ks + 8 * (lane >> 5));
+        int krow = 16 * ks + 8 * (g >> 1) + q;
+        int col = 32 * nt + 16 * (g & 1) + 4 * p;
+        bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4_t*)(zs + krow * Dp + col));
+        bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4_t*)(zs + (krow + 4) * Dp + col));
+        bf16x8_t bb;
+        bb.lo = lo;
+        bb.hi = hi;
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<bf16x8v_t*>(&a), *reinterpret_cast<bf16x8v_t*>(&bb),
+                                                      acc, 0, 0, 0);
+      }
+      const int n = 32 * nt + (lane & 31);
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        int i = (t & 3) + 8 * (t >> 2) + 4 * (lane >> 5);
+        if (i < F && n < D && dZ.p[i] != nullptr) {
+          float v = acc[t];
+          if (i == 0) v += bf2f(dout[b * ldo + n]);
+          unsigned short* d = dZ.p[i] + b * lddz + n;
+          if (acc_mask & (1u << i)) v += bf2f(*d);
+          *d = f2bf(v);
+        }
+      }
+    }
+    FM_WAVE_LDS_SYNC();
+  }
+}
+
+}  // namespace
+
+extern "C" void fm_dot_interaction_fwd(const void* const* z, int F, long ldz, void* out, long ldo, long B, int D, int W,
+                                       int self, hipStream_t s) {
+  PtrTab t;
+  for (int i = 0; i < MAXF; ++i) t.p[i] = i < F ? (const unsigned short*)z[i] : nullptr;
+  int waves = 4;
+  long blocks = std::min<long>((B + waves - 1) / waves, 4096);
+  hipLaunchKernelGGL(fm_dot_fwd, dim3((int)blocks), dim3(64 * waves), waves * W * 2, s, t, ldz, (unsigned short*)out,
+                     ldo, B, F, D, W, self);
+}
+
+extern "C" void fm_dot_interaction_bwd(const void* const* z, int F, long ldz, const void* dout, long ldo, void* const* dz,
+                                       long lddz, unsigned acc_mask, long B, int D, int self, hipStream_t s) {
+  PtrTab t;
+  MPtrTab g;
+  for (int i = 0; i < MAXF; ++i) {
+    t.p[i] = i < F ? (const unsigned short*)z[i] : nullptr;
+    g.p[i] = i < F ? (unsigned short*)dz[i] : nullptr;
+  }
+  int waves = 4;
+  long blocks = std::min<long>((B + waves - 1) / waves, 4096);
+  const int Dp = (D + 31) & ~31;
+  size_t lds = waves * (32 * Dp * 2 + 32 * 32 * 2);
+  hipLaunchKernelGGL(fm_dot_bwd, dim3((int)blocks), dim3(64 * waves), lds, s, t, ldz, (const unsigned short*)dout, ldo,
+                     g, lddz, acc_mask, B, F, D, self);
+}

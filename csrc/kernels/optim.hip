@@ -1,0 +1,84 @@
+// Fused optimizer updates over a rank's flat parameter buffer (replaces the per-parameter Legion
+// tasks of src/runtime/optimizer_kernel.cu:23-41 sgd_update and :134-154 adam_update, and the
+// gradient-replica sums of :96-101 / :220-225 which RCCL all-reduce now does).
+// ONE launch updates every parameter shard of the rank: fp32 master weights, optional momentum /
+// Adam state, and the bf16 compute mirror written in the same pass (no separate cast kernel).
+// Vectorised 16-B loads/stores; lr is read from device memory so the step is graph-capturable.
+#include "common.h"
+
+namespace {
+
+__global__ void fm_sgd_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ V,
+                              unsigned short* __restrict__ Wc, const float* __restrict__ lr_p, long n, float wd,
+                              float mom, int nesterov, int vec) {
+  const float lr = lr_p[0];
+  const long n4 = vec ? n / 4 : 0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    f32x4_t w = reinterpret_cast<f32x4_t*>(W)[i];
+    f32x4_t g = reinterpret_cast<const f32x4_t*>(G)[i] + wd * w;
+    if (mom > 0.f) {
+      f32x4_t v = reinterpret_cast<f32x4_t*>(V)[i] * mom + g;
+      reinterpret_cast<f32x4_t*>(V)[i] = v;
+      g = nesterov ? g + mom * v : v;
+    }
+    w -= lr * g;
+    reinterpret_cast<f32x4_t*>(W)[i] = w;
+    if (Wc) {
+      bf16x4_t o;
+      o[0] = (short)f2bf(w[0]); o[1] = (short)f2bf(w[1]); o[2] = (short)f2bf(w[2]); o[3] = (short)f2bf(w[3]);
+      reinterpret_cast<bf16x4_t*>(Wc)[i] = o;
+    }
+  }
+  // tail
+  for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float g = G[i] + wd * W[i];
+    if (mom > 0.f) {
+      float v = V[i] * mom + g;
+      V[i] = v;
+      g = nesterov ? g + mom * v : v;
+    }
+    W[i] -= lr * g;
+    if (Wc) Wc[i] = f2bf(W[i]);
+  }
+}
+
+__global__ void fm_adam_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ M,
+                               float* __restrict__ V, unsigned short* __restrict__ Wc, long n, float alpha_t, float b1,
+                               float b2, float wd, float eps) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float w = W[i];
+    float g = G[i] + wd * w;
+    float m = b1 * M[i] + (1.f - b1) * g;
+    float v = b2 * V[i] + (1.f - b2) * g * g;
+    M[i] = m;
+    V[i] = v;
+    w -= alpha_t * m / (sqrtf(v) + eps);
+    W[i] = w;
+    if (Wc) Wc[i] = f2bf(w);
+  }
+}
+
+__global__ void fm_cast_bf16_kernel(const float* __restrict__ src, unsigned short* __restrict__ dst, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) dst[i] = f2bf(src[i]);
+}
+
+}  // namespace
+
+extern "C" void fm_sgd_update(float* W, const float* G, float* V, unsigned short* Wc, const float* lr, long n, float wd,
+                              float mom, int nesterov, hipStream_t s) {
+  if (n <= 0) return;
+  bool al = ((((uintptr_t)W) | ((uintptr_t)G) | ((uintptr_t)(V ? V : W))) & 15) == 0 && ((((uintptr_t)(Wc ? Wc : (unsigned short*)W)) & 7) == 0);
+  hipLaunchKernelGGL(fm_sgd_kernel, dim3(fm_grid(al ? n / 4 + 1 : n)), dim3(256), 0, s, W, G, V, Wc, lr, n, wd, mom,
+                     nesterov, al ? 1 : 0);
+}
+
+extern "C" void fm_adam_update(float* W, const float* G, float* M, float* V, unsigned short* Wc, long n, float alpha_t,
+                               float b1, float b2, float wd, float eps, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(fm_adam_kernel, dim3(fm_grid(n)), dim3(256), 0, s, W, G, M, V, Wc, n, alpha_t, b1, b2, wd, eps);
+}
+
+extern "C" void fm_cast_bf16(const float* src, unsigned short* dst, long n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(fm_cast_bf16_kernel, dim3(fm_grid(n)), dim3(256), 0, s, src, dst, n);
+}

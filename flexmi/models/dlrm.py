@@ -1,0 +1,208 @@
+"""DLRM (the reference's headline workload, ``examples/cpp/DLRM/dlrm.cc:26-199``).
+
+Graph: dense input -> bottom MLP; every sparse feature -> embedding bag; feature interaction
+(``cat`` as in the reference, or ``dot`` -- the DLRM/MLPerf interaction the reference left as a
+TODO, caveat C3); top MLP ending in a sigmoid; MSE (reference) or BCE (MLPerf) loss; SGD.
+Initialisers follow ``create_mlp``/``create_emb`` (``dlrm.cc:26-47``): MLP weights
+N(0, sqrt(2/(in+out))), biases N(0, sqrt(2/out)), tables U(±sqrt(1/rows)).
+
+Default strategy (``dlrm_strategy``): embedding tables placed whole on GPUs with a greedy
+size/traffic-balanced assignment (the table-wise model parallelism of
+``src/runtime/dlrm_strategy.cc:242-296``) + data-parallel MLPs; the exchange between the
+table-placed embeddings and the sample-parallel interaction is ONE RCCL all-to-all per direction.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import List
+
+import numpy as np
+import torch
+
+from flexmi.core.initializers import NormInitializer, UniformInitializer
+from flexmi.core.types import ActiMode, AggrMode, DataType, LossType, MetricsType
+from flexmi.parallel.layout import ParallelConfig
+
+# Criteo Terabyte feature cardinalities with --max-ind-range=40M (MLPerf DLRM v1 configuration)
+MLPERF_TABLES = [39884406, 39043, 17289, 7420, 20263, 3, 7120, 1543, 63, 38532951, 2953546, 403346, 10, 2208,
+                 11938, 155, 4, 976, 14, 39979771, 25641295, 39664984, 585935, 12972, 108, 36]
+# run_criteo_kaggle.sh:8 (Kaggle cardinalities)
+KAGGLE_TABLES = [1396, 550, 1761917, 507795, 290, 21, 11948, 608, 3, 58176, 5237, 1497287, 3127, 26, 12153, 1068715,
+                 10, 4836, 2085, 4, 1312273, 17, 15, 110946, 91, 72655]
+
+
+@dataclass
+class DLRMConfig:
+    """``struct DLRMConfig`` (``examples/cpp/DLRM/dlrm.h:24-42``) + flexmi knobs."""
+    sparse_feature_size: int = 2
+    embedding_size: List[int] = field(default_factory=lambda: [4])
+    mlp_bot: List[int] = field(default_factory=lambda: [4, 2])
+    mlp_top: List[int] = field(default_factory=lambda: [8, 2])
+    embedding_bag_size: int = 1
+    sigmoid_bot: int = -1
+    sigmoid_top: int = -1
+    loss_threshold: float = 0.0
+    arch_interaction_op: str = "cat"
+    dataset_path: str = ""
+    data_size: int = -1
+    loss: str = "mse"            # mse (reference) | bce (MLPerf)
+    name: str = "custom"
+
+    @staticmethod
+    def preset(name):
+        if name == "run_random":  # examples/cpp/DLRM/run_random.sh:9
+            return DLRMConfig(64, [1000000] * 8, [64, 512, 512, 64], [576, 1024, 1024, 1024, 1], 1, -1, -1, 0.0,
+                              "cat", "", -1, "mse", "run_random")
+        if name == "mlperf":      # MLPerf DLRM (Criteo Terabyte): 13 dense + 26 sparse, dot, d=128
+            return DLRMConfig(128, list(MLPERF_TABLES), [13, 512, 256, 128], [479, 1024, 1024, 512, 256, 1], 1, -1, -1,
+                              0.0, "dot", "", -1, "bce", "mlperf")
+        if name == "criteo_kaggle":  # run_criteo_kaggle.sh
+            return DLRMConfig(16, list(KAGGLE_TABLES), [13, 512, 256, 64, 16], [224, 512, 256, 1], 1, -1, -1, 0.0,
+                              "cat", "", -1, "mse", "criteo_kaggle")
+        if name == "tiny":
+            return DLRMConfig(16, [100, 50, 200, 30], [13, 32, 16], [64, 32, 1], 1, -1, -1, 0.0, "dot", "", -1, "bce", "tiny")
+        raise KeyError(name)
+
+    @staticmethod
+    def parse_args(argv, base=None):
+        """``parse_input_args`` of ``dlrm.cc:201-264`` (same flag spellings)."""
+        c = base or DLRMConfig()
+        i = 1
+        while i < len(argv):
+            a = argv[i]
+            nx = argv[i + 1] if i + 1 < len(argv) else None
+            if a == "--arch-sparse-feature-size":
+                c.sparse_feature_size = int(nx); i += 1
+            elif a == "--arch-embedding-size":
+                c.embedding_size = [int(x) for x in nx.split("-")]; i += 1
+            elif a == "--embedding-bag-size":
+                c.embedding_bag_size = int(nx); i += 1
+            elif a == "--arch-mlp-bot":
+                c.mlp_bot = [int(x) for x in nx.split("-")]; i += 1
+            elif a == "--arch-mlp-top":
+                c.mlp_top = [int(x) for x in nx.split("-")]; i += 1
+            elif a == "--loss-threshold":
+                c.loss_threshold = float(nx); i += 1
+            elif a == "--sigmoid-top":
+                c.sigmoid_top = int(nx); i += 1
+            elif a == "--sigmoid-bot":
+                c.sigmoid_bot = int(nx); i += 1
+            elif a == "--arch-interaction-op":
+                c.arch_interaction_op = nx; i += 1
+            elif a == "--dataset":
+                c.dataset_path = nx; i += 1
+            elif a == "--data-size":
+                c.data_size = int(nx); i += 1
+            elif a == "--dlrm-loss":
+                c.loss = nx; i += 1
+            i += 1
+        return c
+
+
+def create_mlp(model, x, ln, sigmoid_layer, seed_base=0):
+    """``create_mlp`` (``dlrm.cc:26-39``)."""
+    t = x
+    for i in range(len(ln) - 1):
+        std = math.sqrt(2.0 / (ln[i + 1] + ln[i]))
+        winit = NormInitializer(model._next_seed(), 0.0, std)
+        binit = NormInitializer(model._next_seed(), 0.0, math.sqrt(2.0 / ln[i + 1]))
+        act = ActiMode.AC_MODE_SIGMOID if i == sigmoid_layer else ActiMode.AC_MODE_RELU
+        t = model.dense(t, ln[i + 1], act, True, None, winit, binit)
+    return t
+
+
+def create_emb(model, idx, rows, dim, i):
+    r = math.sqrt(1.0 / rows)
+    return model.embedding(idx, rows, dim, AggrMode.AGGR_MODE_SUM, None, UniformInitializer(model._next_seed(), -r, r),
+                           name=f"embedding{i}")
+
+
+def build_dlrm(model, c: DLRMConfig):
+    """Returns (dense_input, sparse_inputs, output).  Dense input is padded to a multiple of 8
+    columns (zeros) so its GEMM uses 16-B vector loads; the padding does not change the model."""
+    B = model.config.batchSize
+    sparse = [model.create_tensor([B, c.embedding_bag_size], DataType.DT_INT64, name=f"sparse{i}")
+              for i in range(len(c.embedding_size))]
+    dense_in = model.create_tensor([B, c.mlp_bot[0]], DataType.DT_FLOAT, name="dense")
+    bot = list(c.mlp_bot)
+    x = create_mlp(model, dense_in, bot, c.sigmoid_bot)
+    ly = [create_emb(model, sparse[i], c.embedding_size[i], c.sparse_feature_size, i) for i in range(len(sparse))]
+    if c.arch_interaction_op == "cat":
+        z = model.concat([x] + ly, 1, name="concat")
+    elif c.arch_interaction_op == "dot":
+        z = model.dot_interaction(x, ly, name="interaction")
+    else:
+        raise ValueError(c.arch_interaction_op)
+    top = [z.dims[1]] + list(c.mlp_top[1:])
+    sig = c.sigmoid_top if c.sigmoid_top >= 0 else len(top) - 2
+    p = create_mlp(model, z, top, sig)
+    return dense_in, sparse, p
+
+
+def dlrm_strategy(model, num_gpus, table_sizes=None):
+    """Table-wise model parallelism for embeddings + DP elsewhere (``dlrm_strategy.cc:242-296``).
+
+    Tables are assigned greedily (largest first) to the GPU with the least load, where load =
+    lookups (batch x dim, identical per table) + bytes/8 GB -- memory balance for 100 M-row
+    tables and lookup balance for the all-to-all.  Returns {op name: ParallelConfig}."""
+    from flexmi.core.types import OperatorType
+    embs = [op for op in model.layers if op.op_type == OperatorType.OP_EMBEDDING]
+    loads = [0.0] * num_gpus
+    counts = [0] * num_gpus
+    order = sorted(range(len(embs)), key=lambda i: -embs[i].num_entries * embs[i].out_dim)
+    place = {}
+    for i in order:
+        e = embs[i]
+        nbytes = e.num_entries * e.out_dim * 4
+        g = min(range(num_gpus), key=lambda k: (counts[k], loads[k]))
+        place[i] = g
+        loads[g] += nbytes
+        counts[g] += 1
+    strat = {}
+    for i, e in enumerate(embs):
+        strat[e.name] = ParallelConfig([1, 1], [place[i]])
+    return strat
+
+
+class SyntheticDLRMData:
+    """Random-data generator mirroring the reference's random mode (``dlrm.cc:355-424``: indices
+    uniform in [0, rows), dense U[0,1), labels {0,1}); pools of batches are generated ONCE on the
+    device (like ``--data-size``) and cycled, so the timed loop measures training, not RNG."""
+
+    def __init__(self, model, dense_in, sparse, cfg: DLRMConfig, num_batches=4, seed=0):
+        self.model = model
+        self.dense_in, self.sparse, self.cfg = dense_in, sparse, cfg
+        self.nb = num_batches
+        ex = model._ex()
+        dev = ex.device
+        g = torch.Generator(device=dev)
+        g.manual_seed(1234 + seed)
+        B = model.config.batchSize
+        self.pools = {}
+        # each rank only materialises the rows of the tensors it holds (home layout)
+        for t, rows in zip(sparse, cfg.embedding_size):
+            buf = ex.local_buffer(t)
+            if buf is None:
+                continue
+            lay = ex.home[t.guid]
+            box = lay.local_box(ex.rank)
+            n = box[0][1] - box[0][0]
+            self.pools[t.guid] = torch.randint(0, rows, (num_batches, n, buf.shape[1]), generator=g, device=dev,
+                                               dtype=buf.dtype)
+        buf = ex.local_buffer(dense_in)
+        if buf is not None:
+            self.pools[dense_in.guid] = torch.rand((num_batches,) + tuple(buf.shape), generator=g, device=dev).to(buf.dtype)
+        lab = model.get_label_tensor()
+        lbuf = ex.local_buffer(lab)
+        if lbuf is not None:
+            self.pools[lab.guid] = torch.randint(0, 2, (num_batches,) + tuple(lbuf.shape), generator=g, device=dev).to(lbuf.dtype)
+        self.i = 0
+
+    def next_batch(self):
+        ex = self.model.executor
+        k = self.i % self.nb
+        for gid, pool in self.pools.items():
+            t = ex.tensors[gid]
+            ex.local_buffer(t).copy_(pool[k], non_blocking=True)
+        self.i += 1

@@ -1,0 +1,240 @@
+"""Numerics of every HIP kernel vs a plain PyTorch fp32 reference of the same op (MI355X only)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def bf(x):
+    return x.to(torch.bfloat16)
+
+
+def rel_err(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-6)).item()
+
+
+@pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 200, 130), (1024, 512, 256), (33, 1, 64), (8192, 64, 16)])
+def test_gemm_orientations(gpu, a_k, b_k, M, N, K):
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(0)
+    A = torch.randn(M, K, device=gpu)
+    B = torch.randn(K, N, device=gpu)
+    Ab = bf(A) if a_k else bf(A.t().contiguous())      # [M,K] or [K,M]
+    Bb = bf(B.t().contiguous()) if b_k else bf(B)      # [N,K] or [K,N]
+    lda = K if a_k else M
+    ldb = K if b_k else N
+    C = torch.empty(M, N, device=gpu, dtype=torch.float32)
+    Kk.gemm(Ab, lda, a_k, Bb, ldb, b_k, C, N, M, N, K)
+    ref = bf(A).float() @ bf(B).float()
+    assert rel_err(C, ref) < 2e-3, (a_k, b_k, M, N, K)
+
+
+def test_gemm_epilogue_bias_relu_bf16_beta(gpu):
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(1)
+    M, N, K = 512, 384, 192
+    A, W = torch.randn(M, K, device=gpu), torch.randn(N, K, device=gpu)
+    b = torch.randn(N, device=gpu)
+    C = torch.randn(M, N, device=gpu).to(torch.bfloat16)
+    C0 = C.float().clone()
+    Kk.gemm(bf(A), K, True, bf(W), K, True, C, N, M, N, K, bias=b, act=11, beta=True)
+    ref = torch.relu(bf(A).float() @ bf(W).float().t() + b) + C0
+    assert rel_err(C, ref) < 1e-2
+
+
+def test_gemm_splitk_and_batch(gpu):
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(2)
+    M, N, K = 64, 128, 4096
+    A, B = torch.randn(K, M, device=gpu), torch.randn(K, N, device=gpu)
+    C = torch.empty(M, N, device=gpu)
+    ks = Kk.gemm(bf(A), M, False, bf(B), N, False, C, N, M, N, K, ksplit=8)
+    assert ks == 8
+    ref = bf(A).float().t() @ bf(B).float()
+    assert rel_err(C, ref) < 2e-3
+    # batched
+    bs = 5
+    X, Y = torch.randn(bs, 40, 72, device=gpu), torch.randn(bs, 72, 24, device=gpu)
+    O = torch.empty(bs, 40, 24, device=gpu, dtype=torch.bfloat16)
+    Kk.bmm(bf(X), bf(Y), O, False, False, False)
+    assert rel_err(O, bf(X).float() @ bf(Y).float()) < 1e-2
+
+
+def test_init_fill_matches_cpu(gpu):
+    from flexmi.core.initializers import NormInitializer, UniformInitializer
+    for init in [UniformInitializer(7, -0.5, 0.5), NormInitializer(9, 0.0, 2.0)]:
+        dims = (300, 40)
+        box = ((100, 220), (8, 40))
+        cpu = torch.empty(120, 32)
+        init.fill(dims, box, cpu)
+        g = torch.empty(120, 32, device=gpu)
+        init.fill(dims, box, g)
+        assert torch.allclose(g.cpu(), cpu, atol=1e-5), type(init)
+
+
+@pytest.mark.parametrize("bag,D,rows", [(1, 128, 100000), (3, 64, 50), (2, 16, 7)])
+def test_embedding_fwd_bwd(gpu, bag, D, rows):
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(3)
+    B = 1000
+    W = torch.randn(rows, D, device=gpu)
+    idx = torch.randint(0, rows, (B, bag), device=gpu)
+    out = torch.empty(B, D, device=gpu, dtype=torch.bfloat16)
+    Kk.embedding_forward(idx, W, out, 21)
+    ref = W[idx].sum(1)
+    assert rel_err(out, ref) < 1e-2
+    # fused sparse SGD
+    dy = torch.randn(B, D, device=gpu).to(torch.bfloat16)
+    lr = torch.tensor([0.1], device=gpu)
+    W2 = W.clone()
+    Kk.embedding_backward_sgd(idx, dy, W2, lr, 21, {})
+    upd = torch.zeros_like(W)
+    upd.index_add_(0, idx.reshape(-1), dy.float().repeat_interleave(bag, 0))
+    assert torch.allclose(W2, W - 0.1 * upd, atol=1e-4)
+    # dense grad
+    dW = torch.empty_like(W)
+    Kk.embedding_backward_dense(idx, dy, dW, 21)
+    assert torch.allclose(dW, upd, atol=1e-3)
+
+
+@pytest.mark.parametrize("F,D,self_i", [(27, 128, False), (9, 64, True), (4, 32, False)])
+def test_dot_interaction(gpu, F, D, self_i):
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(4)
+    B = 300
+    zs = [torch.randn(B, D, device=gpu).to(torch.bfloat16) for _ in range(F)]
+    npairs = F * (F + 1) // 2 if self_i else F * (F - 1) // 2
+    W = ((D + npairs + 15) // 16) * 16
+    y = torch.empty(B, W, device=gpu, dtype=torch.bfloat16)
+    Kk.dot_interaction_forward(zs, y, self_i)
+    Z = torch.stack([z.float() for z in zs], 1)
+    G = Z @ Z.transpose(1, 2)
+    li, lj = [], []
+    for i in range(F):
+        for j in range(i + 1 if self_i else i):
+            li.append(i)
+            lj.append(j)
+    ref = torch.zeros(B, W, device=gpu)
+    ref[:, :D] = Z[:, 0]
+    ref[:, D:D + npairs] = G[:, li, lj]
+    assert rel_err(y, ref) < 1e-2
+    # backward
+    dy = torch.randn(B, W, device=gpu).to(torch.bfloat16)
+    grads = [torch.empty(B, D, device=gpu, dtype=torch.bfloat16) for _ in range(F)]
+    Kk.dot_interaction_backward(zs, dy, grads, [False] * F, self_i)
+    dG = torch.zeros(B, F, F, device=gpu)
+    dG[:, li, lj] = dy[:, D:D + npairs].float()
+    dZ = (dG + dG.transpose(1, 2)) @ Z
+    dZ[:, 0] += dy[:, :D].float()
+    for i in range(F):
+        assert rel_err(grads[i], dZ[:, i]) < 2e-2, i
+
+
+def test_sgd_adam(gpu):
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(5)
+    n = 10007
+    W, G, V = torch.randn(n, device=gpu), torch.randn(n, device=gpu), torch.randn(n, device=gpu)
+    Wc = torch.empty(n, device=gpu, dtype=torch.bfloat16)
+    W0, V0 = W.clone(), V.clone()
+    lr = torch.tensor([0.05], device=gpu)
+    Kk.sgd_update(W, G, V, Wc, lr, 1e-4, 0.9, True)
+    g = G + 1e-4 * W0
+    v = 0.9 * V0 + g
+    g = g + 0.9 * v
+    assert torch.allclose(W, W0 - 0.05 * g, atol=1e-5) and torch.allclose(V, v, atol=1e-5)
+    assert torch.allclose(Wc.float(), W, atol=2e-2)
+    M_, V_ = torch.zeros(n, device=gpu), torch.zeros(n, device=gpu)
+    W1 = W.clone()
+    Kk.adam_update(W, G, M_, V_, None, 0.01, 0.9, 0.999, 0.0, 1e-8)
+    m = 0.1 * G
+    vv = 0.001 * G * G
+    assert torch.allclose(W, W1 - 0.01 * m / (vv.sqrt() + 1e-8), atol=1e-4)
+
+
+@pytest.mark.parametrize("loss,C", [(54, 1), (52, 1), (51, 10), (50, 7)])
+def test_loss_metrics(gpu, loss, C):
+    from flexmi.core.loss_metrics import loss_and_metrics_torch
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(6)
+    B = 777
+    if C == 1:
+        p = torch.rand(B, 1, device=gpu)
+        lab = torch.randint(0, 2, (B, 1), device=gpu).float()
+    else:
+        p = torch.softmax(torch.randn(B, C, device=gpu), -1)
+        if loss == 51:
+            lab = torch.randint(0, C, (B, 1), device=gpu, dtype=torch.int32)
+        else:
+            lab = torch.nn.functional.one_hot(torch.randint(0, C, (B,), device=gpu), C).float()
+    g = torch.empty(B, C, device=gpu)
+    acc = torch.zeros(8, device=gpu)
+    Kk.loss_forward_backward(loss, p, lab, g, 1.0 / B, acc, 63)
+    gr = torch.empty(B, C)
+    accr = torch.zeros(8)
+    loss_and_metrics_torch(loss, p.cpu(), lab.cpu(), gr, 1.0 / B, accr, 63)
+    assert torch.allclose(g.cpu(), gr, atol=1e-6)
+    for s in [0, 1, 4, 6, 7]:
+        assert abs(acc[s].item() - accr[s].item()) <= 1e-3 * max(1.0, abs(accr[s].item())), (s, acc, accr)
+
+
+def test_elementwise_and_movement(gpu):
+    from flexmi.ops import _kernels as Kk
+    from flexmi.ops.elementwise import unary_bwd_torch, unary_fwd_torch
+    torch.manual_seed(7)
+    x = torch.randn(64, 33, device=gpu)
+    for code in range(5):
+        y = torch.empty_like(x)
+        Kk.unary_forward(code, x, y)
+        assert torch.allclose(y, unary_fwd_torch(code, x), atol=1e-5, rtol=1e-4)
+        dy = torch.randn_like(x)
+        dx = torch.empty_like(x)
+        Kk.unary_backward(code, x, y, dy, dx, False)
+        assert torch.allclose(dx, unary_bwd_torch(code, x, y, dy), atol=1e-5, rtol=1e-4)
+    a, b = torch.randn(1000, device=gpu), torch.rand(1000, device=gpu) + 0.5
+    for code, f in enumerate([torch.add, torch.sub, torch.mul, torch.div]):
+        y = torch.empty_like(a)
+        Kk.binary_forward(code, a, b, y)
+        assert torch.allclose(y, f(a, b), atol=1e-5)
+    # concat / split
+    xs = [torch.randn(8, k, 5, device=gpu) for k in (3, 4, 2)]
+    y = torch.empty(8, 9, 5, device=gpu)
+    Kk.concat_forward(xs, y, 1)
+    assert torch.equal(y, torch.cat(xs, 1))
+    gs = [torch.empty_like(t) for t in xs]
+    Kk.concat_backward(y, gs, [False] * 3, 1)
+    for gg, t in zip(gs, xs):
+        assert torch.equal(gg, t)
+    # permute / reverse / softmax
+    t = torch.randn(4, 5, 6, device=gpu)
+    o = torch.empty(6, 4, 5, device=gpu)
+    Kk.permute(t, o, [2, 0, 1], False)
+    assert torch.equal(o, t.permute(2, 0, 1))
+    r = torch.empty_like(t)
+    Kk.reverse(t, r, 1, False)
+    assert torch.equal(r, torch.flip(t, [1]))
+    s = torch.empty(17, 300, device=gpu)
+    xx = torch.randn(17, 300, device=gpu)
+    Kk.softmax_forward(xx, s)
+    assert torch.allclose(s, torch.softmax(xx, -1), atol=1e-6)
+
+
+def test_act_bwd_bias(gpu):
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(8)
+    B, N = 1000, 260
+    y = torch.relu(torch.randn(B, N, device=gpu)).to(torch.bfloat16)
+    dy = torch.randn(B, N, device=gpu).to(torch.bfloat16)
+    dpre = torch.empty(B, N, device=gpu, dtype=torch.bfloat16)
+    db = torch.zeros(N, device=gpu)
+    torch.ops  # noqa
+    Kk.C().act_bwd_bias(y, dy, dpre, db, B, N, 11)
+    ref = dy.float() * (y.float() > 0)
+    assert rel_err(dpre, ref) < 1e-2
+    assert torch.allclose(db, ref.sum(0), atol=1e-2, rtol=1e-3)

@@ -1,0 +1,111 @@
+"""End-to-end training on MI355X (HIP kernels, bf16 compute) vs the fp32 CPU executor."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _mlp(device, B=64):
+    from flexmi.core import FFConfig, FFModel, SGDOptimizer, LossType, MetricsType, ActiMode
+    cfg = FFConfig()
+    cfg.batchSize = B
+    cfg.device = device
+    cfg.compute_dtype = "bf16" if device == "gpu" else "fp32"
+    m = FFModel(cfg)
+    x = m.create_tensor([B, 32])
+    t = m.dense(x, 64, ActiMode.AC_MODE_RELU)
+    t = m.dense(t, 48, ActiMode.AC_MODE_TANH)
+    t = m.dense(t, 10)
+    t = m.softmax(t)
+    m.compile(SGDOptimizer(m, 0.05), LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY,
+              [MetricsType.METRICS_ACCURACY, MetricsType.METRICS_SPARSE_CATEGORICAL_CROSSENTROPY])
+    m.init_layers()
+    return m, x
+
+
+def test_mlp_gpu_matches_cpu(gpu):
+    from flexmi.core import SingleDataLoader
+    rng = np.random.RandomState(0)
+    X = rng.randn(256, 32).astype(np.float32)
+    Y = rng.randint(0, 10, (256, 1)).astype(np.int32)
+    res = {}
+    for dev in ("cpu", "gpu"):
+        m, x = _mlp(dev)
+        dx = SingleDataLoader(m, x, X, 256)
+        dy = SingleDataLoader(m, m.get_label_tensor(), Y, 256)
+        for _ in range(6):
+            dx.next_batch(m)
+            dy.next_batch(m)
+            m.forward()
+            m.zero_gradients()
+            m.backward()
+            m.update()
+        res[dev] = [w.get_weights(m) for w in m.parameters]
+    for a, b in zip(res["cpu"], res["gpu"]):
+        assert np.abs(a - b).max() < 2e-2 * max(1.0, np.abs(a).max())
+
+
+def test_dlrm_tiny_gpu_matches_cpu(gpu):
+    from flexmi.core import FFConfig, FFModel, SGDOptimizer, LossType, MetricsType
+    from flexmi.models.dlrm import DLRMConfig, build_dlrm
+    B = 128
+    rng = np.random.RandomState(1)
+    dcfg = DLRMConfig.preset("tiny")
+    dense = rng.rand(B, 13).astype(np.float32)
+    sp = [rng.randint(0, r, (B, 1)).astype(np.int64) for r in dcfg.embedding_size]
+    lab = rng.randint(0, 2, (B, 1)).astype(np.float32)
+    out = {}
+    for dev in ("cpu", "gpu"):
+        cfg = FFConfig()
+        cfg.batchSize = B
+        cfg.device = dev
+        cfg.compute_dtype = "bf16" if dev == "gpu" else "fp32"
+        m = FFModel(cfg)
+        d, s, p = build_dlrm(m, dcfg)
+        m.compile(SGDOptimizer(m, 0.1), LossType.LOSS_BINARY_CROSSENTROPY, [MetricsType.METRICS_ACCURACY])
+        ex = m.init_layers()
+        for _ in range(4):
+            ex.scatter_from_host(d, dense)
+            for t, a in zip(s, sp):
+                ex.scatter_from_host(t, a)
+            ex.scatter_from_host(m.get_label_tensor(), lab)
+            ex.train_step()
+        out[dev] = ([w.get_weights(m) for w in m.parameters], m.get_perf_metrics().get_loss())
+    for a, b in zip(out["cpu"][0], out["gpu"][0]):
+        assert np.abs(a - b).max() < 3e-2 * max(1.0, np.abs(a).max()), (a.shape,)
+    assert abs(out["cpu"][1] - out["gpu"][1]) < 2e-2
+
+
+def test_hip_graph_capture_matches_eager(gpu):
+    from flexmi.core import FFConfig, FFModel, SGDOptimizer, LossType, MetricsType
+    from flexmi.models.dlrm import DLRMConfig, build_dlrm, SyntheticDLRMData
+    res = []
+    for use_graph in (False, True):
+        cfg = FFConfig()
+        cfg.batchSize = 512
+        m = FFModel(cfg)
+        dcfg = DLRMConfig.preset("tiny")
+        d, s, p = build_dlrm(m, dcfg)
+        m.compile(SGDOptimizer(m, 0.05), LossType.LOSS_BINARY_CROSSENTROPY, [MetricsType.METRICS_ACCURACY])
+        ex = m.init_layers()
+        data = SyntheticDLRMData(m, d, s, dcfg, num_batches=1)
+        data.next_batch()
+        if use_graph:
+            ex.train_step()
+            g = torch.cuda.CUDAGraph()
+            st = torch.cuda.Stream()
+            st.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(st):
+                with torch.cuda.graph(g, stream=st):
+                    ex.train_step()
+            torch.cuda.current_stream().wait_stream(st)
+            for _ in range(3):
+                g.replay()
+        else:
+            for _ in range(4):
+                ex.train_step()
+        torch.cuda.synchronize()
+        res.append([w.get_weights(m) for w in m.parameters])
+    for a, b in zip(*res):
+        assert np.allclose(a, b, atol=1e-5), a.shape
