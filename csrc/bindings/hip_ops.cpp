@@ -17,6 +17,12 @@ void fm_embedding_fwd(const void* idx, int idx64, const float* W, void* out, int
                       float scale, hipStream_t s);
 void fm_embedding_bwd(const void* idx, int idx64, const void* dy, int dy_bf16, float* W, const float* lr, long B, int bag,
                       int rows, int D, long ldg, float scale, hipStream_t s);
+void fm_embedding_fwd_multi(int n, const float* const* W, const void* const* idx, const int* idx64, void* const* out,
+                            const long* ldo, const int* rows, const int* D, const int* bag, const float* scale, int out_bf16,
+                            long B, hipStream_t st);
+void fm_embedding_bwd_multi(int n, float* const* W, const void* const* idx, const int* idx64, const void* const* dy,
+                            const long* ldg, const int* rows, const int* D, const int* bag, const float* scale, int dy_bf16,
+                            const float* lr, long B, hipStream_t st);
 void fm_dot_interaction_fwd(const void* const* z, int F, long ldz, void* out, long ldo, long B, int D, int W, int self,
                             hipStream_t s);
 void fm_dot_interaction_bwd(const void* const* z, int F, long ldz, const void* dout, long ldo, void* const* dz, long lddz,
@@ -124,6 +130,65 @@ void embedding_bwd(torch::Tensor idx, torch::Tensor dy, int64_t ldg, torch::Tens
                    (int)W.size(1), ldg, (float)scale, cur());
 }
 
+struct TabArgs {
+  std::vector<const float*> Wc;
+  std::vector<float*> Wm;
+  std::vector<const void*> idx;
+  std::vector<int> idx64, rows, D, bag;
+  std::vector<void*> act;
+  std::vector<const void*> cact;
+  std::vector<long> ld;
+  std::vector<float> scale;
+  long B = 0;
+};
+
+TabArgs tab_args(const std::vector<torch::Tensor>& W, const std::vector<torch::Tensor>& idx, const std::vector<torch::Tensor>& act,
+                 const std::vector<int64_t>& ld, const std::vector<double>& scale) {
+  TabArgs a;
+  size_t n = W.size();
+  TORCH_CHECK(idx.size() == n && act.size() == n && ld.size() == n && scale.size() == n, "embedding multi: list sizes");
+  for (size_t i = 0; i < n; ++i) {
+    check_cuda(W[i], "W");
+    check_cuda(idx[i], "idx");
+    check_cuda(act[i], "act");
+    TORCH_CHECK(W[i].scalar_type() == torch::kFloat32 && W[i].is_contiguous() && W[i].dim() == 2, "tables fp32 [rows, D]");
+    TORCH_CHECK(idx[i].dim() == 2 && idx[i].is_contiguous(), "idx [B, bag]");
+    long B = idx[i].size(0);
+    if (i == 0) a.B = B;
+    TORCH_CHECK(B == a.B, "embedding multi: same batch");
+    TORCH_CHECK(act[i].numel() >= (B - 1) * ld[i] + W[i].size(1), "embedding act buffer too small");
+    a.Wc.push_back(W[i].data_ptr<float>());
+    a.Wm.push_back(W[i].data_ptr<float>());
+    a.idx.push_back(idx[i].data_ptr());
+    a.idx64.push_back(idx[i].scalar_type() == torch::kInt64);
+    a.rows.push_back((int)W[i].size(0));
+    a.D.push_back((int)W[i].size(1));
+    a.bag.push_back((int)idx[i].size(1));
+    a.act.push_back(act[i].data_ptr());
+    a.cact.push_back(act[i].data_ptr());
+    a.ld.push_back(ld[i]);
+    a.scale.push_back((float)scale[i]);
+  }
+  return a;
+}
+
+void embedding_fwd_multi(std::vector<torch::Tensor> W, std::vector<torch::Tensor> idx, std::vector<torch::Tensor> out,
+                         std::vector<int64_t> ldo, std::vector<double> scale) {
+  if (W.empty()) return;
+  TabArgs a = tab_args(W, idx, out, ldo, scale);
+  fm_embedding_fwd_multi((int)W.size(), a.Wc.data(), a.idx.data(), a.idx64.data(), a.act.data(), a.ld.data(), a.rows.data(),
+                         a.D.data(), a.bag.data(), a.scale.data(), is_bf16(out[0]), a.B, cur());
+}
+
+void embedding_bwd_multi(std::vector<torch::Tensor> W, std::vector<torch::Tensor> idx, std::vector<torch::Tensor> dy,
+                         std::vector<int64_t> ldg, std::vector<double> scale, c10::optional<torch::Tensor> lr) {
+  if (W.empty()) return;
+  TabArgs a = tab_args(W, idx, dy, ldg, scale);
+  fm_embedding_bwd_multi((int)W.size(), a.Wm.data(), a.idx.data(), a.idx64.data(), a.cact.data(), a.ld.data(), a.rows.data(),
+                         a.D.data(), a.bag.data(), a.scale.data(), is_bf16(dy[0]),
+                         lr.has_value() && lr->defined() ? lr->data_ptr<float>() : nullptr, a.B, cur());
+}
+
 void dot_fwd(std::vector<torch::Tensor> zs, int64_t ldz, torch::Tensor out, int64_t ldo, int64_t D, int64_t W, bool self) {
   TORCH_CHECK(zs.size() >= 1 && zs.size() <= 32, "dot interaction: 1..32 features");
   std::vector<const void*> p;
@@ -226,6 +291,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("init_fill", &init_fill);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
+  m.def("embedding_fwd_multi", &embedding_fwd_multi);
+  m.def("embedding_bwd_multi", &embedding_bwd_multi);
   m.def("dot_fwd", &dot_fwd);
   m.def("dot_bwd", &dot_bwd);
   m.def("sgd", &sgd);

@@ -74,43 +74,59 @@ __global__ void fm_binary_bwd(int code, const T* __restrict__ a, const T* __rest
 }
 
 // ---------------------------------------------------------------- act bwd + bias grad
-// dpre[b][n] = act'(y) * dy ; db[n] += sum_b dpre[b][n]   (4 columns per thread, 64 rows per block-row)
+// dpre[b][n] = act'(y) * dy ; db[n] += sum_b dpre[b][n].
+// Block = 4 waves over ONE 512-column strip (lane owns 8 consecutive columns, 16-B loads) and
+// ROWS rows (wave w takes rows w, w+4, ...); partial column sums are reduced across the 4 waves
+// in LDS and each block issues one fp32 atomic per column.
 template <int ROWS>
-__global__ void fm_act_bwd_colsum(const unsigned short* __restrict__ y, const unsigned short* __restrict__ dy,
-                                  unsigned short* __restrict__ dpre, float* __restrict__ db, long B, int N, int act) {
-  const int c4 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+__global__ void __launch_bounds__(256) fm_act_bwd_colsum(const unsigned short* __restrict__ y,
+                                                        const unsigned short* __restrict__ dy,
+                                                        unsigned short* __restrict__ dpre, float* __restrict__ db,
+                                                        long B, int N, int act) {
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c0 = blockIdx.x * 512 + lane * 8;
   const long r0 = (long)blockIdx.y * ROWS;
-  if (c4 >= N) return;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  const bool vec = (N % 4 == 0);
-  for (long r = r0; r < min(B, r0 + ROWS); ++r) {
-    const long o = r * N + c4;
-    if (vec) {
-      bf16x4_t yy = *reinterpret_cast<const bf16x4_t*>(y + o);
-      bf16x4_t gg = *reinterpret_cast<const bf16x4_t*>(dy + o);
-      float g0 = act_bwd(act, bf2f(yy[0]), bf2f(gg[0]));
-      float g1 = act_bwd(act, bf2f(yy[1]), bf2f(gg[1]));
-      float g2 = act_bwd(act, bf2f(yy[2]), bf2f(gg[2]));
-      float g3 = act_bwd(act, bf2f(yy[3]), bf2f(gg[3]));
-      if (dpre) {
-        bf16x4_t out;
-        out[0] = (short)f2bf(g0); out[1] = (short)f2bf(g1); out[2] = (short)f2bf(g2); out[3] = (short)f2bf(g3);
-        *reinterpret_cast<bf16x4_t*>(dpre + o) = out;
-      }
-      s0 += g0; s1 += g1; s2 += g2; s3 += g3;
-    } else {
-      for (int j = 0; j < 4 && c4 + j < N; ++j) {
-        float g = act_bwd(act, bf2f(y[o + j]), bf2f(dy[o + j]));
-        if (dpre) dpre[o + j] = f2bf(g);
-        (j == 0 ? s0 : j == 1 ? s1 : j == 2 ? s2 : s3) += g;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const bool vec = ((N & 7) == 0) && (c0 + 8 <= N);
+  if (c0 < N) {
+    for (int rr = wave; rr < ROWS; rr += 4) {
+      const long r = r0 + rr;
+      if (r >= B) break;
+      const long o = r * N + c0;
+      if (vec) {
+        bf16x8_t yy = *reinterpret_cast<const bf16x8_t*>(y + o);
+        bf16x8_t gg = *reinterpret_cast<const bf16x8_t*>(dy + o);
+        bf16x8_t out;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float g = act_bwd(act, bf2f((unsigned short)yy[j]), bf2f((unsigned short)gg[j]));
+          s[j] += g;
+          out[j] = (short)f2bf(g);
+        }
+        if (dpre) *reinterpret_cast<bf16x8_t*>(dpre + o) = out;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (c0 + j < N) {
+            float g = act_bwd(act, bf2f(y[o + j]), bf2f(dy[o + j]));
+            s[j] += g;
+            if (dpre) dpre[o + j] = f2bf(g);
+          }
+        }
       }
     }
   }
-  if (db) {
-    atomicAdd(db + c4, s0);
-    if (c4 + 1 < N) atomicAdd(db + c4 + 1, s1);
-    if (c4 + 2 < N) atomicAdd(db + c4 + 2, s2);
-    if (c4 + 3 < N) atomicAdd(db + c4 + 3, s3);
+  if (!db) return;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[wave][lane * 8 + j] = s[j];
+  __syncthreads();
+  for (int c = threadIdx.x; c < 512; c += 256) {
+    const int col = blockIdx.x * 512 + c;
+    if (col < N) {
+      float v = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+      atomicAdd(db + col, v);
+    }
   }
 }
 
@@ -134,8 +150,17 @@ __global__ void fm_multi_copy(CopyTab t) {
   const long total = d.rows * d.cols;
   const T* s = reinterpret_cast<const T*>(d.src);
   T* o = reinterpret_cast<T*>(d.dst);
+  const bool small = total < 0x7fffffffL;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    long r = e / d.cols, c = e % d.cols;
+    long r, c;
+    if (small) {  // 32-bit division (64-bit div/mod is a ~100-instruction sequence on gfx950)
+      unsigned ue = (unsigned)e, uc = (unsigned)d.cols;
+      r = ue / uc;
+      c = ue - (unsigned)r * uc;
+    } else {
+      r = e / d.cols;
+      c = e % d.cols;
+    }
     float v = ld<T>(s + r * d.lds + c);
     if (add) v += ld<T>(o + r * d.ldd + c);
     st<T>(o + r * d.ldd + c, v);
@@ -254,10 +279,9 @@ extern "C" void fm_binary_backward(int code, const void* a, const void* b, const
 
 extern "C" void fm_act_bwd_bias(const void* y, const void* dy, void* dpre, float* db, long B, int N, int act, hipStream_t s) {
   if (B <= 0 || N <= 0) return;
-  constexpr int ROWS = 64;
-  int threads = 256;
-  dim3 grid((unsigned)((N + 4 * threads - 1) / (4 * threads)), (unsigned)((B + ROWS - 1) / ROWS));
-  hipLaunchKernelGGL((fm_act_bwd_colsum<ROWS>), grid, dim3(threads), 0, s, (const unsigned short*)y,
+  constexpr int ROWS = 32;
+  dim3 grid((unsigned)((N + 511) / 512), (unsigned)((B + ROWS - 1) / ROWS));
+  hipLaunchKernelGGL((fm_act_bwd_colsum<ROWS>), grid, dim3(256), 0, s, (const unsigned short*)y,
                      (const unsigned short*)dy, (unsigned short*)dpre, db, B, N, act);
 }
 

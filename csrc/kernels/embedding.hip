@@ -1,142 +1,218 @@
-// Embedding-bag kernels (replace src/ops/embedding.cu:173-224 embed_forward / embed_backward).
+// Embedding-bag kernels (replace src/ops/embedding.cu:173-224 embed_forward / embed_backward, which
+// ran one thread per (sample, column) with the bag loop inside and one launch per table).
 //
-// Forward: thread = (sample, 4 consecutive columns); a table row of D fp32 is read by D/4
-// consecutive lanes with 16-B loads (one 512-B row = 32 lanes for D=128), summed over the bag,
-// written as bf16 (or fp32) activations with 8-B / 16-B stores.  Multi-table variant ("TBE")
-// processes every table of an embedding collection in ONE launch from a descriptor array and
-// writes straight into the interaction input buffer [B, F, D] (concat fused away).
+// All kernels take a TABLE DESCRIPTOR ARRAY and process every table of an embedding group in ONE
+// launch (blockIdx.y = table) -- the executor fuses the independent per-table Embedding ops of a
+// DLRM graph (26 ops in the MLPerf config) into one forward and two backward launches.
 //
-// Backward (fused sparse SGD, no dense gradient): W[idx] -= lr * dy.  Large tables: one
-// wave-instruction = 64 consecutive fp32 atomic adds (256 contiguous bytes: full atomic rate on
-// gfx950).  Tiny tables (rows*D fits LDS): block-private LDS accumulation first, then one
-// global atomic per (touched row, column) per block -- avoids the 14x slowdown of many adders on
-// one row.  Dense-gradient variant for replicated (data-parallel) tables.
+// Forward: lane = 4 consecutive columns of one sample (D/4 lanes per row: a 512-B fp32 row of a
+// D=128 table is read by 32 lanes with 16-B loads), sum over the bag, bf16/fp32 output written
+// with 8/16-B stores straight into the consumer's buffer (row stride ldo).  No 64-bit div/mod in
+// the loop (lane->column mapping fixed per block).
+// Backward (fused sparse SGD: W[idx] -= lr*scale*dy; or dense-grad accumulate when lr == null):
+//   * large tables: one wave-instruction = 64 consecutive fp32 atomic adds (256 contiguous bytes:
+//     the full gfx950 atomic rate, MI355X_MICROARCH "Global float atomics");
+//   * tiny tables (rows*D*4 <= 64 KiB): block-private LDS accumulation over a chunk of samples, then
+//     one global atomic per (row, column) per block -- avoids the ~14x slowdown of many adders on
+//     one row (table with 3 rows in the MLPerf set).
 #include "common.h"
+
+#include <algorithm>
+#include <vector>
 
 namespace {
 
-template <typename OutT, typename IdxT>
-__global__ void fm_emb_fwd_kernel(const IdxT* __restrict__ idx, const float* __restrict__ W, OutT* __restrict__ out,
-                                  long B, int bag, int D, long ldo, float scale) {
-  const int D4 = D >> 2;
-  const long total = B * D4;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    long b = e / D4;
-    int c = (int)(e % D4) * 4;
-    f32x4_t s = {0.f, 0.f, 0.f, 0.f};
-    const IdxT* ib = idx + b * bag;
-    for (int j = 0; j < bag; ++j) {
-      long r = (long)ib[j];
-      s += *reinterpret_cast<const f32x4_t*>(W + r * D + c);
+constexpr int MAXT = 32;
+
+struct TabDesc {
+  const float* W;     // fwd: table (read); bwd: table or dense grad (written)
+  const void* idx;    // [B, bag] int32/int64
+  void* act;          // fwd: out [B, *] (row stride ld); bwd: dy
+  long ld;
+  int rows, D, bag, idx64;
+  float scale;
+};
+struct TabSet {
+  TabDesc t[MAXT];
+  int n;
+};
+
+FM_DEVICE long load_idx(const void* p, long i, int idx64) {
+  return idx64 ? (long)reinterpret_cast<const long long*>(p)[i] : (long)reinterpret_cast<const int*>(p)[i];
+}
+
+template <typename OutT>
+__global__ void __launch_bounds__(256) fm_emb_fwd_multi(TabSet s, long B) {
+  const TabDesc& d = s.t[blockIdx.y];
+  const int D4 = d.D >> 2;
+  const int lpr = D4 < 64 ? D4 : 64;              // lanes per row (D <= 256)
+  const int rpi = 256 / lpr;                       // rows per block-iteration
+  const int sub = threadIdx.x / lpr, lc = threadIdx.x - sub * lpr;
+  if (sub >= rpi) return;
+  for (long b = (long)blockIdx.x * rpi + sub; b < B; b += (long)gridDim.x * rpi) {
+    for (int c4 = lc; c4 < D4; c4 += lpr) {
+      const int c = c4 * 4;
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < d.bag; ++j) {
+        long r = load_idx(d.idx, b * d.bag + j, d.idx64);
+        acc += *reinterpret_cast<const f32x4_t*>(d.W + r * d.D + c);
+      }
+      acc *= d.scale;
+      OutT* o = reinterpret_cast<OutT*>(d.act) + b * d.ld + c;
+      if constexpr (sizeof(OutT) == 4) {
+        *reinterpret_cast<f32x4_t*>(o) = acc;
+      } else {
+        bf16x4_t v;
+        v[0] = (short)f2bf(acc[0]); v[1] = (short)f2bf(acc[1]); v[2] = (short)f2bf(acc[2]); v[3] = (short)f2bf(acc[3]);
+        *reinterpret_cast<bf16x4_t*>(o) = v;
+      }
     }
-    s *= scale;
-    OutT* o = out + b * ldo + c;
-    if constexpr (sizeof(OutT) == 4) {
-      *reinterpret_cast<f32x4_t*>(o) = s;
-    } else {
-      bf16x4_t v;
-      v[0] = (short)f2bf(s[0]); v[1] = (short)f2bf(s[1]); v[2] = (short)f2bf(s[2]); v[3] = (short)f2bf(s[3]);
-      *reinterpret_cast<bf16x4_t*>(o) = v;
+  }
+}
+
+// scalar fallback for D % 4 != 0 (any D)
+template <typename OutT>
+__global__ void __launch_bounds__(256) fm_emb_fwd_multi_scalar(TabSet s, long B) {
+  const TabDesc& d = s.t[blockIdx.y];
+  const int lpr = d.D < 256 ? d.D : 256;
+  const int rpi = 256 / lpr;
+  const int sub = threadIdx.x / lpr, lc = threadIdx.x - sub * lpr;
+  if (sub >= rpi) return;
+  for (long b = (long)blockIdx.x * rpi + sub; b < B; b += (long)gridDim.x * rpi)
+    for (int c = lc; c < d.D; c += lpr) {
+      float acc = 0.f;
+      for (int j = 0; j < d.bag; ++j) acc += d.W[load_idx(d.idx, b * d.bag + j, d.idx64) * d.D + c];
+      st<OutT>(reinterpret_cast<OutT*>(d.act) + b * d.ld + c, acc * d.scale);
     }
-  }
 }
 
-// scalar fallback for D % 4 != 0
-template <typename OutT, typename IdxT>
-__global__ void fm_emb_fwd_scalar(const IdxT* __restrict__ idx, const float* __restrict__ W, OutT* __restrict__ out,
-                                  long B, int bag, int D, long ldo, float scale) {
-  const long total = B * D;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    long b = e / D;
-    int c = (int)(e % D);
-    float s = 0.f;
-    for (int j = 0; j < bag; ++j) s += W[(long)idx[b * bag + j] * D + c];
-    st<OutT>(out + b * ldo + c, s * scale);
-  }
+template <typename GT>
+__global__ void __launch_bounds__(256) fm_emb_bwd_atomic_multi(TabSet s, const float* __restrict__ lr, long B) {
+  const TabDesc& d = s.t[blockIdx.y];
+  const float mul = (lr ? -lr[0] : 1.f) * d.scale;
+  const int lpr = d.D < 256 ? d.D : 256;
+  const int rpi = 256 / lpr;
+  const int sub = threadIdx.x / lpr, lc = threadIdx.x - sub * lpr;
+  if (sub >= rpi) return;
+  float* W = const_cast<float*>(d.W);
+  const GT* dy = reinterpret_cast<const GT*>(d.act);
+  for (long b = (long)blockIdx.x * rpi + sub; b < B; b += (long)gridDim.x * rpi)
+    for (int c = lc; c < d.D; c += lpr) {
+      const float g = ld<GT>(dy + b * d.ld + c) * mul;
+      for (int j = 0; j < d.bag; ++j) atomicAdd(W + load_idx(d.idx, b * d.bag + j, d.idx64) * d.D + c, g);
+    }
 }
 
-// ---- backward: atomics (large tables) --------------------------------------------------
-template <typename GT, typename IdxT>
-__global__ void fm_emb_bwd_atomic(const IdxT* __restrict__ idx, const GT* __restrict__ dy, float* __restrict__ W,
-                                  const float* __restrict__ lr, long B, int bag, int D, long ldg, float scale) {
-  const float neg = lr ? -lr[0] * scale : scale;
-  const long total = B * (long)bag * D;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    long bj = e / D;
-    int c = (int)(e % D);
-    long b = bj / bag;
-    float g = ld<GT>(dy + b * ldg + c) * neg;
-    atomicAdd(W + (long)idx[bj] * D + c, g);
-  }
-}
-
-// ---- backward: LDS-privatised (tiny tables) --------------------------------------------
-template <typename GT, typename IdxT>
-__global__ void fm_emb_bwd_lds(const IdxT* __restrict__ idx, const GT* __restrict__ dy, float* __restrict__ W,
-                               const float* __restrict__ lr, long B, int bag, int rows, int D, long ldg, float scale) {
+template <typename GT>
+__global__ void __launch_bounds__(256) fm_emb_bwd_lds_multi(TabSet s, const float* __restrict__ lr, long B) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* acc = reinterpret_cast<float*>(smem);
-  const int n = rows * D;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) acc[i] = 0.f;
+  const TabDesc& d = s.t[blockIdx.y];
+  const int n = d.rows * d.D;
+  for (int i = threadIdx.x; i < n; i += 256) acc[i] = 0.f;
   __syncthreads();
-  const long total = B * (long)bag * D;
-  const long per_block = (total + gridDim.x - 1) / gridDim.x;
-  const long e0 = blockIdx.x * per_block;
-  const long e1 = min(total, e0 + per_block);
-  for (long e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
-    long bj = e / D;
-    int c = (int)(e % D);
-    long b = bj / bag;
-    atomicAdd(acc + (int)idx[bj] * D + c, ld<GT>(dy + b * ldg + c));
+  const int lpr = d.D < 256 ? d.D : 256;
+  const int rpi = 256 / lpr;
+  const int sub = threadIdx.x / lpr, lc = threadIdx.x - sub * lpr;
+  const long chunk = (B + gridDim.x - 1) / gridDim.x;
+  const long b0 = blockIdx.x * chunk, b1 = min(B, b0 + chunk);
+  const GT* dy = reinterpret_cast<const GT*>(d.act);
+  if (sub < rpi) {
+    for (long b = b0 + sub; b < b1; b += rpi)
+      for (int c = lc; c < d.D; c += lpr) {
+        const float g = ld<GT>(dy + b * d.ld + c);
+        for (int j = 0; j < d.bag; ++j) atomicAdd(acc + load_idx(d.idx, b * d.bag + j, d.idx64) * d.D + c, g);
+      }
   }
   __syncthreads();
-  const float neg = lr ? -lr[0] * scale : scale;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+  const float mul = (lr ? -lr[0] : 1.f) * d.scale;
+  float* W = const_cast<float*>(d.W);
+  for (int i = threadIdx.x; i < n; i += 256) {
     float v = acc[i];
-    if (v != 0.f) atomicAdd(W + i, v * neg);
+    if (v != 0.f) atomicAdd(W + i, v * mul);
   }
 }
+
+constexpr long TINY_BYTES = 64 * 1024;
 
 }  // namespace
 
-// idx64: 1 => int64 indices else int32; out_bf16: output storage
-extern "C" void fm_embedding_fwd(const void* idx, int idx64, const float* W, void* out, int out_bf16, long B, int bag,
-                                 int D, long ldo, float scale, hipStream_t s) {
+// ------------------------------------------------------------------------------------------
+// Launchers.  Arrays describe n tables; act/ld = outputs (fwd) or output grads (bwd).
+extern "C" void fm_embedding_fwd_multi(int n, const float* const* W, const void* const* idx, const int* idx64,
+                                       void* const* out, const long* ldo, const int* rows, const int* D, const int* bag,
+                                       const float* scale, int out_bf16, long B, hipStream_t st) {
   if (B <= 0) return;
-  bool vec = (D % 4 == 0) && (ldo % 4 == 0);
-  long work = vec ? B * (D / 4) : B * D;
-  dim3 g(fm_grid(work, 256, 16384)), blk(256);
-#define FM_EMB_FWD(OT, IT)                                                                                      \
-  if (vec) hipLaunchKernelGGL((fm_emb_fwd_kernel<OT, IT>), g, blk, 0, s, (const IT*)idx, W, (OT*)out, B, bag, D, ldo, scale); \
-  else hipLaunchKernelGGL((fm_emb_fwd_scalar<OT, IT>), g, blk, 0, s, (const IT*)idx, W, (OT*)out, B, bag, D, ldo, scale);
-  if (out_bf16) {
-    if (idx64) { FM_EMB_FWD(unsigned short, long long) } else { FM_EMB_FWD(unsigned short, int) }
-  } else {
-    if (idx64) { FM_EMB_FWD(float, long long) } else { FM_EMB_FWD(float, int) }
+  for (int base = 0; base < n; base += MAXT) {
+    TabSet s;
+    int m = std::min(MAXT, n - base);
+    bool vec = true;
+    for (int i = 0; i < m; ++i) {
+      int k = base + i;
+      s.t[i] = TabDesc{W[k], idx[k], out[k], ldo[k], rows[k], D[k], bag[k], idx64[k], scale[k]};
+      vec = vec && (D[k] % 4 == 0) && (ldo[k] % 4 == 0) && D[k] <= 256;
+    }
+    s.n = m;
+    const int rpi = std::max(1, 256 / std::min(64, std::max(1, D[base] / 4)));
+    dim3 grid((unsigned)std::max<long>(1, std::min<long>((B + rpi - 1) / rpi, 2048)), m);
+    if (vec) {
+      if (out_bf16) hipLaunchKernelGGL(fm_emb_fwd_multi<unsigned short>, grid, dim3(256), 0, st, s, B);
+      else hipLaunchKernelGGL(fm_emb_fwd_multi<float>, grid, dim3(256), 0, st, s, B);
+    } else {
+      if (out_bf16) hipLaunchKernelGGL(fm_emb_fwd_multi_scalar<unsigned short>, grid, dim3(256), 0, st, s, B);
+      else hipLaunchKernelGGL(fm_emb_fwd_multi_scalar<float>, grid, dim3(256), 0, st, s, B);
+    }
   }
-#undef FM_EMB_FWD
 }
 
-// lr != nullptr: fused SGD update of W (W -= lr*scale*grad); lr == nullptr: dense grad accumulate
-// into W (W := dW buffer, +scale*grad).
+// lr != nullptr: fused sparse SGD into W; lr == nullptr: W is a dense grad buffer (accumulate).
+extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const* idx, const int* idx64,
+                                       const void* const* dy, const long* ldg, const int* rows, const int* D,
+                                       const int* bag, const float* scale, int dy_bf16, const float* lr, long B,
+                                       hipStream_t st) {
+  if (B <= 0) return;
+  // partition: tiny tables -> LDS kernel, others -> atomic kernel
+  for (int pass = 0; pass < 2; ++pass) {
+    std::vector<int> sel;
+    for (int k = 0; k < n; ++k) {
+      bool tiny = (long)rows[k] * D[k] * 4 <= TINY_BYTES && B * (long)bag[k] >= 4L * rows[k];
+      if ((pass == 0) == tiny) sel.push_back(k);
+    }
+    for (size_t base = 0; base < sel.size(); base += MAXT) {
+      TabSet s;
+      int m = (int)std::min<size_t>(MAXT, sel.size() - base);
+      int maxD = 1, maxrows = 1;
+      for (int i = 0; i < m; ++i) {
+        int k = sel[base + i];
+        s.t[i] = TabDesc{W[k], idx[k], const_cast<void*>(dy[k]), ldg[k], rows[k], D[k], bag[k], idx64[k], scale[k]};
+        maxD = std::max(maxD, D[k]);
+        maxrows = std::max(maxrows, rows[k]);
+      }
+      s.n = m;
+      if (pass == 0) {
+        size_t lds = (size_t)0;
+        for (int i = 0; i < m; ++i) lds = std::max(lds, (size_t)s.t[i].rows * s.t[i].D * 4);
+        dim3 grid((unsigned)std::max<long>(1, std::min<long>(B / 256, 32)), m);
+        if (dy_bf16) hipLaunchKernelGGL(fm_emb_bwd_lds_multi<unsigned short>, grid, dim3(256), lds, st, s, lr, B);
+        else hipLaunchKernelGGL(fm_emb_bwd_lds_multi<float>, grid, dim3(256), lds, st, s, lr, B);
+      } else {
+        const int rpi = std::max(1, 256 / std::min(256, maxD));
+        dim3 grid((unsigned)std::max<long>(1, std::min<long>((B + rpi - 1) / rpi, 2048)), m);
+        if (dy_bf16) hipLaunchKernelGGL(fm_emb_bwd_atomic_multi<unsigned short>, grid, dim3(256), 0, st, s, lr, B);
+        else hipLaunchKernelGGL(fm_emb_bwd_atomic_multi<float>, grid, dim3(256), 0, st, s, lr, B);
+      }
+    }
+  }
+}
+
+// single-table conveniences
+extern "C" void fm_embedding_fwd(const void* idx, int idx64, const float* W, void* out, int out_bf16, long B, int bag,
+                                 int D, long ldo, float scale, hipStream_t s) {
+  int rows = 0;
+  fm_embedding_fwd_multi(1, &W, &idx, &idx64, &out, &ldo, &rows, &D, &bag, &scale, out_bf16, B, s);
+}
+
 extern "C" void fm_embedding_bwd(const void* idx, int idx64, const void* dy, int dy_bf16, float* W, const float* lr,
                                  long B, int bag, int rows, int D, long ldg, float scale, hipStream_t s) {
-  if (B <= 0) return;
-  long total = B * (long)bag * D;
-  const long lds_bytes = (long)rows * D * 4;
-  if (lds_bytes <= 64 * 1024 && total >= 4L * rows * D) {
-    int blocks = (int)std::min<long>(512, std::max<long>(1, total / (64L * 256)));
-#define FM_EMB_LDS(GT, IT) \
-  hipLaunchKernelGGL((fm_emb_bwd_lds<GT, IT>), dim3(blocks), dim3(256), lds_bytes, s, (const IT*)idx, (const GT*)dy, W, lr, B, bag, rows, D, ldg, scale);
-    if (dy_bf16) { if (idx64) { FM_EMB_LDS(unsigned short, long long) } else { FM_EMB_LDS(unsigned short, int) } }
-    else { if (idx64) { FM_EMB_LDS(float, long long) } else { FM_EMB_LDS(float, int) } }
-#undef FM_EMB_LDS
-    return;
-  }
-  dim3 g(fm_grid(total, 256, 16384)), blk(256);
-#define FM_EMB_AT(GT, IT) \
-  hipLaunchKernelGGL((fm_emb_bwd_atomic<GT, IT>), g, blk, 0, s, (const IT*)idx, (const GT*)dy, W, lr, B, bag, D, ldg, scale);
-  if (dy_bf16) { if (idx64) { FM_EMB_AT(unsigned short, long long) } else { FM_EMB_AT(unsigned short, int) } }
-  else { if (idx64) { FM_EMB_AT(float, long long) } else { FM_EMB_AT(float, int) } }
-#undef FM_EMB_AT
+  fm_embedding_bwd_multi(1, &W, &idx, &idx64, &dy, &ldg, &rows, &D, &bag, &scale, dy_bf16, lr, B, s);
 }

@@ -202,7 +202,5 @@ class SyntheticDLRMData:
     def next_batch(self):
         ex = self.model.executor
         k = self.i % self.nb
-        for gid, pool in self.pools.items():
-            t = ex.tensors[gid]
-            ex.local_buffer(t).copy_(pool[k], non_blocking=True)
+        ex.load_local_many([(ex.tensors[gid], pool[k]) for gid, pool in self.pools.items()])
         self.i += 1

@@ -1,4 +1,5 @@
 """Operators (graph semantics + parallel layouts + local compute) and HIP kernel bindings."""
+import flexmi.core  # noqa: F401  (initialise core first: core.model imports the ops)
 from .base import Op, OpCtx  # noqa
 from .linear import Linear  # noqa
 from .embedding import Embedding  # noqa

@@ -321,6 +321,32 @@ class Executor:
             op.prepare(c)
             self.ctx[op.guid] = c
         self.grad_written = set()
+        self._build_groups(ops)
+
+    def _build_groups(self, ops):
+        """Fuse independent ops of the same kind and placement into one launch (embedding
+        tables of a DLRM graph: 26 ops -> 1 forward + 2 backward launches).  Members run at the
+        first member's position in forward and at the last position (in backward order, i.e.
+        the first member) in backward, when every member's output gradient is final."""
+        from flexmi.core.types import OperatorType
+        self.group_of = {}
+        groups = []
+        for op in ops:
+            c = self.ctx.get(op.guid)
+            if c is None or op.op_type != OperatorType.OP_EMBEDDING:
+                continue
+            pc = self.pcs[op.guid]
+            for g in groups:
+                lead = g[0]
+                if (self.pcs[lead.guid] == pc and type(lead).can_group(lead, op, self.ctx[lead.guid], c)):
+                    g.append(op)
+                    break
+            else:
+                groups.append([op])
+        for g in groups:
+            if len(g) > 1:
+                for op in g:
+                    self.group_of[op.guid] = g
 
     # ------------------------------------------------------------------
     def _build_weights(self, ops):
@@ -348,7 +374,7 @@ class Executor:
                 g = groups[key]
                 e.group = g
                 e.offset = g.numel
-                g.numel += e.numel
+                g.numel += (e.numel + 63) // 64 * 64  # 256-B aligned views: 16-B vector loads in every kernel
                 g.entries.append(e)
         self.groups = list(groups.values())
         mixed = self.cdtype != torch.float32
@@ -367,15 +393,15 @@ class Executor:
                 e.state = {n: s[sl].view(e.shape) for n, s in g.state.items()}
             # buckets (only meaningful for replicated groups)
             cap = max(1, int(self.cfg.grad_bucket_mb * (1 << 20) / 4))
-            start, cur, ids = 0, 0, set()
+            start, ids = 0, set()
             for e in g.entries:
-                if cur > 0 and cur + e.numel > cap:
-                    g.buckets.append([start, start + cur, ids])
-                    start, cur, ids = start + cur, 0, set()
-                cur += e.numel
+                end = e.offset + (e.numel + 63) // 64 * 64
+                if ids and end - start > cap:
+                    g.buckets.append([start, e.offset, ids])
+                    start, ids = e.offset, set()
                 ids.add(e.param.guid)
-            if cur > 0:
-                g.buckets.append([start, start + cur, ids])
+            if ids:
+                g.buckets.append([start, g.numel, ids])
         # communicators for every replicated subset, created in the same order everywhere
         all_sets = []
         for op in ops:
@@ -466,6 +492,12 @@ class Executor:
                 c = self.ctx.get(op.guid)
                 if c is not None:
                     c.training = self.training
+                    grp = self.group_of.get(op.guid)
+                    if grp is not None:
+                        if grp[0] is op:
+                            with tm.scope(op.name + ".group_fwd"):
+                                type(op).forward_group(grp, [self.ctx[o.guid] for o in grp])
+                        continue
                     with tm.scope(op.name + ".fwd"):
                         op.forward(c)
 
@@ -503,8 +535,14 @@ class Executor:
                         if o.guid in self.grad and self.gkey(o.guid) not in self.grad_written:
                             self.grad[o.guid].zero_()   # unused output
                             self.grad_written.add(self.gkey(o.guid))
-                    with tm.scope(op.name + ".bwd"):
-                        op.backward(c)
+                    grp = self.group_of.get(op.guid)
+                    if grp is not None:
+                        if grp[0] is op:
+                            with tm.scope(op.name + ".group_bwd"):
+                                type(op).backward_group(grp, [self.ctx[o.guid] for o in grp])
+                    else:
+                        with tm.scope(op.name + ".bwd"):
+                            op.backward(c)
                     for i, t in enumerate(op.inputs):
                         if c.in_grads[i] is not None and self.need[(op.guid, i)].same_as(self.home[t.guid]):
                             self.grad_written.add(self.gkey(t.guid))
@@ -662,6 +700,27 @@ class Executor:
         if rest:
             src = src[(slice(None),) + rest]
         buf.copy_(src.to(buf.dtype), non_blocking=True)
+
+    def load_local_many(self, pairs):
+        """Copy several (tensor, source-shard) pairs into their home buffers; on MI355X in one
+        multi-copy launch per 16 tensors (bytes moved as 16-bit words)."""
+        if self.backend != "hip":
+            for t, src in pairs:
+                self.local_buffer(t).copy_(src)
+            return
+        from flexmi.ops import _kernels as K
+        src, dst, n = [], [], []
+        for t, s_ in pairs:
+            d = self.local_buffer(t)
+            if d is None:
+                continue
+            sv = s_.contiguous().view(-1).view(torch.int16)
+            dv = d.view(-1).view(torch.int16)
+            src.append(sv)
+            dst.append(dv)
+            n.append(dv.numel())
+        if src:
+            K.C().multi_copy(src, [0] * len(src), dst, [0] * len(dst), [1] * len(n), n, n, n, 0)
 
     # ------------------------------------------------------------------ hipGraph
     def train_step(self):
