@@ -73,6 +73,12 @@ class ElementUnary(Op):
         if not ctx.in_grads or ctx.in_grads[0] is None:
             return
         x, y, dy, dx = ctx.inputs[0], ctx.outputs[0], ctx.out_grads[0], ctx.in_grads[0]
+        if getattr(self, "skip_act_grad", False):   # fused sigmoid + BCE (loss emitted dL/dz)
+            if ctx.hip:
+                K.copy_or_add(dy, dx, ctx.in_grad_accumulate[0])
+            else:
+                store(dx, dy, ctx.in_grad_accumulate[0])
+            return
         if ctx.hip:
             K.unary_backward(self.code, x, y, dy, dx, ctx.in_grad_accumulate[0])
         else:

@@ -113,12 +113,13 @@ class Linear(Op):
         dx2 = None if dx is None else dx.view(-1, dx.shape[-1])
         dw = ctx.weight_grads[0]
         db = ctx.weight_grads[1] if self.use_bias else None
+        act = ActiMode.AC_MODE_NONE if getattr(self, "skip_act_grad", False) else self.activation
         if ctx.hip:
-            K.linear_backward(x2, ctx.wcompute[0], y2, dy2, int(self.activation), dx2,
+            K.linear_backward(x2, ctx.wcompute[0], y2, dy2, int(act), dx2,
                               bool(ctx.in_grad_accumulate[0]) if dx2 is not None else False, dw, db,
                               ctx.workspace)
         else:
-            dpre = act_backward_torch(dy2.float(), y2.float(), self.activation)
+            dpre = act_backward_torch(dy2.float(), y2.float(), act)
             dw.copy_(dpre.t() @ x2.float())
             if db is not None:
                 db.copy_(dpre.sum(0))

@@ -430,6 +430,18 @@ class Executor:
 
     def _build_loss(self):
         final = self.final
+        # BCE on a sigmoid output: the loss kernel emits dL/dz = p - y (numerically exact), so the
+        # producing op must not apply the sigmoid derivative again (fused sigmoid + BCE).
+        if self.loss_type == LossType.LOSS_BINARY_CROSSENTROPY:
+            from flexmi.core.types import ActiMode, OperatorType
+            fop = final.owner_op
+            if getattr(fop, "activation", None) == ActiMode.AC_MODE_SIGMOID:
+                fop.skip_act_grad = True
+            elif fop.op_type == OperatorType.OP_SIGMOID:
+                fop.skip_act_grad = True
+            else:
+                raise ValueError("LOSS_BINARY_CROSSENTROPY expects the model to end in a sigmoid "
+                                 "(dense(..., AC_MODE_SIGMOID) or sigmoid())")
         home = self.home[final.guid]
         deg = [1] * len(final.dims)
         deg[0] = home.degrees[0]

@@ -1,0 +1,144 @@
+"""Multi-rank correctness without GPUs: world_size 2/4 over gloo (SURVEY §7.6 "strategy
+equivalence": any SOAP strategy must train exactly like data parallelism / world 1).
+
+Each case builds the same model on every rank with a strategy, trains a few steps on the same
+global batches and compares the FULL gathered parameters with a world-1 run."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.multiproc
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _build(case, world):
+    from flexmi.core import (ActiMode, FFConfig, FFModel, LossType, MetricsType, SGDOptimizer, PoolType)
+    from flexmi.parallel.layout import ParallelConfig
+    from flexmi.models.dlrm import DLRMConfig, build_dlrm, dlrm_strategy
+    cfg = FFConfig()
+    cfg.device = "cpu"
+    cfg.compute_dtype = "fp32"
+    B = 16
+    cfg.batchSize = B
+    m = FFModel(cfg)
+    strat = {}
+    inputs = {}
+    if case in ("mlp_dp", "mlp_channel"):
+        x = m.create_tensor([B, 12], name="x")
+        h = m.dense(x, 16, ActiMode.AC_MODE_RELU, name="fc1")
+        h = m.dense(h, 8, ActiMode.AC_MODE_TANH, name="fc2")
+        o = m.dense(h, 4, name="fc3")
+        o = m.softmax(o, name="sm")
+        loss = LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY
+        inputs["x"] = (x, (B, 12), "f")
+        if case == "mlp_channel" and world > 1:
+            # fc1: channel (parameter) split over all ranks; fc2: 2-D sample x channel split
+            strat["fc1"] = ParallelConfig([world, 1], list(range(world)))
+            if world % 2 == 0:
+                strat["fc2"] = ParallelConfig([2, world // 2], list(range(world)))
+    elif case.startswith("dlrm"):
+        dcfg = DLRMConfig.preset("tiny")
+        dcfg.arch_interaction_op = "dot" if case == "dlrm_dot" else "cat"
+        d, s, p = build_dlrm(m, dcfg)
+        loss = LossType.LOSS_BINARY_CROSSENTROPY
+        inputs["dense"] = (d, (B, 13), "f")
+        for i, (t, r) in enumerate(zip(s, dcfg.embedding_size)):
+            inputs[f"sparse{i}"] = (t, (B, 1), ("i", r))
+        if world > 1:
+            strat = dlrm_strategy(m, world)
+            if case == "dlrm_colsplit":
+                # column (parameter-dim) split of one table across all ranks
+                strat["embedding1"] = ParallelConfig([world, 1], list(range(world)))
+    elif case == "cnn_spatial":
+        x = m.create_tensor([4, 3, 12, 12], name="img")
+        c = m.conv2d(x, 4, 3, 3, 1, 1, 1, 1, ActiMode.AC_MODE_RELU, name="conv1")
+        c = m.pool2d(c, 3, 3, 2, 2, 1, 1, PoolType.POOL_MAX, name="pool1")
+        c = m.conv2d(c, 4, 3, 3, 1, 1, 1, 1, ActiMode.AC_MODE_NONE, name="conv2")
+        f = m.flat(c, name="flat")
+        o = m.dense(f, 3, name="fc")
+        o = m.softmax(o, name="sm")
+        loss = LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY
+        inputs["img"] = (x, (4, 3, 12, 12), "f")
+        cfg.batchSize = 4
+        if world > 1:
+            # attribute (spatial) split: H split across ranks (exact, with halo exchange)
+            strat["conv1"] = ParallelConfig([1, world, 1, 1], list(range(world)))
+            strat["pool1"] = ParallelConfig([1, world, 1, 1], list(range(world)))
+            strat["conv2"] = ParallelConfig([world, 1, 1, 1], list(range(world)))
+    m.strategies = strat
+    m.compile(SGDOptimizer(m, 0.1), loss, [MetricsType.METRICS_ACCURACY])
+    m.strategies = strat
+    return m, inputs
+
+
+def _run(case, world, rank, steps, out_path):
+    m, inputs = _build(case, world)
+    ex = m.init_layers()
+    for op in m.layers:  # the strategy must really be applied (no silent DP fallback)
+        if op.name in m.strategies:
+            assert ex.pcs[op.guid] == m.strategies[op.name], (op.name, ex.pcs[op.guid])
+    rng = np.random.RandomState(7)
+    for it in range(steps):
+        for name, (t, shape, kind) in inputs.items():
+            if kind == "f":
+                a = rng.rand(*shape).astype(np.float32)
+            else:
+                a = rng.randint(0, kind[1], shape).astype(np.int64)
+            ex.scatter_from_host(t, a)
+        lab = m.get_label_tensor()
+        if lab.data_type.name == "DT_INT32":
+            la = rng.randint(0, m.layers[-1].outputs[0].dims[-1], lab.dims).astype(np.int32)
+        else:
+            la = rng.randint(0, 2, lab.dims).astype(np.float32)
+        ex.scatter_from_host(lab, la)
+        ex.train_step()
+    params = [p.get_weights(m) for p in m.parameters]
+    loss = m.get_perf_metrics().get_loss()
+    if rank == 0:
+        np.savez(out_path, loss=loss, *params)
+
+
+def _worker(rank, world, port, case, steps, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _run(case, world, rank, steps, out_path)
+    finally:
+        dist.destroy_process_group()
+
+
+def _launch(case, world, steps=3):
+    out = tempfile.mktemp(suffix=".npz")
+    if world == 1:
+        _run(case, 1, 0, steps, out)
+    else:
+        mp.start_processes(_worker, args=(world, _free_port(), case, steps, out), nprocs=world, join=True,
+                           start_method="spawn")
+    d = np.load(out)
+    os.unlink(out)
+    return d
+
+
+@pytest.mark.parametrize("case,world", [("mlp_dp", 2), ("mlp_channel", 2), ("mlp_channel", 4), ("dlrm_dot", 2),
+                                        ("dlrm_cat", 2), ("dlrm_colsplit", 2), ("cnn_spatial", 2)])
+def test_strategy_equivalence(case, world):
+    ref = _launch(case, 1)
+    got = _launch(case, world)
+    keys = [k for k in ref.files if k.startswith("arr_")]
+    assert len(keys) == len([k for k in got.files if k.startswith("arr_")])
+    for k in keys:
+        np.testing.assert_allclose(got[k], ref[k], rtol=1e-4, atol=1e-5, err_msg=f"{case} w{world} {k}")
+    assert abs(float(got["loss"]) - float(ref["loss"])) < 1e-4
