@@ -79,19 +79,21 @@ def main():
     t_init = time.time() - t0
     data = SyntheticDLRMData(model, dense_in, sparse, dcfg, num_batches=4, seed=rank)
 
-    use_graph = (not a.no_graph) and world == 1 and torch.cuda.is_available()
-    graphs = None
+    use_graph = (not a.no_graph) and torch.cuda.is_available() and not a.profile
+    step_eager_calls = [0]
 
     def step_eager():
         data.next_batch()
         ex.train_step()
 
     if use_graph:
-        # warm the allocator/kernels, then capture one graph per pooled batch (input copy inside)
+        # warm the allocator / lazily created workspaces, then capture: one small graph per pooled
+        # batch for input staging + the training step as hipGraph segments split at the RCCL
+        # collectives (collectives stay eager between replays when world > 1)
         for _ in range(2):
             step_eager()
         torch.cuda.synchronize()
-        graphs = []
+        stage = []
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         for k in range(data.nb):
@@ -99,14 +101,15 @@ def main():
             with torch.cuda.stream(s):
                 with torch.cuda.graph(g, stream=s):
                     data.i = k
-                    step_eager()
-            graphs.append(g)
+                    data.next_batch()
+            stage.append(g)
         torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
+        run_step = ex.capture_step()
         gi = [0]
 
         def step():
-            graphs[gi[0] % len(graphs)].replay()
+            stage[gi[0] % len(stage)].replay()
+            run_step()
             gi[0] += 1
     else:
         step = step_eager

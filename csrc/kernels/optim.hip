@@ -43,8 +43,9 @@ __global__ void fm_sgd_kernel(float* __restrict__ W, const float* __restrict__ G
 }
 
 __global__ void fm_adam_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ M,
-                               float* __restrict__ V, unsigned short* __restrict__ Wc, long n, float alpha_t, float b1,
-                               float b2, float wd, float eps) {
+                               float* __restrict__ V, unsigned short* __restrict__ Wc, long n,
+                               const float* __restrict__ alpha_t_p, float b1, float b2, float wd, float eps) {
+  const float alpha_t = alpha_t_p[0];  // device-side bias-corrected step size (graph-capturable)
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     float w = W[i];
     float g = G[i] + wd * w;
@@ -72,8 +73,8 @@ extern "C" void fm_sgd_update(float* W, const float* G, float* V, unsigned short
                      nesterov, al ? 1 : 0);
 }
 
-extern "C" void fm_adam_update(float* W, const float* G, float* M, float* V, unsigned short* Wc, long n, float alpha_t,
-                               float b1, float b2, float wd, float eps, hipStream_t s) {
+extern "C" void fm_adam_update(float* W, const float* G, float* M, float* V, unsigned short* Wc, long n,
+                               const float* alpha_t, float b1, float b2, float wd, float eps, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(fm_adam_kernel, dim3(fm_grid(n)), dim3(256), 0, s, W, G, M, V, Wc, n, alpha_t, b1, b2, wd, eps);
 }

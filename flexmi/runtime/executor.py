@@ -29,7 +29,7 @@ from flexmi.core.loss_metrics import NUM_SLOTS, PerfMetrics, loss_and_metrics_to
 from flexmi.core.optimizers import AdamOptimizer, SGDOptimizer
 from flexmi.core.types import DataType, LossType, to_torch_dtype
 from flexmi.ops.base import OpCtx
-from flexmi.parallel.layout import Layout, ParallelConfig, ReshardPlan
+from flexmi.parallel.layout import Layout, ParallelConfig, ReshardPlan, box_volume
 from flexmi.utils.profiling import OpTimer
 
 
@@ -62,38 +62,56 @@ class ReshardStep:
 
     def run(self, comm, src_buf, dst_buf, accumulate=False):
         """src_buf: this rank's shard of the source layout (or None); dst_buf likewise."""
-        plan, r = self.plan, self.rank
-        reduce = plan.src.partial
-        src_box = plan.src.local_box(r) if src_buf is not None else None
-        dst_box = plan.dst.local_box(r) if dst_buf is not None else None
-        if dst_buf is not None and (reduce or not self._covers()) and not accumulate:
+        run_reshards(comm, [(self, src_buf, dst_buf, accumulate)])
+
+    # --- phases used by run_reshards (several reshards share ONE all_to_all) ---------------
+    def prepare_dst(self, dst_buf, accumulate):
+        """Zero the destination when contributions are summed into it; returns add-mode."""
+        reduce = self.plan.src.partial
+        if dst_buf is not None and reduce and not accumulate:
             dst_buf.zero_()
-            accumulate = True if reduce else accumulate
-        if self.local_only or comm.world == 1:
-            for t in self.recvs:
-                piece = src_buf[_slices(t.box, src_box)]
-                self._put(dst_buf, dst_box, t.box, piece, accumulate or reduce)
+        return accumulate or reduce
+
+    def local_copies(self, src_buf, dst_buf, add):
+        r = self.rank
+        if not self.recvs:
             return
-        dtype, device = self.dtype, self.device
-        send = [None] * comm.world
-        per_peer = defaultdict(list)
-        for t in self.sends:
-            per_peer[t.dst].append(src_buf[_slices(t.box, src_box)].reshape(-1))
-        for p, lst in per_peer.items():
-            send[p] = torch.cat(lst) if len(lst) > 1 else lst[0]
-        chunks = comm.all_to_all(send, self.recv_numel, dtype, device)
-        offs = [0] * comm.world
+        src_box = self.plan.src.local_box(r)
+        dst_box = self.plan.dst.local_box(r)
         for t in self.recvs:
+            if t.src == r:
+                self._put(dst_buf, dst_box, t.box, src_buf[_slices(t.box, src_box)], add)
+
+    def remote_sends(self, src_buf):
+        """{peer: [flat pieces]} in plan order (same order the peer unpacks)."""
+        out = defaultdict(list)
+        if not self.sends:
+            return out
+        src_box = self.plan.src.local_box(self.rank)
+        for t in self.sends:
+            if t.dst != self.rank:
+                out[t.dst].append(src_buf[_slices(t.box, src_box)].reshape(-1))
+        return out
+
+    def remote_recv_numel(self):
+        n = defaultdict(int)
+        for t in self.recvs:
+            if t.src != self.rank:
+                n[t.src] += box_volume(t.box)
+        return n
+
+    def unpack(self, chunks, offs, dst_buf, add):
+        if not self.recvs:
+            return
+        dst_box = self.plan.dst.local_box(self.rank)
+        for t in self.recvs:
+            if t.src == self.rank:
+                continue
             shape = tuple(hi - lo for lo, hi in t.box)
-            n = 1
-            for s in shape:
-                n *= s
+            n = box_volume(t.box)
             piece = chunks[t.src][offs[t.src]: offs[t.src] + n].view(shape)
             offs[t.src] += n
-            self._put(dst_buf, dst_box, t.box, piece, accumulate or reduce)
-
-    def _covers(self):
-        return True
+            self._put(dst_buf, dst_box, t.box, piece, add)
 
     @staticmethod
     def _put(dst_buf, dst_box, box, piece, add):
@@ -102,6 +120,99 @@ class ReshardStep:
             v.add_(piece.to(v.dtype))
         else:
             v.copy_(piece)
+
+
+def run_reshards(comm, items):
+    """Execute several reshard steps with ONE all_to_all (collective fusion: e.g. the 26
+    embedding outputs of a DLRM interaction move in a single RCCL call per direction).
+    items: [(ReshardStep, src_buf, dst_buf, accumulate)], all of the same dtype."""
+    adds = []
+    for st, src, dst, acc in items:
+        adds.append(st.prepare_dst(dst, acc))
+    for (st, src, dst, acc), add in zip(items, adds):
+        st.local_copies(src, dst, add)
+    if comm.world == 1 or all(st.local_only for st, *_ in items):
+        return
+    W = comm.world
+    per_peer = defaultdict(list)
+    recv = [0] * W
+    for st, src, dst, acc in items:
+        for p, lst in st.remote_sends(src).items():
+            per_peer[p].extend(lst)
+        for p, n in st.remote_recv_numel().items():
+            recv[p] += n
+    send = [None] * W
+    for p, lst in per_peer.items():
+        send[p] = torch.cat(lst) if len(lst) > 1 else lst[0]
+    st0 = items[0][0]
+    chunks = comm.all_to_all(send, recv, st0.dtype, st0.device)
+    offs = [0] * W
+    for (st, src, dst, acc), add in zip(items, adds):
+        st.unpack(chunks, offs, dst, add)
+
+
+class Item:
+    __slots__ = ("kind", "fn", "name")
+
+    def __init__(self, kind, fn, name):
+        self.kind, self.fn, self.name = kind, fn, name
+
+    def __repr__(self):
+        return f"{self.kind}:{self.name}"
+
+
+class FusedExchange:
+    """Several reshards moved by ONE all_to_all through persistent send/recv buffers, split in
+    pack (compute) / exchange (RCCL) / unpack (compute) so the compute halves can live inside
+    hipGraph segments."""
+
+    def __init__(self, items, world, rank):
+        self.items = items
+        self.world = world
+        self.rank = rank
+        st0 = items[0][0]
+        self.dtype, self.device = st0.dtype, st0.device
+        self.adds = [acc or st.plan.src.partial for st, src, dst, acc in items]
+        send = [0] * world
+        recv = [0] * world
+        for st, src, dst, acc in items:
+            for t in st.sends:
+                if t.dst != rank:
+                    send[t.dst] += box_volume(t.box)
+            for t in st.recvs:
+                if t.src != rank:
+                    recv[t.src] += box_volume(t.box)
+        self.send_sizes, self.recv_sizes = send, recv
+        self.send_buf = torch.empty(sum(send), dtype=self.dtype, device=self.device)
+        self.recv_buf = torch.empty(sum(recv), dtype=self.dtype, device=self.device)
+        self.send_off = [sum(send[:p]) for p in range(world)]
+        self.recv_off = [sum(recv[:p]) for p in range(world)]
+
+    def pack(self):
+        for (st, src, dst, acc), add in zip(self.items, self.adds):
+            st.prepare_dst(dst, acc)
+            st.local_copies(src, dst, add)
+        off = list(self.send_off)
+        per = defaultdict(list)
+        for st, src, dst, acc in self.items:
+            for p, lst in st.remote_sends(src).items():
+                per[p].extend(lst)
+        for p in range(self.world):
+            for piece in per.get(p, []):
+                n = piece.numel()
+                self.send_buf[off[p]: off[p] + n].copy_(piece)
+                off[p] += n
+
+    def exchange(self, comm):
+        import torch.distributed as dist
+        dist.all_to_all_single(self.recv_buf, self.send_buf, self.recv_sizes, self.send_sizes)
+        comm.calls += 1
+
+    def unpack(self):
+        chunks = list(torch.split(self.recv_buf, self.recv_sizes))
+        offs = [0] * self.world
+        for (st, src, dst, acc), add in zip(self.items, self.adds):
+            st.unpack(chunks, offs, dst, add)
 
 
 class WeightEntry:
@@ -225,16 +336,24 @@ class Executor:
         # ---- forward/backward schedules ----------------------------------------
         self.fwd_steps = []
         self.bwd_steps = []
+        made = set()
         for op in ops:
             pc = self.pcs[op.guid]
+            group = defaultdict(list)   # dtype -> reshards of this op's inputs (one all_to_all each)
             for i, t in enumerate(op.inputs):
                 need = self.need[(op.guid, i)]
                 home = self.home[t.guid]
                 if not need.same_as(home):
                     key = (t.guid, need.key())
+                    if key in made:
+                        continue
+                    made.add(key)
                     if key not in self.act and need.local_shape(self.rank) is not None:
                         self.act[key] = self._alloc(need.local_shape(self.rank), self._storage_dtype(t))
-                    self.fwd_steps.append(("reshard", t.guid, home, need, ReshardStep(ReshardPlan(home, need), self.rank, self.world, self._storage_dtype(t), self.device)))
+                    dt = self._storage_dtype(t)
+                    group[dt].append((t.guid, home, need, ReshardStep(ReshardPlan(home, need), self.rank, self.world, dt, self.device)))
+            for dt, lst in group.items():
+                self.fwd_steps.append(("reshard", lst))
             self.fwd_steps.append(("op", op))
 
         # grads: home-layout grad buffers for float tensors that need them
@@ -269,6 +388,7 @@ class Executor:
         self.tmp_grad: Dict[tuple, torch.Tensor] = {}
         for op in reversed(ops):
             self.bwd_steps.append(("op", op))
+            red = []
             for i, t in enumerate(op.inputs):
                 if t.guid not in self.grad_needed or not op.needs_input_grad(i):
                     continue
@@ -278,8 +398,10 @@ class Executor:
                     shp = need.local_shape(self.rank)
                     if shp is not None:
                         self.tmp_grad[(op.guid, i)] = self._alloc(shp, self.cdtype)
-                    self.bwd_steps.append(("reduce", op, i, t.guid,
-                                           ReshardStep(ReshardPlan(need.as_partial(), home), self.rank, self.world, self.cdtype, self.device)))
+                    red.append((op, i, t.guid,
+                                ReshardStep(ReshardPlan(need.as_partial(), home), self.rank, self.world, self.cdtype, self.device)))
+            if red:
+                self.bwd_steps.append(("reduce", red))
 
         # ---- weights ------------------------------------------------------------
         self._build_weights(ops)
@@ -320,8 +442,9 @@ class Executor:
             c.lr = self.lr_tensor
             op.prepare(c)
             self.ctx[op.guid] = c
-        self.grad_written = set()
         self._build_groups(ops)
+        self.adam_state = torch.tensor([1.0, 1.0, 0.0], dtype=torch.float32, device=self.device)
+        self._compile_program()
 
     def _build_groups(self, ops):
         """Fuse independent ops of the same kind and placement into one launch (embedding
@@ -491,161 +614,227 @@ class Executor:
         lay = self.home[t.guid]
         return self.act.get((t.guid, lay.key()))
 
-    def forward(self):
+    # The step is compiled ONCE into a flat program of items; "compute" items only enqueue
+    # HIP work on the current stream (capturable), "comm" items call RCCL.  Eager execution runs
+    # the items in order; graph mode captures every maximal run of compute items into one
+    # hipGraph and runs the collectives eagerly between replays (segmented capture).
+    def _compile_program(self):
         tm = self.timer
+        fwd, bwd, upd = [], [], []
+
+        def C(lst, name, fn):
+            lst.append(Item("compute", fn, name))
+
+        # ---------------- forward
         for st in self.fwd_steps:
             if st[0] == "reshard":
-                _, g, home, need, rs = st
-                src = self.act.get((g, home.key()))
-                dst = self.act.get((g, need.key()))
-                rs.run(self.comm, src, dst)
-            else:
-                op = st[1]
-                c = self.ctx.get(op.guid)
-                if c is not None:
-                    c.training = self.training
-                    grp = self.group_of.get(op.guid)
-                    if grp is not None:
-                        if grp[0] is op:
-                            with tm.scope(op.name + ".group_fwd"):
-                                type(op).forward_group(grp, [self.ctx[o.guid] for o in grp])
-                        continue
-                    with tm.scope(op.name + ".fwd"):
-                        op.forward(c)
+                items = [(rs, self.act.get((g, home.key())), self.act.get((g, need.key())), False)
+                         for g, home, need, rs in st[1]]
+                self._emit_reshards(fwd, items, "reshard.fwd")
+                continue
+            op = st[1]
+            c = self.ctx.get(op.guid)
+            if c is None:
+                continue
+            grp = self.group_of.get(op.guid)
+            if grp is not None:
+                if grp[0] is op:
+                    C(fwd, op.name + ".group_fwd",
+                      (lambda grp=grp: type(grp[0]).forward_group(grp, [self.ctx[o.guid] for o in grp])))
+                continue
+            C(fwd, op.name + ".fwd", (lambda op=op, c=c: self._fwd_op(op, c)))
 
-    def zero_gradients(self):
-        """Reference semantics (``model.cc:1146-1169``): gradients start at zero.  flexmi
-        kernels overwrite on first write, so this only resets the bookkeeping."""
-        self.grad_written = set()
-
-    def backward(self):
-        tm = self.timer
-        self.grad_written = set()
-        # 1. loss gradient (+ metrics) ----------------------------------------
-        with tm.scope("loss"):
-            self._loss_step(compute_grad=True)
-        self.grad_written.add(self.gkey(self.final.guid))
-        # 2. reverse ops ------------------------------------------------------
-        self.pending = {}
+        # ---------------- backward (accumulate flags resolved at compile time)
+        written = set()
+        self._emit_loss(bwd, compute_grad=True)
+        written.add(self.gkey(self.final.guid))
+        bucket_left = {}
         for g in self.groups:
             if g.replicated:
-                g.bucket_left = [len(b[2]) for b in g.buckets]
+                bucket_left[id(g)] = [len(b[2]) for b in g.buckets]
                 g.works = [None] * len(g.buckets)
         for st in self.bwd_steps:
             if st[0] == "op":
                 op = st[1]
                 c = self.ctx.get(op.guid)
                 if c is not None:
+                    flags = []
                     for i, t in enumerate(op.inputs):
-                        if c.in_grads[i] is not None and self.need[(op.guid, i)].same_as(self.home[t.guid]):
-                            c.in_grad_accumulate[i] = self.gkey(t.guid) in self.grad_written
-                        else:
-                            c.in_grad_accumulate[i] = False
-                    if all(g is None for g in c.out_grads) and not op.weights:
-                        pass
+                        same = c.in_grads[i] is not None and self.need[(op.guid, i)].same_as(self.home[t.guid])
+                        flags.append(bool(same and self.gkey(t.guid) in written))
                     for o in op.outputs:
-                        if o.guid in self.grad and self.gkey(o.guid) not in self.grad_written:
-                            self.grad[o.guid].zero_()   # unused output
-                            self.grad_written.add(self.gkey(o.guid))
+                        if o.guid in self.grad and self.gkey(o.guid) not in written:
+                            C(bwd, o.name + ".zero_unused_grad", (lambda t=self.grad[o.guid]: t.zero_()))
+                            written.add(self.gkey(o.guid))
                     grp = self.group_of.get(op.guid)
                     if grp is not None:
                         if grp[0] is op:
-                            with tm.scope(op.name + ".group_bwd"):
-                                type(op).backward_group(grp, [self.ctx[o.guid] for o in grp])
+                            C(bwd, op.name + ".group_bwd",
+                              (lambda grp=grp: type(grp[0]).backward_group(grp, [self.ctx[o.guid] for o in grp])))
                     else:
-                        with tm.scope(op.name + ".bwd"):
-                            op.backward(c)
+                        C(bwd, op.name + ".bwd", (lambda op=op, c=c, flags=flags: self._bwd_op(op, c, flags)))
                     for i, t in enumerate(op.inputs):
                         if c.in_grads[i] is not None and self.need[(op.guid, i)].same_as(self.home[t.guid]):
-                            self.grad_written.add(self.gkey(t.guid))
-                self._weights_done(op)
+                            written.add(self.gkey(t.guid))
+                # gradient buckets completed by this op -> async all-reduce (overlaps the rest of bwd)
+                for w in op.weights:
+                    e = self.wentries.get(w.guid)
+                    if e is None or e.group is None or not e.group.replicated:
+                        continue
+                    g = e.group
+                    for bi, b in enumerate(g.buckets):
+                        if w.guid in b[2]:
+                            bucket_left[id(g)][bi] -= 1
+                            if bucket_left[id(g)][bi] == 0 and self.cfg.overlap_grad_sync:
+                                bwd.append(Item("comm", (lambda g=g, bi=bi: self._launch_bucket(g, bi)),
+                                                f"allreduce.bucket{bi}"))
             else:
-                _, op, i, g, rs = st
-                src = self.tmp_grad.get((op.guid, i))
-                dst = self.grad.get(g)
-                acc = self.gkey(g) in self.grad_written
-                rs.run(self.comm, src, dst, accumulate=acc)
-                self.grad_written.add(self.gkey(g))
+                items, seen = [], set()
+                for op, i, g, rs in st[1]:
+                    key = self.gkey(g)
+                    items.append((rs, self.tmp_grad.get((op.guid, i)), self.grad.get(g), key in written or key in seen))
+                    seen.add(key)
+                self._emit_reshards(bwd, items, "reshard.bwd")
+                for op, i, g, rs in st[1]:
+                    written.add(self.gkey(g))
 
-    def _weights_done(self, op):
-        for w in op.weights:
-            e = self.wentries.get(w.guid)
-            if e is None or e.group is None or not e.group.replicated:
-                continue
-            g = e.group
-            for bi, b in enumerate(g.buckets):
-                if w.guid in b[2]:
-                    g.bucket_left[bi] -= 1
-                    if g.bucket_left[bi] == 0 and self.cfg.overlap_grad_sync:
-                        g.works[bi] = self.comm.all_reduce_async(g.gradbuf[b[0]:b[1]], g.holders)
+        # ---------------- update
+        if any(g.replicated for g in self.groups):
+            upd.append(Item("comm", self._sync_grads, "allreduce.wait"))
+        if self.optimizer is not None:
+            C(upd, "update", self._optimizer_step)
+        self.prog_fwd, self.prog_bwd, self.prog_upd = fwd, bwd, upd
+
+    def _fwd_op(self, op, c):
+        c.training = self.training
+        op.forward(c)
+
+    def _bwd_op(self, op, c, flags):
+        for i, f in enumerate(flags):
+            c.in_grad_accumulate[i] = f
+        op.backward(c)
+
+    def _emit_reshards(self, lst, items, name):
+        if not items:
+            return
+        if self.world == 1 or all(rs.local_only for rs, *_ in items):
+            lst.append(Item("compute", (lambda items=items: run_reshards(self.comm, items)), name))
+            return
+        ex = FusedExchange(items, self.world, self.rank)
+        lst.append(Item("compute", ex.pack, name + ".pack"))
+        lst.append(Item("comm", (lambda ex=ex: ex.exchange(self.comm)), name + ".a2a"))
+        lst.append(Item("compute", ex.unpack, name + ".unpack"))
+
+    def _emit_loss(self, lst, compute_grad):
+        if self.loss_type is None:
+            return
+        if self.loss_reshard is not None:
+            self._emit_reshards(lst, [(self.loss_reshard, self.local_buffer(self.final), self.logits_buf, False)],
+                                "loss.gather")
+        if self.logits_buf is not None:
+            lst.append(Item("compute", (lambda: self._loss_kernel(compute_grad)), "loss"))
+        if compute_grad and self.loss_reshard is not None:
+            self._emit_reshards(lst, [(self.loss_back, self.logit_grad, self.grad.get(self.final.guid), False)],
+                                "loss.scatter")
+
+    def _run(self, prog):
+        tm = self.timer
+        if tm.enabled:
+            for it in prog:
+                with tm.scope(it.name):
+                    it.fn()
+        else:
+            for it in prog:
+                it.fn()
+
+    def forward(self):
+        self._run(self.prog_fwd)
+
+    def zero_gradients(self):
+        """Reference semantics (``model.cc:1146-1169``): gradients start at zero.  flexmi
+        kernels overwrite on first write (decided when the program is compiled), so there is
+        nothing to clear."""
+        return None
+
+    def backward(self):
+        self._run(self.prog_bwd)
+
+    def update(self):
+        self._run(self.prog_upd)
+        if self.optimizer is not None:
+            self.optimizer.next()   # host mirror of the device-side step counters
+        self.step_count += 1
+
+    def _launch_bucket(self, g, bi):
+        b = g.buckets[bi]
+        g.works[bi] = self.comm.all_reduce_async(g.gradbuf[b[0]:b[1]], g.holders)
 
     def _sync_grads(self):
         for g in self.groups:
             if not g.replicated:
                 continue
             for bi, b in enumerate(g.buckets):
-                w = g.works[bi] if hasattr(g, "works") else None
+                w = g.works[bi]
                 if w is None:
                     w = self.comm.all_reduce_async(g.gradbuf[b[0]:b[1]], g.holders)
                 if w is not None:
                     w.wait()
                 g.works[bi] = None
 
-    def update(self):
+    def _optimizer_step(self):
         from flexmi.ops import _kernels as K
-        self._sync_grads()
         opt = self.optimizer
-        if opt is None:
-            return
-        opt.next()
-        with self.timer.scope("update"):
-            for g in self.groups:
-                if g.numel == 0:
-                    continue
-                if self.backend == "hip":
-                    if isinstance(opt, SGDOptimizer):
-                        K.sgd_update(g.master, g.gradbuf, g.state.get("v"), g.compute if g.compute is not g.master else None,
-                                     self.lr_tensor, opt.weight_decay, opt.momentum, opt.nesterov)
-                    else:
-                        K.adam_update(g.master, g.gradbuf, g.state["m"], g.state["v"],
-                                      g.compute if g.compute is not g.master else None,
-                                      opt.alpha_t, opt.beta1, opt.beta2, opt.weight_decay, opt.epsilon)
+        if isinstance(opt, AdamOptimizer):
+            # device-side bias-correction counters (capturable): [beta1^t, beta2^t, alpha_t]
+            st = self.adam_state
+            st[0:1].mul_(opt.beta1)
+            st[1:2].mul_(opt.beta2)
+            st[2:3].copy_(opt.alpha * torch.sqrt(1 - st[1:2]) / (1 - st[0:1]))
+        for g in self.groups:
+            if g.numel == 0:
+                continue
+            comp = g.compute if g.compute is not g.master else None
+            if self.backend == "hip":
+                if isinstance(opt, SGDOptimizer):
+                    K.sgd_update(g.master, g.gradbuf, g.state.get("v"), comp, self.lr_tensor, opt.weight_decay,
+                                 opt.momentum, opt.nesterov)
                 else:
-                    if isinstance(opt, SGDOptimizer):
-                        st = {"v": g.state["v"]} if "v" in g.state else {}
-                        gt = g.gradbuf + opt.weight_decay * g.master
-                        if opt.momentum > 0:
-                            st["v"].mul_(opt.momentum).add_(gt)
-                            gt = gt + opt.momentum * st["v"] if opt.nesterov else st["v"]
-                        g.master.sub_(self.lr_tensor * gt)
-                    else:
-                        opt.update_torch(g.master, g.gradbuf, g.state)
-                    if g.compute is not g.master:
-                        g.compute.copy_(g.master)
-        self.step_count += 1
+                    K.adam_update(g.master, g.gradbuf, g.state["m"], g.state["v"], comp, self.adam_state[2:3],
+                                  opt.beta1, opt.beta2, opt.weight_decay, opt.epsilon)
+            else:
+                if isinstance(opt, SGDOptimizer):
+                    gt = g.gradbuf + opt.weight_decay * g.master
+                    if opt.momentum > 0:
+                        v = g.state["v"]
+                        v.mul_(opt.momentum).add_(gt)
+                        gt = gt + opt.momentum * v if opt.nesterov else v
+                    g.master.sub_(self.lr_tensor * gt)
+                else:
+                    gt = g.gradbuf + opt.weight_decay * g.master
+                    m_, v_ = g.state["m"], g.state["v"]
+                    m_.mul_(opt.beta1).add_((1 - opt.beta1) * gt)
+                    v_.mul_(opt.beta2).add_((1 - opt.beta2) * gt * gt)
+                    g.master.sub_(self.adam_state[2] * m_ / (v_.sqrt() + opt.epsilon))
+                if comp is not None:
+                    comp.copy_(g.master)
 
     # ------------------------------------------------------------------ loss
-    def _loss_step(self, compute_grad):
+    def _loss_kernel(self, compute_grad):
         from flexmi.ops import _kernels as K
-        if self.loss_type is None:
-            return
-        if self.loss_reshard is not None:
-            self.loss_reshard.run(self.comm, self.local_buffer(self.final), self.logits_buf)
-        if self.logits_buf is not None:
-            scale = 1.0 / self.final.dims[0]
-            mask = self.metrics_obj.mask if self.metrics_obj else 0
-            if self.backend == "hip":
-                K.loss_forward_backward(int(self.loss_type), self.logits_buf, self.label_buf,
-                                        self.logit_grad if compute_grad else None, scale,
-                                        self.metric_acc, mask)
-            else:
-                loss_and_metrics_torch(self.loss_type, self.logits_buf, self.label_buf, self.logit_grad,
-                                       scale, self.metric_acc, mask, compute_grad)
-        if compute_grad and self.loss_reshard is not None:
-            self.loss_back.run(self.comm, self.logit_grad, self.grad.get(self.final.guid))
+        scale = 1.0 / self.final.dims[0]
+        mask = self.metrics_obj.mask if self.metrics_obj else 0
+        if self.backend == "hip":
+            K.loss_forward_backward(int(self.loss_type), self.logits_buf, self.label_buf,
+                                    self.logit_grad if compute_grad else None, scale, self.metric_acc, mask)
+        else:
+            loss_and_metrics_torch(self.loss_type, self.logits_buf, self.label_buf, self.logit_grad,
+                                   scale, self.metric_acc, mask, compute_grad)
 
     def compute_metrics(self):
-        self._loss_step(compute_grad=False)
+        if not hasattr(self, "prog_metrics"):
+            self.prog_metrics = []
+            self._emit_loss(self.prog_metrics, compute_grad=False)
+        self._run(self.prog_metrics)
 
     def reset_metrics(self):
         self.metric_acc.zero_()
@@ -737,28 +926,56 @@ class Executor:
     # ------------------------------------------------------------------ hipGraph
     def train_step(self):
         self.forward()
-        self.zero_gradients()
         self.backward()
         self.update()
 
-    def capture_step(self, warmup=2):
-        """Capture forward+backward+update into one hipGraph (static buffers)."""
+    def step_program(self):
+        return self.prog_fwd + self.prog_bwd + self.prog_upd
+
+    def capture_step(self, pre=None):
+        """Capture the training step as hipGraph segments split at the collectives.
+        ``pre``: optional compute callable (e.g. input staging) captured at the head.
+        Returns a callable that replays one step.  The caller must have run >= 1 eager step
+        (allocator warm-up, lazily created workspaces)."""
         assert self.backend == "hip"
+        prog = ([Item("compute", pre, "pre")] if pre is not None else []) + self.step_program()
+        segments = []
+        cur = []
+        for it in prog:
+            if it.kind == "compute":
+                cur.append(it)
+            else:
+                if cur:
+                    segments.append(("graph", cur))
+                    cur = []
+                segments.append(("comm", it))
+        if cur:
+            segments.append(("graph", cur))
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(warmup):
-                self.train_step()
+        runs = []
+        for kind, x in segments:
+            if kind == "graph":
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.stream(s):
+                    with torch.cuda.graph(g, stream=s):
+                        for it in x:
+                            it.fn()
+                runs.append(g.replay)
+            else:
+                runs.append(x.fn)
         torch.cuda.current_stream().wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self.train_step()
-        self._graph = g
-        return g
+        torch.cuda.synchronize()
+        self._graph_segments = segments
+        opt = self.optimizer
 
-    def replay(self):
-        self._graph.replay()
-        self.step_count += 1
+        def replay():
+            for r in runs:
+                r()
+            if opt is not None:
+                opt.next()
+            self.step_count += 1
+        return replay
 
     # ------------------------------------------------------------------ introspection
     def memory_report(self):

@@ -152,7 +152,7 @@ def test_sgd_adam(gpu):
     assert torch.allclose(Wc.float(), W, atol=2e-2)
     M_, V_ = torch.zeros(n, device=gpu), torch.zeros(n, device=gpu)
     W1 = W.clone()
-    Kk.adam_update(W, G, M_, V_, None, 0.01, 0.9, 0.999, 0.0, 1e-8)
+    Kk.adam_update(W, G, M_, V_, None, torch.tensor([0.01], device=gpu), 0.9, 0.999, 0.0, 1e-8)
     m = 0.1 * G
     vv = 0.001 * G * G
     assert torch.allclose(W, W1 - 0.01 * m / (vv.sqrt() + 1e-8), atol=1e-4)

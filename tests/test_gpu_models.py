@@ -84,6 +84,7 @@ def test_hip_graph_capture_matches_eager(gpu):
     for use_graph in (False, True):
         cfg = FFConfig()
         cfg.batchSize = 512
+        cfg.seed = 3
         m = FFModel(cfg)
         dcfg = DLRMConfig.preset("tiny")
         d, s, p = build_dlrm(m, dcfg)
@@ -93,15 +94,9 @@ def test_hip_graph_capture_matches_eager(gpu):
         data.next_batch()
         if use_graph:
             ex.train_step()
-            g = torch.cuda.CUDAGraph()
-            st = torch.cuda.Stream()
-            st.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(st):
-                with torch.cuda.graph(g, stream=st):
-                    ex.train_step()
-            torch.cuda.current_stream().wait_stream(st)
+            run = ex.capture_step()
             for _ in range(3):
-                g.replay()
+                run()
         else:
             for _ in range(4):
                 ex.train_step()
