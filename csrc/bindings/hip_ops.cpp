@@ -10,7 +10,12 @@
 extern "C" {
 int fm_gemm(const void* A, long lda, long sA, int a_kcontig, const void* B, long ldb, long sB, int b_kcontig, void* C,
             long ldc, long sC, int c_fp32, const float* bias, int M, int N, int K, int batch, float alpha, int beta,
-            int act, float* ws, long ws_bytes, int ksplit_req, hipStream_t stream);
+            int act, float* ws, long ws_bytes, int ksplit_req, const void* act_y, long lday, int bwd_act,
+            float* colsum, hipStream_t stream);
+void fm_skinny_fwd(const void* x, long ldx, const void* w, const float* bias, void* y, long ldy, long B, int K, int act,
+                   hipStream_t s);
+void fm_skinny_bwd(const void* x, long ldx, const void* w, const void* y, long ldy, const void* dy, long lddy, void* dx,
+                   long lddx, int dx_acc, float* dw, float* db, long B, int K, int act, hipStream_t s);
 void fm_init_fill(float* out, long rows, long cols, long r0, long c0, long ldg, int kind, unsigned seed, float a, float b,
                   hipStream_t s);
 void fm_embedding_fwd(const void* idx, int idx64, const float* W, void* out, int out_bf16, long B, int bag, int D, long ldo,
@@ -67,7 +72,8 @@ int is_bf16(const torch::Tensor& t) { return t.scalar_type() == torch::kBFloat16
 // ----------------------------------------------------------------------------- GEMM
 int gemm(torch::Tensor A, int64_t lda, int64_t sA, bool a_kcontig, torch::Tensor B, int64_t ldb, int64_t sB, bool b_kcontig,
          torch::Tensor C, int64_t ldc, int64_t sC, c10::optional<torch::Tensor> bias, int64_t M, int64_t N, int64_t K,
-         int64_t batch, double alpha, bool beta, int64_t act, c10::optional<torch::Tensor> ws, int64_t ksplit) {
+         int64_t batch, double alpha, bool beta, int64_t act, c10::optional<torch::Tensor> ws, int64_t ksplit,
+         c10::optional<torch::Tensor> act_y, int64_t lday, int64_t bwd_act, c10::optional<torch::Tensor> colsum) {
   check_cuda(A, "A");
   check_cuda(B, "B");
   check_cuda(C, "C");
@@ -84,6 +90,13 @@ int gemm(torch::Tensor A, int64_t lda, int64_t sA, bool a_kcontig, torch::Tensor
   if (bias.has_value() && bias->defined()) {
     TORCH_CHECK(bias->scalar_type() == torch::kFloat32 && bias->numel() >= N, "bias must be fp32 [N]");
   }
+  if (act_y.has_value() && act_y->defined()) {
+    TORCH_CHECK(act_y->scalar_type() == torch::kBFloat16 && batch == 1 && (M - 1) * lday + N <= act_y->numel(),
+                "gemm act_y: bf16 [M, >=N]");
+  }
+  if (colsum.has_value() && colsum->defined()) {
+    TORCH_CHECK(colsum->scalar_type() == torch::kFloat32 && colsum->numel() >= N && batch == 1, "gemm colsum: fp32 [N]");
+  }
   float* w = nullptr;
   long wsb = 0;
   if (ws.has_value() && ws->defined()) {
@@ -92,7 +105,22 @@ int gemm(torch::Tensor A, int64_t lda, int64_t sA, bool a_kcontig, torch::Tensor
   }
   return fm_gemm(A.data_ptr(), lda, sA, a_kcontig, B.data_ptr(), ldb, sB, b_kcontig, C.data_ptr(), ldc, sC,
                  C.scalar_type() == torch::kFloat32, bias.has_value() && bias->defined() ? bias->data_ptr<float>() : nullptr,
-                 (int)M, (int)N, (int)K, (int)batch, (float)alpha, beta ? 1 : 0, (int)act, w, wsb, (int)ksplit, cur());
+                 (int)M, (int)N, (int)K, (int)batch, (float)alpha, beta ? 1 : 0, (int)act, w, wsb, (int)ksplit,
+                 cptr(act_y), lday, (int)bwd_act, (float*)mptr(colsum), cur());
+}
+
+void skinny_fwd(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor y, int64_t act) {
+  TORCH_CHECK(w.numel() == x.size(1) && y.size(1) == 1 && x.stride(1) == 1, "skinny_fwd: x[B,K] w[1,K] y[B,1]");
+  fm_skinny_fwd(x.data_ptr(), x.stride(0), w.data_ptr(), bias.has_value() && bias->defined() ? bias->data_ptr<float>() : nullptr,
+                y.data_ptr(), y.stride(0), x.size(0), (int)x.size(1), (int)act, cur());
+}
+
+void skinny_bwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, torch::Tensor dy, c10::optional<torch::Tensor> dx, bool dx_acc,
+                torch::Tensor dw, c10::optional<torch::Tensor> db, int64_t act) {
+  TORCH_CHECK(w.numel() == x.size(1) && dw.numel() == x.size(1), "skinny_bwd: shapes");
+  long lddx = (dx.has_value() && dx->defined()) ? dx->stride(0) : 0;
+  fm_skinny_bwd(x.data_ptr(), x.stride(0), w.data_ptr(), y.data_ptr(), y.stride(0), dy.data_ptr(), dy.stride(0), mptr(dx), lddx,
+                dx_acc ? 1 : 0, dw.data_ptr<float>(), (float*)mptr(db), x.size(0), (int)x.size(1), (int)act, cur());
 }
 
 void init_fill(torch::Tensor out, int64_t rows, int64_t cols, int64_t r0, int64_t c0, int64_t ldg, int64_t kind, int64_t seed,
@@ -290,6 +318,8 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "flexmi HIP/CDNA4 kernels (gfx950)";
   m.def("gemm", &gemm);
   m.def("init_fill", &init_fill);
+  m.def("skinny_fwd", &skinny_fwd);
+  m.def("skinny_bwd", &skinny_bwd);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("embedding_fwd_multi", &embedding_fwd_multi);

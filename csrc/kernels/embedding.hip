@@ -118,11 +118,32 @@ __global__ void __launch_bounds__(256) fm_emb_bwd_lds_multi(TabSet s, const floa
   const long b0 = blockIdx.x * chunk, b1 = min(B, b0 + chunk);
   const GT* dy = reinterpret_cast<const GT*>(d.act);
   if (sub < rpi) {
-    for (long b = b0 + sub; b < b1; b += rpi)
-      for (int c = lc; c < d.D; c += lpr) {
-        const float g = ld<GT>(dy + b * d.ld + c);
-        for (int j = 0; j < d.bag; ++j) atomicAdd(acc + load_idx(d.idx, b * d.bag + j, d.idx64) * d.D + c, g);
-      }
+    if (d.bag == 1) {
+      // 8 independent (index, gradient) loads in flight per thread before the LDS adds: the loop
+      // is otherwise one dependent HBM round trip per sample
+      constexpr int U = 8;
+      for (long b = b0 + sub; b < b1; b += (long)rpi * U)
+        for (int c = lc; c < d.D; c += lpr) {
+          float g[U];
+          long r[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const long bb = b + (long)u * rpi;
+            const bool ok = bb < b1;
+            g[u] = ok ? ld<GT>(dy + bb * d.ld + c) : 0.f;
+            r[u] = ok ? load_idx(d.idx, bb, d.idx64) : 0;
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            if (b + (long)u * rpi < b1) atomicAdd(acc + r[u] * d.D + c, g[u]);
+        }
+    } else {
+      for (long b = b0 + sub; b < b1; b += rpi)
+        for (int c = lc; c < d.D; c += lpr) {
+          const float g = ld<GT>(dy + b * d.ld + c);
+          for (int j = 0; j < d.bag; ++j) atomicAdd(acc + load_idx(d.idx, b * d.bag + j, d.idx64) * d.D + c, g);
+        }
+    }
   }
   __syncthreads();
   const float mul = (lr ? -lr[0] : 1.f) * d.scale;

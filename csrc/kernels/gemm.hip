@@ -129,6 +129,11 @@ struct GemmP {
   void* C; long ldc; long sC;
   const float* bias;
   float* ws;          // split-K slabs [batch][split][M][N]
+  // fused backward epilogue of the producing layer below: v = act'(ay) * v ; colsum[n] += sum_m v
+  const unsigned short* ay;
+  long lday;
+  float* colsum;
+  int bact;
   int M, N, K, act, beta, c_fp32, ksplit, batch;
   float alpha;
   int tiles_m, tiles_n;
@@ -241,23 +246,49 @@ __global__ void __launch_bounds__(NT, 2) fm_gemm_kernel(GemmP p) {
       }
     return;
   }
+  float csum[NR][4];
+#pragma unroll
+  for (int j = 0; j < NR; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) csum[j][r] = 0.f;
 #pragma unroll
   for (int i = 0; i < MR; ++i)
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
-      int m = m0 + wm * (BM / 2) + 16 * i + mrow;
-      int n = n0 + wn * (BN / 2) + 16 * j + ncol;
-      if (m >= p.M) continue;
+      const int m = m0 + wm * (BM / 2) + 16 * i + mrow;
+      const int n = n0 + wn * (BN / 2) + 16 * j + ncol;
+      const bool mok = m < p.M;
+      const bool full = (n + 3 < p.N);
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * p.alpha;
-      const bool full = (n + 3 < p.N);
       if (p.bias) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] += (n + r < p.N) ? p.bias[n + r] : 0.f;
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = act_fwd(p.act, v[r]);
+      if (p.ay) {  // fused activation backward of the layer below (dX -> dpre)
+        float yv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (mok) {
+          const unsigned short* yp = p.ay + (long)m * p.lday + n;
+          if (full && ((p.lday & 3) == 0)) {
+            bf16x4_t t = *reinterpret_cast<const bf16x4_t*>(yp);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) yv[r] = bf2f((unsigned short)t[r]);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) yv[r] = (n + r < p.N) ? bf2f(yp[r]) : 0.f;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = act_bwd(p.bact, yv[r], v[r]);
+      }
+      if (p.colsum && mok) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) csum[j][r] += (n + r < p.N) ? v[r] : 0.f;
+      }
+      if (!mok) continue;
       if (p.c_fp32) {
         float* dst = reinterpret_cast<float*>(p.C) + (long)zb * p.sC + (long)m * p.ldc + n;
         if (full && ((p.ldc & 3) == 0) && ((((uintptr_t)dst) & 15) == 0)) {
@@ -286,6 +317,20 @@ __global__ void __launch_bounds__(NT, 2) fm_gemm_kernel(GemmP p) {
         }
       }
     }
+  if (p.colsum) {  // bias gradient of the layer below: reduce the 16 rows of each lane group, 1 atomic/col
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float x = csum[j][r];
+        x += __shfl_xor(x, 1, 64);
+        x += __shfl_xor(x, 2, 64);
+        x += __shfl_xor(x, 4, 64);
+        x += __shfl_xor(x, 8, 64);
+        const int n = n0 + wn * (BN / 2) + 16 * j + ncol + r;
+        if (mrow == 0 && n < p.N) atomicAdd(p.colsum + n, x);
+      }
+  }
 }
 
 __global__ void fm_gemm_splitk_reduce(GemmP p) {
@@ -342,6 +387,7 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
                        void* C, long ldc, long sC, int c_fp32,
                        const float* bias, int M, int N, int K, int batch,
                        float alpha, int beta, int act, float* ws, long ws_bytes, int ksplit_req,
+                       const void* act_y, long lday, int bwd_act, float* colsum,
                        hipStream_t stream) {
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
   GemmP p;
@@ -350,6 +396,7 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
   p.C = C; p.ldc = ldc; p.sC = sC;
   p.bias = bias; p.M = M; p.N = N; p.K = K; p.act = act; p.beta = beta; p.c_fp32 = c_fp32;
   p.alpha = alpha; p.batch = batch; p.ws = ws;
+  p.ay = (const unsigned short*)act_y; p.lday = lday; p.bact = bwd_act; p.colsum = colsum;
   // vector (16-B) loads need the contiguous extent and leading dims to be multiples of 8
   auto al = [](const void* q) { return (((uintptr_t)q) & 15) == 0; };
   bool vec = al(A) && al(B) && (lda % 8 == 0) && (ldb % 8 == 0) && (sA % 8 == 0) && (sB % 8 == 0);
@@ -365,8 +412,9 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
   int ks = 1;
   if (ksplit_req > 0) ks = ksplit_req;
   else if (ws != nullptr) {
-    while (tiles * ks < 512 && ks * 2 <= ktiles / 2 && ks < 16) ks *= 2;
+    while (tiles * ks < 256 && ks * 2 <= ktiles / 2 && ks < 16) ks *= 2;
   }
+  if (act_y != nullptr || colsum != nullptr) ks = 1;  // fused bwd epilogue needs the full K sum
   if (ks > 1) {
     long need = (long)batch * ks * M * (long)N * 4;
     if (ws == nullptr || need > ws_bytes) ks = 1;
@@ -382,4 +430,97 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
     hipLaunchKernelGGL(fm_gemm_splitk_reduce, dim3(fm_grid(total)), dim3(256), 0, stream, p);
   }
   return p.ksplit;
+}
+
+// ------------------------------------------------------------------------------------------
+// Skinny layers (out_features == 1, e.g. the DLRM click-probability layer): an MFMA tile would be
+// 1/128 utilised and the transposed dW path degenerates to scalar loads, so these run as
+// bandwidth-bound GEMV / outer-product / column-reduction kernels instead.
+namespace {
+
+__global__ void __launch_bounds__(256) fm_skinny_fwd_kernel(const unsigned short* __restrict__ x, long ldx,
+                                                           const unsigned short* __restrict__ w,
+                                                           const float* __restrict__ bias, unsigned short* __restrict__ y,
+                                                           long ldy, long B, int K, int act) {
+  const int lane = threadIdx.x & 63;
+  const long waves = (long)gridDim.x * 4;
+  const bool vec = (K % 4 == 0) && (ldx % 4 == 0);
+  for (long b = blockIdx.x * 4 + (threadIdx.x >> 6); b < B; b += waves) {
+    const unsigned short* xr = x + b * ldx;
+    float s = 0.f;
+    if (vec) {
+      for (int k = lane * 4; k < K; k += 256) {
+        bf16x4_t a = *reinterpret_cast<const bf16x4_t*>(xr + k);
+        bf16x4_t c = *reinterpret_cast<const bf16x4_t*>(w + k);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s += bf2f((unsigned short)a[j]) * bf2f((unsigned short)c[j]);
+      }
+    } else {
+      for (int k = lane; k < K; k += 64) s += bf2f(xr[k]) * bf2f(w[k]);
+    }
+    s = wave_reduce_sum(s);
+    if (lane == 0) y[b * ldy] = f2bf(act_fwd(act, s + (bias ? bias[0] : 0.f)));
+  }
+}
+
+template <int ROWS>
+__global__ void __launch_bounds__(256) fm_skinny_bwd_kernel(const unsigned short* __restrict__ x, long ldx,
+                                                           const unsigned short* __restrict__ w,
+                                                           const unsigned short* __restrict__ y, long ldy,
+                                                           const unsigned short* __restrict__ dy, long lddy,
+                                                           unsigned short* __restrict__ dx, long lddx, int dx_acc,
+                                                           float* __restrict__ dw, float* __restrict__ db, long B, int K,
+                                                           int act) {
+  const int groups = (K + 7) / 8;                 // 8 columns per thread
+  const int lpr = groups < 256 ? groups : 256;    // threads per row
+  const int rpi = 256 / lpr;
+  const int sub = threadIdx.x / lpr, g = threadIdx.x - sub * lpr;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float dbs = 0.f;
+  const long r0 = (long)blockIdx.x * ROWS;
+  if (sub < rpi) {
+    for (long r = r0 + sub; r < min(B, r0 + ROWS); r += rpi) {
+      const float d = act_bwd(act, bf2f(y[r * ldy]), bf2f(dy[r * lddy]));
+      if (g == 0) dbs += d;
+      for (int c0 = g * 8; c0 < K; c0 += lpr * 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int c = c0 + j;
+          if (c < K) {
+            if (dx) {
+              float v = d * bf2f(w[c]);
+              if (dx_acc) v += bf2f(dx[r * lddx + c]);
+              dx[r * lddx + c] = f2bf(v);
+            }
+            if (c0 == g * 8) acc[j] += d * bf2f(x[r * ldx + c]);
+          }
+        }
+      }
+    }
+  }
+  if (sub < rpi) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (g * 8 + j < K && acc[j] != 0.f) atomicAdd(dw + g * 8 + j, acc[j]);
+    if (g == 0 && db && dbs != 0.f) atomicAdd(db, dbs);
+  }
+}
+
+}  // namespace
+
+extern "C" void fm_skinny_fwd(const void* x, long ldx, const void* w, const float* bias, void* y, long ldy, long B, int K,
+                              int act, hipStream_t s) {
+  if (B <= 0) return;
+  hipLaunchKernelGGL(fm_skinny_fwd_kernel, dim3((unsigned)std::min<long>((B + 3) / 4, 4096)), dim3(256), 0, s,
+                     (const unsigned short*)x, ldx, (const unsigned short*)w, bias, (unsigned short*)y, ldy, B, K, act);
+}
+
+// dW (fp32 [K]) and db (fp32 [1]) are ACCUMULATED (callers zero them); requires K <= 2048
+extern "C" void fm_skinny_bwd(const void* x, long ldx, const void* w, const void* y, long ldy, const void* dy, long lddy,
+                              void* dx, long lddx, int dx_acc, float* dw, float* db, long B, int K, int act, hipStream_t s) {
+  if (B <= 0) return;
+  constexpr int ROWS = 32;
+  hipLaunchKernelGGL((fm_skinny_bwd_kernel<ROWS>), dim3((unsigned)((B + ROWS - 1) / ROWS)), dim3(256), 0, s,
+                     (const unsigned short*)x, ldx, (const unsigned short*)w, (const unsigned short*)y, ldy,
+                     (const unsigned short*)dy, lddy, (unsigned short*)dx, lddx, dx_acc, dw, db, B, K, act);
 }

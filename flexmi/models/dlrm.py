@@ -118,14 +118,17 @@ def create_emb(model, idx, rows, dim, i):
                            name=f"embedding{i}")
 
 
-def build_dlrm(model, c: DLRMConfig):
+def build_dlrm(model, c: DLRMConfig, pad_dense=True):
     """Returns (dense_input, sparse_inputs, output).  Dense input is padded to a multiple of 8
     columns (zeros) so its GEMM uses 16-B vector loads; the padding does not change the model."""
     B = model.config.batchSize
     sparse = [model.create_tensor([B, c.embedding_bag_size], DataType.DT_INT64, name=f"sparse{i}")
               for i in range(len(c.embedding_size))]
-    dense_in = model.create_tensor([B, c.mlp_bot[0]], DataType.DT_FLOAT, name="dense")
     bot = list(c.mlp_bot)
+    if pad_dense and model.config.device == "gpu":
+        bot[0] = (bot[0] + 7) // 8 * 8   # 13 -> 16: 16-B aligned rows for the first GEMM (pad columns are 0)
+    dense_in = model.create_tensor([B, bot[0]], DataType.DT_FLOAT, name="dense")
+    dense_in.real_features = c.mlp_bot[0]
     x = create_mlp(model, dense_in, bot, c.sigmoid_bot)
     ly = [create_emb(model, sparse[i], c.embedding_size[i], c.sparse_feature_size, i) for i in range(len(sparse))]
     if c.arch_interaction_op == "cat":
@@ -192,7 +195,10 @@ class SyntheticDLRMData:
                                                dtype=buf.dtype)
         buf = ex.local_buffer(dense_in)
         if buf is not None:
-            self.pools[dense_in.guid] = torch.rand((num_batches,) + tuple(buf.shape), generator=g, device=dev).to(buf.dtype)
+            pool = torch.rand((num_batches,) + tuple(buf.shape), generator=g, device=dev)
+            nreal = getattr(dense_in, "real_features", buf.shape[1])
+            pool[..., nreal:] = 0.0        # zero padding columns: the model is unchanged
+            self.pools[dense_in.guid] = pool.to(buf.dtype)
         lab = model.get_label_tensor()
         lbuf = ex.local_buffer(lab)
         if lbuf is not None:

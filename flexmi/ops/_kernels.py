@@ -58,10 +58,13 @@ GEMM_WS_BYTES = 64 << 20
 
 
 def gemm(A, lda, a_kcontig, B, ldb, b_kcontig, Cout, ldc, M, N, K, bias=None, act=10, beta=False, alpha=1.0,
-         batch=1, sA=0, sB=0, sC=0, ksplit=0, use_ws=True):
+         batch=1, sA=0, sB=0, sC=0, ksplit=0, use_ws=True, act_y=None, bwd_act=10, colsum=None):
+    """C = epi(A·B).  Optional fused backward epilogue of the layer below (act_y/bwd_act/colsum):
+    C = act'(act_y) * (A·B) and colsum += column sums of C (its bias gradient)."""
     ws = workspace(Cout.device, GEMM_WS_BYTES) if use_ws else None
+    lday = act_y.stride(0) if act_y is not None else 0
     return C().gemm(A, lda, sA, a_kcontig, B, ldb, sB, b_kcontig, Cout, ldc, sC, bias, M, N, K, batch, alpha, beta, act,
-                    ws, ksplit)
+                    ws, ksplit, act_y, lday, bwd_act, colsum)
 
 
 # ------------------------------------------------------------------ init
@@ -87,28 +90,48 @@ def linear_forward(x2, w, b, act, y2):
     assert x2.stride(1) == 1 and y2.stride(1) == 1 and w.is_contiguous()
     M, K = x2.shape
     N = w.shape[0]
+    if N == 1:
+        C().skinny_fwd(x2, w, b, y2, act)
+        return
     gemm(x2, x2.stride(0), True, w, K, True, y2, y2.stride(0), M, N, K, bias=b, act=act)
 
 
-def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws):
+def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=False, fuse_below=None):
+    """Weight/bias grads ACCUMULATE into dw/db (the executor zeroes the flat gradient buffer once
+    per step).  grad_is_dpre: dy2 already holds act'(y)*dy and db was produced by the consumer's
+    fused GEMM epilogue.  fuse_below = (y_below, act_below, db_below): apply the activation
+    backward of the layer below (and its bias grad) in this layer's dX GEMM epilogue."""
     M, K = x2.shape
     N = w.shape[0]
-    if act != 10:
-        dpre = ws.get("dpre")
-        if dpre is None or dpre.shape != (M, N):
-            dpre = torch.empty((M, N), dtype=torch.bfloat16, device=x2.device)
-            ws["dpre"] = dpre
-    else:
+    if N == 1:
+        C().skinny_bwd(x2, w, y2, dy2, dx2, bool(dx_acc), dw, None if grad_is_dpre else db,
+                       10 if grad_is_dpre else act)
+        if dx2 is not None and fuse_below is not None:
+            raise AssertionError("no fused epilogue on the skinny path")
+        return
+    if grad_is_dpre:
         dpre = dy2
-    if db is not None:
-        db.zero_()
-    if act != 10 or db is not None:
-        C().act_bwd_bias(y2 if act != 10 else dy2, dy2, dpre if act != 10 else None, db, M, N, act)
+    else:
+        if act != 10:
+            dpre = ws.get("dpre")
+            if dpre is None or dpre.shape != (M, N):
+                dpre = torch.empty((M, N), dtype=torch.bfloat16, device=x2.device)
+                ws["dpre"] = dpre
+        else:
+            dpre = dy2
+        if act != 10 or db is not None:
+            C().act_bwd_bias(y2 if act != 10 else dy2, dy2, dpre if act != 10 else None, db, M, N, act)
     # dW[N,K] = dpre^T x   (both operands MN-contiguous: transposing LDS reads)
     gemm(dpre, dpre.stride(0), False, x2, x2.stride(0), False, dw, K, N, K, M)
-    # dX[M,K] = dpre W
+    # dX[M,K] = dpre W   (+ fused act-bwd / bias-grad of the layer below)
     if dx2 is not None:
-        gemm(dpre, dpre.stride(0), True, w, K, False, dx2, dx2.stride(0), M, K, N, beta=bool(dx_acc))
+        if fuse_below is not None:
+            yb, actb, dbb = fuse_below
+            assert not dx_acc
+            gemm(dpre, dpre.stride(0), True, w, K, False, dx2, dx2.stride(0), M, K, N,
+                 act_y=yb.view(M, K), bwd_act=int(actb), colsum=dbb)
+        else:
+            gemm(dpre, dpre.stride(0), True, w, K, False, dx2, dx2.stride(0), M, K, N, beta=bool(dx_acc))
 
 
 def bmm(a, b, out, transA, transB, acc):

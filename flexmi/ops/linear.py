@@ -117,12 +117,12 @@ class Linear(Op):
         if ctx.hip:
             K.linear_backward(x2, ctx.wcompute[0], y2, dy2, int(act), dx2,
                               bool(ctx.in_grad_accumulate[0]) if dx2 is not None else False, dw, db,
-                              ctx.workspace)
+                              ctx.workspace, ctx.saved.get("grad_is_dpre", False), ctx.saved.get("fuse_below"))
         else:
             dpre = act_backward_torch(dy2.float(), y2.float(), act)
-            dw.copy_(dpre.t() @ x2.float())
+            dw.add_(dpre.t() @ x2.float())
             if db is not None:
-                db.copy_(dpre.sum(0))
+                db.add_(dpre.sum(0))
             if dx2 is not None:
                 store(dx2, dpre @ ctx.wcompute[0].float(), ctx.in_grad_accumulate[0])
 

@@ -443,8 +443,32 @@ class Executor:
             op.prepare(c)
             self.ctx[op.guid] = c
         self._build_groups(ops)
+        self._build_epilogue_fusion(ops)
         self.adam_state = torch.tensor([1.0, 1.0, 0.0], dtype=torch.float32, device=self.device)
         self._compile_program()
+
+    def _build_epilogue_fusion(self, ops):
+        """Linear L1 -> Linear L2 (L1's output consumed only by L2, same layout): L2's dX GEMM
+        epilogue applies L1's activation backward and accumulates L1's bias gradient, so L1 skips
+        its separate act-bwd/bias-grad pass (one full read+write of the activation gradient)."""
+        from flexmi.core.types import ActiMode, OperatorType
+        if self.backend != "hip" or self.cdtype != torch.bfloat16:
+            return
+        for op in ops:
+            if op.op_type != OperatorType.OP_LINEAR or getattr(op, "skip_act_grad", False):
+                continue
+            c1 = self.ctx.get(op.guid)
+            t = op.outputs[0]
+            cons = self.consumers.get(t.guid, [])
+            if c1 is None or len(cons) != 1 or t is self.final:
+                continue
+            l2, idx = cons[0]
+            c2 = self.ctx.get(l2.guid)
+            if (l2.op_type != OperatorType.OP_LINEAR or c2 is None or l2.out_dim == 1 or op.out_dim == 1
+                    or not self.need[(l2.guid, idx)].same_as(self.home[t.guid]) or c2.in_grads[0] is None):
+                continue
+            c2.saved["fuse_below"] = (c1.outputs[0], op.activation, c1.weight_grads[1] if op.use_bias else None)
+            c1.saved["grad_is_dpre"] = True
 
     def _build_groups(self, ops):
         """Fuse independent ops of the same kind and placement into one launch (embedding
@@ -646,6 +670,9 @@ class Executor:
 
         # ---------------- backward (accumulate flags resolved at compile time)
         written = set()
+        for g in self.groups:   # weight/bias grads accumulate (atomics in fused epilogues): one memset
+            if g.numel:
+                C(bwd, "zero_grads", (lambda g=g: g.gradbuf.zero_()))
         self._emit_loss(bwd, compute_grad=True)
         written.add(self.gkey(self.final.guid))
         bucket_left = {}
