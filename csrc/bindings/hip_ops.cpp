@@ -11,7 +11,7 @@ extern "C" {
 int fm_gemm(const void* A, long lda, long sA, int a_kcontig, const void* B, long ldb, long sB, int b_kcontig, void* C,
             long ldc, long sC, int c_fp32, const float* bias, int M, int N, int K, int batch, float alpha, int beta,
             int act, float* ws, long ws_bytes, int ksplit_req, const void* act_y, long lday, int bwd_act,
-            float* colsum, hipStream_t stream);
+            float* colsum, float* rowsum_a, hipStream_t stream);
 void fm_skinny_fwd(const void* x, long ldx, const void* w, const float* bias, void* y, long ldy, long B, int K, int act,
                    hipStream_t s);
 void fm_skinny_bwd(const void* x, long ldx, const void* w, const void* y, long ldy, const void* dy, long lddy, void* dx,
@@ -73,7 +73,8 @@ int is_bf16(const torch::Tensor& t) { return t.scalar_type() == torch::kBFloat16
 int gemm(torch::Tensor A, int64_t lda, int64_t sA, bool a_kcontig, torch::Tensor B, int64_t ldb, int64_t sB, bool b_kcontig,
          torch::Tensor C, int64_t ldc, int64_t sC, c10::optional<torch::Tensor> bias, int64_t M, int64_t N, int64_t K,
          int64_t batch, double alpha, bool beta, int64_t act, c10::optional<torch::Tensor> ws, int64_t ksplit,
-         c10::optional<torch::Tensor> act_y, int64_t lday, int64_t bwd_act, c10::optional<torch::Tensor> colsum) {
+         c10::optional<torch::Tensor> act_y, int64_t lday, int64_t bwd_act, c10::optional<torch::Tensor> colsum,
+         c10::optional<torch::Tensor> rowsum_a) {
   check_cuda(A, "A");
   check_cuda(B, "B");
   check_cuda(C, "C");
@@ -94,6 +95,10 @@ int gemm(torch::Tensor A, int64_t lda, int64_t sA, bool a_kcontig, torch::Tensor
     TORCH_CHECK(act_y->scalar_type() == torch::kBFloat16 && batch == 1 && (M - 1) * lday + N <= act_y->numel(),
                 "gemm act_y: bf16 [M, >=N]");
   }
+  if (rowsum_a.has_value() && rowsum_a->defined()) {
+    TORCH_CHECK(!a_kcontig && rowsum_a->scalar_type() == torch::kFloat32 && rowsum_a->numel() >= M && batch == 1,
+                "gemm rowsum_a: fp32 [M], MN-contiguous A");
+  }
   if (colsum.has_value() && colsum->defined()) {
     TORCH_CHECK(colsum->scalar_type() == torch::kFloat32 && colsum->numel() >= N && batch == 1, "gemm colsum: fp32 [N]");
   }
@@ -106,7 +111,7 @@ int gemm(torch::Tensor A, int64_t lda, int64_t sA, bool a_kcontig, torch::Tensor
   return fm_gemm(A.data_ptr(), lda, sA, a_kcontig, B.data_ptr(), ldb, sB, b_kcontig, C.data_ptr(), ldc, sC,
                  C.scalar_type() == torch::kFloat32, bias.has_value() && bias->defined() ? bias->data_ptr<float>() : nullptr,
                  (int)M, (int)N, (int)K, (int)batch, (float)alpha, beta ? 1 : 0, (int)act, w, wsb, (int)ksplit,
-                 cptr(act_y), lday, (int)bwd_act, (float*)mptr(colsum), cur());
+                 cptr(act_y), lday, (int)bwd_act, (float*)mptr(colsum), (float*)mptr(rowsum_a), cur());
 }
 
 void skinny_fwd(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor y, int64_t act) {
@@ -118,6 +123,7 @@ void skinny_fwd(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> b
 void skinny_bwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, torch::Tensor dy, c10::optional<torch::Tensor> dx, bool dx_acc,
                 torch::Tensor dw, c10::optional<torch::Tensor> db, int64_t act) {
   TORCH_CHECK(w.numel() == x.size(1) && dw.numel() == x.size(1), "skinny_bwd: shapes");
+  TORCH_CHECK(x.size(1) % 8 == 0 && x.size(1) <= 2048 && x.stride(0) % 8 == 0, "skinny_bwd: K % 8 == 0, K <= 2048");
   long lddx = (dx.has_value() && dx->defined()) ? dx->stride(0) : 0;
   fm_skinny_bwd(x.data_ptr(), x.stride(0), w.data_ptr(), y.data_ptr(), y.stride(0), dy.data_ptr(), dy.stride(0), mptr(dx), lddx,
                 dx_acc ? 1 : 0, dw.data_ptr<float>(), (float*)mptr(db), x.size(0), (int)x.size(1), (int)act, cur());

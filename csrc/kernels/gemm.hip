@@ -99,6 +99,21 @@ struct Stage {
       *reinterpret_cast<u32x4_t*>(lds + lds_off<KC, R>(a, c)) = v[i];
     }
   }
+
+  // MN-contiguous operand: every chunk a thread loads covers the SAME 8 rows (tid % (R/8)),
+  // so summing the staged chunks over k gives per-row partial sums for free (bias gradient
+  // db[n] = sum_b dpre[b][n] computed inside the dW GEMM, no extra pass over dpre).
+  FM_DEVICE void accumulate_rows(float (&s)[8]) const {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const unsigned w[4] = {v[i][0], v[i][1], v[i][2], v[i][3]};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s[2 * j] += bf2f((unsigned short)(w[j] & 0xFFFF));
+        s[2 * j + 1] += bf2f((unsigned short)(w[j] >> 16));
+      }
+    }
+  }
 };
 
 // ---- LDS -> MFMA fragment (8 bf16: k = 8*(lane>>4)+j for row/col lane&15) -------------
@@ -133,6 +148,7 @@ struct GemmP {
   const unsigned short* ay;
   long lday;
   float* colsum;
+  float* rowsum_a;   // += sum_k A(m,k)  (MN-contiguous A only; used for bias grads in dW GEMMs)
   int bact;
   int M, N, K, act, beta, c_fp32, ksplit, batch;
   float alpha;
@@ -183,11 +199,14 @@ __global__ void __launch_bounds__(NT, 2) fm_gemm_kernel(GemmP p) {
 
   Stage<AK, BM, VEC> sa;
   Stage<BKC, BN, VEC> sb;
+  const bool rowsum = (!AK) && (p.rowsum_a != nullptr) && (tn == 0);
+  float rs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (kt0 < kt1) {
     sa.load(A, p.lda, m0, p.M, kt0 * BK, p.K, tid);
     sb.load(B, p.ldb, n0, p.N, kt0 * BK, p.K, tid);
     sa.store(LDS_A(0), tid);
     sb.store(LDS_B(0), tid);
+    if (rowsum) sa.accumulate_rows(rs);
   }
   __syncthreads();
 
@@ -218,8 +237,24 @@ __global__ void __launch_bounds__(NT, 2) fm_gemm_kernel(GemmP p) {
     if (more) {
       sa.store(LDS_A(cur ^ 1), tid);
       sb.store(LDS_B(cur ^ 1), tid);
+      if (rowsum) sa.accumulate_rows(rs);
     }
     __syncthreads();
+  }
+  if constexpr (!AK) {
+    if (rowsum) {  // reduce the NT/(BM/8) threads that share each 8-row group, then 1 atomic per row
+      float* red = reinterpret_cast<float*>(smem);   // LDS is free after the K loop
+      constexpr int G = BM / 8;                      // row groups
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[(tid / G) * BM + (tid % G) * 8 + j] = rs[j];
+      __syncthreads();
+      if (tid < BM) {
+        float x = 0.f;
+        for (int t = 0; t < NT / G; ++t) x += red[t * BM + tid];
+        if (m0 + tid < p.M) atomicAdd(p.rowsum_a + m0 + tid, x);
+      }
+      __syncthreads();
+    }
   }
 
 #undef LDS_A
@@ -387,7 +422,7 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
                        void* C, long ldc, long sC, int c_fp32,
                        const float* bias, int M, int N, int K, int batch,
                        float alpha, int beta, int act, float* ws, long ws_bytes, int ksplit_req,
-                       const void* act_y, long lday, int bwd_act, float* colsum,
+                       const void* act_y, long lday, int bwd_act, float* colsum, float* rowsum_a,
                        hipStream_t stream) {
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
   GemmP p;
@@ -396,7 +431,7 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
   p.C = C; p.ldc = ldc; p.sC = sC;
   p.bias = bias; p.M = M; p.N = N; p.K = K; p.act = act; p.beta = beta; p.c_fp32 = c_fp32;
   p.alpha = alpha; p.batch = batch; p.ws = ws;
-  p.ay = (const unsigned short*)act_y; p.lday = lday; p.bact = bwd_act; p.colsum = colsum;
+  p.ay = (const unsigned short*)act_y; p.lday = lday; p.bact = bwd_act; p.colsum = colsum; p.rowsum_a = rowsum_a;
   // vector (16-B) loads need the contiguous extent and leading dims to be multiples of 8
   auto al = [](const void* q) { return (((uintptr_t)q) & 15) == 0; };
   bool vec = al(A) && al(B) && (lda % 8 == 0) && (ldb % 8 == 0) && (sA % 8 == 0) && (sB % 8 == 0);
@@ -471,38 +506,54 @@ __global__ void __launch_bounds__(256) fm_skinny_bwd_kernel(const unsigned short
                                                            unsigned short* __restrict__ dx, long lddx, int dx_acc,
                                                            float* __restrict__ dw, float* __restrict__ db, long B, int K,
                                                            int act) {
-  const int groups = (K + 7) / 8;                 // 8 columns per thread
-  const int lpr = groups < 256 ? groups : 256;    // threads per row
+  // thread = 8 consecutive columns (16-B loads/stores) of rows sub, sub+rpi, ...; per-block
+  // partial dW/db reduced in LDS -> one atomic per column per block (B/ROWS adders per address)
+  __shared__ float red[256 * 8];
+  __shared__ float redb[256];
+  const int groups = K / 8;                       // host guarantees K % 8 == 0, K <= 2048
+  const int lpr = groups;                         // threads per row
   const int rpi = 256 / lpr;
   const int sub = threadIdx.x / lpr, g = threadIdx.x - sub * lpr;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float dbs = 0.f;
   const long r0 = (long)blockIdx.x * ROWS;
+  const int c0 = g * 8;
+  bf16x8_t wv = *reinterpret_cast<const bf16x8_t*>(w + c0);
   if (sub < rpi) {
     for (long r = r0 + sub; r < min(B, r0 + ROWS); r += rpi) {
       const float d = act_bwd(act, bf2f(y[r * ldy]), bf2f(dy[r * lddy]));
-      if (g == 0) dbs += d;
-      for (int c0 = g * 8; c0 < K; c0 += lpr * 8) {
+      dbs += d;
+      bf16x8_t xv = *reinterpret_cast<const bf16x8_t*>(x + r * ldx + c0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += d * bf2f((unsigned short)xv[j]);
+      if (dx) {
+        unsigned short* dp = dx + r * lddx + c0;
+        bf16x8_t o;
+        bf16x8_t old = dx_acc ? *reinterpret_cast<const bf16x8_t*>(dp) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const int c = c0 + j;
-          if (c < K) {
-            if (dx) {
-              float v = d * bf2f(w[c]);
-              if (dx_acc) v += bf2f(dx[r * lddx + c]);
-              dx[r * lddx + c] = f2bf(v);
-            }
-            if (c0 == g * 8) acc[j] += d * bf2f(x[r * ldx + c]);
-          }
+          float v = d * bf2f((unsigned short)wv[j]);
+          if (dx_acc) v += bf2f((unsigned short)old[j]);
+          o[j] = (short)f2bf(v);
         }
+        *reinterpret_cast<bf16x8_t*>(dp) = o;
       }
     }
   }
-  if (sub < rpi) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (g * 8 + j < K && acc[j] != 0.f) atomicAdd(dw + g * 8 + j, acc[j]);
-    if (g == 0 && db && dbs != 0.f) atomicAdd(db, dbs);
+  for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = (sub < rpi) ? acc[j] : 0.f;
+  redb[threadIdx.x] = (sub < rpi && g == 0) ? dbs : 0.f;
+  __syncthreads();
+  for (int c = threadIdx.x; c < K; c += 256) {
+    const int gg = c / 8, j = c % 8;
+    float t = 0.f;
+    for (int q = 0; q < rpi; ++q) t += red[(q * lpr + gg) * 8 + j];
+    atomicAdd(dw + c, t);
+  }
+  if (db && threadIdx.x == 0) {
+    float t = 0.f;
+    for (int q = 0; q < rpi; ++q) t += redb[q * lpr];
+    atomicAdd(db, t);
   }
 }
 
@@ -519,7 +570,7 @@ extern "C" void fm_skinny_fwd(const void* x, long ldx, const void* w, const floa
 extern "C" void fm_skinny_bwd(const void* x, long ldx, const void* w, const void* y, long ldy, const void* dy, long lddy,
                               void* dx, long lddx, int dx_acc, float* dw, float* db, long B, int K, int act, hipStream_t s) {
   if (B <= 0) return;
-  constexpr int ROWS = 32;
+  constexpr int ROWS = 256;
   hipLaunchKernelGGL((fm_skinny_bwd_kernel<ROWS>), dim3((unsigned)((B + ROWS - 1) / ROWS)), dim3(256), 0, s,
                      (const unsigned short*)x, ldx, (const unsigned short*)w, (const unsigned short*)y, ldy,
                      (const unsigned short*)dy, lddy, (unsigned short*)dx, lddx, dx_acc, dw, db, B, K, act);

@@ -143,3 +143,26 @@ class NormInitializer(Initializer):
 
 
 NormalInitializer = NormInitializer
+
+
+class ColumnPaddedInitializer(Initializer):
+    """Initialise a [rows, cols_padded] weight exactly like a [rows, cols_logical] one (same
+    fan-in/out, same counter stream) with zero padding columns.  Used when flexmi pads a narrow
+    input (DLRM's 13 dense features -> 16) for 16-B aligned GEMM rows: the padded model is
+    numerically the unpadded one."""
+
+    def __init__(self, base, logical_cols):
+        super().__init__()
+        self.base = base
+        self.logical_cols = int(logical_cols)
+
+    def fill(self, dims, box, out):
+        rows, cols = dims
+        (r0, r1), (c0, c1) = box
+        out.zero_()
+        lc1 = min(c1, self.logical_cols)
+        if lc1 <= c0:
+            return
+        tmp = torch.empty((r1 - r0, lc1 - c0), dtype=out.dtype, device=out.device)
+        self.base.fill((rows, self.logical_cols), ((r0, r1), (c0, lc1)), tmp)
+        out[:, : lc1 - c0].copy_(tmp)

@@ -101,11 +101,15 @@ class DLRMConfig:
 
 
 def create_mlp(model, x, ln, sigmoid_layer, seed_base=0):
-    """``create_mlp`` (``dlrm.cc:26-39``)."""
+    """``create_mlp`` (``dlrm.cc:26-39``).  If ``x`` is a zero-padded input (more columns than
+    ln[0]), the first layer is initialised as the unpadded one (ColumnPaddedInitializer)."""
+    from flexmi.core.initializers import ColumnPaddedInitializer
     t = x
     for i in range(len(ln) - 1):
         std = math.sqrt(2.0 / (ln[i + 1] + ln[i]))
         winit = NormInitializer(model._next_seed(), 0.0, std)
+        if i == 0 and x.dims[-1] != ln[0]:
+            winit = ColumnPaddedInitializer(winit, ln[0])
         binit = NormInitializer(model._next_seed(), 0.0, math.sqrt(2.0 / ln[i + 1]))
         act = ActiMode.AC_MODE_SIGMOID if i == sigmoid_layer else ActiMode.AC_MODE_RELU
         t = model.dense(t, ln[i + 1], act, True, None, winit, binit)
@@ -129,7 +133,7 @@ def build_dlrm(model, c: DLRMConfig, pad_dense=True):
         bot[0] = (bot[0] + 7) // 8 * 8   # 13 -> 16: 16-B aligned rows for the first GEMM (pad columns are 0)
     dense_in = model.create_tensor([B, bot[0]], DataType.DT_FLOAT, name="dense")
     dense_in.real_features = c.mlp_bot[0]
-    x = create_mlp(model, dense_in, bot, c.sigmoid_bot)
+    x = create_mlp(model, dense_in, list(c.mlp_bot), c.sigmoid_bot)
     ly = [create_emb(model, sparse[i], c.embedding_size[i], c.sparse_feature_size, i) for i in range(len(sparse))]
     if c.arch_interaction_op == "cat":
         z = model.concat([x] + ly, 1, name="concat")

@@ -58,13 +58,13 @@ GEMM_WS_BYTES = 64 << 20
 
 
 def gemm(A, lda, a_kcontig, B, ldb, b_kcontig, Cout, ldc, M, N, K, bias=None, act=10, beta=False, alpha=1.0,
-         batch=1, sA=0, sB=0, sC=0, ksplit=0, use_ws=True, act_y=None, bwd_act=10, colsum=None):
+         batch=1, sA=0, sB=0, sC=0, ksplit=0, use_ws=True, act_y=None, bwd_act=10, colsum=None, rowsum_a=None):
     """C = epi(A·B).  Optional fused backward epilogue of the layer below (act_y/bwd_act/colsum):
     C = act'(act_y) * (A·B) and colsum += column sums of C (its bias gradient)."""
     ws = workspace(Cout.device, GEMM_WS_BYTES) if use_ws else None
     lday = act_y.stride(0) if act_y is not None else 0
     return C().gemm(A, lda, sA, a_kcontig, B, ldb, sB, b_kcontig, Cout, ldc, sC, bias, M, N, K, batch, alpha, beta, act,
-                    ws, ksplit, act_y, lday, bwd_act, colsum)
+                    ws, ksplit, act_y, lday, bwd_act, colsum, rowsum_a)
 
 
 # ------------------------------------------------------------------ init
@@ -98,9 +98,9 @@ def linear_forward(x2, w, b, act, y2):
 
 def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=False, fuse_below=None):
     """Weight/bias grads ACCUMULATE into dw/db (the executor zeroes the flat gradient buffer once
-    per step).  grad_is_dpre: dy2 already holds act'(y)*dy and db was produced by the consumer's
-    fused GEMM epilogue.  fuse_below = (y_below, act_below, db_below): apply the activation
-    backward of the layer below (and its bias grad) in this layer's dX GEMM epilogue."""
+    per step).  grad_is_dpre: dy2 already holds act'(y)*dy (written by the consumer's fused dX
+    epilogue).  fuse_below = (y_below, act_below): apply the activation backward of the layer
+    below in this layer's dX GEMM epilogue."""
     M, K = x2.shape
     N = w.shape[0]
     if N == 1:
@@ -109,27 +109,24 @@ def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=F
         if dx2 is not None and fuse_below is not None:
             raise AssertionError("no fused epilogue on the skinny path")
         return
-    if grad_is_dpre:
+    if grad_is_dpre or act == 10:
         dpre = dy2
     else:
-        if act != 10:
-            dpre = ws.get("dpre")
-            if dpre is None or dpre.shape != (M, N):
-                dpre = torch.empty((M, N), dtype=torch.bfloat16, device=x2.device)
-                ws["dpre"] = dpre
-        else:
-            dpre = dy2
-        if act != 10 or db is not None:
-            C().act_bwd_bias(y2 if act != 10 else dy2, dy2, dpre if act != 10 else None, db, M, N, act)
-    # dW[N,K] = dpre^T x   (both operands MN-contiguous: transposing LDS reads)
-    gemm(dpre, dpre.stride(0), False, x2, x2.stride(0), False, dw, K, N, K, M)
-    # dX[M,K] = dpre W   (+ fused act-bwd / bias-grad of the layer below)
+        dpre = ws.get("dpre")
+        if dpre is None or dpre.shape != (M, N):
+            dpre = torch.empty((M, N), dtype=torch.bfloat16, device=x2.device)
+            ws["dpre"] = dpre
+        C().act_bwd_bias(y2, dy2, dpre, None, M, N, act)
+    # dW[N,K] = dpre^T x (both operands MN-contiguous: transposing LDS reads); the bias gradient
+    # db = column sums of dpre is accumulated from the staged A tiles of the same GEMM
+    gemm(dpre, dpre.stride(0), False, x2, x2.stride(0), False, dw, K, N, K, M, rowsum_a=db)
+    # dX[M,K] = dpre W   (+ fused activation backward of the layer below)
     if dx2 is not None:
         if fuse_below is not None:
-            yb, actb, dbb = fuse_below
+            yb, actb = fuse_below[0], fuse_below[1]
             assert not dx_acc
             gemm(dpre, dpre.stride(0), True, w, K, False, dx2, dx2.stride(0), M, K, N,
-                 act_y=yb.view(M, K), bwd_act=int(actb), colsum=dbb)
+                 act_y=yb.view(M, K), bwd_act=int(actb))
         else:
             gemm(dpre, dpre.stride(0), True, w, K, False, dx2, dx2.stride(0), M, K, N, beta=bool(dx_acc))
 

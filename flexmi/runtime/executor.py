@@ -467,7 +467,7 @@ class Executor:
             if (l2.op_type != OperatorType.OP_LINEAR or c2 is None or l2.out_dim == 1 or op.out_dim == 1
                     or not self.need[(l2.guid, idx)].same_as(self.home[t.guid]) or c2.in_grads[0] is None):
                 continue
-            c2.saved["fuse_below"] = (c1.outputs[0], op.activation, c1.weight_grads[1] if op.use_bias else None)
+            c2.saved["fuse_below"] = (c1.outputs[0], op.activation)
             c1.saved["grad_is_dpre"] = True
 
     def _build_groups(self, ops):
