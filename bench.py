@@ -37,8 +37,10 @@ def parse():
     ap.add_argument("--config", default="mlperf", choices=["mlperf", "run_random", "criteo_kaggle", "tiny"])
     ap.add_argument("--batch-per-gpu", type=int, default=8192)
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture of the step")
-    ap.add_argument("--strategy", default="table", choices=["table", "dp"],
-                    help="table: table-wise embedding placement + DP MLPs (default); dp: pure data parallel")
+    ap.add_argument("--strategy", default="table", choices=["table", "dp", "search"],
+                    help="table: table-wise embedding placement + DP MLPs (default); dp: pure data parallel; "
+                         "search: MCMC SOAP search over the MI355X simulator (seeded with 'table')")
+    ap.add_argument("--search-budget", type=int, default=4000)
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--table-scale", type=float, default=1.0, help="debug only: shrink tables (invalid for reporting)")
     return ap.parse_args()
@@ -67,8 +69,16 @@ def main():
     model = FFModel(cfg)
     dense_in, sparse, out = build_dlrm(model, dcfg)
     strategies = {}
-    if world > 1 and a.strategy == "table":
+    search = None
+    if world > 1 and a.strategy in ("table", "search"):
         strategies = dlrm_strategy(model, world)
+    if world > 1 and a.strategy == "search":
+        from flexmi.core import SGDOptimizer as _S
+        from flexmi.parallel.search import optimize
+        model.optimizer = _S(model, 0.01)
+        search = optimize(model, a.search_budget, 1.0, num_devices=world, init=strategies, seed=0,
+                          verbose=(rank == 0))
+        strategies = dict(search.best)
     model.strategies = strategies
     loss = LossType.LOSS_BINARY_CROSSENTROPY if dcfg.loss == "bce" else LossType.LOSS_MEAN_SQUARED_ERROR_AVG_REDUCE
     model.compile(SGDOptimizer(model, 0.01), loss, [MetricsType.METRICS_ACCURACY, MetricsType.METRICS_MEAN_SQUARED_ERROR])
@@ -154,7 +164,8 @@ def main():
                 "model": f"DLRM {dcfg.name} ({'MLPerf-like: 13 dense + 26 sparse, Criteo-TB tables (187.8M rows x 128, fp32), dot interaction' if dcfg.name == 'mlperf' else dcfg.name})",
                 "global_batch": gb,
                 "seq_len": 1,
-                "parallelism": (f"dp{world}" if world == 1 or a.strategy == "dp" else f"table-wise-emb{world}+dp{world}-mlp"),
+                "parallelism": (f"dp{world}" if world == 1 or a.strategy == "dp" else
+                                f"soap-search{world}" if a.strategy == "search" else f"table-wise-emb{world}+dp{world}-mlp"),
                 "tables_rows": sum(dcfg.embedding_size),
                 "embedding_dim": dcfg.sparse_feature_size,
                 "mlp_bot": dcfg.mlp_bot,
@@ -166,6 +177,8 @@ def main():
                 "table_scale": a.table_scale,
             },
         }
+        if search is not None:
+            rec["config"]["search"] = {k: round(v, 4) for k, v in search.summary().items()}
         print(f"ELAPSED TIME = {el:.4f}s, THROUGHPUT = {sps:.2f} samples/s", file=sys.stderr)
         if a.profile:
             ex.timer.print_summary(file=sys.stderr)

@@ -1,0 +1,266 @@
+"""SOAP strategy search: candidate configs -> native MI355X simulator -> Metropolis walk.
+
+Reference: ``FFModel::optimize`` / ``rewrite`` (``src/runtime/model.cc:1082-1144``) start from
+data parallelism, re-draw ONE op's ParallelConfig per step (``Op::get_random_parallel_config``,
+``src/runtime/model.cc:295-324``), simulate (``src/runtime/simulator.cc:275-448``) and accept
+with the Metropolis rule ``rand < exp(-alpha * (next - cur))``; the best strategy can be
+exported to ``.pb`` but was never applied to the running model (caveat C6).
+
+flexmi: every op gets an explicit, finite candidate list -- all degree vectors over the op's
+SOAP-splittable dims (sample / attribute / parameter) whose product divides the device count,
+each placed on every aligned contiguous device window (so table-wise embedding placement on
+any single GPU is a candidate, as are column-parallel Linear groups and sub-node DP).  The
+candidate tables (per-part costs from :mod:`flexmi.parallel.cost`, shard boxes, weight-sync
+groups, per-device memory) are handed to the C++ simulator once (``csrc/sim/simulator.cc``);
+the walk itself runs natively without the GIL.  The result IS applied: ``FFModel.compile``
+installs the best strategy before ``init_layers``.
+"""
+from __future__ import annotations
+
+import itertools
+import json
+import sys
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+from flexmi.core.types import DataType, OperatorType
+from flexmi.parallel.cost import CostModel
+from flexmi.parallel.layout import Layout, ParallelConfig
+from flexmi.parallel.machine import MachineModel
+
+_FLOAT = (DataType.DT_FLOAT, DataType.DT_DOUBLE, DataType.DT_BF16, DataType.DT_HALF)
+
+
+def _divisors(n):
+    return [d for d in range(1, n + 1) if n % d == 0]
+
+
+def candidate_configs(op, ndev: int, max_cands: int = 96) -> List[ParallelConfig]:
+    """Enumerate valid ParallelConfigs of ``op`` on ``ndev`` devices (deterministic order;
+    the data-parallel config first when valid)."""
+    nd = op.out_ndims
+    split = sorted(d for d in op.splittable_dims() if d < nd)
+    out: List[ParallelConfig] = []
+    seen = set()
+
+    def add(pc):
+        k = pc.key()
+        if k not in seen and op.valid_pc(pc):
+            seen.add(k)
+            out.append(pc)
+
+    add(ParallelConfig.data_parallel(nd, ndev))
+    divs = _divisors(ndev)
+    combos = []
+    for degs in itertools.product(*[divs] * len(split)):
+        p = 1
+        for d in degs:
+            p *= d
+        if ndev % p == 0:
+            combos.append(degs)
+    combos.sort(key=lambda d: (-_prod(d), d))
+    for degs in combos:
+        user = [1] * nd
+        for dim, d in zip(split, degs):
+            user[dim] = d
+        P = _prod(degs)
+        for w in range(ndev // P):
+            pc = ParallelConfig.from_user_degrees(user, list(range(w * P, (w + 1) * P)))
+            add(pc)
+            if len(out) >= max_cands:
+                return out
+    if not out:
+        out.append(ParallelConfig([1] * nd, [0]))
+    return out
+
+
+def _prod(s):
+    n = 1
+    for d in s:
+        n *= int(d)
+    return n
+
+
+def _box_shape(box):
+    return tuple(hi - lo for lo, hi in box)
+
+
+def _lay_parts(lay: Layout):
+    return [(tuple(lo for lo, _ in lay.part_box(p)), tuple(hi for _, hi in lay.part_box(p)), tuple(lay.holders[p]))
+            for p in range(lay.num_parts())]
+
+
+@dataclass
+class SearchResult:
+    best: Dict[str, ParallelConfig]
+    best_us: float
+    init_us: float
+    dp_us: float
+    history: list = field(default_factory=list)
+    accepted: int = 0
+    iterations: int = 0
+    seconds: float = 0.0
+
+    @property
+    def speedup_vs_dp(self):
+        return self.dp_us / self.best_us if self.best_us > 0 else float("nan")
+
+    def summary(self):
+        return {"best_ms": self.best_us / 1e3, "dp_ms": self.dp_us / 1e3, "init_ms": self.init_us / 1e3,
+                "speedup_vs_dp": self.speedup_vs_dp, "accepted": self.accepted, "iterations": self.iterations,
+                "seconds": self.seconds}
+
+
+class SimGraph:
+    """The model compiled into the native simulator's candidate tables."""
+
+    def __init__(self, model, ndev: int, machine: Optional[MachineModel] = None, cost: Optional[CostModel] = None,
+                 max_cands: int = 96, extra: Optional[Dict[str, ParallelConfig]] = None):
+        from flexmi import _native
+        self.model = model
+        self.ndev = ndev
+        self.machine = machine or MachineModel.mi355x(ndev)
+        self.machine.ndev = ndev
+        self.cost = cost or CostModel(self.machine, dtype_bytes=2 if model.config.compute_dtype == "bf16" else 4)
+        opt = model.optimizer
+        self.nstates = len(opt.state_names()) if opt is not None and hasattr(opt, "state_names") else 0
+        self.sparse_ok = bool(getattr(opt, "sparse_capable", False))
+        self.ops = list(model.layers)
+        self.sim = _native.Simulator(self.machine.native_dict())
+        self.cands: List[List[ParallelConfig]] = []
+        tid = {}
+        for op in self.ops:
+            for t in op.inputs:
+                if t.guid not in tid:
+                    prod = -1
+                    if t.owner_op is not None:
+                        raise RuntimeError(f"tensor {t.name} consumed before its producer {t.owner_op.name}")
+                    tid[t.guid] = self.sim.add_tensor(self._eb(t), prod, 0, False)
+            idx = len(self.cands)
+            for j, o in enumerate(op.outputs):
+                tid[o.guid] = self.sim.add_tensor(self._eb(o), idx, j, o.data_type in _FLOAT)
+            cl = candidate_configs(op, ndev, max_cands)
+            if extra and op.name in extra:
+                pc = extra[op.name]
+                if op.valid_pc(pc) and max(pc.device_ids) < ndev and pc not in cl:
+                    cl.append(pc)
+            self.cands.append(cl)
+            self.sim.add_op(op.name, [tid[t.guid] for t in op.inputs], [tid[o.guid] for o in op.outputs],
+                            [self._cand(op, pc) for pc in cl], ndev)
+
+    def _eb(self, t):
+        return self.cost.eb if t.data_type in _FLOAT else 8
+
+    def _cand(self, op, pc: ParallelConfig):
+        outs = op.output_layouts(pc)
+        ins = op.input_layouts(pc)
+        wls = op.weight_layouts(pc)
+        fwd, bwd = [], []
+        mem, upd_bytes = {}, {}
+        for p, dev in enumerate(pc.device_ids):
+            in_shapes = []
+            for lay in ins:
+                ps = lay.parts_of(dev)
+                in_shapes.append(_box_shape(lay.part_box(ps[0])) if ps else tuple(0 for _ in lay.shape))
+            out_shapes = [_box_shape(lay.part_box(p)) for lay in outs]
+            f, b = self.cost.op_cost(op, in_shapes, out_shapes)
+            fwd.append(f)
+            bwd.append(b)
+            act = sum(_prod(s) for s in out_shapes)
+            mem[dev] = mem.get(dev, 0.0) + act * self.cost.eb * 2
+        wsync = []
+        for w, lay in zip(op.weights, wls):
+            sparse = op.op_type == OperatorType.OP_EMBEDDING and self.sparse_ok and lay.replication() == 1
+            for p in range(lay.num_parts()):
+                vol = _prod(_box_shape(lay.part_box(p)))
+                h = lay.holders[p]
+                if len(h) > 1:
+                    wsync.append((float(vol * 4), list(h)))
+                for d in h:
+                    if sparse:
+                        mem[d] = mem.get(d, 0.0) + vol * 4.0
+                    else:
+                        mem[d] = mem.get(d, 0.0) + vol * (4.0 + 4.0 + 2.0 + 4.0 * self.nstates)
+                        upd_bytes[d] = upd_bytes.get(d, 0.0) + vol * 4.0
+        return {"part_dev": list(pc.device_ids), "fwd_us": fwd, "bwd_us": bwd,
+                "out": [_lay_parts(l) for l in outs], "inp": [_lay_parts(l) for l in ins],
+                "wsync": wsync, "mem": sorted(mem.items()),
+                "upd": sorted((d, self.cost.update_us(b, self.nstates)) for d, b in upd_bytes.items()),
+                "label": repr(pc)}
+
+    # ------------------------------------------------------------------
+    def dp_assign(self):
+        out = []
+        for op, cl in zip(self.ops, self.cands):
+            dp = ParallelConfig.data_parallel(op.out_ndims, self.ndev)
+            out.append(cl.index(dp) if dp in cl else 0)
+        return out
+
+    def assign_from(self, strategies: Dict[str, ParallelConfig]):
+        a = self.dp_assign()
+        for i, (op, cl) in enumerate(zip(self.ops, self.cands)):
+            pc = strategies.get(op.name)
+            if pc is not None and pc in cl:
+                a[i] = cl.index(pc)
+        return a
+
+    def strategies(self, assign) -> Dict[str, ParallelConfig]:
+        return {op.name: cl[a] for op, cl, a in zip(self.ops, self.cands, assign)}
+
+    def simulate(self, assign):
+        return self.sim.simulate(list(assign))
+
+    def memory(self, assign):
+        return self.sim.memory(list(assign))
+
+    def chrome_trace(self, assign, path):
+        """Predicted timeline (``chrome://tracing``): one row per GPU compute queue, collective
+        channel and xGMI link (validate the cost model against rocprof)."""
+        nd = self.ndev
+        evs = []
+        for name, kind, res, s, e in self.sim.trace(list(assign)):
+            if res < nd:
+                pid, tid = res, "compute"
+            elif res < 2 * nd:
+                pid, tid = res - nd, "collective"
+            else:
+                r = res - 2 * nd
+                pid, tid = r // nd, f"xgmi->{r % nd}"
+            evs.append({"name": f"{name}.{kind}", "ph": "X", "ts": s, "dur": max(e - s, 0.01), "pid": pid, "tid": tid,
+                        "cat": kind})
+        with open(path, "w") as f:
+            json.dump({"traceEvents": evs, "displayTimeUnit": "ns"}, f)
+
+
+def simulate(model, strategies=None, num_devices=None, machine=None, cost_db=None):
+    n = num_devices or max(1, model.config.world_size)
+    g = SimGraph(model, n, machine, CostModel(machine or MachineModel.mi355x(n), cost_db) if cost_db else None,
+                 extra=strategies)
+    return g.simulate(g.assign_from(strategies or {}))
+
+
+def optimize(model, budget, alpha=1.0, num_devices=None, machine=None, cost_db=None, seed=0, init=None,
+             verbose=None) -> SearchResult:
+    """MCMC search (``FFModel::optimize``) over the native simulator; returns the best strategy."""
+    n = num_devices or max(1, model.config.world_size)
+    cfg = model.config
+    if machine is None and getattr(cfg, "machine_file", None):
+        machine = MachineModel.load(cfg.machine_file, n)
+    machine = machine or MachineModel.mi355x(n)
+    cost = CostModel(machine, cost_db if cost_db is not None else (getattr(cfg, "cost_db", "") or None),
+                     dtype_bytes=2 if cfg.compute_dtype == "bf16" else 4)
+    t0 = time.time()
+    g = SimGraph(model, n, machine, cost, extra=init)
+    dp = g.dp_assign()
+    dp_us = g.simulate(dp)
+    start = g.assign_from(init) if init else dp
+    verbose = (cfg.rank == 0) if verbose is None else verbose
+    best, best_us, init_us, hist, acc = g.sim.search(start, int(budget), float(alpha), int(seed), bool(verbose))
+    res = SearchResult(g.strategies(best), best_us, init_us, dp_us, list(hist), acc, int(budget), time.time() - t0)
+    res.graph = g
+    res.assign = list(best)
+    if verbose:
+        print(f"[search] {n} devices, {budget} iters in {res.seconds:.1f}s: best {best_us / 1e3:.3f} ms/iter "
+              f"(data parallel {dp_us / 1e3:.3f} ms, predicted speedup {res.speedup_vs_dp:.2f}x)", file=sys.stderr)
+    return res

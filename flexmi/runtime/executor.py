@@ -360,7 +360,9 @@ class Executor:
         self.grad_needed = set()
         for op in ops:
             for i, t in enumerate(op.inputs):
-                if t.owner_op is not None and op.needs_input_grad(i) and _is_float(t.data_type):
+                # graph inputs get gradients only when asked (cost measurement of a single op)
+                src_ok = t.owner_op is not None or getattr(self.cfg, "input_grads", False)
+                if src_ok and op.needs_input_grad(i) and _is_float(t.data_type):
                     self.grad_needed.add(t.guid)
         final = ops[-1].outputs[0]
         self.final = final

@@ -58,6 +58,18 @@ def _build(case, world):
             inputs[f"sparse{i}"] = (t, (B, 1), ("i", r))
         if world > 1:
             strat = dlrm_strategy(m, world)
+            if case == "dlrm_search":
+                # strategy chosen by the MCMC search over the MI355X simulator (same seed on
+                # every rank => identical strategy); must train exactly like world 1
+                # (slow all-reduce in the machine model => replicated weights are expensive, so
+                # the walk must leave data parallelism for table/column/channel placements)
+                from flexmi.parallel.machine import MachineModel
+                from flexmi.parallel.search import optimize
+                m.optimizer = SGDOptimizer(m, 0.1)
+                mach = MachineModel.mi355x(world, ar_busbw_GBps=1e-4, ar_lat_us=500.0)
+                strat = dict(optimize(m, 400, 1.0, num_devices=world, machine=mach, seed=5, verbose=False).best)
+                dp = ParallelConfig.data_parallel(2, world)
+                assert sum(pc != dp for pc in strat.values()) >= 3, strat
             if case == "dlrm_colsplit":
                 # column (parameter-dim) split of one table across all ranks
                 strat["embedding1"] = ParallelConfig([world, 1], list(range(world)))
@@ -133,7 +145,8 @@ def _launch(case, world, steps=3):
 
 
 @pytest.mark.parametrize("case,world", [("mlp_dp", 2), ("mlp_channel", 2), ("mlp_channel", 4), ("dlrm_dot", 2),
-                                        ("dlrm_cat", 2), ("dlrm_colsplit", 2), ("cnn_spatial", 2)])
+                                        ("dlrm_cat", 2), ("dlrm_colsplit", 2), ("cnn_spatial", 2),
+                                        ("dlrm_search", 2), ("dlrm_search", 4)])
 def test_strategy_equivalence(case, world):
     ref = _launch(case, 1)
     got = _launch(case, world)

@@ -49,7 +49,7 @@ def write_ninja(only=None):
         f"hipcc = {ROCM}/bin/hipcc",
         "cxx = g++",
         f"hipflags = --offload-arch={ARCH} -O3 -std=c++17 -fPIC -Wno-unused-result -munsafe-fp-atomics -I{ROOT}/csrc/kernels",
-        f"cxxflags = -O3 -std=c++17 -fPIC -Wall -Wno-sign-compare -I{ROOT}/csrc/runtime {pyinc}",
+        f"cxxflags = -O3 -std=c++17 -fPIC -Wall -Wno-sign-compare -I{ROOT}/csrc/runtime -I{ROOT}/csrc/sim {pyinc}",
         "rule hipcc",
         "  command = $hipcc $hipflags -MD -MF $out.d -c $in -o $out",
         "  depfile = $out.d",
@@ -89,7 +89,8 @@ def write_ninja(only=None):
         targets.append(out)
     if only in (None, "native"):
         objs = []
-        for src in sorted(glob.glob(os.path.join(ROOT, "csrc", "runtime", "*.cc"))) + [
+        for src in sorted(glob.glob(os.path.join(ROOT, "csrc", "runtime", "*.cc")) +
+                          glob.glob(os.path.join(ROOT, "csrc", "sim", "*.cc"))) + [
                 os.path.join(ROOT, "csrc", "bindings", "native.cc")]:
             if not os.path.exists(src):
                 continue
