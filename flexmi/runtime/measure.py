@@ -47,13 +47,14 @@ def _make_clone(op, m, in_shapes, out_shapes):
     return ins
 
 
-def measure_op(op, in_shapes, out_shapes, reps=20, index_range=None):
-    """(fwd_us, bwd_us) of ``op`` at the given shard shapes on ``cuda``."""
+def measure_op(op, in_shapes, out_shapes, reps=20, index_range=None, device="gpu"):
+    """(fwd_us, bwd_us) of ``op`` at the given shard shapes on ``cuda`` (``device="cpu"``:
+    host timing of the fp32 reference path, used by the CPU tests)."""
     from flexmi.core import FFConfig, FFModel, SGDOptimizer, LossType
     cfg = FFConfig()
     cfg.batchSize = int(in_shapes[0][0]) if in_shapes and in_shapes[0] else 1
-    cfg.device = "gpu"
-    cfg.compute_dtype = "bf16"
+    cfg.device = device
+    cfg.compute_dtype = "bf16" if device == "gpu" else "fp32"
     # the op's input gradient is part of its backward unless the input is a graph input
     cfg.input_grads = not (op.op_type == OperatorType.OP_LINEAR and op.inputs[0].owner_op is None)
     m = FFModel(cfg)
@@ -68,7 +69,7 @@ def measure_op(op, in_shapes, out_shapes, reps=20, index_range=None):
         buf = ex.local_buffer(t)
         if buf is None:
             continue
-        if t.data_type in (DataType.DT_INT32, DataType.DT_INT64, DataType.DT_INT16):
+        if t.data_type in (DataType.DT_INT32, DataType.DT_INT64):
             hi = index_range or getattr(m.layers[0], "num_entries", 2)
             buf.copy_(torch.randint(0, hi, buf.shape, generator=g, device=ex.device))
         else:
@@ -85,6 +86,13 @@ def measure_op(op, in_shapes, out_shapes, reps=20, index_range=None):
     def timed(items):
         if not items:
             return 0.0
+        if device != "gpu":
+            import time
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                for it in items:
+                    it.fn()
+            return (time.perf_counter() - t0) * 1e6 / reps
         for it in items:           # warm-up (lazy workspaces)
             it.fn()
         torch.cuda.synchronize()
@@ -115,5 +123,6 @@ def measure_op(op, in_shapes, out_shapes, reps=20, index_range=None):
     b = timed(bwd)
     m.executor = None
     del ex
-    torch.cuda.empty_cache()
+    if device == "gpu":
+        torch.cuda.empty_cache()
     return f, b

@@ -119,3 +119,22 @@ def test_simulated_trace_and_pb_export(native, tmp_path):
     S.save_strategies_to_file(str(pb), r.best)
     back = S.load_strategies_from_file(str(pb))
     assert {k: (v.dims, v.device_ids) for k, v in back.items()} == {k: (v.dims, v.device_ids) for k, v in r.best.items()}
+
+
+def test_calibration_tool_cpu(native, tmp_path):
+    """tools/calibrate_costs.py end to end on the CPU path (the GPU run fills costdb/mi355x.json)."""
+    import json
+    import subprocess
+    import sys
+    out = tmp_path / "db.json"
+    r = subprocess.run([sys.executable, "tools/calibrate_costs.py", "--model", "dlrm-tiny", "--gpus", "1,2",
+                        "--batch-per-gpu", "32", "--device", "cpu", "--limit", "6", "--reps", "2", "--out", str(out)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    db = json.load(open(out))
+    assert len(db["entries"]) == 6 and all(len(v) == 2 for v in db["entries"].values())
+    assert db["scale"]
+    from flexmi.parallel.cost import CostModel
+    from flexmi.parallel.machine import MachineModel
+    cm = CostModel(MachineModel.mi355x(2), str(out))
+    assert set(cm.db) == set(db["entries"])

@@ -21,12 +21,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def build_model(name, n, batch_per_gpu):
+def build_model(name, n, batch_per_gpu, device="gpu"):
     from flexmi.core import FFConfig, FFModel, SGDOptimizer
     cfg = FFConfig()
     cfg.batchSize = batch_per_gpu * n
-    cfg.device = "gpu"
-    cfg.compute_dtype = "bf16"
+    cfg.device = device
+    cfg.compute_dtype = "bf16" if device == "gpu" else "fp32"
     m = FFModel(cfg)
     if name.startswith("dlrm"):
         from flexmi.models.dlrm import DLRMConfig, build_dlrm
@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--batch-per-gpu", type=int, default=8192)
     ap.add_argument("--out", default=os.path.join(ROOT, "flexmi", "parallel", "costdb", "mi355x.json"))
     ap.add_argument("--limit", type=int, default=0)
+    ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"])
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--time-budget", type=float, default=900.0, help="stop measuring after this many seconds")
     a = ap.parse_args()
@@ -56,7 +57,7 @@ def main():
 
     todo = {}
     for n in [int(x) for x in a.gpus.split(",")]:
-        m = build_model(a.model, n, a.batch_per_gpu)
+        m = build_model(a.model, n, a.batch_per_gpu, a.device)
         for op in m.layers:
             for pc in candidate_configs(op, n):
                 ins, outs = op.input_layouts(pc), op.output_layouts(pc)
@@ -84,7 +85,7 @@ def main():
             print(f"[calibrate] time budget reached after {done} measurements", flush=True)
             break
         op, i_s, o_s = todo[k]
-        r = measure_op(op, i_s, o_s, reps=a.reps)
+        r = measure_op(op, i_s, o_s, reps=a.reps, device=a.device)
         done += 1
         if r is None:
             continue
