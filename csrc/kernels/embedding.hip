@@ -103,46 +103,54 @@ __global__ void __launch_bounds__(256) fm_emb_bwd_atomic_multi(TabSet s, const f
     }
 }
 
+// Tiny tables: block-private LDS copy of the table's gradient.  One WAVE per sample row
+// (lane = column, columns l, l+64, ... so every LDS add of a wave hits 64 distinct banks and
+// no two lanes of a wave ever add to the same address), U samples in flight per wave, a short
+// chunk of samples per block so that the grid has >= 1024 blocks (latency-bound otherwise:
+// the previous 32-block grid ran 128 dependent samples per wave).  The flush adds only touched
+// rows (nonzero) into the table: <= chunk rows per block.
 template <typename GT>
-__global__ void __launch_bounds__(256) fm_emb_bwd_lds_multi(TabSet s, const float* __restrict__ lr, long B) {
+__global__ void __launch_bounds__(256) fm_emb_bwd_lds_multi(TabSet s, const float* __restrict__ lr, long B,
+                                                             int chunk) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* acc = reinterpret_cast<float*>(smem);
   const TabDesc& d = s.t[blockIdx.y];
+  const long b0 = (long)blockIdx.x * chunk;
+  if (b0 >= B) return;
+  const long b1 = min(B, b0 + chunk);
   const int n = d.rows * d.D;
   for (int i = threadIdx.x; i < n; i += 256) acc[i] = 0.f;
   __syncthreads();
-  const int lpr = d.D < 256 ? d.D : 256;
-  const int rpi = 256 / lpr;
-  const int sub = threadIdx.x / lpr, lc = threadIdx.x - sub * lpr;
-  const long chunk = (B + gridDim.x - 1) / gridDim.x;
-  const long b0 = blockIdx.x * chunk, b1 = min(B, b0 + chunk);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const GT* dy = reinterpret_cast<const GT*>(d.act);
-  if (sub < rpi) {
-    if (d.bag == 1) {
-      // 8 independent (index, gradient) loads in flight per thread before the LDS adds: the loop
-      // is otherwise one dependent HBM round trip per sample
-      constexpr int U = 8;
-      for (long b = b0 + sub; b < b1; b += (long)rpi * U)
-        for (int c = lc; c < d.D; c += lpr) {
-          float g[U];
-          long r[U];
+  constexpr int U = 4;
+  for (long b = b0 + wave; b < b1; b += 4 * U) {
+    long r[U];
+    bool ok[U];
 #pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const long bb = b + (long)u * rpi;
-            const bool ok = bb < b1;
-            g[u] = ok ? ld<GT>(dy + bb * d.ld + c) : 0.f;
-            r[u] = ok ? load_idx(d.idx, bb, d.idx64) : 0;
-          }
+    for (int u = 0; u < U; ++u) {
+      const long bb = b + 4L * u;
+      ok[u] = bb < b1;
+      r[u] = ok[u] ? load_idx(d.idx, bb * d.bag, d.idx64) : 0;
+    }
+    for (int c = lane; c < d.D; c += 64) {
+      float g[U];
 #pragma unroll
-          for (int u = 0; u < U; ++u)
-            if (b + (long)u * rpi < b1) atomicAdd(acc + r[u] * d.D + c, g[u]);
+      for (int u = 0; u < U; ++u) g[u] = ok[u] ? ld<GT>(dy + (b + 4L * u) * d.ld + c) : 0.f;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (ok[u]) atomicAdd(acc + r[u] * d.D + c, g[u]);
+    }
+    if (d.bag > 1) {   // remaining bag entries (same gradient row)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (!ok[u]) continue;
+        const long bb = b + 4L * u;
+        for (int j = 1; j < d.bag; ++j) {
+          const long rj = load_idx(d.idx, bb * d.bag + j, d.idx64);
+          for (int c = lane; c < d.D; c += 64) atomicAdd(acc + rj * d.D + c, ld<GT>(dy + bb * d.ld + c));
         }
-    } else {
-      for (long b = b0 + sub; b < b1; b += rpi)
-        for (int c = lc; c < d.D; c += lpr) {
-          const float g = ld<GT>(dy + b * d.ld + c);
-          for (int j = 0; j < d.bag; ++j) atomicAdd(acc + load_idx(d.idx, b * d.bag + j, d.idx64) * d.D + c, g);
-        }
+      }
     }
   }
   __syncthreads();
@@ -213,9 +221,11 @@ extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const
       if (pass == 0) {
         size_t lds = (size_t)0;
         for (int i = 0; i < m; ++i) lds = std::max(lds, (size_t)s.t[i].rows * s.t[i].D * 4);
-        dim3 grid((unsigned)std::max<long>(1, std::min<long>(B / 256, 32)), m);
-        if (dy_bf16) hipLaunchKernelGGL(fm_emb_bwd_lds_multi<unsigned short>, grid, dim3(256), lds, st, s, lr, B);
-        else hipLaunchKernelGGL(fm_emb_bwd_lds_multi<float>, grid, dim3(256), lds, st, s, lr, B);
+        // chunk: >= 64 samples (16 per wave), more for larger tables (flush <= rows*D adds per block)
+        int chunk = std::max(64, std::min(512, ((2 * maxrows + 31) / 32) * 32));
+        dim3 grid((unsigned)((B + chunk - 1) / chunk), m);
+        if (dy_bf16) hipLaunchKernelGGL(fm_emb_bwd_lds_multi<unsigned short>, grid, dim3(256), lds, st, s, lr, B, chunk);
+        else hipLaunchKernelGGL(fm_emb_bwd_lds_multi<float>, grid, dim3(256), lds, st, s, lr, B, chunk);
       } else {
         const int rpi = std::max(1, 256 / std::min(256, maxD));
         dim3 grid((unsigned)std::max<long>(1, std::min<long>((B + rpi - 1) / rpi, 2048)), m);

@@ -131,6 +131,150 @@ __global__ void __launch_bounds__(256) fm_dot_bwd(PtrTab Z, long ldz, const unsi
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Specialised kernels for a compile-time D (32/64/128; DLRM uses 128) and 16-B aligned rows:
+// every global access is a 16-B vector access issued before its first use (no dependent
+// round trips per sample), the x part of the output comes straight from the MFMA operand
+// registers, and the backward stages dOut and Z with vector loads and writes dZ through an
+// LDS transpose with 16-B stores (the generic kernels above issue 2-B scalar loads/stores).
+template <int DT>
+__global__ void __launch_bounds__(256) fm_dot_fwd_t(PtrTab Z, long ldz, unsigned short* __restrict__ out, long ldo,
+                                                   long B, int F, int W, int self) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int KS = DT / 16;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  unsigned short* row = reinterpret_cast<unsigned short*>(smem) + wave * W;
+  const int waves_total = gridDim.x * (blockDim.x >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int npairs = self ? F * (F + 1) / 2 : F * (F - 1) / 2;
+  for (long b = blockIdx.x * (blockDim.x >> 6) + wave; b < B; b += waves_total) {
+    bf16x8_t f[KS];
+    const unsigned short* zr = (r < F) ? (Z.p[r] + b * ldz + 8 * h) : nullptr;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      f[ks] = zr ? *reinterpret_cast<const bf16x8_t*>(zr + 16 * ks) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    f32x16_t acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<bf16x8v_t*>(&f[ks]), *reinterpret_cast<bf16x8v_t*>(&f[ks]),
+                                                    acc, 0, 0, 0);
+    if (r == 0) {   // lanes 0 / 32 hold row 0 = the dense features x
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) *reinterpret_cast<bf16x8_t*>(row + 16 * ks + 8 * h) = f[ks];
+    }
+    for (int c = DT + npairs + lane; c < W; c += 64) row[c] = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      int i = (q & 3) + 8 * (q >> 2) + 4 * h;
+      if (i < F && (self ? r <= i : r < i)) row[DT + pair_pos(i, r, self)] = f2bf(acc[q]);
+    }
+    FM_WAVE_LDS_SYNC();
+    unsigned short* o = out + b * ldo;
+    for (int c = lane * 8; c < W; c += 64 * 8) *reinterpret_cast<u32x4_t*>(o + c) = *reinterpret_cast<const u32x4_t*>(row + c);
+    FM_WAVE_LDS_SYNC();
+  }
+}
+
+template <int DT>
+__global__ void __launch_bounds__(256) fm_dot_bwd_t(PtrTab Z, long ldz, const unsigned short* __restrict__ dout, long ldo,
+                                                   MPtrTab dZ, long lddz, unsigned acc_mask, long B, int F, int W, int self) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int CPR = DT / 8;                 // 16-B chunks per Z row
+  constexpr int ZCH = 32 * CPR / 64;          // Z chunks per lane (rows >= F are zero)
+  constexpr int NT = DT / 32;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wpad = (W + 7) & ~7;
+  char* base = smem + wave * (32 * DT * 2 + 32 * 32 * 2 + wpad * 2);
+  unsigned short* zs = reinterpret_cast<unsigned short*>(base);                        // [32][DT]
+  unsigned short* ss = reinterpret_cast<unsigned short*>(base + 32 * DT * 2);          // [32][32]
+  unsigned short* ds = reinterpret_cast<unsigned short*>(base + 32 * DT * 2 + 2048);   // dOut row [W]
+  const int waves_total = gridDim.x * (blockDim.x >> 6);
+  for (long b = blockIdx.x * (blockDim.x >> 6) + wave; b < B; b += waves_total) {
+    u32x4_t zv[ZCH];
+#pragma unroll
+    for (int t = 0; t < ZCH; ++t) {
+      const int c = lane + 64 * t, i = c / CPR, k = (c % CPR) * 8;
+      zv[t] = i < F ? *reinterpret_cast<const u32x4_t*>(Z.p[i] + b * ldz + k) : u32x4_t{0u, 0u, 0u, 0u};
+    }
+    u32x4_t dv = {0u, 0u, 0u, 0u};
+    const bool dload = lane * 8 < W;
+    if (dload) dv = *reinterpret_cast<const u32x4_t*>(dout + b * ldo + lane * 8);
+#pragma unroll
+    for (int t = 0; t < ZCH; ++t) {
+      const int c = lane + 64 * t, i = c / CPR, k = (c % CPR) * 8;
+      *reinterpret_cast<u32x4_t*>(zs + i * DT + k) = zv[t];
+    }
+    if (dload) *reinterpret_cast<u32x4_t*>(ds + lane * 8) = dv;
+    FM_WAVE_LDS_SYNC();
+    const unsigned short* dp = ds + DT;
+#pragma unroll 4
+    for (int e = lane; e < 32 * 32; e += 64) {
+      int i = e >> 5, j = e & 31;
+      float v = 0.f;
+      if (i < F && j < F) {
+        if (i > j) v = bf2f(dp[pair_pos(i, j, self)]);
+        else if (j > i) v = bf2f(dp[pair_pos(j, i, self)]);
+        else if (self) v = 2.f * bf2f(dp[pair_pos(i, i, self)]);
+      }
+      ss[e] = f2bf(v);
+    }
+    FM_WAVE_LDS_SYNC();
+    const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+    f32x16_t acc[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+#pragma unroll
+      for (int t = 0; t < 16; ++t) acc[nt][t] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(ss + (lane & 31) * 32 + 16 * ks + 8 * (lane >> 5));
+        int krow = 16 * ks + 8 * (g >> 1) + q;
+        int col = 32 * nt + 16 * (g & 1) + 4 * p;
+        bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4_t*)(zs + krow * DT + col));
+        bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4_t*)(zs + (krow + 4) * DT + col));
+        bf16x8_t bb;
+        bb.lo = lo;
+        bb.hi = hi;
+        acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<bf16x8v_t*>(&a),
+                                                          *reinterpret_cast<bf16x8v_t*>(&bb), acc[nt], 0, 0, 0);
+      }
+    }
+    FM_WAVE_LDS_SYNC();    // every lane is done reading zs: reuse it for the dZ tile
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int n = 32 * nt + (lane & 31);
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        int i = (t & 3) + 8 * (t >> 2) + 4 * (lane >> 5);
+        zs[i * DT + n] = f2bf(acc[nt][t]);
+      }
+    }
+    FM_WAVE_LDS_SYNC();
+    for (int c = lane; c < F * CPR; c += 64) {
+      const int i = c / CPR, k = (c % CPR) * 8;
+      unsigned short* d = dZ.p[i];
+      if (d == nullptr) continue;
+      d += b * lddz + k;
+      bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(zs + i * DT + k);
+      const bool add_x = i == 0, add_old = (acc_mask >> i) & 1u;
+      if (add_x || add_old) {
+        bf16x8_t x = add_x ? *reinterpret_cast<const bf16x8_t*>(ds + k) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+        bf16x8_t o = add_old ? *reinterpret_cast<const bf16x8_t*>(d) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          v[e] = (short)f2bf(bf2f((unsigned short)v[e]) + bf2f((unsigned short)x[e]) + bf2f((unsigned short)o[e]));
+      }
+      *reinterpret_cast<bf16x8_t*>(d) = v;
+    }
+    FM_WAVE_LDS_SYNC();
+  }
+}
+
+FM_HOST_DEVICE bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
 }  // namespace
 
 extern "C" void fm_dot_interaction_fwd(const void* const* z, int F, long ldz, void* out, long ldo, long B, int D, int W,
@@ -138,7 +282,15 @@ extern "C" void fm_dot_interaction_fwd(const void* const* z, int F, long ldz, vo
   PtrTab t;
   for (int i = 0; i < MAXF; ++i) t.p[i] = i < F ? (const unsigned short*)z[i] : nullptr;
   int waves = 4;
-  long blocks = std::min<long>((B + waves - 1) / waves, 4096);
+  long blocks = std::min<long>((B + waves - 1) / waves, 8192);
+  bool fast = (D == 32 || D == 64 || D == 128) && F <= 32 && ldz % 8 == 0 && ldo % 8 == 0 && W % 8 == 0 && al16(out);
+  for (int i = 0; i < F; ++i) fast = fast && al16(z[i]);
+  if (fast) {
+    auto k = D == 128 ? fm_dot_fwd_t<128> : D == 64 ? fm_dot_fwd_t<64> : fm_dot_fwd_t<32>;
+    hipLaunchKernelGGL(k, dim3((int)blocks), dim3(64 * waves), waves * W * 2, s, t, ldz, (unsigned short*)out, ldo, B,
+                       F, W, self);
+    return;
+  }
   hipLaunchKernelGGL(fm_dot_fwd, dim3((int)blocks), dim3(64 * waves), waves * W * 2, s, t, ldz, (unsigned short*)out,
                      ldo, B, F, D, W, self);
 }
@@ -152,7 +304,18 @@ extern "C" void fm_dot_interaction_bwd(const void* const* z, int F, long ldz, co
     g.p[i] = i < F ? (unsigned short*)dz[i] : nullptr;
   }
   int waves = 4;
-  long blocks = std::min<long>((B + waves - 1) / waves, 4096);
+  long blocks = std::min<long>((B + waves - 1) / waves, 8192);
+  const int npairs = self ? F * (F + 1) / 2 : F * (F - 1) / 2;
+  const int W = ((D + npairs) + 7) & ~7;    // dOut columns read (x part + packed triangle)
+  bool fast = (D == 32 || D == 64 || D == 128) && F <= 32 && ldz % 8 == 0 && ldo % 8 == 0 && lddz % 8 == 0 && al16(dout);
+  for (int i = 0; i < F; ++i) fast = fast && al16(z[i]) && (dz[i] == nullptr || al16(dz[i]));
+  if (fast) {
+    auto k = D == 128 ? fm_dot_bwd_t<128> : D == 64 ? fm_dot_bwd_t<64> : fm_dot_bwd_t<32>;
+    size_t lds = waves * (32 * D * 2 + 32 * 32 * 2 + W * 2);
+    hipLaunchKernelGGL(k, dim3((int)blocks), dim3(64 * waves), lds, s, t, ldz, (const unsigned short*)dout, ldo, g, lddz,
+                       acc_mask, B, F, W, self);
+    return;
+  }
   const int Dp = (D + 31) & ~31;
   size_t lds = waves * (32 * Dp * 2 + 32 * 32 * 2);
   hipLaunchKernelGGL(fm_dot_bwd, dim3((int)blocks), dim3(64 * waves), lds, s, t, ldz, (const unsigned short*)dout, ldo,

@@ -136,7 +136,7 @@ class Op:
 
     def valid_pc(self, pc: ParallelConfig):
         deg = Layout.from_pc(self.outputs[0].dims, pc).degrees
-        ok = all(d == 1 or i in self.splittable_dims() for i, d in enumerate(deg))
+        ok = all(d == 1 or (i in self.splittable_dims() and d <= self.outputs[0].dims[i]) for i, d in enumerate(deg))
         return ok and all(0 <= x for x in pc.device_ids) and len(pc.device_ids) == pc.num_parts()
 
     def output_layouts(self, pc: ParallelConfig):

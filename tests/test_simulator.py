@@ -114,7 +114,7 @@ def test_simulated_trace_and_pb_export(native, tmp_path):
     r.graph.chrome_trace(r.assign, str(path))
     import json
     ev = json.load(open(path))["traceEvents"]
-    assert any(e["cat"] == "fwd" for e in ev) and max(e["ts"] + e["dur"] for e in ev) == pytest.approx(r.best_us, rel=1e-6)
+    assert any(e["cat"] == "fwd" for e in ev) and max(e["ts"] + e["dur"] for e in ev) == pytest.approx(r.best_us, rel=1e-3)
     pb = tmp_path / "s.pb"
     S.save_strategies_to_file(str(pb), r.best)
     back = S.load_strategies_from_file(str(pb))
