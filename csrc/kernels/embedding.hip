@@ -4,32 +4,38 @@
 // All kernels take a TABLE DESCRIPTOR ARRAY and process every table of an embedding group in ONE
 // launch (blockIdx.y = table) -- the executor fuses the independent per-table Embedding ops of a
 // DLRM graph (26 ops in the MLPerf config) into one forward and two backward launches.
+// The index width (int32/int64) is a template parameter and every load in the hot loops is
+// unconditional (clamped address, predicated use): a runtime width test or a guarded load makes
+// the compiler emit a branch + s_waitcnt vmcnt(0) per load, i.e. one HBM round trip per sample
+// (measured 3-8x slowdowns before this rule was applied).
 //
 // Forward: lane = 4 consecutive columns of one sample (D/4 lanes per row: a 512-B fp32 row of a
 // D=128 table is read by 32 lanes with 16-B loads), sum over the bag, bf16/fp32 output written
-// with 8/16-B stores straight into the consumer's buffer (row stride ldo).  No 64-bit div/mod in
-// the loop (lane->column mapping fixed per block).
+// with 8/16-B stores straight into the consumer's buffer (row stride ldo).
 // Backward (fused sparse SGD: W[idx] -= lr*scale*dy; or dense-grad accumulate when lr == null):
-//   * large tables: one wave-instruction = 64 consecutive fp32 atomic adds (256 contiguous bytes:
+//   * regular tables: one wave-instruction = 64 consecutive fp32 atomic adds (256 contiguous bytes:
 //     the full gfx950 atomic rate, MI355X_MICROARCH "Global float atomics");
-//   * tiny tables (rows*D*4 <= 64 KiB): block-private LDS accumulation over a chunk of samples, then
-//     one global atomic per (row, column) per block -- avoids the ~14x slowdown of many adders on
-//     one row (table with 3 rows in the MLPerf set).
+//   * tiny tables (<= 16 rows: 3, 4, 10, 14 rows in the MLPerf set): thousands of samples hit the
+//     same few addresses, which L2 serialises; each wave accumulates into a PRIVATE LDS copy of the
+//     table gradient with plain read-add-write (row index wave-uniform, lane = column: 64 distinct
+//     banks, no atomics), the block sums its waves' copies and flushes one atomic per (row, col).
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 namespace {
 
 constexpr int MAXT = 32;
+constexpr int TINY_ROWS = 16;
 
 struct TabDesc {
   const float* W;     // fwd: table (read); bwd: table or dense grad (written)
   const void* idx;    // [B, bag] int32/int64
   void* act;          // fwd: out [B, *] (row stride ld); bwd: dy
   long ld;
-  int rows, D, bag, idx64;
+  int rows, D, bag;
   float scale;
 };
 struct TabSet {
@@ -37,11 +43,13 @@ struct TabSet {
   int n;
 };
 
-FM_DEVICE long load_idx(const void* p, long i, int idx64) {
-  return idx64 ? (long)reinterpret_cast<const long long*>(p)[i] : (long)reinterpret_cast<const int*>(p)[i];
+template <bool I64>
+FM_DEVICE long ldi(const void* p, long i) {
+  if constexpr (I64) return (long)reinterpret_cast<const long long*>(p)[i];
+  else return (long)reinterpret_cast<const int*>(p)[i];
 }
 
-template <typename OutT>
+template <typename OutT, bool I64>
 __global__ void __launch_bounds__(256) fm_emb_fwd_multi(TabSet s, long B) {
   const TabDesc& d = s.t[blockIdx.y];
   const int D4 = d.D >> 2;
@@ -54,7 +62,7 @@ __global__ void __launch_bounds__(256) fm_emb_fwd_multi(TabSet s, long B) {
       const int c = c4 * 4;
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
       for (int j = 0; j < d.bag; ++j) {
-        long r = load_idx(d.idx, b * d.bag + j, d.idx64);
+        long r = ldi<I64>(d.idx, b * d.bag + j);
         acc += *reinterpret_cast<const f32x4_t*>(d.W + r * d.D + c);
       }
       acc *= d.scale;
@@ -71,7 +79,7 @@ __global__ void __launch_bounds__(256) fm_emb_fwd_multi(TabSet s, long B) {
 }
 
 // scalar fallback for D % 4 != 0 (any D)
-template <typename OutT>
+template <typename OutT, bool I64>
 __global__ void __launch_bounds__(256) fm_emb_fwd_multi_scalar(TabSet s, long B) {
   const TabDesc& d = s.t[blockIdx.y];
   const int lpr = d.D < 256 ? d.D : 256;
@@ -81,12 +89,12 @@ __global__ void __launch_bounds__(256) fm_emb_fwd_multi_scalar(TabSet s, long B)
   for (long b = (long)blockIdx.x * rpi + sub; b < B; b += (long)gridDim.x * rpi)
     for (int c = lc; c < d.D; c += lpr) {
       float acc = 0.f;
-      for (int j = 0; j < d.bag; ++j) acc += d.W[load_idx(d.idx, b * d.bag + j, d.idx64) * d.D + c];
+      for (int j = 0; j < d.bag; ++j) acc += d.W[ldi<I64>(d.idx, b * d.bag + j) * d.D + c];
       st<OutT>(reinterpret_cast<OutT*>(d.act) + b * d.ld + c, acc * d.scale);
     }
 }
 
-template <typename GT>
+template <typename GT, bool I64>
 __global__ void __launch_bounds__(256) fm_emb_bwd_atomic_multi(TabSet s, const float* __restrict__ lr, long B) {
   const TabDesc& d = s.t[blockIdx.y];
   const float mul = (lr ? -lr[0] : 1.f) * d.scale;
@@ -96,59 +104,53 @@ __global__ void __launch_bounds__(256) fm_emb_bwd_atomic_multi(TabSet s, const f
   if (sub >= rpi) return;
   float* W = const_cast<float*>(d.W);
   const GT* dy = reinterpret_cast<const GT*>(d.act);
-  for (long b = (long)blockIdx.x * rpi + sub; b < B; b += (long)gridDim.x * rpi)
+  for (long b = (long)blockIdx.x * rpi + sub; b < B; b += (long)gridDim.x * rpi) {
+    const long r0 = ldi<I64>(d.idx, b * d.bag);
     for (int c = lc; c < d.D; c += lpr) {
       const float g = ld<GT>(dy + b * d.ld + c) * mul;
-      for (int j = 0; j < d.bag; ++j) atomicAdd(W + load_idx(d.idx, b * d.bag + j, d.idx64) * d.D + c, g);
+      atomicAdd(W + r0 * d.D + c, g);
+      for (int j = 1; j < d.bag; ++j) atomicAdd(W + ldi<I64>(d.idx, b * d.bag + j) * d.D + c, g);
     }
+  }
 }
 
-// Tiny tables: block-private LDS copy of the table's gradient.  One WAVE per sample row
-// (lane = column, columns l, l+64, ... so every LDS add of a wave hits 64 distinct banks and
-// no two lanes of a wave ever add to the same address), U samples in flight per wave, a short
-// chunk of samples per block so that the grid has >= 1024 blocks (latency-bound otherwise:
-// the previous 32-block grid ran 128 dependent samples per wave).  The flush adds only touched
-// rows (nonzero) into the table: <= chunk rows per block.
-template <typename GT>
-__global__ void __launch_bounds__(256) fm_emb_bwd_lds_multi(TabSet s, const float* __restrict__ lr, long B,
-                                                             int chunk) {
+template <typename GT, bool I64>
+__global__ void __launch_bounds__(256) fm_emb_bwd_tiny_multi(TabSet s, const float* __restrict__ lr, long B, int chunk) {
+  constexpr int S = 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* acc = reinterpret_cast<float*>(smem);
+  float* red = reinterpret_cast<float*>(smem);     // [4][rows*D]
   const TabDesc& d = s.t[blockIdx.y];
   const long b0 = (long)blockIdx.x * chunk;
   if (b0 >= B) return;
   const long b1 = min(B, b0 + chunk);
-  const int n = d.rows * d.D;
-  for (int i = threadIdx.x; i < n; i += 256) acc[i] = 0.f;
-  __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n = d.rows * d.D;
+  float* mine = red + wave * n;
+  for (int i = lane; i < n; i += 64) mine[i] = 0.f;
   const GT* dy = reinterpret_cast<const GT*>(d.act);
-  constexpr int U = 4;
-  for (long b = b0 + wave; b < b1; b += 4 * U) {
-    long r[U];
-    bool ok[U];
+  for (long bw = b0 + (long)wave * S; bw < b1; bw += 4L * S) {
+    for (int c0 = 0; c0 < d.D; c0 += 128) {
+      const int ca = c0 + lane, cb = c0 + 64 + lane;
+      const int sa = min(ca, d.D - 1), sb = min(cb, d.D - 1);   // clamped: loads stay unconditional
+      long r[S];
+      float ga[S], gb[S];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long bb = b + 4L * u;
-      ok[u] = bb < b1;
-      r[u] = ok[u] ? load_idx(d.idx, bb * d.bag, d.idx64) : 0;
-    }
-    for (int c = lane; c < d.D; c += 64) {
-      float g[U];
+      for (int u = 0; u < S; ++u) {
+        const long bu = min(bw + u, b1 - 1);
+        r[u] = ldi<I64>(d.idx, bu * d.bag);
+        ga[u] = ld<GT>(dy + bu * d.ld + sa);
+        gb[u] = ld<GT>(dy + bu * d.ld + sb);
+      }
 #pragma unroll
-      for (int u = 0; u < U; ++u) g[u] = ok[u] ? ld<GT>(dy + (b + 4L * u) * d.ld + c) : 0.f;
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (ok[u]) atomicAdd(acc + r[u] * d.D + c, g[u]);
-    }
-    if (d.bag > 1) {   // remaining bag entries (same gradient row)
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (!ok[u]) continue;
-        const long bb = b + 4L * u;
-        for (int j = 1; j < d.bag; ++j) {
-          const long rj = load_idx(d.idx, bb * d.bag + j, d.idx64);
-          for (int c = lane; c < d.D; c += 64) atomicAdd(acc + rj * d.D + c, ld<GT>(dy + bb * d.ld + c));
+      for (int u = 0; u < S; ++u) {
+        if (bw + u >= b1) break;                       // wave-uniform
+        float* p = mine + r[u] * d.D;
+        if (ca < d.D) p[ca] += ga[u];
+        if (cb < d.D) p[cb] += gb[u];
+        for (int j = 1; j < d.bag; ++j) {              // further bag entries share the gradient row
+          float* q = mine + ldi<I64>(d.idx, (bw + u) * d.bag + j) * d.D;
+          if (ca < d.D) q[ca] += ga[u];
+          if (cb < d.D) q[cb] += gb[u];
         }
       }
     }
@@ -157,39 +159,70 @@ __global__ void __launch_bounds__(256) fm_emb_bwd_lds_multi(TabSet s, const floa
   const float mul = (lr ? -lr[0] : 1.f) * d.scale;
   float* W = const_cast<float*>(d.W);
   for (int i = threadIdx.x; i < n; i += 256) {
-    float v = acc[i];
+    const float v = red[i] + red[n + i] + red[2 * n + i] + red[3 * n + i];
     if (v != 0.f) atomicAdd(W + i, v * mul);
   }
 }
 
-constexpr long TINY_BYTES = 64 * 1024;
+template <bool I64>
+void launch_fwd(const TabSet& s, int m, bool vec, bool out_bf16, long B, int D0, hipStream_t st) {
+  const int rpi = std::max(1, 256 / std::min(64, std::max(1, D0 / 4)));
+  dim3 grid((unsigned)std::max<long>(1, std::min<long>((B + rpi - 1) / rpi, 2048)), m);
+  if (vec) {
+    if (out_bf16) hipLaunchKernelGGL((fm_emb_fwd_multi<unsigned short, I64>), grid, dim3(256), 0, st, s, B);
+    else hipLaunchKernelGGL((fm_emb_fwd_multi<float, I64>), grid, dim3(256), 0, st, s, B);
+  } else {
+    if (out_bf16) hipLaunchKernelGGL((fm_emb_fwd_multi_scalar<unsigned short, I64>), grid, dim3(256), 0, st, s, B);
+    else hipLaunchKernelGGL((fm_emb_fwd_multi_scalar<float, I64>), grid, dim3(256), 0, st, s, B);
+  }
+}
+
+template <bool I64>
+void launch_bwd(const TabSet& s, int m, bool tiny, bool dy_bf16, const float* lr, long B, int maxD, hipStream_t st) {
+  if (tiny) {
+    size_t lds = 0;
+    for (int i = 0; i < m; ++i) lds = std::max(lds, (size_t)s.t[i].rows * s.t[i].D * 4 * 4);  // one copy per wave
+    static const int env_chunk = getenv("FM_TINY_CHUNK") ? atoi(getenv("FM_TINY_CHUNK")) : 0;
+    // 64-sample chunks keep the per-wave chain to one round trip; at large B more blocks would
+    // pile onto the same few addresses in the flush (tools/bench_embedding.py: B=8192 -> 64,
+    // B=65536 -> 128..256)
+    const int chunk = env_chunk > 0 ? env_chunk : (B <= 16384 ? 64 : B <= 32768 ? 128 : 256);
+    dim3 grid((unsigned)((B + chunk - 1) / chunk), m);
+    if (dy_bf16) hipLaunchKernelGGL((fm_emb_bwd_tiny_multi<unsigned short, I64>), grid, dim3(256), lds, st, s, lr, B, chunk);
+    else hipLaunchKernelGGL((fm_emb_bwd_tiny_multi<float, I64>), grid, dim3(256), lds, st, s, lr, B, chunk);
+  } else {
+    const int rpi = std::max(1, 256 / std::min(256, maxD));
+    dim3 grid((unsigned)std::max<long>(1, std::min<long>((B + rpi - 1) / rpi, 2048)), m);
+    if (dy_bf16) hipLaunchKernelGGL((fm_emb_bwd_atomic_multi<unsigned short, I64>), grid, dim3(256), 0, st, s, lr, B);
+    else hipLaunchKernelGGL((fm_emb_bwd_atomic_multi<float, I64>), grid, dim3(256), 0, st, s, lr, B);
+  }
+}
 
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
-// Launchers.  Arrays describe n tables; act/ld = outputs (fwd) or output grads (bwd).
+// Launchers.  Arrays describe n tables; act/ld = outputs (fwd) or output grads (bwd).  Tables
+// are batched by index width (and, in backward, by kernel kind) into launches of <= 32 tables.
 extern "C" void fm_embedding_fwd_multi(int n, const float* const* W, const void* const* idx, const int* idx64,
                                        void* const* out, const long* ldo, const int* rows, const int* D, const int* bag,
                                        const float* scale, int out_bf16, long B, hipStream_t st) {
   if (B <= 0) return;
-  for (int base = 0; base < n; base += MAXT) {
-    TabSet s;
-    int m = std::min(MAXT, n - base);
-    bool vec = true;
-    for (int i = 0; i < m; ++i) {
-      int k = base + i;
-      s.t[i] = TabDesc{W[k], idx[k], out[k], ldo[k], rows[k], D[k], bag[k], idx64[k], scale[k]};
-      vec = vec && (D[k] % 4 == 0) && (ldo[k] % 4 == 0) && D[k] <= 256;
-    }
-    s.n = m;
-    const int rpi = std::max(1, 256 / std::min(64, std::max(1, D[base] / 4)));
-    dim3 grid((unsigned)std::max<long>(1, std::min<long>((B + rpi - 1) / rpi, 2048)), m);
-    if (vec) {
-      if (out_bf16) hipLaunchKernelGGL(fm_emb_fwd_multi<unsigned short>, grid, dim3(256), 0, st, s, B);
-      else hipLaunchKernelGGL(fm_emb_fwd_multi<float>, grid, dim3(256), 0, st, s, B);
-    } else {
-      if (out_bf16) hipLaunchKernelGGL(fm_emb_fwd_multi_scalar<unsigned short>, grid, dim3(256), 0, st, s, B);
-      else hipLaunchKernelGGL(fm_emb_fwd_multi_scalar<float>, grid, dim3(256), 0, st, s, B);
+  for (int wide = 0; wide < 2; ++wide) {
+    std::vector<int> sel;
+    for (int k = 0; k < n; ++k)
+      if ((idx64[k] != 0) == (wide != 0)) sel.push_back(k);
+    for (size_t base = 0; base < sel.size(); base += MAXT) {
+      TabSet s;
+      int m = (int)std::min<size_t>(MAXT, sel.size() - base);
+      bool vec = true;
+      for (int i = 0; i < m; ++i) {
+        int k = sel[base + i];
+        s.t[i] = TabDesc{W[k], idx[k], out[k], ldo[k], rows[k], D[k], bag[k], scale[k]};
+        vec = vec && (D[k] % 4 == 0) && (ldo[k] % 4 == 0) && D[k] <= 256;
+      }
+      s.n = m;
+      if (wide) launch_fwd<true>(s, m, vec, out_bf16, B, D[sel[base]], st);
+      else launch_fwd<false>(s, m, vec, out_bf16, B, D[sel[base]], st);
     }
   }
 }
@@ -200,38 +233,25 @@ extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const
                                        const int* bag, const float* scale, int dy_bf16, const float* lr, long B,
                                        hipStream_t st) {
   if (B <= 0) return;
-  // partition: tiny tables -> LDS kernel, others -> atomic kernel
-  for (int pass = 0; pass < 2; ++pass) {
+  for (int pass = 0; pass < 4; ++pass) {
+    const bool tiny = pass < 2, wide = pass & 1;
     std::vector<int> sel;
     for (int k = 0; k < n; ++k) {
-      bool tiny = (long)rows[k] * D[k] * 4 <= TINY_BYTES && B * (long)bag[k] >= 4L * rows[k];
-      if ((pass == 0) == tiny) sel.push_back(k);
+      bool t = rows[k] <= TINY_ROWS && D[k] <= 256 && B * (long)bag[k] >= 16L * rows[k];
+      if (t == tiny && (idx64[k] != 0) == wide) sel.push_back(k);
     }
     for (size_t base = 0; base < sel.size(); base += MAXT) {
       TabSet s;
       int m = (int)std::min<size_t>(MAXT, sel.size() - base);
-      int maxD = 1, maxrows = 1;
+      int maxD = 1;
       for (int i = 0; i < m; ++i) {
         int k = sel[base + i];
-        s.t[i] = TabDesc{W[k], idx[k], const_cast<void*>(dy[k]), ldg[k], rows[k], D[k], bag[k], idx64[k], scale[k]};
+        s.t[i] = TabDesc{W[k], idx[k], const_cast<void*>(dy[k]), ldg[k], rows[k], D[k], bag[k], scale[k]};
         maxD = std::max(maxD, D[k]);
-        maxrows = std::max(maxrows, rows[k]);
       }
       s.n = m;
-      if (pass == 0) {
-        size_t lds = (size_t)0;
-        for (int i = 0; i < m; ++i) lds = std::max(lds, (size_t)s.t[i].rows * s.t[i].D * 4);
-        // chunk: >= 64 samples (16 per wave), more for larger tables (flush <= rows*D adds per block)
-        int chunk = std::max(64, std::min(512, ((2 * maxrows + 31) / 32) * 32));
-        dim3 grid((unsigned)((B + chunk - 1) / chunk), m);
-        if (dy_bf16) hipLaunchKernelGGL(fm_emb_bwd_lds_multi<unsigned short>, grid, dim3(256), lds, st, s, lr, B, chunk);
-        else hipLaunchKernelGGL(fm_emb_bwd_lds_multi<float>, grid, dim3(256), lds, st, s, lr, B, chunk);
-      } else {
-        const int rpi = std::max(1, 256 / std::min(256, maxD));
-        dim3 grid((unsigned)std::max<long>(1, std::min<long>((B + rpi - 1) / rpi, 2048)), m);
-        if (dy_bf16) hipLaunchKernelGGL(fm_emb_bwd_atomic_multi<unsigned short>, grid, dim3(256), 0, st, s, lr, B);
-        else hipLaunchKernelGGL(fm_emb_bwd_atomic_multi<float>, grid, dim3(256), 0, st, s, lr, B);
-      }
+      if (wide) launch_bwd<true>(s, m, tiny, dy_bf16, lr, B, maxD, st);
+      else launch_bwd<false>(s, m, tiny, dy_bf16, lr, B, maxD, st);
     }
   }
 }

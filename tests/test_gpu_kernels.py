@@ -78,7 +78,7 @@ def test_init_fill_matches_cpu(gpu):
         assert torch.allclose(g.cpu(), cpu, atol=1e-5), type(init)
 
 
-@pytest.mark.parametrize("bag,D,rows", [(1, 128, 100000), (3, 64, 50), (2, 16, 7), (1, 128, 3), (1, 128, 100), (4, 24, 5)])
+@pytest.mark.parametrize("bag,D,rows", [(1, 128, 100000), (3, 64, 50), (2, 16, 7), (1, 128, 3), (1, 128, 30), (1, 128, 100), (4, 24, 5), (1, 200, 9)])
 def test_embedding_fwd_bwd(gpu, bag, D, rows):
     from flexmi.ops import _kernels as Kk
     torch.manual_seed(3)
