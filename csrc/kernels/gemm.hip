@@ -18,35 +18,13 @@
 // Epilogue: alpha, fp32 bias[n], activation (relu/sigmoid/tanh), beta=1 accumulate, bf16 or
 // fp32 output.  Split-K writes fp32 slabs reduced by fm_gemm_splitk_reduce (same epilogue).
 // Blocks are remapped so consecutive tiles share an XCD (private 4 MB L2 per XCD).
-#include "common.h"
+#include "gemm_common.h"
+
+#include <cstdlib>
 
 namespace {
 
-constexpr int BK = 64;
 constexpr int NT = 256;
-
-typedef __attribute__((address_space(3))) bf16x4_t lds_v4_t;
-
-template <int R>
-struct MNSwz;
-template <>
-struct MNSwz<128> {  // 256-B rows, 16 chunks
-  static FM_DEVICE int f(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }
-};
-template <>
-struct MNSwz<64> {  // 128-B rows, 8 chunks
-  static FM_DEVICE int f(int k) { return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1)); }
-};
-
-// byte offset inside an operand LDS image
-template <bool KC, int R>
-FM_DEVICE int lds_off(int row_or_k, int chunk) {
-  if constexpr (KC) {
-    return row_or_k * (BK * 2) + 16 * (chunk ^ ((row_or_k >> 1) & 7));
-  } else {
-    return row_or_k * (R * 2) + 16 * (chunk ^ MNSwz<R>::f(row_or_k));
-  }
-}
 
 // ---- global -> registers (one tile of an operand) --------------------------------------
 template <bool KC, int R, bool VEC>
@@ -116,45 +94,6 @@ struct Stage {
   }
 };
 
-// ---- LDS -> MFMA fragment (8 bf16: k = 8*(lane>>4)+j for row/col lane&15) -------------
-template <bool KC, int R>
-FM_DEVICE bf16x8_t frag(const char* lds, int base, int kk, int lane) {
-  if constexpr (KC) {
-    int row = base + (lane & 15);
-    int chunk = 4 * kk + (lane >> 4);
-    return *reinterpret_cast<const bf16x8_t*>(lds + lds_off<true, R>(row, chunk));
-  } else {
-    int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-    int chunk = (base >> 3) + (p >> 1);
-    int k0 = 32 * kk + 8 * g + q;
-    int o0 = lds_off<false, R>(k0, chunk) + 8 * (p & 1);
-    int o1 = lds_off<false, R>(k0 + 4, chunk) + 8 * (p & 1);
-    bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4_t*)(lds + o0));
-    bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4_t*)(lds + o1));
-    bf16x8_t r;
-    r.lo = lo;
-    r.hi = hi;
-    return r;
-  }
-}
-
-struct GemmP {
-  const unsigned short* A; long lda; long sA;
-  const unsigned short* B; long ldb; long sB;
-  void* C; long ldc; long sC;
-  const float* bias;
-  float* ws;          // split-K slabs [batch][split][M][N]
-  // fused backward epilogue of the producing layer below: v = act'(ay) * v ; colsum[n] += sum_m v
-  const unsigned short* ay;
-  long lday;
-  float* colsum;
-  float* rowsum_a;   // += sum_k A(m,k)  (MN-contiguous A only; used for bias grads in dW GEMMs)
-  int bact;
-  int M, N, K, act, beta, c_fp32, ksplit, batch;
-  float alpha;
-  int tiles_m, tiles_n;
-};
-
 template <int BM, int BN, bool AK, bool BKC, bool VEC>
 __global__ void __launch_bounds__(NT, 2) fm_gemm_kernel(GemmP p) {
   constexpr int A_BYTES = BM * BK * 2;
@@ -172,13 +111,9 @@ __global__ void __launch_bounds__(NT, 2) fm_gemm_kernel(GemmP p) {
   const int wm = wave >> 1, wn = wave & 1;
 
   // XCD-aware bijective remap of the tile id (blocks b and b+8 share an XCD)
-  const int ntiles = p.tiles_m * p.tiles_n;
-  int bid = blockIdx.x;
-  {
-    int q = ntiles / 8, r = ntiles % 8, x = bid % 8;
-    if (ntiles >= 8) bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
-  }
-  const int tm = bid % p.tiles_m, tn = bid / p.tiles_m;
+  const int bid = xcd_remap(blockIdx.x, p.tiles_m * p.tiles_n);
+  int tm, tn;
+  tile_coords(p, bid, tm, tn);
   const int zb = blockIdx.y;           // batch
   const int split = blockIdx.z;
   const int m0 = tm * BM, n0 = tn * BN;
@@ -259,113 +194,7 @@ __global__ void __launch_bounds__(NT, 2) fm_gemm_kernel(GemmP p) {
 
 #undef LDS_A
 #undef LDS_B
-  // ---- epilogue: lane owns C[m][n..n+3], m = lane&15, n = 4*(lane>>4) ------------------
-  const int mrow = lane & 15;
-  const int ncol = 4 * (lane >> 4);
-  if (p.ksplit > 1) {
-    float* ws = p.ws + ((long)zb * p.ksplit + split) * (long)p.M * p.N;
-#pragma unroll
-    for (int i = 0; i < MR; ++i)
-#pragma unroll
-      for (int j = 0; j < NR; ++j) {
-        int m = m0 + wm * (BM / 2) + 16 * i + mrow;
-        int n = n0 + wn * (BN / 2) + 16 * j + ncol;
-        if (m >= p.M) continue;
-        float* dst = ws + (long)m * p.N + n;
-        if (n + 3 < p.N && (p.N & 3) == 0) {
-          *reinterpret_cast<f32x4_t*>(dst) = acc[i][j];
-        } else {
-          for (int r = 0; r < 4; ++r)
-            if (n + r < p.N) dst[r] = acc[i][j][r];
-        }
-      }
-    return;
-  }
-  float csum[NR][4];
-#pragma unroll
-  for (int j = 0; j < NR; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) csum[j][r] = 0.f;
-#pragma unroll
-  for (int i = 0; i < MR; ++i)
-#pragma unroll
-    for (int j = 0; j < NR; ++j) {
-      const int m = m0 + wm * (BM / 2) + 16 * i + mrow;
-      const int n = n0 + wn * (BN / 2) + 16 * j + ncol;
-      const bool mok = m < p.M;
-      const bool full = (n + 3 < p.N);
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * p.alpha;
-      if (p.bias) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += (n + r < p.N) ? p.bias[n + r] : 0.f;
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = act_fwd(p.act, v[r]);
-      if (p.ay) {  // fused activation backward of the layer below (dX -> dpre)
-        float yv[4] = {0.f, 0.f, 0.f, 0.f};
-        if (mok) {
-          const unsigned short* yp = p.ay + (long)m * p.lday + n;
-          if (full && ((p.lday & 3) == 0)) {
-            bf16x4_t t = *reinterpret_cast<const bf16x4_t*>(yp);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) yv[r] = bf2f((unsigned short)t[r]);
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) yv[r] = (n + r < p.N) ? bf2f(yp[r]) : 0.f;
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = act_bwd(p.bact, yv[r], v[r]);
-      }
-      if (p.colsum && mok) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) csum[j][r] += (n + r < p.N) ? v[r] : 0.f;
-      }
-      if (!mok) continue;
-      if (p.c_fp32) {
-        float* dst = reinterpret_cast<float*>(p.C) + (long)zb * p.sC + (long)m * p.ldc + n;
-        if (full && ((p.ldc & 3) == 0) && ((((uintptr_t)dst) & 15) == 0)) {
-          f32x4_t o = {v[0], v[1], v[2], v[3]};
-          if (p.beta) o += *reinterpret_cast<f32x4_t*>(dst);
-          *reinterpret_cast<f32x4_t*>(dst) = o;
-        } else {
-          for (int r = 0; r < 4; ++r)
-            if (n + r < p.N) dst[r] = v[r] + (p.beta ? dst[r] : 0.f);
-        }
-      } else {
-        unsigned short* dst = reinterpret_cast<unsigned short*>(p.C) + (long)zb * p.sC + (long)m * p.ldc + n;
-        if (full && ((p.ldc & 3) == 0) && ((((uintptr_t)dst) & 7) == 0)) {
-          if (p.beta) {
-            bf16x4_t old = *reinterpret_cast<bf16x4_t*>(dst);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] += bf2f((unsigned short)old[r]);
-          }
-          bf16x4_t o;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(v[r]);
-          *reinterpret_cast<bf16x4_t*>(dst) = o;
-        } else {
-          for (int r = 0; r < 4; ++r)
-            if (n + r < p.N) dst[r] = f2bf(v[r] + (p.beta ? bf2f(dst[r]) : 0.f));
-        }
-      }
-    }
-  if (p.colsum) {  // bias gradient of the layer below: reduce the 16 rows of each lane group, 1 atomic/col
-#pragma unroll
-    for (int j = 0; j < NR; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float x = csum[j][r];
-        x += __shfl_xor(x, 1, 64);
-        x += __shfl_xor(x, 2, 64);
-        x += __shfl_xor(x, 4, 64);
-        x += __shfl_xor(x, 8, 64);
-        const int n = n0 + wn * (BN / 2) + 16 * j + ncol + r;
-        if (mrow == 0 && n < p.N) atomicAdd(p.colsum + n, x);
-      }
-  }
+  gemm_epilogue<MR, NR>(p, acc, zb, split, m0 + wm * (BM / 2), n0 + wn * (BN / 2), lane);
 }
 
 __global__ void fm_gemm_splitk_reduce(GemmP p) {
@@ -415,6 +244,9 @@ void launch_bm(const GemmP& p, bool ak, bool bk, bool vec, hipStream_t s) {
 
 }  // namespace
 
+extern "C" void fm_gemm_glds_launch(const void* params, int bm, int bn, int a_kcontig, int b_kcontig,
+                                    hipStream_t stream);
+
 // A_kcontig: A stored [M][K] (lda >= K) else [K][M] (lda >= M)
 // B_kcontig: B stored [N][K] (ldb >= K) else [K][N] (ldb >= N)
 extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
@@ -432,10 +264,38 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
   p.bias = bias; p.M = M; p.N = N; p.K = K; p.act = act; p.beta = beta; p.c_fp32 = c_fp32;
   p.alpha = alpha; p.batch = batch; p.ws = ws;
   p.ay = (const unsigned short*)act_y; p.lday = lday; p.bact = bwd_act; p.colsum = colsum; p.rowsum_a = rowsum_a;
+  p.n_fast = M >= N;
   // vector (16-B) loads need the contiguous extent and leading dims to be multiples of 8
   auto al = [](const void* q) { return (((uintptr_t)q) & 15) == 0; };
   bool vec = al(A) && al(B) && (lda % 8 == 0) && (ldb % 8 == 0) && (sA % 8 == 0) && (sB % 8 == 0);
   vec = vec && (a_kcontig ? (K % 8 == 0) : (M % 8 == 0)) && (b_kcontig ? (K % 8 == 0) : (N % 8 == 0));
+  // LDS-DMA pipelined kernel (gemm_glds.hip) whenever K-tiles are whole
+  static const bool no_glds = getenv("FM_GEMM_NO_GLDS") != nullptr;
+  // (measured, tools/bench_gemm.py in hipGraph mode: the pipelined kernel wins for K-contiguous
+  // operands once 256x128 tiles fill the chip; MN-contiguous (transposed-read) operands and small
+  // grids stay on the register-staged kernel's 128x64/128x128 tiles)
+  const long t256 = (long)((M + 255) / 256) * ((N + 127) / 128) * batch;
+  if (vec && !no_glds && K > 0 && K % BK == 0 && M >= 8 && N >= 8 && a_kcontig && b_kcontig && t256 >= 256) {
+    const int bm = 256;
+    p.tiles_m = (M + bm - 1) / bm;
+    p.tiles_n = (N + 127) / 128;
+    const long tiles = (long)p.tiles_m * p.tiles_n * batch;
+    const int ktiles = K / BK;
+    int ks = 1;
+    if (ksplit_req > 0) ks = ksplit_req;
+    else if (ws != nullptr) {
+      while (tiles * ks < 200 && ks * 2 <= ktiles / 4 && ks < 16) ks *= 2;
+    }
+    if (act_y != nullptr || colsum != nullptr) ks = 1;
+    if (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks = 1;
+    p.ksplit = ks;
+    fm_gemm_glds_launch(&p, bm, 128, a_kcontig, b_kcontig, stream);
+    if (p.ksplit > 1) {
+      long total = (long)M * N * batch;
+      hipLaunchKernelGGL(fm_gemm_splitk_reduce, dim3(fm_grid(total)), dim3(256), 0, stream, p);
+    }
+    return p.ksplit;
+  }
   // tile choice: 128x128 when it yields >= 2 waves of blocks on 256 CUs, else narrower N
   int BMv = 128, BNv = 128;
   long t128 = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;

@@ -8,7 +8,7 @@ import time
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from flexmi.ops import _kernels as K  # noqa: E402
 
 B = 8192
@@ -16,20 +16,42 @@ LAYERS = [(16, 512), (512, 256), (256, 128), (480, 1024), (1024, 1024), (1024, 5
 
 
 def timeit(fn, iters=20):
-    for _ in range(3):
-        fn()
+    """GPU time per call: `iters` calls captured in one hipGraph (host launch cost excluded)."""
+    fn()
     torch.cuda.synchronize()
-    t = time.perf_counter()
-    for _ in range(iters):
-        fn()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(iters):
+                fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
     torch.cuda.synchronize()
-    return (time.perf_counter() - t) / iters
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e-3 / iters
 
 
 def main():
     dev = torch.device("cuda")
     rows = []
-    for (k, n) in LAYERS:
+    global B
+    layers = LAYERS
+    if len(sys.argv) > 1:   # custom shapes "M,K,N;M,K,N"
+        layers = []
+        for t in sys.argv[1].split(";"):
+            m_, k_, n_ = (int(v) for v in t.split(","))
+            layers.append((m_, k_, n_))
+    for spec in layers:
+        if len(spec) == 3:
+            B, k, n = spec
+        else:
+            k, n = spec
         x = torch.randn(B, k, device=dev).bfloat16()
         w = torch.randn(n, k, device=dev).bfloat16()
         dy = torch.randn(B, n, device=dev).bfloat16()
