@@ -430,7 +430,7 @@ extern "C" void fm_skinny_fwd(const void* x, long ldx, const void* w, const floa
 extern "C" void fm_skinny_bwd(const void* x, long ldx, const void* w, const void* y, long ldy, const void* dy, long lddy,
                               void* dx, long lddx, int dx_acc, float* dw, float* db, long B, int K, int act, hipStream_t s) {
   if (B <= 0) return;
-  constexpr int ROWS = 256;
+  constexpr int ROWS = 64;   // 128 blocks at B=8192: fills the chip; 128 adders per dW column
   hipLaunchKernelGGL((fm_skinny_bwd_kernel<ROWS>), dim3((unsigned)((B + ROWS - 1) / ROWS)), dim3(256), 0, s,
                      (const unsigned short*)x, ldx, (const unsigned short*)w, (const unsigned short*)y, ldy,
                      (const unsigned short*)dy, lddy, (unsigned short*)dx, lddx, dx_acc, dw, db, B, K, act);
