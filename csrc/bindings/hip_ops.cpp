@@ -58,6 +58,22 @@ void fm_dropout_apply(const void* x, void* y, long n, float rate, unsigned seed,
 
 namespace {
 
+void fm_im2col(const void* x, void* col, int N, int C, int H, int W, int R, int S, int P, int Q, int sh, int sw, int pt,
+               int pl, int ldcol, hipStream_t st);
+void fm_col2im(const void* dcol, void* dx, int N, int C, int H, int W, int R, int S, int P, int Q, int sh, int sw, int pt,
+               int pl, int ldcol, int acc, hipStream_t st);
+void fm_transpose_batched(const void* in, const void* yin, void* out, int N, int A, int B, int act, int mode, hipStream_t st);
+void fm_pool_fwd(const void* x, void* y, int N, int C, int H, int W, int P, int Q, int kh, int kw, int sh, int sw, int pt,
+                 int pl, int is_max, int act, hipStream_t st);
+void fm_pool_bwd(const void* x, const void* y, const void* dy, void* dx, int N, int C, int H, int W, int P, int Q, int kh,
+                 int kw, int sh, int sw, int pt, int pl, int is_max, int act, int acc, hipStream_t st);
+void fm_bn_fwd(const void* x, void* y, const float* gamma, const float* beta, float* stats, float* meaninv, int N, int C,
+               int HW, float eps, int relu, hipStream_t st);
+void fm_bn_bwd(const void* x, const void* y, const void* dy, const float* meaninv, const float* gamma, float* gsum,
+               float* dgamma, float* dbeta, void* dx, int N, int C, int HW, int relu, int acc, hipStream_t st);
+void fm_compact_rows(const float* src, float* dst, int K, int n, int ldp, int acc, hipStream_t st);
+void fm_pad_rows(const void* src, void* dst, int K, int n, int ldp, hipStream_t st);
+
 hipStream_t cur() { return at::hip::getCurrentHIPStream().stream(); }
 
 const void* cptr(const c10::optional<torch::Tensor>& t) { return (t.has_value() && t->defined()) ? t->data_ptr() : nullptr; }
@@ -320,6 +336,83 @@ void dropout(torch::Tensor x, torch::Tensor y, double rate, int64_t seed, int64_
 
 }  // namespace
 
+// ----------------------------------------------------------------------------- CNN
+static void chk4(const torch::Tensor& t, const char* n) {
+  check_cuda(t, n);
+  TORCH_CHECK(t.scalar_type() == torch::kBFloat16 && t.is_contiguous(), n, ": contiguous bf16");
+}
+void im2col(torch::Tensor x, torch::Tensor col, int64_t R, int64_t S, int64_t P, int64_t Q, int64_t sh, int64_t sw,
+            int64_t pt, int64_t pl, int64_t ldcol) {
+  chk4(x, "x");
+  chk4(col, "col");
+  TORCH_CHECK(x.dim() == 4, "im2col: NCHW");
+  const long N = x.size(0), C = x.size(1);
+  TORCH_CHECK(ldcol >= C * R * S && col.numel() >= N * P * Q * ldcol, "im2col: col too small");
+  fm_im2col(x.data_ptr(), col.data_ptr(), N, C, x.size(2), x.size(3), R, S, P, Q, sh, sw, pt, pl, ldcol, cur());
+}
+void col2im(torch::Tensor dcol, torch::Tensor dx, int64_t R, int64_t S, int64_t P, int64_t Q, int64_t sh, int64_t sw,
+            int64_t pt, int64_t pl, int64_t ldcol, bool acc) {
+  chk4(dcol, "dcol");
+  chk4(dx, "dx");
+  const long N = dx.size(0), C = dx.size(1);
+  TORCH_CHECK(ldcol >= C * R * S && dcol.numel() >= N * P * Q * ldcol, "col2im: dcol too small");
+  fm_col2im(dcol.data_ptr(), dx.data_ptr(), N, C, dx.size(2), dx.size(3), R, S, P, Q, sh, sw, pt, pl, ldcol, acc, cur());
+}
+void transpose_batched(torch::Tensor in, c10::optional<torch::Tensor> yin, torch::Tensor out, int64_t N, int64_t A,
+                       int64_t B, int64_t act, int64_t mode) {
+  chk4(out, "out");
+  TORCH_CHECK(in.scalar_type() == torch::kBFloat16 && in.numel() >= N * A * B && out.numel() >= N * A * B,
+              "transpose_batched: bf16 extents");
+  TORCH_CHECK(mode == 0 || (yin.has_value() && yin->numel() >= N * A * B), "transpose_batched: mode 1 needs yin");
+  fm_transpose_batched(in.data_ptr(), cptr(yin), out.data_ptr(), N, A, B, act, mode, cur());
+}
+void pool_fwd(torch::Tensor x, torch::Tensor y, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t pt, int64_t pl,
+              bool is_max, int64_t act) {
+  chk4(x, "x");
+  chk4(y, "y");
+  fm_pool_fwd(x.data_ptr(), y.data_ptr(), x.size(0), x.size(1), x.size(2), x.size(3), y.size(2), y.size(3), kh, kw, sh, sw,
+              pt, pl, is_max, act, cur());
+}
+void pool_bwd(torch::Tensor x, torch::Tensor y, torch::Tensor dy, torch::Tensor dx, int64_t kh, int64_t kw, int64_t sh,
+              int64_t sw, int64_t pt, int64_t pl, bool is_max, int64_t act, bool acc) {
+  chk4(x, "x");
+  chk4(y, "y");
+  chk4(dy, "dy");
+  chk4(dx, "dx");
+  fm_pool_bwd(x.data_ptr(), y.data_ptr(), dy.data_ptr(), dx.data_ptr(), x.size(0), x.size(1), x.size(2), x.size(3),
+              y.size(2), y.size(3), kh, kw, sh, sw, pt, pl, is_max, act, acc, cur());
+}
+void bn_fwd(torch::Tensor x, torch::Tensor y, torch::Tensor gamma, torch::Tensor beta, torch::Tensor stats,
+            torch::Tensor meaninv, double eps, bool relu) {
+  chk4(x, "x");
+  chk4(y, "y");
+  const long C = x.size(1);
+  TORCH_CHECK(gamma.scalar_type() == torch::kFloat32 && beta.scalar_type() == torch::kFloat32 && gamma.numel() >= C,
+              "bn: fp32 gamma/beta [C]");
+  TORCH_CHECK(stats.numel() >= 2 * C && meaninv.numel() >= 2 * C, "bn: stats [2C]");
+  fm_bn_fwd(x.data_ptr(), y.data_ptr(), gamma.data_ptr<float>(), beta.data_ptr<float>(), stats.data_ptr<float>(),
+            meaninv.data_ptr<float>(), x.size(0), C, x.size(2) * x.size(3), (float)eps, relu, cur());
+}
+void bn_bwd(torch::Tensor x, torch::Tensor y, torch::Tensor dy, torch::Tensor meaninv, torch::Tensor gamma,
+            torch::Tensor gsum, torch::Tensor dgamma, torch::Tensor dbeta, c10::optional<torch::Tensor> dx, bool relu,
+            bool acc) {
+  chk4(x, "x");
+  chk4(dy, "dy");
+  const long C = x.size(1);
+  TORCH_CHECK(gsum.numel() >= 2 * C && dgamma.numel() >= C && dbeta.numel() >= C, "bn_bwd: sizes");
+  fm_bn_bwd(x.data_ptr(), y.data_ptr(), dy.data_ptr(), meaninv.data_ptr<float>(), gamma.data_ptr<float>(),
+            gsum.data_ptr<float>(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), mptr(dx), x.size(0), C,
+            x.size(2) * x.size(3), relu, acc, cur());
+}
+void compact_rows(torch::Tensor src, torch::Tensor dst, int64_t K, int64_t n, int64_t ldp, bool acc) {
+  TORCH_CHECK(src.numel() >= K * ldp && dst.numel() >= K * n, "compact_rows: sizes");
+  fm_compact_rows(src.data_ptr<float>(), dst.data_ptr<float>(), K, n, ldp, acc, cur());
+}
+void pad_rows(torch::Tensor src, torch::Tensor dst, int64_t K, int64_t n, int64_t ldp) {
+  TORCH_CHECK(src.numel() >= K * n && dst.numel() >= K * ldp && src.scalar_type() == torch::kBFloat16, "pad_rows: sizes");
+  fm_pad_rows(src.data_ptr(), dst.data_ptr(), K, n, ldp, cur());
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "flexmi HIP/CDNA4 kernels (gfx950)";
   m.def("gemm", &gemm);
@@ -346,5 +439,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("reverse", &reverse);
   m.def("softmax", &softmax);
   m.def("dropout", &dropout);
+  m.def("im2col", &im2col);
+  m.def("col2im", &col2im);
+  m.def("transpose_batched", &transpose_batched);
+  m.def("pool_fwd", &pool_fwd);
+  m.def("pool_bwd", &pool_bwd);
+  m.def("bn_fwd", &bn_fwd);
+  m.def("bn_bwd", &bn_bwd);
+  m.def("compact_rows", &compact_rows);
+  m.def("pad_rows", &pad_rows);
   m.attr("arch") = "gfx950";
 }

@@ -2,9 +2,9 @@
 
 On a GPU run the extension MUST be present: every call goes through :func:`C` which raises if
 ``flexmi._C`` cannot be imported -- there is no silent eager fallback for the hot ops (GEMM,
-embedding, interaction, optimizer, loss, element-wise, data movement).  The only ops still
-routed to PyTorch-ROCm library calls are listed in :data:`LIBRARY_FALLBACK` (CNN conv/pool/BN,
-pending their implicit-GEMM HIP kernels) so the coverage is explicit and testable.
+embedding, interaction, optimizer, loss, element-wise, data movement, and the CNN ops: GEMM
+convolution = HIP im2col/col2im/transposes + the MFMA GEMM, HIP pooling and batch norm).
+:data:`LIBRARY_FALLBACK` lists ops routed to vendor libraries instead (none).
 """
 from __future__ import annotations
 
@@ -15,7 +15,7 @@ import torch
 
 _C = None
 _lock = threading.Lock()
-LIBRARY_FALLBACK = {"conv2d": "torch (MIOpen)", "pool2d": "torch (MIOpen)", "batchnorm": "torch (MIOpen)"}
+LIBRARY_FALLBACK = {}   # every op of the framework runs a flexmi HIP kernel on MI355X
 
 
 def C():
@@ -314,96 +314,98 @@ def dropout_backward(dy, dx, rate, seed, ctx, acc):
     C().dropout(dy, dx, rate, seed + 131 * ctx.rank, ctx.saved.get("step", 0), bool(acc))
 
 
-# ------------------------------------------------------------------ CNN (library fallback, see LIBRARY_FALLBACK)
-def _f(t):
-    return t.float()
+# ------------------------------------------------------------------ CNN
+_scratch = {}
+
+
+def scratch(device, name, numel, dtype=torch.bfloat16):
+    """Grow-only per-device scratch buffers shared by ops that run back to back on one stream
+    (im2col columns, NHWC GEMM outputs, ...).  Sizes settle during the eager warm-up steps, so
+    captured hipGraphs keep valid pointers."""
+    key = (str(device), name, dtype)
+    t = _scratch.get(key)
+    if t is None or t.numel() < numel:
+        t = torch.empty(max(numel, 1), dtype=dtype, device=device)
+        _scratch[key] = t
+    return t[:numel]
+
+
+def _conv_geom(x, w, y):
+    N, Cin, H, W = x.shape
+    Kout, Cg, R, S = w.shape
+    P, Q = y.shape[2], y.shape[3]
+    CRS = Cg * R * S
+    ldc = (CRS + 7) // 8 * 8
+    return N, Cin, H, W, Kout, Cg, R, S, P, Q, CRS, ldc
+
+
+def _conv_weight_matrix(w, Kout, CRS, ldc):
+    if ldc == CRS:
+        return w.reshape(Kout, CRS)
+    wp = scratch(w.device, "conv_wpad", Kout * ldc)
+    C().pad_rows(w.contiguous(), wp, Kout, CRS, ldc)
+    return wp
 
 
 def conv2d_forward(x, w, b, y, stride, pads, act, groups):
-    import torch.nn.functional as F
-    from flexmi.ops.linear import act_forward_torch
-    xp = F.pad(_f(x), (pads[2], pads[3], pads[0], pads[1]))
-    out = F.conv2d(xp, _f(w), None if b is None else b, stride, 0, 1, groups)
-    y.copy_(act_forward_torch(out, act))
+    """GEMM convolution on MFMA: im2col (HIP) -> out[NPQ,K] = col . W^T (+bias, act epilogue)
+    -> NHWC->NCHW tiled transpose (HIP).  pads = (top, bottom, left, right) of this shard."""
+    assert groups == 1, "grouped convolution is not supported on the HIP path"
+    N, Cin, H, W, Kout, Cg, R, S, P, Q, CRS, ldc = _conv_geom(x, w, y)
+    NPQ = N * P * Q
+    col = scratch(x.device, "conv_col", NPQ * ldc)
+    C().im2col(x, col, R, S, P, Q, stride[0], stride[1], pads[0], pads[2], ldc)
+    wm = _conv_weight_matrix(w, Kout, CRS, ldc)
+    out = scratch(x.device, "conv_nhwc", NPQ * Kout)
+    gemm(col, ldc, True, wm, ldc, True, out, Kout, NPQ, Kout, ldc, bias=b, act=act)
+    C().transpose_batched(out, None, y, N, P * Q, Kout, 10, 0)
 
 
 def conv2d_backward(x, w, y, dy, dx, dw, db, stride, pads, act, groups, acc):
-    import torch.nn.functional as F
-    from flexmi.ops.linear import act_backward_torch
-    g = act_backward_torch(_f(dy), _f(y), act)
-    xp = F.pad(_f(x), (pads[2], pads[3], pads[0], pads[1]))
-    gw = torch.nn.grad.conv2d_weight(xp, w.shape, g, stride, 0, 1, groups)
-    dw.copy_(gw)
-    if db is not None:
-        db.copy_(g.sum((0, 2, 3)))
+    """g = act'(y)*dy transposed to NHWC (one fused HIP pass); dW = g^T.col with db from the
+    same GEMM's A-tile row sums; dX = col2im(g . W)."""
+    assert groups == 1, "grouped convolution is not supported on the HIP path"
+    N, Cin, H, W, Kout, Cg, R, S, P, Q, CRS, ldc = _conv_geom(x, w, y)
+    NPQ = N * P * Q
+    g = scratch(x.device, "conv_g", NPQ * Kout)
+    C().transpose_batched(dy, y, g, N, Kout, P * Q, act, 1)
+    col = scratch(x.device, "conv_col", NPQ * ldc)
+    C().im2col(x, col, R, S, P, Q, stride[0], stride[1], pads[0], pads[2], ldc)
+    if ldc == CRS:
+        gemm(g, Kout, False, col, ldc, False, dw.view(Kout, CRS), CRS, Kout, CRS, NPQ, rowsum_a=db)
+    else:
+        dwp = scratch(x.device, "conv_dwpad", Kout * ldc, torch.float32)
+        gemm(g, Kout, False, col, ldc, False, dwp, ldc, Kout, ldc, NPQ, rowsum_a=db)
+        C().compact_rows(dwp, dw.view(-1), Kout, CRS, ldc, False)
     if dx is not None:
-        gx = torch.nn.grad.conv2d_input(xp.shape, _f(w), g, stride, 0, 1, groups)
-        gx = gx[:, :, pads[0]: pads[0] + x.shape[2], pads[2]: pads[2] + x.shape[3]]
-        if acc:
-            dx.add_(gx.to(dx.dtype))
-        else:
-            dx.copy_(gx)
+        wm = _conv_weight_matrix(w, Kout, CRS, ldc)
+        dcol = scratch(x.device, "conv_dcol", NPQ * ldc)
+        gemm(g, Kout, True, wm, ldc, False, dcol, ldc, NPQ, ldc, Kout)
+        C().col2im(dcol, dx, R, S, P, Q, stride[0], stride[1], pads[0], pads[2], ldc, bool(acc))
 
 
 def pool2d_forward(x, y, k, stride, pads, pool_type, act):
-    import torch.nn.functional as F
-    from flexmi.ops.linear import act_forward_torch
-    xf = _f(x)
-    if pool_type == 30:
-        out = F.max_pool2d(F.pad(xf, (pads[2], pads[3], pads[0], pads[1]), value=float("-inf")), k, stride)
-    else:
-        xp = F.pad(xf, (pads[2], pads[3], pads[0], pads[1]))
-        ones = F.pad(torch.ones_like(xf[:1, :1]), (pads[2], pads[3], pads[0], pads[1]))
-        out = F.avg_pool2d(xp, k, stride, divisor_override=1) / F.avg_pool2d(ones, k, stride, divisor_override=1)
-    y.copy_(act_forward_torch(out, act))
+    C().pool_fwd(x, y, k[0], k[1], stride[0], stride[1], pads[0], pads[2], int(pool_type) == 30, int(act))
 
 
 def pool2d_backward(x, y, dy, dx, k, stride, pads, pool_type, act, acc):
-    from flexmi.ops.linear import act_backward_torch
-    g = act_backward_torch(_f(dy), _f(y), act)
-    xx = _f(x).detach().requires_grad_(True)
-    with torch.enable_grad():
-        out = torch.empty(0)
-        yy = torch.empty_like(_f(y))
-        import torch.nn.functional as F
-        if pool_type == 30:
-            out = F.max_pool2d(F.pad(xx, (pads[2], pads[3], pads[0], pads[1]), value=float("-inf")), k, stride)
-        else:
-            xp = F.pad(xx, (pads[2], pads[3], pads[0], pads[1]))
-            ones = F.pad(torch.ones_like(xx[:1, :1]), (pads[2], pads[3], pads[0], pads[1]))
-            out = F.avg_pool2d(xp, k, stride, divisor_override=1) / F.avg_pool2d(ones, k, stride, divisor_override=1)
-        gx, = torch.autograd.grad(out, [xx], g)
-    if acc:
-        dx.add_(gx.to(dx.dtype))
-    else:
-        dx.copy_(gx)
+    C().pool_bwd(x, y, dy, dx, k[0], k[1], stride[0], stride[1], pads[0], pads[2], int(pool_type) == 30, int(act),
+                 bool(acc))
+
+
+def _bn_bufs(saved, C_, device):
+    if "bn_stats" not in saved:
+        saved["bn_stats"] = torch.zeros(2 * C_, dtype=torch.float32, device=device)
+        saved["bn_meaninv"] = torch.zeros(2 * C_, dtype=torch.float32, device=device)
+        saved["bn_gsum"] = torch.zeros(2 * C_, dtype=torch.float32, device=device)
+    return saved["bn_stats"], saved["bn_meaninv"], saved["bn_gsum"]
 
 
 def batchnorm_forward(x, scale, bias, y, relu, eps, saved):
-    xf = _f(x)
-    mean = xf.mean((0, 2, 3))
-    var = xf.var((0, 2, 3), unbiased=False)
-    inv = torch.rsqrt(var + eps)
-    xhat = (xf - mean[None, :, None, None]) * inv[None, :, None, None]
-    out = xhat * scale[None, :, None, None] + bias[None, :, None, None]
-    saved["inv"], saved["xhat"] = inv, xhat
-    y.copy_(torch.relu(out) if relu else out)
+    stats, meaninv, _ = _bn_bufs(saved, x.shape[1], x.device)
+    C().bn_fwd(x, y, scale, bias, stats, meaninv, float(eps), bool(relu))
 
 
 def batchnorm_backward(x, scale, y, dy, dx, dscale, dbias, relu, eps, saved, acc):
-    g = _f(dy)
-    if relu:
-        g = g * (_f(y) > 0)
-    xhat, inv = saved["xhat"], saved["inv"]
-    m = g.shape[0] * g.shape[2] * g.shape[3]
-    dgamma = (g * xhat).sum((0, 2, 3))
-    dbeta = g.sum((0, 2, 3))
-    dscale.copy_(dgamma)
-    dbias.copy_(dbeta)
-    if dx is not None:
-        gx = scale[None, :, None, None] * inv[None, :, None, None] / m * (
-            m * g - dbeta[None, :, None, None] - xhat * dgamma[None, :, None, None])
-        if acc:
-            dx.add_(gx.to(dx.dtype))
-        else:
-            dx.copy_(gx)
+    _, meaninv, gsum = _bn_bufs(saved, x.shape[1], x.device)
+    C().bn_bwd(x, y, dy, meaninv, scale, gsum, dscale, dbias, dx, bool(relu), bool(acc))

@@ -194,3 +194,91 @@ def test_set_get_weights_and_inline_map():
     m.forward()
     out = m.layers[-1].outputs[0].get_array(m.config)
     assert np.allclose(out, W.sum(1)[None, :] + m.parameters[1].get_weights(m)[None, :])
+
+
+# ---------------------------------------------------------------------------- model zoo
+def _zoo_model(name, device="cpu", B=4, **kw):
+    from flexmi.core import FFConfig, FFModel, SGDOptimizer
+    from flexmi.models import zoo
+    cfg = FFConfig()
+    cfg.batchSize = B
+    cfg.device = device
+    cfg.compute_dtype = "bf16" if device == "gpu" else "fp32"
+    cfg.seed = 11
+    m = FFModel(cfg)
+    built = zoo.build(name, m, small=True, **kw)
+    m.compile(SGDOptimizer(m, built.lr * 10), built.loss, built.metrics)
+    return m, built
+
+
+def _zoo_feed(m, built, seed=0):
+    from flexmi.core import DataType
+    rng = np.random.RandomState(seed)
+    ex = m._ex()
+    if "dlrm" in built.extra:
+        dcfg = built.extra["dlrm"]
+        for i, (name, t) in enumerate(built.inputs.items()):
+            if name == "dense":
+                a = np.zeros(t.dims, np.float32)
+                a[:, :13] = rng.rand(t.dims[0], 13)
+                ex.scatter_from_host(t, a)
+            else:
+                ex.scatter_from_host(t, rng.randint(0, dcfg.embedding_size[i - 1], t.dims).astype(np.int64))
+    else:
+        for t in built.inputs.values():
+            ex.scatter_from_host(t, rng.rand(*t.dims).astype(np.float32))
+    lab = m.get_label_tensor()
+    if lab.data_type == DataType.DT_INT32:
+        ex.scatter_from_host(lab, rng.randint(0, built.output.dims[-1], lab.dims).astype(np.int32))
+    else:
+        ex.scatter_from_host(lab, rng.randint(0, 2, lab.dims).astype(np.float32))
+
+
+@pytest.mark.parametrize("name", ["mlp", "mnist_cnn", "cifar10_cnn", "alexnet", "inception_v3", "resnet50",
+                                  "candle_uno", "dlrm"])
+def test_zoo_models_train_cpu(name):
+    m, built = _zoo_model(name)
+    m.init_layers()
+    losses = []
+    for it in range(2):
+        _zoo_feed(m, built, it)
+        m.reset_metrics()
+        m._ex().train_step()
+        losses.append(m.get_perf_metrics().get_loss())
+    assert all(np.isfinite(losses)), losses
+
+
+def test_cifar10_cnn_matches_torch():
+    """flexmi CPU executor vs a plain PyTorch re-implementation (same weights): forward loss and
+    one SGD step of every parameter (the reference op tests' golden style)."""
+    import torch.nn.functional as F
+    m, built = _zoo_model("cifar10_cnn", B=6)
+    ex = m.init_layers()
+    _zoo_feed(m, built, 3)
+    x = torch.from_numpy(ex.gather_to_host(built.inputs["input"]))
+    y = torch.from_numpy(ex.gather_to_host(m.get_label_tensor())).long().view(-1)
+    params = [torch.from_numpy(p.get_weights(m)).requires_grad_(True) for p in m.parameters]
+    ex.train_step()
+    t = x
+    pi = iter(params)
+    for op in m.layers:
+        kind = type(op).__name__
+        if kind == "Conv2D":
+            w, b = next(pi), next(pi)
+            t = torch.relu(F.conv2d(t, w, b, op.sh, op.ph))
+        elif kind == "Pool2D":
+            t = F.max_pool2d(t, op.kh, op.sh)
+        elif kind == "Flat":
+            t = t.reshape(t.shape[0], -1)
+        elif kind == "Linear":
+            w, b = next(pi), next(pi)
+            t = F.linear(t, w, b)
+            if int(op.activation) == 11:
+                t = torch.relu(t)
+        elif kind == "Softmax":
+            pass
+    loss = F.cross_entropy(t, y)
+    grads = torch.autograd.grad(loss, params)
+    lr = m.optimizer.lr
+    for p, g, prm in zip(params, grads, m.parameters):
+        np.testing.assert_allclose(prm.get_weights(m), (p - lr * g).detach().numpy(), rtol=1e-4, atol=1e-5)

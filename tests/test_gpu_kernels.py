@@ -238,3 +238,88 @@ def test_act_bwd_bias(gpu):
     ref = dy.float() * (y.float() > 0)
     assert rel_err(dpre, ref) < 1e-2
     assert torch.allclose(db, ref.sum(0), atol=1e-2, rtol=1e-3)
+
+
+@pytest.mark.parametrize("N,C,H,W,K,R,S,st,pads", [
+    (2, 3, 19, 19, 16, 11, 11, 4, (2, 2, 2, 2)),      # AlexNet conv1-like (CRS=363: padded columns)
+    (3, 16, 9, 9, 24, 3, 3, 1, (1, 1, 1, 1)),
+    (2, 8, 8, 8, 16, 1, 1, 1, (0, 0, 0, 0)),
+    (2, 8, 10, 7, 8, 3, 3, 2, (0, 1, 1, 0)),           # asymmetric (halo-shard) pads
+])
+def test_conv2d_hip(gpu, N, C, H, W, K, R, S, st, pads):
+    import torch.nn.functional as F
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(5)
+    x = torch.randn(N, C, H, W, device=gpu).bfloat16()
+    w = (torch.randn(K, C, R, S, device=gpu) * 0.1).bfloat16()
+    b = torch.randn(K, device=gpu)
+    xp = F.pad(x.float(), (pads[2], pads[3], pads[0], pads[1]))
+    ref = torch.relu(F.conv2d(xp, w.float(), b, st))
+    y = torch.empty(ref.shape, device=gpu, dtype=torch.bfloat16)
+    Kk.conv2d_forward(x, w, b, y, (st, st), pads, 11, 1)
+    assert rel_err(y, ref) < 2e-2
+    dy = torch.randn(ref.shape, device=gpu).bfloat16()
+    dx = torch.empty_like(x)
+    dw = torch.zeros(K, C, R, S, device=gpu)
+    db = torch.zeros(K, device=gpu)
+    Kk.conv2d_backward(x, w, y, dy, dx, dw, db, (st, st), pads, 11, 1, False)
+    g = dy.float() * (y.float() > 0)
+    xr = xp.clone().requires_grad_(True)
+    wr = w.float().clone().requires_grad_(True)
+    out = F.conv2d(xr, wr, None, st)
+    gx, gw = torch.autograd.grad(out, [xr, wr], g)
+    gx = gx[:, :, pads[0]: pads[0] + H, pads[2]: pads[2] + W]
+    assert rel_err(dw, gw) < 2e-2
+    assert rel_err(db, g.sum((0, 2, 3))) < 2e-2
+    assert rel_err(dx, gx) < 2e-2
+
+
+@pytest.mark.parametrize("kind", [30, 31])
+def test_pool2d_hip(gpu, kind):
+    import torch.nn.functional as F
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(6)
+    x = torch.randn(2, 5, 13, 11, device=gpu).bfloat16()
+    k, st, pads = (3, 3), (2, 2), (1, 1, 1, 1)
+    xf = x.float().requires_grad_(True)
+    if kind == 30:
+        ref = F.max_pool2d(F.pad(xf, (1, 1, 1, 1), value=float("-inf")), k, st)
+    else:
+        s_ = F.avg_pool2d(F.pad(xf, (1, 1, 1, 1)), k, st, divisor_override=1)
+        cnt = F.avg_pool2d(F.pad(torch.ones_like(xf[:1, :1]), (1, 1, 1, 1)), k, st, divisor_override=1)
+        ref = s_ / cnt
+    y = torch.empty(ref.shape, device=gpu, dtype=torch.bfloat16)
+    Kk.pool2d_forward(x, y, k, st, pads, kind, 10)
+    assert rel_err(y, ref) < 1e-2
+    dy = torch.randn(ref.shape, device=gpu).bfloat16()
+    gx, = torch.autograd.grad(ref, [xf], dy.float())
+    dx = torch.empty_like(x)
+    Kk.pool2d_backward(x, y, dy, dx, k, st, pads, kind, 10, False)
+    assert rel_err(dx, gx) < 2e-2
+
+
+def test_batchnorm_hip(gpu):
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(7)
+    x = torch.randn(4, 6, 7, 5, device=gpu).bfloat16()
+    gam = torch.rand(6, device=gpu) + 0.5
+    bet = torch.randn(6, device=gpu)
+    xf = x.float().requires_grad_(True)
+    mean = xf.mean((0, 2, 3), keepdim=True)
+    var = xf.var((0, 2, 3), unbiased=False, keepdim=True)
+    ref = torch.relu((xf - mean) / torch.sqrt(var + 1e-5) * gam[None, :, None, None] + bet[None, :, None, None])
+    y = torch.empty_like(x)
+    saved = {}
+    Kk.batchnorm_forward(x, gam, bet, y, True, 1e-5, saved)
+    assert rel_err(y, ref) < 1e-2
+    dy = torch.randn_like(ref).bfloat16()
+    gx, = torch.autograd.grad(ref, [xf], dy.float())
+    dx = torch.empty_like(x)
+    dg = torch.empty(6, device=gpu)
+    dbt = torch.empty(6, device=gpu)
+    Kk.batchnorm_backward(x, gam, y, dy, dx, dg, dbt, True, 1e-5, saved, False)
+    g = dy.float() * (ref > 0)
+    xhat = (xf - mean) / torch.sqrt(var + 1e-5)
+    assert rel_err(dbt, g.sum((0, 2, 3))) < 2e-2
+    assert rel_err(dg, (g * xhat).sum((0, 2, 3))) < 2e-2
+    assert rel_err(dx, gx) < 3e-2

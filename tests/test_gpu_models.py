@@ -108,3 +108,35 @@ def test_hip_graph_capture_matches_eager(gpu):
         res.append([w.get_weights(m) for w in m.parameters])
     for a, b in zip(*res):
         assert np.allclose(a, b, atol=1e-5), a.shape
+
+
+@pytest.mark.parametrize("name,steps", [("mnist_cnn", 3), ("cifar10_cnn", 3), ("alexnet", 2), ("resnet50", 2),
+                                        ("inception_v3", 1), ("candle_uno", 3)])
+def test_zoo_gpu_matches_cpu(gpu, name, steps):
+    """Every zoo model trains on the HIP kernels (bf16, GEMM convolution, HIP pooling) like the
+    fp32 CPU executor: parameters after a few SGD steps agree within bf16 tolerance."""
+    from tests.test_cpu_models import _zoo_feed, _zoo_model
+    res = {}
+    for dev in ("cpu", "gpu"):
+        m, built = _zoo_model(name, device=dev, B=8)
+        m.init_layers()
+        for it in range(steps):
+            _zoo_feed(m, built, it)
+            m._ex().train_step()
+        res[dev] = [p.get_weights(m) for p in m.parameters]
+    for a, b in zip(res["cpu"], res["gpu"]):
+        assert np.abs(a - b).max() < 4e-2 * max(1.0, np.abs(a).max()), (name, a.shape, np.abs(a - b).max())
+
+
+def test_resnet_batchnorm_gpu_matches_cpu(gpu):
+    from tests.test_cpu_models import _zoo_feed, _zoo_model
+    res = {}
+    for dev in ("cpu", "gpu"):
+        m, built = _zoo_model("resnet50", device=dev, B=8, batch_norm=True)
+        m.init_layers()
+        for it in range(2):
+            _zoo_feed(m, built, it)
+            m._ex().train_step()
+        res[dev] = [p.get_weights(m) for p in m.parameters]
+    for a, b in zip(res["cpu"], res["gpu"]):
+        assert np.abs(a - b).max() < 5e-2 * max(1.0, np.abs(a).max()), (a.shape, np.abs(a - b).max())
