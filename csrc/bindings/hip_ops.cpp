@@ -54,10 +54,6 @@ void fm_reverse_axis(const void* x, void* y, long outer, long len, long inner, i
 void fm_softmax_fwd(const void* x, void* y, long rows, int C, int bf16, hipStream_t s);
 void fm_dropout_apply(const void* x, void* y, long n, float rate, unsigned seed, unsigned step, int acc, int bf16,
                       hipStream_t s);
-}
-
-namespace {
-
 void fm_im2col(const void* x, void* col, int N, int C, int H, int W, int R, int S, int P, int Q, int sh, int sw, int pt,
                int pl, int ldcol, hipStream_t st);
 void fm_col2im(const void* dcol, void* dx, int N, int C, int H, int W, int R, int S, int P, int Q, int sh, int sw, int pt,
@@ -73,6 +69,9 @@ void fm_bn_bwd(const void* x, const void* y, const void* dy, const float* meanin
                float* dgamma, float* dbeta, void* dx, int N, int C, int HW, int relu, int acc, hipStream_t st);
 void fm_compact_rows(const float* src, float* dst, int K, int n, int ldp, int acc, hipStream_t st);
 void fm_pad_rows(const void* src, void* dst, int K, int n, int ldp, hipStream_t st);
+}
+
+namespace {
 
 hipStream_t cur() { return at::hip::getCurrentHIPStream().stream(); }
 
