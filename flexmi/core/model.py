@@ -275,6 +275,15 @@ class FFModel:
         ex.training = True
 
     # ------------------------------------------------------------------ introspection
+    # ---- checkpoint / resume (reshard-on-load across strategies and world sizes)
+    def save_checkpoint(self, path, extra=None):
+        from flexmi.runtime.checkpoint import save_checkpoint
+        return save_checkpoint(self, path, extra)
+
+    def load_checkpoint(self, path, strict=True):
+        from flexmi.runtime.checkpoint import load_checkpoint
+        return load_checkpoint(self, path, strict)
+
     def get_layers(self):
         return {i: l for i, l in enumerate(self.layers)}
 

@@ -577,6 +577,9 @@ class Executor:
     def set_lr(self, lr):
         self.lr_tensor.fill_(float(lr))
 
+    def pcs_by_name(self):
+        return {op.name: self.pcs[op.guid] for op in self.model.layers}
+
     def _build_loss(self):
         final = self.final
         # BCE on a sigmoid output: the loss kernel emits dL/dz = p - y (numerically exact), so the
