@@ -55,7 +55,10 @@ def main(argv=None):
         data.next_batch()
     else:
         for t in built.inputs.values():
-            arr = rng.rand(*t.dims).astype(np.float32)
+            if t.data_type in (DataType.DT_INT32, DataType.DT_INT64):
+                arr = rng.randint(0, built.extra.get("int_range", 2), t.dims).astype(np.int32)
+            else:
+                arr = rng.rand(*t.dims).astype(np.float32)
             ex.scatter_from_host(t, arr)
         lab = model.get_label_tensor()
         if lab.data_type == DataType.DT_INT32:

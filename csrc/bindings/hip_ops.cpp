@@ -69,6 +69,12 @@ void fm_bn_bwd(const void* x, const void* y, const void* dy, const float* meanin
                float* dgamma, float* dbeta, void* dx, int N, int C, int HW, int relu, int acc, hipStream_t st);
 void fm_compact_rows(const float* src, float* dst, int K, int n, int ldp, int acc, hipStream_t st);
 void fm_pad_rows(const void* src, void* dst, int K, int n, int ldp, hipStream_t st);
+void fm_lstm_init(const void* h0, const void* c0, void* hprev, long ldhp, float* cinit, int B, int H, hipStream_t s);
+void fm_lstm_cell_fwd(float* G, long ldg, const float* c_prev, long ldcp, float* c_out, long ldc, void* y, long ldy,
+                      void* hprev_next, long ldhp, void* hT, void* cT, int B, int H, hipStream_t s);
+void fm_lstm_cell_bwd(const float* A, long lda, const float* c_t, long ldc, const float* c_prev, long ldcp,
+                      const void* dy, long ldy, const float* dh, float* dc, void* dG, long lddg, int B, int H,
+                      hipStream_t s);
 }
 
 namespace {
@@ -412,6 +418,45 @@ void pad_rows(torch::Tensor src, torch::Tensor dst, int64_t K, int64_t n, int64_
   fm_pad_rows(src.data_ptr(), dst.data_ptr(), K, n, ldp, cur());
 }
 
+// ----------------------------------------------------------------------------- LSTM
+static float* fp(torch::Tensor& t, int64_t off) {
+  TORCH_CHECK(t.scalar_type() == torch::kFloat32 && off >= 0 && off < t.numel(), "lstm: fp32 buffer/offset");
+  return t.data_ptr<float>() + off;
+}
+static void* bp(torch::Tensor& t, int64_t off) {
+  TORCH_CHECK(t.scalar_type() == torch::kBFloat16 && off >= 0 && off < t.numel(), "lstm: bf16 buffer/offset");
+  return (char*)t.data_ptr() + 2 * off;
+}
+void lstm_init(c10::optional<torch::Tensor> h0, c10::optional<torch::Tensor> c0, torch::Tensor hprev, int64_t ldhp,
+               torch::Tensor cinit, int64_t B, int64_t H) {
+  TORCH_CHECK(hprev.numel() >= (B - 1) * ldhp + H && cinit.numel() >= B * H, "lstm_init: sizes");
+  fm_lstm_init(cptr(h0), cptr(c0), bp(hprev, 0), ldhp, fp(cinit, 0), B, H, cur());
+}
+void lstm_cell_fwd(torch::Tensor G, int64_t g_off, int64_t ldg, torch::Tensor cprev, int64_t cp_off, int64_t ldcp,
+                   torch::Tensor cout, int64_t c_off, int64_t ldc, torch::Tensor y, int64_t y_off, int64_t ldy,
+                   torch::Tensor hprev, int64_t hp_off, int64_t ldhp, c10::optional<torch::Tensor> hT,
+                   c10::optional<torch::Tensor> cT, int64_t B, int64_t H) {
+  TORCH_CHECK(g_off + (B - 1) * ldg + 4 * H <= G.numel() && c_off + (B - 1) * ldc + H <= cout.numel() &&
+                  y_off + (B - 1) * ldy + H <= y.numel(), "lstm_cell_fwd: extents");
+  void* hn = hp_off >= 0 ? bp(hprev, hp_off) : nullptr;
+  fm_lstm_cell_fwd(fp(G, g_off), ldg, fp(cprev, cp_off), ldcp, fp(cout, c_off), ldc, bp(y, y_off), ldy, hn, ldhp, mptr(hT),
+                   mptr(cT), B, H, cur());
+}
+void lstm_cell_bwd(torch::Tensor A, int64_t a_off, int64_t lda, torch::Tensor ct, int64_t ct_off, int64_t ldc,
+                   torch::Tensor cprev, int64_t cp_off, int64_t ldcp, c10::optional<torch::Tensor> dy, int64_t dy_off,
+                   int64_t ldy, torch::Tensor dh, torch::Tensor dc, torch::Tensor dG, int64_t dg_off, int64_t lddg,
+                   int64_t B, int64_t H) {
+  TORCH_CHECK(a_off + (B - 1) * lda + 4 * H <= A.numel() && dg_off + (B - 1) * lddg + 4 * H <= dG.numel() &&
+                  dh.numel() >= B * H && dc.numel() >= B * H, "lstm_cell_bwd: extents");
+  const void* dyp = nullptr;
+  if (dy.has_value() && dy->defined()) {
+    TORCH_CHECK(dy_off + (B - 1) * ldy + H <= dy->numel(), "lstm_cell_bwd: dy extent");
+    dyp = (const char*)dy->data_ptr() + 2 * dy_off;
+  }
+  fm_lstm_cell_bwd(fp(A, a_off), lda, fp(ct, ct_off), ldc, fp(cprev, cp_off), ldcp, dyp, ldy, fp(dh, 0), fp(dc, 0),
+                   bp(dG, dg_off), lddg, B, H, cur());
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "flexmi HIP/CDNA4 kernels (gfx950)";
   m.def("gemm", &gemm);
@@ -447,5 +492,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd", &bn_bwd);
   m.def("compact_rows", &compact_rows);
   m.def("pad_rows", &pad_rows);
+  m.def("lstm_init", &lstm_init);
+  m.def("lstm_cell_fwd", &lstm_cell_fwd);
+  m.def("lstm_cell_bwd", &lstm_cell_bwd);
   m.attr("arch") = "gfx950";
 }

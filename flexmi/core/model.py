@@ -156,6 +156,12 @@ class FFModel:
     def dropout(self, input, rate, seed=0, name=None):
         return self._add(Dropout(self, input, rate, seed, name)).outputs[0]
 
+    def lstm(self, input, hidden_size, h0=None, c0=None, name=None):
+        """LSTM over [batch, time, features] (NMT, ``nmt/lstm.cu``); returns (y, h_T, c_T)."""
+        from flexmi.ops.rnn import LSTM
+        op = self._add(LSTM(self, input, hidden_size, h0, c0, name))
+        return op.outputs[0], op.outputs[1], op.outputs[2]
+
     def dot_interaction(self, bottom, embs, self_interaction=False, name=None):
         """DLRM ``dot`` feature interaction (fixes reference caveat C3)."""
         return self._add(DotInteraction(self, bottom, embs, 16, self_interaction, name)).outputs[0]

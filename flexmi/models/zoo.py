@@ -92,6 +92,11 @@ def build(name, model, small=False, **kw):
         ins, out = cu.candle_uno(model, cu.CandleConfig.small() if small else cu.CandleConfig())
         return Built(ins, out, LossType.LOSS_MEAN_SQUARED_ERROR_AVG_REDUCE,
                      [MetricsType.METRICS_MEAN_SQUARED_ERROR], 0.001)
+    if name == "nmt":
+        from . import nmt as N
+        ncfg = N.NMTConfig.small() if small else N.NMTConfig()
+        ins, out = N.nmt(model, ncfg)
+        return Built(ins, out, SCCE, ACC, 0.01, {"int_range": ncfg.vocab})
     if name.startswith("dlrm"):
         from .dlrm import DLRMConfig, build_dlrm
         preset = name.split("-", 1)[1] if "-" in name else ("tiny" if small else "run_random")
@@ -105,4 +110,4 @@ def build(name, model, small=False, **kw):
     raise KeyError(f"unknown model {name!r}")
 
 
-NAMES = ["mlp", "mnist_cnn", "cifar10_cnn", "alexnet", "inception_v3", "resnet50", "candle_uno", "dlrm"]
+NAMES = ["mlp", "mnist_cnn", "cifar10_cnn", "alexnet", "inception_v3", "resnet50", "candle_uno", "dlrm", "nmt"]

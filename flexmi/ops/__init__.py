@@ -7,3 +7,4 @@ from .elementwise import ElementUnary, ElementBinary  # noqa
 from .tensor_ops import Concat, Split, Flat, Reshape, Transpose, Reverse  # noqa
 from .nn_ops import Softmax, Dropout, BatchMatmul, DotInteraction  # noqa
 from .conv import Conv2D, Pool2D, BatchNorm  # noqa
+from .rnn import LSTM  # noqa

@@ -357,20 +357,21 @@ class Executor:
             self.fwd_steps.append(("op", op))
 
         # grads: home-layout grad buffers for float tensors that need them
-        self.grad_needed = set()
-        for op in ops:
+        # backward liveness: an op runs backward only when one of its outputs reaches the loss;
+        # its float inputs then need gradients (graph inputs only when asked, e.g. for the cost
+        # measurement of a single op).  Dead branches (an encoder's unused top output) are skipped.
+        final = ops[-1].outputs[0]
+        self.final = final
+        self.grad_needed = {final.guid}
+        self.bwd_live = set()
+        for op in reversed(ops):
+            if not any(o.guid in self.grad_needed for o in op.outputs):
+                continue
+            self.bwd_live.add(op.guid)
             for i, t in enumerate(op.inputs):
-                # graph inputs get gradients only when asked (cost measurement of a single op)
                 src_ok = t.owner_op is not None or getattr(self.cfg, "input_grads", False)
                 if src_ok and op.needs_input_grad(i) and _is_float(t.data_type):
                     self.grad_needed.add(t.guid)
-        final = ops[-1].outputs[0]
-        self.final = final
-        self.grad_needed.add(final.guid)
-        # outputs of ops whose inputs need grads must have grads too (transitively handled:
-        # every op output that is consumed by a grad-needing op or is final)
-        for g in list(self.grad_needed):
-            pass
         for g in self.grad_needed:
             lay = self.home[g]
             shp = lay.local_shape(self.rank)
@@ -389,6 +390,8 @@ class Executor:
                     self.galias[out.guid] = self.gkey(x.guid)
         self.tmp_grad: Dict[tuple, torch.Tensor] = {}
         for op in reversed(ops):
+            if op.guid not in self.bwd_live:
+                continue
             self.bwd_steps.append(("op", op))
             red = []
             for i, t in enumerate(op.inputs):

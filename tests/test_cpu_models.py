@@ -224,6 +224,12 @@ def _zoo_feed(m, built, seed=0):
                 ex.scatter_from_host(t, a)
             else:
                 ex.scatter_from_host(t, rng.randint(0, dcfg.embedding_size[i - 1], t.dims).astype(np.int64))
+    elif "int_range" in built.extra:     # word ids (NMT): the label is the dst sequence itself
+        for t in built.inputs.values():
+            ex.scatter_from_host(t, rng.randint(0, built.extra["int_range"], t.dims).astype(np.int32))
+        lab = m.get_label_tensor()
+        ex.scatter_from_host(lab, rng.randint(0, built.output.dims[-1], lab.dims).astype(np.int32))
+        return
     else:
         for t in built.inputs.values():
             ex.scatter_from_host(t, rng.rand(*t.dims).astype(np.float32))
@@ -235,7 +241,7 @@ def _zoo_feed(m, built, seed=0):
 
 
 @pytest.mark.parametrize("name", ["mlp", "mnist_cnn", "cifar10_cnn", "alexnet", "inception_v3", "resnet50",
-                                  "candle_uno", "dlrm"])
+                                  "candle_uno", "dlrm", "nmt"])
 def test_zoo_models_train_cpu(name):
     m, built = _zoo_model(name)
     m.init_layers()
@@ -282,3 +288,53 @@ def test_cifar10_cnn_matches_torch():
     lr = m.optimizer.lr
     for p, g, prm in zip(params, grads, m.parameters):
         np.testing.assert_allclose(prm.get_weights(m), (p - lr * g).detach().numpy(), rtol=1e-4, atol=1e-5)
+
+
+# ---------------------------------------------------------------------------- LSTM / NMT
+def _lstm_model(device, B=4, T=5, I=8, H=16, state=False):
+    from flexmi.core import FFConfig, FFModel, SGDOptimizer, LossType, MetricsType
+    cfg = FFConfig()
+    cfg.batchSize, cfg.device = B, device
+    cfg.compute_dtype = "bf16" if device == "gpu" else "fp32"
+    m = FFModel(cfg)
+    x = m.create_tensor([B, T, I], name="x")
+    h0 = c0 = None
+    if state:
+        h0 = m.create_tensor([B, H], name="h0")
+        c0 = m.create_tensor([B, H], name="c0")
+    y, hT, cT = m.lstm(x, H, h0, c0, name="lstm")
+    out = m.reshape(y, [B, T * H], name="flat")
+    m.compile(SGDOptimizer(m, 0.5), LossType.LOSS_MEAN_SQUARED_ERROR_AVG_REDUCE, [MetricsType.METRICS_MEAN_SQUARED_ERROR])
+    return m, x, h0, c0, out
+
+
+def test_lstm_matches_torch_lstm():
+    """flexmi LSTM (CPU executor) vs torch.nn.LSTM: forward output and one SGD step."""
+    B, T, I, H = 4, 5, 8, 16
+    m, x, h0, c0, out = _lstm_model("cpu", B, T, I, H)
+    ex = m.init_layers()
+    ref = torch.nn.LSTM(I, H, batch_first=True)
+    op = m.get_layer_by_name("lstm")
+    with torch.no_grad():
+        op.weights[0].set_weights(m, ref.weight_ih_l0.numpy())
+        op.weights[1].set_weights(m, ref.weight_hh_l0.numpy())
+        op.weights[2].set_weights(m, (ref.bias_ih_l0 + ref.bias_hh_l0).numpy())
+    rng = np.random.RandomState(0)
+    xin = rng.randn(B, T, I).astype(np.float32)
+    lab = rng.randn(B, T * H).astype(np.float32)
+    ex.scatter_from_host(x, xin)
+    ex.scatter_from_host(m.get_label_tensor(), lab)
+    m.forward()
+    yr, _ = ref(torch.from_numpy(xin))
+    np.testing.assert_allclose(ex.gather_to_host(out), yr.reshape(B, -1).detach().numpy(), rtol=1e-5, atol=1e-6)
+    m.backward()
+    m.update()
+    loss = ((yr.reshape(B, -1) - torch.from_numpy(lab)) ** 2).sum(1).mean() / 2 / 1
+    loss = torch.nn.functional.mse_loss(yr.reshape(B, -1), torch.from_numpy(lab), reduction="sum") / (2 * B)
+    gih, ghh, gb = torch.autograd.grad(loss, [ref.weight_ih_l0, ref.weight_hh_l0, ref.bias_ih_l0])
+    np.testing.assert_allclose(op.weights[0].get_weights(m), (ref.weight_ih_l0 - 0.5 * gih).detach().numpy(),
+                               rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(op.weights[1].get_weights(m), (ref.weight_hh_l0 - 0.5 * ghh).detach().numpy(),
+                               rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(op.weights[2].get_weights(m),
+                               (ref.bias_ih_l0 + ref.bias_hh_l0 - 0.5 * gb).detach().numpy(), rtol=1e-4, atol=1e-6)

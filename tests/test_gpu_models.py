@@ -111,7 +111,7 @@ def test_hip_graph_capture_matches_eager(gpu):
 
 
 @pytest.mark.parametrize("name,steps", [("mnist_cnn", 3), ("cifar10_cnn", 3), ("alexnet", 2), ("resnet50", 2),
-                                        ("inception_v3", 1), ("candle_uno", 3)])
+                                        ("inception_v3", 1), ("candle_uno", 3), ("nmt", 3)])
 def test_zoo_gpu_matches_cpu(gpu, name, steps):
     """Every zoo model trains on the HIP kernels (bf16, GEMM convolution, HIP pooling) like the
     fp32 CPU executor: parameters after a few SGD steps agree within bf16 tolerance."""
@@ -140,3 +140,33 @@ def test_resnet_batchnorm_gpu_matches_cpu(gpu):
         res[dev] = [p.get_weights(m) for p in m.parameters]
     for a, b in zip(res["cpu"], res["gpu"]):
         assert np.abs(a - b).max() < 5e-2 * max(1.0, np.abs(a).max()), (a.shape, np.abs(a - b).max())
+
+
+@pytest.mark.parametrize("state", [False, True])
+def test_lstm_gpu_matches_cpu(gpu, state):
+    """HIP LSTM (input-projection GEMM, per-step recurrent GEMM + fused cell kernels) vs the fp32
+    CPU recurrence: outputs, final states and the weights after two SGD steps."""
+    from tests.test_cpu_models import _lstm_model
+    B, T, I, H = 8, 7, 24, 32
+    rng = np.random.RandomState(1)
+    xin = rng.randn(B, T, I).astype(np.float32)
+    hin = 0.5 * rng.randn(B, H).astype(np.float32)
+    cin = 0.5 * rng.randn(B, H).astype(np.float32)
+    lab = 0.3 * rng.randn(B, T * H).astype(np.float32)
+    res = {}
+    for dev in ("cpu", "gpu"):
+        m, x, h0, c0, out = _lstm_model(dev, B, T, I, H, state=state)
+        ex = m.init_layers()
+        ex.scatter_from_host(x, xin)
+        if state:
+            ex.scatter_from_host(h0, hin)
+            ex.scatter_from_host(c0, cin)
+        ex.scatter_from_host(m.get_label_tensor(), lab)
+        m.forward()
+        y = ex.gather_to_host(out)
+        for _ in range(2):
+            ex.train_step()
+        res[dev] = (y, [p.get_weights(m) for p in m.parameters])
+    np.testing.assert_allclose(res["gpu"][0], res["cpu"][0], atol=3e-2)
+    for a, b in zip(res["cpu"][1], res["gpu"][1]):
+        assert np.abs(a - b).max() < 2e-2 * max(1.0, np.abs(a).max()), (a.shape, np.abs(a - b).max())
