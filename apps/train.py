@@ -86,6 +86,12 @@ def main(argv=None):
         print(f"[{a.model}] batch {cfg.batchSize} x {a.iterations} iterations on {comm.world} device(s), "
               f"loss {m.get_loss():.4f} accuracy {m.get_accuracy():.2f}%", file=sys.stderr)
         print(f"ELAPSED TIME = {el:.4f}s, THROUGHPUT = {samples / el:.2f} samples/s", flush=True)
+    if cfg.metrics_log:
+        from flexmi.utils.log import MetricsLogger
+        mlog = MetricsLogger(cfg.metrics_log, cfg)
+        mlog.event("summary", model=a.model, world=comm.world, iterations=a.iterations, elapsed_s=el,
+                   samples_per_s=samples / el, loss=m.get_loss(), accuracy=m.get_accuracy())
+        mlog.close()
     return samples / el
 
 

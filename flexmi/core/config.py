@@ -55,6 +55,10 @@ class FFConfig:
         self.machine_file = ""          # simulator machine model override (JSON)
         self.cost_db = ""               # measured per-op cost database (JSON)
         self.strategy_file = ""         # alias of --import (fixes reference caveat C12)
+        self.watchdog_s = 0.0           # >0: abort a rank whose program makes no progress
+        self.watchdog_mode = "exit"     # exit (EXIT_HANG, launcher tears the job down) | raise
+        self.metrics_log = ""           # per-step JSONL metrics
+        self.log_level = "INFO"
         self.rank, self.world_size = _dist_info()
         self._start = time.perf_counter()
         self.strategies = {}
@@ -126,6 +130,12 @@ class FFConfig:
                 self.cost_db = nxt()
             elif a == "--seed":
                 self.seed = int(nxt())
+            elif a == "--watchdog":
+                self.watchdog_s = float(nxt())
+            elif a == "--metrics-log":
+                self.metrics_log = nxt()
+            elif a == "--log-level":
+                self.log_level = nxt()
             i += 1
         self._finalize()
         return self

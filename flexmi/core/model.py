@@ -249,10 +249,13 @@ class FFModel:
 
     def train(self, dataloaders, epochs=1, batch_size=None):
         """``flexflow_cbinding.py:789-807``."""
+        from flexmi.utils.log import MetricsLogger
         num_samples = dataloaders[0].get_num_samples()
         bs = self.config.get_batch_size()
         ex = self._ex()
         ex.training = True
+        mlog = MetricsLogger(getattr(self.config, "metrics_log", ""), self.config)
+        step = 0
         for epoch in range(epochs):
             for d in dataloaders:
                 d.reset()
@@ -264,6 +267,12 @@ class FFModel:
                 self.zero_gradients()
                 self.backward()
                 self.update()
+                step += 1
+                if mlog.enabled:
+                    mlog.step(step, bs, self.get_perf_metrics(), ex, epoch=epoch)
+            if self.config.rank == 0 and self.config.printFreq:
+                print(self.get_perf_metrics(), file=sys.stderr)
+        mlog.close()
 
     def eval(self, dataloaders):
         num_samples = dataloaders[0].get_num_samples()

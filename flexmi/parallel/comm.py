@@ -76,6 +76,16 @@ class Comm:
             w.wait()
         return t
 
+    def all_reduce_op(self, t: torch.Tensor, ranks=None, op="sum"):
+        """Blocking all-reduce with an explicit reduction (sum | max | min)."""
+        if self.world == 1:
+            return t
+        g = self.group_for(ranks) if ranks is not None else None
+        red = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+        dist.all_reduce(t, op=red, group=g)
+        self.calls += 1
+        return t
+
     def broadcast(self, t: torch.Tensor, src: int):
         if self.world > 1:
             dist.broadcast(t, src)
@@ -98,6 +108,8 @@ def init_distributed(backend=None, timeout_s=600):
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if backend == "nccl":
+        # RCCL errors / peer loss abort the communicator instead of hanging
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         local = int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(local)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

@@ -152,10 +152,11 @@ def run_reshards(comm, items):
 
 
 class Item:
-    __slots__ = ("kind", "fn", "name")
+    __slots__ = ("kind", "fn", "name", "check")
 
-    def __init__(self, kind, fn, name):
+    def __init__(self, kind, fn, name, check=None):
         self.kind, self.fn, self.name = kind, fn, name
+        self.check = check      # debug mode: callable(item) run after fn (NaN/Inf guard)
 
     def __repr__(self):
         return f"{self.kind}:{self.name}"
@@ -266,6 +267,11 @@ class Executor:
         self.label = label_tensor
         self.strategies = strategies
         self.timer = OpTimer(self.cfg.profiling, self.backend == "hip")
+        self.debug = bool(getattr(self.cfg, "debug", False))
+        self.watchdog = None
+        if getattr(self.cfg, "watchdog_s", 0) > 0:
+            from flexmi.runtime.health import Watchdog
+            self.watchdog = Watchdog(self.cfg.watchdog_s, getattr(self.cfg, "watchdog_mode", "exit"))
         self.training = True
         self.step_count = 0
         self._graph = None
@@ -675,6 +681,7 @@ class Executor:
                       (lambda grp=grp: type(grp[0]).forward_group(grp, [self.ctx[o.guid] for o in grp])))
                 continue
             C(fwd, op.name + ".fwd", (lambda op=op, c=c: self._fwd_op(op, c)))
+            fwd[-1].check = (lambda op=op, c=c: self._check_op(op.name + ".fwd", c.outputs, "output"))
 
         # ---------------- backward (accumulate flags resolved at compile time)
         written = set()
@@ -708,6 +715,7 @@ class Executor:
                               (lambda grp=grp: type(grp[0]).backward_group(grp, [self.ctx[o.guid] for o in grp])))
                     else:
                         C(bwd, op.name + ".bwd", (lambda op=op, c=c, flags=flags: self._bwd_op(op, c, flags)))
+                        bwd[-1].check = (lambda op=op, c=c: self._check_op(op.name + ".bwd", c.in_grads, "input grad"))
                     for i, t in enumerate(op.inputs):
                         if c.in_grads[i] is not None and self.need[(op.guid, i)].same_as(self.home[t.guid]):
                             written.add(self.gkey(t.guid))
@@ -773,6 +781,8 @@ class Executor:
                                 "loss.scatter")
 
     def _run(self, prog):
+        if self.debug or self.watchdog is not None:
+            return self._run_guarded(prog)
         tm = self.timer
         if tm.enabled:
             for it in prog:
@@ -781,6 +791,37 @@ class Executor:
         else:
             for it in prog:
                 it.fn()
+
+    def _run_guarded(self, prog):
+        """Debug / watchdog execution: heartbeat per item; in debug mode every item is followed
+        by a device synchronisation and its NaN/Inf guard."""
+        from flexmi.runtime.health import WatchdogTimeout
+        wd = self.watchdog
+        if wd is not None:
+            wd.arm()
+        try:
+            for it in prog:
+                if wd is not None:
+                    wd.beat(it.name)
+                with self.timer.scope(it.name):
+                    it.fn()
+                if self.debug:
+                    if self.backend == "hip":
+                        torch.cuda.synchronize()
+                    if it.check is not None:
+                        it.check()
+        except KeyboardInterrupt:
+            if wd is not None and wd.fired:
+                raise WatchdogTimeout(f"rank {self.rank}: no progress in '{wd.fired_tag}' for "
+                                      f"{wd.timeout_s:.1f}s") from None
+            raise
+        finally:
+            if wd is not None:
+                wd.disarm()
+
+    def _check_op(self, where, tensors, kind):
+        from flexmi.runtime.health import check_finite
+        check_finite(where, tensors, kind)
 
     def forward(self):
         self._run(self.prog_fwd)
@@ -799,6 +840,12 @@ class Executor:
         if self.optimizer is not None:
             self.optimizer.next()   # host mirror of the device-side step counters
         self.step_count += 1
+        if self.debug:
+            from flexmi.runtime.health import check_finite, check_replicas
+            for g in self.groups:
+                if g.numel:
+                    check_finite(f"update step {self.step_count}", [g.master], "weights")
+            check_replicas(self)
 
     def _launch_bucket(self, g, bi):
         b = g.buckets[bi]
