@@ -2,6 +2,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "loader.h"
 #include "strategy_pb.h"
 
 namespace py = pybind11;
@@ -56,4 +57,23 @@ PYBIND11_MODULE(_native, m) {
     return to_tuples(ops);
   });
   register_sim(m);
+
+  // data-loader ring (csrc/runtime/loader.h); pointers are raw addresses of host buffers
+  py::class_<flexmi::BatchRing>(m, "BatchRing")
+      .def(py::init<int64_t, int64_t, int, int, bool, uint64_t>(), py::arg("batch"), py::arg("num_samples"),
+           py::arg("depth") = 3, py::arg("threads") = 2, py::arg("shuffle") = false, py::arg("seed") = 0)
+      .def("add_source",
+           [](flexmi::BatchRing& r, uintptr_t base, int64_t rows, int64_t row_bytes, int64_t col_off,
+              int64_t col_bytes, int64_t row_lo, int64_t row_hi) {
+             return r.add_source((const void*)base, rows, row_bytes, col_off, col_bytes, row_lo, row_hi);
+           })
+      .def("set_slot", [](flexmi::BatchRing& r, int src, int slot, uintptr_t p) { r.set_slot(src, slot, (void*)p); })
+      .def("start", &flexmi::BatchRing::start)
+      .def("stop", &flexmi::BatchRing::stop, py::call_guard<py::gil_scoped_release>())
+      .def("acquire", &flexmi::BatchRing::acquire, py::call_guard<py::gil_scoped_release>())
+      .def("release", &flexmi::BatchRing::release)
+      .def("batch_ids", &flexmi::BatchRing::batch_ids)
+      .def_property_readonly("batches_per_epoch", &flexmi::BatchRing::batches_per_epoch)
+      .def_property_readonly("consumed", &flexmi::BatchRing::consumed)
+      .def_property_readonly("depth", &flexmi::BatchRing::depth);
 }

@@ -6,5 +6,5 @@ from .initializers import (Initializer, GlorotUniformInitializer, ZeroInitialize
                            NormInitializer, NormalInitializer, ConstantInitializer)
 from .optimizers import SGDOptimizer, AdamOptimizer, Optimizer  # noqa
 from .loss_metrics import PerfMetrics  # noqa
-from .dataloader import SingleDataLoader, DataLoader2D, DataLoader4D, NetConfig  # noqa
+from .dataloader import SingleDataLoader, DataLoader2D, DataLoader4D, NetConfig, PrefetchLoader  # noqa
 from .model import FFModel  # noqa

@@ -85,3 +85,108 @@ DataLoader4D = DataLoader2D
 class NetConfig:
     def __init__(self):
         self.dataset_path = ""
+
+
+class PrefetchLoader:
+    """Multi-input prefetching loader on the native ring (``csrc/runtime/loader.{h,cc}``).
+
+    ``pairs``: [(tensor, full host array [num_samples, ...])] -- inputs and the label.  Host
+    worker threads gather each batch's rows (sequential or shuffled per epoch with ``seed``)
+    into ``depth`` pinned staging slots ahead of the training loop; :meth:`next_batch` takes
+    the next staged slot and issues one async H2D copy per input on the current stream, so
+    the gather overlaps the previous step's compute.  Each rank stages only its shard box of
+    every tensor (``python/flexflow_dataloader.cu:97-150`` gathered per shard on the GPU;
+    ``dlrm.cu:19-122``)."""
+
+    def __init__(self, ffmodel, pairs, num_samples, shuffle=False, seed=0, depth=3, threads=2):
+        from flexmi import _native
+        ex = ffmodel._ex()
+        self.ex = ex
+        self.gpu = ex.backend == "hip"
+        B = pairs[0][0].dims[0]
+        self.batch = B
+        self.ring = _native.BatchRing(B, int(num_samples), depth, threads, bool(shuffle), int(seed))
+        self.items = []
+        self._keep = []
+        for t, full in pairs:
+            buf = ex.local_buffer(t)
+            if buf is None:
+                continue
+            assert t.dims[0] == B, "all inputs of a PrefetchLoader share the batch dimension"
+            box = ex.home[t.guid].local_box(ex.rank)
+            src = torch.as_tensor(np.ascontiguousarray(full)).reshape((-1,) + tuple(t.dims[1:]))
+            if src.dtype != buf.dtype:
+                src = src.to(buf.dtype)
+            src = src.contiguous()
+            self._keep.append(src)
+            dims = list(t.dims)
+            es = src.element_size()
+            row_bytes = int(np.prod(dims[1:], dtype=np.int64)) * es
+            split = [j for j in range(1, len(dims)) if box[j] != (0, dims[j])]
+            if not split:
+                col_off, col_bytes = 0, row_bytes
+            else:
+                d = split[0]
+                if any(box[j][1] - box[j][0] != dims[j] for j in range(d + 1, len(dims))) or \
+                        any(dims[j] != 1 for j in range(1, d)):
+                    raise NotImplementedError(f"PrefetchLoader: shard box {box} of {t.name} is not a row slice")
+                inner = int(np.prod(dims[d + 1:], dtype=np.int64)) * es
+                col_off, col_bytes = box[d][0] * inner, (box[d][1] - box[d][0]) * inner
+            si = self.ring.add_source(src.data_ptr(), src.shape[0], row_bytes, col_off, col_bytes, box[0][0], box[0][1])
+            stg = []
+            for s in range(depth):
+                st = torch.empty(tuple(buf.shape), dtype=buf.dtype, pin_memory=self.gpu)
+                self.ring.set_slot(si, s, st.data_ptr())
+                stg.append(st)
+            self.items.append((buf, stg))
+        self.pending = []
+        self.depth = depth
+        self.num_samples = int(num_samples)
+        self.ring.start()
+
+    def get_num_samples(self):
+        return self.num_samples
+
+    def _release_done(self, block=False):
+        while self.pending:
+            slot, ev = self.pending[0]
+            if ev is not None and not ev.query():
+                if not block:
+                    break
+                ev.synchronize()
+            self.ring.release(slot)
+            self.pending.pop(0)
+            block = False
+
+    def next_batch(self, ffmodel=None):
+        self._release_done()
+        if len(self.pending) >= self.depth - 1:
+            self._release_done(block=True)
+        slot = self.ring.acquire()
+        for buf, stg in self.items:
+            buf.copy_(stg[slot], non_blocking=self.gpu)
+        ev = None
+        if self.gpu:
+            ev = torch.cuda.Event()
+            ev.record()
+        self.pending.append((slot, ev))
+        if not self.gpu:
+            self._release_done()
+
+    def reset(self):
+        for _, ev in self.pending:
+            if ev is not None:
+                ev.synchronize()
+        self.pending = []
+        self.ring.stop()
+        self.ring.start()
+
+    def close(self):
+        self.reset()
+        self.ring.stop()
+
+    def __del__(self):
+        try:
+            self.ring.stop()
+        except Exception:
+            pass
