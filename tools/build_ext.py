@@ -3,6 +3,7 @@
 
   flexmi/_C*.so       HIP kernels (csrc/kernels/*.hip, hipcc --offload-arch=gfx950, no torch
                       headers) + torch/pybind11 bindings (csrc/bindings/hip_ops.cpp)
+  flexmi/libflexmi_c.so  C API (csrc/capi/flexmi_c.h; embeds CPython)
   flexmi/_native*.so  C++ runtime: strategy .pb codec, sharding algebra, MI355X execution
                       simulator + MCMC search, data-loader ring (csrc/runtime/*.cc, g++ -O3,
                       pybind11; no GPU dependency -- usable on the CPU box)
@@ -101,6 +102,17 @@ def write_ninja(only=None):
         lines.append(f"build {out}: cxxlink {' '.join(objs)}")
         lines.append("  ldflags = -pthread")
         targets.append(out)
+        # C API (csrc/capi): embeds CPython, so it links libpython
+        capi_src = os.path.join(ROOT, "csrc", "capi", "flexmi_c.cc")
+        capi_o = os.path.join(BUILD, "capi_flexmi_c.o")
+        pyver = sysconfig.get_config_var("LDVERSION") or sysconfig.get_python_version()
+        pylib = sysconfig.get_config_var("LIBDIR")
+        lines.append(f"build {capi_o}: cxx {capi_src}")
+        lines.append(f"  extra = -I{ROOT}/csrc/capi")
+        capi = os.path.join(ROOT, "flexmi", "libflexmi_c.so")
+        lines.append(f"build {capi}: cxxlink {capi_o}")
+        lines.append(f"  ldflags = -L{pylib} -lpython{pyver} -ldl -pthread")
+        targets.append(capi)
     lines.append("default " + " ".join(targets))
     path = os.path.join(BUILD, "build.ninja")
     with open(path, "w") as f:
