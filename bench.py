@@ -83,9 +83,11 @@ def main():
     loss = LossType.LOSS_BINARY_CROSSENTROPY if dcfg.loss == "bce" else LossType.LOSS_MEAN_SQUARED_ERROR_AVG_REDUCE
     model.compile(SGDOptimizer(model, 0.01), loss, [MetricsType.METRICS_ACCURACY, MetricsType.METRICS_MEAN_SQUARED_ERROR])
     model.strategies = strategies
+    cuda = torch.cuda.is_available()
+    sync = torch.cuda.synchronize if cuda else (lambda: None)   # CPU (gloo) rehearsal runs too
     t0 = time.time()
     ex = model.init_layers()
-    torch.cuda.synchronize()
+    sync()
     t_init = time.time() - t0
     data = SyntheticDLRMData(model, dense_in, sparse, dcfg, num_batches=4, seed=rank)
 
@@ -126,20 +128,20 @@ def main():
 
     for _ in range(a.warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     el = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([el], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([el], dtype=torch.float64, device="cuda" if cuda else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     ms = el * 1e3 / a.steps
@@ -158,7 +160,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" if cuda else "fp32",
             "data": "synthetic",
             "config": {
                 "model": f"DLRM {dcfg.name} ({'MLPerf-like: 13 dense + 26 sparse, Criteo-TB tables (187.8M rows x 128, fp32), dot interaction' if dcfg.name == 'mlperf' else dcfg.name})",

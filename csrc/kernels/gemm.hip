@@ -244,8 +244,13 @@ void launch_bm(const GemmP& p, bool ak, bool bk, bool vec, hipStream_t s) {
 
 }  // namespace
 
-extern "C" void fm_gemm_glds_launch(const void* params, int bm, int bn, int a_kcontig, int b_kcontig,
+extern "C" void fm_gemm_glds_launch(const void* params, int bm, int bn, int a_kcontig, int b_kcontig, int prio,
                                     hipStream_t stream);
+
+// dispatch experiments (tools/gemm_probe.py): 1 = never glds, 2 = glds for every orientation and
+// grid size (K % 64 == 0), 4 = glds 128x128 tiles, 8 = s_setprio around the glds MFMA blocks
+static int g_gemm_variant = 0;
+extern "C" void fm_gemm_set_variant(int v) { g_gemm_variant = v; }
 
 // A_kcontig: A stored [M][K] (lda >= K) else [K][M] (lda >= M)
 // B_kcontig: B stored [N][K] (ldb >= K) else [K][N] (ldb >= N)
@@ -270,13 +275,16 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
   bool vec = al(A) && al(B) && (lda % 8 == 0) && (ldb % 8 == 0) && (sA % 8 == 0) && (sB % 8 == 0);
   vec = vec && (a_kcontig ? (K % 8 == 0) : (M % 8 == 0)) && (b_kcontig ? (K % 8 == 0) : (N % 8 == 0));
   // LDS-DMA pipelined kernel (gemm_glds.hip) whenever K-tiles are whole
-  static const bool no_glds = getenv("FM_GEMM_NO_GLDS") != nullptr;
+  static const bool no_glds_env = getenv("FM_GEMM_NO_GLDS") != nullptr;
+  const bool no_glds = no_glds_env || (g_gemm_variant & 1);
+  const bool glds_any = (g_gemm_variant & 2) != 0;
   // (measured, tools/bench_gemm.py in hipGraph mode: the pipelined kernel wins for K-contiguous
   // operands once 256x128 tiles fill the chip; MN-contiguous (transposed-read) operands and small
   // grids stay on the register-staged kernel's 128x64/128x128 tiles)
   const long t256 = (long)((M + 255) / 256) * ((N + 127) / 128) * batch;
-  if (vec && !no_glds && K > 0 && K % BK == 0 && M >= 8 && N >= 8 && a_kcontig && b_kcontig && t256 >= 256) {
-    const int bm = 256;
+  if (vec && !no_glds && K > 0 && K % BK == 0 && M >= 8 && N >= 8 &&
+      ((a_kcontig && b_kcontig && t256 >= 256) || glds_any)) {
+    const int bm = ((g_gemm_variant & 4) || t256 < 256) ? 128 : 256;
     p.tiles_m = (M + bm - 1) / bm;
     p.tiles_n = (N + 127) / 128;
     const long tiles = (long)p.tiles_m * p.tiles_n * batch;
@@ -289,7 +297,7 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
     if (act_y != nullptr || colsum != nullptr) ks = 1;
     if (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks = 1;
     p.ksplit = ks;
-    fm_gemm_glds_launch(&p, bm, 128, a_kcontig, b_kcontig, stream);
+    fm_gemm_glds_launch(&p, bm, 128, a_kcontig, b_kcontig, (g_gemm_variant & 8) ? 1 : 0, stream);
     if (p.ksplit > 1) {
       long total = (long)M * N * batch;
       hipLaunchKernelGGL(fm_gemm_splitk_reduce, dim3(fm_grid(total)), dim3(256), 0, stream, p);
@@ -300,6 +308,13 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
   int BMv = 128, BNv = 128;
   long t128 = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;
   if (t128 < 512 && N <= 64 * 8) BNv = 64;
+  {   // small grids with short K (measured, tools/gemm_probe.py): 64x64 tiles keep >= 2 blocks
+      // resident per CU where 128x64 gives at most one wave of blocks; long-K GEMMs (dW, K =
+      // batch) keep the bigger tile and split K instead
+    long t12864 = (long)((M + 127) / 128) * ((N + 63) / 64) * batch;
+    if (BNv == 64 && t12864 <= 256 && K <= 1024 && !(g_gemm_variant & 16)) BMv = 64;
+  }
+  if (g_gemm_variant & 32) { BMv = 64; BNv = 64; }
   p.tiles_m = (M + BMv - 1) / BMv;
   p.tiles_n = (N + BNv - 1) / BNv;
   long tiles = (long)p.tiles_m * p.tiles_n * batch;
@@ -319,7 +334,8 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
     p.ksplit = 1;
   }
   if (BNv == 128) launch_bm<128, 128>(p, a_kcontig, b_kcontig, vec, stream);
-  else launch_bm<128, 64>(p, a_kcontig, b_kcontig, vec, stream);
+  else if (BMv == 128) launch_bm<128, 64>(p, a_kcontig, b_kcontig, vec, stream);
+  else launch_bm<64, 64>(p, a_kcontig, b_kcontig, vec, stream);
   if (p.ksplit > 1) {
     long total = (long)M * N * batch;
     hipLaunchKernelGGL(fm_gemm_splitk_reduce, dim3(fm_grid(total)), dim3(256), 0, stream, p);

@@ -67,7 +67,7 @@ FM_DEVICE void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
-template <int BM, int BN, bool AK, bool BKC>
+template <int BM, int BN, bool AK, bool BKC, bool PRIO>
 __global__ void __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) fm_gemm_glds_kernel(GemmP p) {
   constexpr int WN = BN / 64;
   constexpr int NW = (BM / 64) * WN;
@@ -145,6 +145,7 @@ __global__ void __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) fm_gemm_glds_ke
       for (int i = 0; i < MR; ++i) af[i] = frag<AK, BM>(la, wm * 64 + 16 * i, kk, lane);
 #pragma unroll
       for (int j = 0; j < NR; ++j) bfr[j] = frag<BKC, BN>(lb, wn * 64 + 16 * j, kk, lane);
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);   // MFMA issue ahead of the other waves' loads
 #pragma unroll
       for (int i = 0; i < MR; ++i)
 #pragma unroll
@@ -152,6 +153,7 @@ __global__ void __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) fm_gemm_glds_ke
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8v_t*>(&bfr[j]),
                                                               *reinterpret_cast<bf16x8v_t*>(&af[i]),
                                                               acc[i][j], 0, 0, 0);
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     }
   }
   // drain the (dummy) prefetches before the LDS is reused or the block exits
@@ -175,15 +177,24 @@ __global__ void __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) fm_gemm_glds_ke
   gemm_epilogue<MR, NR>(p, acc, zb, split, m0 + wm * 64, n0 + wn * 64, lane);
 }
 
-template <int BM, int BN>
+template <int BM, int BN, bool PRIO>
 void launch_glds(const GemmP& p, bool ak, bool bk, hipStream_t s) {
   constexpr int NTH = (BM / 64) * (BN / 64) * 64;
   constexpr int LDS = 3 * (BM + BN) * BK * 2;
+  static bool attr_set = false;
+  if (!attr_set) {   // >64 KiB dynamic LDS needs the opt-in attribute
+    auto set = [](const void* f) { (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS); };
+    set((const void*)fm_gemm_glds_kernel<BM, BN, true, true, PRIO>);
+    set((const void*)fm_gemm_glds_kernel<BM, BN, true, false, PRIO>);
+    set((const void*)fm_gemm_glds_kernel<BM, BN, false, true, PRIO>);
+    set((const void*)fm_gemm_glds_kernel<BM, BN, false, false, PRIO>);
+    attr_set = true;
+  }
   dim3 grid(p.tiles_m * p.tiles_n, p.batch, p.ksplit);
-  if (ak && bk) hipLaunchKernelGGL((fm_gemm_glds_kernel<BM, BN, true, true>), grid, dim3(NTH), LDS, s, p);
-  else if (ak && !bk) hipLaunchKernelGGL((fm_gemm_glds_kernel<BM, BN, true, false>), grid, dim3(NTH), LDS, s, p);
-  else if (!ak && bk) hipLaunchKernelGGL((fm_gemm_glds_kernel<BM, BN, false, true>), grid, dim3(NTH), LDS, s, p);
-  else hipLaunchKernelGGL((fm_gemm_glds_kernel<BM, BN, false, false>), grid, dim3(NTH), LDS, s, p);
+  if (ak && bk) hipLaunchKernelGGL((fm_gemm_glds_kernel<BM, BN, true, true, PRIO>), grid, dim3(NTH), LDS, s, p);
+  else if (ak && !bk) hipLaunchKernelGGL((fm_gemm_glds_kernel<BM, BN, true, false, PRIO>), grid, dim3(NTH), LDS, s, p);
+  else if (!ak && bk) hipLaunchKernelGGL((fm_gemm_glds_kernel<BM, BN, false, true, PRIO>), grid, dim3(NTH), LDS, s, p);
+  else hipLaunchKernelGGL((fm_gemm_glds_kernel<BM, BN, false, false, PRIO>), grid, dim3(NTH), LDS, s, p);
 }
 
 }  // namespace
@@ -191,22 +202,14 @@ void launch_glds(const GemmP& p, bool ak, bool bk, hipStream_t s) {
 // Launch the pipelined kernel for a prepared parameter block (tiles_m/n and ksplit filled in
 // for the chosen tile).  Caller guarantees: K % 64 == 0 (per split: whole tiles), 16-B aligned
 // operands with leading dims % 8 == 0, and M % 8 == 0 / N % 8 == 0 for MN-contiguous operands.
-extern "C" void fm_gemm_glds_launch(const void* params, int bm, int bn, int a_kcontig, int b_kcontig,
+extern "C" void fm_gemm_glds_launch(const void* params, int bm, int bn, int a_kcontig, int b_kcontig, int prio,
                                     hipStream_t stream) {
-  static bool attr_set = false;
-  if (!attr_set) {   // >64 KiB dynamic LDS needs the opt-in attribute
-    auto set = [](const void* f, int bytes) { (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes); };
-    set((const void*)fm_gemm_glds_kernel<256, 128, true, true>, 3 * 384 * BK * 2);
-    set((const void*)fm_gemm_glds_kernel<256, 128, true, false>, 3 * 384 * BK * 2);
-    set((const void*)fm_gemm_glds_kernel<256, 128, false, true>, 3 * 384 * BK * 2);
-    set((const void*)fm_gemm_glds_kernel<256, 128, false, false>, 3 * 384 * BK * 2);
-    set((const void*)fm_gemm_glds_kernel<128, 128, true, true>, 3 * 256 * BK * 2);
-    set((const void*)fm_gemm_glds_kernel<128, 128, true, false>, 3 * 256 * BK * 2);
-    set((const void*)fm_gemm_glds_kernel<128, 128, false, true>, 3 * 256 * BK * 2);
-    set((const void*)fm_gemm_glds_kernel<128, 128, false, false>, 3 * 256 * BK * 2);
-    attr_set = true;
-  }
   const GemmP& p = *reinterpret_cast<const GemmP*>(params);
-  if (bm == 256) launch_glds<256, 128>(p, a_kcontig, b_kcontig, stream);
-  else launch_glds<128, 128>(p, a_kcontig, b_kcontig, stream);
+  if (bm == 256) {
+    if (prio) launch_glds<256, 128, true>(p, a_kcontig, b_kcontig, stream);
+    else launch_glds<256, 128, false>(p, a_kcontig, b_kcontig, stream);
+  } else {
+    if (prio) launch_glds<128, 128, true>(p, a_kcontig, b_kcontig, stream);
+    else launch_glds<128, 128, false>(p, a_kcontig, b_kcontig, stream);
+  }
 }

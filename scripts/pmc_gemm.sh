@@ -1,6 +1,14 @@
+#!/bin/bash
+# PMC counters for one flexmi GEMM shape (tools/gemm_one.py) on the gpurun box:
+#   scripts/pmc_gemm.sh M K N orient tag
+# one rocprofv3 run per counter group (counters only with --kernel-trace-free --pmc runs)
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY" "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS" "SQ_WAIT_ANY SQ_INST_LEVEL_VMEM SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_RD"; do
-  n=$(echo $grp | tr ' ' '_' | cut -c1-20)
-  timeout -k 10 120 rocprofv3 --pmc $grp -d $R/gpurun_out/pmc_$n -o run --output-format csv -- python $R/tools/gemm_one.py 8192 1024 1024 fwd 20 || exit 1
+M=$1; K=$2; N=$3; O=$4; TAG=$5
+i=0
+for grp in "GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_INSTS_MFMA" \
+           "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_REQ_sum" \
+           "SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_WAIT_ANY"; do
+  i=$((i+1))
+  timeout -k 10 120 rocprofv3 --pmc $grp -d $R/gpurun_out/pmc_${TAG}_$i -o run --output-format csv -- python3 $R/tools/gemm_one.py $M $K $N $O 20 || exit 1
 done

@@ -170,3 +170,34 @@ def test_lstm_gpu_matches_cpu(gpu, state):
     np.testing.assert_allclose(res["gpu"][0], res["cpu"][0], atol=3e-2)
     for a, b in zip(res["cpu"][1], res["gpu"][1]):
         assert np.abs(a - b).max() < 2e-2 * max(1.0, np.abs(a).max()), (a.shape, np.abs(a - b).max())
+
+
+def test_prefetch_loader_gpu_matches_single_loader(gpu):
+    """Native prefetch ring with pinned staging + async H2D copies trains exactly like the
+    synchronous SingleDataLoader on the GPU."""
+    from flexmi.core import (ActiMode, FFConfig, FFModel, LossType, MetricsType, PrefetchLoader, SGDOptimizer,
+                             SingleDataLoader)
+    rng = np.random.RandomState(0)
+    n, B = 256, 32
+    xs = rng.rand(n, 64).astype(np.float32)
+    ys = rng.randint(0, 8, (n, 1)).astype(np.int32)
+    res = []
+    for kind in ("single", "prefetch"):
+        cfg = FFConfig()
+        cfg.batchSize = B
+        m = FFModel(cfg)
+        x = m.create_tensor([B, 64], name="x")
+        o = m.softmax(m.dense(m.dense(x, 64, ActiMode.AC_MODE_RELU, name="a"), 8, name="b"))
+        m.compile(SGDOptimizer(m, 0.05), LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, [MetricsType.METRICS_ACCURACY])
+        m.init_layers()
+        if kind == "single":
+            dls = [SingleDataLoader(m, x, xs, n), SingleDataLoader(m, m.get_label_tensor(), ys, n)]
+        else:
+            dls = [PrefetchLoader(m, [(x, xs), (m.get_label_tensor(), ys)], n, depth=3, threads=2)]
+        m.train(dls, epochs=2)
+        torch.cuda.synchronize()
+        res.append([p.get_weights(m) for p in m.parameters])
+        if kind == "prefetch":
+            dls[0].close()
+    for a, b in zip(*res):
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)

@@ -1,0 +1,24 @@
+#!/usr/bin/env python3
+"""Per-dispatch timeline of the last full training step in a rocprofv3 rocpd database
+(kernels between the last two dispatches of the step's first kernel).
+usage: prof_step.py run_results.db [first_kernel_substring]"""
+import sqlite3
+import sys
+
+
+def main(path, first="fm_emb_fwd_multi"):
+    c = sqlite3.connect(path)
+    rows = list(c.execute("select name, duration, grid_x, grid_y, grid_z, workgroup_x, lds_size, vgpr_count, start "
+                          "from kernels order by start"))
+    idx = [i for i, r in enumerate(rows) if first in r[0]]
+    s, e = idx[-2], idx[-1]
+    tot = 0
+    for r in rows[s:e]:
+        n = r[0].replace("(anonymous namespace)::", "")[:80]
+        tot += r[1]
+        print(f"{r[1] / 1e3:7.2f}us grid={r[2] // max(1, r[5])}x{r[3]}x{r[4]} wg={r[5]} lds={r[6]} vgpr={r[7]}  {n}")
+    print(f"step kernel sum {tot / 1e3:.1f}us, span {(rows[e][8] - rows[s][8]) / 1e3:.1f}us")
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
