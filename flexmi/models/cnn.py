@@ -163,3 +163,44 @@ def resnet50(model, batch=None, image=229, num_classes=10, batch_norm=False, blo
     t = m.dense(t, num_classes)
     t = m.softmax(t)
     return x, t
+
+
+# ------------------------------------------------------------------ DenseNet-121
+# The reference's standalone SOAP simulator builds DenseNet-121 (scripts/simulator.cc model
+# builders): dense blocks of (BN-ReLU-Conv1x1(4k)-BN-ReLU-Conv3x3(k)) whose outputs are
+# concatenated onto the block input, transitions BN-Conv1x1(theta=0.5)-AvgPool2, growth k = 32.
+def _dense_layer(m, x, growth):
+    t = m.batch_norm(x)
+    t = m.conv2d(t, 4 * growth, 1, 1, 1, 1, 0, 0, NONE, use_bias=False)
+    t = m.batch_norm(t)
+    t = m.conv2d(t, growth, 3, 3, 1, 1, 1, 1, NONE, use_bias=False)
+    return m.concat([x, t], 1)
+
+
+def densenet121(model, batch=None, image=224, num_classes=10, growth=32, blocks=(6, 12, 24, 16)):
+    b = batch or model.config.batchSize
+    x = model.create_tensor([b, 3, image, image], name="input")
+    m = model
+    t = m.conv2d(x, 2 * growth, 7, 7, 2, 2, 3, 3, NONE, use_bias=False)
+    t = m.batch_norm(t)
+    t = m.pool2d(t, 3, 3, 2, 2, 1, 1)
+    for bi, n in enumerate(blocks):
+        for _ in range(n):
+            t = _dense_layer(m, t, growth)
+        if bi != len(blocks) - 1:
+            c = t.dims[1] // 2
+            t = m.batch_norm(t)
+            t = m.conv2d(t, c, 1, 1, 1, 1, 0, 0, NONE, use_bias=False)
+            t = m.pool2d(t, 2, 2, 2, 2, 0, 0, PoolType.POOL_AVG)
+    t = m.batch_norm(t)
+    k = t.dims[2]
+    t = m.pool2d(t, k, k, 1, 1, 0, 0, PoolType.POOL_AVG)
+    t = m.flat(t)
+    t = m.dense(t, num_classes)
+    t = m.softmax(t)
+    return x, t
+
+
+def resnet101(model, batch=None, image=224, num_classes=10, batch_norm=True):
+    """ResNet-101 (bottlenecks 3-4-23-3), the standalone simulator's ResNet builder."""
+    return resnet50(model, batch, image, num_classes, batch_norm, blocks=(3, 4, 23, 3))

@@ -4,7 +4,8 @@
 input tensors, the output, and the loss / metrics / learning rate the reference example uses.
 Names: ``mlp`` / ``mnist_mlp`` (examples/python/native/mnist_mlp.py), ``mnist_cnn``,
 ``cifar10_cnn`` (examples/python/native/{mnist,cifar10}_cnn.py), ``alexnet``, ``inception_v3``,
-``resnet50`` (examples/cpp/*), ``candle_uno`` (examples/cpp/candle_uno), ``dlrm-<preset>``
+``resnet50`` (examples/cpp/*), ``resnet101`` / ``densenet121`` (the standalone simulator's
+builders, scripts/simulator.cc), ``nmt`` (nmt/), ``candle_uno`` (examples/cpp/candle_uno), ``dlrm-<preset>``
 (examples/cpp/DLRM; presets in flexmi.models.dlrm).  ``small=True`` gives a reduced-size
 instance of the same architecture for tests.
 """
@@ -88,6 +89,14 @@ def build(name, model, small=False, **kw):
         x, t = cnn.resnet50(model, image=kw.get("image", 64 if small else 229), batch_norm=kw.get("batch_norm", False),
                             blocks=(1, 1, 1, 1) if small else (3, 4, 6, 3))
         return Built({"input": x}, t, SCCE, ACC, 0.001)
+    if name == "densenet121":
+        x, t = cnn.densenet121(model, image=kw.get("image", 32 if small else 224),
+                               blocks=(1, 2, 2, 1) if small else (6, 12, 24, 16), growth=8 if small else 32)
+        return Built({"input": x}, t, SCCE, ACC, 0.001)
+    if name == "resnet101":
+        x, t = cnn.resnet101(model, image=kw.get("image", 64 if small else 224),
+                             batch_norm=kw.get("batch_norm", True))
+        return Built({"input": x}, t, SCCE, ACC, 0.001)
     if name == "candle_uno":
         ins, out = cu.candle_uno(model, cu.CandleConfig.small() if small else cu.CandleConfig())
         return Built(ins, out, LossType.LOSS_MEAN_SQUARED_ERROR_AVG_REDUCE,
@@ -110,4 +119,5 @@ def build(name, model, small=False, **kw):
     raise KeyError(f"unknown model {name!r}")
 
 
-NAMES = ["mlp", "mnist_cnn", "cifar10_cnn", "alexnet", "inception_v3", "resnet50", "candle_uno", "dlrm", "nmt"]
+NAMES = ["mlp", "mnist_cnn", "cifar10_cnn", "alexnet", "inception_v3", "resnet50", "resnet101", "densenet121",
+         "candle_uno", "dlrm", "nmt"]

@@ -241,7 +241,7 @@ def _zoo_feed(m, built, seed=0):
 
 
 @pytest.mark.parametrize("name", ["mlp", "mnist_cnn", "cifar10_cnn", "alexnet", "inception_v3", "resnet50",
-                                  "candle_uno", "dlrm", "nmt"])
+                                  "candle_uno", "dlrm", "nmt", "densenet121"])
 def test_zoo_models_train_cpu(name):
     m, built = _zoo_model(name)
     m.init_layers()
