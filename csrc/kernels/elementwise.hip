@@ -135,6 +135,7 @@ struct CopyDesc {
   const void* src;
   void* dst;
   long rows, cols, lds, ldd;
+  int vec;   // 16-B units: pointers, row bytes and leading dims all multiples of 16 B
 };
 constexpr int MAXC = 16;
 struct CopyTab {
@@ -147,6 +148,34 @@ template <typename T>
 __global__ void fm_multi_copy(CopyTab t) {
   const CopyDesc& d = t.d[blockIdx.y];
   const int add = (t.add >> blockIdx.y) & 1;
+  if (d.vec) {   // 16-B vector path: 8 bf16 / 4 fp32 per thread-iteration
+    constexpr int E = 16 / sizeof(T);
+    const long cu = d.cols / E, total = d.rows * cu;
+    const char* s = reinterpret_cast<const char*>(d.src);
+    char* o = reinterpret_cast<char*>(d.dst);
+    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+      const long r = e / cu, c = e - r * cu;
+      const u32x4_t* sp = reinterpret_cast<const u32x4_t*>(s + (r * d.lds + c * E) * (long)sizeof(T));
+      u32x4_t* op = reinterpret_cast<u32x4_t*>(o + (r * d.ldd + c * E) * (long)sizeof(T));
+      u32x4_t v = *sp;
+      if (add) {
+        u32x4_t w = *op;
+        if constexpr (sizeof(T) == 4) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = __float_as_uint(__uint_as_float(v[j]) + __uint_as_float(w[j]));
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float lo = bf2f((unsigned short)(v[j] & 0xFFFF)) + bf2f((unsigned short)(w[j] & 0xFFFF));
+            const float hi = bf2f((unsigned short)(v[j] >> 16)) + bf2f((unsigned short)(w[j] >> 16));
+            v[j] = (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+          }
+        }
+      }
+      *op = v;
+    }
+    return;
+  }
   const long total = d.rows * d.cols;
   const T* s = reinterpret_cast<const T*>(d.src);
   T* o = reinterpret_cast<T*>(d.dst);
@@ -292,8 +321,11 @@ extern "C" void fm_multi_copy2d(int n, const void* const* src, void* const* dst,
     int m = std::min(MAXC, n - base);
     long maxe = 1;
     for (int i = 0; i < m; ++i) {
-      t.d[i] = CopyDesc{src[base + i], dst[base + i], rows[base + i], cols[base + i], lds[base + i], ldd[base + i]};
-      maxe = std::max(maxe, rows[base + i] * cols[base + i]);
+      const long E = 16 / elem_bytes;
+      const int vec = ((((uintptr_t)src[base + i]) | ((uintptr_t)dst[base + i])) & 15) == 0 && cols[base + i] % E == 0 &&
+                      lds[base + i] % E == 0 && ldd[base + i] % E == 0;
+      t.d[i] = CopyDesc{src[base + i], dst[base + i], rows[base + i], cols[base + i], lds[base + i], ldd[base + i], vec};
+      maxe = std::max(maxe, rows[base + i] * cols[base + i] / (vec ? E : 1));
     }
     t.n = m;
     t.add = (add_mask >> base) & ((1 << m) - 1);

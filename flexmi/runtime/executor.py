@@ -29,7 +29,7 @@ from flexmi.core.loss_metrics import NUM_SLOTS, PerfMetrics, loss_and_metrics_to
 from flexmi.core.optimizers import AdamOptimizer, SGDOptimizer
 from flexmi.core.types import DataType, LossType, to_torch_dtype
 from flexmi.ops.base import OpCtx
-from flexmi.parallel.layout import Layout, ParallelConfig, ReshardPlan, box_volume
+from flexmi.parallel.layout import Layout, ParallelConfig, ReshardPlan, box_intersect, box_volume
 from flexmi.utils.profiling import OpTimer
 
 
@@ -162,10 +162,31 @@ class Item:
         return f"{self.kind}:{self.name}"
 
 
+def _box2d(buf, buf_lo, box):
+    """A box of a contiguous shard buffer as one strided 2-D copy: (elem offset, rows, cols,
+    leading dim) -- or None when the box is not row x contiguous-span shaped."""
+    shape = tuple(buf.shape)
+    nd = len(shape)
+    ext = [hi - lo for lo, hi in box]
+    strides = buf.stride()
+    off = sum((lo - l) * st for (lo, _), l, st in zip(box, buf_lo, strides))
+    if nd == 1:
+        return off, 1, ext[0], ext[0]
+    part = [d for d in range(1, nd) if ext[d] != shape[d]]
+    if not part:
+        return off, ext[0], int(np.prod(shape[1:])), strides[0]
+    j = part[0]
+    if any(ext[k] != shape[k] for k in range(j + 1, nd)) or any(shape[k] != 1 for k in range(1, j)):
+        return None
+    return off, ext[0], ext[j] * int(np.prod(shape[j + 1:], dtype=np.int64)), strides[0]
+
+
 class FusedExchange:
     """Several reshards moved by ONE all_to_all through persistent send/recv buffers, split in
-    pack (compute) / exchange (RCCL) / unpack (compute) so the compute halves can live inside
-    hipGraph segments."""
+    pack (compute) / exchange (RCCL, asynchronous) / wait / unpack (compute) so the compute halves
+    live inside hipGraph segments and independent work overlaps the collective.  On MI355X the
+    pack and unpack phases are each ONE multi-descriptor copy launch (per 16 pieces) instead of
+    a copy per (tensor, peer) piece."""
 
     def __init__(self, items, world, rank):
         self.items = items
@@ -188,8 +209,93 @@ class FusedExchange:
         self.recv_buf = torch.empty(sum(recv), dtype=self.dtype, device=self.device)
         self.send_off = [sum(send[:p]) for p in range(world)]
         self.recv_off = [sum(recv[:p]) for p in range(world)]
+        self.work = None
+        self._plan_descriptors()
+
+    def _plan_descriptors(self):
+        """Pre-plan every piece as a strided 2-D copy (HIP backend); falls back to per-piece
+        tensor copies when a box is not 2-D expressible or dtypes differ."""
+        self.fast = self.device is not None and torch.device(self.device).type == "cuda"
+        if not self.fast:
+            return
+        r = self.rank
+        pack, unpack, zero = [], [], []
+        soff = list(self.send_off)
+        roff = list(self.recv_off)
+        per_send = defaultdict(list)
+        for (st, src, dst, acc), add in zip(self.items, self.adds):
+            if dst is not None and st.plan.src.partial and not acc:
+                zero.append(dst)
+            for b in (src, dst):
+                if b is not None and (b.dtype != self.dtype or not b.is_contiguous()):
+                    self.fast = False
+                    return
+            src_lo = [lo for lo, _ in st.plan.src.local_box(r)] if src is not None else None
+            dst_lo = [lo for lo, _ in st.plan.dst.local_box(r)] if dst is not None else None
+            for t in st.recvs:
+                if t.src == r:          # local piece: src box -> dst box
+                    a, b = _box2d(src, src_lo, t.box), _box2d(dst, dst_lo, t.box)
+                    if a is None or b is None or a[1:3] != b[1:3]:
+                        self.fast = False
+                        return
+                    pack.append((src, a[0], dst, b[0], a[1], a[2], a[3], b[3], add, t.box))
+            for t in st.sends:
+                if t.dst != r:
+                    a = _box2d(src, src_lo, t.box)
+                    if a is None:
+                        self.fast = False
+                        return
+                    per_send[t.dst].append((src, a))
+            for t in st.recvs:
+                if t.src != r:
+                    b = _box2d(dst, dst_lo, t.box)
+                    if b is None:
+                        self.fast = False
+                        return
+                    n = box_volume(t.box)
+                    unpack.append((self.recv_buf, roff[t.src], dst, b[0], b[1], b[2], b[2], b[3], add, t.box))
+                    roff[t.src] += n
+        for p in range(self.world):     # sends grouped by peer, in plan order (= peer's unpack order)
+            for src, a in per_send.get(p, []):
+                off, rows, cols, ld = a
+                pack.append((src, off, self.send_buf, soff[p], rows, cols, ld, cols, False, None))
+                soff[p] += rows * cols
+        self.zero_list = zero
+        self.pack_desc, self.unpack_desc = self._launches(pack), self._launches(unpack)
+
+    @staticmethod
+    def _launches(desc):
+        """Split descriptors into launches in which no two pieces write intersecting boxes of
+        the same buffer (pieces of one launch run concurrently; partial-sum pieces add)."""
+        out, cur = [], []
+        for d in desc:
+            clash = d[9] is not None and any(
+                e[2] is d[2] and e[9] is not None and box_intersect(e[9], d[9]) is not None for e in cur)
+            if clash or len(cur) == 32:
+                out.append(cur)
+                cur = []
+            cur.append(d)
+        if cur:
+            out.append(cur)
+        return out
+
+    @staticmethod
+    def _run_desc(launches):
+        from flexmi.ops import _kernels as K
+        for ch in launches:
+            mask = 0
+            for k, d in enumerate(ch):
+                if d[8]:
+                    mask |= 1 << k
+            K.C().multi_copy([d[0] for d in ch], [d[1] for d in ch], [d[2] for d in ch], [d[3] for d in ch],
+                             [d[4] for d in ch], [d[5] for d in ch], [d[6] for d in ch], [d[7] for d in ch], mask)
 
     def pack(self):
+        if self.fast:
+            for z in self.zero_list:
+                z.zero_()
+            self._run_desc(self.pack_desc)
+            return
         for (st, src, dst, acc), add in zip(self.items, self.adds):
             st.prepare_dst(dst, acc)
             st.local_copies(src, dst, add)
@@ -205,11 +311,27 @@ class FusedExchange:
                 off[p] += n
 
     def exchange(self, comm):
+        self.start(comm)
+        self.wait()
+
+    def start(self, comm):
+        """Launch the all_to_all asynchronously (RCCL runs on its own stream; the current
+        stream keeps executing independent work until :meth:`wait`)."""
         import torch.distributed as dist
-        dist.all_to_all_single(self.recv_buf, self.send_buf, self.recv_sizes, self.send_sizes)
+        self.work = dist.all_to_all_single(self.recv_buf, self.send_buf, self.recv_sizes, self.send_sizes,
+                                           async_op=True)
         comm.calls += 1
+        comm.bytes_sent += self.send_buf.numel() * self.send_buf.element_size()
+
+    def wait(self):
+        if self.work is not None:
+            self.work.wait()
+            self.work = None
 
     def unpack(self):
+        if self.fast:
+            self._run_desc(self.unpack_desc)
+            return
         chunks = list(torch.split(self.recv_buf, self.recv_sizes))
         offs = [0] * self.world
         for (st, src, dst, acc), add in zip(self.items, self.adds):
@@ -319,6 +441,9 @@ class Executor:
         for op in ops:
             for t in op.inputs + op.outputs:
                 self.tensors[t.guid] = t
+        self.final_op = ops[-1]
+        ops = self._comm_first_order(ops)
+        self.ops = ops
 
         # ---- activation buffers ------------------------------------------------
         self.act: Dict[tuple, torch.Tensor] = {}
@@ -366,7 +491,7 @@ class Executor:
         # backward liveness: an op runs backward only when one of its outputs reaches the loss;
         # its float inputs then need gradients (graph inputs only when asked, e.g. for the cost
         # measurement of a single op).  Dead branches (an encoder's unused top output) are skipped.
-        final = ops[-1].outputs[0]
+        final = self.final_op.outputs[0]
         self.final = final
         self.grad_needed = {final.guid}
         self.bwd_live = set()
@@ -457,6 +582,53 @@ class Executor:
         self._build_epilogue_fusion(ops)
         self.adam_state = torch.tensor([1.0, 1.0, 0.0], dtype=torch.float32, device=self.device)
         self._compile_program()
+
+    def _comm_first_order(self, ops):
+        """Topological op order that runs the producers of cross-device reshards (and their
+        ancestors) as early as possible, so the asynchronous exchanges started after them
+        overlap the remaining independent ops (DLRM: embeddings first, their all_to_all hides
+        behind the bottom MLP; in backward the bottom MLP then hides the gradient exchange).
+        Depends only on the graph and layouts, so every rank derives the same order (the
+        collectives must be issued in the same order everywhere)."""
+        if self.world == 1:
+            return list(ops)
+        prod = {t.guid: op for op in ops for t in op.outputs}
+        idx = {op.guid: k for k, op in enumerate(ops)}
+        deps = {op.guid: {prod[t.guid].guid for t in op.inputs if t.guid in prod} for op in ops}
+        hot = set()
+        for op in ops:
+            for i, t in enumerate(op.inputs):
+                if t.guid not in prod:
+                    continue
+                need, home = self.need[(op.guid, i)], self.home[t.guid]
+                if not need.same_as(home) and any(tr.src != tr.dst for tr in ReshardPlan(home, need).transfers):
+                    hot.add(prod[t.guid].guid)
+        stack = list(hot)
+        while stack:
+            g = stack.pop()
+            for d in deps[g]:
+                if d not in hot:
+                    hot.add(d)
+                    stack.append(d)
+        by_guid = {op.guid: op for op in ops}
+        indeg = {g: len(d) for g, d in deps.items()}
+        users = defaultdict(list)
+        for g, d in deps.items():
+            for x in d:
+                users[x].append(g)
+        import heapq
+        ready = [(0 if op.guid in hot else 1, idx[op.guid], op.guid) for op in ops if indeg[op.guid] == 0]
+        heapq.heapify(ready)
+        out = []
+        while ready:
+            _, _, g = heapq.heappop(ready)
+            out.append(by_guid[g])
+            for u in users[g]:
+                indeg[u] -= 1
+                if indeg[u] == 0:
+                    heapq.heappush(ready, (0 if u in hot else 1, idx[u], u))
+        assert len(out) == len(ops), "graph has a cycle"
+        return out
 
     def _build_epilogue_fusion(self, ops):
         """Linear L1 -> Linear L2 (L1's output consumed only by L2, same layout): L2's dX GEMM
@@ -664,27 +836,76 @@ class Executor:
             lst.append(Item("compute", fn, name))
 
         # ---------------- forward
-        for st in self.fwd_steps:
+        # cross-device reshards are split: pack + asynchronous all_to_all right after the last
+        # producer of their sources, wait + unpack right before the consumer -- so the ops in
+        # between (e.g. the DLRM bottom MLP) overlap the embedding exchange
+        op_pos = {st[1].guid: k for k, st in enumerate(self.fwd_steps) if st[0] == "op"}
+        launch_after = defaultdict(list)     # fwd step index -> exchanges to start after it
+        deferred = {}                        # fwd step index of a reshard -> its exchange
+        for k, st in enumerate(self.fwd_steps):
+            if st[0] != "reshard":
+                continue
+            items = [(rs, self.act.get((g, home.key())), self.act.get((g, need.key())), False)
+                     for g, home, need, rs in st[1]]
+            if self.world == 1 or all(rs.local_only for rs, *_ in items):
+                continue
+            prods = [op_pos[self.tensors[g].owner_op.guid] for g, *_ in st[1]
+                     if self.tensors[g].owner_op is not None and self.tensors[g].owner_op.guid in op_pos]
+            ex = FusedExchange(items, self.world, self.rank)
+            deferred[k] = ex
+            launch_after[max(prods) if prods else -1].append(ex)
+        for ex in launch_after.get(-1, []):
+            self._emit_exchange_start(fwd, ex, "reshard.fwd")
+        for k, st in enumerate(self.fwd_steps):
             if st[0] == "reshard":
-                items = [(rs, self.act.get((g, home.key())), self.act.get((g, need.key())), False)
-                         for g, home, need, rs in st[1]]
-                self._emit_reshards(fwd, items, "reshard.fwd")
+                if k in deferred:
+                    self._emit_exchange_finish(fwd, deferred[k], "reshard.fwd")
+                else:
+                    items = [(rs, self.act.get((g, home.key())), self.act.get((g, need.key())), False)
+                             for g, home, need, rs in st[1]]
+                    self._emit_reshards(fwd, items, "reshard.fwd")
                 continue
-            op = st[1]
-            c = self.ctx.get(op.guid)
-            if c is None:
-                continue
-            grp = self.group_of.get(op.guid)
-            if grp is not None:
-                if grp[0] is op:
-                    C(fwd, op.name + ".group_fwd",
-                      (lambda grp=grp: type(grp[0]).forward_group(grp, [self.ctx[o.guid] for o in grp])))
-                continue
-            C(fwd, op.name + ".fwd", (lambda op=op, c=c: self._fwd_op(op, c)))
-            fwd[-1].check = (lambda op=op, c=c: self._check_op(op.name + ".fwd", c.outputs, "output"))
+            self._emit_fwd_op(fwd, st[1])
+            for ex in launch_after.get(k, []):
+                self._emit_exchange_start(fwd, ex, "reshard.fwd")
 
         # ---------------- backward (accumulate flags resolved at compile time)
+        self._compile_backward(bwd, C)
+
+        # ---------------- update
+        if any(g.replicated for g in self.groups):
+            upd.append(Item("comm", self._sync_grads, "allreduce.wait"))
+        if self.optimizer is not None:
+            C(upd, "update", self._optimizer_step)
+        self.prog_fwd, self.prog_bwd, self.prog_upd = fwd, bwd, upd
+
+    def _emit_exchange_start(self, lst, ex, name):
+        lst.append(Item("compute", ex.pack, name + ".pack"))
+        lst.append(Item("comm", (lambda ex=ex: ex.start(self.comm)), name + ".a2a"))
+
+    def _emit_exchange_finish(self, lst, ex, name):
+        lst.append(Item("comm", ex.wait, name + ".wait"))
+        lst.append(Item("compute", ex.unpack, name + ".unpack"))
+
+    def _emit_fwd_op(self, fwd, op):
+        c = self.ctx.get(op.guid)
+        if c is None:
+            return
+        grp = self.group_of.get(op.guid)
+        if grp is not None:
+            if grp[0] is op:
+                fwd.append(Item("compute", (lambda grp=grp: type(grp[0]).forward_group(grp, [self.ctx[o.guid] for o in grp])),
+                                op.name + ".group_fwd"))
+            return
+        fwd.append(Item("compute", (lambda op=op, c=c: self._fwd_op(op, c)), op.name + ".fwd"))
+        fwd[-1].check = (lambda op=op, c=c: self._check_op(op.name + ".fwd", c.outputs, "output"))
+
+    def _compile_backward(self, bwd, C):
         written = set()
+        # gradient reductions into a tensor's home grad buffer are started where the consumer's
+        # backward produced them and finished right before the first later step that touches
+        # that buffer (normally the producer op's backward), overlapping the steps in between
+        finish_before = defaultdict(list)
         for g in self.groups:   # weight/bias grads accumulate (atomics in fused epilogues): one memset
             if g.numel:
                 C(bwd, "zero_grads", (lambda g=g: g.gradbuf.zero_()))
@@ -695,7 +916,16 @@ class Executor:
             if g.replicated:
                 bucket_left[id(g)] = [len(b[2]) for b in g.buckets]
                 g.works = [None] * len(g.buckets)
-        for st in self.bwd_steps:
+        steps = self.bwd_steps
+
+        def touches(st, keys):
+            if st[0] == "op":
+                return any(self.gkey(t.guid) in keys for t in st[1].inputs + st[1].outputs)
+            return any(self.gkey(g) in keys for _, _, g, _ in st[1])
+
+        for k, st in enumerate(steps):
+            for ex in finish_before.pop(k, []):
+                self._emit_exchange_finish(bwd, ex, "reshard.bwd")
             if st[0] == "op":
                 op = st[1]
                 c = self.ctx.get(op.guid)
@@ -737,16 +967,19 @@ class Executor:
                     key = self.gkey(g)
                     items.append((rs, self.tmp_grad.get((op.guid, i)), self.grad.get(g), key in written or key in seen))
                     seen.add(key)
-                self._emit_reshards(bwd, items, "reshard.bwd")
+                if self.world == 1 or all(rs.local_only for rs, *_ in items):
+                    self._emit_reshards(bwd, items, "reshard.bwd")
+                else:
+                    ex = FusedExchange(items, self.world, self.rank)
+                    self._emit_exchange_start(bwd, ex, "reshard.bwd")
+                    keys = {self.gkey(g) for _, _, g, _ in st[1]}
+                    nxt = next((j for j in range(k + 1, len(steps)) if touches(steps[j], keys)), len(steps))
+                    finish_before[nxt].append(ex)
                 for op, i, g, rs in st[1]:
                     written.add(self.gkey(g))
-
-        # ---------------- update
-        if any(g.replicated for g in self.groups):
-            upd.append(Item("comm", self._sync_grads, "allreduce.wait"))
-        if self.optimizer is not None:
-            C(upd, "update", self._optimizer_step)
-        self.prog_fwd, self.prog_bwd, self.prog_upd = fwd, bwd, upd
+        for ex in finish_before.pop(len(steps), []):
+            self._emit_exchange_finish(bwd, ex, "reshard.bwd")
+        assert not finish_before
 
     def _fwd_op(self, op, c):
         c.training = self.training
