@@ -245,10 +245,11 @@ void launch_bm(const GemmP& p, bool ak, bool bk, bool vec, hipStream_t s) {
 }  // namespace
 
 extern "C" void fm_gemm_glds_launch(const void* params, int bm, int bn, int a_kcontig, int b_kcontig, int prio,
-                                    hipStream_t stream);
+                                    int wide, hipStream_t stream);
 
 // dispatch experiments (tools/gemm_probe.py): 1 = never glds, 2 = glds for every orientation and
-// grid size (K % 64 == 0), 4 = glds 128x128 tiles, 8 = s_setprio around the glds MFMA blocks
+// grid size (K % 64 == 0), 4 = glds 128x128 tiles, 8 = s_setprio around the glds MFMA blocks,
+// 64 = 256x128 glds tile with 4 waves of 128x64
 static int g_gemm_variant = 0;
 extern "C" void fm_gemm_set_variant(int v) { g_gemm_variant = v; }
 
@@ -297,7 +298,8 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
     if (act_y != nullptr || colsum != nullptr) ks = 1;
     if (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks = 1;
     p.ksplit = ks;
-    fm_gemm_glds_launch(&p, bm, 128, a_kcontig, b_kcontig, (g_gemm_variant & 8) ? 1 : 0, stream);
+    fm_gemm_glds_launch(&p, bm, 128, a_kcontig, b_kcontig, (g_gemm_variant & 8) ? 1 : 0, (g_gemm_variant & 64) ? 1 : 0,
+                        stream);
     if (p.ksplit > 1) {
       long total = (long)M * N * batch;
       hipLaunchKernelGGL(fm_gemm_splitk_reduce, dim3(fm_grid(total)), dim3(256), 0, stream, p);

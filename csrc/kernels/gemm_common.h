@@ -118,6 +118,7 @@ FM_DEVICE void gemm_epilogue(const GemmP& p, const f32x4_t (&acc)[MR][NR], int z
         if (n + 3 < p.N && (p.N & 3) == 0) {
           *reinterpret_cast<f32x4_t*>(dst) = acc[i][j];
         } else {
+#pragma unroll
           for (int r = 0; r < 4; ++r)
             if (n + r < p.N) dst[r] = acc[i][j][r];
         }
@@ -174,6 +175,7 @@ FM_DEVICE void gemm_epilogue(const GemmP& p, const f32x4_t (&acc)[MR][NR], int z
           if (p.beta) o += *reinterpret_cast<f32x4_t*>(dst);
           *reinterpret_cast<f32x4_t*>(dst) = o;
         } else {
+#pragma unroll
           for (int r = 0; r < 4; ++r)
             if (n + r < p.N) dst[r] = v[r] + (p.beta ? dst[r] : 0.f);
         }
@@ -190,6 +192,7 @@ FM_DEVICE void gemm_epilogue(const GemmP& p, const f32x4_t (&acc)[MR][NR], int z
           for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(v[r]);
           *reinterpret_cast<bf16x4_t*>(dst) = o;
         } else {
+#pragma unroll
           for (int r = 0; r < 4; ++r)
             if (n + r < p.N) dst[r] = f2bf(v[r] + (p.beta ? bf2f(dst[r]) : 0.f));
         }

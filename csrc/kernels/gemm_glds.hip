@@ -67,12 +67,12 @@ FM_DEVICE void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
-template <int BM, int BN, bool AK, bool BKC, bool PRIO>
-__global__ void __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) fm_gemm_glds_kernel(GemmP p) {
-  constexpr int WN = BN / 64;
-  constexpr int NW = (BM / 64) * WN;
+template <int BM, int BN, int WM, int WN, bool AK, bool BKC, bool PRIO>
+__global__ void __launch_bounds__(WM * WN * 64, 1) fm_gemm_glds_kernel(GemmP p) {
+  constexpr int NW = WM * WN;
   constexpr int NTH = NW * 64;
-  constexpr int MR = 4, NR = 4;
+  constexpr int TM = BM / WM, TN = BN / WN;     // per-wave output tile
+  constexpr int MR = TM / 16, NR = TN / 16;
   constexpr int A_BYTES = BM * BK * 2;
   constexpr int B_BYTES = BN * BK * 2;
   constexpr int STG = A_BYTES + B_BYTES;
@@ -142,9 +142,9 @@ __global__ void __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) fm_gemm_glds_ke
     for (int kk = 0; kk < BK / 32; ++kk) {
       bf16x8_t af[MR], bfr[NR];
 #pragma unroll
-      for (int i = 0; i < MR; ++i) af[i] = frag<AK, BM>(la, wm * 64 + 16 * i, kk, lane);
+      for (int i = 0; i < MR; ++i) af[i] = frag<AK, BM>(la, wm * TM + 16 * i, kk, lane);
 #pragma unroll
-      for (int j = 0; j < NR; ++j) bfr[j] = frag<BKC, BN>(lb, wn * 64 + 16 * j, kk, lane);
+      for (int j = 0; j < NR; ++j) bfr[j] = frag<BKC, BN>(lb, wn * TN + 16 * j, kk, lane);
       if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);   // MFMA issue ahead of the other waves' loads
 #pragma unroll
       for (int i = 0; i < MR; ++i)
@@ -174,27 +174,27 @@ __global__ void __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) fm_gemm_glds_ke
       }
     }
   }
-  gemm_epilogue<MR, NR>(p, acc, zb, split, m0 + wm * 64, n0 + wn * 64, lane);
+  gemm_epilogue<MR, NR>(p, acc, zb, split, m0 + wm * TM, n0 + wn * TN, lane);
 }
 
-template <int BM, int BN, bool PRIO>
+template <int BM, int BN, int WM, int WN, bool PRIO>
 void launch_glds(const GemmP& p, bool ak, bool bk, hipStream_t s) {
-  constexpr int NTH = (BM / 64) * (BN / 64) * 64;
+  constexpr int NTH = WM * WN * 64;
   constexpr int LDS = 3 * (BM + BN) * BK * 2;
   static bool attr_set = false;
   if (!attr_set) {   // >64 KiB dynamic LDS needs the opt-in attribute
     auto set = [](const void* f) { (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS); };
-    set((const void*)fm_gemm_glds_kernel<BM, BN, true, true, PRIO>);
-    set((const void*)fm_gemm_glds_kernel<BM, BN, true, false, PRIO>);
-    set((const void*)fm_gemm_glds_kernel<BM, BN, false, true, PRIO>);
-    set((const void*)fm_gemm_glds_kernel<BM, BN, false, false, PRIO>);
+    set((const void*)fm_gemm_glds_kernel<BM, BN, WM, WN, true, true, PRIO>);
+    set((const void*)fm_gemm_glds_kernel<BM, BN, WM, WN, true, false, PRIO>);
+    set((const void*)fm_gemm_glds_kernel<BM, BN, WM, WN, false, true, PRIO>);
+    set((const void*)fm_gemm_glds_kernel<BM, BN, WM, WN, false, false, PRIO>);
     attr_set = true;
   }
   dim3 grid(p.tiles_m * p.tiles_n, p.batch, p.ksplit);
-  if (ak && bk) hipLaunchKernelGGL((fm_gemm_glds_kernel<BM, BN, true, true, PRIO>), grid, dim3(NTH), LDS, s, p);
-  else if (ak && !bk) hipLaunchKernelGGL((fm_gemm_glds_kernel<BM, BN, true, false, PRIO>), grid, dim3(NTH), LDS, s, p);
-  else if (!ak && bk) hipLaunchKernelGGL((fm_gemm_glds_kernel<BM, BN, false, true, PRIO>), grid, dim3(NTH), LDS, s, p);
-  else hipLaunchKernelGGL((fm_gemm_glds_kernel<BM, BN, false, false, PRIO>), grid, dim3(NTH), LDS, s, p);
+  if (ak && bk) hipLaunchKernelGGL((fm_gemm_glds_kernel<BM, BN, WM, WN, true, true, PRIO>), grid, dim3(NTH), LDS, s, p);
+  else if (ak && !bk) hipLaunchKernelGGL((fm_gemm_glds_kernel<BM, BN, WM, WN, true, false, PRIO>), grid, dim3(NTH), LDS, s, p);
+  else if (!ak && bk) hipLaunchKernelGGL((fm_gemm_glds_kernel<BM, BN, WM, WN, false, true, PRIO>), grid, dim3(NTH), LDS, s, p);
+  else hipLaunchKernelGGL((fm_gemm_glds_kernel<BM, BN, WM, WN, false, false, PRIO>), grid, dim3(NTH), LDS, s, p);
 }
 
 }  // namespace
@@ -202,14 +202,16 @@ void launch_glds(const GemmP& p, bool ak, bool bk, hipStream_t s) {
 // Launch the pipelined kernel for a prepared parameter block (tiles_m/n and ksplit filled in
 // for the chosen tile).  Caller guarantees: K % 64 == 0 (per split: whole tiles), 16-B aligned
 // operands with leading dims % 8 == 0, and M % 8 == 0 / N % 8 == 0 for MN-contiguous operands.
+// wide: 4 waves with 128x64 wave tiles (fewer LDS fragment reads per MFMA) instead of 8 waves
+// of 64x64 for the 256x128 tile.
 extern "C" void fm_gemm_glds_launch(const void* params, int bm, int bn, int a_kcontig, int b_kcontig, int prio,
-                                    hipStream_t stream) {
+                                    int wide, hipStream_t stream) {
   const GemmP& p = *reinterpret_cast<const GemmP*>(params);
   if (bm == 256) {
-    if (prio) launch_glds<256, 128, true>(p, a_kcontig, b_kcontig, stream);
-    else launch_glds<256, 128, false>(p, a_kcontig, b_kcontig, stream);
+    if (wide) launch_glds<256, 128, 2, 2, false>(p, a_kcontig, b_kcontig, stream);
+    else if (prio) launch_glds<256, 128, 4, 2, true>(p, a_kcontig, b_kcontig, stream);
+    else launch_glds<256, 128, 4, 2, false>(p, a_kcontig, b_kcontig, stream);
   } else {
-    if (prio) launch_glds<128, 128, true>(p, a_kcontig, b_kcontig, stream);
-    else launch_glds<128, 128, false>(p, a_kcontig, b_kcontig, stream);
+    launch_glds<128, 128, 2, 2, false>(p, a_kcontig, b_kcontig, stream);
   }
 }

@@ -49,7 +49,8 @@ def write_ninja(only=None):
         "ninja_required_version = 1.5",
         f"hipcc = {ROCM}/bin/hipcc",
         "cxx = g++",
-        f"hipflags = --offload-arch={ARCH} -O3 -std=c++17 -fPIC -Wno-unused-result -munsafe-fp-atomics -I{ROOT}/csrc/kernels",
+        f"hipflags = --offload-arch={ARCH} -O3 -std=c++17 -fPIC -Wno-unused-result -munsafe-fp-atomics "
+        f"-mllvm -pragma-unroll-threshold=500000 -I{ROOT}/csrc/kernels",
         f"cxxflags = -O3 -std=c++17 -fPIC -Wall -Wno-sign-compare -I{ROOT}/csrc/runtime -I{ROOT}/csrc/sim {pyinc}",
         "rule hipcc",
         "  command = $hipcc $hipflags -MD -MF $out.d -c $in -o $out",
