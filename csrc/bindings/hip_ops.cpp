@@ -28,7 +28,8 @@ void fm_embedding_fwd_multi(int n, const float* const* W, const void* const* idx
                             long B, hipStream_t st);
 void fm_embedding_bwd_multi(int n, float* const* W, const void* const* idx, const int* idx64, const void* const* dy,
                             const long* ldg, const int* rows, const int* D, const int* bag, const float* scale, int dy_bf16,
-                            const float* lr, long B, hipStream_t st);
+                            const float* lr, long B, int* const* owner, int* const* dups, int* const* ndup,
+                            hipStream_t st);
 void fm_dot_interaction_fwd(const void* const* z, int F, long ldz, void* out, long ldo, long B, int D, int W, int self,
                             hipStream_t s);
 void fm_dot_interaction_bwd(const void* const* z, int F, long ldz, const void* dout, long ldo, void* const* dz, long lddz,
@@ -236,13 +237,35 @@ void embedding_fwd_multi(std::vector<torch::Tensor> W, std::vector<torch::Tensor
                          a.D.data(), a.bag.data(), a.scale.data(), is_bf16(out[0]), a.B, cur());
 }
 
+// claim: optional per-table [owner (int32 [rows], -1 filled), dups (int32 [B*bag]), ndup (int32 [1])]
+// triples (owner-computes sparse SGD for mostly-unique tables); None entries use the atomic path
 void embedding_bwd_multi(std::vector<torch::Tensor> W, std::vector<torch::Tensor> idx, std::vector<torch::Tensor> dy,
-                         std::vector<int64_t> ldg, std::vector<double> scale, c10::optional<torch::Tensor> lr) {
+                         std::vector<int64_t> ldg, std::vector<double> scale, c10::optional<torch::Tensor> lr,
+                         c10::optional<std::vector<c10::optional<torch::Tensor>>> claim) {
   if (W.empty()) return;
   TabArgs a = tab_args(W, idx, dy, ldg, scale);
+  std::vector<int*> own(W.size(), nullptr), dup(W.size(), nullptr), nd(W.size(), nullptr);
+  bool any = false;
+  if (claim.has_value()) {
+    TORCH_CHECK(claim->size() == 3 * W.size(), "claim: 3 buffers per table");
+    for (size_t k = 0; k < W.size(); ++k) {
+      const auto& o = (*claim)[3 * k];
+      if (!o.has_value() || !o->defined()) continue;
+      const auto& d = (*claim)[3 * k + 1];
+      const auto& c = (*claim)[3 * k + 2];
+      TORCH_CHECK(o->scalar_type() == torch::kInt32 && o->numel() >= W[k].size(0), "claim owner: int32 [rows]");
+      TORCH_CHECK(d.has_value() && d->scalar_type() == torch::kInt32 && d->numel() >= idx[k].numel(), "claim dups");
+      TORCH_CHECK(c.has_value() && c->scalar_type() == torch::kInt32 && c->numel() >= 1, "claim ndup");
+      own[k] = o->data_ptr<int>();
+      dup[k] = d->data_ptr<int>();
+      nd[k] = c->data_ptr<int>();
+      any = true;
+    }
+  }
   fm_embedding_bwd_multi((int)W.size(), a.Wm.data(), a.idx.data(), a.idx64.data(), a.cact.data(), a.ld.data(), a.rows.data(),
                          a.D.data(), a.bag.data(), a.scale.data(), is_bf16(dy[0]),
-                         lr.has_value() && lr->defined() ? lr->data_ptr<float>() : nullptr, a.B, cur());
+                         lr.has_value() && lr->defined() ? lr->data_ptr<float>() : nullptr, a.B,
+                         any ? own.data() : nullptr, any ? dup.data() : nullptr, any ? nd.data() : nullptr, cur());
 }
 
 void dot_fwd(std::vector<torch::Tensor> zs, int64_t ldz, torch::Tensor out, int64_t ldo, int64_t D, int64_t W, bool self) {

@@ -177,6 +177,103 @@ void launch_fwd(const TabSet& s, int m, bool vec, bool out_bf16, long B, int D0,
   }
 }
 
+// ---- mostly-unique tables (rows > B*bag): owner-computes sparse SGD without row atomics -------
+// claim: every lookup entry e CASes its row's owner slot (-1 -> e); the winner owns the row, the
+// others are appended to a per-table duplicate list.  dup: one wave per duplicate adds its row
+// update with float atomics (few for large tables).  owner (after dup, kernel boundary): each
+// owner does a plain 16-B read-modify-write of its row and releases the claim (-1), so the table
+// is touched with full-line stores at the HBM rate instead of the ~1.3 TB/s atomic rate.
+struct ClaimDesc {
+  float* W;
+  const void* idx;
+  const void* dy;
+  long ld;
+  int D, bag;
+  float scale;
+  int* owner;   // [rows] int32, -1 = free (restored by the owner kernel)
+  int* dups;    // [B*bag]
+  int* ndup;    // [1]
+};
+struct ClaimSet {
+  ClaimDesc t[MAXT];
+  int n;
+};
+
+template <bool I64>
+__global__ void __launch_bounds__(256) fm_emb_claim_multi(ClaimSet s, long B) {
+  const ClaimDesc& d = s.t[blockIdx.y];
+  const long n = B * d.bag;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const long r = ldi<I64>(d.idx, e);
+    const int prev = atomicCAS(d.owner + r, -1, (int)e);
+    if (prev != -1) d.dups[atomicAdd(d.ndup, 1)] = (int)e;
+  }
+}
+
+template <typename GT, bool I64>
+__global__ void __launch_bounds__(256) fm_emb_dup_multi(ClaimSet s, const float* __restrict__ lr) {
+  const ClaimDesc& d = s.t[blockIdx.y];
+  const int nd = *d.ndup;
+  const float mul = -lr[0] * d.scale;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const GT* dy = reinterpret_cast<const GT*>(d.dy);
+  for (long k = blockIdx.x * 4L + wave; k < nd; k += (long)gridDim.x * 4) {
+    const long e = d.dups[k];
+    const long b = e / d.bag, r = ldi<I64>(d.idx, e);
+    for (int c = lane; c < d.D; c += 64) atomicAdd(d.W + r * d.D + c, ld<GT>(dy + b * d.ld + c) * mul);
+  }
+}
+
+template <typename GT, bool I64>
+__global__ void __launch_bounds__(256) fm_emb_owner_multi(ClaimSet s, const float* __restrict__ lr, long B) {
+  const ClaimDesc& d = s.t[blockIdx.y];
+  const float mul = -lr[0] * d.scale;
+  const int D4 = d.D >> 2;
+  const int lpr = D4 < 64 ? D4 : 64;
+  const int rpi = 256 / lpr;
+  const int sub = threadIdx.x / lpr, lc = threadIdx.x - sub * lpr;
+  const long n = B * d.bag;
+  const GT* dy = reinterpret_cast<const GT*>(d.dy);
+  if (sub < rpi) {
+    for (long e = (long)blockIdx.x * rpi + sub; e < n; e += (long)gridDim.x * rpi) {
+      const long r = ldi<I64>(d.idx, e);
+      if (d.owner[r] != (int)e) continue;          // uniform across the row's lanes
+      const long b = e / d.bag;
+      for (int c4 = lc; c4 < D4; c4 += lpr) {
+        const int c = c4 * 4;
+        f32x4_t* wp = reinterpret_cast<f32x4_t*>(d.W + r * d.D + c);
+        f32x4_t w = *wp;
+        if constexpr (sizeof(GT) == 2) {
+          const bf16x4_t g = *reinterpret_cast<const bf16x4_t*>(dy + b * d.ld + c);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) w[j] += mul * bf2f((unsigned short)g[j]);
+        } else {
+          const f32x4_t g = *reinterpret_cast<const f32x4_t*>(dy + b * d.ld + c);
+          w += mul * g;
+        }
+        *wp = w;
+      }
+      if (lc == 0) d.owner[r] = -1;                // release the claim for the next step
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *d.ndup = 0;   // the dup kernel has finished reading it
+}
+
+template <bool I64>
+void launch_claim(const ClaimSet& s, int m, bool dy_bf16, const float* lr, long B, int maxbag, int minD4,
+                  hipStream_t st) {
+  const long n = B * maxbag;
+  dim3 gc((unsigned)std::max<long>(1, std::min<long>((n + 255) / 256, 1024)), m);
+  hipLaunchKernelGGL((fm_emb_claim_multi<I64>), gc, dim3(256), 0, st, s, B);
+  dim3 gd((unsigned)std::max<long>(1, std::min<long>((n + 3) / 4, 1024)), m);
+  if (dy_bf16) hipLaunchKernelGGL((fm_emb_dup_multi<unsigned short, I64>), gd, dim3(256), 0, st, s, lr);
+  else hipLaunchKernelGGL((fm_emb_dup_multi<float, I64>), gd, dim3(256), 0, st, s, lr);
+  const int rpi = 256 / std::min(64, std::max(1, minD4));
+  dim3 go((unsigned)std::max<long>(1, std::min<long>((n + rpi - 1) / rpi, 2048)), m);
+  if (dy_bf16) hipLaunchKernelGGL((fm_emb_owner_multi<unsigned short, I64>), go, dim3(256), 0, st, s, lr, B);
+  else hipLaunchKernelGGL((fm_emb_owner_multi<float, I64>), go, dim3(256), 0, st, s, lr, B);
+}
+
 template <bool I64>
 void launch_bwd(const TabSet& s, int m, bool tiny, bool dy_bf16, const float* lr, long B, int maxD, hipStream_t st) {
   if (tiny) {
@@ -231,12 +328,37 @@ extern "C" void fm_embedding_fwd_multi(int n, const float* const* W, const void*
 extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const* idx, const int* idx64,
                                        const void* const* dy, const long* ldg, const int* rows, const int* D,
                                        const int* bag, const float* scale, int dy_bf16, const float* lr, long B,
-                                       hipStream_t st) {
+                                       int* const* owner, int* const* dups, int* const* ndup, hipStream_t st) {
   if (B <= 0) return;
+  // owner-computes path: fused SGD, claim buffers given, 16-B rows
+  auto claimable = [&](int k) {
+    return lr != nullptr && owner != nullptr && owner[k] != nullptr && D[k] % 4 == 0 && ldg[k] % 4 == 0 &&
+           D[k] <= 256;
+  };
+  for (int wide = 0; wide < 2; ++wide) {
+    std::vector<int> sel;
+    for (int k = 0; k < n; ++k)
+      if (claimable(k) && (idx64[k] != 0) == (wide != 0)) sel.push_back(k);
+    for (size_t base = 0; base < sel.size(); base += MAXT) {
+      ClaimSet s;
+      int m = (int)std::min<size_t>(MAXT, sel.size() - base);
+      int maxbag = 1, minD4 = 64;
+      for (int i = 0; i < m; ++i) {
+        int k = sel[base + i];
+        s.t[i] = ClaimDesc{W[k], idx[k], dy[k], ldg[k], D[k], bag[k], scale[k], owner[k], dups[k], ndup[k]};
+        maxbag = std::max(maxbag, bag[k]);
+        minD4 = std::min(minD4, D[k] / 4);
+      }
+      s.n = m;
+      if (wide) launch_claim<true>(s, m, dy_bf16, lr, B, maxbag, minD4, st);
+      else launch_claim<false>(s, m, dy_bf16, lr, B, maxbag, minD4, st);
+    }
+  }
   for (int pass = 0; pass < 4; ++pass) {
     const bool tiny = pass < 2, wide = pass & 1;
     std::vector<int> sel;
     for (int k = 0; k < n; ++k) {
+      if (claimable(k)) continue;
       bool t = rows[k] <= TINY_ROWS && D[k] <= 256 && B * (long)bag[k] >= 16L * rows[k];
       if (t == tiny && (idx64[k] != 0) == wide) sel.push_back(k);
     }
@@ -265,5 +387,6 @@ extern "C" void fm_embedding_fwd(const void* idx, int idx64, const float* W, voi
 
 extern "C" void fm_embedding_bwd(const void* idx, int idx64, const void* dy, int dy_bf16, float* W, const float* lr,
                                  long B, int bag, int rows, int D, long ldg, float scale, hipStream_t s) {
-  fm_embedding_bwd_multi(1, &W, &idx, &idx64, &dy, &ldg, &rows, &D, &bag, &scale, dy_bf16, lr, B, s);
+  fm_embedding_bwd_multi(1, &W, &idx, &idx64, &dy, &ldg, &rows, &D, &bag, &scale, dy_bf16, lr, B, nullptr, nullptr,
+                         nullptr, s);
 }

@@ -11,6 +11,8 @@
 //   dZ_0 += dOut[:, :D].  Inputs/grads are pointer tables, so it also reads/writes concat slices.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int MAXF = 32;
@@ -148,12 +150,28 @@ __global__ void __launch_bounds__(256) fm_dot_fwd_t(PtrTab Z, long ldz, unsigned
   const int waves_total = gridDim.x * (blockDim.x >> 6);
   const int r = lane & 31, h = lane >> 5;
   const int npairs = self ? F * (F + 1) / 2 : F * (F - 1) / 2;
-  for (long b = blockIdx.x * (blockDim.x >> 6) + wave; b < B; b += waves_total) {
-    bf16x8_t f[KS];
-    const unsigned short* zr = (r < F) ? (Z.p[r] + b * ldz + 8 * h) : nullptr;
+  // persistent waves: the Z rows of the NEXT sample are loaded before this sample's MFMAs and
+  // output writes, so every wave keeps one sample's loads in flight behind its compute
+  const unsigned short* zbase = (r < F) ? Z.p[r] : Z.p[0];
+  const bool zok = r < F;
+  long b = blockIdx.x * (blockDim.x >> 6) + wave;
+  bf16x8_t f[KS];
+  {
+    const unsigned short* zr = zbase + min(b, B - 1) * ldz + 8 * h;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-      f[ks] = zr ? *reinterpret_cast<const bf16x8_t*>(zr + 16 * ks) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    for (int ks = 0; ks < KS; ++ks) f[ks] = *reinterpret_cast<const bf16x8_t*>(zr + 16 * ks);
+  }
+  for (; b < B; b += waves_total) {
+    bf16x8_t fn[KS];
+    {
+      const unsigned short* zr = zbase + min(b + waves_total, B - 1) * ldz + 8 * h;   // clamped: unconditional
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) fn[ks] = *reinterpret_cast<const bf16x8_t*>(zr + 16 * ks);
+    }
+    if (!zok) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) f[ks] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    }
     f32x16_t acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
@@ -175,6 +193,8 @@ __global__ void __launch_bounds__(256) fm_dot_fwd_t(PtrTab Z, long ldz, unsigned
     unsigned short* o = out + b * ldo;
     for (int c = lane * 8; c < W; c += 64 * 8) *reinterpret_cast<u32x4_t*>(o + c) = *reinterpret_cast<const u32x4_t*>(row + c);
     FM_WAVE_LDS_SYNC();
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) f[ks] = fn[ks];
   }
 }
 
@@ -192,16 +212,29 @@ __global__ void __launch_bounds__(256) fm_dot_bwd_t(PtrTab Z, long ldz, const un
   unsigned short* ss = reinterpret_cast<unsigned short*>(base + 32 * DT * 2);          // [32][32]
   unsigned short* ds = reinterpret_cast<unsigned short*>(base + 32 * DT * 2 + 2048);   // dOut row [W]
   const int waves_total = gridDim.x * (blockDim.x >> 6);
-  for (long b = blockIdx.x * (blockDim.x >> 6) + wave; b < B; b += waves_total) {
-    u32x4_t zv[ZCH];
+  // persistent waves with the next sample's Z rows and dOut row prefetched into registers
+  // (clamped addresses: every load unconditional) while this sample is processed
+  const bool dload = lane * 8 < W;
+  auto load = [&](long bb, u32x4_t (&zv)[ZCH], u32x4_t& dv) {
+    bb = min(bb, B - 1);
 #pragma unroll
     for (int t = 0; t < ZCH; ++t) {
       const int c = lane + 64 * t, i = c / CPR, k = (c % CPR) * 8;
-      zv[t] = i < F ? *reinterpret_cast<const u32x4_t*>(Z.p[i] + b * ldz + k) : u32x4_t{0u, 0u, 0u, 0u};
+      zv[t] = *reinterpret_cast<const u32x4_t*>(Z.p[i < F ? i : 0] + bb * ldz + k);
     }
-    u32x4_t dv = {0u, 0u, 0u, 0u};
-    const bool dload = lane * 8 < W;
-    if (dload) dv = *reinterpret_cast<const u32x4_t*>(dout + b * ldo + lane * 8);
+    dv = *reinterpret_cast<const u32x4_t*>(dout + bb * ldo + (dload ? lane * 8 : 0));
+  };
+  long b = blockIdx.x * (blockDim.x >> 6) + wave;
+  u32x4_t zv[ZCH], dv;
+  load(b, zv, dv);
+  for (; b < B; b += waves_total) {
+    u32x4_t zn[ZCH], dn;
+    load(b + waves_total, zn, dn);
+#pragma unroll
+    for (int t = 0; t < ZCH; ++t) {
+      const int i = (lane + 64 * t) / CPR;
+      if (i >= F) zv[t] = u32x4_t{0u, 0u, 0u, 0u};
+    }
 #pragma unroll
     for (int t = 0; t < ZCH; ++t) {
       const int c = lane + 64 * t, i = c / CPR, k = (c % CPR) * 8;
@@ -270,10 +303,23 @@ __global__ void __launch_bounds__(256) fm_dot_bwd_t(PtrTab Z, long ldz, const un
       *reinterpret_cast<bf16x8_t*>(d) = v;
     }
     FM_WAVE_LDS_SYNC();
+#pragma unroll
+    for (int t = 0; t < ZCH; ++t) zv[t] = zn[t];
+    dv = dn;
   }
 }
 
 FM_HOST_DEVICE bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// persistent-grid size of the interaction kernels (4 waves per block; each wave loops over
+// samples with the next one prefetched).  FM_DOT_BLOCKS overrides (tuning runs).
+long dot_block_cap() {
+  static const long cap = [] {
+    const char* e = getenv("FM_DOT_BLOCKS");
+    return e ? std::max(1L, atol(e)) : 512L;
+  }();
+  return cap;
+}
 
 }  // namespace
 
@@ -282,7 +328,7 @@ extern "C" void fm_dot_interaction_fwd(const void* const* z, int F, long ldz, vo
   PtrTab t;
   for (int i = 0; i < MAXF; ++i) t.p[i] = i < F ? (const unsigned short*)z[i] : nullptr;
   int waves = 4;
-  long blocks = std::min<long>((B + waves - 1) / waves, 8192);
+  long blocks = std::min<long>((B + waves - 1) / waves, dot_block_cap());
   bool fast = (D == 32 || D == 64 || D == 128) && F <= 32 && ldz % 8 == 0 && ldo % 8 == 0 && W % 8 == 0 && al16(out);
   for (int i = 0; i < F; ++i) fast = fast && al16(z[i]);
   if (fast) {
@@ -304,7 +350,7 @@ extern "C" void fm_dot_interaction_bwd(const void* const* z, int F, long ldz, co
     g.p[i] = i < F ? (unsigned short*)dz[i] : nullptr;
   }
   int waves = 4;
-  long blocks = std::min<long>((B + waves - 1) / waves, 8192);
+  long blocks = std::min<long>((B + waves - 1) / waves, dot_block_cap());
   const int npairs = self ? F * (F + 1) / 2 : F * (F - 1) / 2;
   const int W = ((D + npairs) + 7) & ~7;    // dOut columns read (x part + packed triangle)
   bool fast = (D == 32 || D == 64 || D == 128) && F <= 32 && ldz % 8 == 0 && ldo % 8 == 0 && lddz % 8 == 0 && al16(dout);

@@ -8,13 +8,16 @@ loop (bug, ``:187-195``); here AVG divides once.
 MI355X: ``csrc/kernels/embedding.hip`` -- lanes gather whole rows with 16-B loads and write bf16
 activations; the executor fuses all embedding ops of one placement into ONE launch (descriptor
 table).  The backward never materialises a dense gradient for SGD: rows are updated in place
-(W[idx] -= lr*dy) with 256-B-contiguous fp32 atomics, tiny tables accumulate in LDS first.
+(W[idx] -= lr*dy).  Mostly-unique (large) tables use owner-computes: each row is claimed by one
+lookup (CAS), duplicates add with atomics, the owner applies a plain 16-B read-modify-write;
+other tables use 256-B-contiguous fp32 atomics; tiny tables accumulate in LDS first.
 SOAP: sample split, **column (parameter) split** of the table and whole-table placement
 (``dims=[1,1]``, device k) -- a 100 M-row table fits one MI355X's 288 GB of HBM.
 """
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -85,7 +88,7 @@ class Embedding(Op):
         if self.sparse_sgd:
             # fused sparse SGD (no dense grad): W[idx] -= lr * dy  (duplicates summed first)
             if ctx.hip:
-                K.embedding_backward_sgd(idx, dy, ctx.weights[0], ctx.lr, int(self.aggr), ctx.workspace)
+                Embedding.backward_group([self], [ctx])
             else:
                 g = dy.float()
                 if self.aggr == AggrMode.AGGR_MODE_AVG:
@@ -141,8 +144,35 @@ class Embedding(Op):
             for t in tables:
                 t.zero_()
             lr = None
+        claim = None
+        if ops[0].sparse_sgd:
+            bufs = [op._claim_buffers(c) for op, c in zip(ops, ctxs)]
+            if any(b is not None for b in bufs):
+                claim = []
+                for b in bufs:
+                    claim.extend(b if b is not None else (None, None, None))
         K.C().embedding_bwd_multi(tables, [c.inputs[0] for c in ctxs], [c.out_grads[0] for c in ctxs],
-                                  [c.out_grads[0].stride(0) for c in ctxs], scales, lr)
+                                  [c.out_grads[0].stride(0) for c in ctxs], scales, lr, claim)
+
+    CLAIM = os.environ.get("FM_EMB_CLAIM", "1") != "0"
+
+    def _claim_buffers(self, ctx):
+        """Owner-computes sparse SGD buffers for a mostly-unique table (rows > lookups per step):
+        a per-row claim slot (int32, -1 = free; restored after every step), the duplicate list
+        and its counter.  Smaller tables keep the atomic / LDS-privatised kernels."""
+        if not Embedding.CLAIM:
+            return None
+        s = ctx.saved
+        if "claim" not in s:
+            w, idx = ctx.weights[0], ctx.inputs[0]
+            if w.shape[0] > idx.numel() and self.out_dim % 4 == 0:
+                dev = w.device
+                s["claim"] = (torch.full((w.shape[0],), -1, dtype=torch.int32, device=dev),
+                              torch.empty(idx.numel(), dtype=torch.int32, device=dev),
+                              torch.zeros(1, dtype=torch.int32, device=dev))
+            else:
+                s["claim"] = None
+        return s["claim"]
 
     def flops(self, in_shapes, out_shapes):
         return float(in_shapes[0][0] * in_shapes[0][1] * out_shapes[0][1])

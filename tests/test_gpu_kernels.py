@@ -323,3 +323,39 @@ def test_batchnorm_hip(gpu):
     assert rel_err(dbt, g.sum((0, 2, 3))) < 2e-2
     assert rel_err(dg, (g * xhat).sum((0, 2, 3))) < 2e-2
     assert rel_err(dx, gx) < 3e-2
+
+
+@pytest.mark.parametrize("idx_dtype", [torch.int64, torch.int32])
+def test_embedding_owner_computes_sgd(gpu, idx_dtype):
+    """Owner-computes sparse SGD for mostly-unique tables (claim CAS -> duplicate atomics ->
+    owner 16-B RMW): matches the dense reference over two consecutive steps (the claim slots
+    and duplicate counters must be restored after every step), mixed with atomic-path tables."""
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(5)
+    B = 1000
+    specs = [(100000, 1, 128), (1500, 1, 128), (5000, 2, 64), (40, 1, 128), (3, 1, 128)]   # rows, bag, D
+    tables, idxs, claim, refs = [], [], [], []
+    for rows, bag, D in specs:
+        W = torch.randn(rows, D, device=gpu)
+        tables.append(W)
+        refs.append(W.clone())
+        idxs.append(torch.randint(0, rows, (B, bag), device=gpu, dtype=idx_dtype))
+        if rows > B * bag:
+            claim += [torch.full((rows,), -1, dtype=torch.int32, device=gpu),
+                      torch.empty(B * bag, dtype=torch.int32, device=gpu), torch.zeros(1, dtype=torch.int32, device=gpu)]
+        else:
+            claim += [None, None, None]
+    lr = torch.tensor([0.05], device=gpu)
+    for step in range(2):
+        dys = [torch.randn(B, D, device=gpu).to(torch.bfloat16) for _, _, D in specs]
+        Kk.C().embedding_bwd_multi(tables, idxs, dys, [d.stride(0) for d in dys], [1.0] * len(specs), lr, claim)
+        for k, ((rows, bag, D), W) in enumerate(zip(specs, refs)):
+            upd = torch.zeros_like(W)
+            upd.index_add_(0, idxs[k].reshape(-1).long(), dys[k].float().repeat_interleave(bag, 0))
+            W -= 0.05 * upd
+        torch.cuda.synchronize()
+        for k in range(len(specs)):
+            assert torch.allclose(tables[k], refs[k], atol=1e-4), (step, specs[k])
+        for k in range(0, len(claim), 3):
+            if claim[k] is not None:
+                assert int((claim[k] != -1).sum()) == 0 and int(claim[k + 2].item()) == 0, "claims not released"
