@@ -111,7 +111,7 @@ def main():
         for k in range(data.nb):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.stream(s):
-                with torch.cuda.graph(g, stream=s):
+                with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                     data.i = k
                     data.next_batch()
             stage.append(g)

@@ -18,6 +18,7 @@ All buffers are allocated once, so the whole step can be captured in a hipGraph
 from __future__ import annotations
 
 import math
+import os
 import time
 from collections import OrderedDict, defaultdict
 from typing import Dict, List
@@ -152,14 +153,99 @@ def run_reshards(comm, items):
 
 
 class Item:
-    __slots__ = ("kind", "fn", "name", "check")
+    __slots__ = ("kind", "fn", "name", "check", "native")
 
-    def __init__(self, kind, fn, name, check=None):
+    def __init__(self, kind, fn, name, check=None, native=None):
         self.kind, self.fn, self.name = kind, fn, name
         self.check = check      # debug mode: callable(item) run after fn (NaN/Inf guard)
+        self.native = native    # comm items: structured form for the native runner (flexmi._rt)
 
     def __repr__(self):
         return f"{self.kind}:{self.name}"
+
+
+def _rt_module():
+    try:
+        from flexmi import _rt
+        return _rt
+    except ImportError:
+        return None
+
+
+class NativeRunner:
+    """Compiles item lists into programs of the native step runner (``csrc/runtime/step_runner.cc``):
+    compute items stay callables (or, once captured, hipGraph launches), comm items become c10d
+    collectives issued from C++ with their Work handles kept in runner slots -- the step loop and
+    every RCCL call run without the Python interpreter in between."""
+
+    def __init__(self, ex):
+        import torch.distributed as dist
+        self.ex = ex
+        self.rt = _rt_module().StepRunner()
+        self.world_pg = dist.group.WORLD if ex.world > 1 else None
+        self.slots = {}
+        self.pids = {}
+        self.keep = []          # Python objects referenced by native steps (graphs, callables)
+
+    def slot(self, key):
+        s = self.slots.get(key)
+        if s is None:
+            s = self.slots[key] = self.rt.new_slot()
+        return s
+
+    def _pg(self, ranks):
+        g = self.ex.comm.group_for(ranks) if ranks is not None else None
+        return self.world_pg if g is None else g
+
+    def add_item(self, pid, it):
+        rt, ex = self.rt, self.ex
+        nat = it.native
+        if nat is None:
+            rt.add_call(pid, it.fn, it.name)
+            return
+        kind = nat[0]
+        if kind in ("a2a", "a2a_sync"):
+            x = nat[1]
+            s = self.slot(("a2a", id(x)))
+            self.keep.append(x)
+            rt.add_all_to_all(pid, s, self.world_pg, x.recv_buf, x.send_buf, list(x.recv_sizes), list(x.send_sizes),
+                              it.name)
+            if kind == "a2a_sync":
+                rt.add_wait(pid, s, it.name + ".wait")
+        elif kind == "wait":
+            rt.add_wait(pid, self.slot(("a2a", id(nat[1]))), it.name)
+        elif kind == "ar":
+            g, bi = nat[1], nat[2]
+            b = g.buckets[bi]
+            rt.add_all_reduce(pid, self.slot(("ar", id(g), bi)), self._pg(g.holders), g.gradbuf[b[0]:b[1]], False,
+                              it.name)
+        elif kind == "ar_sync":
+            for g in ex.groups:
+                if not g.replicated:
+                    continue
+                for bi, b in enumerate(g.buckets):
+                    rt.add_all_reduce(pid, self.slot(("ar", id(g), bi)), self._pg(g.holders), g.gradbuf[b[0]:b[1]],
+                                      True, f"{it.name}.bucket{bi}")
+        else:
+            raise ValueError(f"unknown native item {kind}")
+
+    def program(self, items):
+        """Program id for an item list (compiled once per list)."""
+        pid = self.pids.get(id(items))
+        if pid is None:
+            pid = self.rt.new_program()
+            for it in items:
+                self.add_item(pid, it)
+            self.pids[id(items)] = pid
+            self.keep.append(items)
+        return pid
+
+    def run(self, pid):
+        rt, comm = self.rt, self.ex.comm
+        c0, b0 = rt.collectives, rt.bytes_sent
+        rt.run(pid)
+        comm.calls += rt.collectives - c0
+        comm.bytes_sent += rt.bytes_sent - b0
 
 
 def _box2d(buf, buf_lo, box):
@@ -397,6 +483,7 @@ class Executor:
         self.training = True
         self.step_count = 0
         self._graph = None
+        self._native = None
         self.build()
 
     # ================================================================== build
@@ -874,17 +961,17 @@ class Executor:
 
         # ---------------- update
         if any(g.replicated for g in self.groups):
-            upd.append(Item("comm", self._sync_grads, "allreduce.wait"))
+            upd.append(Item("comm", self._sync_grads, "allreduce.wait", native=("ar_sync",)))
         if self.optimizer is not None:
             C(upd, "update", self._optimizer_step)
         self.prog_fwd, self.prog_bwd, self.prog_upd = fwd, bwd, upd
 
     def _emit_exchange_start(self, lst, ex, name):
         lst.append(Item("compute", ex.pack, name + ".pack"))
-        lst.append(Item("comm", (lambda ex=ex: ex.start(self.comm)), name + ".a2a"))
+        lst.append(Item("comm", (lambda ex=ex: ex.start(self.comm)), name + ".a2a", native=("a2a", ex)))
 
     def _emit_exchange_finish(self, lst, ex, name):
-        lst.append(Item("comm", ex.wait, name + ".wait"))
+        lst.append(Item("comm", ex.wait, name + ".wait", native=("wait", ex)))
         lst.append(Item("compute", ex.unpack, name + ".unpack"))
 
     def _emit_fwd_op(self, fwd, op):
@@ -960,7 +1047,7 @@ class Executor:
                             bucket_left[id(g)][bi] -= 1
                             if bucket_left[id(g)][bi] == 0 and self.cfg.overlap_grad_sync:
                                 bwd.append(Item("comm", (lambda g=g, bi=bi: self._launch_bucket(g, bi)),
-                                                f"allreduce.bucket{bi}"))
+                                                f"allreduce.bucket{bi}", native=("ar", g, bi)))
             else:
                 items, seen = [], set()
                 for op, i, g, rs in st[1]:
@@ -998,7 +1085,7 @@ class Executor:
             return
         ex = FusedExchange(items, self.world, self.rank)
         lst.append(Item("compute", ex.pack, name + ".pack"))
-        lst.append(Item("comm", (lambda ex=ex: ex.exchange(self.comm)), name + ".a2a"))
+        lst.append(Item("comm", (lambda ex=ex: ex.exchange(self.comm)), name + ".a2a", native=("a2a_sync", ex)))
         lst.append(Item("compute", ex.unpack, name + ".unpack"))
 
     def _emit_loss(self, lst, compute_grad):
@@ -1013,9 +1100,25 @@ class Executor:
             self._emit_reshards(lst, [(self.loss_back, self.logit_grad, self.grad.get(self.final.guid), False)],
                                 "loss.scatter")
 
+    def native_runner(self):
+        """The native step runner when it can execute this executor's programs: ``flexmi._rt``
+        built, plain Comm (fault-injecting wrappers stay on the Python path), no per-item
+        debug / watchdog / timer hooks; FLEXMI_NATIVE_RUNNER=0 disables it."""
+        if self._native is None:
+            from flexmi.parallel.comm import Comm
+            ok = (os.environ.get("FLEXMI_NATIVE_RUNNER", "1") != "0" and _rt_module() is not None
+                  and type(self.comm) is Comm and not self.debug and self.watchdog is None
+                  and not self.timer.enabled)
+            self._native = NativeRunner(self) if ok else False
+        return self._native or None
+
     def _run(self, prog):
         if self.debug or self.watchdog is not None:
             return self._run_guarded(prog)
+        nr = self.native_runner()
+        if nr is not None:
+            nr.run(nr.program(prog))
+            return
         tm = self.timer
         if tm.enabled:
             for it in prog:
@@ -1269,20 +1372,45 @@ class Executor:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         runs = []
+        graphs = []
+        # thread_local capture: the RCCL process group's watchdog thread queries events while
+        # a segment is being captured; only this thread's calls belong to the graph
         for kind, x in segments:
             if kind == "graph":
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.stream(s):
-                    with torch.cuda.graph(g, stream=s):
+                    with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                         for it in x:
                             it.fn()
+                graphs.append(g)
                 runs.append(g.replay)
             else:
                 runs.append(x.fn)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         self._graph_segments = segments
+        self._graphs = graphs
         opt = self.optimizer
+        nr = self.native_runner()
+        if nr is not None:
+            # the whole step as ONE native program: hipGraphLaunch per segment, collectives
+            # issued by the C++ runner in between
+            pid = nr.rt.new_program()
+            gi = iter(graphs)
+            for k, (kind, x) in enumerate(segments):
+                if kind == "graph":
+                    g = next(gi)
+                    nr.rt.add_graph(pid, int(g.raw_cuda_graph_exec()), f"segment{k}")
+                else:
+                    nr.add_item(pid, x)
+            nr.keep.append(graphs)
+
+            def replay():
+                nr.run(pid)
+                if opt is not None:
+                    opt.next()
+                self.step_count += 1
+            return replay
 
         def replay():
             for r in runs:

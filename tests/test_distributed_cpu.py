@@ -118,8 +118,10 @@ def _run(case, world, rank, steps, out_path):
         ex.train_step()
     params = [p.get_weights(m) for p in m.parameters]
     loss = m.get_perf_metrics().get_loss()
+    nr = ex.native_runner()
+    native_colls = nr.rt.collectives if nr is not None else -1
     if rank == 0:
-        np.savez(out_path, loss=loss, *params)
+        np.savez(out_path, loss=loss, native_colls=native_colls, *params)
 
 
 def _worker(rank, world, port, case, steps, out_path):
@@ -155,3 +157,11 @@ def test_strategy_equivalence(case, world):
     for k in keys:
         np.testing.assert_allclose(got[k], ref[k], rtol=1e-4, atol=1e-5, err_msg=f"{case} w{world} {k}")
     assert abs(float(got["loss"]) - float(ref["loss"])) < 1e-4
+    try:
+        import flexmi._rt  # noqa: F401
+    except ImportError:
+        return
+    # the steps ran through the native runner (flexmi._rt): its collectives were issued from C++
+    assert int(got["native_colls"]) >= 0, "world>1 training did not go through the native step runner"
+    if case != "dlrm_search":   # a searched strategy may need no collective at all
+        assert int(got["native_colls"]) > 0

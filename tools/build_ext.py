@@ -25,6 +25,7 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 if ARCH != "gfx950":
     ARCH = "gfx950"  # MI355X only
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+TORCH_RUNTIME_SRCS = ("step_runner.cc",)   # csrc/runtime sources built into flexmi/_rt (torch + HIP)
 
 
 def _torch_paths():
@@ -89,12 +90,31 @@ def write_ninja(only=None):
         lines.append(f"build {out}: hiplink {' '.join(objs)}")
         lines.append(f"  ldflags = {ld}")
         targets.append(out)
+    if only in (None, "C", "rt"):
+        # native step runner (csrc/runtime/step_runner.cc): host C++ against torch's c10d and the
+        # HIP runtime API, compiled by g++ like torch itself so pybind11 shares torch's type
+        # registry (the c10d ProcessGroup objects of torch.distributed pass straight through)
+        tinc, tlib, abi = _torch_paths()
+        incs = " ".join(f"-I{p}" for p in tinc)
+        objs = []
+        for name in TORCH_RUNTIME_SRCS:
+            src = os.path.join(ROOT, "csrc", "runtime", name)
+            o = os.path.join(BUILD, "rt_" + name.replace(".cc", ".o"))
+            lines.append(f"build {o}: cxx {src}")
+            lines.append(f"  extra = -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 -DTORCH_EXTENSION_NAME=_rt "
+                         f"-D_GLIBCXX_USE_CXX11_ABI={abi} {incs} -I{ROCM}/include -Wno-unused-parameter")
+            objs.append(o)
+        out = os.path.join(ROOT, "flexmi", "_rt" + ext)
+        lines.append(f"build {out}: cxxlink {' '.join(objs)}")
+        lines.append(f"  ldflags = -L{tlib} -Wl,-rpath,{tlib} -lc10 -lc10_hip -ltorch -ltorch_cpu -ltorch_hip "
+                     f"-ltorch_python -L{ROCM}/lib -Wl,-rpath,{ROCM}/lib -lamdhip64")
+        targets.append(out)
     if only in (None, "native"):
         objs = []
         for src in sorted(glob.glob(os.path.join(ROOT, "csrc", "runtime", "*.cc")) +
                           glob.glob(os.path.join(ROOT, "csrc", "sim", "*.cc"))) + [
                 os.path.join(ROOT, "csrc", "bindings", "native.cc")]:
-            if not os.path.exists(src):
+            if not os.path.exists(src) or os.path.basename(src) in TORCH_RUNTIME_SRCS:
                 continue
             o = os.path.join(BUILD, "n_" + os.path.basename(src).replace(".cc", ".o"))
             lines.append(f"build {o}: cxx {src}")
@@ -135,7 +155,7 @@ def build(only=None, jobs=None, verbose=False):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", choices=["C", "native"], default=None)
+    ap.add_argument("--only", choices=["C", "rt", "native"], default=None)
     ap.add_argument("-j", type=int, default=None)
     ap.add_argument("-v", action="store_true")
     ap.add_argument("--clean", action="store_true")
