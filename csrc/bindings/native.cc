@@ -2,7 +2,10 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <optional>
+
 #include "loader.h"
+#include "shard.h"
 #include "strategy_pb.h"
 
 namespace py = pybind11;
@@ -34,6 +37,21 @@ std::vector<OpStrategy> from_tuples(const std::vector<OpTuple>& t) {
   return ops;
 }
 
+using PyBox = std::vector<std::pair<int64_t, int64_t>>;
+// (shape, degrees, holders, boxes | None, partial)
+using PyLayout = std::tuple<std::vector<int64_t>, std::vector<int64_t>, std::vector<std::vector<int>>,
+                            std::optional<std::vector<PyBox>>, bool>;
+
+flexmi::ShardLayout to_layout(const PyLayout& t) {
+  flexmi::ShardLayout l;
+  l.shape = std::get<0>(t);
+  l.degrees = std::get<1>(t);
+  l.holders = std::get<2>(t);
+  if (std::get<3>(t)) l.boxes = *std::get<3>(t);
+  l.partial = std::get<4>(t);
+  return l;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
@@ -57,6 +75,23 @@ PYBIND11_MODULE(_native, m) {
     return to_tuples(ops);
   });
   register_sim(m);
+
+  // sharding algebra (csrc/runtime/shard.h): layouts are (shape, degrees, holders, boxes|None, partial)
+  m.def("split_extent", &flexmi::split_extent);
+  m.def("part_box", [](const PyLayout& l, int64_t p) { return to_layout(l).part_box(p); });
+  m.def("reshard_transfers", [](const PyLayout& src, const PyLayout& dst) {
+    std::vector<std::tuple<int, int, PyBox, int64_t, int64_t>> out;
+    for (auto& t : flexmi::reshard_transfers(to_layout(src), to_layout(dst)))
+      out.emplace_back(t.src, t.dst, t.box, t.src_part, t.dst_part);
+    return out;
+  });
+  m.def("split_launches", [](const std::vector<int64_t>& dst, const std::vector<std::optional<PyBox>>& boxes,
+                             int max_per_launch) {
+    std::vector<flexmi::Box> b;
+    b.reserve(boxes.size());
+    for (auto& x : boxes) b.push_back(x ? *x : flexmi::Box{});
+    return flexmi::split_launches(dst, b, max_per_launch);
+  });
 
   // data-loader ring (csrc/runtime/loader.h); pointers are raw addresses of host buffers
   py::class_<flexmi::BatchRing>(m, "BatchRing")

@@ -5,7 +5,8 @@ partitions (``src/runtime/model.cc:457-875``) and the dependence analysis that i
 copies between producer and consumer partitions (``src/runtime/simulator.cc:295-326`` models
 exactly those intersection copies).  Here every cross-device byte is planned explicitly:
 a :class:`ReshardPlan` lists (src rank, dst rank, box) transfers that the executor runs as
-one RCCL ``all_to_all`` (``flexmi/parallel/comm.py``).
+one RCCL ``all_to_all`` (``flexmi/parallel/comm.py``).  The transfer planning itself (box
+intersections over all part pairs, holder choice, ordering) is C++: ``csrc/runtime/shard.cc``.
 
 Conventions:
   * ParallelConfig ``dims`` are kept in the reference's *internal* order (innermost first,
@@ -21,6 +22,21 @@ from dataclasses import dataclass, field
 from typing import List, Sequence, Tuple
 
 Box = Tuple[Tuple[int, int], ...]  # per dim [lo, hi)
+
+_NATIVE = None
+
+
+def _native():
+    """flexmi._native (C++ sharding algebra, strategy codec, simulator): always built by
+    tools/build_ext.py -- no Python fallback for the plan compiler's transfer planning."""
+    global _NATIVE
+    if _NATIVE is None:
+        try:
+            from flexmi import _native as mod
+        except ImportError as e:
+            raise RuntimeError("flexmi._native is not built: run `python tools/build_ext.py --only native`") from e
+        _NATIVE = mod
+    return _NATIVE
 
 
 @dataclass
@@ -175,6 +191,11 @@ class Layout:
         bx = None if self.boxes is None else tuple(self.boxes)
         return (self.shape, self.degrees, tuple(self.holders), self.partial, bx)
 
+    def native(self):
+        """The (shape, degrees, holders, boxes|None, partial) tuple of flexmi._native."""
+        bx = None if self.boxes is None else [list(b) for b in self.boxes]
+        return (list(self.shape), list(self.degrees), [list(h) for h in self.holders], bx, bool(self.partial))
+
     # --- constructors -------------------------------------------------
     @staticmethod
     def from_pc(shape, pc: ParallelConfig, replicate_over=None):
@@ -214,23 +235,11 @@ class ReshardPlan:
     def __init__(self, src: Layout, dst: Layout):
         assert src.shape == dst.shape, (src.shape, dst.shape)
         self.src, self.dst = src, dst
-        self.transfers: List[Transfer] = []
         self.reduce = src.partial and not dst.partial
-        for dp in range(dst.num_parts()):
-            dbox = dst.part_box(dp)
-            for sp in range(src.num_parts()):
-                inter = box_intersect(dbox, src.part_box(sp))
-                if inter is None:
-                    continue
-                sh = src.holders[sp]
-                for d in dst.holders[dp]:
-                    if self.reduce:
-                        for s in sh:  # every partial holder contributes
-                            self.transfers.append(Transfer(s, d, inter, sp, dp))
-                    else:
-                        s = d if d in sh else sh[(dp + sp) % len(sh)]
-                        self.transfers.append(Transfer(s, d, inter, sp, dp))
-        self.transfers.sort(key=lambda t: (t.src, t.dst, t.dst_part, t.src_part, t.box))
+        # box intersections + holder choice in C++ (csrc/runtime/shard.cc: reshard_transfers)
+        self.transfers: List[Transfer] = [
+            Transfer(s, d, tuple(tuple(r) for r in box), sp, dp)
+            for s, d, box, sp, dp in _native().reshard_transfers(src.native(), dst.native())]
 
     def is_identity(self):
         return all(t.src == t.dst for t in self.transfers) and not self.reduce_needed_local()

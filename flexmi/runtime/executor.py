@@ -353,16 +353,14 @@ class FusedExchange:
     def _launches(desc):
         """Split descriptors into launches in which no two pieces write intersecting boxes of
         the same buffer (pieces of one launch run concurrently; partial-sum pieces add)."""
-        out, cur = [], []
-        for d in desc:
-            clash = d[9] is not None and any(
-                e[2] is d[2] and e[9] is not None and box_intersect(e[9], d[9]) is not None for e in cur)
-            if clash or len(cur) == 32:
-                out.append(cur)
-                cur = []
-            cur.append(d)
-        if cur:
-            out.append(cur)
+        from flexmi.parallel.layout import _native
+        ids = {}
+        dst = [ids.setdefault(id(d[2]), len(ids)) for d in desc]
+        sizes = _native().split_launches(dst, [None if d[9] is None else [list(r) for r in d[9]] for d in desc], 32)
+        out, k = [], 0
+        for n in sizes:
+            out.append(desc[k:k + n])
+            k += n
         return out
 
     @staticmethod
