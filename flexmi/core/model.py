@@ -32,6 +32,44 @@ from flexmi.parallel.comm import Comm
 from flexmi.parallel.layout import ParallelConfig
 
 
+class DeferredOp:
+    """Functional "no-inout" op (``include/model.h:402-436``): built without its input
+    (``ff.dense(in_dim, out_dim)``, ``ff.relu()``, ``ff.add()`` ...), connected later with
+    ``init_inout(model, input)`` which creates the real op and returns its output tensor.
+    After binding, attribute access (``get_weight_tensor`` ...) goes to the real op."""
+
+    def __init__(self, model, builder, num_inputs=1, check=None, desc=""):
+        self._model = model
+        self._builder = builder
+        self._num_inputs = num_inputs
+        self._check = check
+        self._desc = desc
+        self.op = None
+
+    def init_inout(self, model, input):
+        assert self.op is None, f"{self._desc}: init_inout called twice"
+        ins = list(input) if isinstance(input, (list, tuple)) else [input]
+        assert len(ins) == self._num_inputs, f"{self._desc}: {self._num_inputs} input(s) expected, got {len(ins)}"
+        if self._check is not None:
+            self._check(*ins)
+        out = self._builder(*ins)
+        self.op = out.owner_op
+        return out
+
+    def __call__(self, *inputs):
+        return self.init_inout(self._model, list(inputs) if len(inputs) > 1 else inputs[0])
+
+    def __getattr__(self, name):
+        op = self.__dict__.get("op")
+        if op is None:
+            raise AttributeError(f"{self.__dict__.get('_desc', 'op')} is not connected yet (call init_inout): {name}")
+        return getattr(op, name)
+
+
+def _is_tensor(x):
+    return isinstance(x, Tensor)
+
+
 class FFModel:
     def __init__(self, ffconfig: FFConfig = None):
         self.config = ffconfig or FFConfig()
@@ -74,49 +112,91 @@ class FFModel:
         return None
 
     # ------------------------------------------------------------------ builders
-    def exp(self, x, name=None):
+    def exp(self, x=None, name=None):
+        if x is None:
+            return DeferredOp(self, lambda t: self.exp(t, name), 1, desc="exp")
         return self._add(ElementUnary(self, OperatorType.OP_EXP, x, name)).outputs[0]
 
-    def relu(self, x, name=None):
+    def relu(self, x=None, name=None):
+        if x is None:
+            return DeferredOp(self, lambda t: self.relu(t, name), 1, desc="relu")
         return self._add(ElementUnary(self, OperatorType.OP_RELU, x, name)).outputs[0]
 
-    def sigmoid(self, x, name=None):
+    def sigmoid(self, x=None, name=None):
+        if x is None:
+            return DeferredOp(self, lambda t: self.sigmoid(t, name), 1, desc="sigmoid")
         return self._add(ElementUnary(self, OperatorType.OP_SIGMOID, x, name)).outputs[0]
 
-    def tanh(self, x, name=None):
+    def tanh(self, x=None, name=None):
+        if x is None:
+            return DeferredOp(self, lambda t: self.tanh(t, name), 1, desc="tanh")
         return self._add(ElementUnary(self, OperatorType.OP_TANH, x, name)).outputs[0]
 
-    def elu(self, x, name=None):
+    def elu(self, x=None, name=None):
+        if x is None:
+            return DeferredOp(self, lambda t: self.elu(t, name), 1, desc="elu")
         return self._add(ElementUnary(self, OperatorType.OP_ELU, x, name)).outputs[0]
 
-    def add(self, x, y, name=None):
+    def add(self, x=None, y=None, name=None):
+        if x is None:
+            return DeferredOp(self, lambda a, b: self.add(a, b, name), 2, desc="add")
         return self._add(ElementBinary(self, OperatorType.OP_EW_ADD, x, y, name)).outputs[0]
 
-    def subtract(self, x, y, name=None):
+    def subtract(self, x=None, y=None, name=None):
+        if x is None:
+            return DeferredOp(self, lambda a, b: self.subtract(a, b, name), 2, desc="subtract")
         return self._add(ElementBinary(self, OperatorType.OP_EW_SUB, x, y, name)).outputs[0]
 
-    def multiply(self, x, y, name=None):
+    def multiply(self, x=None, y=None, name=None):
+        if x is None:
+            return DeferredOp(self, lambda a, b: self.multiply(a, b, name), 2, desc="multiply")
         return self._add(ElementBinary(self, OperatorType.OP_EW_MUL, x, y, name)).outputs[0]
 
-    def divide(self, x, y, name=None):
+    def divide(self, x=None, y=None, name=None):
+        if x is None:
+            return DeferredOp(self, lambda a, b: self.divide(a, b, name), 2, desc="divide")
         return self._add(ElementBinary(self, OperatorType.OP_EW_DIV, x, y, name)).outputs[0]
 
     def conv2d(self, input, out_channels, kernel_h, kernel_w, stride_h, stride_w, padding_h, padding_w,
                activation=ActiMode.AC_MODE_NONE, use_bias=True, shared_op=None, kernel_initializer=None,
                bias_initializer=None, name=None, groups=1):
+        if not _is_tensor(input):
+            # functional form conv2d(in_channels, out_channels, kh, kw, sh, sw, ph, pw, act, use_bias,
+            # kernel_init, bias_init) (include/model.h:411-420); shared_op slot = kernel_init here
+            in_c = int(input)
+            ki, bi = shared_op, kernel_initializer
+
+            def chk(t):
+                assert t.dims[1] == in_c, f"conv2d: input has {t.dims[1]} channels, op built for {in_c}"
+            return DeferredOp(self, lambda t: self.conv2d(t, out_channels, kernel_h, kernel_w, stride_h, stride_w,
+                                                          padding_h, padding_w, activation, use_bias, None, ki, bi,
+                                                          name, groups), 1, chk, "conv2d")
         op = Conv2D(self, input, out_channels, kernel_h, kernel_w, stride_h, stride_w, padding_h, padding_w,
                     activation, use_bias, kernel_initializer, bias_initializer, name, groups)
         self._share(op, shared_op)
         return self._add(op).outputs[0]
 
-    def embedding(self, input, num_entries, out_dim, aggr=AggrMode.AGGR_MODE_SUM, shared_op=None,
+    def embedding(self, input, num_entries, out_dim=None, aggr=AggrMode.AGGR_MODE_SUM, shared_op=None,
                   kernel_initializer=None, name=None):
+        if not _is_tensor(input):
+            # functional form embedding(num_entries, out_dim, aggr, kernel_init) (include/model.h:421-425)
+            n_e, d = int(input), int(num_entries)
+            ag = out_dim if out_dim is not None else AggrMode.AGGR_MODE_SUM
+            ki = aggr if not isinstance(aggr, (int, AggrMode)) else None
+            return DeferredOp(self, lambda t: self.embedding(t, n_e, d, ag, None, ki, name), 1, desc="embedding")
         op = Embedding(self, input, num_entries, out_dim, aggr, kernel_initializer, name)
         self._share(op, shared_op)
         return self._add(op).outputs[0]
 
-    def pool2d(self, input, kernel_h, kernel_w, stride_h, stride_w, padding_h, padding_w,
+    def pool2d(self, input, kernel_h, kernel_w, stride_h, stride_w, padding_h, padding_w=None,
                pool_type=PoolType.POOL_MAX, activation=ActiMode.AC_MODE_NONE, name=None):
+        if not _is_tensor(input):
+            # functional form pool2d(kh, kw, sh, sw, ph, pw, type, act) (include/model.h:426-431)
+            args = (input, kernel_h, kernel_w, stride_h, stride_w, padding_h)
+            pt = padding_w if padding_w is not None else PoolType.POOL_MAX
+            ac = pool_type if pool_type in (ActiMode.AC_MODE_NONE, ActiMode.AC_MODE_RELU,
+                                            ActiMode.AC_MODE_SIGMOID, ActiMode.AC_MODE_TANH) else ActiMode.AC_MODE_NONE
+            return DeferredOp(self, lambda t: self.pool2d(t, *args, pt, ac, name), 1, desc="pool2d")
         return self._add(Pool2D(self, input, kernel_h, kernel_w, stride_h, stride_w, padding_h, padding_w,
                                 pool_type, activation, name)).outputs[0]
 
@@ -128,6 +208,16 @@ class FFModel:
 
     def dense(self, input, out_dim, activation=ActiMode.AC_MODE_NONE, use_bias=True, shared_op=None,
               kernel_initializer=None, bias_initializer=None, name=None):
+        if not _is_tensor(input):
+            # functional form dense(in_dim, out_dim, act, use_bias, kernel_init, bias_init)
+            # (include/model.h:432-436: no shared_op slot -> the 5th/6th args are the initialisers)
+            in_dim = int(input)
+            ki, bi = shared_op, kernel_initializer
+
+            def chk(t):
+                assert t.dims[-1] == in_dim, f"dense: input has {t.dims[-1]} features, op built for {in_dim}"
+            return DeferredOp(self, lambda t: self.dense(t, out_dim, activation, use_bias, None, ki, bi, name), 1, chk,
+                              "dense")
         op = Linear(self, input, out_dim, activation, use_bias, kernel_initializer, bias_initializer, name)
         self._share(op, shared_op)
         return self._add(op).outputs[0]
@@ -138,7 +228,9 @@ class FFModel:
     def split(self, input, sizes, axis, name=None):
         return list(self._add(Split(self, input, sizes, axis, name)).outputs)
 
-    def flat(self, input, name=None):
+    def flat(self, input=None, name=None):
+        if input is None:
+            return DeferredOp(self, lambda t: self.flat(t, name), 1, desc="flat")
         return self._add(Flat(self, input, name)).outputs[0]
 
     def softmax(self, input, name=None):

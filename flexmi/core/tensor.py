@@ -91,7 +91,32 @@ class Tensor:
 
     def detach_numpy_array(self, ffconfig=None):
         # the loaders keep their own reference; dropping ours mirrors detach_raw_ptr
-        pass
+        self._attached = None
+
+    def get_raw_ptr(self, ffmodel=None, ffconfig=None):
+        """Device address of this rank's shard buffer (``Tensor::get_raw_ptr``,
+        ``src/runtime/model.cc:46-71``: the reference returned the pointer of the mapped
+        region; flexmi shards are plain HIP allocations owned by the executor)."""
+        buf = self._executor(ffmodel).local_buffer(self)
+        return 0 if buf is None else int(buf.data_ptr())
+
+    def attach_raw_ptr(self, ffmodel, raw_ptr, column_major=False):
+        """Zero-copy attach of host memory at ``raw_ptr`` holding the whole logical tensor
+        (``Tensor::attach_raw_ptr``, ``src/runtime/model.cc:73-86``).  column_major=True means
+        the array is stored with the reference's internal (reversed) dim order."""
+        import ctypes
+        dt = np.dtype(torch.empty(0, dtype=self.torch_dtype).numpy().dtype)
+        n = self.volume()
+        buf = (ctypes.c_char * (n * dt.itemsize)).from_address(int(raw_ptr))
+        arr = np.frombuffer(buf, dtype=dt, count=n)
+        arr = arr.reshape(self.adim).transpose() if column_major else arr.reshape(self.dims)
+        self._attached = torch.from_numpy(np.ascontiguousarray(arr) if column_major else arr)
+        self._raw_ptr = int(raw_ptr)
+        return self._attached
+
+    def detach_raw_ptr(self, ffmodel=None, ffconfig=None):
+        self._attached = None
+        self._raw_ptr = None
 
     def get_owner_op(self):
         return self.owner_op
