@@ -17,7 +17,7 @@
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 
-#include <chrono>
+#include <algorithm>
 #include <cstdint>
 #include <stdexcept>
 #include <string>
@@ -61,6 +61,12 @@ struct Step {
                                                    hipGetErrorString(e_));                     \
   } while (0)
 
+// A C++-owned alias (new TensorImpl over the same storage, no Python object attached) of a
+// tensor handed in from Python.  The collectives' works capture these, so the backend threads
+// that drop the last reference to a finished work never need the GIL -- which they cannot take
+// once the interpreter is shutting down.
+at::Tensor c_alias(const at::Tensor& t) { return at::alias(t); }
+
 class StepRunner {
  public:
   int new_program() {
@@ -69,6 +75,7 @@ class StepRunner {
   }
   int new_slot() {
     slots_.emplace_back();
+    pending_.push_back(false);
     return (int)slots_.size() - 1;
   }
   int num_programs() const { return (int)progs_.size(); }
@@ -103,8 +110,8 @@ class StepRunner {
     s.kind = A2A_START;
     s.slot = slot;
     s.pg = std::move(pg);
-    s.a = std::move(recv);
-    s.b = std::move(send);
+    s.a = c_alias(recv);
+    s.b = c_alias(send);
     s.sa = std::move(recv_splits);
     s.sb = std::move(send_splits);
     s.name = name;
@@ -116,7 +123,7 @@ class StepRunner {
     s.kind = sync ? AR_SYNC : AR_START;
     s.slot = slot;
     s.pg = std::move(pg);
-    s.a = std::move(t);
+    s.a = c_alias(t);
     s.name = name;
     prog(p).push_back(std::move(s));
   }
@@ -131,6 +138,7 @@ class StepRunner {
 
   // Execute program p in order.  The GIL is held only while a Python callable runs.
   void run(int p) {
+    if (released_) throw std::runtime_error("StepRunner: released (process group torn down)");
     auto& steps = prog(p);
     for (size_t i = 0; i < steps.size(); ++i) {
       Step& s = steps[i];
@@ -149,7 +157,17 @@ class StepRunner {
   // drop every pending Work handle (after an error / before tear-down)
   void reset_slots() {
     for (auto& w : slots_) w.reset();
+    std::fill(pending_.begin(), pending_.end(), false);
   }
+
+  // drop every reference the programs hold (process groups, tensors, callables): a c10d process
+  // group must not outlive the interpreter state it was created in
+  void release() {
+    reset_slots();
+    for (auto& p : progs_) p.clear();
+    released_ = true;
+  }
+  bool released() const { return released_; }
 
   py::dict stats() const {
     py::dict d;
@@ -185,6 +203,23 @@ class StepRunner {
     if (slot < 0 || slot >= (int)slots_.size()) throw std::out_of_range("StepRunner: bad slot id");
   }
 
+  // A finished Work stays in its slot until the slot is reused (or released): the backend's
+  // worker thread drops its own reference right after completing the work, so the LAST reference
+  // -- and with it the tensors the work captured -- is released on this thread, never on a
+  // backend thread racing interpreter shutdown.
+  void start(int slot, WorkPtr w) {
+    if (pending_[slot]) slots_[slot]->wait();
+    slots_[slot] = std::move(w);
+    pending_[slot] = true;
+    ++collectives_;
+  }
+  void finish(int slot) {
+    if (!pending_[slot]) return;
+    slots_[slot]->wait();
+    pending_[slot] = false;
+    ++waits_;
+  }
+
   void exec_native(Step& s) {
     switch (s.kind) {
       case GRAPH: {
@@ -194,41 +229,31 @@ class StepRunner {
         break;
       }
       case A2A_START: {
-        if (slots_[s.slot]) slots_[s.slot]->wait();
+        if (pending_[s.slot]) finish(s.slot);
         c10d::AllToAllOptions o;
-        slots_[s.slot] = s.pg->alltoall_base(s.a, s.b, s.sa, s.sb, o);
-        ++collectives_;
+        start(s.slot, s.pg->alltoall_base(s.a, s.b, s.sa, s.sb, o));
         bytes_sent_ += s.b.numel() * s.b.element_size();
         break;
       }
       case AR_START: {
-        if (slots_[s.slot]) slots_[s.slot]->wait();
+        if (pending_[s.slot]) finish(s.slot);
         std::vector<at::Tensor> v{s.a};
-        slots_[s.slot] = s.pg->allreduce(v);
-        ++collectives_;
+        start(s.slot, s.pg->allreduce(v));
         bytes_sent_ += s.a.numel() * s.a.element_size();
         break;
       }
       case AR_SYNC: {
-        if (!slots_[s.slot]) {
+        if (!pending_[s.slot]) {
           std::vector<at::Tensor> v{s.a};
-          slots_[s.slot] = s.pg->allreduce(v);
-          ++collectives_;
+          start(s.slot, s.pg->allreduce(v));
           bytes_sent_ += s.a.numel() * s.a.element_size();
         }
-        slots_[s.slot]->wait();
-        slots_[s.slot].reset();
-        ++waits_;
+        finish(s.slot);
         break;
       }
-      case WAIT: {
-        if (slots_[s.slot]) {
-          slots_[s.slot]->wait();
-          slots_[s.slot].reset();
-          ++waits_;
-        }
+      case WAIT:
+        finish(s.slot);
         break;
-      }
       default:
         throw std::logic_error("StepRunner: unknown step kind");
     }
@@ -236,7 +261,9 @@ class StepRunner {
 
   std::vector<std::vector<Step>> progs_;
   std::vector<WorkPtr> slots_;
+  std::vector<bool> pending_;
   int current_ = -1;
+  bool released_ = false;
   int64_t runs_ = 0, collectives_ = 0, bytes_sent_ = 0, graph_launches_ = 0, waits_ = 0;
 };
 
@@ -259,6 +286,8 @@ PYBIND11_MODULE(_rt, m) {
       .def("add_wait", &StepRunner::add_wait, py::arg("program"), py::arg("slot"), py::arg("name") = "")
       .def("run", &StepRunner::run)
       .def("reset_slots", &StepRunner::reset_slots)
+      .def("release", &StepRunner::release)
+      .def_property_readonly("released", &StepRunner::released)
       .def("stats", &StepRunner::stats)
       .def("current_name", &StepRunner::current_name)
       .def("describe", &StepRunner::describe)

@@ -172,6 +172,42 @@ def _rt_module():
         return None
 
 
+_LIVE_RUNNERS = None
+
+
+def release_native_runners():
+    """Drop the native runners' references to c10d process groups, tensors and callables.  Runs
+    before ``torch.distributed.destroy_process_group`` (hooked) and at exit: a group must be
+    destroyed while every rank is still alive -- one whose last reference goes away during
+    interpreter shutdown, after the peer ranks (and the TCP store host) have exited, aborts."""
+    for r in list(_LIVE_RUNNERS or ()):
+        r.rt.release()
+
+
+def _hook_destroy_process_group():
+    import torch.distributed as dist
+    orig = dist.destroy_process_group
+    if getattr(orig, "_flexmi_hook", False):
+        return
+
+    def destroy_process_group(group=None):
+        if group is None:
+            # a last barrier (its work captures no Python-owned tensor) lets the backend's worker
+            # threads drop every earlier work -- and the Python tensors those captured -- before
+            # the group goes away; then the runners' own references are released
+            try:
+                if dist.is_initialized() and dist.get_world_size() > 1:
+                    dist.barrier()
+            except Exception:
+                pass
+            release_native_runners()
+            return orig()
+        return orig(group)
+    destroy_process_group._flexmi_hook = True
+    destroy_process_group.__doc__ = orig.__doc__
+    dist.destroy_process_group = destroy_process_group
+
+
 class NativeRunner:
     """Compiles item lists into programs of the native step runner (``csrc/runtime/step_runner.cc``):
     compute items stay callables (or, once captured, hipGraph launches), comm items become c10d
@@ -186,6 +222,14 @@ class NativeRunner:
         self.slots = {}
         self.pids = {}
         self.keep = []          # Python objects referenced by native steps (graphs, callables)
+        global _LIVE_RUNNERS
+        if _LIVE_RUNNERS is None:
+            import atexit
+            import weakref
+            _LIVE_RUNNERS = weakref.WeakSet()
+            atexit.register(release_native_runners)
+            _hook_destroy_process_group()
+        _LIVE_RUNNERS.add(self)
 
     def slot(self, key):
         s = self.slots.get(key)

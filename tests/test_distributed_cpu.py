@@ -161,6 +161,8 @@ def test_strategy_equivalence(case, world):
         import flexmi._rt  # noqa: F401
     except ImportError:
         return
+    if os.environ.get("FLEXMI_NATIVE_RUNNER", "1") == "0":
+        return
     # the steps ran through the native runner (flexmi._rt): its collectives were issued from C++
     assert int(got["native_colls"]) >= 0, "world>1 training did not go through the native step runner"
     if case != "dlrm_search":   # a searched strategy may need no collective at all
