@@ -19,17 +19,17 @@ void fm_skinny_bwd(const void* x, long ldx, const void* w, const void* y, long l
                    long lddx, int dx_acc, float* dw, float* db, long B, int K, int act, hipStream_t s);
 void fm_init_fill(float* out, long rows, long cols, long r0, long c0, long ldg, int kind, unsigned seed, float a, float b,
                   hipStream_t s);
-void fm_embedding_fwd(const void* idx, int idx64, const float* W, void* out, int out_bf16, long B, int bag, int D, long ldo,
-                      float scale, hipStream_t s);
+void fm_embedding_fwd(const void* idx, int idx64, const float* W, void* out, int out_bf16, long B, int bag, int rows, int D,
+                      long ldo, float scale, hipStream_t s);
 void fm_embedding_bwd(const void* idx, int idx64, const void* dy, int dy_bf16, float* W, const float* lr, long B, int bag,
                       int rows, int D, long ldg, float scale, hipStream_t s);
 void fm_embedding_fwd_multi(int n, const float* const* W, const void* const* idx, const int* idx64, void* const* out,
-                            const long* ldo, const int* rows, const int* D, const int* bag, const float* scale, int out_bf16,
-                            long B, hipStream_t st);
+                            const long* ldo, const long* lo, const int* rows, const int* D, const int* bag,
+                            const float* scale, int out_bf16, long B, hipStream_t st);
 void fm_embedding_bwd_multi(int n, float* const* W, const void* const* idx, const int* idx64, const void* const* dy,
-                            const long* ldg, const int* rows, const int* D, const int* bag, const float* scale, int dy_bf16,
-                            const float* lr, long B, int* const* owner, int* const* dups, int* const* ndup,
-                            hipStream_t st);
+                            const long* ldg, const long* lo, const int* rows, const int* D, const int* bag,
+                            const float* scale, int dy_bf16, const float* lr, long B, int* const* owner,
+                            int* const* dups, int* const* ndup, hipStream_t st);
 void fm_dot_interaction_fwd(const void* const* z, int F, long ldz, void* out, long ldo, long B, int D, int W, int self,
                             hipStream_t s);
 void fm_dot_interaction_bwd(const void* const* z, int F, long ldz, const void* dout, long ldo, void* const* dz, long lddz,
@@ -171,7 +171,7 @@ void embedding_fwd(torch::Tensor idx, torch::Tensor W, torch::Tensor out, int64_
   int D = W.size(1);
   TORCH_CHECK(out.numel() >= (B - 1) * ldo + D, "embedding out too small");
   fm_embedding_fwd(idx.data_ptr(), idx.scalar_type() == torch::kInt64, W.data_ptr<float>(), out.data_ptr(), is_bf16(out), B,
-                   bag, D, ldo, (float)scale, cur());
+                   bag, (int)W.size(0), D, ldo, (float)scale, cur());
 }
 
 void embedding_bwd(torch::Tensor idx, torch::Tensor dy, int64_t ldg, torch::Tensor W, c10::optional<torch::Tensor> lr,
@@ -229,21 +229,31 @@ TabArgs tab_args(const std::vector<torch::Tensor>& W, const std::vector<torch::T
   return a;
 }
 
+// row_lo: first global row of each (row-sharded) table; empty = whole tables
+std::vector<long> row_offsets(const std::vector<int64_t>& row_lo, size_t n) {
+  TORCH_CHECK(row_lo.empty() || row_lo.size() == n, "embedding multi: one row offset per table");
+  std::vector<long> lo(n, 0);
+  for (size_t i = 0; i < row_lo.size(); ++i) lo[i] = (long)row_lo[i];
+  return lo;
+}
+
 void embedding_fwd_multi(std::vector<torch::Tensor> W, std::vector<torch::Tensor> idx, std::vector<torch::Tensor> out,
-                         std::vector<int64_t> ldo, std::vector<double> scale) {
+                         std::vector<int64_t> ldo, std::vector<double> scale, std::vector<int64_t> row_lo) {
   if (W.empty()) return;
   TabArgs a = tab_args(W, idx, out, ldo, scale);
-  fm_embedding_fwd_multi((int)W.size(), a.Wc.data(), a.idx.data(), a.idx64.data(), a.act.data(), a.ld.data(), a.rows.data(),
-                         a.D.data(), a.bag.data(), a.scale.data(), is_bf16(out[0]), a.B, cur());
+  std::vector<long> lo = row_offsets(row_lo, W.size());
+  fm_embedding_fwd_multi((int)W.size(), a.Wc.data(), a.idx.data(), a.idx64.data(), a.act.data(), a.ld.data(), lo.data(),
+                         a.rows.data(), a.D.data(), a.bag.data(), a.scale.data(), is_bf16(out[0]), a.B, cur());
 }
 
 // claim: optional per-table [owner (int32 [rows], -1 filled), dups (int32 [B*bag]), ndup (int32 [1])]
 // triples (owner-computes sparse SGD for mostly-unique tables); None entries use the atomic path
 void embedding_bwd_multi(std::vector<torch::Tensor> W, std::vector<torch::Tensor> idx, std::vector<torch::Tensor> dy,
                          std::vector<int64_t> ldg, std::vector<double> scale, c10::optional<torch::Tensor> lr,
-                         c10::optional<std::vector<c10::optional<torch::Tensor>>> claim) {
+                         c10::optional<std::vector<c10::optional<torch::Tensor>>> claim, std::vector<int64_t> row_lo) {
   if (W.empty()) return;
   TabArgs a = tab_args(W, idx, dy, ldg, scale);
+  std::vector<long> lo = row_offsets(row_lo, W.size());
   std::vector<int*> own(W.size(), nullptr), dup(W.size(), nullptr), nd(W.size(), nullptr);
   bool any = false;
   if (claim.has_value()) {
@@ -262,8 +272,8 @@ void embedding_bwd_multi(std::vector<torch::Tensor> W, std::vector<torch::Tensor
       any = true;
     }
   }
-  fm_embedding_bwd_multi((int)W.size(), a.Wm.data(), a.idx.data(), a.idx64.data(), a.cact.data(), a.ld.data(), a.rows.data(),
-                         a.D.data(), a.bag.data(), a.scale.data(), is_bf16(dy[0]),
+  fm_embedding_bwd_multi((int)W.size(), a.Wm.data(), a.idx.data(), a.idx64.data(), a.cact.data(), a.ld.data(), lo.data(),
+                         a.rows.data(), a.D.data(), a.bag.data(), a.scale.data(), is_bf16(dy[0]),
                          lr.has_value() && lr->defined() ? lr->data_ptr<float>() : nullptr, a.B,
                          any ? own.data() : nullptr, any ? dup.data() : nullptr, any ? nd.data() : nullptr, cur());
 }
@@ -490,8 +500,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("skinny_bwd", &skinny_bwd);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
-  m.def("embedding_fwd_multi", &embedding_fwd_multi);
-  m.def("embedding_bwd_multi", &embedding_bwd_multi);
+  m.def("embedding_fwd_multi", &embedding_fwd_multi, py::arg("W"), py::arg("idx"), py::arg("out"), py::arg("ldo"),
+        py::arg("scale"), py::arg("row_lo") = std::vector<int64_t>{});
+  m.def("embedding_bwd_multi", &embedding_bwd_multi, py::arg("W"), py::arg("idx"), py::arg("dy"), py::arg("ldg"),
+        py::arg("scale"), py::arg("lr"), py::arg("claim"), py::arg("row_lo") = std::vector<int64_t>{});
   m.def("dot_fwd", &dot_fwd);
   m.def("dot_bwd", &dot_bwd);
   m.def("sgd", &sgd);

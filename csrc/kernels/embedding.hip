@@ -30,14 +30,27 @@ namespace {
 constexpr int MAXT = 32;
 constexpr int TINY_ROWS = 16;
 
+// Row-sharded tables (SOAP row split of the embedding weight): a shard holds the global rows
+// [lo, lo + rows); lookups outside it contribute nothing here (their partial sums come from the
+// shards that hold them).  Whole tables have lo = 0, and out-of-range indices are dropped, never
+// read or written out of bounds.  The range test is a select AFTER an unconditional (clamped)
+// load, so the hot loops keep their branch-free loads.
 struct TabDesc {
   const float* W;     // fwd: table (read); bwd: table or dense grad (written)
   const void* idx;    // [B, bag] int32/int64
   void* act;          // fwd: out [B, *] (row stride ld); bwd: dy
   long ld;
-  int rows, D, bag;
+  long lo;            // first global row held by this shard
+  int rows, D, bag;   // rows: rows held by this shard
   float scale;
 };
+
+// local row of a lookup, clamped into the shard (ok = the shard holds it)
+FM_DEVICE long local_row(long r, long lo, int rows, bool& ok) {
+  const long l = r - lo;
+  ok = (unsigned long)l < (unsigned long)rows;
+  return ok ? l : 0;
+}
 struct TabSet {
   TabDesc t[MAXT];
   int n;
@@ -62,8 +75,10 @@ __global__ void __launch_bounds__(256) fm_emb_fwd_multi(TabSet s, long B) {
       const int c = c4 * 4;
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
       for (int j = 0; j < d.bag; ++j) {
-        long r = ldi<I64>(d.idx, b * d.bag + j);
-        acc += *reinterpret_cast<const f32x4_t*>(d.W + r * d.D + c);
+        bool ok;
+        const long r = local_row(ldi<I64>(d.idx, b * d.bag + j), d.lo, d.rows, ok);
+        const f32x4_t v = *reinterpret_cast<const f32x4_t*>(d.W + r * d.D + c);
+        if (ok) acc += v;
       }
       acc *= d.scale;
       OutT* o = reinterpret_cast<OutT*>(d.act) + b * d.ld + c;
@@ -89,7 +104,12 @@ __global__ void __launch_bounds__(256) fm_emb_fwd_multi_scalar(TabSet s, long B)
   for (long b = (long)blockIdx.x * rpi + sub; b < B; b += (long)gridDim.x * rpi)
     for (int c = lc; c < d.D; c += lpr) {
       float acc = 0.f;
-      for (int j = 0; j < d.bag; ++j) acc += d.W[ldi<I64>(d.idx, b * d.bag + j) * d.D + c];
+      for (int j = 0; j < d.bag; ++j) {
+        bool ok;
+        const long r = local_row(ldi<I64>(d.idx, b * d.bag + j), d.lo, d.rows, ok);
+        const float v = d.W[r * d.D + c];
+        if (ok) acc += v;
+      }
       st<OutT>(reinterpret_cast<OutT*>(d.act) + b * d.ld + c, acc * d.scale);
     }
 }
@@ -105,11 +125,16 @@ __global__ void __launch_bounds__(256) fm_emb_bwd_atomic_multi(TabSet s, const f
   float* W = const_cast<float*>(d.W);
   const GT* dy = reinterpret_cast<const GT*>(d.act);
   for (long b = (long)blockIdx.x * rpi + sub; b < B; b += (long)gridDim.x * rpi) {
-    const long r0 = ldi<I64>(d.idx, b * d.bag);
+    bool ok0;
+    const long r0 = local_row(ldi<I64>(d.idx, b * d.bag), d.lo, d.rows, ok0);
     for (int c = lc; c < d.D; c += lpr) {
       const float g = ld<GT>(dy + b * d.ld + c) * mul;
-      atomicAdd(W + r0 * d.D + c, g);
-      for (int j = 1; j < d.bag; ++j) atomicAdd(W + ldi<I64>(d.idx, b * d.bag + j) * d.D + c, g);
+      if (ok0) atomicAdd(W + r0 * d.D + c, g);
+      for (int j = 1; j < d.bag; ++j) {
+        bool ok;
+        const long r = local_row(ldi<I64>(d.idx, b * d.bag + j), d.lo, d.rows, ok);
+        if (ok) atomicAdd(W + r * d.D + c, g);
+      }
     }
   }
 }
@@ -133,11 +158,12 @@ __global__ void __launch_bounds__(256) fm_emb_bwd_tiny_multi(TabSet s, const flo
       const int ca = c0 + lane, cb = c0 + 64 + lane;
       const int sa = min(ca, d.D - 1), sb = min(cb, d.D - 1);   // clamped: loads stay unconditional
       long r[S];
+      bool rok[S];
       float ga[S], gb[S];
 #pragma unroll
       for (int u = 0; u < S; ++u) {
         const long bu = min(bw + u, b1 - 1);
-        r[u] = ldi<I64>(d.idx, bu * d.bag);
+        r[u] = local_row(ldi<I64>(d.idx, bu * d.bag), d.lo, d.rows, rok[u]);
         ga[u] = ld<GT>(dy + bu * d.ld + sa);
         gb[u] = ld<GT>(dy + bu * d.ld + sb);
       }
@@ -145,12 +171,13 @@ __global__ void __launch_bounds__(256) fm_emb_bwd_tiny_multi(TabSet s, const flo
       for (int u = 0; u < S; ++u) {
         if (bw + u >= b1) break;                       // wave-uniform
         float* p = mine + r[u] * d.D;
-        if (ca < d.D) p[ca] += ga[u];
-        if (cb < d.D) p[cb] += gb[u];
+        if (rok[u] && ca < d.D) p[ca] += ga[u];
+        if (rok[u] && cb < d.D) p[cb] += gb[u];
         for (int j = 1; j < d.bag; ++j) {              // further bag entries share the gradient row
-          float* q = mine + ldi<I64>(d.idx, (bw + u) * d.bag + j) * d.D;
-          if (ca < d.D) q[ca] += ga[u];
-          if (cb < d.D) q[cb] += gb[u];
+          bool ok;
+          float* q = mine + local_row(ldi<I64>(d.idx, (bw + u) * d.bag + j), d.lo, d.rows, ok) * d.D;
+          if (ok && ca < d.D) q[ca] += ga[u];
+          if (ok && cb < d.D) q[cb] += gb[u];
         }
       }
     }
@@ -188,7 +215,8 @@ struct ClaimDesc {
   const void* idx;
   const void* dy;
   long ld;
-  int D, bag;
+  long lo;
+  int rows, D, bag;
   float scale;
   int* owner;   // [rows] int32, -1 = free (restored by the owner kernel)
   int* dups;    // [B*bag]
@@ -204,7 +232,9 @@ __global__ void __launch_bounds__(256) fm_emb_claim_multi(ClaimSet s, long B) {
   const ClaimDesc& d = s.t[blockIdx.y];
   const long n = B * d.bag;
   for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
-    const long r = ldi<I64>(d.idx, e);
+    bool ok;
+    const long r = local_row(ldi<I64>(d.idx, e), d.lo, d.rows, ok);
+    if (!ok) continue;                               // row held by another shard
     const int prev = atomicCAS(d.owner + r, -1, (int)e);
     if (prev != -1) d.dups[atomicAdd(d.ndup, 1)] = (int)e;
   }
@@ -219,7 +249,7 @@ __global__ void __launch_bounds__(256) fm_emb_dup_multi(ClaimSet s, const float*
   const GT* dy = reinterpret_cast<const GT*>(d.dy);
   for (long k = blockIdx.x * 4L + wave; k < nd; k += (long)gridDim.x * 4) {
     const long e = d.dups[k];
-    const long b = e / d.bag, r = ldi<I64>(d.idx, e);
+    const long b = e / d.bag, r = ldi<I64>(d.idx, e) - d.lo;   // dups hold in-shard entries only
     for (int c = lane; c < d.D; c += 64) atomicAdd(d.W + r * d.D + c, ld<GT>(dy + b * d.ld + c) * mul);
   }
 }
@@ -236,8 +266,9 @@ __global__ void __launch_bounds__(256) fm_emb_owner_multi(ClaimSet s, const floa
   const GT* dy = reinterpret_cast<const GT*>(d.dy);
   if (sub < rpi) {
     for (long e = (long)blockIdx.x * rpi + sub; e < n; e += (long)gridDim.x * rpi) {
-      const long r = ldi<I64>(d.idx, e);
-      if (d.owner[r] != (int)e) continue;          // uniform across the row's lanes
+      bool ok;
+      const long r = local_row(ldi<I64>(d.idx, e), d.lo, d.rows, ok);
+      if (!ok || d.owner[r] != (int)e) continue;   // uniform across the row's lanes
       const long b = e / d.bag;
       for (int c4 = lc; c4 < D4; c4 += lpr) {
         const int c = c4 * 4;
@@ -300,9 +331,10 @@ void launch_bwd(const TabSet& s, int m, bool tiny, bool dy_bf16, const float* lr
 // ------------------------------------------------------------------------------------------
 // Launchers.  Arrays describe n tables; act/ld = outputs (fwd) or output grads (bwd).  Tables
 // are batched by index width (and, in backward, by kernel kind) into launches of <= 32 tables.
+// lo: first global row of each table shard (nullptr = whole tables); rows: rows held
 extern "C" void fm_embedding_fwd_multi(int n, const float* const* W, const void* const* idx, const int* idx64,
-                                       void* const* out, const long* ldo, const int* rows, const int* D, const int* bag,
-                                       const float* scale, int out_bf16, long B, hipStream_t st) {
+                                       void* const* out, const long* ldo, const long* lo, const int* rows, const int* D,
+                                       const int* bag, const float* scale, int out_bf16, long B, hipStream_t st) {
   if (B <= 0) return;
   for (int wide = 0; wide < 2; ++wide) {
     std::vector<int> sel;
@@ -314,7 +346,7 @@ extern "C" void fm_embedding_fwd_multi(int n, const float* const* W, const void*
       bool vec = true;
       for (int i = 0; i < m; ++i) {
         int k = sel[base + i];
-        s.t[i] = TabDesc{W[k], idx[k], out[k], ldo[k], rows[k], D[k], bag[k], scale[k]};
+        s.t[i] = TabDesc{W[k], idx[k], out[k], ldo[k], lo ? lo[k] : 0, rows[k], D[k], bag[k], scale[k]};
         vec = vec && (D[k] % 4 == 0) && (ldo[k] % 4 == 0) && D[k] <= 256;
       }
       s.n = m;
@@ -326,7 +358,7 @@ extern "C" void fm_embedding_fwd_multi(int n, const float* const* W, const void*
 
 // lr != nullptr: fused sparse SGD into W; lr == nullptr: W is a dense grad buffer (accumulate).
 extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const* idx, const int* idx64,
-                                       const void* const* dy, const long* ldg, const int* rows, const int* D,
+                                       const void* const* dy, const long* ldg, const long* lo, const int* rows, const int* D,
                                        const int* bag, const float* scale, int dy_bf16, const float* lr, long B,
                                        int* const* owner, int* const* dups, int* const* ndup, hipStream_t st) {
   if (B <= 0) return;
@@ -345,7 +377,8 @@ extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const
       int maxbag = 1, minD4 = 64;
       for (int i = 0; i < m; ++i) {
         int k = sel[base + i];
-        s.t[i] = ClaimDesc{W[k], idx[k], dy[k], ldg[k], D[k], bag[k], scale[k], owner[k], dups[k], ndup[k]};
+        s.t[i] = ClaimDesc{W[k], idx[k], dy[k], ldg[k], lo ? lo[k] : 0, rows[k], D[k], bag[k], scale[k], owner[k], dups[k],
+                           ndup[k]};
         maxbag = std::max(maxbag, bag[k]);
         minD4 = std::min(minD4, D[k] / 4);
       }
@@ -368,7 +401,7 @@ extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const
       int maxD = 1;
       for (int i = 0; i < m; ++i) {
         int k = sel[base + i];
-        s.t[i] = TabDesc{W[k], idx[k], const_cast<void*>(dy[k]), ldg[k], rows[k], D[k], bag[k], scale[k]};
+        s.t[i] = TabDesc{W[k], idx[k], const_cast<void*>(dy[k]), ldg[k], lo ? lo[k] : 0, rows[k], D[k], bag[k], scale[k]};
         maxD = std::max(maxD, D[k]);
       }
       s.n = m;
@@ -380,13 +413,12 @@ extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const
 
 // single-table conveniences
 extern "C" void fm_embedding_fwd(const void* idx, int idx64, const float* W, void* out, int out_bf16, long B, int bag,
-                                 int D, long ldo, float scale, hipStream_t s) {
-  int rows = 0;
-  fm_embedding_fwd_multi(1, &W, &idx, &idx64, &out, &ldo, &rows, &D, &bag, &scale, out_bf16, B, s);
+                                 int rows, int D, long ldo, float scale, hipStream_t s) {
+  fm_embedding_fwd_multi(1, &W, &idx, &idx64, &out, &ldo, nullptr, &rows, &D, &bag, &scale, out_bf16, B, s);
 }
 
 extern "C" void fm_embedding_bwd(const void* idx, int idx64, const void* dy, int dy_bf16, float* W, const float* lr,
                                  long B, int bag, int rows, int D, long ldg, float scale, hipStream_t s) {
-  fm_embedding_bwd_multi(1, &W, &idx, &idx64, &dy, &ldg, &rows, &D, &bag, &scale, dy_bf16, lr, B, nullptr, nullptr,
-                         nullptr, s);
+  fm_embedding_bwd_multi(1, &W, &idx, &idx64, &dy, &ldg, nullptr, &rows, &D, &bag, &scale, dy_bf16, lr, B, nullptr,
+                         nullptr, nullptr, s);
 }

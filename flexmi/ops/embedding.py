@@ -11,8 +11,13 @@ table).  The backward never materialises a dense gradient for SGD: rows are upda
 (W[idx] -= lr*dy).  Mostly-unique (large) tables use owner-computes: each row is claimed by one
 lookup (CAS), duplicates add with atomics, the owner applies a plain 16-B read-modify-write;
 other tables use 256-B-contiguous fp32 atomics; tiny tables accumulate in LDS first.
-SOAP: sample split, **column (parameter) split** of the table and whole-table placement
-(``dims=[1,1]``, device k) -- a 100 M-row table fits one MI355X's 288 GB of HBM.
+SOAP: sample split, **column (parameter) split** of the table, whole-table placement
+(``dims=[1,1]``, device k) -- a 100 M-row table fits one MI355X's 288 GB of HBM -- and **row
+split** (flexmi extension of the strategy format: a third internal degree, ``dims=[c, n, r]``):
+each of r shards holds a contiguous block of rows, looks up only the indices it holds and emits
+a PARTIAL output; the consumer's reshard sums the r partials (one all_to_all with add), and in
+backward every shard receives the full output gradient and updates only its own rows.  Row
+shards split tables too big for one GPU and spread a hot table's lookups over several GPUs.
 """
 from __future__ import annotations
 
@@ -52,17 +57,56 @@ class Embedding(Op):
     def splittable_dims(self):
         return {0, 1}
 
+    @staticmethod
+    def _grid(pc):
+        """(n, c, r, dev): sample / column / row degrees and the device of part (i, j, k); the
+        internal dims are [c, n] or [c, n, r] (internal dim 0 fastest in the device list)."""
+        d = list(pc.dims) + [1] * (3 - len(pc.dims))
+        c, n, r = int(d[0]), int(d[1]), int(d[2])
+        ids = pc.device_ids
+
+        def dev(i, j, k):
+            return ids[j + c * (i + n * k)]
+        return n, c, r, dev
+
+    def valid_pc(self, pc):
+        if len(pc.dims) <= 2:
+            return super().valid_pc(pc)
+        if len(pc.dims) != 3 or len(pc.device_ids) != pc.num_parts() or min(pc.device_ids) < 0:
+            return False
+        n, c, r, _ = self._grid(pc)
+        B, D = self.outputs[0].dims
+        # a rank holds at most one part of each layout: row shards on distinct devices
+        return (n <= B and c <= D and r <= self.num_entries and len(set(pc.device_ids)) == len(pc.device_ids))
+
+    def output_layouts(self, pc):
+        n, c, r, dev = self._grid(pc)
+        if r == 1:
+            return super().output_layouts(pc)
+        holders = [tuple(dev(i, j, k) for k in range(r)) for i in range(n) for j in range(c)]
+        return [Layout(self.outputs[0].dims, (n, c), holders, partial=True)]
+
     def input_layouts(self, pc):
-        out = Layout.from_pc(self.outputs[0].dims, pc)
-        n, c = out.degrees
-        holders = [tuple(out.holders[i * c + j][0] for j in range(c)) for i in range(n)]
+        n, c, r, dev = self._grid(pc)
+        holders = [tuple(dev(i, j, k) for k in range(r) for j in range(c)) for i in range(n)]
         return [Layout(self.inputs[0].dims, (n, 1), holders)]
 
     def weight_layouts(self, pc):
-        out = Layout.from_pc(self.outputs[0].dims, pc)
-        n, c = out.degrees
-        holders = [tuple(out.holders[i * c + j][0] for i in range(n)) for j in range(c)]
-        return [Layout(self.weights[0].dims, (1, c), holders)]
+        n, c, r, dev = self._grid(pc)
+        holders = [tuple(dev(i, j, k) for i in range(n)) for k in range(r) for j in range(c)]
+        return [Layout(self.weights[0].dims, (r, c), holders)]
+
+    @staticmethod
+    def _row_lo(ctx):
+        b = ctx.w_boxes[0] if ctx.w_boxes else None
+        return int(b[0][0]) if b is not None else 0
+
+    @staticmethod
+    def _local_rows(idx, lo, rows):
+        """(local row per lookup clamped into the shard, mask of the lookups this shard holds)."""
+        li = idx.long() - lo
+        ok = (li >= 0) & (li < rows)
+        return li.clamp(0, rows - 1), ok
 
     def needs_input_grad(self, i):
         return False
@@ -73,10 +117,11 @@ class Embedding(Op):
         w = ctx.weights[0]
         out = ctx.outputs[0]
         if ctx.hip:
-            K.embedding_forward(idx, w, out, int(self.aggr))
+            Embedding.forward_group([self], [ctx])
         else:
             bag = idx.shape[1]
-            rows = w.index_select(0, idx.reshape(-1).long()).view(idx.shape[0], bag, -1)
+            li, ok = self._local_rows(idx, self._row_lo(ctx), w.shape[0])
+            rows = w.index_select(0, li.reshape(-1)).view(idx.shape[0], bag, -1) * ok.unsqueeze(-1).to(w.dtype)
             r = rows.sum(1)
             if self.aggr == AggrMode.AGGR_MODE_AVG:
                 r = r / bag
@@ -94,22 +139,23 @@ class Embedding(Op):
                 if self.aggr == AggrMode.AGGR_MODE_AVG:
                     g = g / idx.shape[1]
                 bag = idx.shape[1]
-                flat = idx.reshape(-1).long()
-                gg = g.repeat_interleave(bag, dim=0)
+                li, ok = self._local_rows(idx, self._row_lo(ctx), ctx.weights[0].shape[0])
+                gg = g.repeat_interleave(bag, dim=0) * ok.reshape(-1, 1).to(g.dtype)
                 upd = torch.zeros_like(ctx.weights[0])
-                upd.index_add_(0, flat, gg)
+                upd.index_add_(0, li.reshape(-1), gg)
                 ctx.weights[0].sub_(ctx.lr.to(upd.dtype) * upd)
             return
         dw = ctx.weight_grads[0]
         if ctx.hip:
-            K.embedding_backward_dense(idx, dy, dw, int(self.aggr))
+            Embedding.backward_group([self], [ctx])
         else:
             g = dy.float()
             if self.aggr == AggrMode.AGGR_MODE_AVG:
                 g = g / idx.shape[1]
             bag = idx.shape[1]
+            li, ok = self._local_rows(idx, self._row_lo(ctx), dw.shape[0])
             dw.zero_()
-            dw.index_add_(0, idx.reshape(-1).long(), g.repeat_interleave(bag, dim=0))
+            dw.index_add_(0, li.reshape(-1), g.repeat_interleave(bag, dim=0) * ok.reshape(-1, 1).to(g.dtype))
 
     # ---------------------------------------------------------- fused groups
     @staticmethod
@@ -127,7 +173,8 @@ class Embedding(Op):
         K.C().embedding_fwd_multi([c.weights[0] for c in ctxs], [c.inputs[0] for c in ctxs],
                                   [c.outputs[0] for c in ctxs], [c.outputs[0].stride(0) for c in ctxs],
                                   [1.0 / c.inputs[0].shape[1] if op.aggr == AggrMode.AGGR_MODE_AVG else 1.0
-                                   for op, c in zip(ops, ctxs)])
+                                   for op, c in zip(ops, ctxs)],
+                                  [Embedding._row_lo(c) for c in ctxs])
 
     @staticmethod
     def backward_group(ops, ctxs):
@@ -152,7 +199,8 @@ class Embedding(Op):
                 for b in bufs:
                     claim.extend(b if b is not None else (None, None, None))
         K.C().embedding_bwd_multi(tables, [c.inputs[0] for c in ctxs], [c.out_grads[0] for c in ctxs],
-                                  [c.out_grads[0].stride(0) for c in ctxs], scales, lr, claim)
+                                  [c.out_grads[0].stride(0) for c in ctxs], scales, lr, claim,
+                                  [Embedding._row_lo(c) for c in ctxs])
 
     CLAIM = os.environ.get("FM_EMB_CLAIM", "1") != "0"
 

@@ -663,8 +663,11 @@ class Executor:
                     shp = need.local_shape(self.rank)
                     if shp is not None:
                         self.tmp_grad[(op.guid, i)] = self._alloc(shp, self.cdtype)
+                    # the gradient of a partial-sum output (row-sharded embedding) is the FULL
+                    # gradient on every holder: reduce into home.as_full()
                     red.append((op, i, t.guid,
-                                ReshardStep(ReshardPlan(need.as_partial(), home), self.rank, self.world, self.cdtype, self.device)))
+                                ReshardStep(ReshardPlan(need.as_partial(), home.as_full()), self.rank, self.world,
+                                            self.cdtype, self.device)))
             if red:
                 self.bwd_steps.append(("reduce", red))
 

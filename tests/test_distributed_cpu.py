@@ -70,6 +70,12 @@ def _build(case, world):
                 strat = dict(optimize(m, 400, 1.0, num_devices=world, machine=mach, seed=5, verbose=False).best)
                 dp = ParallelConfig.data_parallel(2, world)
                 assert sum(pc != dp for pc in strat.values()) >= 3, strat
+            if case == "dlrm_rowsplit":
+                # row split of a table: every rank holds a block of rows (partial outputs summed
+                # by the exchange); on 4 ranks a second table is row x sample split (2 x 2)
+                strat["embedding2"] = ParallelConfig([1, 1, world], list(range(world)))
+                if world == 4:
+                    strat["embedding0"] = ParallelConfig([1, 2, 2], [3, 1, 2, 0])
             if case == "dlrm_colsplit":
                 # column (parameter-dim) split of one table across all ranks
                 strat["embedding1"] = ParallelConfig([world, 1], list(range(world)))
@@ -148,7 +154,8 @@ def _launch(case, world, steps=3):
 
 @pytest.mark.parametrize("case,world", [("mlp_dp", 2), ("mlp_channel", 2), ("mlp_channel", 4), ("dlrm_dot", 2),
                                         ("dlrm_cat", 2), ("dlrm_colsplit", 2), ("cnn_spatial", 2),
-                                        ("dlrm_search", 2), ("dlrm_search", 4)])
+                                        ("dlrm_search", 2), ("dlrm_search", 4), ("dlrm_rowsplit", 2),
+                                        ("dlrm_rowsplit", 4)])
 def test_strategy_equivalence(case, world):
     ref = _launch(case, 1)
     got = _launch(case, world)

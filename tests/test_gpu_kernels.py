@@ -359,3 +359,45 @@ def test_embedding_owner_computes_sgd(gpu, idx_dtype):
         for k in range(0, len(claim), 3):
             if claim[k] is not None:
                 assert int((claim[k] != -1).sum()) == 0 and int(claim[k + 2].item()) == 0, "claims not released"
+
+
+@pytest.mark.parametrize("idx_dtype", [torch.int64, torch.int32])
+def test_embedding_row_shards(gpu, idx_dtype):
+    """Row-sharded tables (a shard holds rows [lo, lo+rows)): forward sums only the lookups the
+    shard holds, and every backward path (owner-computes, atomics, tiny-table LDS, dense grad)
+    touches only them -- the shards of a table together equal the unsharded table."""
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(6)
+    B = 1000
+    specs = [(100000, 1, 128), (2000, 2, 64), (12, 1, 128)]   # rows, bag, D
+    lr = torch.tensor([0.05], device=gpu)
+    for rows, bag, D in specs:
+        W = torch.randn(rows, D, device=gpu)
+        idx = torch.randint(0, rows, (B, bag), device=gpu, dtype=idx_dtype)
+        dy = torch.randn(B, D, device=gpu).to(torch.bfloat16)
+        cut = [0, rows // 3, rows]
+        shards = [W[cut[k]:cut[k + 1]].clone() for k in range(2)]
+        # forward: partial sums add up to the full lookup
+        outs = [torch.empty(B, D, device=gpu) for _ in range(2)]
+        Kk.C().embedding_fwd_multi(shards, [idx, idx], outs, [D, D], [1.0, 1.0], [cut[0], cut[1]])
+        ref = W[idx.long()].sum(1)
+        assert torch.allclose(outs[0] + outs[1], ref, atol=1e-4), (rows, "fwd")
+        # fused sparse SGD (owner-computes for the big table, atomics / tiny otherwise)
+        claim = []
+        for k in range(2):
+            r = cut[k + 1] - cut[k]
+            if r > B * bag:
+                claim += [torch.full((r,), -1, dtype=torch.int32, device=gpu),
+                          torch.empty(B * bag, dtype=torch.int32, device=gpu), torch.zeros(1, dtype=torch.int32, device=gpu)]
+            else:
+                claim += [None, None, None]
+        Kk.C().embedding_bwd_multi(shards, [idx, idx], [dy, dy], [D, D], [1.0, 1.0], lr, claim, [cut[0], cut[1]])
+        upd = torch.zeros_like(W)
+        upd.index_add_(0, idx.reshape(-1).long(), dy.float().repeat_interleave(bag, 0))
+        Wn = W - 0.05 * upd
+        torch.cuda.synchronize()
+        assert torch.allclose(torch.cat(shards), Wn, atol=1e-4), (rows, "sgd")
+        # dense gradient
+        grads = [torch.zeros_like(s) for s in shards]
+        Kk.C().embedding_bwd_multi(grads, [idx, idx], [dy, dy], [D, D], [1.0, 1.0], None, None, [cut[0], cut[1]])
+        assert torch.allclose(torch.cat(grads), upd, atol=1e-3), (rows, "dense")
