@@ -271,6 +271,12 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
   p.alpha = alpha; p.batch = batch; p.ws = ws;
   p.ay = (const unsigned short*)act_y; p.lday = lday; p.bact = bwd_act; p.colsum = colsum; p.rowsum_a = rowsum_a;
   p.n_fast = M >= N;
+  p.atomic_c = 0;
+  // split-K partial tiles are added straight into C when C is an fp32 accumulator (beta) without
+  // an epilogue and is small: saves the slab round trip and the reduce launch (measured on the
+  // DLRM dW GEMMs: <= 256K outputs)
+  const bool atomic_ok = c_fp32 && beta && bias == nullptr && act == 10 && act_y == nullptr && colsum == nullptr &&
+                         (long)M * N <= (256L << 10) && getenv("FM_GEMM_NO_ATOMIC_SPLIT") == nullptr;
   // vector (16-B) loads need the contiguous extent and leading dims to be multiples of 8
   auto al = [](const void* q) { return (((uintptr_t)q) & 15) == 0; };
   bool vec = al(A) && al(B) && (lda % 8 == 0) && (ldb % 8 == 0) && (sA % 8 == 0) && (sB % 8 == 0);
@@ -296,11 +302,12 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
       while (tiles * ks < 200 && ks * 2 <= ktiles / 4 && ks < 16) ks *= 2;
     }
     if (act_y != nullptr || colsum != nullptr) ks = 1;
-    if (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks = 1;
+    if (ks > 1 && !atomic_ok && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks = 1;
     p.ksplit = ks;
+    p.atomic_c = ks > 1 && atomic_ok;
     fm_gemm_glds_launch(&p, bm, 128, a_kcontig, b_kcontig, (g_gemm_variant & 8) ? 1 : 0, (g_gemm_variant & 64) ? 1 : 0,
                         stream);
-    if (p.ksplit > 1) {
+    if (p.ksplit > 1 && !p.atomic_c) {
       long total = (long)M * N * batch;
       hipLaunchKernelGGL(fm_gemm_splitk_reduce, dim3(fm_grid(total)), dim3(256), 0, stream, p);
     }
@@ -323,11 +330,11 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
   int ktiles = (K + BK - 1) / BK;
   int ks = 1;
   if (ksplit_req > 0) ks = ksplit_req;
-  else if (ws != nullptr) {
+  else if (ws != nullptr || atomic_ok) {
     while (tiles * ks < 256 && ks * 2 <= ktiles / 2 && ks < 16) ks *= 2;
   }
   if (act_y != nullptr || colsum != nullptr) ks = 1;  // fused bwd epilogue needs the full K sum
-  if (ks > 1) {
+  if (ks > 1 && !atomic_ok) {
     long need = (long)batch * ks * M * (long)N * 4;
     if (ws == nullptr || need > ws_bytes) ks = 1;
   }
@@ -335,10 +342,11 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
   if (K <= 0) {  // degenerate: C = epilogue(0)
     p.ksplit = 1;
   }
+  p.atomic_c = p.ksplit > 1 && atomic_ok;
   if (BNv == 128) launch_bm<128, 128>(p, a_kcontig, b_kcontig, vec, stream);
   else if (BMv == 128) launch_bm<128, 64>(p, a_kcontig, b_kcontig, vec, stream);
   else launch_bm<64, 64>(p, a_kcontig, b_kcontig, vec, stream);
-  if (p.ksplit > 1) {
+  if (p.ksplit > 1 && !p.atomic_c) {
     long total = (long)M * N * batch;
     hipLaunchKernelGGL(fm_gemm_splitk_reduce, dim3(fm_grid(total)), dim3(256), 0, stream, p);
   }

@@ -77,6 +77,7 @@ struct GemmP {
   float alpha;
   int tiles_m, tiles_n;
   int n_fast;   // tile order: column tiles fastest (A row-block reused by consecutive tiles on one XCD)
+  int atomic_c; // split-K into an accumulating fp32 C: every split adds its tile with float atomics
 };
 
 // tile coordinates of remapped block id: consecutive ids share an XCD (xcd_remap), so the
@@ -105,6 +106,24 @@ FM_DEVICE void gemm_epilogue(const GemmP& p, const f32x4_t (&acc)[MR][NR], int z
                              int lane) {
   const int mrow = lane & 15;
   const int ncol = 4 * (lane >> 4);
+  if (p.ksplit > 1 && p.atomic_c) {
+    // C (+)= alpha * partial: the splits meet in C itself (no slabs, no reduce launch).  Each
+    // 16x16 accumulator tile is 16 rows x 64 B; used only for small outputs (dW of narrow
+    // layers), where the ~1.3 TB/s atomic rate beats a slab round trip + an extra kernel.
+    float* Cf = reinterpret_cast<float*>(p.C) + (long)zb * p.sC;
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < NR; ++j) {
+        const int m = mbase + 16 * i + mrow;
+        const int n = nbase + 16 * j + ncol;
+        if (m >= p.M) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (n + r < p.N) atomicAdd(Cf + (long)m * p.ldc + n + r, acc[i][j][r] * p.alpha);
+      }
+    return;
+  }
   if (p.ksplit > 1) {
     float* ws = p.ws + ((long)zb * p.ksplit + split) * (long)p.M * p.N;
 #pragma unroll

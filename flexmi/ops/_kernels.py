@@ -119,7 +119,10 @@ def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=F
         C().act_bwd_bias(y2, dy2, dpre, None, M, N, act)
     # dW[N,K] = dpre^T x (both operands MN-contiguous: transposing LDS reads); the bias gradient
     # db = column sums of dpre is accumulated from the staged A tiles of the same GEMM
-    gemm(dpre, dpre.stride(0), False, x2, x2.stride(0), False, dw, K, N, K, M, rowsum_a=db)
+    # dW ACCUMULATES (beta): the executor zeroes the flat gradient buffer once per step, so weights
+    # used by several ops sum their gradients, and split-K partials of small dW tiles can be added
+    # with atomics straight into dw (no slab / reduce launch)
+    gemm(dpre, dpre.stride(0), False, x2, x2.stride(0), False, dw, K, N, K, M, beta=True, rowsum_a=db)
     # dX[M,K] = dpre W   (+ fused activation backward of the layer below)
     if dx2 is not None:
         if fuse_below is not None:
