@@ -197,6 +197,36 @@ __global__ void __launch_bounds__(NT, 2) fm_gemm_kernel(GemmP p) {
   gemm_epilogue<MR, NR>(p, acc, zb, split, m0 + wm * (BM / 2), n0 + wn * (BN / 2), lane);
 }
 
+__global__ void fm_gemm_splitk_reduce(GemmP p);
+
+// 4 consecutive outputs per thread (16-B slab loads): N % 4 == 0, fp32 C with ldc % 4 == 0
+__global__ void fm_gemm_splitk_reduce4(GemmP p) {
+  const long MN = (long)p.M * p.N;
+  const long total4 = MN * p.batch / 4;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total4; i += (long)gridDim.x * blockDim.x) {
+    const long e4 = i * 4;
+    const long zb = e4 / MN, e = e4 % MN;
+    const int m = (int)(e / p.N), n = (int)(e % p.N);
+    const float* src = p.ws + zb * p.ksplit * MN + e;
+    f32x4_t s = *reinterpret_cast<const f32x4_t*>(src);
+    for (int k = 1; k < p.ksplit; ++k) s += *reinterpret_cast<const f32x4_t*>(src + k * MN);
+    s *= p.alpha;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s[r] = act_fwd(p.act, s[r] + (p.bias ? p.bias[n + r] : 0.f));
+    f32x4_t* d = reinterpret_cast<f32x4_t*>(reinterpret_cast<float*>(p.C) + zb * p.sC + (long)m * p.ldc + n);
+    if (p.beta) s += *d;
+    *d = s;
+  }
+}
+
+void launch_splitk_reduce(const GemmP& p, hipStream_t stream) {
+  const long total = (long)p.M * p.N * p.batch;
+  const bool v4 = p.c_fp32 && (p.N % 4 == 0) && (p.ldc % 4 == 0) && (p.sC % 4 == 0) &&
+                  ((((uintptr_t)p.C) & 15) == 0);
+  if (v4) hipLaunchKernelGGL(fm_gemm_splitk_reduce4, dim3(fm_grid(total / 4)), dim3(256), 0, stream, p);
+  else hipLaunchKernelGGL(fm_gemm_splitk_reduce, dim3(fm_grid(total)), dim3(256), 0, stream, p);
+}
+
 __global__ void fm_gemm_splitk_reduce(GemmP p) {
   const long MN = (long)p.M * p.N;
   const long total = MN * p.batch;
@@ -272,11 +302,12 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
   p.ay = (const unsigned short*)act_y; p.lday = lday; p.bact = bwd_act; p.colsum = colsum; p.rowsum_a = rowsum_a;
   p.n_fast = M >= N;
   p.atomic_c = 0;
-  // split-K partial tiles are added straight into C when C is an fp32 accumulator (beta) without
-  // an epilogue and is small: saves the slab round trip and the reduce launch (measured on the
-  // DLRM dW GEMMs: <= 256K outputs)
+  // opt-in (FM_GEMM_ATOMIC_SPLIT=1): split-K partial tiles added straight into a small fp32
+  // accumulating C with float atomics, no slabs and no reduce launch.  Measured SLOWER on the
+  // DLRM dW GEMMs (profiles/README.md): the 16x16 accumulator layout issues 4-B atomics over 16
+  // rows per wave-instruction, far below the 256-contiguous-byte atomic rate.
   const bool atomic_ok = c_fp32 && beta && bias == nullptr && act == 10 && act_y == nullptr && colsum == nullptr &&
-                         (long)M * N <= (256L << 10) && getenv("FM_GEMM_NO_ATOMIC_SPLIT") == nullptr;
+                         (long)M * N <= (256L << 10) && getenv("FM_GEMM_ATOMIC_SPLIT") != nullptr;
   // vector (16-B) loads need the contiguous extent and leading dims to be multiples of 8
   auto al = [](const void* q) { return (((uintptr_t)q) & 15) == 0; };
   bool vec = al(A) && al(B) && (lda % 8 == 0) && (ldb % 8 == 0) && (sA % 8 == 0) && (sB % 8 == 0);
@@ -308,8 +339,7 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
     fm_gemm_glds_launch(&p, bm, 128, a_kcontig, b_kcontig, (g_gemm_variant & 8) ? 1 : 0, (g_gemm_variant & 64) ? 1 : 0,
                         stream);
     if (p.ksplit > 1 && !p.atomic_c) {
-      long total = (long)M * N * batch;
-      hipLaunchKernelGGL(fm_gemm_splitk_reduce, dim3(fm_grid(total)), dim3(256), 0, stream, p);
+      launch_splitk_reduce(p, stream);
     }
     return p.ksplit;
   }
@@ -347,8 +377,7 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
   else if (BMv == 128) launch_bm<128, 64>(p, a_kcontig, b_kcontig, vec, stream);
   else launch_bm<64, 64>(p, a_kcontig, b_kcontig, vec, stream);
   if (p.ksplit > 1 && !p.atomic_c) {
-    long total = (long)M * N * batch;
-    hipLaunchKernelGGL(fm_gemm_splitk_reduce, dim3(fm_grid(total)), dim3(256), 0, stream, p);
+    launch_splitk_reduce(p, stream);
   }
   return p.ksplit;
 }
