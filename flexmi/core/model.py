@@ -105,7 +105,8 @@ class FFModel:
     def _add(self, op):
         op.layer_id = len(self.layers)
         self.layers.append(op)
-        self.parameters.extend(op.weights)
+        have = {p.guid for p in self.parameters}
+        self.parameters.extend(w for w in op.weights if w.guid not in have)   # shared weights once
         return op
 
     def add_layer(self, op_type, name):
@@ -259,8 +260,22 @@ class FFModel:
         return self._add(DotInteraction(self, bottom, embs, 16, self_interaction, name)).outputs[0]
 
     def _share(self, op, shared_op):
-        if shared_op is not None:
-            raise NotImplementedError("weight sharing between ops is not supported yet")
+        """``shared_op`` (``src/runtime/model.cc:157-171``): the new op uses the weights of
+        ``shared_op``.  The reference only reused the op NAME (so both ops got the same parallel
+        config) and still created separate weights; flexmi ties the weights themselves --
+        one set of Parameters, gradients of both ops summed, one optimizer update -- and runs
+        the sharing op under the owner's parallel config so the weight shards coincide."""
+        if shared_op is None:
+            return
+        if isinstance(shared_op, DeferredOp):
+            shared_op = shared_op.op
+        owner = getattr(shared_op, "shared_from", None) or shared_op
+        assert type(owner) is type(op), f"shared_op must be a {type(op).__name__}, got {type(owner).__name__}"
+        assert len(owner.weights) == len(op.weights) and all(
+            a.dims == b.dims for a, b in zip(owner.weights, op.weights)), \
+            f"shared_op weight shapes {[w.dims for w in owner.weights]} != {[w.dims for w in op.weights]}"
+        op.weights = list(owner.weights)
+        op.shared_from = owner
 
     # ------------------------------------------------------------------ lifecycle
     def set_sgd_optimizer(self, optimizer):

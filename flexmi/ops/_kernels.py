@@ -374,12 +374,13 @@ def conv2d_backward(x, w, y, dy, dx, dw, db, stride, pads, act, groups, acc):
     C().transpose_batched(dy, y, g, N, Kout, P * Q, act, 1)
     col = scratch(x.device, "conv_col", NPQ * ldc)
     C().im2col(x, col, R, S, P, Q, stride[0], stride[1], pads[0], pads[2], ldc)
+    # dW / db ACCUMULATE into the per-step zeroed gradient buffer (tied weights sum their grads)
     if ldc == CRS:
-        gemm(g, Kout, False, col, ldc, False, dw.view(Kout, CRS), CRS, Kout, CRS, NPQ, rowsum_a=db)
+        gemm(g, Kout, False, col, ldc, False, dw.view(Kout, CRS), CRS, Kout, CRS, NPQ, beta=True, rowsum_a=db)
     else:
         dwp = scratch(x.device, "conv_dwpad", Kout * ldc, torch.float32)
         gemm(g, Kout, False, col, ldc, False, dwp, ldc, Kout, ldc, NPQ, rowsum_a=db)
-        C().compact_rows(dwp, dw.view(-1), Kout, CRS, ldc, False)
+        C().compact_rows(dwp, dw.view(-1), Kout, CRS, ldc, True)
     if dx is not None:
         wm = _conv_weight_matrix(w, Kout, CRS, ldc)
         dcol = scratch(x.device, "conv_dcol", NPQ * ldc)

@@ -114,9 +114,9 @@ class Conv2D(_SpatialOp):
         with torch.enable_grad():
             out = F.conv2d(xp, w, None, (self.sh, self.sw), 0, 1, self.groups)
             grads = torch.autograd.grad(out, [w] + ([xp] if dx is not None else []), g)
-        dw.copy_(grads[0])
+        dw.add_(grads[0])          # accumulate: the executor zeroes gradients once per step
         if db is not None:
-            db.copy_(g.sum((0, 2, 3)))
+            db.add_(g.sum((0, 2, 3)))
         if dx is not None:
             gx = grads[1][:, :, pads[0]: pads[0] + x.shape[2], pads[2]: pads[2] + x.shape[3]]
             store(dx, gx, ctx.in_grad_accumulate[0])

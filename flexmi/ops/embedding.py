@@ -154,7 +154,6 @@ class Embedding(Op):
                 g = g / idx.shape[1]
             bag = idx.shape[1]
             li, ok = self._local_rows(idx, self._row_lo(ctx), dw.shape[0])
-            dw.zero_()
             dw.index_add_(0, li.reshape(-1), g.repeat_interleave(bag, dim=0) * ok.reshape(-1, 1).to(g.dtype))
 
     # ---------------------------------------------------------- fused groups
@@ -187,9 +186,7 @@ class Embedding(Op):
             tables = [c.weights[0] for c in ctxs]
             lr = ctxs[0].lr
         else:
-            tables = [c.weight_grads[0] for c in ctxs]
-            for t in tables:
-                t.zero_()
+            tables = [c.weight_grads[0] for c in ctxs]   # accumulate (zeroed once per step)
             lr = None
         claim = None
         if ops[0].sparse_sgd:

@@ -545,6 +545,10 @@ class Executor:
         ops = m.layers
         self.pcs = {}
         for op in ops:
+            owner = getattr(op, "shared_from", None)
+            if owner is not None and owner.guid in self.pcs and op.valid_pc(self.pcs[owner.guid]):
+                self.pcs[op.guid] = self.pcs[owner.guid]   # tied weights: the owner's shards
+                continue
             pc = self.strategies.get(op.name)
             if pc is None or not op.valid_pc(pc) or max(pc.device_ids) >= self.world:
                 pc = ParallelConfig.data_parallel(op.out_ndims, self.world)
@@ -819,6 +823,9 @@ class Executor:
             pc = self.pcs[op.guid]
             lays = op.weight_layouts(pc)
             for wi, w in enumerate(op.weights):
+                if w.guid in self.wentries:   # tied weight (shared_op): one entry, grads summed
+                    assert self.wentries[w.guid].layout.same_as(lays[wi]), f"{op.name}: tied weight sharded differently"
+                    continue
                 e = WeightEntry(w, op, wi, lays[wi], self.rank)
                 self.wentries[w.guid] = e
                 if e.box is None:
@@ -1049,6 +1056,12 @@ class Executor:
                 bucket_left[id(g)] = [len(b[2]) for b in g.buckets]
                 g.works = [None] * len(g.buckets)
         steps = self.bwd_steps
+        # a tied weight's gradient is final after the LAST op (in backward order) that uses it
+        uses_left = defaultdict(int)
+        for st in steps:
+            if st[0] == "op":
+                for w in st[1].weights:
+                    uses_left[w.guid] += 1
 
         def touches(st, keys):
             if st[0] == "op":
@@ -1083,8 +1096,9 @@ class Executor:
                             written.add(self.gkey(t.guid))
                 # gradient buckets completed by this op -> async all-reduce (overlaps the rest of bwd)
                 for w in op.weights:
+                    uses_left[w.guid] -= 1
                     e = self.wentries.get(w.guid)
-                    if e is None or e.group is None or not e.group.replicated:
+                    if e is None or e.group is None or not e.group.replicated or uses_left[w.guid] > 0:
                         continue
                     g = e.group
                     for bi, b in enumerate(g.buckets):

@@ -35,6 +35,15 @@ def _build(case, world):
     m = FFModel(cfg)
     strat = {}
     inputs = {}
+    if case == "mlp_tied":
+        # tied weights (shared_op) under data parallelism: the bucketed all-reduce must wait for
+        # BOTH uses' gradients
+        x = m.create_tensor([B, 12], name="x")
+        h = m.dense(x, 12, ActiMode.AC_MODE_RELU, name="fc1")
+        h = m.dense(h, 12, ActiMode.AC_MODE_TANH, shared_op=h.owner_op, name="fc1_tied")
+        o = m.softmax(m.dense(h, 4, name="fc3"), name="sm")
+        loss = LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY
+        inputs["x"] = (x, (B, 12), "f")
     if case in ("mlp_dp", "mlp_channel"):
         x = m.create_tensor([B, 12], name="x")
         h = m.dense(x, 16, ActiMode.AC_MODE_RELU, name="fc1")
@@ -152,7 +161,7 @@ def _launch(case, world, steps=3):
     return d
 
 
-@pytest.mark.parametrize("case,world", [("mlp_dp", 2), ("mlp_channel", 2), ("mlp_channel", 4), ("dlrm_dot", 2),
+@pytest.mark.parametrize("case,world", [("mlp_dp", 2), ("mlp_tied", 2), ("mlp_channel", 2), ("mlp_channel", 4), ("dlrm_dot", 2),
                                         ("dlrm_cat", 2), ("dlrm_colsplit", 2), ("cnn_spatial", 2),
                                         ("dlrm_search", 2), ("dlrm_search", 4), ("dlrm_rowsplit", 2),
                                         ("dlrm_rowsplit", 4)])

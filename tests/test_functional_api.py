@@ -85,3 +85,42 @@ def test_raw_ptr_attach_and_get():
     t2 = x.attach_raw_ptr(m, cm.ctypes.data, column_major=True)
     np.testing.assert_array_equal(t2.numpy(), host)
     x.detach_raw_ptr(m)
+
+
+def test_shared_op_ties_weights_like_torch():
+    """dense(..., shared_op=op): one set of weights used by two layers; gradients of both uses are
+    summed and applied once (checked against torch autograd with a literally shared module)."""
+    import torch
+    B, D = 8, 6
+    m = FFModel(_cfg(B))
+    x = m.create_tensor([B, D], name="x")
+    h = m.dense(x, D, ActiMode.AC_MODE_RELU, name="fc")
+    owner = h.owner_op
+    h2 = m.dense(h, D, ActiMode.AC_MODE_NONE, shared_op=owner, name="fc_tied")
+    assert h2.owner_op.weights[0] is owner.weights[0] and len(m.parameters) == 2
+    o = m.softmax(m.dense(h2, 3, name="head"))
+    m.compile(SGDOptimizer(m, 0.1), LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, [MetricsType.METRICS_ACCURACY])
+    ex = m.init_layers()
+    W0 = owner.weights[0].get_weights(m).copy()
+    b0 = owner.weights[1].get_weights(m).copy()
+    Wh = m.layers[-2].weights[0].get_weights(m).copy()
+    bh = m.layers[-2].weights[1].get_weights(m).copy()
+    fc = torch.nn.Linear(D, D)
+    head = torch.nn.Linear(D, 3)
+    with torch.no_grad():
+        fc.weight.copy_(torch.from_numpy(W0)); fc.bias.copy_(torch.from_numpy(b0))
+        head.weight.copy_(torch.from_numpy(Wh)); head.bias.copy_(torch.from_numpy(bh))
+    opt = torch.optim.SGD(list(fc.parameters()) + list(head.parameters()), lr=0.1)
+    rng = np.random.RandomState(2)
+    for _ in range(3):
+        xa = rng.rand(B, D).astype(np.float32)
+        ya = rng.randint(0, 3, (B, 1)).astype(np.int32)
+        ex.scatter_from_host(x, xa)
+        ex.scatter_from_host(m.get_label_tensor(), ya)
+        ex.train_step()
+        opt.zero_grad()
+        logits = head(fc(torch.relu(fc(torch.from_numpy(xa)))))
+        torch.nn.functional.cross_entropy(logits, torch.from_numpy(ya[:, 0]).long(), reduction="sum").div(B).backward()
+        opt.step()
+    np.testing.assert_allclose(owner.weights[0].get_weights(m), fc.weight.detach().numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(owner.weights[1].get_weights(m), fc.bias.detach().numpy(), rtol=1e-4, atol=1e-5)
