@@ -1,0 +1,23 @@
+"""Sequential MNIST MLP (reference examples/python/keras/seq_mnist_mlp.py)."""
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import common  # noqa: E402,F401
+from common import ModelAccuracy, epochs, keras_callbacks  # noqa: E402
+
+from flexmi.keras import Model, Sequential, optimizers  # noqa: E402
+from flexmi.keras.layers import (Activation, Concatenate, Conv2D, Dense, Flatten, Input,  # noqa: E402,F401
+                                 MaxPooling2D, Reshape, add, concatenate, subtract)
+
+
+
+def main():
+    x, y = common.mnist_flat()
+    model = Sequential([Dense(512, input_shape=(784,), activation='relu'), Dense(512, activation='relu'),
+                        Dense(10), Activation('softmax')])
+    model.compile(optimizer=optimizers.SGD(learning_rate=0.01), loss='sparse_categorical_crossentropy', metrics=['accuracy', 'sparse_categorical_crossentropy'])
+    print(model.summary())
+    model.fit(x, y, epochs=epochs(20), callbacks=keras_callbacks(ModelAccuracy.MNIST_MLP))
+
+
+if __name__ == '__main__':
+    main()

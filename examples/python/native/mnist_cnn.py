@@ -1,0 +1,36 @@
+"""MNIST CNN (reference examples/python/native/mnist_cnn.py)."""
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from common import ModelAccuracy, check_accuracy, header, mnist_images, report  # noqa: E402
+
+from flexmi.core import (ActiMode, DataType, FFConfig, FFModel, LossType, MetricsType,  # noqa: E402
+                         SGDOptimizer, SingleDataLoader)
+
+
+def main():
+    cfg = FFConfig()
+    cfg.parse_args()
+    header(cfg)
+    model = FFModel(cfg)
+    x = model.create_tensor([cfg.get_batch_size(), 1, 28, 28], DataType.DT_FLOAT)
+    t = model.conv2d(x, 32, 3, 3, 1, 1, 1, 1, ActiMode.AC_MODE_RELU)
+    t = model.conv2d(t, 64, 3, 3, 1, 1, 1, 1, ActiMode.AC_MODE_RELU)
+    t = model.pool2d(t, 2, 2, 2, 2, 0, 0)
+    t = model.flat(t)
+    t = model.dense(t, 128, ActiMode.AC_MODE_RELU)
+    t = model.softmax(model.dense(t, 10))
+    model.compile(optimizer=SGDOptimizer(model, 0.01), loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY,
+                  metrics=[MetricsType.METRICS_ACCURACY, MetricsType.METRICS_SPARSE_CATEGORICAL_CROSSENTROPY])
+    xs, ys = mnist_images()
+    n = len(xs)
+    loaders = (SingleDataLoader(model, x, xs, n), SingleDataLoader(model, model.get_label_tensor(), ys, n))
+    model.init_layers()
+    t0 = cfg.get_current_time()
+    model.train(loaders, cfg.get_epochs())
+    report(cfg, n, cfg.get_epochs(), t0, cfg.get_current_time())
+    check_accuracy(model, ModelAccuracy.MNIST_CNN)
+
+
+if __name__ == "__main__":
+    print("mnist cnn")
+    main()

@@ -1,0 +1,18 @@
+"""Trace the PyTorch MLP with torch.fx and write the FlexFlow text format mlp.ff
+(reference examples/python/pytorch/mnist_mlp_torch.py)."""
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "onnx"))
+import common  # noqa: E402,F401
+
+from _models import MLP  # noqa: E402
+from flexmi.torch.fx import torch_to_flexflow  # noqa: E402
+
+
+def export(path="mlp.ff"):
+    torch_to_flexflow(MLP(), path)
+    return path
+
+
+if __name__ == "__main__":
+    print("wrote", export(sys.argv[1] if len(sys.argv) > 1 else "mlp.ff"))

@@ -93,6 +93,11 @@ class FFModel:
 
     # ------------------------------------------------------------------ tensors
     def create_tensor(self, dims, data_type=DataType.DT_FLOAT, create_grad=True, name=None):
+        if isinstance(data_type, str):
+            # older reference spelling create_tensor(dims, name, data_type) (examples/python/onnx)
+            name, data_type = (data_type or None), (create_grad if not isinstance(create_grad, bool)
+                                                    else DataType.DT_FLOAT)
+            create_grad = True
         t = Tensor(dims, data_type, None, 0, create_grad, self, name)
         self.input_tensors.append(t)
         return t
@@ -323,6 +328,12 @@ class FFModel:
             from flexmi.runtime.executor import Executor
             self.executor = Executor(self, self.strategies, self.comm, self.optimizer, self.loss_type,
                                      self.metrics_op, self.label_tensor)
+            # host arrays mapped / attached before init (inline_map between compile and init)
+            for t in list(self.input_tensors) + ([self.label_tensor] if self.label_tensor is not None else []):
+                pend = getattr(t, "_pending", None)
+                if pend is not None and t.guid in self.executor.home:
+                    self.executor.scatter_from_host(t, pend)
+                    t._pending = None
         return self.executor
 
     def _ex(self):

@@ -59,23 +59,57 @@ class Tensor:
     def _executor(self, ffmodel=None):
         m = ffmodel if ffmodel is not None else self.model
         ex = getattr(m, "executor", None)
+        if ex is None and getattr(m, "loss_op", None) is not None:
+            # compiled but not initialised: weights exist from compile on in the reference
+            # (set_weights between compile and init_layers, keras net2net examples)
+            ex = m.init_layers()
         assert ex is not None, "model is not compiled/initialised"
         return ex
 
+    def _live(self):
+        """The executor holding this tensor's shards, or None (model not initialised yet, or a
+        host-only tensor such as a full dataset that no op consumes)."""
+        ex = getattr(self.model, "executor", None)
+        if ex is None or self.guid not in ex.home:
+            return None
+        return ex
+
+    def _host_dtype(self):
+        return np.float32 if self.data_type in (DataType.DT_FLOAT, DataType.DT_HALF, DataType.DT_DOUBLE) \
+            else torch.empty(0, dtype=self.torch_dtype).numpy().dtype
+
     def inline_map(self, ffconfig=None):
-        self._mapped = self._executor().gather_to_host(self)
+        """Host view of the whole logical tensor.  Before ``init_layers`` (the reference maps
+        input/label regions between compile and init, ``mnist_mlp_attach.py``) the view is a
+        host staging array that ``init_layers`` scatters to the shards."""
+        ex = self._live()
+        if ex is not None:
+            self._mapped = ex.gather_to_host(self)
+        else:
+            pend = getattr(self, "_pending", None)
+            if pend is None:
+                att = getattr(self, "_attached", None)
+                pend = att.numpy().copy() if att is not None else np.zeros(self.dims, self._host_dtype())
+            self._mapped = pend
         return self._mapped
 
     def inline_unmap(self, ffconfig=None):
         if self._mapped is not None:
-            self._executor().scatter_from_host(self, self._mapped)
+            ex = self._live()
+            if ex is not None:
+                ex.scatter_from_host(self, self._mapped)
+            else:
+                self._pending = self._mapped
         self._mapped = None
 
     def is_mapped(self):
-        return self._mapped is not None
+        return self._mapped is not None or getattr(self, "_attached", None) is not None
 
     def get_array(self, ffconfig=None, data_type=None):
         if self._mapped is None:
+            att = getattr(self, "_attached", None)
+            if att is not None and self._live() is None:
+                return att.numpy()
             self.inline_map(ffconfig)
         return self._mapped
 
@@ -87,11 +121,19 @@ class Tensor:
         arr = np.ascontiguousarray(np_array)
         assert tuple(arr.shape) == self.dims or arr.size == self.volume(), (arr.shape, self.dims)
         self._attached = torch.from_numpy(arr.reshape(self.dims))
+        # a tensor the graph consumes (an input / label): its shards take the attached contents
+        # now, or at init_layers; a host-only tensor (a full dataset) is read by the loaders
+        ex = self._live()
+        if ex is not None:
+            ex.scatter_from_host(self, arr)
+        else:
+            self._pending = arr.reshape(self.dims)
         return self._attached
 
     def detach_numpy_array(self, ffconfig=None):
         # the loaders keep their own reference; dropping ours mirrors detach_raw_ptr
         self._attached = None
+        self._mapped = None
 
     def get_raw_ptr(self, ffmodel=None, ffconfig=None):
         """Device address of this rank's shard buffer (``Tensor::get_raw_ptr``,
@@ -139,6 +181,21 @@ class Parameter(Tensor):
 
     def get_weights(self, ffmodel=None):
         return self._executor(ffmodel).get_param_full(self).numpy()
+
+    # a mapped parameter is its full master copy; unmapping writes it back to every shard
+    def inline_map(self, ffconfig=None):
+        self._mapped = self.get_weights()
+        return self._mapped
+
+    def inline_unmap(self, ffconfig=None):
+        if self._mapped is not None:
+            self.set_weights(self.model, self._mapped)
+        self._mapped = None
+
+    def get_array(self, ffconfig=None, data_type=None):
+        if self._mapped is None:
+            self.inline_map(ffconfig)
+        return self._mapped
 
     def __repr__(self):
         return f"Parameter({self.name}, dims={list(self.dims)})"

@@ -87,11 +87,18 @@ class Layer:
 
     # -- weights (Keras API; layer_base.py:102-120) --------------------------------
     def get_weights(self, model):
-        return [w.get_weights(model.ffmodel) for w in (self.ff_op.weights if self.ff_op else [])]
+        """(kernel, bias) of the layer; ``model`` is the Keras model or its ``ffmodel``."""
+        ff = getattr(model, "ffmodel", model)
+        return [w.get_weights(ff) for w in (self.ff_op.weights if self.ff_op else [])]
 
-    def set_weights(self, model, arrays):
+    def set_weights(self, model, *arrays):
+        """``set_weights(ffmodel, kernel, bias)`` (reference ``layer_base.py``) or
+        ``set_weights(model, [kernel, bias])``."""
+        ff = getattr(model, "ffmodel", model)
+        if len(arrays) == 1 and isinstance(arrays[0], (list, tuple)):
+            arrays = arrays[0]
         for w, a in zip(self.ff_op.weights, arrays):
-            w.set_weights(model.ffmodel, a)
+            w.set_weights(ff, a)
 
     def get_summary(self):
         return f"{self.name:24s} {type(self).__name__:20s} {str(self.outputs[0].batch_shape) if self.outputs else ''}\n"

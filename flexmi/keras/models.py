@@ -20,6 +20,7 @@ from flexmi.core.types import DataType
 from . import losses as L
 from . import metrics as Mt
 from .layers import InputLayer, KTensor, Layer
+from .layers import _Merge as _MergeBase
 
 
 class Model:
@@ -38,6 +39,8 @@ class Model:
     # -- graph ------------------------------------------------------------------------
     @property
     def layers(self) -> List[Layer]:
+        if getattr(self, "_snapshot", None) is not None:
+            return [lay for lay, _, _ in self._snapshot]
         order, seen = [], set()
 
         def visit(t):
@@ -50,6 +53,37 @@ class Model:
             order.append(lay)
         visit(self._output)
         return [lay for lay in order if not isinstance(lay, InputLayer)]
+
+    # -- nesting: a model used as a layer replays its layers on the new inputs ----------
+    def __call__(self, x):
+        xs = list(x) if isinstance(x, (list, tuple)) else [x]
+        if len(xs) != len(self._inputs):
+            raise ValueError(f"model {self.name} takes {len(self._inputs)} inputs, got {len(xs)}")
+        if getattr(self, "_snapshot", None) is None:
+            # the layers get rebound to the caller's graph: remember this model's own wiring
+            self._snapshot = [(lay, list(lay.inputs), list(lay.outputs)) for lay in self.layers]
+        env = {id(t): u for t, u in zip(self._inputs, xs)}
+        for lay, lins, louts in self._snapshot:
+            ins = [env[id(t)] for t in lins]
+            old = louts
+            out = lay(ins if len(ins) > 1 or isinstance(lay, _MergeBase) else ins[0])
+            new = out if isinstance(out, list) else [out]
+            for o, n in zip(old, new):
+                env[id(o)] = n
+        return env[id(self._output)]
+
+    @property
+    def input(self):
+        """Input tensors (a list, as the reference's ``model.input[0]`` expects)."""
+        return list(self._inputs)
+
+    @property
+    def output(self):
+        return self._output
+
+    @property
+    def input_shape(self):
+        return self._inputs[0].shape if self._inputs else None
 
     def get_layer(self, name=None, index=None):
         lays = self.layers

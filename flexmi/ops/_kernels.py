@@ -270,19 +270,25 @@ def split_forward(x, outs, axis):
     C().multi_copy(src, so, dst, do, rows, cols, lds, ldd, 0)
 
 
-def split_backward(out_grads, dx, acc, axis):
+def split_backward(out_grads, dx, acc, axis, out_shapes=None):
+    """dx = concat(out_grads) along axis; a None grad (an unused split output) is a zero
+    block -- the caller zeroes dx first when it does not accumulate."""
     outer, tot = _outer_inner(dx.shape, axis)
     src, so, dst, do, rows, cols, lds, ldd = [], [], [], [], [], [], [], []
     off = 0
     mask = 0
     for k, g in enumerate(out_grads):
+        if g is None:
+            off += _outer_inner(out_shapes[k], axis)[1]
+            continue
         _, inner = _outer_inner(g.shape, axis)
         src.append(g); so.append(0); dst.append(dx); do.append(off)
         rows.append(outer); cols.append(inner); lds.append(inner); ldd.append(tot)
         if acc:
             mask |= 1 << k
         off += inner
-    C().multi_copy(src, so, dst, do, rows, cols, lds, ldd, mask)
+    if src:
+        C().multi_copy(src, so, dst, do, rows, cols, lds, ldd, mask)
 
 
 def copy_or_add(src, dst, acc):

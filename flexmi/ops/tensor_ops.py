@@ -114,11 +114,22 @@ class Split(Op):
         if not ctx.in_grads or ctx.in_grads[0] is None:
             return
         dx = ctx.in_grads[0]
+        ogs = list(ctx.out_grads)
+        acc = ctx.in_grad_accumulate[0]
+        if any(g is None for g in ogs):       # unused outputs contribute zero blocks
+            if all(g is None for g in ogs):
+                if not acc:
+                    dx.zero_()
+                return
+            if not acc:
+                dx.zero_()
+                acc = True
         if ctx.hip:
-            K.split_backward(list(ctx.out_grads), dx, ctx.in_grad_accumulate[0], self.axis)
+            K.split_backward(ogs, dx, acc, self.axis, [tuple(y.shape) for y in ctx.outputs])
             return
-        g = torch.cat([d.float() for d in ctx.out_grads], dim=self.axis)
-        store(dx, g, ctx.in_grad_accumulate[0])
+        g = torch.cat([d.float() if d is not None else torch.zeros(y.shape) for d, y in zip(ogs, ctx.outputs)],
+                      dim=self.axis)
+        store(dx, g, acc)
 
 
 class _ViewOp(Op):
