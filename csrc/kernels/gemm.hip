@@ -279,8 +279,37 @@ extern "C" void fm_gemm_glds_launch(const void* params, int bm, int bn, int a_kc
 
 // dispatch experiments (tools/gemm_probe.py): 1 = never glds, 2 = glds for every orientation and
 // grid size (K % 64 == 0), 4 = glds 128x128 tiles, 8 = s_setprio around the glds MFMA blocks,
-// 64 = 256x128 glds tile with 4 waves of 128x64
+// 64 = 256x128 glds tile with 4 waves of 128x64, 128 = in-launch split-K combine (split_counters)
 static int g_gemm_variant = getenv("FM_GEMM_VARIANT") ? atoi(getenv("FM_GEMM_VARIANT")) : 0;
+
+// Per-device tile arrival counters of the in-launch split-K combine (gemm_common.h): zeroed once
+// at allocation; each tile's last arriver resets its own counter, so consecutive launches on the
+// stream reuse them (like the shared slab workspace, split-K GEMMs are stream-ordered).  Never
+// allocated inside a stream capture: a capture before any eager split-K launch keeps the reduce
+// kernel.  OPT-IN (variant bit 128 or FM_GEMM_FUSED_SPLITK=1): measured on the DLRM MLPerf step
+// it is SLOWER than the separate reduce launch (0.96 vs 0.755 ms/step, profiles/README.md): each
+// tile's last arriver pays the agent acquire and then reads the other slices' 32-64 KB sc1 slabs
+// serially at the cross-XCD rate, which costs more than the latency-bound reduce kernel it saves.
+static int* split_counters(hipStream_t s, long n, long slab_bytes) {
+  static const bool env_on = getenv("FM_GEMM_FUSED_SPLITK") != nullptr && atoi(getenv("FM_GEMM_FUSED_SPLITK")) == 1;
+  constexpr long CAP = 1L << 16;
+  static int* cnt[64] = {nullptr};
+  if (!(env_on || (g_gemm_variant & 128)) || n > CAP || slab_bytes >= (1L << 31)) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (cnt[dev] == nullptr) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    int* q = nullptr;
+    if (hipMalloc(&q, CAP * sizeof(int)) != hipSuccess) return nullptr;
+    if (hipMemset(q, 0, CAP * sizeof(int)) != hipSuccess) {
+      (void)hipFree(q);
+      return nullptr;
+    }
+    cnt[dev] = q;
+  }
+  return cnt[dev];
+}
 extern "C" void fm_gemm_set_variant(int v) { g_gemm_variant = v; }
 
 // A_kcontig: A stored [M][K] (lda >= K) else [K][M] (lda >= M)
@@ -302,6 +331,7 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
   p.ay = (const unsigned short*)act_y; p.lday = lday; p.bact = bwd_act; p.colsum = colsum; p.rowsum_a = rowsum_a;
   p.n_fast = M >= N;
   p.atomic_c = 0;
+  p.tile_cnt = nullptr;
   // opt-in (FM_GEMM_ATOMIC_SPLIT=1): split-K partial tiles added straight into a small fp32
   // accumulating C with float atomics, no slabs and no reduce launch.  Measured SLOWER on the
   // DLRM dW GEMMs (profiles/README.md): the 16x16 accumulator layout issues 4-B atomics over 16
@@ -336,9 +366,10 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
     if (ks > 1 && !atomic_ok && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks = 1;
     p.ksplit = ks;
     p.atomic_c = ks > 1 && atomic_ok;
+    if (p.ksplit > 1 && !p.atomic_c) p.tile_cnt = split_counters(stream, tiles, (long)M * N * 4);
     fm_gemm_glds_launch(&p, bm, 128, a_kcontig, b_kcontig, (g_gemm_variant & 8) ? 1 : 0, (g_gemm_variant & 64) ? 1 : 0,
                         stream);
-    if (p.ksplit > 1 && !p.atomic_c) {
+    if (p.ksplit > 1 && !p.atomic_c && p.tile_cnt == nullptr) {
       launch_splitk_reduce(p, stream);
     }
     return p.ksplit;
@@ -376,10 +407,11 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
     p.ksplit = 1;
   }
   p.atomic_c = p.ksplit > 1 && atomic_ok;
+  if (p.ksplit > 1 && !p.atomic_c) p.tile_cnt = split_counters(stream, tiles, (long)M * N * 4);
   if (BNv == 128) launch_bm<128, 128>(p, a_kcontig, b_kcontig, vec, stream);
   else if (BMv == 128) launch_bm<128, 64>(p, a_kcontig, b_kcontig, vec, stream);
   else launch_bm<64, 64>(p, a_kcontig, b_kcontig, vec, stream);
-  if (p.ksplit > 1 && !p.atomic_c) {
+  if (p.ksplit > 1 && !p.atomic_c && p.tile_cnt == nullptr) {
     launch_splitk_reduce(p, stream);
   }
   return p.ksplit;

@@ -78,6 +78,7 @@ struct GemmP {
   int tiles_m, tiles_n;
   int n_fast;   // tile order: column tiles fastest (A row-block reused by consecutive tiles on one XCD)
   int atomic_c; // split-K into an accumulating fp32 C: every split adds its tile with float atomics
+  int* tile_cnt; // in-launch split-K combine: per-tile arrival counters (nullptr = separate reduce launch)
 };
 
 // tile coordinates of remapped block id: consecutive ids share an XCD (xcd_remap), so the
@@ -101,6 +102,9 @@ FM_DEVICE int xcd_remap(int bid, int ntiles) {
 
 // ---- epilogue: lane owns C[m][n..n+3], m = lane&15, n = 4*(lane>>4) of each 16x16 tile;
 // tile (i, j) of the wave covers rows mbase+16i.., cols nbase+16j..
+template <int MR, int NR>
+FM_DEVICE void gemm_epilogue_store(const GemmP& p, const f32x4_t (&acc)[MR][NR], int zb, int mbase, int nbase, int lane);
+
 template <int MR, int NR>
 FM_DEVICE void gemm_epilogue(const GemmP& p, const f32x4_t (&acc)[MR][NR], int zb, int split, int mbase, int nbase,
                              int lane) {
@@ -126,6 +130,8 @@ FM_DEVICE void gemm_epilogue(const GemmP& p, const f32x4_t (&acc)[MR][NR], int z
   }
   if (p.ksplit > 1) {
     float* ws = p.ws + ((long)zb * p.ksplit + split) * (long)p.M * p.N;
+    // with the in-launch combine the slabs are stored WRITE-THROUGH (sc1): no release fence needed
+    const auto wrs = __builtin_amdgcn_make_buffer_rsrc(ws, 0, (int)((long)p.M * p.N * 4), 0x00020000);
 #pragma unroll
     for (int i = 0; i < MR; ++i)
 #pragma unroll
@@ -135,15 +141,78 @@ FM_DEVICE void gemm_epilogue(const GemmP& p, const f32x4_t (&acc)[MR][NR], int z
         if (m >= p.M) continue;
         float* dst = ws + (long)m * p.N + n;
         if (n + 3 < p.N && (p.N & 3) == 0) {
-          *reinterpret_cast<f32x4_t*>(dst) = acc[i][j];
+          if (p.tile_cnt)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[i][j]), wrs,
+                                                   (int)(((long)m * p.N + n) * 4), 0, 16);
+          else
+            *reinterpret_cast<f32x4_t*>(dst) = acc[i][j];
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            if (n + r < p.N) dst[r] = acc[i][j][r];
+            if (n + r < p.N) {
+              if (p.tile_cnt) __hip_atomic_store(dst + r, acc[i][j][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              else dst[r] = acc[i][j][r];
+            }
         }
       }
+    if (p.tile_cnt == nullptr) return;
+    // In-launch split-K combine (cdna_hip_programming.md "In-launch split-K reduction", sc1 form):
+    // every wave drains its write-through slab stores, lane 0 draws a relaxed agent-scope ticket;
+    // the block drawing ksplit-1 acquires once (one buffer_inv sc1), sums the other slices' slabs
+    // into its own registers and runs the regular epilogue -- no reduce launch.  The "I am last"
+    // flag goes through the kernel's one dynamic LDS array (free after the K loop).
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    int* flag = reinterpret_cast<int*>(smem);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int* cnt = p.tile_cnt + (long)blockIdx.y * gridDim.x + blockIdx.x;
+      const int ticket = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = ticket == p.ksplit - 1;
+      if (last) {
+        __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // ready for the next launch
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *flag = last;
+    }
+    __syncthreads();
+    if (*flag == 0) return;
+    const float* wsz = p.ws + (long)zb * p.ksplit * (long)p.M * p.N;
+    f32x4_t tot[MR][NR];
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < NR; ++j) {
+        tot[i][j] = acc[i][j];
+        const int m = mbase + 16 * i + mrow;
+        const int n = nbase + 16 * j + ncol;
+        if (m >= p.M) continue;
+        const bool v4 = n + 3 < p.N && (p.N & 3) == 0;
+        for (int k = 0; k < p.ksplit; ++k) {
+          if (k == split) continue;
+          const float* src = wsz + (long)k * p.M * p.N + (long)m * p.N + n;
+          if (v4) {
+            tot[i][j] += *reinterpret_cast<const f32x4_t*>(src);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (n + r < p.N) tot[i][j][r] += src[r];
+          }
+        }
+      }
+    GemmP q = p;
+    q.ksplit = 1;
+    gemm_epilogue_store<MR, NR>(q, tot, zb, mbase, nbase, lane);
     return;
   }
+  gemm_epilogue_store<MR, NR>(p, acc, zb, mbase, nbase, lane);
+}
+
+template <int MR, int NR>
+FM_DEVICE void gemm_epilogue_store(const GemmP& p, const f32x4_t (&acc)[MR][NR], int zb, int mbase, int nbase, int lane) {
+  const int mrow = lane & 15;
+  const int ncol = 4 * (lane >> 4);
   float csum[NR][4];
 #pragma unroll
   for (int j = 0; j < NR; ++j)

@@ -36,11 +36,15 @@ enum Kind : int {
   AR_START = 3,    // allreduce([t]) -> slot
   WAIT = 4,        // wait(slot) (no-op when the slot is empty)
   AR_SYNC = 5,     // wait(slot) if a work is pending, else allreduce([t]) + wait
+  RS_START = 6,    // _reduce_scatter_base(out, in) -> slot       (ZeRO-1 gradient shard sync)
+  RS_SYNC = 7,     // wait(slot) if pending, else reduce-scatter + wait
+  AG_SYNC = 8,     // _allgather_base(out, in) + wait             (ZeRO-1 parameter gather)
 };
 
 const char* kind_name(int k) {
-  static const char* n[] = {"call", "graph", "all_to_all", "all_reduce", "wait", "all_reduce_sync"};
-  return (k >= 0 && k <= 5) ? n[k] : "?";
+  static const char* n[] = {"call", "graph", "all_to_all", "all_reduce", "wait", "all_reduce_sync",
+                            "reduce_scatter", "reduce_scatter_sync", "all_gather_sync"};
+  return (k >= 0 && k <= 8) ? n[k] : "?";
 }
 
 struct Step {
@@ -124,6 +128,34 @@ class StepRunner {
     s.slot = slot;
     s.pg = std::move(pg);
     s.a = c_alias(t);
+    s.name = name;
+    prog(p).push_back(std::move(s));
+  }
+  // out = this rank's 1/n of the element-wise sum of every rank's `in` (in.numel() == n * out.numel())
+  void add_reduce_scatter(int p, int slot, PG pg, at::Tensor out, at::Tensor in, bool sync, const std::string& name) {
+    check_slot(slot);
+    if (in.numel() != out.numel() * pg->getSize())
+      throw std::invalid_argument("add_reduce_scatter: in.numel() must be group size x out.numel()");
+    Step s;
+    s.kind = sync ? RS_SYNC : RS_START;
+    s.slot = slot;
+    s.pg = std::move(pg);
+    s.a = c_alias(out);
+    s.b = c_alias(in);
+    s.name = name;
+    prog(p).push_back(std::move(s));
+  }
+  // out = concat over ranks of `in` (out.numel() == n * in.numel()), waited on before returning
+  void add_all_gather(int p, int slot, PG pg, at::Tensor out, at::Tensor in, const std::string& name) {
+    check_slot(slot);
+    if (out.numel() != in.numel() * pg->getSize())
+      throw std::invalid_argument("add_all_gather: out.numel() must be group size x in.numel()");
+    Step s;
+    s.kind = AG_SYNC;
+    s.slot = slot;
+    s.pg = std::move(pg);
+    s.a = c_alias(out);
+    s.b = c_alias(in);
     s.name = name;
     prog(p).push_back(std::move(s));
   }
@@ -251,6 +283,25 @@ class StepRunner {
         finish(s.slot);
         break;
       }
+      case RS_START:
+      case RS_SYNC: {
+        if (s.kind == RS_START && pending_[s.slot]) finish(s.slot);
+        if (s.kind == RS_START || !pending_[s.slot]) {
+          c10d::ReduceScatterOptions o;
+          start(s.slot, s.pg->_reduce_scatter_base(s.a, s.b, o));
+          bytes_sent_ += s.b.numel() * s.b.element_size();
+        }
+        if (s.kind == RS_SYNC) finish(s.slot);
+        break;
+      }
+      case AG_SYNC: {
+        if (pending_[s.slot]) finish(s.slot);
+        c10d::AllgatherOptions o;
+        start(s.slot, s.pg->_allgather_base(s.a, s.b, o));
+        bytes_sent_ += s.b.numel() * s.b.element_size();
+        finish(s.slot);
+        break;
+      }
       case WAIT:
         finish(s.slot);
         break;
@@ -283,6 +334,10 @@ PYBIND11_MODULE(_rt, m) {
            py::arg("recv"), py::arg("send"), py::arg("recv_splits"), py::arg("send_splits"), py::arg("name") = "")
       .def("add_all_reduce", &StepRunner::add_all_reduce, py::arg("program"), py::arg("slot"), py::arg("pg"),
            py::arg("tensor"), py::arg("sync") = false, py::arg("name") = "")
+      .def("add_reduce_scatter", &StepRunner::add_reduce_scatter, py::arg("program"), py::arg("slot"), py::arg("pg"),
+           py::arg("out"), py::arg("input"), py::arg("sync") = false, py::arg("name") = "")
+      .def("add_all_gather", &StepRunner::add_all_gather, py::arg("program"), py::arg("slot"), py::arg("pg"),
+           py::arg("out"), py::arg("input"), py::arg("name") = "")
       .def("add_wait", &StepRunner::add_wait, py::arg("program"), py::arg("slot"), py::arg("name") = "")
       .def("run", &StepRunner::run)
       .def("reset_slots", &StepRunner::reset_slots)

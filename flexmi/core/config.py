@@ -52,6 +52,7 @@ class FFConfig:
         self.use_hip_graphs = False     # capture the steady-state iteration (Legion tracing analogue)
         self.grad_bucket_mb = 32.0      # all-reduce bucket size (xGMI ring: fewer, larger buckets)
         self.overlap_grad_sync = True
+        self.zero_stage = 0             # 1: shard optimizer state over each replica set (ZeRO-1)
         self.machine_file = ""          # simulator machine model override (JSON)
         self.cost_db = ""               # measured per-op cost database (JSON)
         self.strategy_file = ""         # alias of --import (fixes reference caveat C12)
@@ -122,6 +123,10 @@ class FFConfig:
                 self.compute_dtype = nxt()
             elif a == "--hip-graphs":
                 self.use_hip_graphs = True
+            elif a == "--zero":
+                self.zero_stage = 1
+            elif a == "--zero-stage":
+                self.zero_stage = int(nxt())
             elif a == "--bucket-mb":
                 self.grad_bucket_mb = float(nxt())
             elif a == "--machine":

@@ -76,6 +76,33 @@ class Comm:
             w.wait()
         return t
 
+    def reduce_scatter_async(self, out: torch.Tensor, inp: torch.Tensor, ranks=None):
+        """out = this rank's 1/n slice of sum over the group of ``inp`` (ZeRO-1 gradient shards)."""
+        if self.world == 1 or (ranks is not None and len(set(ranks)) == 1):
+            out.copy_(inp)
+            return None
+        g = self.group_for(ranks) if ranks is not None else None
+        self.calls += 1
+        self.bytes_sent += inp.numel() * inp.element_size()
+        return dist.reduce_scatter_tensor(out, inp, group=g, async_op=True)
+
+    def reduce_scatter(self, out, inp, ranks=None):
+        w = self.reduce_scatter_async(out, inp, ranks)
+        if w is not None:
+            w.wait()
+        return out
+
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor, ranks=None):
+        """out = concat over the group (rank order) of ``inp``; blocking."""
+        if self.world == 1 or (ranks is not None and len(set(ranks)) == 1):
+            out.copy_(inp)
+            return out
+        g = self.group_for(ranks) if ranks is not None else None
+        self.calls += 1
+        self.bytes_sent += inp.numel() * inp.element_size()
+        dist.all_gather_into_tensor(out, inp, group=g)
+        return out
+
     def all_reduce_op(self, t: torch.Tensor, ranks=None, op="sum"):
         """Blocking all-reduce with an explicit reduction (sum | max | min)."""
         if self.world == 1:

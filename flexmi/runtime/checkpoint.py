@@ -61,6 +61,7 @@ def save_checkpoint(model, path, extra: Dict = None):
         torch.cuda.synchronize()
     entries = []
     keys = _keys(model)
+    ex.zero_materialize_state()          # ZeRO-1: gather the sharded optimizer state (collective)
     for e in ex.wentries.values():
         if e.box is None or (e.holders and e.holders[0] != rank):
             continue
@@ -74,6 +75,7 @@ def save_checkpoint(model, path, extra: Dict = None):
                         "box": [list(b) for b in e.box], "file": f, "states": sorted(e.state)})
     with open(os.path.join(path, f"r{rank}", "shards.json"), "w") as fh:
         json.dump(entries, fh)
+    ex.zero_release_state()
     ex.comm.barrier()
     if rank == 0:
         opt = model.optimizer
@@ -117,6 +119,7 @@ def load_checkpoint(model, path, strict=True):
         return cache[f]
 
     keys = _keys(model)
+    ex.zero_materialize_state()
     for e in ex.wentries.values():
         if e.box is None:
             continue
@@ -150,6 +153,7 @@ def load_checkpoint(model, path, strict=True):
             covered += vol
         if strict and covered != e.numel:
             raise ValueError(f"{name}: checkpoint covers {covered} of {e.numel} local elements")
+    ex.zero_release_state(scatter=True)
     for g in ex.groups:
         if g.compute is not g.master:
             g.compute.copy_(g.master)

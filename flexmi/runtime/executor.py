@@ -263,13 +263,32 @@ class NativeRunner:
             b = g.buckets[bi]
             rt.add_all_reduce(pid, self.slot(("ar", id(g), bi)), self._pg(g.holders), g.gradbuf[b[0]:b[1]], False,
                               it.name)
+        elif kind == "rs":
+            g, bi = nat[1], nat[2]
+            b = g.buckets[bi]
+            sh = ex._zero_pieces(g)[bi][1]
+            rt.add_reduce_scatter(pid, self.slot(("ar", id(g), bi)), self._pg(g.holders), g.gshard[sh],
+                                  g.gradbuf[b[0]:b[1]], False, it.name)
         elif kind == "ar_sync":
             for g in ex.groups:
                 if not g.replicated:
                     continue
                 for bi, b in enumerate(g.buckets):
+                    if g.zero:
+                        sh = ex._zero_pieces(g)[bi][1]
+                        rt.add_reduce_scatter(pid, self.slot(("ar", id(g), bi)), self._pg(g.holders), g.gshard[sh],
+                                              g.gradbuf[b[0]:b[1]], True, f"{it.name}.bucket{bi}")
+                        continue
                     rt.add_all_reduce(pid, self.slot(("ar", id(g), bi)), self._pg(g.holders), g.gradbuf[b[0]:b[1]],
                                       True, f"{it.name}.bucket{bi}")
+        elif kind == "ag_sync":
+            for g in ex.groups:
+                if not g.zero:
+                    continue
+                for bi, (fsl, sh) in enumerate(ex._zero_pieces(g)):
+                    b = g.buckets[bi]
+                    rt.add_all_gather(pid, self.slot(("ag", id(g), bi)), self._pg(g.holders), g.master[b[0]:b[1]],
+                                      g.mshard[sh], f"{it.name}.bucket{bi}")
         else:
             raise ValueError(f"unknown native item {kind}")
 
@@ -494,6 +513,8 @@ class SyncGroup:
         self.entries: List[WeightEntry] = []
         self.numel = 0
         self.buckets = []  # list of (start, end, set(entry ids))
+        self.zero = False   # ZeRO-1 sharded optimizer state (Executor._zero_layout)
+        self.shard_numel = 0
 
     @property
     def replicated(self):
@@ -799,7 +820,7 @@ class Executor:
         groups = []
         for op in ops:
             c = self.ctx.get(op.guid)
-            if c is None or op.op_type != OperatorType.OP_EMBEDDING:
+            if c is None or op.op_type != OperatorType.OP_EMBEDDING or getattr(op, "host_exec", False):
                 continue
             pc = self.pcs[op.guid]
             for g in groups:
@@ -831,6 +852,18 @@ class Executor:
                 if e.box is None:
                     continue
                 from flexmi.core.types import OperatorType
+                if pc.device_type == ParallelConfig.CPU:
+                    # heterogeneous placement (dlrm_strategy_hetero.cc): the table
+                    # lives in (pinned) host memory and its lookups / sparse SGD run on the host
+                    if op.op_type != OperatorType.OP_EMBEDDING or not sparse_ok:
+                        raise NotImplementedError(f"{op.name}: CPU placement is supported for embedding "
+                                                  "tables trained with SGD (the reference's hetero strategy)")
+                    e.sparse = True
+                    op.sparse_sgd = True
+                    op.host_exec = True
+                    e.master = torch.empty(e.shape, dtype=torch.float32, pin_memory=self.backend == "hip")
+                    e.compute = e.master
+                    continue
                 if (op.op_type == OperatorType.OP_EMBEDDING and sparse_ok and lays[wi].replication() == 1):
                     e.sparse = True
                     op.sparse_sgd = True
@@ -847,21 +880,32 @@ class Executor:
                 g.entries.append(e)
         self.groups = list(groups.values())
         mixed = self.cdtype != torch.float32
+        cap = max(1, int(self.cfg.grad_bucket_mb * (1 << 20) / 4))
+        zero = int(getattr(self.cfg, "zero_stage", 0)) >= 1
         for g in self.groups:
+            g.zero = zero and g.replicated
+            if g.zero:
+                self._zero_layout(g, cap)
             g.master = self._alloc((g.numel,), torch.float32)
             g.gradbuf = self._alloc((g.numel,), torch.float32)
             g.gradbuf.zero_()
             g.compute = self._alloc((g.numel,), self.cdtype) if mixed else g.master
-            g.state = {n: torch.zeros(g.numel, dtype=torch.float32, device=self.device)
-                       for n in (self.optimizer.state_names() if self.optimizer else [])}
+            snames = self.optimizer.state_names() if self.optimizer else []
+            # ZeRO-1: optimizer state exists only for this rank's shard of every bucket
+            g.state = {n: torch.zeros(g.shard_numel if g.zero else g.numel, dtype=torch.float32, device=self.device)
+                       for n in snames}
+            if g.zero:
+                g.gshard = self._alloc((g.shard_numel,), torch.float32)
+                g.mshard = self._alloc((g.shard_numel,), torch.float32)
             for e in g.entries:
                 sl = slice(e.offset, e.offset + e.numel)
                 e.master = g.master[sl].view(e.shape)
                 e.grad = g.gradbuf[sl].view(e.shape)
                 e.compute = g.compute[sl].view(e.shape)
-                e.state = {n: s[sl].view(e.shape) for n, s in g.state.items()}
+                e.state = {} if g.zero else {n: s[sl].view(e.shape) for n, s in g.state.items()}
+            if g.zero:
+                continue
             # buckets (only meaningful for replicated groups)
-            cap = max(1, int(self.cfg.grad_bucket_mb * (1 << 20) / 4))
             start, ids = 0, set()
             for e in g.entries:
                 end = e.offset + (e.numel + 63) // 64 * 64
@@ -890,9 +934,104 @@ class Executor:
         for g in self.groups:
             if g.compute is not g.master:
                 g.compute.copy_(g.master)
+            if g.zero:
+                for full, sh in self._zero_pieces(g):
+                    g.mshard[sh].copy_(g.master[full])
         lr = getattr(self.optimizer, "lr", 0.01) if self.optimizer else 0.0
         self.lr_tensor = torch.tensor([lr], dtype=torch.float32, device=self.device)
         self.pending = {}
+
+    # ------------------------------------------------------------------ ZeRO-1 (SURVEY §2.5 P13)
+    # Optimizer-state sharding for replicated weight groups.  Every gradient bucket is padded to a
+    # multiple of (replicas x 64) elements; backward reduce-scatters each bucket as soon as it is
+    # final (RCCL ring reduce-scatter: half the bytes of the all-reduce it replaces), each replica
+    # updates only its 1/R slice of every bucket -- fp32 master shard + optimizer state exist for
+    # that slice only -- and the update all-gathers the fresh master slices back into the full
+    # replicated buffer (the other half of the ring all-reduce).  Same bytes on xGMI as plain DP,
+    # 1/R of the optimizer state and optimizer-kernel work per GPU.
+    def _zero_layout(self, g, cap):
+        R = len(g.holders)
+        quant = R * 64
+        off = start = 0
+        ids = set()
+        g.buckets = []
+        for e in g.entries:
+            sz = (e.numel + 63) // 64 * 64
+            if ids and off + sz - start > cap:
+                end = start + -(-(off - start) // quant) * quant
+                g.buckets.append([start, end, ids])
+                start = off = end
+                ids = set()
+            e.offset = off
+            off += sz
+            ids.add(e.param.guid)
+        end = start + -(-(off - start) // quant) * quant
+        g.buckets.append([start, end, ids])
+        g.numel = end
+        g.zero_rank = sorted(g.holders).index(self.rank)
+        g.zero_R = R
+        g.shard_numel = sum((b[1] - b[0]) // R for b in g.buckets)
+
+    def _zero_pieces(self, g):
+        """[(slice of the full flat buffer owned by this rank, slice of the shard buffers)] per bucket."""
+        out, so = [], 0
+        for b0, b1, _ in g.buckets:
+            n = (b1 - b0) // g.zero_R
+            lo = b0 + g.zero_rank * n
+            out.append((slice(lo, lo + n), slice(so, so + n)))
+            so += n
+        return out
+
+    def _zero_rs(self, g, bi, sync=True):
+        b0, b1, _ = g.buckets[bi]
+        sh = self._zero_pieces(g)[bi][1]
+        return self.comm.reduce_scatter_async(g.gshard[sh], g.gradbuf[b0:b1], g.holders) if not sync else \
+            self.comm.reduce_scatter(g.gshard[sh], g.gradbuf[b0:b1], g.holders)
+
+    def _zero_gather(self):
+        for g in self.groups:
+            if not g.zero:
+                continue
+            for bi, (full, sh) in enumerate(self._zero_pieces(g)):
+                b0, b1, _ = g.buckets[bi]
+                self.comm.all_gather(g.master[b0:b1], g.mshard[sh], g.holders)
+
+    def _zero_cast(self):
+        for g in self.groups:
+            if g.zero and g.compute is not g.master:
+                g.compute.copy_(g.master)
+
+    def zero_materialize_state(self):
+        """Collective: full-size optimizer state for every ZeRO group (entries' ``state`` views
+        point into it) -- for checkpointing, which stores per-parameter state."""
+        for g in self.groups:
+            if not g.zero:
+                continue
+            g.state_full = {}
+            for n, st in g.state.items():
+                full = torch.zeros(g.numel, dtype=torch.float32, device=self.device)
+                for bi, (fsl, sh) in enumerate(self._zero_pieces(g)):
+                    b0, b1, _ = g.buckets[bi]
+                    self.comm.all_gather(full[b0:b1], st[sh].contiguous(), g.holders)
+                g.state_full[n] = full
+            for e in g.entries:
+                sl = slice(e.offset, e.offset + e.numel)
+                e.state = {n: f[sl].view(e.shape) for n, f in g.state_full.items()}
+
+    def zero_release_state(self, scatter=False):
+        """Drop the full-size state views; with ``scatter`` (after a load) keep this rank's slice."""
+        for g in self.groups:
+            if not g.zero or getattr(g, "state_full", None) is None:
+                continue
+            if scatter:
+                for n, st in g.state.items():
+                    for fsl, sh in self._zero_pieces(g):
+                        st[sh].copy_(g.state_full[n][fsl])
+                for fsl, sh in self._zero_pieces(g):
+                    g.mshard[sh].copy_(g.master[fsl])
+            g.state_full = None
+            for e in g.entries:
+                e.state = {}
 
     def set_lr(self, lr):
         self.lr_tensor.fill_(float(lr))
@@ -1016,6 +1155,9 @@ class Executor:
             upd.append(Item("comm", self._sync_grads, "allreduce.wait", native=("ar_sync",)))
         if self.optimizer is not None:
             C(upd, "update", self._optimizer_step)
+            if any(g.zero for g in self.groups):
+                upd.append(Item("comm", self._zero_gather, "zero.allgather", native=("ag_sync",)))
+                C(upd, "zero.cast", self._zero_cast)
         self.prog_fwd, self.prog_bwd, self.prog_upd = fwd, bwd, upd
 
     def _emit_exchange_start(self, lst, ex, name):
@@ -1036,7 +1178,8 @@ class Executor:
                 fwd.append(Item("compute", (lambda grp=grp: type(grp[0]).forward_group(grp, [self.ctx[o.guid] for o in grp])),
                                 op.name + ".group_fwd"))
             return
-        fwd.append(Item("compute", (lambda op=op, c=c: self._fwd_op(op, c)), op.name + ".fwd"))
+        kind = "comm" if getattr(op, "host_exec", False) else "compute"   # host ops are never captured
+        fwd.append(Item(kind, (lambda op=op, c=c: self._fwd_op(op, c)), op.name + ".fwd"))
         fwd[-1].check = (lambda op=op, c=c: self._check_op(op.name + ".fwd", c.outputs, "output"))
 
     def _compile_backward(self, bwd, C):
@@ -1089,13 +1232,18 @@ class Executor:
                             C(bwd, op.name + ".group_bwd",
                               (lambda grp=grp: type(grp[0]).backward_group(grp, [self.ctx[o.guid] for o in grp])))
                     else:
-                        C(bwd, op.name + ".bwd", (lambda op=op, c=c, flags=flags: self._bwd_op(op, c, flags)))
+                        bwd.append(Item("comm" if getattr(op, "host_exec", False) else "compute",
+                                        (lambda op=op, c=c, flags=flags: self._bwd_op(op, c, flags)), op.name + ".bwd"))
                         bwd[-1].check = (lambda op=op, c=c: self._check_op(op.name + ".bwd", c.in_grads, "input grad"))
                     for i, t in enumerate(op.inputs):
                         if c.in_grads[i] is not None and self.need[(op.guid, i)].same_as(self.home[t.guid]):
                             written.add(self.gkey(t.guid))
-                # gradient buckets completed by this op -> async all-reduce (overlaps the rest of bwd)
-                for w in op.weights:
+                # gradient buckets completed by this op -> async all-reduce (overlaps the rest of bwd).
+                # A fused group's members all run backward at the group's step (grp[0]): their
+                # weight gradients are final only there, not at the members' own positions.
+                grp = self.group_of.get(op.guid)
+                done_ops = [op] if grp is None else (list(grp) if grp[0] is op else [])
+                for w in [w for o in done_ops for w in o.weights]:
                     uses_left[w.guid] -= 1
                     e = self.wentries.get(w.guid)
                     if e is None or e.group is None or not e.group.replicated or uses_left[w.guid] > 0:
@@ -1105,8 +1253,12 @@ class Executor:
                         if w.guid in b[2]:
                             bucket_left[id(g)][bi] -= 1
                             if bucket_left[id(g)][bi] == 0 and self.cfg.overlap_grad_sync:
-                                bwd.append(Item("comm", (lambda g=g, bi=bi: self._launch_bucket(g, bi)),
-                                                f"allreduce.bucket{bi}", native=("ar", g, bi)))
+                                if g.zero:
+                                    bwd.append(Item("comm", (lambda g=g, bi=bi: self._launch_bucket(g, bi)),
+                                                    f"reducescatter.bucket{bi}", native=("rs", g, bi)))
+                                else:
+                                    bwd.append(Item("comm", (lambda g=g, bi=bi: self._launch_bucket(g, bi)),
+                                                    f"allreduce.bucket{bi}", native=("ar", g, bi)))
             else:
                 items, seen = [], set()
                 for op, i, g, rs in st[1]:
@@ -1129,12 +1281,41 @@ class Executor:
 
     def _fwd_op(self, op, c):
         c.training = self.training
+        if getattr(op, "host_exec", False):
+            return self._host_op(op, c, "forward")
         op.forward(c)
 
     def _bwd_op(self, op, c, flags):
         for i, f in enumerate(flags):
             c.in_grad_accumulate[i] = f
+        if getattr(op, "host_exec", False):
+            return self._host_op(op, c, "backward")
         op.backward(c)
+
+    def _host_op(self, op, c, phase):
+        """A CPU-placed op (P6) runs its CPU (fp32 torch) path on the host: host copies of the
+        device inputs / output grads in, forward outputs back to the device buffers (H2D).  Its
+        weights -- a host-resident table -- are updated in place by the host sparse SGD."""
+        h = c.saved.get("host_ctx")
+        if h is None:
+            h = OpCtx(op, self.rank, "cpu", torch.float32)
+            h.w_boxes, h.weights, h.wcompute = c.w_boxes, c.weights, c.wcompute
+            h.weight_grads = [None] * len(c.weights)
+            h.in_boxes, h.out_boxes = c.in_boxes, c.out_boxes
+            h.outputs = [torch.empty(tuple(o.shape), dtype=torch.float32) for o in c.outputs]
+            h.in_grads = [None] * len(c.inputs)
+            h.in_grad_accumulate = [False] * len(c.inputs)
+            c.saved["host_ctx"] = h
+        h.training = c.training
+        h.inputs = [x.cpu() if x is not None else None for x in c.inputs]
+        if phase == "forward":
+            op.forward(h)
+            for dev, host in zip(c.outputs, h.outputs):
+                dev.copy_(host)
+        else:
+            h.out_grads = [g.float().cpu() if g is not None else None for g in c.out_grads]
+            h.lr = self.lr_tensor.cpu()
+            op.backward(h)
 
     def _emit_reshards(self, lst, items, name):
         if not items:
@@ -1244,6 +1425,9 @@ class Executor:
 
     def _launch_bucket(self, g, bi):
         b = g.buckets[bi]
+        if g.zero:
+            g.works[bi] = self._zero_rs(g, bi, sync=False)
+            return
         g.works[bi] = self.comm.all_reduce_async(g.gradbuf[b[0]:b[1]], g.holders)
 
     def _sync_grads(self):
@@ -1253,7 +1437,8 @@ class Executor:
             for bi, b in enumerate(g.buckets):
                 w = g.works[bi]
                 if w is None:
-                    w = self.comm.all_reduce_async(g.gradbuf[b[0]:b[1]], g.holders)
+                    w = self._zero_rs(g, bi, sync=False) if g.zero else \
+                        self.comm.all_reduce_async(g.gradbuf[b[0]:b[1]], g.holders)
                 if w is not None:
                     w.wait()
                 g.works[bi] = None
@@ -1269,6 +1454,9 @@ class Executor:
             st[2:3].copy_(opt.alpha * torch.sqrt(1 - st[1:2]) / (1 - st[0:1]))
         for g in self.groups:
             if g.numel == 0:
+                continue
+            if g.zero:
+                self._zero_opt_step(g, opt)
                 continue
             comp = g.compute if g.compute is not g.master else None
             if self.backend == "hip":
@@ -1294,6 +1482,32 @@ class Executor:
                     g.master.sub_(self.adam_state[2] * m_ / (v_.sqrt() + opt.epsilon))
                 if comp is not None:
                     comp.copy_(g.master)
+
+    def _zero_opt_step(self, g, opt):
+        """The optimizer on this rank's shard: fp32 master shard, reduce-scattered gradient shard
+        and the sharded state, one fused kernel launch over the whole shard buffer (the slices of
+        all buckets are packed back to back)."""
+        from flexmi.ops import _kernels as K
+        m, gr, st = g.mshard, g.gshard, g.state
+        if self.backend == "hip":
+            if isinstance(opt, SGDOptimizer):
+                K.sgd_update(m, gr, st.get("v"), None, self.lr_tensor, opt.weight_decay, opt.momentum, opt.nesterov)
+            else:
+                K.adam_update(m, gr, st["m"], st["v"], None, self.adam_state[2:3], opt.beta1, opt.beta2,
+                              opt.weight_decay, opt.epsilon)
+        elif isinstance(opt, SGDOptimizer):
+            gt = gr + opt.weight_decay * m
+            if opt.momentum > 0:
+                v = st["v"]
+                v.mul_(opt.momentum).add_(gt)
+                gt = gt + opt.momentum * v if opt.nesterov else v
+            m.sub_(self.lr_tensor * gt)
+        else:
+            gt = gr + opt.weight_decay * m
+            m_, v_ = st["m"], st["v"]
+            m_.mul_(opt.beta1).add_((1 - opt.beta1) * gt)
+            v_.mul_(opt.beta2).add_((1 - opt.beta2) * gt * gt)
+            m.sub_(self.adam_state[2] * m_ / (v_.sqrt() + opt.epsilon))
 
     # ------------------------------------------------------------------ loss
     def _loss_kernel(self, compute_grad):
@@ -1364,6 +1578,9 @@ class Executor:
         e.master.copy_(full[_slices(e.box, tuple((0, 0) for _ in e.box))].to(e.master.dtype))
         if e.compute is not e.master and e.compute is not None:
             e.compute.copy_(e.master)
+        if e.group is not None and e.group.zero:
+            for fsl, sh in self._zero_pieces(e.group):
+                e.group.mshard[sh].copy_(e.group.master[fsl])
 
     def load_batch(self, t, full_batch: torch.Tensor, start=0):
         """Copy this rank's shard of rows [start, start+B) of a host/device array into the
@@ -1485,6 +1702,6 @@ class Executor:
         for v in self.act.values():
             if v is not None:
                 n += v.numel() * v.element_size()
-        w = sum(g.numel * 4 * (2 + len(g.state)) for g in self.groups)
+        w = sum(g.numel * 4 * 2 + sum(t.numel() for t in g.state.values()) * 4 for g in self.groups)
         sp = sum(e.numel * 4 for e in self.wentries.values() if e.sparse)
         return {"activations": n, "dense_params": w, "sparse_tables": sp}

@@ -29,6 +29,9 @@ def _model(world, strategy, opt):
     from flexmi.parallel.layout import ParallelConfig
     cfg = FFConfig()
     cfg.device, cfg.compute_dtype, cfg.batchSize = "cpu", "fp32", 16
+    if strategy.endswith("_zero"):        # ZeRO-1: optimizer state sharded over the replicas
+        cfg.zero_stage, cfg.grad_bucket_mb = 1, 0.002
+        strategy = strategy[:-5]
     m = FFModel(cfg)
     d, s, _ = build_dlrm(m, DLRMConfig.preset("tiny"))
     strat = {}
@@ -100,7 +103,8 @@ def _launch(world, strategy, opt, ckpt, mode):
 
 @pytest.mark.parametrize("opt", ["sgd", "adam"])
 @pytest.mark.parametrize("save_w,save_s,load_w,load_s", [(2, "table", 1, "dp"), (1, "dp", 2, "colsplit"),
-                                                         (2, "colsplit", 2, "table")])
+                                                         (2, "colsplit", 2, "table"), (2, "dp_zero", 1, "dp"),
+                                                         (1, "dp", 2, "dp_zero"), (2, "table_zero", 2, "dp_zero")])
 def test_resume_under_another_strategy(tmp_path, opt, save_w, save_s, load_w, load_s):
     ref = _launch(1, "dp", opt, None, "full")
     ck = str(tmp_path / "ck")
@@ -108,5 +112,7 @@ def test_resume_under_another_strategy(tmp_path, opt, save_w, save_s, load_w, lo
     assert os.path.exists(os.path.join(ck, "manifest.json")) and os.path.exists(os.path.join(ck, "strategy.pb"))
     got = _launch(load_w, load_s, opt, ck, "load")
     assert len(got) == len(ref)
+    # reduce-scatter sums in another order than the all-reduce: ZeRO runs agree to fp32 rounding
+    tol = dict(rtol=1e-4, atol=1e-5) if "zero" in save_s + load_s else dict(rtol=1e-5, atol=1e-6)
     for a, b in zip(got, ref):
-        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(a, b, **tol)

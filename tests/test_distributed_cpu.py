@@ -44,6 +44,19 @@ def _build(case, world):
         o = m.softmax(m.dense(h, 4, name="fc3"), name="sm")
         loss = LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY
         inputs["x"] = (x, (B, 12), "f")
+    dp_small = case.endswith("_dpsmall")
+    if dp_small:
+        # pure DP (replicated tables, dense grads) with tiny buckets: a bucket may only be reduced
+        # once the fused embedding group's backward has produced every member's gradient
+        case = case[:-8]
+        cfg.grad_bucket_mb = 0.002
+    zero = case.endswith("_zero")
+    if zero:
+        # ZeRO-1: sharded optimizer state, reduce-scatter + all-gather instead of all-reduce;
+        # tiny buckets so several padded buckets (and a padded tail) exist
+        case = case[:-5]
+        cfg.zero_stage = 1
+        cfg.grad_bucket_mb = 0.002
     if case in ("mlp_dp", "mlp_channel"):
         x = m.create_tensor([B, 12], name="x")
         h = m.dense(x, 16, ActiMode.AC_MODE_RELU, name="fc1")
@@ -65,7 +78,7 @@ def _build(case, world):
         inputs["dense"] = (d, (B, 13), "f")
         for i, (t, r) in enumerate(zip(s, dcfg.embedding_size)):
             inputs[f"sparse{i}"] = (t, (B, 1), ("i", r))
-        if world > 1:
+        if world > 1 and not dp_small:
             strat = dlrm_strategy(m, world)
             if case == "dlrm_search":
                 # strategy chosen by the MCMC search over the MI355X simulator (same seed on
@@ -105,7 +118,14 @@ def _build(case, world):
             strat["pool1"] = ParallelConfig([1, world, 1, 1], list(range(world)))
             strat["conv2"] = ParallelConfig([world, 1, 1, 1], list(range(world)))
     m.strategies = strat
-    m.compile(SGDOptimizer(m, 0.1), loss, [MetricsType.METRICS_ACCURACY])
+    if zero and case == "mlp_dp":
+        from flexmi.core import AdamOptimizer
+        opt = AdamOptimizer(m, 0.01)
+    elif zero:
+        opt = SGDOptimizer(m, 0.1, momentum=0.9, weight_decay=0.01)
+    else:
+        opt = SGDOptimizer(m, 0.1)
+    m.compile(opt, loss, [MetricsType.METRICS_ACCURACY])
     m.strategies = strat
     return m, inputs
 
@@ -131,6 +151,11 @@ def _run(case, world, rank, steps, out_path):
             la = rng.randint(0, 2, lab.dims).astype(np.float32)
         ex.scatter_from_host(lab, la)
         ex.train_step()
+    if m.config.zero_stage and world > 1:
+        zg = [g for g in ex.groups if g.zero]
+        assert zg and all(len(g.buckets) > 1 for g in zg), "ZeRO groups / buckets missing"
+        for g in zg:   # optimizer state really is sharded
+            assert all(t.numel() * len(g.holders) == g.numel for t in g.state.values())
     params = [p.get_weights(m) for p in m.parameters]
     loss = m.get_perf_metrics().get_loss()
     nr = ex.native_runner()
@@ -164,7 +189,8 @@ def _launch(case, world, steps=3):
 @pytest.mark.parametrize("case,world", [("mlp_dp", 2), ("mlp_tied", 2), ("mlp_channel", 2), ("mlp_channel", 4), ("dlrm_dot", 2),
                                         ("dlrm_cat", 2), ("dlrm_colsplit", 2), ("cnn_spatial", 2),
                                         ("dlrm_search", 2), ("dlrm_search", 4), ("dlrm_rowsplit", 2),
-                                        ("dlrm_rowsplit", 4)])
+                                        ("dlrm_rowsplit", 4), ("mlp_dp_zero", 2), ("dlrm_dot_zero", 2),
+                                        ("mlp_dp_zero", 4), ("dlrm_cat_dpsmall", 2)])
 def test_strategy_equivalence(case, world):
     ref = _launch(case, 1)
     got = _launch(case, world)

@@ -66,6 +66,37 @@ def test_gemm_splitk_and_batch(gpu):
     assert rel_err(O, bf(X).float() @ bf(Y).float()) < 1e-2
 
 
+@pytest.mark.parametrize("ks", [2, 3, 4])
+@pytest.mark.parametrize("M,N,c_fp32,kc", [(1024, 1024, True, False), (200, 130, True, False), (256, 96, False, False),
+                                           (77, 50, False, False), (2048, 2048, True, True)])
+def test_gemm_splitk_inlaunch_combine(gpu, ks, M, N, c_fp32, kc):
+    """Split-K slices combined INSIDE the launch by each tile's last arriving block (write-through
+    slabs + agent-scope ticket): bias + relu + beta accumulate, fp32 and bf16 C, ragged N, the
+    register-staged and the LDS-DMA kernels; repeated launches reuse the self-resetting counters."""
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(3)
+    K = 4096
+    A, B = torch.randn(K, M, device=gpu), torch.randn(K, N, device=gpu)
+    bias = torch.randn(N, device=gpu)
+    dt = torch.float32 if c_fp32 else torch.bfloat16
+    C = torch.randn(M, N, device=gpu).to(dt)
+    acc = C.float().clone()
+    ref = torch.relu(bf(A).float().t() @ bf(B).float() + bias)
+    if kc:
+        Ab, lda, Bb, ldb = bf(A.t().contiguous()), K, bf(B.t().contiguous()), K
+    else:
+        Ab, lda, Bb, ldb = bf(A), M, bf(B), N
+    Kk.C().gemm_set_variant(128)        # opt-in path (measured slower on DLRM; kept correct)
+    try:
+        for rep in range(3):
+            got = Kk.gemm(Ab, lda, kc, Bb, ldb, kc, C, N, M, N, K, bias=bias, act=11, beta=True, ksplit=ks)
+            assert got == ks
+            acc = acc + ref
+            assert rel_err(C, acc) < (2e-3 if c_fp32 else 2e-2), (rep, ks, M, N, kc)
+    finally:
+        Kk.C().gemm_set_variant(0)
+
+
 def test_init_fill_matches_cpu(gpu):
     from flexmi.core.initializers import NormInitializer, UniformInitializer
     for init in [UniformInitializer(7, -0.5, 0.5), NormInitializer(9, 0.0, 2.0)]:
