@@ -6,8 +6,9 @@
 //   G = Z Z^T with v_mfma_f32_32x32x16_bf16: the A and B fragments of a Gram matrix are the SAME
 //   register (lane l holds Z[l&31][k0 + 8(l>>5) .. +7]), D/16 MFMAs per sample;
 //   out[b] = [x | strictly-lower(G) | 0-pad] assembled in LDS and written with 16-B stores.
-// Backward: S = dG + dG^T built in LDS from dOut's packed triangle; dZ = S Z with the same MFMA
-//   (A = S rows via ds_read_b128, B = Z columns via the transposing ds_read_b64_tr_b16);
+// Backward: S = dG + dG^T gathered from dOut's packed triangle; dZ = S Z with the same MFMA
+//   (A = S rows gathered per lane from the staged dOut row with precomputed positions, B = Z
+//   columns via the transposing ds_read_b64_tr_b16);
 //   dZ_0 += dOut[:, :D].  Inputs/grads are pointer tables, so it also reads/writes concat slices.
 #include "common.h"
 
@@ -207,11 +208,34 @@ __global__ void __launch_bounds__(256) fm_dot_bwd_t(PtrTab Z, long ldz, const un
   constexpr int NT = DT / 32;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wpad = (W + 7) & ~7;
-  char* base = smem + wave * (32 * DT * 2 + 32 * 32 * 2 + wpad * 2);
+  char* base = smem + wave * (32 * DT * 2 + wpad * 2);
   unsigned short* zs = reinterpret_cast<unsigned short*>(base);                        // [32][DT]
-  unsigned short* ss = reinterpret_cast<unsigned short*>(base + 32 * DT * 2);          // [32][32]
-  unsigned short* ds = reinterpret_cast<unsigned short*>(base + 32 * DT * 2 + 2048);   // dOut row [W]
+  unsigned short* ds = reinterpret_cast<unsigned short*>(base + 32 * DT * 2);          // dOut row [W]
   const int waves_total = gridDim.x * (blockDim.x >> 6);
+  // MFMA A operand of dZ = S Z (S = dG + dG^T from dOut's packed triangle) straight from the staged
+  // dOut row: lane (r = lane&31, h = lane>>5) holds S[r][16ks + 8h + e], whose dOut position is
+  // the same for every sample -- computed once here instead of building S in LDS per sample
+  short apos[2][8];           // -1: zero entry
+  unsigned dmask = 0;         // diagonal entries (self interaction: 2 x dG_ii)
+  {
+    const int r = lane & 31;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int j = 16 * ks + 8 * (lane >> 5) + e;
+        int pos = -1;
+        if (r < F && j < F) {
+          if (r > j) pos = pair_pos(r, j, self);
+          else if (j > r) pos = pair_pos(j, r, self);
+          else if (self) {
+            pos = pair_pos(r, r, self);
+            dmask |= 1u << (8 * ks + e);
+          }
+        }
+        apos[ks][e] = (short)pos;
+      }
+  }
   // persistent waves with the next sample's Z rows and dOut row prefetched into registers
   // (clamped addresses: every load unconditional) while this sample is processed
   const bool dload = lane * 8 < W;
@@ -243,18 +267,17 @@ __global__ void __launch_bounds__(256) fm_dot_bwd_t(PtrTab Z, long ldz, const un
     if (dload) *reinterpret_cast<u32x4_t*>(ds + lane * 8) = dv;
     FM_WAVE_LDS_SYNC();
     const unsigned short* dp = ds + DT;
-#pragma unroll 4
-    for (int e = lane; e < 32 * 32; e += 64) {
-      int i = e >> 5, j = e & 31;
-      float v = 0.f;
-      if (i < F && j < F) {
-        if (i > j) v = bf2f(dp[pair_pos(i, j, self)]);
-        else if (j > i) v = bf2f(dp[pair_pos(j, i, self)]);
-        else if (self) v = 2.f * bf2f(dp[pair_pos(i, i, self)]);
+    bf16x8_t afr[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int pos = apos[ks][e];
+        float v = bf2f(dp[pos < 0 ? 0 : pos]);      // unconditional (clamped) LDS read
+        v = pos < 0 ? 0.f : v;
+        if ((dmask >> (8 * ks + e)) & 1u) v *= 2.f;
+        afr[ks][e] = (short)f2bf(v);
       }
-      ss[e] = f2bf(v);
-    }
-    FM_WAVE_LDS_SYNC();
     const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
     f32x16_t acc[NT];
 #pragma unroll
@@ -263,7 +286,7 @@ __global__ void __launch_bounds__(256) fm_dot_bwd_t(PtrTab Z, long ldz, const un
       for (int t = 0; t < 16; ++t) acc[nt][t] = 0.f;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(ss + (lane & 31) * 32 + 16 * ks + 8 * (lane >> 5));
+        bf16x8_t a = afr[ks];
         int krow = 16 * ks + 8 * (g >> 1) + q;
         int col = 32 * nt + 16 * (g & 1) + 4 * p;
         bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4_t*)(zs + krow * DT + col));
@@ -357,7 +380,7 @@ extern "C" void fm_dot_interaction_bwd(const void* const* z, int F, long ldz, co
   for (int i = 0; i < F; ++i) fast = fast && al16(z[i]) && (dz[i] == nullptr || al16(dz[i]));
   if (fast) {
     auto k = D == 128 ? fm_dot_bwd_t<128> : D == 64 ? fm_dot_bwd_t<64> : fm_dot_bwd_t<32>;
-    size_t lds = waves * (32 * D * 2 + 32 * 32 * 2 + W * 2);
+    size_t lds = waves * (32 * D * 2 + W * 2);
     hipLaunchKernelGGL(k, dim3((int)blocks), dim3(64 * waves), lds, s, t, ldz, (const unsigned short*)dout, ldo, g, lddz,
                        acc_mask, B, F, W, self);
     return;
