@@ -349,9 +349,12 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
   // (measured, tools/bench_gemm.py in hipGraph mode: the pipelined kernel wins for K-contiguous
   // operands once 256x128 tiles fill the chip; MN-contiguous (transposed-read) operands and small
   // grids stay on the register-staged kernel's 128x64/128x128 tiles)
+  // (in the DLRM step, where the 1024-wide layers give exactly 256 such tiles, the register kernel's
+  // 512 blocks of 128x128 beat one wave of 256x128 glds blocks: 11.07 vs 10.86 M samples/s,
+  // profiles/README.md -- so glds starts at two waves of its tiles)
   const long t256 = (long)((M + 255) / 256) * ((N + 127) / 128) * batch;
   if (vec && !no_glds && K > 0 && K % BK == 0 && M >= 8 && N >= 8 &&
-      ((a_kcontig && b_kcontig && t256 >= 256) || glds_any)) {
+      ((a_kcontig && b_kcontig && t256 >= 512) || glds_any)) {
     const int bm = ((g_gemm_variant & 4) || t256 < 256) ? 128 : 256;
     p.tiles_m = (M + bm - 1) / bm;
     p.tiles_n = (N + 127) / 128;
