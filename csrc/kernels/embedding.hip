@@ -15,6 +15,8 @@
 // Backward (fused sparse SGD: W[idx] -= lr*scale*dy; or dense-grad accumulate when lr == null):
 //   * regular tables: one wave-instruction = 64 consecutive fp32 atomic adds (256 contiguous bytes:
 //     the full gfx950 atomic rate, MI355X_MICROARCH "Global float atomics");
+//   * small tables (<= 128 KB of fp32 rows), opt-in: one block-shared LDS copy per block with LDS
+//     atomics, flushed with one global atomic per (row, col) (measured slower, see launch site);
 //   * tiny tables (<= 16 rows: 3, 4, 10, 14 rows in the MLPerf set): thousands of samples hit the
 //     same few addresses, which L2 serialises; each wave accumulates into a PRIVATE LDS copy of the
 //     table gradient with plain read-add-write (row index wave-uniform, lane = column: 64 distinct
@@ -189,6 +191,89 @@ __global__ void __launch_bounds__(256) fm_emb_bwd_tiny_multi(TabSet s, const flo
     const float v = red[i] + red[n + i] + red[2 * n + i] + red[3 * n + i];
     if (v != 0.f) atomicAdd(W + i, v * mul);
   }
+}
+
+// Small tables (16 < rows, rows*D*4 <= SMALL_LDS: e.g. 36..155 rows x 128 in the MLPerf set):
+// 8192 lookups pile onto a few thousand addresses, so the per-lookup global atomics of the regular
+// path serialise in L2.  Each block accumulates a chunk of samples into ONE block-shared LDS copy
+// of the table gradient (ds_add_f32: lane = column, 64 distinct banks per wave-instruction) and
+// flushes it with one global atomic per (row, col); blocks per table are sized so the flush stays
+// well below the B*D atomics it replaces.
+constexpr long SMALL_LDS = 128L << 10;
+template <typename GT, bool I64>
+__global__ void __launch_bounds__(256) fm_emb_bwd_small_multi(TabSet s, const float* __restrict__ lr, long B, int chunk) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* acc = reinterpret_cast<float*>(smem);     // [rows][D]
+  const TabDesc& d = s.t[blockIdx.y];
+  const long b0 = (long)blockIdx.x * chunk;
+  if (b0 >= B) return;                             // block-uniform
+  const long b1 = min(B, b0 + chunk);
+  const int n = d.rows * d.D;
+  for (int i = threadIdx.x; i < n; i += 256) acc[i] = 0.f;
+  __syncthreads();
+  const int lpr = d.D < 256 ? d.D : 256;
+  const int rpi = 256 / lpr;
+  const int sub = threadIdx.x / lpr, lc = threadIdx.x - sub * lpr;
+  const GT* dy = reinterpret_cast<const GT*>(d.act);
+  if (sub < rpi) {
+    for (long bb = b0 + sub; bb < b1; bb += 4L * rpi) {
+      for (int c = lc; c < d.D; c += lpr) {
+        float g[4];
+        long r0[4];
+        bool ok0[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {                // loads first (clamped: unconditional)
+          const long b = min(bb + u * rpi, b1 - 1);
+          g[u] = ld<GT>(dy + b * d.ld + c);
+          r0[u] = local_row(ldi<I64>(d.idx, b * d.bag), d.lo, d.rows, ok0[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const long b = bb + u * rpi;
+          if (b >= b1) break;
+          if (ok0[u]) atomicAdd(acc + r0[u] * d.D + c, g[u]);
+          for (int j = 1; j < d.bag; ++j) {
+            bool ok;
+            const long r = local_row(ldi<I64>(d.idx, b * d.bag + j), d.lo, d.rows, ok);
+            if (ok) atomicAdd(acc + r * d.D + c, g[u]);
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const float mul = (lr ? -lr[0] : 1.f) * d.scale;
+  float* W = const_cast<float*>(d.W);
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const float v = acc[i];
+    if (v != 0.f) atomicAdd(W + i, v * mul);
+  }
+}
+
+template <bool I64>
+void launch_small(const TabSet& s, int m, bool dy_bf16, const float* lr, long B, hipStream_t st) {
+  size_t lds = 0;
+  long maxrows = 1, maxbag = 1;
+  for (int i = 0; i < m; ++i) {
+    lds = std::max(lds, (size_t)s.t[i].rows * s.t[i].D * 4);
+    maxrows = std::max<long>(maxrows, s.t[i].rows);
+    maxbag = std::max<long>(maxbag, s.t[i].bag);
+  }
+  static bool attr = false;
+  if (!attr) {     // > 64 KiB of dynamic LDS needs the opt-in attribute
+    (void)hipFuncSetAttribute((const void*)fm_emb_bwd_small_multi<unsigned short, I64>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)SMALL_LDS);
+    (void)hipFuncSetAttribute((const void*)fm_emb_bwd_small_multi<float, I64>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)SMALL_LDS);
+    attr = true;
+  }
+  // ~4 lookups per table row per block: enough duplication that the flush (rows*D atomics per
+  // block) costs a fraction of the per-lookup atomics it replaces
+  const long blocks = std::max(4L, std::min(32L, B * maxbag / (4 * maxrows)));
+  const int chunk = (int)((B + blocks - 1) / blocks);
+  dim3 grid((unsigned)((B + chunk - 1) / chunk), m);
+  if (dy_bf16) hipLaunchKernelGGL((fm_emb_bwd_small_multi<unsigned short, I64>), grid, dim3(256), lds, st, s, lr, B, chunk);
+  else hipLaunchKernelGGL((fm_emb_bwd_small_multi<float, I64>), grid, dim3(256), lds, st, s, lr, B, chunk);
 }
 
 template <bool I64>
@@ -387,13 +472,23 @@ extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const
       else launch_claim<false>(s, m, dy_bf16, lr, B, maxbag, minD4, st);
     }
   }
-  for (int pass = 0; pass < 4; ++pass) {
-    const bool tiny = pass < 2, wide = pass & 1;
+  // kind: 0 tiny (wave-private LDS copies), 1 small (block-shared LDS copy), 2 regular (atomics)
+  // small path OPT-IN (FM_EMB_SMALL=1): on the MLPerf step it measured 113 us for the four 36..155-row
+  // tables against 16.6 us of regular atomics (profiles/README.md): with 1 block/CU of LDS and ~13
+  // blocks per table the serial LDS atomics are latency-bound, and more blocks multiply the flush
+  static const bool small_on = getenv("FM_EMB_SMALL") != nullptr && atoi(getenv("FM_EMB_SMALL")) == 1;
+  auto kind_of = [&](int k) {
+    if (rows[k] <= TINY_ROWS && D[k] <= 256 && B * (long)bag[k] >= 16L * rows[k]) return 0;
+    if (small_on && (long)rows[k] * D[k] * 4 <= SMALL_LDS && D[k] <= 256 && B * (long)bag[k] >= 8L * rows[k]) return 1;
+    return 2;
+  };
+  for (int pass = 0; pass < 6; ++pass) {
+    const int kind = pass >> 1;
+    const bool tiny = kind == 0, wide = pass & 1;
     std::vector<int> sel;
     for (int k = 0; k < n; ++k) {
       if (claimable(k)) continue;
-      bool t = rows[k] <= TINY_ROWS && D[k] <= 256 && B * (long)bag[k] >= 16L * rows[k];
-      if (t == tiny && (idx64[k] != 0) == wide) sel.push_back(k);
+      if (kind_of(k) == kind && (idx64[k] != 0) == wide) sel.push_back(k);
     }
     for (size_t base = 0; base < sel.size(); base += MAXT) {
       TabSet s;
@@ -405,8 +500,14 @@ extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const
         maxD = std::max(maxD, D[k]);
       }
       s.n = m;
-      if (wide) launch_bwd<true>(s, m, tiny, dy_bf16, lr, B, maxD, st);
-      else launch_bwd<false>(s, m, tiny, dy_bf16, lr, B, maxD, st);
+      if (kind == 1) {
+        if (wide) launch_small<true>(s, m, dy_bf16, lr, B, st);
+        else launch_small<false>(s, m, dy_bf16, lr, B, st);
+      } else if (wide) {
+        launch_bwd<true>(s, m, tiny, dy_bf16, lr, B, maxD, st);
+      } else {
+        launch_bwd<false>(s, m, tiny, dy_bf16, lr, B, maxD, st);
+      }
     }
   }
 }

@@ -97,6 +97,33 @@ def test_gemm_splitk_inlaunch_combine(gpu, ks, M, N, c_fp32, kc):
         Kk.C().gemm_set_variant(0)
 
 
+@pytest.mark.parametrize("rows,D,bag,i64", [(36, 128, 1, True), (155, 128, 1, True), (250, 128, 1, False),
+                                          (60, 96, 2, True), (40, 100, 1, True)])
+def test_embedding_small_table_lds_path(gpu, rows, D, bag, i64):
+    """Small tables (16 < rows, <= 128 KB): block-shared LDS accumulation + one flush atomic per
+    (row, col), for the fused sparse SGD and the dense gradient."""
+    import os
+    if os.environ.get("FM_EMB_SMALL") != "1":
+        pytest.skip("small-table LDS path is opt-in (FM_EMB_SMALL=1)")
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(5)
+    B = 8192
+    W = torch.randn(rows, D, device=gpu)
+    idx = torch.randint(0, rows, (B, bag), device=gpu)
+    if not i64:
+        idx = idx.to(torch.int32)
+    dy = torch.randn(B, D, device=gpu).to(torch.bfloat16)
+    lr = torch.tensor([0.05], device=gpu)
+    upd = torch.zeros_like(W)
+    upd.index_add_(0, idx.long().reshape(-1), dy.float().repeat_interleave(bag, 0))
+    W2 = W.clone()
+    Kk.embedding_backward_sgd(idx, dy, W2, lr, 21, {})
+    assert torch.allclose(W2, W - 0.05 * upd, atol=2e-3, rtol=1e-4)
+    dW = torch.empty_like(W)
+    Kk.embedding_backward_dense(idx, dy, dW, 21)
+    assert torch.allclose(dW, upd, atol=2e-2, rtol=1e-4)
+
+
 def test_init_fill_matches_cpu(gpu):
     from flexmi.core.initializers import NormInitializer, UniformInitializer
     for init in [UniformInitializer(7, -0.5, 0.5), NormInitializer(9, 0.0, 2.0)]:
