@@ -20,6 +20,7 @@
 // Blocks are remapped so consecutive tiles share an XCD (private 4 MB L2 per XCD).
 #include "gemm_common.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace {
@@ -398,7 +399,13 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
   int ks = 1;
   if (ksplit_req > 0) ks = ksplit_req;
   else if (ws != nullptr || atomic_ok) {
-    while (tiles * ks < 256 && ks * 2 <= ktiles / 2 && ks < 16) ks *= 2;
+    // split until the grid reaches ~1.5 blocks per CU (measured on the DLRM step, 200-step runs:
+    // target 256 -> 11.05, 384 -> 11.32, 512 -> 11.27, 1024 -> 9.81 M samples/s; FM_GEMM_SPLIT_BLOCKS)
+    // -- long-K (dW at large batch) only: short-K small-batch GEMMs keep 256 (DLRM run_random at
+    // 256/GPU: 1.10 M samples/s at 256 vs 1.04 M at 384)
+    static const long env_target = getenv("FM_GEMM_SPLIT_BLOCKS") ? std::max(1L, atol(getenv("FM_GEMM_SPLIT_BLOCKS"))) : 0L;
+    const long target = env_target > 0 ? env_target : (K >= 4096 ? 384L : 256L);
+    while (tiles * ks < target && ks * 2 <= ktiles / 2 && ks < 16) ks *= 2;
   }
   if (act_y != nullptr || colsum != nullptr) ks = 1;  // fused bwd epilogue needs the full K sum
   if (ks > 1 && !atomic_ok) {
