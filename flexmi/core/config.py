@@ -62,6 +62,7 @@ class FFConfig:
         self.log_level = "INFO"
         self.rank, self.world_size = _dist_info()
         self._start = time.perf_counter()
+        self._models = []               # FFModels built on this config (begin/end_trace targets)
         self.strategies = {}
         if argv is not None:
             self.parse_args(argv)
@@ -175,11 +176,15 @@ class FFConfig:
         return (time.perf_counter() - self._start) * 1e6
 
     def begin_trace(self, trace_id):
-        """Legion tracing analogue: handled by the executor's hipGraph capture."""
-        return None
+        """Legion tracing analogue (``flexflow_cbinding.py`` begin_trace): forwarded to the
+        models built on this config, which replay a recorded training step as hipGraph segments
+        (FFModel.begin_trace)."""
+        for m in self._models:
+            m.begin_trace(trace_id)
 
     def end_trace(self, trace_id):
-        return None
+        for m in self._models:
+            m.end_trace(trace_id)
 
     @property
     def torch_device(self):

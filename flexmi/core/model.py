@@ -81,6 +81,10 @@ class FFModel:
         self.metrics_op = None
         self.label_tensor: Tensor = None
         self.executor = None
+        self._trace = None                 # open trace: {"id", "calls", "defer"}
+        self._traces = {}                  # trace id -> {"seq", "replay", "replayable"}
+        if hasattr(self.config, "_models"):
+            self.config._models.append(self)
         self.strategies: Dict[str, ParallelConfig] = {}
         self._seed = self.config.seed * 1000003 + 12345
         self._tracing_id = 200
@@ -342,16 +346,61 @@ class FFModel:
         return self.executor
 
     def forward(self):
-        self._ex().forward()
+        if not self._traced("forward"):
+            self._ex().forward()
 
     def backward(self):
-        self._ex().backward()
+        if not self._traced("backward"):
+            self._ex().backward()
 
     def update(self):
-        self._ex().update()
+        if not self._traced("update"):
+            self._ex().update()
 
     def zero_gradients(self):
-        self._ex().zero_gradients()
+        if not self._traced("zero_gradients"):
+            self._ex().zero_gradients()
+
+    # ---- Legion tracing analogue (reference: runtime->begin_trace/end_trace around every
+    # iteration from epoch 1, examples/cpp/DLRM/dlrm.cc:178-185, Python trace ids 111/200) --------
+    # The first traced iteration of an id runs eagerly and records its call sequence.  When that
+    # sequence is one training step (forward, [zero_gradients,] backward, update) on MI355X, later
+    # iterations of the id defer their calls and end_trace replays the step as hipGraph segments
+    # (captured on the second iteration) -- the replay of a memoised trace.  Any other sequence,
+    # or a CPU run, simply executes eagerly.
+    def begin_trace(self, trace_id):
+        st = self._traces.get(trace_id)
+        self._trace = {"id": trace_id, "calls": [], "defer": bool(st and st["replayable"])}
+
+    def end_trace(self, trace_id):
+        tr, self._trace = self._trace, None
+        if tr is None or tr["id"] != trace_id:
+            return
+        st = self._traces.get(trace_id)
+        if st is None:
+            calls = [c for c in tr["calls"] if c != "zero_gradients"]
+            ex = self._ex()
+            self._traces[trace_id] = {"seq": tr["calls"], "replay": None,
+                                      "replayable": ex.backend == "hip" and calls == ["forward", "backward", "update"]}
+            return
+        if not tr["defer"]:
+            return
+        if tr["calls"] != st["seq"]:       # another sequence this time: run it eagerly, stop replaying
+            st["replayable"] = False
+            ex = self._ex()
+            for c in tr["calls"]:
+                getattr(ex, c)()
+            return
+        if st["replay"] is None:
+            st["replay"] = self._ex().capture_step()
+        st["replay"]()
+
+    def _traced(self, name):
+        tr = self._trace
+        if tr is None:
+            return False
+        tr["calls"].append(name)
+        return tr["defer"]
 
     def compute_metrics(self):
         self._ex().compute_metrics()
@@ -381,10 +430,14 @@ class FFModel:
             for _ in range(int(num_samples // bs)):
                 for d in dataloaders:
                     d.next_batch(self)
+                if epoch > 0:
+                    self.begin_trace(200)      # reference trace id (flexflow_cbinding.py train)
                 self.forward()
                 self.zero_gradients()
                 self.backward()
                 self.update()
+                if epoch > 0:
+                    self.end_trace(200)
                 step += 1
                 if mlog.enabled:
                     mlog.step(step, bs, self.get_perf_metrics(), ex, epoch=epoch)

@@ -180,11 +180,15 @@ class Model:
                 for d in self._loaders:
                     d.next_batch(m)
                 self._label_loader.next_batch(m)
+                if train and epoch > 0:
+                    m.begin_trace(100)         # reference Keras trace id (base_model.py _train)
                 m.forward()
                 if train:
                     m.zero_gradients()
                     m.backward()
                     m.update()
+                    if epoch > 0:
+                        m.end_trace(100)
                 else:
                     m.compute_metrics()
                 for cb in callbacks:
