@@ -479,23 +479,39 @@ __global__ void __launch_bounds__(256) fm_skinny_bwd_kernel(int ROWS, const unsi
   const int c0 = g * 8;
   bf16x8_t wv = *reinterpret_cast<const bf16x8_t*>(w + c0);
   if (sub < rpi) {
-    for (long r = r0 + sub; r < min(B, r0 + ROWS); r += rpi) {
-      const float d = act_bwd(act, bf2f(y[r * ldy]), bf2f(dy[r * lddy]));
-      dbs += d;
-      bf16x8_t xv = *reinterpret_cast<const bf16x8_t*>(x + r * ldx + c0);
+    // 4 rows per iteration with every load issued first (clamped, unconditional): the per-row
+    // y -> d -> FMA chain no longer pays one HBM round trip per row
+    const long rend = min(B, r0 + ROWS);
+    for (long r = r0 + sub; r < rend; r += 4L * rpi) {
+      float yv[4], gv[4];
+      bf16x8_t xv[4], old[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += d * bf2f((unsigned short)xv[j]);
-      if (dx) {
-        unsigned short* dp = dx + r * lddx + c0;
-        bf16x8_t o;
-        bf16x8_t old = dx_acc ? *reinterpret_cast<const bf16x8_t*>(dp) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      for (int u = 0; u < 4; ++u) {
+        const long rr = min(r + u * rpi, rend - 1);
+        yv[u] = bf2f(y[rr * ldy]);
+        gv[u] = bf2f(dy[rr * lddy]);
+        xv[u] = *reinterpret_cast<const bf16x8_t*>(x + rr * ldx + c0);
+        old[u] = (dx && dx_acc) ? *reinterpret_cast<const bf16x8_t*>(dx + rr * lddx + c0)
+                                : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float v = d * bf2f((unsigned short)wv[j]);
-          if (dx_acc) v += bf2f((unsigned short)old[j]);
-          o[j] = (short)f2bf(v);
+      for (int u = 0; u < 4; ++u) {
+        const long rr = r + u * rpi;
+        if (rr >= rend) break;
+        const float d = act_bwd(act, yv[u], gv[u]);
+        dbs += d;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += d * bf2f((unsigned short)xv[u][j]);
+        if (dx) {
+          bf16x8_t o;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float v = d * bf2f((unsigned short)wv[j]);
+            if (dx_acc) v += bf2f((unsigned short)old[u][j]);
+            o[j] = (short)f2bf(v);
+          }
+          *reinterpret_cast<bf16x8_t*>(dx + rr * lddx + c0) = o;
         }
-        *reinterpret_cast<bf16x8_t*>(dp) = o;
       }
     }
   }

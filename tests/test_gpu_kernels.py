@@ -124,6 +124,31 @@ def test_embedding_small_table_lds_path(gpu, rows, D, bag, i64):
     assert torch.allclose(dW, upd, atol=2e-2, rtol=1e-4)
 
 
+@pytest.mark.parametrize("B,K,act,dx_acc", [(8192, 256, 12, False), (256, 64, 11, True), (1000, 128, 10, False),
+                                            (37, 16, 12, True)])
+def test_skinny_layer_backward(gpu, B, K, act, dx_acc):
+    """out_features == 1 layer backward (DLRM click layer): d = act'(y) * dy, dX = d w, dW += x^T d,
+    db += sum d -- rows processed four at a time with their loads issued first."""
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(7)
+    x = torch.randn(B, K, device=gpu).to(torch.bfloat16)
+    w = torch.randn(1, K, device=gpu).to(torch.bfloat16)
+    pre = x.float() @ w.float().t()
+    y = (torch.sigmoid(pre) if act == 12 else torch.relu(pre) if act == 11 else pre).to(torch.bfloat16)
+    dy = torch.randn(B, 1, device=gpu).to(torch.bfloat16)
+    yf, dyf = y.float(), dy.float()
+    d = dyf * yf * (1 - yf) if act == 12 else dyf * (yf > 0) if act == 11 else dyf
+    dx = torch.randn(B, K, device=gpu).to(torch.bfloat16)
+    dx0 = dx.float().clone()
+    dw = torch.zeros(K, device=gpu)
+    db = torch.zeros(1, device=gpu)
+    Kk.C().skinny_bwd(x, w, y, dy, dx, dx_acc, dw, db, act)
+    ref_dx = d * w.float() + (dx0 if dx_acc else 0)
+    assert rel_err(dx, ref_dx) < 1e-2
+    assert rel_err(dw, (x.float() * d).sum(0)) < 1e-3
+    assert rel_err(db, d.sum().reshape(1)) < 1e-3
+
+
 def test_init_fill_matches_cpu(gpu):
     from flexmi.core.initializers import NormInitializer, UniformInitializer
     for init in [UniformInitializer(7, -0.5, 0.5), NormInitializer(9, 0.0, 2.0)]:
