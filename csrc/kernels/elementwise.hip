@@ -75,43 +75,59 @@ __global__ void fm_binary_bwd(int code, const T* __restrict__ a, const T* __rest
 
 // ---------------------------------------------------------------- act bwd + bias grad
 // dpre[b][n] = act'(y) * dy ; db[n] += sum_b dpre[b][n].
-// Block = 4 waves over ONE 512-column strip (lane owns 8 consecutive columns, 16-B loads) and
-// ROWS rows (wave w takes rows w, w+4, ...); partial column sums are reduced across the 4 waves
-// in LDS and each block issues one fp32 atomic per column.
-template <int ROWS>
+// A block covers a strip of tpr*8 columns (tpr threads per row, a power of two <= 64; a thread owns
+// 8 consecutive columns, 16-B loads) and ROWS rows; its 256 threads take rpb = 256/tpr rows at a
+// time -- so a 128-wide layer keeps every lane busy (16 lanes per row, 16 rows per pass) -- and
+// each thread handles four such rows per iteration with all their loads issued first.  Partial
+// column sums meet in LDS; one fp32 atomic per column per block.
 __global__ void __launch_bounds__(256) fm_act_bwd_colsum(const unsigned short* __restrict__ y,
                                                         const unsigned short* __restrict__ dy,
                                                         unsigned short* __restrict__ dpre, float* __restrict__ db,
-                                                        long B, int N, int act) {
-  __shared__ float red[4][512];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c0 = blockIdx.x * 512 + lane * 8;
+                                                        long B, int N, int act, int tpr, int ROWS) {
+  __shared__ float red[256 * 8];
+  const int tid = threadIdx.x;
+  const int rpb = 256 / tpr;
+  const int sub = tid / tpr, g = tid - sub * tpr;
+  const int c0 = blockIdx.x * tpr * 8 + g * 8;
   const long r0 = (long)blockIdx.y * ROWS;
+  const long rend = min(B, r0 + ROWS);
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const bool vec = ((N & 7) == 0) && (c0 + 8 <= N);
   if (c0 < N) {
-    for (int rr = wave; rr < ROWS; rr += 4) {
-      const long r = r0 + rr;
-      if (r >= B) break;
-      const long o = r * N + c0;
+    for (long r = r0 + sub; r < rend; r += 4L * rpb) {
       if (vec) {
-        bf16x8_t yy = *reinterpret_cast<const bf16x8_t*>(y + o);
-        bf16x8_t gg = *reinterpret_cast<const bf16x8_t*>(dy + o);
-        bf16x8_t out;
+        bf16x8_t yy[4], gg[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float g = act_bwd(act, bf2f((unsigned short)yy[j]), bf2f((unsigned short)gg[j]));
-          s[j] += g;
-          out[j] = (short)f2bf(g);
+        for (int u = 0; u < 4; ++u) {
+          const long o = min(r + u * rpb, rend - 1) * N + c0;    // clamped: unconditional loads
+          yy[u] = *reinterpret_cast<const bf16x8_t*>(y + o);
+          gg[u] = *reinterpret_cast<const bf16x8_t*>(dy + o);
         }
-        if (dpre) *reinterpret_cast<bf16x8_t*>(dpre + o) = out;
-      } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          if (c0 + j < N) {
-            float g = act_bwd(act, bf2f(y[o + j]), bf2f(dy[o + j]));
-            s[j] += g;
-            if (dpre) dpre[o + j] = f2bf(g);
+        for (int u = 0; u < 4; ++u) {
+          const long rr = r + u * rpb;
+          if (rr >= rend) break;
+          bf16x8_t out;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float gv = act_bwd(act, bf2f((unsigned short)yy[u][j]), bf2f((unsigned short)gg[u][j]));
+            s[j] += gv;
+            out[j] = (short)f2bf(gv);
+          }
+          if (dpre) *reinterpret_cast<bf16x8_t*>(dpre + rr * N + c0) = out;
+        }
+      } else {
+        for (int u = 0; u < 4; ++u) {
+          const long rr = r + u * rpb;
+          if (rr >= rend) break;
+          const long o = rr * N + c0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            if (c0 + j < N) {
+              const float gv = act_bwd(act, bf2f(y[o + j]), bf2f(dy[o + j]));
+              s[j] += gv;
+              if (dpre) dpre[o + j] = f2bf(gv);
+            }
           }
         }
       }
@@ -119,12 +135,14 @@ __global__ void __launch_bounds__(256) fm_act_bwd_colsum(const unsigned short* _
   }
   if (!db) return;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) red[wave][lane * 8 + j] = s[j];
+  for (int j = 0; j < 8; ++j) red[tid * 8 + j] = s[j];
   __syncthreads();
-  for (int c = threadIdx.x; c < 512; c += 256) {
-    const int col = blockIdx.x * 512 + c;
+  for (int c = tid; c < tpr * 8; c += 256) {
+    const int col = blockIdx.x * tpr * 8 + c;
     if (col < N) {
-      float v = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+      const int gc = c >> 3, j = c & 7;
+      float v = 0.f;
+      for (int q = 0; q < rpb; ++q) v += red[(q * tpr + gc) * 8 + j];
       atomicAdd(db + col, v);
     }
   }
@@ -308,10 +326,17 @@ extern "C" void fm_binary_backward(int code, const void* a, const void* b, const
 
 extern "C" void fm_act_bwd_bias(const void* y, const void* dy, void* dpre, float* db, long B, int N, int act, hipStream_t s) {
   if (B <= 0 || N <= 0) return;
-  constexpr int ROWS = 32;
-  dim3 grid((unsigned)((N + 511) / 512), (unsigned)((B + ROWS - 1) / ROWS));
-  hipLaunchKernelGGL((fm_act_bwd_colsum<ROWS>), grid, dim3(256), 0, s, (const unsigned short*)y,
-                     (const unsigned short*)dy, (unsigned short*)dpre, db, B, N, act);
+  int tpr = 1;
+  while (tpr < 64 && tpr * 8 < N) tpr *= 2;                 // threads per row (power of two)
+  const int rpb = 256 / tpr;
+  const long strips = (N + tpr * 8 - 1) / (tpr * 8);
+  // ~256 blocks: few column-sum atomics per address, every CU busy at DLRM sizes
+  const long nrb = std::max<long>(1, 256 / strips);
+  long ROWS = (B + nrb - 1) / nrb;
+  ROWS = (ROWS + 4L * rpb - 1) / (4L * rpb) * (4L * rpb);
+  dim3 grid((unsigned)strips, (unsigned)((B + ROWS - 1) / ROWS));
+  hipLaunchKernelGGL(fm_act_bwd_colsum, grid, dim3(256), 0, s, (const unsigned short*)y, (const unsigned short*)dy,
+                     (unsigned short*)dpre, db, B, N, act, tpr, (int)ROWS);
 }
 
 extern "C" void fm_multi_copy2d(int n, const void* const* src, void* const* dst, const long* rows, const long* cols,

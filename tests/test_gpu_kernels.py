@@ -308,19 +308,22 @@ def test_elementwise_and_movement(gpu):
     assert torch.allclose(s, torch.softmax(xx, -1), atol=1e-6)
 
 
-def test_act_bwd_bias(gpu):
+@pytest.mark.parametrize("B,N,act", [(1000, 260, 11), (8192, 128, 11), (8192, 1024, 12), (256, 1024, 11), (37, 20, 13),
+                                     (4096, 64, 10)])
+def test_act_bwd_bias(gpu, B, N, act):
     from flexmi.ops import _kernels as Kk
     torch.manual_seed(8)
-    B, N = 1000, 260
-    y = torch.relu(torch.randn(B, N, device=gpu)).to(torch.bfloat16)
+    pre = torch.randn(B, N, device=gpu)
+    y = (torch.relu(pre) if act == 11 else torch.sigmoid(pre) if act == 12 else torch.tanh(pre) if act == 13
+         else pre).to(torch.bfloat16)
     dy = torch.randn(B, N, device=gpu).to(torch.bfloat16)
     dpre = torch.empty(B, N, device=gpu, dtype=torch.bfloat16)
     db = torch.zeros(N, device=gpu)
-    torch.ops  # noqa
-    Kk.C().act_bwd_bias(y, dy, dpre, db, B, N, 11)
-    ref = dy.float() * (y.float() > 0)
+    Kk.C().act_bwd_bias(y, dy, dpre, db, B, N, act)
+    yf, g = y.float(), dy.float()
+    ref = {11: g * (yf > 0), 12: g * yf * (1 - yf), 13: g * (1 - yf * yf), 10: g}[act]
     assert rel_err(dpre, ref) < 1e-2
-    assert torch.allclose(db, ref.sum(0), atol=1e-2, rtol=1e-3)
+    assert torch.allclose(db, ref.sum(0), atol=2e-2, rtol=1e-3)
 
 
 @pytest.mark.parametrize("N,C,H,W,K,R,S,st,pads", [
