@@ -381,6 +381,7 @@ void launch_claim(const ClaimSet& s, int m, bool dy_bf16, const float* lr, long 
   const long n = B * maxbag;
   dim3 gc((unsigned)std::max<long>(1, std::min<long>((n + 255) / 256, 1024)), m);
   hipLaunchKernelGGL((fm_emb_claim_multi<I64>), gc, dim3(256), 0, st, s, B);
+  // (a 64-block grid measured 18.4 vs 9.5 us/step: 12k..40k-row tables still see thousands of dups)
   dim3 gd((unsigned)std::max<long>(1, std::min<long>((n + 3) / 4, 1024)), m);
   if (dy_bf16) hipLaunchKernelGGL((fm_emb_dup_multi<unsigned short, I64>), gd, dim3(256), 0, st, s, lr);
   else hipLaunchKernelGGL((fm_emb_dup_multi<float, I64>), gd, dim3(256), 0, st, s, lr);

@@ -337,8 +337,11 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
   // accumulating C with float atomics, no slabs and no reduce launch.  Measured SLOWER on the
   // DLRM dW GEMMs (profiles/README.md): the 16x16 accumulator layout issues 4-B atomics over 16
   // rows per wave-instruction, far below the 256-contiguous-byte atomic rate.
+  static const long atomic_max = getenv("FM_GEMM_ATOMIC_SPLIT") ? (getenv("FM_GEMM_ATOMIC_MAX") ? atol(getenv("FM_GEMM_ATOMIC_MAX"))
+                                                                                                : (256L << 10))
+                                                                 : 0L;
   const bool atomic_ok = c_fp32 && beta && bias == nullptr && act == 10 && act_y == nullptr && colsum == nullptr &&
-                         (long)M * N <= (256L << 10) && getenv("FM_GEMM_ATOMIC_SPLIT") != nullptr;
+                         (long)M * N <= atomic_max;
   // vector (16-B) loads need the contiguous extent and leading dims to be multiples of 8
   auto al = [](const void* q) { return (((uintptr_t)q) & 15) == 0; };
   bool vec = al(A) && al(B) && (lda % 8 == 0) && (ldb % 8 == 0) && (sA % 8 == 0) && (sB % 8 == 0);

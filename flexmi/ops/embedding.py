@@ -200,6 +200,8 @@ class Embedding(Op):
                                   [Embedding._row_lo(c) for c in ctxs])
 
     CLAIM = os.environ.get("FM_EMB_CLAIM", "1") != "0"
+    # owner-computes only when rows exceed CLAIM_RATIO x lookups per step (fewer duplicates)
+    CLAIM_RATIO = float(os.environ.get("FM_EMB_CLAIM_RATIO", "1"))
 
     def _claim_buffers(self, ctx):
         """Owner-computes sparse SGD buffers for a mostly-unique table (rows > lookups per step):
@@ -210,7 +212,7 @@ class Embedding(Op):
         s = ctx.saved
         if "claim" not in s:
             w, idx = ctx.weights[0], ctx.inputs[0]
-            if w.shape[0] > idx.numel() and self.out_dim % 4 == 0:
+            if w.shape[0] > Embedding.CLAIM_RATIO * idx.numel() and self.out_dim % 4 == 0:
                 dev = w.device
                 s["claim"] = (torch.full((w.shape[0],), -1, dtype=torch.int32, device=dev),
                               torch.empty(idx.numel(), dtype=torch.int32, device=dev),
