@@ -96,6 +96,10 @@ def linear_forward(x2, w, b, act, y2):
     gemm(x2, x2.stride(0), True, w, K, True, y2, y2.stride(0), M, N, K, bias=b, act=act)
 
 
+DX_LIB = os.environ.get("FM_DX_LIB", "0") == "1"
+DX_LIB_MIN = int(os.environ.get("FM_DX_LIB_MIN", str(1 << 32)))
+
+
 def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=False, fuse_below=None):
     """Weight/bias grads ACCUMULATE into dw/db (the executor zeroes the flat gradient buffer once
     per step).  grad_is_dpre: dy2 already holds act'(y)*dy (written by the consumer's fused dX
@@ -124,6 +128,17 @@ def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=F
     # with atomics straight into dw (no slab / reduce launch)
     gemm(dpre, dpre.stride(0), False, x2, x2.stride(0), False, dw, K, N, K, M, beta=True, rowsum_a=db)
     # dX[M,K] = dpre W   (+ fused activation backward of the layer below)
+    if dx2 is not None and DX_LIB and M * K * N >= DX_LIB_MIN and dx2.is_contiguous():
+        # plain library GEMM (hipBLASLt) for the big dX products, activation backward of the layer
+        # below as a separate pass (FM_DX_LIB=1; A/B in profiles/README.md)
+        t = torch.matmul(dpre, w)
+        if fuse_below is not None:
+            C().act_bwd_bias(fuse_below[0].view(M, K), t, dx2, None, M, K, int(fuse_below[1]))
+        elif dx_acc:
+            dx2.add_(t)
+        else:
+            dx2.copy_(t)
+        return
     if dx2 is not None:
         if fuse_below is not None:
             yb, actb = fuse_below[0], fuse_below[1]
