@@ -100,7 +100,7 @@ DX_LIB = os.environ.get("FM_DX_LIB", "0") == "1"
 DX_LIB_MIN = int(os.environ.get("FM_DX_LIB_MIN", str(1 << 32)))
 
 
-def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=False, fuse_below=None):
+def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=False, fuse_below=None, phase="all"):
     """Weight/bias grads ACCUMULATE into dw/db (the executor zeroes the flat gradient buffer once
     per step).  grad_is_dpre: dy2 already holds act'(y)*dy (written by the consumer's fused dX
     epilogue).  fuse_below = (y_below, act_below): apply the activation backward of the layer
@@ -108,6 +108,8 @@ def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=F
     M, K = x2.shape
     N = w.shape[0]
     if N == 1:
+        if phase == "dw":          # the skinny kernel did dX, dW and db together in the "dx" phase
+            return
         C().skinny_bwd(x2, w, y2, dy2, dx2, bool(dx_acc), dw, None if grad_is_dpre else db,
                        10 if grad_is_dpre else act)
         if dx2 is not None and fuse_below is not None:
@@ -115,6 +117,8 @@ def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=F
         return
     if grad_is_dpre or act == 10:
         dpre = dy2
+    elif phase == "dw":            # computed by this op's "dx" phase (per-op workspace)
+        dpre = ws["dpre"]
     else:
         dpre = ws.get("dpre")
         if dpre is None or dpre.shape != (M, N):
@@ -126,7 +130,10 @@ def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=F
     # dW ACCUMULATES (beta): the executor zeroes the flat gradient buffer once per step, so weights
     # used by several ops sum their gradients, and split-K partials of small dW tiles can be added
     # with atomics straight into dw (no slab / reduce launch)
-    gemm(dpre, dpre.stride(0), False, x2, x2.stride(0), False, dw, K, N, K, M, beta=True, rowsum_a=db)
+    if phase != "dx":
+        gemm(dpre, dpre.stride(0), False, x2, x2.stride(0), False, dw, K, N, K, M, beta=True, rowsum_a=db)
+    if phase == "dw":
+        return
     # dX[M,K] = dpre W   (+ fused activation backward of the layer below)
     if dx2 is not None and DX_LIB and M * K * N >= DX_LIB_MIN and dx2.is_contiguous():
         # plain library GEMM (hipBLASLt) for the big dX products, activation backward of the layer

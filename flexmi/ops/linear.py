@@ -104,7 +104,9 @@ class Linear(Op):
             out = torch.nn.functional.linear(x2.float(), ctx.wcompute[0].float(), None if b is None else b.float())
             y2.copy_(act_forward_torch(out, self.activation))
 
-    def backward(self, ctx: OpCtx):
+    def backward(self, ctx: OpCtx, phase="all"):
+        """phase "dx": input gradient (and the shared act-bwd); "dw": weight / bias gradients --
+        the executor runs dW later to overlap a pending gradient exchange; "all": both."""
         x = ctx.inputs[0]
         x2 = x.reshape(-1, x.shape[-1])
         y2 = ctx.outputs[0].view(-1, ctx.outputs[0].shape[-1])
@@ -117,13 +119,14 @@ class Linear(Op):
         if ctx.hip:
             K.linear_backward(x2, ctx.wcompute[0], y2, dy2, int(act), dx2,
                               bool(ctx.in_grad_accumulate[0]) if dx2 is not None else False, dw, db,
-                              ctx.workspace, ctx.saved.get("grad_is_dpre", False), ctx.saved.get("fuse_below"))
+                              ctx.workspace, ctx.saved.get("grad_is_dpre", False), ctx.saved.get("fuse_below"), phase)
         else:
             dpre = act_backward_torch(dy2.float(), y2.float(), act)
-            dw.add_(dpre.t() @ x2.float())
-            if db is not None:
-                db.add_(dpre.sum(0))
-            if dx2 is not None:
+            if phase != "dx":
+                dw.add_(dpre.t() @ x2.float())
+                if db is not None:
+                    db.add_(dpre.sum(0))
+            if dx2 is not None and phase != "dw":
                 store(dx2, dpre @ ctx.wcompute[0].float(), ctx.in_grad_accumulate[0])
 
     def flops(self, in_shapes, out_shapes):

@@ -1211,6 +1211,41 @@ class Executor:
                 return any(self.gkey(t.guid) in keys for t in st[1].inputs + st[1].outputs)
             return any(self.gkey(g) in keys for _, _, g, _ in st[1])
 
+        # dW of the Linear ops that precede the FIRST cross-device gradient exchange in backward order
+        # (DLRM: the top MLP ahead of the embedding-gradient all-to-all) is deferred until that
+        # exchange has been started, so the weight-gradient GEMMs overlap the all-to-all instead of
+        # delaying it; their bucket all-reduces follow them.
+        from flexmi.core.types import OperatorType
+        has_xchg = self.world > 1 and any(
+            st[0] != "op" and not all(rs.local_only for _, _, _, rs in st[1]) for st in steps)
+        mode = os.environ.get("FLEXMI_DEFER_DW", "1")     # 0: off, force: also without an exchange (tests)
+        defer_ok = (has_xchg or mode == "force") and mode != "0"
+        deferred = []          # [(op, ctx)] whose dW items wait for the first exchange start
+
+        def bucket_done(done_ops):
+            for w in [w for o in done_ops for w in o.weights]:
+                uses_left[w.guid] -= 1
+                e = self.wentries.get(w.guid)
+                if e is None or e.group is None or not e.group.replicated or uses_left[w.guid] > 0:
+                    continue
+                g = e.group
+                for bi, b in enumerate(g.buckets):
+                    if w.guid in b[2]:
+                        bucket_left[id(g)][bi] -= 1
+                        if bucket_left[id(g)][bi] == 0 and self.cfg.overlap_grad_sync:
+                            if g.zero:
+                                bwd.append(Item("comm", (lambda g=g, bi=bi: self._launch_bucket(g, bi)),
+                                                f"reducescatter.bucket{bi}", native=("rs", g, bi)))
+                            else:
+                                bwd.append(Item("comm", (lambda g=g, bi=bi: self._launch_bucket(g, bi)),
+                                                f"allreduce.bucket{bi}", native=("ar", g, bi)))
+
+        def flush_deferred():
+            for dop, dc in deferred:
+                C(bwd, dop.name + ".bwd_dw", (lambda op=dop, c=dc: op.backward(c, "dw")))
+                bucket_done([dop])
+            deferred.clear()
+
         for k, st in enumerate(steps):
             for ex in finish_before.pop(k, []):
                 self._emit_exchange_finish(bwd, ex, "reshard.bwd")
@@ -1231,6 +1266,10 @@ class Executor:
                         if grp[0] is op:
                             C(bwd, op.name + ".group_bwd",
                               (lambda grp=grp: type(grp[0]).backward_group(grp, [self.ctx[o.guid] for o in grp])))
+                    elif defer_ok and op.op_type == OperatorType.OP_LINEAR and op.weights:
+                        C(bwd, op.name + ".bwd_dx", (lambda op=op, c=c, flags=flags: self._bwd_op(op, c, flags, "dx")))
+                        bwd[-1].check = (lambda op=op, c=c: self._check_op(op.name + ".bwd", c.in_grads, "input grad"))
+                        deferred.append((op, c))
                     else:
                         bwd.append(Item("comm" if getattr(op, "host_exec", False) else "compute",
                                         (lambda op=op, c=c, flags=flags: self._bwd_op(op, c, flags)), op.name + ".bwd"))
@@ -1243,22 +1282,9 @@ class Executor:
                 # weight gradients are final only there, not at the members' own positions.
                 grp = self.group_of.get(op.guid)
                 done_ops = [op] if grp is None else (list(grp) if grp[0] is op else [])
-                for w in [w for o in done_ops for w in o.weights]:
-                    uses_left[w.guid] -= 1
-                    e = self.wentries.get(w.guid)
-                    if e is None or e.group is None or not e.group.replicated or uses_left[w.guid] > 0:
-                        continue
-                    g = e.group
-                    for bi, b in enumerate(g.buckets):
-                        if w.guid in b[2]:
-                            bucket_left[id(g)][bi] -= 1
-                            if bucket_left[id(g)][bi] == 0 and self.cfg.overlap_grad_sync:
-                                if g.zero:
-                                    bwd.append(Item("comm", (lambda g=g, bi=bi: self._launch_bucket(g, bi)),
-                                                    f"reducescatter.bucket{bi}", native=("rs", g, bi)))
-                                else:
-                                    bwd.append(Item("comm", (lambda g=g, bi=bi: self._launch_bucket(g, bi)),
-                                                    f"allreduce.bucket{bi}", native=("ar", g, bi)))
+                if deferred and deferred[-1][0] is op:
+                    done_ops = []            # its dW (and bucket) come with the deferred items
+                bucket_done(done_ops)
             else:
                 items, seen = [], set()
                 for op, i, g, rs in st[1]:
@@ -1270,11 +1296,15 @@ class Executor:
                 else:
                     ex = FusedExchange(items, self.world, self.rank)
                     self._emit_exchange_start(bwd, ex, "reshard.bwd")
+                    if defer_ok:
+                        flush_deferred()          # dW GEMMs overlap this exchange
+                        defer_ok = False
                     keys = {self.gkey(g) for _, _, g, _ in st[1]}
                     nxt = next((j for j in range(k + 1, len(steps)) if touches(steps[j], keys)), len(steps))
                     finish_before[nxt].append(ex)
                 for op, i, g, rs in st[1]:
                     written.add(self.gkey(g))
+        flush_deferred()
         for ex in finish_before.pop(len(steps), []):
             self._emit_exchange_finish(bwd, ex, "reshard.bwd")
         assert not finish_before
@@ -1285,12 +1315,15 @@ class Executor:
             return self._host_op(op, c, "forward")
         op.forward(c)
 
-    def _bwd_op(self, op, c, flags):
+    def _bwd_op(self, op, c, flags, phase=None):
         for i, f in enumerate(flags):
             c.in_grad_accumulate[i] = f
         if getattr(op, "host_exec", False):
             return self._host_op(op, c, "backward")
-        op.backward(c)
+        if phase is None:
+            op.backward(c)
+        else:
+            op.backward(c, phase)
 
     def _host_op(self, op, c, phase):
         """A CPU-placed op (P6) runs its CPU (fp32 torch) path on the host: host copies of the

@@ -201,3 +201,11 @@ def test_prefetch_loader_gpu_matches_single_loader(gpu):
             dls[0].close()
     for a, b in zip(*res):
         np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_dlrm_deferred_dw_phases_match_cpu(gpu, monkeypatch):
+    """The split Linear backward (dX first, dW deferred to the end of backward: the schedule used
+    ahead of the embedding-gradient all-to-all on 2+ GPUs), forced at world 1 on MI355X, trains the
+    tiny DLRM like the CPU oracle -- fused act-bwd epilogues and the skinny layer included."""
+    monkeypatch.setenv("FLEXMI_DEFER_DW", "force")
+    test_dlrm_tiny_gpu_matches_cpu(gpu)
