@@ -35,9 +35,9 @@ void fm_dot_interaction_fwd(const void* const* z, int F, long ldz, void* out, lo
 void fm_dot_interaction_bwd(const void* const* z, int F, long ldz, const void* dout, long ldo, void* const* dz, long lddz,
                             unsigned acc_mask, long B, int D, int self, hipStream_t s);
 void fm_sgd_update(float* W, const float* G, float* V, unsigned short* Wc, const float* lr, long n, float wd, float mom,
-                   int nesterov, hipStream_t s);
+                   int nesterov, int zero_g, hipStream_t s);
 void fm_adam_update(float* W, const float* G, float* M, float* V, unsigned short* Wc, long n, const float* alpha_t,
-                    float b1, float b2, float wd, float eps, hipStream_t s);
+                    float b1, float b2, float wd, float eps, int zero_g, hipStream_t s);
 void fm_cast_bf16(const float* src, unsigned short* dst, long n, hipStream_t s);
 void fm_loss_fwd_bwd(const void* logits, int logits_bf16, const void* labels, void* grad, int grad_bf16, long B, int C,
                      int loss_type, float scale, float* acc, int mask, hipStream_t s);
@@ -304,17 +304,17 @@ void dot_bwd(std::vector<torch::Tensor> zs, int64_t ldz, torch::Tensor dout, int
 }
 
 void sgd(torch::Tensor W, torch::Tensor G, c10::optional<torch::Tensor> V, c10::optional<torch::Tensor> Wc, torch::Tensor lr,
-         double wd, double mom, bool nesterov) {
+         double wd, double mom, bool nesterov, bool zero_grad) {
   TORCH_CHECK(W.numel() == G.numel(), "sgd: size mismatch");
   fm_sgd_update(W.data_ptr<float>(), G.data_ptr<float>(), (float*)mptr(V), (unsigned short*)mptr(Wc), lr.data_ptr<float>(),
-                W.numel(), (float)wd, (float)mom, nesterov ? 1 : 0, cur());
+                W.numel(), (float)wd, (float)mom, nesterov ? 1 : 0, zero_grad ? 1 : 0, cur());
 }
 
 void adam(torch::Tensor W, torch::Tensor G, torch::Tensor M, torch::Tensor V, c10::optional<torch::Tensor> Wc,
-          torch::Tensor alpha_t, double b1, double b2, double wd, double eps) {
+          torch::Tensor alpha_t, double b1, double b2, double wd, double eps, bool zero_grad) {
   TORCH_CHECK(alpha_t.scalar_type() == torch::kFloat32 && alpha_t.is_cuda(), "alpha_t: fp32 device scalar");
   fm_adam_update(W.data_ptr<float>(), G.data_ptr<float>(), M.data_ptr<float>(), V.data_ptr<float>(), (unsigned short*)mptr(Wc),
-                 W.numel(), alpha_t.data_ptr<float>(), (float)b1, (float)b2, (float)wd, (float)eps, cur());
+                 W.numel(), alpha_t.data_ptr<float>(), (float)b1, (float)b2, (float)wd, (float)eps, zero_grad ? 1 : 0, cur());
 }
 
 void cast_bf16(torch::Tensor src, torch::Tensor dst) { fm_cast_bf16(src.data_ptr<float>(), (unsigned short*)dst.data_ptr(), src.numel(), cur()); }

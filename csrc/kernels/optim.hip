@@ -10,12 +10,15 @@ namespace {
 
 __global__ void fm_sgd_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ V,
                               unsigned short* __restrict__ Wc, const float* __restrict__ lr_p, long n, float wd,
-                              float mom, int nesterov, int vec) {
+                              float mom, int nesterov, int vec, int zero_g) {
+  // zero_g: the gradient is consumed here -- write it back as 0 so the next step's backward
+  // starts from a clean accumulator without a separate memset (Executor._optimizer_step)
   const float lr = lr_p[0];
   const long n4 = vec ? n / 4 : 0;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     f32x4_t w = reinterpret_cast<f32x4_t*>(W)[i];
     f32x4_t g = reinterpret_cast<const f32x4_t*>(G)[i] + wd * w;
+    if (zero_g) reinterpret_cast<f32x4_t*>(const_cast<float*>(G))[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     if (mom > 0.f) {
       f32x4_t v = reinterpret_cast<f32x4_t*>(V)[i] * mom + g;
       reinterpret_cast<f32x4_t*>(V)[i] = v;
@@ -32,6 +35,7 @@ __global__ void fm_sgd_kernel(float* __restrict__ W, const float* __restrict__ G
   // tail
   for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     float g = G[i] + wd * W[i];
+    if (zero_g) const_cast<float*>(G)[i] = 0.f;
     if (mom > 0.f) {
       float v = V[i] * mom + g;
       V[i] = v;
@@ -44,11 +48,13 @@ __global__ void fm_sgd_kernel(float* __restrict__ W, const float* __restrict__ G
 
 __global__ void fm_adam_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ M,
                                float* __restrict__ V, unsigned short* __restrict__ Wc, long n,
-                               const float* __restrict__ alpha_t_p, float b1, float b2, float wd, float eps) {
+                               const float* __restrict__ alpha_t_p, float b1, float b2, float wd, float eps,
+                               int zero_g) {
   const float alpha_t = alpha_t_p[0];  // device-side bias-corrected step size (graph-capturable)
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     float w = W[i];
     float g = G[i] + wd * w;
+    if (zero_g) const_cast<float*>(G)[i] = 0.f;
     float m = b1 * M[i] + (1.f - b1) * g;
     float v = b2 * V[i] + (1.f - b2) * g * g;
     M[i] = m;
@@ -66,17 +72,19 @@ __global__ void fm_cast_bf16_kernel(const float* __restrict__ src, unsigned shor
 }  // namespace
 
 extern "C" void fm_sgd_update(float* W, const float* G, float* V, unsigned short* Wc, const float* lr, long n, float wd,
-                              float mom, int nesterov, hipStream_t s) {
+                              float mom, int nesterov, int zero_g, hipStream_t s) {
   if (n <= 0) return;
   bool al = ((((uintptr_t)W) | ((uintptr_t)G) | ((uintptr_t)(V ? V : W))) & 15) == 0 && ((((uintptr_t)(Wc ? Wc : (unsigned short*)W)) & 7) == 0);
   hipLaunchKernelGGL(fm_sgd_kernel, dim3(fm_grid(al ? n / 4 + 1 : n)), dim3(256), 0, s, W, G, V, Wc, lr, n, wd, mom,
-                     nesterov, al ? 1 : 0);
+                     nesterov, al ? 1 : 0, zero_g);
 }
 
 extern "C" void fm_adam_update(float* W, const float* G, float* M, float* V, unsigned short* Wc, long n,
-                               const float* alpha_t, float b1, float b2, float wd, float eps, hipStream_t s) {
+                               const float* alpha_t, float b1, float b2, float wd, float eps, int zero_g,
+                               hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(fm_adam_kernel, dim3(fm_grid(n)), dim3(256), 0, s, W, G, M, V, Wc, n, alpha_t, b1, b2, wd, eps);
+  hipLaunchKernelGGL(fm_adam_kernel, dim3(fm_grid(n)), dim3(256), 0, s, W, G, M, V, Wc, n, alpha_t, b1, b2, wd, eps,
+                     zero_g);
 }
 
 extern "C" void fm_cast_bf16(const float* src, unsigned short* dst, long n, hipStream_t s) {

@@ -205,12 +205,13 @@ def dot_interaction_backward(inputs, dy, in_grads, accs, self_inter):
 
 
 # ------------------------------------------------------------------ optimizers / loss
-def sgd_update(master, grad, v, compute, lr_tensor, wd, momentum, nesterov):
-    C().sgd(master, grad, v, compute, lr_tensor, wd, momentum, nesterov)
+def sgd_update(master, grad, v, compute, lr_tensor, wd, momentum, nesterov, zero_grad=False):
+    """zero_grad: the kernel writes the consumed gradient back as zeros (no separate memset)."""
+    C().sgd(master, grad, v, compute, lr_tensor, wd, momentum, nesterov, zero_grad)
 
 
-def adam_update(master, grad, m, v, compute, alpha_t, b1, b2, wd, eps):
-    C().adam(master, grad, m, v, compute, alpha_t, b1, b2, wd, eps)
+def adam_update(master, grad, m, v, compute, alpha_t, b1, b2, wd, eps, zero_grad=False):
+    C().adam(master, grad, m, v, compute, alpha_t, b1, b2, wd, eps, zero_grad)
 
 
 def loss_forward_backward(loss_type, logits, labels, grad, scale, acc, mask):

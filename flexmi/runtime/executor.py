@@ -153,10 +153,11 @@ def run_reshards(comm, items):
 
 
 class Item:
-    __slots__ = ("kind", "fn", "name", "check", "native")
+    __slots__ = ("kind", "fn", "name", "check", "native", "zero_group")
 
     def __init__(self, kind, fn, name, check=None, native=None):
         self.kind, self.fn, self.name = kind, fn, name
+        self.zero_group = None  # the per-step gradient memset of this weight group
         self.check = check      # debug mode: callable(item) run after fn (NaN/Inf guard)
         self.native = native    # comm items: structured form for the native runner (flexmi._rt)
 
@@ -545,6 +546,7 @@ class Executor:
             self.watchdog = Watchdog(self.cfg.watchdog_s, getattr(self.cfg, "watchdog_mode", "exit"))
         self.training = True
         self.step_count = 0
+        self._grads_dirty = False       # gradients not yet consumed by an update (see capture_step)
         self._graph = None
         self._native = None
         self.build()
@@ -1191,6 +1193,7 @@ class Executor:
         for g in self.groups:   # weight/bias grads accumulate (atomics in fused epilogues): one memset
             if g.numel:
                 C(bwd, "zero_grads", (lambda g=g: g.gradbuf.zero_()))
+                bwd[-1].zero_group = g   # dropped from captured steps: the update kernel re-zeroes
         self._emit_loss(bwd, compute_grad=True)
         written.add(self.gkey(self.final.guid))
         bucket_left = {}
@@ -1443,9 +1446,12 @@ class Executor:
 
     def backward(self):
         self._run(self.prog_bwd)
+        self._grads_dirty = True
 
     def update(self):
         self._run(self.prog_upd)
+        if self.backend == "hip" and self.optimizer is not None:
+            self._grads_dirty = any(g.zero for g in self.groups)   # update kernels re-zeroed the rest
         if self.optimizer is not None:
             self.optimizer.next()   # host mirror of the device-side step counters
         self.step_count += 1
@@ -1493,12 +1499,13 @@ class Executor:
                 continue
             comp = g.compute if g.compute is not g.master else None
             if self.backend == "hip":
+                # the kernels consume the gradient and leave it zeroed for the next backward
                 if isinstance(opt, SGDOptimizer):
                     K.sgd_update(g.master, g.gradbuf, g.state.get("v"), comp, self.lr_tensor, opt.weight_decay,
-                                 opt.momentum, opt.nesterov)
+                                 opt.momentum, opt.nesterov, zero_grad=True)
                 else:
                     K.adam_update(g.master, g.gradbuf, g.state["m"], g.state["v"], comp, self.adam_state[2:3],
-                                  opt.beta1, opt.beta2, opt.weight_decay, opt.epsilon)
+                                  opt.beta1, opt.beta2, opt.weight_decay, opt.epsilon, zero_grad=True)
             else:
                 if isinstance(opt, SGDOptimizer):
                     gt = g.gradbuf + opt.weight_decay * g.master
@@ -1660,12 +1667,32 @@ class Executor:
         return self.prog_fwd + self.prog_bwd + self.prog_upd
 
     def capture_step(self, pre=None):
+        """The training step as a replayable hipGraph program (see ``_capture_step``).  The
+        per-step gradient memset is left out of the graph: the update kernels consume the
+        gradients and write them back as zeros, and a replay that follows an eager backward
+        (gradients still dirty) clears them first."""
+        assert self.backend == "hip"
+        memset = [it for it in self.step_program() if getattr(it, "zero_group", None) is not None
+                  and not it.zero_group.zero]
+        skip = {id(it) for it in memset} if self.optimizer is not None else set()
+        replay = self._capture_step(pre, skip)
+        groups = [it.zero_group for it in memset]
+
+        def run():
+            if self._grads_dirty:
+                for g in groups:
+                    g.gradbuf.zero_()
+            replay()
+            self._grads_dirty = bool(skip) and any(g.zero for g in self.groups)
+        return run
+
+    def _capture_step(self, pre=None, skip=()):
         """Capture the training step as hipGraph segments split at the collectives.
         ``pre``: optional compute callable (e.g. input staging) captured at the head.
         Returns a callable that replays one step.  The caller must have run >= 1 eager step
         (allocator warm-up, lazily created workspaces)."""
-        assert self.backend == "hip"
-        prog = ([Item("compute", pre, "pre")] if pre is not None else []) + self.step_program()
+        prog = ([Item("compute", pre, "pre")] if pre is not None else []) + \
+            [it for it in self.step_program() if id(it) not in skip]
         segments = []
         cur = []
         for it in prog:

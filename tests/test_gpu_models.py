@@ -110,6 +110,41 @@ def test_hip_graph_capture_matches_eager(gpu):
         assert np.allclose(a, b, atol=1e-5), a.shape
 
 
+@pytest.mark.parametrize("optname", ["sgd", "adam"])
+def test_captured_step_gradient_reset(gpu, optname):
+    """Captured steps leave out the gradient memset (the update kernels write the consumed
+    gradients back as zeros).  An eager backward WITHOUT an update before the replays leaves dirty
+    gradients, which the replay clears first: the result equals the eager sequence."""
+    from flexmi.core import AdamOptimizer, FFConfig, FFModel, SGDOptimizer, LossType, MetricsType
+    from flexmi.models.dlrm import DLRMConfig, build_dlrm, SyntheticDLRMData
+    res = []
+    for use_graph in (False, True):
+        cfg = FFConfig()
+        cfg.batchSize, cfg.seed = 512, 3
+        m = FFModel(cfg)
+        dcfg = DLRMConfig.preset("tiny")
+        d, s, p = build_dlrm(m, dcfg)
+        opt = SGDOptimizer(m, 0.05, momentum=0.9) if optname == "sgd" else AdamOptimizer(m, 0.01)
+        m.compile(opt, LossType.LOSS_BINARY_CROSSENTROPY, [MetricsType.METRICS_ACCURACY])
+        ex = m.init_layers()
+        data = SyntheticDLRMData(m, d, s, dcfg, num_batches=1)
+        data.next_batch()
+        ex.train_step()
+        ex.forward()
+        ex.backward()                       # no update: gradients stay dirty
+        if use_graph:
+            run = ex.capture_step()
+            for _ in range(3):
+                run()
+        else:
+            for _ in range(3):
+                ex.train_step()
+        torch.cuda.synchronize()
+        res.append([w.get_weights(m) for w in m.parameters])
+    for a, b in zip(*res):
+        assert np.allclose(a, b, atol=1e-5), a.shape
+
+
 @pytest.mark.parametrize("name,steps", [("mnist_cnn", 3), ("cifar10_cnn", 3), ("alexnet", 2), ("resnet50", 2),
                                         ("inception_v3", 1), ("candle_uno", 3), ("nmt", 3)])
 def test_zoo_gpu_matches_cpu(gpu, name, steps):
