@@ -408,7 +408,8 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
     // 256/GPU: 1.10 M samples/s at 256 vs 1.04 M at 384)
     static const long env_target = getenv("FM_GEMM_SPLIT_BLOCKS") ? std::max(1L, atol(getenv("FM_GEMM_SPLIT_BLOCKS"))) : 0L;
     const long target = env_target > 0 ? env_target : (K >= 4096 ? 384L : 256L);
-    while (tiles * ks < target && ks * 2 <= ktiles / 2 && ks < 16) ks *= 2;
+    static const int ks_max = getenv("FM_GEMM_KSPLIT_MAX") ? std::max(1, atoi(getenv("FM_GEMM_KSPLIT_MAX"))) : 16;
+    while (tiles * ks < target && ks * 2 <= ktiles / 2 && ks < ks_max) ks *= 2;
   }
   if (act_y != nullptr || colsum != nullptr) ks = 1;  // fused bwd epilogue needs the full K sum
   if (ks > 1 && !atomic_ok) {
