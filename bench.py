@@ -11,6 +11,13 @@ parallelism) and the MLPs are data parallel (RCCL all-to-all + bucketed all-redu
 
     python bench.py --gpus N --steps K --warmup W          (N>1 under torch.distributed.run)
 
+Precision: the headline ``value`` is the REFERENCE precision, fp32 end to end (the reference is
+fp32 everywhere: cublasSgemm / cuDNN FLOAT) -- fp32 activations, fp32 weights,
+GEMMs on the exact f32-input MFMA (v_mfma_f32_16x16x4_f32).  The bf16 fast mode (bf16
+activations / MFMA operands, fp32 master weights and accumulation) is measured afterwards in the
+same process and reported as a secondary field ``config.bf16`` (``--dtype bf16`` makes it the
+headline, ``--no-secondary`` skips it).
+
 Timed region: W untimed steps, then EXACTLY K full training steps (forward, backward, all
 collectives, SGD update of every parameter incl. the sparse embedding rows) bracketed by a
 barrier + device synchronize on both sides; the max over ranks is reported.  Prints ONE JSON line.
@@ -43,6 +50,9 @@ def parse():
     ap.add_argument("--search-budget", type=int, default=4000)
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--table-scale", type=float, default=1.0, help="debug only: shrink tables (invalid for reporting)")
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="headline compute precision (fp32 = the reference's precision)")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the secondary run in the other precision")
     return ap.parse_args()
 
 
@@ -57,6 +67,30 @@ def main():
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     if torch.cuda.is_available():
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    cuda = torch.cuda.is_available()
+    head = run_once(a, a.dtype, comm)
+    second = None
+    if cuda and not a.no_secondary:
+        second = run_once(a, "bf16" if a.dtype == "fp32" else "fp32", comm)
+    if rank == 0:
+        rec = head["rec"]
+        if second is not None:
+            rec["config"][second["dtype"]] = {"value": second["rec"]["value"], "ms_per_step": second["rec"]["ms_per_step"],
+                                              "loss": second["rec"]["config"]["loss"]}
+        print(f"ELAPSED TIME = {head['el']:.4f}s, THROUGHPUT = {rec['value']:.2f} samples/s", file=sys.stderr)
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def run_once(a, dtype, comm):
+    """Build, warm up and time one DLRM training configuration in compute precision ``dtype``;
+    frees the model before returning (the tables of the two precisions never coexist)."""
+    import gc
+    import torch
+    import torch.distributed as dist
+    rank, world = comm.rank, comm.world
     from flexmi.core import FFConfig, FFModel, SGDOptimizer, LossType, MetricsType
     from flexmi.models.dlrm import DLRMConfig, build_dlrm, dlrm_strategy, SyntheticDLRMData
 
@@ -66,6 +100,7 @@ def main():
     cfg = FFConfig()
     cfg.batchSize = a.batch_per_gpu * world
     cfg.profiling = a.profile
+    cfg.compute_dtype = dtype if torch.cuda.is_available() else "fp32"
     model = FFModel(cfg)
     dense_in, sparse, out = build_dlrm(model, dcfg)
     strategies = {}
@@ -92,7 +127,7 @@ def main():
     data = SyntheticDLRMData(model, dense_in, sparse, dcfg, num_batches=4, seed=rank)
 
     use_graph = (not a.no_graph) and torch.cuda.is_available() and not a.profile
-    step_eager_calls = [0]
+    run_step = stage = None
 
     def step_eager():
         data.next_batch()
@@ -148,46 +183,49 @@ def main():
     gb = cfg.batchSize
     sps = gb * a.steps / el
     met = model.get_perf_metrics()
-    if rank == 0:
-        rec = {
-            "metric": METRIC,
-            "value": round(sps, 1),
-            "unit": "samples/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(ms, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "bf16" if cuda else "fp32",
-            "data": "synthetic",
-            "config": {
-                "model": f"DLRM {dcfg.name} ({'MLPerf-like: 13 dense + 26 sparse, Criteo-TB tables (187.8M rows x 128, fp32), dot interaction' if dcfg.name == 'mlperf' else dcfg.name})",
-                "global_batch": gb,
-                "seq_len": 1,
-                "parallelism": (f"dp{world}" if world == 1 or a.strategy == "dp" else
-                                f"soap-search{world}" if a.strategy == "search" else f"table-wise-emb{world}+dp{world}-mlp"),
-                "tables_rows": sum(dcfg.embedding_size),
-                "embedding_dim": dcfg.sparse_feature_size,
-                "mlp_bot": dcfg.mlp_bot,
-                "mlp_top": dcfg.mlp_top,
-                "interaction": dcfg.arch_interaction_op,
-                "hip_graph": bool(use_graph),
-                "init_s": round(t_init, 2),
-                "loss": round(met.get_loss(), 5),
-                "table_scale": a.table_scale,
-            },
-        }
-        if search is not None:
-            rec["config"]["search"] = {k: round(v, 4) for k, v in search.summary().items()}
-        print(f"ELAPSED TIME = {el:.4f}s, THROUGHPUT = {sps:.2f} samples/s", file=sys.stderr)
-        if a.profile:
-            ex.timer.print_summary(file=sys.stderr)
-        print(json.dumps(rec), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    rec = {
+        "metric": METRIC,
+        "value": round(sps, 1),
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": cfg.compute_dtype,
+        "data": "synthetic",
+        "config": {
+            "model": f"DLRM {dcfg.name} ({'MLPerf-like: 13 dense + 26 sparse, Criteo-TB tables (187.8M rows x 128, fp32), dot interaction' if dcfg.name == 'mlperf' else dcfg.name})",
+            "global_batch": gb,
+            "seq_len": 1,
+            "parallelism": (f"dp{world}" if world == 1 or a.strategy == "dp" else
+                            f"soap-search{world}" if a.strategy == "search" else f"table-wise-emb{world}+dp{world}-mlp"),
+            "tables_rows": sum(dcfg.embedding_size),
+            "embedding_dim": dcfg.sparse_feature_size,
+            "mlp_bot": dcfg.mlp_bot,
+            "mlp_top": dcfg.mlp_top,
+            "interaction": dcfg.arch_interaction_op,
+            "hip_graph": bool(use_graph),
+            "init_s": round(t_init, 2),
+            "loss": round(met.get_loss(), 5),
+            "table_scale": a.table_scale,
+        },
+    }
+    if search is not None:
+        rec["config"]["search"] = {k: round(v, 4) for k, v in search.summary().items()}
+    if rank == 0 and a.profile:
+        ex.timer.print_summary(file=sys.stderr)
+    out = {"rec": rec, "el": el, "dtype": cfg.compute_dtype}
+    # release this configuration's device memory before the next one is built
+    ex.release()
+    ex = model = data = step = run_step = stage = None
+    gc.collect()
+    if cuda:
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    return out
 
 
 if __name__ == "__main__":

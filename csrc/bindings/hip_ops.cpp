@@ -13,6 +13,14 @@ int fm_gemm(const void* A, long lda, long sA, int a_kcontig, const void* B, long
             long ldc, long sC, int c_fp32, const float* bias, int M, int N, int K, int batch, float alpha, int beta,
             int act, float* ws, long ws_bytes, int ksplit_req, const void* act_y, long lday, int bwd_act,
             float* colsum, float* rowsum_a, hipStream_t stream);
+int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, const float* B, long ldb, long sB, int b_kcontig,
+                float* C, long ldc, long sC, const float* bias, int M, int N, int K, int batch, float alpha, int beta,
+                int act, float* ws, long ws_bytes, int ksplit_req, const float* act_y, long lday, int bwd_act,
+                float* colsum, float* rowsum_a, hipStream_t stream);
+void fm_skinny_fwd_f32_launch(const float* x, long ldx, const float* w, const float* bias, float* y, long ldy, long B, int K,
+                              int act, hipStream_t s);
+void fm_skinny_bwd_f32_launch(const float* x, long ldx, const float* w, const float* y, long ldy, const float* dy, long lddy,
+                              float* dx, long lddx, int dx_acc, float* dw, float* db, long B, int K, int act, hipStream_t s);
 void fm_skinny_fwd(const void* x, long ldx, const void* w, const float* bias, void* y, long ldy, long B, int K, int act,
                    hipStream_t s);
 void fm_skinny_bwd(const void* x, long ldx, const void* w, const void* y, long ldy, const void* dy, long lddy, void* dx,
@@ -34,9 +42,13 @@ void fm_dot_interaction_fwd(const void* const* z, int F, long ldz, void* out, lo
                             hipStream_t s);
 void fm_dot_interaction_bwd(const void* const* z, int F, long ldz, const void* dout, long ldo, void* const* dz, long lddz,
                             unsigned acc_mask, long B, int D, int self, hipStream_t s);
-void fm_sgd_update(float* W, const float* G, float* V, unsigned short* Wc, const float* lr, long n, float wd, float mom,
+void fm_dot_interaction_fwd_f32(const float* const* z, int F, long ldz, float* out, long ldo, long B, int D, int W, int self,
+                                hipStream_t s);
+void fm_dot_interaction_bwd_f32(const float* const* z, int F, long ldz, const float* dout, long ldo, float* const* dz,
+                                long lddz, unsigned acc_mask, long B, int D, int self, hipStream_t s);
+void fm_sgd_update(float* W, float* G, float* V, unsigned short* Wc, const float* lr, long n, float wd, float mom,
                    int nesterov, int zero_g, hipStream_t s);
-void fm_adam_update(float* W, const float* G, float* M, float* V, unsigned short* Wc, long n, const float* alpha_t,
+void fm_adam_update(float* W, float* G, float* M, float* V, unsigned short* Wc, long n, const float* alpha_t,
                     float b1, float b2, float wd, float eps, int zero_g, hipStream_t s);
 void fm_cast_bf16(const float* src, unsigned short* dst, long n, hipStream_t s);
 void fm_loss_fwd_bwd(const void* logits, int logits_bf16, const void* labels, void* grad, int grad_bf16, long B, int C,
@@ -47,7 +59,7 @@ void fm_unary_backward(int code, const void* x, const void* y, const void* dy, v
 void fm_binary_forward(int code, const void* a, const void* b, void* y, long n, int bf16, hipStream_t s);
 void fm_binary_backward(int code, const void* a, const void* b, const void* dy, void* da, void* db, long n, int acca,
                         int accb, int bf16, hipStream_t s);
-void fm_act_bwd_bias(const void* y, const void* dy, void* dpre, float* db, long B, int N, int act, hipStream_t s);
+void fm_act_bwd_bias(const void* y, const void* dy, void* dpre, float* db, long B, int N, int act, int bf16, hipStream_t s);
 void fm_multi_copy2d(int n, const void* const* src, void* const* dst, const long* rows, const long* cols, const long* lds,
                      const long* ldd, int add_mask, int elem_bytes, hipStream_t s);
 void fm_permute_nd(const void* x, void* y, int nd, const long* out_dims, const long* in_strides_perm, int acc, int bf16,
@@ -57,25 +69,26 @@ void fm_softmax_fwd(const void* x, void* y, long rows, int C, int bf16, hipStrea
 void fm_dropout_apply(const void* x, void* y, long n, float rate, unsigned seed, unsigned step, int acc, int bf16,
                       hipStream_t s);
 void fm_im2col(const void* x, void* col, int N, int C, int H, int W, int R, int S, int P, int Q, int sh, int sw, int pt,
-               int pl, int ldcol, hipStream_t st);
+               int pl, int ldcol, int bf16, hipStream_t st);
 void fm_col2im(const void* dcol, void* dx, int N, int C, int H, int W, int R, int S, int P, int Q, int sh, int sw, int pt,
-               int pl, int ldcol, int acc, hipStream_t st);
-void fm_transpose_batched(const void* in, const void* yin, void* out, int N, int A, int B, int act, int mode, hipStream_t st);
+               int pl, int ldcol, int acc, int bf16, hipStream_t st);
+void fm_transpose_batched(const void* in, const void* yin, void* out, int N, int A, int B, int act, int mode, int bf16,
+                          hipStream_t st);
 void fm_pool_fwd(const void* x, void* y, int N, int C, int H, int W, int P, int Q, int kh, int kw, int sh, int sw, int pt,
-                 int pl, int is_max, int act, hipStream_t st);
+                 int pl, int is_max, int act, int bf16, hipStream_t st);
 void fm_pool_bwd(const void* x, const void* y, const void* dy, void* dx, int N, int C, int H, int W, int P, int Q, int kh,
-                 int kw, int sh, int sw, int pt, int pl, int is_max, int act, int acc, hipStream_t st);
+                 int kw, int sh, int sw, int pt, int pl, int is_max, int act, int acc, int bf16, hipStream_t st);
 void fm_bn_fwd(const void* x, void* y, const float* gamma, const float* beta, float* stats, float* meaninv, int N, int C,
-               int HW, float eps, int relu, hipStream_t st);
+               int HW, float eps, int relu, int bf16, hipStream_t st);
 void fm_bn_bwd(const void* x, const void* y, const void* dy, const float* meaninv, const float* gamma, float* gsum,
-               float* dgamma, float* dbeta, void* dx, int N, int C, int HW, int relu, int acc, hipStream_t st);
+               float* dgamma, float* dbeta, void* dx, int N, int C, int HW, int relu, int acc, int bf16, hipStream_t st);
 void fm_compact_rows(const float* src, float* dst, int K, int n, int ldp, int acc, hipStream_t st);
-void fm_pad_rows(const void* src, void* dst, int K, int n, int ldp, hipStream_t st);
-void fm_lstm_init(const void* h0, const void* c0, void* hprev, long ldhp, float* cinit, int B, int H, hipStream_t s);
+void fm_pad_rows(const void* src, void* dst, int K, int n, int ldp, int bf16, hipStream_t st);
+void fm_lstm_init(const void* h0, const void* c0, void* hprev, long ldhp, float* cinit, int B, int H, int bf16, hipStream_t s);
 void fm_lstm_cell_fwd(float* G, long ldg, const float* c_prev, long ldcp, float* c_out, long ldc, void* y, long ldy,
-                      void* hprev_next, long ldhp, void* hT, void* cT, int B, int H, hipStream_t s);
+                      void* hprev_next, long ldhp, void* hT, void* cT, int B, int H, int bf16, hipStream_t s);
 void fm_lstm_cell_bwd(const float* A, long lda, const float* c_t, long ldc, const float* c_prev, long ldcp,
-                      const void* dy, long ldy, const float* dh, float* dc, void* dG, long lddg, int B, int H,
+                      const void* dy, long ldy, const float* dh, float* dc, void* dG, long lddg, int B, int H, int bf16,
                       hipStream_t s);
 }
 
@@ -101,8 +114,14 @@ int gemm(torch::Tensor A, int64_t lda, int64_t sA, bool a_kcontig, torch::Tensor
   check_cuda(A, "A");
   check_cuda(B, "B");
   check_cuda(C, "C");
-  TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "gemm operands must be bf16");
+  // bf16 operands (MFMA bf16, bf16 or fp32 C) or fp32 operands (reference-precision path:
+  // v_mfma_f32_16x16x4_f32, fp32 C, gemm_f32.hip)
+  const bool f32 = A.scalar_type() == torch::kFloat32;
+  TORCH_CHECK((A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16) ||
+                  (f32 && B.scalar_type() == torch::kFloat32),
+              "gemm operands must both be bf16 or both fp32");
   TORCH_CHECK(C.scalar_type() == torch::kBFloat16 || C.scalar_type() == torch::kFloat32, "gemm output bf16/fp32");
+  TORCH_CHECK(!f32 || C.scalar_type() == torch::kFloat32, "fp32 gemm: fp32 output");
   // extent checks (the kernel trusts these): last element of each operand must be inside the storage
   auto lastA = a_kcontig ? (M - 1) * lda + (K - 1) : (K - 1) * lda + (M - 1);
   auto lastB = b_kcontig ? (N - 1) * ldb + (K - 1) : (K - 1) * ldb + (N - 1);
@@ -115,8 +134,8 @@ int gemm(torch::Tensor A, int64_t lda, int64_t sA, bool a_kcontig, torch::Tensor
     TORCH_CHECK(bias->scalar_type() == torch::kFloat32 && bias->numel() >= N, "bias must be fp32 [N]");
   }
   if (act_y.has_value() && act_y->defined()) {
-    TORCH_CHECK(act_y->scalar_type() == torch::kBFloat16 && batch == 1 && (M - 1) * lday + N <= act_y->numel(),
-                "gemm act_y: bf16 [M, >=N]");
+    TORCH_CHECK(act_y->scalar_type() == A.scalar_type() && batch == 1 && (M - 1) * lday + N <= act_y->numel(),
+                "gemm act_y: [M, >=N] of the operand dtype");
   }
   if (rowsum_a.has_value() && rowsum_a->defined()) {
     TORCH_CHECK(!a_kcontig && rowsum_a->scalar_type() == torch::kFloat32 && rowsum_a->numel() >= M && batch == 1,
@@ -131,6 +150,11 @@ int gemm(torch::Tensor A, int64_t lda, int64_t sA, bool a_kcontig, torch::Tensor
     w = ws->data_ptr<float>();
     wsb = ws->numel() * 4;
   }
+  if (f32)
+    return fm_gemm_f32(A.data_ptr<float>(), lda, sA, a_kcontig, B.data_ptr<float>(), ldb, sB, b_kcontig, C.data_ptr<float>(),
+                       ldc, sC, bias.has_value() && bias->defined() ? bias->data_ptr<float>() : nullptr, (int)M, (int)N,
+                       (int)K, (int)batch, (float)alpha, beta ? 1 : 0, (int)act, w, wsb, (int)ksplit,
+                       (const float*)cptr(act_y), lday, (int)bwd_act, (float*)mptr(colsum), (float*)mptr(rowsum_a), cur());
   return fm_gemm(A.data_ptr(), lda, sA, a_kcontig, B.data_ptr(), ldb, sB, b_kcontig, C.data_ptr(), ldc, sC,
                  C.scalar_type() == torch::kFloat32, bias.has_value() && bias->defined() ? bias->data_ptr<float>() : nullptr,
                  (int)M, (int)N, (int)K, (int)batch, (float)alpha, beta ? 1 : 0, (int)act, w, wsb, (int)ksplit,
@@ -139,6 +163,13 @@ int gemm(torch::Tensor A, int64_t lda, int64_t sA, bool a_kcontig, torch::Tensor
 
 void skinny_fwd(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor y, int64_t act) {
   TORCH_CHECK(w.numel() == x.size(1) && y.size(1) == 1 && x.stride(1) == 1, "skinny_fwd: x[B,K] w[1,K] y[B,1]");
+  TORCH_CHECK(x.scalar_type() == w.scalar_type() && x.scalar_type() == y.scalar_type(), "skinny_fwd: one dtype");
+  if (x.scalar_type() == torch::kFloat32) {
+    fm_skinny_fwd_f32_launch(x.data_ptr<float>(), x.stride(0), w.data_ptr<float>(),
+                             bias.has_value() && bias->defined() ? bias->data_ptr<float>() : nullptr, y.data_ptr<float>(),
+                             y.stride(0), x.size(0), (int)x.size(1), (int)act, cur());
+    return;
+  }
   fm_skinny_fwd(x.data_ptr(), x.stride(0), w.data_ptr(), bias.has_value() && bias->defined() ? bias->data_ptr<float>() : nullptr,
                 y.data_ptr(), y.stride(0), x.size(0), (int)x.size(1), (int)act, cur());
 }
@@ -146,8 +177,18 @@ void skinny_fwd(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> b
 void skinny_bwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, torch::Tensor dy, c10::optional<torch::Tensor> dx, bool dx_acc,
                 torch::Tensor dw, c10::optional<torch::Tensor> db, int64_t act) {
   TORCH_CHECK(w.numel() == x.size(1) && dw.numel() == x.size(1), "skinny_bwd: shapes");
-  TORCH_CHECK(x.size(1) % 8 == 0 && x.size(1) <= 2048 && x.stride(0) % 8 == 0, "skinny_bwd: K % 8 == 0, K <= 2048");
   long lddx = (dx.has_value() && dx->defined()) ? dx->stride(0) : 0;
+  if (x.scalar_type() == torch::kFloat32) {
+    TORCH_CHECK(w.scalar_type() == torch::kFloat32 && y.scalar_type() == torch::kFloat32 && dy.scalar_type() == torch::kFloat32,
+                "skinny_bwd: fp32 operands");
+    TORCH_CHECK(x.size(1) % 4 == 0 && x.size(1) <= 1024 && x.stride(0) % 4 == 0 && lddx % 4 == 0,
+                "skinny_bwd fp32: K % 4 == 0, K <= 1024");
+    fm_skinny_bwd_f32_launch(x.data_ptr<float>(), x.stride(0), w.data_ptr<float>(), y.data_ptr<float>(), y.stride(0),
+                             dy.data_ptr<float>(), dy.stride(0), (float*)mptr(dx), lddx, dx_acc ? 1 : 0, dw.data_ptr<float>(),
+                             (float*)mptr(db), x.size(0), (int)x.size(1), (int)act, cur());
+    return;
+  }
+  TORCH_CHECK(x.size(1) % 8 == 0 && x.size(1) <= 2048 && x.stride(0) % 8 == 0, "skinny_bwd: K % 8 == 0, K <= 2048");
   fm_skinny_bwd(x.data_ptr(), x.stride(0), w.data_ptr(), y.data_ptr(), y.stride(0), dy.data_ptr(), dy.stride(0), mptr(dx), lddx,
                 dx_acc ? 1 : 0, dw.data_ptr<float>(), (float*)mptr(db), x.size(0), (int)x.size(1), (int)act, cur());
 }
@@ -282,11 +323,20 @@ void dot_fwd(std::vector<torch::Tensor> zs, int64_t ldz, torch::Tensor out, int6
   TORCH_CHECK(zs.size() >= 1 && zs.size() <= 32, "dot interaction: 1..32 features");
   std::vector<const void*> p;
   long B = out.size(0);
+  const auto dt = out.scalar_type();
+  TORCH_CHECK(dt == torch::kBFloat16 || dt == torch::kFloat32, "dot interaction: bf16 or fp32");
+  TORCH_CHECK(out.numel() >= (B - 1) * ldo + W, "dot output too small");
   for (auto& z : zs) {
     check_cuda(z, "z");
-    TORCH_CHECK(z.scalar_type() == torch::kBFloat16, "dot interaction inputs must be bf16");
+    TORCH_CHECK(z.scalar_type() == dt, "dot interaction inputs must match the output dtype");
     TORCH_CHECK(z.numel() >= (B - 1) * ldz + D, "dot input too small");
     p.push_back(z.data_ptr());
+  }
+  if (dt == torch::kFloat32) {
+    TORCH_CHECK(D % 2 == 0, "dot interaction fp32: even D");
+    fm_dot_interaction_fwd_f32((const float* const*)p.data(), (int)p.size(), ldz, out.data_ptr<float>(), ldo, B, (int)D,
+                               (int)W, self ? 1 : 0, cur());
+    return;
   }
   TORCH_CHECK(D % 16 == 0 && W % 8 == 0 && ldz % 8 == 0 && ldo % 8 == 0, "dot interaction: D%16, W%8, ld%8");
   fm_dot_interaction_fwd(p.data(), (int)p.size(), ldz, out.data_ptr(), ldo, B, (int)D, (int)W, self ? 1 : 0, cur());
@@ -298,6 +348,22 @@ void dot_bwd(std::vector<torch::Tensor> zs, int64_t ldz, torch::Tensor dout, int
   std::vector<void*> g;
   for (auto& z : zs) p.push_back(z.data_ptr());
   for (auto& d : dzs) g.push_back(mptr(d));
+  TORCH_CHECK(zs.size() >= 1 && zs.size() <= 32 && dzs.size() == zs.size(), "dot interaction backward: 1..32 features");
+  if (dout.scalar_type() == torch::kFloat32) {
+    const long B = dout.size(0);
+    const long F = (long)zs.size();
+    const long np = self ? F * (F + 1) / 2 : F * (F - 1) / 2;
+    TORCH_CHECK(D % 2 == 0 && D <= 256, "dot interaction backward fp32: even D <= 256");
+    TORCH_CHECK(dout.numel() >= (B - 1) * ldo + ((D + np + 3) & ~3L) && ldo >= ((D + np + 3) & ~3L),
+                "dot interaction backward: dOut row too small");
+    for (size_t i = 0; i < zs.size(); ++i) {
+      TORCH_CHECK(zs[i].scalar_type() == torch::kFloat32 && zs[i].numel() >= (B - 1) * ldz + D, "dot bwd: fp32 inputs");
+      if (g[i]) TORCH_CHECK(dzs[i]->scalar_type() == torch::kFloat32 && dzs[i]->numel() >= (B - 1) * lddz + D, "dot bwd: fp32 grads");
+    }
+    fm_dot_interaction_bwd_f32((const float* const*)p.data(), (int)F, ldz, dout.data_ptr<float>(), ldo, (float* const*)g.data(),
+                               lddz, (unsigned)acc_mask, B, (int)D, self ? 1 : 0, cur());
+    return;
+  }
   TORCH_CHECK(D % 8 == 0 && D <= 256, "dot interaction backward: D % 8 == 0, D <= 256");
   fm_dot_interaction_bwd(p.data(), (int)p.size(), ldz, dout.data_ptr(), ldo, g.data(), lddz, (unsigned)acc_mask,
                          dout.size(0), (int)D, self ? 1 : 0, cur());
@@ -342,8 +408,10 @@ void binary_bwd(int64_t code, torch::Tensor a, torch::Tensor b, torch::Tensor dy
 }
 void act_bwd_bias(torch::Tensor y, torch::Tensor dy, c10::optional<torch::Tensor> dpre, c10::optional<torch::Tensor> db,
                   int64_t B, int64_t N, int64_t act) {
-  TORCH_CHECK(y.scalar_type() == torch::kBFloat16 && dy.scalar_type() == torch::kBFloat16, "act_bwd_bias: bf16");
-  fm_act_bwd_bias(y.data_ptr(), dy.data_ptr(), mptr(dpre), (float*)mptr(db), B, (int)N, (int)act, cur());
+  TORCH_CHECK(y.scalar_type() == dy.scalar_type() && (y.scalar_type() == torch::kBFloat16 || y.scalar_type() == torch::kFloat32),
+              "act_bwd_bias: bf16 or fp32");
+  if (dpre.has_value() && dpre->defined()) TORCH_CHECK(dpre->scalar_type() == y.scalar_type(), "act_bwd_bias: dpre dtype");
+  fm_act_bwd_bias(y.data_ptr(), dy.data_ptr(), mptr(dpre), (float*)mptr(db), B, (int)N, (int)act, is_bf16(y), cur());
 }
 void multi_copy(std::vector<torch::Tensor> src, std::vector<int64_t> src_off, std::vector<torch::Tensor> dst,
                 std::vector<int64_t> dst_off, std::vector<int64_t> rows, std::vector<int64_t> cols, std::vector<int64_t> lds,
@@ -378,39 +446,48 @@ void dropout(torch::Tensor x, torch::Tensor y, double rate, int64_t seed, int64_
 // ----------------------------------------------------------------------------- CNN
 static void chk4(const torch::Tensor& t, const char* n) {
   check_cuda(t, n);
-  TORCH_CHECK(t.scalar_type() == torch::kBFloat16 && t.is_contiguous(), n, ": contiguous bf16");
+  TORCH_CHECK((t.scalar_type() == torch::kBFloat16 || t.scalar_type() == torch::kFloat32) && t.is_contiguous(), n,
+              ": contiguous bf16 or fp32");
+}
+static void same_dt(const torch::Tensor& a, const torch::Tensor& b, const char* n) {
+  TORCH_CHECK(a.scalar_type() == b.scalar_type(), n, ": operands must share one dtype");
 }
 void im2col(torch::Tensor x, torch::Tensor col, int64_t R, int64_t S, int64_t P, int64_t Q, int64_t sh, int64_t sw,
             int64_t pt, int64_t pl, int64_t ldcol) {
   chk4(x, "x");
   chk4(col, "col");
   TORCH_CHECK(x.dim() == 4, "im2col: NCHW");
+  same_dt(x, col, "im2col");
   const long N = x.size(0), C = x.size(1);
   TORCH_CHECK(ldcol >= C * R * S && col.numel() >= N * P * Q * ldcol, "im2col: col too small");
-  fm_im2col(x.data_ptr(), col.data_ptr(), N, C, x.size(2), x.size(3), R, S, P, Q, sh, sw, pt, pl, ldcol, cur());
+  fm_im2col(x.data_ptr(), col.data_ptr(), N, C, x.size(2), x.size(3), R, S, P, Q, sh, sw, pt, pl, ldcol, is_bf16(x), cur());
 }
 void col2im(torch::Tensor dcol, torch::Tensor dx, int64_t R, int64_t S, int64_t P, int64_t Q, int64_t sh, int64_t sw,
             int64_t pt, int64_t pl, int64_t ldcol, bool acc) {
   chk4(dcol, "dcol");
   chk4(dx, "dx");
+  same_dt(dcol, dx, "col2im");
   const long N = dx.size(0), C = dx.size(1);
   TORCH_CHECK(ldcol >= C * R * S && dcol.numel() >= N * P * Q * ldcol, "col2im: dcol too small");
-  fm_col2im(dcol.data_ptr(), dx.data_ptr(), N, C, dx.size(2), dx.size(3), R, S, P, Q, sh, sw, pt, pl, ldcol, acc, cur());
+  fm_col2im(dcol.data_ptr(), dx.data_ptr(), N, C, dx.size(2), dx.size(3), R, S, P, Q, sh, sw, pt, pl, ldcol, acc, is_bf16(dx),
+            cur());
 }
 void transpose_batched(torch::Tensor in, c10::optional<torch::Tensor> yin, torch::Tensor out, int64_t N, int64_t A,
                        int64_t B, int64_t act, int64_t mode) {
   chk4(out, "out");
-  TORCH_CHECK(in.scalar_type() == torch::kBFloat16 && in.numel() >= N * A * B && out.numel() >= N * A * B,
-              "transpose_batched: bf16 extents");
+  TORCH_CHECK(in.scalar_type() == out.scalar_type() && in.numel() >= N * A * B && out.numel() >= N * A * B,
+              "transpose_batched: one dtype, extents");
+  if (mode == 1) TORCH_CHECK(yin.has_value() && yin->scalar_type() == in.scalar_type(), "transpose_batched: yin dtype");
   TORCH_CHECK(mode == 0 || (yin.has_value() && yin->numel() >= N * A * B), "transpose_batched: mode 1 needs yin");
-  fm_transpose_batched(in.data_ptr(), cptr(yin), out.data_ptr(), N, A, B, act, mode, cur());
+  fm_transpose_batched(in.data_ptr(), cptr(yin), out.data_ptr(), N, A, B, act, mode, is_bf16(out), cur());
 }
 void pool_fwd(torch::Tensor x, torch::Tensor y, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t pt, int64_t pl,
               bool is_max, int64_t act) {
   chk4(x, "x");
   chk4(y, "y");
+  same_dt(x, y, "pool_fwd");
   fm_pool_fwd(x.data_ptr(), y.data_ptr(), x.size(0), x.size(1), x.size(2), x.size(3), y.size(2), y.size(3), kh, kw, sh, sw,
-              pt, pl, is_max, act, cur());
+              pt, pl, is_max, act, is_bf16(x), cur());
 }
 void pool_bwd(torch::Tensor x, torch::Tensor y, torch::Tensor dy, torch::Tensor dx, int64_t kh, int64_t kw, int64_t sh,
               int64_t sw, int64_t pt, int64_t pl, bool is_max, int64_t act, bool acc) {
@@ -418,38 +495,45 @@ void pool_bwd(torch::Tensor x, torch::Tensor y, torch::Tensor dy, torch::Tensor 
   chk4(y, "y");
   chk4(dy, "dy");
   chk4(dx, "dx");
+  same_dt(x, y, "pool_bwd");
+  same_dt(x, dy, "pool_bwd");
+  same_dt(x, dx, "pool_bwd");
   fm_pool_bwd(x.data_ptr(), y.data_ptr(), dy.data_ptr(), dx.data_ptr(), x.size(0), x.size(1), x.size(2), x.size(3),
-              y.size(2), y.size(3), kh, kw, sh, sw, pt, pl, is_max, act, acc, cur());
+              y.size(2), y.size(3), kh, kw, sh, sw, pt, pl, is_max, act, acc, is_bf16(x), cur());
 }
 void bn_fwd(torch::Tensor x, torch::Tensor y, torch::Tensor gamma, torch::Tensor beta, torch::Tensor stats,
             torch::Tensor meaninv, double eps, bool relu) {
   chk4(x, "x");
   chk4(y, "y");
+  same_dt(x, y, "bn_fwd");
   const long C = x.size(1);
   TORCH_CHECK(gamma.scalar_type() == torch::kFloat32 && beta.scalar_type() == torch::kFloat32 && gamma.numel() >= C,
               "bn: fp32 gamma/beta [C]");
   TORCH_CHECK(stats.numel() >= 2 * C && meaninv.numel() >= 2 * C, "bn: stats [2C]");
   fm_bn_fwd(x.data_ptr(), y.data_ptr(), gamma.data_ptr<float>(), beta.data_ptr<float>(), stats.data_ptr<float>(),
-            meaninv.data_ptr<float>(), x.size(0), C, x.size(2) * x.size(3), (float)eps, relu, cur());
+            meaninv.data_ptr<float>(), x.size(0), C, x.size(2) * x.size(3), (float)eps, relu, is_bf16(x), cur());
 }
 void bn_bwd(torch::Tensor x, torch::Tensor y, torch::Tensor dy, torch::Tensor meaninv, torch::Tensor gamma,
             torch::Tensor gsum, torch::Tensor dgamma, torch::Tensor dbeta, c10::optional<torch::Tensor> dx, bool relu,
             bool acc) {
   chk4(x, "x");
   chk4(dy, "dy");
+  same_dt(x, dy, "bn_bwd");
+  same_dt(x, y, "bn_bwd");
+  if (dx.has_value() && dx->defined()) same_dt(x, *dx, "bn_bwd");
   const long C = x.size(1);
   TORCH_CHECK(gsum.numel() >= 2 * C && dgamma.numel() >= C && dbeta.numel() >= C, "bn_bwd: sizes");
   fm_bn_bwd(x.data_ptr(), y.data_ptr(), dy.data_ptr(), meaninv.data_ptr<float>(), gamma.data_ptr<float>(),
             gsum.data_ptr<float>(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), mptr(dx), x.size(0), C,
-            x.size(2) * x.size(3), relu, acc, cur());
+            x.size(2) * x.size(3), relu, acc, is_bf16(x), cur());
 }
 void compact_rows(torch::Tensor src, torch::Tensor dst, int64_t K, int64_t n, int64_t ldp, bool acc) {
   TORCH_CHECK(src.numel() >= K * ldp && dst.numel() >= K * n, "compact_rows: sizes");
   fm_compact_rows(src.data_ptr<float>(), dst.data_ptr<float>(), K, n, ldp, acc, cur());
 }
 void pad_rows(torch::Tensor src, torch::Tensor dst, int64_t K, int64_t n, int64_t ldp) {
-  TORCH_CHECK(src.numel() >= K * n && dst.numel() >= K * ldp && src.scalar_type() == torch::kBFloat16, "pad_rows: sizes");
-  fm_pad_rows(src.data_ptr(), dst.data_ptr(), K, n, ldp, cur());
+  TORCH_CHECK(src.numel() >= K * n && dst.numel() >= K * ldp && src.scalar_type() == dst.scalar_type(), "pad_rows: sizes");
+  fm_pad_rows(src.data_ptr(), dst.data_ptr(), K, n, ldp, is_bf16(src), cur());
 }
 
 // ----------------------------------------------------------------------------- LSTM
@@ -457,14 +541,16 @@ static float* fp(torch::Tensor& t, int64_t off) {
   TORCH_CHECK(t.scalar_type() == torch::kFloat32 && off >= 0 && off < t.numel(), "lstm: fp32 buffer/offset");
   return t.data_ptr<float>() + off;
 }
+// activation-dtype (bf16 or fp32) buffer at an element offset
 static void* bp(torch::Tensor& t, int64_t off) {
-  TORCH_CHECK(t.scalar_type() == torch::kBFloat16 && off >= 0 && off < t.numel(), "lstm: bf16 buffer/offset");
-  return (char*)t.data_ptr() + 2 * off;
+  TORCH_CHECK((t.scalar_type() == torch::kBFloat16 || t.scalar_type() == torch::kFloat32) && off >= 0 && off < t.numel(),
+              "lstm: bf16/fp32 buffer/offset");
+  return (char*)t.data_ptr() + t.element_size() * off;
 }
 void lstm_init(c10::optional<torch::Tensor> h0, c10::optional<torch::Tensor> c0, torch::Tensor hprev, int64_t ldhp,
                torch::Tensor cinit, int64_t B, int64_t H) {
   TORCH_CHECK(hprev.numel() >= (B - 1) * ldhp + H && cinit.numel() >= B * H, "lstm_init: sizes");
-  fm_lstm_init(cptr(h0), cptr(c0), bp(hprev, 0), ldhp, fp(cinit, 0), B, H, cur());
+  fm_lstm_init(cptr(h0), cptr(c0), bp(hprev, 0), ldhp, fp(cinit, 0), B, H, is_bf16(hprev), cur());
 }
 void lstm_cell_fwd(torch::Tensor G, int64_t g_off, int64_t ldg, torch::Tensor cprev, int64_t cp_off, int64_t ldcp,
                    torch::Tensor cout, int64_t c_off, int64_t ldc, torch::Tensor y, int64_t y_off, int64_t ldy,
@@ -474,7 +560,7 @@ void lstm_cell_fwd(torch::Tensor G, int64_t g_off, int64_t ldg, torch::Tensor cp
                   y_off + (B - 1) * ldy + H <= y.numel(), "lstm_cell_fwd: extents");
   void* hn = hp_off >= 0 ? bp(hprev, hp_off) : nullptr;
   fm_lstm_cell_fwd(fp(G, g_off), ldg, fp(cprev, cp_off), ldcp, fp(cout, c_off), ldc, bp(y, y_off), ldy, hn, ldhp, mptr(hT),
-                   mptr(cT), B, H, cur());
+                   mptr(cT), B, H, is_bf16(y), cur());
 }
 void lstm_cell_bwd(torch::Tensor A, int64_t a_off, int64_t lda, torch::Tensor ct, int64_t ct_off, int64_t ldc,
                    torch::Tensor cprev, int64_t cp_off, int64_t ldcp, c10::optional<torch::Tensor> dy, int64_t dy_off,
@@ -484,11 +570,11 @@ void lstm_cell_bwd(torch::Tensor A, int64_t a_off, int64_t lda, torch::Tensor ct
                   dh.numel() >= B * H && dc.numel() >= B * H, "lstm_cell_bwd: extents");
   const void* dyp = nullptr;
   if (dy.has_value() && dy->defined()) {
-    TORCH_CHECK(dy_off + (B - 1) * ldy + H <= dy->numel(), "lstm_cell_bwd: dy extent");
-    dyp = (const char*)dy->data_ptr() + 2 * dy_off;
+    TORCH_CHECK(dy_off + (B - 1) * ldy + H <= dy->numel() && dy->scalar_type() == dG.scalar_type(), "lstm_cell_bwd: dy extent");
+    dyp = (const char*)dy->data_ptr() + dy->element_size() * dy_off;
   }
   fm_lstm_cell_bwd(fp(A, a_off), lda, fp(ct, ct_off), ldc, fp(cprev, cp_off), ldcp, dyp, ldy, fp(dh, 0), fp(dc, 0),
-                   bp(dG, dg_off), lddg, B, H, cur());
+                   bp(dG, dg_off), lddg, B, H, is_bf16(dG), cur());
 }
 
 PYBIND11_MODULE(_C, m) {

@@ -20,7 +20,8 @@
 namespace {
 
 // ---- im2col / col2im -------------------------------------------------------------------
-__global__ void __launch_bounds__(256) fm_im2col_kernel(const unsigned short* __restrict__ x, unsigned short* __restrict__ col,
+template <typename T>
+__global__ void __launch_bounds__(256) fm_im2col_kernel(const T* __restrict__ x, T* __restrict__ col,
                                                         int C, int H, int W, int R, int S, int P, int Q, int sh, int sw,
                                                         int pt, int pl, int CRS, int ldcol, long rows) {
   for (long row = blockIdx.x; row < rows; row += gridDim.x) {
@@ -29,10 +30,10 @@ __global__ void __launch_bounds__(256) fm_im2col_kernel(const unsigned short* __
     const int p = (int)(t % P);
     const int n = (int)(t / P);
     const int h0 = p * sh - pt, w0 = q * sw - pl;
-    const unsigned short* xn = x + (long)n * C * H * W;
-    unsigned short* dst = col + row * ldcol;
+    const T* xn = x + (long)n * C * H * W;
+    T* dst = col + row * ldcol;
     for (int k = threadIdx.x; k < ldcol; k += blockDim.x) {
-      unsigned short v = 0;
+      T v = fromf<T>(0.f);
       if (k < CRS) {
         const int s = k % S;
         const int r = (k / S) % R;
@@ -45,7 +46,8 @@ __global__ void __launch_bounds__(256) fm_im2col_kernel(const unsigned short* __
   }
 }
 
-__global__ void __launch_bounds__(256) fm_col2im_kernel(const unsigned short* __restrict__ dcol, unsigned short* __restrict__ dx,
+template <typename T>
+__global__ void __launch_bounds__(256) fm_col2im_kernel(const T* __restrict__ dcol, T* __restrict__ dx,
                                                         int N, int C, int H, int W, int R, int S, int P, int Q, int sh,
                                                         int sw, int pt, int pl, int ldcol, int acc) {
   const long total = (long)N * C * H * W;
@@ -67,18 +69,19 @@ __global__ void __launch_bounds__(256) fm_col2im_kernel(const unsigned short* __
         if (wq < 0 || wq % sw) continue;
         const int q = wq / sw;
         if (q >= Q) continue;
-        s_ += bf2f(dcol[((long)(n * P + p) * Q + q) * ldcol + (c * R + r) * S + s]);
+        s_ += tof(dcol[((long)(n * P + p) * Q + q) * ldcol + (c * R + r) * S + s]);
       }
     }
-    if (acc) s_ += bf2f(dx[i]);
-    dx[i] = f2bf(s_);
+    if (acc) s_ += tof(dx[i]);
+    dx[i] = fromf<T>(s_);
   }
 }
 
 // ---- NHWC <-> NCHW (batched [N][A][B] -> [N][B][A] 32x32 LDS tiles) ----------------------
 // mode 0: plain copy; mode 1: out = act_bwd(act, y_in[same index as in], in) (backward: dy, y NCHW)
-__global__ void __launch_bounds__(256) fm_transpose_kernel(const unsigned short* __restrict__ in, const unsigned short* __restrict__ yin,
-                                                           unsigned short* __restrict__ out, int A, int B, int act, int mode) {
+template <typename T>
+__global__ void __launch_bounds__(256) fm_transpose_kernel(const T* __restrict__ in, const T* __restrict__ yin,
+                                                           T* __restrict__ out, int A, int B, int act, int mode) {
   __shared__ float tile[32][33];
   const long base = (long)blockIdx.z * A * B;
   const int a0 = blockIdx.y * 32, b0 = blockIdx.x * 32;
@@ -88,20 +91,21 @@ __global__ void __launch_bounds__(256) fm_transpose_kernel(const unsigned short*
     float v = 0.f;
     if (a < A && b < B) {
       const long idx = base + (long)a * B + b;
-      v = bf2f(in[idx]);
-      if (mode == 1) v = act_bwd(act, bf2f(yin[idx]), v);
+      v = tof(in[idx]);
+      if (mode == 1) v = act_bwd(act, tof(yin[idx]), v);
     }
     tile[j][tx] = v;
   }
   __syncthreads();
   for (int j = ty; j < 32; j += 8) {
     const int b = b0 + j, a = a0 + tx;
-    if (a < A && b < B) out[base + (long)b * A + a] = f2bf(tile[tx][j]);
+    if (a < A && b < B) out[base + (long)b * A + a] = fromf<T>(tile[tx][j]);
   }
 }
 
 // ---- pooling ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) fm_pool_fwd_kernel(const unsigned short* __restrict__ x, unsigned short* __restrict__ y,
+template <typename T>
+__global__ void __launch_bounds__(256) fm_pool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                           int N, int C, int H, int W, int P, int Q, int kh, int kw, int sh,
                                                           int sw, int pt, int pl, int is_max, int act) {
   const long total = (long)N * C * P * Q;
@@ -110,7 +114,7 @@ __global__ void __launch_bounds__(256) fm_pool_fwd_kernel(const unsigned short* 
     long t = i / Q;
     const int p = (int)(t % P);
     const long nc = t / P;
-    const unsigned short* xp = x + nc * H * W;
+    const T* xp = x + nc * H * W;
     const int h0 = p * sh - pt, w0 = q * sw - pl;
     float m = -INFINITY, s = 0.f;
     int cnt = 0;
@@ -120,19 +124,20 @@ __global__ void __launch_bounds__(256) fm_pool_fwd_kernel(const unsigned short* 
       for (int c = 0; c < kw; ++c) {
         const int w = w0 + c;
         if (w < 0 || w >= W) continue;
-        const float v = bf2f(xp[h * W + w]);
+        const float v = tof(xp[h * W + w]);
         m = fmaxf(m, v);
         s += v;
         ++cnt;
       }
     }
     const float o = is_max ? m : (cnt ? s / cnt : 0.f);
-    y[i] = f2bf(act_fwd(act, o));
+    y[i] = fromf<T>(act_fwd(act, o));
   }
 }
 
-__global__ void __launch_bounds__(256) fm_pool_bwd_kernel(const unsigned short* __restrict__ x, const unsigned short* __restrict__ y,
-                                                          const unsigned short* __restrict__ dy, unsigned short* __restrict__ dx,
+template <typename T>
+__global__ void __launch_bounds__(256) fm_pool_bwd_kernel(const T* __restrict__ x, const T* __restrict__ y,
+                                                          const T* __restrict__ dy, T* __restrict__ dx,
                                                           int N, int C, int H, int W, int P, int Q, int kh, int kw, int sh,
                                                           int sw, int pt, int pl, int is_max, int act, int acc) {
   const long total = (long)N * C * H * W;
@@ -141,7 +146,7 @@ __global__ void __launch_bounds__(256) fm_pool_bwd_kernel(const unsigned short* 
     long t = i / W;
     const int h = (int)(t % H);
     const long nc = t / H;
-    const unsigned short* xp = x + nc * H * W;
+    const T* xp = x + nc * H * W;
     float g = 0.f;
     // windows (p, q) containing (h, w): p*sh - pt <= h < p*sh - pt + kh
     const int pmin = max(0, (h + pt - kh + sh) / sh), pmax = min(P - 1, (h + pt) / sh);
@@ -153,7 +158,7 @@ __global__ void __launch_bounds__(256) fm_pool_bwd_kernel(const unsigned short* 
         const int w0 = q * sw - pl;
         if (w < w0 || w >= w0 + kw) continue;
         const long o = (nc * P + p) * Q + q;
-        const float go = act_bwd(act, bf2f(y[o]), bf2f(dy[o]));
+        const float go = act_bwd(act, tof(y[o]), tof(dy[o]));
         if (is_max) {   // gradient goes to the window's first maximum (row-major scan, like PyTorch)
           float best = -INFINITY;
           int bh = -1, bw = -1;
@@ -163,7 +168,7 @@ __global__ void __launch_bounds__(256) fm_pool_bwd_kernel(const unsigned short* 
             for (int c = 0; c < kw; ++c) {
               const int ww = w0 + c;
               if (ww < 0 || ww >= W) continue;
-              const float v = bf2f(xp[hh * W + ww]);
+              const float v = tof(xp[hh * W + ww]);
               if (v > best) { best = v; bh = hh; bw = ww; }
             }
           }
@@ -174,21 +179,22 @@ __global__ void __launch_bounds__(256) fm_pool_bwd_kernel(const unsigned short* 
         }
       }
     }
-    if (acc) g += bf2f(dx[i]);
-    dx[i] = f2bf(g);
+    if (acc) g += tof(dx[i]);
+    dx[i] = fromf<T>(g);
   }
 }
 
 // ---- batch norm (training mode, per-channel statistics over N*H*W) -----------------------
 // stats[0:C] = sum, stats[C:2C] = sum of squares   (zeroed by the caller)
-__global__ void __launch_bounds__(256) fm_bn_stats_kernel(const unsigned short* __restrict__ x, float* __restrict__ stats,
+template <typename T>
+__global__ void __launch_bounds__(256) fm_bn_stats_kernel(const T* __restrict__ x, float* __restrict__ stats,
                                                           int N, int C, int HW) {
   const int c = blockIdx.y;
   float s = 0.f, s2 = 0.f;
   const long per_c = (long)N * HW;
   for (long j = blockIdx.x * (long)blockDim.x + threadIdx.x; j < per_c; j += (long)gridDim.x * blockDim.x) {
     const long n = j / HW, hw = j % HW;
-    const float v = bf2f(x[(n * C + c) * HW + hw]);
+    const float v = tof(x[(n * C + c) * HW + hw]);
     s += v;
     s2 += v * v;
   }
@@ -207,7 +213,8 @@ __global__ void __launch_bounds__(256) fm_bn_stats_kernel(const unsigned short* 
 }
 
 // y = relu?((x - mean) * inv * gamma + beta); meaninv[0:C] = mean, [C:2C] = inv (saved for bwd)
-__global__ void __launch_bounds__(256) fm_bn_apply_kernel(const unsigned short* __restrict__ x, unsigned short* __restrict__ y,
+template <typename T>
+__global__ void __launch_bounds__(256) fm_bn_apply_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                           const float* __restrict__ stats, const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float* __restrict__ meaninv,
                                                           int N, int C, int HW, float eps, int relu) {
@@ -223,15 +230,16 @@ __global__ void __launch_bounds__(256) fm_bn_apply_kernel(const unsigned short* 
       meaninv[i] = mc;
       meaninv[C + i] = rsqrtf(fmaxf(stats[C + i] / m - mc * mc, 0.f) + eps);
     }
-    float v = (bf2f(x[i]) - mean) * inv * gamma[c] + beta[c];
+    float v = (tof(x[i]) - mean) * inv * gamma[c] + beta[c];
     if (relu) v = fmaxf(v, 0.f);
-    y[i] = f2bf(v);
+    y[i] = fromf<T>(v);
   }
 }
 
 // gsum[0:C] += sum g ; gsum[C:2C] += sum g * xhat   (g = relu-masked dy), zeroed by the caller
-__global__ void __launch_bounds__(256) fm_bn_bwd_stats_kernel(const unsigned short* __restrict__ x, const unsigned short* __restrict__ y,
-                                                              const unsigned short* __restrict__ dy, const float* __restrict__ meaninv,
+template <typename T>
+__global__ void __launch_bounds__(256) fm_bn_bwd_stats_kernel(const T* __restrict__ x, const T* __restrict__ y,
+                                                              const T* __restrict__ dy, const float* __restrict__ meaninv,
                                                               float* __restrict__ gsum, int N, int C, int HW, int relu) {
   const int c = blockIdx.y;
   const float mean = meaninv[c], inv = meaninv[C + c];
@@ -240,10 +248,10 @@ __global__ void __launch_bounds__(256) fm_bn_bwd_stats_kernel(const unsigned sho
   for (long j = blockIdx.x * (long)blockDim.x + threadIdx.x; j < per_c; j += (long)gridDim.x * blockDim.x) {
     const long n = j / HW, hw = j % HW;
     const long idx = (n * C + c) * HW + hw;
-    float g = bf2f(dy[idx]);
-    if (relu && bf2f(y[idx]) <= 0.f) g = 0.f;
+    float g = tof(dy[idx]);
+    if (relu && tof(y[idx]) <= 0.f) g = 0.f;
     s += g;
-    s2 += g * (bf2f(x[idx]) - mean) * inv;
+    s2 += g * (tof(x[idx]) - mean) * inv;
   }
   __shared__ float red[2][4];
   s = wave_reduce_sum(s);
@@ -259,22 +267,23 @@ __global__ void __launch_bounds__(256) fm_bn_bwd_stats_kernel(const unsigned sho
   }
 }
 
-__global__ void __launch_bounds__(256) fm_bn_bwd_apply_kernel(const unsigned short* __restrict__ x, const unsigned short* __restrict__ y,
-                                                              const unsigned short* __restrict__ dy, const float* __restrict__ meaninv,
+template <typename T>
+__global__ void __launch_bounds__(256) fm_bn_bwd_apply_kernel(const T* __restrict__ x, const T* __restrict__ y,
+                                                              const T* __restrict__ dy, const float* __restrict__ meaninv,
                                                               const float* __restrict__ gsum, const float* __restrict__ gamma,
-                                                              unsigned short* __restrict__ dx, int N, int C, int HW, int relu,
+                                                              T* __restrict__ dx, int N, int C, int HW, int relu,
                                                               int acc) {
   const long total = (long)N * C * HW;
   const float m = (float)N * HW;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int c = (int)((i / HW) % C);
     const float mean = meaninv[c], inv = meaninv[C + c];
-    float g = bf2f(dy[i]);
-    if (relu && bf2f(y[i]) <= 0.f) g = 0.f;
-    const float xhat = (bf2f(x[i]) - mean) * inv;
+    float g = tof(dy[i]);
+    if (relu && tof(y[i]) <= 0.f) g = 0.f;
+    const float xhat = (tof(x[i]) - mean) * inv;
     float v = gamma[c] * inv / m * (m * g - gsum[c] - xhat * gsum[C + c]);
-    if (acc) v += bf2f(dx[i]);
-    dx[i] = f2bf(v);
+    if (acc) v += tof(dx[i]);
+    dx[i] = fromf<T>(v);
   }
 }
 
@@ -290,102 +299,150 @@ __global__ void __launch_bounds__(256) fm_compact_kernel(const float* __restrict
 }
 
 // pad [K][n] bf16/fp32 weights into [K][ldp] bf16 with zero columns
-__global__ void __launch_bounds__(256) fm_pad_rows_kernel(const unsigned short* __restrict__ src, unsigned short* __restrict__ dst,
+template <typename T>
+__global__ void __launch_bounds__(256) fm_pad_rows_kernel(const T* __restrict__ src, T* __restrict__ dst,
                                                           int K, int n, int ldp) {
   const long total = (long)K * ldp;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const long k = i / ldp, j = i % ldp;
-    dst[i] = j < n ? src[k * n + j] : (unsigned short)0;
+    dst[i] = j < n ? src[k * n + j] : fromf<T>(0.f);
   }
 }
 
 }  // namespace
 
-extern "C" {
+namespace {
 
-void fm_im2col(const void* x, void* col, int N, int C, int H, int W, int R, int S, int P, int Q, int sh, int sw, int pt,
+template <typename T>
+static void fm_im2col_t(const void* x, void* col, int N, int C, int H, int W, int R, int S, int P, int Q, int sh, int sw, int pt,
                int pl, int ldcol, hipStream_t st) {
   const long rows = (long)N * P * Q;
   if (rows <= 0) return;
   const int blocks = (int)std::min<long>(rows, 65536);
-  hipLaunchKernelGGL(fm_im2col_kernel, dim3(blocks), dim3(ldcol >= 256 ? 256 : 128), 0, st, (const unsigned short*)x,
-                     (unsigned short*)col, C, H, W, R, S, P, Q, sh, sw, pt, pl, C * R * S, ldcol, rows);
+  hipLaunchKernelGGL(fm_im2col_kernel<T>, dim3(blocks), dim3(ldcol >= 256 ? 256 : 128), 0, st, (const T*)x,
+                     (T*)col, C, H, W, R, S, P, Q, sh, sw, pt, pl, C * R * S, ldcol, rows);
 }
 
-void fm_col2im(const void* dcol, void* dx, int N, int C, int H, int W, int R, int S, int P, int Q, int sh, int sw, int pt,
+template <typename T>
+static void fm_col2im_t(const void* dcol, void* dx, int N, int C, int H, int W, int R, int S, int P, int Q, int sh, int sw, int pt,
                int pl, int ldcol, int acc, hipStream_t st) {
   const long total = (long)N * C * H * W;
   if (total <= 0) return;
-  hipLaunchKernelGGL(fm_col2im_kernel, dim3(fm_grid(total)), dim3(256), 0, st, (const unsigned short*)dcol,
-                     (unsigned short*)dx, N, C, H, W, R, S, P, Q, sh, sw, pt, pl, ldcol, acc);
+  hipLaunchKernelGGL(fm_col2im_kernel<T>, dim3(fm_grid(total)), dim3(256), 0, st, (const T*)dcol,
+                     (T*)dx, N, C, H, W, R, S, P, Q, sh, sw, pt, pl, ldcol, acc);
 }
 
 // batched [N][A][B] -> [N][B][A]; mode 1 applies act_bwd(act, yin, in) first
-void fm_transpose_batched(const void* in, const void* yin, void* out, int N, int A, int B, int act, int mode, hipStream_t st) {
+template <typename T>
+static void fm_transpose_batched_t(const void* in, const void* yin, void* out, int N, int A, int B, int act, int mode, hipStream_t st) {
   if ((long)N * A * B <= 0) return;
   dim3 grid((B + 31) / 32, (A + 31) / 32, N);
-  hipLaunchKernelGGL(fm_transpose_kernel, grid, dim3(256), 0, st, (const unsigned short*)in, (const unsigned short*)yin,
-                     (unsigned short*)out, A, B, act, mode);
+  hipLaunchKernelGGL(fm_transpose_kernel<T>, grid, dim3(256), 0, st, (const T*)in, (const T*)yin,
+                     (T*)out, A, B, act, mode);
 }
 
-void fm_pool_fwd(const void* x, void* y, int N, int C, int H, int W, int P, int Q, int kh, int kw, int sh, int sw, int pt,
+template <typename T>
+static void fm_pool_fwd_t(const void* x, void* y, int N, int C, int H, int W, int P, int Q, int kh, int kw, int sh, int sw, int pt,
                  int pl, int is_max, int act, hipStream_t st) {
   const long total = (long)N * C * P * Q;
   if (total <= 0) return;
-  hipLaunchKernelGGL(fm_pool_fwd_kernel, dim3(fm_grid(total)), dim3(256), 0, st, (const unsigned short*)x, (unsigned short*)y,
+  hipLaunchKernelGGL(fm_pool_fwd_kernel<T>, dim3(fm_grid(total)), dim3(256), 0, st, (const T*)x, (T*)y,
                      N, C, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act);
 }
 
-void fm_pool_bwd(const void* x, const void* y, const void* dy, void* dx, int N, int C, int H, int W, int P, int Q, int kh,
+template <typename T>
+static void fm_pool_bwd_t(const void* x, const void* y, const void* dy, void* dx, int N, int C, int H, int W, int P, int Q, int kh,
                  int kw, int sh, int sw, int pt, int pl, int is_max, int act, int acc, hipStream_t st) {
   const long total = (long)N * C * H * W;
   if (total <= 0) return;
-  hipLaunchKernelGGL(fm_pool_bwd_kernel, dim3(fm_grid(total)), dim3(256), 0, st, (const unsigned short*)x,
-                     (const unsigned short*)y, (const unsigned short*)dy, (unsigned short*)dx, N, C, H, W, P, Q, kh, kw, sh,
+  hipLaunchKernelGGL(fm_pool_bwd_kernel<T>, dim3(fm_grid(total)), dim3(256), 0, st, (const T*)x,
+                     (const T*)y, (const T*)dy, (T*)dx, N, C, H, W, P, Q, kh, kw, sh,
                      sw, pt, pl, is_max, act, acc);
 }
 
 // stats / meaninv: fp32 [2C] device buffers owned by the op
-void fm_bn_fwd(const void* x, void* y, const float* gamma, const float* beta, float* stats, float* meaninv, int N, int C,
+template <typename T>
+static void fm_bn_fwd_t(const void* x, void* y, const float* gamma, const float* beta, float* stats, float* meaninv, int N, int C,
                int HW, float eps, int relu, hipStream_t st) {
   (void)hipMemsetAsync(stats, 0, sizeof(float) * 2 * C, st);
   const long per_c = (long)N * HW;
   dim3 g1((unsigned)std::max<long>(1, std::min<long>((per_c + 255) / 256, 64)), C);
-  hipLaunchKernelGGL(fm_bn_stats_kernel, g1, dim3(256), 0, st, (const unsigned short*)x, stats, N, C, HW);
+  hipLaunchKernelGGL(fm_bn_stats_kernel<T>, g1, dim3(256), 0, st, (const T*)x, stats, N, C, HW);
   const long total = (long)N * C * HW;
-  hipLaunchKernelGGL(fm_bn_apply_kernel, dim3(fm_grid(total)), dim3(256), 0, st, (const unsigned short*)x,
-                     (unsigned short*)y, stats, gamma, beta, meaninv, N, C, HW, eps, relu);
+  hipLaunchKernelGGL(fm_bn_apply_kernel<T>, dim3(fm_grid(total)), dim3(256), 0, st, (const T*)x,
+                     (T*)y, stats, gamma, beta, meaninv, N, C, HW, eps, relu);
 }
 
 // dgamma/dbeta: fp32 [C] outputs (overwritten); gsum fp32 [2C] scratch
-void fm_bn_bwd(const void* x, const void* y, const void* dy, const float* meaninv, const float* gamma, float* gsum,
+template <typename T>
+static void fm_bn_bwd_t(const void* x, const void* y, const void* dy, const float* meaninv, const float* gamma, float* gsum,
                float* dgamma, float* dbeta, void* dx, int N, int C, int HW, int relu, int acc, hipStream_t st) {
   (void)hipMemsetAsync(gsum, 0, sizeof(float) * 2 * C, st);
   const long per_c = (long)N * HW;
   dim3 g1((unsigned)std::max<long>(1, std::min<long>((per_c + 255) / 256, 64)), C);
-  hipLaunchKernelGGL(fm_bn_bwd_stats_kernel, g1, dim3(256), 0, st, (const unsigned short*)x, (const unsigned short*)y,
-                     (const unsigned short*)dy, meaninv, gsum, N, C, HW, relu);
+  hipLaunchKernelGGL(fm_bn_bwd_stats_kernel<T>, g1, dim3(256), 0, st, (const T*)x, (const T*)y,
+                     (const T*)dy, meaninv, gsum, N, C, HW, relu);
   (void)hipMemcpyAsync(dbeta, gsum, sizeof(float) * C, hipMemcpyDeviceToDevice, st);
   (void)hipMemcpyAsync(dgamma, gsum + C, sizeof(float) * C, hipMemcpyDeviceToDevice, st);
   if (dx) {
     const long total = (long)N * C * HW;
-    hipLaunchKernelGGL(fm_bn_bwd_apply_kernel, dim3(fm_grid(total)), dim3(256), 0, st, (const unsigned short*)x,
-                       (const unsigned short*)y, (const unsigned short*)dy, meaninv, gsum, gamma, (unsigned short*)dx, N, C,
+    hipLaunchKernelGGL(fm_bn_bwd_apply_kernel<T>, dim3(fm_grid(total)), dim3(256), 0, st, (const T*)x,
+                       (const T*)y, (const T*)dy, meaninv, gsum, gamma, (T*)dx, N, C,
                        HW, relu, acc);
   }
 }
 
-void fm_compact_rows(const float* src, float* dst, int K, int n, int ldp, int acc, hipStream_t st) {
+static void fm_compact_rows_t(const float* src, float* dst, int K, int n, int ldp, int acc, hipStream_t st) {
   const long total = (long)K * n;
   if (total <= 0) return;
   hipLaunchKernelGGL(fm_compact_kernel, dim3(fm_grid(total)), dim3(256), 0, st, src, dst, K, n, ldp, acc);
 }
 
-void fm_pad_rows(const void* src, void* dst, int K, int n, int ldp, hipStream_t st) {
+template <typename T>
+static void fm_pad_rows_t(const void* src, void* dst, int K, int n, int ldp, hipStream_t st) {
   const long total = (long)K * ldp;
   if (total <= 0) return;
-  hipLaunchKernelGGL(fm_pad_rows_kernel, dim3(fm_grid(total)), dim3(256), 0, st, (const unsigned short*)src,
-                     (unsigned short*)dst, K, n, ldp);
+  hipLaunchKernelGGL(fm_pad_rows_kernel<T>, dim3(fm_grid(total)), dim3(256), 0, st, (const T*)src,
+                     (T*)dst, K, n, ldp);
 }
 
+}  // namespace
+
+extern "C" {
+void fm_im2col(const void* x, void* col, int N, int C, int H, int W, int R, int S, int P, int Q, int sh, int sw, int pt, int pl, int ldcol, int bf16, hipStream_t st) {
+  if (bf16) fm_im2col_t<unsigned short>(x, col, N, C, H, W, R, S, P, Q, sh, sw, pt, pl, ldcol, st);
+  else fm_im2col_t<float>(x, col, N, C, H, W, R, S, P, Q, sh, sw, pt, pl, ldcol, st);
+}
+void fm_col2im(const void* dcol, void* dx, int N, int C, int H, int W, int R, int S, int P, int Q, int sh, int sw, int pt, int pl, int ldcol, int acc, int bf16, hipStream_t st) {
+  if (bf16) fm_col2im_t<unsigned short>(dcol, dx, N, C, H, W, R, S, P, Q, sh, sw, pt, pl, ldcol, acc, st);
+  else fm_col2im_t<float>(dcol, dx, N, C, H, W, R, S, P, Q, sh, sw, pt, pl, ldcol, acc, st);
+}
+void fm_transpose_batched(const void* in, const void* yin, void* out, int N, int A, int B, int act, int mode, int bf16, hipStream_t st) {
+  if (bf16) fm_transpose_batched_t<unsigned short>(in, yin, out, N, A, B, act, mode, st);
+  else fm_transpose_batched_t<float>(in, yin, out, N, A, B, act, mode, st);
+}
+void fm_pool_fwd(const void* x, void* y, int N, int C, int H, int W, int P, int Q, int kh, int kw, int sh, int sw, int pt, int pl, int is_max, int act, int bf16, hipStream_t st) {
+  if (bf16) fm_pool_fwd_t<unsigned short>(x, y, N, C, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, st);
+  else fm_pool_fwd_t<float>(x, y, N, C, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, st);
+}
+void fm_pool_bwd(const void* x, const void* y, const void* dy, void* dx, int N, int C, int H, int W, int P, int Q, int kh, int kw, int sh, int sw, int pt, int pl, int is_max, int act, int acc, int bf16, hipStream_t st) {
+  if (bf16) fm_pool_bwd_t<unsigned short>(x, y, dy, dx, N, C, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, acc, st);
+  else fm_pool_bwd_t<float>(x, y, dy, dx, N, C, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, acc, st);
+}
+void fm_bn_fwd(const void* x, void* y, const float* gamma, const float* beta, float* stats, float* meaninv, int N, int C, int HW, float eps, int relu, int bf16, hipStream_t st) {
+  if (bf16) fm_bn_fwd_t<unsigned short>(x, y, gamma, beta, stats, meaninv, N, C, HW, eps, relu, st);
+  else fm_bn_fwd_t<float>(x, y, gamma, beta, stats, meaninv, N, C, HW, eps, relu, st);
+}
+void fm_bn_bwd(const void* x, const void* y, const void* dy, const float* meaninv, const float* gamma, float* gsum, float* dgamma, float* dbeta, void* dx, int N, int C, int HW, int relu, int acc, int bf16, hipStream_t st) {
+  if (bf16) fm_bn_bwd_t<unsigned short>(x, y, dy, meaninv, gamma, gsum, dgamma, dbeta, dx, N, C, HW, relu, acc, st);
+  else fm_bn_bwd_t<float>(x, y, dy, meaninv, gamma, gsum, dgamma, dbeta, dx, N, C, HW, relu, acc, st);
+}
+void fm_pad_rows(const void* src, void* dst, int K, int n, int ldp, int bf16, hipStream_t st) {
+  if (bf16) fm_pad_rows_t<unsigned short>(src, dst, K, n, ldp, st);
+  else fm_pad_rows_t<float>(src, dst, K, n, ldp, st);
+}
+
+void fm_compact_rows(const float* src, float* dst, int K, int n, int ldp, int acc, hipStream_t st) {
+  fm_compact_rows_t(src, dst, K, n, ldp, acc, st);
+}
 }  // extern "C"

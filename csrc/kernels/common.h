@@ -21,6 +21,13 @@ FM_DEVICE unsigned short f2bf(float f) {
   return *reinterpret_cast<unsigned short*>(&b);
 }
 
+// value conversion generic over float / bf16 storage (tof: storage -> f32, fromf<T>: f32 -> storage)
+FM_DEVICE float tof(float v) { return v; }
+FM_DEVICE float tof(unsigned short v) { return bf2f(v); }
+template <typename T> FM_DEVICE T fromf(float v);
+template <> FM_DEVICE float fromf<float>(float v) { return v; }
+template <> FM_DEVICE unsigned short fromf<unsigned short>(float v) { return f2bf(v); }
+
 // element loads/stores generic over float / bf16 storage
 template <typename T> FM_DEVICE float ld(const T* p);
 template <> FM_DEVICE float ld<float>(const float* p) { return *p; }
@@ -28,6 +35,31 @@ template <> FM_DEVICE float ld<unsigned short>(const unsigned short* p) { return
 template <typename T> FM_DEVICE void st(T* p, float v);
 template <> FM_DEVICE void st<float>(float* p, float v) { *p = v; }
 template <> FM_DEVICE void st<unsigned short>(unsigned short* p, float v) { *p = f2bf(v); }
+
+// 8 consecutive elements (16-B aligned) as floats: one b128 access for bf16, two for fp32
+template <typename T> FM_DEVICE void ld8(const T* p, float (&v)[8]);
+template <> FM_DEVICE void ld8<unsigned short>(const unsigned short* p, float (&v)[8]) {
+  const bf16x8_t t = *reinterpret_cast<const bf16x8_t*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = bf2f((unsigned short)t[j]);
+}
+template <> FM_DEVICE void ld8<float>(const float* p, float (&v)[8]) {
+  const f32x4_t a = *reinterpret_cast<const f32x4_t*>(p);
+  const f32x4_t b = *reinterpret_cast<const f32x4_t*>(p + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
+}
+template <typename T> FM_DEVICE void st8(T* p, const float (&v)[8]);
+template <> FM_DEVICE void st8<unsigned short>(unsigned short* p, const float (&v)[8]) {
+  bf16x8_t t;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) t[j] = (short)f2bf(v[j]);
+  *reinterpret_cast<bf16x8_t*>(p) = t;
+}
+template <> FM_DEVICE void st8<float>(float* p, const float (&v)[8]) {
+  *reinterpret_cast<f32x4_t*>(p) = f32x4_t{v[0], v[1], v[2], v[3]};
+  *reinterpret_cast<f32x4_t*>(p + 4) = f32x4_t{v[4], v[5], v[6], v[7]};
+}
 
 // activations (ActiMode values of include/ffconst.h)
 enum { ACT_NONE = 10, ACT_RELU = 11, ACT_SIGMOID = 12, ACT_TANH = 13 };

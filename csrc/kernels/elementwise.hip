@@ -80,9 +80,9 @@ __global__ void fm_binary_bwd(int code, const T* __restrict__ a, const T* __rest
 // time -- so a 128-wide layer keeps every lane busy (16 lanes per row, 16 rows per pass) -- and
 // each thread handles four such rows per iteration with all their loads issued first.  Partial
 // column sums meet in LDS; one fp32 atomic per column per block.
-__global__ void __launch_bounds__(256) fm_act_bwd_colsum(const unsigned short* __restrict__ y,
-                                                        const unsigned short* __restrict__ dy,
-                                                        unsigned short* __restrict__ dpre, float* __restrict__ db,
+template <typename T>
+__global__ void __launch_bounds__(256) fm_act_bwd_colsum(const T* __restrict__ y, const T* __restrict__ dy,
+                                                        T* __restrict__ dpre, float* __restrict__ db,
                                                         long B, int N, int act, int tpr, int ROWS) {
   __shared__ float red[256 * 8];
   const int tid = threadIdx.x;
@@ -96,25 +96,24 @@ __global__ void __launch_bounds__(256) fm_act_bwd_colsum(const unsigned short* _
   if (c0 < N) {
     for (long r = r0 + sub; r < rend; r += 4L * rpb) {
       if (vec) {
-        bf16x8_t yy[4], gg[4];
+        float yy[4][8], gg[4][8];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const long o = min(r + u * rpb, rend - 1) * N + c0;    // clamped: unconditional loads
-          yy[u] = *reinterpret_cast<const bf16x8_t*>(y + o);
-          gg[u] = *reinterpret_cast<const bf16x8_t*>(dy + o);
+          ld8<T>(y + o, yy[u]);
+          ld8<T>(dy + o, gg[u]);
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const long rr = r + u * rpb;
           if (rr >= rend) break;
-          bf16x8_t out;
+          float out[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const float gv = act_bwd(act, bf2f((unsigned short)yy[u][j]), bf2f((unsigned short)gg[u][j]));
-            s[j] += gv;
-            out[j] = (short)f2bf(gv);
+            out[j] = act_bwd(act, yy[u][j], gg[u][j]);
+            s[j] += out[j];
           }
-          if (dpre) *reinterpret_cast<bf16x8_t*>(dpre + rr * N + c0) = out;
+          if (dpre) st8<T>(dpre + rr * N + c0, out);
         }
       } else {
         for (int u = 0; u < 4; ++u) {
@@ -124,9 +123,9 @@ __global__ void __launch_bounds__(256) fm_act_bwd_colsum(const unsigned short* _
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             if (c0 + j < N) {
-              const float gv = act_bwd(act, bf2f(y[o + j]), bf2f(dy[o + j]));
+              const float gv = act_bwd(act, ld<T>(y + o + j), ld<T>(dy + o + j));
               s[j] += gv;
-              if (dpre) dpre[o + j] = f2bf(gv);
+              if (dpre) st<T>(dpre + o + j, gv);
             }
           }
         }
@@ -324,7 +323,8 @@ extern "C" void fm_binary_backward(int code, const void* a, const void* b, const
                           (const float*)dy, (float*)da, (float*)db, n, acca, accb);
 }
 
-extern "C" void fm_act_bwd_bias(const void* y, const void* dy, void* dpre, float* db, long B, int N, int act, hipStream_t s) {
+extern "C" void fm_act_bwd_bias(const void* y, const void* dy, void* dpre, float* db, long B, int N, int act, int bf16,
+                                hipStream_t s) {
   if (B <= 0 || N <= 0) return;
   int tpr = 1;
   while (tpr < 64 && tpr * 8 < N) tpr *= 2;                 // threads per row (power of two)
@@ -335,8 +335,12 @@ extern "C" void fm_act_bwd_bias(const void* y, const void* dy, void* dpre, float
   long ROWS = (B + nrb - 1) / nrb;
   ROWS = (ROWS + 4L * rpb - 1) / (4L * rpb) * (4L * rpb);
   dim3 grid((unsigned)strips, (unsigned)((B + ROWS - 1) / ROWS));
-  hipLaunchKernelGGL(fm_act_bwd_colsum, grid, dim3(256), 0, s, (const unsigned short*)y, (const unsigned short*)dy,
-                     (unsigned short*)dpre, db, B, N, act, tpr, (int)ROWS);
+  if (bf16)
+    hipLaunchKernelGGL((fm_act_bwd_colsum<unsigned short>), grid, dim3(256), 0, s, (const unsigned short*)y,
+                       (const unsigned short*)dy, (unsigned short*)dpre, db, B, N, act, tpr, (int)ROWS);
+  else
+    hipLaunchKernelGGL((fm_act_bwd_colsum<float>), grid, dim3(256), 0, s, (const float*)y, (const float*)dy, (float*)dpre,
+                       db, B, N, act, tpr, (int)ROWS);
 }
 
 extern "C" void fm_multi_copy2d(int n, const void* const* src, void* const* dst, const long* rows, const long* cols,

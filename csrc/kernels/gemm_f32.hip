@@ -1,0 +1,559 @@
+// flexmi fp32 MFMA GEMM for gfx950 (MI355X / CDNA4) -- the reference-precision path.
+//
+//   C[M,N] (+)= epilogue( alpha * sum_k A(m,k) * B(k,n) )      fp32 in, fp32 accumulate, fp32 out
+//
+// The reference is fp32 end to end (cublasSgemm, src/ops/linear.cu:432-441 fwd, :616-634 dW/dX,
+// src/ops/batch_matmul.cu:199-201).  CDNA4 has an exact f32-input MFMA
+// (v_mfma_f32_16x16x4_f32: one k-ordered fmaf chain per output, 64 FLOP/clk/SIMD = 157 TF/s chip
+// peak) and no xf32, so this kernel runs the fp32 products on the matrix cores and leaves the
+// VALU for the fused epilogue.
+//
+// Tile BM x BN x 32 (fp32), 256 threads = 4 waves (2x2); a wave owns (BM/2) x (BN/2) as MR x NR
+// 16x16 MFMA tiles.  The K index inside a 16-wide k-chunk is permuted per lane group
+// (g = lane>>4 takes k = 4g + s at MFMA step s) so that ONE 16-B LDS read feeds several MFMAs:
+//   * K-contiguous operand (A [M][K] / B [N][K]): LDS image [row][32 floats] (128-B rows, 16-B
+//     chunks XOR-swizzled by (row>>1)&7 -> conflict-free ds_read_b128); one b128 read = the 4
+//     k-steps of one 16x16 tile.
+//   * MN-contiguous operand (A [K][M] / B [K][N]): LDS image [k][R floats]; the wave's rows are
+//     INTERLEAVED over its tiles (tile t, lane row q -> row base + T*q + t) so one b128 read at a
+//     fixed k gives the fragments of all T tiles.  No transposed copies, no scalar LDS reads.
+// The epilogue undoes the interleave: each lane owns groups of 4 consecutive output columns
+// (16-B stores).  Fused epilogue like the bf16 kernel (gemm_common.h): alpha, bias[n],
+// activation, activation-backward of the layer below (y fp32) + its bias-gradient column sums,
+// beta accumulate; dW GEMMs fold the bias gradient in as row sums of the staged A tiles.
+// Split-K writes fp32 slabs reduced by one vectorised reduce launch.  XCD-aware tile order.
+#include "common.h"
+
+#include <algorithm>
+#include <cstdlib>
+
+namespace {
+
+constexpr int NTF = 256;   // threads per block
+constexpr int BKF = 32;    // k per LDS tile (fp32)
+
+struct GemmF {
+  const float* A; long lda; long sA;
+  const float* B; long ldb; long sB;
+  float* C; long ldc; long sC;
+  const float* bias;
+  float* ws;            // split-K slabs [batch][split][M][N]
+  const float* ay;      // fused act-bwd of the layer below: v = act'(ay) * v
+  long lday;
+  float* colsum;        // += column sums of the (post act-bwd) output
+  float* rowsum_a;      // += sum_k A(m,k)  (MN-contiguous A only)
+  int bact;
+  int M, N, K, act, beta, ksplit, batch;
+  float alpha;
+  int tiles_m, tiles_n, n_fast;
+};
+
+template <int N>
+using fvec = float __attribute__((ext_vector_type(N)));
+
+FM_DEVICE int xcd_remap_f(int bid, int ntiles) {
+  int q = ntiles / 8, r = ntiles % 8, x = bid % 8;
+  if (ntiles >= 8) bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+  return bid;
+}
+
+// byte offset of 16-B chunk c (4 floats) of row r in a K-contiguous image (128-B rows)
+FM_DEVICE int kc_off(int r, int c) { return r * (BKF * 4) + 16 * (c ^ ((r >> 1) & 7)); }
+
+// ---- global -> registers -> LDS (one operand tile) ----------------------------------------
+template <bool KC, int R, bool VEC>
+struct StageF {
+  static constexpr int CHUNKS = R * BKF / 4;
+  static constexpr int PER_T = CHUNKS / NTF;
+  static_assert(PER_T >= 1 && CHUNKS % NTF == 0, "tile too small for the block");
+  f32x4_t v[PER_T];
+
+  FM_DEVICE void load(const float* __restrict__ p, long ld, int row0, int rows, int k0, int K, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int ci = tid + NTF * i;
+      int gr, gk;
+      if constexpr (KC) {
+        gr = row0 + (ci >> 3);
+        gk = k0 + 4 * (ci & 7);
+      } else {
+        gk = k0 + ci / (R / 4);
+        gr = row0 + 4 * (ci % (R / 4));
+      }
+      if constexpr (VEC) {
+        if (gr < rows && gk < K) {
+          const float* src = KC ? (p + (long)gr * ld + gk) : (p + (long)gk * ld + gr);
+          v[i] = *reinterpret_cast<const f32x4_t*>(src);
+        } else {
+          v[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int rr = KC ? gr : gr + j;
+          const int kk = KC ? gk + j : gk;
+          v[i][j] = (rr < rows && kk < K) ? (KC ? p[(long)rr * ld + kk] : p[(long)kk * ld + rr]) : 0.f;
+        }
+      }
+    }
+  }
+
+  FM_DEVICE void store(char* lds, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int ci = tid + NTF * i;
+      int off;
+      if constexpr (KC) off = kc_off(ci >> 3, ci & 7);
+      else off = (ci / (R / 4)) * (R * 4) + 16 * (ci % (R / 4));
+      *reinterpret_cast<f32x4_t*>(lds + off) = v[i];
+    }
+  }
+
+  // MN-contiguous operand: every chunk of this thread covers the same 4 rows (tid % (R/4)),
+  // so per-thread sums over the staged k are row partial sums (bias grad inside the dW GEMM)
+  FM_DEVICE void accumulate_rows(float (&s)[4]) const {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s[j] += v[i][j];
+  }
+};
+
+// fragments of one operand for one 16-wide k-chunk: f[t][s] = element (tile t, k-step s)
+template <bool KC, int R, int T>
+FM_DEVICE void load_frags(const char* lds, int base, int kk, int lane, float (&f)[T][4]) {
+  const int q = lane & 15, g = lane >> 4;
+  if constexpr (KC) {
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const f32x4_t x = *reinterpret_cast<const f32x4_t*>(lds + kc_off(base + 16 * t + q, 4 * kk + g));
+#pragma unroll
+      for (int s = 0; s < 4; ++s) f[t][s] = x[s];
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int k = 16 * kk + 4 * g + s;
+      const fvec<T> x = *reinterpret_cast<const fvec<T>*>(lds + k * (R * 4) + 4 * (base + T * q));
+#pragma unroll
+      for (int t = 0; t < T; ++t) f[t][s] = x[t];
+    }
+  }
+}
+
+// ---- epilogue ---------------------------------------------------------------------------------
+// lane (q = lane&15, g = lane>>4) holds acc[i][j][r] = C[m(i, q)][n(j, 4g + r)] with
+//   m = IL_A ? mbase + MR*q + i : mbase + 16i + q          (IL = MN-contiguous operand)
+//   n = IL_B ? nbase + NR*qn + j : nbase + 16j + qn        (qn = 4g + r)
+// processed as NR quads of 4 consecutive columns per row.
+template <int MR, int NR, bool IL_A, bool IL_B>
+FM_DEVICE void quad_of(const f32x4_t (&acc)[MR][NR], int i, int u, int nbase, int g, int& n0, float (&v)[4]) {
+  if constexpr (IL_B) {
+    n0 = nbase + 4 * NR * g + 4 * u;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = acc[i][(4 * u + e) % NR][(4 * u + e) / NR];
+  } else {
+    n0 = nbase + 16 * u + 4 * g;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = acc[i][u][e];
+  }
+}
+
+template <int MR, int NR, bool IL_A, bool IL_B>
+FM_DEVICE void epilogue_f32(const GemmF& p, const f32x4_t (&acc)[MR][NR], int zb, int split, int mbase, int nbase,
+                            int lane) {
+  const int q = lane & 15, g = lane >> 4;
+  if (p.ksplit > 1) {
+    float* ws = p.ws + ((long)zb * p.ksplit + split) * (long)p.M * p.N;
+    const bool v4 = (p.N & 3) == 0;
+#pragma unroll
+    for (int i = 0; i < MR; ++i) {
+      const int m = IL_A ? mbase + MR * q + i : mbase + 16 * i + q;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int u = 0; u < NR; ++u) {
+        int n0;
+        float v[4];
+        quad_of<MR, NR, IL_A, IL_B>(acc, i, u, nbase, g, n0, v);
+        float* dst = ws + (long)m * p.N + n0;
+        if (v4 && n0 + 3 < p.N) {
+          *reinterpret_cast<f32x4_t*>(dst) = f32x4_t{v[0], v[1], v[2], v[3]};
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (n0 + e < p.N) dst[e] = v[e];
+        }
+      }
+    }
+    return;
+  }
+  float csum[NR][4];
+#pragma unroll
+  for (int u = 0; u < NR; ++u)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) csum[u][e] = 0.f;
+  float* Cz = p.C + (long)zb * p.sC;
+#pragma unroll
+  for (int i = 0; i < MR; ++i) {
+    const int m = IL_A ? mbase + MR * q + i : mbase + 16 * i + q;
+    const bool mok = m < p.M;
+#pragma unroll
+    for (int u = 0; u < NR; ++u) {
+      int n0;
+      float v[4];
+      quad_of<MR, NR, IL_A, IL_B>(acc, i, u, nbase, g, n0, v);
+      const bool full = n0 + 3 < p.N;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] *= p.alpha;
+        if (p.bias) v[e] += (n0 + e < p.N) ? p.bias[n0 + e] : 0.f;
+        v[e] = act_fwd(p.act, v[e]);
+      }
+      if (p.ay) {
+        float yv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (mok) {
+          const float* yp = p.ay + (long)m * p.lday + n0;
+          if (full && ((p.lday & 3) == 0)) {
+            const f32x4_t t = *reinterpret_cast<const f32x4_t*>(yp);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) yv[e] = t[e];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) yv[e] = (n0 + e < p.N) ? yp[e] : 0.f;
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = act_bwd(p.bact, yv[e], v[e]);
+      }
+      if (p.colsum && mok) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) csum[u][e] += (n0 + e < p.N) ? v[e] : 0.f;
+      }
+      if (!mok) continue;
+      float* dst = Cz + (long)m * p.ldc + n0;
+      if (full && ((p.ldc & 3) == 0) && ((((uintptr_t)dst) & 15) == 0)) {
+        f32x4_t o = {v[0], v[1], v[2], v[3]};
+        if (p.beta) o += *reinterpret_cast<const f32x4_t*>(dst);
+        *reinterpret_cast<f32x4_t*>(dst) = o;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (n0 + e < p.N) dst[e] = v[e] + (p.beta ? dst[e] : 0.f);
+      }
+    }
+  }
+  if (p.colsum) {   // the 16 lanes of a group share every column: reduce over q, one atomic per column
+#pragma unroll
+    for (int u = 0; u < NR; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x = csum[u][e];
+        x += __shfl_xor(x, 1, 64);
+        x += __shfl_xor(x, 2, 64);
+        x += __shfl_xor(x, 4, 64);
+        x += __shfl_xor(x, 8, 64);
+        const int n = (IL_B ? nbase + 4 * NR * g + 4 * u : nbase + 16 * u + 4 * g) + e;
+        if (q == 0 && n < p.N) atomicAdd(p.colsum + n, x);
+      }
+  }
+}
+
+template <int BM, int BN, bool AK, bool BKC, bool VEC>
+__global__ void __launch_bounds__(NTF, 2) fm_gemm_f32_kernel(GemmF p) {
+  constexpr int A_BYTES = BM * BKF * 4;
+  constexpr int B_BYTES = BN * BKF * 4;
+  constexpr int MR = BM / 32;
+  constexpr int NR = BN / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int bid = xcd_remap_f(blockIdx.x, p.tiles_m * p.tiles_n);
+  int tm, tn;
+  if (p.n_fast) { tn = bid % p.tiles_n; tm = bid / p.tiles_n; }
+  else { tm = bid % p.tiles_m; tn = bid / p.tiles_m; }
+  const int zb = blockIdx.y;
+  const int split = blockIdx.z;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const float* A = p.A + (long)zb * p.sA;
+  const float* B = p.B + (long)zb * p.sB;
+
+  const int ktiles_total = (p.K + BKF - 1) / BKF;
+  const int kt_per = (ktiles_total + p.ksplit - 1) / p.ksplit;
+  const int kt0 = split * kt_per;
+  const int kt1 = min(ktiles_total, kt0 + kt_per);
+
+  f32x4_t acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  StageF<AK, BM, VEC> sa;
+  StageF<BKC, BN, VEC> sb;
+  const bool rowsum = (!AK) && (p.rowsum_a != nullptr) && (tn == 0);
+  float rs[4] = {0.f, 0.f, 0.f, 0.f};
+#define LDSF_A(b) (smem + (b) * (A_BYTES + B_BYTES))
+#define LDSF_B(b) (smem + (b) * (A_BYTES + B_BYTES) + A_BYTES)
+  if (kt0 < kt1) {
+    sa.load(A, p.lda, m0, p.M, kt0 * BKF, p.K, tid);
+    sb.load(B, p.ldb, n0, p.N, kt0 * BKF, p.K, tid);
+    sa.store(LDSF_A(0), tid);
+    sb.store(LDSF_B(0), tid);
+    if (rowsum) sa.accumulate_rows(rs);
+  }
+  __syncthreads();
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int cur = (kt - kt0) & 1;
+    const bool more = kt + 1 < kt1;
+    if (more) {
+      sa.load(A, p.lda, m0, p.M, (kt + 1) * BKF, p.K, tid);
+      sb.load(B, p.ldb, n0, p.N, (kt + 1) * BKF, p.K, tid);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BKF / 16; ++kk) {
+      float af[MR][4], bfr[NR][4];
+      load_frags<AK, BM, MR>(LDSF_A(cur), wm * (BM / 2), kk, lane, af);
+      load_frags<BKC, BN, NR>(LDSF_B(cur), wn * (BN / 2), kk, lane, bfr);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+#pragma unroll
+          for (int j = 0; j < NR; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(bfr[j][s], af[i][s], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      sa.store(LDSF_A(cur ^ 1), tid);
+      sb.store(LDSF_B(cur ^ 1), tid);
+      if (rowsum) sa.accumulate_rows(rs);
+    }
+    __syncthreads();
+  }
+#undef LDSF_A
+#undef LDSF_B
+  if constexpr (!AK) {
+    if (rowsum) {   // threads with equal tid % (BM/4) share 4 rows: reduce in LDS, one atomic per row
+      float* red = reinterpret_cast<float*>(smem);
+      constexpr int G = BM / 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[(tid / G) * BM + (tid % G) * 4 + j] = rs[j];
+      __syncthreads();
+      if (tid < BM) {
+        float x = 0.f;
+        for (int t = 0; t < NTF / G; ++t) x += red[t * BM + tid];
+        if (m0 + tid < p.M) atomicAdd(p.rowsum_a + m0 + tid, x);
+      }
+      __syncthreads();
+    }
+  }
+  epilogue_f32<MR, NR, !AK, !BKC>(p, acc, zb, split, m0 + wm * (BM / 2), n0 + wn * (BN / 2), lane);
+}
+
+// split-K reduce: 4 consecutive outputs per thread when N % 4 == 0 (16-B slab loads)
+__global__ void fm_gemm_f32_reduce(GemmF p, int v4) {
+  const long MN = (long)p.M * p.N;
+  const int E = v4 ? 4 : 1;
+  const long total = MN * p.batch / E;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long e0 = i * E;
+    const long zb = e0 / MN, e = e0 % MN;
+    const int m = (int)(e / p.N), n = (int)(e % p.N);
+    const float* src = p.ws + zb * p.ksplit * MN + e;
+    float* d = p.C + zb * p.sC + (long)m * p.ldc + n;
+    if (v4) {
+      f32x4_t s = *reinterpret_cast<const f32x4_t*>(src);
+      for (int k = 1; k < p.ksplit; ++k) s += *reinterpret_cast<const f32x4_t*>(src + k * MN);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s[r] = act_fwd(p.act, s[r] * p.alpha + (p.bias ? p.bias[n + r] : 0.f));
+      if (p.beta) s += *reinterpret_cast<const f32x4_t*>(d);
+      *reinterpret_cast<f32x4_t*>(d) = s;
+    } else {
+      float s = 0.f;
+      for (int k = 0; k < p.ksplit; ++k) s += src[k * MN];
+      s = act_fwd(p.act, s * p.alpha + (p.bias ? p.bias[n] : 0.f));
+      *d = s + (p.beta ? *d : 0.f);
+    }
+  }
+}
+
+template <int BM, int BN, bool AK, bool BKC, bool VEC>
+void launch_f(const GemmF& p, hipStream_t s) {
+  constexpr int LDS = 2 * (BM + BN) * BKF * 4;
+  dim3 grid(p.tiles_m * p.tiles_n, p.batch, p.ksplit);
+  hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC>), grid, dim3(NTF), LDS, s, p);
+}
+
+template <int BM, int BN>
+void launch_fbm(const GemmF& p, bool ak, bool bk, bool vec, hipStream_t s) {
+  if (vec) {
+    if (ak && bk) launch_f<BM, BN, true, true, true>(p, s);
+    else if (ak) launch_f<BM, BN, true, false, true>(p, s);
+    else if (bk) launch_f<BM, BN, false, true, true>(p, s);
+    else launch_f<BM, BN, false, false, true>(p, s);
+  } else {
+    if (ak && bk) launch_f<BM, BN, true, true, false>(p, s);
+    else if (ak) launch_f<BM, BN, true, false, false>(p, s);
+    else if (bk) launch_f<BM, BN, false, true, false>(p, s);
+    else launch_f<BM, BN, false, false, false>(p, s);
+  }
+}
+
+}  // namespace
+
+// Same contract as fm_gemm (gemm.hip) with fp32 operands and output:
+//   A_kcontig: A stored [M][K] (lda >= K) else [K][M] (lda >= M)
+//   B_kcontig: B stored [N][K] (ldb >= K) else [K][N] (ldb >= N)
+extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, const float* B, long ldb, long sB,
+                           int b_kcontig, float* C, long ldc, long sC, const float* bias, int M, int N, int K, int batch,
+                           float alpha, int beta, int act, float* ws, long ws_bytes, int ksplit_req, const float* act_y,
+                           long lday, int bwd_act, float* colsum, float* rowsum_a, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || batch <= 0) return 0;
+  GemmF p;
+  p.A = A; p.lda = lda; p.sA = sA;
+  p.B = B; p.ldb = ldb; p.sB = sB;
+  p.C = C; p.ldc = ldc; p.sC = sC;
+  p.bias = bias; p.ws = ws; p.ay = act_y; p.lday = lday; p.colsum = colsum; p.rowsum_a = rowsum_a;
+  p.bact = bwd_act; p.M = M; p.N = N; p.K = K; p.act = act; p.beta = beta; p.batch = batch; p.alpha = alpha;
+  p.n_fast = M >= N;
+  auto al = [](const void* q) { return (((uintptr_t)q) & 15) == 0; };
+  bool vec = al(A) && al(B) && (lda % 4 == 0) && (ldb % 4 == 0) && (sA % 4 == 0) && (sB % 4 == 0);
+  vec = vec && (a_kcontig ? (K % 4 == 0) : (M % 4 == 0)) && (b_kcontig ? (K % 4 == 0) : (N % 4 == 0));
+  // tiles: 128x128 when that gives >= 2 blocks per CU; narrower N / smaller tiles for small grids
+  int BMv = 128, BNv = 128;
+  const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;
+  if (t128 < 512 && N <= 64 * 8) BNv = 64;
+  if (t128 < 128 && K <= 2048) { BMv = 64; BNv = 64; }
+  p.tiles_m = (M + BMv - 1) / BMv;
+  p.tiles_n = (N + BNv - 1) / BNv;
+  const long tiles = (long)p.tiles_m * p.tiles_n * batch;
+  const int ktiles = (K + BKF - 1) / BKF;
+  int ks = 1;
+  if (ksplit_req > 0) ks = ksplit_req;
+  else if (ws != nullptr) {
+    static const long env_target = getenv("FM_GEMM_F32_SPLIT_BLOCKS") ? std::max(1L, atol(getenv("FM_GEMM_F32_SPLIT_BLOCKS"))) : 0L;
+    const long target = env_target > 0 ? env_target : 512L;   // 2 resident blocks per CU
+    while (tiles * ks < target && ks * 2 <= ktiles / 4 && ks < 16) ks *= 2;
+  }
+  if (act_y != nullptr || colsum != nullptr) ks = 1;   // fused bwd epilogue needs the full K sum
+  if (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks = 1;
+  if (K <= 0) ks = 1;
+  p.ksplit = ks;
+  if (BNv == 128) launch_fbm<128, 128>(p, a_kcontig, b_kcontig, vec, stream);
+  else if (BMv == 128) launch_fbm<128, 64>(p, a_kcontig, b_kcontig, vec, stream);
+  else launch_fbm<64, 64>(p, a_kcontig, b_kcontig, vec, stream);
+  if (ks > 1) {
+    const int v4 = (N % 4 == 0) && (ldc % 4 == 0) && (sC % 4 == 0) && al(C);
+    const long total = (long)M * N * batch / (v4 ? 4 : 1);
+    hipLaunchKernelGGL(fm_gemm_f32_reduce, dim3(fm_grid(total)), dim3(256), 0, stream, p, v4);
+  }
+  return ks;
+}
+
+// ------------------------------------------------------------------------------------------
+// fp32 skinny layers (out_features == 1): GEMV forward, fused act-bwd / dX / dW / db backward.
+namespace {
+
+__global__ void __launch_bounds__(256) fm_skinny_fwd_f32(const float* __restrict__ x, long ldx, const float* __restrict__ w,
+                                                        const float* __restrict__ bias, float* __restrict__ y, long ldy,
+                                                        long B, int K, int act) {
+  const int lane = threadIdx.x & 63;
+  const long waves = (long)gridDim.x * 4;
+  const bool vec = (K % 4 == 0) && (ldx % 4 == 0);
+  for (long b = blockIdx.x * 4 + (threadIdx.x >> 6); b < B; b += waves) {
+    const float* xr = x + b * ldx;
+    float s = 0.f;
+    if (vec) {
+      for (int k = lane * 4; k < K; k += 256) {
+        const f32x4_t a = *reinterpret_cast<const f32x4_t*>(xr + k);
+        const f32x4_t c = *reinterpret_cast<const f32x4_t*>(w + k);
+        s += a[0] * c[0] + a[1] * c[1] + a[2] * c[2] + a[3] * c[3];
+      }
+    } else {
+      for (int k = lane; k < K; k += 64) s += xr[k] * w[k];
+    }
+    s = wave_reduce_sum(s);
+    if (lane == 0) y[b * ldy] = act_fwd(act, s + (bias ? bias[0] : 0.f));
+  }
+}
+
+// thread = 4 consecutive columns of rows sub, sub+rpi, ...; per-block dW/db partials reduced in
+// LDS, one atomic per column per block
+__global__ void __launch_bounds__(256) fm_skinny_bwd_f32(int ROWS, const float* __restrict__ x, long ldx,
+                                                        const float* __restrict__ w, const float* __restrict__ y, long ldy,
+                                                        const float* __restrict__ dy, long lddy, float* __restrict__ dx,
+                                                        long lddx, int dx_acc, float* __restrict__ dw,
+                                                        float* __restrict__ db, long B, int K, int act) {
+  __shared__ float red[256 * 4];
+  __shared__ float redb[256];
+  const int lpr = K / 4;                 // host: K % 4 == 0, K <= 1024
+  const int rpi = 256 / lpr;
+  const int sub = threadIdx.x / lpr, g = threadIdx.x - sub * lpr;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  float dbs = 0.f;
+  const long r0 = (long)blockIdx.x * ROWS;
+  const int c0 = g * 4;
+  const f32x4_t wv = *reinterpret_cast<const f32x4_t*>(w + c0);
+  if (sub < rpi) {
+    const long rend = min(B, r0 + ROWS);
+    for (long r = r0 + sub; r < rend; r += 4L * rpi) {
+      float yv[4], gv[4];
+      f32x4_t xv[4], old[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long rr = min(r + u * rpi, rend - 1);
+        yv[u] = y[rr * ldy];
+        gv[u] = dy[rr * lddy];
+        xv[u] = *reinterpret_cast<const f32x4_t*>(x + rr * ldx + c0);
+        old[u] = (dx && dx_acc) ? *reinterpret_cast<const f32x4_t*>(dx + rr * lddx + c0) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long rr = r + u * rpi;
+        if (rr >= rend) break;
+        const float d = act_bwd(act, yv[u], gv[u]);
+        dbs += d;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] += d * xv[u][j];
+        if (dx) *reinterpret_cast<f32x4_t*>(dx + rr * lddx + c0) = d * wv + old[u];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) red[threadIdx.x * 4 + j] = (sub < rpi) ? acc[j] : 0.f;
+  redb[threadIdx.x] = (sub < rpi && g == 0) ? dbs : 0.f;
+  __syncthreads();
+  for (int c = threadIdx.x; c < K; c += 256) {
+    const int gg = c / 4, j = c % 4;
+    float t = 0.f;
+    for (int q = 0; q < rpi; ++q) t += red[(q * lpr + gg) * 4 + j];
+    atomicAdd(dw + c, t);
+  }
+  if (db && threadIdx.x == 0) {
+    float t = 0.f;
+    for (int q = 0; q < rpi; ++q) t += redb[q * lpr];
+    atomicAdd(db, t);
+  }
+}
+
+}  // namespace
+
+extern "C" void fm_skinny_fwd_f32_launch(const float* x, long ldx, const float* w, const float* bias, float* y, long ldy,
+                                         long B, int K, int act, hipStream_t s) {
+  if (B <= 0) return;
+  hipLaunchKernelGGL(fm_skinny_fwd_f32, dim3((unsigned)std::min<long>((B + 3) / 4, 4096)), dim3(256), 0, s, x, ldx, w,
+                     bias, y, ldy, B, K, act);
+}
+
+// dW (fp32 [K]) and db (fp32 [1]) ACCUMULATE; requires K % 4 == 0, K <= 1024, 16-B aligned rows
+extern "C" void fm_skinny_bwd_f32_launch(const float* x, long ldx, const float* w, const float* y, long ldy,
+                                         const float* dy, long lddy, float* dx, long lddx, int dx_acc, float* dw, float* db,
+                                         long B, int K, int act, hipStream_t s) {
+  if (B <= 0) return;
+  int ROWS = 64;
+  while (ROWS > 2 && (B + ROWS - 1) / ROWS < 128) ROWS /= 2;
+  hipLaunchKernelGGL(fm_skinny_bwd_f32, dim3((unsigned)((B + ROWS - 1) / ROWS)), dim3(256), 0, s, ROWS, x, ldx, w, y, ldy,
+                     dy, lddy, dx, lddx, dx_acc, dw, db, B, K, act);
+}

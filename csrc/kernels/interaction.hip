@@ -332,6 +332,164 @@ __global__ void __launch_bounds__(256) fm_dot_bwd_t(PtrTab Z, long ldz, const un
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// fp32 (reference-precision) interaction on the exact f32-input MFMA v_mfma_f32_32x32x2_f32.
+// Forward: lane (r = lane&31, h = lane>>5) holds row r of Z restricted to the k-half h (the Gram
+// matrix sums over k in any order, so half h takes k in [h*D/2, (h+1)*D/2) and MFMA step s uses
+// k = h*D/2 + s); the same register is the A and B operand.  Backward: dZ = S Z with the A operand
+// S[r][2ks + h] gathered from the staged dOut row through per-lane positions (computed once) and
+// B = Z[2ks + h][32nt + r] from the fp32 Z rows staged in LDS.  DT = D (16/32/64/128) or 0 for a
+// runtime D (scalar loads, any even D).
+struct PtrTabF {
+  const float* p[MAXF];
+};
+struct MPtrTabF {
+  float* p[MAXF];
+};
+
+template <int DT>
+__global__ void __launch_bounds__(256) fm_dot_fwd_f32(PtrTabF Z, long ldz, float* __restrict__ out, long ldo, long B,
+                                                     int F, int Drt, int W, int self) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int D = DT > 0 ? DT : Drt;
+  const int half = D / 2;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* row = reinterpret_cast<float*>(smem) + wave * W;
+  const int waves_total = gridDim.x * (blockDim.x >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int npairs = self ? F * (F + 1) / 2 : F * (F - 1) / 2;
+  const bool zok = r < F;
+  const float* zbase = (zok ? Z.p[r] : Z.p[0]) + h * half;
+  constexpr int NV = DT > 0 ? DT / 8 : 1;    // float4 per lane (k-half of DT floats)
+  for (long b = blockIdx.x * (blockDim.x >> 6) + wave; b < B; b += waves_total) {
+    f32x16_t acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    if constexpr (DT > 0) {
+      f32x4_t z[NV];
+#pragma unroll
+      for (int v = 0; v < NV; ++v) z[v] = *reinterpret_cast<const f32x4_t*>(zbase + b * ldz + 4 * v);
+      if (!zok) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) z[v] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(z[v][e], z[v][e], acc, 0, 0, 0);
+      if (r == 0) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) *reinterpret_cast<f32x4_t*>(row + h * half + 4 * v) = z[v];
+      }
+    } else {
+      for (int k = 0; k < half; ++k) {
+        const float a = zok ? zbase[b * ldz + k] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, a, acc, 0, 0, 0);
+        if (r == 0) row[h * half + k] = a;
+      }
+    }
+    for (int c = D + npairs + lane; c < W; c += 64) row[c] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i = (q & 3) + 8 * (q >> 2) + 4 * h;
+      if (i < F && (self ? r <= i : r < i)) row[D + pair_pos(i, r, self)] = acc[q];
+    }
+    FM_WAVE_LDS_SYNC();
+    float* o = out + b * ldo;
+    if ((W & 3) == 0 && (ldo & 3) == 0) {
+      for (int c = lane * 4; c < W; c += 256) *reinterpret_cast<f32x4_t*>(o + c) = *reinterpret_cast<const f32x4_t*>(row + c);
+    } else {
+      for (int c = lane; c < W; c += 64) o[c] = row[c];
+    }
+    FM_WAVE_LDS_SYNC();
+  }
+}
+
+template <int DT>
+__global__ void __launch_bounds__(256) fm_dot_bwd_f32(PtrTabF Z, long ldz, const float* __restrict__ dout, long ldo,
+                                                     MPtrTabF dZ, long lddz, unsigned acc_mask, long B, int F, int Drt,
+                                                     int W, int self) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int D = DT > 0 ? DT : Drt;
+  const int Dp = (D + 31) & ~31;                 // staged Z rows padded to whole 32-column tiles
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wpad = (W + 3) & ~3;
+  float* zs = reinterpret_cast<float*>(smem) + (long)wave * (32 * Dp + wpad);   // [32][Dp]
+  float* ds = zs + 32 * Dp;                                                     // dOut row [W]
+  const int waves_total = gridDim.x * (blockDim.x >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  // A operand positions: lane holds S[r][j = 2ks + h] (ks = 0..15) = dOut pair (r, j) (+ diag x2)
+  short apos[16];
+  unsigned dmask = 0;
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) {
+    const int j = 2 * ks + h;
+    int pos = -1;
+    if (r < F && j < F) {
+      if (r > j) pos = pair_pos(r, j, self);
+      else if (j > r) pos = pair_pos(j, r, self);
+      else if (self) {
+        pos = pair_pos(r, r, self);
+        dmask |= 1u << ks;
+      }
+    }
+    apos[ks] = (short)pos;
+  }
+  const bool vec = DT > 0;
+  for (long b = blockIdx.x * (blockDim.x >> 6) + wave; b < B; b += waves_total) {
+    // stage Z (rows >= F and columns >= D zero) and the dOut row
+    if (vec) {
+      const int cpr = Dp / 4;
+      for (int c = lane; c < 32 * cpr; c += 64) {
+        const int i = c / cpr, k = (c % cpr) * 4;
+        f32x4_t v = {0.f, 0.f, 0.f, 0.f};
+        if (i < F && k < D) v = *reinterpret_cast<const f32x4_t*>(Z.p[i] + b * ldz + k);
+        *reinterpret_cast<f32x4_t*>(zs + i * Dp + k) = v;
+      }
+      for (int c = lane * 4; c < W; c += 256) *reinterpret_cast<f32x4_t*>(ds + c) = *reinterpret_cast<const f32x4_t*>(dout + b * ldo + c);
+    } else {
+      for (int e = lane; e < 32 * Dp; e += 64) {
+        const int i = e / Dp, k = e % Dp;
+        zs[e] = (i < F && k < D) ? Z.p[i][b * ldz + k] : 0.f;
+      }
+      for (int c = lane; c < W; c += 64) ds[c] = dout[b * ldo + c];
+    }
+    FM_WAVE_LDS_SYNC();
+    const float* dp = ds + D;
+    float a[16];
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      const int pos = apos[ks];
+      float v = dp[pos < 0 ? 0 : pos];
+      v = pos < 0 ? 0.f : v;
+      if ((dmask >> ks) & 1u) v *= 2.f;
+      a[ks] = v;
+    }
+    for (int nt = 0; nt < Dp / 32; ++nt) {
+      f32x16_t acc;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) acc[t] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[ks], zs[(2 * ks + h) * Dp + 32 * nt + r], acc, 0, 0, 0);
+      const int n = 32 * nt + r;
+      if (n < D) {
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          const int i = (t & 3) + 8 * (t >> 2) + 4 * h;
+          if (i >= F || dZ.p[i] == nullptr) continue;
+          float v = acc[t];
+          if (i == 0) v += ds[n];
+          float* d = dZ.p[i] + b * lddz + n;
+          if ((acc_mask >> i) & 1u) v += *d;
+          *d = v;
+        }
+      }
+    }
+    FM_WAVE_LDS_SYNC();
+  }
+}
+
 FM_HOST_DEVICE bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // persistent-grid size of the interaction kernels (4 waves per block; each wave loops over
@@ -345,6 +503,44 @@ long dot_block_cap() {
 }
 
 }  // namespace
+
+extern "C" void fm_dot_interaction_fwd_f32(const float* const* z, int F, long ldz, float* out, long ldo, long B, int D,
+                                           int W, int self, hipStream_t s) {
+  PtrTabF t;
+  for (int i = 0; i < MAXF; ++i) t.p[i] = i < F ? z[i] : nullptr;
+  const int waves = 4;
+  const long blocks = std::min<long>((B + waves - 1) / waves, dot_block_cap());
+  bool fast = (D == 16 || D == 32 || D == 64 || D == 128) && ldz % 4 == 0;
+  for (int i = 0; i < F; ++i) fast = fast && al16(z[i]);
+  const size_t lds = (size_t)waves * W * 4;
+  auto k = !fast ? fm_dot_fwd_f32<0> : D == 128 ? fm_dot_fwd_f32<128> : D == 64 ? fm_dot_fwd_f32<64>
+                                     : D == 32 ? fm_dot_fwd_f32<32> : fm_dot_fwd_f32<16>;
+  hipLaunchKernelGGL(k, dim3((int)blocks), dim3(64 * waves), lds, s, t, ldz, out, ldo, B, F, D, W, self);
+}
+
+extern "C" void fm_dot_interaction_bwd_f32(const float* const* z, int F, long ldz, const float* dout, long ldo,
+                                           float* const* dz, long lddz, unsigned acc_mask, long B, int D, int self,
+                                           hipStream_t s) {
+  PtrTabF t;
+  MPtrTabF g;
+  for (int i = 0; i < MAXF; ++i) {
+    t.p[i] = i < F ? z[i] : nullptr;
+    g.p[i] = i < F ? dz[i] : nullptr;
+  }
+  const int waves = 4;
+  const long blocks = std::min<long>((B + waves - 1) / waves, dot_block_cap());
+  const int npairs = self ? F * (F + 1) / 2 : F * (F - 1) / 2;
+  const int W = D + npairs;                        // dOut columns read
+  const int Dp = (D + 31) & ~31;
+  bool fast = (D == 16 || D == 32 || D == 64 || D == 128) && ldz % 4 == 0 && ldo % 4 == 0 && al16(dout);
+  for (int i = 0; i < F; ++i) fast = fast && al16(z[i]);
+  const int Wr = fast ? ((W + 3) & ~3) : W;        // the vector path stages whole 16-B chunks
+  const size_t lds = (size_t)waves * (32 * Dp + ((Wr + 3) & ~3)) * 4;
+  auto k = !fast ? fm_dot_bwd_f32<0> : D == 128 ? fm_dot_bwd_f32<128> : D == 64 ? fm_dot_bwd_f32<64>
+                                     : D == 32 ? fm_dot_bwd_f32<32> : fm_dot_bwd_f32<16>;
+  hipLaunchKernelGGL(k, dim3((int)blocks), dim3(64 * waves), lds, s, t, ldz, dout, ldo, g, lddz, acc_mask, B, F, D, Wr,
+                     self);
+}
 
 extern "C" void fm_dot_interaction_fwd(const void* const* z, int F, long ldz, void* out, long ldo, long B, int D, int W,
                                        int self, hipStream_t s) {

@@ -8,7 +8,7 @@
 
 namespace {
 
-__global__ void fm_sgd_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ V,
+__global__ void fm_sgd_kernel(float* __restrict__ W, float* __restrict__ G, float* __restrict__ V,
                               unsigned short* __restrict__ Wc, const float* __restrict__ lr_p, long n, float wd,
                               float mom, int nesterov, int vec, int zero_g) {
   // zero_g: the gradient is consumed here -- write it back as 0 so the next step's backward
@@ -17,8 +17,8 @@ __global__ void fm_sgd_kernel(float* __restrict__ W, const float* __restrict__ G
   const long n4 = vec ? n / 4 : 0;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     f32x4_t w = reinterpret_cast<f32x4_t*>(W)[i];
-    f32x4_t g = reinterpret_cast<const f32x4_t*>(G)[i] + wd * w;
-    if (zero_g) reinterpret_cast<f32x4_t*>(const_cast<float*>(G))[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    f32x4_t g = reinterpret_cast<f32x4_t*>(G)[i] + wd * w;
+    if (zero_g) reinterpret_cast<f32x4_t*>(G)[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     if (mom > 0.f) {
       f32x4_t v = reinterpret_cast<f32x4_t*>(V)[i] * mom + g;
       reinterpret_cast<f32x4_t*>(V)[i] = v;
@@ -35,7 +35,7 @@ __global__ void fm_sgd_kernel(float* __restrict__ W, const float* __restrict__ G
   // tail
   for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     float g = G[i] + wd * W[i];
-    if (zero_g) const_cast<float*>(G)[i] = 0.f;
+    if (zero_g) G[i] = 0.f;
     if (mom > 0.f) {
       float v = V[i] * mom + g;
       V[i] = v;
@@ -46,7 +46,7 @@ __global__ void fm_sgd_kernel(float* __restrict__ W, const float* __restrict__ G
   }
 }
 
-__global__ void fm_adam_kernel(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ M,
+__global__ void fm_adam_kernel(float* __restrict__ W, float* __restrict__ G, float* __restrict__ M,
                                float* __restrict__ V, unsigned short* __restrict__ Wc, long n,
                                const float* __restrict__ alpha_t_p, float b1, float b2, float wd, float eps,
                                int zero_g) {
@@ -54,7 +54,7 @@ __global__ void fm_adam_kernel(float* __restrict__ W, const float* __restrict__ 
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     float w = W[i];
     float g = G[i] + wd * w;
-    if (zero_g) const_cast<float*>(G)[i] = 0.f;
+    if (zero_g) G[i] = 0.f;
     float m = b1 * M[i] + (1.f - b1) * g;
     float v = b2 * V[i] + (1.f - b2) * g * g;
     M[i] = m;
@@ -71,7 +71,7 @@ __global__ void fm_cast_bf16_kernel(const float* __restrict__ src, unsigned shor
 
 }  // namespace
 
-extern "C" void fm_sgd_update(float* W, const float* G, float* V, unsigned short* Wc, const float* lr, long n, float wd,
+extern "C" void fm_sgd_update(float* W, float* G, float* V, unsigned short* Wc, const float* lr, long n, float wd,
                               float mom, int nesterov, int zero_g, hipStream_t s) {
   if (n <= 0) return;
   bool al = ((((uintptr_t)W) | ((uintptr_t)G) | ((uintptr_t)(V ? V : W))) & 15) == 0 && ((((uintptr_t)(Wc ? Wc : (unsigned short*)W)) & 7) == 0);
@@ -79,7 +79,7 @@ extern "C" void fm_sgd_update(float* W, const float* G, float* V, unsigned short
                      nesterov, al ? 1 : 0, zero_g);
 }
 
-extern "C" void fm_adam_update(float* W, const float* G, float* M, float* V, unsigned short* Wc, long n,
+extern "C" void fm_adam_update(float* W, float* G, float* M, float* V, unsigned short* Wc, long n,
                                const float* alpha_t, float b1, float b2, float wd, float eps, int zero_g,
                                hipStream_t s) {
   if (n <= 0) return;

@@ -121,8 +121,8 @@ def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=F
         dpre = ws["dpre"]
     else:
         dpre = ws.get("dpre")
-        if dpre is None or dpre.shape != (M, N):
-            dpre = torch.empty((M, N), dtype=torch.bfloat16, device=x2.device)
+        if dpre is None or dpre.shape != (M, N) or dpre.dtype != dy2.dtype:
+            dpre = torch.empty((M, N), dtype=dy2.dtype, device=x2.device)
             ws["dpre"] = dpre
         C().act_bwd_bias(y2, dy2, dpre, None, M, N, act)
     # dW[N,K] = dpre^T x (both operands MN-contiguous: transposing LDS reads); the bias gradient
@@ -257,14 +257,18 @@ def concat_forward(inputs, y, axis):
     C().multi_copy(src, so, dst, do, rows, cols, lds, ldd, 0)
 
 
-def concat_backward(dy, in_grads, accs, axis):
+def concat_backward(dy, in_grads, accs, axis, in_shapes=None):
+    """in_shapes: shapes of the concatenated inputs -- an input without a gradient (e.g. a model
+    input) still occupies its slice of dy, so later slices start after it."""
     outer, tot = _outer_inner(dy.shape, axis)
     src, so, dst, do, rows, cols, lds, ldd = [], [], [], [], [], [], [], []
     mask = 0
     off = 0
     k = 0
-    for g, a in zip(in_grads, accs):
+    for i, (g, a) in enumerate(zip(in_grads, accs)):
         if g is None:
+            assert in_shapes is not None, "concat_backward: input shapes needed to skip a gradient-less input"
+            off += _outer_inner(in_shapes[i], axis)[1]
             continue
         _, inner = _outer_inner(g.shape, axis)
         src.append(dy); so.append(off); dst.append(g); do.append(0)
@@ -275,10 +279,6 @@ def concat_backward(dy, in_grads, accs, axis):
         off += inner
     if src:
         C().multi_copy(src, so, dst, do, rows, cols, lds, ldd, mask)
-
-
-def _concat_offsets(grads, axis):
-    return grads
 
 
 def split_forward(x, outs, axis):
@@ -374,7 +374,7 @@ def _conv_geom(x, w, y):
 def _conv_weight_matrix(w, Kout, CRS, ldc):
     if ldc == CRS:
         return w.reshape(Kout, CRS)
-    wp = scratch(w.device, "conv_wpad", Kout * ldc)
+    wp = scratch(w.device, "conv_wpad", Kout * ldc, w.dtype)
     C().pad_rows(w.contiguous(), wp, Kout, CRS, ldc)
     return wp
 
@@ -385,10 +385,10 @@ def conv2d_forward(x, w, b, y, stride, pads, act, groups):
     assert groups == 1, "grouped convolution is not supported on the HIP path"
     N, Cin, H, W, Kout, Cg, R, S, P, Q, CRS, ldc = _conv_geom(x, w, y)
     NPQ = N * P * Q
-    col = scratch(x.device, "conv_col", NPQ * ldc)
+    col = scratch(x.device, "conv_col", NPQ * ldc, x.dtype)
     C().im2col(x, col, R, S, P, Q, stride[0], stride[1], pads[0], pads[2], ldc)
     wm = _conv_weight_matrix(w, Kout, CRS, ldc)
-    out = scratch(x.device, "conv_nhwc", NPQ * Kout)
+    out = scratch(x.device, "conv_nhwc", NPQ * Kout, x.dtype)
     gemm(col, ldc, True, wm, ldc, True, out, Kout, NPQ, Kout, ldc, bias=b, act=act)
     C().transpose_batched(out, None, y, N, P * Q, Kout, 10, 0)
 
@@ -399,9 +399,9 @@ def conv2d_backward(x, w, y, dy, dx, dw, db, stride, pads, act, groups, acc):
     assert groups == 1, "grouped convolution is not supported on the HIP path"
     N, Cin, H, W, Kout, Cg, R, S, P, Q, CRS, ldc = _conv_geom(x, w, y)
     NPQ = N * P * Q
-    g = scratch(x.device, "conv_g", NPQ * Kout)
+    g = scratch(x.device, "conv_g", NPQ * Kout, x.dtype)
     C().transpose_batched(dy, y, g, N, Kout, P * Q, act, 1)
-    col = scratch(x.device, "conv_col", NPQ * ldc)
+    col = scratch(x.device, "conv_col", NPQ * ldc, x.dtype)
     C().im2col(x, col, R, S, P, Q, stride[0], stride[1], pads[0], pads[2], ldc)
     # dW / db ACCUMULATE into the per-step zeroed gradient buffer (tied weights sum their grads)
     if ldc == CRS:
@@ -412,7 +412,7 @@ def conv2d_backward(x, w, y, dy, dx, dw, db, stride, pads, act, groups, acc):
         C().compact_rows(dwp, dw.view(-1), Kout, CRS, ldc, True)
     if dx is not None:
         wm = _conv_weight_matrix(w, Kout, CRS, ldc)
-        dcol = scratch(x.device, "conv_dcol", NPQ * ldc)
+        dcol = scratch(x.device, "conv_dcol", NPQ * ldc, x.dtype)
         gemm(g, Kout, True, wm, ldc, False, dcol, ldc, NPQ, ldc, Kout)
         C().col2im(dcol, dx, R, S, P, Q, stride[0], stride[1], pads[0], pads[2], ldc, bool(acc))
 

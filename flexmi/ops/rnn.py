@@ -119,9 +119,10 @@ class LSTM(Op):
             T, H = self.T, self.H
             s["G"] = torch.empty(B * T * 4 * H, dtype=torch.float32, device=dev)
             s["C"] = torch.empty(B * T * H, dtype=torch.float32, device=dev)
-            s["Hp"] = torch.empty(B * T * H, dtype=torch.bfloat16, device=dev)
+            adt = ctx.inputs[0].dtype          # activation dtype (bf16, or fp32 in reference-precision mode)
+            s["Hp"] = torch.empty(B * T * H, dtype=adt, device=dev)
             s["cinit"] = torch.empty(B * H, dtype=torch.float32, device=dev)
-            s["dG"] = torch.empty(B * T * 4 * H, dtype=torch.bfloat16, device=dev)
+            s["dG"] = torch.empty(B * T * 4 * H, dtype=adt, device=dev)
             s["dh"] = torch.empty(B * H, dtype=torch.float32, device=dev)
             s["dc"] = torch.empty(B * H, dtype=torch.float32, device=dev)
         return s

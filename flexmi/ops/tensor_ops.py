@@ -60,7 +60,8 @@ class Concat(Op):
     def backward(self, ctx: OpCtx):
         dy = ctx.out_grads[0]
         if ctx.hip:
-            K.concat_backward(dy, list(ctx.in_grads), list(ctx.in_grad_accumulate), self.axis)
+            K.concat_backward(dy, list(ctx.in_grads), list(ctx.in_grad_accumulate), self.axis,
+                              [tuple(x.shape) for x in ctx.inputs])
             return
         off = 0
         for i, x in enumerate(ctx.inputs):

@@ -162,15 +162,31 @@ def run_reshards(comm, items):
 OVERLAP_EMB = os.environ.get("FM_OVERLAP_EMB", "auto")
 
 
+def overlap_embeddings_enabled(ex):
+    """Whether captured steps of executor ``ex`` run the fused embedding groups on a second HIP
+    stream (``OVERLAP_EMB``: "1" / "0" / "auto" = on when an embedding table is >= 128 wide)."""
+    if OVERLAP_EMB == "1":
+        return True
+    if OVERLAP_EMB != "auto":
+        return False
+    return any(st[0] == "op" and type(st[1]).__name__ == "Embedding" and st[1].out_dim >= 128 for st in ex.fwd_steps)
+
+
 def _run_overlapped(items, s, side):
     """Issue one graph segment's items with the embedding groups on ``side`` (fork/join by events,
-    which stream capture records as graph edges)."""
+    which stream capture records as graph edges).  A group forward is hoisted only across plain
+    op forwards that declare what they write (``Item.writes``) and write none of the group's
+    inputs (``Item.reads``): never across reshards, exchange unpacks or another group."""
     fwd = [k for k, it in enumerate(items) if it.name.endswith(".group_fwd")]
     hoist, fork_at = set(), {}
     for k in fwd:
         j = k
-        while j > 0 and items[j - 1].name.endswith(".fwd") and not items[j - 1].name.endswith(".group_fwd"):
-            j -= 1          # hoist across plain op forwards only (never across reshards/unpacks)
+        reads = items[k].reads
+        while j > 0 and reads is not None:
+            prev = items[j - 1]
+            if prev.writes is None or prev.name.endswith(".group_fwd") or (prev.writes & reads):
+                break
+            j -= 1
         if j < k:
             hoist.add(k)
             fork_at.setdefault(j, []).append(k)
@@ -200,11 +216,15 @@ def _run_overlapped(items, s, side):
 
 
 class Item:
-    __slots__ = ("kind", "fn", "name", "check", "native", "zero_group")
+    __slots__ = ("kind", "fn", "name", "check", "native", "zero_group", "reads", "writes")
 
     def __init__(self, kind, fn, name, check=None, native=None):
         self.kind, self.fn, self.name = kind, fn, name
         self.zero_group = None  # the per-step gradient memset of this weight group
+        # tensor guids this item reads / writes (op forwards and embedding-group forwards);
+        # None = unknown -- the second-stream scheduler never reorders across it
+        self.reads = None
+        self.writes = None
         self.check = check      # debug mode: callable(item) run after fn (NaN/Inf guard)
         self.native = native    # comm items: structured form for the native runner (flexmi._rt)
 
@@ -841,7 +861,7 @@ class Executor:
         epilogue applies L1's activation backward and accumulates L1's bias gradient, so L1 skips
         its separate act-bwd/bias-grad pass (one full read+write of the activation gradient)."""
         from flexmi.core.types import ActiMode, OperatorType
-        if self.backend != "hip" or self.cdtype != torch.bfloat16:
+        if self.backend != "hip":
             return
         for op in ops:
             if op.op_type != OperatorType.OP_LINEAR or getattr(op, "skip_act_grad", False):
@@ -867,6 +887,19 @@ class Executor:
         from flexmi.core.types import OperatorType
         self.group_of = {}
         groups = []
+        pos = {st[1].guid: k for k, st in enumerate(self.fwd_steps) if st[0] == "op"}
+
+        def ready_at(op, lead):
+            # a member runs at the leader's forward position: every input must already hold its
+            # values there -- needed in its home layout (no reshard emitted later) and either a
+            # model input or produced by an op scheduled before the leader
+            for i, t in enumerate(op.inputs):
+                if not self.need[(op.guid, i)].same_as(self.home[t.guid]):
+                    return False
+                if t.owner_op is not None and pos.get(t.owner_op.guid, 1 << 30) >= pos[lead.guid]:
+                    return False
+            return True
+
         for op in ops:
             c = self.ctx.get(op.guid)
             if c is None or op.op_type != OperatorType.OP_EMBEDDING or getattr(op, "host_exec", False):
@@ -874,7 +907,8 @@ class Executor:
             pc = self.pcs[op.guid]
             for g in groups:
                 lead = g[0]
-                if (self.pcs[lead.guid] == pc and type(lead).can_group(lead, op, self.ctx[lead.guid], c)):
+                if (self.pcs[lead.guid] == pc and ready_at(op, lead)
+                        and type(lead).can_group(lead, op, self.ctx[lead.guid], c)):
                     g.append(op)
                     break
             else:
@@ -1226,9 +1260,13 @@ class Executor:
             if grp[0] is op:
                 fwd.append(Item("compute", (lambda grp=grp: type(grp[0]).forward_group(grp, [self.ctx[o.guid] for o in grp])),
                                 op.name + ".group_fwd"))
+                fwd[-1].reads = {t.guid for o in grp for t in o.inputs}
+                fwd[-1].writes = {t.guid for o in grp for t in o.outputs}
             return
         kind = "comm" if getattr(op, "host_exec", False) else "compute"   # host ops are never captured
         fwd.append(Item(kind, (lambda op=op, c=c: self._fwd_op(op, c)), op.name + ".fwd"))
+        fwd[-1].reads = {t.guid for t in op.inputs}
+        fwd[-1].writes = {t.guid for t in op.outputs}
         fwd[-1].check = (lambda op=op, c=c: self._check_op(op.name + ".fwd", c.outputs, "output"))
 
     def _compile_backward(self, bwd, C):
@@ -1422,6 +1460,19 @@ class Executor:
         if compute_grad and self.loss_reshard is not None:
             self._emit_reshards(lst, [(self.loss_back, self.logit_grad, self.grad.get(self.final.guid), False)],
                                 "loss.scatter")
+
+    def release(self):
+        """Drop this executor's native-runner references (callables, tensors, process groups held
+        from C++ -- invisible to Python's cycle collector) and its captured graphs, so the model's
+        device memory is freed once the Python objects go away (bench.py builds a second model)."""
+        nr = self._native if self._native not in (None, False) else None
+        if nr is not None:
+            nr.rt.release()
+            nr.keep.clear()
+        self._native = None
+        self._graph = None
+        self._graphs = []
+        self._graph_segments = []
 
     def native_runner(self):
         """The native step runner when it can execute this executor's programs: ``flexmi._rt``
@@ -1754,8 +1805,7 @@ class Executor:
             segments.append(("graph", cur))
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        ov = OVERLAP_EMB == "1" or (OVERLAP_EMB == "auto" and any(
-            st[0] == "op" and type(st[1]).__name__ == "Embedding" and st[1].out_dim >= 128 for st in self.fwd_steps))
+        ov = overlap_embeddings_enabled(self)
         side = torch.cuda.Stream() if ov else None
         runs = []
         graphs = []

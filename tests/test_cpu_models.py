@@ -197,13 +197,13 @@ def test_set_get_weights_and_inline_map():
 
 
 # ---------------------------------------------------------------------------- model zoo
-def _zoo_model(name, device="cpu", B=4, **kw):
+def _zoo_model(name, device="cpu", B=4, dtype=None, **kw):
     from flexmi.core import FFConfig, FFModel, SGDOptimizer
     from flexmi.models import zoo
     cfg = FFConfig()
     cfg.batchSize = B
     cfg.device = device
-    cfg.compute_dtype = "bf16" if device == "gpu" else "fp32"
+    cfg.compute_dtype = dtype or ("bf16" if device == "gpu" else "fp32")
     cfg.seed = 11
     m = FFModel(cfg)
     built = zoo.build(name, m, small=True, **kw)
@@ -291,11 +291,11 @@ def test_cifar10_cnn_matches_torch():
 
 
 # ---------------------------------------------------------------------------- LSTM / NMT
-def _lstm_model(device, B=4, T=5, I=8, H=16, state=False):
+def _lstm_model(device, B=4, T=5, I=8, H=16, state=False, dtype=None):
     from flexmi.core import FFConfig, FFModel, SGDOptimizer, LossType, MetricsType
     cfg = FFConfig()
     cfg.batchSize, cfg.device = B, device
-    cfg.compute_dtype = "bf16" if device == "gpu" else "fp32"
+    cfg.compute_dtype = dtype or ("bf16" if device == "gpu" else "fp32")
     m = FFModel(cfg)
     x = m.create_tensor([B, T, I], name="x")
     h0 = c0 = None

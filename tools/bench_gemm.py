@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """GEMM microbenchmark on the DLRM (MLPerf-like, batch 8192) shapes: flexmi MFMA kernel vs
-hipBLASLt (torch.matmul) on identical random bf16 operands.  Interleaved rounds in one process
-(cdna_hip_programming.md rule 24); prints TFLOP/s per shape and orientation."""
+hipBLASLt (torch.matmul) on identical random operands (bf16, or fp32 with --fp32: the flexmi
+f32-input MFMA kernel vs the library's fp32 GEMM).  Interleaved rounds in one process
+(cdna_hip_programming.md rule 24); prints TFLOP/s per shape and orientation.
+usage: bench_gemm.py [--fp32] ["M,K,N;M,K,N"]"""
 import json
 import sys
 import time
@@ -42,9 +44,12 @@ def main():
     rows = []
     global B
     layers = LAYERS
-    if len(sys.argv) > 1:   # custom shapes "M,K,N;M,K,N"
+    args = [a for a in sys.argv[1:] if a != "--fp32"]
+    dt = torch.float32 if "--fp32" in sys.argv else torch.bfloat16
+    torch.backends.cuda.matmul.allow_tf32 = False
+    if args:   # custom shapes "M,K,N;M,K,N"
         layers = []
-        for t in sys.argv[1].split(";"):
+        for t in args[0].split(";"):
             m_, k_, n_ = (int(v) for v in t.split(","))
             layers.append((m_, k_, n_))
     for spec in layers:
@@ -52,17 +57,17 @@ def main():
             B, k, n = spec
         else:
             k, n = spec
-        x = torch.randn(B, k, device=dev).bfloat16()
-        w = torch.randn(n, k, device=dev).bfloat16()
-        dy = torch.randn(B, n, device=dev).bfloat16()
+        x = torch.randn(B, k, device=dev).to(dt)
+        w = torch.randn(n, k, device=dev).to(dt)
+        dy = torch.randn(B, n, device=dev).to(dt)
         bias = torch.randn(n, device=dev)
-        y = torch.empty(B, n, device=dev, dtype=torch.bfloat16)
-        dx = torch.empty(B, k, device=dev, dtype=torch.bfloat16)
+        y = torch.empty(B, n, device=dev, dtype=dt)
+        dx = torch.empty(B, k, device=dev, dtype=dt)
         dw = torch.empty(n, k, device=dev)
         cases = {
             "fwd": (2.0 * B * k * n,
                     lambda: K.gemm(x, k, True, w, k, True, y, n, B, n, k, bias=bias, act=11),
-                    lambda: torch.relu(torch.addmm(bias.bfloat16(), x, w.t()))),
+                    lambda: torch.relu(torch.addmm(bias.to(dt), x, w.t()))),
             "dX": (2.0 * B * k * n,
                    lambda: K.gemm(dy, n, True, w, k, False, dx, k, B, k, n),
                    lambda: torch.mm(dy, w)),
@@ -73,7 +78,7 @@ def main():
         for name, (fl, mine, ref) in cases.items():
             tm = min(timeit(mine) for _ in range(3))
             tr = min(timeit(ref) for _ in range(3))
-            rows.append({"shape": f"{B}x{k}->{n}", "op": name, "flexmi_us": round(tm * 1e6, 2),
+            rows.append({"dtype": str(dt).replace("torch.", ""), "shape": f"{B}x{k}->{n}", "op": name, "flexmi_us": round(tm * 1e6, 2),
                          "hipblaslt_us": round(tr * 1e6, 2), "flexmi_TF": round(fl / tm / 1e12, 1),
                          "hipblaslt_TF": round(fl / tr / 1e12, 1)})
             print(json.dumps(rows[-1]), flush=True)
