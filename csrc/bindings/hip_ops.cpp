@@ -52,7 +52,7 @@ void fm_adam_update(float* W, float* G, float* M, float* V, unsigned short* Wc, 
                     float b1, float b2, float wd, float eps, int zero_g, hipStream_t s);
 void fm_cast_bf16(const float* src, unsigned short* dst, long n, hipStream_t s);
 void fm_loss_fwd_bwd(const void* logits, int logits_bf16, const void* labels, void* grad, int grad_bf16, long B, int C,
-                     int loss_type, float scale, float* acc, int mask, hipStream_t s);
+                     int loss_type, float scale, float* acc, int mask, float clamp_t, hipStream_t s);
 void fm_unary_forward(int code, const void* x, void* y, long n, int bf16, hipStream_t s);
 void fm_unary_backward(int code, const void* x, const void* y, const void* dy, void* dx, long n, int acc, int bf16,
                        hipStream_t s);
@@ -386,12 +386,12 @@ void adam(torch::Tensor W, torch::Tensor G, torch::Tensor M, torch::Tensor V, c1
 void cast_bf16(torch::Tensor src, torch::Tensor dst) { fm_cast_bf16(src.data_ptr<float>(), (unsigned short*)dst.data_ptr(), src.numel(), cur()); }
 
 void loss(int64_t loss_type, torch::Tensor logits, torch::Tensor labels, c10::optional<torch::Tensor> grad, double scale,
-          torch::Tensor acc, int64_t mask) {
+          torch::Tensor acc, int64_t mask, double clamp_t) {
   long B = logits.size(0);
   int C = (int)(logits.numel() / std::max<long>(1, B));
   int gb = (grad.has_value() && grad->defined()) ? is_bf16(*grad) : 0;
   fm_loss_fwd_bwd(logits.data_ptr(), is_bf16(logits), labels.data_ptr(), mptr(grad), gb, B, C, (int)loss_type, (float)scale,
-                  acc.data_ptr<float>(), (int)mask, cur());
+                  acc.data_ptr<float>(), (int)mask, (float)clamp_t, cur());
 }
 
 void unary_fwd(int64_t code, torch::Tensor x, torch::Tensor y) { fm_unary_forward((int)code, x.data_ptr(), y.data_ptr(), x.numel(), is_bf16(x), cur()); }
@@ -595,7 +595,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("sgd", &sgd);
   m.def("adam", &adam);
   m.def("cast_bf16", &cast_bf16);
-  m.def("loss", &loss);
+  m.def("loss", &loss, py::arg("loss_type"), py::arg("logits"), py::arg("labels"), py::arg("grad"), py::arg("scale"),
+        py::arg("acc"), py::arg("mask"), py::arg("clamp_t") = 0.0);
   m.def("unary_fwd", &unary_fwd);
   m.def("unary_bwd", &unary_bwd);
   m.def("binary_fwd", &binary_fwd);

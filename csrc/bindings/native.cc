@@ -4,6 +4,7 @@
 
 #include <optional>
 
+#include "hdf5_lite.h"
 #include "loader.h"
 #include "shard.h"
 #include "strategy_pb.h"
@@ -93,15 +94,28 @@ PYBIND11_MODULE(_native, m) {
     return flexmi::split_launches(dst, b, max_per_launch);
   });
 
+  // minimal HDF5 reader (csrc/runtime/hdf5_lite.h): datasets with their dtype, shape and the byte
+  // offset of their contiguous data (memory-mapped by flexmi.utils.hdf5)
+  m.def("h5_datasets", [](const std::string& path) {
+    std::vector<flexmi::H5Dataset> ds;
+    std::string err;
+    if (!flexmi::h5_list_datasets(path, ds, err)) throw std::runtime_error("h5_datasets: " + err);
+    std::vector<std::tuple<std::string, std::string, std::vector<int64_t>, int64_t, int64_t>> out;
+    for (auto& d : ds) out.emplace_back(d.name, d.dtype, d.shape, d.offset, d.nbytes);
+    return out;
+  });
+
   // data-loader ring (csrc/runtime/loader.h); pointers are raw addresses of host buffers
   py::class_<flexmi::BatchRing>(m, "BatchRing")
       .def(py::init<int64_t, int64_t, int, int, bool, uint64_t>(), py::arg("batch"), py::arg("num_samples"),
            py::arg("depth") = 3, py::arg("threads") = 2, py::arg("shuffle") = false, py::arg("seed") = 0)
       .def("add_source",
            [](flexmi::BatchRing& r, uintptr_t base, int64_t rows, int64_t row_bytes, int64_t col_off,
-              int64_t col_bytes, int64_t row_lo, int64_t row_hi) {
-             return r.add_source((const void*)base, rows, row_bytes, col_off, col_bytes, row_lo, row_hi);
-           })
+              int64_t col_bytes, int64_t row_lo, int64_t row_hi, int64_t dst_pitch) {
+             return r.add_source((const void*)base, rows, row_bytes, col_off, col_bytes, row_lo, row_hi, dst_pitch);
+           },
+           py::arg("base"), py::arg("rows"), py::arg("row_bytes"), py::arg("col_off"), py::arg("col_bytes"),
+           py::arg("row_lo"), py::arg("row_hi"), py::arg("dst_pitch") = -1)
       .def("set_slot", [](flexmi::BatchRing& r, int src, int slot, uintptr_t p) { r.set_slot(src, slot, (void*)p); })
       .def("start", &flexmi::BatchRing::start)
       .def("stop", &flexmi::BatchRing::stop, py::call_guard<py::gil_scoped_release>())

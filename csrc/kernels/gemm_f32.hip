@@ -401,6 +401,178 @@ void launch_fbm(const GemmF& p, bool ak, bool bk, bool vec, hipStream_t s) {
   }
 }
 
+
+// ---- LDS-DMA pipelined variant ------------------------------------------------------------
+// Operands go global -> LDS with global_load_lds_dwordx4 (no staging VGPRs, no ds_write pass)
+// into a 3-stage ring, two K-tiles in flight behind the one being multiplied (the same schedule
+// as the bf16 gemm_glds.hip):
+//   iteration t: s_waitcnt vmcnt(L) (own loads of tile t landed); lgkmcnt(0); s_barrier
+//                issue tile t+2 -> stage (t+2)%3; MFMAs on stage t%3
+// The DMA destination is lane-linear (wave base + 16*lane), so the K-contiguous image's chunk
+// swizzle is applied to the per-lane SOURCE address; MN-contiguous images are unswizzled rows.
+// Used when K-tiles are whole (K % 32 == 0) and operands allow 16-B access.
+typedef __attribute__((address_space(1))) const void* gptr_f;
+typedef __attribute__((address_space(3))) void* lptr_f;
+
+template <bool KC, int R, int NTH>
+struct GldsF {
+  static constexpr int INSTR = R * BKF * 4 / 1024;
+  static constexpr int NWAVES = NTH / 64;
+  static constexpr int PER_W = INSTR / NWAVES;
+  static_assert(INSTR % NWAVES == 0, "tile bytes must split evenly over waves");
+
+  FM_DEVICE static void issue(const float* __restrict__ p, long ld, int row0, int rows, int k0, char* lds, int wave,
+                              int lane) {
+#pragma unroll
+    for (int i = 0; i < PER_W; ++i) {
+      const int j = wave + NWAVES * i;
+      const float* src;
+      if constexpr (KC) {           // image [row][32 k]: 8 rows of 128 B per instruction
+        const int row = 8 * j + (lane >> 3);
+        const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+        const int gr = min(row0 + row, rows - 1);          // rows past the edge: never stored
+        src = p + (long)gr * ld + k0 + 4 * chunk;
+      } else {                      // image [k][R rows]: 1024/(4R) k-rows per instruction
+        constexpr int CPR = R / 4;                      // 16-B chunks per k-row
+        constexpr int KPI = 1024 / (4 * R);
+        const int krow = KPI * j + lane / CPR;
+        const int gr = min(row0 + 4 * (lane % CPR), rows - 4);
+        src = p + (long)(k0 + krow) * ld + gr;
+      }
+      __builtin_amdgcn_global_load_lds((gptr_f)src, (lptr_f)(lds + j * 1024), 16, 0, 0);
+    }
+  }
+};
+
+template <int N>
+FM_DEVICE void wait_vmcnt_f() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+template <int BM, int BN, int WM, int WN, bool AK, bool BKC>
+__global__ void __launch_bounds__(WM * WN * 64, 1) fm_gemm_f32_glds_kernel(GemmF p) {
+  constexpr int NW = WM * WN;
+  constexpr int NTH = NW * 64;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int MR = TM / 16, NR = TN / 16;
+  constexpr int A_BYTES = BM * BKF * 4;
+  constexpr int B_BYTES = BN * BKF * 4;
+  constexpr int STG = A_BYTES + B_BYTES;
+  constexpr int NS = 3;
+  constexpr int LPT = GldsF<AK, BM, NTH>::PER_W + GldsF<BKC, BN, NTH>::PER_W;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int bid = xcd_remap_f(blockIdx.x, p.tiles_m * p.tiles_n);
+  int tm, tn;
+  if (p.n_fast) { tn = bid % p.tiles_n; tm = bid / p.tiles_n; }
+  else { tm = bid % p.tiles_m; tn = bid / p.tiles_m; }
+  const int zb = blockIdx.y;
+  const int split = blockIdx.z;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const float* A = p.A + (long)zb * p.sA;
+  const float* B = p.B + (long)zb * p.sB;
+
+  const int ktiles_total = p.K / BKF;
+  const int kt_per = (ktiles_total + p.ksplit - 1) / p.ksplit;
+  const int kt0 = split * kt_per;
+  const int kt1 = min(ktiles_total, kt0 + kt_per);
+  const int nkt = max(kt1 - kt0, 0);
+  const int klast = max(min(kt1, ktiles_total) - 1, 0);
+
+  auto issue = [&](int t, int stage) {
+    const int kt = min(kt0 + t, klast);     // prefetches past the end re-read the last tile
+    char* base = smem + stage * STG;
+    GldsF<AK, BM, NTH>::issue(A, p.lda, m0, p.M, kt * BKF, base, wave, lane);
+    GldsF<BKC, BN, NTH>::issue(B, p.ldb, n0, p.N, kt * BKF, base + A_BYTES, wave, lane);
+  };
+
+  f32x4_t acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const bool rowsum = (!AK) && (p.rowsum_a != nullptr) && (tn == 0);
+  constexpr int CPR = BM / 4;
+  float rs[4] = {0.f, 0.f, 0.f, 0.f};
+
+  issue(0, 0);
+  issue(1, 1);
+  for (int t = 0; t < nkt; ++t) {
+    const int stage = t % NS;
+    wait_vmcnt_f<LPT>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue(t + 2, (t + 2) % NS);
+    const char* la = smem + stage * STG;
+    const char* lb = la + A_BYTES;
+    if constexpr (!AK) {
+      if (rowsum) {
+        for (int kr = tid / CPR; kr < BKF; kr += NTH / CPR) {
+          const f32x4_t v = *reinterpret_cast<const f32x4_t*>(la + kr * (BM * 4) + 16 * (tid % CPR));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) rs[e] += v[e];
+        }
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < BKF / 16; ++kk) {
+      float af[MR][4], bfr[NR][4];
+      load_frags<AK, BM, MR>(la, wm * TM, kk, lane, af);
+      load_frags<BKC, BN, NR>(lb, wn * TN, kk, lane, bfr);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+#pragma unroll
+          for (int j = 0; j < NR; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(bfr[j][s], af[i][s], acc[i][j], 0, 0, 0);
+    }
+  }
+  wait_vmcnt_f<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if constexpr (!AK) {
+    if (rowsum) {
+      float* red = reinterpret_cast<float*>(smem);
+      constexpr int G = NTH / CPR;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[(tid / CPR) * BM + (tid % CPR) * 4 + e] = rs[e];
+      __syncthreads();
+      for (int r = tid; r < BM; r += NTH) {
+        float x = 0.f;
+        for (int g = 0; g < G; ++g) x += red[g * BM + r];
+        if (m0 + r < p.M) atomicAdd(p.rowsum_a + m0 + r, x);
+      }
+    }
+  }
+  epilogue_f32<MR, NR, !AK, !BKC>(p, acc, zb, split, m0 + wm * TM, n0 + wn * TN, lane);
+}
+
+template <int BM, int BN, int WM, int WN>
+void launch_f_glds(const GemmF& p, bool ak, bool bk, hipStream_t s) {
+  constexpr int NTH = WM * WN * 64;
+  constexpr int LDS = 3 * (BM + BN) * BKF * 4;
+  static bool attr_set = false;
+  if (!attr_set) {   // > 64 KiB dynamic LDS needs the opt-in attribute
+    auto set = [](const void* f) { (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS); };
+    set((const void*)fm_gemm_f32_glds_kernel<BM, BN, WM, WN, true, true>);
+    set((const void*)fm_gemm_f32_glds_kernel<BM, BN, WM, WN, true, false>);
+    set((const void*)fm_gemm_f32_glds_kernel<BM, BN, WM, WN, false, true>);
+    set((const void*)fm_gemm_f32_glds_kernel<BM, BN, WM, WN, false, false>);
+    attr_set = true;
+  }
+  dim3 grid(p.tiles_m * p.tiles_n, p.batch, p.ksplit);
+  if (ak && bk) hipLaunchKernelGGL((fm_gemm_f32_glds_kernel<BM, BN, WM, WN, true, true>), grid, dim3(NTH), LDS, s, p);
+  else if (ak) hipLaunchKernelGGL((fm_gemm_f32_glds_kernel<BM, BN, WM, WN, true, false>), grid, dim3(NTH), LDS, s, p);
+  else if (bk) hipLaunchKernelGGL((fm_gemm_f32_glds_kernel<BM, BN, WM, WN, false, true>), grid, dim3(NTH), LDS, s, p);
+  else hipLaunchKernelGGL((fm_gemm_f32_glds_kernel<BM, BN, WM, WN, false, false>), grid, dim3(NTH), LDS, s, p);
+}
+
 }  // namespace
 
 // Same contract as fm_gemm (gemm.hip) with fp32 operands and output:
@@ -421,6 +593,40 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
   auto al = [](const void* q) { return (((uintptr_t)q) & 15) == 0; };
   bool vec = al(A) && al(B) && (lda % 4 == 0) && (ldb % 4 == 0) && (sA % 4 == 0) && (sB % 4 == 0);
   vec = vec && (a_kcontig ? (K % 4 == 0) : (M % 4 == 0)) && (b_kcontig ? (K % 4 == 0) : (N % 4 == 0));
+  // variant knob (tools/bench_gemm.py A/B): 1 = never the LDS-DMA kernel, 2 = 4-wave 256x128
+  static const int variant = getenv("FM_GEMM_F32_VARIANT") ? atoi(getenv("FM_GEMM_F32_VARIANT")) : 0;
+  // LDS-DMA pipelined kernel: whole K-tiles, 16-B operands, a grid of >= one block per CU
+  const long t256 = (long)((M + 255) / 256) * ((N + 127) / 128) * batch;
+  const long t128g = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;
+  const bool mn_ok = (a_kcontig || M >= 4) && (b_kcontig || N >= 4);
+  if (vec && !(variant & 1) && K > 0 && K % BKF == 0 && M >= 8 && N >= 8 && mn_ok && K >= 4 * BKF) {
+    const bool big = t256 >= 192;
+    const int bm = big ? 256 : 128;
+    p.tiles_m = (M + bm - 1) / bm;
+    p.tiles_n = (N + 127) / 128;
+    const long tiles = big ? t256 : t128g;
+    const int ktiles = K / BKF;
+    int ks = 1;
+    if (ksplit_req > 0) ks = ksplit_req;
+    else if (ws != nullptr) {
+      while (tiles * ks < 256 && ks * 2 <= ktiles / 4 && ks < 16) ks *= 2;
+    }
+    if (act_y != nullptr || colsum != nullptr) ks = 1;
+    if (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks = 1;
+    p.ksplit = ks;
+    if (big) {
+      if (variant & 2) launch_f_glds<256, 128, 2, 2>(p, a_kcontig, b_kcontig, stream);
+      else launch_f_glds<256, 128, 4, 2>(p, a_kcontig, b_kcontig, stream);
+    } else {
+      launch_f_glds<128, 128, 2, 2>(p, a_kcontig, b_kcontig, stream);
+    }
+    if (ks > 1) {
+      const int v4 = (N % 4 == 0) && (ldc % 4 == 0) && (sC % 4 == 0) && al(C);
+      const long total = (long)M * N * batch / (v4 ? 4 : 1);
+      hipLaunchKernelGGL(fm_gemm_f32_reduce, dim3(fm_grid(total)), dim3(256), 0, stream, p, v4);
+    }
+    return ks;
+  }
   // tiles: 128x128 when that gives >= 2 blocks per CU; narrower N / smaller tiles for small grids
   int BMv = 128, BNv = 128;
   const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;

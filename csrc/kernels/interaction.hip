@@ -361,14 +361,25 @@ __global__ void __launch_bounds__(256) fm_dot_fwd_f32(PtrTabF Z, long ldz, float
   const bool zok = r < F;
   const float* zbase = (zok ? Z.p[r] : Z.p[0]) + h * half;
   constexpr int NV = DT > 0 ? DT / 8 : 1;    // float4 per lane (k-half of DT floats)
-  for (long b = blockIdx.x * (blockDim.x >> 6) + wave; b < B; b += waves_total) {
+  // persistent waves: the next sample's rows are loaded (clamped, unconditional) before this
+  // sample's MFMAs and output write, so every wave keeps one sample of loads in flight
+  f32x4_t zn[NV];
+  const long b_first = blockIdx.x * (blockDim.x >> 6) + wave;
+  if constexpr (DT > 0) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) zn[v] = *reinterpret_cast<const f32x4_t*>(zbase + min(b_first, B - 1) * ldz + 4 * v);
+  }
+  for (long b = b_first; b < B; b += waves_total) {
     f32x16_t acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
     if constexpr (DT > 0) {
       f32x4_t z[NV];
 #pragma unroll
-      for (int v = 0; v < NV; ++v) z[v] = *reinterpret_cast<const f32x4_t*>(zbase + b * ldz + 4 * v);
+      for (int v = 0; v < NV; ++v) z[v] = zn[v];
+      const long bn = min(b + waves_total, B - 1);
+#pragma unroll
+      for (int v = 0; v < NV; ++v) zn[v] = *reinterpret_cast<const f32x4_t*>(zbase + bn * ldz + 4 * v);
       if (!zok) {
 #pragma unroll
         for (int v = 0; v < NV; ++v) z[v] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -435,18 +446,45 @@ __global__ void __launch_bounds__(256) fm_dot_bwd_f32(PtrTabF Z, long ldz, const
     }
     apos[ks] = (short)pos;
   }
+  // DT > 0: persistent waves with the next sample's Z rows and dOut row prefetched into registers
+  // (clamped addresses, every load unconditional) while this sample is staged and multiplied
+  constexpr int DPT = DT > 0 ? ((DT + 31) & ~31) : 32;
+  constexpr int CPRP = DPT / 4;                    // float4 chunks per staged Z row
+  constexpr int ZCH = DT > 0 ? 32 * CPRP / 64 : 1;
+  constexpr int DCH = 4;                           // dOut float4 chunks per lane (W <= 1024)
+  f32x4_t zv[ZCH], dv[DCH];
+  auto load = [&](long bb) {
+    bb = min(bb, B - 1);
+#pragma unroll
+    for (int t = 0; t < ZCH; ++t) {
+      const int c = lane + 64 * t, i = c / CPRP, k = (c % CPRP) * 4;
+      const bool ok = i < F && k < D;
+      zv[t] = *reinterpret_cast<const f32x4_t*>(Z.p[ok ? i : 0] + bb * ldz + (ok ? k : 0));
+      if (!ok) zv[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int t = 0; t < DCH; ++t) {
+      const int c = 4 * (lane + 64 * t);
+      dv[t] = *reinterpret_cast<const f32x4_t*>(dout + bb * ldo + (c < W ? c : 0));
+    }
+  };
   const bool vec = DT > 0;
-  for (long b = blockIdx.x * (blockDim.x >> 6) + wave; b < B; b += waves_total) {
+  const long b_first = blockIdx.x * (blockDim.x >> 6) + wave;
+  if (vec) load(b_first);
+  for (long b = b_first; b < B; b += waves_total) {
     // stage Z (rows >= F and columns >= D zero) and the dOut row
     if (vec) {
-      const int cpr = Dp / 4;
-      for (int c = lane; c < 32 * cpr; c += 64) {
-        const int i = c / cpr, k = (c % cpr) * 4;
-        f32x4_t v = {0.f, 0.f, 0.f, 0.f};
-        if (i < F && k < D) v = *reinterpret_cast<const f32x4_t*>(Z.p[i] + b * ldz + k);
-        *reinterpret_cast<f32x4_t*>(zs + i * Dp + k) = v;
+#pragma unroll
+      for (int t = 0; t < ZCH; ++t) {
+        const int c = lane + 64 * t, i = c / CPRP, k = (c % CPRP) * 4;
+        *reinterpret_cast<f32x4_t*>(zs + i * Dp + k) = zv[t];
       }
-      for (int c = lane * 4; c < W; c += 256) *reinterpret_cast<f32x4_t*>(ds + c) = *reinterpret_cast<const f32x4_t*>(dout + b * ldo + c);
+#pragma unroll
+      for (int t = 0; t < DCH; ++t) {
+        const int c = 4 * (lane + 64 * t);
+        if (c < W) *reinterpret_cast<f32x4_t*>(ds + c) = dv[t];
+      }
+      load(b + waves_total);
     } else {
       for (int e = lane; e < 32 * Dp; e += 64) {
         const int i = e / Dp, k = e % Dp;
@@ -532,7 +570,7 @@ extern "C" void fm_dot_interaction_bwd_f32(const float* const* z, int F, long ld
   const int npairs = self ? F * (F + 1) / 2 : F * (F - 1) / 2;
   const int W = D + npairs;                        // dOut columns read
   const int Dp = (D + 31) & ~31;
-  bool fast = (D == 16 || D == 32 || D == 64 || D == 128) && ldz % 4 == 0 && ldo % 4 == 0 && al16(dout);
+  bool fast = (D == 16 || D == 32 || D == 64 || D == 128) && ldz % 4 == 0 && ldo % 4 == 0 && al16(dout) && W <= 1024;
   for (int i = 0; i < F; ++i) fast = fast && al16(z[i]);
   const int Wr = fast ? ((W + 3) & ~3) : W;        // the vector path stages whole 16-B chunks
   const size_t lds = (size_t)waves * (32 * Dp + ((Wr + 3) & ~3)) * 4;

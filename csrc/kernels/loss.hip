@@ -3,6 +3,8 @@
 // atomicAdd per sample per metric).  One pass over the logits computes dL/dlogit = scale*(p - y)
 // and accumulates all requested metrics; each block reduces in registers/LDS and issues 8 atomics.
 // Slots: 0 all, 1 correct, 2 cce, 3 sparse cce, 4 mse, 5 rmse, 6 mae, 7 loss value.
+// clamp_t in (0, 0.5): DLRM --loss-threshold -- predictions are clamped to [t, 1-t] before the
+// loss and metrics, and clamped predictions pass no gradient (reference dlrm.cc:129 left it a TODO).
 #include "common.h"
 
 namespace {
@@ -31,7 +33,7 @@ FM_DEVICE void block_accumulate(float (&v)[8], float* acc) {
 template <typename LT, typename GT>
 __global__ void __launch_bounds__(256) fm_loss_kernel(const LT* __restrict__ logits, const void* __restrict__ labels,
                                                      GT* __restrict__ grad, long B, int C, int loss_type, float scale,
-                                                     float* __restrict__ acc, int mask) {
+                                                     float* __restrict__ acc, int mask, float clamp_t) {
   float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int lane = threadIdx.x & 63;
   const long waves = (long)gridDim.x * (blockDim.x >> 6);
@@ -45,8 +47,14 @@ __global__ void __launch_bounds__(256) fm_loss_kernel(const LT* __restrict__ log
     float se = 0.f, ae = 0.f, cce = 0.f, lossv = 0.f, plab = 1.f;
     for (int c = lane; c < C; c += 64) {
       float p = ld<LT>(lp + c);
+      bool clipped = false;
+      if (clamp_t > 0.f) {
+        const float pc = fminf(fmaxf(p, clamp_t), 1.f - clamp_t);
+        clipped = pc != p;
+        p = pc;
+      }
       float y = sparse ? (c == lab ? 1.f : 0.f) : yp[c];
-      if (grad) st<GT>(grad + b * C + c, scale * (p - y));
+      if (grad) st<GT>(grad + b * C + c, clipped ? 0.f : scale * (p - y));
       float d = p - y;
       se += d * d;
       ae += fabsf(d);
@@ -99,12 +107,18 @@ __global__ void __launch_bounds__(256) fm_loss_kernel(const LT* __restrict__ log
 template <typename LT, typename GT>
 __global__ void __launch_bounds__(256) fm_loss1_kernel(const LT* __restrict__ logits, const float* __restrict__ labels,
                                                       GT* __restrict__ grad, long B, int loss_type, float scale,
-                                                      float* __restrict__ acc, int mask) {
+                                                      float* __restrict__ acc, int mask, float clamp_t) {
   float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (long b = blockIdx.x * (long)blockDim.x + threadIdx.x; b < B; b += (long)gridDim.x * blockDim.x) {
     float p = ld<LT>(logits + b);
+    bool clipped = false;
+    if (clamp_t > 0.f) {
+      const float pc = fminf(fmaxf(p, clamp_t), 1.f - clamp_t);
+      clipped = pc != p;
+      p = pc;
+    }
     float y = labels[b];
-    if (grad) st<GT>(grad + b, scale * (p - y));
+    if (grad) st<GT>(grad + b, clipped ? 0.f : scale * (p - y));
     float d = p - y;
     v[0] += 1.f;
     v[1] += ((p >= 0.5f) == (y >= 0.5f)) ? 1.f : 0.f;
@@ -126,18 +140,18 @@ __global__ void __launch_bounds__(256) fm_loss1_kernel(const LT* __restrict__ lo
 }  // namespace
 
 extern "C" void fm_loss_fwd_bwd(const void* logits, int logits_bf16, const void* labels, void* grad, int grad_bf16, long B,
-                                int C, int loss_type, float scale, float* acc, int mask, hipStream_t s) {
+                                int C, int loss_type, float scale, float* acc, int mask, float clamp_t, hipStream_t s) {
   if (B <= 0) return;
   if (C == 1 && loss_type != LOSS_SCCE) {
     dim3 g(fm_grid(B, 256, 1024));
-#define L1(LT, GT) hipLaunchKernelGGL((fm_loss1_kernel<LT, GT>), g, dim3(256), 0, s, (const LT*)logits, (const float*)labels, (GT*)grad, B, loss_type, scale, acc, mask)
+#define L1(LT, GT) hipLaunchKernelGGL((fm_loss1_kernel<LT, GT>), g, dim3(256), 0, s, (const LT*)logits, (const float*)labels, (GT*)grad, B, loss_type, scale, acc, mask, clamp_t)
     if (logits_bf16) { if (grad_bf16) L1(unsigned short, unsigned short); else L1(unsigned short, float); }
     else { if (grad_bf16) L1(float, unsigned short); else L1(float, float); }
 #undef L1
     return;
   }
   dim3 g((int)std::min<long>((B + 3) / 4, 2048));
-#define LW(LT, GT) hipLaunchKernelGGL((fm_loss_kernel<LT, GT>), g, dim3(256), 0, s, (const LT*)logits, labels, (GT*)grad, B, C, loss_type, scale, acc, mask)
+#define LW(LT, GT) hipLaunchKernelGGL((fm_loss_kernel<LT, GT>), g, dim3(256), 0, s, (const LT*)logits, labels, (GT*)grad, B, C, loss_type, scale, acc, mask, clamp_t)
   if (logits_bf16) { if (grad_bf16) LW(unsigned short, unsigned short); else LW(unsigned short, float); }
   else { if (grad_bf16) LW(float, unsigned short); else LW(float, float); }
 #undef LW

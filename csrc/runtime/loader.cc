@@ -22,11 +22,13 @@ BatchRing::BatchRing(int64_t batch, int64_t num_samples, int depth, int threads,
 BatchRing::~BatchRing() { stop(); }
 
 int BatchRing::add_source(const void* base, int64_t rows, int64_t row_bytes, int64_t col_off, int64_t col_bytes,
-                          int64_t row_lo, int64_t row_hi) {
+                          int64_t row_lo, int64_t row_hi, int64_t dst_pitch) {
   if (row_lo < 0 || row_hi > batch_ || row_lo > row_hi) throw std::invalid_argument("bad shard rows");
   if (!threads_.empty()) throw std::logic_error("add_source after start");
   if (rows < num_samples_) throw std::invalid_argument("source has fewer rows than num_samples");
   if (col_off < 0 || col_bytes < 0 || col_off + col_bytes > row_bytes) throw std::invalid_argument("bad column block");
+  if (dst_pitch < 0) dst_pitch = col_bytes;
+  if (dst_pitch < col_bytes) throw std::invalid_argument("staging pitch narrower than the column block");
   LoaderSource s;
   s.base = static_cast<const char*>(base);
   s.rows = rows;
@@ -35,6 +37,7 @@ int BatchRing::add_source(const void* base, int64_t rows, int64_t row_bytes, int
   s.col_bytes = col_bytes;
   s.row_lo = row_lo;
   s.row_hi = row_hi;
+  s.dst_pitch = dst_pitch;
   s.slot_ptr.assign(depth_, nullptr);
   src_.push_back(s);
   return (int)src_.size() - 1;
@@ -78,12 +81,12 @@ void BatchRing::fill(int slot, int64_t n) {
     const int64_t nr = s.row_hi - s.row_lo;
     if (nr == 0) continue;
     const int64_t* id = ids.data() + s.row_lo;
-    if (!shuffle_ && s.col_off == 0 && s.col_bytes == s.row_bytes) {  // one contiguous block
+    if (!shuffle_ && s.col_off == 0 && s.col_bytes == s.row_bytes && s.dst_pitch == s.col_bytes) {  // one block
       std::memcpy(dst, s.base + id[0] * s.row_bytes, (size_t)(nr * s.row_bytes));
       continue;
     }
     for (int64_t r = 0; r < nr; ++r)
-      std::memcpy(dst + r * s.col_bytes, s.base + id[r] * s.row_bytes + s.col_off, (size_t)s.col_bytes);
+      std::memcpy(dst + r * s.dst_pitch, s.base + id[r] * s.row_bytes + s.col_off, (size_t)s.col_bytes);
   }
 }
 

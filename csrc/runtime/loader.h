@@ -25,7 +25,8 @@ struct LoaderSource {
   int64_t col_off = 0;          // byte offset of this rank's column block inside a row
   int64_t col_bytes = 0;        // bytes copied per row
   int64_t row_lo = 0, row_hi = 0;  // this rank's rows of every batch
-  std::vector<char*> slot_ptr;  // staging buffer per slot: [shard_rows, col_bytes]
+  int64_t dst_pitch = 0;        // staging row pitch >= col_bytes (wider: zero-padded tensor rows)
+  std::vector<char*> slot_ptr;  // staging buffer per slot: [shard_rows, dst_pitch]
 };
 
 class BatchRing {
@@ -36,7 +37,7 @@ class BatchRing {
 
   // [row_lo, row_hi): the rows of every batch this rank holds for the source (its shard box)
   int add_source(const void* base, int64_t rows, int64_t row_bytes, int64_t col_off, int64_t col_bytes,
-                 int64_t row_lo, int64_t row_hi);
+                 int64_t row_lo, int64_t row_hi, int64_t dst_pitch = -1);
   void set_slot(int source, int slot, void* ptr);
   void start();                 // spawn workers (sources and slots must be complete)
   void stop();                  // join workers; the ring can be start()ed again (from batch 0)

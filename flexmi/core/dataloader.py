@@ -90,7 +90,10 @@ class NetConfig:
 class PrefetchLoader:
     """Multi-input prefetching loader on the native ring (``csrc/runtime/loader.{h,cc}``).
 
-    ``pairs``: [(tensor, full host array [num_samples, ...])] -- inputs and the label.  Host
+    ``pairs``: [(tensor, full host array [num_samples, ...])] or [(tensor, full 2-D array,
+    (c0, c1))] -- inputs and the label; the 3-tuple form feeds columns c0:c1 of a wider array
+    (zero-copy: e.g. one sparse feature of a memory-mapped ``X_cat``), and a source row narrower
+    than the tensor row is zero-padded (the 13 dense features into a 16-wide GPU input).  Host
     worker threads gather each batch's rows (sequential or shuffled per epoch with ``seed``)
     into ``depth`` pinned staging slots ahead of the training loop; :meth:`next_batch` takes
     the next staged slot and issues one async H2D copy per input on the current stream, so
@@ -108,18 +111,36 @@ class PrefetchLoader:
         self.ring = _native.BatchRing(B, int(num_samples), depth, threads, bool(shuffle), int(seed))
         self.items = []
         self._keep = []
-        for t, full in pairs:
+        for pair in pairs:
+            t, full = pair[0], pair[1]
+            cols = pair[2] if len(pair) > 2 else None
             buf = ex.local_buffer(t)
             if buf is None:
                 continue
             assert t.dims[0] == B, "all inputs of a PrefetchLoader share the batch dimension"
             box = ex.home[t.guid].local_box(ex.rank)
+            dims = list(t.dims)
+            tdt = buf.dtype
+            if cols is not None or (full.ndim == 2 and len(dims) == 2 and full.shape[1] < dims[1]):
+                # column block of a 2-D source (zero-copy), zero-padded up to the tensor row
+                c0, c1 = cols if cols is not None else (0, full.shape[1])
+                arr = np.asarray(full)
+                if arr.dtype != np.dtype(str(tdt).replace("torch.", "")):
+                    arr = arr.astype(str(tdt).replace("torch.", ""))
+                arr = np.ascontiguousarray(arr)
+                es = arr.itemsize
+                assert len(dims) == 2 and c1 - c0 <= dims[1] and box[1] == (0, dims[1]), \
+                    "column-block sources feed whole rows of a 2-D input"
+                self._keep.append(arr)
+                si = self.ring.add_source(arr.ctypes.data, arr.shape[0], arr.shape[1] * es, c0 * es, (c1 - c0) * es,
+                                          box[0][0], box[0][1], dims[1] * es)
+                self._add_slots(si, buf, depth, zero=(c1 - c0) < dims[1])
+                continue
             src = torch.as_tensor(np.ascontiguousarray(full)).reshape((-1,) + tuple(t.dims[1:]))
             if src.dtype != buf.dtype:
                 src = src.to(buf.dtype)
             src = src.contiguous()
             self._keep.append(src)
-            dims = list(t.dims)
             es = src.element_size()
             row_bytes = int(np.prod(dims[1:], dtype=np.int64)) * es
             split = [j for j in range(1, len(dims)) if box[j] != (0, dims[j])]
@@ -133,16 +154,19 @@ class PrefetchLoader:
                 inner = int(np.prod(dims[d + 1:], dtype=np.int64)) * es
                 col_off, col_bytes = box[d][0] * inner, (box[d][1] - box[d][0]) * inner
             si = self.ring.add_source(src.data_ptr(), src.shape[0], row_bytes, col_off, col_bytes, box[0][0], box[0][1])
-            stg = []
-            for s in range(depth):
-                st = torch.empty(tuple(buf.shape), dtype=buf.dtype, pin_memory=self.gpu)
-                self.ring.set_slot(si, s, st.data_ptr())
-                stg.append(st)
-            self.items.append((buf, stg))
+            self._add_slots(si, buf, depth)
         self.pending = []
         self.depth = depth
         self.num_samples = int(num_samples)
         self.ring.start()
+
+    def _add_slots(self, si, buf, depth, zero=False):
+        stg = []
+        for s in range(depth):
+            st = (torch.zeros if zero else torch.empty)(tuple(buf.shape), dtype=buf.dtype, pin_memory=self.gpu)
+            self.ring.set_slot(si, s, st.data_ptr())
+            stg.append(st)
+        self.items.append((buf, stg))
 
     def get_num_samples(self):
         return self.num_samples

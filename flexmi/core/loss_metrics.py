@@ -81,12 +81,19 @@ def metrics_mask(metrics):
 LOG_MIN = 1e-7
 
 
-def loss_and_metrics_torch(loss_type, logits, labels, grad, scale, acc, mask, compute_grad=True):
-    """fp32 reference implementation (CPU path and test oracle)."""
+def loss_and_metrics_torch(loss_type, logits, labels, grad, scale, acc, mask, compute_grad=True, clamp=0.0):
+    """fp32 reference implementation (CPU path and test oracle).  clamp in (0, 0.5): predictions
+    clamped to [clamp, 1-clamp] before loss and metrics, no gradient through clamped ones (DLRM
+    --loss-threshold)."""
     p = logits.float()
     B = p.shape[0]
     C = p.shape[-1] if p.dim() > 1 else 1
     p2 = p.reshape(B, -1)
+    keep = None
+    if clamp > 0.0:
+        pc = p2.clamp(clamp, 1.0 - clamp)
+        keep = (pc == p2).to(p2.dtype)
+        p2 = pc
     lt = LossType(loss_type)
     if lt == LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY:
         lab = labels.reshape(B).long()
@@ -104,6 +111,8 @@ def loss_and_metrics_torch(loss_type, logits, labels, grad, scale, acc, mask, co
             g = (p2 - y) * scale
         else:
             raise ValueError(lt)
+        if keep is not None:
+            g = g * keep
         grad.reshape(B, -1).copy_(g)
     # metrics
     acc[M_ALL] += B

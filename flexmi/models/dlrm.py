@@ -60,6 +60,16 @@ class DLRMConfig:
         if name == "criteo_kaggle":  # run_criteo_kaggle.sh
             return DLRMConfig(16, list(KAGGLE_TABLES), [13, 512, 256, 64, 16], [224, 512, 256, 1], 1, -1, -1, 0.0,
                               "cat", "", -1, "mse", "criteo_kaggle")
+        if name == "summit":      # run_summit.sh:3-13 (512 samples per GPU)
+            return DLRMConfig(64, [1000000] * 8, [64, 512, 512, 64], [576, 1024, 1024, 1024, 1], 1, -1, -1, 0.0,
+                              "cat", "", -1, "mse", "summit")
+        if name == "summit_large":  # run_summit_large.sh:3-16 (bag 100, 256 samples per GPU)
+            return DLRMConfig(64, [1000000] * 6, [2048, 4096, 4096, 4096, 4096, 4096],
+                              [10240, 4096, 4096, 4096, 4096, 1], 100, -1, -1, 0.0, "cat", "", -1, "mse", "summit_large")
+        if name == "kaggle_day1":  # run_dlrm_kaggle_day1.sh (batch 128, --dataset kaggle_day_1.h5); the script's
+            # "--arch-sparse-feature-sie 13" is a typo the reference parser ignores -> d follows the bottom MLP (16)
+            return DLRMConfig(16, list(KAGGLE_TABLES), [13, 512, 256, 64, 16], [512, 256, 1], 1, -1, -1, 0.0,
+                              "cat", "", -1, "mse", "kaggle_day1")
         if name == "tiny":
             return DLRMConfig(16, [100, 50, 200, 30], [13, 32, 16], [64, 32, 1], 1, -1, -1, 0.0, "dot", "", -1, "bce", "tiny")
         raise KeyError(name)
@@ -124,8 +134,12 @@ def create_emb(model, idx, rows, dim, i):
 
 def build_dlrm(model, c: DLRMConfig, pad_dense=True):
     """Returns (dense_input, sparse_inputs, output).  Dense input is padded to a multiple of 8
-    columns (zeros) so its GEMM uses 16-B vector loads; the padding does not change the model."""
+    columns (zeros) so its GEMM uses 16-B vector loads; the padding does not change the model.
+    ``loss_threshold`` in (0, 1) clamps predictions to [t, 1-t] in the loss (the clamp the
+    reference leaves as a TODO + assert, dlrm.cc:129-132)."""
     B = model.config.batchSize
+    if 0.0 < c.loss_threshold < 1.0:
+        model.loss_threshold = min(c.loss_threshold, 0.5)
     sparse = [model.create_tensor([B, c.embedding_bag_size], DataType.DT_INT64, name=f"sparse{i}")
               for i in range(len(c.embedding_size))]
     bot = list(c.mlp_bot)
@@ -214,3 +228,49 @@ class SyntheticDLRMData:
         k = self.i % self.nb
         ex.load_local_many([(ex.tensors[gid], pool[k]) for gid, pool in self.pools.items()])
         self.i += 1
+
+
+class HDF5DLRMData:
+    """``--dataset FILE``: the Criteo HDF5 layout written by ``preprocess_hdf.py`` (X_int float32
+    [N, 13] = log(1+x), X_cat int64 [N, tables*bag], y float32 [N]) and loaded by the reference
+    (``dlrm.cc:284-330`` shapes/classes checked, ``:425-483`` whole dataset read, ``:489-589``
+    next_batch = consecutive samples).  flexmi memory-maps the datasets (native HDF5 reader,
+    ``flexmi.utils.hdf5``) and streams batches through the native prefetch ring: each sparse
+    input is a zero-copy column block of X_cat, the 13 dense features are zero-padded into the
+    GPU's 16-wide input, every rank stages only its shard rows.  ``num_samples`` whole batches
+    per epoch (``--data-size`` caps it), consecutive like the reference or shuffled."""
+
+    def __init__(self, model, dense_in, sparse, cfg: DLRMConfig, path=None, shuffle=False, seed=0, depth=3, threads=2):
+        from flexmi.core.dataloader import PrefetchLoader
+        from flexmi.utils.hdf5 import open_h5
+        path = path or cfg.dataset_path
+        d = open_h5(path)
+        for k in ("X_int", "X_cat", "y"):
+            if k not in d:
+                raise ValueError(f"{path}: dataset {k!r} missing (have {sorted(d)})")
+        X_int, X_cat, y = d["X_int"], d["X_cat"], d["y"]
+        if X_int.ndim != 2 or X_int.dtype.kind != "f" or X_int.shape[1] != cfg.mlp_bot[0]:
+            raise ValueError(f"X_int must be float [N, {cfg.mlp_bot[0]}], got {X_int.dtype} {X_int.shape}")
+        N = X_int.shape[0]
+        bag = cfg.embedding_bag_size
+        if X_cat.ndim != 2 or X_cat.dtype.kind not in "iu" or X_cat.shape != (N, len(sparse) * bag):
+            raise ValueError(f"X_cat must be integer [N, {len(sparse) * bag}], got {X_cat.dtype} {X_cat.shape}")
+        if y.shape[0] != N:
+            raise ValueError("y must have one label per sample")
+        self.num_samples = N if cfg.data_size <= 0 else min(N, cfg.data_size)
+        B = model.config.batchSize
+        if self.num_samples < B:
+            raise ValueError(f"dataset has {self.num_samples} samples < batch {B}")
+        self.arrays = d
+        pairs = [(dense_in, X_int, (0, X_int.shape[1]))]
+        pairs += [(t, X_cat, (i * bag, (i + 1) * bag)) for i, t in enumerate(sparse)]
+        pairs.append((model.get_label_tensor(), y.reshape(N, 1), (0, 1)))
+        self.loader = PrefetchLoader(model, pairs, self.num_samples, shuffle=shuffle, seed=seed, depth=depth,
+                                     threads=threads)
+        self.nb = self.num_samples // B
+
+    def next_batch(self):
+        self.loader.next_batch()
+
+    def close(self):
+        self.loader.close()

@@ -214,8 +214,9 @@ def adam_update(master, grad, m, v, compute, alpha_t, b1, b2, wd, eps, zero_grad
     C().adam(master, grad, m, v, compute, alpha_t, b1, b2, wd, eps, zero_grad)
 
 
-def loss_forward_backward(loss_type, logits, labels, grad, scale, acc, mask):
-    C().loss(loss_type, logits, labels, grad, scale, acc, mask)
+def loss_forward_backward(loss_type, logits, labels, grad, scale, acc, mask, clamp=0.0):
+    """clamp in (0, 0.5): predictions clamped to [clamp, 1-clamp] (DLRM --loss-threshold)."""
+    C().loss(loss_type, logits, labels, grad, scale, acc, mask, float(clamp))
 
 
 # ------------------------------------------------------------------ element-wise & data movement

@@ -1652,12 +1652,13 @@ class Executor:
         from flexmi.ops import _kernels as K
         scale = 1.0 / self.final.dims[0]
         mask = self.metrics_obj.mask if self.metrics_obj else 0
+        clamp = float(getattr(self.model, "loss_threshold", 0.0) or 0.0)
         if self.backend == "hip":
             K.loss_forward_backward(int(self.loss_type), self.logits_buf, self.label_buf,
-                                    self.logit_grad if compute_grad else None, scale, self.metric_acc, mask)
+                                    self.logit_grad if compute_grad else None, scale, self.metric_acc, mask, clamp)
         else:
             loss_and_metrics_torch(self.loss_type, self.logits_buf, self.label_buf, self.logit_grad,
-                                   scale, self.metric_acc, mask, compute_grad)
+                                   scale, self.metric_acc, mask, compute_grad, clamp=clamp)
 
     def compute_metrics(self):
         if not hasattr(self, "prog_metrics"):

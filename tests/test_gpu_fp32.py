@@ -20,7 +20,8 @@ def rel_err(a, b):
 # ---------------------------------------------------------------- GEMM
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 200, 130), (1024, 512, 256), (8192, 64, 16),
-                                   (4096, 1024, 1024), (77, 33, 13), (2048, 479, 512)])
+                                   (4096, 1024, 1024), (77, 33, 13), (2048, 479, 512), (8192, 1024, 480),
+                                   (1000, 1020, 8192), (8192, 96, 256)])
 def test_gemm_f32_orientations(gpu, a_k, b_k, M, N, K):
     from flexmi.ops import _kernels as Kk
     torch.manual_seed(0)
@@ -391,3 +392,54 @@ def test_conv2d_f32(gpu, cin, cout, hw, k, s, p):
     assert rel_err(dx, xd.grad) < TOL
     assert rel_err(dw, wd.grad) < TOL
     assert rel_err(db, bd.grad) < TOL
+
+
+def test_loss_threshold_kernel_f32(gpu):
+    """HIP loss with the DLRM --loss-threshold clamp vs the fp32 torch oracle (C == 1 and C > 1)."""
+    from flexmi.core.loss_metrics import NUM_SLOTS, loss_and_metrics_torch
+    from flexmi.core.types import LossType
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(13)
+    for C_, lt in ((1, LossType.LOSS_BINARY_CROSSENTROPY), (1, LossType.LOSS_MEAN_SQUARED_ERROR_AVG_REDUCE),
+                   (5, LossType.LOSS_MEAN_SQUARED_ERROR_AVG_REDUCE)):
+        p = torch.rand(4096, C_, device=gpu)
+        y = torch.randint(0, 2, (4096, C_), device=gpu).float()
+        g, acc = torch.empty_like(p), torch.zeros(NUM_SLOTS, device=gpu)
+        Kk.loss_forward_backward(int(lt), p, y, g, 0.5, acc, 0xFF, 0.05)
+        g2, acc2 = torch.empty(4096, C_), torch.zeros(NUM_SLOTS)
+        loss_and_metrics_torch(lt, p.cpu(), y.cpu(), g2, 0.5, acc2, 0xFF, clamp=0.05)
+        assert rel_err(g.cpu(), g2) < TOL
+        assert (g.cpu()[(p.cpu() < 0.05) | (p.cpu() > 0.95)] == 0).all()
+        assert abs(acc[4].item() - acc2[4].item()) < 1e-3 * acc2[4].item()
+
+
+def test_dlrm_hdf5_dataset_fp32_gpu_matches_cpu(gpu, tmp_path):
+    """--dataset path on the GPU: the 13 dense features are zero-padded into the 16-wide input by
+    the prefetch ring, sparse inputs are column blocks of the memory-mapped X_cat."""
+    from flexmi.core import FFConfig, FFModel, LossType, MetricsType, SGDOptimizer
+    from flexmi.models.dlrm import DLRMConfig, HDF5DLRMData, build_dlrm
+    from flexmi.utils.hdf5 import write_h5
+    rng = np.random.RandomState(0)
+    tables, B, n = [500, 40, 9000, 7], 256, 256 * 4
+    write_h5(str(tmp_path / "d.h5"), {
+        "X_int": np.log(rng.randint(0, 1000, (n, 13)).astype(np.float32) + 1),
+        "X_cat": np.concatenate([rng.randint(0, r, (n, 1)) for r in tables], 1).astype(np.int64),
+        "y": rng.randint(0, 2, n).astype(np.float32)})
+    res = {}
+    for dev in ("cpu", "gpu"):
+        cfg = FFConfig()
+        cfg.batchSize, cfg.device, cfg.compute_dtype, cfg.seed = B, dev, "fp32", 5
+        m = FFModel(cfg)
+        dcfg = DLRMConfig(16, tables, [13, 64, 16], [64, 32, 1], 1, -1, -1, 0.0, "dot", "", -1, "bce", "h5")
+        d, s, p = build_dlrm(m, dcfg)
+        m.compile(SGDOptimizer(m, 0.1), LossType.LOSS_BINARY_CROSSENTROPY, [MetricsType.METRICS_ACCURACY])
+        ex = m.init_layers()
+        data = HDF5DLRMData(m, d, s, dcfg, str(tmp_path / "d.h5"))
+        for _ in range(6):
+            data.next_batch()
+            ex.train_step()
+        data.close()
+        ws = [w.get_weights(m) for w in m.parameters]
+        ws[0] = ws[0][:, :13]
+        res[dev] = ws
+    _assert_params_close(res["cpu"], res["gpu"], 1e-4)
