@@ -9,6 +9,7 @@
 
 extern "C" {
 void fm_gemm_set_variant(int v);
+void fm_gemm_f32_set_variant(int v);
 int fm_gemm(const void* A, long lda, long sA, int a_kcontig, const void* B, long ldb, long sB, int b_kcontig, void* C,
             long ldc, long sC, int c_fp32, const float* bias, int M, int N, int K, int batch, float alpha, int beta,
             int act, float* ws, long ws_bytes, int ksplit_req, const void* act_y, long lday, int bwd_act,
@@ -581,6 +582,7 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "flexmi HIP/CDNA4 kernels (gfx950)";
   m.def("gemm", &gemm);
   m.def("gemm_set_variant", [](int v) { fm_gemm_set_variant(v); });
+  m.def("gemm_f32_set_variant", [](int v) { fm_gemm_f32_set_variant(v); });
   m.def("init_fill", &init_fill);
   m.def("skinny_fwd", &skinny_fwd);
   m.def("skinny_bwd", &skinny_bwd);

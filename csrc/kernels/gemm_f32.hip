@@ -575,6 +575,9 @@ void launch_f_glds(const GemmF& p, bool ak, bool bk, hipStream_t s) {
 
 }  // namespace
 
+static int g_f32_variant = getenv("FM_GEMM_F32_VARIANT") ? atoi(getenv("FM_GEMM_F32_VARIANT")) : 0;
+extern "C" void fm_gemm_f32_set_variant(int v) { g_f32_variant = v; }
+
 // Same contract as fm_gemm (gemm.hip) with fp32 operands and output:
 //   A_kcontig: A stored [M][K] (lda >= K) else [K][M] (lda >= M)
 //   B_kcontig: B stored [N][K] (ldb >= K) else [K][N] (ldb >= N)
@@ -593,13 +596,15 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
   auto al = [](const void* q) { return (((uintptr_t)q) & 15) == 0; };
   bool vec = al(A) && al(B) && (lda % 4 == 0) && (ldb % 4 == 0) && (sA % 4 == 0) && (sB % 4 == 0);
   vec = vec && (a_kcontig ? (K % 4 == 0) : (M % 4 == 0)) && (b_kcontig ? (K % 4 == 0) : (N % 4 == 0));
-  // variant knob (tools/bench_gemm.py A/B): 1 = never the LDS-DMA kernel, 2 = 4-wave 256x128
-  static const int variant = getenv("FM_GEMM_F32_VARIANT") ? atoi(getenv("FM_GEMM_F32_VARIANT")) : 0;
-  // LDS-DMA pipelined kernel: whole K-tiles, 16-B operands, a grid of >= one block per CU
+  // variant knob (tools/bench_gemm.py A/B): 1 = the LDS-DMA kernel where it applies, 2 = its
+  // 4-wave 256x128 form.  OPT-IN: measured on the DLRM fp32 step (profiles/prof_r2_fp32b_*) it
+  // ties the register-staged kernel on the 1024-wide layers (150.8 vs 150.7 us) and loses on the
+  // small-grid ones (one 96 KiB block per CU: 22 -> 39 us, 29 -> 45 us), 1.72 vs 1.68 ms/step.
+  const int variant = g_f32_variant;
   const long t256 = (long)((M + 255) / 256) * ((N + 127) / 128) * batch;
   const long t128g = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;
   const bool mn_ok = (a_kcontig || M >= 4) && (b_kcontig || N >= 4);
-  if (vec && !(variant & 1) && K > 0 && K % BKF == 0 && M >= 8 && N >= 8 && mn_ok && K >= 4 * BKF) {
+  if (vec && (variant & 1) && K > 0 && K % BKF == 0 && M >= 8 && N >= 8 && mn_ok && K >= 4 * BKF) {
     const bool big = t256 >= 192;
     const int bm = big ? 256 : 128;
     p.tiles_m = (M + bm - 1) / bm;

@@ -18,9 +18,14 @@
 #include <c10/hip/HIPStream.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cmath>
 #include <cstdint>
+#include <cstdlib>
+#include <map>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace py = pybind11;
@@ -168,23 +173,45 @@ class StepRunner {
     prog(p).push_back(std::move(s));
   }
 
-  // Execute program p in order.  The GIL is held only while a Python callable runs.
-  void run(int p) {
+  // Execute program p in order.  The GIL is held only while a Python callable runs.  Optional
+  // hooks (debug / watchdog modes): pre(i, name) before and post(i, name) after
+  // every step -- heartbeats and per-item NaN/Inf guards without leaving the native runner.
+  void run(int p, py::object pre = py::none(), py::object post = py::none()) {
     if (released_) throw std::runtime_error("StepRunner: released (process group torn down)");
     auto& steps = prog(p);
+    const bool hooks = !pre.is_none() || !post.is_none();
     for (size_t i = 0; i < steps.size(); ++i) {
       Step& s = steps[i];
       current_ = (int)i;
+      if (!pre.is_none()) pre((int)i, s.name);
       if (s.kind == CALL) {
         s.fn();
-        continue;
+      } else {
+        py::gil_scoped_release nogil;
+        exec_native(s);
       }
-      py::gil_scoped_release nogil;
-      exec_native(s);
+      if (hooks && !post.is_none()) post((int)i, s.name);
     }
     current_ = -1;
     ++runs_;
   }
+
+  // Fault injection into the collectives this runner issues (the native form of
+  // flexmi.runtime.health.FaultyComm): {ordinal of the collective: (kind, arg)} with kind
+  // "delay" (sleep arg seconds first), "drop" (the collective runs on a scratch copy, so this
+  // rank loses its result), "corrupt" (NaN written into the first payload element) or "kill"
+  // (the process exits with code 3).
+  void set_faults(const std::map<int64_t, std::pair<std::string, double>>& f) {
+    faults_.clear();
+    for (auto& kv : f) {
+      const std::string& k = kv.second.first;
+      int kind = k == "delay" ? 0 : k == "drop" ? 1 : k == "corrupt" ? 2 : k == "kill" ? 3 : -1;
+      if (kind < 0) throw std::invalid_argument("set_faults: unknown fault kind " + k);
+      faults_[kv.first] = {kind, kv.second.second};
+    }
+    fault_n_ = 0;
+  }
+  int64_t fault_calls() const { return fault_n_; }
 
   // drop every pending Work handle (after an error / before tear-down)
   void reset_slots() {
@@ -239,6 +266,23 @@ class StepRunner {
   // worker thread drops its own reference right after completing the work, so the LAST reference
   // -- and with it the tensors the work captured -- is released on this thread, never on a
   // backend thread racing interpreter shutdown.
+  struct Fault {
+    int kind;
+    double arg;
+  };
+  // next collective: apply its injected fault (if any); returns the tensor the collective should
+  // write into (a scratch copy when the result is dropped)
+  at::Tensor inject(at::Tensor payload, at::Tensor result) {
+    auto it = faults_.find(fault_n_++);
+    if (it == faults_.end()) return result;
+    const Fault f = it->second;
+    if (f.kind == 0) std::this_thread::sleep_for(std::chrono::duration<double>(f.arg));
+    if (f.kind == 3) std::_Exit(3);
+    if (f.kind == 2 && payload.numel() > 0) payload.reshape({-1}).narrow(0, 0, 1).fill_(NAN);
+    if (f.kind == 1) return result.clone();
+    return result;
+  }
+
   void start(int slot, WorkPtr w) {
     if (pending_[slot]) slots_[slot]->wait();
     slots_[slot] = std::move(w);
@@ -263,20 +307,21 @@ class StepRunner {
       case A2A_START: {
         if (pending_[s.slot]) finish(s.slot);
         c10d::AllToAllOptions o;
-        start(s.slot, s.pg->alltoall_base(s.a, s.b, s.sa, s.sb, o));
+        at::Tensor recv = faults_.empty() ? s.a : inject(s.b, s.a);
+        start(s.slot, s.pg->alltoall_base(recv, s.b, s.sa, s.sb, o));
         bytes_sent_ += s.b.numel() * s.b.element_size();
         break;
       }
       case AR_START: {
         if (pending_[s.slot]) finish(s.slot);
-        std::vector<at::Tensor> v{s.a};
+        std::vector<at::Tensor> v{faults_.empty() ? s.a : inject(s.a, s.a)};
         start(s.slot, s.pg->allreduce(v));
         bytes_sent_ += s.a.numel() * s.a.element_size();
         break;
       }
       case AR_SYNC: {
         if (!pending_[s.slot]) {
-          std::vector<at::Tensor> v{s.a};
+          std::vector<at::Tensor> v{faults_.empty() ? s.a : inject(s.a, s.a)};
           start(s.slot, s.pg->allreduce(v));
           bytes_sent_ += s.a.numel() * s.a.element_size();
         }
@@ -288,7 +333,8 @@ class StepRunner {
         if (s.kind == RS_START && pending_[s.slot]) finish(s.slot);
         if (s.kind == RS_START || !pending_[s.slot]) {
           c10d::ReduceScatterOptions o;
-          start(s.slot, s.pg->_reduce_scatter_base(s.a, s.b, o));
+          at::Tensor out = faults_.empty() ? s.a : inject(s.b, s.a);
+          start(s.slot, s.pg->_reduce_scatter_base(out, s.b, o));
           bytes_sent_ += s.b.numel() * s.b.element_size();
         }
         if (s.kind == RS_SYNC) finish(s.slot);
@@ -297,7 +343,8 @@ class StepRunner {
       case AG_SYNC: {
         if (pending_[s.slot]) finish(s.slot);
         c10d::AllgatherOptions o;
-        start(s.slot, s.pg->_allgather_base(s.a, s.b, o));
+        at::Tensor out = faults_.empty() ? s.a : inject(s.b, s.a);
+        start(s.slot, s.pg->_allgather_base(out, s.b, o));
         bytes_sent_ += s.b.numel() * s.b.element_size();
         finish(s.slot);
         break;
@@ -311,6 +358,8 @@ class StepRunner {
   }
 
   std::vector<std::vector<Step>> progs_;
+  std::map<int64_t, Fault> faults_;
+  int64_t fault_n_ = 0;
   std::vector<WorkPtr> slots_;
   std::vector<bool> pending_;
   int current_ = -1;
@@ -339,7 +388,9 @@ PYBIND11_MODULE(_rt, m) {
       .def("add_all_gather", &StepRunner::add_all_gather, py::arg("program"), py::arg("slot"), py::arg("pg"),
            py::arg("out"), py::arg("input"), py::arg("name") = "")
       .def("add_wait", &StepRunner::add_wait, py::arg("program"), py::arg("slot"), py::arg("name") = "")
-      .def("run", &StepRunner::run)
+      .def("run", &StepRunner::run, py::arg("program"), py::arg("pre") = py::none(), py::arg("post") = py::none())
+      .def("set_faults", &StepRunner::set_faults)
+      .def_property_readonly("fault_calls", &StepRunner::fault_calls)
       .def("reset_slots", &StepRunner::reset_slots)
       .def("release", &StepRunner::release)
       .def_property_readonly("released", &StepRunner::released)

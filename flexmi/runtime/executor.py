@@ -289,6 +289,7 @@ class NativeRunner:
         self.world_pg = dist.group.WORLD if ex.world > 1 else None
         self.slots = {}
         self.pids = {}
+        self.step_items = {}
         self.keep = []          # Python objects referenced by native steps (graphs, callables)
         global _LIVE_RUNNERS
         if _LIVE_RUNNERS is None:
@@ -361,20 +362,26 @@ class NativeRunner:
             raise ValueError(f"unknown native item {kind}")
 
     def program(self, items):
-        """Program id for an item list (compiled once per list)."""
+        """Program id for an item list (compiled once per list).  ``step_items[pid][i]`` is the
+        (item, last step of that item) behind native step i (hooks map steps back to items)."""
         pid = self.pids.get(id(items))
         if pid is None:
             pid = self.rt.new_program()
+            owner = []
             for it in items:
+                n0 = self.rt.program_size(pid)
                 self.add_item(pid, it)
+                n1 = self.rt.program_size(pid)
+                owner.extend((it, k == n1 - 1) for k in range(n0, n1))
             self.pids[id(items)] = pid
+            self.step_items[pid] = owner
             self.keep.append(items)
         return pid
 
-    def run(self, pid):
+    def run(self, pid, pre=None, post=None):
         rt, comm = self.rt, self.ex.comm
         c0, b0 = rt.collectives, rt.bytes_sent
-        rt.run(pid)
+        rt.run(pid, pre, post)
         comm.calls += rt.collectives - c0
         comm.bytes_sent += rt.bytes_sent - b0
 
@@ -1480,16 +1487,24 @@ class Executor:
         debug / watchdog / timer hooks; FLEXMI_NATIVE_RUNNER=0 disables it."""
         if self._native is None:
             from flexmi.parallel.comm import Comm
+            from flexmi.runtime.health import FaultyComm
+            comm = self.comm
+            faults = None
+            if isinstance(comm, FaultyComm) and type(comm.inner) is Comm:
+                faults, comm = comm.faults, comm.inner
             ok = (os.environ.get("FLEXMI_NATIVE_RUNNER", "1") != "0" and _rt_module() is not None
-                  and type(self.comm) is Comm and not self.debug and self.watchdog is None
-                  and not self.timer.enabled)
+                  and type(comm) is Comm and not self.timer.enabled)
             self._native = NativeRunner(self) if ok else False
+            if ok and faults:
+                # FaultyComm's injections on the native path: the runner counts its collectives
+                self._native.rt.set_faults({int(k): (str(v[0]), float(v[1]) if len(v) > 1 else 0.0)
+                                            for k, v in faults.items()})
         return self._native or None
 
     def _run(self, prog):
-        if self.debug or self.watchdog is not None:
-            return self._run_guarded(prog)
         nr = self.native_runner()
+        if self.debug or self.watchdog is not None:
+            return self._run_guarded(prog, nr)
         if nr is not None:
             nr.run(nr.program(prog))
             return
@@ -1502,14 +1517,34 @@ class Executor:
             for it in prog:
                 it.fn()
 
-    def _run_guarded(self, prog):
+    def _run_guarded(self, prog, nr=None):
         """Debug / watchdog execution: heartbeat per item; in debug mode every item is followed
-        by a device synchronisation and its NaN/Inf guard."""
+        by a device synchronisation and its NaN/Inf guard.  With the native
+        step runner the heartbeat and the guards are its per-step hooks, so fault / debug /
+        watchdog runs execute the production program (native collectives included)."""
         from flexmi.runtime.health import WatchdogTimeout
         wd = self.watchdog
         if wd is not None:
             wd.arm()
         try:
+            if nr is not None:
+                pid = nr.program(prog)
+                owner = nr.step_items[pid]
+
+                def pre(i, name):
+                    if wd is not None:
+                        wd.beat(name)
+
+                def post(i, name):
+                    if not self.debug or not owner[i][1]:      # guard after an item's last step
+                        return
+                    if self.backend == "hip":
+                        torch.cuda.synchronize()
+                    it = owner[i][0]
+                    if it.check is not None:
+                        it.check()
+                nr.run(pid, pre, post)
+                return
             for it in prog:
                 if wd is not None:
                     wd.beat(it.name)

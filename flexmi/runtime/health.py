@@ -157,8 +157,11 @@ class Watchdog:
 class FaultyComm:
     """Wraps a Comm; counts collectives (all_to_all + all_reduce) and injects one fault per
     entry of ``faults``: ``{call_index: ("delay", secs) | ("drop",) | ("corrupt",) | ("kill",)}``.
-    ``drop`` skips an all-reduce (the rank keeps its local gradient), ``corrupt`` writes NaN
-    into the payload, ``kill`` ends this rank abruptly (exit code 3)."""
+    ``drop`` loses this rank's result of the collective (it runs on a scratch copy, so the rank
+    keeps its local gradient while its peers get the sum -- no peer is left waiting), ``corrupt``
+    writes NaN into the payload, ``kill`` ends this rank abruptly (exit code 3).  The executor
+    hands ``faults`` to the native step runner (``flexmi._rt`` set_faults), so injection runs on
+    the production path too."""
 
     def __init__(self, inner, faults: Dict[int, tuple]):
         self.inner = inner
@@ -183,6 +186,8 @@ class FaultyComm:
         if f and f[0] == "kill":
             os._exit(3)
         out = self.inner.all_to_all(send, recv_numel, dtype, device)
+        if f and f[0] == "drop":
+            out = [torch.zeros_like(o) for o in out]
         if f and f[0] == "corrupt":
             for o in out:
                 if o.numel():
@@ -197,7 +202,7 @@ class FaultyComm:
         if f and f[0] == "kill":
             os._exit(3)
         if f and f[0] == "drop":
-            return None
+            return self.inner.all_reduce_async(t.clone(), ranks)
         if f and f[0] == "corrupt" and t.numel():
             t.view(-1)[0] = float("nan")
         return self.inner.all_reduce_async(t, ranks)

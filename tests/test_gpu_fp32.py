@@ -35,6 +35,29 @@ def test_gemm_f32_orientations(gpu, a_k, b_k, M, N, K):
     assert rel_err(C, ref) < TOL, (a_k, b_k, M, N, K, rel_err(C, ref))
 
 
+@pytest.mark.parametrize("variant", [1, 3])
+@pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(8192, 1024, 1024), (1024, 1024, 8192), (1000, 520, 512)])
+def test_gemm_f32_lds_dma_variant(gpu, variant, a_k, b_k, M, N, K):
+    """The opt-in LDS-DMA pipelined fp32 kernel (256x128 with 8 or 4 waves, 128x128, split-K)."""
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(4)
+    A, B = torch.randn(M, K, device=gpu), torch.randn(K, N, device=gpu)
+    Ag = A if a_k else A.t().contiguous()
+    Bg = B.t().contiguous() if b_k else B
+    C = torch.empty(M, N, device=gpu)
+    db = torch.zeros(M, device=gpu)
+    Kk.C().gemm_f32_set_variant(variant)
+    try:
+        Kk.gemm(Ag, K if a_k else M, a_k, Bg, K if b_k else N, b_k, C, N, M, N, K,
+                rowsum_a=None if a_k else db)
+    finally:
+        Kk.C().gemm_f32_set_variant(0)
+    assert rel_err(C, A.double() @ B.double()) < TOL
+    if not a_k:
+        assert rel_err(db, A.double().sum(1)) < TOL
+
+
 def test_gemm_f32_epilogue_bias_act_beta(gpu):
     from flexmi.ops import _kernels as Kk
     torch.manual_seed(1)

@@ -61,6 +61,7 @@ def test_watchdog_interrupts_a_stalled_step():
     from flexmi.runtime.health import WatchdogTimeout
     m, x = _mlp(debug=False, watchdog=0.5)
     ex = m.init_layers()
+    assert ex.native_runner() is not None      # heartbeats are the native runner's per-step hooks
     _feed(m, x)
     op = m.get_layer_by_name("fc1")
     orig = op.forward
@@ -90,7 +91,10 @@ def _fault_worker(rank, world, port, fault, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     import datetime
     import torch.distributed as dist
-    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    # rendezvous through a file store in this run's private directory: no TCP port to race for
+    # with the other multi-process tests running in parallel
+    store = dist.FileStore(os.path.join(out_dir, "store"), world)
+    dist.init_process_group("gloo", store=store, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
     res = {"rank": rank, "error": None}
     try:
         from flexmi.runtime.health import FaultyComm
@@ -98,6 +102,8 @@ def _fault_worker(rank, world, port, fault, out_dir):
         if rank == 1:
             m.comm = FaultyComm(m.comm, {0: fault})
         m.init_layers()
+        nr = m._ex().native_runner()
+        res["native"] = nr is not None
         for it in range(2):
             _feed(m, x, it)
             m._ex().train_step()
@@ -137,6 +143,8 @@ def test_dropped_allreduce_is_detected_as_replica_divergence():
     res, hung, _ = _run_faulty(("drop",))
     assert not hung
     assert res[0]["error"] == "ReplicaDivergence" and res[1]["error"] == "ReplicaDivergence", res
+    # the fault was injected by the native step runner (flexmi._rt), the production path
+    assert res[0]["native"] and res[1]["native"], res
 
 
 @pytest.mark.multiproc
@@ -144,6 +152,7 @@ def test_corrupted_allreduce_is_detected_as_nonfinite_weights():
     res, hung, _ = _run_faulty(("corrupt",))
     assert not hung
     assert res[0]["error"] == "NumericalError" and res[1]["error"] == "NumericalError", res
+    assert res[0]["native"] and res[1]["native"], res
 
 
 @pytest.mark.multiproc
