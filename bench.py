@@ -6,8 +6,10 @@ DLRM MLPerf-like configuration (13 dense + 26 sparse features, Criteo-Terabyte t
 max-ind-range 40M = 187.8 M rows x 128 fp32 = 96 GB of tables, dot interaction, bottom MLP
 13-512-256-128, top MLP 479-1024-1024-512-256-1, BCE loss, SGD), synthetic data of that shape and
 random-init weights (no dataset/network).  Weak scaling: per-GPU batch fixed (default 8192, i.e.
-the MLPerf global batch 65536 at 8 GPUs); tables are placed whole on GPUs (table-wise model
-parallelism) and the MLPs are data parallel (RCCL all-to-all + bucketed all-reduce).
+the MLPerf global batch 65536 at 8 GPUs); the four ~40 M-row tables are split on the parameter
+(column) dimension over all GPUs, the others placed whole on one GPU (table-wise model
+parallelism, HBM-balanced: dlrm_strategy), and the MLPs are data parallel (RCCL all-to-all +
+bucketed all-reduce).
 
     python bench.py --gpus N --steps K --warmup W          (N>1 under torch.distributed.run)
 
@@ -201,7 +203,7 @@ def run_once(a, dtype, comm):
             "global_batch": gb,
             "seq_len": 1,
             "parallelism": (f"dp{world}" if world == 1 or a.strategy == "dp" else
-                            f"soap-search{world}" if a.strategy == "search" else f"table-wise-emb{world}+dp{world}-mlp"),
+                            f"soap-search{world}" if a.strategy == "search" else f"table+column-emb{world}+dp{world}-mlp"),
             "tables_rows": sum(dcfg.embedding_size),
             "embedding_dim": dcfg.sparse_feature_size,
             "mlp_bot": dcfg.mlp_bot,

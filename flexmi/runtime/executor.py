@@ -321,7 +321,10 @@ class NativeRunner:
             x = nat[1]
             s = self.slot(("a2a", id(x)))
             self.keep.append(x)
-            rt.add_all_to_all(pid, s, self.world_pg, x.recv_buf, x.send_buf, list(x.recv_sizes), list(x.send_sizes),
+            if not x.active:        # this rank has no piece in the exchange
+                return
+            rs_, ss_ = x.group_splits()
+            rt.add_all_to_all(pid, s, x.pg if x.pg is not None else self.world_pg, x.recv_buf, x.send_buf, rs_, ss_,
                               it.name)
             if kind == "a2a_sync":
                 rt.add_wait(pid, s, it.name + ".wait")
@@ -412,10 +415,23 @@ class FusedExchange:
     pack and unpack phases are each ONE multi-descriptor copy launch (per 16 pieces) instead of
     a copy per (tensor, peer) piece."""
 
-    def __init__(self, items, world, rank):
+    def __init__(self, items, world, rank, comm=None):
         self.items = items
         self.world = world
         self.rank = rank
+        # ranks that send or receive anything in this exchange: a strict subset exchanges on its
+        # own communicator (created here, on every rank in plan order -- new_group is collective)
+        # and the other ranks skip the collective entirely
+        parts = set()
+        for st, *_ in items:
+            for t in st.plan.transfers:
+                if t.src != t.dst:
+                    parts.update((t.src, t.dst))
+        self.participants = sorted(parts)
+        self.active = rank in parts
+        self.pg = None
+        if comm is not None and 0 < len(parts) < world:
+            self.pg = comm.group_for(self.participants)
         st0 = items[0][0]
         self.dtype, self.device = st0.dtype, st0.device
         self.adds = [acc or st.plan.src.partial for st, src, dst, acc in items]
@@ -540,10 +556,18 @@ class FusedExchange:
         """Launch the all_to_all asynchronously (RCCL runs on its own stream; the current
         stream keeps executing independent work until :meth:`wait`)."""
         import torch.distributed as dist
-        self.work = dist.all_to_all_single(self.recv_buf, self.send_buf, self.recv_sizes, self.send_sizes,
-                                           async_op=True)
+        if not self.active:
+            return
+        rs, ss = self.group_splits()
+        self.work = dist.all_to_all_single(self.recv_buf, self.send_buf, rs, ss, group=self.pg, async_op=True)
         comm.calls += 1
         comm.bytes_sent += self.send_buf.numel() * self.send_buf.element_size()
+
+    def group_splits(self):
+        """(recv, send) split sizes in the order of the exchange's communicator."""
+        if self.pg is None:
+            return list(self.recv_sizes), list(self.send_sizes)
+        return [self.recv_sizes[p] for p in self.participants], [self.send_sizes[p] for p in self.participants]
 
     def wait(self):
         if self.work is not None:
@@ -1219,7 +1243,7 @@ class Executor:
                 continue
             prods = [op_pos[self.tensors[g].owner_op.guid] for g, *_ in st[1]
                      if self.tensors[g].owner_op is not None and self.tensors[g].owner_op.guid in op_pos]
-            ex = FusedExchange(items, self.world, self.rank)
+            ex = FusedExchange(items, self.world, self.rank, self.comm)
             deferred[k] = ex
             launch_after[max(prods) if prods else -1].append(ex)
         for ex in launch_after.get(-1, []):
@@ -1389,7 +1413,7 @@ class Executor:
                 if self.world == 1 or all(rs.local_only for rs, *_ in items):
                     self._emit_reshards(bwd, items, "reshard.bwd")
                 else:
-                    ex = FusedExchange(items, self.world, self.rank)
+                    ex = FusedExchange(items, self.world, self.rank, self.comm)
                     self._emit_exchange_start(bwd, ex, "reshard.bwd")
                     if defer_ok:
                         flush_deferred()          # dW GEMMs overlap this exchange
@@ -1451,7 +1475,7 @@ class Executor:
         if self.world == 1 or all(rs.local_only for rs, *_ in items):
             lst.append(Item("compute", (lambda items=items: run_reshards(self.comm, items)), name))
             return
-        ex = FusedExchange(items, self.world, self.rank)
+        ex = FusedExchange(items, self.world, self.rank, self.comm)
         lst.append(Item("compute", ex.pack, name + ".pack"))
         lst.append(Item("comm", (lambda ex=ex: ex.exchange(self.comm)), name + ".a2a", native=("a2a_sync", ex)))
         lst.append(Item("compute", ex.unpack, name + ".unpack"))

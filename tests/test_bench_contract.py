@@ -6,6 +6,8 @@ import socket
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
         "scaling", "vs_baseline", "dtype", "data", "config"}
@@ -46,4 +48,19 @@ def test_bench_two_ranks():
               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
               "--steps", "2", "--warmup", "1", "--config", "tiny", "--batch-per-gpu", "64"])
     _check(r, 2)
-    assert "table-wise" in r["config"]["parallelism"]
+    assert "emb2" in r["config"]["parallelism"]
+
+
+@pytest.mark.multiproc
+@pytest.mark.parametrize("strategy", ["table", "dp", "search"])
+def test_bench_eight_ranks_mlperf_plan(strategy):
+    """The exact 8-GPU plan the driver's scaling run builds (mlperf widths: d=128, 26 tables,
+    bottom 13-512-256-128, top 479-1024-1024-512-256-1; HBM-balanced column/table placement or
+    pure DP or the SOAP search) compiled and stepped on 8 gloo ranks with scaled-down tables."""
+    extra = ["--search-budget", "200"] if strategy == "search" else []
+    r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+              "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "8",
+              "--steps", "2", "--warmup", "1", "--config", "mlperf", "--table-scale", "1e-4",
+              "--batch-per-gpu", "64", "--strategy", strategy] + extra)
+    _check(r, 8)
+    assert r["config"]["embedding_dim"] == 128 and r["config"]["mlp_top"] == [479, 1024, 1024, 512, 256, 1]

@@ -57,6 +57,19 @@ def _build(case, world):
         case = case[:-5]
         cfg.zero_stage = 1
         cfg.grad_bucket_mb = 0.002
+    if case == "mlp_subset":
+        # ops placed on a device subset: fc1 / fc2 on ranks {0, 1} with swapped sample shards, so the
+        # fc1 -> fc2 reshard involves only ranks 0 and 1 (its all_to_all runs on a 2-rank
+        # communicator; ranks 2, 3 skip it)
+        x = m.create_tensor([B, 12], name="x")
+        h = m.dense(x, 16, ActiMode.AC_MODE_RELU, name="fc1")
+        h = m.dense(h, 8, ActiMode.AC_MODE_TANH, name="fc2")
+        o = m.softmax(m.dense(h, 4, name="fc3"), name="sm")
+        loss = LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY
+        inputs["x"] = (x, (B, 12), "f")
+        if world > 2:
+            strat["fc1"] = ParallelConfig([1, 2], [0, 1])
+            strat["fc2"] = ParallelConfig([1, 2], [1, 0])
     if case in ("mlp_dp", "mlp_channel"):
         x = m.create_tensor([B, 12], name="x")
         h = m.dense(x, 16, ActiMode.AC_MODE_RELU, name="fc1")
@@ -70,6 +83,33 @@ def _build(case, world):
             strat["fc1"] = ParallelConfig([world, 1], list(range(world)))
             if world % 2 == 0:
                 strat["fc2"] = ParallelConfig([2, world // 2], list(range(world)))
+    elif case in ("dlrm_mlperf8", "dlrm_shipped8"):
+        # the 8-GPU plans bench.py / the reference use, rehearsed on 8 gloo ranks: the MLPerf table
+        # set (rows scaled 1/20000, d=32 so the big tables column-split 8 ways into 4-float rows)
+        # under dlrm_strategy(model, 8), and run_random (8 x 1e6 rows scaled to 1000) under the
+        # reference's shipped src/runtime/dlrm_strategy_8embs_8gpus.pb
+        if case == "dlrm_mlperf8":
+            from flexmi.models.dlrm import MLPERF_TABLES
+            dcfg = DLRMConfig(32, [max(3, r // 20000) for r in MLPERF_TABLES], [13, 64, 32], [0, 64, 32, 1], 1, -1, -1,
+                              0.0, "dot", "", -1, "bce", "mlperf_scaled")
+        else:
+            dcfg = DLRMConfig.preset("run_random")
+            dcfg.embedding_size = [1000] * 8
+        d, s, p = build_dlrm(m, dcfg)
+        loss = LossType.LOSS_BINARY_CROSSENTROPY if dcfg.loss == "bce" else LossType.LOSS_MEAN_SQUARED_ERROR_AVG_REDUCE
+        inputs["dense"] = (d, (B, dcfg.mlp_bot[0]), "f")
+        for i, (t, r) in enumerate(zip(s, dcfg.embedding_size)):
+            inputs[f"sparse{i}"] = (t, (B, 1), ("i", r))
+        if world > 1:
+            if case == "dlrm_mlperf8":
+                strat = dlrm_strategy(m, world)
+                assert sum(len(pc.device_ids) == world and pc.dims[0] == world for pc in strat.values()) >= 4
+            else:
+                from flexmi.parallel.strategy import load_strategies_from_file
+                ref = "/root/reference/src/runtime/dlrm_strategy_8embs_8gpus.pb"
+                if not os.path.exists(ref):
+                    pytest.skip("reference strategy file not available")
+                strat = load_strategies_from_file(ref)
     elif case.startswith("dlrm"):
         dcfg = DLRMConfig.preset("tiny")
         dcfg.arch_interaction_op = "dot" if case == "dlrm_dot" else "cat"
@@ -160,6 +200,11 @@ def _run(case, world, rank, steps, out_path):
     loss = m.get_perf_metrics().get_loss()
     nr = ex.native_runner()
     native_colls = nr.rt.collectives if nr is not None else -1
+    if case == "mlp_subset" and world > 2:
+        from flexmi.runtime.executor import FusedExchange
+        subs = [x for x in nr.keep if isinstance(x, FusedExchange) and x.participants == [0, 1]]
+        assert subs and all((x.pg is not None) for x in subs), "subset exchange not on its own communicator"
+        assert all(x.active == (rank in (0, 1)) for x in subs)
     if rank == 0:
         np.savez(out_path, loss=loss, native_colls=native_colls, *params)
 
@@ -190,7 +235,8 @@ def _launch(case, world, steps=3):
                                         ("dlrm_cat", 2), ("dlrm_colsplit", 2), ("cnn_spatial", 2),
                                         ("dlrm_search", 2), ("dlrm_search", 4), ("dlrm_rowsplit", 2),
                                         ("dlrm_rowsplit", 4), ("mlp_dp_zero", 2), ("dlrm_dot_zero", 2),
-                                        ("mlp_dp_zero", 4), ("dlrm_cat_dpsmall", 2)])
+                                        ("mlp_dp_zero", 4), ("dlrm_cat_dpsmall", 2), ("dlrm_mlperf8", 8), ("mlp_subset", 4),
+                                        ("dlrm_shipped8", 8)])
 def test_strategy_equivalence(case, world):
     ref = _launch(case, 1)
     got = _launch(case, world)

@@ -172,3 +172,22 @@ def test_loss_threshold_model_level():
     ex.scatter_from_host(m.get_label_tensor(), rng.randint(0, 2, (8, 1)).astype(np.float32))
     ex.train_step()
     assert np.isfinite(m.get_perf_metrics().get_loss())
+
+
+@pytest.mark.parametrize("gpus", [2, 4, 8])
+def test_dlrm_strategy_hbm_balanced(gpus):
+    """The default multi-GPU plan of the MLPerf table set: the ~40 M-row tables split on the
+    parameter dim over all GPUs, the rest table-wise; per-GPU table bytes within 2x of each other
+    (table-wise only at 8 GPUs: 20.9 GB vs 0.27 GB)."""
+    from flexmi.core import FFConfig, FFModel
+    from flexmi.models.dlrm import DLRMConfig, build_dlrm, dlrm_strategy, strategy_table_bytes
+    cfg = FFConfig()
+    cfg.batchSize, cfg.device = 64, "cpu"
+    m = FFModel(cfg)
+    build_dlrm(m, DLRMConfig.preset("mlperf"))
+    st = dlrm_strategy(m, gpus)
+    assert len(st) == 26
+    per = strategy_table_bytes(m, st, gpus)
+    assert abs(sum(per) - 187767399 * 128 * 4) / sum(per) < 1e-9
+    assert max(per) / min(per) < 2.0, per
+    assert max(per) < 288e9 * 0.5
