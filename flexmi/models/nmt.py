@@ -63,3 +63,44 @@ def nmt(model, cfg: NMTConfig = None, batch=None):
     logits = model.reshape(logits, [b * T, cfg.vocab], name="logits")
     out = model.softmax(logits, name="softmax")
     return {"src": src, "dst": dst}, out
+
+
+def nmt_strategy(model, num_gpus, mode="reference"):
+    """Per-chunk placement strategies for the NMT graph (``nmt/nmt.cc:269-309`` set_global_config).
+
+    ``reference``: what the reference ships -- the source-side embedding on GPU 0 and the
+    target-side one on GPU 1 (its ``embed[i]`` configs, i < seq / LSTM_PER_NODE_LENGTH -> 0 else 1),
+    every LSTM chunk, the vocabulary projection and the softmax data parallel over all GPUs.
+    ``pipeline``: chunk (operator) parallelism -- encoder and decoder chunks of layer l, step
+    block j on GPU (l * nchunks + j) mod num_gpus, each chunk whole (no sample split), so
+    consecutive chunks of a layer hand their (h, c) state to the next GPU; embeddings follow their
+    first chunk, projection + softmax stay data parallel.
+    Returns {op name: ParallelConfig}; the simulator can cost either (tools/soap_report.py)."""
+    from flexmi.core.types import OperatorType
+    from flexmi.parallel.layout import ParallelConfig
+    n = num_gpus
+    st = {}
+    lstm = [op for op in model.layers if op.op_type == OperatorType.OP_LSTM]
+    if mode == "reference":
+        st["src_embed"] = ParallelConfig([1, 1], [0])
+        st["dst_embed"] = ParallelConfig([1, 1], [min(1, n - 1)])
+        for op in lstm:
+            st[op.name] = ParallelConfig.data_parallel(op.out_ndims, n)
+        return st
+    if mode != "pipeline":
+        raise ValueError(mode)
+    chunks = {}
+    for op in lstm:                       # names "<enc|dec><layer>.lstm<chunk>"
+        tag, rest = op.name.split(".lstm")
+        layer = int(tag[3:])
+        chunks.setdefault(tag[:3], []).append((layer, int(rest), op))
+    for side in ("enc", "dec"):
+        items = sorted(chunks.get(side, []), key=lambda x: (x[0], x[1]))
+        nch = 1 + max((j for _, j, _ in items), default=0)
+        for layer, j, op in items:
+            dev = (layer * nch + j + (nch if side == "dec" else 0)) % n
+            st[op.name] = ParallelConfig([1] * op.out_ndims, [dev])
+        first = next((op for layer, j, op in items if layer == 0 and j == 0), None)
+        if first is not None:
+            st["src_embed" if side == "enc" else "dst_embed"] = ParallelConfig([1, 1], list(st[first.name].device_ids))
+    return st

@@ -20,7 +20,8 @@ from typing import Dict, List, Sequence, Tuple
 
 from flexmi.core.types import ActiMode, OperatorType
 
-DEFAULT_DB = os.path.join(os.path.dirname(__file__), "costdb", "mi355x.json")
+DEFAULT_DB = os.path.join(os.path.dirname(__file__), "costdb", "mi355x.json")            # bf16 kernels
+DEFAULT_DB_FP32 = os.path.join(os.path.dirname(__file__), "costdb", "mi355x_fp32.json")  # fp32 kernels
 
 
 def _prod(s):
@@ -48,7 +49,8 @@ class CostModel:
         self.eb = dtype_bytes
         self.db: Dict[str, Tuple[float, float]] = {}
         self.scale: Dict[str, float] = {}
-        path = db_path if db_path is not None else DEFAULT_DB
+        self.group_factor: Dict[str, float] = {}   # fused-launch / isolated per-op time (measured)
+        path = db_path if db_path is not None else (DEFAULT_DB_FP32 if dtype_bytes == 4 else DEFAULT_DB)
         if path and os.path.exists(path):
             self.load_db(path)
 
@@ -59,6 +61,7 @@ class CostModel:
         for k, v in d.get("entries", {}).items():
             self.db[k] = (float(v[0]), float(v[1]))
         self.scale.update({k: float(v) for k, v in d.get("scale", {}).items()})
+        self.group_factor.update({k: float(v) for k, v in d.get("group_factor", {}).items()})
 
     @staticmethod
     def fit_scales(entries: Dict[str, Tuple[float, float]], roofline: Dict[str, Tuple[float, float]]):
@@ -79,7 +82,8 @@ class CostModel:
         tiles = math.ceil(M / 128) * math.ceil(N / 64)
         fill = min(1.0, tiles / 256.0)
         eff = m.mfma_eff * max(0.2, fill)
-        t_c = 2.0 * M * N * K / (m.peak_bf16_tflops * 1e12 * eff) * 1e6
+        peak = m.peak_bf16_tflops if self.eb == 2 else m.peak_fp32_tflops
+        t_c = 2.0 * M * N * K / (peak * 1e12 * eff) * 1e6
         t_m = (M * K + N * K + M * N) * self.eb / (m.hbm_GBps * 1e9 * m.hbm_eff) * 1e6
         return max(t_c, t_m)
 
@@ -91,6 +95,7 @@ class CostModel:
         t = op.op_type
         L = self.m.launch_us
         eb = self.eb
+        peak = self.m.peak_bf16_tflops if eb == 2 else self.m.peak_fp32_tflops
         if getattr(op, "is_view", False) or t in (OperatorType.OP_FLAT, OperatorType.OP_RESHAPE):
             return 0.0, 0.0
         if t == OperatorType.OP_LINEAR:
@@ -115,7 +120,7 @@ class CostModel:
             nb = _prod(a[:-2])
             M, K, N = a[-2], a[-1], bb[-1]
             fl = 2.0 * nb * M * N * K
-            tc = fl / (self.m.peak_bf16_tflops * 1e12 * self.m.mfma_eff) * 1e6
+            tc = fl / (peak * 1e12 * self.m.mfma_eff) * 1e6
             tm = self._bytes_us((nb * (M * K + K * N + M * N)) * eb)
             return L + max(tc, tm), 2 * L + 2 * max(tc, tm)
         if t == OperatorType.OP_CONV2D:
@@ -123,13 +128,13 @@ class CostModel:
             _, k, p, q = out_shapes[0]
             kh, kw = getattr(op, "kh", 3), getattr(op, "kw", 3)
             fl = 2.0 * n * k * p * q * c * kh * kw
-            tc = fl / (self.m.peak_bf16_tflops * 1e12 * self.m.mfma_eff) * 1e6
+            tc = fl / (peak * 1e12 * self.m.mfma_eff) * 1e6
             tm = self._bytes_us((n * c * h * w + n * k * p * q) * eb)
             return L + max(tc, tm), 3 * L + 2 * max(tc, tm)
         if t == OperatorType.OP_DOT_INTERACTION:
             fl = 2.0 * in_shapes[0][0] * op.F * op.F * op.d
             byt = sum(_prod(s) for s in list(in_shapes) + list(out_shapes)) * eb
-            tc = fl / (self.m.peak_bf16_tflops * 1e12 * self.m.mfma_eff * 0.5) * 1e6
+            tc = fl / (peak * 1e12 * self.m.mfma_eff * 0.5) * 1e6
             return L + max(tc, self._bytes_us(byt)), L + 2 * max(tc, self._bytes_us(byt))
         # bandwidth-bound ops (elementwise, concat/split, softmax, pool, BN, transpose, ...)
         byt = sum(_prod(s) for s in list(in_shapes) + list(out_shapes)) * eb
@@ -139,7 +144,8 @@ class CostModel:
         key = op_signature(op, in_shapes, out_shapes)
         hit = self.db.get(key)
         if hit is not None:
-            return hit
+            gf = self.group_factor.get(op.op_type.name, 1.0)
+            return hit[0] * gf, hit[1] * gf
         f, b = self.roofline(op, in_shapes, out_shapes)
         s = self.scale.get(op.op_type.name, 1.0)
         return f * s, b * s

@@ -170,13 +170,25 @@ class SimGraph:
             act = sum(_prod(s) for s in out_shapes)
             mem[dev] = mem.get(dev, 0.0) + act * self.cost.eb * 2
         wsync = []
+        emb = op.op_type == OperatorType.OP_EMBEDDING
         for w, lay in zip(op.weights, wls):
-            sparse = op.op_type == OperatorType.OP_EMBEDDING and self.sparse_ok and lay.replication() == 1
+            sparse = emb and self.sparse_ok
             for p in range(lay.num_parts()):
                 vol = _prod(_box_shape(lay.part_box(p)))
                 h = lay.holders[p]
                 if len(h) > 1:
-                    wsync.append((float(vol * 4), list(h)))
+                    if sparse:
+                        # replicated table with the sparse optimizer: only the rows a step touches
+                        # are exchanged (an all-gather of the global batch's row gradients + ids,
+                        # costed as the all-reduce of half that volume), never the dense table
+                        B = op.inputs[0].dims[0]
+                        bag = op.inputs[0].dims[1] if len(op.inputs[0].dims) > 1 else 1
+                        box = lay.part_box(p)
+                        cols = vol // max(1, box[0][1] - box[0][0])
+                        touched = min(vol, B * bag * cols)
+                        wsync.append((float(touched * 4 + B * bag * 8) / 2.0, list(h)))
+                    else:
+                        wsync.append((float(vol * 4), list(h)))
                 for d in h:
                     if sparse:
                         mem[d] = mem.get(d, 0.0) + vol * 4.0

@@ -47,14 +47,15 @@ def _make_clone(op, m, in_shapes, out_shapes):
     return ins
 
 
-def measure_op(op, in_shapes, out_shapes, reps=20, index_range=None, device="gpu"):
-    """(fwd_us, bwd_us) of ``op`` at the given shard shapes on ``cuda`` (``device="cpu"``:
-    host timing of the fp32 reference path, used by the CPU tests)."""
+def measure_op(op, in_shapes, out_shapes, reps=20, index_range=None, device="gpu", dtype="bf16"):
+    """(fwd_us, bwd_us) of ``op`` at the given shard shapes on ``cuda`` in compute precision
+    ``dtype`` (bf16 fast mode or the fp32 reference-precision kernels; ``device="cpu"``: host
+    timing of the fp32 reference path, used by the CPU tests)."""
     from flexmi.core import FFConfig, FFModel, SGDOptimizer, LossType
     cfg = FFConfig()
     cfg.batchSize = int(in_shapes[0][0]) if in_shapes and in_shapes[0] else 1
     cfg.device = device
-    cfg.compute_dtype = "bf16" if device == "gpu" else "fp32"
+    cfg.compute_dtype = dtype if device == "gpu" else "fp32"
     # the op's input gradient is part of its backward unless the input is a graph input
     cfg.input_grads = not (op.op_type == OperatorType.OP_LINEAR and op.inputs[0].owner_op is None)
     m = FFModel(cfg)
@@ -121,6 +122,66 @@ def measure_op(op, in_shapes, out_shapes, reps=20, index_range=None, device="gpu
 
     f = timed(fwd)
     b = timed(bwd)
+    m.executor = None
+    del ex
+    if device == "gpu":
+        torch.cuda.empty_cache()
+    return f, b
+
+
+def measure_embedding_group(ops, batch, reps=20, device="gpu", dtype="bf16"):
+    """(fwd_us, bwd_us) of ALL embedding ``ops`` looked up together at ``batch`` rows -- the fused
+    group launch the executor actually runs (one forward, one sparse-SGD backward for every table
+    of a placement).  tools/calibrate_costs.py divides it by the sum of the per-table isolated
+    measurements to get the DB's ``group_factor``."""
+    from flexmi.core import FFConfig, FFModel, SGDOptimizer, LossType
+    cfg = FFConfig()
+    cfg.batchSize = int(batch)
+    cfg.device = device
+    cfg.compute_dtype = dtype if device == "gpu" else "fp32"
+    m = FFModel(cfg)
+    ins = []
+    for op in ops:
+        t = m.create_tensor([batch, op.inputs[0].dims[1]], op.inputs[0].data_type)
+        m.embedding(t, op.num_entries, op.out_dim, op.aggr)
+        ins.append((t, op.num_entries))
+    last = [m.concat([l.outputs[0] for l in m.layers], 1)] if len(m.layers) > 1 else [m.layers[0].outputs[0]]
+    m.compile(SGDOptimizer(m, 0.001), LossType.LOSS_MEAN_SQUARED_ERROR_AVG_REDUCE, [])
+    ex = m.init_layers()
+    g = torch.Generator(device=ex.device)
+    g.manual_seed(0)
+    for t, rows in ins:
+        buf = ex.local_buffer(t)
+        buf.copy_(torch.randint(0, rows, buf.shape, generator=g, device=ex.device))
+    names = tuple(l.name + "." for l in m.layers if l.op_type == OperatorType.OP_EMBEDDING)
+    fwd = [it for it in ex.prog_fwd if it.kind == "compute" and it.name.startswith(names)]
+    bwd = [it for it in ex.prog_bwd if it.kind == "compute" and it.name.startswith(names)]
+    for gr in ex.grad.values():
+        gr.normal_(0, 1e-3)
+
+    def timed(items):
+        if not items:
+            return 0.0
+        import time
+        for it in items:
+            it.fn()
+        if device != "gpu":
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                for it in items:
+                    it.fn()
+            return (time.perf_counter() - t0) * 1e6 / reps
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            for it in items:
+                it.fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / reps
+
+    f, b = timed(fwd), timed(bwd)
     m.executor = None
     del ex
     if device == "gpu":

@@ -57,6 +57,18 @@ def _build(case, world):
         case = case[:-5]
         cfg.zero_stage = 1
         cfg.grad_bucket_mb = 0.002
+    if case in ("nmt_reference", "nmt_pipeline"):
+        # NMT seq2seq (2 layers, 3-step LSTM chunks) under the reference's chunk placement
+        # (embeddings on GPUs 0 / 1, chunks data parallel) and under chunk (pipeline) placement
+        from flexmi.models.nmt import NMTConfig, nmt, nmt_strategy
+        ncfg = NMTConfig.small()
+        cfg.batchSize = B = 4
+        ins, out = nmt(m, ncfg)
+        loss = LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY
+        for k, t in ins.items():
+            inputs[k] = (t, tuple(t.dims), ("i", ncfg.vocab))
+        if world > 1:
+            strat = nmt_strategy(m, world, case.split("_")[1])
     if case == "mlp_subset":
         # ops placed on a device subset: fc1 / fc2 on ranks {0, 1} with swapped sample shards, so the
         # fc1 -> fc2 reshard involves only ranks 0 and 1 (its all_to_all runs on a 2-rank
@@ -235,7 +247,8 @@ def _launch(case, world, steps=3):
                                         ("dlrm_cat", 2), ("dlrm_colsplit", 2), ("cnn_spatial", 2),
                                         ("dlrm_search", 2), ("dlrm_search", 4), ("dlrm_rowsplit", 2),
                                         ("dlrm_rowsplit", 4), ("mlp_dp_zero", 2), ("dlrm_dot_zero", 2),
-                                        ("mlp_dp_zero", 4), ("dlrm_cat_dpsmall", 2), ("dlrm_mlperf8", 8), ("mlp_subset", 4),
+                                        ("mlp_dp_zero", 4), ("dlrm_cat_dpsmall", 2), ("dlrm_mlperf8", 8), ("mlp_subset", 4), ("nmt_reference", 2),
+                                        ("nmt_pipeline", 2), ("nmt_pipeline", 4),
                                         ("dlrm_shipped8", 8)])
 def test_strategy_equivalence(case, world):
     ref = _launch(case, 1)

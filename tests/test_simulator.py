@@ -88,20 +88,22 @@ def test_candidates_cover_soap_dims(native):
 
 
 def test_search_beats_data_parallel_on_mlperf_dlrm(native):
-    """With 96 GB of tables, pure DP replicates and all-reduces the tables: the search must find
-    table/column placement that is orders of magnitude faster, and at least as good as the
-    hand-written greedy table-wise strategy."""
+    """Pure DP of the 96 GB table set is feasible in 288 GB of HBM and, with the sparse
+    optimizer, exchanges only the rows a step touches (not the dense tables): the search must
+    still beat it clearly and be at least as good as the hand-written HBM-balanced plan."""
     from flexmi.models.dlrm import dlrm_strategy
     from flexmi.parallel.search import SimGraph, optimize
     m = _dlrm(8, 8192, "mlperf")
-    r = optimize(m, 1500, 1.0, num_devices=8, seed=1, verbose=False)
-    assert r.speedup_vs_dp > 10
+    r0 = optimize(m, 1500, 1.0, num_devices=8, seed=1, verbose=False)      # walk from pure DP
+    assert 1.2 < r0.speedup_vs_dp < 100, r0.speedup_vs_dp
+    hand = dlrm_strategy(m, 8)
+    r = optimize(m, 1500, 1.0, num_devices=8, seed=1, verbose=False, init=hand)   # as bench.py seeds it
     g = r.graph
-    greedy = g.simulate(g.assign_from(dlrm_strategy(m, 8)))
-    assert r.best_us <= greedy * 1.001
+    greedy = g.simulate(g.assign_from(hand))
+    assert r.best_us <= greedy * 1.001 and r.best_us <= r0.best_us * 1.001
     assert max(g.memory(r.assign)) <= g.machine.hbm_bytes
     # deterministic for a seed (every rank must derive the same strategy)
-    r2 = optimize(m, 1500, 1.0, num_devices=8, seed=1, verbose=False)
+    r2 = optimize(m, 1500, 1.0, num_devices=8, seed=1, verbose=False, init=hand)
     assert r2.assign == r.assign
 
 

@@ -7,7 +7,8 @@ For every op of the model and every shard shape its candidate ParallelConfigs pr
 and write ``{"entries": {signature: [fwd_us, bwd_us]}, "scale": {op_type: measured/roofline}}``.
 
     python tools/calibrate_costs.py --model dlrm-mlperf --gpus 1,2,4,8 \
-        --out flexmi/parallel/costdb/mi355x.json
+        --out flexmi/parallel/costdb/mi355x.json                       (bf16 fast mode)
+    python tools/calibrate_costs.py --dtype fp32 --out flexmi/parallel/costdb/mi355x_fp32.json
 """
 from __future__ import annotations
 
@@ -21,12 +22,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def build_model(name, n, batch_per_gpu, device="gpu"):
+def build_model(name, n, batch_per_gpu, device="gpu", dtype="bf16"):
     from flexmi.core import FFConfig, FFModel, SGDOptimizer
     cfg = FFConfig()
     cfg.batchSize = batch_per_gpu * n
     cfg.device = device
-    cfg.compute_dtype = "bf16" if device == "gpu" else "fp32"
+    cfg.compute_dtype = dtype if device == "gpu" else "fp32"
     m = FFModel(cfg)
     if name.startswith("dlrm"):
         from flexmi.models.dlrm import DLRMConfig, build_dlrm
@@ -47,6 +48,7 @@ def main():
     ap.add_argument("--limit", type=int, default=0)
     ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"])
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--time-budget", type=float, default=900.0, help="stop measuring after this many seconds")
     a = ap.parse_args()
 
@@ -57,7 +59,7 @@ def main():
 
     todo = {}
     for n in [int(x) for x in a.gpus.split(",")]:
-        m = build_model(a.model, n, a.batch_per_gpu, a.device)
+        m = build_model(a.model, n, a.batch_per_gpu, a.device, a.dtype)
         for op in m.layers:
             for pc in candidate_configs(op, n):
                 ins, outs = op.input_layouts(pc), op.output_layouts(pc)
@@ -70,12 +72,12 @@ def main():
     keys = sorted(todo)
     if a.limit:
         keys = keys[: a.limit]
-    db = {"device": "MI355X", "dtype": "bf16", "model": a.model, "entries": {}, "scale": {}}
+    db = {"device": "MI355X", "dtype": a.dtype, "model": a.model, "entries": {}, "scale": {}}
     if os.path.exists(a.out):
         with open(a.out) as f:
             old = json.load(f)
         db["entries"].update(old.get("entries", {}))
-    cm = CostModel(MachineModel.mi355x(1), db_path="")
+    cm = CostModel(MachineModel.mi355x(1), db_path="", dtype_bytes=4 if a.dtype == "fp32" else 2)
     t0 = time.time()
     done = 0
     for k in keys:
@@ -85,7 +87,7 @@ def main():
             print(f"[calibrate] time budget reached after {done} measurements", flush=True)
             break
         op, i_s, o_s = todo[k]
-        r = measure_op(op, i_s, o_s, reps=a.reps, device=a.device)
+        r = measure_op(op, i_s, o_s, reps=a.reps, device=a.device, dtype=a.dtype)
         done += 1
         if r is None:
             continue
@@ -93,6 +95,24 @@ def main():
         print(f"[calibrate] {done}/{len(keys)} {k}: fwd {r[0]:.2f} us bwd {r[1]:.2f} us", flush=True)
         if done % 20 == 0:
             _write(a.out, db, todo, cm)
+    # fused embedding groups: the step runs every table of a placement in ONE forward and ONE
+    # sparse-SGD launch, so the isolated per-table times overstate it; measure the whole group
+    # at the 1-GPU batch and store measured(group) / sum(isolated tables) as group_factor
+    from flexmi.core.types import OperatorType
+    from flexmi.runtime.measure import measure_embedding_group
+    m1 = build_model(a.model, 1, a.batch_per_gpu, a.device, a.dtype)
+    embs = [op for op in m1.layers if op.op_type == OperatorType.OP_EMBEDDING]
+    if len(embs) > 1:
+        iso = 0.0
+        for op in embs:
+            k = op_signature(op, [tuple(op.inputs[0].dims)], [tuple(op.outputs[0].dims)])
+            if k in db["entries"]:
+                iso += sum(db["entries"][k])
+        gf, gb = measure_embedding_group(embs, a.batch_per_gpu, reps=a.reps, device=a.device, dtype=a.dtype)
+        if iso > 0:
+            db["group_factor"] = {"OP_EMBEDDING": round((gf + gb) / iso, 4)}
+            print(f"[calibrate] embedding group of {len(embs)}: fwd {gf:.1f} us bwd {gb:.1f} us vs isolated "
+                  f"{iso:.1f} us -> group_factor {db['group_factor']}", flush=True)
     _write(a.out, db, todo, cm)
     print(f"[calibrate] {len(db['entries'])} entries -> {a.out}; scales {db['scale']}", flush=True)
 
