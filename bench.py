@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="mlperf", choices=["mlperf", "run_random", "criteo_kaggle", "tiny"])
+    ap.add_argument("--config", default="mlperf", choices=["mlperf", "run_random", "criteo_kaggle", "summit", "summit_large", "kaggle_day1", "tiny"])
     ap.add_argument("--batch-per-gpu", type=int, default=8192)
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture of the step")
     ap.add_argument("--strategy", default="table", choices=["table", "dp", "search"],

@@ -473,14 +473,17 @@ __global__ void __launch_bounds__(256) fm_skinny_bwd_kernel(int ROWS, const unsi
   // partial dW/db reduced in LDS -> one atomic per column per block (B/ROWS adders per address)
   __shared__ float red[256 * 8];
   __shared__ float redb[256];
-  const int groups = K / 8;                       // host guarantees K % 8 == 0, K <= 2048
-  const int lpr = groups;                         // threads per row
+  // column block blockIdx.y covers [2048 y, 2048 y + 2048) of K (host: K % 8 == 0)
+  const int cb = blockIdx.y * 2048;
+  const int Kc = min(2048, K - cb);
+  const int lpr = Kc / 8;                         // threads per row
   const int rpi = 256 / lpr;
   const int sub = threadIdx.x / lpr, g = threadIdx.x - sub * lpr;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float dbs = 0.f;
   const long r0 = (long)blockIdx.x * ROWS;
-  const int c0 = g * 8;
+  const int c0 = cb + g * 8;
+  if (blockIdx.y) db = nullptr;                   // db accumulated once, by column block 0
   bf16x8_t wv = *reinterpret_cast<const bf16x8_t*>(w + c0);
   if (sub < rpi) {
     // 4 rows per iteration with every load issued first (clamped, unconditional): the per-row
@@ -523,11 +526,11 @@ __global__ void __launch_bounds__(256) fm_skinny_bwd_kernel(int ROWS, const unsi
   for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = (sub < rpi) ? acc[j] : 0.f;
   redb[threadIdx.x] = (sub < rpi && g == 0) ? dbs : 0.f;
   __syncthreads();
-  for (int c = threadIdx.x; c < K; c += 256) {
+  for (int c = threadIdx.x; c < Kc; c += 256) {
     const int gg = c / 8, j = c % 8;
     float t = 0.f;
     for (int q = 0; q < rpi; ++q) t += red[(q * lpr + gg) * 8 + j];
-    atomicAdd(dw + c, t);
+    atomicAdd(dw + cb + c, t);
   }
   if (db && threadIdx.x == 0) {
     float t = 0.f;
@@ -545,7 +548,7 @@ extern "C" void fm_skinny_fwd(const void* x, long ldx, const void* w, const floa
                      (const unsigned short*)x, ldx, (const unsigned short*)w, bias, (unsigned short*)y, ldy, B, K, act);
 }
 
-// dW (fp32 [K]) and db (fp32 [1]) are ACCUMULATED (callers zero them); requires K <= 2048
+// dW (fp32 [K]) and db (fp32 [1]) are ACCUMULATED (callers zero them); requires K % 8 == 0
 extern "C" void fm_skinny_bwd(const void* x, long ldx, const void* w, const void* y, long ldy, const void* dy, long lddy,
                               void* dx, long lddx, int dx_acc, float* dw, float* db, long B, int K, int act, hipStream_t s) {
   if (B <= 0) return;
@@ -553,7 +556,8 @@ extern "C" void fm_skinny_bwd(const void* x, long ldx, const void* w, const void
   // small batches shrink it so there are still >= 128 blocks (B=256 -> 2 rows per block)
   int ROWS = 64;
   while (ROWS > 2 && (B + ROWS - 1) / ROWS < 128) ROWS /= 2;
-  hipLaunchKernelGGL(fm_skinny_bwd_kernel, dim3((unsigned)((B + ROWS - 1) / ROWS)), dim3(256), 0, s, ROWS,
+  hipLaunchKernelGGL(fm_skinny_bwd_kernel, dim3((unsigned)((B + ROWS - 1) / ROWS), (unsigned)((K + 2047) / 2048)), dim3(256),
+                     0, s, ROWS,
                      (const unsigned short*)x, ldx, (const unsigned short*)w, (const unsigned short*)y, ldy,
                      (const unsigned short*)dy, lddy, (unsigned short*)dx, lddx, dx_acc, dw, db, B, K, act);
 }

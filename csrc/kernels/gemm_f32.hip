@@ -699,13 +699,17 @@ __global__ void __launch_bounds__(256) fm_skinny_bwd_f32(int ROWS, const float* 
                                                         float* __restrict__ db, long B, int K, int act) {
   __shared__ float red[256 * 4];
   __shared__ float redb[256];
-  const int lpr = K / 4;                 // host: K % 4 == 0, K <= 1024
+  // column block blockIdx.y covers [1024 y, 1024 y + 1024) of K (host: K % 4 == 0)
+  const int cb = blockIdx.y * 1024;
+  const int Kc = min(1024, K - cb);
+  const int lpr = Kc / 4;
   const int rpi = 256 / lpr;
   const int sub = threadIdx.x / lpr, g = threadIdx.x - sub * lpr;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   float dbs = 0.f;
   const long r0 = (long)blockIdx.x * ROWS;
-  const int c0 = g * 4;
+  const int c0 = cb + g * 4;
+  if (blockIdx.y) db = nullptr;          // db accumulated once, by column block 0
   const f32x4_t wv = *reinterpret_cast<const f32x4_t*>(w + c0);
   if (sub < rpi) {
     const long rend = min(B, r0 + ROWS);
@@ -736,11 +740,11 @@ __global__ void __launch_bounds__(256) fm_skinny_bwd_f32(int ROWS, const float* 
   for (int j = 0; j < 4; ++j) red[threadIdx.x * 4 + j] = (sub < rpi) ? acc[j] : 0.f;
   redb[threadIdx.x] = (sub < rpi && g == 0) ? dbs : 0.f;
   __syncthreads();
-  for (int c = threadIdx.x; c < K; c += 256) {
+  for (int c = threadIdx.x; c < Kc; c += 256) {
     const int gg = c / 4, j = c % 4;
     float t = 0.f;
     for (int q = 0; q < rpi; ++q) t += red[(q * lpr + gg) * 4 + j];
-    atomicAdd(dw + c, t);
+    atomicAdd(dw + cb + c, t);
   }
   if (db && threadIdx.x == 0) {
     float t = 0.f;
@@ -758,13 +762,14 @@ extern "C" void fm_skinny_fwd_f32_launch(const float* x, long ldx, const float* 
                      bias, y, ldy, B, K, act);
 }
 
-// dW (fp32 [K]) and db (fp32 [1]) ACCUMULATE; requires K % 4 == 0, K <= 1024, 16-B aligned rows
+// dW (fp32 [K]) and db (fp32 [1]) ACCUMULATE; requires K % 4 == 0 and 16-B aligned rows
 extern "C" void fm_skinny_bwd_f32_launch(const float* x, long ldx, const float* w, const float* y, long ldy,
                                          const float* dy, long lddy, float* dx, long lddx, int dx_acc, float* dw, float* db,
                                          long B, int K, int act, hipStream_t s) {
   if (B <= 0) return;
   int ROWS = 64;
   while (ROWS > 2 && (B + ROWS - 1) / ROWS < 128) ROWS /= 2;
-  hipLaunchKernelGGL(fm_skinny_bwd_f32, dim3((unsigned)((B + ROWS - 1) / ROWS)), dim3(256), 0, s, ROWS, x, ldx, w, y, ldy,
+  hipLaunchKernelGGL(fm_skinny_bwd_f32, dim3((unsigned)((B + ROWS - 1) / ROWS), (unsigned)((K + 1023) / 1024)), dim3(256), 0,
+                     s, ROWS, x, ldx, w, y, ldy,
                      dy, lddy, dx, lddx, dx_acc, dw, db, B, K, act);
 }

@@ -114,7 +114,8 @@ def test_gemm_f32_fused_backward_epilogue(gpu):
 
 
 # ---------------------------------------------------------------- skinny / act-bwd / interaction
-@pytest.mark.parametrize("B,K,act,dx_acc", [(8192, 256, 12, False), (256, 64, 11, True), (37, 16, 10, True)])
+@pytest.mark.parametrize("B,K,act,dx_acc", [(8192, 256, 12, False), (256, 64, 11, True), (37, 16, 10, True),
+                                            (512, 4096, 11, False), (300, 1036, 12, True)])
 def test_skinny_f32(gpu, B, K, act, dx_acc):
     from flexmi.ops import _kernels as Kk
     torch.manual_seed(7)

@@ -125,7 +125,7 @@ def test_embedding_small_table_lds_path(gpu, rows, D, bag, i64):
 
 
 @pytest.mark.parametrize("B,K,act,dx_acc", [(8192, 256, 12, False), (256, 64, 11, True), (1000, 128, 10, False),
-                                            (37, 16, 12, True)])
+                                            (37, 16, 12, True), (512, 4096, 11, False), (300, 2056, 12, True)])
 def test_skinny_layer_backward(gpu, B, K, act, dx_acc):
     """out_features == 1 layer backward (DLRM click layer): d = act'(y) * dy, dX = d w, dW += x^T d,
     db += sum d -- rows processed four at a time with their loads issued first."""
