@@ -75,15 +75,25 @@ void fm_col2im(const void* dcol, void* dx, int N, int C, int H, int W, int R, in
                int pl, int ldcol, int acc, int bf16, hipStream_t st);
 void fm_transpose_batched(const void* in, const void* yin, void* out, int N, int A, int B, int act, int mode, int bf16,
                           hipStream_t st);
-void fm_pool_fwd(const void* x, void* y, int N, int C, int H, int W, int P, int Q, int kh, int kw, int sh, int sw, int pt,
-                 int pl, int is_max, int act, int bf16, hipStream_t st);
-void fm_pool_bwd(const void* x, const void* y, const void* dy, void* dx, int N, int C, int H, int W, int P, int Q, int kh,
-                 int kw, int sh, int sw, int pt, int pl, int is_max, int act, int acc, int bf16, hipStream_t st);
+void fm_pool_fwd(const void* x, void* y, unsigned char* code, int N, int C, int H, int W, int P, int Q, int kh, int kw, int sh,
+                 int sw, int pt, int pl, int is_max, int act, int bf16, hipStream_t st);
+void fm_pool_bwd(const void* x, const void* y, const void* dy, void* dx, unsigned char* code, int code_ready, int N, int C,
+                 int H, int W, int P, int Q, int kh, int kw, int sh, int sw, int pt, int pl, int is_max, int act, int acc,
+                 int bf16, hipStream_t st);
 void fm_bn_fwd(const void* x, void* y, const float* gamma, const float* beta, float* stats, float* meaninv, int N, int C,
                int HW, float eps, int relu, int bf16, hipStream_t st);
 void fm_bn_bwd(const void* x, const void* y, const void* dy, const float* meaninv, const float* gamma, float* gsum,
                float* dgamma, float* dbeta, void* dx, int N, int C, int HW, int relu, int acc, int bf16, hipStream_t st);
 void fm_compact_rows(const float* src, float* dst, int K, int n, int ldp, int acc, hipStream_t st);
+int fm_conv_lda(int cols);
+int fm_conv_fwd(const void* x, const void* w, void* wpad, const float* bias, void* y, int bf16, int N, int C, int H, int W,
+                int K, int R, int S, int P, int Q, int sh, int sw, int pt, int pl, int act, hipStream_t s);
+int fm_conv_dgrad(const void* g, const void* w, void* wt, void* dx, int accum, int bf16, int N, int C, int H, int W, int K,
+                  int R, int S, int P, int Q, int sh, int sw, int pt, int pl, hipStream_t s);
+int fm_conv_wgrad(const void* g, const void* x, float* dw, int bf16, int N, int C, int H, int W, int K, int R, int S, int P,
+                  int Q, int sh, int sw, int pt, int pl, hipStream_t s);
+void fm_conv_act_bwd(const void* dy, const void* y, void* g, float* db, int bf16, int N, int K, int PQ, int act,
+                     hipStream_t s);
 void fm_pad_rows(const void* src, void* dst, int K, int n, int ldp, int bf16, hipStream_t st);
 void fm_lstm_init(const void* h0, const void* c0, void* hprev, long ldhp, float* cinit, int B, int H, int bf16, hipStream_t s);
 void fm_lstm_cell_fwd(float* G, long ldg, const float* c_prev, long ldcp, float* c_out, long ldc, void* y, long ldy,
@@ -182,14 +192,14 @@ void skinny_bwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, torch::Tensor
   if (x.scalar_type() == torch::kFloat32) {
     TORCH_CHECK(w.scalar_type() == torch::kFloat32 && y.scalar_type() == torch::kFloat32 && dy.scalar_type() == torch::kFloat32,
                 "skinny_bwd: fp32 operands");
-    TORCH_CHECK(x.size(1) % 4 == 0 && x.size(1) <= 1024 && x.stride(0) % 4 == 0 && lddx % 4 == 0,
-                "skinny_bwd fp32: K % 4 == 0, K <= 1024");
+    TORCH_CHECK(x.size(1) % 4 == 0 && x.stride(0) % 4 == 0 && lddx % 4 == 0,
+                "skinny_bwd fp32: K % 4 == 0");
     fm_skinny_bwd_f32_launch(x.data_ptr<float>(), x.stride(0), w.data_ptr<float>(), y.data_ptr<float>(), y.stride(0),
                              dy.data_ptr<float>(), dy.stride(0), (float*)mptr(dx), lddx, dx_acc ? 1 : 0, dw.data_ptr<float>(),
                              (float*)mptr(db), x.size(0), (int)x.size(1), (int)act, cur());
     return;
   }
-  TORCH_CHECK(x.size(1) % 8 == 0 && x.size(1) <= 2048 && x.stride(0) % 8 == 0, "skinny_bwd: K % 8 == 0, K <= 2048");
+  TORCH_CHECK(x.size(1) % 8 == 0 && x.stride(0) % 8 == 0, "skinny_bwd: K % 8 == 0");
   fm_skinny_bwd(x.data_ptr(), x.stride(0), w.data_ptr(), y.data_ptr(), y.stride(0), dy.data_ptr(), dy.stride(0), mptr(dx), lddx,
                 dx_acc ? 1 : 0, dw.data_ptr<float>(), (float*)mptr(db), x.size(0), (int)x.size(1), (int)act, cur());
 }
@@ -482,16 +492,98 @@ void transpose_batched(torch::Tensor in, c10::optional<torch::Tensor> yin, torch
   TORCH_CHECK(mode == 0 || (yin.has_value() && yin->numel() >= N * A * B), "transpose_batched: mode 1 needs yin");
   fm_transpose_batched(in.data_ptr(), cptr(yin), out.data_ptr(), N, A, B, act, mode, is_bf16(out), cur());
 }
-void pool_fwd(torch::Tensor x, torch::Tensor y, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t pt, int64_t pl,
-              bool is_max, int64_t act) {
+// implicit-GEMM convolution (csrc/kernels/conv_igemm.hip): x [N,C,H,W], w [K,C,R,S], y [N,K,P,Q]
+static void conv_chk(const torch::Tensor& x, const torch::Tensor& w, const torch::Tensor& y, const char* n) {
+  chk4(x, n);
+  chk4(w, n);
+  chk4(y, n);
+  same_dt(x, w, n);
+  same_dt(x, y, n);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && y.dim() == 4 && w.size(1) == x.size(1) && y.size(1) == w.size(0) &&
+                  y.size(0) == x.size(0), n, ": x [N,C,H,W], w [K,C,R,S], y [N,K,P,Q]");
+  const long lim = (1L << 31) - 64;
+  TORCH_CHECK(x.numel() * x.element_size() < lim && y.numel() * y.element_size() < lim &&
+                  w.numel() * w.element_size() < lim, n, ": every operand must stay under 2 GiB (32-bit buffer offsets)");
+  TORCH_CHECK(((uintptr_t)x.data_ptr() & 15) == 0 && ((uintptr_t)w.data_ptr() & 15) == 0 && ((uintptr_t)y.data_ptr() & 15) == 0,
+              n, ": 16-B aligned operands");
+}
+#define CONV_GEOM(x, w, y) (int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)w.size(0), (int)w.size(2), \
+                           (int)w.size(3), (int)y.size(2), (int)y.size(3)
+int64_t conv_scratch(int64_t rows, int64_t cols) { return rows * fm_conv_lda((int)cols); }
+void conv_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor wpad, c10::optional<torch::Tensor> bias, torch::Tensor y,
+              int64_t sh, int64_t sw, int64_t pt, int64_t pl, int64_t act) {
+  conv_chk(x, w, y, "conv_fwd");
+  chk4(wpad, "conv_fwd wpad");
+  same_dt(w, wpad, "conv_fwd");
+  TORCH_CHECK(wpad.numel() >= conv_scratch(w.size(0), w.size(1) * w.size(2) * w.size(3)) &&
+                  ((uintptr_t)wpad.data_ptr() & 15) == 0, "conv_fwd: wpad scratch too small");
+  const float* b = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == torch::kFloat32 && bias->numel() == w.size(0), "conv_fwd: fp32 bias[K]");
+    b = bias->data_ptr<float>();
+  }
+  fm_conv_fwd(x.data_ptr(), w.data_ptr(), wpad.data_ptr(), b, y.data_ptr(), is_bf16(x), CONV_GEOM(x, w, y), sh, sw, pt, pl, act, cur());
+}
+void conv_dgrad(torch::Tensor g, torch::Tensor w, torch::Tensor wt, torch::Tensor dx, int64_t sh, int64_t sw, int64_t pt,
+                int64_t pl, bool acc) {
+  conv_chk(dx, w, g, "conv_dgrad");
+  chk4(wt, "conv_dgrad wt");
+  same_dt(w, wt, "conv_dgrad");
+  TORCH_CHECK(wt.numel() >= conv_scratch(w.size(1), w.size(0) * w.size(2) * w.size(3)) && ((uintptr_t)wt.data_ptr() & 15) == 0,
+              "conv_dgrad: wt scratch too small");
+  fm_conv_dgrad(g.data_ptr(), w.data_ptr(), wt.data_ptr(), dx.data_ptr(), acc ? 1 : 0, is_bf16(g), CONV_GEOM(dx, w, g), sh, sw,
+                pt, pl, cur());
+}
+void conv_wgrad(torch::Tensor g, torch::Tensor x, torch::Tensor dw, int64_t R, int64_t S, int64_t sh, int64_t sw, int64_t pt,
+                int64_t pl) {
+  check_cuda(dw, "dw");
+  TORCH_CHECK(dw.scalar_type() == torch::kFloat32 && dw.is_contiguous() && dw.numel() == g.size(1) * x.size(1) * R * S,
+              "conv_wgrad: contiguous fp32 dw[K*C*R*S]");
+  chk4(g, "conv_wgrad g");
+  chk4(x, "conv_wgrad x");
+  same_dt(g, x, "conv_wgrad");
+  TORCH_CHECK(g.dim() == 4 && x.dim() == 4 && g.size(0) == x.size(0), "conv_wgrad: g [N,K,P,Q], x [N,C,H,W]");
+  TORCH_CHECK(x.numel() * x.element_size() < (1L << 31) - 64 && g.numel() * g.element_size() < (1L << 31) - 64,
+              "conv_wgrad: operands under 2 GiB");
+  fm_conv_wgrad(g.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), is_bf16(x), (int)x.size(0), (int)x.size(1), (int)x.size(2),
+                (int)x.size(3), (int)g.size(1), (int)R, (int)S, (int)g.size(2), (int)g.size(3), sh, sw, pt, pl, cur());
+}
+void conv_act_bwd(torch::Tensor dy, torch::Tensor y, torch::Tensor g, c10::optional<torch::Tensor> db, int64_t act) {
+  chk4(dy, "dy");
+  chk4(y, "y");
+  chk4(g, "g");
+  same_dt(dy, y, "conv_act_bwd");
+  same_dt(dy, g, "conv_act_bwd");
+  TORCH_CHECK(dy.dim() == 4 && y.sizes() == dy.sizes() && g.sizes() == dy.sizes(), "conv_act_bwd: [N,K,P,Q]");
+  float* dbp = nullptr;
+  if (db.has_value() && db->defined()) {
+    TORCH_CHECK(db->scalar_type() == torch::kFloat32 && db->numel() == dy.size(1), "conv_act_bwd: fp32 db[K]");
+    dbp = db->data_ptr<float>();
+  }
+  fm_conv_act_bwd(dy.data_ptr(), y.data_ptr(), g.data_ptr(), dbp, is_bf16(dy), (int)dy.size(0), (int)dy.size(1),
+                  (int)(dy.size(2) * dy.size(3)), (int)act, cur());
+}
+static unsigned char* code_ptr(const c10::optional<torch::Tensor>& code, const torch::Tensor& y, const char* n) {
+  if (!code.has_value() || !code->defined()) return nullptr;
+  check_cuda(*code, n);
+  TORCH_CHECK(code->scalar_type() == torch::kUInt8 && code->numel() >= y.numel(), n, ": uint8 code[y.numel()]");
+  return code->data_ptr<uint8_t>();
+}
+// code (max pooling, optional): per-window argmax bytes for the backward pass
+void pool_fwd(torch::Tensor x, torch::Tensor y, c10::optional<torch::Tensor> code, int64_t kh, int64_t kw, int64_t sh,
+              int64_t sw, int64_t pt, int64_t pl, bool is_max, int64_t act) {
   chk4(x, "x");
   chk4(y, "y");
   same_dt(x, y, "pool_fwd");
-  fm_pool_fwd(x.data_ptr(), y.data_ptr(), x.size(0), x.size(1), x.size(2), x.size(3), y.size(2), y.size(3), kh, kw, sh, sw,
-              pt, pl, is_max, act, is_bf16(x), cur());
+  TORCH_CHECK(kh * kw < 255 && x.numel() < (1L << 31) && y.numel() < (1L << 31), "pool_fwd: window < 255, 32-bit indexing");
+  fm_pool_fwd(x.data_ptr(), y.data_ptr(), code_ptr(code, y, "pool_fwd"), x.size(0), x.size(1), x.size(2), x.size(3),
+              y.size(2), y.size(3), kh, kw, sh, sw, pt, pl, is_max, act, is_bf16(x), cur());
 }
-void pool_bwd(torch::Tensor x, torch::Tensor y, torch::Tensor dy, torch::Tensor dx, int64_t kh, int64_t kw, int64_t sh,
-              int64_t sw, int64_t pt, int64_t pl, bool is_max, int64_t act, bool acc) {
+// code: uint8 scratch of y.numel() bytes (max pooling's per-window argmax); code_ready: the
+// forward already filled it
+void pool_bwd(torch::Tensor x, torch::Tensor y, torch::Tensor dy, torch::Tensor dx, torch::Tensor code, bool code_ready,
+              int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t pt, int64_t pl, bool is_max, int64_t act, bool acc) {
+  TORCH_CHECK(kh * kw < 255 && x.numel() < (1L << 31), "pool_bwd: window < 255 elements, 32-bit indexing");
   chk4(x, "x");
   chk4(y, "y");
   chk4(dy, "dy");
@@ -499,8 +591,10 @@ void pool_bwd(torch::Tensor x, torch::Tensor y, torch::Tensor dy, torch::Tensor 
   same_dt(x, y, "pool_bwd");
   same_dt(x, dy, "pool_bwd");
   same_dt(x, dx, "pool_bwd");
-  fm_pool_bwd(x.data_ptr(), y.data_ptr(), dy.data_ptr(), dx.data_ptr(), x.size(0), x.size(1), x.size(2), x.size(3),
-              y.size(2), y.size(3), kh, kw, sh, sw, pt, pl, is_max, act, acc, is_bf16(x), cur());
+  unsigned char* c = code_ptr(code, y, "pool_bwd");
+  TORCH_CHECK(c != nullptr, "pool_bwd: code scratch required");
+  fm_pool_bwd(x.data_ptr(), y.data_ptr(), dy.data_ptr(), dx.data_ptr(), c, code_ready ? 1 : 0, x.size(0), x.size(1),
+              x.size(2), x.size(3), y.size(2), y.size(3), kh, kw, sh, sw, pt, pl, is_max, act, acc, is_bf16(x), cur());
 }
 void bn_fwd(torch::Tensor x, torch::Tensor y, torch::Tensor gamma, torch::Tensor beta, torch::Tensor stats,
             torch::Tensor meaninv, double eps, bool relu) {
@@ -586,6 +680,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("init_fill", &init_fill);
   m.def("skinny_fwd", &skinny_fwd);
   m.def("skinny_bwd", &skinny_bwd);
+  m.def("conv_scratch", &conv_scratch);
+  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_act_bwd", &conv_act_bwd);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("embedding_fwd_multi", &embedding_fwd_multi, py::arg("W"), py::arg("idx"), py::arg("out"), py::arg("ldo"),

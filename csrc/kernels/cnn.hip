@@ -104,84 +104,99 @@ __global__ void __launch_bounds__(256) fm_transpose_kernel(const T* __restrict__
 }
 
 // ---- pooling ---------------------------------------------------------------------------
+// pooling forward: one thread per output (32-bit index math, magic-number division); max pooling
+// also records the row-major position of the window's FIRST maximum (PyTorch's tie rule) as a byte
+// code r*kw + c (255: empty window) for the backward pass when ``code`` is given
 template <typename T>
 __global__ void __launch_bounds__(256) fm_pool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
-                                                          int N, int C, int H, int W, int P, int Q, int kh, int kw, int sh,
+                                                          unsigned char* __restrict__ code, int total, FastDiv dQ,
+                                                          FastDiv dP, int H, int W, int P, int Q, int kh, int kw, int sh,
                                                           int sw, int pt, int pl, int is_max, int act) {
-  const long total = (long)N * C * P * Q;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int q = (int)(i % Q);
-    long t = i / Q;
-    const int p = (int)(t % P);
-    const long nc = t / P;
-    const T* xp = x + nc * H * W;
-    const int h0 = p * sh - pt, w0 = q * sw - pl;
-    float m = -INFINITY, s = 0.f;
-    int cnt = 0;
-    for (int r = 0; r < kh; ++r) {
-      const int h = h0 + r;
-      if (h < 0 || h >= H) continue;
-      for (int c = 0; c < kw; ++c) {
-        const int w = w0 + c;
-        if (w < 0 || w >= W) continue;
-        const float v = tof(xp[h * W + w]);
-        m = fmaxf(m, v);
-        s += v;
-        ++cnt;
-      }
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int t = fdiv(i, dQ), q = i - t * Q;
+  const int nc = fdiv(t, dP), p = t - nc * P;
+  const T* xp = x + (long)nc * H * W;
+  const int h0 = p * sh - pt, w0 = q * sw - pl;
+  float m = -INFINITY, s = 0.f;
+  int cnt = 0, bc = 255;
+  for (int r = 0; r < kh; ++r) {
+    const int h = h0 + r;
+    if (h < 0 || h >= H) continue;
+    for (int c = 0; c < kw; ++c) {
+      const int w = w0 + c;
+      if (w < 0 || w >= W) continue;
+      const float v = tof(xp[h * W + w]);
+      if (v > m || bc == 255) bc = r * kw + c;
+      m = fmaxf(m, v);
+      s += v;
+      ++cnt;
     }
-    const float o = is_max ? m : (cnt ? s / cnt : 0.f);
-    y[i] = fromf<T>(act_fwd(act, o));
   }
+  const float o = is_max ? m : (cnt ? s / cnt : 0.f);
+  y[i] = fromf<T>(act_fwd(act, o));
+  if (code) code[i] = (unsigned char)bc;
 }
 
+// max pooling backward without a forward-recorded code: the argmax bytes per output window
 template <typename T>
-__global__ void __launch_bounds__(256) fm_pool_bwd_kernel(const T* __restrict__ x, const T* __restrict__ y,
-                                                          const T* __restrict__ dy, T* __restrict__ dx,
-                                                          int N, int C, int H, int W, int P, int Q, int kh, int kw, int sh,
-                                                          int sw, int pt, int pl, int is_max, int act, int acc) {
-  const long total = (long)N * C * H * W;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int w = (int)(i % W);
-    long t = i / W;
-    const int h = (int)(t % H);
-    const long nc = t / H;
-    const T* xp = x + nc * H * W;
-    float g = 0.f;
-    // windows (p, q) containing (h, w): p*sh - pt <= h < p*sh - pt + kh
-    const int pmin = max(0, (h + pt - kh + sh) / sh), pmax = min(P - 1, (h + pt) / sh);
-    const int qmin = max(0, (w + pl - kw + sw) / sw), qmax = min(Q - 1, (w + pl) / sw);
-    for (int p = pmin; p <= pmax; ++p) {
-      const int h0 = p * sh - pt;
-      if (h < h0 || h >= h0 + kh) continue;
-      for (int q = qmin; q <= qmax; ++q) {
-        const int w0 = q * sw - pl;
-        if (w < w0 || w >= w0 + kw) continue;
-        const long o = (nc * P + p) * Q + q;
-        const float go = act_bwd(act, tof(y[o]), tof(dy[o]));
-        if (is_max) {   // gradient goes to the window's first maximum (row-major scan, like PyTorch)
-          float best = -INFINITY;
-          int bh = -1, bw = -1;
-          for (int r = 0; r < kh; ++r) {
-            const int hh = h0 + r;
-            if (hh < 0 || hh >= H) continue;
-            for (int c = 0; c < kw; ++c) {
-              const int ww = w0 + c;
-              if (ww < 0 || ww >= W) continue;
-              const float v = tof(xp[hh * W + ww]);
-              if (v > best) { best = v; bh = hh; bw = ww; }
-            }
-          }
-          if (bh == h && bw == w) g += go;
-        } else {
-          const int hs = max(h0, 0), he = min(h0 + kh, H), ws = max(w0, 0), we = min(w0 + kw, W);
-          g += go / (float)((he - hs) * (we - ws));
-        }
+__global__ void __launch_bounds__(256) fm_pool_argmax_kernel(const T* __restrict__ x, unsigned char* __restrict__ code,
+                                                             int total, int H, int W, int P, int Q, int kh, int kw, int sh,
+                                                             int sw, int pt, int pl) {
+  const int o = blockIdx.x * 256 + threadIdx.x;
+  if (o >= total) return;
+  const int q = o % Q, t = o / Q, p = t % P, nc = t / P;
+  const T* xp = x + (long)nc * H * W;
+  const int h0 = p * sh - pt, w0 = q * sw - pl;
+  float best = -INFINITY;
+  int bc = 255;
+  for (int r = 0; r < kh; ++r) {
+    const int hh = h0 + r;
+    if (hh < 0 || hh >= H) continue;
+    for (int c = 0; c < kw; ++c) {
+      const int ww = w0 + c;
+      if (ww < 0 || ww >= W) continue;
+      const float v = tof(xp[hh * W + ww]);
+      if (v > best || bc == 255) { best = v; bc = r * kw + c; }
+    }
+  }
+  code[o] = (unsigned char)bc;
+}
+
+// pooling backward, per input element (32-bit index math, one thread per element): sum the
+// gradients of the <= ceil(k/s)^2 windows that route to it (max: the window's argmax code is this
+// element; avg: 1 / clipped window size)
+template <typename T>
+__global__ void __launch_bounds__(256) fm_pool_bwd_kernel(const T* __restrict__ y, const T* __restrict__ dy,
+                                                          const unsigned char* __restrict__ code, T* __restrict__ dx,
+                                                          int total, FastDiv dW, FastDiv dH, int H, int W, int P, int Q,
+                                                          int kh, int kw, int sh, int sw, int pt, int pl, int is_max,
+                                                          int act, int acc) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int t = fdiv(i, dW), w = i - t * W;
+  const int nc = fdiv(t, dH), h = t - nc * H;
+  float g = 0.f;
+  // windows (p, q) containing (h, w): p*sh - pt <= h < p*sh - pt + kh
+  const int pmin = max(0, (h + pt - kh + sh) / sh), pmax = min(P - 1, (h + pt) / sh);
+  const int qmin = max(0, (w + pl - kw + sw) / sw), qmax = min(Q - 1, (w + pl) / sw);
+  for (int p = pmin; p <= pmax; ++p) {
+    const int h0 = p * sh - pt;
+    if (h < h0 || h >= h0 + kh) continue;
+    for (int q = qmin; q <= qmax; ++q) {
+      const int w0 = q * sw - pl;
+      if (w < w0 || w >= w0 + kw) continue;
+      const int o = (nc * P + p) * Q + q;
+      if (is_max) {
+        if (code[o] == (unsigned char)((h - h0) * kw + (w - w0))) g += act_bwd(act, tof(y[o]), tof(dy[o]));
+      } else {
+        const int hs = max(h0, 0), he = min(h0 + kh, H), ws = max(w0, 0), we = min(w0 + kw, W);
+        g += act_bwd(act, tof(y[o]), tof(dy[o])) / (float)((he - hs) * (we - ws));
       }
     }
-    if (acc) g += tof(dx[i]);
-    dx[i] = fromf<T>(g);
   }
+  if (acc) g += tof(dx[i]);
+  dx[i] = fromf<T>(g);
 }
 
 // ---- batch norm (training mode, per-channel statistics over N*H*W) -----------------------
@@ -342,21 +357,27 @@ static void fm_transpose_batched_t(const void* in, const void* yin, void* out, i
 }
 
 template <typename T>
-static void fm_pool_fwd_t(const void* x, void* y, int N, int C, int H, int W, int P, int Q, int kh, int kw, int sh, int sw, int pt,
-                 int pl, int is_max, int act, hipStream_t st) {
-  const long total = (long)N * C * P * Q;
+static void fm_pool_fwd_t(const void* x, void* y, unsigned char* code, int N, int C, int H, int W, int P, int Q, int kh, int kw,
+                          int sh, int sw, int pt, int pl, int is_max, int act, hipStream_t st) {
+  const int total = N * C * P * Q;
   if (total <= 0) return;
-  hipLaunchKernelGGL(fm_pool_fwd_kernel<T>, dim3(fm_grid(total)), dim3(256), 0, st, (const T*)x, (T*)y,
-                     N, C, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act);
+  hipLaunchKernelGGL(fm_pool_fwd_kernel<T>, dim3((total + 255) / 256), dim3(256), 0, st, (const T*)x, (T*)y,
+                     is_max ? code : nullptr, total, make_fastdiv(Q), make_fastdiv(P), H, W, P, Q, kh, kw, sh, sw, pt, pl,
+                     is_max, act);
 }
 
+// code: max pooling's argmax bytes -- filled by the forward when code_ready, else recomputed here
 template <typename T>
-static void fm_pool_bwd_t(const void* x, const void* y, const void* dy, void* dx, int N, int C, int H, int W, int P, int Q, int kh,
-                 int kw, int sh, int sw, int pt, int pl, int is_max, int act, int acc, hipStream_t st) {
-  const long total = (long)N * C * H * W;
+static void fm_pool_bwd_t(const void* x, const void* y, const void* dy, void* dx, unsigned char* code, int code_ready, int N,
+                          int C, int H, int W, int P, int Q, int kh, int kw, int sh, int sw, int pt, int pl, int is_max,
+                          int act, int acc, hipStream_t st) {
+  const int total = N * C * H * W, outs = N * C * P * Q;
   if (total <= 0) return;
-  hipLaunchKernelGGL(fm_pool_bwd_kernel<T>, dim3(fm_grid(total)), dim3(256), 0, st, (const T*)x,
-                     (const T*)y, (const T*)dy, (T*)dx, N, C, H, W, P, Q, kh, kw, sh,
+  if (is_max && !code_ready)
+    hipLaunchKernelGGL(fm_pool_argmax_kernel<T>, dim3((outs + 255) / 256), dim3(256), 0, st, (const T*)x, code, outs, H, W,
+                       P, Q, kh, kw, sh, sw, pt, pl);
+  hipLaunchKernelGGL(fm_pool_bwd_kernel<T>, dim3((total + 255) / 256), dim3(256), 0, st, (const T*)y, (const T*)dy,
+                     (const unsigned char*)code, (T*)dx, total, make_fastdiv(W), make_fastdiv(H), H, W, P, Q, kh, kw, sh,
                      sw, pt, pl, is_max, act, acc);
 }
 
@@ -421,13 +442,13 @@ void fm_transpose_batched(const void* in, const void* yin, void* out, int N, int
   if (bf16) fm_transpose_batched_t<unsigned short>(in, yin, out, N, A, B, act, mode, st);
   else fm_transpose_batched_t<float>(in, yin, out, N, A, B, act, mode, st);
 }
-void fm_pool_fwd(const void* x, void* y, int N, int C, int H, int W, int P, int Q, int kh, int kw, int sh, int sw, int pt, int pl, int is_max, int act, int bf16, hipStream_t st) {
-  if (bf16) fm_pool_fwd_t<unsigned short>(x, y, N, C, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, st);
-  else fm_pool_fwd_t<float>(x, y, N, C, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, st);
+void fm_pool_fwd(const void* x, void* y, unsigned char* code, int N, int C, int H, int W, int P, int Q, int kh, int kw, int sh, int sw, int pt, int pl, int is_max, int act, int bf16, hipStream_t st) {
+  if (bf16) fm_pool_fwd_t<unsigned short>(x, y, code, N, C, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, st);
+  else fm_pool_fwd_t<float>(x, y, code, N, C, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, st);
 }
-void fm_pool_bwd(const void* x, const void* y, const void* dy, void* dx, int N, int C, int H, int W, int P, int Q, int kh, int kw, int sh, int sw, int pt, int pl, int is_max, int act, int acc, int bf16, hipStream_t st) {
-  if (bf16) fm_pool_bwd_t<unsigned short>(x, y, dy, dx, N, C, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, acc, st);
-  else fm_pool_bwd_t<float>(x, y, dy, dx, N, C, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, acc, st);
+void fm_pool_bwd(const void* x, const void* y, const void* dy, void* dx, unsigned char* code, int code_ready, int N, int C, int H, int W, int P, int Q, int kh, int kw, int sh, int sw, int pt, int pl, int is_max, int act, int acc, int bf16, hipStream_t st) {
+  if (bf16) fm_pool_bwd_t<unsigned short>(x, y, dy, dx, code, code_ready, N, C, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, acc, st);
+  else fm_pool_bwd_t<float>(x, y, dy, dx, code, code_ready, N, C, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, acc, st);
 }
 void fm_bn_fwd(const void* x, void* y, const float* gamma, const float* beta, float* stats, float* meaninv, int N, int C, int HW, float eps, int relu, int bf16, hipStream_t st) {
   if (bf16) fm_bn_fwd_t<unsigned short>(x, y, gamma, beta, stats, meaninv, N, C, HW, eps, relu, st);

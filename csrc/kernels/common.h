@@ -78,6 +78,22 @@ FM_DEVICE float act_bwd(int act, float y, float dy) {
   return dy;
 }
 
+// n / d for 0 <= n < 2^31 by multiply-high (round-up magic; d >= 1): built on the host, passed
+// by value in kernel arguments
+struct FastDiv {
+  unsigned m;
+  int l;
+};
+static inline FastDiv make_fastdiv(int d) {
+  FastDiv f;
+  int l = 0;
+  while ((1L << l) < d) ++l;
+  f.l = l;
+  f.m = (unsigned)((((1UL << 32) * ((1UL << l) - (unsigned long)d)) / (unsigned long)d) + 1);
+  return f;
+}
+FM_DEVICE int fdiv(int n, FastDiv f) { return (int)((__umulhi((unsigned)n, f.m) + (unsigned)n) >> f.l); }
+
 FM_DEVICE float wave_reduce_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -3,7 +3,7 @@
 On a GPU run the extension MUST be present: every call goes through :func:`C` which raises if
 ``flexmi._C`` cannot be imported -- there is no silent eager fallback for the hot ops (GEMM,
 embedding, interaction, optimizer, loss, element-wise, data movement, and the CNN ops: GEMM
-convolution = HIP im2col/col2im/transposes + the MFMA GEMM, HIP pooling and batch norm).
+convolution = implicit-GEMM MFMA kernels on NCHW, HIP pooling and batch norm).
 :data:`LIBRARY_FALLBACK` lists ops routed to vendor libraries instead (none).
 """
 from __future__ import annotations
@@ -107,7 +107,8 @@ def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=F
     below in this layer's dX GEMM epilogue."""
     M, K = x2.shape
     N = w.shape[0]
-    if N == 1:
+    vec = 4 if x2.dtype == torch.float32 else 8
+    if N == 1 and K % vec == 0 and x2.stride(0) % vec == 0 and (dx2 is None or dx2.stride(0) % vec == 0):
         if phase == "dw":          # the skinny kernel did dX, dW and db together in the "dx" phase
             return
         C().skinny_bwd(x2, w, y2, dy2, dx2, bool(dx_acc), dw, None if grad_is_dpre else db,
@@ -363,68 +364,55 @@ def scratch(device, name, numel, dtype=torch.bfloat16):
     return t[:numel]
 
 
-def _conv_geom(x, w, y):
-    N, Cin, H, W = x.shape
-    Kout, Cg, R, S = w.shape
-    P, Q = y.shape[2], y.shape[3]
-    CRS = Cg * R * S
-    ldc = (CRS + 7) // 8 * 8
-    return N, Cin, H, W, Kout, Cg, R, S, P, Q, CRS, ldc
-
-
-def _conv_weight_matrix(w, Kout, CRS, ldc):
-    if ldc == CRS:
-        return w.reshape(Kout, CRS)
-    wp = scratch(w.device, "conv_wpad", Kout * ldc, w.dtype)
-    C().pad_rows(w.contiguous(), wp, Kout, CRS, ldc)
-    return wp
-
-
 def conv2d_forward(x, w, b, y, stride, pads, act, groups):
-    """GEMM convolution on MFMA: im2col (HIP) -> out[NPQ,K] = col . W^T (+bias, act epilogue)
-    -> NHWC->NCHW tiled transpose (HIP).  pads = (top, bottom, left, right) of this shard."""
+    """Implicit-GEMM convolution on MFMA straight from NCHW (csrc/kernels/conv_igemm.hip): the
+    image operand is gathered into LDS per tile, bias + activation fused into the NCHW store.
+    pads = (top, bottom, left, right) of this shard (bottom / right are implied by y's extent)."""
     assert groups == 1, "grouped convolution is not supported on the HIP path"
-    N, Cin, H, W, Kout, Cg, R, S, P, Q, CRS, ldc = _conv_geom(x, w, y)
-    NPQ = N * P * Q
-    col = scratch(x.device, "conv_col", NPQ * ldc, x.dtype)
-    C().im2col(x, col, R, S, P, Q, stride[0], stride[1], pads[0], pads[2], ldc)
-    wm = _conv_weight_matrix(w, Kout, CRS, ldc)
-    out = scratch(x.device, "conv_nhwc", NPQ * Kout, x.dtype)
-    gemm(col, ldc, True, wm, ldc, True, out, Kout, NPQ, Kout, ldc, bias=b, act=act)
-    C().transpose_batched(out, None, y, N, P * Q, Kout, 10, 0)
+    Kout, Cg, R, S = w.shape
+    wpad = scratch(x.device, "conv_wpad", C().conv_scratch(Kout, Cg * R * S), w.dtype)
+    C().conv_fwd(x, w.contiguous(), wpad, b, y, stride[0], stride[1], pads[0], pads[2], int(act))
 
 
 def conv2d_backward(x, w, y, dy, dx, dw, db, stride, pads, act, groups, acc):
-    """g = act'(y)*dy transposed to NHWC (one fused HIP pass); dW = g^T.col with db from the
-    same GEMM's A-tile row sums; dX = col2im(g . W)."""
+    """G = act'(y) * dY with db = sum G (one pass; skipped for a linear conv without bias), then
+    dW += G (x) X and dX (+)= Wt (x) G as implicit GEMMs -- no columns, no transposes."""
     assert groups == 1, "grouped convolution is not supported on the HIP path"
-    N, Cin, H, W, Kout, Cg, R, S, P, Q, CRS, ldc = _conv_geom(x, w, y)
-    NPQ = N * P * Q
-    g = scratch(x.device, "conv_g", NPQ * Kout, x.dtype)
-    C().transpose_batched(dy, y, g, N, Kout, P * Q, act, 1)
-    col = scratch(x.device, "conv_col", NPQ * ldc, x.dtype)
-    C().im2col(x, col, R, S, P, Q, stride[0], stride[1], pads[0], pads[2], ldc)
+    g = dy
+    if int(act) != 10 or db is not None:
+        g = scratch(x.device, "conv_g", dy.numel(), dy.dtype).view(dy.shape) if int(act) != 10 else dy
+        C().conv_act_bwd(dy, y, g, db, int(act))
+    Kout, Cg, R, S = w.shape
     # dW / db ACCUMULATE into the per-step zeroed gradient buffer (tied weights sum their grads)
-    if ldc == CRS:
-        gemm(g, Kout, False, col, ldc, False, dw.view(Kout, CRS), CRS, Kout, CRS, NPQ, beta=True, rowsum_a=db)
-    else:
-        dwp = scratch(x.device, "conv_dwpad", Kout * ldc, torch.float32)
-        gemm(g, Kout, False, col, ldc, False, dwp, ldc, Kout, ldc, NPQ, rowsum_a=db)
-        C().compact_rows(dwp, dw.view(-1), Kout, CRS, ldc, True)
+    C().conv_wgrad(g, x, dw.view(-1), R, S, stride[0], stride[1], pads[0], pads[2])
     if dx is not None:
-        wm = _conv_weight_matrix(w, Kout, CRS, ldc)
-        dcol = scratch(x.device, "conv_dcol", NPQ * ldc, x.dtype)
-        gemm(g, Kout, True, wm, ldc, False, dcol, ldc, NPQ, ldc, Kout)
-        C().col2im(dcol, dx, R, S, P, Q, stride[0], stride[1], pads[0], pads[2], ldc, bool(acc))
+        wt = scratch(x.device, "conv_wt", C().conv_scratch(Cg, Kout * R * S), w.dtype)
+        C().conv_dgrad(g, w.contiguous(), wt, dx, stride[0], stride[1], pads[0], pads[2], bool(acc))
 
 
-def pool2d_forward(x, y, k, stride, pads, pool_type, act):
-    C().pool_fwd(x, y, k[0], k[1], stride[0], stride[1], pads[0], pads[2], int(pool_type) == 30, int(act))
+def _pool_code(saved, y):
+    c = saved.get("pool_code")
+    if c is None or c.numel() < y.numel() or c.device != y.device:
+        c = torch.empty(y.numel(), dtype=torch.uint8, device=y.device)
+        saved["pool_code"] = c
+    return c
 
 
-def pool2d_backward(x, y, dy, dx, k, stride, pads, pool_type, act, acc):
-    C().pool_bwd(x, y, dy, dx, k[0], k[1], stride[0], stride[1], pads[0], pads[2], int(pool_type) == 30, int(act),
-                 bool(acc))
+def pool2d_forward(x, y, k, stride, pads, pool_type, act, saved=None):
+    """Max pooling also records each window's argmax byte in the op's saved state (for backward)."""
+    is_max = int(pool_type) == 30
+    code = _pool_code(saved, y) if (is_max and saved is not None) else None
+    C().pool_fwd(x, y, code, k[0], k[1], stride[0], stride[1], pads[0], pads[2], is_max, int(act))
+    if saved is not None:
+        saved["pool_code_ready"] = code is not None
+
+
+def pool2d_backward(x, y, dy, dx, k, stride, pads, pool_type, act, acc, saved=None):
+    saved = {} if saved is None else saved
+    ready = bool(saved.get("pool_code_ready", False))
+    code = _pool_code(saved, y)
+    C().pool_bwd(x, y, dy, dx, code, ready, k[0], k[1], stride[0], stride[1], pads[0], pads[2], int(pool_type) == 30,
+                 int(act), bool(acc))
 
 
 def _bn_bufs(saved, C_, device):

@@ -45,6 +45,9 @@ def _local_pads(out_box, in_box, kh, kw, sh, sw, ph, pw):
 
 class _SpatialOp(Op):
     """Shared halo logic for Conv2D / Pool2D."""
+    # the kernels take only the top / left pads and the output extent, so a local input box
+    # larger than the halo box works unchanged (the executor then skips the halo copy)
+    superset_input_ok = True
 
     def splittable_dims(self):
         return {0, 2, 3}
@@ -109,17 +112,18 @@ class Conv2D(_SpatialOp):
                               bool(ctx.in_grad_accumulate[0]) if dx is not None else False)
             return
         g = act_backward_torch(dy.float(), y.float(), self.activation)
-        xp = F.pad(x.float(), (pads[2], pads[3], pads[0], pads[1])).requires_grad_(dx is not None)
+        xl = x.float().detach().requires_grad_(dx is not None)
         w = ctx.wcompute[0].float().detach().requires_grad_(True)
         with torch.enable_grad():
+            # pads may be negative (a local box bigger than the halo box): F.pad crops those sides
+            xp = F.pad(xl, (pads[2], pads[3], pads[0], pads[1]))
             out = F.conv2d(xp, w, None, (self.sh, self.sw), 0, 1, self.groups)
-            grads = torch.autograd.grad(out, [w] + ([xp] if dx is not None else []), g)
+            grads = torch.autograd.grad(out, [w] + ([xl] if dx is not None else []), g)
         dw.add_(grads[0])          # accumulate: the executor zeroes gradients once per step
         if db is not None:
             db.add_(g.sum((0, 2, 3)))
         if dx is not None:
-            gx = grads[1][:, :, pads[0]: pads[0] + x.shape[2], pads[2]: pads[2] + x.shape[3]]
-            store(dx, gx, ctx.in_grad_accumulate[0])
+            store(dx, grads[1], ctx.in_grad_accumulate[0])
 
     def flops(self, i, o):
         n, c, oh, ow = o[0]
@@ -171,7 +175,7 @@ class Pool2D(_SpatialOp):
         pads = self._pads(ctx)
         if ctx.hip:
             K.pool2d_forward(x, y, (self.kh, self.kw), (self.sh, self.sw), pads,
-                             int(self.pool_type), int(self.activation))
+                             int(self.pool_type), int(self.activation), ctx.saved)
             return
         y.copy_(act_forward_torch(self._torch_fwd(x.float(), pads), self.activation))
 
@@ -182,7 +186,7 @@ class Pool2D(_SpatialOp):
         pads = self._pads(ctx)
         if ctx.hip:
             K.pool2d_backward(x, y, dy, dx, (self.kh, self.kw), (self.sh, self.sw), pads,
-                              int(self.pool_type), int(self.activation), ctx.in_grad_accumulate[0])
+                              int(self.pool_type), int(self.activation), ctx.in_grad_accumulate[0], ctx.saved)
             return
         g = act_backward_torch(dy.float(), y.float(), self.activation)
         xx = x.float().detach().requires_grad_(True)

@@ -34,6 +34,21 @@ from .base import Op, OpCtx, store
 from . import _kernels as K
 
 
+
+NATIVE_CPU = os.environ.get("FM_CPU_NATIVE", "1") != "0"
+_CPU_MOD = []
+
+
+def _cpu_ext():
+    """The native CPU kernel module, or None when it was not built."""
+    if not _CPU_MOD:
+        try:
+            from flexmi import _cpu as m
+        except ImportError:
+            m = None
+        _CPU_MOD.append(m)
+    return _CPU_MOD[0]
+
 class Embedding(Op):
     op_type = OperatorType.OP_EMBEDDING
     name_prefix = "Embed"
@@ -112,12 +127,30 @@ class Embedding(Op):
         return False
 
     # ---------------------------------------------------------- compute
+    @staticmethod
+    def _native_cpu(*ts):
+        """flexmi._cpu (csrc/cpu/cpu_ops.cc) when built and the operands fit it: fp32 tables and
+        rows, integer indices; FM_CPU_NATIVE=0 selects the torch reference path instead."""
+        if not NATIVE_CPU:
+            return None
+        m = _cpu_ext()
+        if m is None:
+            return None
+        w, idx, rows = ts
+        if (w.dtype != torch.float32 or rows.dtype != torch.float32 or not w.is_contiguous()
+                or idx.dtype not in (torch.int32, torch.int64) or rows.stride(-1) != 1 or w.device.type != "cpu"):
+            return None
+        return m
+
     def forward(self, ctx: OpCtx):
         idx = ctx.inputs[0]
         w = ctx.weights[0]
         out = ctx.outputs[0]
         if ctx.hip:
             Embedding.forward_group([self], [ctx])
+        elif self._native_cpu(w, idx, out) is not None:
+            scale = 1.0 / idx.shape[1] if self.aggr == AggrMode.AGGR_MODE_AVG else 1.0
+            _cpu_ext().embedding_fwd(w, idx.contiguous(), out, self._row_lo(ctx), scale)
         else:
             bag = idx.shape[1]
             li, ok = self._local_rows(idx, self._row_lo(ctx), w.shape[0])
@@ -132,8 +165,12 @@ class Embedding(Op):
         dy = ctx.out_grads[0]
         if self.sparse_sgd:
             # fused sparse SGD (no dense grad): W[idx] -= lr * dy  (duplicates summed first)
+            scale = 1.0 / idx.shape[1] if self.aggr == AggrMode.AGGR_MODE_AVG else 1.0
             if ctx.hip:
                 Embedding.backward_group([self], [ctx])
+            elif self._native_cpu(ctx.weights[0], idx, dy) is not None:
+                _cpu_ext().embedding_bwd(ctx.weights[0], idx.contiguous(), dy, self._row_lo(ctx),
+                                         -float(ctx.lr) * scale)
             else:
                 g = dy.float()
                 if self.aggr == AggrMode.AGGR_MODE_AVG:
@@ -148,6 +185,9 @@ class Embedding(Op):
         dw = ctx.weight_grads[0]
         if ctx.hip:
             Embedding.backward_group([self], [ctx])
+        elif self._native_cpu(dw, idx, dy) is not None:
+            scale = 1.0 / idx.shape[1] if self.aggr == AggrMode.AGGR_MODE_AVG else 1.0
+            _cpu_ext().embedding_bwd(dw, idx.contiguous(), dy, self._row_lo(ctx), scale)
         else:
             g = dy.float()
             if self.aggr == AggrMode.AGGR_MODE_AVG:

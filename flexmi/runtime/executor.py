@@ -691,6 +691,30 @@ class Executor:
                 self.consumers[t.guid].append((op, i))
                 if t.owner_op is None and t.guid not in self.home:
                     self.home[t.guid] = lay.as_full()  # model input: first consumer's layout
+        # halo consumers (conv / pool) read the producer's buffer in place when every rank's need
+        # box lies inside the box that rank already holds (no cross-rank halo; e.g. a 3x3/2 pool
+        # that never reads the last row): no copy in forward, no zero + accumulate of the input
+        # gradient in backward -- the op derives its pads from the bigger box
+        for op in ops:
+            if not getattr(op, "superset_input_ok", False):
+                continue
+            for i, t in enumerate(op.inputs):
+                need, home = self.need[(op.guid, i)], self.home.get(t.guid)
+                if home is None or need.same_as(home) or need.partial or home.partial or need.shape != home.shape:
+                    continue
+                if need.ranks() != home.ranks():
+                    continue
+                inside = True
+                for r in need.ranks():
+                    if len(need.parts_of(r)) != 1 or len(home.parts_of(r)) != 1:
+                        inside = False
+                        break
+                    nb, hb = need.local_box(r), home.local_box(r)
+                    if any(a0 < b0 or a1 > b1 for (a0, a1), (b0, b1) in zip(nb, hb)):
+                        inside = False
+                        break
+                if inside:
+                    self.need[(op.guid, i)] = home
         self.tensors = {}
         for op in ops:
             for t in op.inputs + op.outputs:

@@ -360,8 +360,9 @@ def test_conv2d_hip(gpu, N, C, H, W, K, R, S, st, pads):
     assert rel_err(dx, gx) < 2e-2
 
 
+@pytest.mark.parametrize("saved", [False, True], ids=["argmax-in-bwd", "argmax-from-fwd"])
 @pytest.mark.parametrize("kind", [30, 31])
-def test_pool2d_hip(gpu, kind):
+def test_pool2d_hip(gpu, kind, saved):
     import torch.nn.functional as F
     from flexmi.ops import _kernels as Kk
     torch.manual_seed(6)
@@ -375,12 +376,13 @@ def test_pool2d_hip(gpu, kind):
         cnt = F.avg_pool2d(F.pad(torch.ones_like(xf[:1, :1]), (1, 1, 1, 1)), k, st, divisor_override=1)
         ref = s_ / cnt
     y = torch.empty(ref.shape, device=gpu, dtype=torch.bfloat16)
-    Kk.pool2d_forward(x, y, k, st, pads, kind, 10)
+    st_ = {} if saved else None
+    Kk.pool2d_forward(x, y, k, st, pads, kind, 10, st_)
     assert rel_err(y, ref) < 1e-2
     dy = torch.randn(ref.shape, device=gpu).bfloat16()
     gx, = torch.autograd.grad(ref, [xf], dy.float())
     dx = torch.empty_like(x)
-    Kk.pool2d_backward(x, y, dy, dx, k, st, pads, kind, 10, False)
+    Kk.pool2d_backward(x, y, dy, dx, k, st, pads, kind, 10, False, st_)
     assert rel_err(dx, gx) < 2e-2
 
 

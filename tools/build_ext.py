@@ -8,7 +8,10 @@
                       simulator + MCMC search, data-loader ring (csrc/runtime/*.cc, g++ -O3,
                       pybind11; no GPU dependency -- usable on the CPU box)
 
-Usage: python tools/build_ext.py [--only C|native] [-j N] [--clean]
+  flexmi/_cpu*.so     native CPU kernels (csrc/cpu/*.cc: embedding bag / gradient / sparse SGD,
+                      AVX2 + ATen thread pool) for the CPU backend and host-placed tables
+
+Usage: python tools/build_ext.py [--only C|rt|cpu|native] [-j N] [--clean]
 """
 from __future__ import annotations
 
@@ -109,6 +112,21 @@ def write_ninja(only=None):
         lines.append(f"  ldflags = -L{tlib} -Wl,-rpath,{tlib} -lc10 -lc10_hip -ltorch -ltorch_cpu -ltorch_hip "
                      f"-ltorch_python -L{ROCM}/lib -Wl,-rpath,{ROCM}/lib -lamdhip64")
         targets.append(out)
+    if only in (None, "cpu"):
+        # native CPU kernels (csrc/cpu/*.cc): torch CPU extension, ATen intra-op thread pool
+        tinc, tlib, abi = _torch_paths()
+        incs = " ".join(f"-I{p}" for p in tinc)
+        objs = []
+        for src in sorted(glob.glob(os.path.join(ROOT, "csrc", "cpu", "*.cc"))):
+            o = os.path.join(BUILD, "cpu_" + os.path.basename(src).replace(".cc", ".o"))
+            lines.append(f"build {o}: cxx {src}")
+            lines.append(f"  extra = -DTORCH_EXTENSION_NAME=_cpu -D_GLIBCXX_USE_CXX11_ABI={abi} {incs} "
+                         f"-Wno-unused-parameter -fopenmp")
+            objs.append(o)
+        out = os.path.join(ROOT, "flexmi", "_cpu" + ext)
+        lines.append(f"build {out}: cxxlink {' '.join(objs)}")
+        lines.append(f"  ldflags = -L{tlib} -Wl,-rpath,{tlib} -lc10 -ltorch -ltorch_cpu -ltorch_python -fopenmp")
+        targets.append(out)
     if only in (None, "native"):
         objs = []
         for src in sorted(glob.glob(os.path.join(ROOT, "csrc", "runtime", "*.cc")) +
@@ -155,7 +173,7 @@ def build(only=None, jobs=None, verbose=False):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", choices=["C", "rt", "native"], default=None)
+    ap.add_argument("--only", choices=["C", "rt", "cpu", "native"], default=None)
     ap.add_argument("-j", type=int, default=None)
     ap.add_argument("-v", action="store_true")
     ap.add_argument("--clean", action="store_true")
