@@ -56,6 +56,7 @@ struct ConvP {
   FastDiv dRS, dS;                     // reduction index (ch, r, s) decomposition
   FastDiv dPer, dQp;                   // wgrad pixel-vector reduction index (n, p, q0)
   FastDiv dSh, dSw;                    // strided dgrad: divisibility by the stride
+  int adv_c, adv_r, adv_s;             // one bf16 k-tile (64) in (ch, r, s) digits
 };
 
 template <typename T> struct TB;
@@ -77,67 +78,68 @@ FM_DEVICE __amdgpu_buffer_rsrc_t make_rsrc(const void* p, long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
 }
 
-// 8 bf16 from source columns [w0, w0+8) of one row of width Ws (row start rowoff, tensor of
-// nel >= 8 elements): elements with column < 0 or >= min(Ws, lim) become 0.  The 16-B load is
-// placed INSIDE the tensor (a load straddling num_records would come back as zeros) -- at the
-// row start for a left overhang, pulled back from the tensor end for a tail -- and px_finish
-// funnel-shifts the elements into place.  Split in two so the load latency overlaps the MFMAs:
-// px_issue starts the load and packs the fix-up into ``meta``.
-FM_DEVICE u32x4_t px_issue(__amdgpu_buffer_rsrc_t rs, bool ok, int rowoff, int w0, int Ws, int lim, int nel,
-                           unsigned& meta) {
-  int cnt = min(8, min(Ws, lim) - w0);                 // elements t < cnt are inside the row
-  ok = ok && w0 > -8 && cnt > 0;
-  const int want = rowoff + w0;                         // tensor position of element t = 0
-  const int L = min(max(want, rowoff), nel - 8);        // where the load actually starts
-  const int delta = want - L;                           // element t = loaded element t + delta
-  const int lowz = (w0 < 0 && delta >= 0) ? -w0 : 0;    // overhang the shift does not clear
-  cnt = ok ? cnt : 0;
-  meta = (unsigned)(delta + 8) | ((unsigned)lowz << 4) | ((unsigned)cnt << 8);
+// Pixel-vector chunks: 8 bf16 of one source row read by ONE 16-B buffer load at the (unaligned)
+// position of element 0; elements outside the valid window [lowz, cnt) -- left halo (read from
+// the previous row), right halo / row tail (read from the next row) -- are cleared with a mask
+// from a 72-entry LDS table (entry lowz * 9 + cnt).  Only a chunk within 8 elements of the
+// tensor's first / last element needs its load moved inside the tensor (a load straddling
+// num_records comes back as zeros) and a funnel shift; that rare divergent branch lives in
+// px_finish.  Split in two so the load latency overlaps the MFMAs: px_issue starts the load and
+// packs the fix-up into ``meta``.
+constexpr int MASK_ENTRIES = 72;
+constexpr int MASK_BYTES = MASK_ENTRIES * 16;
+
+FM_DEVICE void init_mask_table(char* tab, int tid) {
+  if (tid < MASK_ENTRIES) {
+    const int lowz = tid / 9, cnt = tid % 9;
+    u32x4_t m;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool a = lowz <= 2 * j && 2 * j < cnt, b = lowz <= 2 * j + 1 && 2 * j + 1 < cnt;
+      m[j] = (a ? 0x0000FFFFu : 0u) | (b ? 0xFFFF0000u : 0u);
+    }
+    *reinterpret_cast<u32x4_t*>(tab + tid * 16) = m;
+  }
+}
+
+// want: tensor position of element 0; w0: its source column (< 0: left halo); inside: elements
+// t < inside lie inside the row / window
+FM_DEVICE u32x4_t px_issue(__amdgpu_buffer_rsrc_t rs, bool ok, int want, int w0, int inside, int nel, unsigned& meta) {
+  const int cnt = min(8, inside), lowz = max(0, -w0);
+  ok = ok && cnt > lowz;
+  const int L = min(max(want, 0), nel - 8);             // the load stays inside the tensor
+  const int delta = want - L;                           // 0 except within 8 elements of its ends
+  meta = ok ? (unsigned)(lowz * 9 + cnt) | ((unsigned)(delta + 8) << 8) : (8u << 8);
   return ldb16(rs, ok ? (unsigned)L * 2u : OOB);
 }
 
-FM_DEVICE u32x4_t px_finish(u32x4_t v, unsigned meta) {
-  const int delta = (int)(meta & 15) - 8, lowz = (meta >> 4) & 15, cnt = (meta >> 8) & 15;
-  unsigned long lo = (unsigned long)v[0] | ((unsigned long)v[1] << 32);
-  unsigned long hi = (unsigned long)v[2] | ((unsigned long)v[3] << 32);
-  if (delta < 0) {                                      // left overhang: shift up, zeros enter below
-    const int b = -16 * delta;
-    if (b >= 64) {
-      hi = lo << (b - 64);
-      lo = 0;
+FM_DEVICE u32x4_t px_finish(u32x4_t v, unsigned meta, const char* tab) {
+  const int delta = (int)((meta >> 8) & 15) - 8;
+  if (delta != 0) {                                     // rare: shift the moved load into place
+    unsigned long lo = (unsigned long)v[0] | ((unsigned long)v[1] << 32);
+    unsigned long hi = (unsigned long)v[2] | ((unsigned long)v[3] << 32);
+    if (delta < 0) {
+      const int b = -16 * delta;
+      if (b >= 64) {
+        hi = lo << (b - 64);
+        lo = 0;
+      } else {
+        hi = (hi << b) | (lo >> (64 - b));
+        lo <<= b;
+      }
     } else {
-      hi = (hi << b) | (lo >> (64 - b));
-      lo <<= b;
+      const int b = 16 * delta;
+      if (b >= 64) {
+        lo = hi >> (b - 64);
+        hi = 0;
+      } else {
+        lo = (lo >> b) | (hi << (64 - b));
+        hi >>= b;
+      }
     }
-  } else if (delta > 0) {                               // load pulled back from the tensor end
-    const int b = 16 * delta;
-    if (b >= 64) {
-      lo = hi >> (b - 64);
-      hi = 0;
-    } else {
-      lo = (lo >> b) | (hi << (64 - b));
-      hi >>= b;
-    }
+    v = u32x4_t{(unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32)};
   }
-  if (lowz) {                                           // overhang on a pulled-back load
-    const int b = 16 * lowz;
-    if (b >= 64) {
-      hi &= ~((1UL << (b - 64)) - 1);
-      lo = 0;
-    } else {
-      lo &= ~((1UL << b) - 1);
-    }
-  }
-  const int keep = 16 * cnt;
-  if (keep < 128) {
-    if (keep <= 64) {
-      lo = keep == 64 ? lo : (lo & ((1UL << keep) - 1));
-      hi = 0;
-    } else {
-      hi &= (1UL << (keep - 64)) - 1;
-    }
-  }
-  return u32x4_t{(unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32)};
+  return v & *reinterpret_cast<const u32x4_t*>(tab + (meta & 127) * 16);
 }
 
 // One operand tile (R rows x 128 B of reduction index) gathered into registers, then LDS.
@@ -162,20 +164,36 @@ struct Gather {
   int base;       // role-specific element offset of the row
   int hb, wb;     // role-specific spatial coordinates of the row
   int rr, ss;     // rows (c, r, s): the row's (r, s)
+  // role 5: per chunk, the reduction index (ch, r, s) of its k-row as ch * Hs * Ws, r, r * Ws, s,
+  // advanced by 64 (one k-tile) with carries -- no divisions or multiplies in the main loop
+  int cho[ROLE == 5 ? PER_T : 1], r5[ROLE == 5 ? PER_T : 1], rw5[ROLE == 5 ? PER_T : 1], s5[ROLE == 5 ? PER_T : 1];
 
-  FM_DEVICE void init(const ConvP& p, int row0, int nrows, int tid) {
+  FM_DEVICE void init(const ConvP& p, int row0, int nrows, int tid, int kt0) {
     const int HW = p.H * p.W, PQ = p.P * p.Q;
     if constexpr (ROLE == 5) {
       // this thread's pixel chunk: 8 columns (tid % 16) of the 128-column tile, fixed for the block
+      const bool fwd = MODE == CONV_FWD;
+      const int Cs = fwd ? p.C : p.K, Hs = fwd ? p.H : p.P, Ws = fwd ? p.W : p.Q;
       row = row0 + 8 * (tid & 15);
       rowok = row < nrows;
       const int rw = rowok ? row : 0;
-      const int Po = MODE == CONV_FWD ? p.P : p.H;
+      const int Po = fwd ? p.P : p.H;
       const int per = Po * p.Qp;
       const int n = rw / per, rem = rw - n * per;
-      hb = rem / p.Qp;                  // output row
-      wb = rem - hb * p.Qp;             // first output column of the chunk
-      base = n;                         // image
+      const int orow = rem / p.Qp;                        // output row
+      wb = rem - orow * p.Qp;                             // first output column of the chunk
+      hb = fwd ? orow - p.pt : orow + p.pt;               // source row = hb +/- r
+      wb = fwd ? wb - p.pl : wb + p.pl;                   // source column = wb +/- s
+      base = n * Cs * Hs * Ws + hb * Ws + wb;             // + ch*Hs*Ws +/- r*Ws +/- s
+#pragma unroll
+      for (int i = 0; i < PER_T; ++i) {
+        const int k = kt0 * 64 + (tid >> 4) + 16 * i;
+        const int ch = k / (p.R * p.S), rsi = k - ch * p.R * p.S;
+        r5[i] = rsi / p.S;
+        s5[i] = rsi - r5[i] * p.S;
+        cho[i] = ch * Hs * Ws;
+        rw5[i] = r5[i] * Ws;
+      }
       return;
     }
     row = row0 + tid % R;
@@ -206,10 +224,10 @@ struct Gather {
 
   // finish the chunks issued by load(): pixel fix-up shifts / element packing (after the MFMAs
   // of the current tile, so the loads' latency is hidden behind them)
-  FM_DEVICE void finish() {
+  FM_DEVICE void finish(const char* tab) {
     if constexpr (PIX) {
 #pragma unroll
-      for (int i = 0; i < PER_T; ++i) v[i] = px_finish(v[i], meta[i]);
+      for (int i = 0; i < PER_T; ++i) v[i] = px_finish(v[i], meta[i], tab);
     } else if constexpr (ELT) {
       if (vec_done) return;
 #pragma unroll
@@ -227,17 +245,27 @@ struct Gather {
   // issue this thread's loads of k-tile kt (results land in v / e, completed by finish())
   FM_DEVICE void load(const ConvP& p, __amdgpu_buffer_rsrc_t rs, int kt, int tid) {
     if constexpr (ROLE == 5) {
-      // k-row (tid >> 4) + 16 i of the 64-row k-tile, per lane: (ch, r, s) -> source row / column
+      // k-row (tid >> 4) + 16 i of the 64-row k-tile; source position base + ch*Hs*Ws +/- r*Ws +/- s
       const bool fwd = MODE == CONV_FWD;
-      const int Cs = fwd ? p.C : p.K, Hs = fwd ? p.H : p.P, Ws = fwd ? p.W : p.Q;
+      const int Hs = fwd ? p.H : p.P, Ws = fwd ? p.W : p.Q;
+      const int kb = kt * 64 + (tid >> 4);
 #pragma unroll
       for (int i = 0; i < PER_T; ++i) {
-        const int k = kt * 64 + (tid >> 4) + 16 * i;
-        const int ch = fdiv(k, p.dRS), rsi = k - ch * p.R * p.S, r = fdiv(rsi, p.dS), s = rsi - r * p.S;
-        const int hs = fwd ? hb + r - p.pt : hb + p.pt - r;
-        const int w0 = fwd ? wb + s - p.pl : wb + p.pl - s;
-        const bool ok = rowok && k < p.Kred && (unsigned)hs < (unsigned)Hs;
-        v[i] = px_issue(rs, ok, ((base * Cs + ch) * Hs + hs) * Ws, w0, Ws, 0x7fffffff, p.b_nel, meta[i]);
+        const int hs = fwd ? hb + r5[i] : hb - r5[i];
+        const int w0 = fwd ? wb + s5[i] : wb - s5[i];
+        const bool ok = rowok && kb + 16 * i < p.Kred && (unsigned)hs < (unsigned)Hs;
+        const int want = fwd ? base + cho[i] + rw5[i] + s5[i] : base + cho[i] - rw5[i] - s5[i];
+        v[i] = px_issue(rs, ok, want, w0, Ws - w0, p.b_nel, meta[i]);
+        // advance (ch, r, s) by one k-tile (64 = adv_c*RS + adv_r*S + adv_s)
+        s5[i] += p.adv_s;
+        const bool c1 = s5[i] >= p.S;
+        s5[i] -= c1 ? p.S : 0;
+        r5[i] += p.adv_r + (c1 ? 1 : 0);
+        rw5[i] += p.adv_r * Ws + (c1 ? Ws : 0);
+        const bool c2 = r5[i] >= p.R;
+        r5[i] -= c2 ? p.R : 0;
+        rw5[i] -= c2 ? p.R * Ws : 0;
+        cho[i] += (p.adv_c + (c2 ? 1 : 0)) * Hs * Ws;
       }
       return;
     }
@@ -252,12 +280,12 @@ struct Gather {
         // k = (n, p, q < Qp): 8 consecutive q of one output row
         const int n = fdiv(kb, p.dPer), rem = kb - n * (p.P * p.Qp), pp = fdiv(rem, p.dQp), q0 = rem - pp * p.Qp;
         const bool okk = rowok && kb < p.Kred;
-        if constexpr (ROLE == 6) {
-          v[i] = px_issue(rs, okk, ((n * p.K) * p.P + pp) * p.Q + base, q0, p.Q, p.Q, p.a_nel, meta[i]);
-        } else {
-          const int hs = pp + rr - p.pt;
-          v[i] = px_issue(rs, okk && (unsigned)hs < (unsigned)p.H, ((n * p.C + hb) * p.H + hs) * p.W,
-                          q0 + ss - p.pl, p.W, p.Q + ss - p.pl, p.b_nel, meta[i]);   // t < Q - q0: padded q load as 0
+        if constexpr (ROLE == 6) {       // G[n, row, pp, q0 ..]: lanes differ only in the row
+          v[i] = px_issue(rs, okk, (n * p.K * p.P + pp) * p.Q + q0 + base, q0, p.Q - q0, p.a_nel, meta[i]);
+        } else {                         // X[n, c, pp + r - pt, q0 + s - pl ..]
+          const int hs = pp + rr - p.pt, w0 = q0 + ss - p.pl;
+          v[i] = px_issue(rs, okk && (unsigned)hs < (unsigned)p.H, n * p.C * p.H * p.W + (pp - p.pt) * p.W + q0 - p.pl + base,
+                          w0, min(p.W - w0, p.Q - q0), p.b_nel, meta[i]);   // t < Q - q0: padded q load as 0
         }
         continue;
       } else if constexpr (ROLE == 1) {
@@ -395,7 +423,8 @@ __global__ void __launch_bounds__(CT, 2) fm_conv_igemm(ConvP p) {
   constexpr int AROLE = MODE == CONV_WGRAD ? (PV ? 6 : 3) : 0;
   constexpr int BROLE = MODE == CONV_WGRAD ? (PV ? 7 : 4) : PV ? 5 : MODE == CONV_FWD ? 1 : 2;
   constexpr bool BMN = BROLE == 5;
-  __shared__ __attribute__((aligned(16))) char smem[2 * (A_BYTES + B_BYTES)];
+  extern __shared__ __attribute__((aligned(16))) char smem[];   // 2 x (A, B) tiles + the mask table
+  char* tab = smem + 2 * (A_BYTES + B_BYTES);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -411,8 +440,10 @@ __global__ void __launch_bounds__(CT, 2) fm_conv_igemm(ConvP p) {
   const auto rsb = make_rsrc(p.b, p.b_bytes);
   Gather<T, BM, AROLE, MODE> ga;
   Gather<T, BN, BROLE, MODE> gb;
-  ga.init(p, m0, p.M, tid);
-  gb.init(p, n0, p.Ncols, tid);
+  ga.init(p, m0, p.M, tid, kt0);
+  gb.init(p, n0, p.Ncols, tid, kt0);
+  init_mask_table(tab, tid);
+  __syncthreads();
 
   f32x4_t acc[MR][NR];
 #pragma unroll
@@ -423,8 +454,8 @@ __global__ void __launch_bounds__(CT, 2) fm_conv_igemm(ConvP p) {
   if (kt0 < kt1) {
     ga.load(p, rsa, kt0, tid);
     gb.load(p, rsb, kt0, tid);
-    ga.finish();
-    gb.finish();
+    ga.finish(tab);
+    gb.finish(tab);
     ga.store(smem, tid);
     gb.store(smem + A_BYTES, tid);
   }
@@ -439,8 +470,8 @@ __global__ void __launch_bounds__(CT, 2) fm_conv_igemm(ConvP p) {
     const char* la = smem + cur * (A_BYTES + B_BYTES);
     mma_tile<T, MR, NR, BN, BMN>(la, la + A_BYTES, wm * (BM / 2), wn * (BN / 2), lane, acc);
     if (more) {
-      ga.finish();
-      gb.finish();
+      ga.finish(tab);
+      gb.finish(tab);
       char* nx = smem + (cur ^ 1) * (A_BYTES + B_BYTES);
       ga.store(nx, tid);
       gb.store(nx + A_BYTES, tid);
@@ -620,6 +651,9 @@ int launch(ConvP& p, hipStream_t s) {
   p.dPer = make_fastdiv(p.P * p.Qp);
   p.dQp = make_fastdiv(p.Qp);
   p.dSh = make_fastdiv(p.sh);
+  p.adv_c = 64 / (p.R * p.S);
+  p.adv_r = (64 / p.S) % p.R;
+  p.adv_s = 64 % p.S;
   p.dSw = make_fastdiv(p.sw);
   const bool small_m = p.M <= 64;
   const int BM = small_m ? 64 : 128;
@@ -634,7 +668,17 @@ int launch(ConvP& p, hipStream_t s) {
   p.kt_per = (ktiles + p.ksplit - 1) / p.ksplit;
   p.ksplit = (ktiles + p.kt_per - 1) / p.kt_per;
   dim3 grid(p.tiles_m * p.tiles_n, 1, p.ksplit);
-#define FM_CONV_GO(BMv, PVv) hipLaunchKernelGGL((fm_conv_igemm<T, BMv, MODE, PVv>), grid, dim3(CT), 0, s, p)
+#define FM_CONV_GO(BMv, PVv)                                                                         \
+  do {                                                                                               \
+    const int lds = 2 * (BMv * 128 + 128 * 128) + MASK_BYTES;                                        \
+    static bool attr = false;                                                                        \
+    if (!attr) {                                                                                     \
+      (void)hipFuncSetAttribute((const void*)fm_conv_igemm<T, BMv, MODE, PVv>,                       \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);                    \
+      attr = true;                                                                                   \
+    }                                                                                                \
+    hipLaunchKernelGGL((fm_conv_igemm<T, BMv, MODE, PVv>), grid, dim3(CT), lds, s, p);               \
+  } while (0)
   if constexpr (sizeof(T) == 2) {   // the pixel-vector gathers are bf16 only
     if (pv) {
       if (small_m) FM_CONV_GO(64, true);
