@@ -94,6 +94,10 @@ int fm_conv_wgrad(const void* g, const void* x, float* dw, int bf16, int N, int 
                   int Q, int sh, int sw, int pt, int pl, hipStream_t s);
 void fm_conv_act_bwd(const void* dy, const void* y, void* g, float* db, int bf16, int N, int K, int PQ, int act,
                      hipStream_t s);
+void fm_conv_s2d_run(const void* x, void* xs, int bf16, int N, int C, int H, int W, int s, int pt, int pl, int Hs, int Ws,
+                     int inv, int acc, hipStream_t st);
+void fm_conv_w_s2d_run(const void* w, void* ws, const float* dws, float* dw, int bf16, int K, int C, int R, int S, int s,
+                       int Rs, int Ss, int inv, hipStream_t st);
 void fm_pad_rows(const void* src, void* dst, int K, int n, int ldp, int bf16, hipStream_t st);
 void fm_lstm_init(const void* h0, const void* c0, void* hprev, long ldhp, float* cinit, int B, int H, int bf16, hipStream_t s);
 void fm_lstm_cell_fwd(float* G, long ldg, const float* c_prev, long ldcp, float* c_out, long ldc, void* y, long ldy,
@@ -548,6 +552,31 @@ void conv_wgrad(torch::Tensor g, torch::Tensor x, torch::Tensor dw, int64_t R, i
   fm_conv_wgrad(g.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), is_bf16(x), (int)x.size(0), (int)x.size(1), (int)x.size(2),
                 (int)x.size(3), (int)g.size(1), (int)R, (int)S, (int)g.size(2), (int)g.size(3), sh, sw, pt, pl, cur());
 }
+// space-to-depth: x [N,C,H,W] <-> xs [N, C*s*s, Hs, Ws] (inv scatters xs back into x, acc adds)
+void conv_s2d(torch::Tensor x, torch::Tensor xs, int64_t s, int64_t pt, int64_t pl, bool inv, bool acc) {
+  chk4(x, "conv_s2d x");
+  chk4(xs, "conv_s2d xs");
+  same_dt(x, xs, "conv_s2d");
+  TORCH_CHECK(x.dim() == 4 && xs.dim() == 4 && xs.size(0) == x.size(0) && xs.size(1) == x.size(1) * s * s,
+              "conv_s2d: xs [N, C*s*s, Hs, Ws]");
+  TORCH_CHECK(xs.numel() < (1L << 31) && x.numel() < (1L << 31), "conv_s2d: 32-bit indexing");
+  fm_conv_s2d_run(x.data_ptr(), xs.data_ptr(), is_bf16(x), (int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3),
+                  (int)s, (int)pt, (int)pl, (int)xs.size(2), (int)xs.size(3), inv ? 1 : 0, acc ? 1 : 0, cur());
+}
+// kernel re-layout: ws = S2D(w) (inv = false), or dw += S2D^-1(dws) (inv = true, fp32 gradients)
+void conv_w_s2d(torch::Tensor w, torch::Tensor ws, torch::Tensor dws, torch::Tensor dw, int64_t s, bool inv) {
+  chk4(w, "conv_w_s2d w");
+  chk4(ws, "conv_w_s2d ws");
+  same_dt(w, ws, "conv_w_s2d");
+  TORCH_CHECK(w.dim() == 4 && ws.dim() == 4 && ws.size(1) == w.size(1) * s * s, "conv_w_s2d: ws [K, C*s*s, Rs, Ss]");
+  if (inv)
+    TORCH_CHECK(dws.scalar_type() == torch::kFloat32 && dw.scalar_type() == torch::kFloat32 && dws.numel() == ws.numel() &&
+                    dw.numel() == w.numel(), "conv_w_s2d: fp32 gradients");
+  fm_conv_w_s2d_run(w.data_ptr(), ws.data_ptr(), inv ? dws.data_ptr<float>() : nullptr, inv ? dw.data_ptr<float>() : nullptr,
+                    is_bf16(w), (int)w.size(0),
+                    (int)w.size(1), (int)w.size(2), (int)w.size(3), (int)s, (int)ws.size(2), (int)ws.size(3), inv ? 1 : 0,
+                    cur());
+}
 void conv_act_bwd(torch::Tensor dy, torch::Tensor y, torch::Tensor g, c10::optional<torch::Tensor> db, int64_t act) {
   chk4(dy, "dy");
   chk4(y, "y");
@@ -685,6 +714,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_act_bwd", &conv_act_bwd);
+  m.def("conv_s2d", &conv_s2d);
+  m.def("conv_w_s2d", &conv_w_s2d);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("embedding_fwd_multi", &embedding_fwd_multi, py::arg("W"), py::arg("idx"), py::arg("out"), py::arg("ldo"),

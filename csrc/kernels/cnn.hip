@@ -169,17 +169,20 @@ __global__ void __launch_bounds__(256) fm_pool_argmax_kernel(const T* __restrict
 template <typename T>
 __global__ void __launch_bounds__(256) fm_pool_bwd_kernel(const T* __restrict__ y, const T* __restrict__ dy,
                                                           const unsigned char* __restrict__ code, T* __restrict__ dx,
-                                                          int total, FastDiv dW, FastDiv dH, int H, int W, int P, int Q,
-                                                          int kh, int kw, int sh, int sw, int pt, int pl, int is_max,
-                                                          int act, int acc) {
+                                                          int total, FastDiv dW, FastDiv dH, FastDiv dsh, FastDiv dsw,
+                                                          int H, int W, int P, int Q, int kh, int kw, int sh, int sw,
+                                                          int pt, int pl, int is_max, int act, int acc) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
   const int t = fdiv(i, dW), w = i - t * W;
   const int nc = fdiv(t, dH), h = t - nc * H;
   float g = 0.f;
-  // windows (p, q) containing (h, w): p*sh - pt <= h < p*sh - pt + kh
-  const int pmin = max(0, (h + pt - kh + sh) / sh), pmax = min(P - 1, (h + pt) / sh);
-  const int qmin = max(0, (w + pl - kw + sw) / sw), qmax = min(Q - 1, (w + pl) / sw);
+  // windows (p, q) containing (h, w): p*sh - pt <= h < p*sh - pt + kh (divisions by magic numbers;
+  // arguments kept >= 0: pmin = ceil((h + pt - kh + 1) / sh) clipped at 0)
+  const int pmin = h + pt + 1 >= kh ? fdiv(h + pt - kh + sh, dsh) : 0;
+  const int pmax = h + pt >= 0 ? min(P - 1, fdiv(h + pt, dsh)) : -1;    // pads may be negative (superset boxes)
+  const int qmin = w + pl + 1 >= kw ? fdiv(w + pl - kw + sw, dsw) : 0;
+  const int qmax = w + pl >= 0 ? min(Q - 1, fdiv(w + pl, dsw)) : -1;
   for (int p = pmin; p <= pmax; ++p) {
     const int h0 = p * sh - pt;
     if (h < h0 || h >= h0 + kh) continue;
@@ -188,10 +191,12 @@ __global__ void __launch_bounds__(256) fm_pool_bwd_kernel(const T* __restrict__ 
       if (w < w0 || w >= w0 + kw) continue;
       const int o = (nc * P + p) * Q + q;
       if (is_max) {
-        if (code[o] == (unsigned char)((h - h0) * kw + (w - w0))) g += act_bwd(act, tof(y[o]), tof(dy[o]));
+        if (code[o] == (unsigned char)((h - h0) * kw + (w - w0)))
+          g += act == ACT_NONE ? tof(dy[o]) : act_bwd(act, tof(y[o]), tof(dy[o]));
       } else {
         const int hs = max(h0, 0), he = min(h0 + kh, H), ws = max(w0, 0), we = min(w0 + kw, W);
-        g += act_bwd(act, tof(y[o]), tof(dy[o])) / (float)((he - hs) * (we - ws));
+        const float go = act == ACT_NONE ? tof(dy[o]) : act_bwd(act, tof(y[o]), tof(dy[o]));
+        g += go / (float)((he - hs) * (we - ws));
       }
     }
   }
@@ -377,8 +382,8 @@ static void fm_pool_bwd_t(const void* x, const void* y, const void* dy, void* dx
     hipLaunchKernelGGL(fm_pool_argmax_kernel<T>, dim3((outs + 255) / 256), dim3(256), 0, st, (const T*)x, code, outs, H, W,
                        P, Q, kh, kw, sh, sw, pt, pl);
   hipLaunchKernelGGL(fm_pool_bwd_kernel<T>, dim3((total + 255) / 256), dim3(256), 0, st, (const T*)y, (const T*)dy,
-                     (const unsigned char*)code, (T*)dx, total, make_fastdiv(W), make_fastdiv(H), H, W, P, Q, kh, kw, sh,
-                     sw, pt, pl, is_max, act, acc);
+                     (const unsigned char*)code, (T*)dx, total, make_fastdiv(W), make_fastdiv(H), make_fastdiv(sh),
+                     make_fastdiv(sw), H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, acc);
 }
 
 // stats / meaninv: fp32 [2C] device buffers owned by the op

@@ -547,11 +547,12 @@ __global__ void __launch_bounds__(CT, 2) fm_conv_igemm(ConvP p) {
 }
 
 // G = act'(y) * dY (written only when act != none) and db[k] += sum over (n, p, q) of G.  Block
-// (k, image range); each thread streams 16-B chunks of the (n, k) planes through buffer loads /
-// stores (planes start anywhere: unaligned 16-B accesses), scalar tail per plane.
+// (k, image range); the block's threads stream the (image, 16-B chunk) pairs of its planes
+// (planes start anywhere: unaligned 16-B buffer accesses; scalar tail per plane).
 template <typename T>
 __global__ void __launch_bounds__(256) fm_conv_act_bwd(const T* __restrict__ dy, const T* __restrict__ y, T* __restrict__ g,
-                                                      float* __restrict__ db, int N, int K, int PQ, int act, int nper) {
+                                                      float* __restrict__ db, int N, int K, int PQ, int act, int nper,
+                                                      FastDiv dch) {
   constexpr int E = 16 / (int)sizeof(T);
   __shared__ float red[4];
   const long bytes = (long)N * K * PQ * (long)sizeof(T);
@@ -559,51 +560,50 @@ __global__ void __launch_bounds__(256) fm_conv_act_bwd(const T* __restrict__ dy,
   const int k = blockIdx.x;
   const int n0 = blockIdx.y * nper, n1 = min(N, n0 + nper);
   const int chunks = (PQ + E - 1) / E;
+  const int work = (n1 - n0) * chunks;
   const bool wr = act != ACT_NONE;
   float s = 0.f;
-  for (int n = n0; n < n1; ++n) {
-    const int base = (n * K + k) * PQ;
-    for (int c = threadIdx.x; c < chunks; c += 256) {
-      const int off = base + c * E, cnt = min(E, PQ - c * E);
-      if (cnt == E) {
-        const u32x4_t vd = ldb16(rdy, (unsigned)off * sizeof(T));
-        if (!wr) {
-          if constexpr (sizeof(T) == 2) {
+  for (int w = threadIdx.x; w < work; w += 256) {
+    const int nn = fdiv(w, dch), c = w - nn * chunks;
+    const int off = ((n0 + nn) * K + k) * PQ + c * E, cnt = min(E, PQ - c * E);
+    if (cnt == E) {
+      const u32x4_t vd = ldb16(rdy, (unsigned)off * sizeof(T));
+      if (!wr) {
+        if constexpr (sizeof(T) == 2) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) s += bf2f((unsigned short)(vd[j] & 0xFFFF)) + bf2f((unsigned short)(vd[j] >> 16));
-          } else {
+          for (int j = 0; j < 4; ++j) s += bf2f((unsigned short)(vd[j] & 0xFFFF)) + bf2f((unsigned short)(vd[j] >> 16));
+        } else {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) s += __uint_as_float(vd[j]);
-          }
-          continue;
+          for (int j = 0; j < 4; ++j) s += __uint_as_float(vd[j]);
         }
-        const u32x4_t vy = ldb16(ry, (unsigned)off * sizeof(T));
-        u32x4_t o;
+        continue;
+      }
+      const u32x4_t vy = ldb16(ry, (unsigned)off * sizeof(T));
+      u32x4_t o;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if constexpr (sizeof(T) == 2) {
-            const float d0 = act_bwd(act, bf2f((unsigned short)(vy[j] & 0xFFFF)), bf2f((unsigned short)(vd[j] & 0xFFFF)));
-            const float d1 = act_bwd(act, bf2f((unsigned short)(vy[j] >> 16)), bf2f((unsigned short)(vd[j] >> 16)));
-            const unsigned short b0 = f2bf(d0), b1 = f2bf(d1);
-            s += bf2f(b0) + bf2f(b1);
-            o[j] = (unsigned)b0 | ((unsigned)b1 << 16);
-          } else {
-            const float d = act_bwd(act, __uint_as_float(vy[j]), __uint_as_float(vd[j]));
-            s += d;
-            o[j] = __float_as_uint(d);
-          }
-        }
-        __builtin_amdgcn_raw_buffer_store_b128(o, rg, (unsigned)off * sizeof(T), 0, 0);
-      } else {
-        for (int t = 0; t < cnt; ++t) {
-          float d = ld<T>(dy + off + t);
-          if (wr) {
-            d = act_bwd(act, ld<T>(y + off + t), d);
-            st<T>(g + off + t, d);
-            d = ld<T>(g + off + t);
-          }
+      for (int j = 0; j < 4; ++j) {
+        if constexpr (sizeof(T) == 2) {
+          const float d0 = act_bwd(act, bf2f((unsigned short)(vy[j] & 0xFFFF)), bf2f((unsigned short)(vd[j] & 0xFFFF)));
+          const float d1 = act_bwd(act, bf2f((unsigned short)(vy[j] >> 16)), bf2f((unsigned short)(vd[j] >> 16)));
+          const unsigned short b0 = f2bf(d0), b1 = f2bf(d1);
+          s += bf2f(b0) + bf2f(b1);
+          o[j] = (unsigned)b0 | ((unsigned)b1 << 16);
+        } else {
+          const float d = act_bwd(act, __uint_as_float(vy[j]), __uint_as_float(vd[j]));
           s += d;
+          o[j] = __float_as_uint(d);
         }
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(o, rg, (unsigned)off * sizeof(T), 0, 0);
+    } else {
+      for (int t = 0; t < cnt; ++t) {
+        float d = ld<T>(dy + off + t);
+        if (wr) {
+          d = act_bwd(act, ld<T>(y + off + t), d);
+          st<T>(g + off + t, d);
+          d = ld<T>(g + off + t);
+        }
+        s += d;
       }
     }
   }
@@ -633,6 +633,64 @@ __global__ void fm_conv_wprep(const T* __restrict__ w, T* __restrict__ out, int 
       }
     }
     out[i] = v;
+  }
+}
+
+// Space-to-depth for strided convolutions with few input channels (AlexNet's 11x11/4 stem on 3
+// channels): a stride-s conv over X equals a stride-1 conv over X' (C*s*s channels, phase
+// (a, b) of the padded input: X'[n, (c*s + a)*s + b, i, j] = Xpad[n, c, i*s + a, j*s + b]) with the
+// kernel re-laid the same way (ceil(R/s) x ceil(S/s) taps, zero where r >= R) -- so the stem runs
+// on the pixel-vector path.  inv = 1: scatter back (the data gradient; acc adds).
+template <typename T>
+__global__ void __launch_bounds__(256) fm_conv_s2d(const T* __restrict__ src, T* __restrict__ dst, int total, FastDiv dWs,
+                                                   FastDiv dHs, FastDiv dss, FastDiv ds, int C, int H, int W, int s, int pt,
+                                                   int pl, int Hs, int Ws, int inv, int acc) {
+  const int o = blockIdx.x * 256 + threadIdx.x;     // element of xs [N, C*s*s, Hs, Ws]
+  if (o >= total) return;
+  int t = fdiv(o, dWs);
+  const int j = o - t * Ws;
+  int u = fdiv(t, dHs);
+  const int i = t - u * Hs;                         // u = n * C*s*s + cp
+  const int nc = fdiv(u, dss), ab = u - nc * s * s; // nc = n * C + c
+  const int a = fdiv(ab, ds), b = ab - a * s;
+  const int h = i * s + a - pt, w = j * s + b - pl;
+  const bool in = h >= 0 && h < H && w >= 0 && w < W;
+  const long xo = ((long)nc * H + h) * W + w;
+  if (!inv) {
+    dst[o] = in ? src[xo] : (T)0;
+  } else if (in) {
+    const float v = ld<T>(src + o) + (acc ? ld<T>(dst + xo) : 0.f);
+    st<T>(dst + xo, v);
+  }
+}
+
+// kernel re-layout for space-to-depth: fwd ws[k][(c*s+a)*s+b][i][j] = w[k][c][i*s+a][j*s+b] (0 past R / S);
+// inv: dW[k][c][r][q] += dWs[k][(c*s + r%s)*s + q%s][r/s][q/s] (fp32 gradients)
+template <typename T>
+__global__ void fm_conv_w_s2d(const T* __restrict__ w, T* __restrict__ ws, const float* __restrict__ dws,
+                              float* __restrict__ dw, int K, int C, int R, int S, int s, int Rs, int Ss, int inv) {
+  const long total = inv ? (long)K * C * R * S : (long)K * C * s * s * Rs * Ss;
+  for (long o = blockIdx.x * 256L + threadIdx.x; o < total; o += (long)gridDim.x * 256) {
+    if (!inv) {
+      const int j = (int)(o % Ss);
+      long t = o / Ss;
+      const int i = (int)(t % Rs);
+      t /= Rs;
+      const int cp = (int)(t % (C * s * s));
+      const int k = (int)(t / (C * s * s));
+      const int c = cp / (s * s), a = (cp / s) % s, b = cp % s;
+      const int r = i * s + a, q = j * s + b;
+      ws[o] = (r < R && q < S) ? w[(((long)k * C + c) * R + r) * S + q] : (T)0;
+    } else {
+      const int q = (int)(o % S);
+      long t = o / S;
+      const int r = (int)(t % R);
+      t /= R;
+      const int c = (int)(t % C);
+      const int k = (int)(t / C);
+      const int cp = (c * s + r % s) * s + q % s;
+      dw[o] += dws[(((long)k * C * s * s + cp) * Rs + r / s) * Ss + q / s];
+    }
   }
 }
 
@@ -766,10 +824,40 @@ extern "C" void fm_conv_act_bwd(const void* dy, const void* y, void* g, float* d
   const int want = std::max(1, std::min(N, 2048 / std::max(K, 1)));   // ~2048 blocks over (k, image range)
   const int nper = (N + want - 1) / want;
   const int ny = (N + nper - 1) / nper;
+  const FastDiv dch = make_fastdiv((PQ + (bf16 ? 8 : 4) - 1) / (bf16 ? 8 : 4));
   if (bf16)
     hipLaunchKernelGGL(fm_conv_act_bwd<unsigned short>, dim3(K, ny), dim3(256), 0, s, (const unsigned short*)dy,
-                       (const unsigned short*)y, (unsigned short*)g, db, N, K, PQ, act, nper);
+                       (const unsigned short*)y, (unsigned short*)g, db, N, K, PQ, act, nper, dch);
   else
     hipLaunchKernelGGL(fm_conv_act_bwd<float>, dim3(K, ny), dim3(256), 0, s, (const float*)dy, (const float*)y, (float*)g,
-                       db, N, K, PQ, act, nper);
+                       db, N, K, PQ, act, nper, dch);
+}
+
+// space-to-depth helpers (see fm_conv_s2d): inv = 0: xs = S2D(x); inv = 1: x (+)= S2D^-1(xs)
+extern "C" void fm_conv_s2d_run(const void* x, void* xs, int bf16, int N, int C, int H, int W, int s, int pt, int pl, int Hs,
+                                int Ws, int inv, int acc, hipStream_t st) {
+  const int total = N * C * s * s * Hs * Ws;        // host binding: < 2^31 elements
+  const dim3 grid((total + 255) / 256);
+  const FastDiv dWs = make_fastdiv(Ws), dHs = make_fastdiv(Hs), dss = make_fastdiv(s * s), ds = make_fastdiv(s);
+  if (bf16)
+    hipLaunchKernelGGL(fm_conv_s2d<unsigned short>, grid, dim3(256), 0, st, (const unsigned short*)(inv ? xs : x),
+                       (unsigned short*)(inv ? const_cast<void*>(x) : xs), total, dWs, dHs, dss, ds, C, H, W, s, pt, pl, Hs,
+                       Ws, inv, acc);
+  else
+    hipLaunchKernelGGL(fm_conv_s2d<float>, grid, dim3(256), 0, st, (const float*)(inv ? xs : x),
+                       (float*)(inv ? const_cast<void*>(x) : xs), total, dWs, dHs, dss, ds, C, H, W, s, pt, pl, Hs, Ws, inv,
+                       acc);
+}
+
+// inv = 0: ws = S2D(w); inv = 1: dw += S2D^-1(dws)
+extern "C" void fm_conv_w_s2d_run(const void* w, void* ws, const float* dws, float* dw, int bf16, int K, int C, int R, int S,
+                                  int s, int Rs, int Ss, int inv, hipStream_t st) {
+  const long total = inv ? (long)K * C * R * S : (long)K * C * s * s * Rs * Ss;
+  const int grid = (int)std::min<long>((total + 255) / 256, 1024);
+  if (bf16)
+    hipLaunchKernelGGL(fm_conv_w_s2d<unsigned short>, dim3(grid), dim3(256), 0, st, (const unsigned short*)w,
+                       (unsigned short*)ws, dws, dw, K, C, R, S, s, Rs, Ss, inv);
+  else
+    hipLaunchKernelGGL(fm_conv_w_s2d<float>, dim3(grid), dim3(256), 0, st, (const float*)w, (float*)ws, dws, dw, K, C, R, S,
+                       s, Rs, Ss, inv);
 }

@@ -364,30 +364,87 @@ def scratch(device, name, numel, dtype=torch.bfloat16):
     return t[:numel]
 
 
-def conv2d_forward(x, w, b, y, stride, pads, act, groups):
+def _s2d_plan(x, w, y, stride):
+    """Space-to-depth for a strided bf16 conv whose re-laid kernel costs <= 1.5x the MACs (the
+    AlexNet / ResNet stems on 3 channels): returns (s, Hs, Ws, Rs, Ss) or None."""
+    s_ = stride[0]
+    if s_ < 2 or stride[1] != s_ or x.dtype != torch.bfloat16:
+        return None
+    Kout, Cg, R, S = w.shape
+    Rs, Ss = -(-R // s_), -(-S // s_)
+    if Cg * s_ * s_ * Rs * Ss > 1.5 * Cg * R * S:
+        return None
+    return s_, y.shape[2] + (R - 1) // s_, y.shape[3] + (S - 1) // s_, Rs, Ss
+
+
+def _s2d_operands(x, w, plan, pads, saved):
+    s_, Hs, Ws, Rs, Ss = plan
+    N, Cin = x.shape[0], x.shape[1]
+    Kout = w.shape[0]
+    shp = (N, Cin * s_ * s_, Hs, Ws)
+    xs = saved.get("s2d_x") if saved is not None else None
+    if xs is None or tuple(xs.shape) != shp or xs.dtype != x.dtype:
+        xs = torch.empty(shp, dtype=x.dtype, device=x.device)
+        if saved is not None:
+            saved["s2d_x"] = xs
+    ws = scratch(x.device, "conv_s2d_w", Kout * Cin * s_ * s_ * Rs * Ss, w.dtype).view(Kout, Cin * s_ * s_, Rs, Ss)
+    return xs, ws
+
+
+def conv2d_forward(x, w, b, y, stride, pads, act, groups, saved=None):
     """Implicit-GEMM convolution on MFMA straight from NCHW (csrc/kernels/conv_igemm.hip): the
     image operand is gathered into LDS per tile, bias + activation fused into the NCHW store.
-    pads = (top, bottom, left, right) of this shard (bottom / right are implied by y's extent)."""
+    pads = (top, bottom, left, right) of this shard (bottom / right are implied by y's extent).
+    Strided stems on few channels go through space-to-depth onto the stride-1 pixel-vector path."""
     assert groups == 1, "grouped convolution is not supported on the HIP path"
+    w = w.contiguous()
+    plan = _s2d_plan(x, w, y, stride)
+    if plan is not None:
+        xs, ws = _s2d_operands(x, w, plan, pads, saved)
+        C().conv_s2d(x, xs, plan[0], pads[0], pads[2], False, False)
+        C().conv_w_s2d(w, ws, ws, ws, plan[0], False)
+        if saved is not None:
+            saved["s2d_ready"] = True
+        x, w, stride, pads = xs, ws, (1, 1), (0, 0, 0, 0)
     Kout, Cg, R, S = w.shape
     wpad = scratch(x.device, "conv_wpad", C().conv_scratch(Kout, Cg * R * S), w.dtype)
-    C().conv_fwd(x, w.contiguous(), wpad, b, y, stride[0], stride[1], pads[0], pads[2], int(act))
+    C().conv_fwd(x, w, wpad, b, y, stride[0], stride[1], pads[0], pads[2], int(act))
 
 
-def conv2d_backward(x, w, y, dy, dx, dw, db, stride, pads, act, groups, acc):
+def conv2d_backward(x, w, y, dy, dx, dw, db, stride, pads, act, groups, acc, saved=None):
     """G = act'(y) * dY with db = sum G (one pass; skipped for a linear conv without bias), then
     dW += G (x) X and dX (+)= Wt (x) G as implicit GEMMs -- no columns, no transposes."""
     assert groups == 1, "grouped convolution is not supported on the HIP path"
+    w = w.contiguous()
     g = dy
     if int(act) != 10 or db is not None:
         g = scratch(x.device, "conv_g", dy.numel(), dy.dtype).view(dy.shape) if int(act) != 10 else dy
         C().conv_act_bwd(dy, y, g, db, int(act))
+    plan = _s2d_plan(x, w, y, stride)
+    if plan is not None:
+        s_, Hs, Ws, Rs, Ss = plan
+        xs, ws = _s2d_operands(x, w, plan, pads, saved)
+        if not (saved is not None and saved.get("s2d_ready")):
+            C().conv_s2d(x, xs, s_, pads[0], pads[2], False, False)
+        C().conv_w_s2d(w, ws, ws, ws, s_, False)
+        dws = scratch(x.device, "conv_s2d_dw", ws.numel(), torch.float32)
+        dws.zero_()
+        C().conv_wgrad(g, xs, dws, Rs, Ss, 1, 1, 0, 0)
+        C().conv_w_s2d(w, ws, dws, dw.view(-1), s_, True)
+        if dx is not None:
+            dxs = scratch(x.device, "conv_s2d_dx", xs.numel(), xs.dtype).view(xs.shape)
+            wt = scratch(x.device, "conv_wt", C().conv_scratch(ws.shape[1], ws.shape[0] * Rs * Ss), w.dtype)
+            C().conv_dgrad(g, ws, wt, dxs, 1, 1, 0, 0, False)
+            if not acc:
+                dx.zero_()
+            C().conv_s2d(dx, dxs, s_, pads[0], pads[2], True, True)
+        return
     Kout, Cg, R, S = w.shape
     # dW / db ACCUMULATE into the per-step zeroed gradient buffer (tied weights sum their grads)
     C().conv_wgrad(g, x, dw.view(-1), R, S, stride[0], stride[1], pads[0], pads[2])
     if dx is not None:
         wt = scratch(x.device, "conv_wt", C().conv_scratch(Cg, Kout * R * S), w.dtype)
-        C().conv_dgrad(g, w.contiguous(), wt, dx, stride[0], stride[1], pads[0], pads[2], bool(acc))
+        C().conv_dgrad(g, w, wt, dx, stride[0], stride[1], pads[0], pads[2], bool(acc))
 
 
 def _pool_code(saved, y):

@@ -94,7 +94,8 @@ class Conv2D(_SpatialOp):
         pads = self._pads(ctx)
         b = ctx.weights[1] if self.use_bias else None
         if ctx.hip:
-            K.conv2d_forward(x, ctx.wcompute[0], b, y, (self.sh, self.sw), pads, int(self.activation), self.groups)
+            K.conv2d_forward(x, ctx.wcompute[0], b, y, (self.sh, self.sw), pads, int(self.activation), self.groups,
+                             ctx.saved)
             return
         xp = F.pad(x.float(), (pads[2], pads[3], pads[0], pads[1]))
         out = F.conv2d(xp, ctx.wcompute[0].float(), None if b is None else b.float(), (self.sh, self.sw), 0, 1, self.groups)
@@ -109,7 +110,7 @@ class Conv2D(_SpatialOp):
         if ctx.hip:
             K.conv2d_backward(x, ctx.wcompute[0], y, dy, dx, dw, db, (self.sh, self.sw), pads,
                               int(self.activation), self.groups,
-                              bool(ctx.in_grad_accumulate[0]) if dx is not None else False)
+                              bool(ctx.in_grad_accumulate[0]) if dx is not None else False, ctx.saved)
             return
         g = act_backward_torch(dy.float(), y.float(), self.activation)
         xl = x.float().detach().requires_grad_(dx is not None)

@@ -2,7 +2,8 @@
 oracle: forward (+bias +ReLU), data gradient (overwrite and accumulate), weight gradient and
 bias gradient, for bf16 and fp32, over the geometries the zoo uses -- AlexNet's 11x11/4 stem on
 3 channels, 5x5 and 3x3 same-padding, ResNet 1x1 and strided 3x3, Inception's 1x7 / 7x1, tile tails
-(odd pixel counts, channel counts off the tile) and asymmetric halo-shard pads."""
+(odd pixel counts, channel counts off the tile) and asymmetric halo-shard pads.  Strided bf16 stems on
+3 channels run through space-to-depth (one case with a saved forward buffer, one without)."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -20,6 +21,8 @@ CASES = [
     (2, 24, 9, 9, 40, 7, 1, 1, 1, (3, 3, 0, 0)),        # Inception 7x1
     (2, 8, 10, 7, 8, 3, 3, 2, 2, (0, 1, 1, 0)),         # asymmetric (halo-shard) pads
     (1, 5, 6, 5, 7, 2, 3, 1, 2, (1, 0, 0, 2)),          # everything odd
+    (2, 3, 30, 30, 16, 7, 7, 2, 2, (3, 3, 3, 3)),       # ResNet stem 7x7/2 (bf16: space-to-depth path)
+    (1, 3, 21, 19, 8, 11, 11, 4, 4, (2, 0, 1, 3)),      # strided stem with asymmetric halo pads
 ]
 
 
@@ -50,7 +53,8 @@ def test_conv_igemm(gpu, dtype, case, act, bias):
     b = torch.randn(K, device=gpu) if bias else None
     xd, wd, bd, yr = _ref(x, w, b, (sh, sw), pads, act)
     y = torch.empty(yr.shape, device=gpu, dtype=dt)
-    Kk.conv2d_forward(x, w, b, y, (sh, sw), pads, act, 1)
+    saved = {} if CASES.index(case) % 2 else None       # saved-forward-buffer and recompute variants
+    Kk.conv2d_forward(x, w, b, y, (sh, sw), pads, act, 1, saved)
     assert _err(y, yr.detach()) < tol
     dy = torch.randn(yr.shape, device=gpu).to(dt)
     # the backward consumes the ROUNDED forward output (the activation mask follows y as stored)
@@ -63,7 +67,7 @@ def test_conv_igemm(gpu, dtype, case, act, bias):
         dx = dx0.clone()
         dw = torch.full((K, C, R, S), 0.5, device=gpu)          # dW accumulates
         db = torch.full((K,), 0.25, device=gpu) if bias else None
-        Kk.conv2d_backward(x, w, y, dy, dx, dw, db, (sh, sw), pads, act, 1, acc)
+        Kk.conv2d_backward(x, w, y, dy, dx, dw, db, (sh, sw), pads, act, 1, acc, saved)
         assert _err(dw - 0.5, gw) < tol
         if bias:
             assert _err(db - 0.25, g.sum((0, 2, 3))) < tol

@@ -100,7 +100,9 @@ def _fault_worker(rank, world, port, fault, out_dir):
         from flexmi.runtime.health import FaultyComm
         m, x = _mlp(debug=True, watchdog=20.0)
         if rank == 1:
-            m.comm = FaultyComm(m.comm, {0: fault})
+            # the step's first collectives (gradient bucket and metric reductions; their issue
+            # order may vary with timing) all get the fault, so the gradient exchange is hit
+            m.comm = FaultyComm(m.comm, {0: fault} if fault[0] == "kill" else {0: fault, 1: fault, 2: fault})
         m.init_layers()
         nr = m._ex().native_runner()
         res["native"] = nr is not None
