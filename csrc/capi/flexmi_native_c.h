@@ -1,0 +1,124 @@
+/* flexmi native C API: flexmi's C++ runtime from C without any Python.
+ *
+ * flexmi_c.h is the full model API (it drives the Python front end through an embedded
+ * interpreter, like the reference's cffi layer drives its C++ core).  This header is the
+ * CPython-free layer over the native runtime itself (libflexmi_native_c.so links only the C++
+ * runtime): strategy files in the reference's protobuf format, the sharding algebra of the plan
+ * compiler (partitions, boxes, reshard transfer lists), the MI355X execution simulator and MCMC
+ * SOAP search, the HDF5 dataset reader, the prefetching batch loader ring and the CPU
+ * embedding-bag kernels.  Reference counterparts: src/runtime/strategy.cc (.pb files),
+ * src/runtime/simulator.cc + model.cc:1082-1144 (simulate / optimize), python/flexflow_dataloader.cc
+ * (loaders), src/ops/embedding.cc:87-163 / embedding_avx2.cc (CPU embedding).
+ *
+ * Conventions: handles are opaque; functions return NULL / a negative value on error and the
+ * message is available from fmn_last_error() (thread-local).  Boxes are [lo, hi) per dim,
+ * passed as lo[nd] / hi[nd] arrays.
+ */
+#ifndef FLEXMI_NATIVE_C_H
+#define FLEXMI_NATIVE_C_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct fmn_strategy_s* fmn_strategy_t;
+typedef struct fmn_layout_s* fmn_layout_t;
+typedef struct fmn_sim_s* fmn_sim_t;
+typedef struct fmn_h5_s* fmn_h5_t;
+typedef struct fmn_loader_s* fmn_loader_t;
+
+const char* fmn_last_error(void);
+const char* fmn_version(void);
+
+/* ---- strategy files (reference .pb format: name, device type, dims, device ids) ----------- */
+fmn_strategy_t fmn_strategy_create(void);
+fmn_strategy_t fmn_strategy_load(const char* path);
+int fmn_strategy_save(fmn_strategy_t s, const char* path);
+void fmn_strategy_destroy(fmn_strategy_t s);
+int fmn_strategy_num_ops(fmn_strategy_t s);
+/* index of op `name`, -1 if absent */
+int fmn_strategy_find(fmn_strategy_t s, const char* name);
+/* op i: name (truncated to len), device type (0 GPU, 1 CPU), dims (reference order: innermost
+ * first, sample dim last), device ids; returns the number of parts (product of dims) */
+int fmn_strategy_get(fmn_strategy_t s, int i, char* name, size_t len, int* device_type, int* ndims, int* dims, int max_dims,
+                     int* ndev, int* devs, int max_devs);
+/* add or replace op `name` */
+int fmn_strategy_set(fmn_strategy_t s, const char* name, int device_type, int ndims, const int* dims, int ndev,
+                     const int* devs);
+
+/* ---- sharding algebra ---------------------------------------------------------------------- */
+/* [lo, hi) of block k of n split into d near-equal blocks */
+int fmn_split_extent(int64_t n, int64_t d, int64_t k, int64_t* lo, int64_t* hi);
+/* a layout: shape[nd], degrees[nd] (user order, outer -> inner); part p is held by holders[p]
+ * (one rank each; replicate with fmn_layout_add_holder) */
+fmn_layout_t fmn_layout_create(int nd, const int64_t* shape, const int64_t* degrees, const int* holders, int partial);
+int fmn_layout_add_holder(fmn_layout_t l, int part, int rank);
+int64_t fmn_layout_num_parts(fmn_layout_t l);
+int fmn_layout_part_box(fmn_layout_t l, int64_t part, int64_t* lo, int64_t* hi);
+void fmn_layout_destroy(fmn_layout_t l);
+/* transfers turning src into dst (sorted by src, dst, dst_part, src_part, box): returns the
+ * count; the first max_n are written (src, dst ranks; boxes as nd-wide lo / hi rows) */
+int fmn_reshard_transfers(fmn_layout_t src, fmn_layout_t dst, int max_n, int* src_rank, int* dst_rank, int64_t* lo,
+                          int64_t* hi);
+
+/* ---- MI355X simulator + MCMC SOAP search ----------------------------------------------------- */
+/* ndev GPUs, gpus_per_node per node; link_GBps / ar_busbw_GBps <= 0 keep the MI355X defaults */
+fmn_sim_t fmn_sim_create(int ndev, int gpus_per_node, double link_GBps, double ar_busbw_GBps);
+void fmn_sim_destroy(fmn_sim_t s);
+/* tensor: element bytes, producer op (-1 = graph input) and its output index */
+int fmn_sim_add_tensor(fmn_sim_t s, int elem_bytes, int producer, int producer_out, int needs_grad);
+/* op with inputs / outputs (tensor ids); candidates are added next, in order */
+int fmn_sim_add_op(fmn_sim_t s, const char* name, int n_in, const int* in_t, int n_out, const int* out_t);
+/* candidate of the last added op: parts on devices part_dev[nparts] with per-part fwd / bwd us;
+ * output / needed-input layouts per tensor as nparts boxes (nd-wide lo / hi rows, each part held
+ * by its own device), replicated-weight gradient bytes (all-reduced over the part devices when
+ * > 0) and per-part memory bytes.  Returns the candidate index. */
+int fmn_sim_add_candidate(fmn_sim_t s, int nparts, const int* part_dev, const double* fwd_us, const double* bwd_us, int nd,
+                          const int64_t* out_lo, const int64_t* out_hi, const int64_t* in_lo, const int64_t* in_hi,
+                          double wsync_bytes, double mem_bytes, const char* label);
+/* makespan (us) of one training iteration for candidate choice assign[num_ops] */
+double fmn_sim_simulate(fmn_sim_t s, const int* assign);
+/* Metropolis search from init[num_ops] for `budget` proposals: writes best[num_ops], returns
+ * its simulated time (us) */
+double fmn_sim_search(fmn_sim_t s, const int* init, long budget, double alpha, uint64_t seed, int* best);
+
+/* ---- HDF5 datasets (the DLRM --dataset files) ------------------------------------------------ */
+fmn_h5_t fmn_h5_open(const char* path);
+void fmn_h5_close(fmn_h5_t h);
+int fmn_h5_num_datasets(fmn_h5_t h);
+/* dataset i: name, numpy dtype string ("<f4", "<i8", ...), rank / shape; returns 0 */
+int fmn_h5_dataset_info(fmn_h5_t h, int i, char* name, size_t name_len, char* dtype, size_t dtype_len, int* ndims,
+                        int64_t* shape, int max_dims);
+/* copy rows [row0, row0 + nrows) of dataset `name` (row = product of the trailing dims) into dst */
+int64_t fmn_h5_read_rows(fmn_h5_t h, const char* name, int64_t row0, int64_t nrows, void* dst, size_t dst_bytes);
+
+/* ---- batch loader ring (host threads gather batches ahead of the training loop) --------------- */
+fmn_loader_t fmn_loader_create(int64_t batch, int64_t num_samples, int depth, int threads, int shuffle, uint64_t seed);
+/* a source: full dataset base[rows][row_bytes]; this rank copies bytes [col_off, col_off +
+ * col_bytes) of rows [row_lo, row_hi) of every batch into its staging slots (pitch dst_pitch) */
+int fmn_loader_add_source(fmn_loader_t l, const void* base, int64_t rows, int64_t row_bytes, int64_t col_off,
+                          int64_t col_bytes, int64_t row_lo, int64_t row_hi, int64_t dst_pitch);
+int fmn_loader_set_slot(fmn_loader_t l, int source, int slot, void* ptr);
+int fmn_loader_start(fmn_loader_t l);
+int fmn_loader_acquire(fmn_loader_t l);           /* next batch's slot (blocks) */
+int fmn_loader_release(fmn_loader_t l, int slot);
+int64_t fmn_loader_batches_per_epoch(fmn_loader_t l);
+int fmn_loader_batch_ids(fmn_loader_t l, int64_t n, int64_t* ids, int64_t max_ids);
+void fmn_loader_destroy(fmn_loader_t l);
+
+/* ---- CPU embedding-bag kernels --------------------------------------------------------------- */
+/* out[b * ld_out + d] = scale * sum_j W[idx[b * bag + j] - row_lo][d] (rows outside the shard skipped) */
+int fmn_embedding_bag_forward(const float* W, int64_t rows, int64_t D, const int64_t* idx, int64_t B, int64_t bag,
+                              int64_t row_lo, float scale, float* out, int64_t ld_out);
+/* target[idx[b * bag + j] - row_lo][d] += alpha * dy[b * ld_dy + d]  (gradient: alpha = scale;
+ * fused sparse SGD on the table: alpha = -lr * scale) */
+int fmn_embedding_bag_backward(float* target, int64_t rows, int64_t D, const int64_t* idx, int64_t B, int64_t bag,
+                               int64_t row_lo, const float* dy, int64_t ld_dy, float alpha);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FLEXMI_NATIVE_C_H */

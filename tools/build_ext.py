@@ -3,7 +3,8 @@
 
   flexmi/_C*.so       HIP kernels (csrc/kernels/*.hip, hipcc --offload-arch=gfx950, no torch
                       headers) + torch/pybind11 bindings (csrc/bindings/hip_ops.cpp)
-  flexmi/libflexmi_c.so  C API (csrc/capi/flexmi_c.h; embeds CPython)
+  flexmi/libflexmi_c.so  C API (csrc/capi/flexmi_c.h; embeds CPython for the model API)
+  flexmi/libflexmi_native_c.so  native C API (csrc/capi/flexmi_native_c.h; C++ runtime, no Python)
   flexmi/_native*.so  C++ runtime: strategy .pb codec, sharding algebra, MI355X execution
                       simulator + MCMC search, data-loader ring (csrc/runtime/*.cc, g++ -O3,
                       pybind11; no GPU dependency -- usable on the CPU box)
@@ -141,6 +142,19 @@ def write_ninja(only=None):
         lines.append(f"build {out}: cxxlink {' '.join(objs)}")
         lines.append("  ldflags = -pthread")
         targets.append(out)
+        # native C API (csrc/capi/flexmi_native_c.h): the C++ runtime without Python
+        nobjs = []
+        for src in [os.path.join(ROOT, "csrc", "capi", "flexmi_native_c.cc"), os.path.join(ROOT, "csrc", "cpu", "emb_kernels.cc"),
+                    os.path.join(ROOT, "csrc", "sim", "simulator.cc")] + [
+                os.path.join(ROOT, "csrc", "runtime", n) for n in ("hdf5_lite.cc", "loader.cc", "shard.cc", "strategy_pb.cc")]:
+            o = os.path.join(BUILD, "nc_" + os.path.basename(src).replace(".cc", ".o"))
+            lines.append(f"build {o}: cxx {src}")
+            lines.append(f"  extra = -I{ROOT}/csrc/capi")
+            nobjs.append(o)
+        nc = os.path.join(ROOT, "flexmi", "libflexmi_native_c.so")
+        lines.append(f"build {nc}: cxxlink {' '.join(nobjs)}")
+        lines.append("  ldflags = -pthread")
+        targets.append(nc)
         # C API (csrc/capi): embeds CPython, so it links libpython
         capi_src = os.path.join(ROOT, "csrc", "capi", "flexmi_c.cc")
         capi_o = os.path.join(BUILD, "capi_flexmi_c.o")
