@@ -955,4 +955,242 @@ int flexmi_dataloader_set_num_samples(flexmi_dataloader_t d, int n) {
 
 void flexmi_dataloader_destroy(flexmi_dataloader_t d) { destroy(d); }
 
+// ---------------------------------------------------------------------------------- reference-name parity
+void flexmi_sgd_optimizer_destroy(flexmi_optimizer_t o) { flexmi_optimizer_destroy(o); }
+int flexmi_sgd_optimizer_set_lr(flexmi_optimizer_t o, double lr) { return flexmi_optimizer_set_lr(o, lr); }
+void flexmi_adam_optimizer_destroy(flexmi_optimizer_t o) { flexmi_optimizer_destroy(o); }
+int flexmi_adam_optimizer_set_lr(flexmi_optimizer_t o, double lr) { return flexmi_optimizer_set_lr(o, lr); }
+flexmi_initializer_t flexmi_initializer_create_null(void) {
+  Gil g;
+  Py_INCREF(Py_None);
+  return wrap<flexmi_initializer_s>(Py_None);
+}
+void flexmi_glorot_uniform_initializer_destroy(flexmi_initializer_t i) { flexmi_initializer_destroy(i); }
+void flexmi_zero_initializer_destroy(flexmi_initializer_t i) { flexmi_initializer_destroy(i); }
+void flexmi_uniform_initializer_destroy(flexmi_initializer_t i) { flexmi_initializer_destroy(i); }
+void flexmi_norm_initializer_destroy(flexmi_initializer_t i) { flexmi_initializer_destroy(i); }
+float flexmi_per_metrics_get_accuracy(flexmi_per_metrics_t pm) { return flexmi_perf_metrics_get_accuracy(pm); }
+void flexmi_per_metrics_destroy(flexmi_per_metrics_t pm) { flexmi_perf_metrics_destroy(pm); }
+
+flexmi_tensor_t flexmi_constant_create(flexmi_model_t m, int num_dims, const int* dims, float value, int data_type) {
+  Gil g;
+  PyObject* dt = enum_value("DataType", data_type);
+  if (!dt) return nullptr;
+  return wrap<flexmi_tensor_s>(
+      call(m->o, "create_constant", Py_BuildValue("(NdN)", int_list(dims, num_dims), (double)value, dt)));
+}
+
+static PyObject* init_or_none(flexmi_initializer_t i) { return obj_or_none(i ? i->o : nullptr); }
+
+flexmi_op_t flexmi_model_add_conv2d_no_inout(flexmi_model_t m, int in_channels, int out_channels, int kh, int kw, int sh,
+                                             int sw, int ph, int pw, int act, int use_bias, flexmi_initializer_t ki,
+                                             flexmi_initializer_t bi) {
+  Gil g;
+  PyObject* a = enum_value("ActiMode", act);
+  if (!a) return nullptr;
+  // functional form conv2d(in_c, out_c, kh, kw, sh, sw, ph, pw, act, use_bias, kernel_init, bias_init)
+  return wrap<flexmi_op_s>(call(m->o, "conv2d",
+                                Py_BuildValue("(iiiiiiiiNONN)", in_channels, out_channels, kh, kw, sh, sw, ph, pw, a,
+                                              use_bias ? Py_True : Py_False, init_or_none(ki), init_or_none(bi))));
+}
+
+flexmi_op_t flexmi_model_add_pool2d_no_inout(flexmi_model_t m, int kh, int kw, int sh, int sw, int ph, int pw,
+                                             int pool_type, int act) {
+  Gil g;
+  PyObject* pt = enum_value("PoolType", pool_type);
+  PyObject* a = enum_value("ActiMode", act);
+  if (!pt || !a) {
+    Py_XDECREF(pt);
+    Py_XDECREF(a);
+    return nullptr;
+  }
+  // functional form pool2d(kh, kw, sh, sw, ph, pw, type, act)
+  return wrap<flexmi_op_s>(call(m->o, "pool2d", Py_BuildValue("(iiiiiiNN)", kh, kw, sh, sw, ph, pw, pt, a)));
+}
+
+flexmi_op_t flexmi_model_add_dense_no_inout(flexmi_model_t m, int in_dim, int out_dim, int act, int use_bias,
+                                            flexmi_initializer_t ki, flexmi_initializer_t bi) {
+  Gil g;
+  PyObject* a = enum_value("ActiMode", act);
+  if (!a) return nullptr;
+  // functional form dense(in_dim, out_dim, act, use_bias, kernel_init, bias_init)
+  return wrap<flexmi_op_s>(call(m->o, "dense", Py_BuildValue("(iiNONN)", in_dim, out_dim, a, use_bias ? Py_True : Py_False,
+                                                             init_or_none(ki), init_or_none(bi))));
+}
+
+flexmi_op_t flexmi_model_add_flat_no_inout(flexmi_model_t m) {
+  Gil g;
+  return wrap<flexmi_op_s>(call(m->o, "flat", PyTuple_New(0)));
+}
+
+flexmi_tensor_t flexmi_op_init_inout(flexmi_op_t op, flexmi_model_t m, flexmi_tensor_t input) {
+  Gil g;
+  return wrap<flexmi_tensor_s>(call(op->o, "init_inout", PyTuple_Pack(2, m->o, input->o)));
+}
+
+int flexmi_op_init(flexmi_op_t op, flexmi_model_t m) {
+  Gil g;
+  return call_status(op->o, "init", PyTuple_Pack(1, m->o));
+}
+
+int flexmi_op_forward(flexmi_op_t op, flexmi_model_t m) {
+  Gil g;
+  return call_status(m->o, "forward_op", PyTuple_Pack(1, op->o));
+}
+
+static PyObject* cfg_or_none(flexmi_config_t c) { return obj_or_none(c ? c->o : nullptr); }
+
+int flexmi_tensor_inline_map(flexmi_tensor_t t, flexmi_config_t c) {
+  Gil g;
+  return call_status(t->o, "inline_map", Py_BuildValue("(N)", cfg_or_none(c)));
+}
+
+int flexmi_tensor_inline_unmap(flexmi_tensor_t t, flexmi_config_t c) {
+  Gil g;
+  return call_status(t->o, "inline_unmap", Py_BuildValue("(N)", cfg_or_none(c)));
+}
+
+int flexmi_tensor_is_mapped(flexmi_tensor_t t) {
+  Gil g;
+  PyObject* r = call(t->o, "is_mapped", PyTuple_New(0));
+  if (!r) return -1;
+  int v = PyObject_IsTrue(r);
+  Py_DECREF(r);
+  return v;
+}
+
+static void* raw_ptr(flexmi_tensor_t t) {
+  Gil g;
+  // mapped host array first (the reference returned the mapped region's pointer)
+  PyObject* mp = PyObject_GetAttrString(t->o, "_mapped");
+  if (mp && mp != Py_None) {
+    PyObject* ct = PyObject_GetAttrString(mp, "ctypes");
+    PyObject* d = ct ? PyObject_GetAttrString(ct, "data") : nullptr;
+    void* p = d ? PyLong_AsVoidPtr(d) : nullptr;
+    Py_XDECREF(d);
+    Py_XDECREF(ct);
+    Py_DECREF(mp);
+    if (!p) capture_error("mapped pointer");
+    return p;
+  }
+  Py_XDECREF(mp);
+  PyErr_Clear();
+  PyObject* r = call(t->o, "get_raw_ptr", PyTuple_New(0));
+  if (!r) return nullptr;
+  void* p = PyLong_AsVoidPtr(r);
+  Py_DECREF(r);
+  return p;
+}
+
+float* flexmi_tensor_get_raw_ptr_float(flexmi_tensor_t t, flexmi_config_t) { return (float*)raw_ptr(t); }
+int32_t* flexmi_tensor_get_raw_ptr_int32(flexmi_tensor_t t, flexmi_config_t) { return (int32_t*)raw_ptr(t); }
+
+int flexmi_tensor_attach_raw_ptr(flexmi_tensor_t t, flexmi_config_t, void* ptr, int column_major) {
+  Gil g;
+  PyObject* model = PyObject_GetAttrString(t->o, "model");
+  if (!model) {
+    capture_error("model");
+    return -1;
+  }
+  int rc = call_status(t->o, "attach_raw_ptr",
+                       Py_BuildValue("(NNO)", model, PyLong_FromVoidPtr(ptr), column_major ? Py_True : Py_False));
+  return rc;
+}
+
+int flexmi_tensor_detach_raw_ptr(flexmi_tensor_t t, flexmi_config_t) {
+  Gil g;
+  return call_status(t->o, "detach_raw_ptr", PyTuple_New(0));
+}
+
+struct flexmi_net_config_s {
+  std::string dataset_path;
+};
+
+flexmi_net_config_t flexmi_net_config_create(void) {
+  auto* n = new flexmi_net_config_s();
+  for (size_t i = 0; i + 1 < g_argv.size(); ++i)
+    if (g_argv[i] == "--dataset" || g_argv[i] == "-d") n->dataset_path = g_argv[i + 1];
+  return n;
+}
+void flexmi_net_config_destroy(flexmi_net_config_t n) { delete n; }
+const char* flexmi_net_config_get_dataset_path(flexmi_net_config_t n) { return n ? n->dataset_path.c_str() : ""; }
+
+static flexmi_dataloader_t make_pair_loader(flexmi_model_t m, flexmi_tensor_t input, flexmi_tensor_t label, PyObject* fi,
+                                            PyObject* fl, int num_samples) {
+  PyObject* cls = attr("flexmi.core", "DataLoader2D");
+  if (!cls) {
+    Py_XDECREF(fi);
+    Py_XDECREF(fl);
+    return nullptr;
+  }
+  PyObject* o = PyObject_Call(cls, Py_BuildValue("(OOOONi)", m->o, input->o, label->o, fi, fl, num_samples), nullptr);
+  Py_DECREF(cls);
+  if (!o) capture_error("DataLoader2D");
+  return wrap<flexmi_dataloader_s>(o);
+}
+
+flexmi_dataloader_4d_t flexmi_dataloader_4d_create(flexmi_model_t m, flexmi_net_config_t n, flexmi_tensor_t input,
+                                                   flexmi_tensor_t label) {
+  Gil g;
+  if (n && !n->dataset_path.empty()) {
+    g_err = "dataloader_4d_create: dataset files are read by the HDF5 / PrefetchLoader paths (flexmi.models.dlrm)";
+    return nullptr;
+  }
+  // random synthetic data: 4 batches, uniform inputs, integer labels in [0, 10) (float labels uniform)
+  PyObject* mod = import("flexmi.core.dataloader");
+  if (!mod) return nullptr;
+  PyObject* r = call(mod, "synthetic_pair", PyTuple_Pack(3, m->o, input->o, label->o));
+  Py_DECREF(mod);
+  if (!r) return nullptr;
+  PyObject* fi = PyTuple_GetItem(r, 0);
+  PyObject* fl = PyTuple_GetItem(r, 1);
+  long ns = PyLong_AsLong(PyTuple_GetItem(r, 2));
+  Py_INCREF(fi);
+  Py_INCREF(fl);
+  Py_DECREF(r);
+  return make_pair_loader(m, input, label, fi, fl, (int)ns);
+}
+
+static PyObject* host_array(flexmi_tensor_t t) {
+  PyObject* a = call(t->o, "get_array", PyTuple_New(0));
+  return a;
+}
+
+flexmi_dataloader_4d_t flexmi_dataloader_4d_create_v2(flexmi_model_t m, flexmi_tensor_t input, flexmi_tensor_t label,
+                                                      flexmi_tensor_t full_input, flexmi_tensor_t full_label,
+                                                      int num_samples) {
+  Gil g;
+  PyObject* fi = host_array(full_input);
+  PyObject* fl = fi ? host_array(full_label) : nullptr;
+  if (!fi || !fl) {
+    Py_XDECREF(fi);
+    return nullptr;
+  }
+  return make_pair_loader(m, input, label, fi, fl, num_samples);
+}
+
+flexmi_dataloader_2d_t flexmi_dataloader_2d_create_v2(flexmi_model_t m, flexmi_tensor_t input, flexmi_tensor_t label,
+                                                      flexmi_tensor_t full_input, flexmi_tensor_t full_label,
+                                                      int num_samples) {
+  return flexmi_dataloader_4d_create_v2(m, input, label, full_input, full_label, num_samples);
+}
+
+int flexmi_dataloader_4d_next_batch(flexmi_dataloader_4d_t d, flexmi_model_t m) { return flexmi_dataloader_next_batch(d, m); }
+int flexmi_dataloader_4d_reset(flexmi_dataloader_4d_t d) { return flexmi_dataloader_reset(d); }
+int flexmi_dataloader_4d_get_num_samples(flexmi_dataloader_4d_t d) { return flexmi_dataloader_get_num_samples(d); }
+int flexmi_dataloader_4d_set_num_samples(flexmi_dataloader_4d_t d, int n) { return flexmi_dataloader_set_num_samples(d, n); }
+void flexmi_dataloader_4d_destroy(flexmi_dataloader_4d_t d) { flexmi_dataloader_destroy(d); }
+int flexmi_dataloader_2d_next_batch(flexmi_dataloader_2d_t d, flexmi_model_t m) { return flexmi_dataloader_next_batch(d, m); }
+int flexmi_dataloader_2d_reset(flexmi_dataloader_2d_t d) { return flexmi_dataloader_reset(d); }
+int flexmi_dataloader_2d_get_num_samples(flexmi_dataloader_2d_t d) { return flexmi_dataloader_get_num_samples(d); }
+int flexmi_dataloader_2d_set_num_samples(flexmi_dataloader_2d_t d, int n) { return flexmi_dataloader_set_num_samples(d, n); }
+void flexmi_dataloader_2d_destroy(flexmi_dataloader_2d_t d) { flexmi_dataloader_destroy(d); }
+int flexmi_single_dataloader_reset(flexmi_single_dataloader_t d) { return flexmi_dataloader_reset(d); }
+int flexmi_single_dataloader_get_num_samples(flexmi_single_dataloader_t d) { return flexmi_dataloader_get_num_samples(d); }
+int flexmi_single_dataloader_set_num_samples(flexmi_single_dataloader_t d, int n) {
+  return flexmi_dataloader_set_num_samples(d, n);
+}
+void flexmi_single_dataloader_destroy(flexmi_single_dataloader_t d) { flexmi_dataloader_destroy(d); }
+
 }  // extern "C"
+

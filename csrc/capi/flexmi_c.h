@@ -165,6 +165,83 @@ int flexmi_dataloader_get_num_samples(flexmi_dataloader_t d);
 int flexmi_dataloader_set_num_samples(flexmi_dataloader_t d, int n);
 void flexmi_dataloader_destroy(flexmi_dataloader_t d);
 
+/* ---- reference-name parity (python/flexflow_c.h): typed aliases and the remaining entry points */
+typedef struct flexmi_net_config_s* flexmi_net_config_t;
+typedef flexmi_dataloader_t flexmi_dataloader_2d_t;
+typedef flexmi_dataloader_t flexmi_dataloader_4d_t;
+typedef flexmi_dataloader_t flexmi_single_dataloader_t;
+typedef flexmi_perf_metrics_t flexmi_per_metrics_t;
+
+void flexmi_sgd_optimizer_destroy(flexmi_optimizer_t o);
+int flexmi_sgd_optimizer_set_lr(flexmi_optimizer_t o, double lr);
+void flexmi_adam_optimizer_destroy(flexmi_optimizer_t o);
+int flexmi_adam_optimizer_set_lr(flexmi_optimizer_t o, double lr);
+flexmi_initializer_t flexmi_initializer_create_null(void); /* "no initializer": the op's default */
+void flexmi_glorot_uniform_initializer_destroy(flexmi_initializer_t i);
+void flexmi_zero_initializer_destroy(flexmi_initializer_t i);
+void flexmi_uniform_initializer_destroy(flexmi_initializer_t i);
+void flexmi_norm_initializer_destroy(flexmi_initializer_t i);
+float flexmi_per_metrics_get_accuracy(flexmi_per_metrics_t pm);
+void flexmi_per_metrics_destroy(flexmi_per_metrics_t pm);
+
+/* constant tensor (every element = value) */
+flexmi_tensor_t flexmi_constant_create(flexmi_model_t m, int num_dims, const int* dims, float value, int data_type);
+
+/* functional ("no in/out") layers: built without an input, connected by flexmi_op_init_inout */
+flexmi_op_t flexmi_model_add_conv2d_no_inout(flexmi_model_t m, int in_channels, int out_channels, int kh, int kw, int sh,
+                                             int sw, int ph, int pw, int act, int use_bias, flexmi_initializer_t ki,
+                                             flexmi_initializer_t bi);
+flexmi_op_t flexmi_model_add_pool2d_no_inout(flexmi_model_t m, int kh, int kw, int sh, int sw, int ph, int pw,
+                                             int pool_type, int act);
+flexmi_op_t flexmi_model_add_dense_no_inout(flexmi_model_t m, int in_dim, int out_dim, int act, int use_bias,
+                                            flexmi_initializer_t ki, flexmi_initializer_t bi);
+flexmi_op_t flexmi_model_add_flat_no_inout(flexmi_model_t m);
+flexmi_tensor_t flexmi_op_init_inout(flexmi_op_t op, flexmi_model_t m, flexmi_tensor_t input);
+int flexmi_op_init(flexmi_op_t op, flexmi_model_t m);
+/* run this op's forward compute on this rank (its inputs must already be in place) */
+int flexmi_op_forward(flexmi_op_t op, flexmi_model_t m);
+
+/* host mapping of a whole logical tensor (config may be NULL) */
+int flexmi_tensor_inline_map(flexmi_tensor_t t, flexmi_config_t c);
+int flexmi_tensor_inline_unmap(flexmi_tensor_t t, flexmi_config_t c);
+int flexmi_tensor_is_mapped(flexmi_tensor_t t);
+/* mapped host data (after inline_map), else this rank's device shard */
+float* flexmi_tensor_get_raw_ptr_float(flexmi_tensor_t t, flexmi_config_t c);
+int32_t* flexmi_tensor_get_raw_ptr_int32(flexmi_tensor_t t, flexmi_config_t c);
+/* zero-copy attach of host memory holding the whole logical tensor (column_major: reversed dims) */
+int flexmi_tensor_attach_raw_ptr(flexmi_tensor_t t, flexmi_config_t c, void* raw_ptr, int column_major);
+int flexmi_tensor_detach_raw_ptr(flexmi_tensor_t t, flexmi_config_t c);
+
+/* NetConfig: --dataset of flexmi_init's argv */
+flexmi_net_config_t flexmi_net_config_create(void);
+void flexmi_net_config_destroy(flexmi_net_config_t n);
+const char* flexmi_net_config_get_dataset_path(flexmi_net_config_t n);
+
+/* input + label loaders.  create: random synthetic data (4 batches) unless the net config names a
+ * dataset; create_v2: from host tensors holding the full input / label (attached arrays) */
+flexmi_dataloader_4d_t flexmi_dataloader_4d_create(flexmi_model_t m, flexmi_net_config_t n, flexmi_tensor_t input,
+                                                   flexmi_tensor_t label);
+flexmi_dataloader_4d_t flexmi_dataloader_4d_create_v2(flexmi_model_t m, flexmi_tensor_t input, flexmi_tensor_t label,
+                                                      flexmi_tensor_t full_input, flexmi_tensor_t full_label,
+                                                      int num_samples);
+flexmi_dataloader_2d_t flexmi_dataloader_2d_create_v2(flexmi_model_t m, flexmi_tensor_t input, flexmi_tensor_t label,
+                                                      flexmi_tensor_t full_input, flexmi_tensor_t full_label,
+                                                      int num_samples);
+int flexmi_dataloader_4d_next_batch(flexmi_dataloader_4d_t d, flexmi_model_t m);
+int flexmi_dataloader_4d_reset(flexmi_dataloader_4d_t d);
+int flexmi_dataloader_4d_get_num_samples(flexmi_dataloader_4d_t d);
+int flexmi_dataloader_4d_set_num_samples(flexmi_dataloader_4d_t d, int n);
+void flexmi_dataloader_4d_destroy(flexmi_dataloader_4d_t d);
+int flexmi_dataloader_2d_next_batch(flexmi_dataloader_2d_t d, flexmi_model_t m);
+int flexmi_dataloader_2d_reset(flexmi_dataloader_2d_t d);
+int flexmi_dataloader_2d_get_num_samples(flexmi_dataloader_2d_t d);
+int flexmi_dataloader_2d_set_num_samples(flexmi_dataloader_2d_t d, int n);
+void flexmi_dataloader_2d_destroy(flexmi_dataloader_2d_t d);
+int flexmi_single_dataloader_reset(flexmi_single_dataloader_t d);
+int flexmi_single_dataloader_get_num_samples(flexmi_single_dataloader_t d);
+int flexmi_single_dataloader_set_num_samples(flexmi_single_dataloader_t d, int n);
+void flexmi_single_dataloader_destroy(flexmi_single_dataloader_t d);
+
 #ifdef __cplusplus
 }
 #endif

@@ -82,6 +82,21 @@ class DataLoader2D:
 DataLoader4D = DataLoader2D
 
 
+def synthetic_pair(ffmodel, input, label, batches=4, seed=0):
+    """Random full input / label arrays of ``batches`` batches (the reference loaders' random-data
+    mode when no dataset is given): uniform inputs, integer labels in [0, 10) (uniform floats for
+    float labels).  Returns (full_input, full_label, num_samples)."""
+    rng = np.random.RandomState(seed)
+    n = input.dims[0] * batches
+    x = rng.rand(n, *input.dims[1:]).astype(np.float32)
+    if label.data_type in (DataType.DT_INT32, DataType.DT_INT64):
+        y = rng.randint(0, 10, (n,) + tuple(label.dims[1:])).astype(np.int32 if label.data_type == DataType.DT_INT32
+                                                                      else np.int64)
+    else:
+        y = rng.rand(n, *label.dims[1:]).astype(np.float32)
+    return x, y, n
+
+
 class NetConfig:
     def __init__(self):
         self.dataset_path = ""

@@ -353,6 +353,16 @@ class FFModel:
         if not self._traced("backward"):
             self._ex().backward()
 
+    def forward_op(self, op):
+        """Run one op's forward compute on this rank (``Op::forward``, the C API's op_forward):
+        the op's compute items of the compiled forward program; its inputs must be in place."""
+        op = getattr(op, "op", None) or op
+        ex = self._ex()
+        prefix = op.name + "."
+        for it in ex.prog_fwd:
+            if it.kind == "compute" and (it.name == op.name or it.name.startswith(prefix)):
+                it.fn()
+
     def update(self):
         if not self._traced("update"):
             self._ex().update()
