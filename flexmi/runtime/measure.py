@@ -38,6 +38,9 @@ def _make_clone(op, m, in_shapes, out_shapes):
         m.conv2d(ins[0], out_shapes[0][1], op.kh, op.kw, op.sh, op.sw, op.ph, op.pw, op.activation, op.use_bias)
     elif t == OperatorType.OP_POOL2D:
         m.pool2d(ins[0], op.kh, op.kw, op.sh, op.sw, op.ph, op.pw, op.pool_type, op.activation)
+    elif t == OperatorType.OP_LSTM:
+        st = op.has_state
+        m.lstm(ins[0], op.H, ins[1] if st else None, ins[2] if st else None)
     elif isinstance(op, ElementUnary):
         m._add(ElementUnary(m, op.op_type, ins[0]))
     elif isinstance(op, ElementBinary):

@@ -102,7 +102,7 @@ def main():
     from flexmi.runtime.measure import measure_embedding_group
     m1 = build_model(a.model, 1, a.batch_per_gpu, a.device, a.dtype)
     embs = [op for op in m1.layers if op.op_type == OperatorType.OP_EMBEDDING]
-    if len(embs) > 1:
+    if len(embs) > 1 and a.model.startswith("dlrm"):   # the factor is the DLRM table group's
         iso = 0.0
         for op in embs:
             k = op_signature(op, [tuple(op.inputs[0].dims)], [tuple(op.outputs[0].dims)])
