@@ -77,6 +77,8 @@ def main():
         with open(a.out) as f:
             old = json.load(f)
         db["entries"].update(old.get("entries", {}))
+        if "group_factor" in old:                      # measured on a DLRM run; keep it
+            db["group_factor"] = old["group_factor"]
     cm = CostModel(MachineModel.mi355x(1), db_path="", dtype_bytes=4 if a.dtype == "fp32" else 2)
     t0 = time.time()
     done = 0
