@@ -361,8 +361,10 @@ __global__ void __launch_bounds__(256) fm_dot_fwd_f32(PtrTabF Z, long ldz, float
   const bool zok = r < F;
   const float* zbase = (zok ? Z.p[r] : Z.p[0]) + h * half;
   constexpr int NV = DT > 0 ? DT / 8 : 1;    // float4 per lane (k-half of DT floats)
-  // persistent waves: the next sample's rows are loaded (clamped, unconditional) before this
-  // sample's MFMAs and output write, so every wave keeps one sample of loads in flight
+  // persistent waves, one register set: zn[v] holds this sample's chunk v and is reloaded with the
+  // NEXT sample's chunk right after its four MFMAs are issued (no loop-carried register copies,
+  // which would make the compiler wait for the whole prefetch at the loop back edge).  Lanes with
+  // r >= F read row 0: their Gram rows/columns are never written out.
   f32x4_t zn[NV];
   const long b_first = blockIdx.x * (blockDim.x >> 6) + wave;
   if constexpr (DT > 0) {
@@ -374,23 +376,14 @@ __global__ void __launch_bounds__(256) fm_dot_fwd_f32(PtrTabF Z, long ldz, float
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
     if constexpr (DT > 0) {
-      f32x4_t z[NV];
-#pragma unroll
-      for (int v = 0; v < NV; ++v) z[v] = zn[v];
       const long bn = min(b + waves_total, B - 1);
 #pragma unroll
-      for (int v = 0; v < NV; ++v) zn[v] = *reinterpret_cast<const f32x4_t*>(zbase + bn * ldz + 4 * v);
-      if (!zok) {
+      for (int v = 0; v < NV; ++v) {
 #pragma unroll
-        for (int v = 0; v < NV; ++v) z[v] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int v = 0; v < NV; ++v)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(z[v][e], z[v][e], acc, 0, 0, 0);
-      if (r == 0) {
-#pragma unroll
-        for (int v = 0; v < NV; ++v) *reinterpret_cast<f32x4_t*>(row + h * half + 4 * v) = z[v];
+        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(zn[v][e], zn[v][e], acc, 0, 0, 0);
+        if (r == 0) *reinterpret_cast<f32x4_t*>(row + h * half + 4 * v) = zn[v];
+        zn[v] = *reinterpret_cast<const f32x4_t*>(zbase + bn * ldz + 4 * v);
+        __builtin_amdgcn_sched_barrier(0);   // keep the reload between this chunk's MFMAs and the next's
       }
     } else {
       for (int k = 0; k < half; ++k) {
@@ -407,7 +400,13 @@ __global__ void __launch_bounds__(256) fm_dot_fwd_f32(PtrTabF Z, long ldz, float
     }
     FM_WAVE_LDS_SYNC();
     float* o = out + b * ldo;
-    if ((W & 3) == 0 && (ldo & 3) == 0) {
+    if (DT > 0 && (W & 3) == 0 && (ldo & 3) == 0 && W <= 1024) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {     // fixed trip count: straight-line code keeps the waitcnts exact
+        const int c = lane * 4 + 256 * t;
+        if (c < W) *reinterpret_cast<f32x4_t*>(o + c) = *reinterpret_cast<const f32x4_t*>(row + c);
+      }
+    } else if ((W & 3) == 0 && (ldo & 3) == 0) {
       for (int c = lane * 4; c < W; c += 256) *reinterpret_cast<f32x4_t*>(o + c) = *reinterpret_cast<const f32x4_t*>(row + c);
     } else {
       for (int c = lane; c < W; c += 64) o[c] = row[c];
@@ -528,6 +527,135 @@ __global__ void __launch_bounds__(256) fm_dot_bwd_f32(PtrTabF Z, long ldz, const
   }
 }
 
+// fp32 backward with the B operand straight from global memory (D = 32E, E = 1/2/4): the column
+// map of N-tile e is n = E*r + e, so lane (r, h) loads Z_j[E r .. E r + E-1] of each row
+// j = 2ks + h with ONE E-float load and that register feeds the E MFMAs of step ks; the E
+// accumulators then hold C[i][E r .. E r + E-1] for the lane's 16 rows i -> E-float stores of
+// whole 32E-column rows.  No Z staging in LDS (only the dOut row, for the per-lane S gather),
+// so a wave keeps the NEXT sample's Z rows and dOut chunks in flight in registers while this
+// sample's (F+1)/2 x E MFMAs run.  Steps past F are skipped (uniform), not padded to 32.
+template <int E> struct VecF { using type = float __attribute__((ext_vector_type(E))); };
+template <> struct VecF<1> { using type = float; };
+
+template <int E, int NKS, bool ACC>
+__global__ void __launch_bounds__(256, 2) fm_dot_bwd_f32r(PtrTabF Z, long ldz, const float* __restrict__ dout, long ldo,
+                                                         MPtrTabF dZ, long lddz, unsigned acc_mask, long B, int F,
+                                                         int W, int self) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int D = 32 * E;
+  constexpr int DCH = 4;                           // dOut float4 chunks per lane (W <= 1024)
+  using vecE = typename VecF<E>::type;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wpad = (W + 3) & ~3;
+  float* ds = reinterpret_cast<float*>(smem) + (long)wave * wpad;
+  const int waves_total = gridDim.x * (blockDim.x >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  // A operand positions: S[r][j = 2ks + h]; j >= F -> 0 (the B row loaded for it is row F-1)
+  short apos[NKS];
+  unsigned dmask = 0;
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    const int j = 2 * ks + h;
+    int pos = -1;
+    if (r < F && j < F) {
+      if (r > j) pos = pair_pos(r, j, self);
+      else if (j > r) pos = pair_pos(j, r, self);
+      else if (self) {
+        pos = pair_pos(r, r, self);
+        dmask |= 1u << ks;
+      }
+    }
+    apos[ks] = (short)pos;
+  }
+  // zn[ks] holds row 2ks+h of the CURRENT sample; right after its E MFMAs are issued it is
+  // reloaded with the NEXT sample's row (one register set; the loads overlap the remaining
+  // steps and the stores).  All loops have compile-time trip counts (NKS steps, rows >= F
+  // clamped) so the compiler's vmcnt waits stay exact instead of draining the prefetch.
+  vecE zn[NKS];
+  f32x4_t dn[DCH];
+  auto load_row = [&](long bb, int ks) {
+    const float* p0 = Z.p[min(2 * ks, F - 1)];
+    const float* p1 = Z.p[min(2 * ks + 1, F - 1)];
+    zn[ks] = *reinterpret_cast<const vecE*>((h ? p1 : p0) + bb * ldz + E * r);
+  };
+  auto load_dout = [&](long bb) {
+#pragma unroll
+    for (int t = 0; t < DCH; ++t) {
+      const int c = 4 * (lane + 64 * t);
+      dn[t] = *reinterpret_cast<const f32x4_t*>(dout + bb * ldo + (c < W ? c : 0));
+    }
+  };
+  const long b_first = blockIdx.x * (blockDim.x >> 6) + wave;
+  {
+    const long b0 = min(b_first, B - 1);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) load_row(b0, ks);
+    load_dout(b0);
+  }
+  for (long b = b_first; b < B; b += waves_total) {
+    const long bn = min(b + waves_total, B - 1);
+#pragma unroll
+    for (int t = 0; t < DCH; ++t) {
+      const int c = 4 * (lane + 64 * t);
+      if (c < W) *reinterpret_cast<f32x4_t*>(ds + c) = dn[t];
+    }
+    FM_WAVE_LDS_SYNC();
+    load_dout(bn);
+    const float* dp = ds + D;
+    float a[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int pos = apos[ks];
+      float v = dp[pos < 0 ? 0 : pos];
+      v = pos < 0 ? 0.f : v;
+      if ((dmask >> ks) & 1u) v *= 2.f;
+      a[ks] = v;
+    }
+    const vecE x0 = *reinterpret_cast<const vecE*>(ds + E * r);   // dZ_0 += dOut[:, :D]
+    f32x16_t acc[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+#pragma unroll
+      for (int t = 0; t < 16; ++t) acc[e][t] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        float bz;
+        if constexpr (E == 1) bz = zn[ks];
+        else bz = zn[ks][e];
+        acc[e] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[ks], bz, acc[e], 0, 0, 0);
+      }
+      load_row(bn, ks);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int i0 = (t & 3) + 8 * (t >> 2);
+      if (i0 >= F) continue;                                   // uniform
+      const int i = i0 + 4 * h;
+      float* q0 = dZ.p[i0];
+      float* q1 = dZ.p[i0 + 4];
+      float* q = h ? q1 : q0;
+      vecE v;
+      if constexpr (E == 1) v = acc[0][t];
+      else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[e] = acc[e][t];
+      }
+      if (i == 0) v += x0;
+      if (i < F && q != nullptr) {
+        float* d = q + b * lddz + E * r;
+        if constexpr (ACC) {
+          if ((acc_mask >> i) & 1u) v += *reinterpret_cast<const vecE*>(d);
+        }
+        *reinterpret_cast<vecE*>(d) = v;
+      }
+    }
+    FM_WAVE_LDS_SYNC();
+  }
+}
+
 FM_HOST_DEVICE bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // persistent-grid size of the interaction kernels (4 waves per block; each wave loops over
@@ -572,6 +700,24 @@ extern "C" void fm_dot_interaction_bwd_f32(const float* const* z, int F, long ld
   const int Dp = (D + 31) & ~31;
   bool fast = (D == 16 || D == 32 || D == 64 || D == 128) && ldz % 4 == 0 && ldo % 4 == 0 && al16(dout) && W <= 1024;
   for (int i = 0; i < F; ++i) fast = fast && al16(z[i]);
+  if ((D == 32 || D == 64 || D == 128) && ldo % 4 == 0 && al16(dout) && W <= 1024) {
+    const int E = D / 32;
+    auto alE = [&](const void* q) { return ((uintptr_t)q & (4 * E - 1)) == 0; };
+    bool ok = ldz % E == 0 && lddz % E == 0;
+    for (int i = 0; i < F; ++i) ok = ok && alE(z[i]) && (dz[i] == nullptr || alE(dz[i]));
+    if (ok) {
+      const int wpad = (W + 3) & ~3;
+      const bool acc = acc_mask != 0;
+      const bool k14 = E == 4 && (F + 1) / 2 == 14 && !acc;   // DLRM: 26 tables + dense (F = 27)
+      auto k = k14 ? fm_dot_bwd_f32r<4, 14, false>
+             : E == 4 ? (acc ? fm_dot_bwd_f32r<4, 16, true> : fm_dot_bwd_f32r<4, 16, false>)
+             : E == 2 ? (acc ? fm_dot_bwd_f32r<2, 16, true> : fm_dot_bwd_f32r<2, 16, false>)
+                      : (acc ? fm_dot_bwd_f32r<1, 16, true> : fm_dot_bwd_f32r<1, 16, false>);
+      hipLaunchKernelGGL(k, dim3((int)blocks), dim3(64 * waves), (size_t)waves * wpad * 4, s, t, ldz, dout, ldo, g, lddz,
+                         acc_mask, B, F, W, self);
+      return;
+    }
+  }
   const int Wr = fast ? ((W + 3) & ~3) : W;        // the vector path stages whole 16-B chunks
   const size_t lds = (size_t)waves * (32 * Dp + ((Wr + 3) & ~3)) * 4;
   auto k = !fast ? fm_dot_bwd_f32<0> : D == 128 ? fm_dot_bwd_f32<128> : D == 64 ? fm_dot_bwd_f32<64>

@@ -151,7 +151,8 @@ def test_act_bwd_bias_f32(gpu):
         assert rel_err(db, ref.sum(0)) < TOL
 
 
-@pytest.mark.parametrize("F,D,selfi", [(27, 128, False), (27, 16, False), (9, 64, True), (5, 24, False), (32, 32, False)])
+@pytest.mark.parametrize("F,D,selfi", [(27, 128, False), (27, 16, False), (9, 64, True), (5, 24, False), (32, 32, False),
+                                       (28, 128, True), (2, 64, False), (27, 32, True)])
 def test_dot_interaction_f32(gpu, F, D, selfi):
     from flexmi.ops import _kernels as Kk
     torch.manual_seed(9)
