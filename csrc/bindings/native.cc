@@ -6,6 +6,7 @@
 
 #include "hdf5_lite.h"
 #include "loader.h"
+#include "planner.h"
 #include "shard.h"
 #include "strategy_pb.h"
 
@@ -93,6 +94,38 @@ PYBIND11_MODULE(_native, m) {
     for (auto& x : boxes) b.push_back(x ? *x : flexmi::Box{});
     return flexmi::split_launches(dst, b, max_per_launch);
   });
+
+  // graph planner (csrc/runtime/planner.h): op = (guid, [input], [output guid]) with
+  // input = (tensor, producer, dtype, need, is_float, needs_grad, reshard, remote);
+  // returns (order, fwd, bwd_live, grad_needed, bwd) with steps (kind, op guid, [input idx])
+  using PyIn = std::tuple<int64_t, int64_t, int, int64_t, bool, bool, bool, bool>;
+  using PyOp = std::tuple<int64_t, std::vector<PyIn>, std::vector<int64_t>>;
+  m.def("plan_graph", [](const std::vector<PyOp>& ops, int world, bool input_grads) {
+    std::vector<flexmi::PlanOp> v;
+    v.reserve(ops.size());
+    for (auto& o : ops) {
+      flexmi::PlanOp op;
+      op.guid = std::get<0>(o);
+      for (auto& t : std::get<1>(o)) {
+        flexmi::PlanInput in;
+        std::tie(in.tensor, in.producer, in.dtype, in.need, in.is_float, in.needs_grad, in.reshard, in.remote) = t;
+        op.inputs.push_back(in);
+      }
+      op.outputs = std::get<2>(o);
+      v.push_back(std::move(op));
+    }
+    flexmi::GraphPlan p;
+    {
+      py::gil_scoped_release nogil;
+      p = flexmi::plan_graph(v, world, input_grads);
+    }
+    auto steps = [](const std::vector<flexmi::PlanStep>& s) {
+      std::vector<std::tuple<int, int64_t, std::vector<int>>> out;
+      for (auto& x : s) out.emplace_back(x.kind, x.op, x.inputs);
+      return out;
+    };
+    return py::make_tuple(p.order, steps(p.fwd), p.bwd_live, p.grad_needed, steps(p.bwd));
+  }, py::arg("ops"), py::arg("world"), py::arg("input_grads") = false);
 
   // minimal HDF5 reader (csrc/runtime/hdf5_lite.h): datasets with their dtype, shape and the byte
   // offset of their contiguous data (memory-mapped by flexmi.utils.hdf5)

@@ -258,7 +258,10 @@ FM_DEVICE void epilogue_f32(const GemmF& p, const f32x4_t (&acc)[MR][NR], int zb
   }
 }
 
-template <int BM, int BN, bool AK, bool BKC, bool VEC>
+// OPT (tuning variants, FM_GEMM_F32_VARIANT bits 4/8): 1 = s_setprio(1) around each MFMA cluster;
+// 2 = fragment double buffer: the next k-chunk's LDS fragments are read before this chunk's MFMAs
+// and interleaved with them (sched_group_barrier), so only the first chunk of a K tile waits on LDS.
+template <int BM, int BN, bool AK, bool BKC, bool VEC, int OPT = 0>
 __global__ void __launch_bounds__(NTF, 2) fm_gemm_f32_kernel(GemmF p) {
   constexpr int A_BYTES = BM * BKF * 4;
   constexpr int B_BYTES = BN * BKF * 4;
@@ -305,6 +308,9 @@ __global__ void __launch_bounds__(NTF, 2) fm_gemm_f32_kernel(GemmF p) {
     if (rowsum) sa.accumulate_rows(rs);
   }
   __syncthreads();
+  if constexpr ((OPT & 4) != 0) {   // experiment: de-phase co-resident blocks by ~half a K tile
+    if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(64);
+  }
   for (int kt = kt0; kt < kt1; ++kt) {
     const int cur = (kt - kt0) & 1;
     const bool more = kt + 1 < kt1;
@@ -312,11 +318,43 @@ __global__ void __launch_bounds__(NTF, 2) fm_gemm_f32_kernel(GemmF p) {
       sa.load(A, p.lda, m0, p.M, (kt + 1) * BKF, p.K, tid);
       sb.load(B, p.ldb, n0, p.N, (kt + 1) * BKF, p.K, tid);
     }
+    if constexpr ((OPT & 2) != 0) {
+      float af0[MR][4], bf0[NR][4], af1[MR][4], bf1[NR][4];
+      load_frags<AK, BM, MR>(LDSF_A(cur), wm * (BM / 2), 0, lane, af0);
+      load_frags<BKC, BN, NR>(LDSF_B(cur), wn * (BN / 2), 0, lane, bf0);
+      load_frags<AK, BM, MR>(LDSF_A(cur), wm * (BM / 2), 1, lane, af1);
+      load_frags<BKC, BN, NR>(LDSF_B(cur), wn * (BN / 2), 1, lane, bf1);
+      if constexpr ((OPT & 1) != 0) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+#pragma unroll
+          for (int j = 0; j < NR; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(bf0[j][s], af0[i][s], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+#pragma unroll
+          for (int j = 0; j < NR; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(bf1[j][s], af1[i][s], acc[i][j], 0, 0, 0);
+      if constexpr ((OPT & 1) != 0) __builtin_amdgcn_s_setprio(0);
+      // first chunk's reads, then one ds_read per MFMA for the second chunk's fragments
+      __builtin_amdgcn_sched_group_barrier(0x100, MR + NR, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+#pragma unroll
+      for (int x = 0; x < MR + NR; ++x) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      }
+    } else {
 #pragma unroll
     for (int kk = 0; kk < BKF / 16; ++kk) {
       float af[MR][4], bfr[NR][4];
       load_frags<AK, BM, MR>(LDSF_A(cur), wm * (BM / 2), kk, lane, af);
       load_frags<BKC, BN, NR>(LDSF_B(cur), wn * (BN / 2), kk, lane, bfr);
+      if constexpr ((OPT & 1) != 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -324,6 +362,8 @@ __global__ void __launch_bounds__(NTF, 2) fm_gemm_f32_kernel(GemmF p) {
 #pragma unroll
           for (int j = 0; j < NR; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(bfr[j][s], af[i][s], acc[i][j], 0, 0, 0);
+      if constexpr ((OPT & 1) != 0) __builtin_amdgcn_s_setprio(0);
+    }
     }
     if (more) {
       sa.store(LDSF_A(cur ^ 1), tid);
@@ -380,24 +420,35 @@ __global__ void fm_gemm_f32_reduce(GemmF p, int v4) {
 }
 
 template <int BM, int BN, bool AK, bool BKC, bool VEC>
-void launch_f(const GemmF& p, hipStream_t s) {
+void launch_f(const GemmF& p, hipStream_t s, int opt) {
   constexpr int LDS = 2 * (BM + BN) * BKF * 4;
   dim3 grid(p.tiles_m * p.tiles_n, p.batch, p.ksplit);
-  hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC>), grid, dim3(NTF), LDS, s, p);
+  if (VEC && BM == 128 && BN == 128 && opt == 1)
+    hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 1>), grid, dim3(NTF), LDS, s, p);
+  else if (VEC && BM == 128 && BN == 128 && opt == 2)
+    hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 2>), grid, dim3(NTF), LDS, s, p);
+  else if (VEC && BM == 128 && BN == 128 && opt == 3)
+    hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 3>), grid, dim3(NTF), LDS, s, p);
+  else if (VEC && BM == 128 && BN == 128 && opt == 4)
+    hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 4>), grid, dim3(NTF), LDS, s, p);
+  else if (VEC && BM == 128 && BN == 128 && opt == 6)
+    hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 6>), grid, dim3(NTF), LDS, s, p);
+  else
+    hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC>), grid, dim3(NTF), LDS, s, p);
 }
 
 template <int BM, int BN>
-void launch_fbm(const GemmF& p, bool ak, bool bk, bool vec, hipStream_t s) {
+void launch_fbm(const GemmF& p, bool ak, bool bk, bool vec, hipStream_t s, int opt) {
   if (vec) {
-    if (ak && bk) launch_f<BM, BN, true, true, true>(p, s);
-    else if (ak) launch_f<BM, BN, true, false, true>(p, s);
-    else if (bk) launch_f<BM, BN, false, true, true>(p, s);
-    else launch_f<BM, BN, false, false, true>(p, s);
+    if (ak && bk) launch_f<BM, BN, true, true, true>(p, s, opt);
+    else if (ak) launch_f<BM, BN, true, false, true>(p, s, opt);
+    else if (bk) launch_f<BM, BN, false, true, true>(p, s, opt);
+    else launch_f<BM, BN, false, false, true>(p, s, opt);
   } else {
-    if (ak && bk) launch_f<BM, BN, true, true, false>(p, s);
-    else if (ak) launch_f<BM, BN, true, false, false>(p, s);
-    else if (bk) launch_f<BM, BN, false, true, false>(p, s);
-    else launch_f<BM, BN, false, false, false>(p, s);
+    if (ak && bk) launch_f<BM, BN, true, true, false>(p, s, 0);
+    else if (ak) launch_f<BM, BN, true, false, false>(p, s, 0);
+    else if (bk) launch_f<BM, BN, false, true, false>(p, s, 0);
+    else launch_f<BM, BN, false, false, false>(p, s, 0);
   }
 }
 
@@ -652,9 +703,10 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
   if (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks = 1;
   if (K <= 0) ks = 1;
   p.ksplit = ks;
-  if (BNv == 128) launch_fbm<128, 128>(p, a_kcontig, b_kcontig, vec, stream);
-  else if (BMv == 128) launch_fbm<128, 64>(p, a_kcontig, b_kcontig, vec, stream);
-  else launch_fbm<64, 64>(p, a_kcontig, b_kcontig, vec, stream);
+  const int opt = (variant >> 2) & 7;
+  if (BNv == 128) launch_fbm<128, 128>(p, a_kcontig, b_kcontig, vec, stream, opt);
+  else if (BMv == 128) launch_fbm<128, 64>(p, a_kcontig, b_kcontig, vec, stream, 0);
+  else launch_fbm<64, 64>(p, a_kcontig, b_kcontig, vec, stream, 0);
   if (ks > 1) {
     const int v4 = (N % 4 == 0) && (ldc % 4 == 0) && (sC % 4 == 0) && al(C);
     const long total = (long)M * N * batch / (v4 ? 4 : 1);

@@ -720,7 +720,9 @@ class Executor:
             for t in op.inputs + op.outputs:
                 self.tensors[t.guid] = t
         self.final_op = ops[-1]
-        ops = self._comm_first_order(ops)
+        plan = self._native_plan(ops)
+        by_guid = {op.guid: op for op in ops}
+        ops = [by_guid[g] for g in plan[0]]
         self.ops = ops
 
         # ---- activation buffers ------------------------------------------------
@@ -742,52 +744,37 @@ class Executor:
                     src = self.act[(x.guid, need.key())]
                     self.act[(out.guid, olay.key())] = src.view(olay.local_shape(self.rank))
 
-        # ---- forward/backward schedules ----------------------------------------
+        # ---- forward/backward schedules (graph planner: csrc/runtime/planner.cc) ---
         self.fwd_steps = []
         self.bwd_steps = []
-        made = set()
-        for op in ops:
-            pc = self.pcs[op.guid]
-            group = defaultdict(list)   # dtype -> reshards of this op's inputs (one all_to_all each)
-            for i, t in enumerate(op.inputs):
-                need = self.need[(op.guid, i)]
-                home = self.home[t.guid]
-                if not need.same_as(home):
-                    key = (t.guid, need.key())
-                    if key in made:
-                        continue
-                    made.add(key)
-                    if key not in self.act and need.local_shape(self.rank) is not None:
-                        self.act[key] = self._alloc(need.local_shape(self.rank), self._storage_dtype(t))
-                    dt = self._storage_dtype(t)
-                    group[dt].append((t.guid, home, need, ReshardStep(ReshardPlan(home, need), self.rank, self.world, dt, self.device)))
-            for dt, lst in group.items():
-                self.fwd_steps.append(("reshard", lst))
-            self.fwd_steps.append(("op", op))
+        for kind, g, idxs in plan[1]:
+            op = by_guid[g]
+            if kind == 0:
+                self.fwd_steps.append(("op", op))
+                continue
+            lst = []
+            for i in idxs:
+                t = op.inputs[i]
+                need, home = self.need[(op.guid, i)], self.home[t.guid]
+                key = (t.guid, need.key())
+                if key not in self.act and need.local_shape(self.rank) is not None:
+                    self.act[key] = self._alloc(need.local_shape(self.rank), self._storage_dtype(t))
+                dt = self._storage_dtype(t)
+                lst.append((t.guid, home, need, ReshardStep(ReshardPlan(home, need), self.rank, self.world, dt, self.device)))
+            self.fwd_steps.append(("reshard", lst))
 
-        # grads: home-layout grad buffers for float tensors that need them
-        # backward liveness: an op runs backward only when one of its outputs reaches the loss;
-        # its float inputs then need gradients (graph inputs only when asked, e.g. for the cost
-        # measurement of a single op).  Dead branches (an encoder's unused top output) are skipped.
+        # grads: home-layout grad buffers for float tensors that need them.  Backward liveness
+        # (planner): an op runs backward only when one of its outputs reaches the loss; its float
+        # inputs then need gradients (graph inputs only when asked, e.g. for the cost measurement of
+        # a single op).  Dead branches (an encoder's unused top output) are skipped.
         final = self.final_op.outputs[0]
         self.final = final
-        self.grad_needed = {final.guid}
-        self.bwd_live = set()
-        for op in reversed(ops):
-            if not any(o.guid in self.grad_needed for o in op.outputs):
-                continue
-            self.bwd_live.add(op.guid)
-            for i, t in enumerate(op.inputs):
-                src_ok = t.owner_op is not None or getattr(self.cfg, "input_grads", False)
-                if src_ok and op.needs_input_grad(i) and _is_float(t.data_type):
-                    self.grad_needed.add(t.guid)
+        self.bwd_live = set(plan[2])
+        self.grad_needed = set(plan[3])
         for g in self.grad_needed:
             lay = self.home[g]
             shp = lay.local_shape(self.rank)
             if shp is not None:
-                key = (g, lay.key())
-                if getattr(self.tensors[g].owner_op, "is_view", False) and key in self.act:
-                    pass
                 self.grad[g] = self._alloc(shp, self.cdtype)
         # grads of view-op outputs alias the input grad buffer
         self.galias = {}
@@ -798,27 +785,24 @@ class Executor:
                     self.grad[out.guid] = self.grad[x.guid].view(self.grad[out.guid].shape)
                     self.galias[out.guid] = self.gkey(x.guid)
         self.tmp_grad: Dict[tuple, torch.Tensor] = {}
-        for op in reversed(ops):
-            if op.guid not in self.bwd_live:
+        for kind, g, idxs in plan[4]:
+            op = by_guid[g]
+            if kind == 0:
+                self.bwd_steps.append(("op", op))
                 continue
-            self.bwd_steps.append(("op", op))
             red = []
-            for i, t in enumerate(op.inputs):
-                if t.guid not in self.grad_needed or not op.needs_input_grad(i):
-                    continue
-                need = self.need[(op.guid, i)]
-                home = self.home[t.guid]
-                if not need.same_as(home):
-                    shp = need.local_shape(self.rank)
-                    if shp is not None:
-                        self.tmp_grad[(op.guid, i)] = self._alloc(shp, self.cdtype)
-                    # the gradient of a partial-sum output (row-sharded embedding) is the FULL
-                    # gradient on every holder: reduce into home.as_full()
-                    red.append((op, i, t.guid,
-                                ReshardStep(ReshardPlan(need.as_partial(), home.as_full()), self.rank, self.world,
-                                            self.cdtype, self.device)))
-            if red:
-                self.bwd_steps.append(("reduce", red))
+            for i in idxs:
+                t = op.inputs[i]
+                need, home = self.need[(op.guid, i)], self.home[t.guid]
+                shp = need.local_shape(self.rank)
+                if shp is not None:
+                    self.tmp_grad[(op.guid, i)] = self._alloc(shp, self.cdtype)
+                # the gradient of a partial-sum output (row-sharded embedding) is the FULL
+                # gradient on every holder: reduce into home.as_full()
+                red.append((op, i, t.guid,
+                            ReshardStep(ReshardPlan(need.as_partial(), home.as_full()), self.rank, self.world,
+                                        self.cdtype, self.device)))
+            self.bwd_steps.append(("reduce", red))
 
         # ---- weights ------------------------------------------------------------
         self._build_weights(ops)
@@ -864,52 +848,35 @@ class Executor:
         self.adam_state = torch.tensor([1.0, 1.0, 0.0], dtype=torch.float32, device=self.device)
         self._compile_program()
 
-    def _comm_first_order(self, ops):
-        """Topological op order that runs the producers of cross-device reshards (and their
-        ancestors) as early as possible, so the asynchronous exchanges started after them
-        overlap the remaining independent ops (DLRM: embeddings first, their all_to_all hides
-        behind the bottom MLP; in backward the bottom MLP then hides the gradient exchange).
-        Depends only on the graph and layouts, so every rank derives the same order (the
-        collectives must be issued in the same order everywhere)."""
-        if self.world == 1:
-            return list(ops)
-        prod = {t.guid: op for op in ops for t in op.outputs}
-        idx = {op.guid: k for k, op in enumerate(ops)}
-        deps = {op.guid: {prod[t.guid].guid for t in op.inputs if t.guid in prod} for op in ops}
-        hot = set()
+    def _native_plan(self, ops):
+        """Graph-level plan from the native planner (csrc/runtime/planner.cc, flexmi._native):
+        the communication-first topological order (producers of cross-device reshards and their
+        ancestors first, so the asynchronous exchanges started after them overlap the remaining
+        independent ops: DLRM embeddings first, their all-to-all hides behind the bottom MLP),
+        the forward schedule (input reshards per dtype, each (tensor, layout) once, then the op),
+        backward liveness and the backward schedule (live ops in reverse, each followed by the
+        gradient reduce of its resharded inputs).  Depends only on the graph and layouts, so every
+        rank derives the same plan (collectives are issued in the same order everywhere).
+        Reference: the op walk of FFModel::compile / the task launches of forward/backward,
+        src/runtime/model.cc:374-1180."""
+        from flexmi import _native
+        producer = {t.guid: op.guid for op in ops for t in op.outputs}
+        need_ids, dt_ids = {}, {}
+        spec = []
         for op in ops:
+            ins = []
             for i, t in enumerate(op.inputs):
-                if t.guid not in prod:
-                    continue
                 need, home = self.need[(op.guid, i)], self.home[t.guid]
-                if not need.same_as(home) and any(tr.src != tr.dst for tr in ReshardPlan(home, need).transfers):
-                    hot.add(prod[t.guid].guid)
-        stack = list(hot)
-        while stack:
-            g = stack.pop()
-            for d in deps[g]:
-                if d not in hot:
-                    hot.add(d)
-                    stack.append(d)
-        by_guid = {op.guid: op for op in ops}
-        indeg = {g: len(d) for g, d in deps.items()}
-        users = defaultdict(list)
-        for g, d in deps.items():
-            for x in d:
-                users[x].append(g)
-        import heapq
-        ready = [(0 if op.guid in hot else 1, idx[op.guid], op.guid) for op in ops if indeg[op.guid] == 0]
-        heapq.heapify(ready)
-        out = []
-        while ready:
-            _, _, g = heapq.heappop(ready)
-            out.append(by_guid[g])
-            for u in users[g]:
-                indeg[u] -= 1
-                if indeg[u] == 0:
-                    heapq.heappush(ready, (0 if u in hot else 1, idx[u], u))
-        assert len(out) == len(ops), "graph has a cycle"
-        return out
+                reshard = not need.same_as(home)
+                prod = producer.get(t.guid, -1)
+                remote = (reshard and prod >= 0 and self.world > 1
+                          and any(tr.src != tr.dst for tr in ReshardPlan(home, need).transfers))
+                nid = need_ids.setdefault(need.key(), len(need_ids))
+                did = dt_ids.setdefault(self._storage_dtype(t), len(dt_ids))
+                ins.append((t.guid, prod, did, nid, _is_float(t.data_type), bool(op.needs_input_grad(i)),
+                            reshard, remote))
+            spec.append((op.guid, ins, [o.guid for o in op.outputs]))
+        return _native.plan_graph(spec, self.world, bool(getattr(self.cfg, "input_grads", False)))
 
     def _build_epilogue_fusion(self, ops):
         """Linear L1 -> Linear L2 (L1's output consumed only by L2, same layout): L2's dX GEMM
