@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Train any zoo model on synthetic data and print the reference's throughput line.
 
-    python apps/train.py alexnet -b 256 -e 1 [--iterations 20] [--small] [reference FFConfig flags]
+    python apps/train.py alexnet -b 256 -e 1 [--iterations 20] [--small] [--image-dir DIR] [reference FFConfig flags]
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 apps/train.py inception_v3 -b 64 --budget 2000
 
 Mirrors the reference apps (examples/cpp/{AlexNet,InceptionV3,ResNet,candle_uno,DLRM}): the random
@@ -29,6 +29,9 @@ def main(argv=None):
     ap.add_argument("--iterations", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--graph", action="store_true", help="replay the step as hipGraph segments")
+    ap.add_argument("--image-dir", default=None,
+                    help="ImageNet-style folder (one sub-directory per class): decode + GPU-normalize a new "
+                         "batch every iteration (flexmi.utils.images) instead of the reused random batch")
     a, rest = ap.parse_known_args(argv)
 
     import numpy as np
@@ -67,11 +70,23 @@ def main(argv=None):
         else:
             ex.scatter_from_host(lab, rng.rand(*lab.dims).astype(np.float32))
     sync = (lambda: torch.cuda.synchronize()) if ex.backend == "hip" else (lambda: None)
+    loader = None
+    if a.image_dir:
+        from flexmi.utils.images import ImageFolderLoader
+        img = next(t for t in built.inputs.values() if len(t.dims) == 4)
+        loader = ImageFolderLoader(model, img, model.get_label_tensor(), a.image_dir, shuffle=True, seed=comm.rank)
+        loader.next_batch()
     for _ in range(a.warmup):
         ex.train_step()
     step = ex.train_step
     if a.graph and ex.backend == "hip":
         step = ex.capture_step()
+    if loader is not None:
+        inner = step
+
+        def step():
+            loader.next_batch()
+            inner()
     sync()
     comm.barrier()
     t0 = time.perf_counter()

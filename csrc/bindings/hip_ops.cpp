@@ -8,6 +8,8 @@
 #include <vector>
 
 extern "C" {
+void fm_image_normalize(const unsigned char* src, void* dst, long N, int H, int W, const float* mean, const float* stdv,
+                        int bf16, hipStream_t s);
 void fm_gemm_set_variant(int v);
 void fm_gemm_f32_set_variant(int v);
 int fm_gemm(const void* A, long lda, long sA, int a_kcontig, const void* B, long ldb, long sB, int b_kcontig, void* C,
@@ -428,6 +430,23 @@ void act_bwd_bias(torch::Tensor y, torch::Tensor dy, c10::optional<torch::Tensor
   if (dpre.has_value() && dpre->defined()) TORCH_CHECK(dpre->scalar_type() == y.scalar_type(), "act_bwd_bias: dpre dtype");
   fm_act_bwd_bias(y.data_ptr(), dy.data_ptr(), mptr(dpre), (float*)mptr(db), B, (int)N, (int)act, is_bf16(y), cur());
 }
+// uint8 [N][H][W][3] decoded RGB -> normalized [N][3][H][W] fp32 / bf16 (image.hip)
+void image_normalize(torch::Tensor src, torch::Tensor dst, std::vector<double> mean, std::vector<double> stdv) {
+  check_cuda(src, "src");
+  check_cuda(dst, "dst");
+  TORCH_CHECK(src.scalar_type() == torch::kUInt8 && src.dim() == 4 && src.size(3) == 3 && src.is_contiguous(),
+              "image_normalize: src must be contiguous uint8 [N][H][W][3]");
+  TORCH_CHECK(dst.dim() == 4 && dst.size(0) == src.size(0) && dst.size(1) == 3 && dst.size(2) == src.size(1) &&
+                  dst.size(3) == src.size(2) && dst.is_contiguous(),
+              "image_normalize: dst must be contiguous [N][3][H][W] matching src");
+  TORCH_CHECK(dst.scalar_type() == torch::kFloat32 || dst.scalar_type() == torch::kBFloat16, "image_normalize: fp32/bf16 dst");
+  TORCH_CHECK(mean.size() == 3 && stdv.size() == 3, "image_normalize: 3 means and 3 stds");
+  const float m[3] = {(float)mean[0], (float)mean[1], (float)mean[2]};
+  const float sd[3] = {(float)stdv[0], (float)stdv[1], (float)stdv[2]};
+  fm_image_normalize(src.data_ptr<uint8_t>(), dst.data_ptr(), src.size(0), (int)src.size(1), (int)src.size(2), m, sd,
+                     dst.scalar_type() == torch::kBFloat16, cur());
+}
+
 void multi_copy(std::vector<torch::Tensor> src, std::vector<int64_t> src_off, std::vector<torch::Tensor> dst,
                 std::vector<int64_t> dst_off, std::vector<int64_t> rows, std::vector<int64_t> cols, std::vector<int64_t> lds,
                 std::vector<int64_t> ldd, int64_t add_mask) {
@@ -735,6 +754,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("binary_bwd", &binary_bwd);
   m.def("act_bwd_bias", &act_bwd_bias);
   m.def("multi_copy", &multi_copy);
+  m.def("image_normalize", &image_normalize);
   m.def("permute", &permute);
   m.def("reverse", &reverse);
   m.def("softmax", &softmax);

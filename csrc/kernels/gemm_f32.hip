@@ -423,18 +423,16 @@ template <int BM, int BN, bool AK, bool BKC, bool VEC>
 void launch_f(const GemmF& p, hipStream_t s, int opt) {
   constexpr int LDS = 2 * (BM + BN) * BKF * 4;
   dim3 grid(p.tiles_m * p.tiles_n, p.batch, p.ksplit);
-  if (VEC && BM == 128 && BN == 128 && opt == 1)
-    hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 1>), grid, dim3(NTF), LDS, s, p);
-  else if (VEC && BM == 128 && BN == 128 && opt == 2)
-    hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 2>), grid, dim3(NTF), LDS, s, p);
-  else if (VEC && BM == 128 && BN == 128 && opt == 3)
-    hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 3>), grid, dim3(NTF), LDS, s, p);
-  else if (VEC && BM == 128 && BN == 128 && opt == 4)
-    hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 4>), grid, dim3(NTF), LDS, s, p);
-  else if (VEC && BM == 128 && BN == 128 && opt == 6)
-    hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 6>), grid, dim3(NTF), LDS, s, p);
-  else
-    hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC>), grid, dim3(NTF), LDS, s, p);
+  if constexpr (VEC && BM == 128 && BN == 128) {   // tuning variants only on the main tile
+    switch (opt) {
+      case 1: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 1>), grid, dim3(NTF), LDS, s, p); return;
+      case 2: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 2>), grid, dim3(NTF), LDS, s, p); return;
+      case 4: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 4>), grid, dim3(NTF), LDS, s, p); return;
+      case 6: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 6>), grid, dim3(NTF), LDS, s, p); return;
+      default: break;
+    }
+  }
+  hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC>), grid, dim3(NTF), LDS, s, p);
 }
 
 template <int BM, int BN>

@@ -44,12 +44,13 @@ enum Kind : int {
   RS_START = 6,    // _reduce_scatter_base(out, in) -> slot       (ZeRO-1 gradient shard sync)
   RS_SYNC = 7,     // wait(slot) if pending, else reduce-scatter + wait
   AG_SYNC = 8,     // _allgather_base(out, in) + wait             (ZeRO-1 parameter gather)
+  P2P_START = 9,   // grouped send/recv with the peers of non-zero splits only -> slot
 };
 
 const char* kind_name(int k) {
   static const char* n[] = {"call", "graph", "all_to_all", "all_reduce", "wait", "all_reduce_sync",
-                            "reduce_scatter", "reduce_scatter_sync", "all_gather_sync"};
-  return (k >= 0 && k <= 8) ? n[k] : "?";
+                            "reduce_scatter", "reduce_scatter_sync", "all_gather_sync", "p2p"};
+  return (k >= 0 && k <= 9) ? n[k] : "?";
 }
 
 struct Step {
@@ -84,6 +85,7 @@ class StepRunner {
   }
   int new_slot() {
     slots_.emplace_back();
+    extra_.emplace_back();
     pending_.push_back(false);
     return (int)slots_.size() - 1;
   }
@@ -125,6 +127,15 @@ class StepRunner {
     s.sb = std::move(send_splits);
     s.name = name;
     prog(p).push_back(std::move(s));
+  }
+  // Sparse exchange (halos, pipeline hand-offs, placement-local reshards): same buffers and
+  // per-group-rank splits as add_all_to_all, but only the peers with a non-zero split are posted,
+  // as ONE grouped launch on RCCL (start/endCoalescing) -- point-to-point xGMI transfers instead
+  // of an all-to-all over the whole group.
+  void add_p2p(int p, int slot, PG pg, at::Tensor recv, at::Tensor send, std::vector<int64_t> recv_splits,
+               std::vector<int64_t> send_splits, const std::string& name) {
+    add_all_to_all(p, slot, std::move(pg), recv, send, std::move(recv_splits), std::move(send_splits), name);
+    prog(p).back().kind = P2P_START;
   }
   void add_all_reduce(int p, int slot, PG pg, at::Tensor t, bool sync, const std::string& name) {
     check_slot(slot);
@@ -216,6 +227,7 @@ class StepRunner {
   // drop every pending Work handle (after an error / before tear-down)
   void reset_slots() {
     for (auto& w : slots_) w.reset();
+    for (auto& v : extra_) v.clear();
     std::fill(pending_.begin(), pending_.end(), false);
   }
 
@@ -283,15 +295,18 @@ class StepRunner {
     return result;
   }
 
-  void start(int slot, WorkPtr w) {
-    if (pending_[slot]) slots_[slot]->wait();
+  void start(int slot, WorkPtr w, std::vector<WorkPtr> more = {}) {
+    if (pending_[slot]) finish(slot);
     slots_[slot] = std::move(w);
+    extra_[slot] = std::move(more);
     pending_[slot] = true;
     ++collectives_;
   }
   void finish(int slot) {
     if (!pending_[slot]) return;
-    slots_[slot]->wait();
+    if (slots_[slot]) slots_[slot]->wait();
+    for (auto& w : extra_[slot])
+      if (w) w->wait();
     pending_[slot] = false;
     ++waits_;
   }
@@ -309,6 +324,30 @@ class StepRunner {
         c10d::AllToAllOptions o;
         at::Tensor recv = faults_.empty() ? s.a : inject(s.b, s.a);
         start(s.slot, s.pg->alltoall_base(recv, s.b, s.sa, s.sb, o));
+        bytes_sent_ += s.b.numel() * s.b.element_size();
+        break;
+      }
+      case P2P_START: {
+        if (pending_[s.slot]) finish(s.slot);
+        at::Tensor recv = faults_.empty() ? s.a : inject(s.b, s.a);
+        const bool coalesce = s.pg->getBackendType() == c10d::ProcessGroup::BackendType::NCCL;
+        if (coalesce) s.pg->startCoalescing(recv.device().type());
+        std::vector<WorkPtr> works;
+        int64_t ro = 0, so = 0;
+        for (size_t q = 0; q < s.sa.size(); ++q) {
+          if (s.sb[q] > 0) {
+            std::vector<at::Tensor> t{s.b.narrow(0, so, s.sb[q])};
+            works.push_back(s.pg->send(t, (int)q, 0));
+          }
+          if (s.sa[q] > 0) {
+            std::vector<at::Tensor> t{recv.narrow(0, ro, s.sa[q])};
+            works.push_back(s.pg->recv(t, (int)q, 0));
+          }
+          so += s.sb[q];
+          ro += s.sa[q];
+        }
+        if (coalesce) start(s.slot, s.pg->endCoalescing(recv.device().type()));
+        else start(s.slot, WorkPtr(), std::move(works));
         bytes_sent_ += s.b.numel() * s.b.element_size();
         break;
       }
@@ -361,6 +400,7 @@ class StepRunner {
   std::map<int64_t, Fault> faults_;
   int64_t fault_n_ = 0;
   std::vector<WorkPtr> slots_;
+  std::vector<std::vector<WorkPtr>> extra_;   // further works of a slot (uncoalesced p2p)
   std::vector<bool> pending_;
   int current_ = -1;
   bool released_ = false;
@@ -381,6 +421,8 @@ PYBIND11_MODULE(_rt, m) {
       .def("add_graph", &StepRunner::add_graph, py::arg("program"), py::arg("exec"), py::arg("name") = "")
       .def("add_all_to_all", &StepRunner::add_all_to_all, py::arg("program"), py::arg("slot"), py::arg("pg"),
            py::arg("recv"), py::arg("send"), py::arg("recv_splits"), py::arg("send_splits"), py::arg("name") = "")
+      .def("add_p2p", &StepRunner::add_p2p, py::arg("program"), py::arg("slot"), py::arg("pg"), py::arg("recv"),
+           py::arg("send"), py::arg("recv_splits"), py::arg("send_splits"), py::arg("name") = "")
       .def("add_all_reduce", &StepRunner::add_all_reduce, py::arg("program"), py::arg("slot"), py::arg("pg"),
            py::arg("tensor"), py::arg("sync") = false, py::arg("name") = "")
       .def("add_reduce_scatter", &StepRunner::add_reduce_scatter, py::arg("program"), py::arg("slot"), py::arg("pg"),

@@ -161,6 +161,12 @@ def run_reshards(comm, items):
 # (narrow tables) lose 3-6 %, hence the width rule.
 OVERLAP_EMB = os.environ.get("FM_OVERLAP_EMB", "auto")
 
+# FM_P2P=1/0/auto (default auto): a fused exchange whose transfer graph is sparse -- some pair of
+# participants never exchanges (spatial halos, pipeline hand-offs between neighbouring chunks) --
+# posts grouped point-to-point send/recv with only its real peers (one coalesced RCCL launch, each
+# transfer on its own xGMI link) instead of an all-to-all over every participant.
+P2P_MODE = os.environ.get("FM_P2P", "auto")
+
 
 def overlap_embeddings_enabled(ex):
     """Whether captured steps of executor ``ex`` run the fused embedding groups on a second HIP
@@ -324,8 +330,8 @@ class NativeRunner:
             if not x.active:        # this rank has no piece in the exchange
                 return
             rs_, ss_ = x.group_splits()
-            rt.add_all_to_all(pid, s, x.pg if x.pg is not None else self.world_pg, x.recv_buf, x.send_buf, rs_, ss_,
-                              it.name)
+            add = rt.add_p2p if x.p2p else rt.add_all_to_all
+            add(pid, s, x.pg if x.pg is not None else self.world_pg, x.recv_buf, x.send_buf, rs_, ss_, it.name)
             if kind == "a2a_sync":
                 rt.add_wait(pid, s, it.name + ".wait")
         elif kind == "wait":
@@ -429,8 +435,21 @@ class FusedExchange:
                     parts.update((t.src, t.dst))
         self.participants = sorted(parts)
         self.active = rank in parts
+        peers = defaultdict(set)
+        for st, *_ in items:
+            for t in st.plan.transfers:
+                if t.src != t.dst:
+                    peers[t.src].add(t.dst)
+                    peers[t.dst].add(t.src)
+        n = len(self.participants)
+        # point-to-point when some participants never exchange, or when only two ranks of a
+        # larger world do (a pipeline hand-off: send/recv on the world communicator instead of a
+        # new two-rank communicator).  Decided from the global transfer plan, so every rank picks
+        # the same collective.
+        sparse = (n >= 3 and max(len(v) for v in peers.values()) < n - 1) or (n == 2 and world > 2)
+        self.p2p = n >= 2 and (P2P_MODE == "1" or (P2P_MODE == "auto" and sparse))
         self.pg = None
-        if comm is not None and 0 < len(parts) < world:
+        if comm is not None and 0 < n < world and not self.p2p:
             self.pg = comm.group_for(self.participants)
         st0 = items[0][0]
         self.dtype, self.device = st0.dtype, st0.device
@@ -559,9 +578,25 @@ class FusedExchange:
         if not self.active:
             return
         rs, ss = self.group_splits()
-        self.work = dist.all_to_all_single(self.recv_buf, self.send_buf, rs, ss, group=self.pg, async_op=True)
+        if self.p2p:
+            ops = []
+            so = ro = 0
+            for q, peer in enumerate(self._group_ranks()):
+                if ss[q] > 0:
+                    ops.append(dist.P2POp(dist.isend, self.send_buf[so:so + ss[q]], peer, group=self.pg))
+                if rs[q] > 0:
+                    ops.append(dist.P2POp(dist.irecv, self.recv_buf[ro:ro + rs[q]], peer, group=self.pg))
+                so += ss[q]
+                ro += rs[q]
+            self.work = dist.batch_isend_irecv(ops) if ops else None
+        else:
+            self.work = dist.all_to_all_single(self.recv_buf, self.send_buf, rs, ss, group=self.pg, async_op=True)
         comm.calls += 1
         comm.bytes_sent += self.send_buf.numel() * self.send_buf.element_size()
+
+    def _group_ranks(self):
+        """Global ranks in the order of the exchange's communicator."""
+        return list(self.participants) if self.pg is not None else list(range(self.world))
 
     def group_splits(self):
         """(recv, send) split sizes in the order of the exchange's communicator."""
@@ -571,7 +606,8 @@ class FusedExchange:
 
     def wait(self):
         if self.work is not None:
-            self.work.wait()
+            for w in (self.work if isinstance(self.work, list) else [self.work]):
+                w.wait()
             self.work = None
 
     def unpack(self):
@@ -841,6 +877,9 @@ class Executor:
                 c.weight_grads.append(e.grad if e else None)
                 c.w_boxes.append(e.box if e else None)
             c.lr = self.lr_tensor
+            # a split whose extent does not divide the degree can leave this rank an empty output
+            # box (e.g. 6 rows over 4 ranks -> 2/2/2/0): nothing to compute, zero input gradients
+            c.empty = bool(c.outputs) and all(o is None or o.numel() == 0 for o in c.outputs)
             op.prepare(c)
             self.ctx[op.guid] = c
         self._build_groups(ops)
@@ -1421,6 +1460,8 @@ class Executor:
 
     def _fwd_op(self, op, c):
         c.training = self.training
+        if getattr(c, "empty", False):
+            return
         if getattr(op, "host_exec", False):
             return self._host_op(op, c, "forward")
         op.forward(c)
@@ -1428,6 +1469,12 @@ class Executor:
     def _bwd_op(self, op, c, flags, phase=None):
         for i, f in enumerate(flags):
             c.in_grad_accumulate[i] = f
+        if getattr(c, "empty", False):
+            if phase in (None, "dx"):
+                for g, acc in zip(c.in_grads, c.in_grad_accumulate):
+                    if g is not None and not acc:
+                        g.zero_()
+            return
         if getattr(op, "host_exec", False):
             return self._host_op(op, c, "backward")
         if phase is None:

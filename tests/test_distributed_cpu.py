@@ -183,6 +183,10 @@ def _build(case, world):
 
 
 def _run(case, world, rank, steps, out_path):
+    from flexmi.runtime import executor as E
+    p2p = case.endswith("+p2p")
+    case = case.replace("+p2p", "")
+    E.P2P_MODE = "1" if p2p else os.environ.get("FM_P2P", "auto")
     m, inputs = _build(case, world)
     ex = m.init_layers()
     for op in m.layers:  # the strategy must really be applied (no silent DP fallback)
@@ -215,8 +219,16 @@ def _run(case, world, rank, steps, out_path):
     if case == "mlp_subset" and world > 2:
         from flexmi.runtime.executor import FusedExchange
         subs = [x for x in nr.keep if isinstance(x, FusedExchange) and x.participants == [0, 1]]
-        assert subs and all((x.pg is not None) for x in subs), "subset exchange not on its own communicator"
+        # a subset exchange runs on its own communicator or point-to-point on the world one
+        assert subs and all((x.pg is not None) or x.p2p for x in subs), "subset exchange over the whole world"
         assert all(x.active == (rank in (0, 1)) for x in subs)
+    if world > 1 and (p2p or (case == "cnn_spatial" and world >= 4)):
+        # sparse exchanges (halos, chunk hand-offs) go point-to-point: grouped send/recv with
+        # the real peers only, through the native runner
+        from flexmi.runtime.executor import FusedExchange
+        xs = [x for x in nr.keep if isinstance(x, FusedExchange)]
+        assert any(x.p2p for x in xs), "no point-to-point exchange planned"
+        assert any(k == "p2p" for pid in range(nr.rt.num_programs()) for k, _ in nr.rt.describe(pid))
     if rank == 0:
         np.savez(out_path, loss=loss, native_colls=native_colls, *params)
 
@@ -248,10 +260,11 @@ def _launch(case, world, steps=3):
                                         ("dlrm_search", 2), ("dlrm_search", 4), ("dlrm_rowsplit", 2),
                                         ("dlrm_rowsplit", 4), ("mlp_dp_zero", 2), ("dlrm_dot_zero", 2),
                                         ("mlp_dp_zero", 4), ("dlrm_cat_dpsmall", 2), ("dlrm_mlperf8", 8), ("mlp_subset", 4), ("nmt_reference", 2),
-                                        ("nmt_pipeline", 2), ("nmt_pipeline", 4),
+                                        ("nmt_pipeline", 2), ("nmt_pipeline", 4), ("cnn_spatial", 4),
+                                        ("cnn_spatial+p2p", 2), ("dlrm_dot+p2p", 2),
                                         ("dlrm_shipped8", 8)])
 def test_strategy_equivalence(case, world):
-    ref = _launch(case, 1)
+    ref = _launch(case.replace("+p2p", ""), 1)
     got = _launch(case, world)
     keys = [k for k in ref.files if k.startswith("arr_")]
     assert len(keys) == len([k for k in got.files if k.startswith("arr_")])
