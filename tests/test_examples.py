@@ -74,3 +74,29 @@ def test_launcher_flag_filtering():
                                     "native/split.py", "onnx/resnet.py"])
 def test_example_gpu(script, tmp_path):
     run_example(script, tmp_path, ["-b", "64"], samples=512, device="gpu")
+
+
+def test_example_two_nodes(tmp_path):
+    """Multi-node launch (X9/P12): two launcher processes, one per "node" (--nodes 2 --node-rank
+    0/1, --nproc 2 each, rendezvous at --master 127.0.0.1) form ONE 4-rank job running the same
+    SPMD plan: every rank trains and the per-rank results agree."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, FLEXMI_EXAMPLE_SAMPLES="128", FLEXMI_EXAMPLE_EPOCHS="1", FLEXMI_EXAMPLE_MIN_ACC="0",
+               PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""), MASTER_PORT=str(port),
+               HSA_ENABLE_IPC_MODE_LEGACY="0")
+    procs = []
+    for node in range(2):
+        cmd = [sys.executable, "-m", "flexmi.run", "--nproc", "2", "--nodes", "2", "--node-rank", str(node),
+               "--master", "127.0.0.1", os.path.join(EX, "keras/func_mnist_mlp.py"), "--device", "cpu",
+               "--dtype", "fp32", "-b", "32"]
+        procs.append(subprocess.Popen(cmd, cwd=tmp_path, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                      text=True))
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=600)
+        assert p.returncode == 0, f"node failed:\n{o[-2000:]}\n{e[-3000:]}"
+        outs.append(o)
+    assert sum(o.count("THROUGHPUT") for o in outs) == 4
