@@ -15,6 +15,7 @@
 #include "../cpu/emb_kernels.h"
 #include "../runtime/hdf5_lite.h"
 #include "../runtime/loader.h"
+#include "../runtime/planner.h"
 #include "../runtime/shard.h"
 #include "../runtime/strategy_pb.h"
 #include "../sim/simulator.h"
@@ -451,5 +452,89 @@ int fmn_embedding_bag_backward(float* target, int64_t rows, int64_t D, const int
   flexmi::cpu::embedding_bag_backward<int64_t>(target, rows, D, idx, B, bag, row_lo, dy, ld_dy, alpha, 0);
   return 0;
 }
+
+}  // extern "C"
+
+// ---- graph planner --------------------------------------------------------------------------------
+struct fmn_plan_s {
+  std::vector<flexmi::PlanOp> ops;
+  flexmi::GraphPlan plan;
+  bool planned = false;
+};
+
+extern "C" {
+
+fmn_plan_t fmn_plan_create(void) {
+  return guarded([] { return new fmn_plan_s(); }, (fmn_plan_t) nullptr);
+}
+
+int fmn_plan_add_op(fmn_plan_t p, int64_t guid, int n_out, const int64_t* outputs) {
+  if (!p || n_out < 0 || (n_out > 0 && !outputs)) return fail("fmn_plan_add_op: bad arguments");
+  flexmi::PlanOp op;
+  op.guid = guid;
+  op.outputs.assign(outputs, outputs + n_out);
+  p->ops.push_back(std::move(op));
+  p->planned = false;
+  return (int)p->ops.size() - 1;
+}
+
+int fmn_plan_add_input(fmn_plan_t p, int64_t tensor, int64_t producer, int dtype, int64_t need, int flags) {
+  if (!p || p->ops.empty()) return fail("fmn_plan_add_input: no op");
+  flexmi::PlanInput in;
+  in.tensor = tensor;
+  in.producer = producer;
+  in.dtype = dtype;
+  in.need = need;
+  in.is_float = flags & 1;
+  in.needs_grad = (flags >> 1) & 1;
+  in.reshard = (flags >> 2) & 1;
+  in.remote = (flags >> 3) & 1;
+  p->ops.back().inputs.push_back(in);
+  return (int)p->ops.back().inputs.size() - 1;
+}
+
+int fmn_plan_run(fmn_plan_t p, int world, int input_grads) {
+  if (!p) return fail("fmn_plan_run: null plan");
+  return guarded(
+      [&] {
+        p->plan = flexmi::plan_graph(p->ops, world, input_grads != 0);
+        p->planned = true;
+        return 0;
+      },
+      -1);
+}
+
+static int64_t copy_ids(const fmn_plan_s* p, const std::vector<int64_t>& v, int64_t* out, int64_t max_n) {
+  if (!p || !p->planned) return fail("plan not run");
+  for (int64_t i = 0; i < (int64_t)v.size() && i < max_n; ++i) out[i] = v[i];
+  return (int64_t)v.size();
+}
+
+int64_t fmn_plan_order(fmn_plan_t p, int64_t* guids, int64_t max_n) { return copy_ids(p, p ? p->plan.order : std::vector<int64_t>{}, guids, max_n); }
+int64_t fmn_plan_bwd_live(fmn_plan_t p, int64_t* guids, int64_t max_n) {
+  return copy_ids(p, p ? p->plan.bwd_live : std::vector<int64_t>{}, guids, max_n);
+}
+int64_t fmn_plan_grad_needed(fmn_plan_t p, int64_t* tensors, int64_t max_n) {
+  return copy_ids(p, p ? p->plan.grad_needed : std::vector<int64_t>{}, tensors, max_n);
+}
+
+int64_t fmn_plan_steps(fmn_plan_t p, int backward, int* kind, int64_t* op, int* n_inputs, int* inputs, int64_t max_steps,
+                       int64_t max_inputs) {
+  if (!p || !p->planned) return fail("plan not run");
+  const auto& steps = backward ? p->plan.bwd : p->plan.fwd;
+  int64_t k = 0;
+  for (int64_t i = 0; i < (int64_t)steps.size() && i < max_steps; ++i) {
+    if (kind) kind[i] = steps[i].kind;
+    if (op) op[i] = steps[i].op;
+    if (n_inputs) n_inputs[i] = (int)steps[i].inputs.size();
+    for (int x : steps[i].inputs) {
+      if (inputs && k < max_inputs) inputs[k] = x;
+      ++k;
+    }
+  }
+  return (int64_t)steps.size();
+}
+
+void fmn_plan_destroy(fmn_plan_t p) { delete p; }
 
 }  // extern "C"

@@ -29,6 +29,7 @@ typedef struct fmn_layout_s* fmn_layout_t;
 typedef struct fmn_sim_s* fmn_sim_t;
 typedef struct fmn_h5_s* fmn_h5_t;
 typedef struct fmn_loader_s* fmn_loader_t;
+typedef struct fmn_plan_s* fmn_plan_t;
 
 const char* fmn_last_error(void);
 const char* fmn_version(void);
@@ -108,6 +109,24 @@ int fmn_loader_release(fmn_loader_t l, int slot);
 int64_t fmn_loader_batches_per_epoch(fmn_loader_t l);
 int fmn_loader_batch_ids(fmn_loader_t l, int64_t n, int64_t* ids, int64_t max_ids);
 void fmn_loader_destroy(fmn_loader_t l);
+
+/* ---- graph planner (csrc/runtime/planner.h) ----------------------------------------------------
+ * Build the graph op by op (model order; the loss reads the first output of the LAST op), then
+ * plan: communication-first order, forward reshard schedule, backward liveness and schedule. */
+fmn_plan_t fmn_plan_create(void);
+/* returns the op index; outputs are tensor ids */
+int fmn_plan_add_op(fmn_plan_t p, int64_t guid, int n_out, const int64_t* outputs);
+/* adds an input to the last op: flags bit 0 is_float, 1 needs_grad, 2 reshard, 3 remote */
+int fmn_plan_add_input(fmn_plan_t p, int64_t tensor, int64_t producer, int dtype, int64_t need, int flags);
+int fmn_plan_run(fmn_plan_t p, int world, int input_grads);
+/* results (after fmn_plan_run): counts and copies; steps are (kind, op guid, #inputs) rows whose
+ * input indices follow in `inputs` (kind: 0 op, 1 reshard (fwd) / gradient reduce (bwd)) */
+int64_t fmn_plan_order(fmn_plan_t p, int64_t* guids, int64_t max_n);
+int64_t fmn_plan_bwd_live(fmn_plan_t p, int64_t* guids, int64_t max_n);
+int64_t fmn_plan_grad_needed(fmn_plan_t p, int64_t* tensors, int64_t max_n);
+int64_t fmn_plan_steps(fmn_plan_t p, int backward, int* kind, int64_t* op, int* n_inputs, int* inputs, int64_t max_steps,
+                       int64_t max_inputs);
+void fmn_plan_destroy(fmn_plan_t p);
 
 /* ---- CPU embedding-bag kernels --------------------------------------------------------------- */
 /* out[b * ld_out + d] = scale * sum_j W[idx[b * bag + j] - row_lo][d] (rows outside the shard skipped) */

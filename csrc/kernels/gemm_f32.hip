@@ -314,7 +314,7 @@ __global__ void __launch_bounds__(NTF, 2) fm_gemm_f32_kernel(GemmF p) {
   for (int kt = kt0; kt < kt1; ++kt) {
     const int cur = (kt - kt0) & 1;
     const bool more = kt + 1 < kt1;
-    if (more) {
+    if (more && (OPT & 8) == 0) {   // OPT 8/16: diagnostic variants (wrong results) without the K-loop loads
       sa.load(A, p.lda, m0, p.M, (kt + 1) * BKF, p.K, tid);
       sb.load(B, p.ldb, n0, p.N, (kt + 1) * BKF, p.K, tid);
     }
@@ -365,7 +365,7 @@ __global__ void __launch_bounds__(NTF, 2) fm_gemm_f32_kernel(GemmF p) {
       if constexpr ((OPT & 1) != 0) __builtin_amdgcn_s_setprio(0);
     }
     }
-    if (more) {
+    if (more && (OPT & 16) == 0) {
       sa.store(LDSF_A(cur ^ 1), tid);
       sb.store(LDSF_B(cur ^ 1), tid);
       if (rowsum) sa.accumulate_rows(rs);
@@ -429,6 +429,8 @@ void launch_f(const GemmF& p, hipStream_t s, int opt) {
       case 2: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 2>), grid, dim3(NTF), LDS, s, p); return;
       case 4: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 4>), grid, dim3(NTF), LDS, s, p); return;
       case 6: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 6>), grid, dim3(NTF), LDS, s, p); return;
+      case 8: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 8>), grid, dim3(NTF), LDS, s, p); return;
+      case 24: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 24>), grid, dim3(NTF), LDS, s, p); return;
       default: break;
     }
   }
@@ -701,7 +703,7 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
   if (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks = 1;
   if (K <= 0) ks = 1;
   p.ksplit = ks;
-  const int opt = (variant >> 2) & 7;
+  const int opt = (variant >> 2) & 31;
   if (BNv == 128) launch_fbm<128, 128>(p, a_kcontig, b_kcontig, vec, stream, opt);
   else if (BMv == 128) launch_fbm<128, 64>(p, a_kcontig, b_kcontig, vec, stream, 0);
   else launch_fbm<64, 64>(p, a_kcontig, b_kcontig, vec, stream, 0);

@@ -189,6 +189,36 @@ static int embedding(void) {
   return 0;
 }
 
+/* graph planner: dense chain d1 -> d2 and an embedding chain e0 -> e1 whose output crosses ranks
+ * into the join j; the remote producer and its ancestor are scheduled first */
+static int planner(void) {
+  fmn_plan_t p = fmn_plan_create();
+  CHECK(p != NULL, "plan create");
+  int64_t o;
+  o = 11; fmn_plan_add_op(p, 1, 1, &o); fmn_plan_add_input(p, 100, -1, 0, 0, 3);
+  o = 12; fmn_plan_add_op(p, 2, 1, &o); fmn_plan_add_input(p, 11, 1, 0, 0, 3);
+  o = 13; fmn_plan_add_op(p, 3, 1, &o); fmn_plan_add_input(p, 101, -1, 0, 0, 3);
+  o = 14; fmn_plan_add_op(p, 4, 1, &o); fmn_plan_add_input(p, 13, 3, 0, 0, 3);
+  o = 15; fmn_plan_add_op(p, 5, 1, &o);
+  fmn_plan_add_input(p, 12, 2, 0, 0, 3);
+  fmn_plan_add_input(p, 14, 4, 0, 7, 1 | 2 | 4 | 8);   /* float, grad, reshard, remote */
+  CHECK(fmn_plan_run(p, 2, 0) == 0, "plan run");
+  int64_t order[8];
+  CHECK(fmn_plan_order(p, order, 8) == 5, "order size");
+  CHECK(order[0] == 3 && order[1] == 4 && order[2] == 1 && order[3] == 2 && order[4] == 5, "comm-first order");
+  int kind[16], nin[16], ins[16];
+  int64_t op[16];
+  const int64_t nf = fmn_plan_steps(p, 0, kind, op, nin, ins, 16, 16);
+  CHECK(nf == 6 && kind[4] == 1 && op[4] == 5 && nin[4] == 1 && ins[0] == 1, "forward reshard step");
+  const int64_t nb = fmn_plan_steps(p, 1, kind, op, nin, ins, 16, 16);
+  CHECK(nb == 6 && kind[0] == 0 && op[0] == 5 && kind[1] == 1, "backward gradient reduce after the join");
+  int64_t live[8];
+  CHECK(fmn_plan_bwd_live(p, live, 8) == 5, "all ops live");
+  fmn_plan_destroy(p);
+  printf("ok planner\n");
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: %s <scratch dir> [hdf5] [reference .pb]\n", argv[0]);
@@ -201,6 +231,7 @@ int main(int argc, char** argv) {
   if (argc > 2 && hdf5(argv[2])) return 1;
   if (loader()) return 1;
   if (embedding()) return 1;
+  if (planner()) return 1;
   printf("ALL OK\n");
   return 0;
 }

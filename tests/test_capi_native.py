@@ -1,7 +1,7 @@
 """The CPython-free native C API (csrc/capi/flexmi_native_c.h, flexmi/libflexmi_native_c.so): a C
 program (tests/capi/native_demo.c) compiled with gcc drives the strategy codec (incl. the
 reference's shipped dlrm_strategy_8embs_8gpus.pb), the sharding algebra, the simulator + MCMC
-search, the HDF5 reader, the batch loader ring and the CPU embedding kernels -- and the library
+search, the HDF5 reader, the batch loader ring, the CPU embedding kernels and the graph planner -- and the library
 must not link libpython."""
 import os
 import shutil
@@ -47,7 +47,7 @@ def test_native_c_program(demo):
     p = subprocess.run(args, capture_output=True, text=True, timeout=120, env=dict(os.environ, PYTHONHOME="/nonexistent"))
     assert p.returncode == 0, p.stdout + p.stderr
     out = p.stdout
-    for area in ("strategies", "sharding", "simulator", "hdf5", "loader", "embedding"):
+    for area in ("strategies", "sharding", "simulator", "hdf5", "loader", "embedding", "planner"):
         assert f"ok {area}" in out, out
     s = float(out.split("X_int[3:5] sum")[1].split()[0])
     assert abs(s - float(x[3:5].sum())) < 1e-4

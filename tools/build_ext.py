@@ -146,7 +146,7 @@ def write_ninja(only=None):
         nobjs = []
         for src in [os.path.join(ROOT, "csrc", "capi", "flexmi_native_c.cc"), os.path.join(ROOT, "csrc", "cpu", "emb_kernels.cc"),
                     os.path.join(ROOT, "csrc", "sim", "simulator.cc")] + [
-                os.path.join(ROOT, "csrc", "runtime", n) for n in ("hdf5_lite.cc", "loader.cc", "shard.cc", "strategy_pb.cc")]:
+                os.path.join(ROOT, "csrc", "runtime", n) for n in ("hdf5_lite.cc", "loader.cc", "planner.cc", "shard.cc", "strategy_pb.cc")]:
             o = os.path.join(BUILD, "nc_" + os.path.basename(src).replace(".cc", ".o"))
             lines.append(f"build {o}: cxx {src}")
             lines.append(f"  extra = -I{ROOT}/csrc/capi")
