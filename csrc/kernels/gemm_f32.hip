@@ -61,17 +61,17 @@ FM_DEVICE int xcd_remap_f(int bid, int ntiles) {
 FM_DEVICE int kc_off(int r, int c) { return r * (BKF * 4) + 16 * (c ^ ((r >> 1) & 7)); }
 
 // ---- global -> registers -> LDS (one operand tile) ----------------------------------------
-template <bool KC, int R, bool VEC>
+template <bool KC, int R, bool VEC, int NT = NTF>
 struct StageF {
   static constexpr int CHUNKS = R * BKF / 4;
-  static constexpr int PER_T = CHUNKS / NTF;
-  static_assert(PER_T >= 1 && CHUNKS % NTF == 0, "tile too small for the block");
+  static constexpr int PER_T = CHUNKS / NT;
+  static_assert(PER_T >= 1 && CHUNKS % NT == 0, "tile too small for the block");
   f32x4_t v[PER_T];
 
   FM_DEVICE void load(const float* __restrict__ p, long ld, int row0, int rows, int k0, int K, int tid) {
 #pragma unroll
     for (int i = 0; i < PER_T; ++i) {
-      const int ci = tid + NTF * i;
+      const int ci = tid + NT * i;
       int gr, gk;
       if constexpr (KC) {
         gr = row0 + (ci >> 3);
@@ -101,7 +101,7 @@ struct StageF {
   FM_DEVICE void store(char* lds, int tid) {
 #pragma unroll
     for (int i = 0; i < PER_T; ++i) {
-      const int ci = tid + NTF * i;
+      const int ci = tid + NT * i;
       int off;
       if constexpr (KC) off = kc_off(ci >> 3, ci & 7);
       else off = (ci / (R / 4)) * (R * 4) + 16 * (ci % (R / 4));
@@ -261,17 +261,22 @@ FM_DEVICE void epilogue_f32(const GemmF& p, const f32x4_t (&acc)[MR][NR], int zb
 // OPT (tuning variants, FM_GEMM_F32_VARIANT bits 4/8): 1 = s_setprio(1) around each MFMA cluster;
 // 2 = fragment double buffer: the next k-chunk's LDS fragments are read before this chunk's MFMAs
 // and interleaved with them (sched_group_barrier), so only the first chunk of a K tile waits on LDS.
-template <int BM, int BN, bool AK, bool BKC, bool VEC, int OPT = 0>
-__global__ void __launch_bounds__(NTF, 2) fm_gemm_f32_kernel(GemmF p) {
+// NT = 256 (4 waves, 2x2, wave tile BM/2 x BN/2) or 512 (8 waves, 2x4 for BN >= 128, else 4x2:
+// twice the waves per SIMD to cover the LDS-read and barrier latency of each K tile).
+template <int BM, int BN, bool AK, bool BKC, bool VEC, int OPT = 0, int NT = NTF>
+__global__ void __launch_bounds__(NT, 2) fm_gemm_f32_kernel(GemmF p) {
   constexpr int A_BYTES = BM * BKF * 4;
   constexpr int B_BYTES = BN * BKF * 4;
-  constexpr int MR = BM / 32;
-  constexpr int NR = BN / 32;
+  constexpr int WN = (NT == 512 && BN >= 128) ? 4 : 2;
+  constexpr int WM = NT / 64 / WN;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int MR = TM / 16;
+  constexpr int NR = TN / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
 
   const int bid = xcd_remap_f(blockIdx.x, p.tiles_m * p.tiles_n);
   int tm, tn;
@@ -294,8 +299,8 @@ __global__ void __launch_bounds__(NTF, 2) fm_gemm_f32_kernel(GemmF p) {
 #pragma unroll
     for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  StageF<AK, BM, VEC> sa;
-  StageF<BKC, BN, VEC> sb;
+  StageF<AK, BM, VEC, NT> sa;
+  StageF<BKC, BN, VEC, NT> sb;
   const bool rowsum = (!AK) && (p.rowsum_a != nullptr) && (tn == 0);
   float rs[4] = {0.f, 0.f, 0.f, 0.f};
 #define LDSF_A(b) (smem + (b) * (A_BYTES + B_BYTES))
@@ -320,10 +325,10 @@ __global__ void __launch_bounds__(NTF, 2) fm_gemm_f32_kernel(GemmF p) {
     }
     if constexpr ((OPT & 2) != 0) {
       float af0[MR][4], bf0[NR][4], af1[MR][4], bf1[NR][4];
-      load_frags<AK, BM, MR>(LDSF_A(cur), wm * (BM / 2), 0, lane, af0);
-      load_frags<BKC, BN, NR>(LDSF_B(cur), wn * (BN / 2), 0, lane, bf0);
-      load_frags<AK, BM, MR>(LDSF_A(cur), wm * (BM / 2), 1, lane, af1);
-      load_frags<BKC, BN, NR>(LDSF_B(cur), wn * (BN / 2), 1, lane, bf1);
+      load_frags<AK, BM, MR>(LDSF_A(cur), wm * TM, 0, lane, af0);
+      load_frags<BKC, BN, NR>(LDSF_B(cur), wn * TN, 0, lane, bf0);
+      load_frags<AK, BM, MR>(LDSF_A(cur), wm * TM, 1, lane, af1);
+      load_frags<BKC, BN, NR>(LDSF_B(cur), wn * TN, 1, lane, bf1);
       if constexpr ((OPT & 1) != 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int s = 0; s < 4; ++s)
@@ -352,8 +357,8 @@ __global__ void __launch_bounds__(NTF, 2) fm_gemm_f32_kernel(GemmF p) {
 #pragma unroll
     for (int kk = 0; kk < BKF / 16; ++kk) {
       float af[MR][4], bfr[NR][4];
-      load_frags<AK, BM, MR>(LDSF_A(cur), wm * (BM / 2), kk, lane, af);
-      load_frags<BKC, BN, NR>(LDSF_B(cur), wn * (BN / 2), kk, lane, bfr);
+      load_frags<AK, BM, MR>(LDSF_A(cur), wm * TM, kk, lane, af);
+      load_frags<BKC, BN, NR>(LDSF_B(cur), wn * TN, kk, lane, bfr);
       if constexpr ((OPT & 1) != 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int s = 0; s < 4; ++s)
@@ -383,13 +388,13 @@ __global__ void __launch_bounds__(NTF, 2) fm_gemm_f32_kernel(GemmF p) {
       __syncthreads();
       if (tid < BM) {
         float x = 0.f;
-        for (int t = 0; t < NTF / G; ++t) x += red[t * BM + tid];
+        for (int t = 0; t < NT / G; ++t) x += red[t * BM + tid];
         if (m0 + tid < p.M) atomicAdd(p.rowsum_a + m0 + tid, x);
       }
       __syncthreads();
     }
   }
-  epilogue_f32<MR, NR, !AK, !BKC>(p, acc, zb, split, m0 + wm * (BM / 2), n0 + wn * (BN / 2), lane);
+  epilogue_f32<MR, NR, !AK, !BKC>(p, acc, zb, split, m0 + wm * TM, n0 + wn * TN, lane);
 }
 
 // split-K reduce: 4 consecutive outputs per thread when N % 4 == 0 (16-B slab loads)
@@ -424,14 +429,27 @@ void launch_f(const GemmF& p, hipStream_t s, int opt) {
   constexpr int LDS = 2 * (BM + BN) * BKF * 4;
   dim3 grid(p.tiles_m * p.tiles_n, p.batch, p.ksplit);
   if constexpr (VEC && BM == 128 && BN == 128) {   // tuning variants only on the main tile
+    // default: 8 waves (2x4, 64x32 per wave) with the fragment double buffer -- 4 waves per SIMD
+    // hide the per-K-tile barrier and first-fragment latency (DLRM fp32 GEMMs -3.7 %, the
+    // 1024-wide layers -5..8 %: profiles/gemm_f32_variants_ab.jsonl); opt 5 = the 4-wave kernel
     switch (opt) {
+      case 0: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 2, 512>), grid, dim3(512), LDS, s, p); return;
+      case 5: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 0, 256>), grid, dim3(NTF), LDS, s, p); return;
       case 1: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 1>), grid, dim3(NTF), LDS, s, p); return;
       case 2: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 2>), grid, dim3(NTF), LDS, s, p); return;
       case 4: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 4>), grid, dim3(NTF), LDS, s, p); return;
       case 6: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 6>), grid, dim3(NTF), LDS, s, p); return;
       case 8: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 8>), grid, dim3(NTF), LDS, s, p); return;
       case 24: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 24>), grid, dim3(NTF), LDS, s, p); return;
+      case 32: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 0, 512>), grid, dim3(512), LDS, s, p); return;
+      case 56: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 24, 512>), grid, dim3(512), LDS, s, p); return;
       default: break;
+    }
+  }
+  if constexpr (VEC && BM == 128 && BN == 64) {
+    if (opt == 10) {   // A/B: the 8-wave (4x2) form of the 128x64 tile
+      hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 2, 512>), grid, dim3(512), LDS, s, p);
+      return;
     }
   }
   hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC>), grid, dim3(NTF), LDS, s, p);
@@ -703,9 +721,9 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
   if (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks = 1;
   if (K <= 0) ks = 1;
   p.ksplit = ks;
-  const int opt = (variant >> 2) & 31;
+  const int opt = (variant >> 2) & 63;
   if (BNv == 128) launch_fbm<128, 128>(p, a_kcontig, b_kcontig, vec, stream, opt);
-  else if (BMv == 128) launch_fbm<128, 64>(p, a_kcontig, b_kcontig, vec, stream, 0);
+  else if (BMv == 128) launch_fbm<128, 64>(p, a_kcontig, b_kcontig, vec, stream, opt);
   else launch_fbm<64, 64>(p, a_kcontig, b_kcontig, vec, stream, 0);
   if (ks > 1) {
     const int v4 = (N % 4 == 0) && (ldc % 4 == 0) && (sC % 4 == 0) && al(C);

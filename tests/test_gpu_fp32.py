@@ -89,12 +89,22 @@ def test_gemm_f32_splitk_and_batch(gpu, ks):
     Kk.bmm(X, O, Y.new_empty(bs, 72, 24), True, False, False)    # transposed A operand
 
 
-def test_gemm_f32_fused_backward_epilogue(gpu):
+@pytest.mark.parametrize("M,K,N,variant", [(2048, 512, 256, 0), (8192, 1024, 1024, 0), (8192, 1024, 1024, 20),
+                                           (8192, 480, 1024, 0)])
+def test_gemm_f32_fused_backward_epilogue(gpu, M, K, N, variant):
     """dX GEMM with the activation backward of the layer below (y fp32) and its bias-gradient
-    column sums fused; dW GEMM with the bias gradient as row sums of the staged MN-contiguous A."""
+    column sums fused; dW GEMM with the bias gradient as row sums of the staged MN-contiguous A.
+    The MLPerf shapes run the 8-wave 128x128 kernel (variant 20: the 4-wave one)."""
     from flexmi.ops import _kernels as Kk
     torch.manual_seed(3)
-    M, K, N = 2048, 512, 256           # dpre [M,N], W [N,K] -> dX [M,K]
+    Kk.C().gemm_f32_set_variant(variant)
+    try:
+        _fused_backward_epilogue(Kk, gpu, M, K, N)
+    finally:
+        Kk.C().gemm_f32_set_variant(0)
+
+
+def _fused_backward_epilogue(Kk, gpu, M, K, N):     # dpre [M,N], W [N,K] -> dX [M,K]
     dpre = torch.randn(M, N, device=gpu)
     W = torch.randn(N, K, device=gpu)
     yb = torch.randn(M, K, device=gpu).relu()
