@@ -105,12 +105,15 @@ class ImageFolderLoader:
         self.next_index = 0
         self.pool = ThreadPoolExecutor(max_workers=max(1, threads))
         self._staging = None
+        self._h2d_done = None
+        self._next = None         # (batch ids, future of the decoded uint8 rows) of the NEXT batch
 
     def get_num_samples(self):
         return len(self.files)
 
     def reset(self):
         self.next_index = 0
+        self._next = None
         if self.shuffle:
             self.rng.shuffle(self.order)
 
@@ -121,21 +124,38 @@ class ImageFolderLoader:
         self.next_index += self.batch_size
         return ids
 
+    def _decode_rows(self, ids):
+        """Decode a batch's rows in the thread pool; returns one future per row."""
+        futs = [self.pool.submit(decode_image, self.files[i], self.height, self.width) for i in ids]
+        return futs
+
     def next_batch(self, ffmodel=None):
+        """Load the next batch.  The batch after it is decoded in the background (thread pool)
+        while the caller trains on this one, so the host decode overlaps the GPU step."""
         m = ffmodel or self.model
         ex = m._ex()
-        ids = self._batch_ids()
         buf = ex.local_buffer(self.image)
+        box = ex.home[self.image.guid].local_box(ex.rank) if buf is not None else None
+        if self._next is None:
+            ids = self._batch_ids()
+            futs = self._decode_rows(ids[box[0][0]:box[0][1]]) if box is not None else []
+        else:
+            ids, futs = self._next
+        nxt = self._batch_ids()
+        self._next = (nxt, self._decode_rows(nxt[box[0][0]:box[0][1]]) if box is not None else [])
         if buf is not None:
-            box = ex.home[self.image.guid].local_box(ex.rank)
             r0, r1 = box[0]
-            rows = list(self.pool.map(lambda i: decode_image(self.files[i], self.height, self.width), ids[r0:r1]))
-            u8 = torch.from_numpy(np.stack(rows))
+            u8 = torch.from_numpy(np.stack([f.result() for f in futs]))
             if buf.is_cuda:
                 if self._staging is None or self._staging.shape != u8.shape:
                     self._staging = torch.empty(u8.shape, dtype=torch.uint8).pin_memory()
+                    self._h2d_done = None
+                if self._h2d_done is not None:      # the previous async H2D still reads the staging buffer
+                    self._h2d_done.synchronize()
                 self._staging.copy_(u8)
                 u8 = self._staging.to(buf.device, non_blocking=True)
+                self._h2d_done = torch.cuda.Event()
+                self._h2d_done.record()
             full = tuple(box[1:]) == ((0, 3), (0, self.height), (0, self.width))
             if full and buf.is_contiguous():
                 normalize_images(u8, buf, self.mean, self.std)
