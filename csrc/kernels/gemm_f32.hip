@@ -447,7 +447,9 @@ void launch_f(const GemmF& p, hipStream_t s, int opt) {
     }
   }
   if constexpr (VEC && BM == 128 && BN == 64) {
-    if (opt == 10) {   // A/B: the 8-wave (4x2) form of the 128x64 tile
+    // default: the 8-wave (4x2 waves of 32x32) form; opt 10 = the 4-wave kernel (A/B:
+    // profiles/gemm_f32_8wave_ab.jsonl, the 512/256-wide layers' dX/dW -5..14 %)
+    if (opt != 10) {
       hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 2, 512>), grid, dim3(512), LDS, s, p);
       return;
     }
