@@ -50,6 +50,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--time-budget", type=float, default=900.0, help="stop measuring after this many seconds")
+    ap.add_argument("--refresh", default="", help="comma list of op types (e.g. OP_LINEAR) re-measured even when the "
+                                                  "DB already holds them (after kernel changes)")
     a = ap.parse_args()
 
     from flexmi.parallel.cost import CostModel, op_signature
@@ -82,8 +84,9 @@ def main():
     cm = CostModel(MachineModel.mi355x(1), db_path="", dtype_bytes=4 if a.dtype == "fp32" else 2)
     t0 = time.time()
     done = 0
+    refresh = tuple(t for t in a.refresh.split(",") if t)
     for k in keys:
-        if k in db["entries"]:
+        if k in db["entries"] and not (refresh and k.split("|")[0] in refresh):
             continue
         if time.time() - t0 > a.time_budget:
             print(f"[calibrate] time budget reached after {done} measurements", flush=True)
