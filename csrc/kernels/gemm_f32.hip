@@ -707,7 +707,8 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
   int BMv = 128, BNv = 128;
   const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;
   if (t128 < 512 && N <= 64 * 8) BNv = 64;
-  if (t128 < 128 && K <= 2048) { BMv = 64; BNv = 64; }
+  static const long t64_below = getenv("FM_GEMM_F32_T64") ? atol(getenv("FM_GEMM_F32_T64")) : 128L;   // A/B knob
+  if (t128 < t64_below && K <= 2048) { BMv = 64; BNv = 64; }
   p.tiles_m = (M + BMv - 1) / BMv;
   p.tiles_n = (N + BNv - 1) / BNv;
   const long tiles = (long)p.tiles_m * p.tiles_n * batch;
