@@ -74,7 +74,8 @@ def main(argv=None):
     if a.image_dir:
         from flexmi.utils.images import ImageFolderLoader
         img = next(t for t in built.inputs.values() if len(t.dims) == 4)
-        loader = ImageFolderLoader(model, img, model.get_label_tensor(), a.image_dir, shuffle=True, seed=comm.rank)
+        loader = ImageFolderLoader(model, img, model.get_label_tensor(), a.image_dir, shuffle=True, seed=comm.rank,
+                                   threads=16)
         loader.next_batch()
     for _ in range(a.warmup):
         ex.train_step()

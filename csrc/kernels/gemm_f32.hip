@@ -258,9 +258,10 @@ FM_DEVICE void epilogue_f32(const GemmF& p, const f32x4_t (&acc)[MR][NR], int zb
   }
 }
 
-// OPT (tuning variants, FM_GEMM_F32_VARIANT bits 4/8): 1 = s_setprio(1) around each MFMA cluster;
-// 2 = fragment double buffer: the next k-chunk's LDS fragments are read before this chunk's MFMAs
-// and interleaved with them (sched_group_barrier), so only the first chunk of a K tile waits on LDS.
+// OPT: 1 = s_setprio(1) around each MFMA cluster (A/B only); 2 = fragment double buffer (default):
+// the second k-chunk's LDS fragments are read before the first chunk's MFMAs and interleaved with
+// them (sched_group_barrier).  Measured A/B, incl. removed experiments (de-phased blocks, diagnostic
+// kernels without the K-loop loads / stores): profiles/gemm_f32_variants_ab.jsonl, gemm_f32_diag.jsonl.
 // NT = 256 (4 waves, 2x2, wave tile BM/2 x BN/2) or 512 (8 waves, 2x4 for BN >= 128, else 4x2:
 // twice the waves per SIMD to cover the LDS-read and barrier latency of each K tile).
 template <int BM, int BN, bool AK, bool BKC, bool VEC, int OPT = 0, int NT = NTF>
@@ -313,13 +314,10 @@ __global__ void __launch_bounds__(NT, 2) fm_gemm_f32_kernel(GemmF p) {
     if (rowsum) sa.accumulate_rows(rs);
   }
   __syncthreads();
-  if constexpr ((OPT & 4) != 0) {   // experiment: de-phase co-resident blocks by ~half a K tile
-    if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(64);
-  }
   for (int kt = kt0; kt < kt1; ++kt) {
     const int cur = (kt - kt0) & 1;
     const bool more = kt + 1 < kt1;
-    if (more && (OPT & 8) == 0) {   // OPT 8/16: diagnostic variants (wrong results) without the K-loop loads
+    if (more) {
       sa.load(A, p.lda, m0, p.M, (kt + 1) * BKF, p.K, tid);
       sb.load(B, p.ldb, n0, p.N, (kt + 1) * BKF, p.K, tid);
     }
@@ -370,7 +368,7 @@ __global__ void __launch_bounds__(NT, 2) fm_gemm_f32_kernel(GemmF p) {
       if constexpr ((OPT & 1) != 0) __builtin_amdgcn_s_setprio(0);
     }
     }
-    if (more && (OPT & 16) == 0) {
+    if (more) {
       sa.store(LDSF_A(cur ^ 1), tid);
       sb.store(LDSF_B(cur ^ 1), tid);
       if (rowsum) sa.accumulate_rows(rs);
@@ -437,12 +435,6 @@ void launch_f(const GemmF& p, hipStream_t s, int opt) {
       case 5: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 0, 256>), grid, dim3(NTF), LDS, s, p); return;
       case 1: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 1>), grid, dim3(NTF), LDS, s, p); return;
       case 2: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 2>), grid, dim3(NTF), LDS, s, p); return;
-      case 4: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 4>), grid, dim3(NTF), LDS, s, p); return;
-      case 6: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 6>), grid, dim3(NTF), LDS, s, p); return;
-      case 8: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 8>), grid, dim3(NTF), LDS, s, p); return;
-      case 24: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 24>), grid, dim3(NTF), LDS, s, p); return;
-      case 32: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 0, 512>), grid, dim3(512), LDS, s, p); return;
-      case 56: hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 24, 512>), grid, dim3(512), LDS, s, p); return;
       default: break;
     }
   }
@@ -707,7 +699,9 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
   int BMv = 128, BNv = 128;
   const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;
   if (t128 < 512 && N <= 64 * 8) BNv = 64;
-  static const long t64_below = getenv("FM_GEMM_F32_T64") ? atol(getenv("FM_GEMM_F32_T64")) : 128L;   // A/B knob
+  // 64x64 tiles (no split-K, 4 blocks per CU) up to one wave of 128x128 tiles: the 8192x512->256
+  // forward runs unsplit instead of split-K 2 + reduce (step -0.9 %: profiles/ab_f32_t64.txt)
+  static const long t64_below = getenv("FM_GEMM_F32_T64") ? atol(getenv("FM_GEMM_F32_T64")) : 129L;
   if (t128 < t64_below && K <= 2048) { BMv = 64; BNv = 64; }
   p.tiles_m = (M + BMv - 1) / BMv;
   p.tiles_n = (N + BNv - 1) / BNv;
