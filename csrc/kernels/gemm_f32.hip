@@ -700,7 +700,7 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
   const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;
   if (t128 < 512 && N <= 64 * 8) BNv = 64;
   // 64x64 tiles (no split-K, 4 blocks per CU) up to one wave of 128x128 tiles: the 8192x512->256
-  // forward runs unsplit instead of split-K 2 + reduce (step -0.9 %: profiles/ab_f32_t64.txt)
+  // forward runs unsplit instead of split-K 2 + reduce (step -0.2..0.9 %: profiles/ab_f32_t64.txt)
   static const long t64_below = getenv("FM_GEMM_F32_T64") ? atol(getenv("FM_GEMM_F32_T64")) : 129L;
   if (t128 < t64_below && K <= 2048) { BMv = 64; BNv = 64; }
   p.tiles_m = (M + BMv - 1) / BMv;
