@@ -28,16 +28,16 @@ namespace {
 constexpr int NT = 256;
 
 // ---- global -> registers (one tile of an operand) --------------------------------------
-template <bool KC, int R, bool VEC>
+template <bool KC, int R, bool VEC, int NTH = NT>
 struct Stage {
   static constexpr int CHUNKS = R * BK / 8;
-  static constexpr int PER_T = CHUNKS / NT;
+  static constexpr int PER_T = CHUNKS / NTH;
   u32x4_t v[PER_T];
 
   FM_DEVICE void load(const unsigned short* __restrict__ p, long ld, int row0, int rows, int k0, int K, int tid) {
 #pragma unroll
     for (int i = 0; i < PER_T; ++i) {
-      int ci = tid + NT * i;
+      int ci = tid + NTH * i;
       int r, c, gr, gk;
       if constexpr (KC) {
         r = ci >> 3; c = ci & 7;
@@ -71,7 +71,7 @@ struct Stage {
   FM_DEVICE void store(char* lds, int tid) {
 #pragma unroll
     for (int i = 0; i < PER_T; ++i) {
-      int ci = tid + NT * i;
+      int ci = tid + NTH * i;
       int a, c;
       if constexpr (KC) { a = ci >> 3; c = ci & 7; }
       else { a = ci / (R / 8); c = ci % (R / 8); }
@@ -95,12 +95,16 @@ struct Stage {
   }
 };
 
-template <int BM, int BN, bool AK, bool BKC, bool VEC>
-__global__ void __launch_bounds__(NT, 2) fm_gemm_kernel(GemmP p) {
+// NTH = 256: 4 waves (2x2, wave tile BM/2 x BN/2); 512: 8 waves (2x4 for BN >= 128, else 4x2).
+template <int BM, int BN, bool AK, bool BKC, bool VEC, int NTH = NT>
+__global__ void __launch_bounds__(NTH, 2) fm_gemm_kernel(GemmP p) {
   constexpr int A_BYTES = BM * BK * 2;
   constexpr int B_BYTES = BN * BK * 2;
-  constexpr int MR = BM / 32;  // 16-row subtiles per wave (wave covers BM/2)
-  constexpr int NR = BN / 32;
+  constexpr int WN = (NTH == 512 && BN >= 128) ? 4 : 2;
+  constexpr int WM = NTH / 64 / WN;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int MR = TM / 16;  // 16-row subtiles per wave
+  constexpr int NR = TN / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // buffer b of operand X at smem + b*(A_BYTES+B_BYTES) (+A_BYTES for B)
 #define LDS_A(b) (smem + (b) * (A_BYTES + B_BYTES))
@@ -109,7 +113,7 @@ __global__ void __launch_bounds__(NT, 2) fm_gemm_kernel(GemmP p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
 
   // XCD-aware bijective remap of the tile id (blocks b and b+8 share an XCD)
   const int bid = xcd_remap(blockIdx.x, p.tiles_m * p.tiles_n);
@@ -133,8 +137,8 @@ __global__ void __launch_bounds__(NT, 2) fm_gemm_kernel(GemmP p) {
 #pragma unroll
     for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  Stage<AK, BM, VEC> sa;
-  Stage<BKC, BN, VEC> sb;
+  Stage<AK, BM, VEC, NTH> sa;
+  Stage<BKC, BN, VEC, NTH> sb;
   const bool rowsum = (!AK) && (p.rowsum_a != nullptr) && (tn == 0);
   float rs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (kt0 < kt1) {
@@ -159,9 +163,9 @@ __global__ void __launch_bounds__(NT, 2) fm_gemm_kernel(GemmP p) {
     for (int kk = 0; kk < BK / 32; ++kk) {
       bf16x8_t af[MR], bfr[NR];
 #pragma unroll
-      for (int i = 0; i < MR; ++i) af[i] = frag<AK, BM>(la, wm * (BM / 2) + 16 * i, kk, lane);
+      for (int i = 0; i < MR; ++i) af[i] = frag<AK, BM>(la, wm * TM + 16 * i, kk, lane);
 #pragma unroll
-      for (int j = 0; j < NR; ++j) bfr[j] = frag<BKC, BN>(lb, wn * (BN / 2) + 16 * j, kk, lane);
+      for (int j = 0; j < NR; ++j) bfr[j] = frag<BKC, BN>(lb, wn * TN + 16 * j, kk, lane);
 #pragma unroll
       for (int i = 0; i < MR; ++i)
 #pragma unroll
@@ -186,7 +190,7 @@ __global__ void __launch_bounds__(NT, 2) fm_gemm_kernel(GemmP p) {
       __syncthreads();
       if (tid < BM) {
         float x = 0.f;
-        for (int t = 0; t < NT / G; ++t) x += red[t * BM + tid];
+        for (int t = 0; t < NTH / G; ++t) x += red[t * BM + tid];
         if (m0 + tid < p.M) atomicAdd(p.rowsum_a + m0 + tid, x);
       }
       __syncthreads();
@@ -195,7 +199,7 @@ __global__ void __launch_bounds__(NT, 2) fm_gemm_kernel(GemmP p) {
 
 #undef LDS_A
 #undef LDS_B
-  gemm_epilogue<MR, NR>(p, acc, zb, split, m0 + wm * (BM / 2), n0 + wn * (BN / 2), lane);
+  gemm_epilogue<MR, NR>(p, acc, zb, split, m0 + wm * TM, n0 + wn * TN, lane);
 }
 
 __global__ void fm_gemm_splitk_reduce(GemmP p);
@@ -251,10 +255,18 @@ __global__ void fm_gemm_splitk_reduce(GemmP p) {
   }
 }
 
+static int g_gemm_variant_early();
+
 template <int BM, int BN, bool AK, bool BKC, bool VEC>
 void launch_t(const GemmP& p, hipStream_t s) {
   constexpr int LDS = 2 * (BM + BN) * BK * 2;
   dim3 grid(p.tiles_m * p.tiles_n, p.batch, p.ksplit);
+  if constexpr (VEC && BM == 128) {   // variant bit 256: the 8-wave form of the 128-row tiles (A/B)
+    if (g_gemm_variant_early() & 256) {
+      hipLaunchKernelGGL((fm_gemm_kernel<BM, BN, AK, BKC, VEC, 512>), grid, dim3(512), LDS, s, p);
+      return;
+    }
+  }
   hipLaunchKernelGGL((fm_gemm_kernel<BM, BN, AK, BKC, VEC>), grid, dim3(NT), LDS, s, p);
 }
 
@@ -282,6 +294,9 @@ extern "C" void fm_gemm_glds_launch(const void* params, int bm, int bn, int a_kc
 // grid size (K % 64 == 0), 4 = glds 128x128 tiles, 8 = s_setprio around the glds MFMA blocks,
 // 64 = 256x128 glds tile with 4 waves of 128x64, 128 = in-launch split-K combine (split_counters)
 static int g_gemm_variant = getenv("FM_GEMM_VARIANT") ? atoi(getenv("FM_GEMM_VARIANT")) : 0;
+namespace {
+int g_gemm_variant_early() { return g_gemm_variant; }
+}
 
 // Per-device tile arrival counters of the in-launch split-K combine (gemm_common.h): zeroed once
 // at allocation; each tile's last arriver resets its own counter, so consecutive launches on the
