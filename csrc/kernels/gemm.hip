@@ -261,8 +261,11 @@ template <int BM, int BN, bool AK, bool BKC, bool VEC>
 void launch_t(const GemmP& p, hipStream_t s) {
   constexpr int LDS = 2 * (BM + BN) * BK * 2;
   dim3 grid(p.tiles_m * p.tiles_n, p.batch, p.ksplit);
-  if constexpr (VEC && BM == 128) {   // variant bit 256: the 8-wave form of the 128-row tiles (A/B)
-    if (g_gemm_variant_early() & 256) {
+  // default: the 8-wave form of the 128-row tiles (4 waves per SIMD hide the per-K-tile barrier and
+  // fragment latency: DLRM GEMMs -6 %, bf16 step 0.673 -> 0.626 ms, profiles/gemm_bf16_8wave_ab.jsonl);
+  // variant bit 256 = the 4-wave kernel
+  if constexpr (VEC && BM == 128) {
+    if (!(g_gemm_variant_early() & 256)) {
       hipLaunchKernelGGL((fm_gemm_kernel<BM, BN, AK, BKC, VEC, 512>), grid, dim3(512), LDS, s, p);
       return;
     }
@@ -292,7 +295,8 @@ extern "C" void fm_gemm_glds_launch(const void* params, int bm, int bn, int a_kc
 
 // dispatch experiments (tools/gemm_probe.py): 1 = never glds, 2 = glds for every orientation and
 // grid size (K % 64 == 0), 4 = glds 128x128 tiles, 8 = s_setprio around the glds MFMA blocks,
-// 64 = 256x128 glds tile with 4 waves of 128x64, 128 = in-launch split-K combine (split_counters)
+// 64 = 256x128 glds tile with 4 waves of 128x64, 128 = in-launch split-K combine (split_counters),
+// 256 = 4-wave register-staged kernel instead of the 8-wave default
 static int g_gemm_variant = getenv("FM_GEMM_VARIANT") ? atoi(getenv("FM_GEMM_VARIANT")) : 0;
 namespace {
 int g_gemm_variant_early() { return g_gemm_variant; }
