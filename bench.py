@@ -58,15 +58,38 @@ def parse():
     return ap.parse_args()
 
 
+def launch_ranks(a) -> int:
+    """``--gpus N`` without a torchrun environment: spawn the N rank processes ourselves (one per
+    GPU, rendezvous on 127.0.0.1), like the reference's single ``-ll:gpu N`` command
+    (examples/cpp/DLRM/run_random.sh:9).  This parent never touches the GPU (no torch import at
+    all) and never execs: the ranks are children, rank 0 prints the JSON line on the inherited
+    stdout, and the parent exits with the launcher's return code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
     import torch
     import torch.distributed as dist
     from flexmi.parallel.comm import init_distributed
     comm = init_distributed()
     rank, world = comm.rank, comm.world
-    if world != a.gpus and rank == 0:
-        print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if world != a.gpus:
+        if rank == 0:
+            print(f"[bench] error: --gpus {a.gpus} but the process group has {world} ranks", file=sys.stderr)
+        sys.exit(3)
     if torch.cuda.is_available():
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
     cuda = torch.cuda.is_available()
@@ -213,6 +236,9 @@ def run_once(a, dtype, comm):
             "init_s": round(t_init, 2),
             "loss": round(met.get_loss(), 5),
             "table_scale": a.table_scale,
+            "backend": comm.backend if world > 1 else "none",
+            "rccl_world": dist.get_world_size() if (world > 1 and comm.backend == "nccl") else None,
+            "process_world": world,
         },
     }
     if search is not None:

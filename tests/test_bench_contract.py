@@ -52,6 +52,29 @@ def test_bench_two_ranks():
 
 
 @pytest.mark.multiproc
+def test_bench_self_launches_eight_ranks():
+    """``bench.py --gpus 8`` with no torchrun environment spawns its own 8 ranks (the driver may
+    invoke it exactly so) and still prints ONE JSON line with n_gpus 8."""
+    env_keys = ("WORLD_SIZE", "RANK", "LOCAL_RANK")
+    saved = {k: os.environ.pop(k) for k in env_keys if k in os.environ}
+    try:
+        r = _run([sys.executable, "bench.py", "--gpus", "8", "--steps", "2", "--warmup", "1",
+                  "--config", "mlperf", "--table-scale", "1e-4", "--batch-per-gpu", "64"])
+    finally:
+        os.environ.update(saved)
+    _check(r, 8)
+    assert r["config"]["process_world"] == 8 and r["config"]["backend"] == "gloo"
+
+
+def test_bench_refuses_world_mismatch():
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0",
+                        "--config", "tiny", "--batch-per-gpu", "8"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode != 0 and not [l for l in p.stdout.splitlines() if l.startswith("{")]
+
+
+@pytest.mark.multiproc
 @pytest.mark.parametrize("strategy", ["table", "dp", "search"])
 def test_bench_eight_ranks_mlperf_plan(strategy):
     """The exact 8-GPU plan the driver's scaling run builds (mlperf widths: d=128, 26 tables,
