@@ -46,6 +46,7 @@ struct GemmF {
   int M, N, K, act, beta, ksplit, batch;
   float alpha;
   int tiles_m, tiles_n, n_fast;
+  int atomic;           // split-K partials float-atomically added into C (32x32 kernel, beta = 1)
 };
 
 template <int N>
@@ -636,6 +637,340 @@ void launch_f_glds(const GemmF& p, bool ak, bool bk, hipStream_t s) {
   else hipLaunchKernelGGL((fm_gemm_f32_glds_kernel<BM, BN, WM, WN, false, false>), grid, dim3(NTH), LDS, s, p);
 }
 
+// ---- 32x32x2 kernel ---------------------------------------------------------------------------
+// v_mfma_f32_32x32x2_f32: half the MFMA instructions of the 16x16x4 form for the same tile (64
+// cycles each, latency = issue, so two accumulators in rotation keep the pipe full), and its
+// accumulator puts 32 consecutive OUTPUT COLUMNS on the 32 lanes of each half-wave: every
+// accumulator register is two 128-B row segments of C -- the full-rate shape for stores and for
+// no-return float atomics, so split-K partials are added straight into C (beta = 1 outputs, i.e.
+// the dW GEMMs whose gradients the optimizer zeroes) instead of slabs + a reduce launch.
+//   operand fragments for one 16-wide k-chunk: lane (q = lane & 31, h = lane >> 5) takes
+//   k = 8h + s at MFMA step s (s = 0..7), so two 16-B LDS reads per row feed 8 MFMAs;
+//   K-contiguous images [row][BK] with XOR-swizzled 16-B chunks (conflict-free ds_read_b128);
+//   MN-contiguous A [k][BM] with the wave's rows interleaved over its MR tiles (one b64/b128 read
+//   at a fixed k gives all MR fragments); MN-contiguous B [k][BN] read per lane (b32).
+template <int BK>
+FM_DEVICE int kcx_off(int r, int c) {
+  constexpr int CPR = BK / 4;                                 // 16-B chunks per row
+  constexpr int RPL = (256 / (BK * 4)) > 0 ? 256 / (BK * 4) : 1;   // rows per 256-B bank line
+  return r * (BK * 4) + 16 * (c ^ ((r / RPL) & (CPR - 1)));
+}
+
+template <bool KC, int R, int BK, int NT>
+struct StageX {
+  static constexpr int CHUNKS = R * BK / 4;
+  static constexpr int PER_T = CHUNKS / NT;
+  static_assert(PER_T >= 1 && CHUNKS % NT == 0, "tile too small for the block");
+  f32x4_t v[PER_T];
+
+  FM_DEVICE void load(const float* __restrict__ p, long ld, int row0, int rows, int k0, int K, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int ci = tid + NT * i;
+      int gr, gk;
+      if constexpr (KC) {
+        gr = row0 + ci / (BK / 4);
+        gk = k0 + 4 * (ci % (BK / 4));
+      } else {
+        gk = k0 + ci / (R / 4);
+        gr = row0 + 4 * (ci % (R / 4));
+      }
+      if (gr < rows && gk < K) {
+        const float* src = KC ? (p + (long)gr * ld + gk) : (p + (long)gk * ld + gr);
+        v[i] = *reinterpret_cast<const f32x4_t*>(src);
+      } else {
+        v[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
+  FM_DEVICE void store(char* lds, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int ci = tid + NT * i;
+      int off;
+      if constexpr (KC) off = kcx_off<BK>(ci / (BK / 4), ci % (BK / 4));
+      else off = (ci / (R / 4)) * (R * 4) + 16 * (ci % (R / 4));
+      *reinterpret_cast<f32x4_t*>(lds + off) = v[i];
+    }
+  }
+  FM_DEVICE void accumulate_rows(float (&s)[4]) const {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s[j] += v[i][j];
+  }
+};
+
+// A fragments (M side, T = MR tiles) for k-chunk kk: f[t][s], s = 0..7
+template <bool KC, int R, int BK, int T>
+FM_DEVICE void frags_a32(const char* lds, int base, int kk, int lane, float (&f)[T][8]) {
+  const int q = lane & 31, h = lane >> 5;
+  if constexpr (KC) {
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int row = base + 32 * t + q;
+      const f32x4_t x0 = *reinterpret_cast<const f32x4_t*>(lds + kcx_off<BK>(row, 4 * kk + 2 * h));
+      const f32x4_t x1 = *reinterpret_cast<const f32x4_t*>(lds + kcx_off<BK>(row, 4 * kk + 2 * h + 1));
+#pragma unroll
+      for (int s = 0; s < 4; ++s) { f[t][s] = x0[s]; f[t][4 + s] = x1[s]; }
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int k = 16 * kk + 8 * h + s;
+      const fvec<T> x = *reinterpret_cast<const fvec<T>*>(lds + k * (R * 4) + 4 * (base + T * q));
+#pragma unroll
+      for (int t = 0; t < T; ++t) f[t][s] = x[t];
+    }
+  }
+}
+
+// B fragments (N side, T = NR tiles, never interleaved: lane q <-> column base + 32t + q)
+template <bool KC, int R, int BK, int T>
+FM_DEVICE void frags_b32(const char* lds, int base, int kk, int lane, float (&f)[T][8]) {
+  const int q = lane & 31, h = lane >> 5;
+  if constexpr (KC) {
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int row = base + 32 * t + q;
+      const f32x4_t x0 = *reinterpret_cast<const f32x4_t*>(lds + kcx_off<BK>(row, 4 * kk + 2 * h));
+      const f32x4_t x1 = *reinterpret_cast<const f32x4_t*>(lds + kcx_off<BK>(row, 4 * kk + 2 * h + 1));
+#pragma unroll
+      for (int s = 0; s < 4; ++s) { f[t][s] = x0[s]; f[t][4 + s] = x1[s]; }
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int k = 16 * kk + 8 * h + s;
+#pragma unroll
+      for (int t = 0; t < T; ++t) f[t][s] = *reinterpret_cast<const float*>(lds + k * (R * 4) + 4 * (base + 32 * t + q));
+    }
+  }
+}
+
+// lane (q, h) holds acc[i][j][r] = C[m][n]:  n = nbase + 32 j + q,
+//   im = 8 (r >> 2) + 4 h + (r & 3),  m = IL_A ? mbase + MR im + i : mbase + 32 i + im
+template <int MR, int NR, bool IL_A>
+FM_DEVICE void epilogue_x32(const GemmF& p, const f32x16_t (&acc)[MR][NR], int zb, int split, int mbase, int nbase,
+                            int lane) {
+  const int q = lane & 31, h = lane >> 5;
+  if (p.ksplit > 1 && !p.atomic) {
+    float* ws = p.ws + ((long)zb * p.ksplit + split) * (long)p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int im = 8 * (r >> 2) + 4 * h + (r & 3);
+        const int m = IL_A ? mbase + MR * im + i : mbase + 32 * i + im;
+        if (m >= p.M) continue;
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+          const int n = nbase + 32 * j + q;
+          if (n < p.N) ws[(long)m * p.N + n] = acc[i][j][r];
+        }
+      }
+    return;
+  }
+  float* Cz = p.C + (long)zb * p.sC;
+  if (p.atomic) {   // split-K partials (and any beta = 1 output): no-return float atomics, 128-B rows
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int im = 8 * (r >> 2) + 4 * h + (r & 3);
+        const int m = IL_A ? mbase + MR * im + i : mbase + 32 * i + im;
+        if (m >= p.M) continue;
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+          const int n = nbase + 32 * j + q;
+          if (n < p.N) atomicAdd(Cz + (long)m * p.ldc + n, p.alpha * acc[i][j][r]);
+        }
+      }
+    return;
+  }
+  float bias[NR], csum[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    const int n = nbase + 32 * j + q;
+    bias[j] = (p.bias && n < p.N) ? p.bias[n] : 0.f;
+    csum[j] = 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int im = 8 * (r >> 2) + 4 * h + (r & 3);
+      const int m = IL_A ? mbase + MR * im + i : mbase + 32 * i + im;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int j = 0; j < NR; ++j) {
+        const int n = nbase + 32 * j + q;
+        if (n >= p.N) continue;
+        float v = act_fwd(p.act, acc[i][j][r] * p.alpha + bias[j]);
+        if (p.ay) v = act_bwd(p.bact, p.ay[(long)m * p.lday + n], v);
+        csum[j] += v;
+        float* dst = Cz + (long)m * p.ldc + n;
+        *dst = p.beta ? *dst + v : v;
+      }
+    }
+  if (p.colsum) {
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const float x = csum[j] + __shfl_xor(csum[j], 32, 64);
+      const int n = nbase + 32 * j + q;
+      if (h == 0 && n < p.N) atomicAdd(p.colsum + n, x);
+    }
+  }
+}
+
+// WM x WN waves, wave tile (BM/WM) x (BN/WN) = MR x NR 32x32 tiles; BK-deep LDS tiles, two stages,
+// register-staged global loads of the next tile issued before the current tile's MFMAs.
+template <int BM, int BN, int BK, int WM, int WN, bool AK, bool BKC, int MINB>
+__global__ void __launch_bounds__(WM * WN * 64, MINB) fm_gemm_f32x_kernel(GemmF p) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int MR = TM / 32, NR = TN / 32;
+  static_assert(MR >= 1 && NR >= 1 && MR * NR >= 2, "need >= 2 accumulators (MFMA latency = issue)");
+  static_assert(AK || MR == 1 || MR == 2 || MR == 4, "interleaved A reads b32/b64/b128");
+  constexpr int A_BYTES = BM * BK * 4;
+  constexpr int B_BYTES = BN * BK * 4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+
+  const int bid = xcd_remap_f(blockIdx.x, p.tiles_m * p.tiles_n);
+  int tm, tn;
+  if (p.n_fast) { tn = bid % p.tiles_n; tm = bid / p.tiles_n; }
+  else { tm = bid % p.tiles_m; tn = bid / p.tiles_m; }
+  const int zb = blockIdx.y;
+  const int split = blockIdx.z;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const float* A = p.A + (long)zb * p.sA;
+  const float* B = p.B + (long)zb * p.sB;
+
+  const int ktiles_total = (p.K + BK - 1) / BK;
+  const int kt_per = (ktiles_total + p.ksplit - 1) / p.ksplit;
+  const int kt0 = split * kt_per;
+  const int kt1 = min(ktiles_total, kt0 + kt_per);
+
+  f32x16_t acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  StageX<AK, BM, BK, NT> sa;
+  StageX<BKC, BN, BK, NT> sb;
+  const bool rowsum = (!AK) && (p.rowsum_a != nullptr) && (tn == 0);
+  float rs[4] = {0.f, 0.f, 0.f, 0.f};
+#define LDSX(b) (smem + (b) * (A_BYTES + B_BYTES))
+  if (kt0 < kt1) {
+    sa.load(A, p.lda, m0, p.M, kt0 * BK, p.K, tid);
+    sb.load(B, p.ldb, n0, p.N, kt0 * BK, p.K, tid);
+    sa.store(LDSX(0), tid);
+    sb.store(LDSX(0) + A_BYTES, tid);
+    if (rowsum) sa.accumulate_rows(rs);
+  }
+  __syncthreads();
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int cur = (kt - kt0) & 1;
+    const bool more = kt + 1 < kt1;
+    if (more) {
+      sa.load(A, p.lda, m0, p.M, (kt + 1) * BK, p.K, tid);
+      sb.load(B, p.ldb, n0, p.N, (kt + 1) * BK, p.K, tid);
+    }
+    const char* la = LDSX(cur);
+    const char* lb = la + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      float af[MR][8], bfr[NR][8];
+      frags_a32<AK, BM, BK, MR>(la, wm * TM, kk, lane, af);
+      frags_b32<BKC, BN, BK, NR>(lb, wn * TN, kk, lane, bfr);
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+#pragma unroll
+          for (int j = 0; j < NR; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      sa.store(LDSX(cur ^ 1), tid);
+      sb.store(LDSX(cur ^ 1) + A_BYTES, tid);
+      if (rowsum) sa.accumulate_rows(rs);
+    }
+    __syncthreads();
+  }
+#undef LDSX
+  if constexpr (!AK) {
+    if (rowsum) {
+      float* red = reinterpret_cast<float*>(smem);
+      constexpr int G = BM / 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[(tid / G) * BM + (tid % G) * 4 + j] = rs[j];
+      __syncthreads();
+      for (int r = tid; r < BM; r += NT) {
+        float x = 0.f;
+        for (int t = 0; t < NT / G; ++t) x += red[t * BM + r];
+        if (m0 + r < p.M) atomicAdd(p.rowsum_a + m0 + r, x);
+      }
+      __syncthreads();
+    }
+  }
+  epilogue_x32<MR, NR, !AK>(p, acc, zb, split, m0 + wm * TM, n0 + wn * TN, lane);
+}
+
+template <int BM, int BN, int BK, int WM, int WN, int MINB>
+void launch_x(const GemmF& p, bool ak, bool bk, hipStream_t s) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int LDS = 2 * (BM + BN) * BK * 4;
+  static bool attr_set = false;
+  if (!attr_set) {
+    auto set = [](const void* f) { (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS); };
+    set((const void*)fm_gemm_f32x_kernel<BM, BN, BK, WM, WN, true, true, MINB>);
+    set((const void*)fm_gemm_f32x_kernel<BM, BN, BK, WM, WN, true, false, MINB>);
+    set((const void*)fm_gemm_f32x_kernel<BM, BN, BK, WM, WN, false, true, MINB>);
+    set((const void*)fm_gemm_f32x_kernel<BM, BN, BK, WM, WN, false, false, MINB>);
+    attr_set = true;
+  }
+  dim3 grid(p.tiles_m * p.tiles_n, p.batch, p.ksplit);
+  if (ak && bk) hipLaunchKernelGGL((fm_gemm_f32x_kernel<BM, BN, BK, WM, WN, true, true, MINB>), grid, dim3(NT), LDS, s, p);
+  else if (ak) hipLaunchKernelGGL((fm_gemm_f32x_kernel<BM, BN, BK, WM, WN, true, false, MINB>), grid, dim3(NT), LDS, s, p);
+  else if (bk) hipLaunchKernelGGL((fm_gemm_f32x_kernel<BM, BN, BK, WM, WN, false, true, MINB>), grid, dim3(NT), LDS, s, p);
+  else hipLaunchKernelGGL((fm_gemm_f32x_kernel<BM, BN, BK, WM, WN, false, false, MINB>), grid, dim3(NT), LDS, s, p);
+}
+
+// tile configurations of the 32x32 kernel (index = FM_GEMM_F32_VARIANT - 1000 for A/B runs)
+struct XCfg { int bm, bn, bk, wm, wn; };
+constexpr XCfg kXCfgs[] = {
+    {128, 128, 32, 2, 2},   // 0: 4 waves of 64x64, 64 KB LDS -> 2 blocks / CU
+    {128, 128, 32, 4, 2},   // 1: 8 waves of 32x64
+    {256, 128, 32, 4, 2},   // 2: 8 waves of 64x64, 96 KB LDS -> 1 block / CU
+    {256, 128, 16, 4, 2},   // 3: 8 waves of 64x64, 48 KB LDS -> 2 blocks / CU (VGPR permitting)
+    {128, 256, 32, 2, 4},   // 4: 8 waves of 64x64
+    {128, 128, 16, 2, 2},   // 5: 4 waves, 32 KB LDS
+    {128, 64, 32, 2, 2},    // 6: 4 waves of 64x32
+    {64, 64, 32, 2, 1},     // 7: 2 waves of 32x64
+};
+constexpr int kNumXCfgs = sizeof(kXCfgs) / sizeof(kXCfgs[0]);
+
+void launch_x_cfg(int c, const GemmF& p, bool ak, bool bk, hipStream_t s) {
+  switch (c) {
+    case 0: launch_x<128, 128, 32, 2, 2, 2>(p, ak, bk, s); break;
+    case 1: launch_x<128, 128, 32, 4, 2, 2>(p, ak, bk, s); break;
+    case 2: launch_x<256, 128, 32, 4, 2, 1>(p, ak, bk, s); break;
+    case 3: launch_x<256, 128, 16, 4, 2, 2>(p, ak, bk, s); break;
+    case 4: launch_x<128, 256, 32, 2, 4, 1>(p, ak, bk, s); break;
+    case 5: launch_x<128, 128, 16, 2, 2, 2>(p, ak, bk, s); break;
+    case 6: launch_x<128, 64, 32, 2, 2, 2>(p, ak, bk, s); break;
+    default: launch_x<64, 64, 32, 2, 1, 4>(p, ak, bk, s); break;
+  }
+}
+
 }  // namespace
 
 static int g_f32_variant = getenv("FM_GEMM_F32_VARIANT") ? atoi(getenv("FM_GEMM_F32_VARIANT")) : 0;
@@ -664,6 +999,33 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
   // ties the register-staged kernel on the 1024-wide layers (150.8 vs 150.7 us) and loses on the
   // small-grid ones (one 96 KiB block per CU: 22 -> 39 us, 29 -> 45 us), 1.72 vs 1.68 ms/step.
   const int variant = g_f32_variant;
+  p.atomic = 0;
+  if (vec && variant >= 1000 && variant < 1200 && K > 0) {
+    const XCfg c = kXCfgs[((variant - 1000) % 100) % kNumXCfgs];
+    const bool atomic_ok = ((variant - 1000) / 100 == 1) && beta && bias == nullptr && act == ACT_NONE &&
+                           act_y == nullptr && colsum == nullptr;
+    p.tiles_m = (M + c.bm - 1) / c.bm;
+    p.tiles_n = (N + c.bn - 1) / c.bn;
+    const long tiles = (long)p.tiles_m * p.tiles_n * batch;
+    const int ktiles = (K + c.bk - 1) / c.bk;
+    int ks = 1;
+    if (ksplit_req > 0) ks = ksplit_req;
+    else if (ws != nullptr || atomic_ok) {
+      const long target = (c.bm * c.bn >= 256 * 128) ? 256L : 512L;
+      while (tiles * ks < target && ks * 2 <= ktiles / 4 && ks < 32) ks *= 2;
+    }
+    if (act_y != nullptr || colsum != nullptr) ks = 1;
+    if (ks > 1 && !atomic_ok && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks = 1;
+    p.ksplit = ks;
+    p.atomic = (ks > 1 && atomic_ok) ? 1 : 0;
+    launch_x_cfg((variant - 1000) % 100, p, a_kcontig, b_kcontig, stream);
+    if (ks > 1 && !p.atomic) {
+      const int v4 = (N % 4 == 0) && (ldc % 4 == 0) && (sC % 4 == 0) && al(C);
+      const long total = (long)M * N * batch / (v4 ? 4 : 1);
+      hipLaunchKernelGGL(fm_gemm_f32_reduce, dim3(fm_grid(total)), dim3(256), 0, stream, p, v4);
+    }
+    return ks;
+  }
   const long t256 = (long)((M + 255) / 256) * ((N + 127) / 128) * batch;
   const long t128g = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;
   const bool mn_ok = (a_kcontig || M >= 4) && (b_kcontig || N >= 4);

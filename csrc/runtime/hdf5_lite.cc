@@ -3,6 +3,7 @@
 // continuation messages, v1 B-trees, local heaps, symbol table nodes).
 #include "hdf5_lite.h"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <functional>
@@ -24,7 +25,7 @@ struct File {
     if (f) fclose(f);
   }
   std::vector<uint8_t> read(uint64_t off, size_t n) const {
-    if (off == UNDEF || (int64_t)(off + n) > size) throw std::runtime_error("read past end of file");
+    if (off == UNDEF || off > (uint64_t)size || n > (uint64_t)size - off) throw std::runtime_error("read past end of file");
     std::vector<uint8_t> b(n);
     if (fseeko(f, (off_t)off, SEEK_SET) != 0 || fread(b.data(), 1, n, f) != n) throw std::runtime_error("short read");
     return b;
@@ -35,6 +36,7 @@ struct Cur {   // little-endian cursor over a byte buffer
   const std::vector<uint8_t>& b;
   size_t p;
   uint64_t u(int n) {
+    if (n < 1 || n > 8) throw std::runtime_error("bad field width");
     if (p + n > b.size()) throw std::runtime_error("truncated structure");
     uint64_t v = 0;
     for (int i = 0; i < n; ++i) v |= (uint64_t)b[p + i] << (8 * i);
@@ -46,7 +48,10 @@ struct Cur {   // little-endian cursor over a byte buffer
     if (so < 8 && v == ((1ULL << (8 * so)) - 1)) return UNDEF;
     return v;
   }
-  void skip(size_t n) { p += n; }
+  void skip(size_t n) {
+    if (n > b.size() - std::min(p, b.size())) throw std::runtime_error("truncated structure");
+    p += n;
+  }
 };
 
 struct Msg {
@@ -234,6 +239,7 @@ void walk(const File& F, uint64_t ohdr, const std::string& prefix, std::vector<H
       if (fl & 0x04) c.skip(8);
       if (fl & 0x10) c.skip(1);
       uint64_t nlen = c.u(1 << (fl & 3));
+      if (nlen > m.data.size() - c.p) throw std::runtime_error("link name past message");
       std::string name(m.data.begin() + c.p, m.data.begin() + c.p + nlen);
       c.skip(nlen);
       if (ltype == 0) kids.emplace_back(name, c.addr(F.so));
@@ -252,11 +258,15 @@ void walk(const File& F, uint64_t ohdr, const std::string& prefix, std::vector<H
     ds.dtype = dtype_of(type->data);
     ds.shape = shape_of(F, space->data);
     layout_of(F, layout->data, ds);
-    if (ds.nbytes == 0) {
-      int64_t n = std::stoi(ds.dtype.substr(2));
-      for (auto s : ds.shape) n *= s;
-      ds.nbytes = n;
+    int64_t n = std::stoi(ds.dtype.substr(2));
+    for (auto s : ds.shape) {
+      if (s < 0 || (s > 0 && n > (int64_t(1) << 62) / s)) throw std::runtime_error("bad dataspace extent");
+      n *= s;
     }
+    if (ds.nbytes == 0) ds.nbytes = n;
+    if (ds.nbytes < n) throw std::runtime_error("dataset '" + prefix + "' is smaller than its dataspace");
+    if (ds.offset >= 0 && (ds.offset > F.size || ds.nbytes > F.size - ds.offset))
+      throw std::runtime_error("dataset '" + prefix + "' extends past the end of the file");
     out.push_back(ds);
     return;
   }
@@ -283,11 +293,17 @@ bool h5_list_datasets(const std::string& path, std::vector<H5Dataset>& out, std:
     }
     if (sb < 0) throw std::runtime_error("not an HDF5 file");
     auto h = F.read(sb, std::min<int64_t>(128, F.size - sb));
+    if (h.size() < 16) throw std::runtime_error("truncated superblock");
     int ver = h[8];
     uint64_t root = UNDEF;
+    auto check_sizes = [&]() {
+      auto ok = [](int v) { return v == 2 || v == 4 || v == 8; };
+      if (!ok(F.so) || !ok(F.sl)) throw std::runtime_error("bad superblock offset/length sizes");
+    };
     if (ver <= 1) {
       F.so = h[13];
       F.sl = h[14];
+      check_sizes();
       Cur c{h, (size_t)(ver == 0 ? 24 : 28)};
       F.base = c.addr(F.so);
       c.addr(F.so);   // free-space info
@@ -298,6 +314,7 @@ bool h5_list_datasets(const std::string& path, std::vector<H5Dataset>& out, std:
     } else {
       F.so = h[9];
       F.sl = h[10];
+      check_sizes();
       Cur c{h, 12};
       F.base = c.addr(F.so);
       c.addr(F.so);   // superblock extension

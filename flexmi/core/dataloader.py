@@ -97,6 +97,17 @@ def synthetic_pair(ffmodel, input, label, batches=4, seed=0):
     return x, y, n
 
 
+def _host_array_as(arr, tdt):
+    """``arr`` as a C-contiguous host array whose BYTES are elements of torch dtype ``tdt`` (the
+    native ring copies raw bytes into the staging slots).  numpy has no bfloat16: a bf16 target
+    is converted through torch (round to nearest even) and returned as its int16 bit pattern."""
+    if tdt == torch.bfloat16:
+        t = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.float32)).to(torch.bfloat16)
+        return t.view(torch.int16).numpy()
+    npdt = torch.empty(0, dtype=tdt).numpy().dtype
+    return np.ascontiguousarray(arr, dtype=npdt)
+
+
 class NetConfig:
     def __init__(self):
         self.dataset_path = ""
@@ -139,10 +150,7 @@ class PrefetchLoader:
             if cols is not None or (full.ndim == 2 and len(dims) == 2 and full.shape[1] < dims[1]):
                 # column block of a 2-D source (zero-copy), zero-padded up to the tensor row
                 c0, c1 = cols if cols is not None else (0, full.shape[1])
-                arr = np.asarray(full)
-                if arr.dtype != np.dtype(str(tdt).replace("torch.", "")):
-                    arr = arr.astype(str(tdt).replace("torch.", ""))
-                arr = np.ascontiguousarray(arr)
+                arr = _host_array_as(np.asarray(full), tdt)
                 es = arr.itemsize
                 assert len(dims) == 2 and c1 - c0 <= dims[1] and box[1] == (0, dims[1]), \
                     "column-block sources feed whole rows of a 2-D input"

@@ -48,6 +48,85 @@ def test_hdf5_rejects_non_hdf5(tmp_path, native):
         list_datasets(str(p))
 
 
+def test_hdf5_rejects_truncated_and_corrupted(tmp_path, native):
+    """Malformed files raise a clean error (no read past a buffer, no shift by >= 64 bits)."""
+    from flexmi.utils.hdf5 import list_datasets, write_h5
+    p = str(tmp_path / "ok.h5")
+    write_h5(p, {"a": np.arange(4096, dtype=np.float32).reshape(64, 64)})
+    good = open(p, "rb").read()
+    info = list_datasets(p)
+    off, nb = info["a"][2], info["a"][3]
+    # data cut off: the dataset would extend past the end of the file
+    t = tmp_path / "trunc.h5"
+    t.write_bytes(good[:off + nb // 2])
+    with pytest.raises(RuntimeError, match="past the end|read past"):
+        list_datasets(str(t))
+    # superblock offset size 0 / 16 (would make the address decoder shift by >= 64 bits)
+    for bad in (0, 16):
+        b = bytearray(good)
+        b[9 if good[8] >= 2 else 13] = bad
+        c = tmp_path / f"so{bad}.h5"
+        c.write_bytes(bytes(b))
+        with pytest.raises(RuntimeError, match="sizes"):
+            list_datasets(str(c))
+    # every single-byte corruption of the metadata either parses or raises (never crashes)
+    rng = np.random.RandomState(0)
+    for i in range(64):
+        b = bytearray(good)
+        pos = int(rng.randint(0, min(off, len(good))))
+        b[pos] ^= int(rng.randint(1, 256))
+        c = tmp_path / f"c{i}.h5"
+        c.write_bytes(bytes(b))
+        try:
+            list_datasets(str(c))
+        except RuntimeError:
+            pass
+
+
+def test_host_array_as_bf16_staging():
+    """Column-block sources feeding a bf16 input are staged as bf16 bit patterns (numpy has no
+    bfloat16): round to nearest even, same as torch's cast."""
+    from flexmi.core.dataloader import _host_array_as
+    x = np.random.RandomState(0).randn(33, 13).astype(np.float32)
+    got = _host_array_as(x, torch.bfloat16)
+    assert got.dtype == np.int16 and got.shape == x.shape and got.flags["C_CONTIGUOUS"]
+    exp = torch.from_numpy(x).to(torch.bfloat16)
+    assert torch.equal(torch.from_numpy(got).view(torch.bfloat16), exp)
+    assert _host_array_as(x.astype(np.float64), torch.float32).dtype == np.float32
+    assert _host_array_as(np.arange(6), torch.int32).dtype == np.int32
+
+
+@pytest.mark.gpu
+def test_dlrm_dataset_default_bf16_on_gpu(tmp_path, native):
+    """apps/dlrm.py --dataset with the GPU default (bf16 compute): the dense column block is
+    staged as bf16 and the step trains (this crashed in numpy)."""
+    from flexmi.core import FFConfig, FFModel, LossType, MetricsType, SGDOptimizer
+    from flexmi.models.dlrm import DLRMConfig, HDF5DLRMData, build_dlrm
+    from flexmi.utils.hdf5 import write_h5
+    tables = [50, 20, 70, 9]
+    dcfg = DLRMConfig(8, tables, [13, 16, 8], [40, 16, 1], 1, -1, -1, 0.0, "cat", "", -1, "mse", "h5")
+    B, n = 32, 32 * 5
+    arrays = _criteo_like(n, tables)
+    path = str(tmp_path / "kaggle.h5")
+    write_h5(path, arrays)
+    cfg = FFConfig()
+    cfg.batchSize = B
+    m = FFModel(cfg)
+    d, s, _ = build_dlrm(m, dcfg)
+    m.compile(SGDOptimizer(m, 0.1), LossType.LOSS_MEAN_SQUARED_ERROR_AVG_REDUCE, [MetricsType.METRICS_ACCURACY])
+    ex = m.init_layers()
+    data = HDF5DLRMData(m, d, s, dcfg, path)
+    for _ in range(6):
+        data.next_batch()
+        ex.train_step()
+    torch.cuda.synchronize()
+    data.close()
+    dense = ex.local_buffer(d)
+    assert dense.dtype == torch.bfloat16
+    met = m.get_perf_metrics()
+    assert met.train_all == 6 * B and np.isfinite(met.get_loss())
+
+
 def _dlrm_model(dcfg, B, lt=0.0):
     from flexmi.core import FFConfig, FFModel, LossType, MetricsType, SGDOptimizer
     from flexmi.models.dlrm import build_dlrm
