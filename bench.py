@@ -20,6 +20,12 @@ activations / MFMA operands, fp32 master weights and accumulation) is measured a
 same process and reported as a secondary field ``config.bf16`` (``--dtype bf16`` makes it the
 headline, ``--no-secondary`` skips it).
 
+SOAP vs DP (N > 1): after the headline plan, the same model / precision / batch is built and timed
+under pure data parallelism -- every table replicated on every GPU and trained by touched-row
+exchange (each replica coalesces its lookups, one all-gather of (row, gradient) payloads, every
+replica applies them in rank order; no table-sized gradient) -- and reported as ``config.dp``
+with ``config.soap_speedup_vs_dp`` = value / dp.value (``--no-dp`` skips it).
+
 Timed region: W untimed steps, then EXACTLY K full training steps (forward, backward, all
 collectives, SGD update of every parameter incl. the sparse embedding rows) bracketed by a
 barrier + device synchronize on both sides; the max over ranks is reported.  Prints ONE JSON line.
@@ -55,6 +61,8 @@ def parse():
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
                     help="headline compute precision (fp32 = the reference's precision)")
     ap.add_argument("--no-secondary", action="store_true", help="skip the secondary run in the other precision")
+    ap.add_argument("--no-dp", action="store_true",
+                    help="N>1: skip the pure data-parallel comparison run (config.dp / config.soap_speedup_vs_dp)")
     return ap.parse_args()
 
 
@@ -97,11 +105,22 @@ def main():
     second = None
     if cuda and not a.no_secondary:
         second = run_once(a, "bf16" if a.dtype == "fp32" else "fp32", comm)
+    dp = None
+    if world > 1 and a.strategy != "dp" and not a.no_dp:
+        # the second half of the BASELINE metric: the same model, precision and batch under pure
+        # data parallelism (replicated tables trained by touched-row all-gather, DP MLPs)
+        dp = run_once(a, a.dtype, comm, strategy="dp")
     if rank == 0:
         rec = head["rec"]
         if second is not None:
             rec["config"][second["dtype"]] = {"value": second["rec"]["value"], "ms_per_step": second["rec"]["ms_per_step"],
                                               "loss": second["rec"]["config"]["loss"]}
+        if dp is not None:
+            rec["config"]["dp"] = {"value": dp["rec"]["value"], "ms_per_step": dp["rec"]["ms_per_step"],
+                                   "loss": dp["rec"]["config"]["loss"], "parallelism": dp["rec"]["config"]["parallelism"]}
+            rec["config"]["soap_speedup_vs_dp"] = round(rec["value"] / dp["rec"]["value"], 3)
+        elif world == 1:
+            rec["config"]["soap_speedup_vs_dp"] = 1.0   # one GPU: the searched plan IS data parallel
         print(f"ELAPSED TIME = {head['el']:.4f}s, THROUGHPUT = {rec['value']:.2f} samples/s", file=sys.stderr)
         print(json.dumps(rec), flush=True)
     if world > 1:
@@ -109,9 +128,11 @@ def main():
         dist.destroy_process_group()
 
 
-def run_once(a, dtype, comm):
-    """Build, warm up and time one DLRM training configuration in compute precision ``dtype``;
-    frees the model before returning (the tables of the two precisions never coexist)."""
+def run_once(a, dtype, comm, strategy=None):
+    """Build, warm up and time one DLRM training configuration in compute precision ``dtype``
+    under ``strategy`` (default ``--strategy``); frees the model before returning (the tables of
+    two configurations never coexist)."""
+    strategy = strategy or a.strategy
     import gc
     import torch
     import torch.distributed as dist
@@ -130,9 +151,9 @@ def run_once(a, dtype, comm):
     dense_in, sparse, out = build_dlrm(model, dcfg)
     strategies = {}
     search = None
-    if world > 1 and a.strategy in ("table", "search"):
+    if world > 1 and strategy in ("table", "search"):
         strategies = dlrm_strategy(model, world)
-    if world > 1 and a.strategy == "search":
+    if world > 1 and strategy == "search":
         from flexmi.core import SGDOptimizer as _S
         from flexmi.parallel.search import optimize
         model.optimizer = _S(model, 0.01)
@@ -225,8 +246,8 @@ def run_once(a, dtype, comm):
             "model": f"DLRM {dcfg.name} ({'MLPerf-like: 13 dense + 26 sparse, Criteo-TB tables (187.8M rows x 128, fp32), dot interaction' if dcfg.name == 'mlperf' else dcfg.name})",
             "global_batch": gb,
             "seq_len": 1,
-            "parallelism": (f"dp{world}" if world == 1 or a.strategy == "dp" else
-                            f"soap-search{world}" if a.strategy == "search" else f"table+column-emb{world}+dp{world}-mlp"),
+            "parallelism": (f"dp{world}" if world == 1 or strategy == "dp" else
+                            f"soap-search{world}" if strategy == "search" else f"table+column-emb{world}+dp{world}-mlp"),
             "tables_rows": sum(dcfg.embedding_size),
             "embedding_dim": dcfg.sparse_feature_size,
             "mlp_bot": dcfg.mlp_bot,

@@ -41,6 +41,12 @@ void fm_embedding_bwd_multi(int n, float* const* W, const void* const* idx, cons
                             const long* ldg, const long* lo, const int* rows, const int* D, const int* bag,
                             const float* scale, int dy_bf16, const float* lr, long B, int* const* owner,
                             int* const* dups, int* const* ndup, hipStream_t st);
+void fm_sdp_coalesce(int n, const void* const* idx, const int* idx64, const void* const* dy, const long* ldg,
+                     const long* lo, const int* rows, const int* D, const int* bag, const float* scale, int dy_bf16, long B,
+                     int* const* slot, int* const* cid, int* const* ids, float* const* g, int* const* count, hipStream_t st);
+void fm_sdp_apply_segments(int n, int segs, int own_seg, float* const* W, const int* D, const int* const* seg_ids,
+                           const float* const* seg_g, const int* const* seg_count, int* const* slot, int* const* own_count,
+                           const int* nmax, const float* lr, hipStream_t st);
 void fm_dot_interaction_fwd(const void* const* z, int F, long ldz, void* out, long ldo, long B, int D, int W, int self,
                             hipStream_t s);
 void fm_dot_interaction_bwd(const void* const* z, int F, long ldz, const void* dout, long ldo, void* const* dz, long lddz,
@@ -334,6 +340,73 @@ void embedding_bwd_multi(std::vector<torch::Tensor> W, std::vector<torch::Tensor
                          a.rows.data(), a.D.data(), a.bag.data(), a.scale.data(), is_bf16(dy[0]),
                          lr.has_value() && lr->defined() ? lr->data_ptr<float>() : nullptr, a.B,
                          any ? own.data() : nullptr, any ? dup.data() : nullptr, any ? nd.data() : nullptr, cur());
+}
+
+// sparse data parallelism for replicated tables (embedding.hip): coalesce this rank's lookups
+// into (count, unique local rows, summed gradients) payload views of the all-gather send buffer
+void sdp_coalesce(std::vector<torch::Tensor> W, std::vector<torch::Tensor> idx, std::vector<torch::Tensor> dy,
+                  std::vector<int64_t> ldg, std::vector<double> scale, std::vector<int64_t> row_lo,
+                  std::vector<torch::Tensor> slot, std::vector<torch::Tensor> cid, std::vector<torch::Tensor> ids,
+                  std::vector<torch::Tensor> g, std::vector<torch::Tensor> count) {
+  if (W.empty()) return;
+  TabArgs a = tab_args(W, idx, dy, ldg, scale);
+  std::vector<long> lo = row_offsets(row_lo, W.size());
+  const size_t n = W.size();
+  TORCH_CHECK(slot.size() == n && cid.size() == n && ids.size() == n && g.size() == n && count.size() == n,
+              "sdp_coalesce: one buffer of each kind per table");
+  std::vector<int*> ps, pc, pi, pn;
+  std::vector<float*> pg;
+  for (size_t k = 0; k < n; ++k) {
+    TORCH_CHECK(slot[k].scalar_type() == torch::kInt32 && slot[k].numel() >= W[k].size(0), "sdp slot: int32 [rows]");
+    TORCH_CHECK(cid[k].scalar_type() == torch::kInt32 && cid[k].numel() >= idx[k].numel(), "sdp cid: int32 [B*bag]");
+    TORCH_CHECK(ids[k].scalar_type() == torch::kInt32 && ids[k].numel() >= idx[k].numel(), "sdp ids: int32 [B*bag]");
+    TORCH_CHECK(g[k].scalar_type() == torch::kFloat32 && g[k].numel() >= idx[k].numel() * W[k].size(1),
+                "sdp g: fp32 [B*bag, D]");
+    TORCH_CHECK(count[k].scalar_type() == torch::kInt32 && count[k].numel() >= 1, "sdp count: int32 [1]");
+    ps.push_back(slot[k].data_ptr<int>());
+    pc.push_back(cid[k].data_ptr<int>());
+    pi.push_back(ids[k].data_ptr<int>());
+    pg.push_back(g[k].data_ptr<float>());
+    pn.push_back(count[k].data_ptr<int>());
+  }
+  fm_sdp_coalesce((int)n, a.idx.data(), a.idx64.data(), a.cact.data(), a.ld.data(), lo.data(), a.rows.data(), a.D.data(),
+                  a.bag.data(), a.scale.data(), is_bf16(dy[0]), a.B, ps.data(), pc.data(), pi.data(), pg.data(), pn.data(),
+                  cur());
+}
+
+// apply the gathered segments (segs x n payloads, segment-major) in order; own_seg frees the slots
+void sdp_apply(std::vector<torch::Tensor> W, std::vector<torch::Tensor> seg_ids, std::vector<torch::Tensor> seg_g,
+               std::vector<torch::Tensor> seg_count, std::vector<torch::Tensor> slot, std::vector<torch::Tensor> own_count,
+               int64_t segs, int64_t own_seg, torch::Tensor lr) {
+  const size_t n = W.size();
+  if (n == 0) return;
+  TORCH_CHECK(seg_ids.size() == n * segs && seg_g.size() == n * segs && seg_count.size() == n * segs,
+              "sdp_apply: segs x tables payload views");
+  TORCH_CHECK(slot.size() == n && own_count.size() == n, "sdp_apply: slot / own_count per table");
+  check_cuda(lr, "lr");
+  std::vector<float*> pw;
+  std::vector<int> D, nmax;
+  std::vector<const int*> pi, pn;
+  std::vector<const float*> pg;
+  std::vector<int*> ps, po;
+  for (size_t k = 0; k < n; ++k) {
+    check_cuda(W[k], "W");
+    TORCH_CHECK(W[k].scalar_type() == torch::kFloat32 && W[k].is_contiguous() && W[k].dim() == 2, "tables fp32 [rows, D]");
+    pw.push_back(W[k].data_ptr<float>());
+    D.push_back((int)W[k].size(1));
+    nmax.push_back((int)seg_ids[k].numel());
+    ps.push_back(slot[k].data_ptr<int>());
+    po.push_back(own_count[k].data_ptr<int>());
+  }
+  for (size_t j = 0; j < n * segs; ++j) {
+    const size_t k = j % n;
+    TORCH_CHECK(seg_ids[j].numel() == nmax[k] && seg_g[j].numel() >= (int64_t)nmax[k] * D[k], "sdp_apply: payload sizes");
+    pi.push_back(seg_ids[j].data_ptr<int>());
+    pg.push_back(seg_g[j].data_ptr<float>());
+    pn.push_back(seg_count[j].data_ptr<int>());
+  }
+  fm_sdp_apply_segments((int)n, (int)segs, (int)own_seg, pw.data(), D.data(), pi.data(), pg.data(), pn.data(), ps.data(),
+                        po.data(), nmax.data(), lr.data_ptr<float>(), cur());
 }
 
 void dot_fwd(std::vector<torch::Tensor> zs, int64_t ldz, torch::Tensor out, int64_t ldo, int64_t D, int64_t W, bool self) {
@@ -741,6 +814,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("scale"), py::arg("row_lo") = std::vector<int64_t>{});
   m.def("embedding_bwd_multi", &embedding_bwd_multi, py::arg("W"), py::arg("idx"), py::arg("dy"), py::arg("ldg"),
         py::arg("scale"), py::arg("lr"), py::arg("claim"), py::arg("row_lo") = std::vector<int64_t>{});
+  m.def("sdp_coalesce", &sdp_coalesce);
+  m.def("sdp_apply", &sdp_apply);
   m.def("dot_fwd", &dot_fwd);
   m.def("dot_bwd", &dot_bwd);
   m.def("sgd", &sgd);

@@ -412,6 +412,124 @@ void launch_bwd(const TabSet& s, int m, bool tiny, bool dy_bf16, const float* lr
   }
 }
 
+// ---- sparse data parallelism for replicated tables ---------------------------------------------
+// A table replicated over R ranks (DP on its sample dim) is trained WITHOUT a dense gradient: each
+// replica coalesces its own lookups into (unique local row, summed gradient) pairs, the replica set
+// all-gathers those payloads, and every replica applies the R segments in rank order -- the same
+// fp32 operations in the same order everywhere, so the replicas stay bit-identical.  Within one
+// segment the rows are unique: the apply is a plain read-modify-write, no atomics.
+//   claim  : every in-shard lookup e CASes its row's slot (-1 -> e)
+//   assign : the winner takes a compact id u (one atomic per unique row), writes cid[e] = u,
+//            ids[u] = row and g[u] = scale * dy[b] with plain stores
+//   dups   : every other lookup of the row atomically adds its gradient into g[cid[slot[row]]]
+//   apply  : per segment r: W[ids[u]] -= lr * g[u] for u < count; the own segment also frees the
+//            slots (slot = -1) and zeroes its count for the next step
+struct SdpDesc {
+  const void* idx;    // [B, bag] int32/int64 (global rows)
+  const void* dy;     // [B, *] bf16/fp32, row stride ld
+  long ld;
+  long lo;            // first global row of this shard
+  int rows, D, bag;
+  float scale;
+  int* slot;          // [rows] int32, -1 = free
+  int* cid;           // [B*bag] compact id of an owner entry (scratch)
+  int* ids;           // [nmax] unique local rows      (payload)
+  float* g;           // [nmax][D] summed gradients   (payload)
+  int* count;         // [1] unique rows              (payload)
+};
+struct SdpSet {
+  SdpDesc t[MAXT];
+  int n;
+};
+
+template <bool I64>
+__global__ void __launch_bounds__(256) fm_sdp_claim(SdpSet s, long B) {
+  const SdpDesc& d = s.t[blockIdx.y];
+  const long n = B * d.bag;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    bool ok;
+    const long r = local_row(ldi<I64>(d.idx, e), d.lo, d.rows, ok);
+    if (ok) atomicCAS(d.slot + r, -1, (int)e);
+  }
+}
+
+// one wave per lookup entry (lane = column): the row's owner entry takes the compact id
+template <typename GT, bool I64>
+__global__ void __launch_bounds__(256) fm_sdp_assign(SdpSet s, long B) {
+  const SdpDesc& d = s.t[blockIdx.y];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long n = B * d.bag;
+  const GT* dy = reinterpret_cast<const GT*>(d.dy);
+  for (long e = blockIdx.x * 4L + wave; e < n; e += (long)gridDim.x * 4) {
+    bool ok;
+    const long r = local_row(ldi<I64>(d.idx, e), d.lo, d.rows, ok);
+    if (!ok || d.slot[r] != (int)e) continue;       // wave-uniform
+    int u = 0;
+    if (lane == 0) u = atomicAdd(d.count, 1);
+    u = __shfl(u, 0, 64);
+    const long b = e / d.bag;
+    float* gu = d.g + (long)u * d.D;
+    for (int c = lane; c < d.D; c += 64) gu[c] = ld<GT>(dy + b * d.ld + c) * d.scale;
+    if (lane == 0) {
+      d.ids[u] = (int)r;
+      d.cid[e] = u;
+    }
+  }
+}
+
+template <typename GT, bool I64>
+__global__ void __launch_bounds__(256) fm_sdp_dups(SdpSet s, long B) {
+  const SdpDesc& d = s.t[blockIdx.y];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long n = B * d.bag;
+  const GT* dy = reinterpret_cast<const GT*>(d.dy);
+  for (long e = blockIdx.x * 4L + wave; e < n; e += (long)gridDim.x * 4) {
+    bool ok;
+    const long r = local_row(ldi<I64>(d.idx, e), d.lo, d.rows, ok);
+    if (!ok) continue;
+    const int own = d.slot[r];
+    if (own == (int)e) continue;                     // the owner entry wrote g[u] itself
+    const long b = e / d.bag;
+    float* gu = d.g + (long)d.cid[own] * d.D;
+    for (int c = lane; c < d.D; c += 64) atomicAdd(gu + c, ld<GT>(dy + b * d.ld + c) * d.scale);
+  }
+}
+
+// one segment of the gathered payloads: W[ids[u]] -= lr * g[u] (rows unique within a segment)
+struct SdpApply {
+  float* W;
+  const int* ids;
+  const float* g;
+  const int* count;
+  int D;
+  int* slot;          // own segment: free the claimed slots; else nullptr
+  int* own_count;     // own segment: this rank's count, zeroed after use; else nullptr
+};
+struct SdpApplySet {
+  SdpApply t[MAXT];
+  int n;
+};
+
+__global__ void __launch_bounds__(256) fm_sdp_apply(SdpApplySet s, const float* __restrict__ lr, int nmax) {
+  const SdpApply& d = s.t[blockIdx.y];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int cnt = min(*d.count, nmax);
+  const float mlr = -lr[0];
+  for (long u = blockIdx.x * 4L + wave; u < cnt; u += (long)gridDim.x * 4) {
+    const long r = d.ids[u];
+    float* w = d.W + r * d.D;
+    const float* gu = d.g + u * d.D;
+    for (int c = lane; c < d.D; c += 64) w[c] += mlr * gu[c];
+    if (d.slot && lane == 0) d.slot[r] = -1;
+  }
+}
+
+// zero the own counts once every segment has been applied (a separate tiny launch: the own
+// segment's count may be read by later segments' launches only through the gathered copy)
+__global__ void fm_sdp_reset_counts(SdpApplySet s) {
+  if (threadIdx.x < s.n && s.t[threadIdx.x].own_count) *s.t[threadIdx.x].own_count = 0;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
@@ -523,4 +641,80 @@ extern "C" void fm_embedding_bwd(const void* idx, int idx64, const void* dy, int
                                  long B, int bag, int rows, int D, long ldg, float scale, hipStream_t s) {
   fm_embedding_bwd_multi(1, &W, &idx, &idx64, &dy, &ldg, nullptr, &rows, &D, &bag, &scale, dy_bf16, lr, B, nullptr,
                          nullptr, nullptr, s);
+}
+
+// ---- sparse DP launchers -------------------------------------------------------------------
+// coalesce: this rank's lookups of n replicated tables -> (count, ids, g) payloads
+extern "C" void fm_sdp_coalesce(int n, const void* const* idx, const int* idx64, const void* const* dy, const long* ldg,
+                                const long* lo, const int* rows, const int* D, const int* bag, const float* scale,
+                                int dy_bf16, long B, int* const* slot, int* const* cid, int* const* ids, float* const* g,
+                                int* const* count, hipStream_t st) {
+  if (B <= 0 || n <= 0) return;
+  for (int wide = 0; wide < 2; ++wide) {
+    std::vector<int> sel;
+    for (int k = 0; k < n; ++k)
+      if ((idx64[k] != 0) == (wide != 0)) sel.push_back(k);
+    for (size_t base = 0; base < sel.size(); base += MAXT) {
+      SdpSet s;
+      const int m = (int)std::min<size_t>(MAXT, sel.size() - base);
+      int maxbag = 1;
+      for (int i = 0; i < m; ++i) {
+        const int k = sel[base + i];
+        s.t[i] = SdpDesc{idx[k], dy[k], ldg[k], lo ? lo[k] : 0, rows[k], D[k], bag[k], scale[k], slot[k], cid[k], ids[k],
+                         g[k], count[k]};
+        maxbag = std::max(maxbag, bag[k]);
+      }
+      s.n = m;
+      const long ne = B * maxbag;
+      dim3 gc((unsigned)std::max<long>(1, std::min<long>((ne + 255) / 256, 1024)), m);
+      dim3 gw((unsigned)std::max<long>(1, std::min<long>((ne + 3) / 4, 2048)), m);
+      if (wide) {
+        hipLaunchKernelGGL((fm_sdp_claim<true>), gc, dim3(256), 0, st, s, B);
+        if (dy_bf16) {
+          hipLaunchKernelGGL((fm_sdp_assign<unsigned short, true>), gw, dim3(256), 0, st, s, B);
+          hipLaunchKernelGGL((fm_sdp_dups<unsigned short, true>), gw, dim3(256), 0, st, s, B);
+        } else {
+          hipLaunchKernelGGL((fm_sdp_assign<float, true>), gw, dim3(256), 0, st, s, B);
+          hipLaunchKernelGGL((fm_sdp_dups<float, true>), gw, dim3(256), 0, st, s, B);
+        }
+      } else {
+        hipLaunchKernelGGL((fm_sdp_claim<false>), gc, dim3(256), 0, st, s, B);
+        if (dy_bf16) {
+          hipLaunchKernelGGL((fm_sdp_assign<unsigned short, false>), gw, dim3(256), 0, st, s, B);
+          hipLaunchKernelGGL((fm_sdp_dups<unsigned short, false>), gw, dim3(256), 0, st, s, B);
+        } else {
+          hipLaunchKernelGGL((fm_sdp_assign<float, false>), gw, dim3(256), 0, st, s, B);
+          hipLaunchKernelGGL((fm_sdp_dups<float, false>), gw, dim3(256), 0, st, s, B);
+        }
+      }
+    }
+  }
+}
+
+// apply the gathered segments in order: segs x n tables; seg_ids/seg_g/seg_count[s*n + k]; the
+// own segment (own_seg) frees slot[k] and zeroes own_count[k] afterwards
+extern "C" void fm_sdp_apply_segments(int n, int segs, int own_seg, float* const* W, const int* D, const int* const* seg_ids,
+                                      const float* const* seg_g, const int* const* seg_count, int* const* slot,
+                                      int* const* own_count, const int* nmax, const float* lr, hipStream_t st) {
+  if (n <= 0) return;
+  for (size_t base = 0; base < (size_t)n; base += MAXT) {
+    const int m = (int)std::min<size_t>(MAXT, n - base);
+    int nm = 1;
+    for (int i = 0; i < m; ++i) nm = std::max(nm, nmax[base + i]);
+    dim3 grid((unsigned)std::max(1, std::min((nm + 3) / 4, 2048)), m);
+    SdpApplySet last;
+    for (int sg = 0; sg < segs; ++sg) {
+      SdpApplySet s;
+      for (int i = 0; i < m; ++i) {
+        const int k = (int)base + i;
+        const bool own = sg == own_seg;
+        s.t[i] = SdpApply{W[k], seg_ids[sg * n + k], seg_g[sg * n + k], seg_count[sg * n + k], D[k], own ? slot[k] : nullptr,
+                          own ? own_count[k] : nullptr};
+      }
+      s.n = m;
+      hipLaunchKernelGGL(fm_sdp_apply, grid, dim3(256), 0, st, s, lr, nm);
+      if (sg == own_seg) last = s;
+    }
+    if (own_seg >= 0 && own_seg < segs) hipLaunchKernelGGL(fm_sdp_reset_counts, dim3(1), dim3(64), 0, st, last);
+  }
 }

@@ -49,6 +49,55 @@ def _cpu_ext():
         _CPU_MOD.append(m)
     return _CPU_MOD[0]
 
+class SparseDPState:
+    """Payload buffers of one replicated embedding group (see :meth:`Embedding.sdp_pack`).
+
+    One int32 send buffer per rank: [count per table (padded to 64)] [ids per table: B*bag]
+    [gradients per table: B*bag*D fp32 bits]; the all-gather fills ``recv`` = R segments of that
+    layout in replica-rank order (the order of the sorted replica set = the group's rank order)."""
+
+    def __init__(self, ops, ctxs, holders, rank):
+        self.holders = tuple(sorted(holders))
+        self.R = len(self.holders)
+        self.seg = self.holders.index(rank)
+        dev = ctxs[0].weights[0].device
+        n = len(ctxs)
+        nmax = [c.inputs[0].numel() for c in ctxs]
+        D = [c.weights[0].shape[1] for c in ctxs]
+        hdr = (n + 63) // 64 * 64
+        offs_i, offs_g, o = [], [], hdr
+        for k in range(n):
+            offs_i.append(o)
+            o += (nmax[k] + 63) // 64 * 64
+        for k in range(n):
+            offs_g.append(o)
+            o += (nmax[k] * D[k] + 63) // 64 * 64
+        self.P = o
+        self.send = torch.zeros(self.P, dtype=torch.int32, device=dev)
+        self.recv = torch.zeros(self.R * self.P, dtype=torch.int32, device=dev)
+
+        def views(buf):
+            cnt = [buf[k:k + 1] for k in range(n)]
+            ids = [buf[offs_i[k]:offs_i[k] + nmax[k]] for k in range(n)]
+            g = [buf[offs_g[k]:offs_g[k] + nmax[k] * D[k]].view(torch.float32) for k in range(n)]
+            return cnt, ids, g
+        # own payload lives in the send buffer; every segment (own included) is read from recv
+        self.count, self.ids, self.g = {}, {}, {}
+        self.count[self.seg], self.ids[self.seg], self.g[self.seg] = views(self.send)
+        self.rcount, self.rids, self.rg = [], [], []
+        for s in range(self.R):
+            c, i, g = views(self.recv[s * self.P:(s + 1) * self.P])
+            self.rcount.append(c)
+            self.rids.append(i)
+            self.rg.append(g)
+        hip = ctxs[0].hip
+        self.slot = [torch.full((c.weights[0].shape[0],), -1, dtype=torch.int32, device=dev) for c in ctxs] if hip else []
+        self.cid = [torch.empty(nmax[k], dtype=torch.int32, device=dev) for k in range(n)] if hip else []
+
+    def exchange(self, comm):
+        comm.all_gather(self.recv, self.send, self.holders)
+
+
 class Embedding(Op):
     op_type = OperatorType.OP_EMBEDDING
     name_prefix = "Embed"
@@ -66,8 +115,10 @@ class Embedding(Op):
             kernel_initializer = UniformInitializer(model._next_seed() if model else 0, -r, r)
         self._add_weight((self.num_entries, self.out_dim), kernel_initializer, "weight")
         self._finish([(input.dims[0], self.out_dim)])
-        # set by the executor when a fused sparse optimizer applies to this table
+        # set by the executor when a fused sparse optimizer applies to this table; sparse_dp =
+        # the replica set of a replicated table trained by touched-row exchange
         self.sparse_sgd = False
+        self.sparse_dp = None
 
     def splittable_dims(self):
         return {0, 1}
@@ -201,6 +252,7 @@ class Embedding(Op):
     def can_group(a, b, ca, cb):
         """Executor fusion: independent embeddings with the same placement run as ONE launch."""
         return (ca.outputs[0].dtype == cb.outputs[0].dtype and a.sparse_sgd == b.sparse_sgd
+                and getattr(a, "sparse_dp", None) == getattr(b, "sparse_dp", None)
                 and ca.inputs[0].shape[0] == cb.inputs[0].shape[0])
 
     @staticmethod
@@ -239,6 +291,67 @@ class Embedding(Op):
                                   [c.out_grads[0].stride(0) for c in ctxs], scales, lr, claim,
                                   [Embedding._row_lo(c) for c in ctxs])
 
+    # ---------------------------------------------------------- sparse data parallelism
+    # A table REPLICATED over a set of ranks (sample-split lookups, e.g. pure DP) is trained with
+    # touched-row exchange instead of the reference's dense per-replica gradient + replica sum
+    # (src/ops/embedding.cu:108-135 partitions, src/runtime/model.cc:697-724 grad replicas,
+    # src/runtime/optimizer_kernel.cu:96-101 replica reduction -- a table-sized gradient, 96 GB
+    # at MLPerf scale).  Per step: (1) pack -- each replica coalesces its lookups into (unique
+    # local rows, summed gradients) payloads; (2) one all-gather of the payloads over the replica
+    # set; (3) apply -- every replica applies the R segments in rank order (plain row updates,
+    # rows unique per segment), so all replicas perform the same fp32 operations and stay
+    # bit-identical.  Nothing table-sized is allocated besides the table itself and an int32
+    # claim slot per row (GPU).
+    @staticmethod
+    def sdp_state(ops, ctxs, holders, rank):
+        c0 = ctxs[0]
+        st = c0.saved.get("sdp")
+        if st is None:
+            st = SparseDPState(ops, ctxs, holders, rank)
+            c0.saved["sdp"] = st
+        return st
+
+    @staticmethod
+    def sdp_pack(ops, ctxs):
+        st = ctxs[0].saved["sdp"]
+        scales = [1.0 / c.inputs[0].shape[1] if op.aggr == AggrMode.AGGR_MODE_AVG else 1.0 for op, c in zip(ops, ctxs)]
+        if ctxs[0].hip:
+            K.C().sdp_coalesce([c.weights[0] for c in ctxs], [c.inputs[0] for c in ctxs], [c.out_grads[0] for c in ctxs],
+                               [c.out_grads[0].stride(0) for c in ctxs], scales, [Embedding._row_lo(c) for c in ctxs],
+                               st.slot, st.cid, st.ids[st.seg], st.g[st.seg], st.count[st.seg])
+            return
+        for k, (op, c) in enumerate(zip(ops, ctxs)):
+            idx, w = c.inputs[0], c.weights[0]
+            bag = idx.shape[1]
+            li, ok = Embedding._local_rows(idx, Embedding._row_lo(c), w.shape[0])
+            sel = ok.reshape(-1)
+            rows = li.reshape(-1)[sel]
+            g = (c.out_grads[0].float() * scales[k]).repeat_interleave(bag, dim=0)[sel]
+            uniq, inv = torch.unique(rows, return_inverse=True)
+            summed = torch.zeros((uniq.numel(), w.shape[1]), dtype=torch.float32).index_add_(0, inv, g)
+            n = uniq.numel()
+            st.count[st.seg][k].fill_(n)
+            st.ids[st.seg][k][:n].copy_(uniq.to(torch.int32))
+            st.g[st.seg][k][:n * w.shape[1]].copy_(summed.reshape(-1))
+
+    @staticmethod
+    def sdp_apply(ops, ctxs):
+        st = ctxs[0].saved["sdp"]
+        lr = ctxs[0].lr
+        if ctxs[0].hip:
+            K.C().sdp_apply([c.weights[0] for c in ctxs], [t for s in range(st.R) for t in st.rids[s]],
+                            [t for s in range(st.R) for t in st.rg[s]], [t for s in range(st.R) for t in st.rcount[s]],
+                            st.slot, st.count[st.seg], st.R, st.seg, lr)
+            return
+        mlr = -lr.to(torch.float32)
+        for s in range(st.R):
+            for k, c in enumerate(ctxs):
+                w = c.weights[0]
+                n = int(st.rcount[s][k].item())
+                if n:
+                    D = w.shape[1]
+                    w.index_add_(0, st.rids[s][k][:n].long(), mlr * st.rg[s][k][:n * D].view(n, D))
+
     CLAIM = os.environ.get("FM_EMB_CLAIM", "1") != "0"
     # owner-computes only when rows exceed CLAIM_RATIO x lookups per step (fewer duplicates)
     CLAIM_RATIO = float(os.environ.get("FM_EMB_CLAIM_RATIO", "1"))
@@ -263,6 +376,12 @@ class Embedding(Op):
 
     def flops(self, in_shapes, out_shapes):
         return float(in_shapes[0][0] * in_shapes[0][1] * out_shapes[0][1])
+
+    @staticmethod
+    def sdp_payload_words(lookups, D):
+        """int32 words one replica contributes per table to the sparse-DP all-gather (the worst
+        case: every lookup a distinct row) -- used by the cost model (flexmi/parallel/search.py)."""
+        return 1 + lookups * (1 + D)
 
     def bytes_moved(self, in_shapes, out_shapes, elem=2):
         b, bag = in_shapes[0]

@@ -247,6 +247,9 @@ def _rt_module():
 
 
 _LIVE_RUNNERS = None
+# replicated embedding tables (DP) trained by touched-row exchange instead of a dense gradient
+# all-reduce (FLEXMI_SPARSE_DP=0: the reference's dense replica gradients, for A/B)
+SPARSE_DP = os.environ.get("FLEXMI_SPARSE_DP", "1") != "0"
 
 
 def release_native_runners():
@@ -359,6 +362,9 @@ class NativeRunner:
                         continue
                     rt.add_all_reduce(pid, self.slot(("ar", id(g), bi)), self._pg(g.holders), g.gradbuf[b[0]:b[1]],
                                       True, f"{it.name}.bucket{bi}")
+        elif kind == "ag_buf":      # all-gather of explicit buffers over a replica set (sparse DP)
+            out, inp, ranks = nat[1], nat[2], nat[3]
+            rt.add_all_gather(pid, self.slot(("agb", id(out))), self._pg(ranks), out, inp, it.name)
         elif kind == "ag_sync":
             for g in ex.groups:
                 if not g.zero:
@@ -1008,9 +1014,16 @@ class Executor:
                     e.master = torch.empty(e.shape, dtype=torch.float32, pin_memory=self.backend == "hip")
                     e.compute = e.master
                     continue
-                if (op.op_type == OperatorType.OP_EMBEDDING and sparse_ok and lays[wi].replication() == 1):
+                if op.op_type == OperatorType.OP_EMBEDDING:
+                    op.sparse_dp = None
+                if (op.op_type == OperatorType.OP_EMBEDDING and sparse_ok
+                        and (lays[wi].replication() == 1 or SPARSE_DP)):
+                    # non-replicated: fused sparse SGD; replicated: sparse data parallelism
+                    # (touched-row all-gather over the replica set, Embedding.sdp_*)
                     e.sparse = True
                     op.sparse_sgd = True
+                    if lays[wi].replication() > 1:
+                        op.sparse_dp = tuple(sorted(e.holders))
                     e.master = self._alloc(e.shape, torch.float32)
                     e.compute = e.master
                     continue
@@ -1411,7 +1424,9 @@ class Executor:
                             C(bwd, o.name + ".zero_unused_grad", (lambda t=self.grad[o.guid]: t.zero_()))
                             written.add(self.gkey(o.guid))
                     grp = self.group_of.get(op.guid)
-                    if grp is not None:
+                    if getattr(op, "sparse_dp", None) and (grp is None or grp[0] is op):
+                        self._emit_sparse_dp(bwd, grp or [op])
+                    elif grp is not None:
                         if grp[0] is op:
                             C(bwd, op.name + ".group_bwd",
                               (lambda grp=grp: type(grp[0]).backward_group(grp, [self.ctx[o.guid] for o in grp])))
@@ -1457,6 +1472,19 @@ class Executor:
         for ex in finish_before.pop(len(steps), []):
             self._emit_exchange_finish(bwd, ex, "reshard.bwd")
         assert not finish_before
+
+    def _emit_sparse_dp(self, bwd, grp):
+        """Replicated embedding tables: pack (coalesce this rank's lookups) -> all-gather of the
+        payloads over the replica set (RCCL) -> apply every replica's segment in rank order."""
+        ctxs = [self.ctx[o.guid] for o in grp]
+        op = grp[0]
+        cls = type(op)
+        st = cls.sdp_state(grp, ctxs, op.sparse_dp, self.rank)
+        name = op.name + (".group" if len(grp) > 1 else "")
+        bwd.append(Item("compute", (lambda grp=grp, ctxs=ctxs: cls.sdp_pack(grp, ctxs)), name + ".sdp_pack"))
+        bwd.append(Item("comm", (lambda st=st: st.exchange(self.comm)), name + ".sdp_allgather",
+                        native=("ag_buf", st.recv, st.send, st.holders)))
+        bwd.append(Item("compute", (lambda grp=grp, ctxs=ctxs: cls.sdp_apply(grp, ctxs)), name + ".sdp_apply"))
 
     def _fwd_op(self, op, c):
         c.training = self.training
@@ -1965,4 +1993,11 @@ class Executor:
                 n += v.numel() * v.element_size()
         w = sum(g.numel * 4 * 2 + sum(t.numel() for t in g.state.values()) * 4 for g in self.groups)
         sp = sum(e.numel * 4 for e in self.wentries.values() if e.sparse)
-        return {"activations": n, "dense_params": w, "sparse_tables": sp}
+        # sparse data parallelism: the all-gather payload buffers (send + R segments) and the
+        # claim slots -- per-step lookups, not table-sized gradients
+        sdp = 0
+        for c in self.ctx.values():
+            st = c.saved.get("sdp")
+            if st is not None:
+                sdp += (st.send.numel() + st.recv.numel()) * 4 + sum(t.numel() * 4 for t in st.slot + st.cid)
+        return {"activations": n, "dense_params": w, "sparse_tables": sp, "sparse_dp_payload": sdp}

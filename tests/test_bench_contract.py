@@ -49,6 +49,10 @@ def test_bench_two_ranks():
               "--steps", "2", "--warmup", "1", "--config", "tiny", "--batch-per-gpu", "64"])
     _check(r, 2)
     assert "emb2" in r["config"]["parallelism"]
+    # the second half of the metric: the same step under pure DP, and the SOAP speedup over it
+    dp = r["config"]["dp"]
+    assert dp["parallelism"] == "dp2" and dp["value"] > 0 and dp["ms_per_step"] > 0
+    assert r["config"]["soap_speedup_vs_dp"] == round(r["value"] / dp["value"], 3)
 
 
 @pytest.mark.multiproc
@@ -87,3 +91,7 @@ def test_bench_eight_ranks_mlperf_plan(strategy):
               "--batch-per-gpu", "64", "--strategy", strategy] + extra)
     _check(r, 8)
     assert r["config"]["embedding_dim"] == 128 and r["config"]["mlp_top"] == [479, 1024, 1024, 512, 256, 1]
+    if strategy == "dp":
+        assert r["config"]["parallelism"] == "dp8" and "soap_speedup_vs_dp" not in r["config"]
+    else:
+        assert r["config"]["dp"]["parallelism"] == "dp8" and r["config"]["soap_speedup_vs_dp"] > 0

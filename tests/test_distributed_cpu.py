@@ -124,13 +124,13 @@ def _build(case, world):
                 strat = load_strategies_from_file(ref)
     elif case.startswith("dlrm"):
         dcfg = DLRMConfig.preset("tiny")
-        dcfg.arch_interaction_op = "dot" if case == "dlrm_dot" else "cat"
+        dcfg.arch_interaction_op = "dot" if case in ("dlrm_dot", "dlrm_dp") else "cat"
         d, s, p = build_dlrm(m, dcfg)
         loss = LossType.LOSS_BINARY_CROSSENTROPY
         inputs["dense"] = (d, (B, 13), "f")
         for i, (t, r) in enumerate(zip(s, dcfg.embedding_size)):
             inputs[f"sparse{i}"] = (t, (B, 1), ("i", r))
-        if world > 1 and not dp_small:
+        if world > 1 and not dp_small and case != "dlrm_dp":   # dlrm_dp: pure data parallelism
             strat = dlrm_strategy(m, world)
             if case == "dlrm_search":
                 # strategy chosen by the MCMC search over the MI355X simulator (same seed on
@@ -212,6 +212,16 @@ def _run(case, world, rank, steps, out_path):
         assert zg and all(len(g.buckets) > 1 for g in zg), "ZeRO groups / buckets missing"
         for g in zg:   # optimizer state really is sharded
             assert all(t.numel() * len(g.holders) == g.numel for t in g.state.values())
+    if case in ("dlrm_dp", "dlrm_cat_dpsmall") and world > 1:
+        # sparse data parallelism: replicated tables train by touched-row all-gather, no
+        # table-sized gradient buffer and no table in a dense all-reduce group
+        from flexmi.core.types import OperatorType
+        embs = [e for e in ex.wentries.values() if e.op.op_type == OperatorType.OP_EMBEDDING]
+        assert embs and all(e.sparse and e.group is None and e.grad is None for e in embs)
+        assert all(e.op.sparse_dp == tuple(range(world)) for e in embs)
+        assert not [e for g in ex.groups for e in g.entries if e.op.op_type == OperatorType.OP_EMBEDDING]
+        rep = ex.memory_report()
+        assert rep["sparse_tables"] == sum(e.numel * 4 for e in embs) and rep["sparse_dp_payload"] > 0, rep
     params = [p.get_weights(m) for p in m.parameters]
     loss = m.get_perf_metrics().get_loss()
     nr = ex.native_runner()
@@ -262,7 +272,7 @@ def _launch(case, world, steps=3):
                                         ("mlp_dp_zero", 4), ("dlrm_cat_dpsmall", 2), ("dlrm_mlperf8", 8), ("mlp_subset", 4), ("nmt_reference", 2),
                                         ("nmt_pipeline", 2), ("nmt_pipeline", 4), ("cnn_spatial", 4),
                                         ("cnn_spatial+p2p", 2), ("dlrm_dot+p2p", 2),
-                                        ("dlrm_shipped8", 8)])
+                                        ("dlrm_shipped8", 8), ("dlrm_dp", 2), ("dlrm_dp", 4), ("dlrm_dp", 8)])
 def test_strategy_equivalence(case, world):
     ref = _launch(case.replace("+p2p", ""), 1)
     got = _launch(case, world)
