@@ -86,6 +86,7 @@ class StepRunner {
   int new_slot() {
     slots_.emplace_back();
     extra_.emplace_back();
+    drops_.emplace_back();
     pending_.push_back(false);
     return (int)slots_.size() - 1;
   }
@@ -228,6 +229,7 @@ class StepRunner {
   void reset_slots() {
     for (auto& w : slots_) w.reset();
     for (auto& v : extra_) v.clear();
+    for (auto& d : drops_) d = {};
     std::fill(pending_.begin(), pending_.end(), false);
   }
 
@@ -284,6 +286,9 @@ class StepRunner {
   };
   // next collective: apply its injected fault (if any); returns the tensor the collective should
   // write into (a scratch copy when the result is dropped)
+  // A dropped result: the collective writes into a scratch copy that stays alive (drops_) until
+  // the slot's works have finished; an out-of-place result buffer is then zeroed and an in-place
+  // one (all-reduce) keeps this rank's local values -- the outcomes of the Python FaultyComm.
   at::Tensor inject(at::Tensor payload, at::Tensor result) {
     auto it = faults_.find(fault_n_++);
     if (it == faults_.end()) return result;
@@ -291,7 +296,10 @@ class StepRunner {
     if (f.kind == 0) std::this_thread::sleep_for(std::chrono::duration<double>(f.arg));
     if (f.kind == 3) std::_Exit(3);
     if (f.kind == 2 && payload.numel() > 0) payload.reshape({-1}).narrow(0, 0, 1).fill_(NAN);
-    if (f.kind == 1) return result.clone();
+    if (f.kind == 1) {   // in-place collectives (all-reduce) keep this rank's local data instead
+      pending_drop_ = {result.clone(), payload.is_same(result) ? at::Tensor() : result};
+      return pending_drop_.first;
+    }
     return result;
   }
 
@@ -299,6 +307,8 @@ class StepRunner {
     if (pending_[slot]) finish(slot);
     slots_[slot] = std::move(w);
     extra_[slot] = std::move(more);
+    drops_[slot] = std::move(pending_drop_);
+    pending_drop_ = {};
     pending_[slot] = true;
     ++collectives_;
   }
@@ -307,6 +317,10 @@ class StepRunner {
     if (slots_[slot]) slots_[slot]->wait();
     for (auto& w : extra_[slot])
       if (w) w->wait();
+    if (drops_[slot].first.defined()) {
+      if (drops_[slot].second.defined()) drops_[slot].second.zero_();
+      drops_[slot] = {};
+    }
     pending_[slot] = false;
     ++waits_;
   }
@@ -401,6 +415,8 @@ class StepRunner {
   int64_t fault_n_ = 0;
   std::vector<WorkPtr> slots_;
   std::vector<std::vector<WorkPtr>> extra_;   // further works of a slot (uncoalesced p2p)
+  std::vector<std::pair<at::Tensor, at::Tensor>> drops_;   // (scratch, real result) of a dropped collective
+  std::pair<at::Tensor, at::Tensor> pending_drop_;
   std::vector<bool> pending_;
   int current_ = -1;
   bool released_ = false;

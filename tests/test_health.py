@@ -102,13 +102,19 @@ def _fault_worker(rank, world, port, fault, out_dir):
         if rank == 1:
             # the step's first collectives (gradient bucket and metric reductions; their issue
             # order may vary with timing) all get the fault, so the gradient exchange is hit
-            m.comm = FaultyComm(m.comm, {0: fault} if fault[0] == "kill" else {0: fault, 1: fault, 2: fault})
+            m.comm = FaultyComm(m.comm, {0: fault} if fault[0] == "kill" else {k: fault for k in range(6)})
         m.init_layers()
         nr = m._ex().native_runner()
         res["native"] = nr is not None
+        res["steps"] = []
         for it in range(2):
             _feed(m, x, it)
-            m._ex().train_step()
+            try:
+                m._ex().train_step()
+            finally:   # evidence for a failed expectation: collectives issued / faults consumed
+                res["steps"].append({"collectives": nr.rt.collectives if nr else None,
+                                     "fault_calls": nr.rt.fault_calls if nr else None,
+                                     "programs": [nr.rt.describe(p) for p in range(nr.rt.num_programs())] if nr else None})
     except BaseException as e:  # noqa: BLE001 -- report every failure kind to the parent
         res["error"] = type(e).__name__
         res["msg"] = str(e)[:300]
