@@ -178,15 +178,21 @@ class SimGraph:
                 h = lay.holders[p]
                 if len(h) > 1:
                     if sparse:
-                        # replicated table with the sparse optimizer: only the rows a step touches
-                        # are exchanged (an all-gather of the global batch's row gradients + ids,
-                        # costed as the all-reduce of half that volume), never the dense table
+                        # replicated table with the sparse optimizer = the executor's sparse data
+                        # parallelism (Embedding.sdp_*): every replica all-gathers a fixed payload of
+                        # its sample shard's lookups -- count + ids + fp32 row gradients, padded to
+                        # one slot per lookup -- and applies all R segments.  A ring all-gather of
+                        # R payloads moves what a ring all-reduce of R*payload/2 bytes moves.
+                        R = len(h)
                         B = op.inputs[0].dims[0]
                         bag = op.inputs[0].dims[1] if len(op.inputs[0].dims) > 1 else 1
                         box = lay.part_box(p)
                         cols = vol // max(1, box[0][1] - box[0][0])
-                        touched = min(vol, B * bag * cols)
-                        wsync.append((float(touched * 4 + B * bag * 8) / 2.0, list(h)))
+                        lookups = -(-B // R) * bag
+                        payload = 4.0 * op.sdp_payload_words(lookups, cols)
+                        wsync.append((R * payload / 2.0, list(h)))
+                        for d in h:   # the apply: R segments of row read-modify-writes
+                            upd_bytes[d] = upd_bytes.get(d, 0.0) + float(min(vol, B * bag * cols)) * 4.0
                     else:
                         wsync.append((float(vol * 4), list(h)))
                 for d in h:
