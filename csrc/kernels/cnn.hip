@@ -15,6 +15,8 @@
 // per-channel block partial sums + atomics into a [2C] fp32 buffer, then an elementwise pass.
 #include "common.h"
 
+#include <cstdlib>
+
 #include <algorithm>
 
 namespace {
@@ -204,6 +206,75 @@ __global__ void __launch_bounds__(256) fm_pool_bwd_kernel(const T* __restrict__ 
   dx[i] = fromf<T>(g);
 }
 
+// pooling backward, row segments: one thread = VW consecutive input columns of one (n, c, h) row.
+// The windows that route to the segment are the same rows p for all VW columns and a short run of
+// columns q, so each window's argmax code / output gradient is loaded ONCE per thread instead of
+// once per element (the per-element kernel above re-derived and re-loaded them for every input
+// element: 572 us/step of AlexNet b256 bf16, profiles/prof_r2_alexnet_b256_bf16_kernels.txt);
+// the VW results leave as one 16-B (bf16) / two 16-B (fp32) store when the row allows it.
+template <typename T, int VW>
+__global__ void __launch_bounds__(256) fm_pool_bwd_rows(const T* __restrict__ y, const T* __restrict__ dy,
+                                                        const unsigned char* __restrict__ code, T* __restrict__ dx,
+                                                        int total, FastDiv dWS, FastDiv dH, FastDiv dsh, FastDiv dsw,
+                                                        int WS, int H, int W, int P, int Q, int kh, int kw, int sh, int sw,
+                                                        int pt, int pl, int is_max, int act, int acc) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int t = fdiv(i, dWS), ws = i - t * WS;
+  const int nc = fdiv(t, dH), h = t - nc * H;
+  const int wb = ws * VW;
+  const int we = min(W, wb + VW) - 1;                  // last column of the segment
+  float g[VW];
+#pragma unroll
+  for (int e = 0; e < VW; ++e) g[e] = 0.f;
+  const int pmin = h + pt + 1 >= kh ? fdiv(h + pt - kh + sh, dsh) : 0;
+  const int pmax = h + pt >= 0 ? min(P - 1, fdiv(h + pt, dsh)) : -1;
+  const int qmin = wb + pl + 1 >= kw ? fdiv(wb + pl - kw + sw, dsw) : 0;
+  const int qmax = we + pl >= 0 ? min(Q - 1, fdiv(we + pl, dsw)) : -1;
+  for (int p = pmin; p <= pmax; ++p) {
+    const int h0 = p * sh - pt;
+    if (h < h0 || h >= h0 + kh) continue;
+    const int orow = (nc * P + p) * Q;
+    for (int q = qmin; q <= qmax; ++q) {
+      const int w0 = q * sw - pl;
+      const int o = orow + q;
+      const float gd = tof(dy[o]);
+      const float go = act == ACT_NONE ? gd : act_bwd(act, tof(y[o]), gd);
+      if (is_max) {
+        const int cd = code[o];
+        if (cd == 255) continue;
+        const int ch = cd / kw, cw = cd - ch * kw;
+        if (h0 + ch != h) continue;                    // the window's max is on another row
+        const int w = w0 + cw - wb;
+#pragma unroll
+        for (int e = 0; e < VW; ++e)
+          if (e == w) g[e] += go;
+      } else {
+        const int hs = max(h0, 0), hend = min(h0 + kh, H), wsx = max(w0, 0), wend = min(w0 + kw, W);
+        const float v = go / (float)((hend - hs) * (wend - wsx));
+#pragma unroll
+        for (int e = 0; e < VW; ++e) {
+          const int w = wb + e;
+          if (w >= w0 && w < w0 + kw) g[e] += v;
+        }
+      }
+    }
+  }
+  T* dp = dx + (long)t * W + wb;
+  const bool vec = (we - wb + 1 == VW) && ((((uintptr_t)dp) & 15) == 0);
+  if (vec) {
+    if (acc) {
+      float old[VW];
+      if constexpr (VW == 8) ld8<T>(dp, old);
+#pragma unroll
+      for (int e = 0; e < VW; ++e) g[e] += old[e];
+    }
+    if constexpr (VW == 8) st8<T>(dp, g);
+  } else {
+    for (int e = 0; e <= we - wb; ++e) dp[e] = fromf<T>(g[e] + (acc ? tof(dp[e]) : 0.f));
+  }
+}
+
 // ---- batch norm (training mode, per-channel statistics over N*H*W) -----------------------
 // stats[0:C] = sum, stats[C:2C] = sum of squares   (zeroed by the caller)
 template <typename T>
@@ -381,6 +452,16 @@ static void fm_pool_bwd_t(const void* x, const void* y, const void* dy, void* dx
   if (is_max && !code_ready)
     hipLaunchKernelGGL(fm_pool_argmax_kernel<T>, dim3((outs + 255) / 256), dim3(256), 0, st, (const T*)x, code, outs, H, W,
                        P, Q, kh, kw, sh, sw, pt, pl);
+  static const bool per_elem = getenv("FM_POOL_BWD_ELEM") != nullptr;   // A/B: the per-element kernel
+  if (!per_elem) {
+    constexpr int VW = 8;
+    const int WS = (W + VW - 1) / VW;
+    const int rows_total = N * C * H * WS;
+    hipLaunchKernelGGL((fm_pool_bwd_rows<T, VW>), dim3((rows_total + 255) / 256), dim3(256), 0, st, (const T*)y,
+                       (const T*)dy, (const unsigned char*)code, (T*)dx, rows_total, make_fastdiv(WS), make_fastdiv(H),
+                       make_fastdiv(sh), make_fastdiv(sw), WS, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, acc);
+    return;
+  }
   hipLaunchKernelGGL(fm_pool_bwd_kernel<T>, dim3((total + 255) / 256), dim3(256), 0, st, (const T*)y, (const T*)dy,
                      (const unsigned char*)code, (T*)dx, total, make_fastdiv(W), make_fastdiv(H), make_fastdiv(sh),
                      make_fastdiv(sw), H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, acc);

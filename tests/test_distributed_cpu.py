@@ -154,6 +154,36 @@ def _build(case, world):
             if case == "dlrm_colsplit":
                 # column (parameter-dim) split of one table across all ranks
                 strat["embedding1"] = ParallelConfig([world, 1], list(range(world)))
+    elif case == "inception8":
+        # BASELINE config 3 rehearsed on 8 gloo ranks: InceptionV3 (75x75 images, the smallest the
+        # stride-2 stages allow) under a strategy from the MCMC search over the MI355X simulator,
+        # seeded with attribute (spatial h) splits of the stem and operator placement of the
+        # first inception block's branches on device subsets (reference README.md:52-61,
+        # examples/cpp/InceptionV3/inception.cc:26-174)
+        from flexmi.models import cnn
+        cfg.batchSize = B = 8
+        x, o = cnn.inception_v3(m, image=75)
+        loss = LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY
+        inputs["img"] = (x, (B, 3, 75, 75), "f")
+        if world > 1:
+            from flexmi.core.types import OperatorType
+            convs = [op for op in m.layers if op.op_type == OperatorType.OP_CONV2D]
+            pools = [op for op in m.layers if op.op_type == OperatorType.OP_POOL2D]
+            hand = {}
+            for op in convs[:3] + pools[:1]:          # stem: h split 2 x sample split 4
+                hand[op.name] = ParallelConfig([1, 2, 1, world // 2], list(range(world)))
+            half = world // 2
+            blk = convs[5:12]                          # first inception_a block's branch convs
+            for i, op in enumerate(blk):
+                lo = 0 if i < 3 else half
+                hand[op.name] = ParallelConfig([1, 1, 1, half], list(range(lo, lo + half)))
+            from flexmi.parallel.search import optimize
+            m.optimizer = SGDOptimizer(m, 0.1)
+            r = optimize(m, 200, 1.0, num_devices=world, init=hand, seed=3, verbose=False)
+            strat = dict(r.best)
+            spatial = [k for k, pc in strat.items() if len(pc.dims) == 4 and (pc.dims[0] > 1 or pc.dims[1] > 1)]
+            subset = [k for k, pc in strat.items() if len(set(pc.device_ids)) < world]
+            assert spatial and subset, (spatial, subset)
     elif case == "cnn_spatial":
         x = m.create_tensor([4, 3, 12, 12], name="img")
         c = m.conv2d(x, 4, 3, 3, 1, 1, 1, 1, ActiMode.AC_MODE_RELU, name="conv1")
@@ -284,7 +314,8 @@ def _launch(case, world, steps=3):
                                         ("mlp_dp_zero", 4), ("dlrm_cat_dpsmall", 2), ("dlrm_mlperf8", 8), ("mlp_subset", 4), ("nmt_reference", 2),
                                         ("nmt_pipeline", 2), ("nmt_pipeline", 4), ("cnn_spatial", 4),
                                         ("cnn_spatial+p2p", 2), ("dlrm_dot+p2p", 2),
-                                        ("dlrm_shipped8", 8), ("dlrm_dp", 2), ("dlrm_dp", 4), ("dlrm_dp", 8)])
+                                        ("dlrm_shipped8", 8), ("dlrm_dp", 2), ("dlrm_dp", 4), ("dlrm_dp", 8),
+                                        ("inception8", 8)])
 def test_strategy_equivalence(case, world):
     ref = _launch(case.replace("+p2p", ""), 1)
     got = _launch(case, world)
