@@ -214,7 +214,7 @@ def _run_overlapped(items, s, side):
                 it.fn()
             bwd_pending = True
             continue
-        if bwd_pending and not (it.name.endswith(".bwd") or it.name.endswith(".bwd_dw")):
+        if bwd_pending and not it.name.endswith((".bwd", ".bwd_dw", ".bwd_dx")):
             s.wait_stream(side)
             bwd_pending = False
         it.fn()
