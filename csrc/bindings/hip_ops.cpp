@@ -47,6 +47,8 @@ void fm_sdp_coalesce(int n, const void* const* idx, const int* idx64, const void
 void fm_sdp_apply_segments(int n, int segs, int own_seg, float* const* W, const int* D, const int* const* seg_ids,
                            const float* const* seg_g, const int* const* seg_count, int* const* slot, int* const* own_count,
                            const int* nmax, const float* lr, hipStream_t st);
+void fm_strided_copy4_run(const void* src, void* dst, int bf16, const int* d, const long* ss, const long* ts, long so,
+                          long to, int acc, hipStream_t st);
 void fm_dot_interaction_fwd(const void* const* z, int F, long ldz, void* out, long ldo, long B, int D, int W, int self,
                             hipStream_t s);
 void fm_dot_interaction_bwd(const void* const* z, int F, long ldz, const void* dout, long ldo, void* const* dz, long lddz,
@@ -407,6 +409,32 @@ void sdp_apply(std::vector<torch::Tensor> W, std::vector<torch::Tensor> seg_ids,
   }
   fm_sdp_apply_segments((int)n, (int)segs, (int)own_seg, pw.data(), D.data(), pi.data(), pg.data(), pn.data(), ps.data(),
                         po.data(), nmax.data(), lr.data_ptr<float>(), cur());
+}
+
+// dst[to + sum i_k ts_k] (+)= src[so + sum i_k ss_k] over the box d[4] (element offsets / strides
+// into the two buffers' storage; same dtype, bf16 or fp32)
+void strided_copy4(torch::Tensor src, torch::Tensor dst, std::vector<int64_t> d, std::vector<int64_t> ss,
+                   std::vector<int64_t> ts, int64_t so, int64_t to, bool acc) {
+  check_cuda(src, "src");
+  check_cuda(dst, "dst");
+  TORCH_CHECK(src.scalar_type() == dst.scalar_type() && (is_bf16(src) || src.scalar_type() == torch::kFloat32),
+              "strided_copy4: same dtype, bf16 or fp32");
+  TORCH_CHECK(d.size() == 4 && ss.size() == 4 && ts.size() == 4, "strided_copy4: 4-D box");
+  int64_t smax = so, tmax = to;
+  for (int k = 0; k < 4; ++k) {
+    TORCH_CHECK(d[k] >= 1 && ss[k] >= 0 && ts[k] >= 0, "strided_copy4: positive extents / strides");
+    smax += (d[k] - 1) * ss[k];
+    tmax += (d[k] - 1) * ts[k];
+  }
+  TORCH_CHECK(so >= 0 && to >= 0 && smax < src.numel() && tmax < dst.numel(), "strided_copy4: box outside the buffers");
+  int di[4];
+  long sl[4], tl[4];
+  for (int k = 0; k < 4; ++k) {
+    di[k] = (int)d[k];
+    sl[k] = ss[k];
+    tl[k] = ts[k];
+  }
+  fm_strided_copy4_run(src.data_ptr(), dst.data_ptr(), is_bf16(src), di, sl, tl, so, to, acc ? 1 : 0, cur());
 }
 
 void dot_fwd(std::vector<torch::Tensor> zs, int64_t ldz, torch::Tensor out, int64_t ldo, int64_t D, int64_t W, bool self) {
@@ -814,6 +842,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("scale"), py::arg("row_lo") = std::vector<int64_t>{});
   m.def("embedding_bwd_multi", &embedding_bwd_multi, py::arg("W"), py::arg("idx"), py::arg("dy"), py::arg("ldg"),
         py::arg("scale"), py::arg("lr"), py::arg("claim"), py::arg("row_lo") = std::vector<int64_t>{});
+  m.def("strided_copy4", &strided_copy4);
   m.def("sdp_coalesce", &sdp_coalesce);
   m.def("sdp_apply", &sdp_apply);
   m.def("dot_fwd", &dot_fwd);

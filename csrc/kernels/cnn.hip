@@ -275,6 +275,123 @@ __global__ void __launch_bounds__(256) fm_pool_bwd_rows(const T* __restrict__ y,
   }
 }
 
+// ---- pooling on whole planes (one block per (n, c) plane staged in LDS) -------------------
+// The plane's operands are read ONCE, contiguously (coalesced), into LDS; every output of the
+// forward and every input element of the backward is then computed from LDS and written
+// contiguously -- no per-element global re-reads of the overlapping windows.  Used when the
+// staged plane fits PLANE_LDS bytes; larger planes take the row / element kernels.
+constexpr int PLANE_LDS = 48 * 1024;
+
+template <typename T>
+__global__ void __launch_bounds__(256) fm_pool_fwd_plane(const T* __restrict__ x, T* __restrict__ y,
+                                                         unsigned char* __restrict__ code, int H, int W, int P, int Q,
+                                                         int kh, int kw, int sh, int sw, int pt, int pl, int is_max,
+                                                         int act) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* xs = reinterpret_cast<T*>(smem);
+  const long plane = blockIdx.x;
+  const int HW = H * W, PQ = P * Q;
+  const T* xp = x + plane * HW;
+  for (int i = threadIdx.x; i < HW; i += 256) xs[i] = xp[i];
+  __syncthreads();
+  T* yp = y + plane * PQ;
+  unsigned char* cp = code ? code + plane * PQ : nullptr;
+  for (int o = threadIdx.x; o < PQ; o += 256) {
+    const int p = o / Q, q = o - p * Q;
+    const int h0 = p * sh - pt, w0 = q * sw - pl;
+    float m = -INFINITY, sum = 0.f;
+    int cnt = 0, bc = 255;
+    for (int r = 0; r < kh; ++r) {
+      const int h = h0 + r;
+      if (h < 0 || h >= H) continue;
+      for (int c = 0; c < kw; ++c) {
+        const int w = w0 + c;
+        if (w < 0 || w >= W) continue;
+        const float v = tof(xs[h * W + w]);
+        if (v > m || bc == 255) bc = r * kw + c;
+        m = fmaxf(m, v);
+        sum += v;
+        ++cnt;
+      }
+    }
+    const float out = is_max ? m : (cnt ? sum / cnt : 0.f);
+    yp[o] = fromf<T>(act_fwd(act, out));
+    if (cp) cp[o] = (unsigned char)bc;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) fm_pool_bwd_plane(const T* __restrict__ y, const T* __restrict__ dy,
+                                                         const unsigned char* __restrict__ code, T* __restrict__ dx, int H,
+                                                         int W, int P, int Q, int kh, int kw, int sh, int sw, int pt, int pl,
+                                                         int is_max, int act, int acc) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const long plane = blockIdx.x;
+  const int HW = H * W, PQ = P * Q;
+  float* gs = reinterpret_cast<float*>(smem);                       // [PQ] output gradients (act-bwd applied)
+  unsigned char* cs = reinterpret_cast<unsigned char*>(gs + PQ);    // [PQ] argmax codes
+  const T* dyp = dy + plane * PQ;
+  const T* ypp = y + plane * PQ;
+  for (int o = threadIdx.x; o < PQ; o += 256) {
+    const float g = tof(dyp[o]);
+    gs[o] = act == ACT_NONE ? g : act_bwd(act, tof(ypp[o]), g);
+    if (is_max) cs[o] = code[plane * PQ + o];
+  }
+  __syncthreads();
+  T* dxp = dx + plane * HW;
+  for (int e = threadIdx.x; e < HW; e += 256) {
+    const int h = e / W, w = e - h * W;
+    const int pmin = h + pt + 1 >= kh ? (h + pt - kh + sh) / sh : 0;
+    const int pmax = h + pt >= 0 ? min(P - 1, (h + pt) / sh) : -1;
+    const int qmin = w + pl + 1 >= kw ? (w + pl - kw + sw) / sw : 0;
+    const int qmax = w + pl >= 0 ? min(Q - 1, (w + pl) / sw) : -1;
+    float g = 0.f;
+    for (int p = pmin; p <= pmax; ++p) {
+      const int h0 = p * sh - pt;
+      if (h < h0 || h >= h0 + kh) continue;
+      for (int q = qmin; q <= qmax; ++q) {
+        const int w0 = q * sw - pl;
+        if (w < w0 || w >= w0 + kw) continue;
+        const int o = p * Q + q;
+        if (is_max) {
+          if (cs[o] == (unsigned char)((h - h0) * kw + (w - w0))) g += gs[o];
+        } else {
+          const int hs = max(h0, 0), he = min(h0 + kh, H), ws = max(w0, 0), we = min(w0 + kw, W);
+          g += gs[o] / (float)((he - hs) * (we - ws));
+        }
+      }
+    }
+    if (acc) g += tof(dxp[e]);
+    dxp[e] = fromf<T>(g);
+  }
+}
+
+// ---- generic 4-D strided copy (stride-phase convolutions) ----------------------------------
+// dst[o_d + sum i_k t_k] (+)= src[o_s + sum i_k s_k] over the box d0 x d1 x d2 x d3 (innermost
+// d3): gathers an input phase x[:, :, a::s, b::s], scatters a phase gradient back, and moves the
+// taps of a sub-kernel w[:, :, r0::s, t0::s] in both directions.  Consecutive threads walk d3.
+struct Strided4 {
+  int d[4];
+  long ss[4], ts[4];
+  long so, to;
+};
+template <typename T>
+__global__ void __launch_bounds__(256) fm_strided_copy4(const T* __restrict__ src, T* __restrict__ dst, Strided4 g,
+                                                        long total, int acc) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    long r = i;
+    const int i3 = (int)(r % g.d[3]); r /= g.d[3];
+    const int i2 = (int)(r % g.d[2]); r /= g.d[2];
+    const int i1 = (int)(r % g.d[1]);
+    const int i0 = (int)(r / g.d[1]);
+    const long si = g.so + i0 * g.ss[0] + i1 * g.ss[1] + i2 * g.ss[2] + i3 * g.ss[3];
+    const long ti = g.to + i0 * g.ts[0] + i1 * g.ts[1] + i2 * g.ts[2] + i3 * g.ts[3];
+    float v = tof(src[si]);
+    if (acc) v += tof(dst[ti]);
+    dst[ti] = fromf<T>(v);
+  }
+}
+
 // ---- batch norm (training mode, per-channel statistics over N*H*W) -----------------------
 // stats[0:C] = sum, stats[C:2C] = sum of squares   (zeroed by the caller)
 template <typename T>
@@ -437,6 +554,12 @@ static void fm_pool_fwd_t(const void* x, void* y, unsigned char* code, int N, in
                           int sh, int sw, int pt, int pl, int is_max, int act, hipStream_t st) {
   const int total = N * C * P * Q;
   if (total <= 0) return;
+  static const bool no_plane = getenv("FM_POOL_PLANE") != nullptr && atoi(getenv("FM_POOL_PLANE")) == 0;
+  if (!no_plane && (long)H * W * sizeof(T) <= PLANE_LDS) {
+    hipLaunchKernelGGL(fm_pool_fwd_plane<T>, dim3(N * C), dim3(256), (size_t)H * W * sizeof(T), st, (const T*)x, (T*)y,
+                       is_max ? code : nullptr, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act);
+    return;
+  }
   hipLaunchKernelGGL(fm_pool_fwd_kernel<T>, dim3((total + 255) / 256), dim3(256), 0, st, (const T*)x, (T*)y,
                      is_max ? code : nullptr, total, make_fastdiv(Q), make_fastdiv(P), H, W, P, Q, kh, kw, sh, sw, pt, pl,
                      is_max, act);
@@ -453,6 +576,12 @@ static void fm_pool_bwd_t(const void* x, const void* y, const void* dy, void* dx
     hipLaunchKernelGGL(fm_pool_argmax_kernel<T>, dim3((outs + 255) / 256), dim3(256), 0, st, (const T*)x, code, outs, H, W,
                        P, Q, kh, kw, sh, sw, pt, pl);
   static const bool per_elem = getenv("FM_POOL_BWD_ELEM") != nullptr;   // A/B: the per-element kernel
+  static const bool no_plane = getenv("FM_POOL_PLANE") != nullptr && atoi(getenv("FM_POOL_PLANE")) == 0;
+  if (!per_elem && !no_plane && (long)P * Q * 5 <= PLANE_LDS) {
+    hipLaunchKernelGGL(fm_pool_bwd_plane<T>, dim3(N * C), dim3(256), (size_t)P * Q * 5, st, (const T*)y, (const T*)dy,
+                       (const unsigned char*)code, (T*)dx, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, acc);
+    return;
+  }
   if (!per_elem) {
     constexpr int VW = 8;
     const int WS = (W + VW - 1) / VW;
@@ -547,6 +676,25 @@ void fm_bn_bwd(const void* x, const void* y, const void* dy, const float* meanin
 void fm_pad_rows(const void* src, void* dst, int K, int n, int ldp, int bf16, hipStream_t st) {
   if (bf16) fm_pad_rows_t<unsigned short>(src, dst, K, n, ldp, st);
   else fm_pad_rows_t<float>(src, dst, K, n, ldp, st);
+}
+
+void fm_strided_copy4_run(const void* src, void* dst, int bf16, const int* d, const long* ss, const long* ts, long so,
+                          long to, int acc, hipStream_t st) {
+  Strided4 g;
+  long total = 1;
+  for (int k = 0; k < 4; ++k) {
+    g.d[k] = d[k];
+    g.ss[k] = ss[k];
+    g.ts[k] = ts[k];
+    total *= d[k];
+  }
+  g.so = so;
+  g.to = to;
+  if (total <= 0) return;
+  if (bf16) hipLaunchKernelGGL(fm_strided_copy4<unsigned short>, dim3(fm_grid(total, 256, 8192)), dim3(256), 0, st,
+                               (const unsigned short*)src, (unsigned short*)dst, g, total, acc);
+  else hipLaunchKernelGGL(fm_strided_copy4<float>, dim3(fm_grid(total, 256, 8192)), dim3(256), 0, st, (const float*)src,
+                          (float*)dst, g, total, acc);
 }
 
 void fm_compact_rows(const float* src, float* dst, int K, int n, int ldp, int acc, hipStream_t st) {

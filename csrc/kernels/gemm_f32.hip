@@ -265,8 +265,8 @@ FM_DEVICE void epilogue_f32(const GemmF& p, const f32x4_t (&acc)[MR][NR], int zb
 // kernels without the K-loop loads / stores): profiles/gemm_f32_variants_ab.jsonl, gemm_f32_diag.jsonl.
 // NT = 256 (4 waves, 2x2, wave tile BM/2 x BN/2) or 512 (8 waves, 2x4 for BN >= 128, else 4x2:
 // twice the waves per SIMD to cover the LDS-read and barrier latency of each K tile).
-template <int BM, int BN, bool AK, bool BKC, bool VEC, int OPT = 0, int NT = NTF>
-__global__ void __launch_bounds__(NT, 2) fm_gemm_f32_kernel(GemmF p) {
+template <int BM, int BN, bool AK, bool BKC, bool VEC, int OPT = 0, int NT = NTF, int MINB = 2>
+__global__ void __launch_bounds__(NT, MINB) fm_gemm_f32_kernel(GemmF p) {
   constexpr int A_BYTES = BM * BKF * 4;
   constexpr int B_BYTES = BN * BKF * 4;
   constexpr int WN = (NT == 512 && BN >= 128) ? 4 : 2;
@@ -427,6 +427,21 @@ template <int BM, int BN, bool AK, bool BKC, bool VEC>
 void launch_f(const GemmF& p, hipStream_t s, int opt) {
   constexpr int LDS = 2 * (BM + BN) * BKF * 4;
   dim3 grid(p.tiles_m * p.tiles_n, p.batch, p.ksplit);
+  if constexpr (VEC && BM == 256 && BN == 128) {
+    // one 4-wave block per CU, one wave per SIMD with a 128x64 wave tile (the shape hipBLASLt's
+    // fp32 kernel uses on these GEMMs: 8x4 16x16 accumulators, 512-VGPR budget)
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 0, 256, 1>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+      (void)hipFuncSetAttribute((const void*)fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 2, 256, 1>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+      attr = true;
+    }
+    if (opt == 2) hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 2, 256, 1>), grid, dim3(256), LDS, s, p);
+    else hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 0, 256, 1>), grid, dim3(256), LDS, s, p);
+    return;
+  } else {
   if constexpr (VEC && BM == 128 && BN == 128) {   // tuning variants only on the main tile
     // default: 8 waves (2x4, 64x32 per wave) with the fragment double buffer -- 4 waves per SIMD
     // hide the per-K-tile barrier and first-fragment latency (DLRM fp32 GEMMs -3.7 %, the
@@ -448,6 +463,7 @@ void launch_f(const GemmF& p, hipStream_t s, int opt) {
     }
   }
   hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC>), grid, dim3(NTF), LDS, s, p);
+  }
 }
 
 template <int BM, int BN>
@@ -1065,6 +1081,8 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
   // forward runs unsplit instead of split-K 2 + reduce (step -0.2..0.9 %: profiles/ab_f32_t64.txt)
   static const long t64_below = getenv("FM_GEMM_F32_T64") ? atol(getenv("FM_GEMM_F32_T64")) : 129L;
   if (t128 < t64_below && K <= 2048) { BMv = 64; BNv = 64; }
+  // variant bit 4096 (A/B): 256x128 tiles, one 4-wave block per CU, when they fill >= 3/4 of the chip
+  if ((variant & 4096) && vec && (long)((M + 255) / 256) * ((N + 127) / 128) * batch >= 192) { BMv = 256; BNv = 128; }
   p.tiles_m = (M + BMv - 1) / BMv;
   p.tiles_n = (N + BNv - 1) / BNv;
   const long tiles = (long)p.tiles_m * p.tiles_n * batch;
@@ -1081,7 +1099,8 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
   if (K <= 0) ks = 1;
   p.ksplit = ks;
   const int opt = (variant >> 2) & 63;
-  if (BNv == 128) launch_fbm<128, 128>(p, a_kcontig, b_kcontig, vec, stream, opt);
+  if (vec && BMv == 256) launch_fbm<256, 128>(p, a_kcontig, b_kcontig, vec, stream, opt);
+  else if (BNv == 128) launch_fbm<128, 128>(p, a_kcontig, b_kcontig, vec, stream, opt);
   else if (BMv == 128) launch_fbm<128, 64>(p, a_kcontig, b_kcontig, vec, stream, opt);
   else launch_fbm<64, 64>(p, a_kcontig, b_kcontig, vec, stream, 0);
   if (ks > 1) {

@@ -527,6 +527,71 @@ __global__ void __launch_bounds__(256) fm_dot_bwd_f32(PtrTabF Z, long ldz, const
   }
 }
 
+// fp32 forward with COALESCED loads: the per-lane row layout above (lane (r, h) reads 16 B of row
+// r per instruction, 54 rows x 16 B per wave-instruction) is request-bound at ~2.9 TB/s.  Here a
+// wave-instruction loads whole rows (D/4 lanes per row, 64 / (D/4) rows per instruction, 16 B
+// per lane), stages the sample's Z (F <= 32 rows) in a per-wave LDS tile padded to D + 4 floats a
+// row (the row-per-lane ds_read_b128 of the MFMA operands is then bank-conflict free), and keeps
+// the NEXT sample's rows in flight in registers while this sample's MFMAs and stores run.
+template <int D>
+__global__ void __launch_bounds__(256, 2) fm_dot_fwd_f32s(PtrTabF Z, long ldz, float* __restrict__ out, long ldo, long B,
+                                                          int F, int W, int self) {
+  constexpr int LPR = D / 4, RPI = 64 / LPR, NI = 32 / RPI, RS = D + 4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wpad = (W + 3) & ~3;
+  float* zs = reinterpret_cast<float*>(smem) + (long)wave * (32 * RS + wpad);
+  float* row = zs + 32 * RS;
+  const int waves_total = gridDim.x * (blockDim.x >> 6);
+  const int lr = lane / LPR, lc = lane - lr * LPR;
+  const int r = lane & 31, h = lane >> 5;
+  const int npairs = self ? F * (F + 1) / 2 : F * (F - 1) / 2;
+  f32x4_t zr[NI];
+  auto load = [&](long bb) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int j = i * RPI + lr;
+      zr[i] = *reinterpret_cast<const f32x4_t*>(Z.p[j < F ? j : F - 1] + bb * ldz + 4 * lc);
+    }
+  };
+  const long b_first = blockIdx.x * (blockDim.x >> 6) + wave;
+  load(min(b_first, B - 1));
+  for (long b = b_first; b < B; b += waves_total) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int j = i * RPI + lr;
+      if (j < F) *reinterpret_cast<f32x4_t*>(zs + j * RS + 4 * lc) = zr[i];
+    }
+    FM_WAVE_LDS_SYNC();
+    load(min(b + waves_total, B - 1));
+    f32x16_t acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int v = 0; v < D / 8; ++v) {
+      const f32x4_t x = *reinterpret_cast<const f32x4_t*>(zs + r * RS + h * (D / 2) + 4 * v);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x[e], x[e], acc, 0, 0, 0);
+    }
+    // output row: [ z_0 (D) | pairs | zero pad ]
+    for (int c = 4 * lane; c < D; c += 256) *reinterpret_cast<f32x4_t*>(row + c) = *reinterpret_cast<const f32x4_t*>(zs + c);
+    for (int c = D + npairs + lane; c < W; c += 64) row[c] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i = (q & 3) + 8 * (q >> 2) + 4 * h;
+      if (i < F && (self ? r <= i : r < i)) row[D + pair_pos(i, r, self)] = acc[q];
+    }
+    FM_WAVE_LDS_SYNC();
+    float* o = out + b * ldo;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int c = lane * 4 + 256 * t;
+      if (c < W) *reinterpret_cast<f32x4_t*>(o + c) = *reinterpret_cast<const f32x4_t*>(row + c);
+    }
+    FM_WAVE_LDS_SYNC();
+  }
+}
+
 // fp32 backward with the B operand straight from global memory (D = 32E, E = 1/2/4): the column
 // map of N-tile e is n = E*r + e, so lane (r, h) loads Z_j[E r .. E r + E-1] of each row
 // j = 2ks + h with ONE E-float load and that register feeds the E MFMAs of step ks; the E
@@ -678,6 +743,20 @@ extern "C" void fm_dot_interaction_fwd_f32(const float* const* z, int F, long ld
   const long blocks = std::min<long>((B + waves - 1) / waves, dot_block_cap());
   bool fast = (D == 16 || D == 32 || D == 64 || D == 128) && ldz % 4 == 0;
   for (int i = 0; i < F; ++i) fast = fast && al16(z[i]);
+  static const bool staged = getenv("FM_DOT_FWD_STAGED") == nullptr || atoi(getenv("FM_DOT_FWD_STAGED")) != 0;
+  if (staged && fast && D >= 32 && F <= 32 && (W & 3) == 0 && (ldo & 3) == 0 && W <= 1024 && al16(out)) {
+    const size_t lds_s = (size_t)waves * (32 * (D + 4) + ((W + 3) & ~3)) * 4;
+    auto ks = D == 128 ? fm_dot_fwd_f32s<128> : D == 64 ? fm_dot_fwd_f32s<64> : fm_dot_fwd_f32s<32>;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)fm_dot_fwd_f32s<128>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10);
+      (void)hipFuncSetAttribute((const void*)fm_dot_fwd_f32s<64>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10);
+      (void)hipFuncSetAttribute((const void*)fm_dot_fwd_f32s<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10);
+      attr = true;
+    }
+    hipLaunchKernelGGL(ks, dim3((int)blocks), dim3(64 * waves), lds_s, s, t, ldz, out, ldo, B, F, W, self);
+    return;
+  }
   const size_t lds = (size_t)waves * W * 4;
   auto k = !fast ? fm_dot_fwd_f32<0> : D == 128 ? fm_dot_fwd_f32<128> : D == 64 ? fm_dot_fwd_f32<64>
                                      : D == 32 ? fm_dot_fwd_f32<32> : fm_dot_fwd_f32<16>;

@@ -407,6 +407,17 @@ def conv2d_forward(x, w, b, y, stride, pads, act, groups, saved=None):
             saved["s2d_ready"] = True
         x, w, stride, pads = xs, ws, (1, 1), (0, 0, 0, 0)
     Kout, Cg, R, S = w.shape
+    if (PHASE_CONV and R == 1 and S == 1 and stride[0] == stride[1] and stride[0] > 1 and x.dtype == torch.bfloat16):
+        # a strided 1x1 conv reads ONE input phase: gather x[:, :, a::s, b::s] and run the
+        # stride-1 pixel-vector kernel on it (the ResNet downsampling shortcuts)
+        s_ = stride[0]
+        N, Cin, H, W = x.shape
+        a, b_ = (-pads[0]) % s_, (-pads[2]) % s_
+        Ha, Wb = -(-(H - a) // s_), -(-(W - b_) // s_)
+        xa = scratch(x.device, "conv_phase_xf", N * Cin * Ha * Wb, x.dtype).view(N, Cin, Ha, Wb)
+        _strided(x, xa, (N, Cin, Ha, Wb), (Cin * H * W, H * W, s_ * W, s_), (Cin * Ha * Wb, Ha * Wb, Wb, 1), a * W + b_,
+                 0, False)
+        x, stride, pads = xa, (1, 1), ((pads[0] + a) // s_, 0, (pads[2] + b_) // s_, 0)
     wpad = scratch(x.device, "conv_wpad", C().conv_scratch(Kout, Cg * R * S), w.dtype)
     C().conv_fwd(x, w, wpad, b, y, stride[0], stride[1], pads[0], pads[2], int(act))
 
@@ -440,11 +451,74 @@ def conv2d_backward(x, w, y, dy, dx, dw, db, stride, pads, act, groups, acc, sav
             C().conv_s2d(dx, dxs, s_, pads[0], pads[2], True, True)
         return
     Kout, Cg, R, S = w.shape
+    if PHASE_CONV and stride[0] == stride[1] and stride[0] > 1 and x.dtype == torch.bfloat16:
+        _conv_backward_phases(x, w, g, dx, dw, stride[0], pads, acc)
+        return
     # dW / db ACCUMULATE into the per-step zeroed gradient buffer (tied weights sum their grads)
     C().conv_wgrad(g, x, dw.view(-1), R, S, stride[0], stride[1], pads[0], pads[2])
     if dx is not None:
         wt = scratch(x.device, "conv_wt", C().conv_scratch(Cg, Kout * R * S), w.dtype)
         C().conv_dgrad(g, w, wt, dx, stride[0], stride[1], pads[0], pads[2], bool(acc))
+
+
+# Stride-phase decomposition of a strided convolution's backward (FM_CONV_PHASE=0: the strided
+# element-gather kernels instead).  For input phase (a, b) -- rows h = a + s*h', columns
+# w = b + s*w' -- only the taps r = r0 + s*i (r0 = (a + pt) mod s) and t = t0 + s*j reach it, and
+#   dX[:, :, a::s, b::s] = dgrad_stride1(G, W[:, :, r0::s, t0::s], pads (oa, ob))
+#   dW[:, :, r0::s, t0::s] += wgrad_stride1(G, X[:, :, a::s, b::s], pads (oa, ob))
+# with oa = (a + pt - r0) / s: s*s stride-1 problems on the pixel-vector MFMA path that together do
+# exactly the convolution's useful MACs (the strided element path computes every tap of every
+# output position and keeps a quarter: 567 us per ResNet-50 b64 downsampling dgrad,
+# profiles/prof_r3_resnet50_b64_bf16_kernels.txt).
+PHASE_CONV = os.environ.get("FM_CONV_PHASE", "1") != "0"
+
+
+def _strided(src, dst, d, ss, ts, so, to, acc):
+    C().strided_copy4(src, dst, list(d), list(ss), list(ts), int(so), int(to), bool(acc))
+
+
+def _conv_backward_phases(x, w, g, dx, dw, s_, pads, acc):
+    N, Cin, H, W = x.shape
+    Kout, _, R, S = w.shape
+    pt, pl = pads[0], pads[2]
+    dev = x.device
+    for a in range(s_):
+        r0 = (a + pt) % s_
+        nr = -(-(R - r0) // s_) if r0 < R else 0
+        oa = (a + pt - r0) // s_
+        Ha = -(-(H - a) // s_) if a < H else 0
+        for b in range(s_):
+            t0 = (b + pl) % s_
+            nt = -(-(S - t0) // s_) if t0 < S else 0
+            ob = (b + pl - t0) // s_
+            Wb = -(-(W - b) // s_) if b < W else 0
+            if Ha == 0 or Wb == 0:
+                continue
+            box = (N, Cin, Ha, Wb)
+            xstr = (Cin * H * W, H * W, s_ * W, s_)          # x[:, :, a::s, b::s] in x's storage
+            if nr == 0 or nt == 0:                           # no tap reaches this phase
+                if dx is not None and not acc:
+                    z = scratch(dev, "conv_phase_zero", 1, dx.dtype).zero_()
+                    _strided(z, dx, box, (0, 0, 0, 0), xstr, 0, a * W + b, False)
+                continue
+            # sub-kernel W[:, :, r0::s, t0::s] -> contiguous [K, C, nr, nt]
+            wsub = scratch(dev, "conv_phase_w", Kout * Cin * nr * nt, w.dtype).view(Kout, Cin, nr, nt)
+            _strided(w, wsub, (Kout, Cin, nr, nt), (Cin * R * S, R * S, s_ * S, s_), (Cin * nr * nt, nr * nt, nt, 1),
+                     r0 * S + t0, 0, False)
+            # weight gradient: wgrad(G, x phase) into a fp32 [K, C, nr, nt] block, added to dW's taps
+            xa = scratch(dev, "conv_phase_x", N * Cin * Ha * Wb, x.dtype).view(box)
+            _strided(x, xa, box, xstr, (Cin * Ha * Wb, Ha * Wb, Wb, 1), a * W + b, 0, False)
+            dws = scratch(dev, "conv_phase_dw", Kout * Cin * nr * nt, torch.float32).view(Kout, Cin, nr, nt)
+            dws.zero_()
+            C().conv_wgrad(g, xa, dws.view(-1), nr, nt, 1, 1, oa, ob)
+            _strided(dws, dw, (Kout, Cin, nr, nt), (Cin * nr * nt, nr * nt, nt, 1), (Cin * R * S, R * S, s_ * S, s_),
+                     0, r0 * S + t0, True)
+            if dx is None:
+                continue
+            dxa = scratch(dev, "conv_phase_dx", N * Cin * Ha * Wb, dx.dtype).view(box)
+            wt = scratch(dev, "conv_wt", C().conv_scratch(Cin, Kout * nr * nt), w.dtype)
+            C().conv_dgrad(g, wsub, wt, dxa, 1, 1, oa, ob, False)
+            _strided(dxa, dx, box, (Cin * Ha * Wb, Ha * Wb, Wb, 1), xstr, 0, a * W + b, acc)
 
 
 def _pool_code(saved, y):
