@@ -6,6 +6,7 @@
 
 #include "hdf5_lite.h"
 #include "loader.h"
+#include "native_model.h"
 #include "planner.h"
 #include "shard.h"
 #include "strategy_pb.h"
@@ -100,6 +101,12 @@ PYBIND11_MODULE(_native, m) {
   // returns (order, fwd, bwd_live, grad_needed, bwd) with steps (kind, op guid, [input idx])
   using PyIn = std::tuple<int64_t, int64_t, int, int64_t, bool, bool, bool, bool>;
   using PyOp = std::tuple<int64_t, std::vector<PyIn>, std::vector<int64_t>>;
+  // flat weight buffer + gradient all-reduce buckets (native_model.cc): offsets, numel, buckets
+  // [begin, end, entry ids...] -- shared by the Python executor and the native model
+  m.def("plan_weights", [](const std::vector<int64_t>& numels, int64_t cap) {
+    const flexmi::WeightPlan p = flexmi::plan_weights(numels, cap);
+    return py::make_tuple(p.offset, p.numel, p.buckets);
+  });
   m.def("plan_graph", [](const std::vector<PyOp>& ops, int world, bool input_grads) {
     std::vector<flexmi::PlanOp> v;
     v.reserve(ops.size());

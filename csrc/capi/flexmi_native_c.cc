@@ -19,6 +19,7 @@
 #include "../runtime/shard.h"
 #include "../runtime/strategy_pb.h"
 #include "../sim/simulator.h"
+#include "../runtime/native_model.h"
 
 namespace {
 
@@ -536,5 +537,110 @@ int64_t fmn_plan_steps(fmn_plan_t p, int backward, int* kind, int64_t* op, int* 
 }
 
 void fmn_plan_destroy(fmn_plan_t p) { delete p; }
+
+}  // extern "C"
+
+// ---- native model -----------------------------------------------------------------------------
+struct fmn_model_s {
+  std::unique_ptr<flexmi::nm::Model> m;
+};
+
+extern "C" {
+
+fmn_model_t fmn_model_create(int global_batch, int device, int rank, int world, const char* rendezvous) {
+  return guarded(
+      [&] {
+        auto* h = new fmn_model_s();
+        h->m = std::make_unique<flexmi::nm::Model>(global_batch, device, rank, world, rendezvous ? rendezvous : "");
+        return h;
+      },
+      (fmn_model_t) nullptr);
+}
+
+void fmn_model_destroy(fmn_model_t m) { delete m; }
+
+int fmn_model_input(fmn_model_t m, int features) {
+  if (!m) return fail("fmn_model_input: null model");
+  return guarded([&] { return m->m->input(features); }, -1);
+}
+
+int fmn_model_dense(fmn_model_t m, int input_tensor, int out_dim, int activation, int use_bias) {
+  if (!m) return fail("fmn_model_dense: null model");
+  return guarded([&] { return m->m->dense(input_tensor, out_dim, activation, use_bias != 0); }, -1);
+}
+
+int fmn_model_compile(fmn_model_t m, int loss_type, float lr, double bucket_mb) {
+  if (!m) return fail("fmn_model_compile: null model");
+  return guarded(
+      [&] {
+        m->m->compile(loss_type, lr, bucket_mb);
+        return 0;
+      },
+      -1);
+}
+
+int fmn_model_init_weights(fmn_model_t m, uint64_t seed) {
+  if (!m) return fail("fmn_model_init_weights: null model");
+  return guarded(
+      [&] {
+        m->m->init_weights(seed);
+        return 0;
+      },
+      -1);
+}
+
+int fmn_model_num_params(fmn_model_t m) { return m ? m->m->num_params() : fail("null model"); }
+
+int64_t fmn_model_param_numel(fmn_model_t m, int i) {
+  if (!m) return fail("null model");
+  return guarded([&] { return m->m->param_numel(i); }, (int64_t)-1);
+}
+
+int fmn_model_set_param(fmn_model_t m, int i, const float* host) {
+  if (!m || !host) return fail("fmn_model_set_param: bad arguments");
+  return guarded(
+      [&] {
+        m->m->set_param(i, host);
+        return 0;
+      },
+      -1);
+}
+
+int fmn_model_get_param(fmn_model_t m, int i, float* host) {
+  if (!m || !host) return fail("fmn_model_get_param: bad arguments");
+  return guarded(
+      [&] {
+        m->m->get_param(i, host);
+        return 0;
+      },
+      -1);
+}
+
+int fmn_model_train_step(fmn_model_t m, const float* x, const void* labels, double* loss, int64_t* correct) {
+  if (!m || !x || !labels) return fail("fmn_model_train_step: bad arguments");
+  return guarded(
+      [&] {
+        const flexmi::nm::StepStat s = m->m->train_step(x, labels);
+        if (loss) *loss = s.loss;
+        if (correct) *correct = s.correct;
+        return 0;
+      },
+      -1);
+}
+
+int64_t fmn_model_describe(fmn_model_t m, char* buf, int64_t len) {
+  if (!m) return fail("null model");
+  return guarded(
+      [&] {
+        const std::string d = m->m->describe();
+        if (buf && len > 0) {
+          const size_t n = std::min<size_t>(d.size(), (size_t)len - 1);
+          memcpy(buf, d.data(), n);
+          buf[n] = 0;
+        }
+        return (int64_t)d.size();
+      },
+      (int64_t)-1);
+}
 
 }  // extern "C"

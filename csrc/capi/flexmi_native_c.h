@@ -137,6 +137,35 @@ int fmn_embedding_bag_forward(const float* W, int64_t rows, int64_t D, const int
 int fmn_embedding_bag_backward(float* target, int64_t rows, int64_t D, const int64_t* idx, int64_t B, int64_t bag,
                                int64_t row_lo, const float* dy, int64_t ld_dy, float alpha);
 
+/* ---- native model: build, plan and train an MLP entirely in C++ ----------------------------------
+ * The plan compiler (csrc/runtime/native_model.cc) lays out one rank's buffers for data
+ * parallelism (sample split; replicated weights in one flat buffer; gradient all-reduce buckets
+ * in backward order), decides the fused epilogues and runs the step on an engine:
+ * device 0 = CPU (reference fp32 loops, one rank), device 1 = HIP (flexmi's gfx950 kernels from
+ * libflexmi_kernels.so, RCCL across `world` processes that share the `rendezvous` directory).
+ * Reference: FFModel compile / init_layers / forward / backward / update (src/runtime/model.cc). */
+typedef struct fmn_model_s* fmn_model_t;
+fmn_model_t fmn_model_create(int global_batch, int device, int rank, int world, const char* rendezvous);
+void fmn_model_destroy(fmn_model_t m);
+/* tensor ids: the input (features per sample), then a chain of dense layers (act: 10 none,
+ * 11 relu, 12 sigmoid, 13 tanh) */
+int fmn_model_input(fmn_model_t m, int features);
+int fmn_model_dense(fmn_model_t m, int input_tensor, int out_dim, int activation, int use_bias);
+/* loss: 51 sparse categorical CE (softmax of the last layer's logits, int32 labels), 52 MSE (avg),
+ * 54 binary CE (sigmoid output); bucket_mb = gradient all-reduce bucket size */
+int fmn_model_compile(fmn_model_t m, int loss_type, float lr, double bucket_mb);
+int fmn_model_init_weights(fmn_model_t m, uint64_t seed);
+/* parameter entries in model order: weight [out][in] then bias [out] of every dense layer */
+int fmn_model_num_params(fmn_model_t m);
+int64_t fmn_model_param_numel(fmn_model_t m, int i);
+int fmn_model_set_param(fmn_model_t m, int i, const float* host);
+int fmn_model_get_param(fmn_model_t m, int i, float* host);
+/* one training step on the GLOBAL batch x [B][features] (each rank takes its sample shard) and
+ * labels ([B] int32 for loss 51, [B][out] float otherwise); loss = this rank's mean loss */
+int fmn_model_train_step(fmn_model_t m, const float* x, const void* labels, double* loss, int64_t* correct);
+/* human-readable plan (layers, fused epilogues, flat buffer, buckets); returns the length */
+int64_t fmn_model_describe(fmn_model_t m, char* buf, int64_t len);
+
 #ifdef __cplusplus
 }
 #endif

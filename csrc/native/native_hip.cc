@@ -1,0 +1,240 @@
+// HIP engine of the native model (native_model.h): flexmi's gfx950 kernels (linked from
+// libflexmi_kernels.so, no PyTorch) and flexmi's own RCCL communicator.
+//
+//   dense forward  fm_gemm_f32 (v_mfma_f32_16x16x4_f32, bias + activation in the epilogue) or
+//                  the skinny N = 1 kernel
+//   dense backward fm_act_bwd_bias (act'), fm_gemm_f32 dW (+= , bias gradient as the staged A
+//                  tiles' row sums) and dX (activation backward of the layer below fused into
+//                  the epilogue) -- the same kernel sequence as flexmi/ops/_kernels.py linear_backward
+//   loss / SGD     fm_loss_fwd_bwd, fm_sgd_update (zeroes the consumed gradients)
+//   communication  one RCCL communicator per model (unique id handed over through a file in the
+//                  rendezvous directory); bucket all-reduces on a second HIP stream, started as
+//                  soon as the bucket's last gradient kernel is enqueued (event dependency) and
+//                  joined before the update -- overlapped with the rest of the backward.
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cstdio>
+#include <fstream>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <unistd.h>
+#include <vector>
+
+#include "native_model.h"
+
+extern "C" {
+int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, const float* B, long ldb, long sB, int b_kcontig, float* C,
+                long ldc, long sC, const float* bias, int M, int N, int K, int batch, float alpha, int beta, int act, float* ws,
+                long ws_bytes, int ksplit_req, const float* act_y, long lday, int bwd_act, float* colsum, float* rowsum_a,
+                hipStream_t stream);
+void fm_skinny_fwd_f32_launch(const float* x, long ldx, const float* w, const float* bias, float* y, long ldy, long B, int K,
+                              int act, hipStream_t s);
+void fm_skinny_bwd_f32_launch(const float* x, long ldx, const float* w, const float* y, long ldy, const float* dy, long lddy,
+                              float* dx, long lddx, int dx_acc, float* dw, float* db, long B, int K, int act, hipStream_t s);
+void fm_act_bwd_bias(const void* y, const void* dy, void* dpre, float* db, long B, int N, int act, int bf16, hipStream_t s);
+void fm_softmax_fwd(const void* x, void* y, long rows, int C, int bf16, hipStream_t s);
+void fm_loss_fwd_bwd(const void* logits, int logits_bf16, const void* labels, void* grad, int grad_bf16, long B, int C,
+                     int loss_type, float scale, float* acc, int mask, float clamp_t, hipStream_t s);
+void fm_sgd_update(float* W, float* G, float* V, unsigned short* Wc, const float* lr, long n, float wd, float mom, int nesterov,
+                   int zero_g, hipStream_t s);
+}
+
+namespace flexmi {
+namespace nm {
+
+namespace {
+
+#define HIPX(x)                                                                                            \
+  do {                                                                                                     \
+    hipError_t e_ = (x);                                                                                   \
+    if (e_ != hipSuccess) throw std::runtime_error(std::string("native hip engine: ") + #x + ": " + hipGetErrorString(e_)); \
+  } while (0)
+#define NCCLX(x)                                                                                           \
+  do {                                                                                                     \
+    ncclResult_t r_ = (x);                                                                                 \
+    if (r_ != ncclSuccess) throw std::runtime_error(std::string("native hip engine: ") + #x + ": " + ncclGetErrorString(r_)); \
+  } while (0)
+
+constexpr long WS_BYTES = 64L << 20;   // split-K slabs of the dW GEMMs
+
+class HipEngine : public Engine {
+ public:
+  HipEngine(int rank, int world, const std::string& rendezvous) : rank_(rank), world_(world) {
+    int ndev = 0;
+    HIPX(hipGetDeviceCount(&ndev));
+    if (ndev <= 0) throw std::runtime_error("native hip engine: no GPU");
+    HIPX(hipSetDevice(rank % ndev));
+    HIPX(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+    HIPX(hipStreamCreateWithFlags(&comm_st_, hipStreamNonBlocking));
+    HIPX(hipMalloc(&ws_, WS_BYTES));
+    HIPX(hipMalloc(&slots_, 16 * sizeof(float)));
+    HIPX(hipMalloc(&lr_, sizeof(float)));
+    if (world > 1) init_comm(rendezvous);
+  }
+  ~HipEngine() override {
+    hipStreamSynchronize(st_);
+    hipStreamSynchronize(comm_st_);
+    for (auto e : events_) hipEventDestroy(e);
+    if (comm_) ncclCommDestroy(comm_);
+    hipFree(ws_);
+    hipFree(slots_);
+    hipFree(lr_);
+    hipStreamDestroy(comm_st_);
+    hipStreamDestroy(st_);
+  }
+
+  void* alloc(size_t bytes) override {
+    void* p = nullptr;
+    HIPX(hipMalloc(&p, std::max<size_t>(bytes, 256)));
+    HIPX(hipMemsetAsync(p, 0, std::max<size_t>(bytes, 256), st_));
+    return p;
+  }
+  void release(void* p) override { hipFree(p); }
+  void h2d(void* dst, const void* src, size_t bytes) override {
+    HIPX(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st_));
+    HIPX(hipStreamSynchronize(st_));   // the host buffer may be reused right after
+  }
+  void d2h(void* dst, const void* src, size_t bytes) override {
+    HIPX(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st_));
+    HIPX(hipStreamSynchronize(st_));
+  }
+  void sync() override { HIPX(hipStreamSynchronize(st_)); }
+
+  void dense_fwd(const float* x, const float* W, const float* b, float* y, int M, int K, int N, int act) override {
+    if (N == 1) {
+      fm_skinny_fwd_f32_launch(x, K, W, b, y, 1, M, K, act, st_);
+      return;
+    }
+    fm_gemm_f32(x, K, 0, 1, W, K, 0, 1, y, N, 0, b, M, N, K, 1, 1.f, 0, act, ws_, WS_BYTES, 0, nullptr, 0, ACT_NONE, nullptr,
+                nullptr, st_);
+  }
+
+  void dense_bwd(const float* x, const float* W, const float* y, const float* dy, float* dx, float* dW, float* db, int M,
+                 int K, int N, int act, bool grad_is_dpre, const float* y_below, int act_below) override {
+    if (N == 1 && K % 4 == 0 && y_below == nullptr) {
+      fm_skinny_bwd_f32_launch(x, K, W, y, 1, dy, 1, dx, K, 0, dW, db, M, K, grad_is_dpre ? ACT_NONE : act, st_);
+      return;
+    }
+    const float* dpre = dy;
+    if (!grad_is_dpre && act != ACT_NONE) {
+      float* t = scratch((size_t)M * N);
+      fm_act_bwd_bias(y, dy, t, nullptr, M, N, act, 0, st_);
+      dpre = t;
+    }
+    // dW[N][K] += dpre^T x (both operands MN-contiguous), db += column sums of dpre
+    fm_gemm_f32(dpre, N, 0, 0, x, K, 0, 0, dW, K, 0, nullptr, N, K, M, 1, 1.f, 1, ACT_NONE, ws_, WS_BYTES, 0, nullptr, 0,
+                ACT_NONE, nullptr, db, st_);
+    if (!dx) return;
+    // dX[M][K] = dpre W (+ act' of the layer below)
+    fm_gemm_f32(dpre, N, 0, 1, W, K, 0, 0, dx, K, 0, nullptr, M, K, N, 1, 1.f, 0, ACT_NONE, ws_, WS_BYTES, 0, y_below,
+                y_below ? K : 0, y_below ? act_below : ACT_NONE, nullptr, nullptr, st_);
+  }
+
+  void softmax(const float* x, float* y, int M, int C) override { fm_softmax_fwd(x, y, M, C, 0, st_); }
+
+  void loss(int type, const float* p, const void* labels, float* grad, int M, int C, float scale, float* stats) override {
+    HIPX(hipMemsetAsync(slots_, 0, 16 * sizeof(float), st_));
+    fm_loss_fwd_bwd(p, 0, labels, grad, 0, M, C, type, scale, slots_, 1, 0.f, st_);
+    // metric slots: [1] correct, [7] loss sum
+    HIPX(hipMemcpyAsync(stats, slots_ + 7, sizeof(float), hipMemcpyDeviceToDevice, st_));
+    HIPX(hipMemcpyAsync(stats + 1, slots_ + 1, sizeof(float), hipMemcpyDeviceToDevice, st_));
+  }
+
+  void sgd(float* w, float* g, int64_t n, float lr) override {
+    if (lr != lr_host_) {
+      HIPX(hipMemcpyAsync(lr_, &lr, sizeof(float), hipMemcpyHostToDevice, st_));
+      HIPX(hipStreamSynchronize(st_));
+      lr_host_ = lr;
+    }
+    fm_sgd_update(w, g, nullptr, nullptr, lr_, n, 0.f, 0.f, 0, 1, st_);
+  }
+
+  void allreduce_start(float* buf, int64_t n) override {
+    if (!comm_) return;
+    hipEvent_t ready = event();
+    HIPX(hipEventRecord(ready, st_));
+    HIPX(hipStreamWaitEvent(comm_st_, ready, 0));
+    NCCLX(ncclAllReduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, comm_, comm_st_));
+    pending_ = true;
+  }
+  void allreduce_wait() override {
+    if (!pending_) return;
+    hipEvent_t done = event();
+    HIPX(hipEventRecord(done, comm_st_));
+    HIPX(hipStreamWaitEvent(st_, done, 0));
+    pending_ = false;
+    ev_next_ = 0;
+  }
+
+ private:
+  hipEvent_t event() {
+    if (ev_next_ == events_.size()) {
+      hipEvent_t e;
+      HIPX(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      events_.push_back(e);
+    }
+    return events_[ev_next_++];
+  }
+  float* scratch(size_t n) {
+    if (n > scratch_n_) {
+      if (scratch_) {
+        HIPX(hipStreamSynchronize(st_));
+        hipFree(scratch_);
+      }
+      HIPX(hipMalloc(&scratch_, n * sizeof(float)));
+      scratch_n_ = n;
+    }
+    return scratch_;
+  }
+  // rank 0 creates the RCCL unique id and publishes it as <rendezvous>/rccl_id (written to a
+  // temporary name, then renamed: readers never see a partial file); the others poll for it
+  void init_comm(const std::string& dir) {
+    if (dir.empty()) throw std::runtime_error("native hip engine: world > 1 needs a rendezvous directory");
+    ncclUniqueId id;
+    const std::string path = dir + "/rccl_id";
+    if (rank_ == 0) {
+      NCCLX(ncclGetUniqueId(&id));
+      const std::string tmp = path + ".tmp";
+      {
+        std::ofstream f(tmp, std::ios::binary);
+        f.write(reinterpret_cast<const char*>(&id), sizeof(id));
+      }
+      if (std::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("native hip engine: publish rccl id");
+    } else {
+      const auto t0 = std::chrono::steady_clock::now();
+      while (true) {
+        std::ifstream f(path, std::ios::binary);
+        if (f && f.read(reinterpret_cast<char*>(&id), sizeof(id)) && f.gcount() == sizeof(id)) break;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120))
+          throw std::runtime_error("native hip engine: no rccl id from rank 0 in " + dir);
+        std::this_thread::sleep_for(std::chrono::milliseconds(20));
+      }
+    }
+    NCCLX(ncclCommInitRank(&comm_, world_, id, rank_));
+  }
+
+  int rank_, world_;
+  hipStream_t st_ = nullptr, comm_st_ = nullptr;
+  ncclComm_t comm_ = nullptr;
+  float* ws_ = nullptr;
+  float* slots_ = nullptr;
+  float* lr_ = nullptr;
+  float lr_host_ = -1.f;
+  float* scratch_ = nullptr;
+  size_t scratch_n_ = 0;
+  std::vector<hipEvent_t> events_;
+  size_t ev_next_ = 0;
+  bool pending_ = false;
+};
+
+}  // namespace
+
+std::unique_ptr<Engine> make_hip_engine(int rank, int world, const std::string& rendezvous) {
+  return std::make_unique<HipEngine>(rank, world, rendezvous);
+}
+
+}  // namespace nm
+}  // namespace flexmi

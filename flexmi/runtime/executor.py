@@ -1032,17 +1032,24 @@ class Executor:
                     groups[key] = SyncGroup(key)
                 g = groups[key]
                 e.group = g
-                e.offset = g.numel
-                g.numel += (e.numel + 63) // 64 * 64  # 256-B aligned views: 16-B vector loads in every kernel
                 g.entries.append(e)
         self.groups = list(groups.values())
         mixed = self.cdtype != torch.float32
         cap = max(1, int(self.cfg.grad_bucket_mb * (1 << 20) / 4))
         zero = int(getattr(self.cfg, "zero_stage", 0)) >= 1
+        from flexmi import _native
         for g in self.groups:
             g.zero = zero and g.replicated
             if g.zero:
                 self._zero_layout(g, cap)
+            else:
+                # flat buffer layout + all-reduce buckets from the native plan compiler (the same
+                # planner as the C++ model, csrc/runtime/native_model.cc plan_weights): 256-B aligned
+                # views (16-B vector loads in every kernel), buckets in backward order
+                offs, g.numel, bks = _native.plan_weights([e.numel for e in g.entries], cap)
+                for e, o in zip(g.entries, offs):
+                    e.offset = int(o)
+                g.buckets = [[int(b[0]), int(b[1]), {g.entries[int(i)].param.guid for i in b[2:]}] for b in bks]
             g.master = self._alloc((g.numel,), torch.float32)
             g.gradbuf = self._alloc((g.numel,), torch.float32)
             g.gradbuf.zero_()
@@ -1060,18 +1067,7 @@ class Executor:
                 e.grad = g.gradbuf[sl].view(e.shape)
                 e.compute = g.compute[sl].view(e.shape)
                 e.state = {} if g.zero else {n: s[sl].view(e.shape) for n, s in g.state.items()}
-            if g.zero:
-                continue
-            # buckets (only meaningful for replicated groups)
-            start, ids = 0, set()
-            for e in g.entries:
-                end = e.offset + (e.numel + 63) // 64 * 64
-                if ids and end - start > cap:
-                    g.buckets.append([start, e.offset, ids])
-                    start, ids = e.offset, set()
-                ids.add(e.param.guid)
-            if ids:
-                g.buckets.append([start, g.numel, ids])
+
         # communicators for every replicated subset, created in the same order everywhere
         all_sets = []
         for op in ops:

@@ -1,0 +1,120 @@
+"""The native C++ model (csrc/runtime/native_model.cc: plan compiler + engines) driven from a C
+program through libflexmi_native_c alone -- no CPython in the process -- must train exactly like
+flexmi's Python executor: same initial weights, same batches, same final weights.  The GPU test
+runs the same C program on the HIP engine (flexmi's gfx950 kernels + RCCL communicator) and
+compares with the CPU engine."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "flexmi", "libflexmi_native_c.so")
+
+
+def _build(tmp_path):
+    if not os.path.exists(LIB):
+        pytest.skip("libflexmi_native_c.so not built")
+    exe = str(tmp_path / "native_mlp")
+    subprocess.run(["gcc", "-O2", "-I" + os.path.join(ROOT, "csrc", "capi"), os.path.join(ROOT, "tests", "capi", "native_mlp.c"),
+                    "-L" + os.path.join(ROOT, "flexmi"), "-Wl,-rpath," + os.path.join(ROOT, "flexmi"), "-lflexmi_native_c",
+                    "-o", exe], check=True)
+    # no interpreter behind the C API: the binary links no libpython / libtorch
+    ldd = subprocess.run(["ldd", exe], capture_output=True, text=True).stdout
+    assert "libpython" not in ldd and "libtorch" not in ldd, ldd
+    return exe
+
+
+def _parse(path):
+    b = open(path, "rb").read()
+    o = 0
+
+    def take(fmt, n=1):
+        nonlocal o
+        sz = np.dtype(fmt).itemsize * n
+        v = np.frombuffer(b, dtype=np.dtype(fmt), count=n, offset=o)
+        o += sz
+        return v
+    npar = int(take("<i4")[0])
+    init = []
+    for _ in range(npar):
+        n = int(take("<i8")[0])
+        init.append(take("<f4", n).copy())
+    B, F, C, steps, loss = (int(v) for v in take("<i4", 5))
+    batches = []
+    for _ in range(steps):
+        x = take("<f4", B * F).reshape(B, F).copy()
+        y = take("<i4", B).copy() if loss == 51 else take("<f4", B * C).reshape(B, C).copy()
+        batches.append((x, y))
+    losses = take("<f8", steps).copy()
+    final = [take("<f4", len(w)).copy() for w in init]
+    return dict(init=init, B=B, F=F, C=C, steps=steps, loss=loss, batches=batches, losses=losses, final=final)
+
+
+def _replay(rec):
+    """The same network and batches through flexmi's Python executor (CPU, fp32)."""
+    from flexmi.core import ActiMode, FFConfig, FFModel, LossType, MetricsType, SGDOptimizer
+    cfg = FFConfig()
+    cfg.batchSize, cfg.device, cfg.compute_dtype = rec["B"], "cpu", "fp32"
+    m = FFModel(cfg)
+    x = m.create_tensor([rec["B"], rec["F"]], name="x")
+    h = m.dense(x, 64, ActiMode.AC_MODE_RELU)
+    h = m.dense(h, 32, ActiMode.AC_MODE_TANH)
+    h = m.dense(h, 16, ActiMode.AC_MODE_RELU)
+    last = ActiMode.AC_MODE_SIGMOID if rec["loss"] == 54 else ActiMode.AC_MODE_NONE
+    h = m.dense(h, rec["C"], last)
+    if rec["loss"] == 51:
+        h = m.softmax(h)
+    m.compile(SGDOptimizer(m, 0.05), LossType(rec["loss"]), [MetricsType.METRICS_ACCURACY])
+    ex = m.init_layers()
+    assert len(m.parameters) == len(rec["init"])
+    for p, w in zip(m.parameters, rec["init"]):
+        p.set_weights(m, w.reshape(p.dims))
+    for xb, yb in rec["batches"]:
+        ex.scatter_from_host(x, xb)
+        lab = m.get_label_tensor()
+        ex.scatter_from_host(lab, yb.reshape(lab.dims))
+        ex.train_step()
+    return [p.get_weights(m).reshape(-1) for p in m.parameters]
+
+
+@pytest.mark.parametrize("loss", [51, 52, 54])
+def test_native_c_program_trains_like_the_executor(tmp_path, loss):
+    exe = _build(tmp_path)
+    out = str(tmp_path / "cpu.bin")
+    r = subprocess.run([exe, "cpu", out, "6", str(loss)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "native_mlp ok" in r.stdout, r.stderr
+    # the plan: fused act-bwd epilogues, one flat buffer, several all-reduce buckets
+    assert "[dX epilogue: act' below]" in r.stdout and "all-reduce bucket" in r.stdout
+    rec = _parse(out)
+    got = _replay(rec)
+    for a, b in zip(rec["final"], got):
+        np.testing.assert_allclose(a, b, rtol=2e-5, atol=2e-6)
+    assert np.all(np.isfinite(rec["losses"]))
+
+
+def test_plan_weights_matches_executor_buckets():
+    """flexmi._native.plan_weights is the bucket planner of the Python executor and the native
+    model alike (256-B aligned offsets, buckets closed at the cap in backward order)."""
+    from flexmi import _native
+    offs, numel, buckets = _native.plan_weights([10, 200, 64, 1000, 3], 300)
+    assert list(offs) == [0, 64, 320, 384, 1408] and numel == 1472
+    assert [tuple(b[:2]) for b in buckets] == [(0, 64), (64, 320), (320, 384), (384, 1408), (1408, 1472)]
+    assert [list(b[2:]) for b in buckets] == [[0], [1], [2], [3], [4]]
+    offs, numel, buckets = _native.plan_weights([10, 20, 30, 4000], 1000)
+    assert list(offs) == [0, 64, 128, 192] and [list(b) for b in buckets] == [[0, 192, 0, 1, 2], [192, 4224, 3]]
+
+
+@pytest.mark.gpu
+def test_native_c_program_hip_engine_matches_cpu(tmp_path):
+    exe = _build(tmp_path)
+    for dev in ("cpu", "hip"):
+        r = subprocess.run([exe, dev, str(tmp_path / f"{dev}.bin"), "6", "51"], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0 and "native_mlp ok" in r.stdout, (dev, r.stderr[-2000:])
+    c, h = _parse(str(tmp_path / "cpu.bin")), _parse(str(tmp_path / "hip.bin"))
+    for a, b in zip(c["init"], h["init"]):
+        np.testing.assert_array_equal(a, b)
+    for a, b in zip(c["final"], h["final"]):
+        np.testing.assert_allclose(b, a, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(h["losses"], c["losses"], rtol=1e-4)

@@ -151,9 +151,31 @@ def write_ninja(only=None):
             lines.append(f"build {o}: cxx {src}")
             lines.append(f"  extra = -I{ROOT}/csrc/capi")
             nobjs.append(o)
+        # the native model (csrc/runtime/native_model.cc) with its HIP engine (csrc/native/
+        # native_hip.cc: flexmi's kernels + RCCL) -- libflexmi_kernels.so is the kernel objects
+        # alone, no PyTorch
+        for src in [os.path.join(ROOT, "csrc", "runtime", "native_model.cc")]:
+            o = os.path.join(BUILD, "nc_" + os.path.basename(src).replace(".cc", ".o"))
+            lines.append(f"build {o}: cxx {src}")
+            lines.append(f"  extra = -I{ROOT}/csrc/capi")
+            nobjs.append(o)
+        hip_o = os.path.join(BUILD, "nc_native_hip.o")
+        lines.append(f"build {hip_o}: cxx {os.path.join(ROOT, 'csrc', 'native', 'native_hip.cc')}")
+        lines.append(f"  extra = -D__HIP_PLATFORM_AMD__=1 -I{ROCM}/include -I{ROOT}/csrc/runtime")
+        nobjs.append(hip_o)
+        kobjs = [os.path.join(BUILD, "k_" + os.path.basename(src).replace(".hip", ".o"))
+                 for src in sorted(glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.hip")))]
+        if only == "native":   # kernel objects come from the C target's rules otherwise
+            for src in sorted(glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.hip"))):
+                lines.append(f"build {os.path.join(BUILD, 'k_' + os.path.basename(src).replace('.hip', '.o'))}: hipcc {src}")
+        klib = os.path.join(ROOT, "flexmi", "libflexmi_kernels.so")
+        lines.append(f"build {klib}: hiplink {' '.join(kobjs)}")
+        lines.append(f"  ldflags = -L{ROCM}/lib -Wl,-rpath,{ROCM}/lib -lamdhip64")
+        targets.append(klib)
         nc = os.path.join(ROOT, "flexmi", "libflexmi_native_c.so")
-        lines.append(f"build {nc}: cxxlink {' '.join(nobjs)}")
-        lines.append("  ldflags = -pthread")
+        lines.append(f"build {nc}: cxxlink {' '.join(nobjs)} | {klib}")
+        lines.append(f"  ldflags = -pthread -L{ROOT}/flexmi -Wl,-rpath,'$$ORIGIN' -lflexmi_kernels "
+                     f"-L{ROCM}/lib -Wl,-rpath,{ROCM}/lib -lamdhip64 -lrccl")
         targets.append(nc)
         # C API (csrc/capi): embeds CPython, so it links libpython
         capi_src = os.path.join(ROOT, "csrc", "capi", "flexmi_c.cc")
