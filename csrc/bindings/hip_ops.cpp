@@ -12,6 +12,8 @@ void fm_image_normalize(const unsigned char* src, void* dst, long N, int H, int 
                         int bf16, hipStream_t s);
 void fm_gemm_set_variant(int v);
 void fm_gemm_f32_set_variant(int v);
+void fm_gemm_async_arm(int on);
+void fm_gemm_join(hipStream_t s);
 int fm_gemm(const void* A, long lda, long sA, int a_kcontig, const void* B, long ldb, long sB, int b_kcontig, void* C,
             long ldc, long sC, int c_fp32, const float* bias, int M, int N, int K, int batch, float alpha, int beta,
             int act, float* ws, long ws_bytes, int ksplit_req, const void* act_y, long lday, int bwd_act,
@@ -135,7 +137,7 @@ int gemm(torch::Tensor A, int64_t lda, int64_t sA, bool a_kcontig, torch::Tensor
          torch::Tensor C, int64_t ldc, int64_t sC, c10::optional<torch::Tensor> bias, int64_t M, int64_t N, int64_t K,
          int64_t batch, double alpha, bool beta, int64_t act, c10::optional<torch::Tensor> ws, int64_t ksplit,
          c10::optional<torch::Tensor> act_y, int64_t lday, int64_t bwd_act, c10::optional<torch::Tensor> colsum,
-         c10::optional<torch::Tensor> rowsum_a) {
+         c10::optional<torch::Tensor> rowsum_a, bool async_reduce) {
   check_cuda(A, "A");
   check_cuda(B, "B");
   check_cuda(C, "C");
@@ -175,16 +177,25 @@ int gemm(torch::Tensor A, int64_t lda, int64_t sA, bool a_kcontig, torch::Tensor
     w = ws->data_ptr<float>();
     wsb = ws->numel() * 4;
   }
+  // async_reduce: the split-K reduce of THIS GEMM may run on a side stream (gemm_async.hip); the
+  // caller joins (gemm_join) before anything reads C
+  fm_gemm_async_arm(async_reduce ? 1 : 0);
+  int ks;
   if (f32)
-    return fm_gemm_f32(A.data_ptr<float>(), lda, sA, a_kcontig, B.data_ptr<float>(), ldb, sB, b_kcontig, C.data_ptr<float>(),
-                       ldc, sC, bias.has_value() && bias->defined() ? bias->data_ptr<float>() : nullptr, (int)M, (int)N,
-                       (int)K, (int)batch, (float)alpha, beta ? 1 : 0, (int)act, w, wsb, (int)ksplit,
-                       (const float*)cptr(act_y), lday, (int)bwd_act, (float*)mptr(colsum), (float*)mptr(rowsum_a), cur());
-  return fm_gemm(A.data_ptr(), lda, sA, a_kcontig, B.data_ptr(), ldb, sB, b_kcontig, C.data_ptr(), ldc, sC,
+    ks = fm_gemm_f32(A.data_ptr<float>(), lda, sA, a_kcontig, B.data_ptr<float>(), ldb, sB, b_kcontig, C.data_ptr<float>(),
+                     ldc, sC, bias.has_value() && bias->defined() ? bias->data_ptr<float>() : nullptr, (int)M, (int)N,
+                     (int)K, (int)batch, (float)alpha, beta ? 1 : 0, (int)act, w, wsb, (int)ksplit,
+                     (const float*)cptr(act_y), lday, (int)bwd_act, (float*)mptr(colsum), (float*)mptr(rowsum_a), cur());
+  else
+    ks = fm_gemm(A.data_ptr(), lda, sA, a_kcontig, B.data_ptr(), ldb, sB, b_kcontig, C.data_ptr(), ldc, sC,
                  C.scalar_type() == torch::kFloat32, bias.has_value() && bias->defined() ? bias->data_ptr<float>() : nullptr,
                  (int)M, (int)N, (int)K, (int)batch, (float)alpha, beta ? 1 : 0, (int)act, w, wsb, (int)ksplit,
                  cptr(act_y), lday, (int)bwd_act, (float*)mptr(colsum), (float*)mptr(rowsum_a), cur());
+  fm_gemm_async_arm(0);
+  return ks;
 }
+
+void gemm_join() { fm_gemm_join(cur()); }
 
 void skinny_fwd(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor y, int64_t act) {
   TORCH_CHECK(w.numel() == x.size(1) && y.size(1) == 1 && x.stride(1) == 1, "skinny_fwd: x[B,K] w[1,K] y[B,1]");
@@ -824,6 +835,7 @@ void lstm_cell_bwd(torch::Tensor A, int64_t a_off, int64_t lda, torch::Tensor ct
 PYBIND11_MODULE(_C, m) {
   m.doc() = "flexmi HIP/CDNA4 kernels (gfx950)";
   m.def("gemm", &gemm);
+  m.def("gemm_join", &gemm_join);
   m.def("gemm_set_variant", [](int v) { fm_gemm_set_variant(v); });
   m.def("gemm_f32_set_variant", [](int v) { fm_gemm_f32_set_variant(v); });
   m.def("init_fill", &init_fill);

@@ -278,8 +278,10 @@ __global__ void __launch_bounds__(256) fm_pool_bwd_rows(const T* __restrict__ y,
 // ---- pooling on whole planes (one block per (n, c) plane staged in LDS) -------------------
 // The plane's operands are read ONCE, contiguously (coalesced), into LDS; every output of the
 // forward and every input element of the backward is then computed from LDS and written
-// contiguously -- no per-element global re-reads of the overlapping windows.  Used when the
-// staged plane fits PLANE_LDS bytes; larger planes take the row / element kernels.
+// contiguously -- no per-element global re-reads of the overlapping windows.  Opt-in
+// (FM_POOL_PLANE=1, planes that fit PLANE_LDS bytes): measured slower than the row / element
+// kernels on AlexNet b256 (pool bwd 479 vs 286 us/step) and ResNet-50 b64 (fwd 335 vs 137) --
+// one block per plane leaves too few waves in flight to hide the HBM latency of the staging.
 constexpr int PLANE_LDS = 48 * 1024;
 
 template <typename T>
@@ -554,7 +556,7 @@ static void fm_pool_fwd_t(const void* x, void* y, unsigned char* code, int N, in
                           int sh, int sw, int pt, int pl, int is_max, int act, hipStream_t st) {
   const int total = N * C * P * Q;
   if (total <= 0) return;
-  static const bool no_plane = getenv("FM_POOL_PLANE") != nullptr && atoi(getenv("FM_POOL_PLANE")) == 0;
+  static const bool no_plane = !(getenv("FM_POOL_PLANE") != nullptr && atoi(getenv("FM_POOL_PLANE")) == 1);   // opt-in: loses to the row kernels (profiles/prof_r3e_*)
   if (!no_plane && (long)H * W * sizeof(T) <= PLANE_LDS) {
     hipLaunchKernelGGL(fm_pool_fwd_plane<T>, dim3(N * C), dim3(256), (size_t)H * W * sizeof(T), st, (const T*)x, (T*)y,
                        is_max ? code : nullptr, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act);
@@ -576,7 +578,7 @@ static void fm_pool_bwd_t(const void* x, const void* y, const void* dy, void* dx
     hipLaunchKernelGGL(fm_pool_argmax_kernel<T>, dim3((outs + 255) / 256), dim3(256), 0, st, (const T*)x, code, outs, H, W,
                        P, Q, kh, kw, sh, sw, pt, pl);
   static const bool per_elem = getenv("FM_POOL_BWD_ELEM") != nullptr;   // A/B: the per-element kernel
-  static const bool no_plane = getenv("FM_POOL_PLANE") != nullptr && atoi(getenv("FM_POOL_PLANE")) == 0;
+  static const bool no_plane = !(getenv("FM_POOL_PLANE") != nullptr && atoi(getenv("FM_POOL_PLANE")) == 1);   // opt-in: loses to the row kernels (profiles/prof_r3e_*)
   if (!per_elem && !no_plane && (long)P * Q * 5 <= PLANE_LDS) {
     hipLaunchKernelGGL(fm_pool_bwd_plane<T>, dim3(N * C), dim3(256), (size_t)P * Q * 5, st, (const T*)y, (const T*)dy,
                        (const unsigned char*)code, (T*)dx, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, acc);

@@ -224,12 +224,23 @@ __global__ void fm_gemm_splitk_reduce4(GemmP p) {
   }
 }
 
+}  // namespace
+
+// split-K reduce off the critical path (gemm_async.hip)
+extern "C" void fm_gemm_join(hipStream_t s);
+extern "C" hipStream_t fm_gemm_async_fork(hipStream_t s);
+extern "C" void fm_gemm_async_forked(hipStream_t side);
+
+namespace {
+
 void launch_splitk_reduce(const GemmP& p, hipStream_t stream) {
   const long total = (long)p.M * p.N * p.batch;
   const bool v4 = p.c_fp32 && (p.N % 4 == 0) && (p.ldc % 4 == 0) && (p.sC % 4 == 0) &&
                   ((((uintptr_t)p.C) & 15) == 0);
-  if (v4) hipLaunchKernelGGL(fm_gemm_splitk_reduce4, dim3(fm_grid(total / 4)), dim3(256), 0, stream, p);
-  else hipLaunchKernelGGL(fm_gemm_splitk_reduce, dim3(fm_grid(total)), dim3(256), 0, stream, p);
+  hipStream_t rs = fm_gemm_async_fork(stream);
+  if (v4) hipLaunchKernelGGL(fm_gemm_splitk_reduce4, dim3(fm_grid(total / 4)), dim3(256), 0, rs, p);
+  else hipLaunchKernelGGL(fm_gemm_splitk_reduce, dim3(fm_grid(total)), dim3(256), 0, rs, p);
+  if (rs != stream) fm_gemm_async_forked(rs);
 }
 
 __global__ void fm_gemm_splitk_reduce(GemmP p) {
@@ -342,6 +353,7 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
                        const void* act_y, long lday, int bwd_act, float* colsum, float* rowsum_a,
                        hipStream_t stream) {
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
+  if (beta) fm_gemm_join(stream);      // C may be a gradient an async reduce is still writing
   GemmP p;
   p.A = (const unsigned short*)A; p.lda = lda; p.sA = sA;
   p.B = (const unsigned short*)B; p.ldb = ldb; p.sB = sB;
@@ -392,6 +404,7 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
     if (ks > 1 && !atomic_ok && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks = 1;
     p.ksplit = ks;
     p.atomic_c = ks > 1 && atomic_ok;
+    if (ks > 1) fm_gemm_join(stream);  // the slab workspace is shared
     if (p.ksplit > 1 && !p.atomic_c) p.tile_cnt = split_counters(stream, tiles, (long)M * N * 4);
     fm_gemm_glds_launch(&p, bm, 128, a_kcontig, b_kcontig, (g_gemm_variant & 8) ? 1 : 0, (g_gemm_variant & 64) ? 1 : 0,
                         stream);
@@ -440,6 +453,7 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
     p.ksplit = 1;
   }
   p.atomic_c = p.ksplit > 1 && atomic_ok;
+  if (p.ksplit > 1) fm_gemm_join(stream);
   if (p.ksplit > 1 && !p.atomic_c) p.tile_cnt = split_counters(stream, tiles, (long)M * N * 4);
   if (BNv == 128) launch_bm<128, 128>(p, a_kcontig, b_kcontig, vec, stream);
   else if (BMv == 128) launch_bm<128, 64>(p, a_kcontig, b_kcontig, vec, stream);

@@ -423,6 +423,21 @@ __global__ void fm_gemm_f32_reduce(GemmF p, int v4) {
   }
 }
 
+}  // namespace
+
+// split-K reduce off the critical path (gemm_async.hip)
+extern "C" void fm_gemm_join(hipStream_t s);
+extern "C" hipStream_t fm_gemm_async_fork(hipStream_t s);
+extern "C" void fm_gemm_async_forked(hipStream_t side);
+
+namespace {
+
+void launch_reduce_f32(const GemmF& p, int v4, long total, hipStream_t stream) {
+  hipStream_t rs = fm_gemm_async_fork(stream);
+  hipLaunchKernelGGL(fm_gemm_f32_reduce, dim3(fm_grid(total)), dim3(256), 0, rs, p, v4);
+  if (rs != stream) fm_gemm_async_forked(rs);
+}
+
 template <int BM, int BN, bool AK, bool BKC, bool VEC>
 void launch_f(const GemmF& p, hipStream_t s, int opt) {
   constexpr int LDS = 2 * (BM + BN) * BKF * 4;
@@ -1000,6 +1015,7 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
                            float alpha, int beta, int act, float* ws, long ws_bytes, int ksplit_req, const float* act_y,
                            long lday, int bwd_act, float* colsum, float* rowsum_a, hipStream_t stream) {
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
+  if (beta) fm_gemm_join(stream);      // C may be a gradient an async reduce is still writing
   GemmF p;
   p.A = A; p.lda = lda; p.sA = sA;
   p.B = B; p.ldb = ldb; p.sB = sB;
@@ -1034,11 +1050,12 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
     if (ks > 1 && !atomic_ok && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks = 1;
     p.ksplit = ks;
     p.atomic = (ks > 1 && atomic_ok) ? 1 : 0;
+    if (ks > 1) fm_gemm_join(stream);  // the slab workspace is shared
     launch_x_cfg((variant - 1000) % 100, p, a_kcontig, b_kcontig, stream);
     if (ks > 1 && !p.atomic) {
       const int v4 = (N % 4 == 0) && (ldc % 4 == 0) && (sC % 4 == 0) && al(C);
       const long total = (long)M * N * batch / (v4 ? 4 : 1);
-      hipLaunchKernelGGL(fm_gemm_f32_reduce, dim3(fm_grid(total)), dim3(256), 0, stream, p, v4);
+      launch_reduce_f32(p, v4, total, stream);
     }
     return ks;
   }
@@ -1060,6 +1077,7 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
     if (act_y != nullptr || colsum != nullptr) ks = 1;
     if (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks = 1;
     p.ksplit = ks;
+    if (ks > 1) fm_gemm_join(stream);
     if (big) {
       if (variant & 2) launch_f_glds<256, 128, 2, 2>(p, a_kcontig, b_kcontig, stream);
       else launch_f_glds<256, 128, 4, 2>(p, a_kcontig, b_kcontig, stream);
@@ -1069,7 +1087,7 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
     if (ks > 1) {
       const int v4 = (N % 4 == 0) && (ldc % 4 == 0) && (sC % 4 == 0) && al(C);
       const long total = (long)M * N * batch / (v4 ? 4 : 1);
-      hipLaunchKernelGGL(fm_gemm_f32_reduce, dim3(fm_grid(total)), dim3(256), 0, stream, p, v4);
+      launch_reduce_f32(p, v4, total, stream);
     }
     return ks;
   }
@@ -1098,6 +1116,7 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
   if (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks = 1;
   if (K <= 0) ks = 1;
   p.ksplit = ks;
+  if (ks > 1) fm_gemm_join(stream);
   const int opt = (variant >> 2) & 63;
   if (vec && BMv == 256) launch_fbm<256, 128>(p, a_kcontig, b_kcontig, vec, stream, opt);
   else if (BNv == 128) launch_fbm<128, 128>(p, a_kcontig, b_kcontig, vec, stream, opt);
@@ -1106,7 +1125,7 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
   if (ks > 1) {
     const int v4 = (N % 4 == 0) && (ldc % 4 == 0) && (sC % 4 == 0) && al(C);
     const long total = (long)M * N * batch / (v4 ? 4 : 1);
-    hipLaunchKernelGGL(fm_gemm_f32_reduce, dim3(fm_grid(total)), dim3(256), 0, stream, p, v4);
+    launch_reduce_f32(p, v4, total, stream);
   }
   return ks;
 }

@@ -2,6 +2,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <cmath>
 #include <limits>
 
@@ -54,6 +55,7 @@ Candidate to_cand(const py::dict& d, int ndev) {
   if (d.contains("mem")) c.mem = d["mem"].cast<std::vector<std::pair<int, double>>>();
   if (d.contains("upd")) c.upd_us = d["upd"].cast<std::vector<std::pair<int, double>>>();
   if (d.contains("label")) c.label = d["label"].cast<std::string>();
+  if (d.contains("sample_only")) c.sample_only = d["sample_only"].cast<bool>();
   return c;
 }
 
@@ -73,6 +75,8 @@ Machine to_machine(const py::dict& d) {
   get("hbm_bytes", m.hbm_bytes);
   get("bucket_bytes", m.bucket_bytes);
   if (d.contains("overlap")) m.overlap = d["overlap"].cast<bool>();
+  if (d.contains("xchg_chunks")) m.xchg_chunks = std::max(1, d["xchg_chunks"].cast<int>());
+  get("chunk_us", m.chunk_us);
   if (m.ndev < 1 || m.gpus_per_node < 1) throw std::runtime_error("bad machine");
   return m;
 }
@@ -93,9 +97,10 @@ void register_sim(py::module_& m) {
            })
       .def("add_op",
            [](Simulator& s, const std::string& name, const std::vector<int>& in_t, const std::vector<int>& out_t,
-              const py::list& cands, int ndev) {
+              const py::list& cands, int ndev, bool rowwise) {
              OpD op;
              op.name = name;
+             op.rowwise = rowwise;
              op.in_t = in_t;
              op.out_t = out_t;
              for (auto c : cands) {
@@ -105,7 +110,8 @@ void register_sim(py::module_& m) {
              }
              if (op.cands.empty()) throw std::runtime_error("op without candidates: " + name);
              return s.add_op(std::move(op));
-           })
+           },
+           py::arg("name"), py::arg("in_t"), py::arg("out_t"), py::arg("cands"), py::arg("ndev"), py::arg("rowwise") = false)
       .def("num_ops", &Simulator::num_ops)
       .def("num_cands", [](const Simulator& s, int i) { return (int)s.op(i).cands.size(); })
       .def("simulate",

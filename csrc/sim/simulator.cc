@@ -25,6 +25,7 @@ bool intersect(const Box& a, const Box& b, Box* out) {
 
 int Simulator::add_op(OpD op) {
   int idx = (int)ops_.size();
+  op.edge0 = (int)edges_.size();
   for (int j = 0; j < (int)op.in_t.size(); ++j) {
     int t = op.in_t[j];
     if ((int)consumers_.size() <= t) consumers_.resize(t + 1);
@@ -104,6 +105,29 @@ std::vector<double> Simulator::memory(const std::vector<int>& assign) const {
   return mem;
 }
 
+std::vector<int> Simulator::chunks(const std::vector<int>& assign) {
+  const int nops = (int)ops_.size();
+  std::vector<int> nch(nops, 1);
+  const int K = m_.xchg_chunks;
+  if (K <= 1 || m_.ndev <= 1) return nch;
+  // the tail: the longest suffix of row-wise ops on sample-split candidates
+  int s = nops;
+  while (s > 0 && ops_[s - 1].rowwise && ops_[s - 1].cands[assign[s - 1]].sample_only) --s;
+  // it is pipelined from the last of its ops fed across devices by an op before the tail (the
+  // executor chunks the LAST cross-device exchange of the forward and everything after it)
+  int r = -1;
+  for (int i = s; i < nops; ++i)
+    for (int j = 0; j < (int)ops_[i].in_t.size(); ++j) {
+      const TensorD& t = tensors_[ops_[i].in_t[j]];
+      if (t.producer < 0 || t.producer >= s) continue;
+      for (const Xfer& x : transfers(ops_[i].edge0 + j, assign[t.producer], assign[i]))
+        if (x.src_dev != x.dst_dev && x.bytes > 0) r = i;
+    }
+  if (r < 0) return nch;
+  for (int i = r; i < nops; ++i) nch[i] = K;
+  return nch;
+}
+
 namespace {
 struct Task {
   double dur = 0, ready = 0;
@@ -143,44 +167,94 @@ double Simulator::simulate(const std::vector<int>& assign, std::vector<TraceEven
     tasks[b].npred++;
   };
   const int nops = (int)ops_.size();
-  std::vector<std::vector<int>> fwd(nops), bwd(nops);
+  const std::vector<int> nch = chunks(assign);
+  // fwd[i][p][k] / bwd[i][p][k]: task of part p, micro-batch chunk k (one chunk outside the tail)
+  std::vector<std::vector<std::vector<int>>> fwd(nops), bwd(nops);
   for (int i = 0; i < nops; ++i) {
     const Candidate& c = ops_[i].cands[assign[i]];
-    int np = (int)c.part_dev.size();
-    fwd[i].resize(np);
-    bwd[i].resize(np);
-    for (int p = 0; p < np; ++p) {
-      fwd[i][p] = new_task(0, c.fwd_us[p], c.part_dev[p], i, p);
-      bwd[i][p] = new_task(1, c.bwd_us[p], c.part_dev[p], i, p);
-      dep(fwd[i][p], bwd[i][p]);
+    const int np = (int)c.part_dev.size(), K = nch[i];
+    const double ov = K > 1 ? m_.chunk_us : 0.0;
+    fwd[i].assign(np, std::vector<int>(K));
+    bwd[i].assign(np, std::vector<int>(K));
+    for (int p = 0; p < np; ++p)
+      for (int k = 0; k < K; ++k) {
+        fwd[i][p][k] = new_task(0, c.fwd_us[p] / K + ov, c.part_dev[p], i, p);
+        bwd[i][p][k] = new_task(1, c.bwd_us[p] / K + 2.0 * ov, c.part_dev[p], i, p);
+        dep(fwd[i][p][k], bwd[i][p][k]);
+      }
+    if (K > 1 && i == nops - 1)   // the loss runs on the whole batch: every chunk's forward first
+      for (int p = 0; p < np; ++p)
+        for (int k = 0; k < K; ++k)
+          for (int kk = 0; kk < K; ++kk)
+            if (kk != k) dep(fwd[i][p][kk], bwd[i][p][k]);
+  }
+  // producer -> consumer data movement (forward) and gradient return (backward).  All inputs of
+  // one consumer move in ONE fused exchange (the executor's FusedExchange: one all-to-all per
+  // reshard step), so the transfers of a consumer part are merged per directed link -- one
+  // latency per link, after the last producer.  Inside the tail chunk k feeds chunk k; into the
+  // tail the exchange is split per consumer chunk.
+  struct Merged {
+    double bytes = 0;
+    std::vector<int> pf, pb;
+  };
+  for (int i = 0; i < nops; ++i) {
+    const int kc = nch[i];
+    std::map<std::tuple<int, int, int, int>, Merged> links;   // (cons part, chunk, src, dst)
+    for (int j = 0; j < (int)ops_[i].in_t.size(); ++j) {
+      const int e = ops_[i].edge0 + j;
+      const TensorD& t = tensors_[edges_[e].tensor];
+      if (t.producer < 0) continue;
+      const int kp = nch[t.producer];
+      for (const Xfer& x : transfers(e, assign[t.producer], assign[i])) {
+        const bool local = x.src_dev == x.dst_dev || x.bytes <= 0;
+        for (int k = 0; k < kc; ++k) {
+          // producer tasks chunk k depends on: the aligned chunk, or all of them
+          std::vector<int> pf, pb;
+          if (x.prod_part >= 0) {
+            const auto& F = fwd[t.producer][x.prod_part];
+            const auto& B = bwd[t.producer][x.prod_part];
+            if (kp == kc) {
+              pf.push_back(F[k]);
+              pb.push_back(B[k]);
+            } else if (kp == 1) {
+              pf.push_back(F[0]);
+              pb.push_back(B[0]);
+            } else {
+              pf = F;
+              pb = B;
+            }
+          }
+          if (local) {
+            for (int f : pf) dep(f, fwd[i][x.cons_part][k]);
+            if (t.needs_grad)
+              for (int q : pb) dep(bwd[i][x.cons_part][k], q);
+            continue;
+          }
+          Merged& mg = links[{x.cons_part, k, x.src_dev, x.dst_dev}];
+          mg.bytes += kp == kc || kp == 1 ? x.bytes / kc : x.bytes;
+          mg.pf.insert(mg.pf.end(), pf.begin(), pf.end());
+          if (t.needs_grad) mg.pb.insert(mg.pb.end(), pb.begin(), pb.end());
+        }
+      }
+    }
+    for (auto& kv : links) {
+      const auto [cp, k, sd, dd] = kv.first;
+      Merged& mg = kv.second;
+      int cf = new_task(2, xfer_us(sd, dd, mg.bytes), link_res(sd, dd), i, cp);
+      std::sort(mg.pf.begin(), mg.pf.end());
+      mg.pf.erase(std::unique(mg.pf.begin(), mg.pf.end()), mg.pf.end());
+      for (int f : mg.pf) dep(f, cf);
+      dep(cf, fwd[i][cp][k]);
+      if (!mg.pb.empty()) {
+        int cb = new_task(2, xfer_us(dd, sd, mg.bytes), link_res(dd, sd), i, cp);
+        dep(bwd[i][cp][k], cb);
+        std::sort(mg.pb.begin(), mg.pb.end());
+        mg.pb.erase(std::unique(mg.pb.begin(), mg.pb.end()), mg.pb.end());
+        for (int q : mg.pb) dep(cb, q);
+      }
     }
   }
-  // producer -> consumer data movement (forward) and gradient return (backward)
-  for (int e = 0; e < (int)edges_.size(); ++e) {
-    const Edge& ed = edges_[e];
-    const TensorD& t = tensors_[ed.tensor];
-    if (t.producer < 0) continue;
-    const auto& xs = transfers(e, assign[t.producer], assign[ed.op]);
-    for (const Xfer& x : xs) {
-      int ft = fwd[ed.op][x.cons_part];
-      int bt = bwd[ed.op][x.cons_part];
-      int pf = x.prod_part >= 0 ? fwd[t.producer][x.prod_part] : -1;
-      int pb = x.prod_part >= 0 ? bwd[t.producer][x.prod_part] : -1;
-      if (x.src_dev == x.dst_dev || x.bytes <= 0) {
-        if (pf >= 0) dep(pf, ft);
-        if (pb >= 0 && t.needs_grad) dep(bt, pb);
-        continue;
-      }
-      int cf = new_task(2, xfer_us(x.src_dev, x.dst_dev, x.bytes), link_res(x.src_dev, x.dst_dev), ed.op, x.cons_part);
-      if (pf >= 0) dep(pf, cf);
-      dep(cf, ft);
-      if (t.needs_grad && pb >= 0) {
-        int cb = new_task(2, xfer_us(x.dst_dev, x.src_dev, x.bytes), link_res(x.dst_dev, x.src_dev), ed.op, x.cons_part);
-        dep(bt, cb);
-        dep(cb, pb);
-      }
-    }
-  }
+
   // parameter synchronisation + optimizer update
   std::vector<int> upd(nd, -1);
   std::vector<double> upd_us(nd, 0.0);
@@ -190,13 +264,15 @@ double Simulator::simulate(const std::vector<int>& assign, std::vector<TraceEven
   for (int d = 0; d < nd; ++d) upd[d] = new_task(4, upd_us[d], d, -1, d);
   for (int i = 0; i < nops; ++i) {
     const Candidate& c = ops_[i].cands[assign[i]];
-    for (int p = 0; p < (int)c.part_dev.size(); ++p) dep(bwd[i][p], upd[c.part_dev[p]]);
+    for (int p = 0; p < (int)c.part_dev.size(); ++p)
+      for (int b : bwd[i][p]) dep(b, upd[c.part_dev[p]]);
   }
   int barrier = -1;
   if (!m_.overlap) {
     barrier = new_task(5, 0.0, -1, -1, -1);
     for (int i = 0; i < nops; ++i)
-      for (int b : bwd[i]) dep(b, barrier);
+      for (auto& bp : bwd[i])
+        for (int b : bp) dep(b, barrier);
   }
   struct Bucket {
     double bytes = 0;
@@ -226,7 +302,8 @@ double Simulator::simulate(const std::vector<int>& assign, std::vector<TraceEven
       b.bytes += ws.bytes;
       b.last_op = i;
       for (int p = 0; p < (int)c.part_dev.size(); ++p)
-        if (std::binary_search(grp.begin(), grp.end(), c.part_dev[p])) b.preds.push_back(bwd[i][p]);
+        if (std::binary_search(grp.begin(), grp.end(), c.part_dev[p]))
+          b.preds.insert(b.preds.end(), bwd[i][p].begin(), bwd[i][p].end());
       if (b.bytes >= m_.bucket_bytes) flush(grp, b);
     }
   }

@@ -61,6 +61,8 @@ struct Candidate {
   std::vector<std::pair<int, double>> mem;     // (device, bytes)
   std::vector<std::pair<int, double>> upd_us;  // (device, optimizer update time)
   std::string label;                     // for traces / debugging
+  // one-holder sample split over every device (dim 0 only): may run as micro-batch chunks
+  bool sample_only = false;
 };
 
 struct TensorD {
@@ -74,6 +76,8 @@ struct OpD {
   std::string name;
   std::vector<int> in_t, out_t;
   std::vector<Candidate> cands;
+  bool rowwise = false;   // every output row depends on the same input rows only (Linear, interaction, concat)
+  int edge0 = 0;          // index of the edge of input 0
 };
 
 struct Machine {
@@ -88,6 +92,11 @@ struct Machine {
   double hbm_bytes = 288e9 * 0.92;
   double bucket_bytes = 32.0 * (1 << 20);
   bool overlap = true;             // gradient sync overlapped with backward (else BSP barrier)
+  // micro-batch pipelining of the last exchange into a sample-split row-wise tail (executor:
+  // FLEXMI_XCHG_CHUNKS): the tail's tasks and its inbound / gradient transfers split in this
+  // many chunks, each chunk op paying chunk_us of extra kernel boundaries
+  int xchg_chunks = 1;
+  double chunk_us = 1.6;
 };
 
 struct TraceEvent {
@@ -132,6 +141,7 @@ class Simulator {
     int op, input, tensor;
   };
   const std::vector<Xfer>& transfers(int edge, int pc, int cc);
+  std::vector<int> chunks(const std::vector<int>& assign);   // micro-batch chunks per op
   double xfer_us(int s, int d, double bytes) const;
   double allreduce_us(const std::vector<int>& group, double bytes) const;
   int link_res(int s, int d) const { return 2 * m_.ndev + s * m_.ndev + d; }

@@ -58,13 +58,28 @@ GEMM_WS_BYTES = 64 << 20
 
 
 def gemm(A, lda, a_kcontig, B, ldb, b_kcontig, Cout, ldc, M, N, K, bias=None, act=10, beta=False, alpha=1.0,
-         batch=1, sA=0, sB=0, sC=0, ksplit=0, use_ws=True, act_y=None, bwd_act=10, colsum=None, rowsum_a=None):
+         batch=1, sA=0, sB=0, sC=0, ksplit=0, use_ws=True, act_y=None, bwd_act=10, colsum=None, rowsum_a=None,
+         async_reduce=False):
     """C = epi(A·B).  Optional fused backward epilogue of the layer below (act_y/bwd_act/colsum):
-    C = act'(act_y) * (A·B) and colsum += column sums of C (its bias gradient)."""
+    C = act'(act_y) * (A·B) and colsum += column sums of C (its bias gradient).  async_reduce: a
+    split-K reduce may run on a side stream (csrc/kernels/gemm_async.hip) -- the caller must
+    gemm_join() before anything reads Cout."""
     ws = workspace(Cout.device, GEMM_WS_BYTES) if use_ws else None
     lday = act_y.stride(0) if act_y is not None else 0
     return C().gemm(A, lda, sA, a_kcontig, B, ldb, sB, b_kcontig, Cout, ldc, sC, bias, M, N, K, batch, alpha, beta, act,
-                    ws, ksplit, act_y, lday, bwd_act, colsum, rowsum_a)
+                    ws, ksplit, act_y, lday, bwd_act, colsum, rowsum_a, bool(async_reduce))
+
+
+# FM_GEMM_ASYNC_REDUCE=1: the executor's dW GEMMs run their split-K reduce on a side stream.
+# OPT-IN: measured SLOWER on the DLRM MLPerf step (fp32 1.52-1.54 vs 1.47-1.48 ms, bf16 0.70-0.72
+# vs 0.63 ms, profiles/bench_ab_async_reduce_r3h.txt): in the captured graph the reduce still ran
+# before the next GEMM, and the cross-stream edges added gaps
+ASYNC_DW = os.environ.get("FM_GEMM_ASYNC_REDUCE", "0") == "1"
+
+
+def gemm_join():
+    """Current stream waits for a pending side-stream split-K reduce (no-op when none)."""
+    C().gemm_join()
 
 
 # ------------------------------------------------------------------ init
@@ -100,11 +115,13 @@ DX_LIB = os.environ.get("FM_DX_LIB", "0") == "1"
 DX_LIB_MIN = int(os.environ.get("FM_DX_LIB_MIN", str(1 << 32)))
 
 
-def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=False, fuse_below=None, phase="all"):
+def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=False, fuse_below=None, phase="all",
+                    async_dw=False):
     """Weight/bias grads ACCUMULATE into dw/db (the executor zeroes the flat gradient buffer once
     per step).  grad_is_dpre: dy2 already holds act'(y)*dy (written by the consumer's fused dX
     epilogue).  fuse_below = (y_below, act_below): apply the activation backward of the layer
-    below in this layer's dX GEMM epilogue."""
+    below in this layer's dX GEMM epilogue.  async_dw: the dW GEMM's split-K reduce may run on a
+    side stream, overlapping the dX GEMM (the caller joins with gemm_join() before dw is read)."""
     M, K = x2.shape
     N = w.shape[0]
     vec = 4 if x2.dtype == torch.float32 else 8
@@ -132,7 +149,8 @@ def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=F
     # used by several ops sum their gradients, and split-K partials of small dW tiles can be added
     # with atomics straight into dw (no slab / reduce launch)
     if phase != "dx":
-        gemm(dpre, dpre.stride(0), False, x2, x2.stride(0), False, dw, K, N, K, M, beta=True, rowsum_a=db)
+        gemm(dpre, dpre.stride(0), False, x2, x2.stride(0), False, dw, K, N, K, M, beta=True, rowsum_a=db,
+             async_reduce=async_dw and ASYNC_DW)
     if phase == "dw":
         return
     # dX[M,K] = dpre W   (+ fused activation backward of the layer below)

@@ -140,15 +140,42 @@ class CostModel:
         byt = sum(_prod(s) for s in list(in_shapes) + list(out_shapes)) * eb
         return L + self._bytes_us(byt), L + self._bytes_us(2 * byt)
 
+    @staticmethod
+    def kernels(op):
+        """(forward, backward) kernel launches of one op shard in a captured step (grouped
+        embedding tables share one launch per group: a quarter each)."""
+        t = op.op_type
+        if getattr(op, "is_view", False) or t in (OperatorType.OP_FLAT, OperatorType.OP_RESHAPE):
+            return 0.0, 0.0
+        if t == OperatorType.OP_LINEAR:
+            return 1.0, 2.0 if op.inputs[0].owner_op is None else 3.0
+        if t == OperatorType.OP_EMBEDDING:
+            return 0.25, 0.25
+        if t in (OperatorType.OP_CONV2D,):
+            return 1.0, 3.0
+        if t == OperatorType.OP_BATCHMATMUL:
+            return 1.0, 2.0
+        return 1.0, 1.0
+
     def op_cost(self, op, in_shapes, out_shapes):
+        """Measured (DB hit) or scaled roofline time of one shard.  A roofline miss scales only
+        its work terms by the fitted measured/roofline ratio, not its kernel boundaries, and no
+        launch runs shorter than the machine's kernel floor: the small-batch configs are
+        launch-bound (criteo_kaggle projected -57 % before)."""
         key = op_signature(op, in_shapes, out_shapes)
         hit = self.db.get(key)
+        nkf, nkb = self.kernels(op)
+        floor = getattr(self.m, "kernel_floor_us", 0.0)
         if hit is not None:
             gf = self.group_factor.get(op.op_type.name, 1.0)
-            return hit[0] * gf, hit[1] * gf
+            return max(hit[0] * gf, nkf * floor), max(hit[1] * gf, nkb * floor)
         f, b = self.roofline(op, in_shapes, out_shapes)
         s = self.scale.get(op.op_type.name, 1.0)
-        return f * s, b * s
+        L = self.m.launch_us
+        ff, fb = min(f, nkf * L), min(b, nkb * L)
+        f = ff + s * (f - ff)
+        b = fb + s * (b - fb)
+        return max(f, nkf * floor), max(b, nkb * floor)
 
     def update_us(self, dense_param_bytes_fp32, nstates):
         """Fused optimizer update over a device's dense parameters (read master+grad+states,

@@ -256,6 +256,24 @@ class ReshardPlan:
                 out[(t.src, t.dst)] = out.get((t.src, t.dst), 0) + box_volume(t.box) * elem_size
         return out
 
+    def clip_rows(self, side, rows):
+        """The part of this plan that moves one micro-batch chunk: every transfer's dim-0 extent
+        clipped to ``rows(lo, hi) -> (a, b)``, the chunk's global rows inside the [lo, hi) rows
+        held by the transfer's destination (``side="dst"``: a forward exchange into a sample
+        split) or source (``side="src"``: the gradient return out of one).  Transfers outside the
+        chunk are dropped; the chunks of 0..K-1 partition the plan."""
+        lay = self.dst if side == "dst" else self.src
+        out = ReshardPlan.__new__(ReshardPlan)
+        out.src, out.dst, out.reduce = self.src, self.dst, self.reduce
+        out.transfers = []
+        for t in self.transfers:
+            lo, hi = lay.local_box(t.dst if side == "dst" else t.src)[0]
+            a, b = rows(lo, hi)
+            x0, x1 = max(a, t.box[0][0]), min(b, t.box[0][1])
+            if x0 < x1:
+                out.transfers.append(Transfer(t.src, t.dst, ((x0, x1),) + tuple(t.box[1:]), t.src_part, t.dst_part))
+        return out
+
     def sends_of(self, rank):
         return [t for t in self.transfers if t.src == rank]
 

@@ -39,9 +39,17 @@ class MachineModel:
     mfma_eff: float = 0.22          # achieved/peak on DLRM-sized GEMMs (profiles/: 240-560 TF)
     hbm_eff: float = 0.75
     launch_us: float = 1.6          # kernel boundary inside a hipGraph replay
+    # shortest launch inside a replayed step: small-batch layers are launch-bound, not roofline-bound.
+    # 4.0 puts the 1-GPU projections of run_random / criteo_kaggle (batch 256) at +5 % / -20 % of
+    # the measured steps, from -13 % / -57 % without it (tools/soap_report.py, profiles/soap_vs_dp_fp32.txt)
+    kernel_floor_us: float = 4.0
     atomic_TBps: float = 1.3        # chip-wide fp32 atomic add rate (MI355X_MICROARCH.md)
     bucket_mb: float = 32.0
     overlap: bool = True
+    # micro-batch pipelining of the exchange into the sample-split tail (executor
+    # FLEXMI_XCHG_CHUNKS); 0 = the executor's auto rule for the model's per-GPU batch
+    xchg_chunks: int = 0
+    chunk_us: float = 1.6           # extra kernel boundaries per chunk and op
 
     @staticmethod
     def mi355x(ndev=8, **kw):
@@ -67,4 +75,5 @@ class MachineModel:
         return {"ndev": self.ndev, "gpus_per_node": self.gpus_per_node, "link_GBps": self.link_GBps,
                 "link_lat_us": self.link_lat_us, "nic_GBps": self.nic_GBps, "nic_lat_us": self.nic_lat_us,
                 "ar_busbw_GBps": self.ar_busbw_GBps, "ar_lat_us": self.ar_lat_us, "hbm_bytes": self.hbm_bytes,
-                "bucket_bytes": self.bucket_mb * (1 << 20), "overlap": self.overlap}
+                "bucket_bytes": self.bucket_mb * (1 << 20), "overlap": self.overlap,
+                "xchg_chunks": int(self.xchg_chunks), "chunk_us": self.chunk_us}

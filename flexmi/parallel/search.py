@@ -112,6 +112,20 @@ class SearchResult:
                 "seconds": self.seconds}
 
 
+def _rowwise(op):
+    """Ops the executor runs as micro-batch chunks in a pipelined tail (Executor._plan_pipeline)."""
+    return op.op_type in (OperatorType.OP_LINEAR, OperatorType.OP_DOT_INTERACTION) or (
+        op.op_type == OperatorType.OP_CONCAT and op.axis != 0)
+
+
+def auto_chunks(rows_per_gpu):
+    """The executor's chunk count for a per-GPU batch (FLEXMI_XCHG_CHUNKS, default auto)."""
+    from flexmi.runtime import executor as E
+    if E.XCHG_CHUNKS != "auto":
+        return max(1, int(E.XCHG_CHUNKS))
+    return 2 if rows_per_gpu >= 1024 else 1
+
+
 class SimGraph:
     """The model compiled into the native simulator's candidate tables."""
 
@@ -127,7 +141,11 @@ class SimGraph:
         self.nstates = len(opt.state_names()) if opt is not None and hasattr(opt, "state_names") else 0
         self.sparse_ok = bool(getattr(opt, "sparse_capable", False))
         self.ops = list(model.layers)
-        self.sim = _native.Simulator(self.machine.native_dict())
+        md = self.machine.native_dict()
+        if not md["xchg_chunks"]:
+            md["xchg_chunks"] = auto_chunks(model.config.batchSize // max(1, ndev))
+        self.xchg_chunks = md["xchg_chunks"]
+        self.sim = _native.Simulator(md)
         self.cands: List[List[ParallelConfig]] = []
         tid = {}
         for op in self.ops:
@@ -147,7 +165,7 @@ class SimGraph:
                     cl.append(pc)
             self.cands.append(cl)
             self.sim.add_op(op.name, [tid[t.guid] for t in op.inputs], [tid[o.guid] for o in op.outputs],
-                            [self._cand(op, pc) for pc in cl], ndev)
+                            [self._cand(op, pc) for pc in cl], ndev, _rowwise(op))
 
     def _eb(self, t):
         return self.cost.eb if t.data_type in _FLOAT else 8
@@ -201,7 +219,10 @@ class SimGraph:
                     else:
                         mem[d] = mem.get(d, 0.0) + vol * (4.0 + 4.0 + 2.0 + 4.0 * self.nstates)
                         upd_bytes[d] = upd_bytes.get(d, 0.0) + vol * 4.0
-        return {"part_dev": list(pc.device_ids), "fwd_us": fwd, "bwd_us": bwd,
+        W = self.ndev
+        sample_only = (list(pc.device_ids) == list(range(W)) and all(
+            l.degrees[0] == W and all(d == 1 for d in l.degrees[1:]) and l.replication() == 1 for l in outs + ins))
+        return {"sample_only": sample_only, "part_dev": list(pc.device_ids), "fwd_us": fwd, "bwd_us": bwd,
                 "out": [_lay_parts(l) for l in outs], "inp": [_lay_parts(l) for l in ins],
                 "wsync": wsync, "mem": sorted(mem.items()),
                 "upd": sorted((d, self.cost.update_us(b, self.nstates)) for d, b in upd_bytes.items()),

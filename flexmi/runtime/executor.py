@@ -168,6 +168,26 @@ OVERLAP_EMB = os.environ.get("FM_OVERLAP_EMB", "auto")
 P2P_MODE = os.environ.get("FM_P2P", "auto")
 
 
+# FLEXMI_XCHG_CHUNKS=K / auto (default auto: 2 when every rank holds >= 1024 samples): micro-batch
+# pipelining of the last cross-device exchange of the forward when everything after it is a
+# sample-split row-wise tail (DLRM: embedding all-to-all -> interaction -> top MLP).  The exchange
+# is split into K all-to-alls over row chunks of the destination's samples; chunk c's tail
+# forward runs as soon as chunk c has landed, overlapping the all-to-all of chunk c+1.  Backward
+# mirrors it: the tail's input-gradient passes run per chunk and each chunk's gradient
+# all-to-all starts right after, overlapping the next chunk; the tail's weight gradients run on
+# the whole batch afterwards (overlapping the last chunk).  Reference: the DLRM strategy moves
+# every embedding output in one exchange (src/runtime/dlrm_strategy.cc:252-263).
+XCHG_CHUNKS = os.environ.get("FLEXMI_XCHG_CHUNKS", "auto")
+# test hook: chunk the row-wise tail at world 1 too (no exchange; exercises the chunked kernels)
+XCHG_LOCAL = os.environ.get("FLEXMI_XCHG_CHUNKS_LOCAL") == "1"
+PIPE_ROW_ALIGN = 8          # chunk boundaries on 8-row multiples: 16-B aligned rows for the kernels
+
+
+def chunk_bounds(n, k):
+    """Row boundaries of k micro-batch chunks of n local rows (boundaries on 8-row multiples)."""
+    return [0] + [(n * c // k) // PIPE_ROW_ALIGN * PIPE_ROW_ALIGN for c in range(1, k)] + [n]
+
+
 def overlap_embeddings_enabled(ex):
     """Whether captured steps of executor ``ex`` run the fused embedding groups on a second HIP
     stream (``OVERLAP_EMB``: "1" / "0" / "auto" = on when an embedding table is >= 128 wide)."""
@@ -475,6 +495,7 @@ class FusedExchange:
         self.send_off = [sum(send[:p]) for p in range(world)]
         self.recv_off = [sum(recv[:p]) for p in range(world)]
         self.work = None
+        self.tag = None            # program item name prefix (micro-batch chunk exchanges)
         self._plan_descriptors()
 
     def _plan_descriptors(self):
@@ -890,6 +911,14 @@ class Executor:
             self.ctx[op.guid] = c
         self._build_groups(ops)
         self._build_epilogue_fusion(ops)
+        if self.backend == "hip":
+            # dW split-K reduces on a side stream (csrc/kernels/gemm_async.hip), joined before
+            # every collective and at the end of the backward program (_with_gemm_joins)
+            from flexmi.core.types import OperatorType
+            for op in ops:
+                c = self.ctx.get(op.guid)
+                if c is not None and op.op_type == OperatorType.OP_LINEAR:
+                    c.saved["async_dw"] = True
         self.adam_state = torch.tensor([1.0, 1.0, 0.0], dtype=torch.float32, device=self.device)
         self._compile_program()
 
@@ -1259,6 +1288,144 @@ class Executor:
     # HIP work on the current stream (capturable), "comm" items call RCCL.  Eager execution runs
     # the items in order; graph mode captures every maximal run of compute items into one
     # hipGraph and runs the collectives eagerly between replays (segmented capture).
+    # ------------------------------------------------------------ micro-batch pipeline
+    def _plan_pipeline(self):
+        """The chunked tail of XCHG_CHUNKS, or None.  Decided from global layouts only (every rank
+        takes the same decision: the chunk all-to-alls are collectives).  Conditions: the last
+        cross-device forward exchange is followed by ops only; each is a row-wise kind (Linear,
+        DotInteraction, Concat off the sample dim) whose outputs and needed inputs are one-holder sample splits over the
+        whole world with identical per-rank rows; every rank holds >= 8 rows per chunk."""
+        from flexmi.core.types import OperatorType
+        if self.world == 1 and not XCHG_LOCAL:
+            return None
+        steps = self.fwd_steps
+        W = self.world
+
+        def rowwise(op):
+            return op.op_type in (OperatorType.OP_LINEAR, OperatorType.OP_DOT_INTERACTION) or (
+                op.op_type == OperatorType.OP_CONCAT and op.axis != 0)
+
+        xk = [k for k, st in enumerate(steps)
+              if st[0] == "reshard" and not all(rs.local_only for *_, rs in st[1])]
+        if xk:
+            k0 = xk[-1]
+        elif XCHG_LOCAL:
+            k0 = len(steps) - 1       # the longest row-wise suffix, after an op step
+            while k0 >= 0 and steps[k0][0] == "op" and rowwise(steps[k0][1]):
+                k0 -= 1
+            if k0 < 0 or steps[k0][0] != "op":
+                return None
+        else:
+            return None
+        if k0 == len(steps) - 1 or any(st[0] != "op" for st in steps[k0 + 1:]):
+            return None
+        region = [st[1] for st in steps[k0 + 1:]]
+
+        def sample_split(lay):
+            return (not lay.partial and lay.boxes is None and all(d == 1 for d in lay.degrees[1:])
+                    and lay.degrees[0] == W and all(len(h) == 1 for h in lay.holders)
+                    and sorted(h[0] for h in lay.holders) == list(range(W)))
+
+        rows = None
+        for op in region:
+            if not rowwise(op) or getattr(op, "host_exec", False) or op.guid in self.group_of:
+                return None
+            lays = [self.home[o.guid] for o in op.outputs] + [self.need[(op.guid, i)] for i in range(len(op.inputs))]
+            for lay in lays:
+                if not sample_split(lay):
+                    return None
+                ext = tuple(tuple(lay.local_box(r)[0]) for r in range(W))
+                if rows is None:
+                    rows = ext
+                elif ext != rows:
+                    return None
+        nmin = min(hi - lo for lo, hi in rows)
+        K = (2 if nmin >= 1024 else 1) if XCHG_CHUNKS == "auto" else int(XCHG_CHUNKS)
+        if K <= 1 or nmin < PIPE_ROW_ALIGN * K:
+            return None
+        # backward: the tail's ops contiguous in backward order, then the gradient return of
+        # exactly their inputs -- otherwise the backward runs whole-batch (forward still chunked)
+        rset = {op.guid for op in region}
+        bs = self.bwd_steps
+        pos = [k for k, st in enumerate(bs) if st[0] == "op" and st[1].guid in rset]
+        kb = None
+        if pos and pos == list(range(pos[0], pos[0] + len(region))) and [bs[k][1] for k in pos] == list(reversed(region)):
+            nxt = bs[pos[-1] + 1] if pos[-1] + 1 < len(bs) else None
+            if nxt is None or nxt[0] != "reduce":
+                kb = pos[0] if not xk else None          # world-1 test hook: no gradient return
+            elif all(op.guid in rset for op, *_ in nxt[1]):
+                kb = pos[0]
+        lo_r, hi_r = rows[self.rank]
+        b = chunk_bounds(hi_r - lo_r, K)
+        ctx = [{op.guid: self._chunk_ctx(op, b[c], b[c + 1]) for op in region} for c in range(K)]
+        return {"k": k0, "region": region, "K": K, "rows": rows, "kb": kb, "ctx": ctx}
+
+    def _chunk_ctx(self, op, a, b):
+        """Op context of local rows [a, b): row views of the whole-batch buffers (so the chunks'
+        forward fills the same activations the backward reads), shared weights / gradients; a
+        Linear's act-backward scratch is one whole-batch buffer whose row slices the chunks'
+        input-gradient passes fill and the whole-batch weight-gradient pass reads."""
+        import copy
+        from flexmi.core.types import ActiMode, OperatorType
+        c = self.ctx[op.guid]
+        cc = copy.copy(c)
+
+        def rows(t):
+            if t is None:
+                return None
+            return t[a:b]
+
+        cc.inputs = [rows(t) for t in c.inputs]
+        cc.outputs = [rows(t) for t in c.outputs]
+        cc.in_grads = [rows(t) for t in c.in_grads]
+        cc.out_grads = [rows(t) for t in c.out_grads]
+        cc.in_grad_accumulate = list(c.in_grad_accumulate)
+        cc.in_boxes = [None if bx is None else ((bx[0][0] + a, bx[0][0] + b),) + tuple(bx[1:]) for bx in c.in_boxes]
+        cc.out_boxes = [None if bx is None else ((bx[0][0] + a, bx[0][0] + b),) + tuple(bx[1:]) for bx in c.out_boxes]
+        cc.saved = dict(c.saved)
+        fb = c.saved.get("fuse_below")
+        if fb is not None:
+            cc.saved["fuse_below"] = (fb[0][a:b], fb[1])
+        cc.workspace = {}
+        if (op.op_type == OperatorType.OP_LINEAR and c.hip and op.activation != ActiMode.AC_MODE_NONE
+                and not getattr(op, "skip_act_grad", False) and not c.saved.get("grad_is_dpre", False)
+                and c.out_grads and c.out_grads[0] is not None):
+            y = c.outputs[0]
+            inner = y.numel() // max(1, y.shape[0] * y.shape[-1])
+            full = c.workspace.get("dpre")
+            shp = (y.numel() // y.shape[-1], y.shape[-1])
+            if full is None or tuple(full.shape) != shp:
+                full = torch.empty(shp, dtype=c.out_grads[0].dtype, device=y.device)
+                c.workspace["dpre"] = full
+            cc.workspace["dpre"] = full[a * inner: b * inner]
+        return cc
+
+    def _chunk_items(self, items, side, c, pipe):
+        """Reshard items of chunk c: each plan clipped to chunk c of the sample-split side's rows;
+        a partial-sum destination is zeroed by chunk 0 only (later chunks add into it)."""
+        K = pipe["K"]
+
+        def rows(lo, hi):
+            b = chunk_bounds(hi - lo, K)
+            return lo + b[c], lo + b[c + 1]
+
+        out = []
+        for rs, src, dst, acc in items:
+            st = ReshardStep(rs.plan.clip_rows(side, rows), self.rank, self.world, rs.dtype, rs.device)
+            out.append((st, src, dst, acc if c == 0 else (acc or rs.plan.src.partial)))
+        return out
+
+    def _emit_pipelined_fwd(self, fwd, exs, pipe):
+        for c in range(pipe["K"]):
+            if exs:
+                self._emit_exchange_finish(fwd, exs[c], "reshard.fwd")
+            for op in pipe["region"]:
+                cc = pipe["ctx"][c][op.guid]
+                fwd.append(Item("compute", (lambda op=op, cc=cc: self._fwd_op(op, cc)), f"{op.name}.c{c}.fwd"))
+                fwd[-1].reads = {t.guid for t in op.inputs}
+                fwd[-1].writes = {t.guid for t in op.outputs}
+                fwd[-1].check = (lambda op=op, cc=cc: self._check_op(op.name + ".fwd", cc.outputs, "output"))
+
     def _compile_program(self):
         tm = self.timer
         fwd, bwd, upd = [], [], []
@@ -1270,6 +1437,7 @@ class Executor:
         # cross-device reshards are split: pack + asynchronous all_to_all right after the last
         # producer of their sources, wait + unpack right before the consumer -- so the ops in
         # between (e.g. the DLRM bottom MLP) overlap the embedding exchange
+        pipe = self.pipe = self._plan_pipeline()
         op_pos = {st[1].guid: k for k, st in enumerate(self.fwd_steps) if st[0] == "op"}
         launch_after = defaultdict(list)     # fwd step index -> exchanges to start after it
         deferred = {}                        # fwd step index of a reshard -> its exchange
@@ -1282,15 +1450,26 @@ class Executor:
                 continue
             prods = [op_pos[self.tensors[g].owner_op.guid] for g, *_ in st[1]
                      if self.tensors[g].owner_op is not None and self.tensors[g].owner_op.guid in op_pos]
-            ex = FusedExchange(items, self.world, self.rank, self.comm)
-            deferred[k] = ex
-            launch_after[max(prods) if prods else -1].append(ex)
+            if pipe is not None and k == pipe["k"]:
+                exs = [FusedExchange(self._chunk_items(items, "dst", c, pipe), self.world, self.rank, self.comm)
+                       for c in range(pipe["K"])]
+                for c, ex in enumerate(exs):
+                    ex.tag = f"reshard.fwd.c{c}"
+            else:
+                exs = [FusedExchange(items, self.world, self.rank, self.comm)]
+            deferred[k] = exs
+            launch_after[max(prods) if prods else -1].extend(exs)
         for ex in launch_after.get(-1, []):
             self._emit_exchange_start(fwd, ex, "reshard.fwd")
         for k, st in enumerate(self.fwd_steps):
+            if pipe is not None and k > pipe["k"]:
+                break                          # the tail was emitted chunk by chunk
             if st[0] == "reshard":
                 if k in deferred:
-                    self._emit_exchange_finish(fwd, deferred[k], "reshard.fwd")
+                    if pipe is not None and k == pipe["k"]:
+                        self._emit_pipelined_fwd(fwd, deferred[k], pipe)
+                    else:
+                        self._emit_exchange_finish(fwd, deferred[k][0], "reshard.fwd")
                 else:
                     items = [(rs, self.act.get((g, home.key())), self.act.get((g, need.key())), False)
                              for g, home, need, rs in st[1]]
@@ -1299,6 +1478,8 @@ class Executor:
             self._emit_fwd_op(fwd, st[1])
             for ex in launch_after.get(k, []):
                 self._emit_exchange_start(fwd, ex, "reshard.fwd")
+            if pipe is not None and k == pipe["k"]:
+                self._emit_pipelined_fwd(fwd, [], pipe)     # world-1 test hook: no exchange
 
         # ---------------- backward (accumulate flags resolved at compile time)
         self._compile_backward(bwd, C)
@@ -1311,13 +1492,32 @@ class Executor:
             if any(g.zero for g in self.groups):
                 upd.append(Item("comm", self._zero_gather, "zero.allgather", native=("ag_sync",)))
                 C(upd, "zero.cast", self._zero_cast)
+        from flexmi.ops import _kernels as K
+        if self.backend == "hip" and K.ASYNC_DW:
+            bwd = self._with_gemm_joins(bwd)
         self.prog_fwd, self.prog_bwd, self.prog_upd = fwd, bwd, upd
 
+    @staticmethod
+    def _with_gemm_joins(items):
+        """A side-stream split-K reduce (Linear dW) is joined into the compute stream before every
+        collective -- it may read the gradient, and a captured segment must join its forks -- and
+        at the end of the program."""
+        from flexmi.ops import _kernels as K
+        out = []
+        for it in items:
+            if it.kind == "comm":
+                out.append(Item("compute", K.gemm_join, "gemm.join"))
+            out.append(it)
+        out.append(Item("compute", K.gemm_join, "gemm.join"))
+        return out
+
     def _emit_exchange_start(self, lst, ex, name):
+        name = getattr(ex, "tag", None) or name
         lst.append(Item("compute", ex.pack, name + ".pack"))
         lst.append(Item("comm", (lambda ex=ex: ex.start(self.comm)), name + ".a2a", native=("a2a", ex)))
 
     def _emit_exchange_finish(self, lst, ex, name):
+        name = getattr(ex, "tag", None) or name
         lst.append(Item("comm", ex.wait, name + ".wait", native=("wait", ex)))
         lst.append(Item("compute", ex.unpack, name + ".unpack"))
 
@@ -1404,9 +1604,20 @@ class Executor:
                 bucket_done([dop])
             deferred.clear()
 
+        pipe = getattr(self, "pipe", None)
+        kb = pipe["kb"] if pipe is not None else None
+        skip_to = -1
         for k, st in enumerate(steps):
             for ex in finish_before.pop(k, []):
                 self._emit_exchange_finish(bwd, ex, "reshard.bwd")
+            if k < skip_to:
+                continue
+            if k == kb:
+                skip_to = self._emit_pipelined_bwd(bwd, C, pipe, k, written, bucket_done, finish_before, touches)
+                if defer_ok:
+                    flush_deferred()
+                    defer_ok = False
+                continue
             if st[0] == "op":
                 op = st[1]
                 c = self.ctx.get(op.guid)
@@ -1468,6 +1679,66 @@ class Executor:
         for ex in finish_before.pop(len(steps), []):
             self._emit_exchange_finish(bwd, ex, "reshard.bwd")
         assert not finish_before
+
+    def _emit_pipelined_bwd(self, bwd, C, pipe, kb, written, bucket_done, finish_before, touches):
+        """The tail's backward chunk by chunk (see XCHG_CHUNKS); returns the first step after the
+        tail's gradient return."""
+        from flexmi.core.types import OperatorType
+        steps = self.bwd_steps
+        region_b = list(reversed(pipe["region"]))
+        kr = kb + len(region_b)
+        flags = {}
+        for op in region_b:
+            c = self.ctx[op.guid]
+            fl = []
+            for i, t in enumerate(op.inputs):
+                same = c.in_grads[i] is not None and self.need[(op.guid, i)].same_as(self.home[t.guid])
+                fl.append(bool(same and self.gkey(t.guid) in written))
+            for o in op.outputs:
+                if o.guid in self.grad and self.gkey(o.guid) not in written:
+                    C(bwd, o.name + ".zero_unused_grad", (lambda t=self.grad[o.guid]: t.zero_()))
+                    written.add(self.gkey(o.guid))
+            flags[op.guid] = fl
+            for i, t in enumerate(op.inputs):
+                if c.in_grads[i] is not None and self.need[(op.guid, i)].same_as(self.home[t.guid]):
+                    written.add(self.gkey(t.guid))
+        red = steps[kr][1] if kr < len(steps) and steps[kr][0] == "reduce" else []
+        items, seen = [], set()
+        for op, i, g, rs in red:
+            key = self.gkey(g)
+            items.append((rs, self.tmp_grad.get((op.guid, i)), self.grad.get(g), key in written or key in seen))
+            seen.add(key)
+        exs = []
+        if items:
+            exs = [FusedExchange(self._chunk_items(items, "src", c, pipe), self.world, self.rank, self.comm)
+                   for c in range(pipe["K"])]
+        for c, ex in enumerate(exs):
+            ex.tag = f"reshard.bwd.c{c}"
+        split = {op.guid for op in region_b if op.op_type == OperatorType.OP_LINEAR and op.weights}
+        for c in range(pipe["K"]):
+            for op in region_b:
+                cc = pipe["ctx"][c][op.guid]
+                fl = flags[op.guid]
+                if op.guid in split:
+                    C(bwd, f"{op.name}.c{c}.bwd_dx", (lambda op=op, cc=cc, fl=fl: self._bwd_op(op, cc, fl, "dx")))
+                else:
+                    bwd.append(Item("compute", (lambda op=op, cc=cc, fl=fl: self._bwd_op(op, cc, fl)), f"{op.name}.c{c}.bwd"))
+                bwd[-1].check = (lambda op=op, cc=cc: self._check_op(op.name + ".bwd", cc.in_grads, "input grad"))
+            if exs:
+                self._emit_exchange_start(bwd, exs[c], "reshard.bwd")
+        # whole-batch weight gradients (overlapping the last chunk's all-to-all), then their buckets
+        for op in region_b:
+            if op.guid in split:
+                C(bwd, op.name + ".bwd_dw", (lambda op=op: op.backward(self.ctx[op.guid], "dw")))
+            bucket_done([op])
+        if not red:
+            return kr
+        keys = {self.gkey(g) for _, _, g, _ in red}
+        nxt = next((j for j in range(kr + 1, len(steps)) if touches(steps[j], keys)), len(steps))
+        finish_before[nxt].extend(exs)
+        for op, i, g, rs in red:
+            written.add(self.gkey(g))
+        return kr + 1
 
     def _emit_sparse_dp(self, bwd, grp):
         """Replicated embedding tables: pack (coalesce this rank's lookups) -> all-gather of the

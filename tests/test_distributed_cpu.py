@@ -31,7 +31,9 @@ def _build(case, world):
     cfg = FFConfig()
     cfg.device = "cpu"
     cfg.compute_dtype = "fp32"
-    B = 16
+    pipe = "+pipe" in case
+    case = case.split("+pipe")[0]
+    B = 128 if pipe else 16     # micro-batch pipelining: >= 8 rows per chunk on every rank
     cfg.batchSize = B
     m = FFModel(cfg)
     strat = {}
@@ -218,8 +220,20 @@ def _run(case, world, rank, steps, out_path):
     p2p = case.endswith("+p2p")
     case = case.replace("+p2p", "")
     E.P2P_MODE = "1" if p2p else os.environ.get("FM_P2P", "auto")
+    suffix = case.split("+pipe")[1] if "+pipe" in case else ""
+    chunks = int(suffix) if suffix else 0
+    E.XCHG_CHUNKS = str(chunks) if chunks else os.environ.get("FLEXMI_XCHG_CHUNKS", "auto")
     m, inputs = _build(case, world)
     ex = m.init_layers()
+    if chunks and world > 1:
+        # the exchange feeding the interaction + top MLP really is split into chunk all-to-alls,
+        # forward and backward, and the tail runs chunk by chunk
+        assert ex.pipe is not None and ex.pipe["K"] == chunks and ex.pipe["kb"] is not None, ex.pipe
+        names = [it.name for it in ex.prog_fwd + ex.prog_bwd]
+        for c in range(chunks):
+            assert f"reshard.fwd.c{c}.a2a" in names and f"reshard.bwd.c{c}.a2a" in names, names
+            assert any(n.endswith(f".c{c}.fwd") for n in names) and any(n.endswith(f".c{c}.bwd_dx") for n in names)
+    case = case.split("+pipe")[0]
     for op in m.layers:  # the strategy must really be applied (no silent DP fallback)
         if op.name in m.strategies:
             assert ex.pcs[op.guid] == m.strategies[op.name], (op.name, ex.pcs[op.guid])
@@ -315,9 +329,10 @@ def _launch(case, world, steps=3):
                                         ("nmt_pipeline", 2), ("nmt_pipeline", 4), ("cnn_spatial", 4),
                                         ("cnn_spatial+p2p", 2), ("dlrm_dot+p2p", 2),
                                         ("dlrm_shipped8", 8), ("dlrm_dp", 2), ("dlrm_dp", 4), ("dlrm_dp", 8),
-                                        ("inception8", 8)])
+                                        ("inception8", 8), ("dlrm_dot+pipe2", 2), ("dlrm_dot+pipe3", 2),
+                                        ("dlrm_cat+pipe2", 4), ("dlrm_mlperf8+pipe2", 8)])
 def test_strategy_equivalence(case, world):
-    ref = _launch(case.replace("+p2p", ""), 1)
+    ref = _launch(case.replace("+p2p", "").split("+pipe")[0] + ("+pipe" if "+pipe" in case else ""), 1)
     got = _launch(case, world)
     keys = [k for k in ref.files if k.startswith("arr_")]
     assert len(keys) == len([k for k in got.files if k.startswith("arr_")])

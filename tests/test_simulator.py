@@ -29,6 +29,30 @@ def test_chain_with_transfer(native):
     assert kinds.count("xfer") == 2 and kinds.count("fwd") == 2 and kinds.count("bwd") == 2
 
 
+@pytest.mark.parametrize("chunks,expect", [(1, 114.0), (2, 98.0)])
+def test_micro_batch_pipelined_exchange(native, chunks, expect):
+    """An exchange into a sample-split row-wise tail, split in micro-batch chunks (executor:
+    FLEXMI_XCHG_CHUNKS): chunk 1's transfer overlaps chunk 0's compute, and chunk 0's gradient
+    returns while chunk 1 runs backward."""
+    from flexmi import _native
+    s = _native.Simulator(dict(BIG, xchg_chunks=chunks, chunk_us=0.0))
+    t0 = s.add_tensor(4, -1, 0, False)
+    t1 = s.add_tensor(4, 0, 0, True)
+    full = ((0, 0), (8, 1000), (0,))
+    e = {"part_dev": [0], "fwd_us": [10.0], "bwd_us": [10.0], "out": [[full]], "inp": [[full]]}
+    s.add_op("E", [t0], [t1], [e], 2)
+    t2 = s.add_tensor(4, 1, 0, True)
+    p0, p1 = ((0, 0), (4, 1000), (0,)), ((4, 0), (8, 1000), (1,))
+    tail = {"part_dev": [0, 1], "fwd_us": [20.0, 20.0], "bwd_us": [40.0, 40.0], "out": [[p0, p1]], "inp": [[p0, p1]],
+            "sample_only": True}
+    s.add_op("T", [t1], [t2], [tail], 2, True)
+    # K=1: E 0-10, xfer 16 kB (1 + 16 us) 10-27, T[1] fwd 27-47, bwd 47-87, grad 87-104, E.bwd 104-114
+    # K=2: xfers 10-19, 19-28; T[1] fwd 19-29, 29-39; bwd 39-59, 59-79; grads 59-68, 79-88; E.bwd 88-98
+    assert s.simulate([0, 0]) == pytest.approx(expect)
+    kinds = [k for _, k, _, _, _ in s.trace([0, 0])]
+    assert kinds.count("xfer") == 2 * chunks and kinds.count("fwd") == 1 + 2 * chunks
+
+
 def test_data_parallel_allreduce_and_update(native):
     from flexmi import _native
     s = _native.Simulator(BIG)
