@@ -4,7 +4,7 @@ On a GPU run the extension MUST be present: every call goes through :func:`C` wh
 ``flexmi._C`` cannot be imported -- there is no silent eager fallback for the hot ops (GEMM,
 embedding, interaction, optimizer, loss, element-wise, data movement, and the CNN ops: GEMM
 convolution = implicit-GEMM MFMA kernels on NCHW, HIP pooling and batch norm).
-:data:`LIBRARY_FALLBACK` lists ops routed to vendor libraries instead (none).
+:data:`LIBRARY_FALLBACK` lists ops routed to vendor libraries instead (the big fp32 dW GEMMs).
 """
 from __future__ import annotations
 
@@ -15,7 +15,8 @@ import torch
 
 _C = None
 _lock = threading.Lock()
-LIBRARY_FALLBACK = {}   # every op of the framework runs a flexmi HIP kernel on MI355X
+# ops routed to a vendor library instead of a flexmi kernel (plain GEMMs only, measured faster)
+LIBRARY_FALLBACK = {"linear dW, fp32, out >= 512 and in >= 480 features": "hipBLASLt via torch addmm_ (FM_DW_LIB)"}
 
 
 def C():
@@ -111,6 +112,20 @@ def linear_forward(x2, w, b, act, y2):
     gemm(x2, x2.stride(0), True, w, K, True, y2, y2.stride(0), M, N, K, bias=b, act=act)
 
 
+# FM_DW_LIB=auto/1/0: the fp32 weight-gradient GEMM dW += dpre^T x of the big layers is a plain
+# library GEMM (hipBLASLt, beta = 1 accumulate; bias gradient from the act-backward pass or one
+# column-sum pass).  auto = the shapes where hipBLASLt measured faster than the flexmi kernel plus
+# its split-K reduce (profiles/gemm_fp32_vs_hipblaslt.jsonl: 480->1024 66 vs 85 us, 1024->1024 125
+# vs 150, 1024->512 68 vs 84; the 256/128/16-wide ones stay on flexmi, where it wins)
+DW_LIB = os.environ.get("FM_DW_LIB", "auto")
+
+
+def _dw_lib(M, N, K, dtype):
+    if DW_LIB == "0" or dtype != torch.float32:
+        return False
+    return DW_LIB == "1" or (N >= 512 and K >= 480 and M >= 4096)
+
+
 DX_LIB = os.environ.get("FM_DX_LIB", "0") == "1"
 DX_LIB_MIN = int(os.environ.get("FM_DX_LIB_MIN", str(1 << 32)))
 
@@ -133,6 +148,8 @@ def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=F
         if dx2 is not None and fuse_below is not None:
             raise AssertionError("no fused epilogue on the skinny path")
         return
+    lib = _dw_lib(M, N, K, x2.dtype)
+    fold_db = lib and not (grad_is_dpre or act == 10)    # db from the act-backward pass below
     if grad_is_dpre or act == 10:
         dpre = dy2
     elif phase == "dw":            # computed by this op's "dx" phase (per-op workspace)
@@ -142,13 +159,19 @@ def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=F
         if dpre is None or dpre.shape != (M, N) or dpre.dtype != dy2.dtype:
             dpre = torch.empty((M, N), dtype=dy2.dtype, device=x2.device)
             ws["dpre"] = dpre
-        C().act_bwd_bias(y2, dy2, dpre, None, M, N, act)
+        C().act_bwd_bias(y2, dy2, dpre, db if fold_db else None, M, N, act)
+    if lib and phase != "dx":
+        dw.addmm_(dpre.t(), x2)                          # hipBLASLt, accumulates (beta = 1)
+        if db is not None and not fold_db:
+            C().act_bwd_bias(dpre, dpre, None, db, M, N, 10)   # column sums of dpre
+        if phase == "dw":
+            return
     # dW[N,K] = dpre^T x (both operands MN-contiguous: transposing LDS reads); the bias gradient
     # db = column sums of dpre is accumulated from the staged A tiles of the same GEMM
     # dW ACCUMULATES (beta): the executor zeroes the flat gradient buffer once per step, so weights
     # used by several ops sum their gradients, and split-K partials of small dW tiles can be added
     # with atomics straight into dw (no slab / reduce launch)
-    if phase != "dx":
+    if phase != "dx" and not lib:
         gemm(dpre, dpre.stride(0), False, x2, x2.stride(0), False, dw, K, N, K, M, beta=True, rowsum_a=db,
              async_reduce=async_dw and ASYNC_DW)
     if phase == "dw":
