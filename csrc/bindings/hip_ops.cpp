@@ -111,6 +111,20 @@ void fm_conv_s2d_run(const void* x, void* xs, int bf16, int N, int C, int H, int
 void fm_conv_w_s2d_run(const void* w, void* ws, const float* dws, float* dw, int bf16, int K, int C, int R, int S, int s,
                        int Rs, int Ss, int inv, hipStream_t st);
 void fm_pad_rows(const void* src, void* dst, int K, int n, int ldp, int bf16, hipStream_t st);
+void fm_nhwc_stage_run(const void* src, void* dst, int N, int C, int H, int W, int Cp, int Hp, int Wp, int top, int left,
+                       int dh, int dw, hipStream_t s);
+void fm_nhwc_stage_grad_run(const void* dy, const void* y, void* dst, int act, int N, int C, int H, int W, int Cp, int Hp,
+                            int Wp, int top, int left, int dh, int dw, hipStream_t s);
+long fm_conv_nhwc_wgrad_ws(int N, int K, int P, int Q, int R, int S, int Cp);
+void fm_cnhwc_wprep_run(const void* w, void* out, const float* g2, float* dw, int K, int C, int R, int S, int Cp, int Kp,
+                        int mode, int nsplit, hipStream_t s);
+void fm_conv_nhwc_fwd(const void* xs, long xs_bytes, const void* wf, const float* bias, void* y, int N, int K, int P, int Q,
+                      int R, int S, int Cp, int Hp, int Wp, int sh, int sw, int act, hipStream_t s);
+void fm_conv_nhwc_dgrad(const void* gs, long gs_bytes, const void* wd, void* dx, int accum, int N, int C, int H, int W, int R,
+                        int S, int Kp, int Hg, int Wg, hipStream_t s);
+int fm_conv_nhwc_wgrad(const void* gs, long gs_bytes, const void* xs, long xs_bytes, float* g2, float* db, int N, int K, int Kp, int P,
+                        int Q, int Hg, int Wg, int gt, int gl, int gsh, int gsw, int R, int S, int Cp, int Hp, int Wp, int sh,
+                        int sw, int* ptab, hipStream_t s);
 void fm_lstm_init(const void* h0, const void* c0, void* hprev, long ldhp, float* cinit, int B, int H, int bf16, hipStream_t s);
 void fm_lstm_cell_fwd(float* G, long ldg, const float* c_prev, long ldcp, float* c_out, long ldc, void* y, long ldy,
                       void* hprev_next, long ldhp, void* hT, void* cT, int B, int H, int bf16, hipStream_t s);
@@ -708,6 +722,120 @@ void conv_w_s2d(torch::Tensor w, torch::Tensor ws, torch::Tensor dws, torch::Ten
                     (int)w.size(1), (int)w.size(2), (int)w.size(3), (int)s, (int)ws.size(2), (int)ws.size(3), inv ? 1 : 0,
                     cur());
 }
+// NHWC-staged bf16 convolution (csrc/kernels/conv_nhwc.hip).  Every extent the kernels index is
+// checked here: staged operands [N][Hp][Wp][Cp] (Cp % 8 == 0), 16-B aligned, under 2 GiB.
+static void nhwc_chk(const torch::Tensor& t, long need, const char* n) {
+  check_cuda(t, n);
+  TORCH_CHECK(t.scalar_type() == torch::kBFloat16 && t.is_contiguous(), n, ": contiguous bf16");
+  TORCH_CHECK(t.numel() >= need, n, ": too small (", t.numel(), " < ", need, ")");
+  TORCH_CHECK(t.numel() * 2 < (1L << 31) - 64, n, ": under 2 GiB (32-bit buffer offsets)");
+  TORCH_CHECK(((uintptr_t)t.data_ptr() & 15) == 0, n, ": 16-B aligned");
+}
+void nhwc_stage(torch::Tensor src, torch::Tensor dst, int64_t Cp, int64_t Hp, int64_t Wp, int64_t top, int64_t left, int64_t dh,
+                int64_t dw) {
+  TORCH_CHECK(dh >= 1 && dw >= 1, "nhwc_stage: dilation >= 1");
+  TORCH_CHECK(src.dim() == 4, "nhwc_stage: src [N,C,H,W]");
+  const long N = src.size(0), C = src.size(1);
+  TORCH_CHECK(Cp % 8 == 0 && Cp >= C && Hp > 0 && Wp > 0, "nhwc_stage: Cp % 8 == 0, Cp >= C");
+  nhwc_chk(src, src.numel(), "nhwc_stage src");
+  nhwc_chk(dst, N * Hp * Wp * Cp, "nhwc_stage dst");
+  TORCH_CHECK(N * Hp < (1L << 31), "nhwc_stage: grid");
+  fm_nhwc_stage_run(src.data_ptr(), dst.data_ptr(), (int)N, (int)C, (int)src.size(2), (int)src.size(3), (int)Cp, (int)Hp,
+                    (int)Wp, (int)top, (int)left, (int)dh, (int)dw, cur());
+}
+// gradient staging with the activation backward and bias gradient fused: dst = stage(act'(y)*dy)
+void nhwc_stage_grad(torch::Tensor dy, torch::Tensor y, torch::Tensor dst, int64_t act, int64_t Cp, int64_t Hp, int64_t Wp,
+                     int64_t top, int64_t left, int64_t dh, int64_t dw) {
+  TORCH_CHECK(dy.dim() == 4 && y.sizes() == dy.sizes(), "nhwc_stage_grad: dy, y [N,K,P,Q]");
+  TORCH_CHECK(dh >= 1 && dw >= 1, "nhwc_stage_grad: dilation >= 1");
+  const long N = dy.size(0), C = dy.size(1);
+  TORCH_CHECK(Cp % 8 == 0 && Cp >= C && Hp > 0 && Wp > 0, "nhwc_stage_grad: Cp % 8 == 0, Cp >= C");
+  nhwc_chk(dy, dy.numel(), "nhwc_stage_grad dy");
+  nhwc_chk(y, y.numel(), "nhwc_stage_grad y");
+  nhwc_chk(dst, N * Hp * Wp * Cp, "nhwc_stage_grad dst");
+  fm_nhwc_stage_grad_run(dy.data_ptr(), y.data_ptr(), dst.data_ptr(), (int)act, (int)N, (int)C, (int)dy.size(2),
+                         (int)dy.size(3), (int)Cp, (int)Hp, (int)Wp, (int)top, (int)left, (int)dh, (int)dw, cur());
+}
+int64_t conv_nhwc_wgrad_ws(int64_t N, int64_t K, int64_t P, int64_t Q, int64_t R, int64_t S, int64_t Cp) {
+  return fm_conv_nhwc_wgrad_ws((int)N, (int)K, (int)P, (int)Q, (int)R, (int)S, (int)Cp);
+}
+// mode 0: out = fwd weight matrix [K][R*S*Cp]; 1: dgrad matrix [C][R*S*Kp]; 2: dw (fp32 [K,C,R,S]) += fold(g2)
+void cnhwc_wprep(torch::Tensor w, torch::Tensor out, torch::Tensor g2, torch::Tensor dw, int64_t Cp, int64_t Kp, int64_t mode,
+                 int64_t nsplit) {
+  TORCH_CHECK(nsplit >= 1, "cnhwc_wprep: nsplit >= 1");
+  TORCH_CHECK(w.dim() == 4, "cnhwc_wprep: w [K,C,R,S]");
+  const long K = w.size(0), C = w.size(1), RS = w.size(2) * w.size(3);
+  TORCH_CHECK(Cp % 8 == 0 && Cp >= C && Kp % 8 == 0 && Kp >= K, "cnhwc_wprep: padded channel counts");
+  if (mode == 0 || mode == 1) {
+    nhwc_chk(w, K * C * RS, "cnhwc_wprep w");
+    nhwc_chk(out, mode == 0 ? K * RS * Cp : C * RS * Kp, "cnhwc_wprep out");
+  } else {
+    TORCH_CHECK(mode == 2, "cnhwc_wprep: mode 0/1/2");
+    check_cuda(g2, "g2");
+    check_cuda(dw, "dw");
+    TORCH_CHECK(g2.scalar_type() == torch::kFloat32 && g2.is_contiguous() && g2.numel() >= nsplit * K * RS * Cp,
+                "cnhwc_wprep: fp32 g2 [nsplit][K][R*S*Cp]");
+    TORCH_CHECK(dw.scalar_type() == torch::kFloat32 && dw.is_contiguous() && dw.numel() == K * C * RS,
+                "cnhwc_wprep: fp32 dw [K*C*R*S]");
+  }
+  fm_cnhwc_wprep_run(w.data_ptr(), mode == 2 ? nullptr : out.data_ptr(), mode == 2 ? g2.data_ptr<float>() : nullptr,
+                     mode == 2 ? dw.data_ptr<float>() : nullptr, (int)K, (int)C, (int)w.size(2), (int)w.size(3), (int)Cp,
+                     (int)Kp, (int)mode, (int)nsplit, cur());
+}
+void conv_nhwc_fwd(torch::Tensor xs, torch::Tensor wf, c10::optional<torch::Tensor> bias, torch::Tensor y, int64_t R,
+                   int64_t S, int64_t Cp, int64_t Hp, int64_t Wp, int64_t sh, int64_t sw, int64_t act) {
+  TORCH_CHECK(y.dim() == 4 && y.scalar_type() == torch::kBFloat16 && y.is_contiguous(), "conv_nhwc_fwd: bf16 y [N,K,P,Q]");
+  const long N = y.size(0), K = y.size(1), P = y.size(2), Q = y.size(3);
+  TORCH_CHECK(Cp % 8 == 0 && (P - 1) * sh + R <= Hp && (Q - 1) * sw + S <= Wp, "conv_nhwc_fwd: staged window extent");
+  nhwc_chk(xs, N * Hp * Wp * Cp, "conv_nhwc_fwd xs");
+  nhwc_chk(wf, K * R * S * Cp, "conv_nhwc_fwd wf");
+  nhwc_chk(y, N * K * P * Q, "conv_nhwc_fwd y");
+  const float* b = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == torch::kFloat32 && bias->numel() == K && bias->is_cuda(), "conv_nhwc_fwd: fp32 bias[K]");
+    b = bias->data_ptr<float>();
+  }
+  fm_conv_nhwc_fwd(xs.data_ptr(), xs.numel() * 2, wf.data_ptr(), b, y.data_ptr(), (int)N, (int)K, (int)P, (int)Q, (int)R,
+                   (int)S, (int)Cp, (int)Hp, (int)Wp, (int)sh, (int)sw, (int)act, cur());
+}
+void conv_nhwc_dgrad(torch::Tensor gs, torch::Tensor wd, torch::Tensor dx, int64_t R, int64_t S, int64_t Kp, int64_t Hg,
+                     int64_t Wg, bool acc) {
+  TORCH_CHECK(dx.dim() == 4, "conv_nhwc_dgrad: dx [N,C,H,W]");
+  const long N = dx.size(0), C = dx.size(1), H = dx.size(2), W = dx.size(3);
+  TORCH_CHECK(Kp % 8 == 0 && H + R - 1 <= Hg && W + S - 1 <= Wg, "conv_nhwc_dgrad: staged G extent");
+  nhwc_chk(gs, N * Hg * Wg * Kp, "conv_nhwc_dgrad gs");
+  nhwc_chk(wd, C * R * S * Kp, "conv_nhwc_dgrad wd");
+  nhwc_chk(dx, N * C * H * W, "conv_nhwc_dgrad dx");
+  fm_conv_nhwc_dgrad(gs.data_ptr(), gs.numel() * 2, wd.data_ptr(), dx.data_ptr(), acc ? 1 : 0, (int)N, (int)C, (int)H, (int)W,
+                     (int)R, (int)S, (int)Kp, (int)Hg, (int)Wg, cur());
+}
+int64_t conv_nhwc_wgrad(torch::Tensor gs, torch::Tensor xs, torch::Tensor g2, c10::optional<torch::Tensor> db, int64_t N, int64_t K, int64_t Kp, int64_t P,
+                     int64_t Q, int64_t Hg, int64_t Wg, int64_t gt, int64_t gl, int64_t gsh, int64_t gsw, int64_t R, int64_t S,
+                     int64_t Cp, int64_t Hp, int64_t Wp, int64_t sh, int64_t sw, torch::Tensor ptab) {
+  TORCH_CHECK(Kp % 8 == 0 && Kp >= K && Cp % 8 == 0 && gt >= 0 && gl >= 0 && gsh >= 1 && gsw >= 1 &&
+                  gt + (P - 1) * gsh < Hg && gl + (Q - 1) * gsw < Wg &&
+                  (P - 1) * sh + R <= Hp && (Q - 1) * sw + S <= Wp,
+              "conv_nhwc_wgrad: staged extents");
+  nhwc_chk(gs, N * Hg * Wg * Kp, "conv_nhwc_wgrad gs");
+  nhwc_chk(xs, N * Hp * Wp * Cp, "conv_nhwc_wgrad xs");
+  check_cuda(g2, "g2");
+  TORCH_CHECK(g2.scalar_type() == torch::kFloat32 && g2.is_contiguous() &&
+                  g2.numel() >= fm_conv_nhwc_wgrad_ws((int)N, (int)K, (int)P, (int)Q, (int)R, (int)S, (int)Cp),
+              "conv_nhwc_wgrad: fp32 g2 slabs (conv_nhwc_wgrad_ws floats)");
+  float* dbp = nullptr;
+  if (db.has_value() && db->defined()) {
+    TORCH_CHECK(db->is_cuda() && db->scalar_type() == torch::kFloat32 && db->numel() == K && db->is_contiguous(),
+                "conv_nhwc_wgrad: fp32 db[K]");
+    dbp = db->data_ptr<float>();
+  }
+  TORCH_CHECK(N * P * Q < (1L << 28), "conv_nhwc_wgrad: pixel count");
+  check_cuda(ptab, "ptab");
+  TORCH_CHECK(ptab.scalar_type() == torch::kInt32 && ptab.is_contiguous() && ptab.numel() >= 2 * N * P * Q,
+              "conv_nhwc_wgrad: int32 ptab[2*N*P*Q]");
+  return fm_conv_nhwc_wgrad(gs.data_ptr(), gs.numel() * 2, xs.data_ptr(), xs.numel() * 2, g2.data_ptr<float>(), dbp, (int)N, (int)K,
+                     (int)Kp, (int)P, (int)Q, (int)Hg, (int)Wg, (int)gt, (int)gl, (int)gsh, (int)gsw, (int)R, (int)S, (int)Cp,
+                     (int)Hp, (int)Wp, (int)sh, (int)sw, ptab.data_ptr<int>(), cur());
+}
 void conv_act_bwd(torch::Tensor dy, torch::Tensor y, torch::Tensor g, c10::optional<torch::Tensor> db, int64_t act) {
   chk4(dy, "dy");
   chk4(y, "y");
@@ -846,6 +974,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_act_bwd", &conv_act_bwd);
+  m.def("nhwc_stage", &nhwc_stage);
+  m.def("nhwc_stage_grad", &nhwc_stage_grad);
+  m.def("conv_nhwc_wgrad_ws", &conv_nhwc_wgrad_ws);
+  m.def("cnhwc_wprep", &cnhwc_wprep);
+  m.def("conv_nhwc_fwd", &conv_nhwc_fwd);
+  m.def("conv_nhwc_dgrad", &conv_nhwc_dgrad);
+  m.def("conv_nhwc_wgrad", &conv_nhwc_wgrad);
   m.def("conv_s2d", &conv_s2d);
   m.def("conv_w_s2d", &conv_w_s2d);
   m.def("embedding_fwd", &embedding_fwd);

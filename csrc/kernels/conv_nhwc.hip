@@ -1,0 +1,689 @@
+// NHWC-staged implicit-GEMM convolution for gfx950 (MI355X / CDNA4), bf16 operands, fp32
+// accumulate.  The NCHW kernels (conv_igemm.hip) gather every operand chunk from NCHW with
+// per-element index math, halo masks and funnel shifts; PMC on ResNet-50 layers shows them
+// instruction-bound (r2 3x3 fwd: ~21 VALU instructions per MFMA, 1x1 fwd 64:1, wgrad heavy on
+// SALU; profiles/pmc_conv_nchw_r3l.txt).  This path first re-lays each image operand ONCE into a
+// zero-padded NHWC copy ("staging"), after which every 16-B operand chunk of the implicit GEMM is
+// 8 consecutive channels at one pixel -- one aligned buffer_load_b128 with no bounds math beyond
+// the tile edges:
+//
+//   staged S[n][i][j][c], i in [0,Hp), j in [0,Wp), c in [0,Cp) (Cp = roundup(C, 8), zeros in the
+//   halo, in the channel pad and, for the data gradient, around G)
+//   pixel pix = (n, p, q) -> window origin  org(pix) = ((n*Hp + p*sh + oh)*Wp + q*sw + ow) * Cp
+//   reduction chunk j of (r, s, c8)  ->  tap(j) = (r*Wp + s) * Cp + 8*c8
+//
+//   fwd    Y[k][pix]      = sum_{(r,s,c)}  Wf[k][(r,s,c)]  * Xs[org(pix) + tap]         (NCHW Y)
+//   dgrad dX[c][pix]      = sum_{(r,s,k)}  Wd[c][(r,s,k)]  * Gs[org(pix) + tap]         (Gs = G
+//          placed at (R-1-pt, S-1-pl), dilated by the stride; Wd = W flipped in (r,s) and
+//          transposed; NCHW dX.  A stride-s layer multiplies s*s times the useful MACs here.)
+//   wgrad dW2[k][(r,s,c)] = sum_pix Gs[orgG(pix) + k] * Xs[orgX(pix) + tap(r,s,c)]     (fp32)
+//
+// fwd / dgrad: A = weights K-contiguous [M][K] (plain rows), B = gathered pixels K-contiguous
+// (the thread's pixel rows are fixed for the whole K loop: origins computed once; a k-tile costs
+// one tap() per thread).  wgrad: both operands MN-contiguous (k = pixel rows, channel chunks
+// along M / N) -> LDS images [k][R] read with ds_read_b64_tr_b16 like gemm.hip's MN operands.
+// MFMA core, LDS images and swizzles are gemm.hip's (gemm_common.h): v_mfma_f32_16x16x32_bf16,
+// BM x BN x 64 tiles, register-staged double-buffered LDS, one barrier per k-tile, XCD-aware
+// tile order, 8-wave blocks for 128x128 tiles.  Epilogues: fwd bias + activation into NCHW y;
+// dgrad (+)= into NCHW dx; wgrad fp32 [K][R*S*Cp] (float atomics across split-K slices), folded
+// into dW[K][C][R][S] by fm_cnhwc_wprep mode 2.
+// Replaces the reference's cuDNN calls (src/ops/conv_2d.cu:285-296 forward, :405-432 backward).
+#include "gemm_common.h"
+
+#include <algorithm>
+#include <type_traits>
+
+namespace {
+
+constexpr unsigned OOBN = 0x80000000u;   // buffer offset past num_records: the load returns 0
+
+enum { CN_FWD = 0, CN_DGRAD = 1, CN_WGRAD = 2 };
+
+// pixel geometry of one staged operand (pixel = (n, p, q) of the GEMM's pixel index space)
+struct PixG {
+  FastDiv dPQ, dQ;
+  int PQ, Q;
+  int Hp, Wp, Cp;
+  int sh, sw, oh, ow;
+};
+
+// reduction / column taps over (r, s, c8) with c8 fastest
+struct TapG {
+  FastDiv dC8, dS;
+  int C8, S, Wp, Cp;
+};
+
+struct ConvN {
+  const unsigned short* A;  long a_bytes;   // fwd/dgrad: weight matrix [M][K]; wgrad: staged G
+  const unsigned short* B;  long b_bytes;   // staged image operand
+  void* out;                                // fwd: y (bf16 NCHW); dgrad: dx (bf16 NCHW); wgrad: fp32 [M][N]
+  const float* bias;
+  int M, N, K;          // GEMM sizes (K = reduction length, a multiple of 8)
+  int Mp;               // wgrad: staged channel count of A (loads below Mp read real memory)
+  int npix;             // pixels of the pixel index space
+  PixG ga, gb;
+  TapG tb;
+  const int* ptab;      // wgrad: {orgA, orgB} per pixel (fm_pix_table)
+  float* db;            // wgrad: bias gradient (+)= sum over pixels of the staged G (may be null)
+  FastDiv dOPQ;         // fwd/dgrad output pixels per image
+  int OPQ;
+  int act, accum, ksplit, kt_per, tiles_m, tiles_n;
+};
+
+FM_DEVICE __amdgpu_buffer_rsrc_t rsrc_n(const void* p, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+
+FM_DEVICE u32x4_t ld16(__amdgpu_buffer_rsrc_t rs, bool ok, int elem_off) {
+  return __builtin_bit_cast(u32x4_t,
+                            __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? (unsigned)elem_off * 2u : OOBN, 0, 0));
+}
+
+FM_DEVICE void pix_nqp(const PixG& g, int pix, int& n, int& p, int& q) {
+  n = fdiv(pix, g.dPQ);
+  const int rem = pix - n * g.PQ;
+  p = fdiv(rem, g.dQ);
+  q = rem - p * g.Q;
+}
+
+FM_DEVICE int pix_org(const PixG& g, int n, int p, int q) {
+  return ((n * g.Hp + p * g.sh + g.oh) * g.Wp + q * g.sw + g.ow) * g.Cp;
+}
+
+FM_DEVICE int tap_off(const TapG& t, int j) {
+  const int rs = fdiv(j, t.dC8), c8 = j - rs * t.C8;
+  const int r = fdiv(rs, t.dS), s = rs - r * t.S;
+  return (r * t.Wp + s) * t.Cp + 8 * c8;
+}
+
+// ---- operand loaders (global -> registers -> LDS image) ----------------------------------
+// K-contiguous rows (fwd/dgrad A: weight rows; B: gathered pixel rows).  Chunk ci = tid + NTH*i:
+// row ci >> 3, k-chunk ci & 7 (the same for every i of a thread).
+template <int R, int NTH, bool GATHER>
+struct LoadKC {
+  static constexpr int PER_T = R * 8 / NTH;
+  u32x4_t v[PER_T];
+  int org[PER_T];
+  bool rok[PER_T];
+
+  FM_DEVICE void init(const ConvN& p, int row0, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int row = row0 + ((tid + NTH * i) >> 3);
+      if constexpr (GATHER) {
+        rok[i] = row < p.N;
+        int n, pp, q;
+        pix_nqp(p.gb, rok[i] ? row : 0, n, pp, q);
+        org[i] = pix_org(p.gb, n, pp, q);
+      } else {
+        rok[i] = row < p.M;
+        org[i] = (rok[i] ? row : 0) * p.K;
+      }
+    }
+  }
+
+  FM_DEVICE void load(const ConvN& p, __amdgpu_buffer_rsrc_t rs, int kt, int tid) {
+    const int j = kt * 8 + (tid & 7);       // reduction chunk of this thread
+    const bool kok = j * 8 < p.K;
+    int t;
+    if constexpr (GATHER) t = tap_off(p.tb, kok ? j : 0);
+    else t = 8 * j;
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) v[i] = ld16(rs, kok && rok[i], org[i] + t);
+  }
+
+  FM_DEVICE void store(char* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int ci = tid + NTH * i;
+      *reinterpret_cast<u32x4_t*>(lds + lds_off<true, R>(ci >> 3, ci & 7)) = v[i];
+    }
+  }
+};
+
+// MN-contiguous (wgrad): k-row = pixel, chunks of 8 channels / taps along the R rows of the tile.
+// Chunk ci = tid + NTH*i: k-row ci / (R/8), chunk ci % (R/8) (fixed per thread).  The window
+// origins of a k-tile's pixels come from the per-pass origin table (fm_pix_table: {orgA, orgB} per
+// pixel), read one k-tile AHEAD: load(kt) issues the data loads of k-tile kt with the origins in
+// registers, then the table loads of k-tile kt+1 -- no pixel index math in the K loop.
+template <int R, int NTH, bool IS_A>
+struct LoadMN {
+  static constexpr int PER_T = R * 8 / NTH;
+  static constexpr int CPR = R / 8;       // chunks per k-row
+  u32x4_t v[PER_T];
+  int org[PER_T];
+  int coff;       // fixed column offset of this thread's chunk (channel or tap)
+  bool cok;
+
+  FM_DEVICE void init(const ConvN& p, int col0, int tid, int kt0) {
+    const int c = col0 + 8 * (tid % CPR);
+    if constexpr (IS_A) {
+      cok = c < p.Mp;
+      coff = c;
+    } else {
+      cok = c < p.N;
+      coff = tap_off(p.tb, cok ? c / 8 : 0);
+    }
+    const PixG& g = IS_A ? p.ga : p.gb;
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int pix = kt0 * 64 + (tid + NTH * i) / CPR;
+      int n, pp, q;
+      pix_nqp(g, pix < p.npix ? pix : 0, n, pp, q);
+      org[i] = pix_org(g, n, pp, q);
+    }
+  }
+
+  FM_DEVICE void load(const ConvN& p, __amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t rtab, int kt, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int pix = kt * 64 + (tid + NTH * i) / CPR;
+      v[i] = ld16(rs, cok && pix < p.npix, org[i] + coff);
+    }
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {       // origins of k-tile kt+1 (0 past the table)
+      const int pix = (kt + 1) * 64 + (tid + NTH * i) / CPR;
+      org[i] = __builtin_amdgcn_raw_buffer_load_b32(rtab, pix < p.npix ? (unsigned)(2 * pix + (IS_A ? 0 : 1)) * 4u : OOBN,
+                                                    0, 0);
+    }
+  }
+
+  FM_DEVICE void store(char* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int ci = tid + NTH * i;
+      *reinterpret_cast<u32x4_t*>(lds + lds_off<false, R>(ci / CPR, ci % CPR)) = v[i];
+    }
+  }
+
+  // every chunk of this thread covers the same 8 channels: summing the staged chunks gives the
+  // per-channel partial sums of G (the bias gradient) without another pass over G
+  FM_DEVICE void accumulate(float (&s)[8]) const {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s[2 * j] += bf2f((unsigned short)(v[i][j] & 0xFFFF));
+        s[2 * j + 1] += bf2f((unsigned short)(v[i][j] >> 16));
+      }
+  }
+};
+
+// {orgA, orgB} window origins of every pixel of a wgrad pass (both operands share the pixel space)
+__global__ void __launch_bounds__(256) fm_pix_table(int* __restrict__ tab, int npix, PixG ga, PixG gb) {
+  for (int pix = blockIdx.x * 256 + threadIdx.x; pix < npix; pix += gridDim.x * 256) {
+    int n, p, q;
+    pix_nqp(ga, pix, n, p, q);
+    tab[2 * pix] = pix_org(ga, n, p, q);
+    tab[2 * pix + 1] = pix_org(gb, n, p, q);
+  }
+}
+
+// ---- the kernel -------------------------------------------------------------------------------
+template <int BM, int BN, int MODE, int NTH>
+__global__ void __launch_bounds__(NTH, 2) fm_conv_nhwc(ConvN p) {
+  constexpr bool KCM = MODE != CN_WGRAD;     // both operands K-contiguous (fwd / dgrad)
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int WN = (NTH == 512 && BN >= 128) ? 4 : 2;
+  constexpr int WM = NTH / 64 / WN;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int MR = TM / 16, NR = TN / 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int bid = xcd_remap(blockIdx.x, p.tiles_m * p.tiles_n);
+  const int tm = bid % p.tiles_m, tn = bid / p.tiles_m;   // row tiles fastest: the big pixel operand is shared
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int ktiles = (p.K + BK - 1) / BK;
+  const int kt0 = blockIdx.z * p.kt_per, kt1 = min(ktiles, kt0 + p.kt_per);
+
+  const auto rsa = rsrc_n(p.A, p.a_bytes);
+  const auto rsb = rsrc_n(p.B, p.b_bytes);
+  using LA = typename std::conditional<KCM, LoadKC<BM, NTH, false>, LoadMN<BM, NTH, true>>::type;
+  using LB = typename std::conditional<KCM, LoadKC<BN, NTH, true>, LoadMN<BN, NTH, false>>::type;
+  LA la;
+  LB lb;
+  const auto rst = rsrc_n(p.ptab, KCM ? 0 : (long)p.npix * 8);
+  if constexpr (KCM) {
+    la.init(p, m0, tid);
+    lb.init(p, n0, tid);
+  } else {
+    la.init(p, m0, tid, kt0);
+    lb.init(p, n0, tid, kt0);
+  }
+#define FM_CN_LOAD(kt)                \
+  do {                                \
+    if constexpr (KCM) {              \
+      la.load(p, rsa, kt, tid);       \
+      lb.load(p, rsb, kt, tid);       \
+    } else {                          \
+      la.load(p, rsa, rst, kt, tid);  \
+      lb.load(p, rsb, rst, kt, tid);  \
+    }                                 \
+  } while (0)
+
+  f32x4_t acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  float dbs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  bool dbrow = false;
+  if constexpr (!KCM) dbrow = p.db != nullptr && tn == 0;
+  if (kt0 < kt1) {
+    FM_CN_LOAD(kt0);
+    if constexpr (!KCM) {
+      if (dbrow) la.accumulate(dbs);
+    }
+    la.store(smem, tid);
+    lb.store(smem + A_BYTES, tid);
+  }
+  __syncthreads();
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int cur = (kt - kt0) & 1;
+    const bool more = kt + 1 < kt1;
+    if (more) FM_CN_LOAD(kt + 1);
+    const char* sa = smem + cur * (A_BYTES + B_BYTES);
+    const char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8_t af[MR], bfr[NR];
+#pragma unroll
+      for (int i = 0; i < MR; ++i) af[i] = frag<KCM, BM>(sa, wm * TM + 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < NR; ++j) bfr[j] = frag<KCM, BN>(sb, wn * TN + 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8v_t*>(&bfr[j]),
+                                                              *reinterpret_cast<bf16x8v_t*>(&af[i]), acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      char* nx = smem + (cur ^ 1) * (A_BYTES + B_BYTES);
+      if constexpr (!KCM) {
+        if (dbrow) la.accumulate(dbs);
+      }
+      la.store(nx, tid);
+      lb.store(nx + A_BYTES, tid);
+    }
+    __syncthreads();
+  }
+#undef FM_CN_LOAD
+  if constexpr (!KCM) {
+    if (dbrow) {   // reduce the NTH/(BM/8) threads sharing each 8-channel column, 1 atomic per channel
+      constexpr int CPR = BM / 8;
+      float* red = reinterpret_cast<float*>(smem);   // LDS is free after the K loop
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[(tid / CPR) * BM + (tid % CPR) * 8 + j] = dbs[j];
+      __syncthreads();
+      if (tid < BM && m0 + tid < p.M) {
+        float x = 0.f;
+        for (int t = 0; t < NTH / CPR; ++t) x += red[t * BM + tid];
+        atomicAdd(p.db + m0 + tid, x);
+      }
+    }
+  }
+
+  // epilogue: lane owns C[m][n .. n+3], m = mbase + 16 i + (lane & 15), n = nbase + 16 j + 4 (lane >> 4)
+  const int mbase = m0 + wm * TM, nbase = n0 + wn * TN;
+#pragma unroll
+  for (int i = 0; i < MR; ++i) {
+    const int m = mbase + 16 * i + (lane & 15);
+    if (m >= p.M) continue;
+    const float bm = (MODE == CN_FWD && p.bias) ? p.bias[m] : 0.f;
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const int n = nbase + 16 * j + 4 * (lane >> 4);
+      if (n >= p.N) continue;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r];
+      if constexpr (MODE == CN_WGRAD) {
+        // split-K slab z = blockIdx.z of [ksplit][M][N] (N % 8 == 0: one 16-B store)
+        float* dw = reinterpret_cast<float*>(p.out) + ((long)blockIdx.z * p.M + m) * p.N + n;
+        *reinterpret_cast<f32x4_t*>(dw) = f32x4_t{v[0], v[1], v[2], v[3]};
+      } else {
+        if constexpr (MODE == CN_FWD) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = act_fwd(p.act, v[r] + bm);
+        }
+        const bool add = MODE == CN_DGRAD && p.accum;
+        unsigned short* out = reinterpret_cast<unsigned short*>(p.out);
+        const int img = fdiv(n, p.dOPQ), px = n - img * p.OPQ;
+        const long o = ((long)img * p.M + m) * p.OPQ + px;
+        if (n + 3 < p.N && px + 3 < p.OPQ && (o & 3) == 0) {
+          bf16x4_t w4;
+          if (add) {
+            const bf16x4_t old = *reinterpret_cast<const bf16x4_t*>(out + o);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) w4[r] = (short)f2bf(v[r] + bf2f((unsigned short)old[r]));
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) w4[r] = (short)f2bf(v[r]);
+          }
+          *reinterpret_cast<bf16x4_t*>(out + o) = w4;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int nn = n + r;
+            if (nn >= p.N) break;
+            const int im = fdiv(nn, p.dOPQ), pr = nn - im * p.OPQ;
+            unsigned short* d = out + ((long)im * p.M + m) * p.OPQ + pr;
+            *d = f2bf(v[r] + (add ? bf2f(*d) : 0.f));
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---- staging: NCHW -> zero-padded NHWC ------------------------------------------------------
+// dst [N][Hp][Wp][Cp]: dst[n][i][j][c] = v[n][c][(i - top)/dh][(j - left)/dw] where the division is
+// exact and inside, 0 elsewhere (top / left may be negative: leading source rows / columns are
+// skipped; dilation dh, dw > 1 spreads a strided convolution's G for its stride-1 data gradient).
+// v = src, or for the gradient staging (GRAD) v = act'(y) * dy rounded to bf16 (one pass instead of
+// an activation-backward pass + a copy; the bias gradient is summed by the wgrad kernel).
+// Block = 64 destination columns x 64 channels of one destination row; loads coalesce along the
+// source row (w), the 16-B stores along the channels.
+template <bool GRAD>
+__global__ void __launch_bounds__(256) fm_nhwc_stage(const unsigned short* __restrict__ src, const unsigned short* __restrict__ ysrc,
+                                                     unsigned short* __restrict__ dst, int act,
+                                                     int C, int H, int W, int Cp, int Hp, int Wp, int top, int left, int dh,
+                                                     int dw) {
+  __shared__ __attribute__((aligned(16))) unsigned short tile[64][72];   // [channel][column], 144-B rows
+  const int j0 = blockIdx.y * 64, c0 = blockIdx.z * 64;
+  const int ni = blockIdx.x;
+  const int n = ni / Hp, i = ni - n * Hp;
+  const int hd = i - top, h = hd / dh;
+  const bool rowin = hd >= 0 && h * dh == hd && h < H;
+  if (rowin) {
+    if (dw == 1) {
+      // 8 consecutive source columns per thread-chunk: one (unaligned) 16-B buffer load where the
+      // chunk lies inside the row, element loads only for the chunks on the row's edges
+      const long rowel = (long)H * W;
+      const auto rs = rsrc_n(src, (long)gridDim.x / Hp * C * rowel * 2);
+      const auto ry = rsrc_n(GRAD ? ysrc : src, (long)gridDim.x / Hp * C * rowel * 2);
+      for (int e = threadIdx.x; e < 64 * 8; e += 256) {
+        const int cc = e >> 3, ch = e & 7;
+        const int c = c0 + cc, w0 = j0 + 8 * ch - left;
+        u32x4_t v = {0u, 0u, 0u, 0u};
+        if (c < C) {
+          const long o = (((long)n * C + c) * H + h) * W + w0;
+          if (w0 >= 0 && w0 + 8 <= W) {
+            v = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(o * 2), 0, 0));
+            if constexpr (GRAD) {
+              if (act != ACT_NONE) {
+                const u32x4_t yv =
+                    __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(ry, (unsigned)(o * 2), 0, 0));
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                  const unsigned short lo = f2bf(act_bwd(act, bf2f((unsigned short)(yv[u] & 0xFFFF)),
+                                                         bf2f((unsigned short)(v[u] & 0xFFFF))));
+                  const unsigned short hi = f2bf(act_bwd(act, bf2f((unsigned short)(yv[u] >> 16)),
+                                                         bf2f((unsigned short)(v[u] >> 16))));
+                  v[u] = (unsigned)lo | ((unsigned)hi << 16);
+                }
+              }
+            }
+          } else {
+            unsigned short e8[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+              const int w = w0 + t;
+              unsigned short x = 0;
+              if (w >= 0 && w < W) {
+                x = src[o + t];
+                if constexpr (GRAD) {
+                  if (act != ACT_NONE) x = f2bf(act_bwd(act, bf2f(ysrc[o + t]), bf2f(x)));
+                }
+              }
+              e8[t] = x;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = (unsigned)e8[2 * u] | ((unsigned)e8[2 * u + 1] << 16);
+          }
+        }
+        *reinterpret_cast<u32x4_t*>(&tile[cc][8 * ch]) = v;
+      }
+    } else {
+      for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+        const int cc = e >> 6, jj = e & 63;
+        const int c = c0 + cc, wd = j0 + jj - left, w = wd / dw;
+        unsigned short v = 0;
+        if (c < C && wd >= 0 && w * dw == wd && w < W) {
+          const long o = (((long)n * C + c) * H + h) * W + w;
+          v = src[o];
+          if constexpr (GRAD) {
+            if (act != ACT_NONE) v = f2bf(act_bwd(act, bf2f(ysrc[o]), bf2f(v)));
+          }
+        }
+        tile[cc][jj] = v;
+      }
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 512; e += 256) {
+    const int jj = e >> 3, cg = e & 7;
+    const int j = j0 + jj, c = c0 + 8 * cg;
+    if (j >= Wp || c >= Cp) continue;
+    u32x4_t o = {0u, 0u, 0u, 0u};
+    if (rowin) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        o[u] = (unsigned)tile[8 * cg + 2 * u][jj] | ((unsigned)tile[8 * cg + 2 * u + 1][jj] << 16);
+    }
+    *reinterpret_cast<u32x4_t*>(dst + (((long)n * Hp + i) * Wp + j) * Cp + c) = o;
+  }
+}
+
+// weight re-layouts: mode 0 (fwd)  out[k][(r*S+s)*Cp + c] = w[k][c][r][s]            (0 for c >= C)
+//                    mode 1 (dgrad) out[c][(r*S+s)*Kp + k] = w[k][c][R-1-r][S-1-s]    (0 for k >= K)
+__global__ void fm_cnhwc_wprep(const unsigned short* __restrict__ w, unsigned short* __restrict__ out,
+                               const float* __restrict__ g2, float* __restrict__ dw, int K, int C, int R, int S, int Cp,
+                               int Kp, int mode, int nsplit) {
+  const int RS = R * S;
+  const long total = mode == 0 ? (long)K * RS * Cp : mode == 1 ? (long)C * RS * Kp : (long)K * RS * Cp;
+  for (long o = blockIdx.x * 256L + threadIdx.x; o < total; o += (long)gridDim.x * 256) {
+    if (mode == 0) {
+      const int c = (int)(o % Cp);
+      const long t = o / Cp;
+      const int rs = (int)(t % RS), k = (int)(t / RS);
+      out[o] = c < C ? w[((long)k * C + c) * RS + rs] : (unsigned short)0;
+    } else if (mode == 1) {
+      const int k = (int)(o % Kp);
+      const long t = o / Kp;
+      const int rs = (int)(t % RS), c = (int)(t / RS);
+      const int r = rs / S, s = rs - r * S;
+      out[o] = k < K ? w[((long)k * C + c) * RS + (R - 1 - r) * S + (S - 1 - s)] : (unsigned short)0;
+    }
+  }
+}
+
+PixG make_pix(int PQ, int Q, int Hp, int Wp, int Cp, int sh, int sw, int oh, int ow) {
+  PixG g;
+  g.dPQ = make_fastdiv(PQ);
+  g.dQ = make_fastdiv(Q);
+  g.PQ = PQ; g.Q = Q; g.Hp = Hp; g.Wp = Wp; g.Cp = Cp;
+  g.sh = sh; g.sw = sw; g.oh = oh; g.ow = ow;
+  return g;
+}
+
+TapG make_tap(int Cp, int S, int Wp) {
+  TapG t;
+  t.C8 = Cp / 8;
+  t.dC8 = make_fastdiv(t.C8);
+  t.S = S;
+  t.dS = make_fastdiv(S);
+  t.Wp = Wp;
+  t.Cp = Cp;
+  return t;
+}
+
+// wgrad fold: dw[k][c][r][s] += sum_z g2[z][k][(r*S+s)*Cp + c] over the split-K slabs.  Block = 32
+// consecutive slab elements x 8 split groups (coalesced 128-B slab reads, the split sum reduced in
+// LDS) -- hundreds of splits stay parallel instead of one serial loop per output.
+__global__ void __launch_bounds__(256) fm_cnhwc_fold(const float* __restrict__ g2, float* __restrict__ dw, int K, int C, int RS,
+                                                     int Cp, int nsplit) {
+  __shared__ float red[8][33];
+  const long slab = (long)K * RS * Cp;
+  const int ol = threadIdx.x & 31, zg = threadIdx.x >> 5;
+  const long o = blockIdx.x * 32L + ol;
+  float acc = 0.f;
+  if (o < slab)
+    for (int z = zg; z < nsplit; z += 8) acc += g2[z * slab + o];
+  red[zg][ol] = acc;
+  __syncthreads();
+  if (threadIdx.x < 32 && o < slab) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) t += red[g][ol];
+    const int c = (int)(o % Cp);
+    if (c < C) {
+      const long q = o / Cp;
+      const int rs = (int)(q % RS), k = (int)(q / RS);
+      dw[((long)k * C + c) * RS + rs] += t;
+    }
+  }
+}
+
+// launch plan: tile shape (0: 128x128 / 8 waves, 1: 64x128, 2: 64x64 / 4 waves), tiles, k split.
+// 128x128 when it still gives >= 256 tiles (or wgrad, which splits K), else the smaller tiles
+// that fill the 256 CUs.  wgrad splits its long pixel reduction until ~2 blocks per CU; the
+// splits write fp32 slabs [ksplit][M][N] that fm_cnhwc_wprep mode 2 sums while folding.
+struct Plan {
+  int shape, tiles_m, tiles_n, ksplit, kt_per;
+};
+
+Plan make_plan(int mode, int M, int N, int K) {
+  auto tiles = [&](int bm, int bn) { return (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
+  Plan q;
+  if (M > 64 && (mode == CN_WGRAD || tiles(128, 128) >= 256)) q.shape = 0;
+  else if (mode == CN_WGRAD || tiles(64, 128) >= 256) q.shape = 1;
+  else q.shape = 2;
+  const int bm = q.shape == 0 ? 128 : 64, bn = q.shape == 2 ? 64 : 128;
+  q.tiles_m = (M + bm - 1) / bm;
+  q.tiles_n = (N + bn - 1) / bn;
+  const int ktiles = (K + BK - 1) / BK;
+  int ks = 1;
+  if (mode == CN_WGRAD) ks = std::max(1, std::min(512 / std::max(q.tiles_m * q.tiles_n, 1), ktiles / 4));
+  q.kt_per = (ktiles + ks - 1) / ks;
+  q.ksplit = (ktiles + q.kt_per - 1) / q.kt_per;
+  return q;
+}
+
+template <int BM, int BN, int MODE, int NTH>
+void go(ConvN& p, const Plan& q, hipStream_t s) {
+  p.tiles_m = q.tiles_m;
+  p.tiles_n = q.tiles_n;
+  p.ksplit = q.ksplit;
+  p.kt_per = q.kt_per;
+  const int lds = 2 * (BM + BN) * BK * 2;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)fm_conv_nhwc<BM, BN, MODE, NTH>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((fm_conv_nhwc<BM, BN, MODE, NTH>), dim3(p.tiles_m * p.tiles_n, 1, p.ksplit), dim3(NTH), lds, s, p);
+}
+
+template <int MODE>
+int dispatch(ConvN& p, hipStream_t s) {
+  const Plan q = make_plan(MODE, p.M, p.N, p.K);
+  if (q.shape == 0) go<128, 128, MODE, 512>(p, q, s);
+  else if (q.shape == 1) go<64, 128, MODE, 256>(p, q, s);
+  else go<64, 64, MODE, 256>(p, q, s);
+  return q.ksplit;
+}
+
+}  // namespace
+
+// stage src [N][C][H][W] (bf16) into dst [N][Hp][Wp][Cp] at (top, left), zeros elsewhere
+extern "C" void fm_nhwc_stage_run(const void* src, void* dst, int N, int C, int H, int W, int Cp, int Hp, int Wp, int top,
+                                  int left, int dh, int dw, hipStream_t s) {
+  dim3 grid(N * Hp, (Wp + 63) / 64, (Cp + 63) / 64);
+  hipLaunchKernelGGL(fm_nhwc_stage<false>, grid, dim3(256), 0, s, (const unsigned short*)src, nullptr, (unsigned short*)dst,
+                     ACT_NONE, C, H, W, Cp, Hp, Wp, top, left, dh, dw);
+}
+
+// gradient staging: dst = stage(act'(y) * dy) (y unused when act == none)
+extern "C" void fm_nhwc_stage_grad_run(const void* dy, const void* y, void* dst, int act, int N, int C, int H, int W, int Cp,
+                                       int Hp, int Wp, int top, int left, int dh, int dw, hipStream_t s) {
+  dim3 grid(N * Hp, (Wp + 63) / 64, (Cp + 63) / 64);
+  hipLaunchKernelGGL(fm_nhwc_stage<true>, grid, dim3(256), 0, s, (const unsigned short*)dy, (const unsigned short*)y,
+                     (unsigned short*)dst, act, C, H, W, Cp, Hp, Wp, top, left, dh, dw);
+}
+
+extern "C" void fm_cnhwc_wprep_run(const void* w, void* out, const float* g2, float* dw, int K, int C, int R, int S, int Cp,
+                                   int Kp, int mode, int nsplit, hipStream_t s) {
+  if (mode == 2) {
+    const long slab = (long)K * R * S * Cp;
+    hipLaunchKernelGGL(fm_cnhwc_fold, dim3((unsigned)((slab + 31) / 32)), dim3(256), 0, s, g2, dw, K, C, R * S, Cp, nsplit);
+    return;
+  }
+  const long total = mode == 0 ? (long)K * R * S * Cp : (long)C * R * S * Kp;
+  hipLaunchKernelGGL(fm_cnhwc_wprep, dim3(fm_grid(total, 256, 1024)), dim3(256), 0, s, (const unsigned short*)w,
+                     (unsigned short*)out, g2, dw, K, C, R, S, Cp, Kp, mode, nsplit);
+}
+
+// fp32 floats of the wgrad split-K slab workspace for these sizes (ksplit * K * R*S*Cp)
+extern "C" long fm_conv_nhwc_wgrad_ws(int N, int K, int P, int Q, int R, int S, int Cp) {
+  const Plan q = make_plan(CN_WGRAD, K, R * S * Cp, N * P * Q);
+  return (long)q.ksplit * K * R * S * Cp;
+}
+
+// fwd: xs staged [N][Hp][Wp][Cp] (window origin of output (p, q) at row p*sh, col q*sw),
+// wf [K][R*S*Cp] (mode 0), y [N][K][P][Q] bf16, bias fp32 [K] or null
+extern "C" void fm_conv_nhwc_fwd(const void* xs, long xs_bytes, const void* wf, const float* bias, void* y, int N, int K,
+                                 int P, int Q, int R, int S, int Cp, int Hp, int Wp, int sh, int sw, int act, hipStream_t s) {
+  ConvN p{};
+  p.A = (const unsigned short*)wf; p.a_bytes = (long)K * R * S * Cp * 2;
+  p.B = (const unsigned short*)xs; p.b_bytes = xs_bytes;
+  p.out = y; p.bias = bias; p.act = act;
+  p.M = K; p.N = N * P * Q; p.K = R * S * Cp;
+  p.npix = p.N;
+  p.gb = make_pix(P * Q, Q, Hp, Wp, Cp, sh, sw, 0, 0);
+  p.tb = make_tap(Cp, S, Wp);
+  p.OPQ = P * Q; p.dOPQ = make_fastdiv(P * Q);
+  dispatch<CN_FWD>(p, s);
+}
+
+// dgrad: gs staged G [N][Hg][Wg][Kp] with G at (R-1-pt, S-1-pl) dilated by the stride, wd [C][R*S*Kp] (mode 1),
+// dx [N][C][H][W] bf16 (accum: +=)
+extern "C" void fm_conv_nhwc_dgrad(const void* gs, long gs_bytes, const void* wd, void* dx, int accum, int N, int C, int H,
+                                   int W, int R, int S, int Kp, int Hg, int Wg, hipStream_t s) {
+  ConvN p{};
+  p.A = (const unsigned short*)wd; p.a_bytes = (long)C * R * S * Kp * 2;
+  p.B = (const unsigned short*)gs; p.b_bytes = gs_bytes;
+  p.out = dx; p.accum = accum;
+  p.M = C; p.N = N * H * W; p.K = R * S * Kp;
+  p.npix = p.N;
+  p.gb = make_pix(H * W, W, Hg, Wg, Kp, 1, 1, 0, 0);
+  p.tb = make_tap(Kp, S, Wg);
+  p.OPQ = H * W; p.dOPQ = make_fastdiv(H * W);
+  dispatch<CN_DGRAD>(p, s);
+}
+
+// wgrad: g2 fp32 slabs [ksplit][K][R*S*Cp] (fm_conv_nhwc_wgrad_ws floats; returns ksplit) = sum over output pixels of
+// Gs[orgG + k] * Xs[orgX + tap]; gs staged G [N][Hg][Wg][Kp], pixel (p, q) at (gt + p*gsh, gl + q*gsw)
+// (gsh, gsw > 1: the stride-dilated G of the data gradient); xs as in fwd; ptab: int scratch of
+// 2 * N*P*Q entries (the pass's pixel origin table)
+extern "C" int fm_conv_nhwc_wgrad(const void* gs, long gs_bytes, const void* xs, long xs_bytes, float* g2, float* db, int N,
+                                  int K, int Kp, int P, int Q, int Hg, int Wg, int gt, int gl, int gsh, int gsw, int R, int S,
+                                  int Cp, int Hp, int Wp, int sh, int sw, int* ptab, hipStream_t s) {
+  ConvN p{};
+  p.A = (const unsigned short*)gs; p.a_bytes = gs_bytes;
+  p.B = (const unsigned short*)xs; p.b_bytes = xs_bytes;
+  p.out = g2;
+  p.M = K; p.Mp = Kp; p.N = R * S * Cp; p.K = N * P * Q;
+  p.npix = p.K;
+  p.ga = make_pix(P * Q, Q, Hg, Wg, Kp, gsh, gsw, gt, gl);
+  p.gb = make_pix(P * Q, Q, Hp, Wp, Cp, sh, sw, 0, 0);
+  p.tb = make_tap(Cp, S, Wp);
+  p.ptab = ptab;
+  p.db = db;
+  hipLaunchKernelGGL(fm_pix_table, dim3(fm_grid(p.npix, 256, 2048)), dim3(256), 0, s, ptab, p.npix, p.ga, p.gb);
+  return dispatch<CN_WGRAD>(p, s);
+}

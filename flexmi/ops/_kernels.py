@@ -439,6 +439,9 @@ def conv2d_forward(x, w, b, y, stride, pads, act, groups, saved=None):
     Strided stems on few channels go through space-to-depth onto the stride-1 pixel-vector path."""
     assert groups == 1, "grouped convolution is not supported on the HIP path"
     w = w.contiguous()
+    if _nhwc_ok(x, w, groups):
+        _nhwc_forward(x, w, b, y, stride, pads, act, saved)
+        return
     plan = _s2d_plan(x, w, y, stride)
     if plan is not None:
         xs, ws = _s2d_operands(x, w, plan, pads, saved)
@@ -468,6 +471,8 @@ def conv2d_backward(x, w, y, dy, dx, dw, db, stride, pads, act, groups, acc, sav
     dW += G (x) X and dX (+)= Wt (x) G as implicit GEMMs -- no columns, no transposes."""
     assert groups == 1, "grouped convolution is not supported on the HIP path"
     w = w.contiguous()
+    if _nhwc_ok(x, w, groups) and _nhwc_backward(x, w, y, dy, int(act), db, dx, dw, stride, pads, acc, saved):
+        return
     g = dy
     if int(act) != 10 or db is not None:
         g = scratch(x.device, "conv_g", dy.numel(), dy.dtype).view(dy.shape) if int(act) != 10 else dy
@@ -560,6 +565,96 @@ def _conv_backward_phases(x, w, g, dx, dw, s_, pads, acc):
             wt = scratch(dev, "conv_wt", C().conv_scratch(Cin, Kout * nr * nt), w.dtype)
             C().conv_dgrad(g, wsub, wt, dxa, 1, 1, oa, ob, False)
             _strided(dxa, dx, box, (Cin * Ha * Wb, Ha * Wb, Wb, 1), xstr, 0, a * W + b, acc)
+
+
+# FM_CONV_NHWC=1/0 (default 1): bf16 convolutions on >= 16 input channels run on the NHWC-staged
+# implicit GEMM (csrc/kernels/conv_nhwc.hip): the image operand is re-laid ONCE per pass into a
+# zero-padded NHWC copy, so every 16-B operand chunk of the GEMM is 8 channels of one pixel (no
+# per-element gather math, no halo masks).  The forward's staged input is kept in ``saved`` for
+# the weight gradient.  Stems on few channels keep the NCHW kernels (space-to-depth).
+NHWC_CONV = os.environ.get("FM_CONV_NHWC", "1") != "0"
+
+
+def _r8(v):
+    return (v + 7) // 8 * 8
+
+
+def _nhwc_ok(x, w, groups):
+    return NHWC_CONV and groups == 1 and x.dtype == torch.bfloat16 and w.shape[1] >= 16
+
+
+def _nhwc_stage_x(x, w, y, stride, pads, saved):
+    """Stage x into its zero-padded NHWC window image [N][Hp][Wp][Cp] (output (p, q) reads rows
+    p*sh .. p*sh+R-1); kept in ``saved`` (one buffer per op) for the backward."""
+    N, Cin = x.shape[0], x.shape[1]
+    R, S = w.shape[2], w.shape[3]
+    P, Q = y.shape[2], y.shape[3]
+    Cp, Hp, Wp = _r8(Cin), (P - 1) * stride[0] + R, (Q - 1) * stride[1] + S
+    shp = (N, Hp, Wp, Cp)
+    if saved is not None:
+        xs = saved.get("nhwc_x")
+        if xs is None or tuple(xs.shape) != shp or xs.device != x.device:
+            xs = torch.empty(shp, dtype=x.dtype, device=x.device)
+            saved["nhwc_x"] = xs
+    else:
+        xs = scratch(x.device, "cn_xs", N * Hp * Wp * Cp, x.dtype).view(shp)
+    C().nhwc_stage(x, xs, Cp, Hp, Wp, pads[0], pads[2], 1, 1)
+    return xs, Cp, Hp, Wp
+
+
+def _nhwc_forward(x, w, b, y, stride, pads, act, saved):
+    Kout, Cin, R, S = w.shape
+    xs, Cp, Hp, Wp = _nhwc_stage_x(x, w, y, stride, pads, saved)
+    if saved is not None:
+        saved["nhwc_x_ready"] = True
+    wf = scratch(x.device, "cn_wf", Kout * R * S * Cp, w.dtype)
+    C().cnhwc_wprep(w, wf, w, w, Cp, _r8(Kout), 0, 1)
+    C().conv_nhwc_fwd(xs, wf, b, y, R, S, Cp, Hp, Wp, stride[0], stride[1], int(act))
+
+
+def _nhwc_backward(x, w, y, dy, act, db, dx, dw, stride, pads, acc, saved):
+    """Weight gradient (and, for any stride, the data gradient) on the NHWC-staged kernels.
+    G = act'(y) * dY is staged once (the bias gradient db (+)= sum G is summed by the wgrad kernel):
+    placed at (R-1-pt, S-1-pl) and dilated by the stride when dX is needed (the data gradient is
+    then a stride-1 convolution of the flipped kernel over it), unpadded otherwise.  Returns False
+    (nothing done; the caller falls back) when the layout is outside what the staging supports."""
+    N, Cin, H, W = x.shape
+    Kout, _, R, S = w.shape
+    P, Q = dy.shape[2], dy.shape[3]
+    sh, sw = stride
+    pt, pl = pads[0], pads[2]
+    Kp = _r8(Kout)
+    dev = x.device
+    if dx is not None:
+        gt, gl = R - 1 - pt, S - 1 - pl
+        if gt < 0 or gl < 0:
+            return False
+        Hg = max(H + R - 1, gt + (P - 1) * sh + 1)
+        Wg = max(W + S - 1, gl + (Q - 1) * sw + 1)
+        dh, dwl = sh, sw
+    else:
+        gt = gl = 0
+        Hg, Wg, dh, dwl = P, Q, 1, 1
+    gs = scratch(dev, "cn_gs", N * Hg * Wg * Kp, dy.dtype).view(N, Hg, Wg, Kp)
+    C().nhwc_stage_grad(dy, y, gs, act, Kp, Hg, Wg, gt, gl, dh, dwl)
+    if saved is not None and saved.get("nhwc_x_ready") and "nhwc_x" in saved:
+        xs = saved["nhwc_x"]
+        Cp, Hp, Wp = xs.shape[3], xs.shape[1], xs.shape[2]
+    else:
+        # no forward staging to reuse (eager backward without a saved context): stage again
+        xs, Cp, Hp, Wp = _nhwc_stage_x(x, w, dy, stride, pads, None)
+    # weight gradient: fp32 [K][R*S*Cp] over the output pixels; in a dilated G, pixel (p, q) sits at
+    # (gt + p*sh, gl + q*sw)
+    # (split-K fp32 slabs summed by the fold into dW[K,C,R,S]; db (+)= sum G from the same kernel)
+    g2 = scratch(dev, "cn_g2", C().conv_nhwc_wgrad_ws(N, Kout, P, Q, R, S, Cp), torch.float32)
+    ptab = scratch(dev, "cn_ptab", 2 * N * P * Q, torch.int32)
+    nsplit = C().conv_nhwc_wgrad(gs, xs, g2, db, N, Kout, Kp, P, Q, Hg, Wg, gt, gl, dh, dwl, R, S, Cp, Hp, Wp, sh, sw, ptab)
+    C().cnhwc_wprep(w, w, g2, dw.view(-1), Cp, Kp, 2, nsplit)
+    if dx is not None:
+        wd = scratch(dev, "cn_wd", Cin * R * S * Kp, w.dtype)
+        C().cnhwc_wprep(w, wd, w, w, _r8(Cin), Kp, 1, 1)
+        C().conv_nhwc_dgrad(gs, wd, dx, R, S, Kp, Hg, Wg, bool(acc))
+    return True
 
 
 def _pool_code(saved, y):

@@ -41,12 +41,18 @@ def list_image_folder(root):
 
 def nearest_resize_hwc(img: np.ndarray, height: int, width: int) -> np.ndarray:
     """The reference's nearest-neighbour sampling (``model.cu:56-74``): source row
-    ``min(round(y * oh / h), oh - 1)`` and column likewise; HWC in, HWC out."""
+    ``min(roundf(y * scale), oh - 1)`` with a float32 ``scale = oh / h`` and roundf's half-away-
+    from-zero rounding (not numpy's half-to-even), column likewise; HWC in, HWC out."""
     oh, ow = img.shape[:2]
     if (oh, ow) == (height, width):
         return img
-    ys = np.minimum(np.rint(np.arange(height) * (oh / height)).astype(np.int64), oh - 1)
-    xs = np.minimum(np.rint(np.arange(width) * (ow / width)).astype(np.int64), ow - 1)
+
+    def src(n_out, n_in):
+        scale = np.float32(n_in) / np.float32(n_out)
+        pos = np.arange(n_out, dtype=np.float32) * scale
+        return np.minimum(np.floor(pos + np.float32(0.5)).astype(np.int64), n_in - 1)
+
+    ys, xs = src(height, oh), src(width, ow)
     return img[ys[:, None], xs[None, :]]
 
 

@@ -35,9 +35,10 @@ def test_list_and_decode(tmp_path):
     assert img.shape == (8, 12, 3) and img.dtype == np.uint8
     from PIL import Image
     full = np.asarray(Image.open(files[0]).convert("RGB"))
-    # reference sampling: row round(y * 20/8) clamped, column round(x * 30/12) clamped
+    # reference sampling: row roundf(y * 20/8) clamped, column roundf(x * 30/12) clamped
+    # (half away from zero: x = 5 -> 12.5 -> 13)
     for y, x in [(0, 0), (3, 5), (7, 11)]:
-        sy, sx = min(int(np.rint(y * 20 / 8)), 19), min(int(np.rint(x * 30 / 12)), 29)
+        sy, sx = min(int(np.floor(y * 20 / 8 + 0.5)), 19), min(int(np.floor(x * 30 / 12 + 0.5)), 29)
         assert (img[y, x] == full[sy, sx]).all()
 
 
@@ -86,3 +87,22 @@ def test_normalize_hip(gpu, dt, W):
     ref = _ref_normalize(u8.cpu())
     tol = 1e-6 if dt == torch.float32 else 8e-3
     torch.testing.assert_close(out.double().cpu(), ref, rtol=tol, atol=tol)
+
+
+def test_nearest_resize_rounds_half_away_from_zero():
+    # 5 -> 2 columns / rows: scale 2.5, output 1 samples source 2.5 exactly.  The reference's
+    # roundf (model.cu:64-66) picks 3; numpy's rint (half to even) would pick 2.
+    img = np.arange(5 * 5 * 3, dtype=np.uint8).reshape(5, 5, 3)
+    out = I.nearest_resize_hwc(img, 2, 2)
+
+    def ref_idx(n_out, n_in):
+        scale = np.float32(n_in) / np.float32(n_out)
+        return [min(int(np.floor(np.float32(i) * scale + np.float32(0.5))), n_in - 1) for i in range(n_out)]
+
+    ys, xs = ref_idx(2, 5), ref_idx(2, 5)
+    assert ys == [0, 3]
+    np.testing.assert_array_equal(out, img[np.ix_(ys, xs)])
+    # a generic shrink/enlarge keeps the min(.., n-1) clamp
+    big = I.nearest_resize_hwc(img, 7, 11)
+    assert big.shape == (7, 11, 3)
+    np.testing.assert_array_equal(big[-1, -1], img[4, 4])

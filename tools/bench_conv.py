@@ -31,12 +31,15 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="", help="fwd / dgrad / wgrad")
     ap.add_argument("--layer", default="", help="one layer name (e.g. conv2)")
+    ap.add_argument("--path", default="raw", choices=["raw", "op"],
+                    help="raw: the NCHW kernels (fwd / dgrad / wgrad); op: the framework's conv2d_forward / "
+                         "conv2d_backward as dispatched (NHWC staging included; bwd = dgrad + wgrad + act/bias)")
     a = ap.parse_args()
     import torch
     from flexmi.ops import _kernels as K
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     layers = sum((NETS[n] for n in (NETS if a.net == "all" else [a.net])), [])
-    tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
+    tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0, "bwd": 0.0}
     for name, N, C, H, W, Ko, R, S, st, pd in layers:
         if a.layer and name != a.layer:
             continue
@@ -54,11 +57,19 @@ def main():
         C_ = K.C()
         wt = K.scratch(x.device, "bench_wt", C_.conv_scratch(C, Ko * R * S), dt)
         wp = K.scratch(x.device, "bench_wp", C_.conv_scratch(Ko, C * R * S), dt)
-        runs = {
-            "fwd": lambda: C_.conv_fwd(x, w, wp, b, y, st, st, pd, pd, 11),
-            "dgrad": lambda: C_.conv_dgrad(dy, w, wt, dx, st, st, pd, pd, False),
-            "wgrad": lambda: C_.conv_wgrad(dy, x, dw.view(-1), R, S, st, st, pd, pd),
-        }
+        if a.path == "raw":
+            runs = {
+                "fwd": lambda: C_.conv_fwd(x, w, wp, b, y, st, st, pd, pd, 11),
+                "dgrad": lambda: C_.conv_dgrad(dy, w, wt, dx, st, st, pd, pd, False),
+                "wgrad": lambda: C_.conv_wgrad(dy, x, dw.view(-1), R, S, st, st, pd, pd),
+            }
+        else:
+            saved = {}
+            db = torch.zeros(Ko, device="cuda")
+            runs = {
+                "fwd": lambda: K.conv2d_forward(x, w, b, y, (st, st), pads, 11, 1, saved),
+                "bwd": lambda: K.conv2d_backward(x, w, y, dy, dx, dw, db, (st, st), pads, 11, 1, False, saved),
+            }
         line = f"{name:8s} N{N} C{C} {H}x{W} K{Ko} {R}x{S}/{st}:"
         for k, fn in runs.items():
             if a.only and k != a.only:
@@ -73,7 +84,8 @@ def main():
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / a.reps
             tot[k] += us
-            line += f"  {k} {us:8.1f} us {flop / us / 1e6:6.1f} TF"
+            fl = 2 * flop if k == "bwd" else flop
+            line += f"  {k} {us:8.1f} us {fl / us / 1e6:6.1f} TF"
         print(line, flush=True)
     print("total us:", {k: round(v, 1) for k, v in tot.items()}, flush=True)
 
