@@ -69,9 +69,9 @@ void fm_loss_fwd_bwd(const void* logits, int logits_bf16, const void* labels, vo
 void fm_unary_forward(int code, const void* x, void* y, long n, int bf16, hipStream_t s);
 void fm_unary_backward(int code, const void* x, const void* y, const void* dy, void* dx, long n, int acc, int bf16,
                        hipStream_t s);
-void fm_binary_forward(int code, const void* a, const void* b, void* y, long n, int bf16, hipStream_t s);
-void fm_binary_backward(int code, const void* a, const void* b, const void* dy, void* da, void* db, long n, int acca,
-                        int accb, int bf16, hipStream_t s);
+void fm_binary_forward(int code, const void* a, const void* b, void* y, long n, int relu, int bf16, hipStream_t s);
+void fm_binary_backward(int code, const void* a, const void* b, const void* dy, const void* ymask, void* da, void* db,
+                        long n, int acca, int accb, int bf16, hipStream_t s);
 void fm_act_bwd_bias(const void* y, const void* dy, void* dpre, float* db, long B, int N, int act, int bf16, hipStream_t s);
 void fm_multi_copy2d(int n, const void* const* src, void* const* dst, const long* rows, const long* cols, const long* lds,
                      const long* ldd, int add_mask, int elem_bytes, hipStream_t s);
@@ -116,15 +116,15 @@ void fm_nhwc_stage_run(const void* src, void* dst, int N, int C, int H, int W, i
 void fm_nhwc_stage_grad_run(const void* dy, const void* y, void* dst, int act, int N, int C, int H, int W, int Cp, int Hp,
                             int Wp, int top, int left, int dh, int dw, hipStream_t s);
 long fm_conv_nhwc_wgrad_ws(int N, int K, int P, int Q, int R, int S, int Cp);
-void fm_cnhwc_wprep_run(const void* w, void* out, const float* g2, float* dw, int K, int C, int R, int S, int Cp, int Kp,
-                        int mode, int nsplit, hipStream_t s);
+void fm_cnhwc_wprep_run(const void* w, void* out, void* out2, const float* g2, float* dw, int K, int C, int R, int S, int Cp,
+                        int Kp, int mode, int nsplit, hipStream_t s);
 void fm_conv_nhwc_fwd(const void* xs, long xs_bytes, const void* wf, const float* bias, void* y, int N, int K, int P, int Q,
                       int R, int S, int Cp, int Hp, int Wp, int sh, int sw, int act, hipStream_t s);
 void fm_conv_nhwc_dgrad(const void* gs, long gs_bytes, const void* wd, void* dx, int accum, int N, int C, int H, int W, int R,
                         int S, int Kp, int Hg, int Wg, hipStream_t s);
 int fm_conv_nhwc_wgrad(const void* gs, long gs_bytes, const void* xs, long xs_bytes, float* g2, float* db, int N, int K, int Kp, int P,
                         int Q, int Hg, int Wg, int gt, int gl, int gsh, int gsw, int R, int S, int Cp, int Hp, int Wp, int sh,
-                        int sw, int* ptab, hipStream_t s);
+                        int sw, int* ptab, int build_tab, hipStream_t s);
 void fm_lstm_init(const void* h0, const void* c0, void* hprev, long ldhp, float* cinit, int B, int H, int bf16, hipStream_t s);
 void fm_lstm_cell_fwd(float* G, long ldg, const float* c_prev, long ldcp, float* c_out, long ldc, void* y, long ldy,
                       void* hprev_next, long ldhp, void* hT, void* cT, int B, int H, int bf16, hipStream_t s);
@@ -541,13 +541,19 @@ void unary_fwd(int64_t code, torch::Tensor x, torch::Tensor y) { fm_unary_forwar
 void unary_bwd(int64_t code, torch::Tensor x, torch::Tensor y, torch::Tensor dy, torch::Tensor dx, bool acc) {
   fm_unary_backward((int)code, x.data_ptr(), y.data_ptr(), dy.data_ptr(), dx.data_ptr(), x.numel(), acc, is_bf16(x), cur());
 }
-void binary_fwd(int64_t code, torch::Tensor a, torch::Tensor b, torch::Tensor y) {
-  fm_binary_forward((int)code, a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), is_bf16(a), cur());
+// relu: y = relu(a op b); ymask (backward): the incoming gradient is zeroed where ymask <= 0
+void binary_fwd(int64_t code, torch::Tensor a, torch::Tensor b, torch::Tensor y, bool relu) {
+  TORCH_CHECK(a.numel() == b.numel() && a.numel() == y.numel() && a.scalar_type() == b.scalar_type() &&
+                  a.scalar_type() == y.scalar_type(), "binary_fwd: same-size same-dtype operands");
+  fm_binary_forward((int)code, a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), relu ? 1 : 0, is_bf16(a), cur());
 }
-void binary_bwd(int64_t code, torch::Tensor a, torch::Tensor b, torch::Tensor dy, c10::optional<torch::Tensor> da,
-                c10::optional<torch::Tensor> db, bool acca, bool accb) {
-  fm_binary_backward((int)code, a.data_ptr(), b.data_ptr(), dy.data_ptr(), mptr(da), mptr(db), a.numel(), acca, accb, is_bf16(a),
-                     cur());
+void binary_bwd(int64_t code, torch::Tensor a, torch::Tensor b, torch::Tensor dy, c10::optional<torch::Tensor> ymask,
+                c10::optional<torch::Tensor> da, c10::optional<torch::Tensor> db, bool acca, bool accb) {
+  TORCH_CHECK(dy.numel() == a.numel() && dy.numel() == b.numel() && dy.scalar_type() == a.scalar_type(), "binary_bwd: operands");
+  if (ymask.has_value() && ymask->defined())
+    TORCH_CHECK(ymask->numel() == dy.numel() && ymask->scalar_type() == dy.scalar_type(), "binary_bwd: ymask");
+  fm_binary_backward((int)code, a.data_ptr(), b.data_ptr(), dy.data_ptr(), cptr(ymask), mptr(da), mptr(db), a.numel(), acca,
+                     accb, is_bf16(a), cur());
 }
 void act_bwd_bias(torch::Tensor y, torch::Tensor dy, c10::optional<torch::Tensor> dpre, c10::optional<torch::Tensor> db,
                   int64_t B, int64_t N, int64_t act) {
@@ -759,18 +765,20 @@ void nhwc_stage_grad(torch::Tensor dy, torch::Tensor y, torch::Tensor dst, int64
 int64_t conv_nhwc_wgrad_ws(int64_t N, int64_t K, int64_t P, int64_t Q, int64_t R, int64_t S, int64_t Cp) {
   return fm_conv_nhwc_wgrad_ws((int)N, (int)K, (int)P, (int)Q, (int)R, (int)S, (int)Cp);
 }
-// mode 0: out = fwd weight matrix [K][R*S*Cp]; 1: dgrad matrix [C][R*S*Kp]; 2: dw (fp32 [K,C,R,S]) += fold(g2)
-void cnhwc_wprep(torch::Tensor w, torch::Tensor out, torch::Tensor g2, torch::Tensor dw, int64_t Cp, int64_t Kp, int64_t mode,
-                 int64_t nsplit) {
-  TORCH_CHECK(nsplit >= 1, "cnhwc_wprep: nsplit >= 1");
+// mode 0: out = fwd weight matrix [K][R*S*Cp]; 1: dgrad matrix [C][R*S*Kp]; 3: both (out, out2);
+// 2: dw (fp32 [K,C,R,S]) += fold(g2 slabs)
+void cnhwc_wprep(torch::Tensor w, torch::Tensor out, torch::Tensor out2, torch::Tensor g2, torch::Tensor dw, int64_t Cp,
+                 int64_t Kp, int64_t mode, int64_t nsplit) {
+  TORCH_CHECK(nsplit >= 1 && mode >= 0 && mode <= 3, "cnhwc_wprep: mode 0..3, nsplit >= 1");
   TORCH_CHECK(w.dim() == 4, "cnhwc_wprep: w [K,C,R,S]");
   const long K = w.size(0), C = w.size(1), RS = w.size(2) * w.size(3);
   TORCH_CHECK(Cp % 8 == 0 && Cp >= C && Kp % 8 == 0 && Kp >= K, "cnhwc_wprep: padded channel counts");
-  if (mode == 0 || mode == 1) {
+  if (mode != 2) {
     nhwc_chk(w, K * C * RS, "cnhwc_wprep w");
-    nhwc_chk(out, mode == 0 ? K * RS * Cp : C * RS * Kp, "cnhwc_wprep out");
+    if (mode == 0 || mode == 3) nhwc_chk(out, K * RS * Cp, "cnhwc_wprep out (fwd matrix)");
+    if (mode == 1) nhwc_chk(out, C * RS * Kp, "cnhwc_wprep out (dgrad matrix)");
+    if (mode == 3) nhwc_chk(out2, C * RS * Kp, "cnhwc_wprep out2 (dgrad matrix)");
   } else {
-    TORCH_CHECK(mode == 2, "cnhwc_wprep: mode 0/1/2");
     check_cuda(g2, "g2");
     check_cuda(dw, "dw");
     TORCH_CHECK(g2.scalar_type() == torch::kFloat32 && g2.is_contiguous() && g2.numel() >= nsplit * K * RS * Cp,
@@ -778,9 +786,9 @@ void cnhwc_wprep(torch::Tensor w, torch::Tensor out, torch::Tensor g2, torch::Te
     TORCH_CHECK(dw.scalar_type() == torch::kFloat32 && dw.is_contiguous() && dw.numel() == K * C * RS,
                 "cnhwc_wprep: fp32 dw [K*C*R*S]");
   }
-  fm_cnhwc_wprep_run(w.data_ptr(), mode == 2 ? nullptr : out.data_ptr(), mode == 2 ? g2.data_ptr<float>() : nullptr,
-                     mode == 2 ? dw.data_ptr<float>() : nullptr, (int)K, (int)C, (int)w.size(2), (int)w.size(3), (int)Cp,
-                     (int)Kp, (int)mode, (int)nsplit, cur());
+  fm_cnhwc_wprep_run(w.data_ptr(), mode == 2 ? nullptr : out.data_ptr(), mode == 3 ? out2.data_ptr() : nullptr,
+                     mode == 2 ? g2.data_ptr<float>() : nullptr, mode == 2 ? dw.data_ptr<float>() : nullptr, (int)K, (int)C,
+                     (int)w.size(2), (int)w.size(3), (int)Cp, (int)Kp, (int)mode, (int)nsplit, cur());
 }
 void conv_nhwc_fwd(torch::Tensor xs, torch::Tensor wf, c10::optional<torch::Tensor> bias, torch::Tensor y, int64_t R,
                    int64_t S, int64_t Cp, int64_t Hp, int64_t Wp, int64_t sh, int64_t sw, int64_t act) {
@@ -811,7 +819,7 @@ void conv_nhwc_dgrad(torch::Tensor gs, torch::Tensor wd, torch::Tensor dx, int64
 }
 int64_t conv_nhwc_wgrad(torch::Tensor gs, torch::Tensor xs, torch::Tensor g2, c10::optional<torch::Tensor> db, int64_t N, int64_t K, int64_t Kp, int64_t P,
                      int64_t Q, int64_t Hg, int64_t Wg, int64_t gt, int64_t gl, int64_t gsh, int64_t gsw, int64_t R, int64_t S,
-                     int64_t Cp, int64_t Hp, int64_t Wp, int64_t sh, int64_t sw, torch::Tensor ptab) {
+                     int64_t Cp, int64_t Hp, int64_t Wp, int64_t sh, int64_t sw, torch::Tensor ptab, bool build_tab) {
   TORCH_CHECK(Kp % 8 == 0 && Kp >= K && Cp % 8 == 0 && gt >= 0 && gl >= 0 && gsh >= 1 && gsw >= 1 &&
                   gt + (P - 1) * gsh < Hg && gl + (Q - 1) * gsw < Wg &&
                   (P - 1) * sh + R <= Hp && (Q - 1) * sw + S <= Wp,
@@ -834,7 +842,7 @@ int64_t conv_nhwc_wgrad(torch::Tensor gs, torch::Tensor xs, torch::Tensor g2, c1
               "conv_nhwc_wgrad: int32 ptab[2*N*P*Q]");
   return fm_conv_nhwc_wgrad(gs.data_ptr(), gs.numel() * 2, xs.data_ptr(), xs.numel() * 2, g2.data_ptr<float>(), dbp, (int)N, (int)K,
                      (int)Kp, (int)P, (int)Q, (int)Hg, (int)Wg, (int)gt, (int)gl, (int)gsh, (int)gsw, (int)R, (int)S, (int)Cp,
-                     (int)Hp, (int)Wp, (int)sh, (int)sw, ptab.data_ptr<int>(), cur());
+                     (int)Hp, (int)Wp, (int)sh, (int)sw, ptab.data_ptr<int>(), build_tab ? 1 : 0, cur());
 }
 void conv_act_bwd(torch::Tensor dy, torch::Tensor y, torch::Tensor g, c10::optional<torch::Tensor> db, int64_t act) {
   chk4(dy, "dy");

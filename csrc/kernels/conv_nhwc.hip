@@ -481,23 +481,28 @@ __global__ void __launch_bounds__(256) fm_nhwc_stage(const unsigned short* __res
 
 // weight re-layouts: mode 0 (fwd)  out[k][(r*S+s)*Cp + c] = w[k][c][r][s]            (0 for c >= C)
 //                    mode 1 (dgrad) out[c][(r*S+s)*Kp + k] = w[k][c][R-1-r][S-1-s]    (0 for k >= K)
+//                    mode 3 both (fwd into out, dgrad into out2): one launch per forward
 __global__ void fm_cnhwc_wprep(const unsigned short* __restrict__ w, unsigned short* __restrict__ out,
-                               const float* __restrict__ g2, float* __restrict__ dw, int K, int C, int R, int S, int Cp,
-                               int Kp, int mode, int nsplit) {
+                               unsigned short* __restrict__ out2, int K, int C, int R, int S, int Cp, int Kp, int mode) {
   const int RS = R * S;
-  const long total = mode == 0 ? (long)K * RS * Cp : mode == 1 ? (long)C * RS * Kp : (long)K * RS * Cp;
-  for (long o = blockIdx.x * 256L + threadIdx.x; o < total; o += (long)gridDim.x * 256) {
-    if (mode == 0) {
+  const long t0 = (long)K * RS * Cp, t1 = (long)C * RS * Kp;
+  const long total = mode == 0 ? t0 : mode == 1 ? t1 : t0 + t1;
+  for (long oo = blockIdx.x * 256L + threadIdx.x; oo < total; oo += (long)gridDim.x * 256) {
+    // mode 3: both layouts in one launch (fwd matrix into out, dgrad matrix into out2)
+    const bool second = mode == 1 || (mode == 3 && oo >= t0);
+    const long o = mode == 3 && second ? oo - t0 : oo;
+    unsigned short* dst = mode == 3 && second ? out2 : out;
+    if (!second) {
       const int c = (int)(o % Cp);
       const long t = o / Cp;
       const int rs = (int)(t % RS), k = (int)(t / RS);
-      out[o] = c < C ? w[((long)k * C + c) * RS + rs] : (unsigned short)0;
-    } else if (mode == 1) {
+      dst[o] = c < C ? w[((long)k * C + c) * RS + rs] : (unsigned short)0;
+    } else {
       const int k = (int)(o % Kp);
       const long t = o / Kp;
       const int rs = (int)(t % RS), c = (int)(t / RS);
       const int r = rs / S, s = rs - r * S;
-      out[o] = k < K ? w[((long)k * C + c) * RS + (R - 1 - r) * S + (S - 1 - s)] : (unsigned short)0;
+      dst[o] = k < K ? w[((long)k * C + c) * RS + (R - 1 - r) * S + (S - 1 - s)] : (unsigned short)0;
     }
   }
 }
@@ -550,9 +555,10 @@ __global__ void __launch_bounds__(256) fm_cnhwc_fold(const float* __restrict__ g
 }
 
 // launch plan: tile shape (0: 128x128 / 8 waves, 1: 64x128, 2: 64x64 / 4 waves), tiles, k split.
-// 128x128 when it still gives >= 256 tiles (or wgrad, which splits K), else the smaller tiles
-// that fill the 256 CUs.  wgrad splits its long pixel reduction until ~2 blocks per CU; the
-// splits write fp32 slabs [ksplit][M][N] that fm_cnhwc_wprep mode 2 sums while folding.
+// 128x128 when it still gives >= 256 tiles, else the smaller tiles that fill the 256 CUs.  wgrad
+// (M = K out channels, N = R*S*Cp taps) takes 128-row tiles for M > 64 and 64x64 for N <= 64, and
+// splits its long pixel reduction until ~2 blocks per CU (>= 8 k-tiles each); the splits write
+// fp32 slabs [ksplit][M][N] that fm_cnhwc_fold sums while folding.
 struct Plan {
   int shape, tiles_m, tiles_n, ksplit, kt_per;
 };
@@ -560,15 +566,16 @@ struct Plan {
 Plan make_plan(int mode, int M, int N, int K) {
   auto tiles = [&](int bm, int bn) { return (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
   Plan q;
-  if (M > 64 && (mode == CN_WGRAD || tiles(128, 128) >= 256)) q.shape = 0;
-  else if (mode == CN_WGRAD || tiles(64, 128) >= 256) q.shape = 1;
+  if (mode == CN_WGRAD) q.shape = N <= 64 ? 2 : M > 64 ? 0 : 1;
+  else if (M > 64 && tiles(128, 128) >= 256) q.shape = 0;
+  else if (tiles(64, 128) >= 256) q.shape = 1;
   else q.shape = 2;
   const int bm = q.shape == 0 ? 128 : 64, bn = q.shape == 2 ? 64 : 128;
   q.tiles_m = (M + bm - 1) / bm;
   q.tiles_n = (N + bn - 1) / bn;
   const int ktiles = (K + BK - 1) / BK;
   int ks = 1;
-  if (mode == CN_WGRAD) ks = std::max(1, std::min(512 / std::max(q.tiles_m * q.tiles_n, 1), ktiles / 4));
+  if (mode == CN_WGRAD) ks = std::max(1, std::min(512 / std::max(q.tiles_m * q.tiles_n, 1), ktiles / 8));
   q.kt_per = (ktiles + ks - 1) / ks;
   q.ksplit = (ktiles + q.kt_per - 1) / q.kt_per;
   return q;
@@ -616,16 +623,17 @@ extern "C" void fm_nhwc_stage_grad_run(const void* dy, const void* y, void* dst,
                      (unsigned short*)dst, act, C, H, W, Cp, Hp, Wp, top, left, dh, dw);
 }
 
-extern "C" void fm_cnhwc_wprep_run(const void* w, void* out, const float* g2, float* dw, int K, int C, int R, int S, int Cp,
-                                   int Kp, int mode, int nsplit, hipStream_t s) {
+extern "C" void fm_cnhwc_wprep_run(const void* w, void* out, void* out2, const float* g2, float* dw, int K, int C, int R, int S,
+                                   int Cp, int Kp, int mode, int nsplit, hipStream_t s) {
   if (mode == 2) {
     const long slab = (long)K * R * S * Cp;
     hipLaunchKernelGGL(fm_cnhwc_fold, dim3((unsigned)((slab + 31) / 32)), dim3(256), 0, s, g2, dw, K, C, R * S, Cp, nsplit);
     return;
   }
-  const long total = mode == 0 ? (long)K * R * S * Cp : (long)C * R * S * Kp;
+  const long t0 = (long)K * R * S * Cp, t1 = (long)C * R * S * Kp;
+  const long total = mode == 0 ? t0 : mode == 1 ? t1 : t0 + t1;
   hipLaunchKernelGGL(fm_cnhwc_wprep, dim3(fm_grid(total, 256, 1024)), dim3(256), 0, s, (const unsigned short*)w,
-                     (unsigned short*)out, g2, dw, K, C, R, S, Cp, Kp, mode, nsplit);
+                     (unsigned short*)out, (unsigned short*)out2, K, C, R, S, Cp, Kp, mode);
 }
 
 // fp32 floats of the wgrad split-K slab workspace for these sizes (ksplit * K * R*S*Cp)
@@ -669,10 +677,11 @@ extern "C" void fm_conv_nhwc_dgrad(const void* gs, long gs_bytes, const void* wd
 // wgrad: g2 fp32 slabs [ksplit][K][R*S*Cp] (fm_conv_nhwc_wgrad_ws floats; returns ksplit) = sum over output pixels of
 // Gs[orgG + k] * Xs[orgX + tap]; gs staged G [N][Hg][Wg][Kp], pixel (p, q) at (gt + p*gsh, gl + q*gsw)
 // (gsh, gsw > 1: the stride-dilated G of the data gradient); xs as in fwd; ptab: int scratch of
-// 2 * N*P*Q entries (the pass's pixel origin table)
+// 2 * N*P*Q entries (the pass's pixel origin table: built when build_tab, else reused -- it depends
+// on the geometry only, so an op builds it once)
 extern "C" int fm_conv_nhwc_wgrad(const void* gs, long gs_bytes, const void* xs, long xs_bytes, float* g2, float* db, int N,
                                   int K, int Kp, int P, int Q, int Hg, int Wg, int gt, int gl, int gsh, int gsw, int R, int S,
-                                  int Cp, int Hp, int Wp, int sh, int sw, int* ptab, hipStream_t s) {
+                                  int Cp, int Hp, int Wp, int sh, int sw, int* ptab, int build_tab, hipStream_t s) {
   ConvN p{};
   p.A = (const unsigned short*)gs; p.a_bytes = gs_bytes;
   p.B = (const unsigned short*)xs; p.b_bytes = xs_bytes;
@@ -684,6 +693,6 @@ extern "C" int fm_conv_nhwc_wgrad(const void* gs, long gs_bytes, const void* xs,
   p.tb = make_tap(Cp, S, Wp);
   p.ptab = ptab;
   p.db = db;
-  hipLaunchKernelGGL(fm_pix_table, dim3(fm_grid(p.npix, 256, 2048)), dim3(256), 0, s, ptab, p.npix, p.ga, p.gb);
+  if (build_tab) hipLaunchKernelGGL(fm_pix_table, dim3(fm_grid(p.npix, 256, 2048)), dim3(256), 0, s, ptab, p.npix, p.ga, p.gb);
   return dispatch<CN_WGRAD>(p, s);
 }

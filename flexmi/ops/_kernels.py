@@ -270,12 +270,12 @@ def unary_backward(code, x, y, dy, dx, acc):
     C().unary_bwd(code, x, y, dy, dx, bool(acc))
 
 
-def binary_forward(code, a, b, y):
-    C().binary_fwd(code, a, b, y)
+def binary_forward(code, a, b, y, relu=False):
+    C().binary_fwd(code, a, b, y, bool(relu))
 
 
-def binary_backward(code, a, b, dy, da, db, acca, accb):
-    C().binary_bwd(code, a, b, dy, da, db, bool(acca), bool(accb))
+def binary_backward(code, a, b, dy, da, db, acca, accb, ymask=None):
+    C().binary_bwd(code, a, b, dy, ymask, da, db, bool(acca), bool(accb))
 
 
 def _outer_inner(shape, axis):
@@ -608,7 +608,17 @@ def _nhwc_forward(x, w, b, y, stride, pads, act, saved):
     if saved is not None:
         saved["nhwc_x_ready"] = True
     wf = scratch(x.device, "cn_wf", Kout * R * S * Cp, w.dtype)
-    C().cnhwc_wprep(w, wf, w, w, Cp, _r8(Kout), 0, 1)
+    if saved is not None:
+        # the backward's flipped / transposed matrix comes out of the same launch (weights do not
+        # change between an op's forward and backward)
+        nwd = Cin * R * S * _r8(Kout)
+        wd = saved.get("nhwc_wd")
+        if wd is None or wd.numel() != nwd or wd.device != w.device:
+            wd = torch.empty(nwd, dtype=w.dtype, device=w.device)
+            saved["nhwc_wd"] = wd
+        C().cnhwc_wprep(w, wf, wd, w, w, Cp, _r8(Kout), 3, 1)
+    else:
+        C().cnhwc_wprep(w, wf, w, w, w, Cp, _r8(Kout), 0, 1)
     C().conv_nhwc_fwd(xs, wf, b, y, R, S, Cp, Hp, Wp, stride[0], stride[1], int(act))
 
 
@@ -647,12 +657,26 @@ def _nhwc_backward(x, w, y, dy, act, db, dx, dw, stride, pads, acc, saved):
     # (gt + p*sh, gl + q*sw)
     # (split-K fp32 slabs summed by the fold into dW[K,C,R,S]; db (+)= sum G from the same kernel)
     g2 = scratch(dev, "cn_g2", C().conv_nhwc_wgrad_ws(N, Kout, P, Q, R, S, Cp), torch.float32)
-    ptab = scratch(dev, "cn_ptab", 2 * N * P * Q, torch.int32)
-    nsplit = C().conv_nhwc_wgrad(gs, xs, g2, db, N, Kout, Kp, P, Q, Hg, Wg, gt, gl, dh, dwl, R, S, Cp, Hp, Wp, sh, sw, ptab)
-    C().cnhwc_wprep(w, w, g2, dw.view(-1), Cp, Kp, 2, nsplit)
+    # the pixel-origin table depends on the geometry only: an op builds it once
+    geo = (N, P, Q, Hg, Wg, gt, gl, dh, dwl, Hp, Wp, Cp, Kp, sh, sw)
+    build = True
+    if saved is not None:
+        ptab = saved.get("nhwc_ptab")
+        if ptab is not None and saved.get("nhwc_ptab_geo") == geo and ptab.device == dev:
+            build = False
+        else:
+            ptab = torch.empty(2 * N * P * Q, dtype=torch.int32, device=dev)
+            saved["nhwc_ptab"], saved["nhwc_ptab_geo"] = ptab, geo
+    else:
+        ptab = scratch(dev, "cn_ptab", 2 * N * P * Q, torch.int32)
+    nsplit = C().conv_nhwc_wgrad(gs, xs, g2, db, N, Kout, Kp, P, Q, Hg, Wg, gt, gl, dh, dwl, R, S, Cp, Hp, Wp, sh, sw, ptab,
+                                 build)
+    C().cnhwc_wprep(w, w, w, g2, dw.view(-1), Cp, Kp, 2, nsplit)
     if dx is not None:
-        wd = scratch(dev, "cn_wd", Cin * R * S * Kp, w.dtype)
-        C().cnhwc_wprep(w, wd, w, w, _r8(Cin), Kp, 1, 1)
+        wd = saved.get("nhwc_wd") if saved is not None and saved.get("nhwc_x_ready") else None
+        if wd is None or wd.numel() != Cin * R * S * Kp:
+            wd = scratch(dev, "cn_wd", Cin * R * S * Kp, w.dtype)
+            C().cnhwc_wprep(w, wd, w, w, w, _r8(Cin), Kp, 1, 1)
         C().conv_nhwc_dgrad(gs, wd, dx, R, S, Kp, Hg, Wg, bool(acc))
     return True
 

@@ -63,6 +63,8 @@ class ElementUnary(Op):
         return set(range(self.out_ndims))
 
     def forward(self, ctx: OpCtx):
+        if ctx.saved.get("fused_into_binary"):   # the producing ElementBinary wrote relu(a op b) here
+            return
         x, y = ctx.inputs[0], ctx.outputs[0]
         if ctx.hip:
             K.unary_forward(self.code, x, y)
@@ -70,7 +72,7 @@ class ElementUnary(Op):
             y.copy_(unary_fwd_torch(self.code, x.float()))
 
     def backward(self, ctx: OpCtx):
-        if not ctx.in_grads or ctx.in_grads[0] is None:
+        if not ctx.in_grads or ctx.in_grads[0] is None or ctx.saved.get("fused_into_binary"):
             return
         x, y, dy, dx = ctx.inputs[0], ctx.outputs[0], ctx.out_grads[0], ctx.in_grads[0]
         if getattr(self, "skip_act_grad", False):   # fused sigmoid + BCE (loss emitted dL/dz)
@@ -101,6 +103,10 @@ class ElementBinary(Op):
 
     def forward(self, ctx: OpCtx):
         a, b, y = ctx.inputs[0], ctx.inputs[1], ctx.outputs[0]
+        fused = ctx.saved.get("fused_relu")      # (relu output, its gradient): executor fusion
+        if ctx.hip and fused is not None:
+            K.binary_forward(self.code, a, b, fused[0], relu=True)
+            return
         if ctx.hip:
             K.binary_forward(self.code, a, b, y)
         else:
@@ -112,6 +118,11 @@ class ElementBinary(Op):
         da = ctx.in_grads[0] if len(ctx.in_grads) > 0 else None
         db = ctx.in_grads[1] if len(ctx.in_grads) > 1 else None
         if ctx.hip:
+            fused = ctx.saved.get("fused_relu")
+            if fused is not None:
+                K.binary_backward(self.code, a, b, fused[1], da, db, ctx.in_grad_accumulate[0], ctx.in_grad_accumulate[1],
+                                  ymask=fused[0])
+                return
             K.binary_backward(self.code, a, b, dy, da, db,
                               ctx.in_grad_accumulate[0], ctx.in_grad_accumulate[1])
             return

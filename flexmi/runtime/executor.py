@@ -911,6 +911,7 @@ class Executor:
             self.ctx[op.guid] = c
         self._build_groups(ops)
         self._build_epilogue_fusion(ops)
+        self._build_binary_relu_fusion(ops)
         if self.backend == "hip":
             # dW split-K reduces on a side stream (csrc/kernels/gemm_async.hip), joined before
             # every collective and at the end of the backward program (_with_gemm_joins)
@@ -974,6 +975,36 @@ class Executor:
                 continue
             c2.saved["fuse_below"] = (c1.outputs[0], op.activation)
             c1.saved["grad_is_dpre"] = True
+
+    def _build_binary_relu_fusion(self, ops):
+        """ElementBinary A -> ReLU B (A's output consumed only by B, same layout, B's input gradient
+        A's output gradient): A writes relu(a op b) straight into B's output and, in backward, masks
+        B's output gradient by (B's output > 0) itself; B runs nothing.  The ResNet residual add +
+        ReLU then costs one pass per direction instead of two (reference: element_binary.cu and
+        element_unary.cu as separate cuDNN calls).  Off under --debug (A's own output stays unwritten)."""
+        from flexmi.core.types import OperatorType
+        if self.backend != "hip" or self.debug:
+            return
+        bin_types = (OperatorType.OP_EW_ADD, OperatorType.OP_EW_SUB, OperatorType.OP_EW_MUL, OperatorType.OP_EW_DIV)
+        for op in ops:
+            if op.op_type not in bin_types:
+                continue
+            ca = self.ctx.get(op.guid)
+            t = op.outputs[0]
+            cons = self.consumers.get(t.guid, [])
+            if ca is None or ca.empty or len(cons) != 1 or t is self.final:
+                continue
+            b, idx = cons[0]
+            cb = self.ctx.get(b.guid)
+            if (b.op_type != OperatorType.OP_RELU or cb is None or cb.empty
+                    or op.guid in self.group_of or b.guid in self.group_of
+                    or not self.need[(b.guid, idx)].same_as(self.home[t.guid])
+                    or not self.home[b.outputs[0].guid].same_as(self.home[t.guid])
+                    or cb.outputs[0] is None or cb.out_grads[0] is None
+                    or cb.outputs[0].shape != ca.outputs[0].shape):
+                continue
+            ca.saved["fused_relu"] = (cb.outputs[0], cb.out_grads[0])
+            cb.saved["fused_into_binary"] = True
 
     def _build_groups(self, ops):
         """Fuse independent ops of the same kind and placement into one launch (embedding

@@ -244,3 +244,74 @@ def test_dlrm_deferred_dw_phases_match_cpu(gpu, monkeypatch):
     tiny DLRM like the CPU oracle -- fused act-bwd epilogues and the skinny layer included."""
     monkeypatch.setenv("FLEXMI_DEFER_DW", "force")
     test_dlrm_tiny_gpu_matches_cpu(gpu)
+
+
+def _residual(device, B=64, fuse_shape=(48,)):
+    from flexmi.core import FFConfig, FFModel, SGDOptimizer, LossType, MetricsType, ActiMode
+    cfg = FFConfig()
+    cfg.batchSize = B
+    cfg.device = device
+    cfg.compute_dtype = "bf16" if device == "gpu" else "fp32"
+    m = FFModel(cfg)
+    x = m.create_tensor([B, 40])
+    a = m.dense(x, 48, ActiMode.AC_MODE_RELU)
+    b = m.dense(a, 48)
+    t = m.relu(m.add(a, b))              # residual add + ReLU: fused by the executor on HIP
+    t = m.relu(m.subtract(t, m.dense(t, 48)))
+    t = m.dense(t, 10)
+    t = m.softmax(t)
+    m.compile(SGDOptimizer(m, 0.05), LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, [MetricsType.METRICS_ACCURACY])
+    m.init_layers()
+    return m, x
+
+
+def test_binary_relu_fusion_matches_cpu(gpu):
+    """ElementBinary -> ReLU fused (one kernel per direction, relu(a op b) written into the ReLU's
+    output, gradient masked by it) trains like the unfused fp32 CPU executor; both pairs fuse."""
+    from flexmi.core import SingleDataLoader
+    rng = np.random.RandomState(1)
+    X = rng.randn(256, 40).astype(np.float32)
+    Y = rng.randint(0, 10, (256, 1)).astype(np.int32)
+    res = {}
+    for dev in ("cpu", "gpu"):
+        m, x = _residual(dev)
+        dx = SingleDataLoader(m, x, X, 256)
+        dy = SingleDataLoader(m, m.get_label_tensor(), Y, 256)
+        for _ in range(5):
+            dx.next_batch(m)
+            dy.next_batch(m)
+            m.forward()
+            m.zero_gradients()
+            m.backward()
+            m.update()
+        if dev == "gpu":
+            ex = m._ex()
+            fused = [c for c in ex.ctx.values() if "fused_relu" in c.saved]
+            assert len(fused) == 2
+        res[dev] = [w.get_weights(m) for w in m.parameters]
+    for a, b in zip(res["cpu"], res["gpu"]):
+        assert np.abs(a - b).max() < 2e-2 * max(1.0, np.abs(a).max())
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,off", [(4096 * 8 + 5, 0), (1003, 1)])
+def test_elementwise_vector_and_tail(gpu, dt, n, off):
+    """Vectorised (8 per thread) unary / binary kernels, their scalar tails and the unaligned
+    fallback (a view starting one element in), fused relu and ymask, against torch."""
+    from flexmi.ops import _kernels as K
+    torch.manual_seed(n)
+    buf = [torch.randn(n + off, device=gpu).to(dt) for _ in range(4)]
+    a, b, g, m = (t[off:] for t in buf)
+    y = torch.empty_like(a)
+    K.binary_forward(0, a, b, y, relu=True)
+    torch.testing.assert_close(y.float(), torch.relu(a.float() + b.float()).to(dt).float(), rtol=1e-2, atol=1e-2)
+    da, db = torch.zeros_like(a), torch.ones_like(a)
+    K.binary_backward(2, a, b, g, da, db, False, True, ymask=m)
+    gm = g.float() * (m.float() > 0)
+    torch.testing.assert_close(da.float(), (gm * b.float()).to(dt).float(), rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(db.float(), (1 + gm * a.float()).to(dt).float(), rtol=2e-2, atol=2e-2)
+    K.unary_forward(1, a, y)
+    torch.testing.assert_close(y.float(), torch.sigmoid(a.float()).to(dt).float(), rtol=1e-2, atol=1e-2)
+    dx = torch.full_like(a, 0.5)
+    K.unary_backward(0, a, y, g, dx, True)
+    torch.testing.assert_close(dx.float(), (0.5 + g.float() * (a.float() > 0)).to(dt).float(), rtol=1e-2, atol=1e-2)
