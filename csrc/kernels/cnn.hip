@@ -275,6 +275,109 @@ __global__ void __launch_bounds__(256) fm_pool_bwd_rows(const T* __restrict__ y,
   }
 }
 
+// ---- pooling on row bands (one block per (n, c, band) staged in LDS) ----------------------
+// The forward block reads the input rows its band of output rows needs as ONE contiguous chunk
+// of the plane (coalesced 2-B loads, each input element loaded once instead of once per window
+// that covers it), computes the band's outputs from LDS and writes them contiguously.  The
+// backward block stages the output-gradient rows (act'(y)*dy as fp32, plus max pooling's argmax
+// bytes) that reach its band of input rows, then every input element gathers its <= ceil(k/s)^2
+// windows from LDS.  Bands are sized to ~4 K staged elements so a layer launches thousands of
+// blocks (the whole-plane kernels below ran one block per plane: too few waves).
+template <typename T>
+__global__ void __launch_bounds__(256) fm_pool_fwd_band(const T* __restrict__ x, T* __restrict__ y,
+                                                        unsigned char* __restrict__ code, int H, int W, int P, int Q, int kh,
+                                                        int kw, int sh, int sw, int pt, int pl, int is_max, int act, int PB,
+                                                        int nbands, FastDiv dQ) {
+  extern __shared__ float sx[];
+  const int nc = blockIdx.x / nbands, band = blockIdx.x - nc * nbands;
+  const int p0 = band * PB, p1 = min(P, p0 + PB);
+  const int hlo = max(0, p0 * sh - pt), hhi = min(H, (p1 - 1) * sh - pt + kh);
+  const int rows = max(0, hhi - hlo);
+  const T* xp = x + ((long)nc * H + hlo) * W;
+  for (int e = threadIdx.x; e < rows * W; e += 256) sx[e] = tof(xp[e]);
+  __syncthreads();
+  const int nout = (p1 - p0) * Q;
+  for (int o = threadIdx.x; o < nout; o += 256) {
+    const int pr = fdiv(o, dQ), q = o - pr * Q;
+    const int p = p0 + pr;
+    const int h0 = p * sh - pt, w0 = q * sw - pl;
+    // the window clipped to the plane: no per-tap bounds tests
+    const int r0 = max(0, -h0), r1 = min(kh, H - h0), c0 = max(0, -w0), c1 = min(kw, W - w0);
+    float m = -INFINITY, sacc = 0.f;
+    int bc = 255;
+    for (int r = r0; r < r1; ++r) {
+      const float* row = sx + (h0 + r - hlo) * W + w0;
+      for (int c = c0; c < c1; ++c) {
+        const float v = row[c];
+        if (v > m || bc == 255) bc = r * kw + c;
+        m = fmaxf(m, v);
+        sacc += v;
+      }
+    }
+    const int cnt = max(0, r1 - r0) * max(0, c1 - c0);
+    const long oi = ((long)nc * P + p) * Q + q;
+    y[oi] = fromf<T>(act_fwd(act, is_max ? m : (cnt ? sacc / cnt : 0.f)));
+    if (code) code[oi] = (unsigned char)bc;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) fm_pool_bwd_band(const T* __restrict__ y, const T* __restrict__ dy,
+                                                        const unsigned char* __restrict__ code, T* __restrict__ dx, int H,
+                                                        int W, int P, int Q, int kh, int kw, int sh, int sw, int pt, int pl,
+                                                        int is_max, int act, int acc, int HB, int nbands, int maxprows,
+                                                        FastDiv dW, FastDiv dQ, FastDiv dsh, FastDiv dsw) {
+  extern __shared__ float sg[];                       // [prows][Q] gradients, then [prows][Q] argmax bytes
+  unsigned char* sc = reinterpret_cast<unsigned char*>(sg + maxprows * Q);
+  const int nc = blockIdx.x / nbands, band = blockIdx.x - nc * nbands;
+  const int h0b = band * HB, h1b = min(H, h0b + HB);
+  // output rows whose windows reach input rows [h0b, h1b): p*sh - pt <= h1b-1 and p*sh - pt + kh > h0b
+  const int plo = (h0b + pt - kh + 1) > 0 ? fdiv(h0b + pt - kh + sh, dsh) : 0;
+  const int phi = min(P, (h1b - 1 + pt) >= 0 ? fdiv(h1b - 1 + pt, dsh) + 1 : 0);
+  const int prows = max(0, phi - plo);
+  const long obase = ((long)nc * P + plo) * Q;
+  // stage g = act'(y) * dy per output window; average pooling divides by the window's clipped size
+  // here, once per window instead of once per (input element, window) pair
+  for (int e = threadIdx.x; e < prows * Q; e += 256) {
+    const float gd = tof(dy[obase + e]);
+    float g = act == ACT_NONE ? gd : act_bwd(act, tof(y[obase + e]), gd);
+    if (is_max) {
+      sc[e] = code[obase + e];
+    } else {
+      const int pr = fdiv(e, dQ), q = e - pr * Q;
+      const int hw0 = (plo + pr) * sh - pt, ww0 = q * sw - pl;
+      g /= (float)((min(hw0 + kh, H) - max(hw0, 0)) * (min(ww0 + kw, W) - max(ww0, 0)));
+    }
+    sg[e] = g;
+  }
+  __syncthreads();
+  const int nin = (h1b - h0b) * W;
+  T* dxp = dx + ((long)nc * H + h0b) * W;
+  for (int e = threadIdx.x; e < nin; e += 256) {
+    const int hr = fdiv(e, dW), w = e - hr * W;
+    const int h = h0b + hr;
+    // windows holding (h, w): p in [ceil((h+pt-kh+1)/sh), floor((h+pt)/sh)], q likewise
+    const int pmin = max(plo, h + pt + 1 > kh ? fdiv(h + pt - kh + sh, dsh) : 0);
+    const int pmax = min(phi - 1, h + pt >= 0 ? fdiv(h + pt, dsh) : -1);
+    const int qmin = w + pl + 1 > kw ? fdiv(w + pl - kw + sw, dsw) : 0;
+    const int qmax = min(Q - 1, w + pl >= 0 ? fdiv(w + pl, dsw) : -1);
+    float g = 0.f;
+    for (int p = pmin; p <= pmax; ++p) {
+      const float* gr = sg + (p - plo) * Q;
+      if (is_max) {
+        const unsigned char* cr = sc + (p - plo) * Q;
+        const int rr = (h - (p * sh - pt)) * kw;
+        for (int q = qmin; q <= qmax; ++q)
+          if (cr[q] == (unsigned char)(rr + w - (q * sw - pl))) g += gr[q];
+      } else {
+        for (int q = qmin; q <= qmax; ++q) g += gr[q];
+      }
+    }
+    if (acc) g += tof(dxp[e]);
+    dxp[e] = fromf<T>(g);
+  }
+}
+
 // ---- pooling on whole planes (one block per (n, c) plane staged in LDS) -------------------
 // The plane's operands are read ONCE, contiguously (coalesced), into LDS; every output of the
 // forward and every input element of the backward is then computed from LDS and written
@@ -562,6 +665,17 @@ static void fm_pool_fwd_t(const void* x, void* y, unsigned char* code, int N, in
                        is_max ? code : nullptr, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act);
     return;
   }
+  // FM_POOL_BAND=0: the per-output kernel instead of the LDS row bands
+  static const bool band = !(getenv("FM_POOL_BAND") != nullptr && atoi(getenv("FM_POOL_BAND")) == 0);
+  if (band && (long)kh * W <= 4096) {
+    const int PB = std::max(1, std::min(P, ((4096 / W) - kh) / sh + 1));
+    const int nbands = (P + PB - 1) / PB;
+    const int rows = std::min(H, (PB - 1) * sh + kh);
+    hipLaunchKernelGGL(fm_pool_fwd_band<T>, dim3(N * C * nbands), dim3(256), (size_t)rows * W * sizeof(float), st,
+                       (const T*)x, (T*)y, is_max ? code : nullptr, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, PB,
+                       nbands, make_fastdiv(Q));
+    return;
+  }
   hipLaunchKernelGGL(fm_pool_fwd_kernel<T>, dim3((total + 255) / 256), dim3(256), 0, st, (const T*)x, (T*)y,
                      is_max ? code : nullptr, total, make_fastdiv(Q), make_fastdiv(P), H, W, P, Q, kh, kw, sh, sw, pt, pl,
                      is_max, act);
@@ -583,6 +697,20 @@ static void fm_pool_bwd_t(const void* x, const void* y, const void* dy, void* dx
     hipLaunchKernelGGL(fm_pool_bwd_plane<T>, dim3(N * C), dim3(256), (size_t)P * Q * 5, st, (const T*)y, (const T*)dy,
                        (const unsigned char*)code, (T*)dx, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, acc);
     return;
+  }
+  static const bool band = !(getenv("FM_POOL_BAND") != nullptr && atoi(getenv("FM_POOL_BAND")) == 0);
+  if (!per_elem && band) {
+    // input-row band HB: ~4 K input elements; it needs <= (HB + kh - 1) / sh + 1 output rows staged
+    const int HB = std::max(1, std::min(H, 4096 / W));
+    const int maxprows = std::min(P, (HB + kh - 1) / sh + 2);
+    const size_t lds = (size_t)maxprows * Q * 5;
+    if (lds <= 48 * 1024) {
+      const int nbands = (H + HB - 1) / HB;
+      hipLaunchKernelGGL(fm_pool_bwd_band<T>, dim3(N * C * nbands), dim3(256), lds, st, (const T*)y, (const T*)dy,
+                         (const unsigned char*)code, (T*)dx, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, acc, HB, nbands,
+                         maxprows, make_fastdiv(W), make_fastdiv(Q), make_fastdiv(sh), make_fastdiv(sw));
+      return;
+    }
   }
   if (!per_elem) {
     constexpr int VW = 8;

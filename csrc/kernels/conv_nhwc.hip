@@ -479,6 +479,77 @@ __global__ void __launch_bounds__(256) fm_nhwc_stage(const unsigned short* __res
   }
 }
 
+// Narrow images (Wp < 32): the row kernel above would leave most of its 64 columns empty (Inception
+// 17x17 / 8x8, ResNet 14x14 / 7x7).  This form tiles 64 consecutive destination PIXELS of one
+// image (flattened i*Wp + j, crossing rows) x 64 channels: a per-block LDS table maps each pixel
+// slot to its source offset (or -1 in the halo / dilation gaps), the loads walk the slots (runs
+// of one source row are contiguous) and the 16-B stores of a block cover one contiguous
+// [64 pixels][Cp] run of the destination.
+template <bool GRAD>
+__global__ void __launch_bounds__(256) fm_nhwc_stage_flat(const unsigned short* __restrict__ src,
+                                                          const unsigned short* __restrict__ ysrc,
+                                                          unsigned short* __restrict__ dst, int act, int C, int H, int W,
+                                                          int Cp, int Hp, int Wp, int top, int left, int dh, int dw,
+                                                          int blocks_per_img) {
+  __shared__ __attribute__((aligned(16))) unsigned short tile[64][72];
+  __shared__ int soff[64];
+  const int n = blockIdx.x / blocks_per_img;
+  const int pix0 = (blockIdx.x - n * blocks_per_img) * 64;
+  const int c0 = blockIdx.y * 64;
+  const int npix = Hp * Wp;
+  if (threadIdx.x < 64) {
+    const int pi = pix0 + threadIdx.x;
+    int off = -1;
+    if (pi < npix) {
+      const int i = pi / Wp, j = pi - i * Wp;
+      const int hd = i - top, wd = j - left;
+      const int h = hd / dh, w = wd / dw;
+      if (hd >= 0 && wd >= 0 && h * dh == hd && w * dw == wd && h < H && w < W) off = h * W + w;
+    }
+    soff[threadIdx.x] = off;
+  }
+  __syncthreads();
+  const long plane = (long)H * W;
+  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+    const int cc = e >> 6, jj = e & 63;
+    const int c = c0 + cc, off = soff[jj];
+    unsigned short v = 0;
+    if (c < C && off >= 0) {
+      const long o = ((long)n * C + c) * plane + off;
+      v = src[o];
+      if constexpr (GRAD) {
+        if (act != ACT_NONE) v = f2bf(act_bwd(act, bf2f(ysrc[o]), bf2f(v)));
+      }
+    }
+    tile[cc][jj] = v;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 512; e += 256) {
+    const int jj = e >> 3, cg = e & 7;
+    const int pi = pix0 + jj, c = c0 + 8 * cg;
+    if (pi >= npix || c >= Cp) continue;
+    u32x4_t o;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      o[u] = (unsigned)tile[8 * cg + 2 * u][jj] | ((unsigned)tile[8 * cg + 2 * u + 1][jj] << 16);
+    *reinterpret_cast<u32x4_t*>(dst + ((long)n * npix + pi) * Cp + c) = o;
+  }
+}
+
+template <bool GRAD>
+void stage_launch(const void* src, const void* y, void* dst, int act, int N, int C, int H, int W, int Cp, int Hp, int Wp, int top,
+                  int left, int dh, int dw, hipStream_t s) {
+  if (Wp < 32) {
+    const int bpi = (Hp * Wp + 63) / 64;
+    hipLaunchKernelGGL(fm_nhwc_stage_flat<GRAD>, dim3(N * bpi, (Cp + 63) / 64), dim3(256), 0, s, (const unsigned short*)src,
+                       (const unsigned short*)y, (unsigned short*)dst, act, C, H, W, Cp, Hp, Wp, top, left, dh, dw, bpi);
+    return;
+  }
+  dim3 grid(N * Hp, (Wp + 63) / 64, (Cp + 63) / 64);
+  hipLaunchKernelGGL(fm_nhwc_stage<GRAD>, grid, dim3(256), 0, s, (const unsigned short*)src, (const unsigned short*)y,
+                     (unsigned short*)dst, act, C, H, W, Cp, Hp, Wp, top, left, dh, dw);
+}
+
 // weight re-layouts: mode 0 (fwd)  out[k][(r*S+s)*Cp + c] = w[k][c][r][s]            (0 for c >= C)
 //                    mode 1 (dgrad) out[c][(r*S+s)*Kp + k] = w[k][c][R-1-r][S-1-s]    (0 for k >= K)
 //                    mode 3 both (fwd into out, dgrad into out2): one launch per forward
@@ -610,17 +681,13 @@ int dispatch(ConvN& p, hipStream_t s) {
 // stage src [N][C][H][W] (bf16) into dst [N][Hp][Wp][Cp] at (top, left), zeros elsewhere
 extern "C" void fm_nhwc_stage_run(const void* src, void* dst, int N, int C, int H, int W, int Cp, int Hp, int Wp, int top,
                                   int left, int dh, int dw, hipStream_t s) {
-  dim3 grid(N * Hp, (Wp + 63) / 64, (Cp + 63) / 64);
-  hipLaunchKernelGGL(fm_nhwc_stage<false>, grid, dim3(256), 0, s, (const unsigned short*)src, nullptr, (unsigned short*)dst,
-                     ACT_NONE, C, H, W, Cp, Hp, Wp, top, left, dh, dw);
+  stage_launch<false>(src, nullptr, dst, ACT_NONE, N, C, H, W, Cp, Hp, Wp, top, left, dh, dw, s);
 }
 
 // gradient staging: dst = stage(act'(y) * dy) (y unused when act == none)
 extern "C" void fm_nhwc_stage_grad_run(const void* dy, const void* y, void* dst, int act, int N, int C, int H, int W, int Cp,
                                        int Hp, int Wp, int top, int left, int dh, int dw, hipStream_t s) {
-  dim3 grid(N * Hp, (Wp + 63) / 64, (Cp + 63) / 64);
-  hipLaunchKernelGGL(fm_nhwc_stage<true>, grid, dim3(256), 0, s, (const unsigned short*)dy, (const unsigned short*)y,
-                     (unsigned short*)dst, act, C, H, W, Cp, Hp, Wp, top, left, dh, dw);
+  stage_launch<true>(dy, y, dst, act, N, C, H, W, Cp, Hp, Wp, top, left, dh, dw, s);
 }
 
 extern "C" void fm_cnhwc_wprep_run(const void* w, void* out, void* out2, const float* g2, float* dw, int K, int C, int R, int S,
