@@ -294,7 +294,21 @@ __global__ void __launch_bounds__(256) fm_pool_fwd_band(const T* __restrict__ x,
   const int hlo = max(0, p0 * sh - pt), hhi = min(H, (p1 - 1) * sh - pt + kh);
   const int rows = max(0, hhi - hlo);
   const T* xp = x + ((long)nc * H + hlo) * W;
-  for (int e = threadIdx.x; e < rows * W; e += 256) sx[e] = tof(xp[e]);
+  // 8 loads in flight per thread before the LDS stores (a load -> store loop waits on every load)
+  const int nst = rows * W;
+  for (int b0 = 0; b0 < nst; b0 += 256 * 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = b0 + u * 256 + (int)threadIdx.x;
+      v[u] = tof(xp[min(e, nst - 1)]);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = b0 + u * 256 + (int)threadIdx.x;
+      if (e < nst) sx[e] = v[u];
+    }
+  }
   __syncthreads();
   const int nout = (p1 - p0) * Q;
   for (int o = threadIdx.x; o < nout; o += 256) {
@@ -338,17 +352,31 @@ __global__ void __launch_bounds__(256) fm_pool_bwd_band(const T* __restrict__ y,
   const long obase = ((long)nc * P + plo) * Q;
   // stage g = act'(y) * dy per output window; average pooling divides by the window's clipped size
   // here, once per window instead of once per (input element, window) pair
-  for (int e = threadIdx.x; e < prows * Q; e += 256) {
-    const float gd = tof(dy[obase + e]);
-    float g = act == ACT_NONE ? gd : act_bwd(act, tof(y[obase + e]), gd);
+  const int nst = prows * Q;
+  for (int b0 = 0; b0 < nst; b0 += 256 * 4) {
+    float gd[4], yv[4];
+    unsigned char cd[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {           // 4 (dy, y, code) loads in flight per thread
+      const long oi = obase + min(b0 + u * 256 + (int)threadIdx.x, max(nst - 1, 0));
+      gd[u] = tof(dy[oi]);
+      yv[u] = act == ACT_NONE ? 0.f : tof(y[oi]);
+      cd[u] = is_max ? code[oi] : (unsigned char)0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+    const int e = b0 + u * 256 + (int)threadIdx.x;
+    if (e >= nst) continue;
+    float g = act == ACT_NONE ? gd[u] : act_bwd(act, yv[u], gd[u]);
     if (is_max) {
-      sc[e] = code[obase + e];
+      sc[e] = cd[u];
     } else {
       const int pr = fdiv(e, dQ), q = e - pr * Q;
       const int hw0 = (plo + pr) * sh - pt, ww0 = q * sw - pl;
       g /= (float)((min(hw0 + kh, H) - max(hw0, 0)) * (min(ww0 + kw, W) - max(ww0, 0)));
     }
     sg[e] = g;
+    }
   }
   __syncthreads();
   const int nin = (h1b - h0b) * W;

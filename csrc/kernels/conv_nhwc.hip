@@ -31,6 +31,7 @@
 #include "gemm_common.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 namespace {
@@ -510,18 +511,29 @@ __global__ void __launch_bounds__(256) fm_nhwc_stage_flat(const unsigned short* 
   }
   __syncthreads();
   const long plane = (long)H * W;
-  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
-    const int cc = e >> 6, jj = e & 63;
-    const int c = c0 + cc, off = soff[jj];
-    unsigned short v = 0;
-    if (c < C && off >= 0) {
+  // 8 element loads in flight per thread (clamped addresses, predicated use) before the LDS stores
+#pragma unroll
+  for (int b0 = 0; b0 < 64 * 64; b0 += 256 * 8) {
+    unsigned short v[8], yv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = b0 + u * 256 + (int)threadIdx.x;
+      const int cc = e >> 6, jj = e & 63;
+      const int c = min(c0 + cc, C - 1), off = max(soff[jj], 0);
       const long o = ((long)n * C + c) * plane + off;
-      v = src[o];
-      if constexpr (GRAD) {
-        if (act != ACT_NONE) v = f2bf(act_bwd(act, bf2f(ysrc[o]), bf2f(v)));
-      }
+      v[u] = src[o];
+      if constexpr (GRAD) yv[u] = act != ACT_NONE ? ysrc[o] : (unsigned short)0;
     }
-    tile[cc][jj] = v;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = b0 + u * 256 + (int)threadIdx.x;
+      const int cc = e >> 6, jj = e & 63;
+      unsigned short x = (c0 + cc < C && soff[jj] >= 0) ? v[u] : (unsigned short)0;
+      if constexpr (GRAD) {
+        if (act != ACT_NONE && x != 0) x = f2bf(act_bwd(act, bf2f(yv[u]), bf2f(x)));
+      }
+      tile[cc][jj] = x;
+    }
   }
   __syncthreads();
   for (int e = threadIdx.x; e < 512; e += 256) {
@@ -667,10 +679,15 @@ void go(ConvN& p, const Plan& q, hipStream_t s) {
   hipLaunchKernelGGL((fm_conv_nhwc<BM, BN, MODE, NTH>), dim3(p.tiles_m * p.tiles_n, 1, p.ksplit), dim3(NTH), lds, s, p);
 }
 
+// FM_CONV_NHWC_4WAVE=1 (A/B): the 128x128 tiles as 4-wave blocks (64x64 per wave, twice the MFMAs
+// per k-tile per wave) instead of 8 waves
+static const bool g_cn_4wave = getenv("FM_CONV_NHWC_4WAVE") != nullptr && atoi(getenv("FM_CONV_NHWC_4WAVE")) == 1;
+
 template <int MODE>
 int dispatch(ConvN& p, hipStream_t s) {
   const Plan q = make_plan(MODE, p.M, p.N, p.K);
-  if (q.shape == 0) go<128, 128, MODE, 512>(p, q, s);
+  if (q.shape == 0 && g_cn_4wave) go<128, 128, MODE, 256>(p, q, s);
+  else if (q.shape == 0) go<128, 128, MODE, 512>(p, q, s);
   else if (q.shape == 1) go<64, 128, MODE, 256>(p, q, s);
   else go<64, 64, MODE, 256>(p, q, s);
   return q.ksplit;

@@ -426,6 +426,9 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
   // few 128x128 tiles and a short K (small-batch layers, e.g. DLRM run_random at 256 samples
   // per GPU): 64x64 tiles give 4x the blocks without split-K slabs (measured +26 % step rate)
   if (t128 < 128 && K <= 2048 && !(g_gemm_variant & 16)) { BMv = 64; BNv = 64; }
+  // a fused backward epilogue cannot split K: small grids take 64x64 tiles for 4x the blocks
+  // (summit_large dX, 256 x 4096 x 4096: 64 -> 256 blocks)
+  if ((act_y != nullptr || colsum != nullptr) && t128 < 256 && !(g_gemm_variant & 16)) { BMv = 64; BNv = 64; }
   if (g_gemm_variant & 32) { BMv = 64; BNv = 64; }
   p.tiles_m = (M + BMv - 1) / BMv;
   p.tiles_n = (N + BNv - 1) / BNv;

@@ -1099,6 +1099,10 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
   // forward runs unsplit instead of split-K 2 + reduce (step -0.2..0.9 %: profiles/ab_f32_t64.txt)
   static const long t64_below = getenv("FM_GEMM_F32_T64") ? atol(getenv("FM_GEMM_F32_T64")) : 129L;
   if (t128 < t64_below && K <= 2048) { BMv = 64; BNv = 64; }
+  // a fused backward epilogue (act-bwd of the layer below / bias-grad column sums) cannot split K:
+  // small grids take 64x64 tiles for 4x the blocks (summit_large dX, 256 x 4096 x 4096: 64 -> 256
+  // blocks on 256 CUs)
+  if ((act_y != nullptr || colsum != nullptr) && t128 < 256) { BMv = 64; BNv = 64; }
   // variant bit 4096 (A/B): 256x128 tiles, one 4-wave block per CU, when they fill >= 3/4 of the chip
   if ((variant & 4096) && vec && (long)((M + 255) / 256) * ((N + 127) / 128) * batch >= 192) { BMv = 256; BNv = 128; }
   p.tiles_m = (M + BMv - 1) / BMv;
