@@ -119,9 +119,11 @@ long fm_conv_nhwc_wgrad_ws(int N, int K, int P, int Q, int R, int S, int Cp);
 void fm_cnhwc_wprep_run(const void* w, void* out, void* out2, const float* g2, float* dw, int K, int C, int R, int S, int Cp,
                         int Kp, int mode, int nsplit, hipStream_t s);
 void fm_conv_nhwc_fwd(const void* xs, long xs_bytes, const void* wf, const float* bias, void* y, int N, int K, int P, int Q,
-                      int R, int S, int Cp, int Hp, int Wp, int sh, int sw, int act, hipStream_t s);
+                      int R, int S, int Cp, int Hp, int Wp, int sh, int sw, int act, void* out2, int H2, int W2, int C2, int t2,
+                      int l2, int d2h, int d2w, int write_nchw, hipStream_t s);
 void fm_conv_nhwc_dgrad(const void* gs, long gs_bytes, const void* wd, void* dx, int accum, int N, int C, int H, int W, int R,
-                        int S, int Kp, int Hg, int Wg, hipStream_t s);
+                        int S, int Kp, int Hg, int Wg, void* out2, int H2, int W2, int C2, int t2, int l2, int d2h, int d2w,
+                        int write_nchw, hipStream_t s);
 int fm_conv_nhwc_wgrad(const void* gs, long gs_bytes, const void* xs, long xs_bytes, float* g2, float* db, int N, int K, int Kp, int P,
                         int Q, int Hg, int Wg, int gt, int gl, int gsh, int gsw, int R, int S, int Cp, int Hp, int Wp, int sh,
                         int sw, int* ptab, int build_tab, hipStream_t s);
@@ -790,8 +792,20 @@ void cnhwc_wprep(torch::Tensor w, torch::Tensor out, torch::Tensor out2, torch::
                      mode == 2 ? g2.data_ptr<float>() : nullptr, mode == 2 ? dw.data_ptr<float>() : nullptr, (int)K, (int)C,
                      (int)w.size(2), (int)w.size(3), (int)Cp, (int)Kp, (int)mode, (int)nsplit, cur());
 }
+// second output of a conv GEMM: a consumer's staged operand [N][H2][W2][C2] (o2 = {H2, W2, C2, t2, l2,
+// d2h, d2w, write_nchw}); every position the epilogue can address lies inside it
+static void* out2_chk(const c10::optional<torch::Tensor>& out2, const std::vector<int64_t>& o2, long N, long M, long OH,
+                      long OW) {
+  if (!out2.has_value() || !out2->defined()) return nullptr;
+  TORCH_CHECK(o2.size() == 8, "out2 geometry: {H2, W2, C2, t2, l2, d2h, d2w, write_nchw}");
+  TORCH_CHECK(o2[2] >= M && o2[5] >= 1 && o2[6] >= 1, "out2: C2 >= channels, dilation >= 1");
+  nhwc_chk(*out2, N * o2[0] * o2[1] * o2[2], "out2");
+  (void)OH; (void)OW;   // rows / columns outside [0,H2) x [0,W2) are dropped by the kernel
+  return out2->data_ptr();
+}
 void conv_nhwc_fwd(torch::Tensor xs, torch::Tensor wf, c10::optional<torch::Tensor> bias, torch::Tensor y, int64_t R,
-                   int64_t S, int64_t Cp, int64_t Hp, int64_t Wp, int64_t sh, int64_t sw, int64_t act) {
+                   int64_t S, int64_t Cp, int64_t Hp, int64_t Wp, int64_t sh, int64_t sw, int64_t act,
+                   c10::optional<torch::Tensor> out2, std::vector<int64_t> o2) {
   TORCH_CHECK(y.dim() == 4 && y.scalar_type() == torch::kBFloat16 && y.is_contiguous(), "conv_nhwc_fwd: bf16 y [N,K,P,Q]");
   const long N = y.size(0), K = y.size(1), P = y.size(2), Q = y.size(3);
   TORCH_CHECK(Cp % 8 == 0 && (P - 1) * sh + R <= Hp && (Q - 1) * sw + S <= Wp, "conv_nhwc_fwd: staged window extent");
@@ -803,19 +817,26 @@ void conv_nhwc_fwd(torch::Tensor xs, torch::Tensor wf, c10::optional<torch::Tens
     TORCH_CHECK(bias->scalar_type() == torch::kFloat32 && bias->numel() == K && bias->is_cuda(), "conv_nhwc_fwd: fp32 bias[K]");
     b = bias->data_ptr<float>();
   }
+  void* o2p = out2_chk(out2, o2, N, K, P, Q);
   fm_conv_nhwc_fwd(xs.data_ptr(), xs.numel() * 2, wf.data_ptr(), b, y.data_ptr(), (int)N, (int)K, (int)P, (int)Q, (int)R,
-                   (int)S, (int)Cp, (int)Hp, (int)Wp, (int)sh, (int)sw, (int)act, cur());
+                   (int)S, (int)Cp, (int)Hp, (int)Wp, (int)sh, (int)sw, (int)act, o2p, o2p ? (int)o2[0] : 0,
+                   o2p ? (int)o2[1] : 0, o2p ? (int)o2[2] : 0, o2p ? (int)o2[3] : 0, o2p ? (int)o2[4] : 0,
+                   o2p ? (int)o2[5] : 1, o2p ? (int)o2[6] : 1, o2p ? (int)o2[7] : 1, cur());
 }
 void conv_nhwc_dgrad(torch::Tensor gs, torch::Tensor wd, torch::Tensor dx, int64_t R, int64_t S, int64_t Kp, int64_t Hg,
-                     int64_t Wg, bool acc) {
+                     int64_t Wg, bool acc, c10::optional<torch::Tensor> out2, std::vector<int64_t> o2) {
   TORCH_CHECK(dx.dim() == 4, "conv_nhwc_dgrad: dx [N,C,H,W]");
   const long N = dx.size(0), C = dx.size(1), H = dx.size(2), W = dx.size(3);
   TORCH_CHECK(Kp % 8 == 0 && H + R - 1 <= Hg && W + S - 1 <= Wg, "conv_nhwc_dgrad: staged G extent");
   nhwc_chk(gs, N * Hg * Wg * Kp, "conv_nhwc_dgrad gs");
   nhwc_chk(wd, C * R * S * Kp, "conv_nhwc_dgrad wd");
   nhwc_chk(dx, N * C * H * W, "conv_nhwc_dgrad dx");
+  void* o2p = out2_chk(out2, o2, N, C, H, W);
+  TORCH_CHECK(o2p == nullptr || !acc, "conv_nhwc_dgrad: a second output needs the non-accumulating data gradient");
   fm_conv_nhwc_dgrad(gs.data_ptr(), gs.numel() * 2, wd.data_ptr(), dx.data_ptr(), acc ? 1 : 0, (int)N, (int)C, (int)H, (int)W,
-                     (int)R, (int)S, (int)Kp, (int)Hg, (int)Wg, cur());
+                     (int)R, (int)S, (int)Kp, (int)Hg, (int)Wg, o2p, o2p ? (int)o2[0] : 0, o2p ? (int)o2[1] : 0,
+                     o2p ? (int)o2[2] : 0, o2p ? (int)o2[3] : 0, o2p ? (int)o2[4] : 0, o2p ? (int)o2[5] : 1,
+                     o2p ? (int)o2[6] : 1, o2p ? (int)o2[7] : 1, cur());
 }
 int64_t conv_nhwc_wgrad(torch::Tensor gs, torch::Tensor xs, torch::Tensor g2, c10::optional<torch::Tensor> db, int64_t N, int64_t K, int64_t Kp, int64_t P,
                      int64_t Q, int64_t Hg, int64_t Wg, int64_t gt, int64_t gl, int64_t gsh, int64_t gsw, int64_t R, int64_t S,

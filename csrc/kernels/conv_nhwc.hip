@@ -68,6 +68,12 @@ struct ConvN {
   float* db;            // wgrad: bias gradient (+)= sum over pixels of the staged G (may be null)
   FastDiv dOPQ;         // fwd/dgrad output pixels per image
   int OPQ;
+  // fwd/dgrad second output: the result also stored straight into a CONSUMER's staged NHWC operand
+  // (out2[n][p*d2h + t2][q*d2w + l2][m], rows / columns outside [0,H2) x [0,W2) dropped) so the
+  // consumer skips its staging pass; write_nchw = 0 skips the NCHW store when nothing reads it
+  unsigned short* out2;
+  FastDiv dOQ;          // output pixels per row (p, q split of the output pixel)
+  int OQ, H2, W2, C2, t2, l2, d2h, d2w, write_nchw;
   int act, accum, ksplit, kt_per, tiles_m, tiles_n;
 };
 
@@ -355,6 +361,19 @@ __global__ void __launch_bounds__(NTH, 2) fm_conv_nhwc(ConvN p) {
         unsigned short* out = reinterpret_cast<unsigned short*>(p.out);
         const int img = fdiv(n, p.dOPQ), px = n - img * p.OPQ;
         const long o = ((long)img * p.M + m) * p.OPQ + px;
+        if (p.out2 != nullptr) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int nn = n + r;
+            if (nn >= p.N) break;
+            const int im = fdiv(nn, p.dOPQ), pr = nn - im * p.OPQ;
+            const int pp = fdiv(pr, p.dOQ), qq = pr - pp * p.OQ;
+            const int i2 = pp * p.d2h + p.t2, j2 = qq * p.d2w + p.l2;
+            if ((unsigned)i2 < (unsigned)p.H2 && (unsigned)j2 < (unsigned)p.W2)
+              p.out2[(((long)im * p.H2 + i2) * p.W2 + j2) * p.C2 + m] = f2bf(v[r]);
+          }
+          if (!p.write_nchw) continue;
+        }
         if (n + 3 < p.N && px + 3 < p.OPQ && (o & 3) == 0) {
           bf16x4_t w4;
           if (add) {
@@ -551,7 +570,9 @@ __global__ void __launch_bounds__(256) fm_nhwc_stage_flat(const unsigned short* 
 template <bool GRAD>
 void stage_launch(const void* src, const void* y, void* dst, int act, int N, int C, int H, int W, int Cp, int Hp, int Wp, int top,
                   int left, int dh, int dw, hipStream_t s) {
-  if (Wp < 32) {
+  // FM_STAGE_FLAT_BELOW (A/B, default 128; 32 / 64 / 128 measured in profiles/ab_stage_wgrad_r3y.txt): image widths below it take the flattened-pixel kernel
+  static const int flat_below = getenv("FM_STAGE_FLAT_BELOW") ? atoi(getenv("FM_STAGE_FLAT_BELOW")) : 128;
+  if (Wp < flat_below) {
     const int bpi = (Hp * Wp + 63) / 64;
     hipLaunchKernelGGL(fm_nhwc_stage_flat<GRAD>, dim3(N * bpi, (Cp + 63) / 64), dim3(256), 0, s, (const unsigned short*)src,
                        (const unsigned short*)y, (unsigned short*)dst, act, C, H, W, Cp, Hp, Wp, top, left, dh, dw, bpi);
@@ -658,7 +679,9 @@ Plan make_plan(int mode, int M, int N, int K) {
   q.tiles_n = (N + bn - 1) / bn;
   const int ktiles = (K + BK - 1) / BK;
   int ks = 1;
-  if (mode == CN_WGRAD) ks = std::max(1, std::min(512 / std::max(q.tiles_m * q.tiles_n, 1), ktiles / 8));
+  // FM_CONV_WGRAD_BLOCKS (A/B, default 512): split-K target of the weight gradient in blocks
+  static const int wg_blocks = getenv("FM_CONV_WGRAD_BLOCKS") ? std::max(1, atoi(getenv("FM_CONV_WGRAD_BLOCKS"))) : 512;
+  if (mode == CN_WGRAD) ks = std::max(1, std::min(wg_blocks / std::max(q.tiles_m * q.tiles_n, 1), ktiles / 8));
   q.kt_per = (ktiles + ks - 1) / ks;
   q.ksplit = (ktiles + q.kt_per - 1) / q.kt_per;
   return q;
@@ -728,8 +751,11 @@ extern "C" long fm_conv_nhwc_wgrad_ws(int N, int K, int P, int Q, int R, int S, 
 
 // fwd: xs staged [N][Hp][Wp][Cp] (window origin of output (p, q) at row p*sh, col q*sw),
 // wf [K][R*S*Cp] (mode 0), y [N][K][P][Q] bf16, bias fp32 [K] or null
+// out2 (may be null): the consumer's staged input [N][H2][W2][C2], this output at (t2, l2), or with
+// dilation (d2h, d2w); write_nchw = 0: y is not written
 extern "C" void fm_conv_nhwc_fwd(const void* xs, long xs_bytes, const void* wf, const float* bias, void* y, int N, int K,
-                                 int P, int Q, int R, int S, int Cp, int Hp, int Wp, int sh, int sw, int act, hipStream_t s) {
+                                 int P, int Q, int R, int S, int Cp, int Hp, int Wp, int sh, int sw, int act, void* out2,
+                                 int H2, int W2, int C2, int t2, int l2, int d2h, int d2w, int write_nchw, hipStream_t s) {
   ConvN p{};
   p.A = (const unsigned short*)wf; p.a_bytes = (long)K * R * S * Cp * 2;
   p.B = (const unsigned short*)xs; p.b_bytes = xs_bytes;
@@ -739,13 +765,18 @@ extern "C" void fm_conv_nhwc_fwd(const void* xs, long xs_bytes, const void* wf, 
   p.gb = make_pix(P * Q, Q, Hp, Wp, Cp, sh, sw, 0, 0);
   p.tb = make_tap(Cp, S, Wp);
   p.OPQ = P * Q; p.dOPQ = make_fastdiv(P * Q);
+  p.out2 = (unsigned short*)out2;
+  p.OQ = Q; p.dOQ = make_fastdiv(Q);
+  p.H2 = H2; p.W2 = W2; p.C2 = C2; p.t2 = t2; p.l2 = l2; p.d2h = d2h; p.d2w = d2w;
+  p.write_nchw = out2 == nullptr ? 1 : write_nchw;
   dispatch<CN_FWD>(p, s);
 }
 
 // dgrad: gs staged G [N][Hg][Wg][Kp] with G at (R-1-pt, S-1-pl) dilated by the stride, wd [C][R*S*Kp] (mode 1),
 // dx [N][C][H][W] bf16 (accum: +=)
 extern "C" void fm_conv_nhwc_dgrad(const void* gs, long gs_bytes, const void* wd, void* dx, int accum, int N, int C, int H,
-                                   int W, int R, int S, int Kp, int Hg, int Wg, hipStream_t s) {
+                                   int W, int R, int S, int Kp, int Hg, int Wg, void* out2, int H2, int W2, int C2, int t2,
+                                   int l2, int d2h, int d2w, int write_nchw, hipStream_t s) {
   ConvN p{};
   p.A = (const unsigned short*)wd; p.a_bytes = (long)C * R * S * Kp * 2;
   p.B = (const unsigned short*)gs; p.b_bytes = gs_bytes;
@@ -755,6 +786,10 @@ extern "C" void fm_conv_nhwc_dgrad(const void* gs, long gs_bytes, const void* wd
   p.gb = make_pix(H * W, W, Hg, Wg, Kp, 1, 1, 0, 0);
   p.tb = make_tap(Kp, S, Wg);
   p.OPQ = H * W; p.dOPQ = make_fastdiv(H * W);
+  p.out2 = (unsigned short*)out2;
+  p.OQ = W; p.dOQ = make_fastdiv(W);
+  p.H2 = H2; p.W2 = W2; p.C2 = C2; p.t2 = t2; p.l2 = l2; p.d2h = d2h; p.d2w = d2w;
+  p.write_nchw = out2 == nullptr ? 1 : write_nchw;
   dispatch<CN_DGRAD>(p, s);
 }
 

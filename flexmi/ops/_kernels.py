@@ -593,6 +593,8 @@ def _nhwc_stage_x(x, w, y, stride, pads, saved):
     shp = (N, Hp, Wp, Cp)
     if saved is not None:
         xs = saved.get("nhwc_x")
+        if xs is not None and saved.get("nhwc_x_prestaged") and tuple(xs.shape) == shp:
+            return xs, Cp, Hp, Wp     # the producing conv's epilogue already wrote it (conv chain fusion)
         if xs is None or tuple(xs.shape) != shp or xs.device != x.device:
             xs = torch.empty(shp, dtype=x.dtype, device=x.device)
             saved["nhwc_x"] = xs
@@ -600,6 +602,29 @@ def _nhwc_stage_x(x, w, y, stride, pads, saved):
         xs = scratch(x.device, "cn_xs", N * Hp * Wp * Cp, x.dtype).view(shp)
     C().nhwc_stage(x, xs, Cp, Hp, Wp, pads[0], pads[2], 1, 1)
     return xs, Cp, Hp, Wp
+
+
+def nhwc_x_geometry(x_shape, w_shape, y_shape, stride, pads):
+    """(N, Hp, Wp, Cp, top, left) of a conv's staged input (see _nhwc_stage_x)."""
+    R, S = w_shape[2], w_shape[3]
+    P, Q = y_shape[2], y_shape[3]
+    return x_shape[0], (P - 1) * stride[0] + R, (Q - 1) * stride[1] + S, _r8(x_shape[1]), pads[0], pads[2]
+
+
+def nhwc_g_geometry(x_shape, w_shape, y_shape, stride, pads, need_dx):
+    """(N, Hg, Wg, Kp, gt, gl, dh, dw) of a conv's staged output gradient (see _nhwc_backward), or
+    None where the staging does not apply."""
+    N, Cin, H, W = x_shape
+    Kout, _, R, S = w_shape
+    P, Q = y_shape[2], y_shape[3]
+    sh, sw = stride
+    pt, pl = pads[0], pads[2]
+    if need_dx:
+        gt, gl = R - 1 - pt, S - 1 - pl
+        if gt < 0 or gl < 0:
+            return None
+        return (N, max(H + R - 1, gt + (P - 1) * sh + 1), max(W + S - 1, gl + (Q - 1) * sw + 1), _r8(Kout), gt, gl, sh, sw)
+    return (N, P, Q, _r8(Kout), 0, 0, 1, 1)
 
 
 def _nhwc_forward(x, w, b, y, stride, pads, act, saved):
@@ -619,7 +644,9 @@ def _nhwc_forward(x, w, b, y, stride, pads, act, saved):
         C().cnhwc_wprep(w, wf, wd, w, w, Cp, _r8(Kout), 3, 1)
     else:
         C().cnhwc_wprep(w, wf, w, w, w, Cp, _r8(Kout), 0, 1)
-    C().conv_nhwc_fwd(xs, wf, b, y, R, S, Cp, Hp, Wp, stride[0], stride[1], int(act))
+    o2 = saved.get("nhwc_out2") if saved is not None else None   # conv chain fusion: the consumer's staged input
+    C().conv_nhwc_fwd(xs, wf, b, y, R, S, Cp, Hp, Wp, stride[0], stride[1], int(act), o2[0] if o2 else None,
+                      list(o2[1]) if o2 else [])
 
 
 def _nhwc_backward(x, w, y, dy, act, db, dx, dw, stride, pads, acc, saved):
@@ -635,18 +662,15 @@ def _nhwc_backward(x, w, y, dy, act, db, dx, dw, stride, pads, acc, saved):
     pt, pl = pads[0], pads[2]
     Kp = _r8(Kout)
     dev = x.device
-    if dx is not None:
-        gt, gl = R - 1 - pt, S - 1 - pl
-        if gt < 0 or gl < 0:
-            return False
-        Hg = max(H + R - 1, gt + (P - 1) * sh + 1)
-        Wg = max(W + S - 1, gl + (Q - 1) * sw + 1)
-        dh, dwl = sh, sw
-    else:
-        gt = gl = 0
-        Hg, Wg, dh, dwl = P, Q, 1, 1
-    gs = scratch(dev, "cn_gs", N * Hg * Wg * Kp, dy.dtype).view(N, Hg, Wg, Kp)
-    C().nhwc_stage_grad(dy, y, gs, act, Kp, Hg, Wg, gt, gl, dh, dwl)
+    geo_g = nhwc_g_geometry(x.shape, w.shape, dy.shape, stride, pads, dx is not None)
+    if geo_g is None:
+        return False
+    _, Hg, Wg, _, gt, gl, dh, dwl = geo_g
+    gs = saved.get("nhwc_gs") if saved is not None and saved.get("nhwc_g_prestaged") else None
+    if gs is None or tuple(gs.shape) != (N, Hg, Wg, Kp):
+        gs = scratch(dev, "cn_gs", N * Hg * Wg * Kp, dy.dtype).view(N, Hg, Wg, Kp)
+        C().nhwc_stage_grad(dy, y, gs, act, Kp, Hg, Wg, gt, gl, dh, dwl)
+    # else: the consumer conv's data-gradient epilogue already wrote G here (conv chain fusion)
     if saved is not None and saved.get("nhwc_x_ready") and "nhwc_x" in saved:
         xs = saved["nhwc_x"]
         Cp, Hp, Wp = xs.shape[3], xs.shape[1], xs.shape[2]
@@ -677,7 +701,8 @@ def _nhwc_backward(x, w, y, dy, act, db, dx, dw, stride, pads, acc, saved):
         if wd is None or wd.numel() != Cin * R * S * Kp:
             wd = scratch(dev, "cn_wd", Cin * R * S * Kp, w.dtype)
             C().cnhwc_wprep(w, wd, w, w, w, _r8(Cin), Kp, 1, 1)
-        C().conv_nhwc_dgrad(gs, wd, dx, R, S, Kp, Hg, Wg, bool(acc))
+        o2 = saved.get("nhwc_dgrad_out2") if saved is not None and not acc else None   # the producer's staged G
+        C().conv_nhwc_dgrad(gs, wd, dx, R, S, Kp, Hg, Wg, bool(acc), o2[0] if o2 else None, list(o2[1]) if o2 else [])
     return True
 
 

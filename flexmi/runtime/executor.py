@@ -912,6 +912,7 @@ class Executor:
         self._build_groups(ops)
         self._build_epilogue_fusion(ops)
         self._build_binary_relu_fusion(ops)
+        self._build_conv_chain_fusion(ops)
         if self.backend == "hip":
             # dW split-K reduces on a side stream (csrc/kernels/gemm_async.hip), joined before
             # every collective and at the end of the backward program (_with_gemm_joins)
@@ -1005,6 +1006,57 @@ class Executor:
                 continue
             ca.saved["fused_relu"] = (cb.outputs[0], cb.out_grads[0])
             cb.saved["fused_into_binary"] = True
+
+    def _build_conv_chain_fusion(self, ops):
+        """Conv A -> Conv B (A's output consumed only by B, same layout, both on the NHWC-staged bf16
+        path): A's forward epilogue also writes its output straight into B's staged NHWC input, so B
+        skips its staging pass, and when A is linear (no activation) A's NCHW output is not written
+        at all.  Backward mirror (A linear, B the sole consumer): B's data-gradient epilogue writes
+        A's staged output gradient (padded / stride-dilated for A's own data gradient), so A skips
+        its gradient staging and B's NCHW dX is not written.  The staged buffers are per-op and
+        zero-initialised once: their halos / dilation gaps are never written.  FM_CONV_CHAIN=0 turns
+        it off (A/B); off under --debug (skipped NCHW buffers stay unwritten)."""
+        from flexmi.core.types import ActiMode, OperatorType
+        from flexmi.ops import _kernels as K
+        if self.backend != "hip" or self.debug or os.environ.get("FM_CONV_CHAIN", "1") == "0":
+            return
+        for op in ops:
+            if op.op_type != OperatorType.OP_CONV2D:
+                continue
+            ca = self.ctx.get(op.guid)
+            t = op.outputs[0]
+            cons = self.consumers.get(t.guid, [])
+            if ca is None or ca.empty or len(cons) != 1 or t is self.final or op.guid in self.group_of:
+                continue
+            b, idx = cons[0]
+            cb = self.ctx.get(b.guid)
+            if (b.op_type != OperatorType.OP_CONV2D or cb is None or cb.empty or b.guid in self.group_of
+                    or not self.need[(b.guid, idx)].same_as(self.home[t.guid])):
+                continue
+            xa, wa, ya = ca.inputs[0], ca.wcompute[0], ca.outputs[0]
+            xb, wb, yb = cb.inputs[0], cb.wcompute[0], cb.outputs[0]
+            if any(v is None for v in (xa, wa, ya, xb, wb, yb)) or xb.shape != ya.shape:
+                continue
+            if not (K._nhwc_ok(xa, wa, op.groups) and K._nhwc_ok(xb, wb, b.groups)):
+                continue
+            dev = ya.device
+            # forward: A's epilogue -> B's staged input
+            N, Hp, Wp, Cp, top, left = K.nhwc_x_geometry(xb.shape, wb.shape, yb.shape, (b.sh, b.sw), b._pads(cb))
+            xs_b = torch.zeros((N, Hp, Wp, Cp), dtype=ya.dtype, device=dev)
+            cb.saved["nhwc_x"], cb.saved["nhwc_x_prestaged"] = xs_b, True
+            linear = op.activation == ActiMode.AC_MODE_NONE
+            ca.saved["nhwc_out2"] = (xs_b, (Hp, Wp, Cp, top, left, 1, 1, 0 if linear else 1))
+            # backward: B's data gradient -> A's staged output gradient (G_A = dY_A for a linear A)
+            if not linear or not cb.in_grads or cb.in_grads[0] is None or cb.in_grad_accumulate[0]:
+                continue
+            need_dx = bool(ca.in_grads) and ca.in_grads[0] is not None
+            geo = K.nhwc_g_geometry(xa.shape, wa.shape, ya.shape, (op.sh, op.sw), op._pads(ca), need_dx)
+            if geo is None:
+                continue
+            N, Hg, Wg, Kp, gt, gl, dh, dw = geo
+            gs_a = torch.zeros((N, Hg, Wg, Kp), dtype=ya.dtype, device=dev)
+            ca.saved["nhwc_gs"], ca.saved["nhwc_g_prestaged"] = gs_a, True
+            cb.saved["nhwc_dgrad_out2"] = (gs_a, (Hg, Wg, Kp, gt, gl, dh, dw, 0))
 
     def _build_groups(self, ops):
         """Fuse independent ops of the same kind and placement into one launch (embedding

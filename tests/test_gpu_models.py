@@ -315,3 +315,53 @@ def test_elementwise_vector_and_tail(gpu, dt, n, off):
     dx = torch.full_like(a, 0.5)
     K.unary_backward(0, a, y, g, dx, True)
     torch.testing.assert_close(dx.float(), (0.5 + g.float() * (a.float() > 0)).to(dt).float(), rtol=1e-2, atol=1e-2)
+
+
+def _convchain(device, B=8):
+    from flexmi.core import FFConfig, FFModel, SGDOptimizer, LossType, MetricsType, ActiMode
+    cfg = FFConfig()
+    cfg.batchSize = B
+    cfg.device = device
+    cfg.compute_dtype = "bf16" if device == "gpu" else "fp32"
+    m = FFModel(cfg)
+    x = m.create_tensor([B, 16, 14, 14])
+    NONE = ActiMode.AC_MODE_NONE
+    t = m.conv2d(x, 32, 1, 1, 1, 1, 0, 0, NONE)            # linear -> 3x3: fwd + bwd chain fusion
+    t = m.conv2d(t, 32, 3, 3, 2, 2, 1, 1, NONE)            # strided (dilated staged G for its dX)
+    t = m.conv2d(t, 48, 3, 3, 1, 1, 1, 1, ActiMode.AC_MODE_RELU)   # relu -> 1x1: forward fusion only
+    t = m.conv2d(t, 24, 1, 1, 1, 1, 0, 0)
+    t = m.flat(t)
+    t = m.dense(t, 10)
+    t = m.softmax(t)
+    m.compile(SGDOptimizer(m, 0.02), LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, [MetricsType.METRICS_ACCURACY])
+    m.init_layers()
+    return m, x
+
+
+def test_conv_chain_fusion_matches_cpu(gpu):
+    """Conv -> Conv chains on the NHWC path: the producer's epilogue writes the consumer's staged
+    input (and, for a linear producer, the consumer's data gradient writes the producer's staged G);
+    training matches the fp32 CPU executor."""
+    from flexmi.core import SingleDataLoader
+    rng = np.random.RandomState(2)
+    X = rng.randn(32, 16, 14, 14).astype(np.float32)
+    Y = rng.randint(0, 10, (32, 1)).astype(np.int32)
+    res = {}
+    for dev in ("cpu", "gpu"):
+        m, x = _convchain(dev)
+        dx = SingleDataLoader(m, x, X, 32)
+        dy = SingleDataLoader(m, m.get_label_tensor(), Y, 32)
+        for _ in range(4):
+            dx.next_batch(m)
+            dy.next_batch(m)
+            m.forward()
+            m.zero_gradients()
+            m.backward()
+            m.update()
+        if dev == "gpu":
+            ctxs = list(m._ex().ctx.values())
+            assert sum("nhwc_out2" in c.saved for c in ctxs) == 3
+            assert sum("nhwc_dgrad_out2" in c.saved for c in ctxs) == 2
+        res[dev] = [w.get_weights(m) for w in m.parameters]
+    for a, b in zip(res["cpu"], res["gpu"]):
+        assert np.abs(a - b).max() < 3e-2 * max(1.0, np.abs(a).max()), (a.shape, np.abs(a - b).max())
