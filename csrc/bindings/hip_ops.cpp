@@ -115,6 +115,10 @@ void fm_nhwc_stage_run(const void* src, void* dst, int N, int C, int H, int W, i
                        int dh, int dw, hipStream_t s);
 void fm_nhwc_stage_grad_run(const void* dy, const void* y, void* dst, int act, int N, int C, int H, int W, int Cp, int Hp,
                             int Wp, int top, int left, int dh, int dw, hipStream_t s);
+void fm_conv_nhwc_dgrad_strided(const void* gs, long gs_bytes, const void* w, void* wsub, void* dx, int accum, int N, int C,
+                                int H, int W, int K, int R, int S, int Kp, int Hg, int Wg, int gt, int gl, int sh, int sw,
+                                void* out2, int H2, int W2, int C2, int t2, int l2, int d2h, int d2w, int write_nchw,
+                                hipStream_t s);
 long fm_conv_nhwc_wgrad_ws(int N, int K, int P, int Q, int R, int S, int Cp);
 void fm_cnhwc_wprep_run(const void* w, void* out, void* out2, const float* g2, float* dw, int K, int C, int R, int S, int Cp,
                         int Kp, int mode, int nsplit, hipStream_t s);
@@ -838,6 +842,28 @@ void conv_nhwc_dgrad(torch::Tensor gs, torch::Tensor wd, torch::Tensor dx, int64
                      o2p ? (int)o2[2] : 0, o2p ? (int)o2[3] : 0, o2p ? (int)o2[4] : 0, o2p ? (int)o2[5] : 1,
                      o2p ? (int)o2[6] : 1, o2p ? (int)o2[7] : 1, cur());
 }
+// strided data gradient by stride phases over the stride-dilated staged G (w: the bf16 weights
+// [K,C,R,S]; wsub: bf16 scratch of C*R*S*Kp for the phases' sub-kernels)
+void conv_nhwc_dgrad_strided(torch::Tensor gs, torch::Tensor w, torch::Tensor wsub, torch::Tensor dx, int64_t Kp, int64_t Hg,
+                             int64_t Wg, int64_t gt, int64_t gl, int64_t sh, int64_t sw, bool acc,
+                             c10::optional<torch::Tensor> out2, std::vector<int64_t> o2) {
+  TORCH_CHECK(dx.dim() == 4 && w.dim() == 4 && w.size(1) == dx.size(1), "conv_nhwc_dgrad_strided: dx [N,C,H,W], w [K,C,R,S]");
+  const long N = dx.size(0), C = dx.size(1), H = dx.size(2), W = dx.size(3);
+  const long K = w.size(0), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(sh >= 1 && sw >= 1 && Kp % 8 == 0 && Kp >= K && gt >= 0 && gl >= 0 && H + R - 1 <= Hg && W + S - 1 <= Wg,
+              "conv_nhwc_dgrad_strided: staged G extent");
+  nhwc_chk(gs, N * Hg * Wg * Kp, "conv_nhwc_dgrad_strided gs");
+  nhwc_chk(w, K * C * R * S, "conv_nhwc_dgrad_strided w");
+  nhwc_chk(wsub, C * R * S * Kp, "conv_nhwc_dgrad_strided wsub");
+  nhwc_chk(dx, N * C * H * W, "conv_nhwc_dgrad_strided dx");
+  void* o2p = out2_chk(out2, o2, N, C, H, W);
+  TORCH_CHECK(o2p == nullptr || !acc, "conv_nhwc_dgrad_strided: a second output needs the non-accumulating data gradient");
+  fm_conv_nhwc_dgrad_strided(gs.data_ptr(), gs.numel() * 2, w.data_ptr(), wsub.data_ptr(), dx.data_ptr(), acc ? 1 : 0, (int)N,
+                             (int)C, (int)H, (int)W, (int)K, (int)R, (int)S, (int)Kp, (int)Hg, (int)Wg, (int)gt, (int)gl,
+                             (int)sh, (int)sw, o2p, o2p ? (int)o2[0] : 0, o2p ? (int)o2[1] : 0, o2p ? (int)o2[2] : 0,
+                             o2p ? (int)o2[3] : 0, o2p ? (int)o2[4] : 0, o2p ? (int)o2[5] : 1, o2p ? (int)o2[6] : 1,
+                             o2p ? (int)o2[7] : 1, cur());
+}
 int64_t conv_nhwc_wgrad(torch::Tensor gs, torch::Tensor xs, torch::Tensor g2, c10::optional<torch::Tensor> db, int64_t N, int64_t K, int64_t Kp, int64_t P,
                      int64_t Q, int64_t Hg, int64_t Wg, int64_t gt, int64_t gl, int64_t gsh, int64_t gsw, int64_t R, int64_t S,
                      int64_t Cp, int64_t Hp, int64_t Wp, int64_t sh, int64_t sw, torch::Tensor ptab, bool build_tab) {
@@ -1009,6 +1035,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("cnhwc_wprep", &cnhwc_wprep);
   m.def("conv_nhwc_fwd", &conv_nhwc_fwd);
   m.def("conv_nhwc_dgrad", &conv_nhwc_dgrad);
+  m.def("conv_nhwc_dgrad_strided", &conv_nhwc_dgrad_strided);
   m.def("conv_nhwc_wgrad", &conv_nhwc_wgrad);
   m.def("conv_s2d", &conv_s2d);
   m.def("conv_w_s2d", &conv_w_s2d);

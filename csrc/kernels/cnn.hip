@@ -283,19 +283,31 @@ __global__ void __launch_bounds__(256) fm_pool_bwd_rows(const T* __restrict__ y,
 // bytes) that reach its band of input rows, then every input element gathers its <= ceil(k/s)^2
 // windows from LDS.  Bands are sized to ~4 K staged elements so a layer launches thousands of
 // blocks (the whole-plane kernels below ran one block per plane: too few waves).
+// G > 1 (whole-plane bands only): one block takes G consecutive (n, c) planes -- a contiguous chunk
+// too -- so 17x17 / 8x8 Inception planes do not pay a block per 289 / 64 elements.
 template <typename T>
 __global__ void __launch_bounds__(256) fm_pool_fwd_band(const T* __restrict__ x, T* __restrict__ y,
-                                                        unsigned char* __restrict__ code, int H, int W, int P, int Q, int kh,
-                                                        int kw, int sh, int sw, int pt, int pl, int is_max, int act, int PB,
-                                                        int nbands, FastDiv dQ) {
+                                                        unsigned char* __restrict__ code, int NC, int H, int W, int P, int Q,
+                                                        int kh, int kw, int sh, int sw, int pt, int pl, int is_max, int act,
+                                                        int PB, int nbands, int G, FastDiv dQ, FastDiv dPQ) {
   extern __shared__ float sx[];
-  const int nc = blockIdx.x / nbands, band = blockIdx.x - nc * nbands;
+  int nc0, band, planes;
+  if (G > 1) {
+    nc0 = blockIdx.x * G;
+    band = 0;
+    planes = min(G, NC - nc0);
+  } else {
+    nc0 = blockIdx.x / nbands;
+    band = blockIdx.x - nc0 * nbands;
+    planes = 1;
+  }
   const int p0 = band * PB, p1 = min(P, p0 + PB);
-  const int hlo = max(0, p0 * sh - pt), hhi = min(H, (p1 - 1) * sh - pt + kh);
+  const int hlo = G > 1 ? 0 : max(0, p0 * sh - pt);
+  const int hhi = G > 1 ? H : min(H, (p1 - 1) * sh - pt + kh);
   const int rows = max(0, hhi - hlo);
-  const T* xp = x + ((long)nc * H + hlo) * W;
+  const T* xp = x + ((long)nc0 * H + hlo) * W;
   // 8 loads in flight per thread before the LDS stores (a load -> store loop waits on every load)
-  const int nst = rows * W;
+  const int nst = planes * rows * W;
   for (int b0 = 0; b0 < nst; b0 += 256 * 8) {
     float v[8];
 #pragma unroll
@@ -310,26 +322,33 @@ __global__ void __launch_bounds__(256) fm_pool_fwd_band(const T* __restrict__ x,
     }
   }
   __syncthreads();
-  const int nout = (p1 - p0) * Q;
+  const int nout1 = (p1 - p0) * Q;
+  const int nout = planes * nout1;
   for (int o = threadIdx.x; o < nout; o += 256) {
-    const int pr = fdiv(o, dQ), q = o - pr * Q;
+    int gi = 0, r = o;
+    if (G > 1) {
+      gi = fdiv(o, dPQ);
+      r = o - gi * nout1;
+    }
+    const int pr = fdiv(r, dQ), q = r - pr * Q;
     const int p = p0 + pr;
     const int h0 = p * sh - pt, w0 = q * sw - pl;
     // the window clipped to the plane: no per-tap bounds tests
     const int r0 = max(0, -h0), r1 = min(kh, H - h0), c0 = max(0, -w0), c1 = min(kw, W - w0);
+    const float* plane = sx + gi * rows * W;
     float m = -INFINITY, sacc = 0.f;
     int bc = 255;
-    for (int r = r0; r < r1; ++r) {
-      const float* row = sx + (h0 + r - hlo) * W + w0;
+    for (int rr = r0; rr < r1; ++rr) {
+      const float* row = plane + (h0 + rr - hlo) * W + w0;
       for (int c = c0; c < c1; ++c) {
         const float v = row[c];
-        if (v > m || bc == 255) bc = r * kw + c;
+        if (v > m || bc == 255) bc = rr * kw + c;
         m = fmaxf(m, v);
         sacc += v;
       }
     }
     const int cnt = max(0, r1 - r0) * max(0, c1 - c0);
-    const long oi = ((long)nc * P + p) * Q + q;
+    const long oi = ((long)(nc0 + gi) * P + p) * Q + q;
     y[oi] = fromf<T>(act_fwd(act, is_max ? m : (cnt ? sacc / cnt : 0.f)));
     if (code) code[oi] = (unsigned char)bc;
   }
@@ -337,22 +356,33 @@ __global__ void __launch_bounds__(256) fm_pool_fwd_band(const T* __restrict__ x,
 
 template <typename T>
 __global__ void __launch_bounds__(256) fm_pool_bwd_band(const T* __restrict__ y, const T* __restrict__ dy,
-                                                        const unsigned char* __restrict__ code, T* __restrict__ dx, int H,
-                                                        int W, int P, int Q, int kh, int kw, int sh, int sw, int pt, int pl,
-                                                        int is_max, int act, int acc, int HB, int nbands, int maxprows,
-                                                        FastDiv dW, FastDiv dQ, FastDiv dsh, FastDiv dsw) {
-  extern __shared__ float sg[];                       // [prows][Q] gradients, then [prows][Q] argmax bytes
-  unsigned char* sc = reinterpret_cast<unsigned char*>(sg + maxprows * Q);
-  const int nc = blockIdx.x / nbands, band = blockIdx.x - nc * nbands;
+                                                        const unsigned char* __restrict__ code, T* __restrict__ dx, int NC,
+                                                        int H, int W, int P, int Q, int kh, int kw, int sh, int sw, int pt,
+                                                        int pl, int is_max, int act, int acc, int HB, int nbands, int maxprows,
+                                                        int G, FastDiv dW, FastDiv dQ, FastDiv dsh, FastDiv dsw, FastDiv dPQ,
+                                                        FastDiv dHW) {
+  extern __shared__ float sg[];                       // [planes][prows][Q] gradients, then the argmax bytes
+  unsigned char* sc = reinterpret_cast<unsigned char*>(sg + G * maxprows * Q);
+  int nc0, band, planes;
+  if (G > 1) {
+    nc0 = blockIdx.x * G;
+    band = 0;
+    planes = min(G, NC - nc0);
+  } else {
+    nc0 = blockIdx.x / nbands;
+    band = blockIdx.x - nc0 * nbands;
+    planes = 1;
+  }
   const int h0b = band * HB, h1b = min(H, h0b + HB);
   // output rows whose windows reach input rows [h0b, h1b): p*sh - pt <= h1b-1 and p*sh - pt + kh > h0b
-  const int plo = (h0b + pt - kh + 1) > 0 ? fdiv(h0b + pt - kh + sh, dsh) : 0;
-  const int phi = min(P, (h1b - 1 + pt) >= 0 ? fdiv(h1b - 1 + pt, dsh) + 1 : 0);
+  const int plo = G > 1 ? 0 : ((h0b + pt - kh + 1) > 0 ? fdiv(h0b + pt - kh + sh, dsh) : 0);
+  const int phi = G > 1 ? P : min(P, (h1b - 1 + pt) >= 0 ? fdiv(h1b - 1 + pt, dsh) + 1 : 0);
   const int prows = max(0, phi - plo);
-  const long obase = ((long)nc * P + plo) * Q;
+  const int nst1 = prows * Q;
+  const long obase = ((long)nc0 * P + plo) * Q;
+  const int nst = planes * nst1;                      // planes > 1: prows == P, contiguous
   // stage g = act'(y) * dy per output window; average pooling divides by the window's clipped size
   // here, once per window instead of once per (input element, window) pair
-  const int nst = prows * Q;
   for (int b0 = 0; b0 < nst; b0 += 256 * 4) {
     float gd[4], yv[4];
     unsigned char cd[4];
@@ -365,35 +395,44 @@ __global__ void __launch_bounds__(256) fm_pool_bwd_band(const T* __restrict__ y,
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-    const int e = b0 + u * 256 + (int)threadIdx.x;
-    if (e >= nst) continue;
-    float g = act == ACT_NONE ? gd[u] : act_bwd(act, yv[u], gd[u]);
-    if (is_max) {
-      sc[e] = cd[u];
-    } else {
-      const int pr = fdiv(e, dQ), q = e - pr * Q;
-      const int hw0 = (plo + pr) * sh - pt, ww0 = q * sw - pl;
-      g /= (float)((min(hw0 + kh, H) - max(hw0, 0)) * (min(ww0 + kw, W) - max(ww0, 0)));
-    }
-    sg[e] = g;
+      const int e = b0 + u * 256 + (int)threadIdx.x;
+      if (e >= nst) continue;
+      float g = act == ACT_NONE ? gd[u] : act_bwd(act, yv[u], gd[u]);
+      if (is_max) {
+        sc[e] = cd[u];
+      } else {
+        const int r = G > 1 ? e - fdiv(e, dPQ) * nst1 : e;
+        const int pr = fdiv(r, dQ), q = r - pr * Q;
+        const int hw0 = (plo + pr) * sh - pt, ww0 = q * sw - pl;
+        g /= (float)((min(hw0 + kh, H) - max(hw0, 0)) * (min(ww0 + kw, W) - max(ww0, 0)));
+      }
+      sg[e] = g;
     }
   }
   __syncthreads();
-  const int nin = (h1b - h0b) * W;
-  T* dxp = dx + ((long)nc * H + h0b) * W;
+  const int nin1 = (h1b - h0b) * W;
+  const int nin = planes * nin1;
+  T* dxp = dx + ((long)nc0 * H + h0b) * W;
   for (int e = threadIdx.x; e < nin; e += 256) {
-    const int hr = fdiv(e, dW), w = e - hr * W;
+    int gi = 0, r = e;
+    if (G > 1) {
+      gi = fdiv(e, dHW);
+      r = e - gi * nin1;
+    }
+    const int hr = fdiv(r, dW), w = r - hr * W;
     const int h = h0b + hr;
     // windows holding (h, w): p in [ceil((h+pt-kh+1)/sh), floor((h+pt)/sh)], q likewise
     const int pmin = max(plo, h + pt + 1 > kh ? fdiv(h + pt - kh + sh, dsh) : 0);
     const int pmax = min(phi - 1, h + pt >= 0 ? fdiv(h + pt, dsh) : -1);
     const int qmin = w + pl + 1 > kw ? fdiv(w + pl - kw + sw, dsw) : 0;
     const int qmax = min(Q - 1, w + pl >= 0 ? fdiv(w + pl, dsw) : -1);
+    const float* gp = sg + gi * nst1;
+    const unsigned char* cp = sc + gi * nst1;
     float g = 0.f;
     for (int p = pmin; p <= pmax; ++p) {
-      const float* gr = sg + (p - plo) * Q;
+      const float* gr = gp + (p - plo) * Q;
       if (is_max) {
-        const unsigned char* cr = sc + (p - plo) * Q;
+        const unsigned char* cr = cp + (p - plo) * Q;
         const int rr = (h - (p * sh - pt)) * kw;
         for (int q = qmin; q <= qmax; ++q)
           if (cr[q] == (unsigned char)(rr + w - (q * sw - pl))) g += gr[q];
@@ -401,6 +440,64 @@ __global__ void __launch_bounds__(256) fm_pool_bwd_band(const T* __restrict__ y,
         for (int q = qmin; q <= qmax; ++q) g += gr[q];
       }
     }
+    if (acc) g += tof(dxp[e]);
+    dxp[e] = fromf<T>(g);
+  }
+}
+
+// Max pooling backward as a SCATTER: every output window routes its gradient to exactly one input
+// (its recorded argmax), so a block zeroes its dx band (or plane group) in LDS, adds each window's
+// gradient at the argmax with an LDS float atomic (overlapping windows can share an argmax), and
+// writes the band out once -- ~1/4 of the per-element gather's VALU work at stride 2, where the
+// gather re-derived each input's <= 4 candidate windows.
+template <typename T>
+__global__ void __launch_bounds__(256) fm_pool_bwd_max_scatter(const T* __restrict__ y, const T* __restrict__ dy,
+                                                               const unsigned char* __restrict__ code, T* __restrict__ dx,
+                                                               int NC, int H, int W, int P, int Q, int kh, int kw, int sh,
+                                                               int pt, int pl, int sw, int act, int acc, int HB, int nbands,
+                                                               int G, FastDiv dQ, FastDiv dPQ, FastDiv dkw, FastDiv dsh) {
+  extern __shared__ float sdx[];
+  int nc0, band, planes;
+  if (G > 1) {
+    nc0 = blockIdx.x * G;
+    band = 0;
+    planes = min(G, NC - nc0);
+  } else {
+    nc0 = blockIdx.x / nbands;
+    band = blockIdx.x - nc0 * nbands;
+    planes = 1;
+  }
+  const int h0b = band * HB, h1b = min(H, h0b + HB);
+  const int rows = h1b - h0b;
+  const int nin = planes * rows * W;
+  for (int e = threadIdx.x; e < nin; e += 256) sdx[e] = 0.f;
+  __syncthreads();
+  const int plo = G > 1 ? 0 : ((h0b + pt - kh + 1) > 0 ? fdiv(h0b + pt - kh + sh, dsh) : 0);
+  const int phi = G > 1 ? P : min(P, (h1b - 1 + pt) >= 0 ? fdiv(h1b - 1 + pt, dsh) + 1 : 0);
+  const int nwin1 = max(0, phi - plo) * Q;
+  const int nwin = planes * nwin1;
+  for (int e = threadIdx.x; e < nwin; e += 256) {
+    int gi = 0, r = e;
+    if (G > 1) {
+      gi = fdiv(e, dPQ);
+      r = e - gi * nwin1;
+    }
+    const int pr = fdiv(r, dQ), q = r - pr * Q;
+    const int p = plo + pr;
+    const long oi = ((long)(nc0 + gi) * P + p) * Q + q;
+    const int cd = code[oi];
+    if (cd == 255) continue;
+    const int rr = fdiv(cd, dkw), cc = cd - rr * kw;
+    const int h = p * sh - pt + rr;
+    if (h < h0b || h >= h1b) continue;             // this window's max lies in another band
+    const int w = q * sw - pl + cc;
+    const float gd = tof(dy[oi]);
+    atomicAdd(&sdx[(gi * rows + h - h0b) * W + w], act == ACT_NONE ? gd : act_bwd(act, tof(y[oi]), gd));
+  }
+  __syncthreads();
+  T* dxp = dx + ((long)nc0 * H + h0b) * W;
+  for (int e = threadIdx.x; e < nin; e += 256) {
+    float g = sdx[e];
     if (acc) g += tof(dxp[e]);
     dxp[e] = fromf<T>(g);
   }
@@ -698,10 +795,14 @@ static void fm_pool_fwd_t(const void* x, void* y, unsigned char* code, int N, in
   if (band && (long)kh * W <= 4096) {
     const int PB = std::max(1, std::min(P, ((4096 / W) - kh) / sh + 1));
     const int nbands = (P + PB - 1) / PB;
-    const int rows = std::min(H, (PB - 1) * sh + kh);
-    hipLaunchKernelGGL(fm_pool_fwd_band<T>, dim3(N * C * nbands), dim3(256), (size_t)rows * W * sizeof(float), st,
-                       (const T*)x, (T*)y, is_max ? code : nullptr, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, PB,
-                       nbands, make_fastdiv(Q));
+    const int NC = N * C;
+    // whole planes that are small: several per block
+    const int G = (nbands == 1 && (long)H * W <= 2048) ? std::max(1, std::min(NC, 4096 / (H * W))) : 1;
+    const int rows = G > 1 ? H : std::min(H, (PB - 1) * sh + kh);
+    const int blocks = G > 1 ? (NC + G - 1) / G : NC * nbands;
+    hipLaunchKernelGGL(fm_pool_fwd_band<T>, dim3(blocks), dim3(256), (size_t)G * rows * W * sizeof(float), st, (const T*)x,
+                       (T*)y, is_max ? code : nullptr, NC, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, PB, nbands, G,
+                       make_fastdiv(Q), make_fastdiv(P * Q));
     return;
   }
   hipLaunchKernelGGL(fm_pool_fwd_kernel<T>, dim3((total + 255) / 256), dim3(256), 0, st, (const T*)x, (T*)y,
@@ -730,13 +831,25 @@ static void fm_pool_bwd_t(const void* x, const void* y, const void* dy, void* dx
   if (!per_elem && band) {
     // input-row band HB: ~4 K input elements; it needs <= (HB + kh - 1) / sh + 1 output rows staged
     const int HB = std::max(1, std::min(H, 4096 / W));
-    const int maxprows = std::min(P, (HB + kh - 1) / sh + 2);
-    const size_t lds = (size_t)maxprows * Q * 5;
+    const int nbands = (H + HB - 1) / HB;
+    const int NC = N * C;
+    const int G = (nbands == 1 && (long)H * W <= 2048) ? std::max(1, std::min(NC, 4096 / (H * W))) : 1;
+    const int maxprows = G > 1 ? P : std::min(P, (HB + kh - 1) / sh + 2);
+    const size_t lds = (size_t)G * maxprows * Q * 5;
+    if (is_max) {                        // max pooling: scatter through the recorded argmax
+      const int blocks = G > 1 ? (NC + G - 1) / G : NC * nbands;
+      const size_t lds_s = (size_t)(G > 1 ? G * H : HB) * W * sizeof(float);
+      hipLaunchKernelGGL(fm_pool_bwd_max_scatter<T>, dim3(blocks), dim3(256), lds_s, st, (const T*)y, (const T*)dy,
+                         (const unsigned char*)code, (T*)dx, NC, H, W, P, Q, kh, kw, sh, pt, pl, sw, act, acc, HB, nbands, G,
+                         make_fastdiv(Q), make_fastdiv(P * Q), make_fastdiv(kw), make_fastdiv(sh));
+      return;
+    }
     if (lds <= 48 * 1024) {
-      const int nbands = (H + HB - 1) / HB;
-      hipLaunchKernelGGL(fm_pool_bwd_band<T>, dim3(N * C * nbands), dim3(256), lds, st, (const T*)y, (const T*)dy,
-                         (const unsigned char*)code, (T*)dx, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, acc, HB, nbands,
-                         maxprows, make_fastdiv(W), make_fastdiv(Q), make_fastdiv(sh), make_fastdiv(sw));
+      const int blocks = G > 1 ? (NC + G - 1) / G : NC * nbands;
+      hipLaunchKernelGGL(fm_pool_bwd_band<T>, dim3(blocks), dim3(256), lds, st, (const T*)y, (const T*)dy,
+                         (const unsigned char*)code, (T*)dx, NC, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, acc, HB,
+                         nbands, maxprows, G, make_fastdiv(W), make_fastdiv(Q), make_fastdiv(sh), make_fastdiv(sw),
+                         make_fastdiv(P * Q), make_fastdiv(H * W));
       return;
     }
   }

@@ -52,6 +52,8 @@ struct PixG {
 struct TapG {
   FastDiv dC8, dS;
   int C8, S, Wp, Cp;
+  int t0, rstep, sstep;   // tap (r, s, c8) at t0 + r*rstep + s*sstep + 8*c8 (a stride-phase sub-kernel
+                          // walks every sh-th row / sw-th column of the staged G)
 };
 
 struct ConvN {
@@ -74,6 +76,9 @@ struct ConvN {
   unsigned short* out2;
   FastDiv dOQ;          // output pixels per row (p, q split of the output pixel)
   int OQ, H2, W2, C2, t2, l2, d2h, d2w, write_nchw;
+  // strided NCHW output (a stride-phase data gradient): pixel (h', w') of the GEMM lands at
+  // (o_oh + o_sh*h', o_ow + o_sw*w') of an o_H x o_W plane
+  int strided_out, o_sh, o_sw, o_oh, o_ow, o_H, o_W;
   int act, accum, ksplit, kt_per, tiles_m, tiles_n;
 };
 
@@ -100,7 +105,7 @@ FM_DEVICE int pix_org(const PixG& g, int n, int p, int q) {
 FM_DEVICE int tap_off(const TapG& t, int j) {
   const int rs = fdiv(j, t.dC8), c8 = j - rs * t.C8;
   const int r = fdiv(rs, t.dS), s = rs - r * t.S;
-  return (r * t.Wp + s) * t.Cp + 8 * c8;
+  return t.t0 + r * t.rstep + s * t.sstep + 8 * c8;
 }
 
 // ---- operand loaders (global -> registers -> LDS image) ----------------------------------
@@ -374,6 +379,18 @@ __global__ void __launch_bounds__(NTH, 2) fm_conv_nhwc(ConvN p) {
           }
           if (!p.write_nchw) continue;
         }
+        if (p.strided_out) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int nn = n + r;
+            if (nn >= p.N) break;
+            const int im = fdiv(nn, p.dOPQ), pr = nn - im * p.OPQ;
+            const int hh = fdiv(pr, p.dOQ), ww = pr - hh * p.OQ;
+            unsigned short* d = out + (((long)im * p.M + m) * p.o_H + p.o_oh + p.o_sh * hh) * p.o_W + p.o_ow + p.o_sw * ww;
+            *d = f2bf(v[r] + (add ? bf2f(*d) : 0.f));
+          }
+          continue;
+        }
         if (n + 3 < p.N && px + 3 < p.OPQ && (o & 3) == 0) {
           bf16x4_t w4;
           if (add) {
@@ -628,7 +645,25 @@ TapG make_tap(int Cp, int S, int Wp) {
   t.dS = make_fastdiv(S);
   t.Wp = Wp;
   t.Cp = Cp;
+  t.t0 = 0;
+  t.rstep = Wp * Cp;
+  t.sstep = Cp;
   return t;
+}
+
+// stride-phase sub-kernel of the dgrad matrix: out[c][(ri*Ss + si)*Kp + k] =
+// w[k][c][R-1-(r0 + sh*ri)][S-1-(s0 + sw*si)] (0 for k >= K)
+__global__ void fm_cnhwc_wphase(const unsigned short* __restrict__ w, unsigned short* __restrict__ out, int K, int C, int R,
+                                int S, int Kp, int r0, int s0, int sh, int sw, int Rs, int Ss) {
+  const long total = (long)C * Rs * Ss * Kp;
+  for (long o = blockIdx.x * 256L + threadIdx.x; o < total; o += (long)gridDim.x * 256) {
+    const int k = (int)(o % Kp);
+    const long t = o / Kp;
+    const int rs = (int)(t % (Rs * Ss)), c = (int)(t / (Rs * Ss));
+    const int ri = rs / Ss, si = rs - ri * Ss;
+    const int r = R - 1 - (r0 + sh * ri), q = S - 1 - (s0 + sw * si);
+    out[o] = k < K ? w[(((long)k * C + c) * R + r) * S + q] : (unsigned short)0;
+  }
 }
 
 // wgrad fold: dw[k][c][r][s] += sum_z g2[z][k][(r*S+s)*Cp + c] over the split-K slabs.  Block = 32
@@ -641,8 +676,17 @@ __global__ void __launch_bounds__(256) fm_cnhwc_fold(const float* __restrict__ g
   const int ol = threadIdx.x & 31, zg = threadIdx.x >> 5;
   const long o = blockIdx.x * 32L + ol;
   float acc = 0.f;
-  if (o < slab)
-    for (int z = zg; z < nsplit; z += 8) acc += g2[z * slab + o];
+  if (o < slab) {
+    // 4 independent slab loads in flight per thread
+    float a4[4] = {0.f, 0.f, 0.f, 0.f};
+    int z = zg;
+    for (; z + 24 < nsplit; z += 32) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a4[u] += g2[(long)(z + 8 * u) * slab + o];
+    }
+    for (; z < nsplit; z += 8) a4[0] += g2[(long)z * slab + o];
+    acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+  }
   red[zg][ol] = acc;
   __syncthreads();
   if (threadIdx.x < 32 && o < slab) {
@@ -774,6 +818,10 @@ extern "C" void fm_conv_nhwc_fwd(const void* xs, long xs_bytes, const void* wf, 
 
 // dgrad: gs staged G [N][Hg][Wg][Kp] with G at (R-1-pt, S-1-pl) dilated by the stride, wd [C][R*S*Kp] (mode 1),
 // dx [N][C][H][W] bf16 (accum: +=)
+static void dgrad_phases(const void* gs, long gs_bytes, const void* w, void* wsub, void* dx, int accum, int N, int C, int H,
+                         int W, int K, int R, int S, int Kp, int Hg, int Wg, int gt, int gl, int sh, int sw, void* out2, int H2,
+                         int W2, int C2, int t2, int l2, int d2h, int d2w, int write_nchw, hipStream_t s);
+
 extern "C" void fm_conv_nhwc_dgrad(const void* gs, long gs_bytes, const void* wd, void* dx, int accum, int N, int C, int H,
                                    int W, int R, int S, int Kp, int Hg, int Wg, void* out2, int H2, int W2, int C2, int t2,
                                    int l2, int d2h, int d2w, int write_nchw, hipStream_t s) {
@@ -814,4 +862,67 @@ extern "C" int fm_conv_nhwc_wgrad(const void* gs, long gs_bytes, const void* xs,
   p.db = db;
   if (build_tab) hipLaunchKernelGGL(fm_pix_table, dim3(fm_grid(p.npix, 256, 2048)), dim3(256), 0, s, ptab, p.npix, p.ga, p.gb);
   return dispatch<CN_WGRAD>(p, s);
+}
+
+// Strided data gradient by stride phases: output pixels (a + sh*h', b + sw*w') of phase (a, b) only
+// meet the taps r' = r0 + sh*i, s' = s0 + sw*j of the flipped kernel (r0 = (gt - a) mod sh) at
+// nonzero rows of the stride-dilated staged G -- so each phase is a dense GEMM over its sub-kernel
+// (Rs x Ss taps) with a strided NCHW store, and the phases together do exactly the layer's MACs
+// (the dilated form computed every tap of every output pixel: sh*sw times the work).  wsub: bf16
+// scratch of C * R*S * Kp (the phases' sub-kernels partition the R*S taps).
+static void dgrad_phases(const void* gs, long gs_bytes, const void* w, void* wsub, void* dx, int accum, int N, int C, int H,
+                         int W, int K, int R, int S, int Kp, int Hg, int Wg, int gt, int gl, int sh, int sw, void* out2, int H2,
+                         int W2, int C2, int t2, int l2, int d2h, int d2w, int write_nchw, hipStream_t s) {
+  bool empty_phase = false;
+  for (int a = 0; a < sh && a < H; ++a)
+    for (int b = 0; b < sw && b < W; ++b) {
+      const int r0 = ((gt - a) % sh + sh) % sh, s0 = ((gl - b) % sw + sw) % sw;
+      if (r0 >= R || s0 >= S) empty_phase = true;
+    }
+  // phases without taps receive no gradient: zero the outputs first (the others overwrite theirs)
+  if (empty_phase && !accum) {
+    if (write_nchw || out2 == nullptr) (void)hipMemsetAsync(dx, 0, (size_t)N * C * H * W * 2, s);
+  }
+  long woff = 0;
+  for (int a = 0; a < sh && a < H; ++a)
+    for (int b = 0; b < sw && b < W; ++b) {
+      const int r0 = ((gt - a) % sh + sh) % sh, s0 = ((gl - b) % sw + sw) % sw;
+      if (r0 >= R || s0 >= S) continue;
+      const int Rs = (R - r0 + sh - 1) / sh, Ss = (S - s0 + sw - 1) / sw;
+      const int Ha = (H - a + sh - 1) / sh, Wb = (W - b + sw - 1) / sw;
+      unsigned short* wp = (unsigned short*)wsub + woff;
+      const long nw = (long)C * Rs * Ss * Kp;
+      woff += nw;
+      hipLaunchKernelGGL(fm_cnhwc_wphase, dim3(fm_grid(nw, 256, 1024)), dim3(256), 0, s, (const unsigned short*)w, wp, K, C, R,
+                         S, Kp, r0, s0, sh, sw, Rs, Ss);
+      ConvN p{};
+      p.A = wp; p.a_bytes = nw * 2;
+      p.B = (const unsigned short*)gs; p.b_bytes = gs_bytes;
+      p.out = dx; p.accum = accum;
+      p.M = C; p.N = N * Ha * Wb; p.K = Rs * Ss * Kp;
+      p.npix = p.N;
+      p.gb = make_pix(Ha * Wb, Wb, Hg, Wg, Kp, sh, sw, a, b);
+      p.tb = make_tap(Kp, Ss, Wg);
+      p.tb.t0 = (r0 * Wg + s0) * Kp;
+      p.tb.rstep = sh * Wg * Kp;
+      p.tb.sstep = sw * Kp;
+      p.OPQ = Ha * Wb; p.dOPQ = make_fastdiv(Ha * Wb);
+      p.OQ = Wb; p.dOQ = make_fastdiv(Wb);
+      p.strided_out = 1;
+      p.o_sh = sh; p.o_sw = sw; p.o_oh = a; p.o_ow = b; p.o_H = H; p.o_W = W;
+      p.out2 = (unsigned short*)out2;
+      p.H2 = H2; p.W2 = W2; p.C2 = C2;
+      p.t2 = t2 + a * d2h; p.l2 = l2 + b * d2w; p.d2h = d2h * sh; p.d2w = d2w * sw;
+      p.write_nchw = out2 == nullptr ? 1 : write_nchw;
+      dispatch<CN_DGRAD>(p, s);
+    }
+}
+
+// strided data gradient (sh or sw > 1) over the stride-dilated staged G, by stride phases
+extern "C" void fm_conv_nhwc_dgrad_strided(const void* gs, long gs_bytes, const void* w, void* wsub, void* dx, int accum, int N,
+                                           int C, int H, int W, int K, int R, int S, int Kp, int Hg, int Wg, int gt, int gl,
+                                           int sh, int sw, void* out2, int H2, int W2, int C2, int t2, int l2, int d2h,
+                                           int d2w, int write_nchw, hipStream_t s) {
+  dgrad_phases(gs, gs_bytes, w, wsub, dx, accum, N, C, H, W, K, R, S, Kp, Hg, Wg, gt, gl, sh, sw, out2, H2, W2, C2, t2, l2,
+               d2h, d2w, write_nchw, s);
 }

@@ -573,6 +573,9 @@ def _conv_backward_phases(x, w, g, dx, dw, s_, pads, acc):
 # per-element gather math, no halo masks).  The forward's staged input is kept in ``saved`` for
 # the weight gradient.  Stems on few channels keep the NCHW kernels (space-to-depth).
 NHWC_CONV = os.environ.get("FM_CONV_NHWC", "1") != "0"
+# FM_CONV_PHASE_DGRAD=0 (A/B): strided data gradients as one GEMM over the stride-dilated G (s*s the
+# MACs) instead of one GEMM per stride phase
+STRIDE_PHASE_DGRAD = os.environ.get("FM_CONV_PHASE_DGRAD", "1") != "0"
 
 
 def _r8(v):
@@ -697,11 +700,17 @@ def _nhwc_backward(x, w, y, dy, act, db, dx, dw, stride, pads, acc, saved):
                                  build)
     C().cnhwc_wprep(w, w, w, g2, dw.view(-1), Cp, Kp, 2, nsplit)
     if dx is not None:
+        o2 = saved.get("nhwc_dgrad_out2") if saved is not None and not acc else None   # the producer's staged G
+        if (dh > 1 or dwl > 1) and STRIDE_PHASE_DGRAD:
+            # strided: one dense GEMM per stride phase over its sub-kernel (no dilation waste)
+            wsub = scratch(dev, "cn_wsub", Cin * R * S * Kp, w.dtype)
+            C().conv_nhwc_dgrad_strided(gs, w, wsub, dx, Kp, Hg, Wg, gt, gl, dh, dwl, bool(acc), o2[0] if o2 else None,
+                                        list(o2[1]) if o2 else [])
+            return True
         wd = saved.get("nhwc_wd") if saved is not None and saved.get("nhwc_x_ready") else None
         if wd is None or wd.numel() != Cin * R * S * Kp:
             wd = scratch(dev, "cn_wd", Cin * R * S * Kp, w.dtype)
             C().cnhwc_wprep(w, wd, w, w, w, _r8(Cin), Kp, 1, 1)
-        o2 = saved.get("nhwc_dgrad_out2") if saved is not None and not acc else None   # the producer's staged G
         C().conv_nhwc_dgrad(gs, wd, dx, R, S, Kp, Hg, Wg, bool(acc), o2[0] if o2 else None, list(o2[1]) if o2 else [])
     return True
 

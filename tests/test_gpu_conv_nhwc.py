@@ -117,3 +117,28 @@ def test_conv_nhwc_matches_nchw_path(gpu, monkeypatch):
         Kk.conv2d_forward(x, w, b, y, (1, 1), (1, 1, 1, 1), 11, 1, {})
         outs.append(y.float())
     assert _err(outs[0], outs[1]) < 1e-2
+
+
+@pytest.mark.parametrize("phase", [True, False])
+def test_strided_dgrad_phase_and_dilated_agree(gpu, monkeypatch, phase):
+    """Strided data gradient: the per-stride-phase GEMMs (default) and the single GEMM over the
+    stride-dilated G both match the float64 oracle, incl. a phase without taps (1x1 / 2)."""
+    from flexmi.ops import _kernels as Kk
+    monkeypatch.setattr(Kk, "STRIDE_PHASE_DGRAD", phase)
+    for (N, C, H, W, K, R, S, s, pads) in [(2, 32, 15, 14, 40, 3, 3, 2, (1, 1, 1, 1)), (2, 24, 13, 13, 16, 1, 1, 2, (0, 0, 0, 0)),
+                                           (1, 16, 16, 17, 24, 5, 5, 3, (2, 2, 1, 1))]:
+        torch.manual_seed(C + K)
+        x = torch.randn(N, C, H, W, device=gpu).bfloat16()
+        w = (torch.randn(K, C, R, S, device=gpu) / (C * R * S) ** 0.5).bfloat16()
+        _, _, yr = _oracle(x, w, None, s, pads)
+        y = torch.empty(yr.shape, device=gpu, dtype=torch.bfloat16)
+        Kk.conv2d_forward(x, w, None, y, (s, s), pads, 10, 1, {})
+        dy = torch.randn(yr.shape, device=gpu).bfloat16()
+        gx, gw = _grads(x, w, s, pads, dy.double().cpu())
+        for acc in (False, True):
+            dx0 = torch.randn(N, C, H, W, device=gpu).bfloat16()
+            dx = dx0.clone()
+            dw = torch.zeros(K, C, R, S, device=gpu)
+            Kk.conv2d_backward(x, w, y, dy, dx, dw, None, (s, s), pads, 10, 1, acc, None)
+            assert _err(dx, gx + (dx0.double().cpu() if acc else 0)) < 1.5e-2, (phase, acc, R, s)
+            assert _err(dw, gw) < 1.5e-2
