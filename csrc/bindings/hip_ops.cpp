@@ -18,6 +18,8 @@ int fm_gemm(const void* A, long lda, long sA, int a_kcontig, const void* B, long
             long ldc, long sC, int c_fp32, const float* bias, int M, int N, int K, int batch, float alpha, int beta,
             int act, float* ws, long ws_bytes, int ksplit_req, const void* act_y, long lday, int bwd_act,
             float* colsum, float* rowsum_a, hipStream_t stream);
+void fm_gemm_f32_set_split(int on);
+int fm_gemm_f32_get_split();
 int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, const float* B, long ldb, long sB, int b_kcontig,
                 float* C, long ldc, long sC, const float* bias, int M, int N, int K, int batch, float alpha, int beta,
                 int act, float* ws, long ws_bytes, int ksplit_req, const float* act_y, long lday, int bwd_act,
@@ -1035,6 +1037,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("cnhwc_wprep", &cnhwc_wprep);
   m.def("conv_nhwc_fwd", &conv_nhwc_fwd);
   m.def("conv_nhwc_dgrad", &conv_nhwc_dgrad);
+  m.def("gemm_f32_set_split", [](bool on) { fm_gemm_f32_set_split(on ? 1 : 0); });
+  m.def("gemm_f32_get_split", []() { return fm_gemm_f32_get_split() != 0; });
   m.def("conv_nhwc_dgrad_strided", &conv_nhwc_dgrad_strided);
   m.def("conv_nhwc_wgrad", &conv_nhwc_wgrad);
   m.def("conv_s2d", &conv_s2d);

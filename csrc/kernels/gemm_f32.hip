@@ -22,7 +22,7 @@
 // activation, activation-backward of the layer below (y fp32) + its bias-gradient column sums,
 // beta accumulate; dW GEMMs fold the bias gradient in as row sums of the staged A tiles.
 // Split-K writes fp32 slabs reduced by one vectorised reduce launch.  XCD-aware tile order.
-#include "common.h"
+#include "gemm_common.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -420,6 +420,266 @@ __global__ void fm_gemm_f32_reduce(GemmF p, int v4) {
       s = act_fwd(p.act, s * p.alpha + (p.bias ? p.bias[n] : 0.f));
       *d = s + (p.beta ? *d : 0.f);
     }
+  }
+}
+
+// ---- fp32 GEMM on the bf16 matrix cores by exact three-way splitting --------------------------
+// CDNA4's fp32 MFMA (v_mfma_f32_16x16x4_f32, 157 TF/s) is 16x slower than its bf16 MFMA.  Every fp32
+// operand x is split EXACTLY into three bf16 terms at LDS-store time: h = bf16(x), m = bf16(x - h),
+// l = bf16(x - h - m) (x - h and x - h - m are exact fp32 differences; h + m + l carries 24
+// significant bits, the fp32 mantissa, with a final rounding error <= 2^-25 |x|).  The products
+// x*y are then sum over the six terms with i + j <= 2 (hh, hm, mh, hl, mm, lh) on
+// v_mfma_f32_16x16x32_bf16 with fp32 accumulation: every bf16 x bf16 product is exact in fp32, and
+// the dropped terms (ml, lm, ll) are <= 2^-24 |x y| -- the same order as the fp32 product rounding
+// itself, so the result has native-fp32 accuracy (tests/test_gpu_fp32.py checks it against float64
+// at the native kernel's tolerance).  Cost per k: 6 bf16 MFMA (16 cycles) vs 8 fp32 MFMA (32
+// cycles) for a 16x16x32 block: 2.7x the fp32 MFMA rate.
+// Tile 128x128x64, 512 threads (8 waves, 64x32 per wave), six bf16 LDS planes (3 per operand,
+// gemm_common.h images: K-contiguous 128-B rows / MN-contiguous transposed reads) = 96 KB, one
+// block per CU; the next k-tile's fp32 operands are loaded into registers during this tile's MFMAs.
+constexpr int X3_BK = 64;
+
+FM_DEVICE void split3(const float (&x)[8], u32x4_t& h, u32x4_t& m, u32x4_t& l) {
+  unsigned short hs[8], ms[8], ls[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    hs[t] = f2bf(x[t]);
+    const float r1 = x[t] - bf2f(hs[t]);
+    ms[t] = f2bf(r1);
+    ls[t] = f2bf(r1 - bf2f(ms[t]));
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    h[u] = (unsigned)hs[2 * u] | ((unsigned)hs[2 * u + 1] << 16);
+    m[u] = (unsigned)ms[2 * u] | ((unsigned)ms[2 * u + 1] << 16);
+    l[u] = (unsigned)ls[2 * u] | ((unsigned)ls[2 * u + 1] << 16);
+  }
+}
+
+template <bool KC, int R>
+struct StageX3 {
+  static constexpr int NTH = 512;
+  static constexpr int PER_T = R * X3_BK / 8 / NTH;
+  float v[PER_T][8];
+
+  FM_DEVICE void load(const float* __restrict__ p, long ld, int row0, int rows, int k0, int K, int tid, int vec) {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int ci = tid + NTH * i;
+      int gr, gk;
+      if constexpr (KC) {
+        gr = row0 + (ci >> 3);
+        gk = k0 + 8 * (ci & 7);
+      } else {
+        gk = k0 + ci / (R / 8);
+        gr = row0 + 8 * (ci % (R / 8));
+      }
+      const bool full = KC ? (gr < rows && gk + 8 <= K) : (gk < K && gr + 8 <= rows);
+      if (vec && full) {
+        const float* src = KC ? p + (long)gr * ld + gk : p + (long)gk * ld + gr;
+        const f32x4_t a = *reinterpret_cast<const f32x4_t*>(src);
+        const f32x4_t b = *reinterpret_cast<const f32x4_t*>(src + 4);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          v[i][t] = a[t];
+          v[i][4 + t] = b[t];
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int r = KC ? gr : gr + t, k = KC ? gk + t : gk;
+          v[i][t] = (r < rows && k < K) ? (KC ? p[(long)r * ld + k] : p[(long)k * ld + r]) : 0.f;
+        }
+      }
+    }
+  }
+
+  FM_DEVICE void store(char* l0, char* l1, char* l2, int tid) const {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int ci = tid + NTH * i;
+      int a, c;
+      if constexpr (KC) {
+        a = ci >> 3;
+        c = ci & 7;
+      } else {
+        a = ci / (R / 8);
+        c = ci % (R / 8);
+      }
+      u32x4_t h, m, l;
+      split3(v[i], h, m, l);
+      const int off = lds_off<KC, R>(a, c);
+      *reinterpret_cast<u32x4_t*>(l0 + off) = h;
+      *reinterpret_cast<u32x4_t*>(l1 + off) = m;
+      *reinterpret_cast<u32x4_t*>(l2 + off) = l;
+    }
+  }
+
+  // MN-contiguous operand: a thread's chunks cover the same 8 rows (bias-gradient row sums)
+  FM_DEVICE void rowsum(float (&s)[8]) const {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) s[t] += v[i][t];
+  }
+};
+
+template <bool AK, bool BKC>
+__global__ void __launch_bounds__(512, 1) fm_gemm_x3_kernel(GemmF p, int vec) {
+  constexpr int BM = 128, BN = 128, NTH = 512, WN = 4, TM = 64, TN = 32, MR = TM / 16, NR = TN / 16;
+  constexpr int PL = 128 * X3_BK * 2;   // one bf16 plane of one operand
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const la0 = smem;
+  char* const lb0 = smem + 3 * PL;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int bid = xcd_remap_f(blockIdx.x, p.tiles_m * p.tiles_n);
+  int tm, tn;
+  if (p.n_fast) {
+    tn = bid % p.tiles_n;
+    tm = bid / p.tiles_n;
+  } else {
+    tm = bid % p.tiles_m;
+    tn = bid / p.tiles_m;
+  }
+  const int zb = blockIdx.y, split = blockIdx.z;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const float* A = p.A + (long)zb * p.sA;
+  const float* B = p.B + (long)zb * p.sB;
+  const int ktiles = (p.K + X3_BK - 1) / X3_BK;
+  const int kt_per = (ktiles + p.ksplit - 1) / p.ksplit;
+  const int kt0 = split * kt_per, kt1 = min(ktiles, kt0 + kt_per);
+
+  f32x4_t acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  StageX3<AK, BM> sa;
+  StageX3<BKC, BN> sb;
+  const bool dorow = (!AK) && p.rowsum_a != nullptr && tn == 0;
+  float rs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int va = vec & 1, vb = (vec >> 1) & 1;
+  if (kt0 < kt1) {
+    sa.load(A, p.lda, m0, p.M, kt0 * X3_BK, p.K, tid, va);
+    sb.load(B, p.ldb, n0, p.N, kt0 * X3_BK, p.K, tid, vb);
+  }
+  for (int kt = kt0; kt < kt1; ++kt) {
+    __syncthreads();                              // every wave is done reading the previous tile
+    sa.store(la0, la0 + PL, la0 + 2 * PL, tid);
+    sb.store(lb0, lb0 + PL, lb0 + 2 * PL, tid);
+    if constexpr (!AK) {
+      if (dorow) sa.rowsum(rs);
+    }
+    __syncthreads();
+    if (kt + 1 < kt1) {                           // next tile's operands land during the MFMAs
+      sa.load(A, p.lda, m0, p.M, (kt + 1) * X3_BK, p.K, tid, va);
+      sb.load(B, p.ldb, n0, p.N, (kt + 1) * X3_BK, p.K, tid, vb);
+    }
+#pragma unroll
+    for (int kk = 0; kk < X3_BK / 32; ++kk) {
+      bf16x8_t af[3][MR], bfr[3][NR];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+        for (int i = 0; i < MR; ++i) af[pl][i] = frag<AK, BM>(la0 + pl * PL, wm * TM + 16 * i, kk, lane);
+#pragma unroll
+        for (int j = 0; j < NR; ++j) bfr[pl][j] = frag<BKC, BN>(lb0 + pl * PL, wn * TN + 16 * j, kk, lane);
+      }
+      // small terms first, the dominant h*h product last
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+          constexpr int PA[6] = {2, 1, 0, 1, 0, 0};
+          constexpr int PB[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+          for (int t = 0; t < 6; ++t)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8v_t*>(&bfr[PB[t]][j]),
+                                                                *reinterpret_cast<bf16x8v_t*>(&af[PA[t]][i]), acc[i][j],
+                                                                0, 0, 0);
+        }
+    }
+  }
+  if constexpr (!AK) {
+    if (dorow) {   // reduce the threads sharing each 8-row group, one atomic per row
+      __syncthreads();
+      float* red = reinterpret_cast<float*>(smem);
+      constexpr int G = BM / 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[(tid / G) * BM + (tid % G) * 8 + j] = rs[j];
+      __syncthreads();
+      if (tid < BM) {
+        float x = 0.f;
+        for (int t = 0; t < NTH / G; ++t) x += red[t * BM + tid];
+        if (m0 + tid < p.M) atomicAdd(p.rowsum_a + m0 + tid, x);
+      }
+    }
+  }
+
+  // epilogue: lane owns C[m][n .. n+3], m = mbase + 16 i + (lane & 15), n = nbase + 16 j + 4 (lane >> 4)
+  const int mbase = m0 + wm * TM, nbase = n0 + wn * TN;
+  const int mrow = lane & 15, ncol = 4 * (lane >> 4);
+  float csum[NR][4];
+#pragma unroll
+  for (int j = 0; j < NR; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) csum[j][r] = 0.f;
+#pragma unroll
+  for (int i = 0; i < MR; ++i) {
+    const int m = mbase + 16 * i + mrow;
+    const bool mok = m < p.M;
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const int n = nbase + 16 * j + ncol;
+      if (!mok || n >= p.N) continue;
+      const bool full = n + 3 < p.N;
+      if (p.ksplit > 1) {   // fp32 slab of this split: the reduce launch applies the epilogue
+        float* dst = p.ws + (((long)zb * p.ksplit + split) * p.M + m) * (long)p.N + n;
+        if (full && (p.N & 3) == 0) {
+          *reinterpret_cast<f32x4_t*>(dst) = acc[i][j];
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (n + r < p.N) dst[r] = acc[i][j][r];
+        }
+        continue;
+      }
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool ok = n + r < p.N;
+        v[r] = acc[i][j][r] * p.alpha + ((p.bias && ok) ? p.bias[n + r] : 0.f);
+        v[r] = act_fwd(p.act, v[r]);
+        if (p.ay) v[r] = act_bwd(p.bact, ok ? p.ay[(long)m * p.lday + n + r] : 0.f, v[r]);
+        if (p.colsum && ok) csum[j][r] += v[r];
+      }
+      float* dst = p.C + (long)zb * p.sC + (long)m * p.ldc + n;
+      if (full && (p.ldc & 3) == 0 && ((((uintptr_t)dst) & 15) == 0)) {
+        f32x4_t o = {v[0], v[1], v[2], v[3]};
+        if (p.beta) o += *reinterpret_cast<f32x4_t*>(dst);
+        *reinterpret_cast<f32x4_t*>(dst) = o;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (n + r < p.N) dst[r] = v[r] + (p.beta ? dst[r] : 0.f);
+      }
+    }
+  }
+  if (p.colsum && p.ksplit == 1) {   // bias gradient of the layer below: 16 rows per lane group, 1 atomic/col
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float x = csum[j][r];
+        x += __shfl_xor(x, 1, 64);
+        x += __shfl_xor(x, 2, 64);
+        x += __shfl_xor(x, 4, 64);
+        x += __shfl_xor(x, 8, 64);
+        const int n = nbase + 16 * j + ncol + r;
+        if (mrow == 0 && n < p.N) atomicAdd(p.colsum + n, x);
+      }
   }
 }
 
@@ -1010,6 +1270,10 @@ extern "C" void fm_gemm_f32_set_variant(int v) { g_f32_variant = v; }
 // Same contract as fm_gemm (gemm.hip) with fp32 operands and output:
 //   A_kcontig: A stored [M][K] (lda >= K) else [K][M] (lda >= M)
 //   B_kcontig: B stored [N][K] (ldb >= K) else [K][N] (ldb >= N)
+static int g_f32_split = -1;   // -1: from FM_F32_SPLIT at the first call
+extern "C" void fm_gemm_f32_set_split(int on) { g_f32_split = on ? 1 : 0; }
+extern "C" int fm_gemm_f32_get_split() { return g_f32_split == 1 ? 1 : 0; }
+
 extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, const float* B, long ldb, long sB,
                            int b_kcontig, float* C, long ldc, long sC, const float* bias, int M, int N, int K, int batch,
                            float alpha, int beta, int act, float* ws, long ws_bytes, int ksplit_req, const float* act_y,
@@ -1032,6 +1296,49 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
   // small-grid ones (one 96 KiB block per CU: 22 -> 39 us, 29 -> 45 us), 1.72 vs 1.68 ms/step.
   const int variant = g_f32_variant;
   p.atomic = 0;
+  // fp32 on the bf16 matrix cores (exact three-way operand split, fm_gemm_x3_kernel): FM_F32_SPLIT=1
+  // or fm_gemm_f32_set_split(1)
+  if (g_f32_split < 0) g_f32_split = (getenv("FM_F32_SPLIT") != nullptr && atoi(getenv("FM_F32_SPLIT")) == 1) ? 1 : 0;
+  if (g_f32_split == 1 && K >= 64 && M >= 64 && N >= 64) {
+    const bool fused = act_y != nullptr || colsum != nullptr;
+    p.tiles_m = (M + 127) / 128;
+    p.tiles_n = (N + 127) / 128;
+    const long tiles = (long)p.tiles_m * p.tiles_n * batch;
+    const int ktiles = (K + X3_BK - 1) / X3_BK;
+    int ks = 1;
+    if (ksplit_req > 0) ks = ksplit_req;
+    else if (ws != nullptr && !fused)   // one 96 KB block per CU: split until the grid covers 256 CUs
+      while (tiles * ks < 256 && ks * 2 <= ktiles / 2 && ks < 16) ks *= 2;
+    if (fused) ks = 1;
+    if (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks = 1;
+    p.ksplit = ks;
+    if (ks > 1) fm_gemm_join(stream);
+    const int lds = 6 * 128 * X3_BK * 2;
+    dim3 grid(p.tiles_m * p.tiles_n, batch, ks);
+    // per-operand 16-B load permission (bit 0: A, bit 1: B); k / m / n tails take element loads
+    const int vmask = ((al(A) && lda % 4 == 0 && sA % 4 == 0) ? 1 : 0) | ((al(B) && ldb % 4 == 0 && sB % 4 == 0) ? 2 : 0);
+#define FM_X3_GO(AKv, BKv)                                                                                     \
+    do {                                                                                                       \
+      static bool attr = false;                                                                                \
+      if (!attr) {                                                                                             \
+        (void)hipFuncSetAttribute((const void*)fm_gemm_x3_kernel<AKv, BKv>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                  lds);                                                                        \
+        attr = true;                                                                                           \
+      }                                                                                                        \
+      hipLaunchKernelGGL((fm_gemm_x3_kernel<AKv, BKv>), grid, dim3(512), lds, stream, p, vmask);               \
+    } while (0)
+    if (a_kcontig && b_kcontig) FM_X3_GO(true, true);
+    else if (a_kcontig) FM_X3_GO(true, false);
+    else if (b_kcontig) FM_X3_GO(false, true);
+    else FM_X3_GO(false, false);
+#undef FM_X3_GO
+    if (ks > 1) {
+      const int v4 = (N % 4 == 0) && (ldc % 4 == 0) && (sC % 4 == 0) && al(C);
+      const long total = (long)M * N * batch / (v4 ? 4 : 1);
+      launch_reduce_f32(p, v4, total, stream);
+    }
+    return ks;
+  }
   if (vec && variant >= 1000 && variant < 1200 && K > 0) {
     const XCfg c = kXCfgs[((variant - 1000) % 100) % kNumXCfgs];
     const bool atomic_ok = ((variant - 1000) / 100 == 1) && beta && bias == nullptr && act == ACT_NONE &&
