@@ -434,6 +434,12 @@ __global__ void fm_gemm_f32_reduce(GemmF p, int v4) {
 // itself, so the result has native-fp32 accuracy (tests/test_gpu_fp32.py checks it against float64
 // at the native kernel's tolerance).  Cost per k: 6 bf16 MFMA (16 cycles) vs 8 fp32 MFMA (32
 // cycles) for a 16x16x32 block: 2.7x the fp32 MFMA rate.
+// MEASURED (profiles/gemm_f32_split_vs_native_r4c.jsonl): accuracy at the native kernel's level
+// (tests/test_gpu_fp32_split.py), speed only at parity -- 1362 vs 1391 us over the DLRM shapes,
+// hipBLASLt fp32 1287 us, and the DLRM step 1.53 vs 1.45 ms (profiles/bench_ab_f32_split_r4c.txt).
+// Three planes per operand triple the LDS fragment reads per k (18 b128 reads per 48 MFMAs per
+// wave: ~96 B/clk/CU of the 128 B/clk LDS rate) and the 96 KB of planes leave one block per CU, so
+// the kernel is LDS- and latency-bound well before the 2.7x MFMA headroom.  OPT-IN.
 // Tile 128x128x64, 512 threads (8 waves, 64x32 per wave), six bf16 LDS planes (3 per operand,
 // gemm_common.h images: K-contiguous 128-B rows / MN-contiguous transposed reads) = 96 KB, one
 // block per CU; the next k-tile's fp32 operands are loaded into registers during this tile's MFMAs.
