@@ -266,6 +266,53 @@ __global__ void fm_gemm_splitk_reduce(GemmP p) {
   }
 }
 
+// split-K reduce with the FUSED BACKWARD epilogue (bf16 act_y): v = act_bwd(bact, ay, act(alpha*sum +
+// bias)), colsum[n] += column sums of v.  Thread = 4 columns x RB rows (one atomic per column and
+// block); lets small-batch dX GEMMs split K (summit_large 256 x 4096 x 4096).
+__global__ void __launch_bounds__(256) fm_gemm_splitk_reduce_bwd(GemmP p, int RB) {
+  const int n = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (n >= p.N) return;
+  const int m0 = blockIdx.y * RB, m1 = min(p.M, m0 + RB);
+  const long MN = (long)p.M * p.N;
+  const bool v4 = n + 3 < p.N && (p.N & 3) == 0;
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int m = m0; m < m1; ++m) {
+    const float* src = p.ws + (long)m * p.N + n;
+    float sv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (v4) {
+      f32x4_t a = *reinterpret_cast<const f32x4_t*>(src);
+      for (int k = 1; k < p.ksplit; ++k) a += *reinterpret_cast<const f32x4_t*>(src + k * MN);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sv[r] = a[r];
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (n + r < p.N)
+          for (int k = 0; k < p.ksplit; ++k) sv[r] += src[k * MN + r];
+    }
+    const long ci = (long)m * p.ldc + n;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (n + r >= p.N) break;
+      float v = act_fwd(p.act, sv[r] * p.alpha + (p.bias ? p.bias[n + r] : 0.f));
+      if (p.ay) v = act_bwd(p.bact, bf2f(p.ay[(long)m * p.lday + n + r]), v);
+      cs[r] += v;                               // as the in-tile epilogue: the unrounded value
+      if (p.c_fp32) {
+        float* d = reinterpret_cast<float*>(p.C) + ci + r;
+        *d = v + (p.beta ? *d : 0.f);
+      } else {
+        unsigned short* d = reinterpret_cast<unsigned short*>(p.C) + ci + r;
+        *d = f2bf(v + (p.beta ? bf2f(*d) : 0.f));
+      }
+    }
+  }
+  if (p.colsum) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (n + r < p.N) atomicAdd(p.colsum + n + r, cs[r]);
+  }
+}
+
 static int g_gemm_variant_early();
 
 template <int BM, int BN, bool AK, bool BKC, bool VEC>
@@ -426,9 +473,13 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
   // few 128x128 tiles and a short K (small-batch layers, e.g. DLRM run_random at 256 samples
   // per GPU): 64x64 tiles give 4x the blocks without split-K slabs (measured +26 % step rate)
   if (t128 < 128 && K <= 2048 && !(g_gemm_variant & 16)) { BMv = 64; BNv = 64; }
-  // a fused backward epilogue cannot split K: small grids take 64x64 tiles for 4x the blocks
-  // (summit_large dX, 256 x 4096 x 4096: 64 -> 256 blocks)
-  if ((act_y != nullptr || colsum != nullptr) && t128 < 256 && !(g_gemm_variant & 16)) { BMv = 64; BNv = 64; }
+  // a fused backward epilogue in the tile cannot split K: small grids with a long K split it and run
+  // the epilogue in the reduce (fm_gemm_splitk_reduce_bwd), short ones take 64x64 tiles for 4x the
+  // blocks (summit_large dX, 256 x 4096 x 4096)
+  const bool fused_ep = act_y != nullptr || colsum != nullptr;
+  const bool fused_split = fused_ep && t128 < 256 && K >= 1024 && ws != nullptr && batch == 1 && ksplit_req <= 0 &&
+                           (long)M * N * 4 * 2 <= ws_bytes;
+  if (fused_ep && t128 < 256 && !fused_split && !(g_gemm_variant & 16)) { BMv = 64; BNv = 64; }
   if (g_gemm_variant & 32) { BMv = 64; BNv = 64; }
   p.tiles_m = (M + BMv - 1) / BMv;
   p.tiles_n = (N + BNv - 1) / BNv;
@@ -446,10 +497,9 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
     static const int ks_max = getenv("FM_GEMM_KSPLIT_MAX") ? std::max(1, atoi(getenv("FM_GEMM_KSPLIT_MAX"))) : 16;
     while (tiles * ks < target && ks * 2 <= ktiles / 2 && ks < ks_max) ks *= 2;
   }
-  if (act_y != nullptr || colsum != nullptr) ks = 1;  // fused bwd epilogue needs the full K sum
+  if (fused_ep && !fused_split) ks = 1;  // fused bwd epilogue in the tile needs the full K sum
   if (ks > 1 && !atomic_ok) {
-    long need = (long)batch * ks * M * (long)N * 4;
-    if (ws == nullptr || need > ws_bytes) ks = 1;
+    while (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks /= 2;
   }
   p.ksplit = ks;
   if (K <= 0) {  // degenerate: C = epilogue(0)
@@ -457,11 +507,17 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
   }
   p.atomic_c = p.ksplit > 1 && atomic_ok;
   if (p.ksplit > 1) fm_gemm_join(stream);
-  if (p.ksplit > 1 && !p.atomic_c) p.tile_cnt = split_counters(stream, tiles, (long)M * N * 4);
+  const bool reduce_bwd = p.ksplit > 1 && fused_ep;
+  if (p.ksplit > 1 && !p.atomic_c && !reduce_bwd) p.tile_cnt = split_counters(stream, tiles, (long)M * N * 4);
   if (BNv == 128) launch_bm<128, 128>(p, a_kcontig, b_kcontig, vec, stream);
   else if (BMv == 128) launch_bm<128, 64>(p, a_kcontig, b_kcontig, vec, stream);
   else launch_bm<64, 64>(p, a_kcontig, b_kcontig, vec, stream);
-  if (p.ksplit > 1 && !p.atomic_c && p.tile_cnt == nullptr) {
+  if (reduce_bwd) {
+    const int bx = (N + 1023) / 1024;
+    const int by = std::max(1, std::min(M, 1024 / bx));
+    const int RB = (M + by - 1) / by;
+    hipLaunchKernelGGL(fm_gemm_splitk_reduce_bwd, dim3(bx, (M + RB - 1) / RB), dim3(256), 0, stream, p, RB);
+  } else if (p.ksplit > 1 && !p.atomic_c && p.tile_cnt == nullptr) {
     launch_splitk_reduce(p, stream);
   }
   return p.ksplit;

@@ -689,6 +689,49 @@ __global__ void __launch_bounds__(512, 1) fm_gemm_x3_kernel(GemmF p, int vec) {
   }
 }
 
+// split-K reduce of a GEMM with the FUSED BACKWARD epilogue (dX of a layer whose input has an
+// activation): v = act_bwd(bact, ay, act(alpha * sum + bias)), colsum[n] += sum over rows of v.
+// Thread = 4 columns x RB rows: the column sums stay in registers, one atomic per (column, block),
+// so small-batch dX GEMMs (summit_large: 256 x 4096 x 4096) can split K instead of running 64
+// blocks of 128x128 tiles or 64x64 tiles at ~60 % of the big-tile rate.
+__global__ void __launch_bounds__(256) fm_gemm_f32_reduce_bwd(GemmF p, int RB) {
+  const int n = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (n >= p.N) return;
+  const int m0 = blockIdx.y * RB, m1 = min(p.M, m0 + RB);
+  const long MN = (long)p.M * p.N;
+  const bool v4 = n + 3 < p.N && (p.N & 3) == 0;
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int m = m0; m < m1; ++m) {
+    const float* src = p.ws + (long)m * p.N + n;
+    float sv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (v4) {
+      f32x4_t a = *reinterpret_cast<const f32x4_t*>(src);
+      for (int k = 1; k < p.ksplit; ++k) a += *reinterpret_cast<const f32x4_t*>(src + k * MN);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sv[r] = a[r];
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (n + r < p.N)
+          for (int k = 0; k < p.ksplit; ++k) sv[r] += src[k * MN + r];
+    }
+    float* d = p.C + (long)m * p.ldc + n;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (n + r >= p.N) break;
+      float v = act_fwd(p.act, sv[r] * p.alpha + (p.bias ? p.bias[n + r] : 0.f));
+      if (p.ay) v = act_bwd(p.bact, p.ay[(long)m * p.lday + n + r], v);
+      cs[r] += v;
+      d[r] = v + (p.beta ? d[r] : 0.f);
+    }
+  }
+  if (p.colsum) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (n + r < p.N) atomicAdd(p.colsum + n + r, cs[r]);
+  }
+}
+
 }  // namespace
 
 // split-K reduce off the critical path (gemm_async.hip)
@@ -1415,7 +1458,12 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
   // a fused backward epilogue (act-bwd of the layer below / bias-grad column sums) cannot split K:
   // small grids take 64x64 tiles for 4x the blocks (summit_large dX, 256 x 4096 x 4096: 64 -> 256
   // blocks on 256 CUs)
-  if ((act_y != nullptr || colsum != nullptr) && t128 < 256) { BMv = 64; BNv = 64; }
+  // ... unless K is long enough to split it: then 128x128 tiles split K and the fused epilogue runs in
+  // the reduce (fm_gemm_f32_reduce_bwd)
+  const bool fused_ep = act_y != nullptr || colsum != nullptr;
+  const bool fused_split = fused_ep && t128 < 256 && K >= 1024 && ws != nullptr && batch == 1 && ksplit_req <= 0 &&
+                           (long)M * N * 4 * 2 <= ws_bytes;
+  if (fused_ep && t128 < 256 && !fused_split) { BMv = 64; BNv = 64; }
   // variant bit 4096 (A/B): 256x128 tiles, one 4-wave block per CU, when they fill >= 3/4 of the chip
   if ((variant & 4096) && vec && (long)((M + 255) / 256) * ((N + 127) / 128) * batch >= 192) { BMv = 256; BNv = 128; }
   p.tiles_m = (M + BMv - 1) / BMv;
@@ -1429,8 +1477,8 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
     const long target = env_target > 0 ? env_target : 512L;   // 2 resident blocks per CU
     while (tiles * ks < target && ks * 2 <= ktiles / 4 && ks < 16) ks *= 2;
   }
-  if (act_y != nullptr || colsum != nullptr) ks = 1;   // fused bwd epilogue needs the full K sum
-  if (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks = 1;
+  if (fused_ep && !fused_split) ks = 1;   // fused bwd epilogue in the tile: needs the full K sum
+  while (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks /= 2;
   if (K <= 0) ks = 1;
   p.ksplit = ks;
   if (ks > 1) fm_gemm_join(stream);
@@ -1439,7 +1487,12 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
   else if (BNv == 128) launch_fbm<128, 128>(p, a_kcontig, b_kcontig, vec, stream, opt);
   else if (BMv == 128) launch_fbm<128, 64>(p, a_kcontig, b_kcontig, vec, stream, opt);
   else launch_fbm<64, 64>(p, a_kcontig, b_kcontig, vec, stream, 0);
-  if (ks > 1) {
+  if (ks > 1 && fused_ep) {
+    const int bx = (N + 1023) / 1024;
+    const int by = std::max(1, std::min(M, 1024 / bx));
+    const int RB = (M + by - 1) / by;
+    hipLaunchKernelGGL(fm_gemm_f32_reduce_bwd, dim3(bx, (M + RB - 1) / RB), dim3(256), 0, stream, p, RB);
+  } else if (ks > 1) {
     const int v4 = (N % 4 == 0) && (ldc % 4 == 0) && (sC % 4 == 0) && al(C);
     const long total = (long)M * N * batch / (v4 ? 4 : 1);
     launch_reduce_f32(p, v4, total, stream);

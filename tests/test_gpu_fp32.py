@@ -478,3 +478,25 @@ def test_dlrm_hdf5_dataset_fp32_gpu_matches_cpu(gpu, tmp_path):
         ws[0] = ws[0][:, :13]
         res[dev] = ws
     _assert_params_close(res["cpu"], res["gpu"], 1e-4)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_fused_backward_epilogue_split_k_small_batch(gpu, dtype):
+    """Small-batch dX GEMM with the fused backward epilogue (summit_large: 256 x 4096 x 4096): the
+    grid is small, so K is split and the act-bwd + bias-gradient column sums run in the split-K
+    reduce (fm_gemm_f32_reduce_bwd / fm_gemm_splitk_reduce_bwd) -- same results as the oracle."""
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(9)
+    dt = torch.float32 if dtype == "fp32" else torch.bfloat16
+    tol = TOL if dtype == "fp32" else 2e-2
+    M, K, N = 256, 2048, 4096          # dpre [M, N] . W [N, K] -> dX [M, K]
+    dpre = torch.randn(M, N, device=gpu).to(dt)
+    W = (torch.randn(N, K, device=gpu) * 0.05).to(dt)
+    yb = torch.randn(M, K, device=gpu).relu().to(dt)
+    dx = torch.empty(M, K, device=gpu, dtype=dt)
+    colsum = torch.zeros(K, device=gpu)
+    ks = Kk.gemm(dpre, N, True, W, K, False, dx, K, M, K, N, act_y=yb, bwd_act=11, colsum=colsum)
+    assert ks > 1
+    ref = (dpre.double() @ W.double()) * (yb.double() > 0)
+    assert rel_err(dx, ref) < tol
+    assert rel_err(colsum, ref.sum(0)) < tol
