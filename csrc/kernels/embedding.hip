@@ -76,7 +76,22 @@ __global__ void __launch_bounds__(256) fm_emb_fwd_multi(TabSet s, long B) {
     for (int c4 = lc; c4 < D4; c4 += lpr) {
       const int c = c4 * 4;
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-      for (int j = 0; j < d.bag; ++j) {
+      int j = 0;
+      // long bags (summit_large: 100 lookups per sample, 256 samples): 8 index loads, then 8 row
+      // loads in flight per lane instead of one dependent index -> row round trip per lookup
+      for (; j + 8 <= d.bag; j += 8) {
+        long r[8];
+        bool ok[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) r[u] = local_row(ldi<I64>(d.idx, b * d.bag + j + u), d.lo, d.rows, ok[u]);
+        f32x4_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const f32x4_t*>(d.W + r[u] * d.D + c);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (ok[u]) acc += v[u];
+      }
+      for (; j < d.bag; ++j) {
         bool ok;
         const long r = local_row(ldi<I64>(d.idx, b * d.bag + j), d.lo, d.rows, ok);
         const f32x4_t v = *reinterpret_cast<const f32x4_t*>(d.W + r * d.D + c);
