@@ -430,7 +430,10 @@ __global__ void __launch_bounds__(256) fm_nhwc_stage(const unsigned short* __res
                                                      unsigned short* __restrict__ dst, int act,
                                                      int C, int H, int W, int Cp, int Hp, int Wp, int top, int left, int dh,
                                                      int dw) {
-  __shared__ __attribute__((aligned(16))) unsigned short tile[64][72];   // [channel][column], 144-B rows
+  // [channel][column] with 132-B rows (33 dwords): the store phase's lanes read 8 rows x 8 columns at
+  // stride 8 rows = 264 dwords = 8 banks apart -> conflict-free (a 144-B pitch put every other
+  // lane group on the same bank: 6.7 conflicts per LDS instruction, profiles/pmc_conv_nhwc_r4g.txt)
+  __shared__ __attribute__((aligned(16))) unsigned short tile[64][66];
   const int j0 = blockIdx.y * 64, c0 = blockIdx.z * 64;
   const int ni = blockIdx.x;
   const int n = ni / Hp, i = ni - n * Hp;
@@ -483,7 +486,9 @@ __global__ void __launch_bounds__(256) fm_nhwc_stage(const unsigned short* __res
             for (int u = 0; u < 4; ++u) v[u] = (unsigned)e8[2 * u] | ((unsigned)e8[2 * u + 1] << 16);
           }
         }
-        *reinterpret_cast<u32x4_t*>(&tile[cc][8 * ch]) = v;
+        unsigned* tw = reinterpret_cast<unsigned*>(&tile[cc][8 * ch]);   // 4-B aligned (132-B rows)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) tw[u] = v[u];
       }
     } else {
       for (int e = threadIdx.x; e < 64 * 64; e += 256) {
@@ -528,7 +533,7 @@ __global__ void __launch_bounds__(256) fm_nhwc_stage_flat(const unsigned short* 
                                                           unsigned short* __restrict__ dst, int act, int C, int H, int W,
                                                           int Cp, int Hp, int Wp, int top, int left, int dh, int dw,
                                                           int blocks_per_img) {
-  __shared__ __attribute__((aligned(16))) unsigned short tile[64][72];
+  __shared__ __attribute__((aligned(16))) unsigned short tile[64][66];   // 132-B rows: conflict-free reads
   __shared__ int soff[64];
   const int n = blockIdx.x / blocks_per_img;
   const int pix0 = (blockIdx.x - n * blocks_per_img) * 64;
