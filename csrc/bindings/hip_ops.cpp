@@ -8,12 +8,20 @@
 #include <vector>
 
 extern "C" {
+void fm_sgd_update_segs(float* W, float* G, float* V, unsigned short* Wc, const float* lr, const long* off,
+                        const long* len, int nseg, float wd, float mom, int nesterov, int zero_g, hipStream_t s);
 void fm_image_normalize(const unsigned char* src, void* dst, long N, int H, int W, const float* mean, const float* stdv,
                         int bf16, hipStream_t s);
 void fm_gemm_set_variant(int v);
 void fm_gemm_f32_set_variant(int v);
 void fm_gemm_async_arm(int on);
 void fm_gemm_join(hipStream_t s);
+int fm_gemm_dw_sgd(const void* A, long lda, const void* B, long ldb, float* W, long ldw, unsigned short* Wc, float* V,
+                   const float* lr, float wd, float mom, int nesterov, int M, int N, int K, float* ws, long ws_bytes,
+                   float* rowsum_a, hipStream_t stream);
+int fm_gemm_f32_dw_sgd(const float* A, long lda, const float* B, long ldb, float* W, long ldw, unsigned short* Wc,
+                       float* V, const float* lr, float wd, float mom, int nesterov, int M, int N, int K, float* ws,
+                       long ws_bytes, float* rowsum_a, hipStream_t stream);
 int fm_gemm(const void* A, long lda, long sA, int a_kcontig, const void* B, long ldb, long sB, int b_kcontig, void* C,
             long ldc, long sC, int c_fp32, const float* bias, int M, int N, int K, int batch, float alpha, int beta,
             int act, float* ws, long ws_bytes, int ksplit_req, const void* act_y, long lday, int bwd_act,
@@ -218,6 +226,60 @@ int gemm(torch::Tensor A, int64_t lda, int64_t sA, bool a_kcontig, torch::Tensor
 }
 
 void gemm_join() { fm_gemm_join(cur()); }
+
+// fm_sgd over disjoint [off, off + len) ranges of one flat master / grad / state / mirror set
+void sgd_segs(torch::Tensor W, torch::Tensor G, c10::optional<torch::Tensor> V, c10::optional<torch::Tensor> Wc,
+              torch::Tensor lr, std::vector<int64_t> off, std::vector<int64_t> len, double wd, double mom, bool nesterov,
+              bool zero_g) {
+  TORCH_CHECK(off.size() == len.size(), "sgd_segs: off/len");
+  TORCH_CHECK(W.is_cuda() && W.scalar_type() == torch::kFloat32 && W.is_contiguous() && G.scalar_type() == torch::kFloat32 &&
+                  G.is_contiguous() && G.numel() == W.numel(), "sgd_segs: fp32 W / G");
+  TORCH_CHECK(mom <= 0.0 || (V.has_value() && V->defined() && V->numel() == W.numel()), "sgd_segs: momentum buffer");
+  if (Wc.has_value() && Wc->defined())
+    TORCH_CHECK(Wc->scalar_type() == torch::kBFloat16 && Wc->numel() == W.numel(), "sgd_segs: bf16 mirror");
+  for (size_t i = 0; i < off.size(); ++i)
+    TORCH_CHECK(off[i] >= 0 && len[i] >= 0 && off[i] + len[i] <= W.numel(), "sgd_segs: range outside the buffer");
+  std::vector<long> o(off.begin(), off.end()), l(len.begin(), len.end());
+  fm_sgd_update_segs(W.data_ptr<float>(), G.data_ptr<float>(), (float*)mptr(V), (unsigned short*)mptr(Wc),
+                     lr.data_ptr<float>(), o.data(), l.data(), (int)o.size(), (float)wd, (float)mom, nesterov ? 1 : 0,
+                     zero_g ? 1 : 0, cur());
+}
+
+// dW = dpre^T x with the SGD update fused into the epilogue (gemm.hip fm_gemm_dw_sgd): W [N_out, K_in]
+// fp32 master, optional bf16 mirror Wc and momentum V of the same shape; db (optional) += column sums
+// of dpre.  Returns the split-K factor, or -1 when the fused form does not apply (the caller then
+// computes the gradient and runs the optimizer kernel itself).
+int gemm_dw_sgd(torch::Tensor dpre, torch::Tensor x, torch::Tensor W, c10::optional<torch::Tensor> Wc,
+                c10::optional<torch::Tensor> V, torch::Tensor lr, double wd, double mom, bool nesterov,
+                c10::optional<torch::Tensor> db, torch::Tensor ws) {
+  check_cuda(dpre, "dpre");
+  check_cuda(x, "x");
+  check_cuda(W, "W");
+  const bool f32 = dpre.scalar_type() == torch::kFloat32;
+  const int64_t B = dpre.size(0), Nout = dpre.size(1), Kin = x.size(1);
+  TORCH_CHECK(x.scalar_type() == dpre.scalar_type() && (f32 || dpre.scalar_type() == torch::kBFloat16) && x.size(0) == B &&
+                  dpre.stride(1) == 1 && x.stride(1) == 1,
+              "gemm_dw_sgd: dpre [B, out], x [B, in] (both bf16 or both fp32), unit column stride");
+  TORCH_CHECK(W.scalar_type() == torch::kFloat32 && W.is_contiguous() && W.numel() == Nout * Kin, "gemm_dw_sgd: W [out, in] fp32");
+  if (Wc.has_value() && Wc->defined())
+    TORCH_CHECK(Wc->scalar_type() == torch::kBFloat16 && Wc->is_contiguous() && Wc->numel() == W.numel(), "gemm_dw_sgd: Wc");
+  if (V.has_value() && V->defined())
+    TORCH_CHECK(V->scalar_type() == torch::kFloat32 && V->is_contiguous() && V->numel() == W.numel(), "gemm_dw_sgd: V");
+  TORCH_CHECK(mom <= 0.0 || (V.has_value() && V->defined()), "gemm_dw_sgd: momentum needs V");
+  TORCH_CHECK(lr.scalar_type() == torch::kFloat32 && lr.numel() >= 1 && lr.is_cuda(), "gemm_dw_sgd: lr device fp32 scalar");
+  if (db.has_value() && db->defined())
+    TORCH_CHECK(db->scalar_type() == torch::kFloat32 && db->numel() >= Nout, "gemm_dw_sgd: db fp32 [out]");
+  TORCH_CHECK((B - 1) * dpre.stride(0) + Nout <= dpre.numel() && (B - 1) * x.stride(0) + Kin <= x.numel(), "gemm_dw_sgd: extents");
+  if (f32)
+    return fm_gemm_f32_dw_sgd(dpre.data_ptr<float>(), dpre.stride(0), x.data_ptr<float>(), x.stride(0), W.data_ptr<float>(),
+                              Kin, (unsigned short*)mptr(Wc), (float*)mptr(V), lr.data_ptr<float>(), (float)wd,
+                              (float)mom, nesterov ? 1 : 0, (int)Nout, (int)Kin, (int)B, ws.data_ptr<float>(),
+                              ws.numel() * 4, (float*)mptr(db), cur());
+  return fm_gemm_dw_sgd(dpre.data_ptr(), dpre.stride(0), x.data_ptr(), x.stride(0), W.data_ptr<float>(), Kin,
+                        (unsigned short*)mptr(Wc), (float*)mptr(V), lr.data_ptr<float>(), (float)wd, (float)mom,
+                        nesterov ? 1 : 0, (int)Nout, (int)Kin, (int)B, ws.data_ptr<float>(), ws.numel() * 4,
+                        (float*)mptr(db), cur());
+}
 
 void skinny_fwd(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor y, int64_t act) {
   TORCH_CHECK(w.numel() == x.size(1) && y.size(1) == 1 && x.stride(1) == 1, "skinny_fwd: x[B,K] w[1,K] y[B,1]");
@@ -1021,6 +1083,8 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "flexmi HIP/CDNA4 kernels (gfx950)";
   m.def("gemm", &gemm);
   m.def("gemm_join", &gemm_join);
+  m.def("gemm_dw_sgd", &gemm_dw_sgd);
+  m.def("sgd_segs", &sgd_segs);
   m.def("gemm_set_variant", [](int v) { fm_gemm_set_variant(v); });
   m.def("gemm_f32_set_variant", [](int v) { fm_gemm_f32_set_variant(v); });
   m.def("init_fill", &init_fill);

@@ -70,9 +70,12 @@ bool avx2() { return flexmi::cpu::has_avx2(); }
 
 }  // namespace
 
+void register_init_metrics(pybind11::module& m);  // init_metrics.cc
+
 PYBIND11_MODULE(_cpu, m) {
-  m.doc() = "flexmi native CPU kernels (embedding bag forward / backward / fused sparse SGD)";
+  m.doc() = "flexmi native CPU kernels (embedding bag forward / backward / fused sparse SGD, counter-based init, loss + metrics)";
   m.def("embedding_fwd", &embedding_fwd, "out = scale * bag-sum of table rows");
   m.def("embedding_bwd", &embedding_bwd, "table rows += alpha * dy (dense grad or fused SGD)");
   m.def("avx2", &avx2);
+  register_init_metrics(m);
 }

@@ -216,6 +216,10 @@ __global__ void fm_gemm_splitk_reduce4(GemmP p) {
     f32x4_t s = *reinterpret_cast<const f32x4_t*>(src);
     for (int k = 1; k < p.ksplit; ++k) s += *reinterpret_cast<const f32x4_t*>(src + k * MN);
     s *= p.alpha;
+    if (p.uw) {
+      sgd_apply4(p, (long)m * p.ldc + n, s);
+      continue;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) s[r] = act_fwd(p.act, s[r] + (p.bias ? p.bias[n + r] : 0.f));
     f32x4_t* d = reinterpret_cast<f32x4_t*>(reinterpret_cast<float*>(p.C) + zb * p.sC + (long)m * p.ldc + n);
@@ -253,6 +257,10 @@ __global__ void fm_gemm_splitk_reduce(GemmP p) {
     float s = 0.f;
     for (int k = 0; k < p.ksplit; ++k) s += src[k * MN];
     float v = s * p.alpha;
+    if (p.uw) {
+      sgd_apply1(p, (long)m * p.ldc + n, v);
+      continue;
+    }
     if (p.bias) v += p.bias[n];
     v = act_fwd(p.act, v);
     long ci = zb * p.sC + (long)m * p.ldc + n;
@@ -392,6 +400,18 @@ extern "C" void fm_gemm_set_variant(int v) { g_gemm_variant = v; }
 
 // A_kcontig: A stored [M][K] (lda >= K) else [K][M] (lda >= M)
 // B_kcontig: B stored [N][K] (ldb >= K) else [K][N] (ldb >= N)
+struct SgdUpd {
+  float* w; unsigned short* wc; float* v; const float* lr; float wd, mom; int nest;
+};
+
+static int gemm_run(const void* A, long lda, long sA, int a_kcontig,
+                    const void* B, long ldb, long sB, int b_kcontig,
+                    void* C, long ldc, long sC, int c_fp32,
+                    const float* bias, int M, int N, int K, int batch,
+                    float alpha, int beta, int act, float* ws, long ws_bytes, int ksplit_req,
+                    const void* act_y, long lday, int bwd_act, float* colsum, float* rowsum_a,
+                    const SgdUpd* upd, hipStream_t stream);
+
 extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
                        const void* B, long ldb, long sB, int b_kcontig,
                        void* C, long ldc, long sC, int c_fp32,
@@ -399,7 +419,33 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
                        float alpha, int beta, int act, float* ws, long ws_bytes, int ksplit_req,
                        const void* act_y, long lday, int bwd_act, float* colsum, float* rowsum_a,
                        hipStream_t stream) {
+  return gemm_run(A, lda, sA, a_kcontig, B, ldb, sB, b_kcontig, C, ldc, sC, c_fp32, bias, M, N, K, batch, alpha, beta,
+                  act, ws, ws_bytes, ksplit_req, act_y, lday, bwd_act, colsum, rowsum_a, nullptr, stream);
+}
+
+// Weight-gradient GEMM with the SGD update fused into its epilogue (or its split-K reduce):
+// W[M][ldw] -= lr * (A^T B + wd W) (momentum / Nesterov as fm_sgd_update), bf16 mirror Wc
+// rewritten; the gradient itself is never stored.  A = dpre [K][M], B = x [K][N] (MN-contiguous,
+// the dW orientation), rowsum_a += column sums of dpre (the bias gradient).  Returns the split.
+extern "C" int fm_gemm_dw_sgd(const void* A, long lda, const void* B, long ldb, float* W, long ldw,
+                              unsigned short* Wc, float* V, const float* lr, float wd, float mom, int nesterov,
+                              int M, int N, int K, float* ws, long ws_bytes, float* rowsum_a, hipStream_t stream) {
+  SgdUpd u{W, Wc, V, lr, wd, mom, nesterov};
+  return gemm_run(A, lda, 0, 0, B, ldb, 0, 0, W, ldw, 0, 1, nullptr, M, N, K, 1, 1.f, 0, 10, ws, ws_bytes, 0, nullptr,
+                  0, 10, nullptr, rowsum_a, &u, stream);
+}
+
+static int gemm_run(const void* A, long lda, long sA, int a_kcontig,
+                    const void* B, long ldb, long sB, int b_kcontig,
+                    void* C, long ldc, long sC, int c_fp32,
+                    const float* bias, int M, int N, int K, int batch,
+                    float alpha, int beta, int act, float* ws, long ws_bytes, int ksplit_req,
+                    const void* act_y, long lday, int bwd_act, float* colsum, float* rowsum_a,
+                    const SgdUpd* upd, hipStream_t stream) {
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
+  if (upd && (K <= 0 || ldc % 4 != 0 || (((uintptr_t)upd->w | (uintptr_t)(upd->v ? upd->v : upd->w)) & 15) ||
+              (((uintptr_t)(upd->wc ? (void*)upd->wc : (void*)upd->w)) & 7)))
+    return -1;                         // the caller computes the gradient and runs the update itself
   if (beta) fm_gemm_join(stream);      // C may be a gradient an async reduce is still writing
   GemmP p;
   p.A = (const unsigned short*)A; p.lda = lda; p.sA = sA;
@@ -411,6 +457,13 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
   p.n_fast = M >= N;
   p.atomic_c = 0;
   p.tile_cnt = nullptr;
+  p.uw = upd ? upd->w : nullptr;
+  p.uwc = upd ? upd->wc : nullptr;
+  p.uv = upd ? upd->v : nullptr;
+  p.ulr = upd ? upd->lr : nullptr;
+  p.uwd = upd ? upd->wd : 0.f;
+  p.umom = upd ? upd->mom : 0.f;
+  p.unest = upd ? upd->nest : 0;
   // opt-in (FM_GEMM_ATOMIC_SPLIT=1): split-K partial tiles added straight into a small fp32
   // accumulating C with float atomics, no slabs and no reduce launch.  Measured SLOWER on the
   // DLRM dW GEMMs (profiles/README.md): the 16x16 accumulator layout issues 4-B atomics over 16
@@ -418,7 +471,7 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
   static const long atomic_max = getenv("FM_GEMM_ATOMIC_SPLIT") ? (getenv("FM_GEMM_ATOMIC_MAX") ? atol(getenv("FM_GEMM_ATOMIC_MAX"))
                                                                                                 : (256L << 10))
                                                                  : 0L;
-  const bool atomic_ok = c_fp32 && beta && bias == nullptr && act == 10 && act_y == nullptr && colsum == nullptr &&
+  const bool atomic_ok = !upd && c_fp32 && beta && bias == nullptr && act == 10 && act_y == nullptr && colsum == nullptr &&
                          (long)M * N <= atomic_max;
   // vector (16-B) loads need the contiguous extent and leading dims to be multiples of 8
   auto al = [](const void* q) { return (((uintptr_t)q) & 15) == 0; };
@@ -435,7 +488,7 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
   // 512 blocks of 128x128 beat one wave of 256x128 glds blocks: 11.07 vs 10.86 M samples/s,
   // profiles/README.md -- so glds starts at two waves of its tiles)
   const long t256 = (long)((M + 255) / 256) * ((N + 127) / 128) * batch;
-  if (vec && !no_glds && K > 0 && K % BK == 0 && M >= 8 && N >= 8 &&
+  if (vec && !no_glds && !upd && K > 0 && K % BK == 0 && M >= 8 && N >= 8 &&
       ((a_kcontig && b_kcontig && t256 >= 512) || glds_any)) {
     const int bm = ((g_gemm_variant & 4) || t256 < 256) ? 128 : 256;
     p.tiles_m = (M + bm - 1) / bm;

@@ -79,7 +79,54 @@ struct GemmP {
   int n_fast;   // tile order: column tiles fastest (A row-block reused by consecutive tiles on one XCD)
   int atomic_c; // split-K into an accumulating fp32 C: every split adds its tile with float atomics
   int* tile_cnt; // in-launch split-K combine: per-tile arrival counters (nullptr = separate reduce launch)
+  // fused SGD (dW GEMMs whose gradient has no other consumer): instead of storing the gradient,
+  // the epilogue updates the fp32 master W (same [M][ldc] layout as C), its momentum and bf16 mirror
+  // exactly as fm_sgd_kernel would (optim.hip) -- the gradient never round-trips through HBM
+  float* uw;             // nullptr = plain GEMM
+  unsigned short* uwc;   // bf16 compute mirror (nullptr: none)
+  float* uv;             // momentum buffer (used when umom > 0)
+  const float* ulr;      // device-side learning rate
+  float uwd, umom;
+  int unest;
 };
+
+// W -= lr * (g + wd W) (momentum / Nesterov as fm_sgd_kernel), one element at offset o of W
+// (P = GemmP or gemm_f32.hip's GemmF: the same uw / uwc / uv / ulr / uwd / umom / unest fields)
+template <class P>
+FM_DEVICE void sgd_apply1(const P& p, long o, float g) {
+  const float lr = p.ulr[0];
+  float w = p.uw[o];
+  g += p.uwd * w;
+  if (p.umom > 0.f) {
+    const float v = p.uv[o] * p.umom + g;
+    p.uv[o] = v;
+    g = p.unest ? g + p.umom * v : v;
+  }
+  w -= lr * g;
+  p.uw[o] = w;
+  if (p.uwc) p.uwc[o] = f2bf(w);
+}
+
+// four consecutive elements at a 16-B aligned offset o
+template <class P>
+FM_DEVICE void sgd_apply4(const P& p, long o, f32x4_t g) {
+  const float lr = p.ulr[0];
+  f32x4_t w = *reinterpret_cast<const f32x4_t*>(p.uw + o);
+  g += p.uwd * w;
+  if (p.umom > 0.f) {
+    const f32x4_t v = *reinterpret_cast<const f32x4_t*>(p.uv + o) * p.umom + g;
+    *reinterpret_cast<f32x4_t*>(p.uv + o) = v;
+    g = p.unest ? g + p.umom * v : v;
+  }
+  w -= lr * g;
+  *reinterpret_cast<f32x4_t*>(p.uw + o) = w;
+  if (p.uwc) {
+    bf16x4_t c;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) c[r] = (short)f2bf(w[r]);
+    *reinterpret_cast<bf16x4_t*>(p.uwc + o) = c;
+  }
+}
 
 // tile coordinates of remapped block id: consecutive ids share an XCD (xcd_remap), so the
 // operand traversed slowest stays resident in that XCD's 4 MB L2 while the other streams
@@ -256,6 +303,17 @@ FM_DEVICE void gemm_epilogue_store(const GemmP& p, const f32x4_t (&acc)[MR][NR],
         for (int r = 0; r < 4; ++r) csum[j][r] += (n + r < p.N) ? v[r] : 0.f;
       }
       if (!mok) continue;
+      if (p.uw) {   // fused SGD: the host guarantees ldc % 4 == 0 and 16-B aligned W / V / C
+        const long o = (long)m * p.ldc + n;
+        if (full) {
+          sgd_apply4(p, o, f32x4_t{v[0], v[1], v[2], v[3]});
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (n + r < p.N) sgd_apply1(p, o + r, v[r]);
+        }
+        continue;
+      }
       if (p.c_fp32) {
         float* dst = reinterpret_cast<float*>(p.C) + (long)zb * p.sC + (long)m * p.ldc + n;
         if (full && ((p.ldc & 3) == 0) && ((((uintptr_t)dst) & 15) == 0)) {

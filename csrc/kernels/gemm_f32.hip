@@ -47,6 +47,14 @@ struct GemmF {
   float alpha;
   int tiles_m, tiles_n, n_fast;
   int atomic;           // split-K partials float-atomically added into C (32x32 kernel, beta = 1)
+  // fused SGD (fm_gemm_f32_dw_sgd; default register-staged kernel and its reduce only): the
+  // epilogue updates W (same [M][ldc] layout as C) instead of storing the gradient
+  float* uw;
+  unsigned short* uwc;
+  float* uv;
+  const float* ulr;
+  float uwd, umom;
+  int unest;
 };
 
 template <int N>
@@ -231,6 +239,17 @@ FM_DEVICE void epilogue_f32(const GemmF& p, const f32x4_t (&acc)[MR][NR], int zb
         for (int e = 0; e < 4; ++e) csum[u][e] += (n0 + e < p.N) ? v[e] : 0.f;
       }
       if (!mok) continue;
+      if (p.uw) {
+        const long o = (long)m * p.ldc + n0;
+        if (full) {
+          sgd_apply4(p, o, f32x4_t{v[0], v[1], v[2], v[3]});
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (n0 + e < p.N) sgd_apply1(p, o + e, v[e]);
+        }
+        continue;
+      }
       float* dst = Cz + (long)m * p.ldc + n0;
       if (full && ((p.ldc & 3) == 0) && ((((uintptr_t)dst) & 15) == 0)) {
         f32x4_t o = {v[0], v[1], v[2], v[3]};
@@ -410,6 +429,10 @@ __global__ void fm_gemm_f32_reduce(GemmF p, int v4) {
     if (v4) {
       f32x4_t s = *reinterpret_cast<const f32x4_t*>(src);
       for (int k = 1; k < p.ksplit; ++k) s += *reinterpret_cast<const f32x4_t*>(src + k * MN);
+      if (p.uw) {
+        sgd_apply4(p, (long)m * p.ldc + n, s * p.alpha);
+        continue;
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) s[r] = act_fwd(p.act, s[r] * p.alpha + (p.bias ? p.bias[n + r] : 0.f));
       if (p.beta) s += *reinterpret_cast<const f32x4_t*>(d);
@@ -417,6 +440,10 @@ __global__ void fm_gemm_f32_reduce(GemmF p, int v4) {
     } else {
       float s = 0.f;
       for (int k = 0; k < p.ksplit; ++k) s += src[k * MN];
+      if (p.uw) {
+        sgd_apply1(p, (long)m * p.ldc + n, s * p.alpha);
+        continue;
+      }
       s = act_fwd(p.act, s * p.alpha + (p.bias ? p.bias[n] : 0.f));
       *d = s + (p.beta ? *d : 0.f);
     }
@@ -1323,11 +1350,43 @@ static int g_f32_split = -1;   // -1: from FM_F32_SPLIT at the first call
 extern "C" void fm_gemm_f32_set_split(int on) { g_f32_split = on ? 1 : 0; }
 extern "C" int fm_gemm_f32_get_split() { return g_f32_split == 1 ? 1 : 0; }
 
+struct SgdUpdF {
+  float* w; unsigned short* wc; float* v; const float* lr; float wd, mom; int nest;
+};
+
+static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const float* B, long ldb, long sB,
+                        int b_kcontig, float* C, long ldc, long sC, const float* bias, int M, int N, int K, int batch,
+                        float alpha, int beta, int act, float* ws, long ws_bytes, int ksplit_req, const float* act_y,
+                        long lday, int bwd_act, float* colsum, float* rowsum_a, const SgdUpdF* upd, hipStream_t stream);
+
 extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, const float* B, long ldb, long sB,
                            int b_kcontig, float* C, long ldc, long sC, const float* bias, int M, int N, int K, int batch,
                            float alpha, int beta, int act, float* ws, long ws_bytes, int ksplit_req, const float* act_y,
                            long lday, int bwd_act, float* colsum, float* rowsum_a, hipStream_t stream) {
+  return gemm_f32_run(A, lda, sA, a_kcontig, B, ldb, sB, b_kcontig, C, ldc, sC, bias, M, N, K, batch, alpha, beta, act, ws,
+                      ws_bytes, ksplit_req, act_y, lday, bwd_act, colsum, rowsum_a, nullptr, stream);
+}
+
+// fp32 weight-gradient GEMM with the SGD update fused in (same contract as gemm.hip fm_gemm_dw_sgd):
+// A = dpre [K][M], B = x [K][N], W [M][ldw] updated in place, the gradient never stored; -1 when
+// the fused form does not apply (the caller falls back to GEMM + optimizer kernel).  Always the
+// default register-staged kernel (the split-bf16 and A/B variants carry no update epilogue).
+extern "C" int fm_gemm_f32_dw_sgd(const float* A, long lda, const float* B, long ldb, float* W, long ldw,
+                                  unsigned short* Wc, float* V, const float* lr, float wd, float mom, int nesterov,
+                                  int M, int N, int K, float* ws, long ws_bytes, float* rowsum_a, hipStream_t stream) {
+  SgdUpdF u{W, Wc, V, lr, wd, mom, nesterov};
+  return gemm_f32_run(A, lda, 0, 0, B, ldb, 0, 0, W, ldw, 0, nullptr, M, N, K, 1, 1.f, 0, 10, ws, ws_bytes, 0, nullptr, 0,
+                      10, nullptr, rowsum_a, &u, stream);
+}
+
+static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const float* B, long ldb, long sB,
+                        int b_kcontig, float* C, long ldc, long sC, const float* bias, int M, int N, int K, int batch,
+                        float alpha, int beta, int act, float* ws, long ws_bytes, int ksplit_req, const float* act_y,
+                        long lday, int bwd_act, float* colsum, float* rowsum_a, const SgdUpdF* upd, hipStream_t stream) {
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
+  if (upd && (K <= 0 || ldc % 4 != 0 || (((uintptr_t)upd->w | (uintptr_t)(upd->v ? upd->v : upd->w)) & 15) ||
+              (((uintptr_t)(upd->wc ? (void*)upd->wc : (void*)upd->w)) & 7)))
+    return -1;
   if (beta) fm_gemm_join(stream);      // C may be a gradient an async reduce is still writing
   GemmF p;
   p.A = A; p.lda = lda; p.sA = sA;
@@ -1336,6 +1395,13 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
   p.bias = bias; p.ws = ws; p.ay = act_y; p.lday = lday; p.colsum = colsum; p.rowsum_a = rowsum_a;
   p.bact = bwd_act; p.M = M; p.N = N; p.K = K; p.act = act; p.beta = beta; p.batch = batch; p.alpha = alpha;
   p.n_fast = M >= N;
+  p.uw = upd ? upd->w : nullptr;
+  p.uwc = upd ? upd->wc : nullptr;
+  p.uv = upd ? upd->v : nullptr;
+  p.ulr = upd ? upd->lr : nullptr;
+  p.uwd = upd ? upd->wd : 0.f;
+  p.umom = upd ? upd->mom : 0.f;
+  p.unest = upd ? upd->nest : 0;
   auto al = [](const void* q) { return (((uintptr_t)q) & 15) == 0; };
   bool vec = al(A) && al(B) && (lda % 4 == 0) && (ldb % 4 == 0) && (sA % 4 == 0) && (sB % 4 == 0);
   vec = vec && (a_kcontig ? (K % 4 == 0) : (M % 4 == 0)) && (b_kcontig ? (K % 4 == 0) : (N % 4 == 0));
@@ -1343,12 +1409,12 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
   // 4-wave 256x128 form.  OPT-IN: measured on the DLRM fp32 step (profiles/prof_r2_fp32b_*) it
   // ties the register-staged kernel on the 1024-wide layers (150.8 vs 150.7 us) and loses on the
   // small-grid ones (one 96 KiB block per CU: 22 -> 39 us, 29 -> 45 us), 1.72 vs 1.68 ms/step.
-  const int variant = g_f32_variant;
+  const int variant = upd ? 0 : g_f32_variant;
   p.atomic = 0;
   // fp32 on the bf16 matrix cores (exact three-way operand split, fm_gemm_x3_kernel): FM_F32_SPLIT=1
   // or fm_gemm_f32_set_split(1)
   if (g_f32_split < 0) g_f32_split = (getenv("FM_F32_SPLIT") != nullptr && atoi(getenv("FM_F32_SPLIT")) == 1) ? 1 : 0;
-  if (g_f32_split == 1 && K >= 64 && M >= 64 && N >= 64) {
+  if (g_f32_split == 1 && !upd && K >= 64 && M >= 64 && N >= 64) {
     const bool fused = act_y != nullptr || colsum != nullptr;
     p.tiles_m = (M + 127) / 128;
     p.tiles_n = (N + 127) / 128;

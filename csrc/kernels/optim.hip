@@ -46,6 +46,37 @@ __global__ void fm_sgd_kernel(float* __restrict__ W, float* __restrict__ G, floa
   }
 }
 
+// The same update over up to 32 disjoint ranges of one flat buffer (blockIdx.y = range): the
+// parameters left to the optimizer launch when most weights were updated inside their dW GEMMs
+// (gemm.hip fm_gemm_dw_sgd) -- one launch instead of one per bias-sized gap.
+struct SgdSegs {
+  long off[32];
+  long len[32];
+};
+
+__global__ void fm_sgd_segs_kernel(float* __restrict__ W, float* __restrict__ G, float* __restrict__ V,
+                                   unsigned short* __restrict__ Wc, const float* __restrict__ lr_p, SgdSegs segs,
+                                   float wd, float mom, int nesterov, int zero_g) {
+  const float lr = lr_p[0];
+  const long o = segs.off[blockIdx.y], n = segs.len[blockIdx.y];
+  float* w = W + o;
+  float* g = G + o;
+  float* v = V ? V + o : nullptr;
+  unsigned short* wc = Wc ? Wc + o : nullptr;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float gi = g[i] + wd * w[i];
+    if (zero_g) g[i] = 0.f;
+    if (mom > 0.f) {
+      const float vi = v[i] * mom + gi;
+      v[i] = vi;
+      gi = nesterov ? gi + mom * vi : vi;
+    }
+    const float wi = w[i] - lr * gi;
+    w[i] = wi;
+    if (wc) wc[i] = f2bf(wi);
+  }
+}
+
 __global__ void fm_adam_kernel(float* __restrict__ W, float* __restrict__ G, float* __restrict__ M,
                                float* __restrict__ V, unsigned short* __restrict__ Wc, long n,
                                const float* __restrict__ alpha_t_p, float b1, float b2, float wd, float eps,
@@ -77,6 +108,24 @@ extern "C" void fm_sgd_update(float* W, float* G, float* V, unsigned short* Wc, 
   bool al = ((((uintptr_t)W) | ((uintptr_t)G) | ((uintptr_t)(V ? V : W))) & 15) == 0 && ((((uintptr_t)(Wc ? Wc : (unsigned short*)W)) & 7) == 0);
   hipLaunchKernelGGL(fm_sgd_kernel, dim3(fm_grid(al ? n / 4 + 1 : n)), dim3(256), 0, s, W, G, V, Wc, lr, n, wd, mom,
                      nesterov, al ? 1 : 0, zero_g);
+}
+
+extern "C" void fm_sgd_update_segs(float* W, float* G, float* V, unsigned short* Wc, const float* lr, const long* off,
+                                   const long* len, int nseg, float wd, float mom, int nesterov, int zero_g,
+                                   hipStream_t s) {
+  for (int b = 0; b < nseg; b += 32) {
+    SgdSegs sg;
+    long mx = 0;
+    const int k = nseg - b < 32 ? nseg - b : 32;
+    for (int i = 0; i < 32; ++i) {
+      sg.off[i] = i < k ? off[b + i] : 0;
+      sg.len[i] = i < k ? len[b + i] : 0;
+      mx = sg.len[i] > mx ? sg.len[i] : mx;
+    }
+    if (mx <= 0) continue;
+    const int gx = (int)((mx + 255) / 256 < 256 ? (mx + 255) / 256 : 256);
+    hipLaunchKernelGGL(fm_sgd_segs_kernel, dim3(gx, k), dim3(256), 0, s, W, G, V, Wc, lr, sg, wd, mom, nesterov, zero_g);
+  }
 }
 
 extern "C" void fm_adam_update(float* W, float* G, float* M, float* V, unsigned short* Wc, long n,

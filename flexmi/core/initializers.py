@@ -63,6 +63,21 @@ def counter_fill_cpu(kind, seed, a, b, shape, box):
     return (a + b * z).astype(np.float32)
 
 
+_CPU = False
+
+
+def _native_cpu():
+    """flexmi._cpu (native CPU kernels) or None when it is not built."""
+    global _CPU
+    if _CPU is False:
+        try:
+            from flexmi import _cpu as m
+            _CPU = m if hasattr(m, "counter_fill") else None
+        except ImportError:
+            _CPU = None
+    return _CPU
+
+
 class Initializer:
     kind = KIND_ZERO
 
@@ -79,6 +94,10 @@ class Initializer:
         if out.is_cuda:
             from flexmi.ops import _kernels as K
             K.init_fill(out, tuple(dims), tuple(box), kind, seed, float(a), float(b))
+        elif _native_cpu() is not None and out.dtype == torch.float32 and out.is_contiguous():
+            # csrc/cpu/init_metrics.cc: same values as the numpy oracle, on ATen's thread pool
+            _native_cpu().counter_fill(out, [int(d) for d in dims], [(int(lo), int(hi)) for lo, hi in box],
+                                       int(kind), int(seed), float(a), float(b))
         else:
             out.copy_(torch.from_numpy(counter_fill_cpu(kind, seed, a, b, tuple(dims), tuple(box))).reshape(out.shape))
 

@@ -130,23 +130,51 @@ DX_LIB = os.environ.get("FM_DX_LIB", "0") == "1"
 DX_LIB_MIN = int(os.environ.get("FM_DX_LIB_MIN", str(1 << 32)))
 
 
+class FusedSGD:
+    """The SGD update of one Linear weight, fused into its weight-gradient GEMM (``upd`` of
+    linear_backward): fp32 master ``w``, bf16 mirror ``wc`` (or None), momentum ``v`` (or None),
+    device-side ``lr`` and the optimizer's constants.  Only for weights whose gradient has no
+    other consumer (not all-reduced, not tied, single dW GEMM) -- Executor._plan_fused_sgd."""
+    __slots__ = ("w", "wc", "v", "lr", "wd", "mom", "nesterov")
+
+    def __init__(self, w, wc, v, lr, wd, mom, nesterov):
+        self.w, self.wc, self.v, self.lr = w, wc, v, lr
+        self.wd, self.mom, self.nesterov = float(wd), float(mom), bool(nesterov)
+
+    def apply(self, grad):
+        """Unfused fallback: the optimizer kernel over this weight's consumed gradient."""
+        sgd_update(self.w, grad, self.v, self.wc, self.lr, self.wd, self.mom, self.nesterov, zero_grad=True)
+
+
+def _dw_fused_sgd(dpre, x2, dw, db, upd):
+    """dW GEMM + SGD in one kernel (csrc/kernels/gemm.hip fm_gemm_dw_sgd, gemm_f32.hip
+    fm_gemm_f32_dw_sgd); False when it does not apply (misaligned views, ldw % 4 != 0) and the
+    caller must compute dW itself."""
+    ks = C().gemm_dw_sgd(dpre, x2, upd.w, upd.wc, upd.v, upd.lr, upd.wd, upd.mom, upd.nesterov, db,
+                         workspace(dpre.device, GEMM_WS_BYTES))
+    return ks >= 0
+
+
 def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=False, fuse_below=None, phase="all",
-                    async_dw=False):
+                    async_dw=False, upd=None):
     """Weight/bias grads ACCUMULATE into dw/db (the executor zeroes the flat gradient buffer once
     per step).  grad_is_dpre: dy2 already holds act'(y)*dy (written by the consumer's fused dX
     epilogue).  fuse_below = (y_below, act_below): apply the activation backward of the layer
     below in this layer's dX GEMM epilogue.  async_dw: the dW GEMM's split-K reduce may run on a
-    side stream, overlapping the dX GEMM (the caller joins with gemm_join() before dw is read)."""
+    side stream, overlapping the dX GEMM (the caller joins with gemm_join() before dw is read).
+    upd (FusedSGD): the weight is updated in place by this call (after its dX GEMM, which reads
+    it) and dw stays zero; the bias gradient is still accumulated into db."""
     M, K = x2.shape
     N = w.shape[0]
     vec = 4 if x2.dtype == torch.float32 else 8
     if N == 1 and K % vec == 0 and x2.stride(0) % vec == 0 and (dx2 is None or dx2.stride(0) % vec == 0):
-        if phase == "dw":          # the skinny kernel did dX, dW and db together in the "dx" phase
-            return
-        C().skinny_bwd(x2, w, y2, dy2, dx2, bool(dx_acc), dw, None if grad_is_dpre else db,
-                       10 if grad_is_dpre else act)
-        if dx2 is not None and fuse_below is not None:
-            raise AssertionError("no fused epilogue on the skinny path")
+        if phase != "dw":          # the skinny kernel does dX, dW and db together in the "dx" phase
+            C().skinny_bwd(x2, w, y2, dy2, dx2, bool(dx_acc), dw, None if grad_is_dpre else db,
+                           10 if grad_is_dpre else act)
+            if dx2 is not None and fuse_below is not None:
+                raise AssertionError("no fused epilogue on the skinny path")
+        if upd is not None and phase != "dx":
+            upd.apply(dw)
         return
     lib = _dw_lib(M, N, K, x2.dtype)
     fold_db = lib and not (grad_is_dpre or act == 10)    # db from the act-backward pass below
@@ -160,6 +188,22 @@ def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=F
             dpre = torch.empty((M, N), dtype=dy2.dtype, device=x2.device)
             ws["dpre"] = dpre
         C().act_bwd_bias(y2, dy2, dpre, db if fold_db else None, M, N, act)
+    if upd is not None:
+        # dX first (it reads W), then dW with the update fused in (or dW + the optimizer kernel)
+        if phase != "dw" and dx2 is not None:
+            _linear_dx(dpre, w, dx2, dx_acc, fuse_below, M, N, K)
+        if phase == "dx":
+            return
+        if not lib and M > 0 and _dw_fused_sgd(dpre, x2, dw, db, upd):
+            return
+        if lib:
+            dw.addmm_(dpre.t(), x2)
+            if db is not None and not fold_db:
+                C().act_bwd_bias(dpre, dpre, None, db, M, N, 10)
+        else:
+            gemm(dpre, dpre.stride(0), False, x2, x2.stride(0), False, dw, K, N, K, M, beta=True, rowsum_a=db)
+        upd.apply(dw)
+        return
     if lib and phase != "dx":
         dw.addmm_(dpre.t(), x2)                          # hipBLASLt, accumulates (beta = 1)
         if db is not None and not fold_db:
@@ -176,8 +220,13 @@ def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=F
              async_reduce=async_dw and ASYNC_DW)
     if phase == "dw":
         return
+    if dx2 is not None:
+        _linear_dx(dpre, w, dx2, dx_acc, fuse_below, M, N, K)
+
+
+def _linear_dx(dpre, w, dx2, dx_acc, fuse_below, M, N, K):
     # dX[M,K] = dpre W   (+ fused activation backward of the layer below)
-    if dx2 is not None and DX_LIB and M * K * N >= DX_LIB_MIN and dx2.is_contiguous():
+    if DX_LIB and M * K * N >= DX_LIB_MIN and dx2.is_contiguous():
         # plain library GEMM (hipBLASLt) for the big dX products, activation backward of the layer
         # below as a separate pass (FM_DX_LIB=1; A/B in profiles/README.md)
         t = torch.matmul(dpre, w)

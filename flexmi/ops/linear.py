@@ -45,6 +45,13 @@ def act_backward_torch(dy, y, act):
     return dy
 
 
+def _armed_sgd(ctx):
+    """The FusedSGD of this op's weight while the executor runs its fused training step
+    (Executor._plan_fused_sgd), else None."""
+    upd = getattr(ctx, "fused_sgd", None)
+    return upd if upd is not None and ctx.fused_sgd_state["on"] else None
+
+
 class Linear(Op):
     op_type = OperatorType.OP_LINEAR
     name_prefix = "Dense"
@@ -120,7 +127,7 @@ class Linear(Op):
             K.linear_backward(x2, ctx.wcompute[0], y2, dy2, int(act), dx2,
                               bool(ctx.in_grad_accumulate[0]) if dx2 is not None else False, dw, db,
                               ctx.workspace, ctx.saved.get("grad_is_dpre", False), ctx.saved.get("fuse_below"), phase,
-                              ctx.saved.get("async_dw", False))
+                              ctx.saved.get("async_dw", False), upd=_armed_sgd(ctx))
         else:
             dpre = act_backward_torch(dy2.float(), y2.float(), act)
             if phase != "dx":

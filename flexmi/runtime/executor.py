@@ -27,6 +27,7 @@ import numpy as np
 import torch
 
 from flexmi.core.loss_metrics import NUM_SLOTS, PerfMetrics, loss_and_metrics_torch
+from flexmi.core.initializers import _native_cpu
 from flexmi.core.optimizers import AdamOptimizer, SGDOptimizer
 from flexmi.core.types import DataType, LossType, to_torch_dtype
 from flexmi.ops.base import OpCtx
@@ -1579,6 +1580,77 @@ class Executor:
         if self.backend == "hip" and K.ASYNC_DW:
             bwd = self._with_gemm_joins(bwd)
         self.prog_fwd, self.prog_bwd, self.prog_upd = fwd, bwd, upd
+        self._plan_fused_sgd()
+
+    def _plan_fused_sgd(self):
+        """SGD fused into the weight-gradient GEMMs of the training step (FM_FUSED_SGD, default on).
+
+        A Linear weight qualifies when its gradient has no consumer besides the optimizer: SGD,
+        HIP backend, the weight's group is not replicated (no all-reduce) nor ZeRO-sharded, the
+        weight belongs to one op (not tied), and no debug guards.  For those, the step program
+        (``step_program`` / ``train_step``) runs the backward with ``ctx.fused_sgd`` armed: the op's
+        dW GEMM updates master, momentum and bf16 mirror in its epilogue after the op's dX GEMM
+        (csrc/kernels/gemm.hip fm_gemm_dw_sgd), and the update program runs the optimizer over the
+        remaining ranges only (one segmented launch).  ``backward()`` / ``update()`` called
+        separately keep the unfused semantics (gradients materialised, then updated).
+        Reference: the separate dW (linear.cu:592-635) and sgd_update (optimizer_kernel.cu:23-41)
+        tasks, which this removes the gradient's HBM round trip (write, read, re-zero) between."""
+        from flexmi.core.types import OperatorType
+        from flexmi.ops import _kernels as K
+        self.fused_sgd_state = {"on": False}
+        self.fused_sgd_entries = []
+        self.prog_bwd_fused = self.prog_upd_fused = None
+        opt = self.optimizer
+        if (self.backend != "hip" or not isinstance(opt, SGDOptimizer) or self.debug
+                or os.environ.get("FM_FUSED_SGD", "1") == "0"):
+            return
+        uses = defaultdict(int)
+        for st in self.bwd_steps:
+            if st[0] == "op":
+                for w in st[1].weights:
+                    uses[w.guid] += 1
+        for e in self.wentries.values():
+            g = e.group
+            if (g is None or g.replicated or g.zero or not e.numel or e.widx != 0 or uses[e.param.guid] != 1
+                    or e.op.op_type != OperatorType.OP_LINEAR):
+                continue
+            c = self.ctx.get(e.op.guid)
+            if c is None or not c.weight_grads or c.weight_grads[0] is not e.grad or not c.inputs:
+                continue
+            # weights whose dW runs in the library GEMM (fp32 big layers) or the skinny kernel keep
+            # their gradient and stay in the one segmented optimizer launch
+            n_out, n_in = e.master.shape[0], e.master.numel() // max(1, e.master.shape[0])
+            rows = c.inputs[0].numel() // max(1, c.inputs[0].shape[-1])
+            if n_out == 1 or K._dw_lib(rows, n_out, n_in, self.cdtype):
+                continue
+            c.fused_sgd = K.FusedSGD(e.master, e.compute if g.compute is not g.master else None,
+                                     e.state.get("v") if opt.momentum > 0 else None, self.lr_tensor,
+                                     opt.weight_decay, opt.momentum, opt.nesterov)
+            c.fused_sgd_state = self.fused_sgd_state
+            self.fused_sgd_entries.append(e)
+        if not self.fused_sgd_entries:
+            return
+        # per group: the ranges the update program still covers (gaps between fused weights)
+        fused = defaultdict(list)
+        for e in self.fused_sgd_entries:
+            fused[id(e.group)].append((e.offset, e.offset + e.numel))
+        for g in self.groups:
+            spans = sorted(fused.get(id(g), []))
+            rest, at = [], 0
+            for lo, hi in spans:
+                if lo > at:
+                    rest.append((at, lo - at))
+                at = max(at, hi)
+            if at < g.numel:
+                rest.append((at, g.numel - at))
+            g.sgd_rest = rest if spans else None
+
+        def arm(on):
+            self.fused_sgd_state["on"] = on
+        self.prog_bwd_fused = ([Item("compute", (lambda: arm(True)), "fused_sgd.arm")] + self.prog_bwd +
+                               [Item("compute", (lambda: arm(False)), "fused_sgd.disarm")])
+        self.prog_upd_fused = [Item("compute", (lambda: self._optimizer_step(fused=True)), "update")
+                               if it.name == "update" else it for it in self.prog_upd]
 
     @staticmethod
     def _with_gemm_joins(items):
@@ -2023,6 +2095,9 @@ class Executor:
 
     def update(self):
         self._run(self.prog_upd)
+        self._after_update()
+
+    def _after_update(self):
         if self.backend == "hip" and self.optimizer is not None:
             self._grads_dirty = any(g.zero for g in self.groups)   # update kernels re-zeroed the rest
         if self.optimizer is not None:
@@ -2055,7 +2130,9 @@ class Executor:
                     w.wait()
                 g.works[bi] = None
 
-    def _optimizer_step(self):
+    def _optimizer_step(self, fused=False):
+        """fused: the weights in ``fused_sgd_entries`` were already updated inside their dW GEMMs
+        (_plan_fused_sgd); only the remaining ranges of each group are updated here."""
         from flexmi.ops import _kernels as K
         opt = self.optimizer
         if isinstance(opt, AdamOptimizer):
@@ -2071,6 +2148,13 @@ class Executor:
                 self._zero_opt_step(g, opt)
                 continue
             comp = g.compute if g.compute is not g.master else None
+            rest = getattr(g, "sgd_rest", None) if fused else None
+            if rest is not None:
+                if rest:
+                    K.C().sgd_segs(g.master, g.gradbuf, g.state.get("v") if opt.momentum > 0 else None, comp,
+                                   self.lr_tensor, [r[0] for r in rest], [r[1] for r in rest], opt.weight_decay,
+                                   opt.momentum, opt.nesterov, True)
+                continue
             if self.backend == "hip":
                 # the kernels consume the gradient and leave it zeroed for the next backward
                 if isinstance(opt, SGDOptimizer):
@@ -2131,6 +2215,11 @@ class Executor:
         if self.backend == "hip":
             K.loss_forward_backward(int(self.loss_type), self.logits_buf, self.label_buf,
                                     self.logit_grad if compute_grad else None, scale, self.metric_acc, mask, clamp)
+        elif (_native_cpu() is not None and self.logits_buf.dtype == torch.float32 and self.logits_buf.is_contiguous()
+              and self.metric_acc.device.type == "cpu"):
+            # csrc/cpu/init_metrics.cc loss_metrics: one pass, gradient + metrics
+            _native_cpu().loss_metrics(int(self.loss_type), self.logits_buf, self.label_buf,
+                                       self.logit_grad if compute_grad else None, scale, self.metric_acc, mask, clamp)
         else:
             loss_and_metrics_torch(self.loss_type, self.logits_buf, self.label_buf, self.logit_grad,
                                    scale, self.metric_acc, mask, compute_grad, clamp=clamp)
@@ -2234,10 +2323,18 @@ class Executor:
     # ------------------------------------------------------------------ hipGraph
     def train_step(self):
         self.forward()
-        self.backward()
-        self.update()
+        if self.prog_bwd_fused is None:
+            self.backward()
+            self.update()
+            return
+        self._run(self.prog_bwd_fused)     # dW GEMMs of fused weights update them in place
+        self._grads_dirty = True
+        self._run(self.prog_upd_fused)
+        self._after_update()
 
     def step_program(self):
+        if self.prog_bwd_fused is not None:
+            return self.prog_fwd + self.prog_bwd_fused + self.prog_upd_fused
         return self.prog_fwd + self.prog_bwd + self.prog_upd
 
     def capture_step(self, pre=None):
