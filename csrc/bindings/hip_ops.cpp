@@ -239,6 +239,9 @@ void sgd_segs(torch::Tensor W, torch::Tensor G, c10::optional<torch::Tensor> V, 
     TORCH_CHECK(Wc->scalar_type() == torch::kBFloat16 && Wc->numel() == W.numel(), "sgd_segs: bf16 mirror");
   for (size_t i = 0; i < off.size(); ++i)
     TORCH_CHECK(off[i] >= 0 && len[i] >= 0 && off[i] + len[i] <= W.numel(), "sgd_segs: range outside the buffer");
+  // the kernel's vector body assumes the flat buffers start 16-B aligned (8-B for the bf16 mirror)
+  TORCH_CHECK((((uintptr_t)W.data_ptr() | (uintptr_t)G.data_ptr() | (uintptr_t)mptr(V)) & 15) == 0 &&
+                  (((uintptr_t)mptr(Wc)) & 7) == 0, "sgd_segs: 16-B aligned buffers");
   std::vector<long> o(off.begin(), off.end()), l(len.begin(), len.end());
   fm_sgd_update_segs(W.data_ptr<float>(), G.data_ptr<float>(), (float*)mptr(V), (unsigned short*)mptr(Wc),
                      lr.data_ptr<float>(), o.data(), l.data(), (int)o.size(), (float)wd, (float)mom, nesterov ? 1 : 0,

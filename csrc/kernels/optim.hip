@@ -59,22 +59,43 @@ __global__ void fm_sgd_segs_kernel(float* __restrict__ W, float* __restrict__ G,
                                    float wd, float mom, int nesterov, int zero_g) {
   const float lr = lr_p[0];
   const long o = segs.off[blockIdx.y], n = segs.len[blockIdx.y];
-  float* w = W + o;
-  float* g = G + o;
-  float* v = V ? V + o : nullptr;
-  unsigned short* wc = Wc ? Wc + o : nullptr;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    float gi = g[i] + wd * w[i];
-    if (zero_g) g[i] = 0.f;
+  // scalar head up to a 4-element boundary of the flat buffers (16-B W / G / V, 8-B Wc), vector body
+  const long head = min(n, (4 - (o & 3)) & 3L);
+  const long n4 = (n - head) / 4;
+  const long stride = (long)gridDim.x * blockDim.x, t0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  auto one = [&](long i) {
+    float gi = G[i] + wd * W[i];
+    if (zero_g) G[i] = 0.f;
     if (mom > 0.f) {
-      const float vi = v[i] * mom + gi;
-      v[i] = vi;
+      const float vi = V[i] * mom + gi;
+      V[i] = vi;
       gi = nesterov ? gi + mom * vi : vi;
     }
-    const float wi = w[i] - lr * gi;
-    w[i] = wi;
-    if (wc) wc[i] = f2bf(wi);
+    const float wi = W[i] - lr * gi;
+    W[i] = wi;
+    if (Wc) Wc[i] = f2bf(wi);
+  };
+  for (long i = t0; i < head; i += stride) one(o + i);
+  const long b = o + head;   // multiple of 4
+  for (long i = t0; i < n4; i += stride) {
+    const long e = b + 4 * i;
+    f32x4_t w = *reinterpret_cast<const f32x4_t*>(W + e);
+    f32x4_t g = *reinterpret_cast<const f32x4_t*>(G + e) + wd * w;
+    if (zero_g) *reinterpret_cast<f32x4_t*>(G + e) = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    if (mom > 0.f) {
+      const f32x4_t v = *reinterpret_cast<const f32x4_t*>(V + e) * mom + g;
+      *reinterpret_cast<f32x4_t*>(V + e) = v;
+      g = nesterov ? g + mom * v : v;
+    }
+    w -= lr * g;
+    *reinterpret_cast<f32x4_t*>(W + e) = w;
+    if (Wc) {
+      bf16x4_t c;
+      c[0] = (short)f2bf(w[0]); c[1] = (short)f2bf(w[1]); c[2] = (short)f2bf(w[2]); c[3] = (short)f2bf(w[3]);
+      *reinterpret_cast<bf16x4_t*>(Wc + e) = c;
+    }
   }
+  for (long i = head + 4 * n4 + t0; i < n; i += stride) one(o + i);
 }
 
 __global__ void fm_adam_kernel(float* __restrict__ W, float* __restrict__ G, float* __restrict__ M,
@@ -123,7 +144,8 @@ extern "C" void fm_sgd_update_segs(float* W, float* G, float* V, unsigned short*
       mx = sg.len[i] > mx ? sg.len[i] : mx;
     }
     if (mx <= 0) continue;
-    const int gx = (int)((mx + 255) / 256 < 256 ? (mx + 255) / 256 : 256);
+    const long per = (mx + 3) / 4;   // one 4-element group per thread
+    const int gx = (int)((per + 255) / 256 < 1024 ? (per + 255) / 256 : 1024);
     hipLaunchKernelGGL(fm_sgd_segs_kernel, dim3(gx, k), dim3(256), 0, s, W, G, V, Wc, lr, sg, wd, mom, nesterov, zero_g);
   }
 }

@@ -1604,6 +1604,10 @@ class Executor:
         if (self.backend != "hip" or not isinstance(opt, SGDOptimizer) or self.debug
                 or os.environ.get("FM_FUSED_SGD", "1") == "0"):
             return
+        # only weights big enough for the saved gradient round trip to matter: on the MLPerf DLRM
+        # (<= 1 M-element candidates) fusing measured 0.3-0.9 % slower, on summit_large
+        # (16-42 M-element layers) 1.61 -> 1.17 ms bf16 (profiles/fused_sgd_ab_r4i.txt)
+        min_numel = int(os.environ.get("FM_FUSED_SGD_MIN", str(1 << 21)))
         uses = defaultdict(int)
         for st in self.bwd_steps:
             if st[0] == "op":
@@ -1611,7 +1615,7 @@ class Executor:
                     uses[w.guid] += 1
         for e in self.wentries.values():
             g = e.group
-            if (g is None or g.replicated or g.zero or not e.numel or e.widx != 0 or uses[e.param.guid] != 1
+            if (g is None or g.replicated or g.zero or e.numel < max(1, min_numel) or e.widx != 0 or uses[e.param.guid] != 1
                     or e.op.op_type != OperatorType.OP_LINEAR):
                 continue
             c = self.ctx.get(e.op.guid)

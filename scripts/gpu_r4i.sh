@@ -15,5 +15,9 @@ for cfg in summit_large:256 mlperf:8192; do
     FM_FUSED_SGD=$f timeout -k 10 300 python3 bench.py --config ${cfg%%:*} --batch-per-gpu ${cfg##*:} --steps 30 --warmup 5 --no-dp >> $L 2>> $O/r4i_bench.err || exit $?
   done
 done
+for f in 1 0; do
+  echo "== alexnet -b 256 FM_FUSED_SGD=$f" >> $O/r4i_cnn.txt
+  FM_FUSED_SGD=$f timeout -k 10 240 python3 apps/train.py alexnet -b 256 --iterations 20 --graph --dtype bf16 >> $O/r4i_cnn.txt 2>&1 || exit $?
+done
 bash scripts/gpu_profile_step.sh r4i_sl --config summit_large --batch-per-gpu 256 --no-dp || exit $?
 exit 0

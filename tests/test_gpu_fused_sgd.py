@@ -62,6 +62,7 @@ def _train(monkeypatch, fused, graph, momentum, dtype="bf16"):
     from flexmi.core import FFConfig, FFModel, SGDOptimizer, LossType, MetricsType
     from flexmi.models.dlrm import DLRMConfig, build_dlrm, SyntheticDLRMData
     monkeypatch.setenv("FM_FUSED_SGD", "1" if fused else "0")
+    monkeypatch.setenv("FM_FUSED_SGD_MIN", "0")      # the tiny model's layers are below the default size
     cfg = FFConfig()
     cfg.batchSize = 512
     cfg.seed = 5
@@ -114,6 +115,7 @@ def test_separate_backward_update_keeps_gradients(gpu, monkeypatch):
     from flexmi.core import FFConfig, FFModel, SGDOptimizer, LossType, MetricsType
     from flexmi.models.dlrm import DLRMConfig, build_dlrm, SyntheticDLRMData
     monkeypatch.setenv("FM_FUSED_SGD", "1")
+    monkeypatch.setenv("FM_FUSED_SGD_MIN", "0")
     cfg = FFConfig()
     cfg.batchSize = 256
     m = FFModel(cfg)
@@ -129,3 +131,37 @@ def test_separate_backward_update_keeps_gradients(gpu, monkeypatch):
     assert ex.fused_sgd_entries
     assert any(float(e.grad.abs().max()) > 0 for e in ex.fused_sgd_entries)
     ex.update()
+
+
+@pytest.mark.parametrize("mom", [0.0, 0.9])
+def test_sgd_segs_matches_full_update(gpu, mom):
+    """The segmented optimizer launch (ranges off the 4-element grain, tiny and long ranges) updates
+    exactly the listed ranges like fm_sgd, and leaves everything else untouched."""
+    from flexmi.ops import _kernels as K
+    torch.manual_seed(2)
+    n = 100003
+    w0 = torch.randn(n, device=gpu)
+    g0 = torch.randn(n, device=gpu)
+    v0 = torch.randn(n, device=gpu) if mom > 0 else None
+    lr = torch.tensor([0.1], device=gpu)
+    segs = [(0, 5), (7, 1), (13, 40000), (40021, 3), (50001, 49999), (100000, 3)]
+    w, g = w0.clone(), g0.clone()
+    v = v0.clone() if v0 is not None else None
+    c = torch.zeros(n, device=gpu, dtype=torch.bfloat16)
+    K.C().sgd_segs(w, g, v, c, lr, [a for a, _ in segs], [b for _, b in segs], 1e-3, mom, True, True)
+    wr, gr = w0.clone(), g0.clone()
+    vr = v0.clone() if v0 is not None else None
+    cr = torch.zeros(n, device=gpu, dtype=torch.bfloat16)
+    for a, b in segs:
+        K.sgd_update(wr[a:a + b], gr[a:a + b], vr[a:a + b] if vr is not None else None, cr[a:a + b], lr, 1e-3, mom, True,
+                     zero_grad=True)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(w, wr, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(g, gr, rtol=0, atol=0)
+    torch.testing.assert_close(c.float(), cr.float(), rtol=0, atol=0)
+    if v is not None:
+        torch.testing.assert_close(v, vr, rtol=1e-6, atol=1e-7)
+    untouched = torch.ones(n, dtype=torch.bool, device=gpu)
+    for a, b in segs:
+        untouched[a:a + b] = False
+    assert torch.equal(w[untouched], w0[untouched])

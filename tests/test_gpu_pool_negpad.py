@@ -29,7 +29,8 @@ def _ref_pool(x, k, s, pt, pl, P, Q, is_max):
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("is_max", [True, False])
 @pytest.mark.parametrize("H,W,k,s,pt,pl", [(13, 27, 3, 2, 1, 1), (16, 16, 3, 2, -1, -1), (12, 55, 3, 2, 0, -1),
-                                            (9, 33, 2, 2, -1, 0), (11, 8, 3, 1, 1, 1)])
+                                            (9, 33, 2, 2, -1, 0), (11, 8, 3, 1, 1, 1), (55, 55, 3, 2, 0, 0),
+                                            (27, 27, 3, 2, 0, 0)])
 def test_pool_rows_and_negative_pads(dt, is_max, H, W, k, s, pt, pl):
     from flexmi.ops import _kernels as Kk
     torch.manual_seed(H * W + k)
