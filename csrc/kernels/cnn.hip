@@ -495,38 +495,10 @@ __global__ void __launch_bounds__(256) fm_pool_bwd_max_scatter(const T* __restri
     atomicAdd(&sdx[(gi * rows + h - h0b) * W + w], act == ACT_NONE ? gd : act_bwd(act, tof(y[oi]), gd));
   }
   __syncthreads();
-  // the band's input rows are contiguous in dx: 16-B vector stores (8 bf16 / 4 fp32 per lane)
-  // between a scalar head up to the first 16-B boundary and a scalar tail
+  // (a 16-B vector-store form of this loop -- 8 bf16 per lane between scalar head / tail -- measured
+  // SLOWER on AlexNet b256: 177 -> 200 us/step, profiles/prof_r4m_alexnet_b256_kernels.txt)
   T* dxp = dx + ((long)nc0 * H + h0b) * W;
-  constexpr int VE = 16 / (int)sizeof(T);
-  const int mis = (int)((reinterpret_cast<uintptr_t>(dxp) / sizeof(T)) & (VE - 1));
-  const int head = mis ? min(nin, VE - mis) : 0;
-  const int nv = (nin - head) / VE;
-  for (int e = threadIdx.x; e < head; e += 256) {
-    float g = sdx[e];
-    if (acc) g += tof(dxp[e]);
-    dxp[e] = fromf<T>(g);
-  }
-  for (int i = threadIdx.x; i < nv; i += 256) {
-    const int e0 = head + i * VE;
-    float g[VE];
-#pragma unroll
-    for (int j = 0; j < VE; ++j) g[j] = sdx[e0 + j];
-    if (acc) {
-#pragma unroll
-      for (int j = 0; j < VE; ++j) g[j] += tof(dxp[e0 + j]);
-    }
-    u32x4_t o;
-    if constexpr (sizeof(T) == 2) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = (unsigned)f2bf(g[2 * j]) | ((unsigned)f2bf(g[2 * j + 1]) << 16);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = __float_as_uint(g[j]);
-    }
-    *reinterpret_cast<u32x4_t*>(dxp + e0) = o;
-  }
-  for (int e = head + nv * VE + threadIdx.x; e < nin; e += 256) {
+  for (int e = threadIdx.x; e < nin; e += 256) {
     float g = sdx[e];
     if (acc) g += tof(dxp[e]);
     dxp[e] = fromf<T>(g);

@@ -96,6 +96,46 @@ struct Stage {
 };
 
 // NTH = 256: 4 waves (2x2, wave tile BM/2 x BN/2); 512: 8 waves (2x4 for BN >= 128, else 4x2).
+// Fused-SGD epilogue of an unsplit dW tile, staged through LDS: the accumulator layout gives each
+// lane 4 columns of one row, i.e. 64-B row pieces per 16x16 tile -- a scattered pattern that held the
+// W read-modify-write (fp32 master + bf16 mirror, ~10 B per element) at ~2.8 TB/s.  The waves first
+// park the BM x BN fp32 tile in the (free) operand LDS, 16-B chunks XOR-swizzled by row so both the
+// accumulator writes and the row reads stay conflict-light, then every wave updates whole rows:
+// BN*4 contiguous bytes of W per row (512 B for BN = 128).  The tile fits the K-loop LDS exactly
+// (BM*BN*4 <= 2*(BM+BN)*BK*2).
+template <int BM, int BN, int NTH, int MR, int NR>
+FM_DEVICE void sgd_epilogue_lds(const GemmP& p, const f32x4_t (&acc)[MR][NR], char* smem, int m0, int n0, int mb,
+                                int nb, int lane, int tid) {
+  constexpr int CPR = BN / 4;                       // 16-B chunks per tile row
+  f32x4_t* t = reinterpret_cast<f32x4_t*>(smem);
+  __syncthreads();                                  // every wave is done with the operand tiles
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const int r = mb + 16 * i + (lane & 15);
+      const int c = (nb + 16 * j + 4 * (lane >> 4)) >> 2;
+      t[r * CPR + (c ^ (r & 7))] = acc[i][j] * p.alpha;
+    }
+  __syncthreads();
+  const bool n4 = (p.N & 3) == 0;
+#pragma unroll 4
+  for (int q = tid; q < BM * CPR; q += NTH) {
+    const int r = q / CPR, c = q % CPR;
+    const int m = m0 + r, n = n0 + 4 * c;
+    if (m >= p.M || n >= p.N) continue;
+    const f32x4_t g = t[r * CPR + (c ^ (r & 7))];
+    const long o = (long)m * p.ldc + n;
+    if (n4 && n + 3 < p.N) {
+      sgd_apply4(p, o, g);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (n + e < p.N) sgd_apply1(p, o + e, g[e]);
+    }
+  }
+}
+
 template <int BM, int BN, bool AK, bool BKC, bool VEC, int NTH = NT>
 __global__ void __launch_bounds__(NTH, 2) fm_gemm_kernel(GemmP p) {
   constexpr int A_BYTES = BM * BK * 2;
@@ -199,6 +239,10 @@ __global__ void __launch_bounds__(NTH, 2) fm_gemm_kernel(GemmP p) {
 
 #undef LDS_A
 #undef LDS_B
+  if (p.uw && p.ksplit == 1 && p.ulds) {
+    sgd_epilogue_lds<BM, BN, NTH, MR, NR>(p, acc, smem, m0, n0, wm * TM, wn * TN, lane, tid);
+    return;
+  }
   gemm_epilogue<MR, NR>(p, acc, zb, split, m0 + wm * TM, n0 + wn * TN, lane);
 }
 
@@ -464,6 +508,9 @@ static int gemm_run(const void* A, long lda, long sA, int a_kcontig,
   p.uwd = upd ? upd->wd : 0.f;
   p.umom = upd ? upd->mom : 0.f;
   p.unest = upd ? upd->nest : 0;
+  // A/B knob FM_SGD_EPI_DIRECT=1: the update straight from the accumulator layout (no LDS staging)
+  static const bool sgd_direct = getenv("FM_SGD_EPI_DIRECT") != nullptr && atoi(getenv("FM_SGD_EPI_DIRECT")) == 1;
+  p.ulds = upd && !sgd_direct;
   // opt-in (FM_GEMM_ATOMIC_SPLIT=1): split-K partial tiles added straight into a small fp32
   // accumulating C with float atomics, no slabs and no reduce launch.  Measured SLOWER on the
   // DLRM dW GEMMs (profiles/README.md): the 16x16 accumulator layout issues 4-B atomics over 16

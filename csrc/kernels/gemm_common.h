@@ -88,6 +88,7 @@ struct GemmP {
   const float* ulr;      // device-side learning rate
   float uwd, umom;
   int unest;
+  int ulds;              // unsplit tiles stage the update through LDS (gemm.hip sgd_epilogue_lds)
 };
 
 // W -= lr * (g + wd W) (momentum / Nesterov as fm_sgd_kernel), one element at offset o of W

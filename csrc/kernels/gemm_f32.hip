@@ -55,6 +55,7 @@ struct GemmF {
   const float* ulr;
   float uwd, umom;
   int unest;
+  int ulds;             // unsplit tiles stage the update through LDS (sgd_epilogue_lds_f32)
 };
 
 template <int N>
@@ -278,6 +279,48 @@ FM_DEVICE void epilogue_f32(const GemmF& p, const f32x4_t (&acc)[MR][NR], int zb
   }
 }
 
+// Fused-SGD epilogue of an unsplit fp32 dW tile through LDS (same scheme as gemm.hip
+// sgd_epilogue_lds): the accumulator quads (quad_of, incl. the interleaved layouts) are parked in
+// the free operand LDS with row-XOR-swizzled 16-B chunks, then whole rows of W are updated with
+// contiguous BN*4-byte accesses.  BM*BN*4 <= 2*(BM+BN)*BKF*4: the tile fits the K-loop LDS.
+template <int BM, int BN, int NT, int MR, int NR, bool IL_A, bool IL_B>
+FM_DEVICE void sgd_epilogue_lds_f32(const GemmF& p, const f32x4_t (&acc)[MR][NR], char* smem, int m0, int n0,
+                                    int mbase, int nbase, int lane, int tid) {
+  constexpr int CPR = BN / 4;
+  f32x4_t* t = reinterpret_cast<f32x4_t*>(smem);
+  const int q = lane & 15, g = lane >> 4;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < MR; ++i) {
+    const int r = (IL_A ? mbase + MR * q + i : mbase + 16 * i + q) - m0;
+#pragma unroll
+    for (int u = 0; u < NR; ++u) {
+      int nn;
+      float v[4];
+      quad_of<MR, NR, IL_A, IL_B>(acc, i, u, nbase, g, nn, v);
+      const int c = (nn - n0) >> 2;
+      t[r * CPR + (c ^ (r & 7))] = f32x4_t{v[0], v[1], v[2], v[3]} * p.alpha;
+    }
+  }
+  __syncthreads();
+  const bool n4 = (p.N & 3) == 0;
+#pragma unroll 4
+  for (int e = tid; e < BM * CPR; e += NT) {
+    const int r = e / CPR, c = e % CPR;
+    const int m = m0 + r, n = n0 + 4 * c;
+    if (m >= p.M || n >= p.N) continue;
+    const f32x4_t gv = t[r * CPR + (c ^ (r & 7))];
+    const long o = (long)m * p.ldc + n;
+    if (n4 && n + 3 < p.N) {
+      sgd_apply4(p, o, gv);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (n + k < p.N) sgd_apply1(p, o + k, gv[k]);
+    }
+  }
+}
+
 // OPT: 1 = s_setprio(1) around each MFMA cluster (A/B only); 2 = fragment double buffer (default):
 // the second k-chunk's LDS fragments are read before the first chunk's MFMAs and interleaved with
 // them (sched_group_barrier).  Measured A/B, incl. removed experiments (de-phased blocks, diagnostic
@@ -411,6 +454,10 @@ __global__ void __launch_bounds__(NT, MINB) fm_gemm_f32_kernel(GemmF p) {
       }
       __syncthreads();
     }
+  }
+  if (p.uw && p.ksplit == 1 && p.ulds) {
+    sgd_epilogue_lds_f32<BM, BN, NT, MR, NR, !AK, !BKC>(p, acc, smem, m0, n0, m0 + wm * TM, n0 + wn * TN, lane, tid);
+    return;
   }
   epilogue_f32<MR, NR, !AK, !BKC>(p, acc, zb, split, m0 + wm * TM, n0 + wn * TN, lane);
 }
@@ -1402,6 +1449,8 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
   p.uwd = upd ? upd->wd : 0.f;
   p.umom = upd ? upd->mom : 0.f;
   p.unest = upd ? upd->nest : 0;
+  static const bool sgd_direct = getenv("FM_SGD_EPI_DIRECT") != nullptr && atoi(getenv("FM_SGD_EPI_DIRECT")) == 1;
+  p.ulds = upd && !sgd_direct;
   auto al = [](const void* q) { return (((uintptr_t)q) & 15) == 0; };
   bool vec = al(A) && al(B) && (lda % 4 == 0) && (ldb % 4 == 0) && (sA % 4 == 0) && (sB % 4 == 0);
   vec = vec && (a_kcontig ? (K % 4 == 0) : (M % 4 == 0)) && (b_kcontig ? (K % 4 == 0) : (N % 4 == 0));

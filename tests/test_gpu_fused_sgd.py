@@ -9,9 +9,10 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-# B (= GEMM K), out (= M), in (= N): 256x4096-like in-tile epilogue, long-K split-K through the
-# reduce, M / N tails off the tiles, in % 8 != 0 (scalar operand loads)
-SHAPES = [(256, 512, 384), (8192, 256, 128), (96, 100, 36), (64, 40, 20)]
+# B (= GEMM K), out (= M), in (= N): split-K through the reduce (small grids, long K), unsplit tiles
+# through the LDS-staged update (128x128 / 64x64 tiles, M / N tails), in % 8 != 0 (scalar loads)
+SHAPES = [(256, 512, 384), (8192, 256, 128), (96, 100, 36), (64, 40, 20), (64, 2000, 1028), (256, 2048, 2048),
+          (128, 4096, 512)]
 
 
 @pytest.mark.parametrize("shape", SHAPES, ids=[f"s{i}" for i in range(len(SHAPES))])
