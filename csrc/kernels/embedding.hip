@@ -110,6 +110,59 @@ __global__ void __launch_bounds__(256) fm_emb_fwd_multi(TabSet s, long B) {
   }
 }
 
+// Long bags on small batches (summit_large: 256 samples x 100 lookups per table): one lane group
+// per sample leaves ~100 blocks for 256 CUs, each lane walking the whole bag.  Here SP lane groups
+// share a sample -- group k sums lookups k, k+SP, ... -- and the block folds the SP partial rows
+// through LDS.  D <= 256 (one 16-B column chunk per lane, lpr = D/4 lanes per row).
+template <typename OutT, bool I64>
+__global__ void __launch_bounds__(256) fm_emb_fwd_split(TabSet s, long B, int sp) {
+  __shared__ f32x4_t part[256];
+  const TabDesc& d = s.t[blockIdx.y];
+  const int lpr = d.D >> 2;                        // <= 64
+  const int rpi = 256 / lpr;                       // lane groups per block
+  const int spb = rpi / sp;                        // samples per block
+  const int sub = threadIdx.x / lpr, lc = threadIdx.x - sub * lpr;
+  const bool live = sub < spb * sp;                // whole sample groups only
+  const int si = sub / sp, k = sub - si * sp;
+  const long b = (long)blockIdx.x * spb + si;
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  if (live && b < B) {
+    const int c = lc * 4;
+    int j = k;
+    for (; j + 3 * sp < d.bag; j += 4 * sp) {
+      long r[4];
+      bool ok[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) r[u] = local_row(ldi<I64>(d.idx, b * d.bag + j + u * sp), d.lo, d.rows, ok[u]);
+      f32x4_t v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const f32x4_t*>(d.W + r[u] * d.D + c);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (ok[u]) acc += v[u];
+    }
+    for (; j < d.bag; j += sp) {
+      bool ok;
+      const long r = local_row(ldi<I64>(d.idx, b * d.bag + j), d.lo, d.rows, ok);
+      const f32x4_t v = *reinterpret_cast<const f32x4_t*>(d.W + r * d.D + c);
+      if (ok) acc += v;
+    }
+  }
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  if (!live || k != 0 || b >= B) return;
+  for (int q = 1; q < sp; ++q) acc += part[threadIdx.x + q * lpr];
+  acc *= d.scale;
+  OutT* o = reinterpret_cast<OutT*>(d.act) + b * d.ld + lc * 4;
+  if constexpr (sizeof(OutT) == 4) {
+    *reinterpret_cast<f32x4_t*>(o) = acc;
+  } else {
+    bf16x4_t v;
+    v[0] = (short)f2bf(acc[0]); v[1] = (short)f2bf(acc[1]); v[2] = (short)f2bf(acc[2]); v[3] = (short)f2bf(acc[3]);
+    *reinterpret_cast<bf16x4_t*>(o) = v;
+  }
+}
+
 // scalar fallback for D % 4 != 0 (any D)
 template <typename OutT, bool I64>
 __global__ void __launch_bounds__(256) fm_emb_fwd_multi_scalar(TabSet s, long B) {
@@ -294,6 +347,26 @@ void launch_small(const TabSet& s, int m, bool dy_bf16, const float* lr, long B,
 template <bool I64>
 void launch_fwd(const TabSet& s, int m, bool vec, bool out_bf16, long B, int D0, hipStream_t st) {
   const int rpi = std::max(1, 256 / std::min(64, std::max(1, D0 / 4)));
+  // long bags with too few samples to fill the chip: split every bag over SP lane groups
+  // (FM_EMB_FWD_SPLIT=0 disables; measured on summit_large, profiles/README.md)
+  static const bool split_ok = !(getenv("FM_EMB_FWD_SPLIT") != nullptr && atoi(getenv("FM_EMB_FWD_SPLIT")) == 0);
+  int minbag = 1 << 30, maxD = 0, minD = 1 << 30;
+  for (int i = 0; i < m; ++i) {
+    minbag = std::min(minbag, s.t[i].bag);
+    maxD = std::max(maxD, s.t[i].D);
+    minD = std::min(minD, s.t[i].D);
+  }
+  if (split_ok && vec && maxD == minD && maxD <= 256 && minbag >= 16 && (B + rpi - 1) / rpi * m < 1024) {
+    int sp = 1;
+    while (sp * 2 <= rpi && sp * 2 <= minbag / 4 && (B * sp * 2 + rpi - 1) / rpi * m <= 2048) sp *= 2;
+    if (sp > 1) {
+      const int spb = rpi / sp;
+      dim3 grid((unsigned)((B + spb - 1) / spb), m);
+      if (out_bf16) hipLaunchKernelGGL((fm_emb_fwd_split<unsigned short, I64>), grid, dim3(256), 0, st, s, B, sp);
+      else hipLaunchKernelGGL((fm_emb_fwd_split<float, I64>), grid, dim3(256), 0, st, s, B, sp);
+      return;
+    }
+  }
   dim3 grid((unsigned)std::max<long>(1, std::min<long>((B + rpi - 1) / rpi, 2048)), m);
   if (vec) {
     if (out_bf16) hipLaunchKernelGGL((fm_emb_fwd_multi<unsigned short, I64>), grid, dim3(256), 0, st, s, B);

@@ -13,7 +13,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace -d $O/${TAG}_prof -o run -- python3 $
 DB=$(find $O/${TAG}_prof -name "*results.db" | head -1)
 cd $R
 python3 tools/prof_summary.py $DB 27 > $O/${TAG}_kernels.txt 2>&1
-python3 tools/prof_step.py $DB "fm_emb_fwd_multi<float" > $O/${TAG}_step_fp32.txt 2>&1
-python3 tools/prof_step.py $DB "fm_emb_fwd_multi<unsigned short" > $O/${TAG}_step_bf16.txt 2>&1
+python3 tools/prof_step.py $DB "fm_emb_fwd_multi<float|fm_emb_fwd_split<float" > $O/${TAG}_step_fp32.txt 2>&1
+python3 tools/prof_step.py $DB "fm_emb_fwd_multi<unsigned short|fm_emb_fwd_split<unsigned short" > $O/${TAG}_step_bf16.txt 2>&1
 rm -f $DB
 exit 0

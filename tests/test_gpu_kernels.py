@@ -489,3 +489,26 @@ def test_embedding_row_shards(gpu, idx_dtype):
         grads = [torch.zeros_like(s) for s in shards]
         Kk.C().embedding_bwd_multi(grads, [idx, idx], [dy, dy], [D, D], [1.0, 1.0], None, None, [cut[0], cut[1]])
         assert torch.allclose(torch.cat(grads), upd, atol=1e-3), (rows, "dense")
+
+
+@pytest.mark.parametrize("B,bag,D", [(256, 100, 64), (37, 20, 128), (5, 16, 48), (300, 33, 256)])
+@pytest.mark.parametrize("out_dt", [torch.float32, torch.bfloat16])
+def test_embedding_fwd_long_bag_split(gpu, B, bag, D, out_dt):
+    """Long bags on small batches (summit_large: 256 x 100) run the bag-split forward
+    (embedding.hip fm_emb_fwd_split): several tables, row shards, avg scale, vs a float64 oracle."""
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(B + bag)
+    rows = 5000
+    Ws = [torch.randn(rows, D, device=gpu) for _ in range(3)]
+    idxs = [torch.randint(0, rows, (B, bag), device=gpu) for _ in range(3)]
+    lo = [0, 0, 1000]            # third table: a row shard holding [1000, 6000)
+    scales = [1.0, 1.0 / bag, 1.0]
+    outs = [torch.empty(B, D, device=gpu, dtype=out_dt) for _ in range(3)]
+    Kk.C().embedding_fwd_multi(Ws, idxs, outs, [D] * 3, scales, lo)
+    torch.cuda.synchronize()
+    for W, idx, l, sc, o in zip(Ws, idxs, lo, scales, outs):
+        r = idx.long() - l
+        ok = (r >= 0) & (r < rows)
+        ref = (W.double()[r.clamp(0, rows - 1)] * ok[..., None]).sum(1) * sc
+        tol = 1e-5 if out_dt == torch.float32 else 1e-2
+        assert rel_err(o, ref) < tol, (B, bag, D)

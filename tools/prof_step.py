@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-dispatch timeline of the last full training step in a rocprofv3 rocpd database
 (kernels between the last two dispatches of the step's first kernel).
-usage: prof_step.py run_results.db [first_kernel_substring]"""
+usage: prof_step.py run_results.db [first_kernel_substring[|alternative...]]"""
 import sqlite3
 import sys
 
@@ -10,7 +10,8 @@ def main(path, first="fm_emb_fwd_multi"):
     c = sqlite3.connect(path)
     rows = list(c.execute("select name, duration, grid_x, grid_y, grid_z, workgroup_x, lds_size, vgpr_count, start "
                           "from kernels order by start"))
-    idx = [i for i, r in enumerate(rows) if first in r[0]]
+    keys = first.split("|")   # alternatives, e.g. "fm_emb_fwd_multi<float|fm_emb_fwd_split<float"
+    idx = [i for i, r in enumerate(rows) if any(k in r[0] for k in keys)]
     s, e = idx[-2], idx[-1]
     tot = 0
     for r in rows[s:e]:
