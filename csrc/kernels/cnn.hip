@@ -496,7 +496,9 @@ __global__ void __launch_bounds__(256) fm_pool_bwd_max_scatter(const T* __restri
   }
   __syncthreads();
   // (a 16-B vector-store form of this loop -- 8 bf16 per lane between scalar head / tail -- measured
-  // SLOWER on AlexNet b256: 177 -> 200 us/step, profiles/prof_r4m_alexnet_b256_kernels.txt)
+  // SLOWER on AlexNet b256: 177 -> 200 us/step, profiles/prof_r4m_alexnet_b256_kernels.txt: its
+  // 8-float-per-lane LDS reads conflict 8 ways); bf16 pairs per lane (4-B stores) measured neutral
+  // (176.7 us/step, profiles/prof_r4j_alexnet_b256_kernels.txt).
   T* dxp = dx + ((long)nc0 * H + h0b) * W;
   for (int e = threadIdx.x; e < nin; e += 256) {
     float g = sdx[e];

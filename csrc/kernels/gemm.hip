@@ -136,7 +136,7 @@ FM_DEVICE void sgd_epilogue_lds(const GemmP& p, const f32x4_t (&acc)[MR][NR], ch
   }
 }
 
-template <int BM, int BN, bool AK, bool BKC, bool VEC, int NTH = NT>
+template <int BM, int BN, bool AK, bool BKC, bool VEC, int NTH = NT, bool SGD = false>
 __global__ void __launch_bounds__(NTH, 2) fm_gemm_kernel(GemmP p) {
   constexpr int A_BYTES = BM * BK * 2;
   constexpr int B_BYTES = BN * BK * 2;
@@ -239,16 +239,20 @@ __global__ void __launch_bounds__(NTH, 2) fm_gemm_kernel(GemmP p) {
 
 #undef LDS_A
 #undef LDS_B
-  if (p.uw && p.ksplit == 1 && p.ulds) {
-    sgd_epilogue_lds<BM, BN, NTH, MR, NR>(p, acc, smem, m0, n0, wm * TM, wn * TN, lane, tid);
-    return;
+  if constexpr (SGD) {
+    if (p.ksplit == 1 && p.ulds) {
+      sgd_epilogue_lds<BM, BN, NTH, MR, NR>(p, acc, smem, m0, n0, wm * TM, wn * TN, lane, tid);
+      return;
+    }
   }
-  gemm_epilogue<MR, NR>(p, acc, zb, split, m0 + wm * TM, n0 + wn * TN, lane);
+  gemm_epilogue<MR, NR, SGD>(p, acc, zb, split, m0 + wm * TM, n0 + wn * TN, lane);
 }
 
+template <bool SGD>
 __global__ void fm_gemm_splitk_reduce(GemmP p);
 
 // 4 consecutive outputs per thread (16-B slab loads): N % 4 == 0, fp32 C with ldc % 4 == 0
+template <bool SGD>
 __global__ void fm_gemm_splitk_reduce4(GemmP p) {
   const long MN = (long)p.M * p.N;
   const long total4 = MN * p.batch / 4;
@@ -260,7 +264,7 @@ __global__ void fm_gemm_splitk_reduce4(GemmP p) {
     f32x4_t s = *reinterpret_cast<const f32x4_t*>(src);
     for (int k = 1; k < p.ksplit; ++k) s += *reinterpret_cast<const f32x4_t*>(src + k * MN);
     s *= p.alpha;
-    if (p.uw) {
+    if constexpr (SGD) {
       sgd_apply4(p, (long)m * p.ldc + n, s);
       continue;
     }
@@ -286,11 +290,17 @@ void launch_splitk_reduce(const GemmP& p, hipStream_t stream) {
   const bool v4 = p.c_fp32 && (p.N % 4 == 0) && (p.ldc % 4 == 0) && (p.sC % 4 == 0) &&
                   ((((uintptr_t)p.C) & 15) == 0);
   hipStream_t rs = fm_gemm_async_fork(stream);
-  if (v4) hipLaunchKernelGGL(fm_gemm_splitk_reduce4, dim3(fm_grid(total / 4)), dim3(256), 0, rs, p);
-  else hipLaunchKernelGGL(fm_gemm_splitk_reduce, dim3(fm_grid(total)), dim3(256), 0, rs, p);
+  if (p.uw) {
+    if (v4) hipLaunchKernelGGL(fm_gemm_splitk_reduce4<true>, dim3(fm_grid(total / 4)), dim3(256), 0, rs, p);
+    else hipLaunchKernelGGL(fm_gemm_splitk_reduce<true>, dim3(fm_grid(total)), dim3(256), 0, rs, p);
+  } else {
+    if (v4) hipLaunchKernelGGL(fm_gemm_splitk_reduce4<false>, dim3(fm_grid(total / 4)), dim3(256), 0, rs, p);
+    else hipLaunchKernelGGL(fm_gemm_splitk_reduce<false>, dim3(fm_grid(total)), dim3(256), 0, rs, p);
+  }
   if (rs != stream) fm_gemm_async_forked(rs);
 }
 
+template <bool SGD>
 __global__ void fm_gemm_splitk_reduce(GemmP p) {
   const long MN = (long)p.M * p.N;
   const long total = MN * p.batch;
@@ -301,7 +311,7 @@ __global__ void fm_gemm_splitk_reduce(GemmP p) {
     float s = 0.f;
     for (int k = 0; k < p.ksplit; ++k) s += src[k * MN];
     float v = s * p.alpha;
-    if (p.uw) {
+    if constexpr (SGD) {
       sgd_apply1(p, (long)m * p.ldc + n, v);
       continue;
     }
@@ -371,6 +381,18 @@ template <int BM, int BN, bool AK, bool BKC, bool VEC>
 void launch_t(const GemmP& p, hipStream_t s) {
   constexpr int LDS = 2 * (BM + BN) * BK * 2;
   dim3 grid(p.tiles_m * p.tiles_n, p.batch, p.ksplit);
+  if constexpr (!AK && !BKC) {   // fused-SGD dW GEMMs (both operands MN-contiguous): own instantiation
+    if (p.uw) {
+      if constexpr (VEC && BM == 128) {
+        if (!(g_gemm_variant_early() & 256)) {
+          hipLaunchKernelGGL((fm_gemm_kernel<BM, BN, AK, BKC, VEC, 512, true>), grid, dim3(512), LDS, s, p);
+          return;
+        }
+      }
+      hipLaunchKernelGGL((fm_gemm_kernel<BM, BN, AK, BKC, VEC, NT, true>), grid, dim3(NT), LDS, s, p);
+      return;
+    }
+  }
   // default: the 8-wave form of the 128-row tiles (4 waves per SIMD hide the per-K-tile barrier and
   // fragment latency: DLRM GEMMs -6 %, bf16 step 0.673 -> 0.626 ms, profiles/gemm_bf16_8wave_ab.jsonl);
   // variant bit 256 = the 4-wave kernel

@@ -150,10 +150,11 @@ FM_DEVICE int xcd_remap(int bid, int ntiles) {
 
 // ---- epilogue: lane owns C[m][n..n+3], m = lane&15, n = 4*(lane>>4) of each 16x16 tile;
 // tile (i, j) of the wave covers rows mbase+16i.., cols nbase+16j..
-template <int MR, int NR>
+// SGD: the fused-SGD instantiation (dW GEMMs of fm_gemm_dw_sgd); plain GEMMs compile without it
+template <int MR, int NR, bool SGD = false>
 FM_DEVICE void gemm_epilogue_store(const GemmP& p, const f32x4_t (&acc)[MR][NR], int zb, int mbase, int nbase, int lane);
 
-template <int MR, int NR>
+template <int MR, int NR, bool SGD = false>
 FM_DEVICE void gemm_epilogue(const GemmP& p, const f32x4_t (&acc)[MR][NR], int zb, int split, int mbase, int nbase,
                              int lane) {
   const int mrow = lane & 15;
@@ -251,13 +252,13 @@ FM_DEVICE void gemm_epilogue(const GemmP& p, const f32x4_t (&acc)[MR][NR], int z
       }
     GemmP q = p;
     q.ksplit = 1;
-    gemm_epilogue_store<MR, NR>(q, tot, zb, mbase, nbase, lane);
+    gemm_epilogue_store<MR, NR, SGD>(q, tot, zb, mbase, nbase, lane);
     return;
   }
-  gemm_epilogue_store<MR, NR>(p, acc, zb, mbase, nbase, lane);
+  gemm_epilogue_store<MR, NR, SGD>(p, acc, zb, mbase, nbase, lane);
 }
 
-template <int MR, int NR>
+template <int MR, int NR, bool SGD>
 FM_DEVICE void gemm_epilogue_store(const GemmP& p, const f32x4_t (&acc)[MR][NR], int zb, int mbase, int nbase, int lane) {
   const int mrow = lane & 15;
   const int ncol = 4 * (lane >> 4);
@@ -304,7 +305,7 @@ FM_DEVICE void gemm_epilogue_store(const GemmP& p, const f32x4_t (&acc)[MR][NR],
         for (int r = 0; r < 4; ++r) csum[j][r] += (n + r < p.N) ? v[r] : 0.f;
       }
       if (!mok) continue;
-      if (p.uw) {   // fused SGD: the host guarantees ldc % 4 == 0 and 16-B aligned W / V / C
+      if constexpr (SGD) {   // fused SGD: the host guarantees ldc % 4 == 0 and 16-B aligned W / V / C
         const long o = (long)m * p.ldc + n;
         if (full) {
           sgd_apply4(p, o, f32x4_t{v[0], v[1], v[2], v[3]});

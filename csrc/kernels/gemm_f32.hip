@@ -169,7 +169,7 @@ FM_DEVICE void quad_of(const f32x4_t (&acc)[MR][NR], int i, int u, int nbase, in
   }
 }
 
-template <int MR, int NR, bool IL_A, bool IL_B>
+template <int MR, int NR, bool IL_A, bool IL_B, bool SGD = false>
 FM_DEVICE void epilogue_f32(const GemmF& p, const f32x4_t (&acc)[MR][NR], int zb, int split, int mbase, int nbase,
                             int lane) {
   const int q = lane & 15, g = lane >> 4;
@@ -240,7 +240,7 @@ FM_DEVICE void epilogue_f32(const GemmF& p, const f32x4_t (&acc)[MR][NR], int zb
         for (int e = 0; e < 4; ++e) csum[u][e] += (n0 + e < p.N) ? v[e] : 0.f;
       }
       if (!mok) continue;
-      if (p.uw) {
+      if constexpr (SGD) {
         const long o = (long)m * p.ldc + n0;
         if (full) {
           sgd_apply4(p, o, f32x4_t{v[0], v[1], v[2], v[3]});
@@ -327,7 +327,7 @@ FM_DEVICE void sgd_epilogue_lds_f32(const GemmF& p, const f32x4_t (&acc)[MR][NR]
 // kernels without the K-loop loads / stores): profiles/gemm_f32_variants_ab.jsonl, gemm_f32_diag.jsonl.
 // NT = 256 (4 waves, 2x2, wave tile BM/2 x BN/2) or 512 (8 waves, 2x4 for BN >= 128, else 4x2:
 // twice the waves per SIMD to cover the LDS-read and barrier latency of each K tile).
-template <int BM, int BN, bool AK, bool BKC, bool VEC, int OPT = 0, int NT = NTF, int MINB = 2>
+template <int BM, int BN, bool AK, bool BKC, bool VEC, int OPT = 0, int NT = NTF, int MINB = 2, bool SGD = false>
 __global__ void __launch_bounds__(NT, MINB) fm_gemm_f32_kernel(GemmF p) {
   constexpr int A_BYTES = BM * BKF * 4;
   constexpr int B_BYTES = BN * BKF * 4;
@@ -455,14 +455,17 @@ __global__ void __launch_bounds__(NT, MINB) fm_gemm_f32_kernel(GemmF p) {
       __syncthreads();
     }
   }
-  if (p.uw && p.ksplit == 1 && p.ulds) {
-    sgd_epilogue_lds_f32<BM, BN, NT, MR, NR, !AK, !BKC>(p, acc, smem, m0, n0, m0 + wm * TM, n0 + wn * TN, lane, tid);
-    return;
+  if constexpr (SGD) {
+    if (p.ksplit == 1 && p.ulds) {
+      sgd_epilogue_lds_f32<BM, BN, NT, MR, NR, !AK, !BKC>(p, acc, smem, m0, n0, m0 + wm * TM, n0 + wn * TN, lane, tid);
+      return;
+    }
   }
-  epilogue_f32<MR, NR, !AK, !BKC>(p, acc, zb, split, m0 + wm * TM, n0 + wn * TN, lane);
+  epilogue_f32<MR, NR, !AK, !BKC, SGD>(p, acc, zb, split, m0 + wm * TM, n0 + wn * TN, lane);
 }
 
 // split-K reduce: 4 consecutive outputs per thread when N % 4 == 0 (16-B slab loads)
+template <bool SGD>
 __global__ void fm_gemm_f32_reduce(GemmF p, int v4) {
   const long MN = (long)p.M * p.N;
   const int E = v4 ? 4 : 1;
@@ -476,7 +479,7 @@ __global__ void fm_gemm_f32_reduce(GemmF p, int v4) {
     if (v4) {
       f32x4_t s = *reinterpret_cast<const f32x4_t*>(src);
       for (int k = 1; k < p.ksplit; ++k) s += *reinterpret_cast<const f32x4_t*>(src + k * MN);
-      if (p.uw) {
+      if constexpr (SGD) {
         sgd_apply4(p, (long)m * p.ldc + n, s * p.alpha);
         continue;
       }
@@ -487,7 +490,7 @@ __global__ void fm_gemm_f32_reduce(GemmF p, int v4) {
     } else {
       float s = 0.f;
       for (int k = 0; k < p.ksplit; ++k) s += src[k * MN];
-      if (p.uw) {
+      if constexpr (SGD) {
         sgd_apply1(p, (long)m * p.ldc + n, s * p.alpha);
         continue;
       }
@@ -817,7 +820,8 @@ namespace {
 
 void launch_reduce_f32(const GemmF& p, int v4, long total, hipStream_t stream) {
   hipStream_t rs = fm_gemm_async_fork(stream);
-  hipLaunchKernelGGL(fm_gemm_f32_reduce, dim3(fm_grid(total)), dim3(256), 0, rs, p, v4);
+  if (p.uw) hipLaunchKernelGGL(fm_gemm_f32_reduce<true>, dim3(fm_grid(total)), dim3(256), 0, rs, p, v4);
+  else hipLaunchKernelGGL(fm_gemm_f32_reduce<false>, dim3(fm_grid(total)), dim3(256), 0, rs, p, v4);
   if (rs != stream) fm_gemm_async_forked(rs);
 }
 
@@ -825,6 +829,16 @@ template <int BM, int BN, bool AK, bool BKC, bool VEC>
 void launch_f(const GemmF& p, hipStream_t s, int opt) {
   constexpr int LDS = 2 * (BM + BN) * BKF * 4;
   dim3 grid(p.tiles_m * p.tiles_n, p.batch, p.ksplit);
+  if constexpr (!AK && !BKC && BM <= 128) {   // fused-SGD dW GEMMs: own instantiation of the default forms
+    if (p.uw) {
+      if constexpr (VEC && BM == 128) {
+        hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 2, 512, 2, true>), grid, dim3(512), LDS, s, p);
+      } else {
+        hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 0, NTF, 2, true>), grid, dim3(NTF), LDS, s, p);
+      }
+      return;
+    }
+  }
   if constexpr (VEC && BM == 256 && BN == 128) {
     // one 4-wave block per CU, one wave per SIMD with a 128x64 wave tile (the shape hipBLASLt's
     // fp32 kernel uses on these GEMMs: 8x4 16x16 accumulators, 512-VGPR budget)

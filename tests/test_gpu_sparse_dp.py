@@ -50,7 +50,10 @@ def test_sdp_coalesce_and_apply(dy_dtype):
         order = torch.argsort(got_ids)
         assert torch.equal(got_ids[order], uniq)
         got = g[k][:n * D].view(n, D)[order].double()
-        torch.testing.assert_close(got, s, rtol=1e-5, atol=1e-5)
+        # fp32 sums in atomic (run-dependent) order: the 3-row table folds ~340 duplicates per row,
+        # whose rounding reached 1.3e-5 absolute in one run -- bound it by the duplicate count
+        dup = B * bag / max(1, uniq.numel())
+        torch.testing.assert_close(got, s, rtol=1e-5, atol=1e-5 * max(1.0, dup ** 0.5))
     # apply two segments in order: own (0) and a peer's payload with unique rows
     lr = torch.tensor([0.05], device=dev)
     seg1_ids, seg1_g, seg1_cnt = [], [], []
