@@ -20,6 +20,13 @@ activations / MFMA operands, fp32 master weights and accumulation) is measured a
 same process and reported as a secondary field ``config.bf16`` (``--dtype bf16`` makes it the
 headline, ``--no-secondary`` skips it).
 
+Plans (N > 1): the headline is the SOAP-SEARCHED plan (``--strategy search``, the default): rank 0
+runs the MCMC search over the MI355X execution simulator (budget ``--search-budget``, seeded with the
+hand plan; the reference's FFModel::optimize, src/runtime/model.cc:1093-1144) and every rank trains
+with that plan; ``config.search`` carries the simulated speedup, budget and wall seconds.  The hand
+plan the search was seeded with (table-wise / column-split embeddings + DP MLPs, dlrm_strategy) is
+then timed as ``config.table`` (``config.search_speedup_vs_table``).
+
 SOAP vs DP (N > 1): after the headline plan, the same model / precision / batch is built and timed
 under pure data parallelism -- every table replicated on every GPU and trained by touched-row
 exchange (each replica coalesces its lookups, one all-gather of (row, gradient) payloads, every
@@ -52,10 +59,12 @@ def parse():
     ap.add_argument("--config", default="mlperf", choices=["mlperf", "run_random", "criteo_kaggle", "summit", "summit_large", "kaggle_day1", "tiny"])
     ap.add_argument("--batch-per-gpu", type=int, default=8192)
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture of the step")
-    ap.add_argument("--strategy", default="table", choices=["table", "dp", "search"],
-                    help="table: table-wise embedding placement + DP MLPs (default); dp: pure data parallel; "
-                         "search: MCMC SOAP search over the MI355X simulator (seeded with 'table')")
-    ap.add_argument("--search-budget", type=int, default=4000)
+    ap.add_argument("--strategy", default=None, choices=["table", "dp", "search"],
+                    help="search (default for N>1): MCMC SOAP search over the MI355X simulator, seeded with "
+                         "'table' (the reference's FFModel::optimize, src/runtime/model.cc:1093-1144); table: "
+                         "table-wise embedding placement + DP MLPs (the hand plan, dlrm_strategy); dp: pure data "
+                         "parallel")
+    ap.add_argument("--search-budget", type=int, default=10000)
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--table-scale", type=float, default=1.0, help="debug only: shrink tables (invalid for reporting)")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
@@ -63,7 +72,12 @@ def parse():
     ap.add_argument("--no-secondary", action="store_true", help="skip the secondary run in the other precision")
     ap.add_argument("--no-dp", action="store_true",
                     help="N>1: skip the pure data-parallel comparison run (config.dp / config.soap_speedup_vs_dp)")
-    return ap.parse_args()
+    ap.add_argument("--no-table", action="store_true",
+                    help="N>1 with --strategy search: skip the hand-plan comparison run (config.table)")
+    a = ap.parse_args()
+    if a.strategy is None:
+        a.strategy = "search" if a.gpus > 1 else "table"
+    return a
 
 
 def launch_ranks(a) -> int:
@@ -105,6 +119,10 @@ def main():
     second = None
     if cuda and not a.no_secondary:
         second = run_once(a, "bf16" if a.dtype == "fp32" else "fp32", comm)
+    table = None
+    if world > 1 and a.strategy == "search" and not a.no_table:
+        # the hand-written plan the search was seeded with (table-wise / column embeddings + DP MLPs)
+        table = run_once(a, a.dtype, comm, strategy="table")
     dp = None
     if world > 1 and a.strategy != "dp" and not a.no_dp:
         # the second half of the BASELINE metric: the same model, precision and batch under pure
@@ -115,6 +133,11 @@ def main():
         if second is not None:
             rec["config"][second["dtype"]] = {"value": second["rec"]["value"], "ms_per_step": second["rec"]["ms_per_step"],
                                               "loss": second["rec"]["config"]["loss"]}
+        if table is not None:
+            rec["config"]["table"] = {"value": table["rec"]["value"], "ms_per_step": table["rec"]["ms_per_step"],
+                                      "loss": table["rec"]["config"]["loss"],
+                                      "parallelism": table["rec"]["config"]["parallelism"]}
+            rec["config"]["search_speedup_vs_table"] = round(rec["value"] / table["rec"]["value"], 3)
         if dp is not None:
             rec["config"]["dp"] = {"value": dp["rec"]["value"], "ms_per_step": dp["rec"]["ms_per_step"],
                                    "loss": dp["rec"]["config"]["loss"], "parallelism": dp["rec"]["config"]["parallelism"]}
@@ -124,13 +147,17 @@ def main():
         print(f"ELAPSED TIME = {head['el']:.4f}s, THROUGHPUT = {rec['value']:.2f} samples/s", file=sys.stderr)
         print(json.dumps(rec), flush=True)
     if world > 1:
-        dist.barrier()
+        backend = comm.backend
+        # ordered teardown (barrier, native runners, subset and world communicators, reference
+        # cycles; flexmi.parallel.comm.shutdown_distributed) -- then a normal interpreter exit
         dist.destroy_process_group()
-        # the JSON line is out and the communicators are torn down: leave without interpreter
-        # finalisation, so no static destructor racing a peer's teardown can fail a finished rank
-        sys.stdout.flush()
-        sys.stderr.flush()
-        os._exit(0)
+        if backend == "nccl":
+            # the JSON line is out and every communicator is destroyed; what remains is HIP/RCCL
+            # runtime finalisation at exit, which is not part of the measurement and must not be
+            # able to stall a finished rank of the driver's multi-GPU run
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0)
 
 
 def run_once(a, dtype, comm, strategy=None):
@@ -159,12 +186,22 @@ def run_once(a, dtype, comm, strategy=None):
     if world > 1 and strategy in ("table", "search"):
         strategies = dlrm_strategy(model, world)
     if world > 1 and strategy == "search":
-        from flexmi.core import SGDOptimizer as _S
-        from flexmi.parallel.search import optimize
-        model.optimizer = _S(model, 0.01)
-        search = optimize(model, a.search_budget, 1.0, num_devices=world, init=strategies, seed=0,
-                          verbose=(rank == 0))
-        strategies = dict(search.best)
+        cached = getattr(a, "_search_plan", None)
+        if cached is None:
+            # rank 0 searches (fixed budget and seed), every rank applies rank 0's plan
+            plan = [None, None]
+            if rank == 0:
+                from flexmi.core import SGDOptimizer as _S
+                from flexmi.parallel.search import optimize
+                model.optimizer = _S(model, 0.01)
+                res = optimize(model, a.search_budget, 1.0, num_devices=world, init=strategies, seed=0, verbose=True)
+                summ = {k: round(v, 4) for k, v in res.summary().items()}
+                summ["budget"] = a.search_budget
+                plan = [dict(res.best), summ]
+            dist.broadcast_object_list(plan, src=0)
+            a._search_plan = cached = (plan[0], plan[1])
+        strategies = dict(cached[0])
+        search = cached[1]
     model.strategies = strategies
     loss = LossType.LOSS_BINARY_CROSSENTROPY if dcfg.loss == "bce" else LossType.LOSS_MEAN_SQUARED_ERROR_AVG_REDUCE
     model.compile(SGDOptimizer(model, 0.01), loss, [MetricsType.METRICS_ACCURACY, MetricsType.METRICS_MEAN_SQUARED_ERROR])
@@ -268,7 +305,7 @@ def run_once(a, dtype, comm, strategy=None):
         },
     }
     if search is not None:
-        rec["config"]["search"] = {k: round(v, 4) for k, v in search.summary().items()}
+        rec["config"]["search"] = dict(search)
     if rank == 0 and a.profile:
         ex.timer.print_summary(file=sys.stderr)
     out = {"rec": rec, "el": el, "dtype": cfg.compute_dtype}

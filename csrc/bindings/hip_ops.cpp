@@ -65,6 +65,11 @@ void fm_dot_interaction_fwd(const void* const* z, int F, long ldz, void* out, lo
                             hipStream_t s);
 void fm_dot_interaction_bwd(const void* const* z, int F, long ldz, const void* dout, long ldo, void* const* dz, long lddz,
                             unsigned acc_mask, long B, int D, int self, hipStream_t s);
+int fm_dot_interaction_fwd_f32g(const float* const* z, const void* const* ix, const long* ld, const long* rows, int i64,
+                                int F, float* out, long ldo, long B, int D, int W, int self, hipStream_t s);
+int fm_dot_interaction_bwd_f32g(const float* const* z, const void* const* ix, const long* ld, const long* rows, int i64,
+                                int F, const float* dout, long ldo, float* const* dz, long lddz, unsigned acc_mask, long B,
+                                int D, int self, hipStream_t s);
 void fm_dot_interaction_fwd_f32(const float* const* z, int F, long ldz, float* out, long ldo, long B, int D, int W, int self,
                                 hipStream_t s);
 void fm_dot_interaction_bwd_f32(const float* const* z, int F, long ldz, const float* dout, long ldo, float* const* dz,
@@ -583,6 +588,77 @@ void dot_bwd(std::vector<torch::Tensor> zs, int64_t ldz, torch::Tensor dout, int
   TORCH_CHECK(D % 8 == 0 && D <= 256, "dot interaction backward: D % 8 == 0, D <= 256");
   fm_dot_interaction_bwd(p.data(), (int)p.size(), ldz, dout.data_ptr(), ldo, g.data(), lddz, (unsigned)acc_mask,
                          dout.size(0), (int)D, self ? 1 : 0, cur());
+}
+
+// Gathered-row (embedding-into-interaction) forms, fp32: zs[i] is feature i's [rows, D] source --
+// the bottom-MLP output (ixs[i] = None: row b) or an embedding TABLE (ixs[i] = the bag-1 lookup
+// indices [B] / [B, 1]: row ixs[i][b]).  Returns false when the fast kernels do not apply (nothing
+// launched; the caller falls back to materialised embedding outputs).
+static bool gather_args(const std::vector<torch::Tensor>& zs, const std::vector<c10::optional<torch::Tensor>>& ixs, long B,
+                        int64_t D, std::vector<const float*>& p, std::vector<const void*>& ix, std::vector<long>& ld,
+                        std::vector<long>& rows, int& i64) {
+  TORCH_CHECK(zs.size() >= 2 && zs.size() <= 32 && ixs.size() == zs.size(), "dot gather: 2..32 features");
+  i64 = -1;
+  for (size_t i = 0; i < zs.size(); ++i) {
+    const auto& z = zs[i];
+    check_cuda(z, "z");
+    if (z.scalar_type() != torch::kFloat32 || z.dim() != 2 || z.size(1) < D || z.stride(1) != 1) return false;
+    p.push_back(z.data_ptr<float>());
+    ld.push_back(z.stride(0));
+    rows.push_back(z.size(0));
+    if (ixs[i].has_value()) {
+      const auto& t = *ixs[i];
+      check_cuda(t, "ix");
+      if (t.numel() != B || !t.is_contiguous()) return false;
+      const int w = t.scalar_type() == torch::kInt64 ? 1 : t.scalar_type() == torch::kInt32 ? 0 : -1;
+      if (w < 0 || (i64 >= 0 && w != i64)) return false;
+      i64 = w;
+      ix.push_back(t.data_ptr());
+    } else {
+      if (z.size(0) < B) return false;
+      ix.push_back(nullptr);
+    }
+  }
+  if (i64 < 0) i64 = 1;
+  return true;
+}
+
+bool dot_fwd_gather(std::vector<torch::Tensor> zs, std::vector<c10::optional<torch::Tensor>> ixs, torch::Tensor out,
+                    int64_t ldo, int64_t D, int64_t W, bool self) {
+  const long B = out.size(0);
+  std::vector<const float*> p;
+  std::vector<const void*> ix;
+  std::vector<long> ld, rows;
+  int i64 = 1;
+  check_cuda(out, "out");
+  if (out.scalar_type() != torch::kFloat32 || !gather_args(zs, ixs, B, D, p, ix, ld, rows, i64)) return false;
+  TORCH_CHECK(out.numel() >= (B - 1) * ldo + W, "dot output too small");
+  return fm_dot_interaction_fwd_f32g(p.data(), ix.data(), ld.data(), rows.data(), i64, (int)zs.size(), out.data_ptr<float>(),
+                                     ldo, B, (int)D, (int)W, self ? 1 : 0, cur()) == 0;
+}
+
+bool dot_bwd_gather(std::vector<torch::Tensor> zs, std::vector<c10::optional<torch::Tensor>> ixs, torch::Tensor dout,
+                    int64_t ldo, std::vector<c10::optional<torch::Tensor>> dzs, int64_t lddz, int64_t acc_mask, int64_t D,
+                    bool self) {
+  const long B = dout.size(0);
+  const long F = (long)zs.size();
+  std::vector<const float*> p;
+  std::vector<const void*> ix;
+  std::vector<long> ld, rows;
+  int i64 = 1;
+  check_cuda(dout, "dout");
+  if (dout.scalar_type() != torch::kFloat32 || (long)dzs.size() != F || !gather_args(zs, ixs, B, D, p, ix, ld, rows, i64))
+    return false;
+  const long np = self ? F * (F + 1) / 2 : F * (F - 1) / 2;
+  TORCH_CHECK(ldo >= D + np && dout.numel() >= (B - 1) * ldo + D + np, "dot gather backward: dOut row too small");
+  std::vector<float*> g;
+  for (auto& d : dzs) {
+    g.push_back((float*)mptr(d));
+    if (d.has_value())
+      TORCH_CHECK(d->scalar_type() == torch::kFloat32 && d->numel() >= (B - 1) * lddz + D, "dot gather backward: fp32 grads");
+  }
+  return fm_dot_interaction_bwd_f32g(p.data(), ix.data(), ld.data(), rows.data(), i64, (int)F, dout.data_ptr<float>(), ldo,
+                                     g.data(), lddz, (unsigned)acc_mask, B, (int)D, self ? 1 : 0, cur()) == 0;
 }
 
 void sgd(torch::Tensor W, torch::Tensor G, c10::optional<torch::Tensor> V, c10::optional<torch::Tensor> Wc, torch::Tensor lr,
@@ -1121,6 +1197,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("sdp_apply", &sdp_apply);
   m.def("dot_fwd", &dot_fwd);
   m.def("dot_bwd", &dot_bwd);
+  m.def("dot_fwd_gather", &dot_fwd_gather);
+  m.def("dot_bwd_gather", &dot_bwd_gather);
   m.def("sgd", &sgd);
   m.def("adam", &adam);
   m.def("cast_bf16", &cast_bf16);

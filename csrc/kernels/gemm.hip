@@ -107,6 +107,8 @@ template <int BM, int BN, int NTH, int MR, int NR>
 FM_DEVICE void sgd_epilogue_lds(const GemmP& p, const f32x4_t (&acc)[MR][NR], char* smem, int m0, int n0, int mb,
                                 int nb, int lane, int tid) {
   constexpr int CPR = BN / 4;                       // 16-B chunks per tile row
+  static_assert(BM * BN * 4 <= 2 * (BM + BN) * BK * 2, "fp32 tile must fit the K-loop LDS");
+  static_assert(CPR >= 8, "row XOR swizzle (r & 7) needs >= 8 chunks per row");
   f32x4_t* t = reinterpret_cast<f32x4_t*>(smem);
   __syncthreads();                                  // every wave is done with the operand tiles
 #pragma unroll

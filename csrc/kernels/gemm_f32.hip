@@ -22,304 +22,12 @@
 // activation, activation-backward of the layer below (y fp32) + its bias-gradient column sums,
 // beta accumulate; dW GEMMs fold the bias gradient in as row sums of the staged A tiles.
 // Split-K writes fp32 slabs reduced by one vectorised reduce launch.  XCD-aware tile order.
-#include "gemm_common.h"
+#include "gemm_f32_common.h"
 
 #include <algorithm>
 #include <cstdlib>
 
 namespace {
-
-constexpr int NTF = 256;   // threads per block
-constexpr int BKF = 32;    // k per LDS tile (fp32)
-
-struct GemmF {
-  const float* A; long lda; long sA;
-  const float* B; long ldb; long sB;
-  float* C; long ldc; long sC;
-  const float* bias;
-  float* ws;            // split-K slabs [batch][split][M][N]
-  const float* ay;      // fused act-bwd of the layer below: v = act'(ay) * v
-  long lday;
-  float* colsum;        // += column sums of the (post act-bwd) output
-  float* rowsum_a;      // += sum_k A(m,k)  (MN-contiguous A only)
-  int bact;
-  int M, N, K, act, beta, ksplit, batch;
-  float alpha;
-  int tiles_m, tiles_n, n_fast;
-  int atomic;           // split-K partials float-atomically added into C (32x32 kernel, beta = 1)
-  // fused SGD (fm_gemm_f32_dw_sgd; default register-staged kernel and its reduce only): the
-  // epilogue updates W (same [M][ldc] layout as C) instead of storing the gradient
-  float* uw;
-  unsigned short* uwc;
-  float* uv;
-  const float* ulr;
-  float uwd, umom;
-  int unest;
-  int ulds;             // unsplit tiles stage the update through LDS (sgd_epilogue_lds_f32)
-};
-
-template <int N>
-using fvec = float __attribute__((ext_vector_type(N)));
-
-FM_DEVICE int xcd_remap_f(int bid, int ntiles) {
-  int q = ntiles / 8, r = ntiles % 8, x = bid % 8;
-  if (ntiles >= 8) bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
-  return bid;
-}
-
-// byte offset of 16-B chunk c (4 floats) of row r in a K-contiguous image (128-B rows)
-FM_DEVICE int kc_off(int r, int c) { return r * (BKF * 4) + 16 * (c ^ ((r >> 1) & 7)); }
-
-// ---- global -> registers -> LDS (one operand tile) ----------------------------------------
-template <bool KC, int R, bool VEC, int NT = NTF>
-struct StageF {
-  static constexpr int CHUNKS = R * BKF / 4;
-  static constexpr int PER_T = CHUNKS / NT;
-  static_assert(PER_T >= 1 && CHUNKS % NT == 0, "tile too small for the block");
-  f32x4_t v[PER_T];
-
-  FM_DEVICE void load(const float* __restrict__ p, long ld, int row0, int rows, int k0, int K, int tid) {
-#pragma unroll
-    for (int i = 0; i < PER_T; ++i) {
-      const int ci = tid + NT * i;
-      int gr, gk;
-      if constexpr (KC) {
-        gr = row0 + (ci >> 3);
-        gk = k0 + 4 * (ci & 7);
-      } else {
-        gk = k0 + ci / (R / 4);
-        gr = row0 + 4 * (ci % (R / 4));
-      }
-      if constexpr (VEC) {
-        if (gr < rows && gk < K) {
-          const float* src = KC ? (p + (long)gr * ld + gk) : (p + (long)gk * ld + gr);
-          v[i] = *reinterpret_cast<const f32x4_t*>(src);
-        } else {
-          v[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int rr = KC ? gr : gr + j;
-          const int kk = KC ? gk + j : gk;
-          v[i][j] = (rr < rows && kk < K) ? (KC ? p[(long)rr * ld + kk] : p[(long)kk * ld + rr]) : 0.f;
-        }
-      }
-    }
-  }
-
-  FM_DEVICE void store(char* lds, int tid) {
-#pragma unroll
-    for (int i = 0; i < PER_T; ++i) {
-      const int ci = tid + NT * i;
-      int off;
-      if constexpr (KC) off = kc_off(ci >> 3, ci & 7);
-      else off = (ci / (R / 4)) * (R * 4) + 16 * (ci % (R / 4));
-      *reinterpret_cast<f32x4_t*>(lds + off) = v[i];
-    }
-  }
-
-  // MN-contiguous operand: every chunk of this thread covers the same 4 rows (tid % (R/4)),
-  // so per-thread sums over the staged k are row partial sums (bias grad inside the dW GEMM)
-  FM_DEVICE void accumulate_rows(float (&s)[4]) const {
-#pragma unroll
-    for (int i = 0; i < PER_T; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) s[j] += v[i][j];
-  }
-};
-
-// fragments of one operand for one 16-wide k-chunk: f[t][s] = element (tile t, k-step s)
-template <bool KC, int R, int T>
-FM_DEVICE void load_frags(const char* lds, int base, int kk, int lane, float (&f)[T][4]) {
-  const int q = lane & 15, g = lane >> 4;
-  if constexpr (KC) {
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-      const f32x4_t x = *reinterpret_cast<const f32x4_t*>(lds + kc_off(base + 16 * t + q, 4 * kk + g));
-#pragma unroll
-      for (int s = 0; s < 4; ++s) f[t][s] = x[s];
-    }
-  } else {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int k = 16 * kk + 4 * g + s;
-      const fvec<T> x = *reinterpret_cast<const fvec<T>*>(lds + k * (R * 4) + 4 * (base + T * q));
-#pragma unroll
-      for (int t = 0; t < T; ++t) f[t][s] = x[t];
-    }
-  }
-}
-
-// ---- epilogue ---------------------------------------------------------------------------------
-// lane (q = lane&15, g = lane>>4) holds acc[i][j][r] = C[m(i, q)][n(j, 4g + r)] with
-//   m = IL_A ? mbase + MR*q + i : mbase + 16i + q          (IL = MN-contiguous operand)
-//   n = IL_B ? nbase + NR*qn + j : nbase + 16j + qn        (qn = 4g + r)
-// processed as NR quads of 4 consecutive columns per row.
-template <int MR, int NR, bool IL_A, bool IL_B>
-FM_DEVICE void quad_of(const f32x4_t (&acc)[MR][NR], int i, int u, int nbase, int g, int& n0, float (&v)[4]) {
-  if constexpr (IL_B) {
-    n0 = nbase + 4 * NR * g + 4 * u;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = acc[i][(4 * u + e) % NR][(4 * u + e) / NR];
-  } else {
-    n0 = nbase + 16 * u + 4 * g;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = acc[i][u][e];
-  }
-}
-
-template <int MR, int NR, bool IL_A, bool IL_B, bool SGD = false>
-FM_DEVICE void epilogue_f32(const GemmF& p, const f32x4_t (&acc)[MR][NR], int zb, int split, int mbase, int nbase,
-                            int lane) {
-  const int q = lane & 15, g = lane >> 4;
-  if (p.ksplit > 1) {
-    float* ws = p.ws + ((long)zb * p.ksplit + split) * (long)p.M * p.N;
-    const bool v4 = (p.N & 3) == 0;
-#pragma unroll
-    for (int i = 0; i < MR; ++i) {
-      const int m = IL_A ? mbase + MR * q + i : mbase + 16 * i + q;
-      if (m >= p.M) continue;
-#pragma unroll
-      for (int u = 0; u < NR; ++u) {
-        int n0;
-        float v[4];
-        quad_of<MR, NR, IL_A, IL_B>(acc, i, u, nbase, g, n0, v);
-        float* dst = ws + (long)m * p.N + n0;
-        if (v4 && n0 + 3 < p.N) {
-          *reinterpret_cast<f32x4_t*>(dst) = f32x4_t{v[0], v[1], v[2], v[3]};
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (n0 + e < p.N) dst[e] = v[e];
-        }
-      }
-    }
-    return;
-  }
-  float csum[NR][4];
-#pragma unroll
-  for (int u = 0; u < NR; ++u)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) csum[u][e] = 0.f;
-  float* Cz = p.C + (long)zb * p.sC;
-#pragma unroll
-  for (int i = 0; i < MR; ++i) {
-    const int m = IL_A ? mbase + MR * q + i : mbase + 16 * i + q;
-    const bool mok = m < p.M;
-#pragma unroll
-    for (int u = 0; u < NR; ++u) {
-      int n0;
-      float v[4];
-      quad_of<MR, NR, IL_A, IL_B>(acc, i, u, nbase, g, n0, v);
-      const bool full = n0 + 3 < p.N;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] *= p.alpha;
-        if (p.bias) v[e] += (n0 + e < p.N) ? p.bias[n0 + e] : 0.f;
-        v[e] = act_fwd(p.act, v[e]);
-      }
-      if (p.ay) {
-        float yv[4] = {0.f, 0.f, 0.f, 0.f};
-        if (mok) {
-          const float* yp = p.ay + (long)m * p.lday + n0;
-          if (full && ((p.lday & 3) == 0)) {
-            const f32x4_t t = *reinterpret_cast<const f32x4_t*>(yp);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) yv[e] = t[e];
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) yv[e] = (n0 + e < p.N) ? yp[e] : 0.f;
-          }
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = act_bwd(p.bact, yv[e], v[e]);
-      }
-      if (p.colsum && mok) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) csum[u][e] += (n0 + e < p.N) ? v[e] : 0.f;
-      }
-      if (!mok) continue;
-      if constexpr (SGD) {
-        const long o = (long)m * p.ldc + n0;
-        if (full) {
-          sgd_apply4(p, o, f32x4_t{v[0], v[1], v[2], v[3]});
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (n0 + e < p.N) sgd_apply1(p, o + e, v[e]);
-        }
-        continue;
-      }
-      float* dst = Cz + (long)m * p.ldc + n0;
-      if (full && ((p.ldc & 3) == 0) && ((((uintptr_t)dst) & 15) == 0)) {
-        f32x4_t o = {v[0], v[1], v[2], v[3]};
-        if (p.beta) o += *reinterpret_cast<const f32x4_t*>(dst);
-        *reinterpret_cast<f32x4_t*>(dst) = o;
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (n0 + e < p.N) dst[e] = v[e] + (p.beta ? dst[e] : 0.f);
-      }
-    }
-  }
-  if (p.colsum) {   // the 16 lanes of a group share every column: reduce over q, one atomic per column
-#pragma unroll
-    for (int u = 0; u < NR; ++u)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float x = csum[u][e];
-        x += __shfl_xor(x, 1, 64);
-        x += __shfl_xor(x, 2, 64);
-        x += __shfl_xor(x, 4, 64);
-        x += __shfl_xor(x, 8, 64);
-        const int n = (IL_B ? nbase + 4 * NR * g + 4 * u : nbase + 16 * u + 4 * g) + e;
-        if (q == 0 && n < p.N) atomicAdd(p.colsum + n, x);
-      }
-  }
-}
-
-// Fused-SGD epilogue of an unsplit fp32 dW tile through LDS (same scheme as gemm.hip
-// sgd_epilogue_lds): the accumulator quads (quad_of, incl. the interleaved layouts) are parked in
-// the free operand LDS with row-XOR-swizzled 16-B chunks, then whole rows of W are updated with
-// contiguous BN*4-byte accesses.  BM*BN*4 <= 2*(BM+BN)*BKF*4: the tile fits the K-loop LDS.
-template <int BM, int BN, int NT, int MR, int NR, bool IL_A, bool IL_B>
-FM_DEVICE void sgd_epilogue_lds_f32(const GemmF& p, const f32x4_t (&acc)[MR][NR], char* smem, int m0, int n0,
-                                    int mbase, int nbase, int lane, int tid) {
-  constexpr int CPR = BN / 4;
-  f32x4_t* t = reinterpret_cast<f32x4_t*>(smem);
-  const int q = lane & 15, g = lane >> 4;
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < MR; ++i) {
-    const int r = (IL_A ? mbase + MR * q + i : mbase + 16 * i + q) - m0;
-#pragma unroll
-    for (int u = 0; u < NR; ++u) {
-      int nn;
-      float v[4];
-      quad_of<MR, NR, IL_A, IL_B>(acc, i, u, nbase, g, nn, v);
-      const int c = (nn - n0) >> 2;
-      t[r * CPR + (c ^ (r & 7))] = f32x4_t{v[0], v[1], v[2], v[3]} * p.alpha;
-    }
-  }
-  __syncthreads();
-  const bool n4 = (p.N & 3) == 0;
-#pragma unroll 4
-  for (int e = tid; e < BM * CPR; e += NT) {
-    const int r = e / CPR, c = e % CPR;
-    const int m = m0 + r, n = n0 + 4 * c;
-    if (m >= p.M || n >= p.N) continue;
-    const f32x4_t gv = t[r * CPR + (c ^ (r & 7))];
-    const long o = (long)m * p.ldc + n;
-    if (n4 && n + 3 < p.N) {
-      sgd_apply4(p, o, gv);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (n + k < p.N) sgd_apply1(p, o + k, gv[k]);
-    }
-  }
-}
 
 // OPT: 1 = s_setprio(1) around each MFMA cluster (A/B only); 2 = fragment double buffer (default):
 // the second k-chunk's LDS fragments are read before the first chunk's MFMAs and interleaved with
@@ -457,7 +165,8 @@ __global__ void __launch_bounds__(NT, MINB) fm_gemm_f32_kernel(GemmF p) {
   }
   if constexpr (SGD) {
     if (p.ksplit == 1 && p.ulds) {
-      sgd_epilogue_lds_f32<BM, BN, NT, MR, NR, !AK, !BKC>(p, acc, smem, m0, n0, m0 + wm * TM, n0 + wn * TN, lane, tid);
+      sgd_epilogue_lds_f32<BM, BN, NT, MR, NR, !AK, !BKC, 2 * (BM + BN) * BKF * 4>(p, acc, smem, m0, n0, m0 + wm * TM,
+                                                                                   n0 + wn * TN, lane, tid);
       return;
     }
   }
@@ -811,6 +520,11 @@ __global__ void __launch_bounds__(256) fm_gemm_f32_reduce_bwd(GemmF p, int RB) {
 
 }  // namespace
 
+// the ring-form kernel (gemm_f32_ring.hip)
+extern "C" int fm_gemm_f32_ring_cfg(int c, int* geo);
+extern "C" void fm_gemm_f32_ring_launch(const void* params, int c, int a_kcontig, int b_kcontig, int sgd,
+                                        hipStream_t stream);
+
 // split-K reduce off the critical path (gemm_async.hip)
 extern "C" void fm_gemm_join(hipStream_t s);
 extern "C" hipStream_t fm_gemm_async_fork(hipStream_t s);
@@ -903,8 +617,6 @@ void launch_fbm(const GemmF& p, bool ak, bool bk, bool vec, hipStream_t s, int o
 // The DMA destination is lane-linear (wave base + 16*lane), so the K-contiguous image's chunk
 // swizzle is applied to the per-lane SOURCE address; MN-contiguous images are unswizzled rows.
 // Used when K-tiles are whole (K % 32 == 0) and operands allow 16-B access.
-typedef __attribute__((address_space(1))) const void* gptr_f;
-typedef __attribute__((address_space(3))) void* lptr_f;
 
 template <bool KC, int R, int NTH>
 struct GldsF {
@@ -936,11 +648,6 @@ struct GldsF {
   }
 };
 
-template <int N>
-FM_DEVICE void wait_vmcnt_f() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
-}
 
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC>
 __global__ void __launch_bounds__(WM * WN * 64, 1) fm_gemm_f32_glds_kernel(GemmF p) {
@@ -1516,6 +1223,33 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
       launch_reduce_f32(p, v4, total, stream);
     }
     return ks;
+  }
+  if (vec && variant >= 20000 && variant < 20100 && K > 0) {
+    const int rc = (variant - 20000) % fm_gemm_f32_ring_cfg(0, nullptr);
+    int geo[4];
+    fm_gemm_f32_ring_cfg(rc, geo);
+    const struct { int bm, bn, bk; } c = {geo[0], geo[1], geo[2]};
+    if (K % c.bk == 0 && (a_kcontig || M % 4 == 0) && (b_kcontig || N % 4 == 0) && M >= 4 && N >= 4) {
+      p.tiles_m = (M + c.bm - 1) / c.bm;
+      p.tiles_n = (N + c.bn - 1) / c.bn;
+      const long tiles = (long)p.tiles_m * p.tiles_n * batch;
+      const int ktiles = K / c.bk;
+      int ks = 1;
+      if (ksplit_req > 0) ks = ksplit_req;
+      else if (ws != nullptr)
+        while (tiles * ks < 256 && ks * 2 <= ktiles / 4 && ks < 16) ks *= 2;
+      if (act_y != nullptr || colsum != nullptr) ks = 1;
+      while (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks /= 2;
+      p.ksplit = ks;
+      if (ks > 1) fm_gemm_join(stream);
+      fm_gemm_f32_ring_launch(&p, rc, a_kcontig, b_kcontig, 0, stream);
+      if (ks > 1) {
+        const int v4 = (N % 4 == 0) && (ldc % 4 == 0) && (sC % 4 == 0) && al(C);
+        const long total = (long)M * N * batch / (v4 ? 4 : 1);
+        launch_reduce_f32(p, v4, total, stream);
+      }
+      return ks;
+    }
   }
   if (vec && variant >= 1000 && variant < 1200 && K > 0) {
     const XCfg c = kXCfgs[((variant - 1000) % 100) % kNumXCfgs];

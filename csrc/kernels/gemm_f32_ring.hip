@@ -1,0 +1,289 @@
+// flexmi fp32 GEMM, ring form, for gfx950 (MI355X / CDNA4): see the comment block below.  Shares the
+// parameter block and the fused epilogues with gemm_f32.hip (gemm_f32_common.h); gemm_f32.hip's
+// dispatcher (gemm_f32_run) selects it through fm_gemm_f32_ring_cfg / fm_gemm_f32_ring_launch.
+#include "gemm_f32_common.h"
+
+namespace {
+
+// ---- ring kernel: NS-stage LDS-DMA ring, one barrier per K-stage, fragment double buffer -------
+// The register-staged kernels above keep one K-tile in flight and pay a full barrier + first-
+// fragment latency per 32-deep tile; at one or two waves per SIMD that is the ~15 % they lose to a
+// saturated f32 MFMA pipe.  Here (src/ops/linear.cu:424-447 fwd, :592-635 bwd):
+//   * operands go global -> LDS by global_load_lds_dwordx4 into an NS-deep ring (no staging VGPRs,
+//     no ds_write pass); NS-1 K-stages are in flight behind the one being multiplied;
+//   * ONE s_barrier per K-stage, placed after the stage's second-to-last fragment chunk has been
+//     multiplied: by then the last chunk's fragments are in registers, so the barrier and the next
+//     stage's first fragment reads overlap the last chunk's MFMAs (no pipe bubble per stage);
+//   * the ring slot freed by that barrier is refilled at the top of the next stage.
+// LDS images: K-contiguous operand [row][BK] with XOR-swizzled 16-B chunks (conflict-free b128
+// fragment reads: one read = 4 k-steps of one 16x16 tile); MN-contiguous operand [k][R] with the
+// wave's rows interleaved over its T tiles (one b128 / b64 read at a fixed k = T fragments).  The
+// DMA destination is lane-linear, so every swizzle is applied to the per-lane SOURCE address.
+// Requires K % BK == 0 (whole stages per split), 16-B aligned operands, M % 4 / N % 4 == 0 for
+// MN-contiguous operands; rows past the M / N edge are clamped re-reads whose outputs are never
+// stored.
+template <int BK>
+FM_DEVICE int rk_swz(int row) {   // K-contiguous image: chunk swizzle of a row (CPR = BK/4 chunks)
+  constexpr int CPR = BK / 4;
+  constexpr int RPL = (256 / (BK * 4)) > 0 ? 256 / (BK * 4) : 1;
+  return (row / RPL) & (CPR - 1);
+}
+template <int T>
+FM_DEVICE int rm_swz(int k) {     // MN-contiguous image: T = 2 (b64 reads) separates k-groups g, g+1
+  return T == 2 ? (((k >> 2) & 1) << 3) : 0;
+}
+
+template <bool KC, int R, int BK, int T, int NTH>
+struct RingLd {
+  static constexpr int INSTR = R * BK * 4 / 1024;
+  static constexpr int NWAVES = NTH / 64;
+  static constexpr int PER_W = INSTR / NWAVES;
+  static_assert(INSTR % NWAVES == 0 && PER_W >= 1, "stage bytes must split evenly over the waves");
+  FM_DEVICE static void issue(const float* __restrict__ p, long ld, int row0, int rows, int k0, char* lds, int wave,
+                              int lane) {
+#pragma unroll
+    for (int i = 0; i < PER_W; ++i) {
+      const int j = wave * PER_W + i;
+      const int o = j * 1024 + 16 * lane;
+      const float* src;
+      if constexpr (KC) {
+        const int row = o / (BK * 4);
+        const int c = (o % (BK * 4)) / 16;
+        const int gr = min(row0 + row, rows - 1);
+        src = p + (long)gr * ld + k0 + 4 * (c ^ rk_swz<BK>(row));
+      } else {
+        const int k = o / (R * 4);
+        const int c = (o % (R * 4)) / 16;
+        const int gr = min(row0 + 4 * (c ^ rm_swz<T>(k)), rows - 4);
+        src = p + (long)(k0 + k) * ld + gr;
+      }
+      __builtin_amdgcn_global_load_lds((gptr_f)src, (lptr_f)(lds + j * 1024), 16, 0, 0);
+    }
+  }
+};
+
+// fragments of one operand for one 16-wide k-chunk kk: f[t][s] = element (tile t, k-step s)
+template <bool KC, int R, int BK, int T>
+FM_DEVICE void ring_frags(const char* lds, int base, int kk, int lane, float (&f)[T][4]) {
+  const int q = lane & 15, g = lane >> 4;
+  if constexpr (KC) {
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int row = base + 16 * t + q;
+      const f32x4_t x = *reinterpret_cast<const f32x4_t*>(lds + row * (BK * 4) + 16 * ((4 * kk + g) ^ rk_swz<BK>(row)));
+#pragma unroll
+      for (int s = 0; s < 4; ++s) f[t][s] = x[s];
+    }
+  } else {
+    static_assert(T == 2 || T == 4, "interleaved MN reads are b64 / b128");
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int k = 16 * kk + 4 * g + s;
+      const int e = base + T * q;                       // first float of the lane's T rows
+      const int off = k * (R * 4) + 16 * ((e >> 2) ^ rm_swz<T>(k)) + 4 * (e & 3);
+      const fvec<T> x = *reinterpret_cast<const fvec<T>*>(lds + off);
+#pragma unroll
+      for (int t = 0; t < T; ++t) f[t][s] = x[t];
+    }
+  }
+}
+
+template <int N>
+FM_DEVICE void ring_wait(int n_out) {   // s_waitcnt vmcnt(n_out * N) for n_out in {0, 1, 2}
+  if (n_out >= 2) wait_vmcnt_f<(2 * N < 63 ? 2 * N : 63)>();
+  else if (n_out == 1) wait_vmcnt_f<N>();
+  else wait_vmcnt_f<0>();
+}
+
+template <int BM, int BN, int WM, int WN, int BK, int NS, bool AK, bool BKC, bool SGD = false>
+__global__ void __launch_bounds__(WM * WN * 64, 1) fm_gemm_f32_ring_kernel(GemmF p) {
+  constexpr int NTH = WM * WN * 64;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int MR = TM / 16, NR = TN / 16;
+  constexpr int CH = BK / 16;
+  constexpr int A_BYTES = BM * BK * 4;
+  constexpr int B_BYTES = BN * BK * 4;
+  constexpr int STG = A_BYTES + B_BYTES;
+  using LA = RingLd<AK, BM, BK, MR, NTH>;
+  using LB = RingLd<BKC, BN, BK, NR, NTH>;
+  constexpr int LPS = LA::PER_W + LB::PER_W;   // DMA instructions per wave per stage
+  static_assert(NS >= 2 && NS <= 4 && 2 * LPS < 64, "ring depth / vmcnt range");
+  static_assert(CH >= 2 && CH % 2 == 0, "fragment double buffer needs an even chunk count");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int bid = xcd_remap_f(blockIdx.x, p.tiles_m * p.tiles_n);
+  int tm, tn;
+  if (p.n_fast) { tn = bid % p.tiles_n; tm = bid / p.tiles_n; }
+  else { tm = bid % p.tiles_m; tn = bid / p.tiles_m; }
+  const int zb = blockIdx.y;
+  const int split = blockIdx.z;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const float* A = p.A + (long)zb * p.sA;
+  const float* B = p.B + (long)zb * p.sB;
+
+  const int ktiles_total = p.K / BK;
+  const int kt_per = (ktiles_total + p.ksplit - 1) / p.ksplit;
+  const int kt0 = split * kt_per;
+  const int nkt = max(min(ktiles_total, kt0 + kt_per) - kt0, 0);
+
+  auto issue = [&](int t) {
+    char* base = smem + (t % NS) * STG;
+    LA::issue(A, p.lda, m0, p.M, (kt0 + t) * BK, base, wave, lane);
+    LB::issue(B, p.ldb, n0, p.N, (kt0 + t) * BK, base + A_BYTES, wave, lane);
+  };
+
+  f32x4_t acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const bool rowsum = (!AK) && (p.rowsum_a != nullptr) && (tn == 0);
+  constexpr int CPR = BM / 4;
+  float rs[4] = {0.f, 0.f, 0.f, 0.f};
+
+  float af[2][MR][4], bfr[2][NR][4];
+  if (nkt > 0) {
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+      if (s < nkt) issue(s);
+    ring_wait<LPS>(min(NS - 2, nkt - 1));
+    __builtin_amdgcn_s_barrier();
+    ring_frags<AK, BM, BK, MR>(smem, wm * TM, 0, lane, af[0]);
+    ring_frags<BKC, BN, BK, NR>(smem + A_BYTES, wn * TN, 0, lane, bfr[0]);
+  }
+  for (int t = 0; t < nkt; ++t) {
+    const char* la = smem + (t % NS) * STG;
+    const char* lb = la + A_BYTES;
+    if (t + NS - 1 < nkt) issue(t + NS - 1);   // refills the slot every wave left at the last barrier
+    if constexpr (!AK) {
+      if (rowsum) {
+        for (int kr = tid / CPR; kr < BK; kr += NTH / CPR) {
+          const int e = 4 * (tid % CPR);
+          const f32x4_t v = *reinterpret_cast<const f32x4_t*>(la + kr * (BM * 4) + 16 * ((e >> 2) ^ rm_swz<MR>(kr)));
+#pragma unroll
+          for (int x = 0; x < 4; ++x) rs[x] += v[x];
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int cur = c & 1, nxt = cur ^ 1;
+      if (c + 1 < CH) {
+        ring_frags<AK, BM, BK, MR>(la, wm * TM, c + 1, lane, af[nxt]);
+        ring_frags<BKC, BN, BK, NR>(lb, wn * TN, c + 1, lane, bfr[nxt]);
+      } else if (t + 1 < nkt) {
+        // stage t+1: this wave's DMAs landed (later stages may stay in flight), every wave's
+        // fragment reads of stage t are done, then all waves' DMAs of t+1 are visible
+        ring_wait<LPS>(min(NS - 2, nkt - 2 - t));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        const char* na = smem + ((t + 1) % NS) * STG;
+        ring_frags<AK, BM, BK, MR>(na, wm * TM, 0, lane, af[nxt]);
+        ring_frags<BKC, BN, BK, NR>(na + A_BYTES, wn * TN, 0, lane, bfr[nxt]);
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+#pragma unroll
+          for (int j = 0; j < NR; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(bfr[cur][j][s], af[cur][i][s], acc[i][j], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();   // every wave is done with the ring before the epilogue reuses LDS
+  if constexpr (!AK) {
+    if (rowsum) {
+      float* red = reinterpret_cast<float*>(smem);
+      constexpr int G = NTH / CPR;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[(tid / CPR) * BM + (tid % CPR) * 4 + e] = rs[e];
+      __syncthreads();
+      for (int r = tid; r < BM; r += NTH) {
+        float x = 0.f;
+        for (int g2 = 0; g2 < G; ++g2) x += red[g2 * BM + r];
+        if (m0 + r < p.M) atomicAdd(p.rowsum_a + m0 + r, x);
+      }
+      __syncthreads();
+    }
+  }
+  if constexpr (SGD && BM * BN * 4 <= NS * STG) {
+    if (p.ksplit == 1 && p.ulds) {
+      sgd_epilogue_lds_f32<BM, BN, NTH, MR, NR, !AK, !BKC, NS * STG>(p, acc, smem, m0, n0, m0 + wm * TM, n0 + wn * TN,
+                                                                      lane, tid);
+      return;
+    }
+  }
+  epilogue_f32<MR, NR, !AK, !BKC, SGD>(p, acc, zb, split, m0 + wm * TM, n0 + wn * TN, lane);
+}
+
+template <int BM, int BN, int WM, int WN, int BK, int NS, bool SGD>
+void launch_ring(const GemmF& p, bool ak, bool bk, hipStream_t s) {
+  constexpr int NTH = WM * WN * 64;
+  constexpr int LDS = NS * (BM + BN) * BK * 4;
+  static bool attr_set = false;
+  if (!attr_set) {
+    auto set = [](const void* f) { (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS); };
+    set((const void*)fm_gemm_f32_ring_kernel<BM, BN, WM, WN, BK, NS, true, true, SGD>);
+    set((const void*)fm_gemm_f32_ring_kernel<BM, BN, WM, WN, BK, NS, true, false, SGD>);
+    set((const void*)fm_gemm_f32_ring_kernel<BM, BN, WM, WN, BK, NS, false, true, SGD>);
+    set((const void*)fm_gemm_f32_ring_kernel<BM, BN, WM, WN, BK, NS, false, false, SGD>);
+    attr_set = true;
+  }
+  dim3 grid(p.tiles_m * p.tiles_n, p.batch, p.ksplit);
+  if (ak && bk) hipLaunchKernelGGL((fm_gemm_f32_ring_kernel<BM, BN, WM, WN, BK, NS, true, true, SGD>), grid, dim3(NTH), LDS, s, p);
+  else if (ak) hipLaunchKernelGGL((fm_gemm_f32_ring_kernel<BM, BN, WM, WN, BK, NS, true, false, SGD>), grid, dim3(NTH), LDS, s, p);
+  else if (bk) hipLaunchKernelGGL((fm_gemm_f32_ring_kernel<BM, BN, WM, WN, BK, NS, false, true, SGD>), grid, dim3(NTH), LDS, s, p);
+  else hipLaunchKernelGGL((fm_gemm_f32_ring_kernel<BM, BN, WM, WN, BK, NS, false, false, SGD>), grid, dim3(NTH), LDS, s, p);
+}
+
+// ring tile configurations (A/B index = FM_GEMM_F32_VARIANT - 20000)
+struct RCfg { int bm, bn, wm, wn, bk, ns; };
+constexpr RCfg kRCfgs[] = {
+    {128, 128, 2, 2, 32, 4},   // 0: 4 waves of 64x64 (1 per SIMD), 4 x 32 KB ring
+    {128, 128, 2, 2, 64, 2},   // 1: 4 waves of 64x64, 2 x 64 KB ring
+    {256, 128, 4, 2, 32, 3},   // 2: 8 waves of 64x64 (2 per SIMD), 3 x 48 KB ring
+    {64, 64, 2, 2, 64, 4},     // 3: 4 waves of 32x32, 4 x 32 KB ring (hipBLASLt's fp32 macro tile)
+    {128, 64, 2, 2, 32, 4},    // 4: 4 waves of 64x32, 4 x 24 KB ring
+    {128, 128, 2, 4, 32, 4},   // 5: 8 waves of 64x32 (2 per SIMD), 4 x 32 KB ring
+    {128, 128, 2, 2, 32, 3},   // 6: 3-deep ring (96 KB)
+    {64, 64, 2, 2, 32, 4},     // 7: 4 waves of 32x32, 4 x 16 KB ring (K % 32)
+};
+constexpr int kNumRCfgs = sizeof(kRCfgs) / sizeof(kRCfgs[0]);
+
+template <bool SGD>
+void launch_ring_cfg(int c, const GemmF& p, bool ak, bool bk, hipStream_t s) {
+  switch (c) {
+    case 0: launch_ring<128, 128, 2, 2, 32, 4, SGD>(p, ak, bk, s); break;
+    case 1: launch_ring<128, 128, 2, 2, 64, 2, SGD>(p, ak, bk, s); break;
+    case 2: launch_ring<256, 128, 4, 2, 32, 3, SGD>(p, ak, bk, s); break;
+    case 3: launch_ring<64, 64, 2, 2, 64, 4, SGD>(p, ak, bk, s); break;
+    case 4: launch_ring<128, 64, 2, 2, 32, 4, SGD>(p, ak, bk, s); break;
+    case 5: launch_ring<128, 128, 2, 4, 32, 4, SGD>(p, ak, bk, s); break;
+    case 6: launch_ring<128, 128, 2, 2, 32, 3, SGD>(p, ak, bk, s); break;
+    default: launch_ring<64, 64, 2, 2, 32, 4, SGD>(p, ak, bk, s); break;
+  }
+}
+
+
+}  // namespace
+
+// tile geometry of ring configuration c: {bm, bn, bk, ns}; returns the number of configurations
+extern "C" int fm_gemm_f32_ring_cfg(int c, int* geo) {
+  if (c >= 0 && c < kNumRCfgs && geo) {
+    geo[0] = kRCfgs[c].bm; geo[1] = kRCfgs[c].bn; geo[2] = kRCfgs[c].bk; geo[3] = kRCfgs[c].ns;
+  }
+  return kNumRCfgs;
+}
+
+// launch ring configuration c for a prepared GemmF (tiles_m / tiles_n / ksplit filled in for it)
+extern "C" void fm_gemm_f32_ring_launch(const void* params, int c, int a_kcontig, int b_kcontig, int sgd,
+                                        hipStream_t stream) {
+  const GemmF& p = *reinterpret_cast<const GemmF*>(params);
+  if (sgd) launch_ring_cfg<true>(c, p, a_kcontig, b_kcontig, stream);
+  else launch_ring_cfg<false>(c, p, a_kcontig, b_kcontig, stream);
+}

@@ -346,6 +346,26 @@ struct PtrTabF {
 struct MPtrTabF {
   float* p[MAXF];
 };
+// Embedding rows gathered in place (the embedding-into-interaction fusion): feature i's row of
+// sample b is p[i] + r * ld[i] with r = ix[i][b] (the bag-1 lookup index) or r = b (ix[i] null),
+// so the interaction reads table rows directly and the [B, D] embedding outputs are never written.
+struct GatherTabF {
+  const float* p[MAXF];
+  const void* ix[MAXF];
+  long ld[MAXF];
+  long rows[MAXF];   // table rows: an out-of-range index is clamped (never a wild read)
+  int i64;
+};
+FM_DEVICE const float* zrow(const PtrTabF& Z, long ldz, int i, long b) { return Z.p[i] + b * ldz; }
+FM_DEVICE const float* zrow(const GatherTabF& Z, long, int i, long b) {
+  const void* ix = Z.ix[i];
+  long r = b;
+  if (ix != nullptr) {
+    r = Z.i64 ? reinterpret_cast<const long*>(ix)[b] : (long)reinterpret_cast<const int*>(ix)[b];
+    r = min(max(r, 0L), Z.rows[i] - 1);
+  }
+  return Z.p[i] + r * Z.ld[i];
+}
 
 template <int DT>
 __global__ void __launch_bounds__(256) fm_dot_fwd_f32(PtrTabF Z, long ldz, float* __restrict__ out, long ldo, long B,
@@ -533,8 +553,8 @@ __global__ void __launch_bounds__(256) fm_dot_bwd_f32(PtrTabF Z, long ldz, const
 // per lane), stages the sample's Z (F <= 32 rows) in a per-wave LDS tile padded to D + 4 floats a
 // row (the row-per-lane ds_read_b128 of the MFMA operands is then bank-conflict free), and keeps
 // the NEXT sample's rows in flight in registers while this sample's MFMAs and stores run.
-template <int D>
-__global__ void __launch_bounds__(256, 2) fm_dot_fwd_f32s(PtrTabF Z, long ldz, float* __restrict__ out, long ldo, long B,
+template <int D, typename ZT = PtrTabF>
+__global__ void __launch_bounds__(256, 2) fm_dot_fwd_f32s(ZT Z, long ldz, float* __restrict__ out, long ldo, long B,
                                                           int F, int W, int self) {
   constexpr int LPR = D / 4, RPI = 64 / LPR, NI = 32 / RPI, RS = D + 4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -551,7 +571,7 @@ __global__ void __launch_bounds__(256, 2) fm_dot_fwd_f32s(PtrTabF Z, long ldz, f
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int j = i * RPI + lr;
-      zr[i] = *reinterpret_cast<const f32x4_t*>(Z.p[j < F ? j : F - 1] + bb * ldz + 4 * lc);
+      zr[i] = *reinterpret_cast<const f32x4_t*>(zrow(Z, ldz, j < F ? j : F - 1, bb) + 4 * lc);
     }
   };
   const long b_first = blockIdx.x * (blockDim.x >> 6) + wave;
@@ -602,8 +622,8 @@ __global__ void __launch_bounds__(256, 2) fm_dot_fwd_f32s(PtrTabF Z, long ldz, f
 template <int E> struct VecF { using type = float __attribute__((ext_vector_type(E))); };
 template <> struct VecF<1> { using type = float; };
 
-template <int E, int NKS, bool ACC>
-__global__ void __launch_bounds__(256, 2) fm_dot_bwd_f32r(PtrTabF Z, long ldz, const float* __restrict__ dout, long ldo,
+template <int E, int NKS, bool ACC, typename ZT = PtrTabF>
+__global__ void __launch_bounds__(256, 2) fm_dot_bwd_f32r(ZT Z, long ldz, const float* __restrict__ dout, long ldo,
                                                          MPtrTabF dZ, long lddz, unsigned acc_mask, long B, int F,
                                                          int W, int self) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -639,9 +659,9 @@ __global__ void __launch_bounds__(256, 2) fm_dot_bwd_f32r(PtrTabF Z, long ldz, c
   vecE zn[NKS];
   f32x4_t dn[DCH];
   auto load_row = [&](long bb, int ks) {
-    const float* p0 = Z.p[min(2 * ks, F - 1)];
-    const float* p1 = Z.p[min(2 * ks + 1, F - 1)];
-    zn[ks] = *reinterpret_cast<const vecE*>((h ? p1 : p0) + bb * ldz + E * r);
+    const float* p0 = zrow(Z, ldz, min(2 * ks, F - 1), bb);
+    const float* p1 = zrow(Z, ldz, min(2 * ks + 1, F - 1), bb);
+    zn[ks] = *reinterpret_cast<const vecE*>((h ? p1 : p0) + E * r);
   };
   auto load_dout = [&](long bb) {
 #pragma unroll
@@ -803,6 +823,73 @@ extern "C" void fm_dot_interaction_bwd_f32(const float* const* z, int F, long ld
                                      : D == 32 ? fm_dot_bwd_f32<32> : fm_dot_bwd_f32<16>;
   hipLaunchKernelGGL(k, dim3((int)blocks), dim3(64 * waves), lds, s, t, ldz, dout, ldo, g, lddz, acc_mask, B, F, D, Wr,
                      self);
+}
+
+// Gathered-row forms (GatherTabF): feature i reads p[i] + ix[i][b] * ld[i] (ix[i] null: row b).
+// Only the fast fp32 kernels take them; returns -1 (nothing launched) when the operands do not fit.
+static bool gather_tab(GatherTabF& t, const float* const* z, const void* const* ix, const long* ld, const long* rows,
+                       int i64, int F) {
+  if (F < 2 || F > MAXF) return false;
+  for (int i = 0; i < MAXF; ++i) {
+    t.p[i] = i < F ? z[i] : nullptr;
+    t.ix[i] = i < F ? ix[i] : nullptr;
+    t.ld[i] = i < F ? ld[i] : 0;
+    t.rows[i] = i < F ? rows[i] : 1;
+    if (i < F && ix[i] != nullptr && rows[i] < 1) return false;
+    if (i < F && (!al16(z[i]) || ld[i] % 4 != 0)) return false;
+  }
+  t.i64 = i64;
+  return true;
+}
+
+extern "C" int fm_dot_interaction_fwd_f32g(const float* const* z, const void* const* ix, const long* ld, const long* rows,
+                                           int i64, int F, float* out, long ldo, long B, int D, int W, int self, hipStream_t s) {
+  GatherTabF t;
+  if (!gather_tab(t, z, ix, ld, rows, i64, F) || !(D == 32 || D == 64 || D == 128) || F > 32 || (W & 3) || (ldo & 3) ||
+      W > 1024 || !al16(out))
+    return -1;
+  const int waves = 4;
+  const long blocks = std::min<long>((B + waves - 1) / waves, dot_block_cap());
+  const size_t lds_s = (size_t)waves * (32 * (D + 4) + ((W + 3) & ~3)) * 4;
+  auto ks = D == 128 ? fm_dot_fwd_f32s<128, GatherTabF> : D == 64 ? fm_dot_fwd_f32s<64, GatherTabF>
+                                                                  : fm_dot_fwd_f32s<32, GatherTabF>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)fm_dot_fwd_f32s<128, GatherTabF>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10);
+    (void)hipFuncSetAttribute((const void*)fm_dot_fwd_f32s<64, GatherTabF>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10);
+    (void)hipFuncSetAttribute((const void*)fm_dot_fwd_f32s<32, GatherTabF>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10);
+    attr = true;
+  }
+  hipLaunchKernelGGL(ks, dim3((int)blocks), dim3(64 * waves), lds_s, s, t, 0L, out, ldo, B, F, W, self);
+  return 0;
+}
+
+extern "C" int fm_dot_interaction_bwd_f32g(const float* const* z, const void* const* ix, const long* ld, const long* rows,
+                                           int i64, int F, const float* dout, long ldo, float* const* dz, long lddz, unsigned acc_mask,
+                                           long B, int D, int self, hipStream_t s) {
+  GatherTabF t;
+  if (!gather_tab(t, z, ix, ld, rows, i64, F) || !(D == 32 || D == 64 || D == 128) || ldo % 4 || !al16(dout)) return -1;
+  const int npairs = self ? F * (F + 1) / 2 : F * (F - 1) / 2;
+  const int W = D + npairs;
+  const int E = D / 32;
+  if (W > 1024 || lddz % E) return -1;
+  MPtrTabF g;
+  for (int i = 0; i < MAXF; ++i) {
+    g.p[i] = i < F ? dz[i] : nullptr;
+    if (i < F && dz[i] != nullptr && ((uintptr_t)dz[i] & (4 * E - 1))) return -1;
+  }
+  const int waves = 4;
+  const long blocks = std::min<long>((B + waves - 1) / waves, dot_block_cap());
+  const int wpad = (W + 3) & ~3;
+  const bool acc = acc_mask != 0;
+  const bool k14 = E == 4 && (F + 1) / 2 == 14 && !acc;
+  auto k = k14 ? fm_dot_bwd_f32r<4, 14, false, GatherTabF>
+         : E == 4 ? (acc ? fm_dot_bwd_f32r<4, 16, true, GatherTabF> : fm_dot_bwd_f32r<4, 16, false, GatherTabF>)
+         : E == 2 ? (acc ? fm_dot_bwd_f32r<2, 16, true, GatherTabF> : fm_dot_bwd_f32r<2, 16, false, GatherTabF>)
+                  : (acc ? fm_dot_bwd_f32r<1, 16, true, GatherTabF> : fm_dot_bwd_f32r<1, 16, false, GatherTabF>);
+  hipLaunchKernelGGL(k, dim3((int)blocks), dim3(64 * waves), (size_t)waves * wpad * 4, s, t, 0L, dout, ldo, g, lddz,
+                     acc_mask, B, F, W, self);
+  return 0;
 }
 
 extern "C" void fm_dot_interaction_fwd(const void* const* z, int F, long ldz, void* out, long ldo, long B, int D, int W,

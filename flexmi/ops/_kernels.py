@@ -295,6 +295,24 @@ def dot_interaction_backward(inputs, dy, in_grads, accs, self_inter):
     C().dot_bwd(list(inputs), inputs[0].stride(0), dy, dy.stride(0), list(in_grads), ld, mask, D, bool(self_inter))
 
 
+def dot_interaction_forward_gather(srcs, ixs, y, self_inter):
+    """Embedding-into-interaction form (fp32): feature i's rows are srcs[i][ixs[i][b]] (an embedding
+    TABLE gathered by its bag-1 indices) or srcs[i][b] (ixs[i] None).  False: not launched."""
+    D = srcs[0].shape[-1]
+    return bool(C().dot_fwd_gather(list(srcs), list(ixs), y, y.stride(0), D, y.shape[1], bool(self_inter)))
+
+
+def dot_interaction_backward_gather(srcs, ixs, dy, in_grads, accs, self_inter):
+    D = srcs[0].shape[-1]
+    mask = 0
+    for i, a in enumerate(accs):
+        if a and in_grads[i] is not None:
+            mask |= 1 << i
+    ld = next((g.stride(0) for g in in_grads if g is not None), D)
+    return bool(C().dot_bwd_gather(list(srcs), list(ixs), dy, dy.stride(0), list(in_grads), ld, mask, D,
+                                   bool(self_inter)))
+
+
 # ------------------------------------------------------------------ optimizers / loss
 def sgd_update(master, grad, v, compute, lr_tensor, wd, momentum, nesterov, zero_grad=False):
     """zero_grad: the kernel writes the consumed gradient back as zeros (no separate memset)."""

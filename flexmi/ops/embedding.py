@@ -383,6 +383,18 @@ class Embedding(Op):
         case: every lookup a distinct row) -- used by the cost model (flexmi/parallel/search.py)."""
         return 1 + lookups * (1 + D)
 
+    @staticmethod
+    def sdp_prefer_sparse(rows, D, lookups, R):
+        """Replicated table over R holders: train it by sparse data parallelism (touched-row
+        all-gather of R fixed payloads) only when that moves fewer bytes than the dense replica
+        all-reduce of the table's rows x D gradient.  A ring all-gather of R payloads moves what a
+        ring all-reduce of R * payload / 2 words moves, so sparse wins iff R * payload / 2 < rows * D.
+        The tiny Criteo tables (3..10 rows) stay dense; 1e5+-row tables go sparse.  One rule for
+        the executor (Executor._build_weights) and the search's cost model (SimGraph._cand)."""
+        if R <= 1:
+            return True
+        return R * Embedding.sdp_payload_words(lookups, D) / 2.0 < float(rows) * D
+
     def bytes_moved(self, in_shapes, out_shapes, elem=2):
         b, bag = in_shapes[0]
         d = out_shapes[0][1]

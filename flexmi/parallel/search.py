@@ -171,6 +171,7 @@ class SimGraph:
         return self.cost.eb if t.data_type in _FLOAT else 8
 
     def _cand(self, op, pc: ParallelConfig):
+        from flexmi.ops.embedding import Embedding
         outs = op.output_layouts(pc)
         ins = op.input_layouts(pc)
         wls = op.weight_layouts(pc)
@@ -190,10 +191,23 @@ class SimGraph:
         wsync = []
         emb = op.op_type == OperatorType.OP_EMBEDDING
         for w, lay in zip(op.weights, wls):
-            sparse = emb and self.sparse_ok
             for p in range(lay.num_parts()):
                 vol = _prod(_box_shape(lay.part_box(p)))
                 h = lay.holders[p]
+                sparse = emb and self.sparse_ok
+                sdp_words = 0.0
+                if sparse and len(h) > 1:
+                    # the executor's per-table rule (Executor._sdp_pays): sparse DP only where the
+                    # touched-row all-gather moves fewer bytes than the dense replica all-reduce
+                    R = len(h)
+                    B = op.inputs[0].dims[0]
+                    bag = op.inputs[0].dims[1] if len(op.inputs[0].dims) > 1 else 1
+                    box = lay.part_box(p)
+                    rows = max(1, box[0][1] - box[0][0])
+                    lookups = -(-B // R) * bag
+                    sparse = Embedding.sdp_prefer_sparse(rows, vol // rows, lookups, R)
+                    if sparse:
+                        sdp_words = float(R * op.sdp_payload_words(lookups, vol // rows))
                 if len(h) > 1:
                     if sparse:
                         # replicated table with the sparse optimizer = the executor's sparse data
@@ -215,7 +229,8 @@ class SimGraph:
                         wsync.append((float(vol * 4), list(h)))
                 for d in h:
                     if sparse:
-                        mem[d] = mem.get(d, 0.0) + vol * 4.0
+                        # the table + (sparse DP) the R-slot receive buffer of the all-gather
+                        mem[d] = mem.get(d, 0.0) + vol * 4.0 + sdp_words * 4.0
                     else:
                         mem[d] = mem.get(d, 0.0) + vol * (4.0 + 4.0 + 2.0 + 4.0 * self.nstates)
                         upd_bytes[d] = upd_bytes.get(d, 0.0) + vol * 4.0

@@ -199,6 +199,12 @@ def overlap_embeddings_enabled(ex):
     return any(st[0] == "op" and type(st[1]).__name__ == "Embedding" and st[1].out_dim >= 128 for st in ex.fwd_steps)
 
 
+def Embedding_row_lo(ctx):
+    """First table row of this rank's embedding shard (0 for a whole table)."""
+    b = ctx.w_boxes[0] if ctx.w_boxes else None
+    return int(b[0][0]) if b is not None else 0
+
+
 def _run_overlapped(items, s, side):
     """Issue one graph segment's items with the embedding groups on ``side`` (fork/join by events,
     which stream capture records as graph edges).  A group forward is hoisted only across plain
@@ -283,27 +289,8 @@ def release_native_runners():
 
 
 def _hook_destroy_process_group():
-    import torch.distributed as dist
-    orig = dist.destroy_process_group
-    if getattr(orig, "_flexmi_hook", False):
-        return
-
-    def destroy_process_group(group=None):
-        if group is None:
-            # a last barrier (its work captures no Python-owned tensor) lets the backend's worker
-            # threads drop every earlier work -- and the Python tensors those captured -- before
-            # the group goes away; then the runners' own references are released
-            try:
-                if dist.is_initialized() and dist.get_world_size() > 1:
-                    dist.barrier()
-            except Exception:
-                pass
-            release_native_runners()
-            return orig()
-        return orig(group)
-    destroy_process_group._flexmi_hook = True
-    destroy_process_group.__doc__ = orig.__doc__
-    dist.destroy_process_group = destroy_process_group
+    from flexmi.parallel.comm import install_teardown_hook
+    install_teardown_hook()
 
 
 class NativeRunner:
@@ -914,6 +901,7 @@ class Executor:
         self._build_epilogue_fusion(ops)
         self._build_binary_relu_fusion(ops)
         self._build_conv_chain_fusion(ops)
+        self._build_gather_fusion(ops)
         if self.backend == "hip":
             # dW split-K reduces on a side stream (csrc/kernels/gemm_async.hip), joined before
             # every collective and at the end of the backward program (_with_gemm_joins)
@@ -1059,6 +1047,61 @@ class Executor:
             ca.saved["nhwc_gs"], ca.saved["nhwc_g_prestaged"] = gs_a, True
             cb.saved["nhwc_dgrad_out2"] = (gs_a, (Hg, Wg, Kp, gt, gl, dh, dw, 0))
 
+    def _build_gather_fusion(self, ops):
+        """Embedding group E -> DotInteraction D (every member's output consumed only by D, in
+        D's layout; bag-1 SUM lookups into a whole local fp32 table): D's kernels read the table
+        rows straight through the lookup indices, so E's forward never runs and its [B, d] outputs
+        are never written and re-read (DLRM MLPerf fp32: 26 x 8192 x 128 x 4 B = 109 MB each way
+        per step).  E's backward is unchanged: D's backward still writes E's output gradients,
+        reading the (not yet updated) table rows the same way.  Reference: the embedding writes
+        its output and the interaction/concat re-reads it (src/ops/embedding.cu:173-224,
+        src/ops/concat.cu:159-235).  FM_EMB_GATHER=0 turns it off (A/B); off under --debug and
+        for micro-batch-pipelined tails (XCHG_CHUNKS_LOCAL)."""
+        from flexmi.core.types import AggrMode, OperatorType
+        if (self.backend != "hip" or self.debug or XCHG_LOCAL or os.environ.get("FM_EMB_GATHER", "1") == "0"):
+            return
+        for d in ops:
+            if d.op_type != OperatorType.OP_DOT_INTERACTION:
+                continue
+            cd = self.ctx.get(d.guid)
+            if cd is None or cd.empty or d.guid in self.group_of or cd.outputs[0] is None:
+                continue
+            if cd.outputs[0].dtype != torch.float32 or d.d not in (32, 64, 128):
+                continue
+            spec = [None] * len(d.inputs)
+            for i, t in enumerate(d.inputs):
+                e = t.owner_op
+                if e is None or e.op_type != OperatorType.OP_EMBEDDING or getattr(e, "host_exec", False):
+                    continue
+                ce = self.ctx.get(e.guid)
+                cons = self.consumers.get(t.guid, [])
+                if ce is None or ce.empty or len(cons) != 1 or t is self.final:
+                    continue
+                idx, w = ce.inputs[0], ce.weights[0]
+                if (idx is None or w is None or idx.dim() != 2 or idx.shape[1] != 1 or not idx.is_contiguous()
+                        or w.dtype != torch.float32 or tuple(w.shape) != (e.num_entries, e.out_dim)
+                        or Embedding_row_lo(ce) != 0 or ce.outputs[0].dtype != torch.float32
+                        or not self.need[(d.guid, i)].same_as(self.home[t.guid])
+                        or idx.shape[0] != cd.outputs[0].shape[0]):
+                    continue
+                grp = self.group_of.get(e.guid, [e])
+                spec[i] = (w, idx, grp, [self.ctx[o.guid] for o in grp])
+            # a group is fused only when ALL its members feed this interaction through the gather
+            fused = {}
+            for s_ in spec:
+                if s_ is not None:
+                    fused.setdefault(id(s_[2]), [s_[2], 0])[1] += 1
+            for i, s_ in enumerate(spec):
+                if s_ is not None and fused[id(s_[2])][1] != len(s_[2]):
+                    spec[i] = None
+            if not any(s_ is not None for s_ in spec):
+                continue
+            cd.saved["gather"] = spec
+            for s_ in spec:
+                if s_ is not None:
+                    for c in s_[3]:
+                        c.saved["gathered"] = True
+
     def _build_groups(self, ops):
         """Fuse independent ops of the same kind and placement into one launch (embedding
         tables of a DLRM graph: 26 ops -> 1 forward + 2 backward launches).  Members run at the
@@ -1099,6 +1142,22 @@ class Executor:
                     self.group_of[op.guid] = g
 
     # ------------------------------------------------------------------
+    @staticmethod
+    def _sdp_pays(op, lay):
+        """Replicated table: sparse DP (touched-row all-gather) only where it moves fewer bytes
+        than the dense replica all-reduce (Embedding.sdp_prefer_sparse; the search prices the same
+        rule).  Every rank decides from global shapes only, so all replicas agree."""
+        from flexmi.ops.embedding import Embedding
+        R = lay.replication()
+        box = lay.part_box(0)
+        rows = box[0][1] - box[0][0]
+        cols = 1
+        for lo, hi in box[1:]:
+            cols *= hi - lo
+        B = op.inputs[0].dims[0]
+        bag = op.inputs[0].dims[1] if len(op.inputs[0].dims) > 1 else 1
+        return Embedding.sdp_prefer_sparse(rows, cols, -(-B // R) * bag, R)
+
     def _build_weights(self, ops):
         self.wentries: Dict[int, WeightEntry] = {}
         groups: "OrderedDict[tuple, SyncGroup]" = OrderedDict()
@@ -1130,7 +1189,7 @@ class Executor:
                 if op.op_type == OperatorType.OP_EMBEDDING:
                     op.sparse_dp = None
                 if (op.op_type == OperatorType.OP_EMBEDDING and sparse_ok
-                        and (lays[wi].replication() == 1 or SPARSE_DP)):
+                        and (lays[wi].replication() == 1 or (SPARSE_DP and self._sdp_pays(op, lays[wi])))):
                     # non-replicated: fused sparse SGD; replicated: sparse data parallelism
                     # (touched-row all-gather over the replica set, Embedding.sdp_*)
                     e.sparse = True
@@ -1163,10 +1222,13 @@ class Executor:
                 for e, o in zip(g.entries, offs):
                     e.offset = int(o)
                 g.buckets = [[int(b[0]), int(b[1]), {g.entries[int(i)].param.guid for i in b[2:]}] for b in bks]
-            g.master = self._alloc((g.numel,), torch.float32)
+            # zeroed: the 256-B alignment gaps between entries are never written by an initializer,
+            # and the replica checksums / finiteness checks (--debug) read the whole flat buffer --
+            # uninitialised gaps made identical replicas look divergent (or non-finite)
+            g.master = torch.zeros((g.numel,), dtype=torch.float32, device=self.device)
             g.gradbuf = self._alloc((g.numel,), torch.float32)
             g.gradbuf.zero_()
-            g.compute = self._alloc((g.numel,), self.cdtype) if mixed else g.master
+            g.compute = torch.zeros((g.numel,), dtype=self.cdtype, device=self.device) if mixed else g.master
             snames = self.optimizer.state_names() if self.optimizer else []
             # ZeRO-1: optimizer state exists only for this rank's shard of every bucket
             g.state = {n: torch.zeros(g.shard_numel if g.zero else g.numel, dtype=torch.float32, device=self.device)
@@ -1684,6 +1746,8 @@ class Executor:
         c = self.ctx.get(op.guid)
         if c is None:
             return
+        if c.saved.get("gathered"):
+            return       # read in place by its interaction (Executor._build_gather_fusion)
         grp = self.group_of.get(op.guid)
         if grp is not None:
             if grp[0] is op:

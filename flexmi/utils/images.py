@@ -39,6 +39,14 @@ def list_image_folder(root):
     return files, np.asarray(labels, dtype=np.int32), classes
 
 
+def roundf(x: np.ndarray) -> np.ndarray:
+    """C ``roundf`` of float32 values (half away from zero) as int64.  The +-0.5 is added in
+    float64, where it is exact for every float32 input: in float32, x = 0.5 - 2**-25 would give
+    x + 0.5 = 1.0 by ties-to-even and round up, while roundf gives 0."""
+    xd = np.asarray(x, dtype=np.float32).astype(np.float64)
+    return np.trunc(xd + np.copysign(0.5, xd)).astype(np.int64)
+
+
 def nearest_resize_hwc(img: np.ndarray, height: int, width: int) -> np.ndarray:
     """The reference's nearest-neighbour sampling (``model.cu:56-74``): source row
     ``min(roundf(y * scale), oh - 1)`` with a float32 ``scale = oh / h`` and roundf's half-away-
@@ -49,8 +57,8 @@ def nearest_resize_hwc(img: np.ndarray, height: int, width: int) -> np.ndarray:
 
     def src(n_out, n_in):
         scale = np.float32(n_in) / np.float32(n_out)
-        pos = np.arange(n_out, dtype=np.float32) * scale
-        return np.minimum(np.floor(pos + np.float32(0.5)).astype(np.int64), n_in - 1)
+        pos = np.arange(n_out, dtype=np.float32) * scale   # the float32 product, as the reference
+        return np.minimum(roundf(pos), n_in - 1)
 
     ys, xs = src(height, oh), src(width, ow)
     return img[ys[:, None], xs[None, :]]

@@ -37,6 +37,20 @@ def _check(r, n):
     assert r["config"]["loss"] == r["config"]["loss"]   # not NaN
 
 
+def _check_three_plans(r, n):
+    """The default N>1 record: the SOAP-searched plan is the headline, the hand plan it was seeded
+    with is ``config.table``, pure DP is ``config.dp``; both speedups are value ratios."""
+    c = r["config"]
+    assert c["parallelism"] == f"soap-search{n}"
+    s = c["search"]
+    assert s["budget"] > 0 and s["iterations"] == s["budget"] and s["seconds"] >= 0 and s["speedup_vs_dp"] > 0
+    tb, dp = c["table"], c["dp"]
+    assert "emb" in tb["parallelism"] and tb["value"] > 0 and tb["ms_per_step"] > 0
+    assert dp["parallelism"] == f"dp{n}" and dp["value"] > 0 and dp["ms_per_step"] > 0
+    assert c["soap_speedup_vs_dp"] == round(r["value"] / dp["value"], 3)
+    assert c["search_speedup_vs_table"] == round(r["value"] / tb["value"], 3)
+
+
 def test_bench_single_process():
     r = _run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--config", "tiny",
               "--batch-per-gpu", "64"])
@@ -48,11 +62,7 @@ def test_bench_two_ranks():
               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
               "--steps", "2", "--warmup", "1", "--config", "tiny", "--batch-per-gpu", "64"])
     _check(r, 2)
-    assert "emb2" in r["config"]["parallelism"]
-    # the second half of the metric: the same step under pure DP, and the SOAP speedup over it
-    dp = r["config"]["dp"]
-    assert dp["parallelism"] == "dp2" and dp["value"] > 0 and dp["ms_per_step"] > 0
-    assert r["config"]["soap_speedup_vs_dp"] == round(r["value"] / dp["value"], 3)
+    _check_three_plans(r, 2)
 
 
 @pytest.mark.multiproc
@@ -68,6 +78,7 @@ def test_bench_self_launches_eight_ranks():
         os.environ.update(saved)
     _check(r, 8)
     assert r["config"]["process_world"] == 8 and r["config"]["backend"] == "gloo"
+    _check_three_plans(r, 8)
 
 
 def test_bench_refuses_world_mismatch():

@@ -92,13 +92,8 @@ def _worker(rank, world, port, *args):
         traceback.print_exc()
         rc = 1
     finally:
-        dist.destroy_process_group()
-    # leave without interpreter finalisation: the rank has torn its process group down, and
-    # static destructors of the backends' thread pools racing a peer's teardown must not turn a
-    # finished rank into a SIGABRT (VERDICT r2 "What's weak" #6)
-    sys.stdout.flush()
-    sys.stderr.flush()
-    os._exit(rc)
+        dist.destroy_process_group()   # ordered teardown: normal interpreter exit afterwards
+    sys.exit(rc)
 
 
 def _launch(world, strategy, opt, ckpt, mode):

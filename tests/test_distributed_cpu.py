@@ -127,13 +127,17 @@ def _build(case, world):
                 strat = load_strategies_from_file(ref)
     elif case.startswith("dlrm"):
         dcfg = DLRMConfig.preset("tiny")
-        dcfg.arch_interaction_op = "dot" if case in ("dlrm_dot", "dlrm_dp") else "cat"
+        dcfg.arch_interaction_op = "dot" if case in ("dlrm_dot", "dlrm_dp", "dlrm_dpmix") else "cat"
+        if case == "dlrm_dpmix":
+            # one 3-row table: its dense replica all-reduce (48 words) is cheaper than the
+            # touched-row all-gather, so it trains densely while the others go sparse
+            dcfg.embedding_size = [100, 3, 200, 30]
         d, s, p = build_dlrm(m, dcfg)
         loss = LossType.LOSS_BINARY_CROSSENTROPY
         inputs["dense"] = (d, (B, 13), "f")
         for i, (t, r) in enumerate(zip(s, dcfg.embedding_size)):
             inputs[f"sparse{i}"] = (t, (B, 1), ("i", r))
-        if world > 1 and not dp_small and case != "dlrm_dp":   # dlrm_dp: pure data parallelism
+        if world > 1 and not dp_small and case not in ("dlrm_dp", "dlrm_dpmix"):   # pure data parallelism
             strat = dlrm_strategy(m, world)
             if case == "dlrm_search":
                 # strategy chosen by the MCMC search over the MI355X simulator (same seed on
@@ -257,16 +261,23 @@ def _run(case, world, rank, steps, out_path):
         assert zg and all(len(g.buckets) > 1 for g in zg), "ZeRO groups / buckets missing"
         for g in zg:   # optimizer state really is sharded
             assert all(t.numel() * len(g.holders) == g.numel for t in g.state.values())
-    if case in ("dlrm_dp", "dlrm_cat_dpsmall") and world > 1:
-        # sparse data parallelism: replicated tables train by touched-row all-gather, no
-        # table-sized gradient buffer and no table in a dense all-reduce group
+    if case in ("dlrm_dp", "dlrm_cat_dpsmall", "dlrm_dpmix") and world > 1:
+        # sparse data parallelism: replicated tables train by touched-row all-gather (no
+        # table-sized gradient, no dense all-reduce) where that moves fewer bytes than the dense
+        # replica all-reduce (Embedding.sdp_prefer_sparse); the others stay in a dense group
         from flexmi.core.types import OperatorType
         embs = [e for e in ex.wentries.values() if e.op.op_type == OperatorType.OP_EMBEDDING]
-        assert embs and all(e.sparse and e.group is None and e.grad is None for e in embs)
-        assert all(e.op.sparse_dp == tuple(range(world)) for e in embs)
-        assert not [e for g in ex.groups for e in g.entries if e.op.op_type == OperatorType.OP_EMBEDDING]
+        sp = [e for e in embs if ex._sdp_pays(e.op, e.layout)]
+        dn = [e for e in embs if e not in sp]
+        assert sp and all(e.sparse and e.group is None and e.grad is None for e in sp)
+        assert all(e.op.sparse_dp == tuple(range(world)) for e in sp)
+        dense_in_groups = [e for g in ex.groups for e in g.entries if e.op.op_type == OperatorType.OP_EMBEDDING]
+        assert sorted(id(e) for e in dense_in_groups) == sorted(id(e) for e in dn)
+        assert all(not e.sparse and e.op.sparse_dp is None for e in dn)
+        if case == "dlrm_dpmix":
+            assert [e.shape[0] for e in dn] == [3], [e.shape for e in dn]
         rep = ex.memory_report()
-        assert rep["sparse_tables"] == sum(e.numel * 4 for e in embs) and rep["sparse_dp_payload"] > 0, rep
+        assert rep["sparse_tables"] == sum(e.numel * 4 for e in sp) and rep["sparse_dp_payload"] > 0, rep
     params = [p.get_weights(m) for p in m.parameters]
     loss = m.get_perf_metrics().get_loss()
     nr = ex.native_runner()
@@ -300,13 +311,10 @@ def _worker(rank, world, port, case, steps, out_path):
         traceback.print_exc()
         rc = 1
     finally:
+        # ordered teardown (flexmi.parallel.comm.shutdown_distributed): every backend thread is
+        # joined before the interpreter finalises, so the rank exits normally
         dist.destroy_process_group()
-    # leave without interpreter finalisation: the rank has torn its process group down, and
-    # static destructors of the backends' thread pools racing a peer's teardown must not turn a
-    # finished rank into a SIGABRT (VERDICT r2 "What's weak" #6)
-    sys.stdout.flush()
-    sys.stderr.flush()
-    os._exit(rc)
+    sys.exit(rc)
 
 
 def _launch(case, world, steps=3):
@@ -328,7 +336,7 @@ def _launch(case, world, steps=3):
                                         ("mlp_dp_zero", 4), ("dlrm_cat_dpsmall", 2), ("dlrm_mlperf8", 8), ("mlp_subset", 4), ("nmt_reference", 2),
                                         ("nmt_pipeline", 2), ("nmt_pipeline", 4), ("cnn_spatial", 4),
                                         ("cnn_spatial+p2p", 2), ("dlrm_dot+p2p", 2),
-                                        ("dlrm_shipped8", 8), ("dlrm_dp", 2), ("dlrm_dp", 4), ("dlrm_dp", 8),
+                                        ("dlrm_shipped8", 8), ("dlrm_dp", 2), ("dlrm_dp", 4), ("dlrm_dp", 8), ("dlrm_dpmix", 2), ("dlrm_dpmix", 4),
                                         ("inception8", 8), ("dlrm_dot+pipe2", 2), ("dlrm_dot+pipe3", 2),
                                         ("dlrm_cat+pipe2", 4), ("dlrm_mlperf8+pipe2", 8)])
 def test_strategy_equivalence(case, world):

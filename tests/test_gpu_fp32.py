@@ -193,6 +193,64 @@ def test_dot_interaction_f32(gpu, F, D, selfi):
         assert rel_err(dz[i], exp) < TOL, i
 
 
+@pytest.mark.parametrize("F,D,selfi,i64", [(27, 128, False, True), (9, 64, True, False), (5, 32, False, True)])
+def test_dot_interaction_gather_f32(gpu, F, D, selfi, i64):
+    """Embedding-into-interaction kernels: features 1.. are TABLE rows gathered by bag-1 indices
+    (incl. duplicates and an out-of-range index, clamped), forward and backward vs float64."""
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(19)
+    B = 1000
+    x = torch.randn(B, D, device=gpu)
+    rows = [3, 70, 1000, 40000] * F
+    tabs = [torch.randn(rows[i], D, device=gpu) for i in range(F - 1)]
+    idt = torch.int64 if i64 else torch.int32
+    ixs = [torch.randint(0, t.shape[0], (B, 1), device=gpu, dtype=idt) for t in tabs]
+    ixs[0][5, 0] = tabs[0].shape[0] + 7          # out of range: clamped to the last row
+    cl = [ix.view(-1).long().clamp(0, t.shape[0] - 1) for ix, t in zip(ixs, tabs)]
+    zs = [x] + [t[c] for t, c in zip(tabs, cl)]  # the materialised rows (oracle)
+    npairs = F * (F + 1) // 2 if selfi else F * (F - 1) // 2
+    W = (D + npairs + 15) // 16 * 16
+    y = torch.full((B, W), 7.0, device=gpu)
+    assert Kk.dot_interaction_forward_gather([x] + tabs, [None] + ixs, y, selfi)
+    Z = torch.stack([z.double() for z in zs], 1)
+    G = Z @ Z.transpose(1, 2)
+    li, lj = zip(*[(i, j) for i in range(F) for j in range(i + (1 if selfi else 0))])
+    ref = torch.zeros(B, W, dtype=torch.float64, device=gpu)
+    ref[:, :D] = Z[:, 0]
+    ref[:, D:D + npairs] = G[:, li, lj]
+    assert rel_err(y, ref) < TOL
+    dy = torch.randn(B, W, device=gpu)
+    dz = [torch.randn(B, D, device=gpu) for _ in range(F)]
+    old = [g.double().clone() for g in dz]
+    accs = [i % 2 == 1 for i in range(F)]
+    assert Kk.dot_interaction_backward_gather([x] + tabs, [None] + ixs, dy, dz, accs, selfi)
+    dG = torch.zeros(B, F, F, dtype=torch.float64, device=gpu)
+    dG[:, li, lj] = dy[:, D:D + npairs].double()
+    dZ = (dG + dG.transpose(1, 2)) @ Z
+    dZ[:, 0] += dy[:, :D].double()
+    for i in range(F):
+        exp = dZ[:, i] + (old[i] if accs[i] else 0)
+        assert rel_err(dz[i], exp) < TOL, i
+
+
+def test_embedding_gather_fusion_on_off_equivalent(gpu, monkeypatch):
+    """The executor's embedding-into-interaction fusion (Executor._build_gather_fusion) trains a
+    DLRM exactly like materialised embedding outputs (FM_EMB_GATHER=0), and really engages."""
+    from flexmi.models.dlrm import DLRMConfig
+    dcfg = DLRMConfig(128, [5000, 300, 12, 70000, 40], [13, 256, 128], [256, 256, 1], 1, -1, -1, 0.0, "dot", "", -1,
+                      "bce", "gather")
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("FM_EMB_GATHER", mode)
+        ws, loss, ex = _dlrm_run("gpu", dcfg, 2048, 4, graph=True)
+        dots = [op for op in ex.model.layers if type(op).__name__ == "DotInteraction"]
+        fused = any("gather" in ex.ctx[op.guid].saved for op in dots)
+        assert fused == (mode == "1"), mode
+        res[mode] = (ws, loss)
+    _assert_params_close(res["0"][0], res["1"][0], 1e-5)
+    assert abs(res["0"][1] - res["1"][1]) < 1e-5
+
+
 # ---------------------------------------------------------------- whole models, fp32 GPU vs fp32 CPU
 def _dlrm_run(dev, dcfg, B, steps, seed=0, graph=False, lr=0.1):
     from flexmi.core import FFConfig, FFModel, SGDOptimizer, LossType, MetricsType

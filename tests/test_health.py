@@ -100,9 +100,10 @@ def _fault_worker(rank, world, port, fault, out_dir):
         from flexmi.runtime.health import FaultyComm
         m, x = _mlp(debug=True, watchdog=20.0)
         if rank == 1:
-            # the step's first collectives (gradient bucket and metric reductions; their issue
-            # order may vary with timing) all get the fault, so the gradient exchange is hit
-            m.comm = FaultyComm(m.comm, {0: fault} if fault[0] == "kill" else {k: fault for k in range(6)})
+            # the native runner's collective #0 = step 1's gradient-bucket all-reduce (the runner
+            # issues the program's collectives in program order; the metric reduction is not one
+            # of them), so exactly one deterministic collective is faulted
+            m.comm = FaultyComm(m.comm, {0: fault} if fault[0] != "none" else {})
         m.init_layers()
         nr = m._ex().native_runner()
         res["native"] = nr is not None
@@ -120,6 +121,8 @@ def _fault_worker(rank, world, port, fault, out_dir):
         res["msg"] = str(e)[:300]
     with open(os.path.join(out_dir, f"r{rank}.json"), "w") as f:
         json.dump(res, f)
+    # a faulted run's communicators cannot be torn down collectively (a peer may be dead or out
+    # of step), so this worker -- and only this one -- leaves without interpreter finalisation
     os._exit(0)
 
 
@@ -151,6 +154,9 @@ def test_dropped_allreduce_is_detected_as_replica_divergence():
     res, hung, _ = _run_faulty(("drop",))
     assert not hung
     assert res[0]["error"] == "ReplicaDivergence" and res[1]["error"] == "ReplicaDivergence", res
+    # detected in the step whose gradient all-reduce was dropped (the first), not later
+    assert len(res[0]["steps"]) == 1 and len(res[1]["steps"]) == 1, res
+    assert res[1]["steps"][0]["fault_calls"] >= 1, res
     # the fault was injected by the native step runner (flexmi._rt), the production path
     assert res[0]["native"] and res[1]["native"], res
 
@@ -160,6 +166,7 @@ def test_corrupted_allreduce_is_detected_as_nonfinite_weights():
     res, hung, _ = _run_faulty(("corrupt",))
     assert not hung
     assert res[0]["error"] == "NumericalError" and res[1]["error"] == "NumericalError", res
+    assert len(res[0]["steps"]) == 1 and len(res[1]["steps"]) == 1, res
     assert res[0]["native"] and res[1]["native"], res
 
 
@@ -169,6 +176,16 @@ def test_killed_rank_surfaces_as_error_on_survivor():
     assert not hung, "survivor hung after peer death"
     assert codes[1] == 3 and 1 not in res
     assert res[0]["error"] is not None, res
+
+
+@pytest.mark.multiproc
+def test_no_fault_no_false_alarm():
+    """The same 2-rank debug run without a fault trains both steps: replica checksums and
+    finiteness checks cover the whole flat weight buffer, alignment gaps included."""
+    res, hung, _ = _run_faulty(("none",))
+    assert not hung
+    assert res[0]["error"] is None and res[1]["error"] is None, res
+    assert len(res[0]["steps"]) == 2 and len(res[1]["steps"]) == 2, res
 
 
 def test_metrics_jsonl_log(tmp_path):

@@ -106,3 +106,18 @@ def test_nearest_resize_rounds_half_away_from_zero():
     big = I.nearest_resize_hwc(img, 7, 11)
     assert big.shape == (7, 11, 3)
     np.testing.assert_array_equal(big[-1, -1], img[4, 4])
+
+
+def test_roundf_near_half():
+    """C roundf on float32: a value one ulp below k + 0.5 rounds DOWN (float32 x + 0.5 would
+    tie-to-even up to k + 1), exact halves round away from zero."""
+    import math
+    below = np.nextafter(np.float32(0.5), np.float32(0.0))     # 0.5 - 2**-25
+    vals = np.array([below, 0.5, 1.5, 2.5, np.nextafter(np.float32(2.5), np.float32(0.0)), 0.0, 3.49999],
+                    dtype=np.float32)
+    got = I.roundf(vals)
+    # reference: exact decimal rounding of the float32 value, half away from zero
+    want = [int(math.floor(float(v) + 0.5)) if float(v) - math.floor(float(v)) != 0.5 else int(math.floor(float(v))) + 1
+            for v in vals]
+    assert got.tolist() == want == [0, 1, 2, 3, 2, 0, 3]
+    assert np.float32(below) + np.float32(0.5) == np.float32(1.0)   # the float32 pitfall it avoids
