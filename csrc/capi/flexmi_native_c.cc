@@ -569,6 +569,54 @@ int fmn_model_dense(fmn_model_t m, int input_tensor, int out_dim, int activation
   return guarded([&] { return m->m->dense(input_tensor, out_dim, activation, use_bias != 0); }, -1);
 }
 
+int fmn_model_sparse_input(fmn_model_t m, int bag) {
+  if (!m) return fail("fmn_model_sparse_input: null model");
+  return guarded([&] { return m->m->sparse_input(bag); }, -1);
+}
+
+int fmn_model_embedding(fmn_model_t m, int sparse_input, int64_t rows, int dim) {
+  if (!m) return fail("fmn_model_embedding: null model");
+  return guarded([&] { return m->m->embedding(sparse_input, rows, dim); }, -1);
+}
+
+int fmn_model_dot_interaction(fmn_model_t m, int bottom, int n, const int* embeddings, int pad_to) {
+  if (!m || n < 1 || !embeddings) return fail("fmn_model_dot_interaction: bad arguments");
+  return guarded([&] { return m->m->dot_interaction(bottom, std::vector<int>(embeddings, embeddings + n), pad_to); }, -1);
+}
+
+int fmn_model_set_table_owner(fmn_model_t m, int table, int rank) {
+  if (!m) return fail("fmn_model_set_table_owner: null model");
+  return guarded(
+      [&] {
+        m->m->set_table_owner(table, rank);
+        return 0;
+      },
+      -1);
+}
+
+int fmn_model_table_owner(fmn_model_t m, int table) {
+  if (!m) return fail("fmn_model_table_owner: null model");
+  return guarded([&] { return m->m->table_owner(table); }, -1);
+}
+
+int fmn_model_param_local(fmn_model_t m, int i) {
+  if (!m) return fail("fmn_model_param_local: null model");
+  return guarded([&] { return m->m->param_local(i) ? 1 : 0; }, -1);
+}
+
+int fmn_model_train_step_sparse(fmn_model_t m, const float* x, const int64_t* const* sparse, const void* labels,
+                                double* loss, int64_t* correct) {
+  if (!m || !x || !labels) return fail("fmn_model_train_step_sparse: bad arguments");
+  return guarded(
+      [&] {
+        const flexmi::nm::StepStat s = m->m->train_step(x, sparse, labels);
+        if (loss) *loss = s.loss;
+        if (correct) *correct = s.correct;
+        return 0;
+      },
+      -1);
+}
+
 int fmn_model_compile(fmn_model_t m, int loss_type, float lr, double bucket_mb) {
   if (!m) return fail("fmn_model_compile: null model");
   return guarded(

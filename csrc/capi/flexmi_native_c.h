@@ -137,13 +137,17 @@ int fmn_embedding_bag_forward(const float* W, int64_t rows, int64_t D, const int
 int fmn_embedding_bag_backward(float* target, int64_t rows, int64_t D, const int64_t* idx, int64_t B, int64_t bag,
                                int64_t row_lo, const float* dy, int64_t ld_dy, float alpha);
 
-/* ---- native model: build, plan and train an MLP entirely in C++ ----------------------------------
- * The plan compiler (csrc/runtime/native_model.cc) lays out one rank's buffers for data
- * parallelism (sample split; replicated weights in one flat buffer; gradient all-reduce buckets
- * in backward order), decides the fused epilogues and runs the step on an engine:
- * device 0 = CPU (reference fp32 loops, one rank), device 1 = HIP (flexmi's gfx950 kernels from
+/* ---- native model: build, plan and train an MLP or a DLRM entirely in C++ -------------------------
+ * The plan compiler (csrc/runtime/native_model.cc) lays out one rank's buffers: data parallelism
+ * for the dense layers (sample split; replicated weights in one flat buffer; gradient all-reduce
+ * buckets in backward order) and TABLE-WISE model parallelism for embedding tables (each table
+ * whole on one rank, global-batch lookups there, an all-to-all to the sample shards and back,
+ * sparse SGD of the touched rows on the owner); it decides the fused epilogues and runs the step
+ * on an engine: device 0 = CPU (reference fp32 loops; `world` rank PROCESSES exchange through a
+ * shared mapping in the `rendezvous` directory), device 1 = HIP (flexmi's gfx950 kernels from
  * libflexmi_kernels.so, RCCL across `world` processes that share the `rendezvous` directory).
- * Reference: FFModel compile / init_layers / forward / backward / update (src/runtime/model.cc). */
+ * Reference: FFModel compile / init_layers / forward / backward / update (src/runtime/model.cc),
+ * the DLRM app and strategy (examples/cpp/DLRM/dlrm.cc, src/runtime/dlrm_strategy.cc). */
 typedef struct fmn_model_s* fmn_model_t;
 fmn_model_t fmn_model_create(int global_batch, int device, int rank, int world, const char* rendezvous);
 void fmn_model_destroy(fmn_model_t m);
@@ -151,18 +155,34 @@ void fmn_model_destroy(fmn_model_t m);
  * 11 relu, 12 sigmoid, 13 tanh) */
 int fmn_model_input(fmn_model_t m, int features);
 int fmn_model_dense(fmn_model_t m, int input_tensor, int out_dim, int activation, int use_bias);
+/* DLRM graphs: a sparse input (int64 [B][bag] lookup indices of the GLOBAL batch) -> its id; an
+ * embedding table rows x dim over a sparse input (SUM bag) -> its [B][dim] tensor id; the dot
+ * interaction of a bottom tensor and n embedding tensors -> its [B][W] tensor id (W = dim +
+ * F(F-1)/2 padded to pad_to).  Every tensor has one consumer. */
+int fmn_model_sparse_input(fmn_model_t m, int bag);
+int fmn_model_embedding(fmn_model_t m, int sparse_input, int64_t rows, int dim);
+int fmn_model_dot_interaction(fmn_model_t m, int bottom, int n, const int* embeddings, int pad_to);
+/* place table t (embedding creation order) on `rank` (before compile; default: greedy by rows) */
+int fmn_model_set_table_owner(fmn_model_t m, int table, int rank);
+int fmn_model_table_owner(fmn_model_t m, int table);
 /* loss: 51 sparse categorical CE (softmax of the last layer's logits, int32 labels), 52 MSE (avg),
  * 54 binary CE (sigmoid output); bucket_mb = gradient all-reduce bucket size */
 int fmn_model_compile(fmn_model_t m, int loss_type, float lr, double bucket_mb);
 int fmn_model_init_weights(fmn_model_t m, uint64_t seed);
-/* parameter entries in model order: weight [out][in] then bias [out] of every dense layer */
+/* parameter entries in model order: weight [out][in] then bias [out] of every dense layer, the
+ * [rows][dim] table of every embedding; a table is readable / writable on its owner only
+ * (fmn_model_param_local) */
 int fmn_model_num_params(fmn_model_t m);
 int64_t fmn_model_param_numel(fmn_model_t m, int i);
+int fmn_model_param_local(fmn_model_t m, int i);
 int fmn_model_set_param(fmn_model_t m, int i, const float* host);
 int fmn_model_get_param(fmn_model_t m, int i, float* host);
 /* one training step on the GLOBAL batch x [B][features] (each rank takes its sample shard) and
  * labels ([B] int32 for loss 51, [B][out] float otherwise); loss = this rank's mean loss */
 int fmn_model_train_step(fmn_model_t m, const float* x, const void* labels, double* loss, int64_t* correct);
+/* the same with the sparse inputs: sparse[s] = GLOBAL [B][bag] int64 indices of sparse input s */
+int fmn_model_train_step_sparse(fmn_model_t m, const float* x, const int64_t* const* sparse, const void* labels,
+                                double* loss, int64_t* correct);
 /* human-readable plan (layers, fused epilogues, flat buffer, buckets); returns the length */
 int64_t fmn_model_describe(fmn_model_t m, char* buf, int64_t len);
 

@@ -7,6 +7,9 @@
 //                  tiles' row sums) and dX (activation backward of the layer below fused into
 //                  the epilogue) -- the same kernel sequence as flexmi/ops/_kernels.py linear_backward
 //   loss / SGD     fm_loss_fwd_bwd, fm_sgd_update (zeroes the consumed gradients)
+//   embeddings     fm_embedding_fwd (global-batch lookups on the owner), fm_embedding_bwd with a
+//                  device lr (fused sparse SGD of the touched rows); fm_dot_interaction_{fwd,bwd}_f32
+//                  (v_mfma_f32_32x32x2_f32); the exchange = RCCL grouped send / recv per peer
 //   communication  one RCCL communicator per model (unique id handed over through a file in the
 //                  rendezvous directory); bucket all-reduces on a second HIP stream, started as
 //                  soon as the bucket's last gradient kernel is enqueued (event dependency) and
@@ -40,6 +43,14 @@ void fm_loss_fwd_bwd(const void* logits, int logits_bf16, const void* labels, vo
                      int loss_type, float scale, float* acc, int mask, float clamp_t, hipStream_t s);
 void fm_sgd_update(float* W, float* G, float* V, unsigned short* Wc, const float* lr, long n, float wd, float mom, int nesterov,
                    int zero_g, hipStream_t s);
+void fm_embedding_fwd(const void* idx, int idx64, const float* W, void* out, int out_bf16, long B, int bag, int rows, int D,
+                      long ldo, float scale, hipStream_t s);
+void fm_embedding_bwd(const void* idx, int idx64, const void* dy, int dy_bf16, float* W, const float* lr, long B, int bag,
+                      int rows, int D, long ldg, float scale, hipStream_t s);
+void fm_dot_interaction_fwd_f32(const float* const* z, int F, long ldz, float* out, long ldo, long B, int D, int W, int self,
+                                hipStream_t s);
+void fm_dot_interaction_bwd_f32(const float* const* z, int F, long ldz, const float* dout, long ldo, float* const* dz,
+                                long lddz, unsigned acc_mask, long B, int D, int self, hipStream_t s);
 }
 
 namespace flexmi {
@@ -144,12 +155,40 @@ class HipEngine : public Engine {
   }
 
   void sgd(float* w, float* g, int64_t n, float lr) override {
-    if (lr != lr_host_) {
-      HIPX(hipMemcpyAsync(lr_, &lr, sizeof(float), hipMemcpyHostToDevice, st_));
-      HIPX(hipStreamSynchronize(st_));
-      lr_host_ = lr;
-    }
+    set_lr(lr);
     fm_sgd_update(w, g, nullptr, nullptr, lr_, n, 0.f, 0.f, 0, 1, st_);
+  }
+
+  void copy(void* dst, const void* src, size_t bytes) override {
+    HIPX(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st_));
+  }
+  void emb_fwd(const float* W, int64_t rows, const int64_t* idx, int bag, float* out, int64_t B, int D) override {
+    fm_embedding_fwd(idx, 1, W, out, 0, B, bag, (int)rows, D, D, 1.f, st_);
+  }
+  void emb_sgd(float* W, int64_t rows, const int64_t* idx, int bag, const float* g, int64_t B, int D, float lr) override {
+    set_lr(lr);
+    fm_embedding_bwd(idx, 1, g, 0, W, lr_, B, bag, (int)rows, D, D, 1.f, st_);
+  }
+  void dot_fwd(const float* const* z, int F, float* y, int M, int D, int W) override {
+    fm_dot_interaction_fwd_f32(z, F, D, y, W, M, D, W, 0, st_);
+  }
+  void dot_bwd(const float* const* z, int F, const float* dy, float* const* dz, int M, int D, int W) override {
+    fm_dot_interaction_bwd_f32(z, F, D, dy, W, dz, D, 0u, M, D, 0, st_);
+  }
+  void all_to_all(const float* send, const int64_t* send_counts, float* recv, const int64_t* recv_counts) override {
+    if (!comm_) {
+      HIPX(hipMemcpyAsync(recv, send, (size_t)send_counts[0] * sizeof(float), hipMemcpyDeviceToDevice, st_));
+      return;
+    }
+    int64_t so = 0, ro = 0;
+    NCCLX(ncclGroupStart());
+    for (int p = 0; p < world_; ++p) {
+      if (send_counts[p]) NCCLX(ncclSend(send + so, (size_t)send_counts[p], ncclFloat32, p, comm_, st_));
+      if (recv_counts[p]) NCCLX(ncclRecv(recv + ro, (size_t)recv_counts[p], ncclFloat32, p, comm_, st_));
+      so += send_counts[p];
+      ro += recv_counts[p];
+    }
+    NCCLX(ncclGroupEnd());
   }
 
   void allreduce_start(float* buf, int64_t n) override {
@@ -170,6 +209,13 @@ class HipEngine : public Engine {
   }
 
  private:
+  void set_lr(float lr) {
+    if (lr != lr_host_) {
+      HIPX(hipMemcpyAsync(lr_, &lr, sizeof(float), hipMemcpyHostToDevice, st_));
+      HIPX(hipStreamSynchronize(st_));
+      lr_host_ = lr;
+    }
+  }
   hipEvent_t event() {
     if (ev_next_ == events_.size()) {
       hipEvent_t e;

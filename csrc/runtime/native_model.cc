@@ -1,6 +1,8 @@
 // flexmi native model: plan compiler + CPU engine (see native_model.h).
 #include "native_model.h"
 
+#include "host_comm.h"
+
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -54,9 +56,13 @@ inline float act_b(int act, float y, float g) {
   return g;
 }
 
-// reference fp32 engine: plain loops in the executor's order of operations
+// reference fp32 engine: plain loops in the executor's order of operations; a HostComm carries
+// the collectives between rank processes
 class CpuEngine : public Engine {
  public:
+  CpuEngine(int rank, int world, const std::string& dir, size_t slot_bytes) {
+    if (world > 1) comm_ = std::make_unique<HostComm>(dir, rank, world, slot_bytes);
+  }
   void* alloc(size_t bytes) override { return std::calloc(std::max<size_t>(bytes, 16), 1); }
   void release(void* p) override { std::free(p); }
   void h2d(void* dst, const void* src, size_t bytes) override { std::memcpy(dst, src, bytes); }
@@ -141,8 +147,82 @@ class CpuEngine : public Engine {
       g[i] = 0.f;
     }
   }
-  void allreduce_start(float*, int64_t) override {}
+  void allreduce_start(float* buf, int64_t n) override {
+    if (comm_) comm_->all_reduce_sum(buf, n);   // host collectives complete in place
+  }
   void allreduce_wait() override {}
+  void copy(void* dst, const void* src, size_t bytes) override { std::memcpy(dst, src, bytes); }
+  void emb_fwd(const float* W, int64_t rows, const int64_t* idx, int bag, float* out, int64_t B, int D) override {
+    for (int64_t b = 0; b < B; ++b) {
+      float* o = out + b * D;
+      for (int d = 0; d < D; ++d) o[d] = 0.f;
+      for (int j = 0; j < bag; ++j) {
+        const int64_t r = idx[b * bag + j];
+        if (r < 0 || r >= rows) continue;
+        const float* w = W + r * D;
+        for (int d = 0; d < D; ++d) o[d] += w[d];
+      }
+    }
+  }
+  void emb_sgd(float* W, int64_t rows, const int64_t* idx, int bag, const float* g, int64_t B, int D, float lr) override {
+    for (int64_t b = 0; b < B; ++b)
+      for (int j = 0; j < bag; ++j) {
+        const int64_t r = idx[b * bag + j];
+        if (r < 0 || r >= rows) continue;
+        float* w = W + r * D;
+        const float* gr = g + b * D;
+        for (int d = 0; d < D; ++d) w[d] -= lr * gr[d];
+      }
+  }
+  void dot_fwd(const float* const* z, int F, float* y, int M, int D, int W) override {
+    for (int m = 0; m < M; ++m) {
+      float* o = y + (int64_t)m * W;
+      for (int c = 0; c < W; ++c) o[c] = 0.f;
+      for (int d = 0; d < D; ++d) o[d] = z[0][(int64_t)m * D + d];
+      int p = D;
+      for (int i = 0; i < F; ++i)
+        for (int j = 0; j < i; ++j) {
+          const float* a = z[i] + (int64_t)m * D;
+          const float* b = z[j] + (int64_t)m * D;
+          float s = 0.f;
+          for (int d = 0; d < D; ++d) s += a[d] * b[d];
+          o[p++] = s;
+        }
+    }
+  }
+  void dot_bwd(const float* const* z, int F, const float* dy, float* const* dz, int M, int D, int W) override {
+    std::vector<float> S((size_t)F * F);
+    for (int m = 0; m < M; ++m) {
+      const float* g = dy + (int64_t)m * W;
+      int p = D;
+      std::fill(S.begin(), S.end(), 0.f);
+      for (int i = 0; i < F; ++i)
+        for (int j = 0; j < i; ++j) {
+          S[(size_t)i * F + j] = g[p];
+          S[(size_t)j * F + i] = g[p];
+          ++p;
+        }
+      for (int i = 0; i < F; ++i) {
+        if (!dz[i]) continue;
+        float* o = dz[i] + (int64_t)m * D;
+        for (int d = 0; d < D; ++d) {
+          float s = i == 0 ? g[d] : 0.f;
+          for (int j = 0; j < F; ++j) s += S[(size_t)i * F + j] * z[j][(int64_t)m * D + d];
+          o[d] = s;
+        }
+      }
+    }
+  }
+  void all_to_all(const float* send, const int64_t* send_counts, float* recv, const int64_t* recv_counts) override {
+    if (comm_) {
+      comm_->all_to_all(send, send_counts, recv, recv_counts);
+      return;
+    }
+    std::memcpy(recv, send, (size_t)send_counts[0] * sizeof(float));
+  }
+
+ private:
+  std::unique_ptr<HostComm> comm_;
 };
 
 uint64_t splitmix(uint64_t& s) {
@@ -154,7 +234,9 @@ uint64_t splitmix(uint64_t& s) {
 
 }  // namespace
 
-std::unique_ptr<Engine> make_cpu_engine() { return std::make_unique<CpuEngine>(); }
+std::unique_ptr<Engine> make_cpu_engine(int rank, int world, const std::string& rendezvous, size_t slot_bytes) {
+  return std::make_unique<CpuEngine>(rank, world, rendezvous, slot_bytes);
+}
 
 // strong definition in native_hip.cc (libflexmi_native_c); builds without it report the engine
 // as unavailable
@@ -167,7 +249,6 @@ Model::Model(int global_batch, int device, int rank, int world, const std::strin
   if (world < 1 || rank < 0 || rank >= world) throw std::invalid_argument("native model: bad rank / world");
   if (global_batch % world) throw std::invalid_argument("native model: the global batch must divide over the ranks");
   Bl_ = global_batch / world;
-  if (device == 0 && world > 1) throw std::invalid_argument("native model: the CPU engine runs one rank");
 }
 
 Model::~Model() {
@@ -180,22 +261,32 @@ Model::~Model() {
   rel(grads_);
   for (auto* p : act_) rel(p);
   for (auto* p : grad_) rel(p);
+  for (auto* p : table_) rel(p);
+  for (auto* p : emb_full_) rel(p);
+  for (auto* p : idx_) rel(p);
+  rel(xsend_);
+  rel(xrecv_);
   rel(probs_);
   rel(labels_);
   rel(stats_);
 }
 
+void Model::check_tensor(int t, const char* what) const {
+  if (t < 0 || t >= (int)cols_.size()) throw std::invalid_argument(std::string("native model: unknown tensor for ") + what);
+  if (consumers_[t] > 0) throw std::invalid_argument(std::string("native model: tensor consumed twice (") + what + ")");
+}
+
 int Model::input(int features) {
   if (compiled_ || input_ >= 0) throw std::logic_error("native model: one input, before compile");
   cols_.push_back(features);
+  consumers_.push_back(0);
   input_ = (int)cols_.size() - 1;
   return input_;
 }
 
 int Model::dense(int x, int out_dim, int act, bool bias) {
   if (compiled_) throw std::logic_error("native model: dense after compile");
-  if (x < 0 || x >= (int)cols_.size()) throw std::invalid_argument("native model: unknown input tensor");
-  if (!ops_.empty() && x != ops_.back().y) throw std::invalid_argument("native model: layers form a chain");
+  check_tensor(x, "dense");
   if (act != ACT_NONE && act != ACT_RELU && act != ACT_SIGMOID && act != ACT_TANH)
     throw std::invalid_argument("native model: activation");
   Dense d;
@@ -204,16 +295,93 @@ int Model::dense(int x, int out_dim, int act, bool bias) {
   d.N = out_dim;
   d.act = act;
   d.bias = bias;
+  consumers_[x]++;
   cols_.push_back(out_dim);
+  consumers_.push_back(0);
   d.y = (int)cols_.size() - 1;
   d.w = (int)pnumel_.size();
   pnumel_.push_back((int64_t)d.N * d.K);
+  entry_table_.push_back(-1);
   if (bias) {
     d.b = (int)pnumel_.size();
     pnumel_.push_back(d.N);
+    entry_table_.push_back(-1);
   }
   ops_.push_back(d);
+  nodes_.push_back({K_DENSE, (int)ops_.size() - 1});
   return d.y;
+}
+
+int Model::sparse_input(int bag) {
+  if (compiled_) throw std::logic_error("native model: sparse input after compile");
+  if (bag < 1) throw std::invalid_argument("native model: bag >= 1");
+  sparse_bag_.push_back(bag);
+  return (int)sparse_bag_.size() - 1;
+}
+
+int Model::embedding(int sparse, int64_t rows, int dim) {
+  if (compiled_) throw std::logic_error("native model: embedding after compile");
+  if (sparse < 0 || sparse >= (int)sparse_bag_.size()) throw std::invalid_argument("native model: unknown sparse input");
+  for (const Emb& e : embs_)
+    if (e.sparse == sparse) throw std::invalid_argument("native model: sparse input used twice");
+  if (rows < 1 || dim < 1) throw std::invalid_argument("native model: embedding shape");
+  Emb e;
+  e.sparse = sparse;
+  e.rows = rows;
+  e.D = dim;
+  e.bag = sparse_bag_[sparse];
+  cols_.push_back(dim);
+  consumers_.push_back(0);
+  e.y = (int)cols_.size() - 1;
+  e.w = (int)pnumel_.size();
+  pnumel_.push_back(rows * dim);
+  entry_table_.push_back((int)embs_.size());
+  e.owner = -1;
+  embs_.push_back(e);
+  nodes_.push_back({K_EMB, (int)embs_.size() - 1});
+  return e.y;
+}
+
+int Model::dot_interaction(int bottom, const std::vector<int>& embs, int pad_to) {
+  if (compiled_) throw std::logic_error("native model: interaction after compile");
+  if (embs.empty() || embs.size() > 31) throw std::invalid_argument("native model: 1..31 embeddings per interaction");
+  Dot d;
+  d.in.push_back(bottom);
+  for (int t : embs) d.in.push_back(t);
+  check_tensor(bottom, "interaction");
+  d.D = cols_[bottom];
+  for (int t : d.in) {
+    check_tensor(t, "interaction");
+    if (cols_[t] != d.D) throw std::invalid_argument("native model: interaction inputs of different widths");
+  }
+  for (int t : d.in) consumers_[t]++;
+  const int F = (int)d.in.size();
+  d.npairs = F * (F - 1) / 2;
+  const int p = std::max(1, pad_to);
+  d.W = (d.D + d.npairs + p - 1) / p * p;
+  cols_.push_back(d.W);
+  consumers_.push_back(0);
+  d.y = (int)cols_.size() - 1;
+  dots_.push_back(d);
+  nodes_.push_back({K_DOT, (int)dots_.size() - 1});
+  return d.y;
+}
+
+void Model::set_table_owner(int table, int rank) {
+  if (compiled_) throw std::logic_error("native model: placement after compile");
+  if (table < 0 || table >= (int)embs_.size() || rank < 0 || rank >= world_)
+    throw std::invalid_argument("native model: table / rank");
+  embs_[table].owner = rank;
+}
+
+int Model::dense_out_node() const {
+  if (nodes_.empty() || nodes_.back().kind != K_DENSE) throw std::logic_error("native model: the last op must be dense");
+  return nodes_.back().idx;
+}
+
+bool Model::param_local(int i) const {
+  const int t = entry_table_.at(i);
+  return t < 0 || embs_[t].owner == rank_;
 }
 
 void Model::compile(int loss_type, float lr, double bucket_mb) {
@@ -222,24 +390,44 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
     throw std::invalid_argument("native model: loss type");
   loss_ = loss_type;
   lr_ = lr;
-  Dense& last = ops_.back();
+  Dense& last = ops_[dense_out_node()];
   if (loss_ == LOSS_BCE) {
     if (last.act != ACT_SIGMOID) throw std::invalid_argument("native model: BCE needs a sigmoid output layer");
     last.skip_act_grad = true;   // the loss emits dL/dz = p - y
   }
   if (loss_ == LOSS_SCCE && last.act != ACT_NONE) throw std::invalid_argument("native model: SCCE takes logits");
-  ops_.front().need_dx = false;
-  // fused epilogues: layer i+1's dX GEMM applies layer i's activation backward (and then layer
-  // i's backward reads its incoming gradient as dpre); GEMM layers only (N > 1 both sides)
-  for (size_t i = 0; i + 1 < ops_.size(); ++i) {
-    Dense& lo = ops_[i];
-    Dense& hi = ops_[i + 1];
+  // producers of the dense tensors
+  std::vector<int> dense_of(cols_.size(), -1);
+  for (size_t i = 0; i < ops_.size(); ++i) dense_of[ops_[i].y] = (int)i;
+  for (Dense& d : ops_) d.need_dx = d.x != input_;
+  // fused epilogues: a dense layer whose input is another dense layer's output applies that
+  // layer's activation backward in its dX GEMM (the producer then reads its gradient as dpre)
+  for (Dense& hi : ops_) {
+    const int lo_i = dense_of[hi.x];
+    if (lo_i < 0) continue;
+    Dense& lo = ops_[lo_i];
     if (lo.act != ACT_NONE && lo.N > 1 && hi.N > 1 && !lo.skip_act_grad) {
       hi.fuse_below = true;
+      hi.below = lo_i;
       lo.grad_is_dpre = true;
     }
   }
-  // parameter entries in backward order -> one flat buffer, all-reduce buckets
+  // table-wise placement: unplaced tables go to the rank with the fewest rows (largest first)
+  {
+    std::vector<int64_t> load(world_, 0);
+    for (const Emb& e : embs_)
+      if (e.owner >= 0) load[e.owner] += e.rows;
+    std::vector<int> order;
+    for (int t = 0; t < (int)embs_.size(); ++t)
+      if (embs_[t].owner < 0) order.push_back(t);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return embs_[a].rows > embs_[b].rows; });
+    for (int t : order) {
+      const int r = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+      embs_[t].owner = r;
+      load[r] += embs_[t].rows;
+    }
+  }
+  // dense parameter entries in backward order -> one flat buffer, all-reduce buckets
   porder_.clear();
   for (auto it = ops_.rbegin(); it != ops_.rend(); ++it) {
     porder_.push_back(it->w);
@@ -251,8 +439,23 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
   wplan_ = plan_weights(nums, cap);
   pofs_.assign(pnumel_.size(), 0);
   for (size_t j = 0; j < porder_.size(); ++j) pofs_[porder_[j]] = wplan_.offset[j];
+  // embedding exchange: every owner sends each peer its shard rows of every owned table (table
+  // order); each rank receives, per peer, that peer's tables (table order)
+  xcount_send_.assign(world_, 0);
+  xcount_recv_.assign(world_, 0);
+  for (const Emb& e : embs_)
+    for (int p = 0; p < world_; ++p) {
+      if (e.owner == rank_) xcount_send_[p] += (int64_t)Bl_ * e.D;
+      if (e.owner == p) xcount_recv_[p] += (int64_t)Bl_ * e.D;
+    }
+  int64_t xs = 0, xr = 0;
+  for (int p = 0; p < world_; ++p) {
+    xs += xcount_send_[p];
+    xr += xcount_recv_[p];
+  }
   // engine + buffers
-  eng_ = device_ == 1 ? make_hip_engine(rank_, world_, rendezvous_) : make_cpu_engine();
+  const size_t slot = std::max<size_t>((size_t)std::max(xs, xr) * 4 + 4096, 4u << 20);
+  eng_ = device_ == 1 ? make_hip_engine(rank_, world_, rendezvous_) : make_cpu_engine(rank_, world_, rendezvous_, slot);
   params_ = (float*)eng_->alloc(wplan_.numel * 4);
   grads_ = (float*)eng_->alloc(wplan_.numel * 4);
   act_.assign(cols_.size(), nullptr);
@@ -260,6 +463,20 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
   for (size_t t = 0; t < cols_.size(); ++t) {
     act_[t] = (float*)eng_->alloc((size_t)Bl_ * cols_[t] * 4);
     if ((int)t != input_) grad_[t] = (float*)eng_->alloc((size_t)Bl_ * cols_[t] * 4);
+  }
+  table_.assign(embs_.size(), nullptr);
+  emb_full_.assign(embs_.size(), nullptr);
+  idx_.assign(embs_.size(), nullptr);
+  for (size_t t = 0; t < embs_.size(); ++t) {
+    const Emb& e = embs_[t];
+    if (e.owner != rank_) continue;
+    table_[t] = (float*)eng_->alloc((size_t)e.rows * e.D * 4);
+    idx_[t] = (int64_t*)eng_->alloc((size_t)B_ * e.bag * 8);
+    if (world_ > 1) emb_full_[t] = (float*)eng_->alloc((size_t)B_ * e.D * 4);
+  }
+  if (world_ > 1 && !embs_.empty()) {
+    xsend_ = (float*)eng_->alloc((size_t)std::max<int64_t>(xs, 1) * 4);
+    xrecv_ = (float*)eng_->alloc((size_t)std::max<int64_t>(xr, 1) * 4);
   }
   const int C = last.N;
   if (loss_ == LOSS_SCCE) probs_ = (float*)eng_->alloc((size_t)Bl_ * C * 4);
@@ -281,35 +498,97 @@ void Model::init_weights(uint64_t seed) {
       set_param(d.b, z.data());
     }
   }
+  for (const Emb& e : embs_) {
+    if (e.owner != rank_) continue;
+    std::vector<float> w((size_t)e.rows * e.D);
+    const float lim = std::sqrt(1.f / (float)e.rows);
+    uint64_t s = seed * 1000003ULL + (uint64_t)e.w;
+    for (auto& v : w) v = ((float)(splitmix(s) >> 40) / (float)(1ULL << 24) * 2.f - 1.f) * lim;
+    set_param(e.w, w.data());
+  }
 }
 
 void Model::set_param(int i, const float* host) {
   if (!compiled_) throw std::logic_error("native model: set_param after compile");
-  eng_->h2d(params_ + pofs_.at(i), host, pnumel_.at(i) * 4);
+  const int t = entry_table_.at(i);
+  if (t >= 0) {
+    if (embs_[t].owner != rank_) throw std::invalid_argument("native model: table not on this rank");
+    eng_->h2d(table_[t], host, pnumel_[i] * 4);
+  } else {
+    eng_->h2d(params_ + pofs_.at(i), host, pnumel_.at(i) * 4);
+  }
   eng_->sync();
 }
 
 void Model::get_param(int i, float* host) const {
   if (!compiled_) throw std::logic_error("native model: get_param after compile");
   eng_->sync();
-  eng_->d2h(host, params_ + pofs_.at(i), pnumel_.at(i) * 4);
+  const int t = entry_table_.at(i);
+  if (t >= 0) {
+    if (embs_[t].owner != rank_) throw std::invalid_argument("native model: table not on this rank");
+    eng_->d2h(host, table_[t], pnumel_[i] * 4);
+  } else {
+    eng_->d2h(host, params_ + pofs_.at(i), pnumel_.at(i) * 4);
+  }
 }
 
-StepStat Model::train_step(const float* x, const void* labels) {
+StepStat Model::train_step(const float* x, const int64_t* const* sparse, const void* labels) {
   if (!compiled_) throw std::logic_error("native model: train_step before compile");
-  const Dense& last = ops_.back();
+  if (!embs_.empty() && !sparse) throw std::invalid_argument("native model: this model needs sparse inputs");
+  const Dense& last = ops_[dense_out_node()];
   const int C = last.N;
-  // this rank's sample shard of the global batch
+  // this rank's sample shard of the global batch; the owned tables' GLOBAL indices
   const int64_t r0 = (int64_t)rank_ * Bl_;
   eng_->h2d(act_[input_], x + r0 * cols_[input_], (size_t)Bl_ * cols_[input_] * 4);
   const size_t lab_row = loss_ == LOSS_SCCE ? 4 : (size_t)C * 4;
   eng_->h2d(labels_, static_cast<const char*>(labels) + r0 * lab_row, (size_t)Bl_ * lab_row);
+  for (size_t t = 0; t < embs_.size(); ++t)
+    if (embs_[t].owner == rank_) eng_->h2d(idx_[t], sparse[embs_[t].sparse], (size_t)B_ * embs_[t].bag * 8);
   float zero[2] = {0.f, 0.f};
   eng_->h2d(stats_, zero, sizeof(zero));
-  // forward
-  for (const Dense& d : ops_)
-    eng_->dense_fwd(act_[d.x], params_ + pofs_[d.w], d.b >= 0 ? params_ + pofs_[d.b] : nullptr, act_[d.y], Bl_, d.K, d.N,
-                    d.act);
+
+  // embedding lookups (owners, global batch) and the exchange to the sample shards, issued ahead
+  // of the first consumer
+  auto emb_forward = [&]() {
+    for (size_t t = 0; t < embs_.size(); ++t) {
+      const Emb& e = embs_[t];
+      if (e.owner != rank_) continue;
+      eng_->emb_fwd(table_[t], e.rows, idx_[t], e.bag, world_ > 1 ? emb_full_[t] : act_[e.y], B_, e.D);
+    }
+    if (world_ == 1 || embs_.empty()) return;
+    // pack: per peer p, every owned table's rows [p*Bl, (p+1)*Bl)
+    int64_t o = 0;
+    for (int p = 0; p < world_; ++p)
+      for (size_t t = 0; t < embs_.size(); ++t) {
+        const Emb& e = embs_[t];
+        if (e.owner != rank_) continue;
+        eng_->copy(xsend_ + o, emb_full_[t] + (int64_t)p * Bl_ * e.D, (size_t)Bl_ * e.D * 4);
+        o += (int64_t)Bl_ * e.D;
+      }
+    eng_->all_to_all(xsend_, xcount_send_.data(), xrecv_, xcount_recv_.data());
+    o = 0;
+    for (int p = 0; p < world_; ++p)
+      for (size_t t = 0; t < embs_.size(); ++t) {
+        const Emb& e = embs_[t];
+        if (e.owner != p) continue;
+        eng_->copy(act_[e.y], xrecv_ + o, (size_t)Bl_ * e.D * 4);
+        o += (int64_t)Bl_ * e.D;
+      }
+  };
+  emb_forward();
+  // forward in creation order
+  for (const Node& n : nodes_) {
+    if (n.kind == K_DENSE) {
+      const Dense& d = ops_[n.idx];
+      eng_->dense_fwd(act_[d.x], params_ + pofs_[d.w], d.b >= 0 ? params_ + pofs_[d.b] : nullptr, act_[d.y], Bl_, d.K,
+                      d.N, d.act);
+    } else if (n.kind == K_DOT) {
+      const Dot& d = dots_[n.idx];
+      std::vector<const float*> z;
+      for (int t : d.in) z.push_back(act_[t]);
+      eng_->dot_fwd(z.data(), (int)z.size(), act_[d.y], Bl_, d.D, d.W);
+    }
+  }
   // loss: gradient scaled by 1 / global batch (the reference's convention), so summing the
   // ranks' gradients gives the global mean gradient
   const float* pred = act_[last.y];
@@ -318,27 +597,65 @@ StepStat Model::train_step(const float* x, const void* labels) {
     pred = probs_;
   }
   eng_->loss(loss_, pred, labels_, grad_[last.y], Bl_, C, 1.f / (float)B_, stats_);
-  // backward (reverse layer order) with bucketed gradient all-reduces
+  // backward (reverse creation order) with bucketed gradient all-reduces of the dense entries
   std::vector<int> left;
   for (auto& b : wplan_.buckets) left.push_back((int)b.size() - 2);
   std::vector<int> bucket_of(pnumel_.size(), -1);
   for (size_t bi = 0; bi < wplan_.buckets.size(); ++bi)
     for (size_t k = 2; k < wplan_.buckets[bi].size(); ++k) bucket_of[porder_[wplan_.buckets[bi][k]]] = (int)bi;
-  for (int i = (int)ops_.size() - 1; i >= 0; --i) {
-    const Dense& d = ops_[i];
-    const Dense* below = i > 0 ? &ops_[i - 1] : nullptr;
-    const bool fuse = d.fuse_below && below;
-    const bool is_dpre = d.grad_is_dpre || d.skip_act_grad;
-    eng_->dense_bwd(act_[d.x], params_ + pofs_[d.w], act_[d.y], grad_[d.y], d.need_dx ? grad_[d.x] : nullptr,
-                    grads_ + pofs_[d.w], d.b >= 0 ? grads_ + pofs_[d.b] : nullptr, Bl_, d.K, d.N, d.act, is_dpre,
-                    fuse ? act_[below->y] : nullptr, fuse ? below->act : ACT_NONE);
-    if (world_ > 1) {
-      for (int e : {d.w, d.b}) {
-        if (e < 0) continue;
-        const int bi = bucket_of[e];
-        if (--left[bi] == 0)
-          eng_->allreduce_start(grads_ + wplan_.buckets[bi][0], wplan_.buckets[bi][1] - wplan_.buckets[bi][0]);
+  for (int ni = (int)nodes_.size() - 1; ni >= 0; --ni) {
+    const Node& n = nodes_[ni];
+    if (n.kind == K_DENSE) {
+      const Dense& d = ops_[n.idx];
+      const Dense* below = d.fuse_below ? &ops_[d.below] : nullptr;
+      const bool is_dpre = d.grad_is_dpre || d.skip_act_grad;
+      eng_->dense_bwd(act_[d.x], params_ + pofs_[d.w], act_[d.y], grad_[d.y], d.need_dx ? grad_[d.x] : nullptr,
+                      grads_ + pofs_[d.w], d.b >= 0 ? grads_ + pofs_[d.b] : nullptr, Bl_, d.K, d.N, d.act, is_dpre,
+                      below ? act_[below->y] : nullptr, below ? below->act : ACT_NONE);
+      if (world_ > 1) {
+        for (int e : {d.w, d.b}) {
+          if (e < 0) continue;
+          const int bi = bucket_of[e];
+          if (--left[bi] == 0)
+            eng_->allreduce_start(grads_ + wplan_.buckets[bi][0], wplan_.buckets[bi][1] - wplan_.buckets[bi][0]);
+        }
       }
+    } else if (n.kind == K_DOT) {
+      const Dot& d = dots_[n.idx];
+      std::vector<const float*> z;
+      std::vector<float*> dz;
+      for (int t : d.in) {
+        z.push_back(act_[t]);
+        dz.push_back(grad_[t]);
+      }
+      eng_->dot_bwd(z.data(), (int)z.size(), grad_[d.y], dz.data(), Bl_, d.D, d.W);
+    }
+  }
+  // embedding gradients back to the owners (reverse exchange), then sparse SGD of the touched rows
+  if (!embs_.empty()) {
+    if (world_ > 1) {
+      int64_t o = 0;
+      for (int p = 0; p < world_; ++p)
+        for (size_t t = 0; t < embs_.size(); ++t) {
+          const Emb& e = embs_[t];
+          if (e.owner != p) continue;
+          eng_->copy(xrecv_ + o, grad_[e.y], (size_t)Bl_ * e.D * 4);
+          o += (int64_t)Bl_ * e.D;
+        }
+      eng_->all_to_all(xrecv_, xcount_recv_.data(), xsend_, xcount_send_.data());
+      o = 0;
+      for (int p = 0; p < world_; ++p)
+        for (size_t t = 0; t < embs_.size(); ++t) {
+          const Emb& e = embs_[t];
+          if (e.owner != rank_) continue;
+          eng_->copy(emb_full_[t] + (int64_t)p * Bl_ * e.D, xsend_ + o, (size_t)Bl_ * e.D * 4);
+          o += (int64_t)Bl_ * e.D;
+        }
+    }
+    for (size_t t = 0; t < embs_.size(); ++t) {
+      const Emb& e = embs_[t];
+      if (e.owner != rank_) continue;
+      eng_->emb_sgd(table_[t], e.rows, idx_[t], e.bag, world_ > 1 ? emb_full_[t] : grad_[e.y], B_, e.D, lr_);
     }
   }
   if (world_ > 1) eng_->allreduce_wait();
@@ -357,10 +674,27 @@ std::string Model::describe() const {
   std::ostringstream o;
   o << "native model: global batch " << B_ << " over " << world_ << " rank(s) (" << Bl_ << " per rank), engine "
     << (device_ == 1 ? "hip" : "cpu") << "\n";
-  for (size_t i = 0; i < ops_.size(); ++i) {
-    const Dense& d = ops_[i];
-    o << "  dense" << i << ": " << d.K << " -> " << d.N << " act " << d.act << (d.fuse_below ? " [dX epilogue: act' below]" : "")
-      << (d.grad_is_dpre ? " [grad arrives as dpre]" : "") << (d.skip_act_grad ? " [sigmoid folded into BCE]" : "") << "\n";
+  for (const Node& n : nodes_) {
+    if (n.kind == K_DENSE) {
+      const Dense& d = ops_[n.idx];
+      o << "  dense" << n.idx << ": " << d.K << " -> " << d.N << " act " << d.act
+        << (d.fuse_below ? " [dX epilogue: act' below]" : "") << (d.grad_is_dpre ? " [grad arrives as dpre]" : "")
+        << (d.skip_act_grad ? " [sigmoid folded into BCE]" : "") << "\n";
+    } else if (n.kind == K_EMB) {
+      const Emb& e = embs_[n.idx];
+      o << "  embedding" << n.idx << ": " << e.rows << " x " << e.D << " bag " << e.bag << " on rank " << e.owner
+        << (e.owner == rank_ ? " (local: global-batch lookups, sparse SGD)" : "") << "\n";
+    } else {
+      const Dot& d = dots_[n.idx];
+      o << "  dot interaction: " << d.in.size() << " features x " << d.D << " -> " << d.W << "\n";
+    }
+  }
+  if (!embs_.empty() && world_ > 1) {
+    o << "  embedding exchange (all-to-all) floats per peer: send";
+    for (auto c : xcount_send_) o << " " << c;
+    o << " / recv";
+    for (auto c : xcount_recv_) o << " " << c;
+    o << "\n";
   }
   o << "  flat parameters " << wplan_.numel << " floats, " << wplan_.buckets.size() << " all-reduce bucket(s)\n";
   for (auto& b : wplan_.buckets) {

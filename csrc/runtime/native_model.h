@@ -1,4 +1,7 @@
 // flexmi native model: graph -> per-rank execution plan -> execution, entirely in C++ (no Python).
+// Graphs: dense (MLP) chains, embedding tables and the DLRM dot interaction (a DLRM-shaped DAG:
+// bottom MLP + tables -> interaction -> top MLP); tables are placed table-wise over the ranks,
+// MLPs are data parallel.
 //
 // Reference: FFModel::compile / init_layers / forward / backward / update
 // (src/runtime/model.cc:374-1180) build the per-op regions, the replica gradient regions and
@@ -43,8 +46,30 @@ struct Dense {
   // plan
   bool grad_is_dpre = false;   // the consumer's dX epilogue already applied this layer's act'
   bool fuse_below = false;     // this layer's dX epilogue applies the producer layer's act'
+  int below = -1;              // dense node whose activation backward that is
   bool skip_act_grad = false;  // sigmoid folded into BCE
   bool need_dx = true;
+};
+
+// An embedding table (SUM bag lookups of one sparse input), placed WHOLE on one rank: table-wise
+// model parallelism (the reference's DLRM strategy, src/runtime/dlrm_strategy.cc:242-296; the
+// embedding op src/ops/embedding.cu:173-224).  The owner looks up the GLOBAL batch; an all-to-all
+// hands every rank its sample shard; the reverse all-to-all returns the row gradients, and the
+// owner applies sparse SGD to the touched rows (no dense table gradient).
+struct Emb {
+  int sparse = -1;             // sparse input id
+  int64_t rows = 0;
+  int D = 0, bag = 1;
+  int y = -1;                  // tensor id of the [local batch][D] output
+  int w = -1;                  // parameter entry id (the table)
+  int owner = 0;               // rank holding the table (plan)
+};
+
+// DLRM dot interaction (src/ops/tests/test_harness.py:96-186 DotCompressor; caveat C3):
+// y = [x | strictly-lower(Z Z^T) | 0 pad], Z = [x; e_1; ..; e_{F-1}] per sample
+struct Dot {
+  std::vector<int> in;         // tensor ids: bottom output first, then the embeddings
+  int y = -1, D = 0, W = 0, npairs = 0;
 };
 
 struct StepStat {
@@ -61,27 +86,56 @@ class Model {
   ~Model();
   int input(int features);
   int dense(int x, int out_dim, int act, bool bias);
+  // sparse index input [B][bag] (int64, the GLOBAL batch on every rank); returns its id
+  int sparse_input(int bag);
+  // embedding table rows x dim looked up by sparse input `sparse` (SUM over the bag); returns the
+  // [B][dim] output tensor id
+  int embedding(int sparse, int64_t rows, int dim);
+  // dot interaction of the bottom tensor and the embedding tensors (all [B][D]); the output width
+  // D + F(F-1)/2 is padded up to a multiple of pad_to
+  int dot_interaction(int bottom, const std::vector<int>& embs, int pad_to);
+  // table placement before compile (default: greedy by rows over the ranks)
+  void set_table_owner(int table, int rank);
   void compile(int loss_type, float lr, double bucket_mb);
-  void init_weights(uint64_t seed);            // Glorot-uniform weights, zero biases (host RNG)
+  void init_weights(uint64_t seed);            // Glorot-uniform weights, zero biases, U(+-sqrt(1/rows)) tables
   int num_params() const { return (int)pnumel_.size(); }
   int64_t param_numel(int i) const { return pnumel_.at(i); }
+  // tables: only the owner holds the rows (param_local(i) == false elsewhere)
+  bool param_local(int i) const;
+  int table_owner(int table) const { return embs_.at(table).owner; }
+  int num_tables() const { return (int)embs_.size(); }
   void set_param(int i, const float* host);
   void get_param(int i, float* host) const;
-  // x: the GLOBAL batch [B][features]; labels: [B] int32 (SCCE) or [B][out] float
-  StepStat train_step(const float* x, const void* labels);
+  // x: the GLOBAL dense batch [B][features]; sparse[s]: the GLOBAL [B][bag] int64 indices of
+  // sparse input s (null for a model without embeddings); labels: [B] int32 (SCCE) or [B][out]
+  StepStat train_step(const float* x, const void* labels) { return train_step(x, nullptr, labels); }
+  StepStat train_step(const float* x, const int64_t* const* sparse, const void* labels);
   std::string describe() const;
   const WeightPlan& weight_plan() const { return wplan_; }
 
  private:
+  enum Kind { K_DENSE = 0, K_EMB = 1, K_DOT = 2 };
+  struct Node {
+    int kind, idx;
+  };
+  int dense_out_node() const;
+  void check_tensor(int t, const char* what) const;
+
   int B_, Bl_, device_, rank_, world_;
   std::string rendezvous_;
   std::vector<int> cols_;                     // tensor id -> features
+  std::vector<int> consumers_;                // tensor id -> number of consumers
   int input_ = -1;
+  std::vector<Node> nodes_;                   // creation (= topological) order
   std::vector<Dense> ops_;
-  std::vector<int64_t> pnumel_;               // parameter entries (model order: w, b per layer)
-  std::vector<int> porder_;                   // backward order of entries
+  std::vector<Emb> embs_;
+  std::vector<Dot> dots_;
+  std::vector<int> sparse_bag_;
+  std::vector<int> entry_table_;              // parameter entry -> table id (-1: dense DP entry)
+  std::vector<int64_t> pnumel_;               // parameter entries (model order)
+  std::vector<int> porder_;                   // backward order of the dense entries
   WeightPlan wplan_;
-  std::vector<int64_t> pofs_;                 // entry -> flat offset
+  std::vector<int64_t> pofs_;                 // dense entry -> flat offset
   int loss_ = LOSS_MSE_AVG;
   float lr_ = 0.01f;
   bool compiled_ = false;
@@ -91,6 +145,12 @@ class Model {
   float* grads_ = nullptr;
   std::vector<float*> act_;                   // tensor id -> [Bl][cols]
   std::vector<float*> grad_;                  // tensor id -> [Bl][cols]
+  std::vector<float*> table_;                 // table id -> [rows][D] (owner only)
+  std::vector<float*> emb_full_;              // table id -> [B][D] owner-side lookups (world > 1)
+  std::vector<int64_t*> idx_;                 // table id -> [B][bag] indices (owner only)
+  float* xsend_ = nullptr;                    // all-to-all staging (world > 1)
+  float* xrecv_ = nullptr;
+  std::vector<int64_t> xcount_send_, xcount_recv_;
   float* probs_ = nullptr;                    // SCCE: softmax of the logits
   void* labels_ = nullptr;
   float* stats_ = nullptr;                    // [loss, correct] accumulators
@@ -120,9 +180,23 @@ class Engine {
   // before the update
   virtual void allreduce_start(float* buf, int64_t n) = 0;
   virtual void allreduce_wait() = 0;
+  // ---- embeddings / interaction / exchange (DLRM plans) ----
+  virtual void copy(void* dst, const void* src, size_t bytes) = 0;   // device -> device
+  // out[b] = sum_j W[idx[b][j]]  (b < B; an index outside [0, rows) contributes nothing)
+  virtual void emb_fwd(const float* W, int64_t rows, const int64_t* idx, int bag, float* out, int64_t B, int D) = 0;
+  // W[idx[b][j]] -= lr * g[b]  (duplicates accumulate)
+  virtual void emb_sgd(float* W, int64_t rows, const int64_t* idx, int bag, const float* g, int64_t B, int D, float lr) = 0;
+  // y[M][W] = [z0 | lower(Z Z^T) | 0] ; dz[i] = (S Z)_i (+ dy[:, :D] for i = 0), S = dG + dG^T
+  virtual void dot_fwd(const float* const* z, int F, float* y, int M, int D, int W) = 0;
+  virtual void dot_bwd(const float* const* z, int F, const float* dy, float* const* dz, int M, int D, int W) = 0;
+  // per-peer float counts; send / recv contiguous by peer
+  virtual void all_to_all(const float* send, const int64_t* send_counts, float* recv, const int64_t* recv_counts) = 0;
 };
 
-std::unique_ptr<Engine> make_cpu_engine();
+// CPU engine; world > 1 ranks (one process each) exchange through a HostComm in `rendezvous`
+// staging up to slot_bytes per rank
+std::unique_ptr<Engine> make_cpu_engine(int rank = 0, int world = 1, const std::string& rendezvous = "",
+                                        size_t slot_bytes = 0);
 // HIP engine (native_hip.cc): flexmi's gfx950 kernels, RCCL over the ranks of `rendezvous`
 std::unique_ptr<Engine> make_hip_engine(int rank, int world, const std::string& rendezvous);
 

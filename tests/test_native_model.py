@@ -118,3 +118,132 @@ def test_native_c_program_hip_engine_matches_cpu(tmp_path):
     for a, b in zip(c["final"], h["final"]):
         np.testing.assert_allclose(b, a, rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(h["losses"], c["losses"], rtol=1e-4)
+
+
+# ---------------------------------------------------------------------- native DLRM (table-wise)
+_DLRM_ROWS = [100, 50, 200, 30]
+
+
+def _build_dlrm_c(tmp_path):
+    if not os.path.exists(LIB):
+        pytest.skip("libflexmi_native_c.so not built")
+    exe = str(tmp_path / "native_dlrm")
+    subprocess.run(["gcc", "-O2", "-I" + os.path.join(ROOT, "csrc", "capi"), os.path.join(ROOT, "tests", "capi", "native_dlrm.c"),
+                    "-L" + os.path.join(ROOT, "flexmi"), "-Wl,-rpath," + os.path.join(ROOT, "flexmi"), "-lflexmi_native_c",
+                    "-o", exe], check=True)
+    ldd = subprocess.run(["ldd", exe], capture_output=True, text=True).stdout
+    assert "libpython" not in ldd and "libtorch" not in ldd, ldd
+    return exe
+
+
+def _parse_dlrm(prefix, world):
+    b = open(prefix + ".init.bin", "rb").read()
+    o = 0
+
+    def take(buf, fmt, n=1):
+        nonlocal o
+        v = np.frombuffer(buf, dtype=np.dtype(fmt), count=n, offset=o)
+        o += np.dtype(fmt).itemsize * n
+        return v
+    B, steps, npar = (int(v) for v in take(b, "<i4", 3))
+    init = []
+    for _ in range(npar):
+        n = int(take(b, "<i8")[0])
+        init.append(take(b, "<f4", n).copy())
+    batches = []
+    for _ in range(steps):
+        dense = take(b, "<f4", B * 13).reshape(B, 13).copy()
+        idx = take(b, "<i8", 4 * B).reshape(4, B).copy()
+        lab = take(b, "<f4", B).copy()
+        batches.append((dense, idx, lab))
+    ranks = []
+    for r in range(world):
+        rb = open(f"{prefix}.r{r}.bin", "rb").read()
+        o = 0
+        rk, n = (int(v) for v in take(rb, "<i4", 2))
+        assert rk == r and n == npar
+        final = []
+        for i in range(npar):
+            local = int(take(rb, "<i4")[0])
+            final.append(take(rb, "<f4", len(init[i])).copy() if local else None)
+        losses = take(rb, "<f8", steps).copy()
+        ranks.append((final, losses))
+    return dict(B=B, steps=steps, init=init, batches=batches, ranks=ranks)
+
+
+def _replay_dlrm(rec):
+    """The same DLRM, weights and batches through flexmi's Python executor (CPU, fp32, world 1)."""
+    from flexmi.core import ActiMode, AggrMode, DataType, FFConfig, FFModel, LossType, MetricsType, SGDOptimizer
+    B = rec["B"]
+    cfg = FFConfig()
+    cfg.batchSize, cfg.device, cfg.compute_dtype = B, "cpu", "fp32"
+    m = FFModel(cfg)
+    x = m.create_tensor([B, 13], name="dense")
+    h = m.dense(x, 32, ActiMode.AC_MODE_RELU)
+    h = m.dense(h, 16, ActiMode.AC_MODE_RELU)
+    sp = [m.create_tensor([B, 1], DataType.DT_INT64, name=f"sparse{i}") for i in range(4)]
+    embs = [m.embedding(s, r, 16, AggrMode.AGGR_MODE_SUM) for s, r in zip(sp, _DLRM_ROWS)]
+    z = m.dot_interaction(h, embs)
+    t = m.dense(z, 32, ActiMode.AC_MODE_RELU)
+    t = m.dense(t, 1, ActiMode.AC_MODE_SIGMOID)
+    m.compile(SGDOptimizer(m, 0.1), LossType.LOSS_BINARY_CROSSENTROPY, [MetricsType.METRICS_ACCURACY])
+    ex = m.init_layers()
+    assert len(m.parameters) == len(rec["init"])
+    for p, w in zip(m.parameters, rec["init"]):
+        p.set_weights(m, w.reshape(p.dims))
+    for dense, idx, lab in rec["batches"]:
+        ex.scatter_from_host(x, dense)
+        for s, ix in zip(sp, idx):
+            ex.scatter_from_host(s, ix.reshape(B, 1))
+        labt = m.get_label_tensor()
+        ex.scatter_from_host(labt, lab.reshape(labt.dims))
+        ex.train_step()
+    return [p.get_weights(m).reshape(-1) for p in m.parameters]
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_native_c_dlrm_tablewise_trains_like_the_executor(tmp_path, world):
+    """a C program trains a DLRM through libflexmi_native_c with no CPython --
+    embedding tables placed table-wise over `world` rank processes (global-batch lookups on the
+    owner, all-to-all to the sample shards and back, sparse SGD of the touched rows), DP MLPs
+    with bucketed all-reduce, dot interaction -- and ends with the Python executor's parameters."""
+    exe = _build_dlrm_c(tmp_path)
+    rdv = tmp_path / "rdv"
+    rdv.mkdir()
+    prefix = str(tmp_path / "run")
+    r = subprocess.run([exe, "cpu", prefix, "5", str(world), str(rdv)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "native_dlrm ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "dot interaction: 5 features" in r.stdout
+    if world > 1:
+        assert "embedding exchange (all-to-all)" in r.stdout and "on rank 1" in r.stdout
+    rec = _parse_dlrm(prefix, world)
+    got = _replay_dlrm(rec)
+    for i, want in enumerate(got):
+        holders = [f[i] for f, _ in rec["ranks"] if f[i] is not None]
+        assert holders, f"param {i} held by no rank"
+        for h in holders[1:]:            # DP replicas are bit-identical (rank-order reductions)
+            np.testing.assert_array_equal(h, holders[0])
+        np.testing.assert_allclose(holders[0], want, rtol=2e-5, atol=2e-6, err_msg=f"param {i}")
+    # the tables really are spread: each rank holds only its own
+    if world > 1:
+        tables = range(4, 8)
+        assert [sum(f[i] is not None for f, _ in rec["ranks"]) for i in tables] == [1, 1, 1, 1]
+        assert all(rec["ranks"][1][0][i] is not None for i in (5, 7))
+
+
+@pytest.mark.gpu
+def test_native_c_dlrm_hip_engine_matches_cpu(tmp_path):
+    """The same C program on the HIP engine (flexmi's embedding / interaction / GEMM kernels,
+    world 1) ends with the CPU engine's parameters."""
+    exe = _build_dlrm_c(tmp_path)
+    recs = {}
+    for dev in ("cpu", "hip"):
+        rdv = tmp_path / f"rdv_{dev}"
+        rdv.mkdir()
+        prefix = str(tmp_path / dev)
+        r = subprocess.run([exe, dev, prefix, "5", "1", str(rdv)], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0 and "native_dlrm ok" in r.stdout, (dev, r.stderr[-2000:])
+        recs[dev] = _parse_dlrm(prefix, 1)
+    for a, b in zip(recs["cpu"]["ranks"][0][0], recs["hip"]["ranks"][0][0]):
+        np.testing.assert_allclose(b, a, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(recs["hip"]["ranks"][0][1], recs["cpu"]["ranks"][0][1], rtol=1e-4)

@@ -154,7 +154,7 @@ def write_ninja(only=None):
         # the native model (csrc/runtime/native_model.cc) with its HIP engine (csrc/native/
         # native_hip.cc: flexmi's kernels + RCCL) -- libflexmi_kernels.so is the kernel objects
         # alone, no PyTorch
-        for src in [os.path.join(ROOT, "csrc", "runtime", "native_model.cc")]:
+        for src in [os.path.join(ROOT, "csrc", "runtime", "native_model.cc"), os.path.join(ROOT, "csrc", "runtime", "host_comm.cc")]:
             o = os.path.join(BUILD, "nc_" + os.path.basename(src).replace(".cc", ".o"))
             lines.append(f"build {o}: cxx {src}")
             lines.append(f"  extra = -I{ROOT}/csrc/capi")
