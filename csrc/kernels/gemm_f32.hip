@@ -1226,10 +1226,11 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
   }
   if (vec && variant >= 20000 && variant < 20100 && K > 0) {
     const int rc = (variant - 20000) % fm_gemm_f32_ring_cfg(0, nullptr);
-    int geo[4];
+    int geo[5];
     fm_gemm_f32_ring_cfg(rc, geo);
-    const struct { int bm, bn, bk; } c = {geo[0], geo[1], geo[2]};
-    if (K % c.bk == 0 && (a_kcontig || M % 4 == 0) && (b_kcontig || N % 4 == 0) && M >= 4 && N >= 4) {
+    const struct { int bm, bn, bk, mode; } c = {geo[0], geo[1], geo[2], geo[4]};
+    const bool pers_ok = c.mode == 0 || (rowsum_a == nullptr && batch == 1);
+    if (K % c.bk == 0 && (a_kcontig || M % 4 == 0) && (b_kcontig || N % 4 == 0) && M >= 4 && N >= 4 && pers_ok) {
       p.tiles_m = (M + c.bm - 1) / c.bm;
       p.tiles_n = (N + c.bn - 1) / c.bn;
       const long tiles = (long)p.tiles_m * p.tiles_n * batch;
@@ -1240,6 +1241,7 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
         while (tiles * ks < 256 && ks * 2 <= ktiles / 4 && ks < 16) ks *= 2;
       if (act_y != nullptr || colsum != nullptr) ks = 1;
       while (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks /= 2;
+      while (ks > 1 && c.mode != 0 && ktiles % ks != 0) ks /= 2;   // persistent: equal stages per unit
       p.ksplit = ks;
       if (ks > 1) fm_gemm_join(stream);
       fm_gemm_f32_ring_launch(&p, rc, a_kcontig, b_kcontig, 0, stream);

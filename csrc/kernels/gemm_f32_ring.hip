@@ -3,6 +3,8 @@
 // dispatcher (gemm_f32_run) selects it through fm_gemm_f32_ring_cfg / fm_gemm_f32_ring_launch.
 #include "gemm_f32_common.h"
 
+#include <algorithm>
+
 namespace {
 
 // ---- ring kernel: NS-stage LDS-DMA ring, one barrier per K-stage, fragment double buffer -------
@@ -241,41 +243,269 @@ void launch_ring(const GemmF& p, bool ak, bool bk, hipStream_t s) {
   else hipLaunchKernelGGL((fm_gemm_f32_ring_kernel<BM, BN, WM, WN, BK, NS, false, false, SGD>), grid, dim3(NTH), LDS, s, p);
 }
 
-// ring tile configurations (A/B index = FM_GEMM_F32_VARIANT - 20000)
-struct RCfg { int bm, bn, wm, wn, bk, ns; };
+// ---- persistent ring kernel ------------------------------------------------------------------
+// One block per CU slot loops over work units (tile, K-split) u = blockIdx.x + j * gridDim.x,
+// and the K-stage sequence runs ACROSS units: the prefetch (LDS-DMA ring, or register-staged
+// loads) of the next unit's first stages is in flight while this unit's last stage multiplies,
+// and its fragments are in registers before this unit's epilogue issues its stores -- so the
+// per-tile prologue (first loads) and epilogue (C stores) overlap MFMA work instead of bracketing
+// every tile of a one-tile-per-CU launch (measured on the fp32 MFMA probe, tools/mfma_probe.hip:
+// ~8-10 % of a 1024-wide DLRM GEMM).  Units of one block share an XCD (u % 8 fixed), and
+// xcd_remap_f hands each XCD contiguous tiles (shared A / B panels in its L2).
+//   MODE 1: LDS-DMA NS-stage ring (as the ring kernel);
+//   MODE 2: register-staged -- the stage after next is loaded into VGPRs (global_load_dwordx4)
+//           during this stage and written to the free LDS slot (ds_write_b128, swizzled) right
+//           before the stage's barrier: two LDS slots, no M0 / DMA issue cost.
+// Epilogues: the direct forms of epilogue_f32 (bias / act / act-bwd + column sums / beta / split-K
+// slabs / fused SGD, all from registers); no LDS epilogue (the ring is live across units), no
+// row sums (rowsum_a requests take the other kernels).
+template <bool KC, int R, int BK, int NTH>
+struct RegLd {
+  static constexpr int CH = R * BK / 4;          // 16-B chunks of the operand tile
+  static constexpr int PER_T = CH / NTH;
+  static_assert(PER_T >= 1 && CH % NTH == 0, "stage chunks must split evenly over the threads");
+  f32x4_t v[PER_T];
+  template <int T>
+  FM_DEVICE void load(const float* __restrict__ p, long ld, int row0, int rows, int k0, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int ci = tid + NTH * i;
+      const float* src;
+      if constexpr (KC) {
+        const int row = ci / (BK / 4), kc = ci % (BK / 4);
+        src = p + (long)min(row0 + row, rows - 1) * ld + k0 + 4 * kc;
+      } else {
+        const int k = ci / (R / 4), c = ci % (R / 4);
+        src = p + (long)(k0 + k) * ld + min(row0 + 4 * c, rows - 4);
+      }
+      v[i] = *reinterpret_cast<const f32x4_t*>(src);
+    }
+  }
+  template <int T>
+  FM_DEVICE void store(char* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int ci = tid + NTH * i;
+      int off;
+      if constexpr (KC) {
+        const int row = ci / (BK / 4), kc = ci % (BK / 4);
+        off = row * (BK * 4) + 16 * (kc ^ rk_swz<BK>(row));
+      } else {
+        const int k = ci / (R / 4), c = ci % (R / 4);
+        off = k * (R * 4) + 16 * (c ^ rm_swz<T>(k));
+      }
+      *reinterpret_cast<f32x4_t*>(lds + off) = v[i];
+    }
+  }
+};
+
+template <int BM, int BN, int WM, int WN, int BK, int NS, int MODE, bool AK, bool BKC, bool SGD>
+__global__ void __launch_bounds__(WM * WN * 64, 1) fm_gemm_f32_pring_kernel(GemmF p, int units, int nkt) {
+  constexpr int NTH = WM * WN * 64;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int MR = TM / 16, NR = TN / 16;
+  constexpr int CH = BK / 16;
+  constexpr int A_BYTES = BM * BK * 4;
+  constexpr int B_BYTES = BN * BK * 4;
+  constexpr int STG = A_BYTES + B_BYTES;
+  constexpr int SLOTS = MODE == 1 ? NS : 2;
+  using LA = RingLd<AK, BM, BK, MR, NTH>;
+  using LB = RingLd<BKC, BN, BK, NR, NTH>;
+  constexpr int LPS = LA::PER_W + LB::PER_W;
+  static_assert(MODE == 1 || MODE == 2, "mode");
+  static_assert(MODE == 2 || (NS >= 2 && NS <= 4 && 2 * LPS < 64), "ring depth / vmcnt range");
+  static_assert(CH >= 2 && CH % 2 == 0, "fragment double buffer needs an even chunk count");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int tiles = p.tiles_m * p.tiles_n;
+  const int nmy = units > (int)blockIdx.x ? (units - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
+  const int S = nmy * nkt;                          // this block's K-stages over all its units
+
+  // unit j of this block -> (m0, n0, first k-tile)
+  auto unit_geo = [&](int j, int& m0, int& n0, int& kt0, int& split) {
+    const int u = (int)blockIdx.x + j * (int)gridDim.x;
+    const int r = xcd_remap_f(u, units);
+    split = r / tiles;
+    const int tl = r % tiles;
+    int tm, tn;
+    if (p.n_fast) { tn = tl % p.tiles_n; tm = tl / p.tiles_n; }
+    else { tm = tl % p.tiles_m; tn = tl / p.tiles_m; }
+    m0 = tm * BM;
+    n0 = tn * BN;
+    kt0 = split * nkt;
+  };
+
+  RegLd<AK, BM, BK, NTH> ra;
+  RegLd<BKC, BN, BK, NTH> rb;
+  auto issue = [&](int g) {                         // MODE 1: DMA stage g into its ring slot
+    int m0, n0, kt0, sp;
+    unit_geo(g / nkt, m0, n0, kt0, sp);
+    char* base = smem + (g % SLOTS) * STG;
+    const int k0 = (kt0 + g % nkt) * BK;
+    LA::issue(p.A, p.lda, m0, p.M, k0, base, wave, lane);
+    LB::issue(p.B, p.ldb, n0, p.N, k0, base + A_BYTES, wave, lane);
+  };
+  auto reg_load = [&](int g) {                      // MODE 2: stage g into registers
+    int m0, n0, kt0, sp;
+    unit_geo(g / nkt, m0, n0, kt0, sp);
+    const int k0 = (kt0 + g % nkt) * BK;
+    ra.template load<MR>(p.A, p.lda, m0, p.M, k0, tid);
+    rb.template load<NR>(p.B, p.ldb, n0, p.N, k0, tid);
+  };
+  auto reg_store = [&](int g) {
+    char* base = smem + (g % SLOTS) * STG;
+    ra.template store<MR>(base, tid);
+    rb.template store<NR>(base + A_BYTES, tid);
+  };
+
+  f32x4_t acc[MR][NR];
+  float af[2][MR][4], bfr[2][NR][4];
+  if (S > 0) {
+    if constexpr (MODE == 1) {
+#pragma unroll
+      for (int s = 0; s < NS - 1; ++s)
+        if (s < S) issue(s);
+      ring_wait<LPS>(min(NS - 2, S - 1));
+    } else {
+      reg_load(0);
+      reg_store(0);
+      if (S > 1) reg_load(1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    ring_frags<AK, BM, BK, MR>(smem, wm * TM, 0, lane, af[0]);
+    ring_frags<BKC, BN, BK, NR>(smem + A_BYTES, wn * TN, 0, lane, bfr[0]);
+  }
+  int m0 = 0, n0 = 0, kt0 = 0, split = 0;
+  for (int g = 0; g < S; ++g) {
+    const int t = g % nkt;
+    if (t == 0) {
+      unit_geo(g / nkt, m0, n0, kt0, split);
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+    const char* la = smem + (g % SLOTS) * STG;
+    const char* lb = la + A_BYTES;
+    if constexpr (MODE == 1) {
+      if (g + NS - 1 < S) issue(g + NS - 1);
+    }
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int cur = c & 1, nxt = cur ^ 1;
+      if (c + 1 < CH) {
+        ring_frags<AK, BM, BK, MR>(la, wm * TM, c + 1, lane, af[nxt]);
+        ring_frags<BKC, BN, BK, NR>(lb, wn * TN, c + 1, lane, bfr[nxt]);
+      } else if (g + 1 < S) {
+        if constexpr (MODE == 1) {
+          ring_wait<LPS>(min(NS - 2, S - 2 - g));
+        } else {
+          // stage g+1 (in registers since stage g-1) -> the slot stage g-1 used; then the
+          // stage after next into registers
+          reg_store(g + 1);
+          if (g + 2 < S) reg_load(g + 2);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        const char* na = smem + ((g + 1) % SLOTS) * STG;
+        ring_frags<AK, BM, BK, MR>(na, wm * TM, 0, lane, af[nxt]);
+        ring_frags<BKC, BN, BK, NR>(na + A_BYTES, wn * TN, 0, lane, bfr[nxt]);
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+#pragma unroll
+          for (int j = 0; j < NR; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(bfr[cur][j][s], af[cur][i][s], acc[i][j], 0, 0, 0);
+    }
+    if (t == nkt - 1) epilogue_f32<MR, NR, !AK, !BKC, SGD>(p, acc, 0, split, m0 + wm * TM, n0 + wn * TN, lane);
+  }
+  if constexpr (MODE == 1) wait_vmcnt_f<0>();
+}
+
+template <int BM, int BN, int WM, int WN, int BK, int NS, int MODE, bool SGD>
+void launch_pring(const GemmF& p, bool ak, bool bk, hipStream_t s) {
+  constexpr int NTH = WM * WN * 64;
+  constexpr int LDS = (MODE == 1 ? NS : 2) * (BM + BN) * BK * 4;
+  static bool attr_set = false;
+  if (!attr_set) {
+    auto set = [](const void* f) { (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS); };
+    set((const void*)fm_gemm_f32_pring_kernel<BM, BN, WM, WN, BK, NS, MODE, true, true, SGD>);
+    set((const void*)fm_gemm_f32_pring_kernel<BM, BN, WM, WN, BK, NS, MODE, true, false, SGD>);
+    set((const void*)fm_gemm_f32_pring_kernel<BM, BN, WM, WN, BK, NS, MODE, false, true, SGD>);
+    set((const void*)fm_gemm_f32_pring_kernel<BM, BN, WM, WN, BK, NS, MODE, false, false, SGD>);
+    attr_set = true;
+  }
+  const int units = p.tiles_m * p.tiles_n * p.ksplit;
+  const int nkt = p.K / BK / p.ksplit;
+  // persistent grid = the blocks that are RESIDENT at once (occupancy API: VGPRs, LDS, waves);
+  // a statically assigned unit list on a block that only starts after another retired would
+  // serialise the launch
+  static int resident = 0;
+  if (resident == 0) {
+    int dev = 0, cus = 0, occ = 1 << 20;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const void* ks[4] = {(const void*)fm_gemm_f32_pring_kernel<BM, BN, WM, WN, BK, NS, MODE, true, true, SGD>,
+                         (const void*)fm_gemm_f32_pring_kernel<BM, BN, WM, WN, BK, NS, MODE, true, false, SGD>,
+                         (const void*)fm_gemm_f32_pring_kernel<BM, BN, WM, WN, BK, NS, MODE, false, true, SGD>,
+                         (const void*)fm_gemm_f32_pring_kernel<BM, BN, WM, WN, BK, NS, MODE, false, false, SGD>};
+    for (const void* k : ks) {   // the lowest occupancy of the four operand orientations
+      int o = 0;
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k, NTH, LDS);
+      occ = std::min(occ, std::max(1, o));
+    }
+    resident = std::max(1, cus) * occ;
+  }
+  const int grid = std::max(1, std::min(units, resident));
+  if (ak && bk) hipLaunchKernelGGL((fm_gemm_f32_pring_kernel<BM, BN, WM, WN, BK, NS, MODE, true, true, SGD>), dim3(grid), dim3(NTH), LDS, s, p, units, nkt);
+  else if (ak) hipLaunchKernelGGL((fm_gemm_f32_pring_kernel<BM, BN, WM, WN, BK, NS, MODE, true, false, SGD>), dim3(grid), dim3(NTH), LDS, s, p, units, nkt);
+  else if (bk) hipLaunchKernelGGL((fm_gemm_f32_pring_kernel<BM, BN, WM, WN, BK, NS, MODE, false, true, SGD>), dim3(grid), dim3(NTH), LDS, s, p, units, nkt);
+  else hipLaunchKernelGGL((fm_gemm_f32_pring_kernel<BM, BN, WM, WN, BK, NS, MODE, false, false, SGD>), dim3(grid), dim3(NTH), LDS, s, p, units, nkt);
+}
+
+// ring tile configurations (A/B index = FM_GEMM_F32_VARIANT - 20000); mode 0 = one tile per
+// block (ring kernel), 1 = persistent LDS-DMA ring, 2 = persistent register-staged
+struct RCfg { int bm, bn, wm, wn, bk, ns, mode; };
 constexpr RCfg kRCfgs[] = {
-    {128, 128, 2, 2, 32, 4},   // 0: 4 waves of 64x64 (1 per SIMD), 4 x 32 KB ring
-    {128, 128, 2, 2, 64, 2},   // 1: 4 waves of 64x64, 2 x 64 KB ring
-    {256, 128, 4, 2, 32, 3},   // 2: 8 waves of 64x64 (2 per SIMD), 3 x 48 KB ring
-    {64, 64, 2, 2, 64, 4},     // 3: 4 waves of 32x32, 4 x 32 KB ring (hipBLASLt's fp32 macro tile)
-    {128, 64, 2, 2, 32, 4},    // 4: 4 waves of 64x32, 4 x 24 KB ring
-    {128, 128, 2, 4, 32, 4},   // 5: 8 waves of 64x32 (2 per SIMD), 4 x 32 KB ring
-    {128, 128, 2, 2, 32, 3},   // 6: 3-deep ring (96 KB)
-    {64, 64, 2, 2, 32, 4},     // 7: 4 waves of 32x32, 4 x 16 KB ring (K % 32)
+    {128, 128, 2, 4, 32, 4, 0},   // 0: 8 waves of 64x32 (2 per SIMD), 4 x 32 KB ring
+    {128, 128, 2, 4, 32, 4, 1},   // 1: persistent, same tile and ring
+    {128, 128, 2, 4, 32, 2, 2},   // 2: persistent, register-staged, 64 KB (2 blocks / CU)
+    {256, 128, 4, 2, 32, 2, 2},   // 3: persistent, register-staged, 8 waves of 64x64, 96 KB
+    {256, 128, 4, 2, 32, 3, 1},   // 4: persistent, 3 x 48 KB ring, 8 waves of 64x64
+    {128, 64, 2, 2, 32, 2, 2},    // 5: persistent, register-staged, 4 waves of 64x32, 48 KB (3 blocks / CU)
+    {64, 64, 2, 2, 64, 2, 2},     // 6: persistent, register-staged, 4 waves of 32x32, BK 64 (hipBLASLt's tile)
+    {64, 64, 2, 2, 64, 4, 1},     // 7: persistent, 4 x 32 KB ring, 4 waves of 32x32
 };
 constexpr int kNumRCfgs = sizeof(kRCfgs) / sizeof(kRCfgs[0]);
 
 template <bool SGD>
 void launch_ring_cfg(int c, const GemmF& p, bool ak, bool bk, hipStream_t s) {
   switch (c) {
-    case 0: launch_ring<128, 128, 2, 2, 32, 4, SGD>(p, ak, bk, s); break;
-    case 1: launch_ring<128, 128, 2, 2, 64, 2, SGD>(p, ak, bk, s); break;
-    case 2: launch_ring<256, 128, 4, 2, 32, 3, SGD>(p, ak, bk, s); break;
-    case 3: launch_ring<64, 64, 2, 2, 64, 4, SGD>(p, ak, bk, s); break;
-    case 4: launch_ring<128, 64, 2, 2, 32, 4, SGD>(p, ak, bk, s); break;
-    case 5: launch_ring<128, 128, 2, 4, 32, 4, SGD>(p, ak, bk, s); break;
-    case 6: launch_ring<128, 128, 2, 2, 32, 3, SGD>(p, ak, bk, s); break;
-    default: launch_ring<64, 64, 2, 2, 32, 4, SGD>(p, ak, bk, s); break;
+    case 0: launch_ring<128, 128, 2, 4, 32, 4, SGD>(p, ak, bk, s); break;
+    case 1: launch_pring<128, 128, 2, 4, 32, 4, 1, SGD>(p, ak, bk, s); break;
+    case 2: launch_pring<128, 128, 2, 4, 32, 2, 2, SGD>(p, ak, bk, s); break;
+    case 3: launch_pring<256, 128, 4, 2, 32, 2, 2, SGD>(p, ak, bk, s); break;
+    case 4: launch_pring<256, 128, 4, 2, 32, 3, 1, SGD>(p, ak, bk, s); break;
+    case 5: launch_pring<128, 64, 2, 2, 32, 2, 2, SGD>(p, ak, bk, s); break;
+    case 6: launch_pring<64, 64, 2, 2, 64, 2, 2, SGD>(p, ak, bk, s); break;
+    default: launch_pring<64, 64, 2, 2, 64, 4, 1, SGD>(p, ak, bk, s); break;
   }
 }
 
-
 }  // namespace
 
-// tile geometry of ring configuration c: {bm, bn, bk, ns}; returns the number of configurations
+// tile geometry of ring configuration c: {bm, bn, bk, ns, mode}; returns the number of configurations
 extern "C" int fm_gemm_f32_ring_cfg(int c, int* geo) {
   if (c >= 0 && c < kNumRCfgs && geo) {
     geo[0] = kRCfgs[c].bm; geo[1] = kRCfgs[c].bn; geo[2] = kRCfgs[c].bk; geo[3] = kRCfgs[c].ns;
+    geo[4] = kRCfgs[c].mode;
   }
   return kNumRCfgs;
 }

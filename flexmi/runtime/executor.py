@@ -1055,10 +1055,13 @@ class Executor:
         per step).  E's backward is unchanged: D's backward still writes E's output gradients,
         reading the (not yet updated) table rows the same way.  Reference: the embedding writes
         its output and the interaction/concat re-reads it (src/ops/embedding.cu:173-224,
-        src/ops/concat.cu:159-235).  FM_EMB_GATHER=0 turns it off (A/B); off under --debug and
-        for micro-batch-pipelined tails (XCHG_CHUNKS_LOCAL)."""
+        src/ops/concat.cu:159-235).  OPT-IN (FM_EMB_GATHER=1): measured on the DLRM MLPerf fp32
+        step it LOSES 33 us (1.492 vs 1.459 ms/step, profiles/emb_gather_ab_r5c.txt) -- unfused,
+        the embedding forward runs on a side stream under the bottom MLP, fused the random row
+        gather sits on the critical path inside the interaction kernel.  Off under --debug and for
+        micro-batch-pipelined tails (XCHG_CHUNKS_LOCAL)."""
         from flexmi.core.types import AggrMode, OperatorType
-        if (self.backend != "hip" or self.debug or XCHG_LOCAL or os.environ.get("FM_EMB_GATHER", "1") == "0"):
+        if (self.backend != "hip" or self.debug or XCHG_LOCAL or os.environ.get("FM_EMB_GATHER", "0") != "1"):
             return
         for d in ops:
             if d.op_type != OperatorType.OP_DOT_INTERACTION:
