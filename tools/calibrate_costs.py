@@ -81,6 +81,10 @@ def main():
         db["entries"].update(old.get("entries", {}))
         if "group_factor" in old:                      # measured on a DLRM run; keep it
             db["group_factor"] = old["group_factor"]
+        # per-type scales of op types another model's run already fitted stay (a DB serves several
+        # models: refitting OP_LINEAR on InceptionV3's one classifier would rescale every
+        # unmeasured DLRM MLP shape); --refresh TYPE refits them
+        db["scale_keep"] = {t: v for t, v in old.get("scale", {}).items() if t not in a.refresh.split(",")}
     cm = CostModel(MachineModel.mi355x(1), db_path="", dtype_bytes=4 if a.dtype == "fp32" else 2)
     t0 = time.time()
     done = 0
@@ -124,11 +128,13 @@ def main():
 
 def _write(path, db, todo, cm):
     roof = {k: cm.roofline(*todo[k]) for k in db["entries"] if k in todo}
-    db["scale"] = {t: round(v, 4) for t, v in cm.fit_scales(
-        {k: tuple(v) for k, v in db["entries"].items()}, roof).items()}
-    os.makedirs(os.path.dirname(path), exist_ok=True)
+    fit = {t: round(v, 4) for t, v in cm.fit_scales({k: tuple(v) for k, v in db["entries"].items()}, roof).items()}
+    keep = db.get("scale_keep", {})
+    db["scale"] = {**fit, **keep}
+    out = {k: v for k, v in db.items() if k != "scale_keep"}
+    os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
     with open(path, "w") as f:
-        json.dump(db, f, indent=0, sort_keys=True)
+        json.dump(out, f, indent=0, sort_keys=True)
 
 
 if __name__ == "__main__":

@@ -48,6 +48,38 @@ def describe(model, strat, n):
     return sp, sub, ch
 
 
+def explain(model, r, n, top=12):
+    """Why the searched strategy differs from DP: every op the search moved off data parallelism,
+    its config and the simulated step-time cost of putting just that op back on DP (positive = the
+    move pays), with the op's weight bytes (gradient all-reduce volume under DP)."""
+    g = r.graph
+    dp = g.dp_assign()
+    rows = []
+    for i, op in enumerate(g.ops):
+        if r.assign[i] == dp[i]:
+            continue
+        a = list(r.assign)
+        a[i] = dp[i]
+        delta = g.simulate(a) - r.best_us
+        wb = sum(_numel(w.dims) for w in op.weights) * 4
+        pc = g.cands[i][r.assign[i]]
+        rows.append((delta, op.name, op.op_type.name, list(pc.dims), len(set(pc.device_ids)), wb))
+    rows.sort(reverse=True)
+    out = [f"#   {n} GPUs: {len(rows)} ops off DP; the {min(top, len(rows))} that matter most "
+           f"(delta = simulated ms/step added by reverting only that op to DP):"]
+    for delta, name, t, dims, nd, wb in rows[:top]:
+        out.append(f"#     {name:28s} {t:12s} dims={dims} on {nd} GPU(s), weights {wb / 2**20:7.2f} MiB, "
+                   f"delta {delta / 1e3:+.3f} ms")
+    return out
+
+
+def _numel(d):
+    n = 1
+    for v in d:
+        n *= v
+    return n
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dtype", default="bf16", choices=["fp32", "bf16"])
@@ -61,6 +93,7 @@ def main():
           f"PROJECTIONS (measured MI355X cost DB, xGMI machine model); MCMC budget {a.budget} from data parallelism")
     print(f"{'gpus':>4s} {'batch':>6s} {'dp_ms':>9s} {'search_ms':>9s} {'search/dp':>9s} {'img/s(search)':>14s} "
           f"{'spatial':>7s} {'subset':>6s} {'channel':>7s} {'secs':>6s}")
+    notes = []
     for n in [int(x) for x in a.gpus.split(",")]:
         m = build(n, a.per_gpu, a.dtype, a.image)
         t0 = time.time()
@@ -69,6 +102,10 @@ def main():
         print(f"{n:4d} {m.config.batchSize:6d} {r.dp_us / 1e3:9.3f} {r.best_us / 1e3:9.3f} {r.speedup_vs_dp:9.3f} "
               f"{m.config.batchSize / (r.best_us * 1e-6):14.0f} {sp:7d} {sub:6d} {ch:7d} {time.time() - t0:6.1f}",
               flush=True)
+        if n > 1:
+            notes += explain(m, r, n)
+    for line in notes:
+        print(line)
 
 
 if __name__ == "__main__":
