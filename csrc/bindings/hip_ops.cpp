@@ -27,11 +27,17 @@ int fm_gemm(const void* A, long lda, long sA, int a_kcontig, const void* B, long
             int act, float* ws, long ws_bytes, int ksplit_req, const void* act_y, long lday, int bwd_act,
             float* colsum, float* rowsum_a, hipStream_t stream);
 void fm_gemm_f32_set_split(int on);
+void fm_embedding_set_bwd_mode(int count);
 int fm_gemm_f32_get_split();
 int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, const float* B, long ldb, long sB, int b_kcontig,
                 float* C, long ldc, long sC, const float* bias, int M, int N, int K, int batch, float alpha, int beta,
                 int act, float* ws, long ws_bytes, int ksplit_req, const float* act_y, long lday, int bwd_act,
                 float* colsum, float* rowsum_a, hipStream_t stream);
+int fm_smallk_fwd_f32_launch(const float* x, long ldx, const float* w, const float* bias, float* y, long ldy, long M,
+                             int K, int N, int act, hipStream_t s);
+int fm_smallk_dw_f32_launch(const float* dpre, long ldd, const float* x, long ldx, float* dw, float* db, long M, int K,
+                            int N, float* ws, long ws_bytes, float* V, unsigned short* Wc, const float* lr, float wd,
+                            float mom, int nesterov, hipStream_t s);
 void fm_skinny_fwd_f32_launch(const float* x, long ldx, const float* w, const float* bias, float* y, long ldy, long B, int K,
                               int act, hipStream_t s);
 void fm_skinny_bwd_f32_launch(const float* x, long ldx, const float* w, const float* y, long ldy, const float* dy, long lddy,
@@ -287,6 +293,50 @@ int gemm_dw_sgd(torch::Tensor dpre, torch::Tensor x, torch::Tensor W, c10::optio
                         (unsigned short*)mptr(Wc), (float*)mptr(V), lr.data_ptr<float>(), (float)wd, (float)mom,
                         nesterov ? 1 : 0, (int)Nout, (int)Kin, (int)B, ws.data_ptr<float>(), ws.numel() * 4,
                         (float*)mptr(db), cur());
+}
+
+// thin-input fp32 Linear (gemm_small.hip): y = act(x W^T + b) for in_features K <= 32, K % 4 == 0.
+// Returns false (nothing launched) when the shape / alignment is outside the kernel's limits.
+bool smallk_fwd(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor y, int64_t act) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.scalar_type() == torch::kFloat32 && w.scalar_type() == torch::kFloat32 && y.scalar_type() == torch::kFloat32,
+              "smallk_fwd: fp32");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2 && w.is_contiguous() && x.stride(1) == 1 && y.stride(1) == 1 &&
+                  w.size(1) == x.size(1) && y.size(0) == x.size(0) && y.size(1) == w.size(0),
+              "smallk_fwd: x [M, K], w [N, K], y [M, N]");
+  if (bias.has_value() && bias->defined())
+    TORCH_CHECK(bias->scalar_type() == torch::kFloat32 && bias->numel() == w.size(0), "smallk_fwd: bias [N] fp32");
+  return fm_smallk_fwd_f32_launch(x.data_ptr<float>(), x.stride(0), w.data_ptr<float>(), (const float*)mptr(bias),
+                                  y.data_ptr<float>(), y.stride(0), x.size(0), (int)x.size(1), (int)w.size(0), (int)act,
+                                  cur()) == 0;
+}
+
+// dW [N, K] += dpre^T x and db [N] += colsum(dpre) (gemm_small.hip, deterministic two-pass); with lr
+// the SGD step is applied to W = dw in the same pass instead (V / Wc optional, like gemm_dw_sgd).
+bool smallk_dw(torch::Tensor dpre, torch::Tensor x, torch::Tensor dw, c10::optional<torch::Tensor> db, torch::Tensor ws,
+               c10::optional<torch::Tensor> V, c10::optional<torch::Tensor> Wc, c10::optional<torch::Tensor> lr, double wd,
+               double mom, bool nesterov) {
+  check_cuda(dpre, "dpre");
+  TORCH_CHECK(dpre.scalar_type() == torch::kFloat32 && x.scalar_type() == torch::kFloat32 && dw.scalar_type() == torch::kFloat32 &&
+                  ws.scalar_type() == torch::kFloat32,
+              "smallk_dw: fp32");
+  const int64_t M = dpre.size(0), N = dpre.size(1), K = x.size(1);
+  TORCH_CHECK(x.size(0) == M && dpre.stride(1) == 1 && x.stride(1) == 1 && dw.is_contiguous() && dw.numel() == N * K,
+              "smallk_dw: dpre [M, N], x [M, K], dw [N, K]");
+  if (db.has_value() && db->defined()) TORCH_CHECK(db->scalar_type() == torch::kFloat32 && db->numel() >= N, "smallk_dw: db");
+  const bool upd = lr.has_value() && lr->defined();
+  if (upd) {
+    TORCH_CHECK(lr->scalar_type() == torch::kFloat32 && lr->is_cuda(), "smallk_dw: lr device fp32 scalar");
+    TORCH_CHECK(mom <= 0.0 || (V.has_value() && V->defined()), "smallk_dw: momentum needs V");
+    if (V.has_value() && V->defined()) TORCH_CHECK(V->is_contiguous() && V->numel() == dw.numel(), "smallk_dw: V");
+    if (Wc.has_value() && Wc->defined())
+      TORCH_CHECK(Wc->scalar_type() == torch::kBFloat16 && Wc->is_contiguous() && Wc->numel() == dw.numel(), "smallk_dw: Wc");
+  }
+  return fm_smallk_dw_f32_launch(dpre.data_ptr<float>(), dpre.stride(0), x.data_ptr<float>(), x.stride(0),
+                                 dw.data_ptr<float>(), (float*)mptr(db), M, (int)K, (int)N, ws.data_ptr<float>(),
+                                 ws.numel() * 4, upd ? (float*)mptr(V) : nullptr,
+                                 upd ? (unsigned short*)mptr(Wc) : nullptr, upd ? lr->data_ptr<float>() : nullptr,
+                                 (float)wd, (float)mom, nesterov ? 1 : 0, cur()) == 0;
 }
 
 void skinny_fwd(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, torch::Tensor y, int64_t act) {
@@ -1167,6 +1217,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_set_variant", [](int v) { fm_gemm_set_variant(v); });
   m.def("gemm_f32_set_variant", [](int v) { fm_gemm_f32_set_variant(v); });
   m.def("init_fill", &init_fill);
+  m.def("smallk_fwd", &smallk_fwd);
+  m.def("smallk_dw", &smallk_dw);
   m.def("skinny_fwd", &skinny_fwd);
   m.def("skinny_bwd", &skinny_bwd);
   m.def("conv_scratch", &conv_scratch);
@@ -1180,8 +1232,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("cnhwc_wprep", &cnhwc_wprep);
   m.def("conv_nhwc_fwd", &conv_nhwc_fwd);
   m.def("conv_nhwc_dgrad", &conv_nhwc_dgrad);
-  m.def("gemm_f32_set_split", [](bool on) { fm_gemm_f32_set_split(on ? 1 : 0); });
-  m.def("gemm_f32_get_split", []() { return fm_gemm_f32_get_split() != 0; });
+  // 0 = native fp32 MFMA, 1 = split-bf16 kernel (gemm_f32.hip x3), 2 = its second form (gemm_x3.hip);
+  // bools map to 0 / 1 for the older callers
+  m.def("gemm_f32_set_split", [](int mode) { fm_gemm_f32_set_split(mode); });
+  m.def("gemm_f32_get_split", []() { return fm_gemm_f32_get_split(); });
+  // sparse-SGD kernels of tables with slot buffers: 1 = count / update, 0 = claim / dup / owner
+  m.def("embedding_set_bwd_mode", [](bool count) { fm_embedding_set_bwd_mode(count ? 1 : 0); });
   m.def("conv_nhwc_dgrad_strided", &conv_nhwc_dgrad_strided);
   m.def("conv_nhwc_wgrad", &conv_nhwc_wgrad);
   m.def("conv_s2d", &conv_s2d);

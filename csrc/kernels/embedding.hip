@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 namespace {
@@ -463,6 +464,81 @@ __global__ void __launch_bounds__(256) fm_emb_owner_multi(ClaimSet s, const floa
   if (blockIdx.x == 0 && threadIdx.x == 0) *d.ndup = 0;   // the dup kernel has finished reading it
 }
 
+// ---- count-based sparse SGD (FM_EMB_BWD=count): two launches for every non-tiny table ---------
+// count: every in-shard lookup e adds one to its row's slot (slot = lookups - 1; -1 = untouched)
+// and records in own[e] (the dups array) whether it arrived first.  update: a lookup whose row was
+// hit exactly once (slot == 0) applies a plain 16-B read-modify-write and frees the slot; rows hit
+// more often take float atomics (lane = column: 256 contiguous bytes per wave-instruction) and
+// their first arrival frees the slot.  A freed slot reads -1, never 0, so the plain path stays
+// exclusive to single-lookup rows whatever the order of the lookups -- the claim / dup / owner
+// kernels' work in one pass, and the mid-size tables (where most rows repeat) no longer need a
+// kernel of their own.
+template <bool I64>
+__global__ void __launch_bounds__(256) fm_emb_count_multi(ClaimSet s, long B) {
+  const ClaimDesc& d = s.t[blockIdx.y];
+  const long n = B * d.bag;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    bool ok;
+    const long r = local_row(ldi<I64>(d.idx, e), d.lo, d.rows, ok);
+    int own = 0;
+    if (ok) own = atomicAdd(d.owner + r, 1) == -1;
+    d.dups[e] = own;
+  }
+}
+
+template <typename GT, bool I64>
+__global__ void __launch_bounds__(256) fm_emb_update_multi(ClaimSet s, const float* __restrict__ lr, long B) {
+  const ClaimDesc& d = s.t[blockIdx.y];
+  const float mul = -lr[0] * d.scale;
+  const int D4 = d.D >> 2;
+  const int lpr = D4 < 64 ? D4 : 64;
+  const int rpi = 256 / lpr;
+  const int sub = threadIdx.x / lpr, lc = threadIdx.x - sub * lpr;
+  const long n = B * d.bag;
+  const GT* dy = reinterpret_cast<const GT*>(d.dy);
+  if (sub >= rpi) return;
+  for (long e = (long)blockIdx.x * rpi + sub; e < n; e += (long)gridDim.x * rpi) {
+    bool ok;
+    const long r = local_row(ldi<I64>(d.idx, e), d.lo, d.rows, ok);
+    if (!ok) continue;                                // uniform across the row's lanes
+    const int c = __hip_atomic_load(d.owner + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int own = d.dups[e];
+    const long b = e / d.bag;
+    const GT* g = dy + b * d.ld;
+    float* wr = d.W + r * d.D;
+    if (c == 0) {                                     // the row's only lookup: plain 16-B RMW
+      for (int c4 = lc; c4 < D4; c4 += lpr) {
+        const int col = c4 * 4;
+        f32x4_t* wp = reinterpret_cast<f32x4_t*>(wr + col);
+        f32x4_t w = *wp;
+        if constexpr (sizeof(GT) == 2) {
+          const bf16x4_t gv = *reinterpret_cast<const bf16x4_t*>(g + col);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) w[j] += mul * bf2f((unsigned short)gv[j]);
+        } else {
+          w += mul * *reinterpret_cast<const f32x4_t*>(g + col);
+        }
+        *wp = w;
+      }
+    } else {                                          // repeated row: lane = column atomics
+      for (int col = lc; col < d.D; col += lpr) atomicAdd(wr + col, mul * ld<GT>(g + col));
+    }
+    if (lc == 0 && (c == 0 || own)) __hip_atomic_store(d.owner + r, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <bool I64>
+void launch_count(const ClaimSet& s, int m, bool dy_bf16, const float* lr, long B, int maxbag, int minD4,
+                  hipStream_t st) {
+  const long n = B * maxbag;
+  dim3 gc((unsigned)std::max<long>(1, std::min<long>((n + 255) / 256, 1024)), m);
+  hipLaunchKernelGGL((fm_emb_count_multi<I64>), gc, dim3(256), 0, st, s, B);
+  const int rpi = 256 / std::min(64, std::max(1, minD4));
+  dim3 gu((unsigned)std::max<long>(1, std::min<long>((n + rpi - 1) / rpi, 2048)), m);
+  if (dy_bf16) hipLaunchKernelGGL((fm_emb_update_multi<unsigned short, I64>), gu, dim3(256), 0, st, s, lr, B);
+  else hipLaunchKernelGGL((fm_emb_update_multi<float, I64>), gu, dim3(256), 0, st, s, lr, B);
+}
+
 template <bool I64>
 void launch_claim(const ClaimSet& s, int m, bool dy_bf16, const float* lr, long B, int maxbag, int minD4,
                   hipStream_t st) {
@@ -648,13 +724,19 @@ extern "C" void fm_embedding_fwd_multi(int n, const float* const* W, const void*
   }
 }
 
+static int g_emb_count = -1;   // -1: from FM_EMB_BWD at the first call
+extern "C" void fm_embedding_set_bwd_mode(int count) { g_emb_count = count ? 1 : 0; }
+
 // lr != nullptr: fused sparse SGD into W; lr == nullptr: W is a dense grad buffer (accumulate).
 extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const* idx, const int* idx64,
                                        const void* const* dy, const long* ldg, const long* lo, const int* rows, const int* D,
                                        const int* bag, const float* scale, int dy_bf16, const float* lr, long B,
                                        int* const* owner, int* const* dups, int* const* ndup, hipStream_t st) {
   if (B <= 0) return;
-  // owner-computes path: fused SGD, claim buffers given, 16-B rows
+  // owner-computes path: fused SGD, claim buffers given, 16-B rows; FM_EMB_BWD=count: the
+  // count / update pair instead of claim / dup / owner (the buffers are the same)
+  if (g_emb_count < 0) g_emb_count = getenv("FM_EMB_BWD") != nullptr && strcmp(getenv("FM_EMB_BWD"), "count") == 0;
+  const bool count_mode = g_emb_count == 1;
   auto claimable = [&](int k) {
     return lr != nullptr && owner != nullptr && owner[k] != nullptr && D[k] % 4 == 0 && ldg[k] % 4 == 0 &&
            D[k] <= 256;
@@ -675,8 +757,14 @@ extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const
         minD4 = std::min(minD4, D[k] / 4);
       }
       s.n = m;
-      if (wide) launch_claim<true>(s, m, dy_bf16, lr, B, maxbag, minD4, st);
-      else launch_claim<false>(s, m, dy_bf16, lr, B, maxbag, minD4, st);
+      if (count_mode) {
+        if (wide) launch_count<true>(s, m, dy_bf16, lr, B, maxbag, minD4, st);
+        else launch_count<false>(s, m, dy_bf16, lr, B, maxbag, minD4, st);
+      } else if (wide) {
+        launch_claim<true>(s, m, dy_bf16, lr, B, maxbag, minD4, st);
+      } else {
+        launch_claim<false>(s, m, dy_bf16, lr, B, maxbag, minD4, st);
+      }
     }
   }
   // kind: 0 tiny (wave-private LDS copies), 1 small (block-shared LDS copy), 2 regular (atomics)

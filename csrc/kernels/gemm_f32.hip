@@ -520,6 +520,8 @@ __global__ void __launch_bounds__(256) fm_gemm_f32_reduce_bwd(GemmF p, int RB) {
 
 }  // namespace
 
+// the split-bf16 kernel, second form (gemm_x3.hip)
+extern "C" int fm_gemm_x3v2_launch(const void* params, int bm, int a_kcontig, int b_kcontig, int sgd, hipStream_t s);
 // the ring-form kernel (gemm_f32_ring.hip)
 extern "C" int fm_gemm_f32_ring_cfg(int c, int* geo);
 extern "C" void fm_gemm_f32_ring_launch(const void* params, int c, int a_kcontig, int b_kcontig, int sgd,
@@ -1115,8 +1117,12 @@ extern "C" void fm_gemm_f32_set_variant(int v) { g_f32_variant = v; }
 //   A_kcontig: A stored [M][K] (lda >= K) else [K][M] (lda >= M)
 //   B_kcontig: B stored [N][K] (ldb >= K) else [K][N] (ldb >= N)
 static int g_f32_split = -1;   // -1: from FM_F32_SPLIT at the first call
-extern "C" void fm_gemm_f32_set_split(int on) { g_f32_split = on ? 1 : 0; }
-extern "C" int fm_gemm_f32_get_split() { return g_f32_split == 1 ? 1 : 0; }
+extern "C" void fm_gemm_f32_set_split(int on) { g_f32_split = on < 0 ? 0 : on; }
+static int f32_split_mode() {
+  if (g_f32_split < 0) g_f32_split = getenv("FM_F32_SPLIT") != nullptr ? std::max(0, atoi(getenv("FM_F32_SPLIT"))) : 0;
+  return g_f32_split;
+}
+extern "C" int fm_gemm_f32_get_split() { return f32_split_mode(); }
 
 struct SgdUpdF {
   float* w; unsigned short* wc; float* v; const float* lr; float wd, mom; int nest;
@@ -1183,7 +1189,43 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
   p.atomic = 0;
   // fp32 on the bf16 matrix cores (exact three-way operand split, fm_gemm_x3_kernel): FM_F32_SPLIT=1
   // or fm_gemm_f32_set_split(1)
-  if (g_f32_split < 0) g_f32_split = (getenv("FM_F32_SPLIT") != nullptr && atoi(getenv("FM_F32_SPLIT")) == 1) ? 1 : 0;
+  f32_split_mode();
+  // second split form (gemm_x3.hip): split in the register staging pass, double-buffered planes,
+  // 64x64 per wave; FM_F32_SPLIT=2.  K-contiguous operands need 16-B rows, MN-contiguous ones 8-B
+  // pairs of rows (even row counts).
+  if (g_f32_split == 2 && K > 0 && K % 32 == 0 && M >= 64 && N >= 64) {
+    auto opnd_ok = [&](const float* X, long ld, long sX, bool kc, int rows) {
+      return kc ? (al(X) && ld % 4 == 0 && sX % 4 == 0)
+                : ((((uintptr_t)X) & 7) == 0 && ld % 2 == 0 && sX % 2 == 0 && rows % 2 == 0);
+    };
+    if (opnd_ok(A, lda, sA, a_kcontig, M) && opnd_ok(B, ldb, sB, b_kcontig, N)) {
+      // 256x128 (8 waves, 2 per SIMD) whenever M fills it, split-K for the grid; FM_X3_BM=128 forces
+      // the 4-wave 128x128 tile
+      static const int bm_env = getenv("FM_X3_BM") ? atoi(getenv("FM_X3_BM")) : 0;
+      const int bm = (bm_env == 128 || bm_env == 256) ? bm_env : (M >= 256 ? 256 : 128);
+      p.tiles_m = (M + bm - 1) / bm;
+      p.tiles_n = (N + 127) / 128;
+      const long tiles = (long)p.tiles_m * p.tiles_n * batch;
+      const int ktiles = K / 32;
+      const bool fused = act_y != nullptr || colsum != nullptr;
+      int ks = 1;
+      if (ksplit_req > 0) ks = ksplit_req;
+      else if (ws != nullptr && !fused)
+        while (tiles * ks < 256 && ks * 2 <= ktiles / 4 && ks < 16) ks *= 2;
+      if (fused) ks = 1;
+      while (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks /= 2;
+      p.ksplit = ks;
+      if (ks > 1) fm_gemm_join(stream);
+      if (fm_gemm_x3v2_launch(&p, bm, a_kcontig, b_kcontig, upd != nullptr && ks == 1, stream) == 0) {
+        if (ks > 1) {
+          const int v4 = (N % 4 == 0) && (ldc % 4 == 0) && (sC % 4 == 0) && al(C);
+          const long total = (long)M * N * batch / (v4 ? 4 : 1);
+          launch_reduce_f32(p, v4, total, stream);
+        }
+        return ks;
+      }
+    }
+  }
   if (g_f32_split == 1 && !upd && K >= 64 && M >= 64 && N >= 64) {
     const bool fused = act_y != nullptr || colsum != nullptr;
     p.tiles_m = (M + 127) / 128;
@@ -1229,7 +1271,7 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
     int geo[5];
     fm_gemm_f32_ring_cfg(rc, geo);
     const struct { int bm, bn, bk, mode; } c = {geo[0], geo[1], geo[2], geo[4]};
-    const bool pers_ok = c.mode == 0 || (rowsum_a == nullptr && batch == 1);
+    const bool pers_ok = c.mode == 0 || batch == 1;
     if (K % c.bk == 0 && (a_kcontig || M % 4 == 0) && (b_kcontig || N % 4 == 0) && M >= 4 && N >= 4 && pers_ok) {
       p.tiles_m = (M + c.bm - 1) / c.bm;
       p.tiles_n = (N + c.bn - 1) / c.bn;

@@ -257,8 +257,10 @@ void launch_ring(const GemmF& p, bool ak, bool bk, hipStream_t s) {
 //           during this stage and written to the free LDS slot (ds_write_b128, swizzled) right
 //           before the stage's barrier: two LDS slots, no M0 / DMA issue cost.
 // Epilogues: the direct forms of epilogue_f32 (bias / act / act-bwd + column sums / beta / split-K
-// slabs / fused SGD, all from registers); no LDS epilogue (the ring is live across units), no
-// row sums (rowsum_a requests take the other kernels).
+// slabs / fused SGD, all from registers); no LDS epilogue (the ring is live across units).  The
+// dW GEMMs' folded bias gradient (row sums of the MN-contiguous A tiles, tn == 0 units) is summed
+// from the staged A image per stage, reduced across the lanes of a wave that share rows and
+// added with one float atomic per (row, wave) at the end of the unit.
 template <bool KC, int R, int BK, int NTH>
 struct RegLd {
   static constexpr int CH = R * BK / 4;          // 16-B chunks of the operand tile
@@ -364,6 +366,9 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) fm_gemm_f32_pring_kernel(Gemm
 
   f32x4_t acc[MR][NR];
   float af[2][MR][4], bfr[2][NR][4];
+  constexpr int CPR = BM / 4;                       // 16-B chunks per k-row of an MN-contiguous A image
+  float rs[4] = {0.f, 0.f, 0.f, 0.f};
+  bool rowsum = false;
   if (S > 0) {
     if constexpr (MODE == 1) {
 #pragma unroll
@@ -389,11 +394,22 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) fm_gemm_f32_pring_kernel(Gemm
       for (int i = 0; i < MR; ++i)
 #pragma unroll
         for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      rowsum = (!AK) && p.rowsum_a != nullptr && n0 == 0;
     }
     const char* la = smem + (g % SLOTS) * STG;
     const char* lb = la + A_BYTES;
     if constexpr (MODE == 1) {
       if (g + NS - 1 < S) issue(g + NS - 1);
+    }
+    if constexpr (!AK) {
+      if (rowsum) {   // this stage's k-rows of the A image, 4 rows (one 16-B chunk) per thread
+        for (int kr = tid / CPR; kr < BK; kr += NTH / CPR) {
+          const int cc = tid % CPR;
+          const f32x4_t v = *reinterpret_cast<const f32x4_t*>(la + kr * (BM * 4) + 16 * (cc ^ rm_swz<MR>(kr)));
+#pragma unroll
+          for (int x = 0; x < 4; ++x) rs[x] += v[x];
+        }
+      }
     }
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
@@ -424,7 +440,28 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) fm_gemm_f32_pring_kernel(Gemm
           for (int j = 0; j < NR; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(bfr[cur][j][s], af[cur][i][s], acc[i][j], 0, 0, 0);
     }
-    if (t == nkt - 1) epilogue_f32<MR, NR, !AK, !BKC, SGD>(p, acc, 0, split, m0 + wm * TM, n0 + wn * TN, lane);
+    if (t == nkt - 1) {
+      if constexpr (!AK) {
+        if (rowsum) {   // lanes l, l + CPR, ... of a wave hold the same 4 rows
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+            float v = rs[x];
+#pragma unroll
+            for (int o = CPR; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+            rs[x] = v;
+          }
+          const int r = m0 + 4 * (tid % CPR);
+          if (lane < CPR || CPR >= 64) {
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+              if (r + x < p.M) atomicAdd(p.rowsum_a + r + x, rs[x]);
+          }
+#pragma unroll
+          for (int x = 0; x < 4; ++x) rs[x] = 0.f;
+        }
+      }
+      epilogue_f32<MR, NR, !AK, !BKC, SGD>(p, acc, 0, split, m0 + wm * TM, n0 + wn * TN, lane);
+    }
   }
   if constexpr (MODE == 1) wait_vmcnt_f<0>();
 }

@@ -1,0 +1,345 @@
+// flexmi fp32 GEMM on the bf16 matrix cores, second form: exact three-way operand split done in
+// the register staging pass, double-buffered planes, 64x64 output per wave (gfx950 / MI355X).
+//
+//   C[M,N] (+)= epilogue( alpha * sum_k A(m,k) * B(k,n) )      fp32 in, fp32 accumulate, fp32 out
+//
+// Every fp32 operand x is split EXACTLY into three bf16 terms by truncation: h = x with the low 16
+// bits cleared, r = x - h (exact: <= 16 significant bits), m = r truncated the same way, l = r - m
+// (<= 8 significant bits: exactly a bf16).  x*y is then the sum of the six products with
+// i + j <= 2 (hh, hm, mh, hl, mm, lh) on v_mfma_f32_16x16x32_bf16 with fp32 accumulation: each
+// bf16 x bf16 product is exact in fp32, and the dropped terms (ml, lm, ll) are <= 2^-24 |x y|, the
+// order of the fp32 product rounding itself -- native-fp32 accuracy (tests/test_gpu_fp32.py checks
+// it against float64 at the native kernel's tolerance).  The reference computes these GEMMs with
+// cublasSgemm (src/ops/linear.cu:424-447 forward, :592-635 backward).
+//
+// Cost per 16x16x32 block: 6 bf16 MFMA x 16 cycles against 8 fp32 MFMA x 32 cycles (2.7x the fp32
+// MFMA rate).  The first split kernel (gemm_f32.hip fm_gemm_x3_kernel: 128x128 tile, one LDS
+// buffer, 64x32 per wave, split at the LDS store between two barriers) measured at parity with the
+// native fp32 kernel (profiles/gemm_f32_split_vs_native_r4c.jsonl): its waves read 18 b128
+// fragments per 48 MFMAs and stalled on the store phase.  This form:
+//   * 64x64 output per wave (4x4 tiles): 24 b128 fragment reads per 96 MFMAs;
+//   * two LDS stages of three bf16 planes per operand, [row][32 k] images with 64-B rows and the
+//     16-B chunk XOR-swizzled by (row >> 1) & 3 (conflict-free ds_read_b128 fragment reads);
+//   * one barrier per 32-deep k step: after it, the staged registers of step t+1 are split into the
+//     free stage, the loads of step t+2 are issued, and the MFMAs of step t run -- the global loads
+//     have a whole step of MFMAs to land;
+//   * MN-contiguous operands (dX's W, both dW operands) are transposed in registers: a staging
+//     unit is 2 rows x 4 k (four 8-B loads), written as 8-B halves of the rows' chunks.
+// Tiles: 256x128 (8 waves, 144 KiB LDS) or 128x128 (4 waves, 96 KiB), one block per CU,
+// XCD-aware tile order, split-K slabs / fused epilogues / fused SGD shared with the native kernel
+// (gemm_f32_common.h epilogue_f32).
+#include "gemm_f32_common.h"
+
+#include <cstdlib>
+
+namespace {
+
+constexpr int XK = 32;   // k per stage
+
+// byte offset of 16-B chunk c (8 bf16) of row r in a [row][32 bf16] plane
+FM_DEVICE int x3_off(int r, int c) { return r * 64 + 16 * (c ^ ((r >> 1) & 3)); }
+
+// exact truncation split of one fp32 value: x = h + m + l, each a bf16 (returned as fp32 bits
+// with zero low halves)
+FM_DEVICE void split1(float x, unsigned& h, unsigned& m, unsigned& l) {
+  h = __float_as_uint(x) & 0xffff0000u;
+  const float r = x - __uint_as_float(h);
+  m = __float_as_uint(r) & 0xffff0000u;
+  l = __float_as_uint(r - __uint_as_float(m)) & 0xffff0000u;
+}
+
+// two fp32 -> one packed bf16 pair per plane (element a in the low half)
+FM_DEVICE void split2(float a, float b, unsigned& h, unsigned& m, unsigned& l) {
+  unsigned ha, ma, la, hb, mb, lb;
+  split1(a, ha, ma, la);
+  split1(b, hb, mb, lb);
+  h = (ha >> 16) | hb;
+  m = (ma >> 16) | mb;
+  l = (la >> 16) | lb;
+}
+
+// One operand's k step (R rows x 32 k) staged through registers.  K-contiguous: unit = (row,
+// k-octet), two 16-B loads.  MN-contiguous (global [k][rows]): unit = (row pair, k-quad), four 8-B
+// loads, transposed in registers.  Rows past the edge load a clamped row and are zeroed.
+template <bool KC, int R, int NTH>
+struct X3Stage {
+  static constexpr int UNITS = R * 4;
+  static constexpr int PER_T = (UNITS + NTH - 1) / NTH;
+  float v[PER_T][8];
+
+  FM_DEVICE void load(const float* __restrict__ p, long ld, int row0, int rows, int k0, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int ci = tid + NTH * i;
+      if (UNITS % NTH != 0 && ci >= UNITS) continue;
+      if constexpr (KC) {
+        const int r = row0 + (ci >> 2), c = ci & 3;
+        const float* src = p + (long)min(r, rows - 1) * ld + k0 + 8 * c;
+        const f32x4_t a = *reinterpret_cast<const f32x4_t*>(src);
+        const f32x4_t b = *reinterpret_cast<const f32x4_t*>(src + 4);
+        const bool ok = r < rows;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[i][e] = ok ? a[e] : 0.f;
+          v[i][4 + e] = ok ? b[e] : 0.f;
+        }
+      } else {
+        constexpr int RP = R / 2;
+        const int rp = ci % RP, kq = ci / RP;
+        const int r = row0 + 2 * rp;
+        const float* src = p + (long)(k0 + 4 * kq) * ld + min(r, rows - 2);
+        typedef float f32x2_t __attribute__((ext_vector_type(2)));
+        const bool ok0 = r < rows, ok1 = r + 1 < rows;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const f32x2_t t = *reinterpret_cast<const f32x2_t*>(src + kk * ld);
+          v[i][kk] = ok0 ? t[0] : 0.f;        // row r, k = 4 kq + kk
+          v[i][4 + kk] = ok1 ? t[1] : 0.f;    // row r + 1
+        }
+      }
+    }
+  }
+
+  FM_DEVICE void store(char* pl0, char* pl1, char* pl2, int tid) const {
+    constexpr int PL = R * 64;
+    (void)PL;
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int ci = tid + NTH * i;
+      if (UNITS % NTH != 0 && ci >= UNITS) continue;
+      if constexpr (KC) {
+        u32x4_t h, m, l;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          unsigned hh, mm, ll;
+          split2(v[i][2 * u], v[i][2 * u + 1], hh, mm, ll);
+          h[u] = hh;
+          m[u] = mm;
+          l[u] = ll;
+        }
+        const int off = x3_off(ci >> 2, ci & 3);
+        *reinterpret_cast<u32x4_t*>(pl0 + off) = h;
+        *reinterpret_cast<u32x4_t*>(pl1 + off) = m;
+        *reinterpret_cast<u32x4_t*>(pl2 + off) = l;
+      } else {
+        constexpr int RP = R / 2;
+        const int rp = ci % RP, kq = ci / RP;
+        typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          u32x2_t h, m, l;
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            unsigned hh, mm, ll;
+            split2(v[i][4 * e + 2 * u], v[i][4 * e + 2 * u + 1], hh, mm, ll);
+            h[u] = hh;
+            m[u] = mm;
+            l[u] = ll;
+          }
+          const int off = x3_off(2 * rp + e, kq >> 1) + 8 * (kq & 1);
+          *reinterpret_cast<u32x2_t*>(pl0 + off) = h;
+          *reinterpret_cast<u32x2_t*>(pl1 + off) = m;
+          *reinterpret_cast<u32x2_t*>(pl2 + off) = l;
+        }
+      }
+    }
+  }
+
+  // MN-contiguous A (dW): per-thread sums of its two rows over the staged k (bias gradient)
+  FM_DEVICE void rowsum(float (&s)[2], int tid) const {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int ci = tid + NTH * i;
+      if (UNITS % NTH != 0 && ci >= UNITS) continue;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        s[0] += v[i][kk];
+        s[1] += v[i][4 + kk];
+      }
+    }
+  }
+};
+
+template <int BM, int BN, bool AK, bool BKC, bool SGD, int SCHED>
+__global__ void __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) fm_gemm_x3v2_kernel(GemmF p) {
+  constexpr int WM = BM / 64, WN = BN / 64, NTH = WM * WN * 64;
+  constexpr int MR = 4, NR = 4;
+  constexpr int PA_ = BM * 64, PB_ = BN * 64;          // bytes of one bf16 plane per operand
+  constexpr int STG = 3 * (PA_ + PB_);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int bid = xcd_remap_f(blockIdx.x, p.tiles_m * p.tiles_n);
+  int tm, tn;
+  if (p.n_fast) {
+    tn = bid % p.tiles_n;
+    tm = bid / p.tiles_n;
+  } else {
+    tm = bid % p.tiles_m;
+    tn = bid / p.tiles_m;
+  }
+  const int zb = blockIdx.y, split = blockIdx.z;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const float* A = p.A + (long)zb * p.sA;
+  const float* B = p.B + (long)zb * p.sB;
+  const int ktiles = p.K / XK;
+  const int kt_per = (ktiles + p.ksplit - 1) / p.ksplit;
+  const int kt0 = split * kt_per, kt1 = min(ktiles, kt0 + kt_per);
+  const int nst = kt1 - kt0;
+
+  f32x4_t acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  X3Stage<AK, BM, NTH> sa;
+  X3Stage<BKC, BN, NTH> sb;
+  const bool dorow = (!AK) && p.rowsum_a != nullptr && tn == 0;
+  float rs[2] = {0.f, 0.f};
+  auto stage = [&](int s) { return smem + s * STG; };
+  auto put = [&](int s) {
+    char* b = stage(s);
+    sa.store(b, b + PA_, b + 2 * PA_, tid);
+    sb.store(b + 3 * PA_, b + 3 * PA_ + PB_, b + 3 * PA_ + 2 * PB_, tid);
+    if constexpr (!AK) {
+      if (dorow) sa.rowsum(rs, tid);
+    }
+  };
+  auto get = [&](int kt) {
+    sa.load(A, p.lda, m0, p.M, kt * XK, tid);
+    sb.load(B, p.ldb, n0, p.N, kt * XK, tid);
+  };
+  if (nst > 0) {
+    get(kt0);
+    put(0);
+    if (nst > 1) get(kt0 + 1);
+  }
+  const int q = lane & 15, g = lane >> 4;
+  constexpr int TA[6] = {2, 1, 0, 1, 0, 0};    // small terms first, the dominant h*h product last
+  constexpr int TB[6] = {0, 1, 2, 0, 1, 0};
+  for (int t = 0; t < nst; ++t) {
+    __syncthreads();                 // stage t&1 complete; stage (t+1)&1 no longer read
+    const char* b = stage(t & 1);
+    const char* la = b;
+    const char* lb = b + 3 * PA_;
+    bf16x8_t bf[3][NR];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+        bf[pl][j] = *reinterpret_cast<const bf16x8_t*>(lb + pl * PB_ + x3_off(wn * 64 + 16 * j + q, g));
+    if constexpr (SCHED == 1) {
+      // every fragment of the step first, then the staging pass (split + ds_write of step t+1,
+      // loads of step t+2), then the MFMAs: nothing orders the MFMAs behind the staging VALU /
+      // LDS writes, so the scheduler can interleave them
+      bf16x8_t af[MR][3];
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          af[i][pl] = *reinterpret_cast<const bf16x8_t*>(la + pl * PA_ + x3_off(wm * 64 + 16 * i + q, g));
+      if (t + 1 < nst) {
+        put((t + 1) & 1);
+        if (t + 2 < nst) get(kt0 + t + 2);
+      }
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int s = 0; s < 6; ++s)
+#pragma unroll
+          for (int j = 0; j < NR; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8v_t*>(&bf[TB[s]][j]),
+                                                                *reinterpret_cast<bf16x8v_t*>(&af[i][TA[s]]), acc[i][j],
+                                                                0, 0, 0);
+    } else {
+      if (t + 1 < nst) {
+        put((t + 1) & 1);
+        if (t + 2 < nst) get(kt0 + t + 2);
+      }
+#pragma unroll
+      for (int i = 0; i < MR; ++i) {
+        bf16x8_t af[3];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          af[pl] = *reinterpret_cast<const bf16x8_t*>(la + pl * PA_ + x3_off(wm * 64 + 16 * i + q, g));
+        // NR independent accumulator chains per term
+#pragma unroll
+        for (int s = 0; s < 6; ++s)
+#pragma unroll
+          for (int j = 0; j < NR; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8v_t*>(&bf[TB[s]][j]),
+                                                                *reinterpret_cast<bf16x8v_t*>(&af[TA[s]]), acc[i][j],
+                                                                0, 0, 0);
+      }
+    }
+  }
+  if constexpr (!AK) {
+    if (dorow) {   // threads sharing a row pair: reduce through LDS, one atomic per row
+      __syncthreads();
+      float* red = reinterpret_cast<float*>(smem);
+      constexpr int RP = BM / 2;
+      red[tid * 2] = rs[0];
+      red[tid * 2 + 1] = rs[1];
+      __syncthreads();
+      if (tid < BM) {
+        const int rp = tid >> 1, e = tid & 1;
+        float x = 0.f;
+        for (int s = rp; s < NTH; s += RP) x += red[2 * s + e];
+        if (m0 + tid < p.M) atomicAdd(p.rowsum_a + m0 + tid, x);
+      }
+    }
+  }
+  epilogue_f32<MR, NR, false, false, SGD>(p, acc, zb, split, m0 + wm * 64, n0 + wn * 64, lane);
+}
+
+template <int BM, int BN, bool SGD, int SCHED>
+void launch_x3v2_s(const GemmF& p, bool ak, bool bk, hipStream_t s) {
+  constexpr int NTH = (BM / 64) * (BN / 64) * 64;
+  constexpr int LDS = 2 * 3 * (BM + BN) * 64;
+  dim3 grid(p.tiles_m * p.tiles_n, p.batch, p.ksplit);
+#define FM_X3V2(AKv, BKv)                                                                                        \
+  do {                                                                                                           \
+    static bool attr = false;                                                                                    \
+    if (!attr) {                                                                                                 \
+      (void)hipFuncSetAttribute((const void*)fm_gemm_x3v2_kernel<BM, BN, AKv, BKv, SGD, SCHED>,                        \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS);                                \
+      attr = true;                                                                                               \
+    }                                                                                                            \
+    hipLaunchKernelGGL((fm_gemm_x3v2_kernel<BM, BN, AKv, BKv, SGD, SCHED>), grid, dim3(NTH), LDS, s, p);              \
+  } while (0)
+  if (ak && bk) FM_X3V2(true, true);
+  else if (ak) FM_X3V2(true, false);
+  else if (bk) FM_X3V2(false, true);
+  else FM_X3V2(false, false);
+#undef FM_X3V2
+}
+
+// FM_X3_SCHED=1: all fragment reads of a step ahead of its staging pass (A/B)
+template <int BM, int BN, bool SGD>
+void launch_x3v2(const GemmF& p, bool ak, bool bk, hipStream_t s) {
+  static const int sched = getenv("FM_X3_SCHED") ? atoi(getenv("FM_X3_SCHED")) : 0;
+  if (sched == 1) launch_x3v2_s<BM, BN, SGD, 1>(p, ak, bk, s);
+  else launch_x3v2_s<BM, BN, SGD, 0>(p, ak, bk, s);
+}
+
+}  // namespace
+
+// Launch on a prepared parameter block (tiles_m / tiles_n / ksplit filled for the bm x 128 tile).
+// Caller guarantees: K % 32 == 0 (per split: whole steps); K-contiguous operands 16-B aligned with
+// ld % 4 == 0; MN-contiguous operands 8-B aligned with ld % 2 == 0 and an even row count.
+// sgd: the fused-SGD epilogue (unsplit tiles only).  Returns -1 for an unsupported tile.
+extern "C" int fm_gemm_x3v2_launch(const void* params, int bm, int a_kcontig, int b_kcontig, int sgd, hipStream_t s) {
+  const GemmF& p = *static_cast<const GemmF*>(params);
+  if (sgd && p.ksplit > 1) return -1;
+  if (bm == 256) {
+    if (sgd) launch_x3v2<256, 128, true>(p, a_kcontig, b_kcontig, s);
+    else launch_x3v2<256, 128, false>(p, a_kcontig, b_kcontig, s);
+  } else if (bm == 128) {
+    if (sgd) launch_x3v2<128, 128, true>(p, a_kcontig, b_kcontig, s);
+    else launch_x3v2<128, 128, false>(p, a_kcontig, b_kcontig, s);
+  } else {
+    return -1;
+  }
+  return 0;
+}

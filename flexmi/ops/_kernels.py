@@ -109,6 +109,8 @@ def linear_forward(x2, w, b, act, y2):
     if N == 1:
         C().skinny_fwd(x2, w, b, y2, act)
         return
+    if _smallk(x2, K) and C().smallk_fwd(x2, w, b, y2, act):
+        return
     gemm(x2, x2.stride(0), True, w, K, True, y2, y2.stride(0), M, N, K, bias=b, act=act)
 
 
@@ -123,7 +125,30 @@ DW_LIB = os.environ.get("FM_DW_LIB", "auto")
 def _dw_lib(M, N, K, dtype):
     if DW_LIB == "0" or dtype != torch.float32:
         return False
+    if DW_LIB == "auto" and C().gemm_f32_get_split() == 2:
+        return False               # the split-bf16 kernel (gemm_x3.hip) takes every fp32 dW
     return DW_LIB == "1" or (N >= 512 and K >= 480 and M >= 4096)
+
+
+# FM_SMALLK=1/0: thin-input fp32 Linear layers (in_features <= 32, the 13->512 bottom layer of
+# DLRM) on the VALU kernels of gemm_small.hip instead of a 1-2 step K loop of MFMA tiles (forward)
+# and a split-K GEMM + reduce (dW)
+SMALLK = os.environ.get("FM_SMALLK", "1") == "1"
+
+
+def _smallk(x2, K):
+    return SMALLK and x2.dtype == torch.float32 and K <= 32 and K % 4 == 0 and x2.stride(0) % 4 == 0
+
+
+def _dw_smallk(dpre, x2, dw, db, upd):
+    """dW (+ db) of a thin-input layer on gemm_small.hip; with upd the SGD step is applied to the
+    weight in the same launch pair.  False when the kernel does not apply."""
+    if ASYNC_DW:
+        gemm_join()                # the shared workspace may still feed an async split-K reduce
+    ws = workspace(dpre.device, GEMM_WS_BYTES)
+    if upd is None:
+        return C().smallk_dw(dpre, x2, dw, db, ws, None, None, None, 0.0, 0.0, False)
+    return C().smallk_dw(dpre, x2, upd.w, db, ws, upd.v, upd.wc, upd.lr, upd.wd, upd.mom, upd.nesterov)
 
 
 DX_LIB = os.environ.get("FM_DX_LIB", "0") == "1"
@@ -194,6 +219,8 @@ def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=F
             _linear_dx(dpre, w, dx2, dx_acc, fuse_below, M, N, K)
         if phase == "dx":
             return
+        if _smallk(x2, K) and _dw_smallk(dpre, x2, dw, db, upd):
+            return
         if not lib and M > 0 and _dw_fused_sgd(dpre, x2, dw, db, upd):
             return
         if lib:
@@ -215,7 +242,7 @@ def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=F
     # dW ACCUMULATES (beta): the executor zeroes the flat gradient buffer once per step, so weights
     # used by several ops sum their gradients, and split-K partials of small dW tiles can be added
     # with atomics straight into dw (no slab / reduce launch)
-    if phase != "dx" and not lib:
+    if phase != "dx" and not lib and not (_smallk(x2, K) and _dw_smallk(dpre, x2, dw, db, None)):
         gemm(dpre, dpre.stride(0), False, x2, x2.stride(0), False, dw, K, N, K, M, beta=True, rowsum_a=db,
              async_reduce=async_dw and ASYNC_DW)
     if phase == "dw":

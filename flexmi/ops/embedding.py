@@ -355,6 +355,10 @@ class Embedding(Op):
     CLAIM = os.environ.get("FM_EMB_CLAIM", "1") != "0"
     # owner-computes only when rows exceed CLAIM_RATIO x lookups per step (fewer duplicates)
     CLAIM_RATIO = float(os.environ.get("FM_EMB_CLAIM_RATIO", "1"))
+    # FM_EMB_BWD=count: the count / update kernel pair (csrc/kernels/embedding.hip) for every table
+    # above the tiny-table LDS kernel's 16 rows, on the same slot / flag buffers
+    COUNT = os.environ.get("FM_EMB_BWD", "claim") == "count"
+    TINY_ROWS = 16
 
     def _claim_buffers(self, ctx):
         """Owner-computes sparse SGD buffers for a mostly-unique table (rows > lookups per step):
@@ -365,7 +369,8 @@ class Embedding(Op):
         s = ctx.saved
         if "claim" not in s:
             w, idx = ctx.weights[0], ctx.inputs[0]
-            if w.shape[0] > Embedding.CLAIM_RATIO * idx.numel() and self.out_dim % 4 == 0:
+            big = w.shape[0] > (Embedding.TINY_ROWS if Embedding.COUNT else Embedding.CLAIM_RATIO * idx.numel())
+            if big and self.out_dim % 4 == 0:
                 dev = w.device
                 s["claim"] = (torch.full((w.shape[0],), -1, dtype=torch.int32, device=dev),
                               torch.empty(idx.numel(), dtype=torch.int32, device=dev),

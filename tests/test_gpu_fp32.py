@@ -558,3 +558,63 @@ def test_fused_backward_epilogue_split_k_small_batch(gpu, dtype):
     ref = (dpre.double() @ W.double()) * (yb.double() > 0)
     assert rel_err(dx, ref) < tol
     assert rel_err(colsum, ref.sum(0)) < tol
+
+
+# ---------------------------------------------------------------- thin-input Linear (gemm_small.hip)
+@pytest.mark.parametrize("act", [10, 11, 12])
+@pytest.mark.parametrize("M,K,N", [(8192, 16, 512), (1000, 4, 12), (333, 32, 1024), (4096, 20, 260)])
+def test_smallk_forward(gpu, act, M, K, N):
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(11)
+    x, w, b = torch.randn(M, K, device=gpu), torch.randn(N, K, device=gpu), torch.randn(N, device=gpu)
+    y = torch.full((M, N), float("nan"), device=gpu)
+    assert Kk.C().smallk_fwd(x, w, b, y, act)
+    ref = x.double() @ w.double().t() + b.double()
+    ref = {10: ref, 11: ref.clamp_min(0), 12: torch.sigmoid(ref)}[act]
+    assert rel_err(y, ref) < TOL
+    # outside the limits nothing is launched and the caller falls back
+    assert not Kk.C().smallk_fwd(torch.randn(M, 13, device=gpu), torch.randn(N, 13, device=gpu), b, y, act)
+
+
+@pytest.mark.parametrize("M,K,N", [(8192, 16, 512), (1000, 4, 12), (333, 32, 1032), (77, 8, 4), (8192, 28, 2052)])
+def test_smallk_dw(gpu, M, K, N):
+    """dW += dpre^T x and db += colsum(dpre) (accumulating, two-pass deterministic)."""
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(12)
+    dpre, x = torch.randn(M, N, device=gpu), torch.randn(M, K, device=gpu)
+    dw0, db0 = torch.randn(N, K, device=gpu), torch.randn(N, device=gpu)
+    dw, db = dw0.clone(), db0.clone()
+    ws = Kk.workspace(dpre.device, Kk.GEMM_WS_BYTES)
+    assert Kk.C().smallk_dw(dpre, x, dw, db, ws, None, None, None, 0.0, 0.0, False)
+    assert rel_err(dw - dw0, dpre.double().t() @ x.double()) < TOL
+    assert rel_err(db - db0, dpre.double().sum(0)) < TOL
+    dw2, db2 = dw0.clone(), db0.clone()
+    assert Kk.C().smallk_dw(dpre, x, dw2, db2, ws, None, None, None, 0.0, 0.0, False)
+    assert torch.equal(dw2, dw) and torch.equal(db2, db)          # fixed summation order
+
+
+@pytest.mark.parametrize("mom,nesterov,mirror", [(0.0, False, False), (0.9, False, True), (0.9, True, False)])
+def test_smallk_dw_fused_sgd(gpu, mom, nesterov, mirror):
+    """The SGD step applied in the dW reduce == gradient + optim.hip SGD kernel."""
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(13)
+    M, K, N, lr, wd = 8192, 16, 512, 0.05, 1e-3
+    dpre, x = torch.randn(M, N, device=gpu), torch.randn(M, K, device=gpu)
+    w = torch.randn(N, K, device=gpu)
+    v = torch.randn(N, K, device=gpu) if mom > 0 else None
+    wc = torch.empty(N, K, device=gpu, dtype=torch.bfloat16) if mirror else None
+    db = torch.zeros(N, device=gpu)
+    lr_t = torch.tensor([lr], device=gpu)
+    g = dpre.double().t() @ x.double() + wd * w.double()
+    if mom > 0:
+        v_ref = v.double() * mom + g
+        g = g + mom * v_ref if nesterov else v_ref
+    w_ref = w.double() - lr * g
+    ws = Kk.workspace(dpre.device, Kk.GEMM_WS_BYTES)
+    assert Kk.C().smallk_dw(dpre, x, w, db, ws, v, wc, lr_t, wd, mom, nesterov)
+    assert rel_err(w, w_ref) < TOL
+    assert rel_err(db, dpre.double().sum(0)) < TOL
+    if mom > 0:
+        assert rel_err(v, v_ref) < TOL
+    if mirror:
+        assert torch.equal(wc, w.to(torch.bfloat16))

@@ -1,5 +1,6 @@
 """fp32 GEMM on the bf16 matrix cores by exact three-way operand splitting (csrc/kernels/gemm_f32.hip
-fm_gemm_x3_kernel, FM_F32_SPLIT=1 / gemm_f32_set_split): every orientation, tails, epilogues, the
+fm_gemm_x3_kernel, FM_F32_SPLIT=1, and its second form csrc/kernels/gemm_x3.hip, FM_F32_SPLIT=2 /
+gemm_f32_set_split(mode)): every orientation, tails, epilogues, fused SGD, the
 fused backward epilogue, row sums and split-K against a float64 oracle at the fp32 test tolerance,
 with its error compared to the native v_mfma_f32_16x16x4_f32 kernel's on the same inputs."""
 import pytest
@@ -10,12 +11,15 @@ from tests.test_gpu_fp32 import TOL, _fused_backward_epilogue, rel_err
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture
-def split():
+MODES = [1, 2]
+
+
+@pytest.fixture(params=MODES)
+def split(request):
     from flexmi.ops import _kernels as Kk
-    Kk.C().gemm_f32_set_split(True)
+    Kk.C().gemm_f32_set_split(request.param)
     yield Kk
-    Kk.C().gemm_f32_set_split(False)
+    Kk.C().gemm_f32_set_split(0)
 
 
 def _gemm(Kk, A, B, a_k, b_k, M, N, K):
@@ -26,21 +30,23 @@ def _gemm(Kk, A, B, a_k, b_k, M, N, K):
     return C
 
 
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 200, 130), (8192, 1024, 1024), (2048, 479, 512),
-                                   (8192, 1024, 480), (1000, 1020, 8192), (256, 4096, 4096), (129, 67, 67)])
-def test_split_gemm_orientations_vs_native(gpu, a_k, b_k, M, N, K):
+                                   (8192, 1024, 480), (1000, 1020, 8192), (256, 4096, 4096), (129, 67, 67),
+                                   (330, 194, 96), (8192, 512, 1024), (1024, 480, 8192)])
+def test_split_gemm_orientations_vs_native(gpu, mode, a_k, b_k, M, N, K):
     from flexmi.ops import _kernels as Kk
     torch.manual_seed(M + N + K)
     A, B = torch.randn(M, K, device=gpu), torch.randn(K, N, device=gpu)
     ref = A.double() @ B.double()
-    Kk.C().gemm_f32_set_split(False)
+    Kk.C().gemm_f32_set_split(0)
     e_native = rel_err(_gemm(Kk, A, B, a_k, b_k, M, N, K), ref)
-    Kk.C().gemm_f32_set_split(True)
+    Kk.C().gemm_f32_set_split(mode)
     try:
         e_split = rel_err(_gemm(Kk, A, B, a_k, b_k, M, N, K), ref)
     finally:
-        Kk.C().gemm_f32_set_split(False)
+        Kk.C().gemm_f32_set_split(0)
     assert e_split < TOL, (e_split, e_native)
     assert e_split < 4 * e_native + 1e-6, (e_split, e_native)     # fp32-class accuracy, not bf16's ~1e-2
 
@@ -73,7 +79,8 @@ def test_split_splitk(gpu, split, ks):
     assert rel_err(C, A.double().t() @ B.double() + bias.double()) < TOL
 
 
-def test_split_wide_dynamic_range(gpu):
+@pytest.mark.parametrize("mode", MODES)
+def test_split_wide_dynamic_range(gpu, mode):
     """Operands spanning many binades (the split terms are relative to each element's own exponent)."""
     from flexmi.ops import _kernels as Kk
     torch.manual_seed(5)
@@ -81,16 +88,61 @@ def test_split_wide_dynamic_range(gpu):
     A = torch.randn(M, K, device=gpu) * torch.exp2(torch.randint(-20, 20, (M, K), device=gpu).float())
     B = torch.randn(K, N, device=gpu) * torch.exp2(torch.randint(-20, 20, (K, N), device=gpu).float())
     ref = A.double() @ B.double()
-    Kk.C().gemm_f32_set_split(False)
+    Kk.C().gemm_f32_set_split(0)
     e_native = rel_err(_gemm(Kk, A, B, True, False, M, N, K), ref)
-    Kk.C().gemm_f32_set_split(True)
+    Kk.C().gemm_f32_set_split(mode)
     try:
         e_split = rel_err(_gemm(Kk, A, B, True, False, M, N, K), ref)
     finally:
-        Kk.C().gemm_f32_set_split(False)
+        Kk.C().gemm_f32_set_split(0)
     assert e_split < 4 * e_native + 1e-6, (e_split, e_native)
 
 
 def test_split_dlrm_mlperf_widths_matches_cpu(gpu, split):
     from tests.test_gpu_fp32 import test_dlrm_mlperf_widths_fp32_gpu_matches_cpu as t
     t(gpu, True)
+
+
+@pytest.mark.parametrize("Nout,Kin", [(1024, 480), (512, 1024), (256, 130)])
+def test_split2_dw_rowsum(gpu, Nout, Kin):
+    """dW += dpre^T x with the bias-gradient row sums (both operands MN-contiguous)."""
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(6)
+    B = 8192
+    dpre, x = torch.randn(B, Nout, device=gpu), torch.randn(B, Kin, device=gpu)
+    dw0, db0 = torch.randn(Nout, Kin, device=gpu), torch.randn(Nout, device=gpu)
+    dw, db = dw0.clone(), db0.clone()
+    Kk.C().gemm_f32_set_split(2)
+    try:
+        Kk.gemm(dpre, Nout, False, x, Kin, False, dw, Kin, Nout, Kin, B, beta=True, rowsum_a=db)
+    finally:
+        Kk.C().gemm_f32_set_split(0)
+    assert rel_err(dw - dw0, dpre.double().t() @ x.double()) < TOL
+    assert rel_err(db - db0, dpre.double().sum(0)) < TOL
+
+
+@pytest.mark.parametrize("mom,nesterov", [(0.0, False), (0.9, True)])
+@pytest.mark.parametrize("Nout,Kin", [(1024, 1024), (256, 512)])
+def test_split2_dw_fused_sgd(gpu, mom, nesterov, Nout, Kin):
+    """The SGD step fused into the split kernel's dW epilogue (unsplit) or its split-K reduce."""
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(7)
+    B, lr, wd = 8192, 0.05, 1e-4
+    dpre, x = torch.randn(B, Nout, device=gpu), torch.randn(B, Kin, device=gpu)
+    w = torch.randn(Nout, Kin, device=gpu)
+    v = torch.randn(Nout, Kin, device=gpu) if mom > 0 else None
+    db = torch.zeros(Nout, device=gpu)
+    g = dpre.double().t() @ x.double() + wd * w.double()
+    if mom > 0:
+        v_ref = v.double() * mom + g
+        g = g + mom * v_ref if nesterov else v_ref
+    w_ref = w.double() - lr * g
+    Kk.C().gemm_f32_set_split(2)
+    try:
+        ks = Kk.C().gemm_dw_sgd(dpre, x, w, None, v, torch.tensor([lr], device=gpu), wd, mom, nesterov, db,
+                                Kk.workspace(gpu, Kk.GEMM_WS_BYTES))
+    finally:
+        Kk.C().gemm_f32_set_split(0)
+    assert ks >= 1
+    assert rel_err(w, w_ref) < TOL
+    assert rel_err(db, dpre.double().sum(0)) < TOL

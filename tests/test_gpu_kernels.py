@@ -449,6 +449,52 @@ def test_embedding_owner_computes_sgd(gpu, idx_dtype):
                 assert int((claim[k] != -1).sum()) == 0 and int(claim[k + 2].item()) == 0, "claims not released"
 
 
+@pytest.mark.parametrize("dy_dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("idx_dtype", [torch.int64, torch.int32])
+def test_embedding_count_update_sgd(gpu, idx_dtype, dy_dtype):
+    """Count / update sparse SGD (FM_EMB_BWD=count: slot = lookups - 1, plain RMW for single-lookup
+    rows, atomics for repeated rows) on every table above 16 rows, incl. a row shard, over three
+    steps: matches the dense reference and leaves every slot free (-1) after each step."""
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(9)
+    B = 2000
+    specs = [(400000, 1, 128, 0), (1500, 1, 128, 0), (5000, 2, 64, 0), (40, 1, 128, 0), (3, 1, 128, 0),
+             (30000, 1, 128, 10000)]    # rows, bag, D, first row held (row shard of a 40000-row table)
+    tables, idxs, claim, refs, los = [], [], [], [], []
+    for rows, bag, D, lo in specs:
+        W = torch.randn(rows, D, device=gpu)
+        tables.append(W)
+        refs.append(W.clone())
+        idxs.append(torch.randint(0, rows + lo, (B, bag), device=gpu, dtype=idx_dtype))
+        los.append(lo)
+        if rows > 16:
+            claim += [torch.full((rows,), -1, dtype=torch.int32, device=gpu),
+                      torch.empty(B * bag, dtype=torch.int32, device=gpu), torch.zeros(1, dtype=torch.int32, device=gpu)]
+        else:
+            claim += [None, None, None]
+    lr = torch.tensor([0.05], device=gpu)
+    Kk.C().embedding_set_bwd_mode(True)
+    try:
+        for step in range(3):
+            dys = [torch.randn(B, D, device=gpu).to(dy_dtype) for _, _, D, _ in specs]
+            Kk.C().embedding_bwd_multi(tables, idxs, dys, [d.stride(0) for d in dys], [1.0] * len(specs), lr, claim,
+                                       los)
+            for k, ((rows, bag, D, lo), W) in enumerate(zip(specs, refs)):
+                flat = idxs[k].reshape(-1).long() - lo
+                keep = (flat >= 0) & (flat < rows)
+                upd = torch.zeros_like(W)
+                upd.index_add_(0, flat[keep], dys[k].float().repeat_interleave(bag, 0)[keep])
+                W -= 0.05 * upd
+            torch.cuda.synchronize()
+            for k in range(len(specs)):
+                assert torch.allclose(tables[k], refs[k], atol=1e-4), (step, specs[k])
+            for k in range(0, len(claim), 3):
+                if claim[k] is not None:
+                    assert int((claim[k] != -1).sum()) == 0, ("slots not freed", step, k // 3)
+    finally:
+        Kk.C().embedding_set_bwd_mode(False)
+
+
 @pytest.mark.parametrize("idx_dtype", [torch.int64, torch.int32])
 def test_embedding_row_shards(gpu, idx_dtype):
     """Row-sharded tables (a shard holds rows [lo, lo+rows)): forward sums only the lookups the

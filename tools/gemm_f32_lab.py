@@ -4,7 +4,7 @@ orientations, exactly as the executor issues them (fwd with bias+ReLU epilogue; 
 beta = 1 accumulation and the fused bias-gradient row sums), for a list of FM_GEMM_F32_VARIANT
 values, against hipBLASLt (torch.matmul, fp32).  Checks every variant against a float64 oracle
 and reports the best-of-rounds GPU time per call (hipGraph of 20 calls, interleaved rounds).
-usage: gemm_f32_lab.py v0,v1,... ["M,K,N;..."]"""
+usage: gemm_f32_lab.py v0,v1,... ["M,K,N;..."]   (negative v: split-bf16 form -v, FM_F32_SPLIT)"""
 import json
 import os
 import sys
@@ -26,7 +26,10 @@ def main():
     if len(args) > 1:
         shapes = [tuple(int(v) for v in t.split(",")) for t in args[1].split(";")]
     torch.backends.cuda.matmul.allow_tf32 = False
-    setv = K.C().gemm_f32_set_variant
+    def setv(v):
+        K.C().gemm_f32_set_split(-v if v < 0 else 0)
+        K.C().gemm_f32_set_variant(v if v > 0 else 0)
+
     dev = torch.device("cuda")
     torch.manual_seed(0)
     tot = {v: 0.0 for v in variants}
