@@ -41,11 +41,12 @@ int fm_smallk_dw_f32_launch(const float* dpre, long ldd, const float* x, long ld
 void fm_skinny_fwd_f32_launch(const float* x, long ldx, const float* w, const float* bias, float* y, long ldy, long B, int K,
                               int act, hipStream_t s);
 void fm_skinny_bwd_f32_launch(const float* x, long ldx, const float* w, const float* y, long ldy, const float* dy, long lddy,
-                              float* dx, long lddx, int dx_acc, float* dw, float* db, long B, int K, int act, hipStream_t s);
+                              float* dx, long lddx, int dx_acc, float* dw, float* db, long B, int K, int act, int bact,
+                              hipStream_t s);
 void fm_skinny_fwd(const void* x, long ldx, const void* w, const float* bias, void* y, long ldy, long B, int K, int act,
                    hipStream_t s);
 void fm_skinny_bwd(const void* x, long ldx, const void* w, const void* y, long ldy, const void* dy, long lddy, void* dx,
-                   long lddx, int dx_acc, float* dw, float* db, long B, int K, int act, hipStream_t s);
+                   long lddx, int dx_acc, float* dw, float* db, long B, int K, int act, int bact, hipStream_t s);
 void fm_init_fill(float* out, long rows, long cols, long r0, long c0, long ldg, int kind, unsigned seed, float a, float b,
                   hipStream_t s);
 void fm_embedding_fwd(const void* idx, int idx64, const float* W, void* out, int out_bf16, long B, int bag, int rows, int D,
@@ -353,7 +354,8 @@ void skinny_fwd(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> b
 }
 
 void skinny_bwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, torch::Tensor dy, c10::optional<torch::Tensor> dx, bool dx_acc,
-                torch::Tensor dw, c10::optional<torch::Tensor> db, int64_t act) {
+                torch::Tensor dw, c10::optional<torch::Tensor> db, int64_t act, int64_t bact) {
+  // bact: activation backward of the layer below (output x) fused into dX; 10 = none
   TORCH_CHECK(w.numel() == x.size(1) && dw.numel() == x.size(1), "skinny_bwd: shapes");
   long lddx = (dx.has_value() && dx->defined()) ? dx->stride(0) : 0;
   if (x.scalar_type() == torch::kFloat32) {
@@ -363,12 +365,12 @@ void skinny_bwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, torch::Tensor
                 "skinny_bwd fp32: K % 4 == 0");
     fm_skinny_bwd_f32_launch(x.data_ptr<float>(), x.stride(0), w.data_ptr<float>(), y.data_ptr<float>(), y.stride(0),
                              dy.data_ptr<float>(), dy.stride(0), (float*)mptr(dx), lddx, dx_acc ? 1 : 0, dw.data_ptr<float>(),
-                             (float*)mptr(db), x.size(0), (int)x.size(1), (int)act, cur());
+                             (float*)mptr(db), x.size(0), (int)x.size(1), (int)act, (int)bact, cur());
     return;
   }
   TORCH_CHECK(x.size(1) % 8 == 0 && x.stride(0) % 8 == 0, "skinny_bwd: K % 8 == 0");
   fm_skinny_bwd(x.data_ptr(), x.stride(0), w.data_ptr(), y.data_ptr(), y.stride(0), dy.data_ptr(), dy.stride(0), mptr(dx), lddx,
-                dx_acc ? 1 : 0, dw.data_ptr<float>(), (float*)mptr(db), x.size(0), (int)x.size(1), (int)act, cur());
+                dx_acc ? 1 : 0, dw.data_ptr<float>(), (float*)mptr(db), x.size(0), (int)x.size(1), (int)act, (int)bact, cur());
 }
 
 void init_fill(torch::Tensor out, int64_t rows, int64_t cols, int64_t r0, int64_t c0, int64_t ldg, int64_t kind, int64_t seed,
@@ -1220,7 +1222,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("smallk_fwd", &smallk_fwd);
   m.def("smallk_dw", &smallk_dw);
   m.def("skinny_fwd", &skinny_fwd);
-  m.def("skinny_bwd", &skinny_bwd);
+  m.def("skinny_bwd", &skinny_bwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("dy"), py::arg("dx"), py::arg("dx_acc"),
+        py::arg("dw"), py::arg("db"), py::arg("act"), py::arg("bact") = 10);
   m.def("conv_scratch", &conv_scratch);
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_dgrad", &conv_dgrad);

@@ -684,7 +684,8 @@ __global__ void __launch_bounds__(256) fm_skinny_bwd_kernel(int ROWS, const unsi
                                                            const unsigned short* __restrict__ dy, long lddy,
                                                            unsigned short* __restrict__ dx, long lddx, int dx_acc,
                                                            float* __restrict__ dw, float* __restrict__ db, long B, int K,
-                                                           int act) {
+                                                           int act, int bact) {
+  // bact: activation backward of the layer below applied to dX (see the fp32 kernel)
   // thread = 8 consecutive columns (16-B loads/stores) of rows sub, sub+rpi, ...; per-block
   // partial dW/db reduced in LDS -> one atomic per column per block (B/ROWS adders per address)
   __shared__ float red[256 * 8];
@@ -731,6 +732,7 @@ __global__ void __launch_bounds__(256) fm_skinny_bwd_kernel(int ROWS, const unsi
           for (int j = 0; j < 8; ++j) {
             float v = d * bf2f((unsigned short)wv[j]);
             if (dx_acc) v += bf2f((unsigned short)old[u][j]);
+            if (bact != ACT_NONE) v = act_bwd(bact, bf2f((unsigned short)xv[u][j]), v);
             o[j] = (short)f2bf(v);
           }
           *reinterpret_cast<bf16x8_t*>(dx + rr * lddx + c0) = o;
@@ -766,7 +768,8 @@ extern "C" void fm_skinny_fwd(const void* x, long ldx, const void* w, const floa
 
 // dW (fp32 [K]) and db (fp32 [1]) are ACCUMULATED (callers zero them); requires K % 8 == 0
 extern "C" void fm_skinny_bwd(const void* x, long ldx, const void* w, const void* y, long ldy, const void* dy, long lddy,
-                              void* dx, long lddx, int dx_acc, float* dw, float* db, long B, int K, int act, hipStream_t s) {
+                              void* dx, long lddx, int dx_acc, float* dw, float* db, long B, int K, int act, int bact,
+                              hipStream_t s) {
   if (B <= 0) return;
   // rows per block: 64 gives 128 blocks at B=8192 (fills the chip, 128 adders per dW column);
   // small batches shrink it so there are still >= 128 blocks (B=256 -> 2 rows per block)
@@ -775,5 +778,5 @@ extern "C" void fm_skinny_bwd(const void* x, long ldx, const void* w, const void
   hipLaunchKernelGGL(fm_skinny_bwd_kernel, dim3((unsigned)((B + ROWS - 1) / ROWS), (unsigned)((K + 2047) / 2048)), dim3(256),
                      0, s, ROWS,
                      (const unsigned short*)x, ldx, (const unsigned short*)w, (const unsigned short*)y, ldy,
-                     (const unsigned short*)dy, lddy, (unsigned short*)dx, lddx, dx_acc, dw, db, B, K, act);
+                     (const unsigned short*)dy, lddy, (unsigned short*)dx, lddx, dx_acc, dw, db, B, K, act, bact);
 }

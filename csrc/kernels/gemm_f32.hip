@@ -1191,9 +1191,14 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
   // or fm_gemm_f32_set_split(1)
   f32_split_mode();
   // second split form (gemm_x3.hip): split in the register staging pass, double-buffered planes,
-  // 64x64 per wave; FM_F32_SPLIT=2.  K-contiguous operands need 16-B rows, MN-contiguous ones 8-B
-  // pairs of rows (even row counts).
-  if (g_f32_split == 2 && K > 0 && K % 32 == 0 && M >= 64 && N >= 64) {
+  // 64x64 per wave.  FM_F32_SPLIT=2: every eligible GEMM; 3 (auto): only the big ones, where it
+  // measured faster than the native kernel (min(M, N) >= FM_X3_MIN_MN and K >= FM_X3_MIN_K, both
+  // 480 by default).  K-contiguous operands need 16-B rows, MN-contiguous ones 8-B pairs of rows
+  // (even row counts).
+  static const int x3_min_mn = getenv("FM_X3_MIN_MN") ? atoi(getenv("FM_X3_MIN_MN")) : 480;
+  static const int x3_min_k = getenv("FM_X3_MIN_K") ? atoi(getenv("FM_X3_MIN_K")) : 480;
+  const bool x3_pick = g_f32_split == 2 || (g_f32_split == 3 && std::min(M, N) >= x3_min_mn && K >= x3_min_k);
+  if (x3_pick && K > 0 && K % 32 == 0 && M >= 64 && N >= 64) {
     auto opnd_ok = [&](const float* X, long ld, long sX, bool kc, int rows) {
       return kc ? (al(X) && ld % 4 == 0 && sX % 4 == 0)
                 : ((((uintptr_t)X) & 7) == 0 && ld % 2 == 0 && sX % 2 == 0 && rows % 2 == 0);
@@ -1440,7 +1445,10 @@ __global__ void __launch_bounds__(256) fm_skinny_bwd_f32(int ROWS, const float* 
                                                         const float* __restrict__ w, const float* __restrict__ y, long ldy,
                                                         const float* __restrict__ dy, long lddy, float* __restrict__ dx,
                                                         long lddx, int dx_acc, float* __restrict__ dw,
-                                                        float* __restrict__ db, long B, int K, int act) {
+                                                        float* __restrict__ db, long B, int K, int act, int bact) {
+  // bact != ACT_NONE: the activation backward of the layer below (whose output is x) is applied to
+  // dX here, so that layer's separate act-bwd / bias-gradient pass is skipped (its dW GEMM then
+  // takes dX as its pre-activation gradient and sums the bias gradient itself)
   __shared__ float red[256 * 4];
   __shared__ float redb[256];
   // column block blockIdx.y covers [1024 y, 1024 y + 1024) of K (host: K % 4 == 0)
@@ -1476,7 +1484,14 @@ __global__ void __launch_bounds__(256) fm_skinny_bwd_f32(int ROWS, const float* 
         dbs += d;
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[j] += d * xv[u][j];
-        if (dx) *reinterpret_cast<f32x4_t*>(dx + rr * lddx + c0) = d * wv + old[u];
+        if (dx) {
+          f32x4_t v = d * wv + old[u];
+          if (bact != ACT_NONE) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = act_bwd(bact, xv[u][j], v[j]);
+          }
+          *reinterpret_cast<f32x4_t*>(dx + rr * lddx + c0) = v;
+        }
       }
     }
   }
@@ -1509,11 +1524,11 @@ extern "C" void fm_skinny_fwd_f32_launch(const float* x, long ldx, const float* 
 // dW (fp32 [K]) and db (fp32 [1]) ACCUMULATE; requires K % 4 == 0 and 16-B aligned rows
 extern "C" void fm_skinny_bwd_f32_launch(const float* x, long ldx, const float* w, const float* y, long ldy,
                                          const float* dy, long lddy, float* dx, long lddx, int dx_acc, float* dw, float* db,
-                                         long B, int K, int act, hipStream_t s) {
+                                         long B, int K, int act, int bact, hipStream_t s) {
   if (B <= 0) return;
   int ROWS = 64;
   while (ROWS > 2 && (B + ROWS - 1) / ROWS < 128) ROWS /= 2;
   hipLaunchKernelGGL(fm_skinny_bwd_f32, dim3((unsigned)((B + ROWS - 1) / ROWS), (unsigned)((K + 1023) / 1024)), dim3(256), 0,
                      s, ROWS, x, ldx, w, y, ldy,
-                     dy, lddy, dx, lddx, dx_acc, dw, db, B, K, act);
+                     dy, lddy, dx, lddx, dx_acc, dw, db, B, K, act, bact);
 }

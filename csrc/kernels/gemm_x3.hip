@@ -60,12 +60,21 @@ FM_DEVICE void split2(float a, float b, unsigned& h, unsigned& m, unsigned& l) {
 
 // One operand's k step (R rows x 32 k) staged through registers.  K-contiguous: unit = (row,
 // k-octet), two 16-B loads.  MN-contiguous (global [k][rows]): unit = (row pair, k-quad), four 8-B
-// loads, transposed in registers.  Rows past the edge load a clamped row and are zeroed.
+// loads, transposed in registers.  Rows past the edge load a clamped (valid) row and are NOT
+// zeroed: row r of A only reaches output row r (and B row n output column n), which the epilogue
+// never stores, and the row sums are stored for in-range rows only.  The loaded vectors are kept
+// as they arrive -- no select on them -- so the wait for a load lands at its use in the next
+// step's split, a whole step of MFMAs later (a select right after the load made hipcc wait for
+// every load as soon as it was issued).
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+
 template <bool KC, int R, int NTH>
 struct X3Stage {
   static constexpr int UNITS = R * 4;
   static constexpr int PER_T = (UNITS + NTH - 1) / NTH;
-  float v[PER_T][8];
+  f32x4_t a[PER_T], b[PER_T];        // K-contiguous: k 0..3 / 4..7 of the unit's row
+  f32x2_t c[PER_T][4];               // MN-contiguous: rows (r, r+1) at k = 4 kq + kk
 
   FM_DEVICE void load(const float* __restrict__ p, long ld, int row0, int rows, int k0, int tid) {
 #pragma unroll
@@ -73,36 +82,21 @@ struct X3Stage {
       const int ci = tid + NTH * i;
       if (UNITS % NTH != 0 && ci >= UNITS) continue;
       if constexpr (KC) {
-        const int r = row0 + (ci >> 2), c = ci & 3;
-        const float* src = p + (long)min(r, rows - 1) * ld + k0 + 8 * c;
-        const f32x4_t a = *reinterpret_cast<const f32x4_t*>(src);
-        const f32x4_t b = *reinterpret_cast<const f32x4_t*>(src + 4);
-        const bool ok = r < rows;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[i][e] = ok ? a[e] : 0.f;
-          v[i][4 + e] = ok ? b[e] : 0.f;
-        }
+        const int r = row0 + (ci >> 2), cc = ci & 3;
+        const float* src = p + (long)min(r, rows - 1) * ld + k0 + 8 * cc;
+        a[i] = *reinterpret_cast<const f32x4_t*>(src);
+        b[i] = *reinterpret_cast<const f32x4_t*>(src + 4);
       } else {
         constexpr int RP = R / 2;
         const int rp = ci % RP, kq = ci / RP;
-        const int r = row0 + 2 * rp;
-        const float* src = p + (long)(k0 + 4 * kq) * ld + min(r, rows - 2);
-        typedef float f32x2_t __attribute__((ext_vector_type(2)));
-        const bool ok0 = r < rows, ok1 = r + 1 < rows;
+        const float* src = p + (long)(k0 + 4 * kq) * ld + min(row0 + 2 * rp, rows - 2);
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const f32x2_t t = *reinterpret_cast<const f32x2_t*>(src + kk * ld);
-          v[i][kk] = ok0 ? t[0] : 0.f;        // row r, k = 4 kq + kk
-          v[i][4 + kk] = ok1 ? t[1] : 0.f;    // row r + 1
-        }
+        for (int kk = 0; kk < 4; ++kk) c[i][kk] = *reinterpret_cast<const f32x2_t*>(src + kk * ld);
       }
     }
   }
 
   FM_DEVICE void store(char* pl0, char* pl1, char* pl2, int tid) const {
-    constexpr int PL = R * 64;
-    (void)PL;
 #pragma unroll
     for (int i = 0; i < PER_T; ++i) {
       const int ci = tid + NTH * i;
@@ -111,8 +105,9 @@ struct X3Stage {
         u32x4_t h, m, l;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
+          const f32x4_t& v = u < 2 ? a[i] : b[i];
           unsigned hh, mm, ll;
-          split2(v[i][2 * u], v[i][2 * u + 1], hh, mm, ll);
+          split2(v[2 * (u & 1)], v[2 * (u & 1) + 1], hh, mm, ll);
           h[u] = hh;
           m[u] = mm;
           l[u] = ll;
@@ -124,14 +119,13 @@ struct X3Stage {
       } else {
         constexpr int RP = R / 2;
         const int rp = ci % RP, kq = ci / RP;
-        typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
+        for (int e = 0; e < 2; ++e) {        // row 2 rp + e: its 4 k values are c[i][0..3][e]
           u32x2_t h, m, l;
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
             unsigned hh, mm, ll;
-            split2(v[i][4 * e + 2 * u], v[i][4 * e + 2 * u + 1], hh, mm, ll);
+            split2(c[i][2 * u][e], c[i][2 * u + 1][e], hh, mm, ll);
             h[u] = hh;
             m[u] = mm;
             l[u] = ll;
@@ -153,8 +147,8 @@ struct X3Stage {
       if (UNITS % NTH != 0 && ci >= UNITS) continue;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
-        s[0] += v[i][kk];
-        s[1] += v[i][4 + kk];
+        s[0] += c[i][kk][0];
+        s[1] += c[i][kk][1];
       }
     }
   }
@@ -253,7 +247,11 @@ __global__ void __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) fm_gemm_x3v2_ke
                                                                 *reinterpret_cast<bf16x8v_t*>(&af[i][TA[s]]), acc[i][j],
                                                                 0, 0, 0);
     } else {
-      if (t + 1 < nst) {
+      // SCHED 2: the two waves sharing a SIMD (w and w + 4) run the step's two phases in opposite
+      // order -- one splits / stores while the other issues MFMAs -- instead of both idling the
+      // MFMA pipe through the staging pass together
+      const bool mfma_first = SCHED == 2 && ((wave >> 2) & 1);
+      if (!mfma_first && t + 1 < nst) {
         put((t + 1) & 1);
         if (t + 2 < nst) get(kt0 + t + 2);
       }
@@ -271,6 +269,10 @@ __global__ void __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) fm_gemm_x3v2_ke
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8v_t*>(&bf[TB[s]][j]),
                                                                 *reinterpret_cast<bf16x8v_t*>(&af[TA[s]]), acc[i][j],
                                                                 0, 0, 0);
+      }
+      if (mfma_first && t + 1 < nst) {
+        put((t + 1) & 1);
+        if (t + 2 < nst) get(kt0 + t + 2);
       }
     }
   }
@@ -315,11 +317,13 @@ void launch_x3v2_s(const GemmF& p, bool ak, bool bk, hipStream_t s) {
 #undef FM_X3V2
 }
 
-// FM_X3_SCHED=1: all fragment reads of a step ahead of its staging pass (A/B)
+// FM_X3_SCHED (A/B): 1 = all fragment reads of a step ahead of its staging pass; 2 = the two waves
+// of a SIMD run staging and MFMAs in opposite order (8-wave tile only)
 template <int BM, int BN, bool SGD>
 void launch_x3v2(const GemmF& p, bool ak, bool bk, hipStream_t s) {
   static const int sched = getenv("FM_X3_SCHED") ? atoi(getenv("FM_X3_SCHED")) : 0;
   if (sched == 1) launch_x3v2_s<BM, BN, SGD, 1>(p, ak, bk, s);
+  else if (sched == 2 && BM == 256) launch_x3v2_s<BM, BN, SGD, 2>(p, ak, bk, s);
   else launch_x3v2_s<BM, BN, SGD, 0>(p, ak, bk, s);
 }
 

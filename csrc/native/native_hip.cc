@@ -36,7 +36,8 @@ int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, const float* B
 void fm_skinny_fwd_f32_launch(const float* x, long ldx, const float* w, const float* bias, float* y, long ldy, long B, int K,
                               int act, hipStream_t s);
 void fm_skinny_bwd_f32_launch(const float* x, long ldx, const float* w, const float* y, long ldy, const float* dy, long lddy,
-                              float* dx, long lddx, int dx_acc, float* dw, float* db, long B, int K, int act, hipStream_t s);
+                              float* dx, long lddx, int dx_acc, float* dw, float* db, long B, int K, int act, int bact,
+                              hipStream_t s);
 void fm_act_bwd_bias(const void* y, const void* dy, void* dpre, float* db, long B, int N, int act, int bf16, hipStream_t s);
 void fm_softmax_fwd(const void* x, void* y, long rows, int C, int bf16, hipStream_t s);
 void fm_loss_fwd_bwd(const void* logits, int logits_bf16, const void* labels, void* grad, int grad_bf16, long B, int C,
@@ -126,7 +127,7 @@ class HipEngine : public Engine {
   void dense_bwd(const float* x, const float* W, const float* y, const float* dy, float* dx, float* dW, float* db, int M,
                  int K, int N, int act, bool grad_is_dpre, const float* y_below, int act_below) override {
     if (N == 1 && K % 4 == 0 && y_below == nullptr) {
-      fm_skinny_bwd_f32_launch(x, K, W, y, 1, dy, 1, dx, K, 0, dW, db, M, K, grad_is_dpre ? ACT_NONE : act, st_);
+      fm_skinny_bwd_f32_launch(x, K, W, y, 1, dy, 1, dx, K, 0, dW, db, M, K, grad_is_dpre ? ACT_NONE : act, ACT_NONE, st_);
       return;
     }
     const float* dpre = dy;

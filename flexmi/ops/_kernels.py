@@ -125,8 +125,8 @@ DW_LIB = os.environ.get("FM_DW_LIB", "auto")
 def _dw_lib(M, N, K, dtype):
     if DW_LIB == "0" or dtype != torch.float32:
         return False
-    if DW_LIB == "auto" and C().gemm_f32_get_split() == 2:
-        return False               # the split-bf16 kernel (gemm_x3.hip) takes every fp32 dW
+    if DW_LIB == "auto" and C().gemm_f32_get_split() in (2, 3):
+        return False               # the split-bf16 kernel (gemm_x3.hip) takes the big fp32 dW GEMMs
     return DW_LIB == "1" or (N >= 512 and K >= 480 and M >= 4096)
 
 
@@ -194,10 +194,11 @@ def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=F
     vec = 4 if x2.dtype == torch.float32 else 8
     if N == 1 and K % vec == 0 and x2.stride(0) % vec == 0 and (dx2 is None or dx2.stride(0) % vec == 0):
         if phase != "dw":          # the skinny kernel does dX, dW and db together in the "dx" phase
+            # fuse_below: the layer below's activation backward applied to dX in the same pass
+            bact = int(fuse_below[1]) if (dx2 is not None and fuse_below is not None) else 10
+            assert bact == 10 or not dx_acc
             C().skinny_bwd(x2, w, y2, dy2, dx2, bool(dx_acc), dw, None if grad_is_dpre else db,
-                           10 if grad_is_dpre else act)
-            if dx2 is not None and fuse_below is not None:
-                raise AssertionError("no fused epilogue on the skinny path")
+                           10 if grad_is_dpre else act, bact)
         if upd is not None and phase != "dx":
             upd.apply(dw)
         return

@@ -960,7 +960,8 @@ class Executor:
                 continue
             l2, idx = cons[0]
             c2 = self.ctx.get(l2.guid)
-            if (l2.op_type != OperatorType.OP_LINEAR or c2 is None or l2.out_dim == 1 or op.out_dim == 1
+            # (a 1-wide L2 runs the skinny kernel, which applies L1's activation backward to its dX too)
+            if (l2.op_type != OperatorType.OP_LINEAR or c2 is None or op.out_dim == 1
                     or not self.need[(l2.guid, idx)].same_as(self.home[t.guid]) or c2.in_grads[0] is None):
                 continue
             c2.saved["fuse_below"] = (c1.outputs[0], op.activation)

@@ -149,6 +149,26 @@ def test_skinny_layer_backward(gpu, B, K, act, dx_acc):
     assert rel_err(db, d.sum().reshape(1)) < 1e-3
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,K", [(8192, 256), (1000, 128), (300, 2056)])
+def test_skinny_backward_fused_below(gpu, dtype, B, K):
+    """The layer below's ReLU backward fused into the skinny layer's dX (bact): dX = (x > 0) * d w."""
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(8)
+    x = torch.relu(torch.randn(B, K, device=gpu)).to(dtype)
+    w = torch.randn(1, K, device=gpu).to(dtype)
+    y = torch.sigmoid(x.float() @ w.float().t()).to(dtype)
+    dy = torch.randn(B, 1, device=gpu).to(dtype)
+    d = dy.float() * y.float() * (1 - y.float())
+    dx = torch.empty(B, K, device=gpu, dtype=dtype)
+    dw = torch.zeros(K, device=gpu)
+    db = torch.zeros(1, device=gpu)
+    Kk.C().skinny_bwd(x, w, y, dy, dx, False, dw, db, 12, 11)
+    tol = 1e-4 if dtype == torch.float32 else 1e-2
+    assert rel_err(dx, (d * w.float()) * (x.float() > 0)) < tol
+    assert rel_err(dw, (x.float() * d).sum(0)) < (1e-4 if dtype == torch.float32 else 1e-3)
+
+
 def test_init_fill_matches_cpu(gpu):
     from flexmi.core.initializers import NormInitializer, UniformInitializer
     for init in [UniformInitializer(7, -0.5, 0.5), NormInitializer(9, 0.0, 2.0)]:
