@@ -304,6 +304,13 @@ def run_once(a, dtype, comm, strategy=None):
             "process_world": world,
         },
     }
+    if cuda and cfg.compute_dtype == "fp32":
+        # how the fp32 GEMMs run: 3 = the exact three-way bf16 split kernel (gemm_x3.hip, products
+        # exact in fp32, fp32 accumulation; float64-oracle tests at the native kernel's tolerance)
+        # for the big layers, the native v_mfma_f32_16x16x4_f32 kernel for the rest
+        from flexmi.ops import _kernels as _K
+        rec["config"]["fp32_gemm"] = {0: "native-f32-mfma", 1: "bf16x3-split-v1", 2: "bf16x3-split-all",
+                                      3: "bf16x3-split-big+native-f32-mfma"}.get(_K.C().gemm_f32_get_split(), "?")
     if search is not None:
         rec["config"]["search"] = dict(search)
     if rank == 0 and a.profile:

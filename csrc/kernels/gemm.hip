@@ -263,8 +263,7 @@ __global__ void fm_gemm_splitk_reduce4(GemmP p) {
     const long zb = e4 / MN, e = e4 % MN;
     const int m = (int)(e / p.N), n = (int)(e % p.N);
     const float* src = p.ws + zb * p.ksplit * MN + e;
-    f32x4_t s = *reinterpret_cast<const f32x4_t*>(src);
-    for (int k = 1; k < p.ksplit; ++k) s += *reinterpret_cast<const f32x4_t*>(src + k * MN);
+    f32x4_t s = slab_sum4(src, MN, p.ksplit);
     s *= p.alpha;
     if constexpr (SGD) {
       sgd_apply4(p, (long)m * p.ldc + n, s);
@@ -310,8 +309,7 @@ __global__ void fm_gemm_splitk_reduce(GemmP p) {
     long zb = i / MN, e = i % MN;
     int m = (int)(e / p.N), n = (int)(e % p.N);
     const float* src = p.ws + zb * p.ksplit * MN + e;
-    float s = 0.f;
-    for (int k = 0; k < p.ksplit; ++k) s += src[k * MN];
+    float s = slab_sum1(src, MN, p.ksplit);
     float v = s * p.alpha;
     if constexpr (SGD) {
       sgd_apply1(p, (long)m * p.ldc + n, v);
@@ -344,15 +342,14 @@ __global__ void __launch_bounds__(256) fm_gemm_splitk_reduce_bwd(GemmP p, int RB
     const float* src = p.ws + (long)m * p.N + n;
     float sv[4] = {0.f, 0.f, 0.f, 0.f};
     if (v4) {
-      f32x4_t a = *reinterpret_cast<const f32x4_t*>(src);
-      for (int k = 1; k < p.ksplit; ++k) a += *reinterpret_cast<const f32x4_t*>(src + k * MN);
+      f32x4_t a = slab_sum4(src, MN, p.ksplit);
 #pragma unroll
       for (int r = 0; r < 4; ++r) sv[r] = a[r];
     } else {
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         if (n + r < p.N)
-          for (int k = 0; k < p.ksplit; ++k) sv[r] += src[k * MN + r];
+          sv[r] = slab_sum1(src + r, MN, p.ksplit);
     }
     const long ci = (long)m * p.ldc + n;
 #pragma unroll

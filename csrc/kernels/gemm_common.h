@@ -141,6 +141,44 @@ FM_DEVICE void tile_coords(const GemmP& p, int bid, int& tm, int& tn) {
   }
 }
 
+// Sum of ks split-K slabs (MN floats apart) in slab order, with up to eight loads in flight: a
+// plain `for k: s += slab[k]` waits for each load before issuing the next (one HBM round trip per
+// slab -- 16 us for a 16-way reduce).  Same additions in the same order as that loop.
+FM_DEVICE f32x4_t slab_sum4(const float* __restrict__ src, long MN, int ks) {
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  int k = 0;
+  for (; k + 8 <= ks; k += 8) {
+    f32x4_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const f32x4_t*>(src + (long)(k + u) * MN);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  if (k + 4 <= ks) {
+    f32x4_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const f32x4_t*>(src + (long)(k + u) * MN);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc += v[u];
+    k += 4;
+  }
+  for (; k < ks; ++k) acc += *reinterpret_cast<const f32x4_t*>(src + (long)k * MN);
+  return acc;
+}
+FM_DEVICE float slab_sum1(const float* __restrict__ src, long MN, int ks) {
+  float acc = 0.f;
+  int k = 0;
+  for (; k + 8 <= ks; k += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = src[(long)(k + u) * MN];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  for (; k < ks; ++k) acc += src[(long)k * MN];
+  return acc;
+}
+
 // XCD-aware bijective remap of the tile id (blocks b and b+8 share an XCD)
 FM_DEVICE int xcd_remap(int bid, int ntiles) {
   int q = ntiles / 8, r = ntiles % 8, x = bid % 8;

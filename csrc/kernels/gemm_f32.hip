@@ -186,8 +186,7 @@ __global__ void fm_gemm_f32_reduce(GemmF p, int v4) {
     const float* src = p.ws + zb * p.ksplit * MN + e;
     float* d = p.C + zb * p.sC + (long)m * p.ldc + n;
     if (v4) {
-      f32x4_t s = *reinterpret_cast<const f32x4_t*>(src);
-      for (int k = 1; k < p.ksplit; ++k) s += *reinterpret_cast<const f32x4_t*>(src + k * MN);
+      f32x4_t s = slab_sum4(src, MN, p.ksplit);
       if constexpr (SGD) {
         sgd_apply4(p, (long)m * p.ldc + n, s * p.alpha);
         continue;
@@ -197,8 +196,7 @@ __global__ void fm_gemm_f32_reduce(GemmF p, int v4) {
       if (p.beta) s += *reinterpret_cast<const f32x4_t*>(d);
       *reinterpret_cast<f32x4_t*>(d) = s;
     } else {
-      float s = 0.f;
-      for (int k = 0; k < p.ksplit; ++k) s += src[k * MN];
+      float s = slab_sum1(src, MN, p.ksplit);
       if constexpr (SGD) {
         sgd_apply1(p, (long)m * p.ldc + n, s * p.alpha);
         continue;
@@ -491,15 +489,14 @@ __global__ void __launch_bounds__(256) fm_gemm_f32_reduce_bwd(GemmF p, int RB) {
     const float* src = p.ws + (long)m * p.N + n;
     float sv[4] = {0.f, 0.f, 0.f, 0.f};
     if (v4) {
-      f32x4_t a = *reinterpret_cast<const f32x4_t*>(src);
-      for (int k = 1; k < p.ksplit; ++k) a += *reinterpret_cast<const f32x4_t*>(src + k * MN);
+      f32x4_t a = slab_sum4(src, MN, p.ksplit);
 #pragma unroll
       for (int r = 0; r < 4; ++r) sv[r] = a[r];
     } else {
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         if (n + r < p.N)
-          for (int k = 0; k < p.ksplit; ++k) sv[r] += src[k * MN + r];
+          sv[r] = slab_sum1(src + r, MN, p.ksplit);
     }
     float* d = p.C + (long)m * p.ldc + n;
 #pragma unroll
@@ -1118,8 +1115,10 @@ extern "C" void fm_gemm_f32_set_variant(int v) { g_f32_variant = v; }
 //   B_kcontig: B stored [N][K] (ldb >= K) else [K][N] (ldb >= N)
 static int g_f32_split = -1;   // -1: from FM_F32_SPLIT at the first call
 extern "C" void fm_gemm_f32_set_split(int on) { g_f32_split = on < 0 ? 0 : on; }
+// default 3: the split kernel (gemm_x3.hip) for the big GEMMs, where it beat both the native
+// fp32 MFMA kernel and hipBLASLt on every DLRM shape and orientation (profiles/gemm_f32_lab_r5i_*)
 static int f32_split_mode() {
-  if (g_f32_split < 0) g_f32_split = getenv("FM_F32_SPLIT") != nullptr ? std::max(0, atoi(getenv("FM_F32_SPLIT"))) : 0;
+  if (g_f32_split < 0) g_f32_split = getenv("FM_F32_SPLIT") != nullptr ? std::max(0, atoi(getenv("FM_F32_SPLIT"))) : 3;
   return g_f32_split;
 }
 extern "C" int fm_gemm_f32_get_split() { return f32_split_mode(); }
@@ -1197,7 +1196,9 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
   // (even row counts).
   static const int x3_min_mn = getenv("FM_X3_MIN_MN") ? atoi(getenv("FM_X3_MIN_MN")) : 480;
   static const int x3_min_k = getenv("FM_X3_MIN_K") ? atoi(getenv("FM_X3_MIN_K")) : 480;
-  const bool x3_pick = g_f32_split == 2 || (g_f32_split == 3 && std::min(M, N) >= x3_min_mn && K >= x3_min_k);
+  // (an explicit A/B kernel variant, FM_GEMM_F32_VARIANT / fm_gemm_f32_set_variant, bypasses the auto policy)
+  const bool x3_pick = g_f32_split == 2 || (g_f32_split == 3 && (upd || g_f32_variant == 0) &&
+                                            std::min(M, N) >= x3_min_mn && K >= x3_min_k);
   if (x3_pick && K > 0 && K % 32 == 0 && M >= 64 && N >= 64) {
     auto opnd_ok = [&](const float* X, long ld, long sX, bool kc, int rows) {
       return kc ? (al(X) && ld % 4 == 0 && sX % 4 == 0)

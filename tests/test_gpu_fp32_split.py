@@ -17,9 +17,19 @@ MODES = [1, 2]
 @pytest.fixture(params=MODES)
 def split(request):
     from flexmi.ops import _kernels as Kk
+    prev = Kk.C().gemm_f32_get_split()
     Kk.C().gemm_f32_set_split(request.param)
     yield Kk
-    Kk.C().gemm_f32_set_split(0)
+    Kk.C().gemm_f32_set_split(prev)
+
+
+@pytest.fixture(autouse=True)
+def _restore_split_mode():
+    """Tests below switch the split mode explicitly; leave the process default (3) behind."""
+    from flexmi.ops import _kernels as Kk
+    prev = Kk.C().gemm_f32_get_split()
+    yield
+    Kk.C().gemm_f32_set_split(prev)
 
 
 def _gemm(Kk, A, B, a_k, b_k, M, N, K):
