@@ -80,7 +80,7 @@ int fm_dot_interaction_bwd_f32g(const float* const* z, const void* const* ix, co
 void fm_dot_interaction_fwd_f32(const float* const* z, int F, long ldz, float* out, long ldo, long B, int D, int W, int self,
                                 hipStream_t s);
 void fm_dot_interaction_bwd_f32(const float* const* z, int F, long ldz, const float* dout, long ldo, float* const* dz,
-                                long lddz, unsigned acc_mask, long B, int D, int self, hipStream_t s);
+                                long lddz, unsigned acc_mask, long B, int D, int self, int act0, hipStream_t s);
 void fm_sgd_update(float* W, float* G, float* V, unsigned short* Wc, const float* lr, long n, float wd, float mom,
                    int nesterov, int zero_g, hipStream_t s);
 void fm_adam_update(float* W, float* G, float* M, float* V, unsigned short* Wc, long n, const float* alpha_t,
@@ -615,8 +615,10 @@ void dot_fwd(std::vector<torch::Tensor> zs, int64_t ldz, torch::Tensor out, int6
   fm_dot_interaction_fwd(p.data(), (int)p.size(), ldz, out.data_ptr(), ldo, B, (int)D, (int)W, self ? 1 : 0, cur());
 }
 
+// act0 (fp32 only): activation backward of feature 0's producer applied to dz[0] (10 = none)
 void dot_bwd(std::vector<torch::Tensor> zs, int64_t ldz, torch::Tensor dout, int64_t ldo,
-             std::vector<c10::optional<torch::Tensor>> dzs, int64_t lddz, int64_t acc_mask, int64_t D, bool self) {
+             std::vector<c10::optional<torch::Tensor>> dzs, int64_t lddz, int64_t acc_mask, int64_t D, bool self,
+             int64_t act0) {
   std::vector<const void*> p;
   std::vector<void*> g;
   for (auto& z : zs) p.push_back(z.data_ptr());
@@ -634,9 +636,10 @@ void dot_bwd(std::vector<torch::Tensor> zs, int64_t ldz, torch::Tensor dout, int
       if (g[i]) TORCH_CHECK(dzs[i]->scalar_type() == torch::kFloat32 && dzs[i]->numel() >= (B - 1) * lddz + D, "dot bwd: fp32 grads");
     }
     fm_dot_interaction_bwd_f32((const float* const*)p.data(), (int)F, ldz, dout.data_ptr<float>(), ldo, (float* const*)g.data(),
-                               lddz, (unsigned)acc_mask, B, (int)D, self ? 1 : 0, cur());
+                               lddz, (unsigned)acc_mask, B, (int)D, self ? 1 : 0, (int)act0, cur());
     return;
   }
+  TORCH_CHECK(act0 == 10, "dot interaction backward: act0 is fp32-only");
   TORCH_CHECK(D % 8 == 0 && D <= 256, "dot interaction backward: D % 8 == 0, D <= 256");
   fm_dot_interaction_bwd(p.data(), (int)p.size(), ldz, dout.data_ptr(), ldo, g.data(), lddz, (unsigned)acc_mask,
                          dout.size(0), (int)D, self ? 1 : 0, cur());
@@ -1255,7 +1258,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("sdp_coalesce", &sdp_coalesce);
   m.def("sdp_apply", &sdp_apply);
   m.def("dot_fwd", &dot_fwd);
-  m.def("dot_bwd", &dot_bwd);
+  m.def("dot_bwd", &dot_bwd, py::arg("zs"), py::arg("ldz"), py::arg("dout"), py::arg("ldo"), py::arg("dzs"),
+        py::arg("lddz"), py::arg("acc_mask"), py::arg("D"), py::arg("self"), py::arg("act0") = 10);
   m.def("dot_fwd_gather", &dot_fwd_gather);
   m.def("dot_bwd_gather", &dot_bwd_gather);
   m.def("sgd", &sgd);

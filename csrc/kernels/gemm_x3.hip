@@ -25,6 +25,9 @@
 //     have a whole step of MFMAs to land;
 //   * MN-contiguous operands (dX's W, both dW operands) are transposed in registers: a staging
 //     unit is 2 rows x 4 k (four 8-B loads), written as 8-B halves of the rows' chunks.
+// Measured and dropped: fp32 LDS images with the split done per fragment in registers (LDS stage
+// 48 instead of 72 KiB) -- 119 vs 95 us on 8192x1024x1024, the per-wave split VALU work (8 floats
+// per fragment, 24 fragments a step) outweighs the staging split it replaces (gpurun_out r5j).
 // Tiles: 256x128 (8 waves, 144 KiB LDS) or 128x128 (4 waves, 96 KiB), one block per CU,
 // XCD-aware tile order, split-K slabs / fused epilogues / fused SGD shared with the native kernel
 // (gemm_f32_common.h epilogue_f32).
@@ -38,9 +41,6 @@ constexpr int XK = 32;   // k per stage
 
 // byte offset of 16-B chunk c (8 bf16) of row r in a [row][32 bf16] plane
 FM_DEVICE int x3_off(int r, int c) { return r * 64 + 16 * (c ^ ((r >> 1) & 3)); }
-
-// byte offset of 16-B chunk c (4 fp32) of row r in a [row][32 fp32] image (register-split form)
-FM_DEVICE int x3r_off(int r, int c) { return r * 128 + 16 * (c ^ (r & 7)); }
 
 // exact truncation split of one fp32 value: x = h + m + l, each a bf16 (returned as fp32 bits
 // with zero low halves)
@@ -138,28 +138,6 @@ struct X3Stage {
           *reinterpret_cast<u32x2_t*>(pl1 + off) = m;
           *reinterpret_cast<u32x2_t*>(pl2 + off) = l;
         }
-      }
-    }
-  }
-
-  // register-split form: the raw fp32 values into a [row][32 fp32] image (128-B rows, 16-B chunk c
-  // of row r at r * 128 + 16 * (c ^ (r & 7)))
-  FM_DEVICE void store_f32(char* img, int tid) const {
-#pragma unroll
-    for (int i = 0; i < PER_T; ++i) {
-      const int ci = tid + NTH * i;
-      if (UNITS % NTH != 0 && ci >= UNITS) continue;
-      if constexpr (KC) {
-        const int r = ci >> 2, cc = ci & 3;
-        *reinterpret_cast<f32x4_t*>(img + x3r_off(r, 2 * cc)) = a[i];
-        *reinterpret_cast<f32x4_t*>(img + x3r_off(r, 2 * cc + 1)) = b[i];
-      } else {
-        constexpr int RP = R / 2;
-        const int rp = ci % RP, kq = ci / RP;
-#pragma unroll
-        for (int e = 0; e < 2; ++e)
-          *reinterpret_cast<f32x4_t*>(img + x3r_off(2 * rp + e, kq)) =
-              f32x4_t{c[i][0][e], c[i][1][e], c[i][2][e], c[i][3][e]};
       }
     }
   }
@@ -320,153 +298,6 @@ __global__ void __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) fm_gemm_x3v2_ke
   epilogue_f32<MR, NR, false, false, SGD>(p, acc, zb, split, m0 + wm * 64, n0 + wn * 64, lane);
 }
 
-// Register-split form (FM_X3_MODE=1): the LDS stages hold the raw fp32 operands (48 KiB per
-// 256x128x32 stage instead of 72 KiB of planes, no split in the staging pass); each wave splits
-// the fragments it reads -- two 16-B reads give the 8 k values of one bf16 fragment -- in
-// registers, where the split VALU work sits between MFMAs instead of ahead of them.
-template <bool KC>
-FM_DEVICE void x3r_frag(const char* img, int row, int g, bf16x8_t& h, bf16x8_t& m, bf16x8_t& l) {
-  const f32x4_t lo = *reinterpret_cast<const f32x4_t*>(img + x3r_off(row, 2 * g));
-  const f32x4_t hi = *reinterpret_cast<const f32x4_t*>(img + x3r_off(row, 2 * g + 1));
-  u32x4_t hh, mm, ll;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const f32x4_t& v = u < 2 ? lo : hi;
-    unsigned a, b, c;
-    split2(v[2 * (u & 1)], v[2 * (u & 1) + 1], a, b, c);
-    hh[u] = a;
-    mm[u] = b;
-    ll[u] = c;
-  }
-  h = __builtin_bit_cast(bf16x8_t, hh);
-  m = __builtin_bit_cast(bf16x8_t, mm);
-  l = __builtin_bit_cast(bf16x8_t, ll);
-}
-
-template <int BM, int BN, bool AK, bool BKC, bool SGD>
-__global__ void __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) fm_gemm_x3r_kernel(GemmF p) {
-  constexpr int WM = BM / 64, WN = BN / 64, NTH = WM * WN * 64;
-  constexpr int MR = 4, NR = 4;
-  constexpr int IA = BM * 128, IB = BN * 128;          // bytes of the fp32 images
-  constexpr int STG = IA + IB;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const int bid = xcd_remap_f(blockIdx.x, p.tiles_m * p.tiles_n);
-  int tm, tn;
-  if (p.n_fast) {
-    tn = bid % p.tiles_n;
-    tm = bid / p.tiles_n;
-  } else {
-    tm = bid % p.tiles_m;
-    tn = bid / p.tiles_m;
-  }
-  const int zb = blockIdx.y, split = blockIdx.z;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const float* A = p.A + (long)zb * p.sA;
-  const float* B = p.B + (long)zb * p.sB;
-  const int ktiles = p.K / XK;
-  const int kt_per = (ktiles + p.ksplit - 1) / p.ksplit;
-  const int kt0 = split * kt_per, kt1 = min(ktiles, kt0 + kt_per);
-  const int nst = kt1 - kt0;
-
-  f32x4_t acc[MR][NR];
-#pragma unroll
-  for (int i = 0; i < MR; ++i)
-#pragma unroll
-    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  X3Stage<AK, BM, NTH> sa;
-  X3Stage<BKC, BN, NTH> sb;
-  const bool dorow = (!AK) && p.rowsum_a != nullptr && tn == 0;
-  float rs[2] = {0.f, 0.f};
-  auto put = [&](int s) {
-    char* b = smem + s * STG;
-    sa.store_f32(b, tid);
-    sb.store_f32(b + IA, tid);
-    if constexpr (!AK) {
-      if (dorow) sa.rowsum(rs, tid);
-    }
-  };
-  auto get = [&](int kt) {
-    sa.load(A, p.lda, m0, p.M, kt * XK, tid);
-    sb.load(B, p.ldb, n0, p.N, kt * XK, tid);
-  };
-  if (nst > 0) {
-    get(kt0);
-    put(0);
-    if (nst > 1) get(kt0 + 1);
-  }
-  const int q = lane & 15, g = lane >> 4;
-  for (int t = 0; t < nst; ++t) {
-    __syncthreads();                 // stage t&1 complete; stage (t+1)&1 no longer read
-    const char* la = smem + (t & 1) * STG;
-    const char* lb = la + IA;
-    bf16x8_t bh[NR], bm[NR], bl[NR];
-#pragma unroll
-    for (int j = 0; j < NR; ++j) x3r_frag<BKC>(lb, wn * 64 + 16 * j + q, g, bh[j], bm[j], bl[j]);
-    if (t + 1 < nst) {
-      put((t + 1) & 1);
-      if (t + 2 < nst) get(kt0 + t + 2);
-    }
-#pragma unroll
-    for (int i = 0; i < MR; ++i) {
-      bf16x8_t ah, am, al;
-      x3r_frag<AK>(la, wm * 64 + 16 * i + q, g, ah, am, al);
-      // small terms first, the dominant h*h product last; NR independent chains per term
-#define X3R_MFMA(BP, AP)                                                                                     \
-  _Pragma("unroll") for (int j = 0; j < NR; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(          \
-      *reinterpret_cast<bf16x8v_t*>(&BP[j]), *reinterpret_cast<bf16x8v_t*>(&AP), acc[i][j], 0, 0, 0);
-      X3R_MFMA(bh, al)
-      X3R_MFMA(bm, am)
-      X3R_MFMA(bl, ah)
-      X3R_MFMA(bh, am)
-      X3R_MFMA(bm, ah)
-      X3R_MFMA(bh, ah)
-#undef X3R_MFMA
-    }
-  }
-  if constexpr (!AK) {
-    if (dorow) {   // threads sharing a row pair: reduce through LDS, one atomic per row
-      __syncthreads();
-      float* red = reinterpret_cast<float*>(smem);
-      constexpr int RP = BM / 2;
-      red[tid * 2] = rs[0];
-      red[tid * 2 + 1] = rs[1];
-      __syncthreads();
-      if (tid < BM) {
-        const int rp = tid >> 1, e = tid & 1;
-        float x = 0.f;
-        for (int s = rp; s < NTH; s += RP) x += red[2 * s + e];
-        if (m0 + tid < p.M) atomicAdd(p.rowsum_a + m0 + tid, x);
-      }
-    }
-  }
-  epilogue_f32<MR, NR, false, false, SGD>(p, acc, zb, split, m0 + wm * 64, n0 + wn * 64, lane);
-}
-
-template <int BM, int BN, bool SGD>
-void launch_x3r(const GemmF& p, bool ak, bool bk, hipStream_t s) {
-  constexpr int NTH = (BM / 64) * (BN / 64) * 64;
-  constexpr int LDS = 2 * (BM + BN) * 128;
-  dim3 grid(p.tiles_m * p.tiles_n, p.batch, p.ksplit);
-#define FM_X3R(AKv, BKv)                                                                                         \
-  do {                                                                                                           \
-    static bool attr = false;                                                                                    \
-    if (!attr) {                                                                                                 \
-      (void)hipFuncSetAttribute((const void*)fm_gemm_x3r_kernel<BM, BN, AKv, BKv, SGD>,                         \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS);                                \
-      attr = true;                                                                                               \
-    }                                                                                                            \
-    hipLaunchKernelGGL((fm_gemm_x3r_kernel<BM, BN, AKv, BKv, SGD>), grid, dim3(NTH), LDS, s, p);               \
-  } while (0)
-  if (ak && bk) FM_X3R(true, true);
-  else if (ak) FM_X3R(true, false);
-  else if (bk) FM_X3R(false, true);
-  else FM_X3R(false, false);
-#undef FM_X3R
-}
-
 template <int BM, int BN, bool SGD, int SCHED>
 void launch_x3v2_s(const GemmF& p, bool ak, bool bk, hipStream_t s) {
   constexpr int NTH = (BM / 64) * (BN / 64) * 64;
@@ -493,11 +324,6 @@ void launch_x3v2_s(const GemmF& p, bool ak, bool bk, hipStream_t s) {
 // of a SIMD run staging and MFMAs in opposite order (8-wave tile only)
 template <int BM, int BN, bool SGD>
 void launch_x3v2(const GemmF& p, bool ak, bool bk, hipStream_t s) {
-  static const int mode = getenv("FM_X3_MODE") ? atoi(getenv("FM_X3_MODE")) : 0;
-  if (mode == 1) {
-    launch_x3r<BM, BN, SGD>(p, ak, bk, s);
-    return;
-  }
   // default 2 (de-phased waves): 1013 vs 1016 us over the DLRM lab shapes, step 1.225 vs 1.234 ms
   static const int sched = getenv("FM_X3_SCHED") ? atoi(getenv("FM_X3_SCHED")) : 2;
   if (sched == 1) launch_x3v2_s<BM, BN, SGD, 1>(p, ak, bk, s);

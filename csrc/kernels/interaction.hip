@@ -438,7 +438,7 @@ __global__ void __launch_bounds__(256) fm_dot_fwd_f32(PtrTabF Z, long ldz, float
 template <int DT>
 __global__ void __launch_bounds__(256) fm_dot_bwd_f32(PtrTabF Z, long ldz, const float* __restrict__ dout, long ldo,
                                                      MPtrTabF dZ, long lddz, unsigned acc_mask, long B, int F, int Drt,
-                                                     int W, int self) {
+                                                     int W, int self, int act0) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int D = DT > 0 ? DT : Drt;
   const int Dp = (D + 31) & ~31;                 // staged Z rows padded to whole 32-column tiles
@@ -536,7 +536,10 @@ __global__ void __launch_bounds__(256) fm_dot_bwd_f32(PtrTabF Z, long ldz, const
           const int i = (t & 3) + 8 * (t >> 2) + 4 * h;
           if (i >= F || dZ.p[i] == nullptr) continue;
           float v = acc[t];
-          if (i == 0) v += ds[n];
+          if (i == 0) {
+            v += ds[n];
+            if (act0 != ACT_NONE) v = act_bwd(act0, zs[n], v);   // z0 staged as row 0
+          }
           float* d = dZ.p[i] + b * lddz + n;
           if ((acc_mask >> i) & 1u) v += *d;
           *d = v;
@@ -625,7 +628,7 @@ template <> struct VecF<1> { using type = float; };
 template <int E, int NKS, bool ACC, typename ZT = PtrTabF>
 __global__ void __launch_bounds__(256, 2) fm_dot_bwd_f32r(ZT Z, long ldz, const float* __restrict__ dout, long ldo,
                                                          MPtrTabF dZ, long lddz, unsigned acc_mask, long B, int F,
-                                                         int W, int self) {
+                                                         int W, int self, int act0) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int D = 32 * E;
   constexpr int DCH = 4;                           // dOut float4 chunks per lane (W <= 1024)
@@ -697,6 +700,7 @@ __global__ void __launch_bounds__(256, 2) fm_dot_bwd_f32r(ZT Z, long ldz, const 
       a[ks] = v;
     }
     const vecE x0 = *reinterpret_cast<const vecE*>(ds + E * r);   // dZ_0 += dOut[:, :D]
+    const vecE z0 = zn[0];         // lanes h = 0: row 0 of this sample (for act0; zn is reloaded below)
     f32x16_t acc[E];
 #pragma unroll
     for (int e = 0; e < E; ++e)
@@ -728,7 +732,18 @@ __global__ void __launch_bounds__(256, 2) fm_dot_bwd_f32r(ZT Z, long ldz, const 
 #pragma unroll
         for (int e = 0; e < E; ++e) v[e] = acc[e][t];
       }
-      if (i == 0) v += x0;
+      if (i == 0) {
+        v += x0;
+        // act0: the activation backward of feature 0's producer (the bottom MLP's last layer,
+        // whose output z0 is), so that layer skips its own act-bwd pass
+        if (act0 != ACT_NONE) {
+          if constexpr (E == 1) v = act_bwd(act0, z0, v);
+          else {
+#pragma unroll
+            for (int e = 0; e < E; ++e) v[e] = act_bwd(act0, z0[e], v[e]);
+          }
+        }
+      }
       if (i < F && q != nullptr) {
         float* d = q + b * lddz + E * r;
         if constexpr (ACC) {
@@ -783,9 +798,10 @@ extern "C" void fm_dot_interaction_fwd_f32(const float* const* z, int F, long ld
   hipLaunchKernelGGL(k, dim3((int)blocks), dim3(64 * waves), lds, s, t, ldz, out, ldo, B, F, D, W, self);
 }
 
+// act0: activation backward (of z[0]'s producer) applied to dz[0]; ACT_NONE = plain gradient
 extern "C" void fm_dot_interaction_bwd_f32(const float* const* z, int F, long ldz, const float* dout, long ldo,
                                            float* const* dz, long lddz, unsigned acc_mask, long B, int D, int self,
-                                           hipStream_t s) {
+                                           int act0, hipStream_t s) {
   PtrTabF t;
   MPtrTabF g;
   for (int i = 0; i < MAXF; ++i) {
@@ -813,7 +829,7 @@ extern "C" void fm_dot_interaction_bwd_f32(const float* const* z, int F, long ld
              : E == 2 ? (acc ? fm_dot_bwd_f32r<2, 16, true> : fm_dot_bwd_f32r<2, 16, false>)
                       : (acc ? fm_dot_bwd_f32r<1, 16, true> : fm_dot_bwd_f32r<1, 16, false>);
       hipLaunchKernelGGL(k, dim3((int)blocks), dim3(64 * waves), (size_t)waves * wpad * 4, s, t, ldz, dout, ldo, g, lddz,
-                         acc_mask, B, F, W, self);
+                         acc_mask, B, F, W, self, act0);
       return;
     }
   }
@@ -822,7 +838,7 @@ extern "C" void fm_dot_interaction_bwd_f32(const float* const* z, int F, long ld
   auto k = !fast ? fm_dot_bwd_f32<0> : D == 128 ? fm_dot_bwd_f32<128> : D == 64 ? fm_dot_bwd_f32<64>
                                      : D == 32 ? fm_dot_bwd_f32<32> : fm_dot_bwd_f32<16>;
   hipLaunchKernelGGL(k, dim3((int)blocks), dim3(64 * waves), lds, s, t, ldz, dout, ldo, g, lddz, acc_mask, B, F, D, Wr,
-                     self);
+                     self, act0);
 }
 
 // Gathered-row forms (GatherTabF): feature i reads p[i] + ix[i][b] * ld[i] (ix[i] null: row b).
@@ -888,7 +904,7 @@ extern "C" int fm_dot_interaction_bwd_f32g(const float* const* z, const void* co
          : E == 2 ? (acc ? fm_dot_bwd_f32r<2, 16, true, GatherTabF> : fm_dot_bwd_f32r<2, 16, false, GatherTabF>)
                   : (acc ? fm_dot_bwd_f32r<1, 16, true, GatherTabF> : fm_dot_bwd_f32r<1, 16, false, GatherTabF>);
   hipLaunchKernelGGL(k, dim3((int)blocks), dim3(64 * waves), (size_t)waves * wpad * 4, s, t, 0L, dout, ldo, g, lddz,
-                     acc_mask, B, F, W, self);
+                     acc_mask, B, F, W, self, (int)ACT_NONE);
   return 0;
 }
 

@@ -51,7 +51,7 @@ void fm_embedding_bwd(const void* idx, int idx64, const void* dy, int dy_bf16, f
 void fm_dot_interaction_fwd_f32(const float* const* z, int F, long ldz, float* out, long ldo, long B, int D, int W, int self,
                                 hipStream_t s);
 void fm_dot_interaction_bwd_f32(const float* const* z, int F, long ldz, const float* dout, long ldo, float* const* dz,
-                                long lddz, unsigned acc_mask, long B, int D, int self, hipStream_t s);
+                                long lddz, unsigned acc_mask, long B, int D, int self, int act0, hipStream_t s);
 }
 
 namespace flexmi {
@@ -174,7 +174,7 @@ class HipEngine : public Engine {
     fm_dot_interaction_fwd_f32(z, F, D, y, W, M, D, W, 0, st_);
   }
   void dot_bwd(const float* const* z, int F, const float* dy, float* const* dz, int M, int D, int W) override {
-    fm_dot_interaction_bwd_f32(z, F, D, dy, W, dz, D, 0u, M, D, 0, st_);
+    fm_dot_interaction_bwd_f32(z, F, D, dy, W, dz, D, 0u, M, D, 0, ACT_NONE, st_);
   }
   void all_to_all(const float* send, const int64_t* send_counts, float* recv, const int64_t* recv_counts) override {
     if (!comm_) {

@@ -313,14 +313,17 @@ def dot_interaction_forward(inputs, y, self_inter):
     C().dot_fwd(list(inputs), inputs[0].stride(0), y, y.stride(0), D, y.shape[1], bool(self_inter))
 
 
-def dot_interaction_backward(inputs, dy, in_grads, accs, self_inter):
+def dot_interaction_backward(inputs, dy, in_grads, accs, self_inter, act0=10):
+    """act0 (fp32): the activation backward of input 0's producer applied to its gradient (the
+    executor's bottom-MLP fusion: that Linear then takes the gradient as its pre-activation one)."""
     D = inputs[0].shape[-1]
     mask = 0
     for i, a in enumerate(accs):
         if a and in_grads[i] is not None:
             mask |= 1 << i
     ld = next((g.stride(0) for g in in_grads if g is not None), D)
-    C().dot_bwd(list(inputs), inputs[0].stride(0), dy, dy.stride(0), list(in_grads), ld, mask, D, bool(self_inter))
+    C().dot_bwd(list(inputs), inputs[0].stride(0), dy, dy.stride(0), list(in_grads), ld, mask, D, bool(self_inter),
+                int(act0))
 
 
 def dot_interaction_forward_gather(srcs, ixs, y, self_inter):

@@ -238,7 +238,8 @@ class DotInteraction(Op):
                 assert ok, f"{self.name}: gathered interaction backward did not launch (forward did)"
                 return
             K.dot_interaction_backward(list(ctx.inputs), dy, list(ctx.in_grads),
-                                       list(ctx.in_grad_accumulate), self.self_interaction)
+                                       list(ctx.in_grad_accumulate), self.self_interaction,
+                                       ctx.saved.get("act0", 10))
             return
         Z = torch.stack([t.float() for t in ctx.inputs], dim=1)
         B = Z.shape[0]

@@ -902,6 +902,7 @@ class Executor:
         self._build_binary_relu_fusion(ops)
         self._build_conv_chain_fusion(ops)
         self._build_gather_fusion(ops)
+        self._build_interaction_act_fusion(ops)    # after the gather fusion: not with gathered rows
         if self.backend == "hip":
             # dW split-K reduces on a side stream (csrc/kernels/gemm_async.hip), joined before
             # every collective and at the end of the backward program (_with_gemm_joins)
@@ -965,6 +966,30 @@ class Executor:
                     or not self.need[(l2.guid, idx)].same_as(self.home[t.guid]) or c2.in_grads[0] is None):
                 continue
             c2.saved["fuse_below"] = (c1.outputs[0], op.activation)
+            c1.saved["grad_is_dpre"] = True
+
+    def _build_interaction_act_fusion(self, ops):
+        """Linear L -> DotInteraction input 0 (the DLRM bottom MLP's last layer; L's output consumed
+        only there, same layout, fp32): the interaction backward applies L's activation backward to
+        the gradient it writes (interaction.hip act0), so L skips its separate act-bwd / bias-grad
+        pass and sums its bias gradient in its dW GEMM."""
+        from flexmi.core.types import OperatorType
+        if self.backend != "hip" or self.cfg.compute_dtype != "fp32" or os.environ.get("FM_DOT_ACT0", "1") == "0":
+            return
+        for op in ops:
+            if op.op_type != OperatorType.OP_LINEAR or getattr(op, "skip_act_grad", False):
+                continue
+            c1 = self.ctx.get(op.guid)
+            t = op.outputs[0]
+            cons = self.consumers.get(t.guid, [])
+            if c1 is None or len(cons) != 1 or t is self.final or c1.saved.get("grad_is_dpre"):
+                continue
+            dop, idx = cons[0]
+            cd = self.ctx.get(dop.guid)
+            if (type(dop).__name__ != "DotInteraction" or idx != 0 or cd is None or cd.in_grads[0] is None
+                    or "gather" in cd.saved or not self.need[(dop.guid, idx)].same_as(self.home[t.guid])):
+                continue
+            cd.saved["act0"] = int(op.activation)
             c1.saved["grad_is_dpre"] = True
 
     def _build_binary_relu_fusion(self, ops):

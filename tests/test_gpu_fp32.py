@@ -193,6 +193,31 @@ def test_dot_interaction_f32(gpu, F, D, selfi):
         assert rel_err(dz[i], exp) < TOL, i
 
 
+@pytest.mark.parametrize("F,D,selfi", [(27, 128, False), (27, 64, False), (9, 24, True), (5, 128, True)])
+def test_dot_interaction_f32_act0(gpu, F, D, selfi):
+    """act0: the bottom MLP's ReLU backward applied to feature 0's gradient inside the interaction
+    backward (fast and fallback kernels), vs a float64 oracle."""
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(10)
+    B = 1000
+    zs = [torch.randn(B, D, device=gpu) for _ in range(F)]
+    zs[0] = torch.relu(zs[0])                          # a ReLU output: about half the entries 0
+    npairs = F * (F + 1) // 2 if selfi else F * (F - 1) // 2
+    W = (D + npairs + 15) // 16 * 16
+    Z = torch.stack([z.double() for z in zs], 1)
+    li, lj = zip(*[(i, j) for i in range(F) for j in range(i + (1 if selfi else 0))])
+    dy = torch.randn(B, W, device=gpu)
+    dz = [torch.empty(B, D, device=gpu) for _ in range(F)]
+    Kk.dot_interaction_backward(zs, dy, dz, [False] * F, selfi, act0=11)
+    dG = torch.zeros(B, F, F, dtype=torch.float64, device=gpu)
+    dG[:, li, lj] = dy[:, D:D + npairs].double()
+    dZ = (dG + dG.transpose(1, 2)) @ Z
+    dZ[:, 0] += dy[:, :D].double()
+    dZ[:, 0] *= (Z[:, 0] > 0).double()
+    for i in range(F):
+        assert rel_err(dz[i], dZ[:, i]) < TOL, i
+
+
 @pytest.mark.parametrize("F,D,selfi,i64", [(27, 128, False, True), (9, 64, True, False), (5, 32, False, True)])
 def test_dot_interaction_gather_f32(gpu, F, D, selfi, i64):
     """Embedding-into-interaction kernels: features 1.. are TABLE rows gathered by bag-1 indices
