@@ -1192,8 +1192,7 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
   // second split form (gemm_x3.hip): split in the register staging pass, double-buffered planes,
   // 64x64 per wave.  FM_F32_SPLIT=2: every eligible GEMM; 3 (auto): only the big ones, where it
   // measured faster than the native kernel (min(M, N) >= FM_X3_MIN_MN and K >= FM_X3_MIN_K, both
-  // 480 by default).  K-contiguous operands need 16-B rows, MN-contiguous ones 8-B pairs of rows
-  // (even row counts).
+  // 480 by default).  K-contiguous operands need 16-B rows; MN-contiguous ones are read per element.
   static const int x3_min_mn = getenv("FM_X3_MIN_MN") ? atoi(getenv("FM_X3_MIN_MN")) : 480;
   static const int x3_min_k = getenv("FM_X3_MIN_K") ? atoi(getenv("FM_X3_MIN_K")) : 480;
   // (an explicit A/B kernel variant, FM_GEMM_F32_VARIANT / fm_gemm_f32_set_variant, bypasses the auto policy)
@@ -1201,8 +1200,8 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
                                             std::min(M, N) >= x3_min_mn && K >= x3_min_k);
   if (x3_pick && K > 0 && K % 32 == 0 && M >= 64 && N >= 64) {
     auto opnd_ok = [&](const float* X, long ld, long sX, bool kc, int rows) {
-      return kc ? (al(X) && ld % 4 == 0 && sX % 4 == 0)
-                : ((((uintptr_t)X) & 7) == 0 && ld % 2 == 0 && sX % 2 == 0 && rows % 2 == 0);
+      (void)rows;
+      return kc ? (al(X) && ld % 4 == 0 && sX % 4 == 0) : true;   // MN-contiguous: 4-B loads
     };
     if (opnd_ok(A, lda, sA, a_kcontig, M) && opnd_ok(B, ldb, sB, b_kcontig, N)) {
       // 256x128 (8 waves, 2 per SIMD) whenever M fills it, split-K for the grid; FM_X3_BM=128 forces

@@ -24,7 +24,7 @@
 //     free stage, the loads of step t+2 are issued, and the MFMAs of step t run -- the global loads
 //     have a whole step of MFMAs to land;
 //   * MN-contiguous operands (dX's W, both dW operands) are transposed in registers: a staging
-//     unit is 2 rows x 4 k (four 8-B loads), written as 8-B halves of the rows' chunks.
+//     unit is one row x 8 k (eight 4-B loads, 256 contiguous bytes per wave-instruction).
 // Measured and dropped: fp32 LDS images with the split done per fragment in registers (LDS stage
 // 48 instead of 72 KiB) -- 119 vs 95 us on 8192x1024x1024, the per-wave split VALU work (8 floats
 // per fragment, 24 fragments a step) outweighs the staging split it replaces (gpurun_out r5j).
@@ -61,40 +61,53 @@ FM_DEVICE void split2(float a, float b, unsigned& h, unsigned& m, unsigned& l) {
   l = (la >> 16) | lb;
 }
 
-// One operand's k step (R rows x 32 k) staged through registers.  K-contiguous: unit = (row,
-// k-octet), two 16-B loads.  MN-contiguous (global [k][rows]): unit = (row pair, k-quad), four 8-B
-// loads, transposed in registers.  Rows past the edge load a clamped (valid) row and are NOT
-// zeroed: row r of A only reaches output row r (and B row n output column n), which the epilogue
-// never stores, and the row sums are stored for in-range rows only.  The loaded vectors are kept
-// as they arrive -- no select on them -- so the wait for a load lands at its use in the next
-// step's split, a whole step of MFMAs later (a select right after the load made hipcc wait for
-// every load as soon as it was issued).
-typedef float f32x2_t __attribute__((ext_vector_type(2)));
-typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
-
+// One operand's k step (R rows x 32 k) staged through registers; unit = (row, k-octet): the 8 k
+// values of one row, split and written as one 16-B chunk per plane.  K-contiguous: two 16-B loads
+// per unit, consecutive lanes take consecutive octets.  MN-contiguous (global [k][rows]): eight
+// 4-B loads per unit (one per k row), consecutive lanes take consecutive rows, so each load
+// instruction reads 256 contiguous bytes and the LDS writes land exactly like the K-contiguous
+// ones (an earlier row-pair x k-quad unit wrote 8-B halves 4-way bank-conflicted: 14 M conflicts
+// per 8192x1024x1024 dW, gpurun_out r5k).  Rows past the edge load a clamped (valid) row and are
+// NOT zeroed: row r of A only reaches output row r (and B row n output column n), which the
+// epilogue never stores, and the row sums are stored for in-range rows only.  The loaded values
+// are kept as they arrive -- no select on them -- so the wait for a load lands at its use in the
+// next step's split, a whole step of MFMAs later (a select right after the load made hipcc wait
+// for every load as soon as it was issued).
 template <bool KC, int R, int NTH>
 struct X3Stage {
   static constexpr int UNITS = R * 4;
   static constexpr int PER_T = (UNITS + NTH - 1) / NTH;
-  f32x4_t a[PER_T], b[PER_T];        // K-contiguous: k 0..3 / 4..7 of the unit's row
-  f32x2_t c[PER_T][4];               // MN-contiguous: rows (r, r+1) at k = 4 kq + kk
+  f32x4_t a[PER_T], b[PER_T];        // k 0..3 / 4..7 of the unit's row
+
+  FM_DEVICE static void unit(int ci, int& r, int& c) {
+    if constexpr (KC) {
+      r = ci >> 2;
+      c = ci & 3;
+    } else {
+      r = ci % R;
+      c = ci / R;
+    }
+  }
 
   FM_DEVICE void load(const float* __restrict__ p, long ld, int row0, int rows, int k0, int tid) {
 #pragma unroll
     for (int i = 0; i < PER_T; ++i) {
       const int ci = tid + NTH * i;
       if (UNITS % NTH != 0 && ci >= UNITS) continue;
+      int r, c;
+      unit(ci, r, c);
+      const int gr = min(row0 + r, rows - 1);
       if constexpr (KC) {
-        const int r = row0 + (ci >> 2), cc = ci & 3;
-        const float* src = p + (long)min(r, rows - 1) * ld + k0 + 8 * cc;
+        const float* src = p + (long)gr * ld + k0 + 8 * c;
         a[i] = *reinterpret_cast<const f32x4_t*>(src);
         b[i] = *reinterpret_cast<const f32x4_t*>(src + 4);
       } else {
-        constexpr int RP = R / 2;
-        const int rp = ci % RP, kq = ci / RP;
-        const float* src = p + (long)(k0 + 4 * kq) * ld + min(row0 + 2 * rp, rows - 2);
+        const float* src = p + (long)(k0 + 8 * c) * ld + gr;
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) c[i][kk] = *reinterpret_cast<const f32x2_t*>(src + kk * ld);
+        for (int kk = 0; kk < 4; ++kk) {
+          a[i][kk] = src[kk * ld];
+          b[i][kk] = src[(kk + 4) * ld];
+        }
       }
     }
   }
@@ -104,55 +117,33 @@ struct X3Stage {
     for (int i = 0; i < PER_T; ++i) {
       const int ci = tid + NTH * i;
       if (UNITS % NTH != 0 && ci >= UNITS) continue;
-      if constexpr (KC) {
-        u32x4_t h, m, l;
+      int r, c;
+      unit(ci, r, c);
+      u32x4_t h, m, l;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const f32x4_t& v = u < 2 ? a[i] : b[i];
-          unsigned hh, mm, ll;
-          split2(v[2 * (u & 1)], v[2 * (u & 1) + 1], hh, mm, ll);
-          h[u] = hh;
-          m[u] = mm;
-          l[u] = ll;
-        }
-        const int off = x3_off(ci >> 2, ci & 3);
-        *reinterpret_cast<u32x4_t*>(pl0 + off) = h;
-        *reinterpret_cast<u32x4_t*>(pl1 + off) = m;
-        *reinterpret_cast<u32x4_t*>(pl2 + off) = l;
-      } else {
-        constexpr int RP = R / 2;
-        const int rp = ci % RP, kq = ci / RP;
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {        // row 2 rp + e: its 4 k values are c[i][0..3][e]
-          u32x2_t h, m, l;
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            unsigned hh, mm, ll;
-            split2(c[i][2 * u][e], c[i][2 * u + 1][e], hh, mm, ll);
-            h[u] = hh;
-            m[u] = mm;
-            l[u] = ll;
-          }
-          const int off = x3_off(2 * rp + e, kq >> 1) + 8 * (kq & 1);
-          *reinterpret_cast<u32x2_t*>(pl0 + off) = h;
-          *reinterpret_cast<u32x2_t*>(pl1 + off) = m;
-          *reinterpret_cast<u32x2_t*>(pl2 + off) = l;
-        }
+      for (int u = 0; u < 4; ++u) {
+        const f32x4_t& v = u < 2 ? a[i] : b[i];
+        unsigned hh, mm, ll;
+        split2(v[2 * (u & 1)], v[2 * (u & 1) + 1], hh, mm, ll);
+        h[u] = hh;
+        m[u] = mm;
+        l[u] = ll;
       }
+      const int off = x3_off(r, c);
+      *reinterpret_cast<u32x4_t*>(pl0 + off) = h;
+      *reinterpret_cast<u32x4_t*>(pl1 + off) = m;
+      *reinterpret_cast<u32x4_t*>(pl2 + off) = l;
     }
   }
 
-  // MN-contiguous A (dW): per-thread sums of its two rows over the staged k (bias gradient)
-  FM_DEVICE void rowsum(float (&s)[2], int tid) const {
+  // MN-contiguous A (dW): per-thread sums of its row (tid % R, every unit) over the staged k
+  FM_DEVICE void rowsum(float& s, int tid) const {
 #pragma unroll
     for (int i = 0; i < PER_T; ++i) {
       const int ci = tid + NTH * i;
       if (UNITS % NTH != 0 && ci >= UNITS) continue;
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        s[0] += c[i][kk][0];
-        s[1] += c[i][kk][1];
-      }
+      for (int kk = 0; kk < 4; ++kk) s += a[i][kk] + b[i][kk];
     }
   }
 };
@@ -193,7 +184,7 @@ __global__ void __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) fm_gemm_x3v2_ke
   X3Stage<AK, BM, NTH> sa;
   X3Stage<BKC, BN, NTH> sb;
   const bool dorow = (!AK) && p.rowsum_a != nullptr && tn == 0;
-  float rs[2] = {0.f, 0.f};
+  float rs = 0.f;
   auto stage = [&](int s) { return smem + s * STG; };
   auto put = [&](int s) {
     char* b = stage(s);
@@ -280,17 +271,15 @@ __global__ void __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) fm_gemm_x3v2_ke
     }
   }
   if constexpr (!AK) {
-    if (dorow) {   // threads sharing a row pair: reduce through LDS, one atomic per row
+    if (dorow) {   // the NTH / BM threads of each row: reduce through LDS, one atomic per row
+      static_assert(NTH % BM == 0, "every thread's A units share one row");
       __syncthreads();
       float* red = reinterpret_cast<float*>(smem);
-      constexpr int RP = BM / 2;
-      red[tid * 2] = rs[0];
-      red[tid * 2 + 1] = rs[1];
+      red[tid] = rs;
       __syncthreads();
       if (tid < BM) {
-        const int rp = tid >> 1, e = tid & 1;
         float x = 0.f;
-        for (int s = rp; s < NTH; s += RP) x += red[2 * s + e];
+        for (int s = tid; s < NTH; s += BM) x += red[s];
         if (m0 + tid < p.M) atomicAdd(p.rowsum_a + m0 + tid, x);
       }
     }
@@ -335,7 +324,7 @@ void launch_x3v2(const GemmF& p, bool ak, bool bk, hipStream_t s) {
 
 // Launch on a prepared parameter block (tiles_m / tiles_n / ksplit filled for the bm x 128 tile).
 // Caller guarantees: K % 32 == 0 (per split: whole steps); K-contiguous operands 16-B aligned with
-// ld % 4 == 0; MN-contiguous operands 8-B aligned with ld % 2 == 0 and an even row count.
+// ld % 4 == 0 (MN-contiguous ones: no constraint).
 // sgd: the fused-SGD epilogue (unsplit tiles only).  Returns -1 for an unsupported tile.
 extern "C" int fm_gemm_x3v2_launch(const void* params, int bm, int a_kcontig, int b_kcontig, int sgd, hipStream_t s) {
   const GemmF& p = *static_cast<const GemmF*>(params);

@@ -4,7 +4,8 @@ On a GPU run the extension MUST be present: every call goes through :func:`C` wh
 ``flexmi._C`` cannot be imported -- there is no silent eager fallback for the hot ops (GEMM,
 embedding, interaction, optimizer, loss, element-wise, data movement, and the CNN ops: GEMM
 convolution = implicit-GEMM MFMA kernels on NCHW, HIP pooling and batch norm).
-:data:`LIBRARY_FALLBACK` lists ops routed to vendor libraries instead (the big fp32 dW GEMMs).
+:data:`LIBRARY_FALLBACK` lists ops routed to vendor libraries instead: none by default (the big fp32
+dW GEMMs went to hipBLASLt until the split-bf16 kernel beat it; ``FM_DW_LIB=1`` restores that).
 """
 from __future__ import annotations
 
@@ -15,8 +16,8 @@ import torch
 
 _C = None
 _lock = threading.Lock()
-# ops routed to a vendor library instead of a flexmi kernel (plain GEMMs only, measured faster)
-LIBRARY_FALLBACK = {"linear dW, fp32, out >= 512 and in >= 480 features": "hipBLASLt via torch addmm_ (FM_DW_LIB)"}
+# ops routed to a vendor library instead of a flexmi kernel by default (none: opt-in FM_DW_LIB=1 only)
+LIBRARY_FALLBACK = {}
 
 
 def C():
