@@ -368,7 +368,11 @@ void launch_fwd(const TabSet& s, int m, bool vec, bool out_bf16, long B, int D0,
       return;
     }
   }
-  dim3 grid((unsigned)std::max<long>(1, std::min<long>((B + rpi - 1) / rpi, 2048)), m);
+  // FM_EMB_FWD_BLOCKS: blocks per table (default 256).  The forward runs beside the bottom MLP on
+  // a second stream; fewer, longer-running blocks leave CUs to its GEMMs: MLPerf fp32 step 1.181 ms
+  // at 2048 blocks per table, 1.164 at 256, 1.172 at 64 (profiles/bench_ab_x3_sched_embgrid_r5n.txt)
+  static const long cap_env = getenv("FM_EMB_FWD_BLOCKS") ? std::max(1L, atol(getenv("FM_EMB_FWD_BLOCKS"))) : 256L;
+  dim3 grid((unsigned)std::max<long>(1, std::min<long>((B + rpi - 1) / rpi, cap_env)), m);
   if (vec) {
     if (out_bf16) hipLaunchKernelGGL((fm_emb_fwd_multi<unsigned short, I64>), grid, dim3(256), 0, st, s, B);
     else hipLaunchKernelGGL((fm_emb_fwd_multi<float, I64>), grid, dim3(256), 0, st, s, B);

@@ -181,92 +181,129 @@ __global__ void __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) fm_gemm_x3v2_ke
 #pragma unroll
     for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  X3Stage<AK, BM, NTH> sa;
-  X3Stage<BKC, BN, NTH> sb;
+  // staging register sets: SCHED 3 keeps two (loads two steps ahead), the others one
+  X3Stage<AK, BM, NTH> sa, sa1;
+  X3Stage<BKC, BN, NTH> sb, sb1;
   const bool dorow = (!AK) && p.rowsum_a != nullptr && tn == 0;
   float rs = 0.f;
   auto stage = [&](int s) { return smem + s * STG; };
-  auto put = [&](int s) {
+  auto put_from = [&](int s, auto& SA, auto& SB) {
     char* b = stage(s);
-    sa.store(b, b + PA_, b + 2 * PA_, tid);
-    sb.store(b + 3 * PA_, b + 3 * PA_ + PB_, b + 3 * PA_ + 2 * PB_, tid);
+    SA.store(b, b + PA_, b + 2 * PA_, tid);
+    SB.store(b + 3 * PA_, b + 3 * PA_ + PB_, b + 3 * PA_ + 2 * PB_, tid);
     if constexpr (!AK) {
-      if (dorow) sa.rowsum(rs, tid);
+      if (dorow) SA.rowsum(rs, tid);
     }
   };
-  auto get = [&](int kt) {
-    sa.load(A, p.lda, m0, p.M, kt * XK, tid);
-    sb.load(B, p.ldb, n0, p.N, kt * XK, tid);
+  auto get_into = [&](int kt, auto& SA, auto& SB) {
+    SA.load(A, p.lda, m0, p.M, kt * XK, tid);
+    SB.load(B, p.ldb, n0, p.N, kt * XK, tid);
   };
-  if (nst > 0) {
-    get(kt0);
-    put(0);
-    if (nst > 1) get(kt0 + 1);
-  }
   const int q = lane & 15, g = lane >> 4;
   constexpr int TA[6] = {2, 1, 0, 1, 0, 0};    // small terms first, the dominant h*h product last
   constexpr int TB[6] = {0, 1, 2, 0, 1, 0};
-  for (int t = 0; t < nst; ++t) {
-    __syncthreads();                 // stage t&1 complete; stage (t+1)&1 no longer read
-    const char* b = stage(t & 1);
-    const char* la = b;
-    const char* lb = b + 3 * PA_;
-    bf16x8_t bf[3][NR];
+  auto load_b = [&](const char* lb, bf16x8_t (&bf)[3][NR]) {
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
       for (int j = 0; j < NR; ++j)
         bf[pl][j] = *reinterpret_cast<const bf16x8_t*>(lb + pl * PB_ + x3_off(wn * 64 + 16 * j + q, g));
-    if constexpr (SCHED == 1) {
-      // every fragment of the step first, then the staging pass (split + ds_write of step t+1,
-      // loads of step t+2), then the MFMAs: nothing orders the MFMAs behind the staging VALU /
-      // LDS writes, so the scheduler can interleave them
-      bf16x8_t af[MR][3];
+  };
+  // MFMAs of one step, A fragments read per tile row (NR independent accumulator chains per term)
+  auto mfma_rows = [&](const char* la, const bf16x8_t (&bf)[3][NR]) {
 #pragma unroll
-      for (int i = 0; i < MR; ++i)
+    for (int i = 0; i < MR; ++i) {
+      bf16x8_t af[3];
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-          af[i][pl] = *reinterpret_cast<const bf16x8_t*>(la + pl * PA_ + x3_off(wm * 64 + 16 * i + q, g));
-      if (t + 1 < nst) {
-        put((t + 1) & 1);
-        if (t + 2 < nst) get(kt0 + t + 2);
-      }
+      for (int pl = 0; pl < 3; ++pl)
+        af[pl] = *reinterpret_cast<const bf16x8_t*>(la + pl * PA_ + x3_off(wm * 64 + 16 * i + q, g));
 #pragma unroll
-      for (int i = 0; i < MR; ++i)
+      for (int s = 0; s < 6; ++s)
 #pragma unroll
-        for (int s = 0; s < 6; ++s)
-#pragma unroll
-          for (int j = 0; j < NR; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8v_t*>(&bf[TB[s]][j]),
-                                                                *reinterpret_cast<bf16x8v_t*>(&af[i][TA[s]]), acc[i][j],
-                                                                0, 0, 0);
-    } else {
-      // SCHED 2: the two waves sharing a SIMD (w and w + 4) run the step's two phases in opposite
-      // order -- one splits / stores while the other issues MFMAs -- instead of both idling the
-      // MFMA pipe through the staging pass together
-      const bool mfma_first = SCHED == 2 && ((wave >> 2) & 1);
+        for (int j = 0; j < NR; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8v_t*>(&bf[TB[s]][j]),
+                                                              *reinterpret_cast<const bf16x8v_t*>(&af[TA[s]]), acc[i][j],
+                                                              0, 0, 0);
+    }
+  };
+  if constexpr (SCHED == 3) {
+    // de-phased waves (as SCHED 2) with the global loads two steps ahead: step t splits the
+    // registers of step t+1 (set (t+1)&1) into stage (t+1)&1 and reloads that set with step t+3
+    if (nst > 0) {
+      get_into(kt0, sa, sb);
+      put_from(0, sa, sb);
+      if (nst > 1) get_into(kt0 + 1, sa1, sb1);
+      if (nst > 2) get_into(kt0 + 2, sa, sb);
+    }
+    const bool mfma_first = (wave >> 2) & 1;
+    auto body = [&](int t, auto& SA, auto& SB) {
+      __syncthreads();               // stage t&1 complete; stage (t+1)&1 no longer read
+      const char* b = stage(t & 1);
+      bf16x8_t bf[3][NR];
+      load_b(b + 3 * PA_, bf);
       if (!mfma_first && t + 1 < nst) {
-        put((t + 1) & 1);
-        if (t + 2 < nst) get(kt0 + t + 2);
+        put_from((t + 1) & 1, SA, SB);
+        if (t + 3 < nst) get_into(kt0 + t + 3, SA, SB);
       }
-#pragma unroll
-      for (int i = 0; i < MR; ++i) {
-        bf16x8_t af[3];
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-          af[pl] = *reinterpret_cast<const bf16x8_t*>(la + pl * PA_ + x3_off(wm * 64 + 16 * i + q, g));
-        // NR independent accumulator chains per term
-#pragma unroll
-        for (int s = 0; s < 6; ++s)
-#pragma unroll
-          for (int j = 0; j < NR; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8v_t*>(&bf[TB[s]][j]),
-                                                                *reinterpret_cast<bf16x8v_t*>(&af[TA[s]]), acc[i][j],
-                                                                0, 0, 0);
-      }
+      mfma_rows(b, bf);
       if (mfma_first && t + 1 < nst) {
-        put((t + 1) & 1);
-        if (t + 2 < nst) get(kt0 + t + 2);
+        put_from((t + 1) & 1, SA, SB);
+        if (t + 3 < nst) get_into(kt0 + t + 3, SA, SB);
+      }
+    };
+    for (int t = 0; t < nst; t += 2) {
+      body(t, sa1, sb1);             // step t stages step t+1 from set 1
+      if (t + 1 < nst) body(t + 1, sa, sb);
+    }
+  } else {
+    if (nst > 0) {
+      get_into(kt0, sa, sb);
+      put_from(0, sa, sb);
+      if (nst > 1) get_into(kt0 + 1, sa, sb);
+    }
+    for (int t = 0; t < nst; ++t) {
+      __syncthreads();               // stage t&1 complete; stage (t+1)&1 no longer read
+      const char* b = stage(t & 1);
+      const char* la = b;
+      bf16x8_t bf[3][NR];
+      load_b(b + 3 * PA_, bf);
+      if constexpr (SCHED == 1) {
+        // every fragment of the step first, then the staging pass (split + ds_write of step t+1,
+        // loads of step t+2), then the MFMAs: nothing orders the MFMAs behind the staging VALU /
+        // LDS writes, so the scheduler can interleave them
+        bf16x8_t af[MR][3];
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            af[i][pl] = *reinterpret_cast<const bf16x8_t*>(la + pl * PA_ + x3_off(wm * 64 + 16 * i + q, g));
+        if (t + 1 < nst) {
+          put_from((t + 1) & 1, sa, sb);
+          if (t + 2 < nst) get_into(kt0 + t + 2, sa, sb);
+        }
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+#pragma unroll
+          for (int s = 0; s < 6; ++s)
+#pragma unroll
+            for (int j = 0; j < NR; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8v_t*>(&bf[TB[s]][j]),
+                                                                  *reinterpret_cast<bf16x8v_t*>(&af[i][TA[s]]),
+                                                                  acc[i][j], 0, 0, 0);
+      } else {
+        // SCHED 2: the two waves sharing a SIMD (w and w + 4) run the step's two phases in
+        // opposite order -- one splits / stores while the other issues MFMAs -- instead of both
+        // idling the MFMA pipe through the staging pass together
+        const bool mfma_first = SCHED == 2 && ((wave >> 2) & 1);
+        if (!mfma_first && t + 1 < nst) {
+          put_from((t + 1) & 1, sa, sb);
+          if (t + 2 < nst) get_into(kt0 + t + 2, sa, sb);
+        }
+        mfma_rows(la, bf);
+        if (mfma_first && t + 1 < nst) {
+          put_from((t + 1) & 1, sa, sb);
+          if (t + 2 < nst) get_into(kt0 + t + 2, sa, sb);
+        }
       }
     }
   }
@@ -310,13 +347,16 @@ void launch_x3v2_s(const GemmF& p, bool ak, bool bk, hipStream_t s) {
 }
 
 // FM_X3_SCHED (A/B): 1 = all fragment reads of a step ahead of its staging pass; 2 = the two waves
-// of a SIMD run staging and MFMAs in opposite order (8-wave tile only)
+// of a SIMD run staging and MFMAs in opposite order (8-wave tile only); 3 = 2 with the global loads
+// two steps ahead (a second staging register set)
 template <int BM, int BN, bool SGD>
 void launch_x3v2(const GemmF& p, bool ak, bool bk, hipStream_t s) {
-  // default 2 (de-phased waves): 1013 vs 1016 us over the DLRM lab shapes, step 1.225 vs 1.234 ms
-  static const int sched = getenv("FM_X3_SCHED") ? atoi(getenv("FM_X3_SCHED")) : 2;
+  // default 3 (de-phased waves, loads two steps ahead): 972.6 vs 975.6 us (sched 2) over the DLRM
+  // lab shapes, step 1.181 vs 1.186 ms (profiles/bench_ab_x3_sched_embgrid_r5n.txt)
+  static const int sched = getenv("FM_X3_SCHED") ? atoi(getenv("FM_X3_SCHED")) : 3;
   if (sched == 1) launch_x3v2_s<BM, BN, SGD, 1>(p, ak, bk, s);
   else if (sched == 2 && BM == 256) launch_x3v2_s<BM, BN, SGD, 2>(p, ak, bk, s);
+  else if (sched == 3 && BM == 256) launch_x3v2_s<BM, BN, SGD, 3>(p, ak, bk, s);
   else launch_x3v2_s<BM, BN, SGD, 0>(p, ak, bk, s);
 }
 
