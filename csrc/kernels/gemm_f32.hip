@@ -1387,7 +1387,10 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
   else if (ws != nullptr) {
     static const long env_target = getenv("FM_GEMM_F32_SPLIT_BLOCKS") ? std::max(1L, atol(getenv("FM_GEMM_F32_SPLIT_BLOCKS"))) : 0L;
     const long target = env_target > 0 ? env_target : 512L;   // 2 resident blocks per CU
-    while (tiles * ks < target && ks * 2 <= ktiles / 4 && ks < 16) ks *= 2;
+    // up to 16-way, or 64-way for a handful of tiles (the bottom-MLP dW GEMMs: 128 x 256 x 8192
+    // made 64 blocks at 16-way, 30 us)
+    const int ks_max = tiles <= 8 ? 64 : 16;
+    while (tiles * ks < target && ks * 2 <= ktiles / 4 && ks < ks_max) ks *= 2;
   }
   if (fused_ep && !fused_split) ks = 1;   // fused bwd epilogue in the tile: needs the full K sum
   while (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks /= 2;
@@ -1465,11 +1468,14 @@ __global__ void __launch_bounds__(256) fm_skinny_bwd_f32(int ROWS, const float* 
   const f32x4_t wv = *reinterpret_cast<const f32x4_t*>(w + c0);
   if (sub < rpi) {
     const long rend = min(B, r0 + ROWS);
-    for (long r = r0 + sub; r < rend; r += 4L * rpi) {
-      float yv[4], gv[4];
-      f32x4_t xv[4], old[4];
+    // SU rows per iteration with every load issued first: at 64 rows per block a thread walks 16
+    // rows, so 8-deep batches leave two dependent rounds instead of four
+    constexpr int SU = 8;
+    for (long r = r0 + sub; r < rend; r += (long)SU * rpi) {
+      float yv[SU], gv[SU];
+      f32x4_t xv[SU], old[SU];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < SU; ++u) {
         const long rr = min(r + u * rpi, rend - 1);
         yv[u] = y[rr * ldy];
         gv[u] = dy[rr * lddy];
@@ -1477,7 +1483,7 @@ __global__ void __launch_bounds__(256) fm_skinny_bwd_f32(int ROWS, const float* 
         old[u] = (dx && dx_acc) ? *reinterpret_cast<const f32x4_t*>(dx + rr * lddx + c0) : f32x4_t{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < SU; ++u) {
         const long rr = r + u * rpi;
         if (rr >= rend) break;
         const float d = act_bwd(act, yv[u], gv[u]);
