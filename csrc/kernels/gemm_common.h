@@ -147,13 +147,6 @@ FM_DEVICE void tile_coords(const GemmP& p, int bid, int& tm, int& tn) {
 FM_DEVICE f32x4_t slab_sum4(const float* __restrict__ src, long MN, int ks) {
   f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
   int k = 0;
-  for (; k + 16 <= ks; k += 16) {   // deep split-K (tiny-tile dW GEMMs split 32-64 ways)
-    f32x4_t v[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) v[u] = *reinterpret_cast<const f32x4_t*>(src + (long)(k + u) * MN);
-#pragma unroll
-    for (int u = 0; u < 16; ++u) acc += v[u];
-  }
   for (; k + 8 <= ks; k += 8) {
     f32x4_t v[8];
 #pragma unroll
