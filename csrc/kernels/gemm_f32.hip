@@ -1162,7 +1162,6 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
     return -1;
   if (beta) fm_gemm_join(stream);      // C may be a gradient an async reduce is still writing
   GemmF p;
-  p.ablate = 0;
   p.A = A; p.lda = lda; p.sA = sA;
   p.B = B; p.ldb = ldb; p.sB = sB;
   p.C = C; p.ldc = ldc; p.sC = sC;
@@ -1222,8 +1221,6 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
       while (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks /= 2;
       p.ksplit = ks;
       if (ks > 1) fm_gemm_join(stream);
-      static const int x3_ablate = getenv("FM_X3_ABLATE") ? atoi(getenv("FM_X3_ABLATE")) : 0;
-      p.ablate = x3_ablate;
       if (fm_gemm_x3v2_launch(&p, bm, a_kcontig, b_kcontig, upd != nullptr && ks == 1, stream) == 0) {
         if (ks > 1) {
           const int v4 = (N % 4 == 0) && (ldc % 4 == 0) && (sC % 4 == 0) && al(C);

@@ -34,7 +34,6 @@ struct GemmF {
   float uwd, umom;
   int unest;
   int ulds;             // unsplit tiles stage the update through LDS (sgd_epilogue_lds_f32)
-  int ablate;           // gemm_x3.hip timing ablations (FM_X3_ABLATE, tools only: wrong results)
 };
 
 template <int N>

@@ -236,25 +236,17 @@ __global__ void __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) fm_gemm_x3v2_ke
       if (nst > 2) get_into(kt0 + 2, sa, sb);
     }
     const bool mfma_first = (wave >> 2) & 1;
-    // p.ablate (timing experiments only, results are wrong): 1 = no staging in the loop (MFMAs on
-    // the prologue's stage), 2 = no MFMAs (staging and fragment reads only)
-    const bool do_stage = p.ablate != 1, do_mfma = p.ablate != 2;
     auto body = [&](int t, auto& SA, auto& SB) {
       __syncthreads();               // stage t&1 complete; stage (t+1)&1 no longer read
       const char* b = stage(t & 1);
       bf16x8_t bf[3][NR];
       load_b(b + 3 * PA_, bf);
-      if (!mfma_first && t + 1 < nst && do_stage) {
+      if (!mfma_first && t + 1 < nst) {
         put_from((t + 1) & 1, SA, SB);
         if (t + 3 < nst) get_into(kt0 + t + 3, SA, SB);
       }
-      if (do_mfma) {
-        mfma_rows(b, bf);
-      } else {
-#pragma unroll
-        for (int j = 0; j < NR; ++j) asm volatile("" ::"v"(bf[0][j]), "v"(bf[1][j]), "v"(bf[2][j]));
-      }
-      if (mfma_first && t + 1 < nst && do_stage) {
+      mfma_rows(b, bf);
+      if (mfma_first && t + 1 < nst) {
         put_from((t + 1) & 1, SA, SB);
         if (t + 3 < nst) get_into(kt0 + t + 3, SA, SB);
       }
