@@ -28,6 +28,7 @@ int fm_gemm(const void* A, long lda, long sA, int a_kcontig, const void* B, long
             float* colsum, float* rowsum_a, hipStream_t stream);
 void fm_gemm_f32_set_split(int on);
 void fm_embedding_set_bwd_mode(int count);
+void fm_embedding_set_rowblock(int on);
 int fm_gemm_f32_get_split();
 int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, const float* B, long ldb, long sB, int b_kcontig,
                 float* C, long ldc, long sC, const float* bias, int M, int N, int K, int batch, float alpha, int beta,
@@ -1244,6 +1245,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_f32_get_split", []() { return fm_gemm_f32_get_split(); });
   // sparse-SGD kernels of tables with slot buffers: 1 = count / update, 0 = claim / dup / owner
   m.def("embedding_set_bwd_mode", [](bool count) { fm_embedding_set_bwd_mode(count ? 1 : 0); });
+  m.def("embedding_set_rowblock", [](bool on) { fm_embedding_set_rowblock(on ? 1 : 0); });
   m.def("conv_nhwc_dgrad_strided", &conv_nhwc_dgrad_strided);
   m.def("conv_nhwc_wgrad", &conv_nhwc_wgrad);
   m.def("conv_s2d", &conv_s2d);

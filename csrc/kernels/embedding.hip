@@ -543,18 +543,25 @@ void launch_count(const ClaimSet& s, int m, bool dy_bf16, const float* lr, long 
   else hipLaunchKernelGGL((fm_emb_update_multi<float, I64>), gu, dim3(256), 0, st, s, lr, B);
 }
 
+// FM_EMB_BWD_BLOCKS: cap on the blocks per table of the grid-stride backward kernels (claim / dup /
+// owner / atomic; 0 = uncapped).  They run beside the bottom-MLP backward GEMMs on a second stream.
+long emb_bwd_cap(long want) {
+  static const long cap = getenv("FM_EMB_BWD_BLOCKS") ? std::max(0L, atol(getenv("FM_EMB_BWD_BLOCKS"))) : 0L;
+  return cap > 0 ? std::min(want, cap) : want;
+}
+
 template <bool I64>
 void launch_claim(const ClaimSet& s, int m, bool dy_bf16, const float* lr, long B, int maxbag, int minD4,
                   hipStream_t st) {
   const long n = B * maxbag;
-  dim3 gc((unsigned)std::max<long>(1, std::min<long>((n + 255) / 256, 1024)), m);
+  dim3 gc((unsigned)std::max<long>(1, emb_bwd_cap(std::min<long>((n + 255) / 256, 1024))), m);
   hipLaunchKernelGGL((fm_emb_claim_multi<I64>), gc, dim3(256), 0, st, s, B);
   // (a 64-block grid measured 18.4 vs 9.5 us/step: 12k..40k-row tables still see thousands of dups)
-  dim3 gd((unsigned)std::max<long>(1, std::min<long>((n + 3) / 4, 1024)), m);
+  dim3 gd((unsigned)std::max<long>(1, emb_bwd_cap(std::min<long>((n + 3) / 4, 1024))), m);
   if (dy_bf16) hipLaunchKernelGGL((fm_emb_dup_multi<unsigned short, I64>), gd, dim3(256), 0, st, s, lr);
   else hipLaunchKernelGGL((fm_emb_dup_multi<float, I64>), gd, dim3(256), 0, st, s, lr);
   const int rpi = 256 / std::min(64, std::max(1, minD4));
-  dim3 go((unsigned)std::max<long>(1, std::min<long>((n + rpi - 1) / rpi, 2048)), m);
+  dim3 go((unsigned)std::max<long>(1, emb_bwd_cap(std::min<long>((n + rpi - 1) / rpi, 2048))), m);
   if (dy_bf16) hipLaunchKernelGGL((fm_emb_owner_multi<unsigned short, I64>), go, dim3(256), 0, st, s, lr, B);
   else hipLaunchKernelGGL((fm_emb_owner_multi<float, I64>), go, dim3(256), 0, st, s, lr, B);
 }
@@ -574,9 +581,179 @@ void launch_bwd(const TabSet& s, int m, bool tiny, bool dy_bf16, const float* lr
     else hipLaunchKernelGGL((fm_emb_bwd_tiny_multi<float, I64>), grid, dim3(256), lds, st, s, lr, B, chunk);
   } else {
     const int rpi = std::max(1, 256 / std::min(256, maxD));
-    dim3 grid((unsigned)std::max<long>(1, std::min<long>((B + rpi - 1) / rpi, 2048)), m);
+    dim3 grid((unsigned)std::max<long>(1, emb_bwd_cap(std::min<long>((B + rpi - 1) / rpi, 2048))), m);
     if (dy_bf16) hipLaunchKernelGGL((fm_emb_bwd_atomic_multi<unsigned short, I64>), grid, dim3(256), 0, st, s, lr, B);
     else hipLaunchKernelGGL((fm_emb_bwd_atomic_multi<float, I64>), grid, dim3(256), 0, st, s, lr, B);
+  }
+}
+
+// ---- row-block ownership (tables of up to ~64 LDS blocks of rows: 3 .. 8192 rows x 128) --------
+// Every block OWNS a range of RR table rows (RR*D*4 <= 64 KiB) and one chunk of the lookups: it
+// scans the chunk's indices (L2-resident, read by every row block of the table), compacts the
+// lookups that hit its rows into an LDS list (wave ballot), adds their gradient rows into an LDS
+// copy of its rows (each wave owns a quarter of the rows: lane = column, plain read-add-write in
+// list order, 8 lookups' loads in flight) and applies the result once.  With one chunk the block is the rows' only
+// writer and the apply is a plain read-modify-write; tables with so few rows that one block would
+// serialise thousands of lookups (3 .. 155 rows) split the lookups over up to 32 chunks and flush
+// with one float atomic per (row, col, chunk).  Replaces both the per-lookup global atomics (which
+// pile onto the same addresses for 36 .. 8192-row tables and run at the L2 atomic rate) and the
+// tiny-table kernel: no global atomics at all for the mid-size tables.
+struct RbDesc {
+  float* W;
+  const void* idx;
+  const void* dy;
+  long ld;
+  long lo;
+  int rows, D, bag;
+  float scale;
+  int rr;       // rows per block
+  int chunks;   // lookup chunks per row block
+  int first;    // first blockIdx.x of this table
+};
+struct RbSet {
+  RbDesc t[MAXT];
+  int n;
+};
+constexpr int RB_LDS = 64 << 10;
+constexpr int RB_SCAN = 2048;   // lookups scanned per round (8 per thread, loads issued together)
+
+template <typename GT, bool I64, int NQ>
+__global__ void __launch_bounds__(256) fm_emb_bwd_rowblock(RbSet s, const float* __restrict__ lr, long B) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int le[RB_SCAN];
+  __shared__ short lrow[RB_SCAN];
+  __shared__ int nlist;
+  int ti = 0;
+  for (int i = 1; i < s.n; ++i)
+    if ((int)blockIdx.x >= s.t[i].first) ti = i;
+  const RbDesc& d = s.t[ti];
+  const int local = (int)blockIdx.x - d.first;
+  const int rbi = local / d.chunks, ci = local - rbi * d.chunks;
+  const long r0 = (long)rbi * d.rr;
+  const int nr = (int)min((long)d.rr, (long)d.rows - r0);
+  if (nr <= 0) return;                                   // block-uniform
+  const int D = d.D, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  float* acc = reinterpret_cast<float*>(smem);           // [nr][D]
+  for (int i = tid; i < nr * D; i += 256) acc[i] = 0.f;
+  const long n = B * d.bag;
+  const long per = (n + d.chunks - 1) / d.chunks;
+  const long e0 = (long)ci * per, e1 = min(n, e0 + per);
+  const GT* dy = reinterpret_cast<const GT*>(d.dy);
+  constexpr int PT = RB_SCAN / 256;
+  constexpr int U = 8;
+  for (long base = e0; base < e1; base += RB_SCAN) {
+    if (tid == 0) nlist = 0;
+    __syncthreads();
+    long rv[PT];
+#pragma unroll
+    for (int u = 0; u < PT; ++u) rv[u] = ldi<I64>(d.idx, min(base + u * 256 + tid, e1 - 1));   // clamped
+#pragma unroll
+    for (int u = 0; u < PT; ++u) {
+      const long e = base + u * 256 + tid;
+      const long l = rv[u] - d.lo - r0;
+      const bool m = e < e1 && (unsigned long)l < (unsigned long)nr;
+      const unsigned long long mask = __ballot(m);
+      int wb = 0;
+      if (lane == 0 && mask) wb = atomicAdd(&nlist, __popcll(mask));
+      wb = __shfl(wb, 0);
+      if (m) {
+        const int pos = wb + __popcll(mask & ((1ull << lane) - 1ull));
+        le[pos] = (int)e;
+        lrow[pos] = (short)l;
+      }
+    }
+    __syncthreads();
+    const int nm = nlist;
+    // wave w owns the block's rows with lrow % 4 == w and applies its lookups with plain LDS
+    // read-add-writes in list order (no LDS float atomics: ds_add_f32 ran ~5x slower than the
+    // global-atomic kernel it replaced, gpurun_out r5t); U lookups' gradient loads in flight
+    for (int j0 = 0; j0 < nm; j0 += 64) {
+      const int jr = min(j0 + lane, nm - 1);
+      const int lrj = lrow[jr], lej = le[jr];
+      unsigned long long mine = __ballot(j0 + lane < nm && (lrj & 3) == wave);
+      while (mine) {                                     // wave-uniform
+        int rw[U];
+        float g[U][NQ];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int sl = mine ? __builtin_ctzll(mine) : 0;
+          rw[u] = mine ? __builtin_amdgcn_readlane(lrj, sl) : -1;
+          mine &= mine - 1;                              // 0 stays 0
+          const int e = __builtin_amdgcn_readlane(lej, sl);
+          const long b = d.bag == 1 ? (long)e : (long)(e / d.bag);
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) g[u][q] = ld<GT>(dy + b * d.ld + min(lane + 64 * q, D - 1));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (rw[u] < 0) break;                          // wave-uniform
+          float* a = acc + rw[u] * D;
+#pragma unroll
+          for (int q = 0; q < NQ; ++q)
+            if (lane + 64 * q < D) a[lane + 64 * q] += g[u][q];
+        }
+      }
+    }
+    __syncthreads();                                     // the list is rebuilt next round
+  }
+  const float mul = (lr ? -lr[0] : 1.f) * d.scale;
+  float* W = d.W + r0 * D;
+  if (d.chunks == 1) {                                   // sole writer of these rows
+    for (int i = tid; i < nr * D; i += 256) {
+      const float v = acc[i];
+      if (v != 0.f) W[i] += v * mul;
+    }
+  } else {
+    for (int i = tid; i < nr * D; i += 256) {
+      const float v = acc[i];
+      if (v != 0.f) atomicAdd(W + i, v * mul);
+    }
+  }
+}
+
+// rows per block and lookup chunks of a table on the row-block path (false: not eligible)
+bool rowblock_shape(int rows, int D, long n, int& rr, int& chunks) {
+  if (D <= 0 || D > 256 || rows <= 0 || n <= 0) return false;
+  rr = std::min(rows, std::min(RB_LDS / (D * 4), 32767));
+  const long rbn = (rows + rr - 1) / rr;
+  if (rbn > 64) return false;                            // every row block rescans all lookups
+  // ~256 lookups per block; a split chunk costs one flush atomic per (row, col)
+  chunks = (int)std::max(1L, std::min(32L, n / (rbn * 256)));
+  if (chunks > 1 && (long)chunks * rows * 4 > n) chunks = std::max(1L, n / (4L * rows));
+  return true;
+}
+
+template <bool I64>
+void launch_rowblock(RbSet& s, int m, bool dy_bf16, const float* lr, long B, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)fm_emb_bwd_rowblock<unsigned short, I64, 2>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, RB_LDS);
+    (void)hipFuncSetAttribute((const void*)fm_emb_bwd_rowblock<float, I64, 2>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, RB_LDS);
+    (void)hipFuncSetAttribute((const void*)fm_emb_bwd_rowblock<unsigned short, I64, 4>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, RB_LDS);
+    (void)hipFuncSetAttribute((const void*)fm_emb_bwd_rowblock<float, I64, 4>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, RB_LDS);
+    attr = true;
+  }
+  int blocks = 0, maxD = 1;
+  size_t lds = 0;
+  for (int i = 0; i < m; ++i) {
+    s.t[i].first = blocks;
+    blocks += (s.t[i].rows + s.t[i].rr - 1) / s.t[i].rr * s.t[i].chunks;
+    lds = std::max(lds, (size_t)std::min(s.t[i].rr, s.t[i].rows) * s.t[i].D * 4);
+    maxD = std::max(maxD, s.t[i].D);
+  }
+  s.n = m;
+  if (blocks <= 0) return;
+  const dim3 grid(blocks);
+  if (maxD <= 128) {
+    if (dy_bf16) hipLaunchKernelGGL((fm_emb_bwd_rowblock<unsigned short, I64, 2>), grid, dim3(256), lds, st, s, lr, B);
+    else hipLaunchKernelGGL((fm_emb_bwd_rowblock<float, I64, 2>), grid, dim3(256), lds, st, s, lr, B);
+  } else {
+    if (dy_bf16) hipLaunchKernelGGL((fm_emb_bwd_rowblock<unsigned short, I64, 4>), grid, dim3(256), lds, st, s, lr, B);
+    else hipLaunchKernelGGL((fm_emb_bwd_rowblock<float, I64, 4>), grid, dim3(256), lds, st, s, lr, B);
   }
 }
 
@@ -730,6 +907,8 @@ extern "C" void fm_embedding_fwd_multi(int n, const float* const* W, const void*
 
 static int g_emb_count = -1;   // -1: from FM_EMB_BWD at the first call
 extern "C" void fm_embedding_set_bwd_mode(int count) { g_emb_count = count ? 1 : 0; }
+static int g_emb_rowblock = -1;  // -1: from FM_EMB_ROWBLOCK at the first call
+extern "C" void fm_embedding_set_rowblock(int on) { g_emb_rowblock = on ? 1 : 0; }
 
 // lr != nullptr: fused sparse SGD into W; lr == nullptr: W is a dense grad buffer (accumulate).
 extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const* idx, const int* idx64,
@@ -776,6 +955,37 @@ extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const
   // tables against 16.6 us of regular atomics (profiles/README.md): with 1 block/CU of LDS and ~13
   // blocks per table the serial LDS atomics are latency-bound, and more blocks multiply the flush
   static const bool small_on = getenv("FM_EMB_SMALL") != nullptr && atoi(getenv("FM_EMB_SMALL")) == 1;
+  // row-block ownership for the other tables small enough: OPT-IN (FM_EMB_ROWBLOCK=1).  Measured
+  // slower than the atomic / tiny kernels on the MLPerf set at B = 8192 (tools/bench_emb_bwd.py,
+  // profiles/emb_bwd_rowblock_r5u.jsonl: 76 vs 48 us for the 13 tables of <= 8192 rows; a 976-row
+  // table alone 47 vs 6 us): ~16 blocks per table leave each wave a serial chain of gradient-row
+  // loads and LDS read-add-writes, where the atomic kernel spreads 1 M fire-and-forget atomics over
+  // 2048 blocks.  (Its first form, LDS float atomics, ran 199 us: ds_add_f32 is slow.)
+  if (g_emb_rowblock < 0) g_emb_rowblock = getenv("FM_EMB_ROWBLOCK") != nullptr && atoi(getenv("FM_EMB_ROWBLOCK")) == 1;
+  const bool rb_on = g_emb_rowblock == 1;
+  std::vector<char> on_rb(n, 0);
+  if (rb_on) {
+    for (int wide = 0; wide < 2; ++wide) {
+      RbSet s;
+      int m = 0;
+      for (int k = 0; k < n; ++k) {
+        if (claimable(k) || (idx64[k] != 0) != (wide != 0)) continue;
+        int rr = 0, chunks = 0;
+        if (!rowblock_shape(rows[k], D[k], B * (long)bag[k], rr, chunks)) continue;
+        on_rb[k] = 1;
+        s.t[m++] = RbDesc{W[k], idx[k], dy[k], ldg[k], lo ? lo[k] : 0, rows[k], D[k], bag[k], scale[k], rr, chunks, 0};
+        if (m == MAXT) {
+          if (wide) launch_rowblock<true>(s, m, dy_bf16, lr, B, st);
+          else launch_rowblock<false>(s, m, dy_bf16, lr, B, st);
+          m = 0;
+        }
+      }
+      if (m > 0) {
+        if (wide) launch_rowblock<true>(s, m, dy_bf16, lr, B, st);
+        else launch_rowblock<false>(s, m, dy_bf16, lr, B, st);
+      }
+    }
+  }
   auto kind_of = [&](int k) {
     if (rows[k] <= TINY_ROWS && D[k] <= 256 && B * (long)bag[k] >= 16L * rows[k]) return 0;
     if (small_on && (long)rows[k] * D[k] * 4 <= SMALL_LDS && D[k] <= 256 && B * (long)bag[k] >= 8L * rows[k]) return 1;
@@ -786,7 +996,7 @@ extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const
     const bool tiny = kind == 0, wide = pass & 1;
     std::vector<int> sel;
     for (int k = 0; k < n; ++k) {
-      if (claimable(k)) continue;
+      if (claimable(k) || on_rb[k]) continue;
       if (kind_of(k) == kind && (idx64[k] != 0) == wide) sel.push_back(k);
     }
     for (size_t base = 0; base < sel.size(); base += MAXT) {

@@ -515,6 +515,55 @@ def test_embedding_count_update_sgd(gpu, idx_dtype, dy_dtype):
         Kk.C().embedding_set_bwd_mode(False)
 
 
+@pytest.mark.parametrize("rowblock", [False, True])
+@pytest.mark.parametrize("dy_dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("idx_dtype", [torch.int64, torch.int32])
+def test_embedding_rowblock_tables(gpu, idx_dtype, dy_dtype, rowblock):
+    """The MLPerf set's non-claimed table sizes (3 .. 7420 rows at B = 8192) through the default
+    atomic / tiny kernels and through the opt-in row-block ownership kernel (embedding.hip
+    fm_emb_bwd_rowblock: one-chunk plain apply, multi-chunk atomic flush), plus D = 256 / 200 / 24
+    columns, a bag of 3 and a row shard, over two steps, for the fused sparse SGD and the dense
+    gradient, against a float64 oracle."""
+    from flexmi.ops import _kernels as Kk
+    Kk.C().embedding_set_rowblock(rowblock)
+    try:
+        _embedding_small_tables_case(gpu, idx_dtype, dy_dtype)
+    finally:
+        Kk.C().embedding_set_rowblock(False)
+
+
+def _embedding_small_tables_case(gpu, idx_dtype, dy_dtype):
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(12)
+    B = 8192
+    specs = [(7420, 1, 128, 0), (976, 1, 128, 0), (155, 1, 128, 0), (36, 1, 128, 0), (3, 1, 128, 0),
+             (300, 3, 256, 0), (90, 1, 200, 0), (500, 2, 24, 0), (1000, 1, 128, 400)]   # rows, bag, D, lo
+    tables, idxs, refs = [], [], []
+    for rows, bag, D, lo in specs:
+        W = torch.randn(rows, D, device=gpu)
+        tables.append(W)
+        refs.append(W.double())
+        idxs.append(torch.randint(0, rows + lo, (B, bag), device=gpu, dtype=idx_dtype))
+    lr = torch.tensor([0.05], device=gpu)
+    none = [None] * (3 * len(specs))
+    for step in range(2):
+        dys = [torch.randn(B, D, device=gpu).to(dy_dtype) for _, _, D, _ in specs]
+        Kk.C().embedding_bwd_multi(tables, idxs, dys, [d.stride(0) for d in dys], [1.0] * len(specs), lr, none,
+                                   [s[3] for s in specs])
+        grads = [torch.zeros_like(W) for W in tables]
+        Kk.C().embedding_bwd_multi(grads, idxs, dys, [d.stride(0) for d in dys], [0.5] * len(specs), None, None,
+                                   [s[3] for s in specs])
+        torch.cuda.synchronize()
+        for k, (rows, bag, D, lo) in enumerate(specs):
+            flat = idxs[k].reshape(-1).long() - lo
+            keep = (flat >= 0) & (flat < rows)
+            upd = torch.zeros(rows, D, device=gpu, dtype=torch.float64)
+            upd.index_add_(0, flat[keep], dys[k].double().repeat_interleave(bag, 0)[keep])
+            refs[k] -= 0.05 * upd
+            assert torch.allclose(tables[k].double(), refs[k], atol=2e-4), (step, specs[k], "sgd")
+            assert torch.allclose(grads[k].double(), 0.5 * upd, atol=2e-3, rtol=1e-5), (step, specs[k], "dense")
+
+
 @pytest.mark.parametrize("idx_dtype", [torch.int64, torch.int32])
 def test_embedding_row_shards(gpu, idx_dtype):
     """Row-sharded tables (a shard holds rows [lo, lo+rows)): forward sums only the lookups the
