@@ -423,6 +423,7 @@ void launch_bm(const GemmP& p, bool ak, bool bk, bool vec, hipStream_t s) {
 
 extern "C" void fm_gemm_glds_launch(const void* params, int bm, int bn, int a_kcontig, int b_kcontig, int prio,
                                     int wide, hipStream_t stream);
+extern "C" int fm_gemm_x1_launch(const void* params, int bm, int a_kcontig, int b_kcontig, int sgd, hipStream_t s);
 
 // dispatch experiments (tools/gemm_probe.py): 1 = never glds, 2 = glds for every orientation and
 // grid size (K % 64 == 0), 4 = glds 128x128 tiles, 8 = s_setprio around the glds MFMA blocks,
@@ -545,6 +546,40 @@ static int gemm_run(const void* A, long lda, long sA, int a_kcontig,
   auto al = [](const void* q) { return (((uintptr_t)q) & 15) == 0; };
   bool vec = al(A) && al(B) && (lda % 8 == 0) && (ldb % 8 == 0) && (sA % 8 == 0) && (sB % 8 == 0);
   vec = vec && (a_kcontig ? (K % 8 == 0) : (M % 8 == 0)) && (b_kcontig ? (K % 8 == 0) : (N % 8 == 0));
+  // big-tile kernel (gemm_x1.hip: 256x128 tiles of 8 64x64 waves, loads two steps ahead) for grids
+  // that fill the chip, K split to get there; FM_GEMM_X1=0 or variant bit 1024 disables, bit 512
+  // forces it wherever it applies; FM_GEMM_X1_MIN = blocks (tiles x splits) it needs (default 192)
+  {
+    static const int x1_env = getenv("FM_GEMM_X1") ? atoi(getenv("FM_GEMM_X1")) : 1;
+    static const long x1_min = getenv("FM_GEMM_X1_MIN") ? atol(getenv("FM_GEMM_X1_MIN")) : 192L;
+    const bool force = (g_gemm_variant & 512) != 0;
+    const bool off = x1_env == 0 || (g_gemm_variant & 1024) != 0;
+    if (!off && vec && !atomic_ok && K > 0 && K % 32 == 0 && M >= 64 && N >= 64) {
+      const int bm = M >= 256 ? 256 : 128;
+      GemmP q = p;
+      q.tiles_m = (M + bm - 1) / bm;
+      q.tiles_n = (N + 127) / 128;
+      const long tiles = (long)q.tiles_m * q.tiles_n * batch;
+      const int ktiles = K / 32;
+      int ks = 1;
+      if (ksplit_req > 0) ks = ksplit_req;
+      else if (ws != nullptr) {
+        while (tiles * ks < 256 && ks * 2 <= ktiles / 4 && ks < 16) ks *= 2;
+      }
+      if (act_y != nullptr || colsum != nullptr) ks = 1;       // fused epilogue needs the full sum
+      while (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks /= 2;
+      if (ks <= ktiles && (force || tiles * ks >= x1_min)) {
+        q.ksplit = ks;
+        q.atomic_c = 0;
+        q.tile_cnt = nullptr;
+        if (ks > 1) fm_gemm_join(stream);  // the slab workspace is shared
+        if (fm_gemm_x1_launch(&q, bm, a_kcontig, b_kcontig, upd != nullptr && ks == 1, stream) == 0) {
+          if (ks > 1) launch_splitk_reduce(q, stream);
+          return ks;
+        }
+      }
+    }
+  }
   // LDS-DMA pipelined kernel (gemm_glds.hip) whenever K-tiles are whole
   static const bool no_glds_env = getenv("FM_GEMM_NO_GLDS") != nullptr;
   const bool no_glds = no_glds_env || (g_gemm_variant & 1);

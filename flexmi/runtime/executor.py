@@ -205,11 +205,19 @@ def Embedding_row_lo(ctx):
     return int(b[0][0]) if b is not None else 0
 
 
-def _run_overlapped(items, s, side):
+# items after the embedding-group backward that touch nothing it writes when every group table is
+# trained by fused sparse SGD (no dense table gradient): the dense optimizer step and the split-K
+# stream join run on the main stream without waiting for the side stream, which is joined at the
+# segment end instead (FM_EMB_LATE_JOIN=0: join before them, as for dense-gradient tables)
+LATE_JOIN_OK = ("update", "gemm.join", "fused_sgd.disarm")
+
+
+def _run_overlapped(items, s, side, late_join=False):
     """Issue one graph segment's items with the embedding groups on ``side`` (fork/join by events,
     which stream capture records as graph edges).  A group forward is hoisted only across plain
     op forwards that declare what they write (``Item.writes``) and write none of the group's
-    inputs (``Item.reads``): never across reshards, exchange unpacks or another group."""
+    inputs (``Item.reads``): never across reshards, exchange unpacks or another group.
+    ``late_join``: the items named in LATE_JOIN_OK do not wait for a pending group backward."""
     fwd = [k for k, it in enumerate(items) if it.name.endswith(".group_fwd")]
     hoist, fork_at = set(), {}
     for k in fwd:
@@ -241,7 +249,8 @@ def _run_overlapped(items, s, side):
                 it.fn()
             bwd_pending = True
             continue
-        if bwd_pending and not it.name.endswith((".bwd", ".bwd_dw", ".bwd_dx")):
+        if bwd_pending and not it.name.endswith((".bwd", ".bwd_dw", ".bwd_dx")) and not (
+                late_join and it.name in LATE_JOIN_OK):
             s.wait_stream(side)
             bwd_pending = False
         it.fn()
@@ -2434,6 +2443,13 @@ class Executor:
             return self.prog_fwd + self.prog_bwd_fused + self.prog_upd_fused
         return self.prog_fwd + self.prog_bwd + self.prog_upd
 
+    def _groups_sparse_only(self):
+        """Every fused embedding group's tables are trained by fused sparse SGD on this rank (no
+        dense gradient, no sparse-DP collectives): their backward writes only the tables."""
+        ops = {id(op): op for grp in self.group_of.values() for op in grp}.values()
+        return bool(ops) and all(getattr(op, "sparse_sgd", False) and not getattr(op, "sparse_dp", None)
+                                 and not getattr(op, "host_exec", False) for op in ops)
+
     def capture_step(self, pre=None):
         """The training step as a replayable hipGraph program (see ``_capture_step``).  The
         per-step gradient memset is left out of the graph: the update kernels consume the
@@ -2477,6 +2493,7 @@ class Executor:
         s.wait_stream(torch.cuda.current_stream())
         ov = overlap_embeddings_enabled(self)
         side = torch.cuda.Stream() if ov else None
+        late = ov and os.environ.get("FM_EMB_LATE_JOIN", "1") != "0" and self._groups_sparse_only()
         runs = []
         graphs = []
         # thread_local capture: the RCCL process group's watchdog thread queries events while
@@ -2487,7 +2504,7 @@ class Executor:
                 with torch.cuda.stream(s):
                     with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                         if ov:
-                            _run_overlapped(x, s, side)
+                            _run_overlapped(x, s, side, late)
                         else:
                             for it in x:
                                 it.fn()

@@ -434,13 +434,17 @@ def test_embedding_overlap_on_off_equivalent(gpu, monkeypatch):
     dcfg = DLRMConfig(128, [5000, 300, 12, 70000, 40], [13, 256, 128], [256, 256, 1], 1, -1, -1, 0.0, "dot", "", -1,
                       "bce", "overlap")
     res = {}
-    for mode in ("0", "1"):
-        monkeypatch.setattr(E, "OVERLAP_EMB", mode)
+    for mode in ("0", "1", "1-early-join"):
+        monkeypatch.setattr(E, "OVERLAP_EMB", mode[0])
+        # late join (default): the dense update does not wait for the sparse-SGD table backward
+        monkeypatch.setenv("FM_EMB_LATE_JOIN", "0" if mode == "1-early-join" else "1")
         ws, loss, ex = _dlrm_run("gpu", dcfg, 2048, 4, graph=True)
-        assert E.overlap_embeddings_enabled(ex) == (mode == "1")
+        assert E.overlap_embeddings_enabled(ex) == (mode[0] == "1")
+        assert ex._groups_sparse_only()
         res[mode] = (ws, loss)
-    _assert_params_close(res["0"][0], res["1"][0], 1e-5)
-    assert abs(res["0"][1] - res["1"][1]) < 1e-5
+    for mode in ("1", "1-early-join"):
+        _assert_params_close(res["0"][0], res[mode][0], 1e-5)
+        assert abs(res["0"][1] - res[mode][1]) < 1e-5
 
 
 # ---------------------------------------------------------------- CNN kernels (fp32)

@@ -627,3 +627,70 @@ def test_embedding_fwd_long_bag_split(gpu, B, bag, D, out_dt):
         ref = (W.double()[r.clamp(0, rows - 1)] * ok[..., None]).sum(1) * sc
         tol = 1e-5 if out_dt == torch.float32 else 1e-2
         assert rel_err(o, ref) < tol, (B, bag, D)
+
+
+@pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K,ks", [(1024, 512, 256, 1), (300, 200, 96, 1), (8192, 256, 512, 0), (256, 1024, 4096, 4),
+                                      (77, 130, 64, 1)])
+def test_gemm_x1_bigtile(gpu, a_k, b_k, M, N, K, ks):
+    """Big-tile bf16 kernel (gemm_x1.hip, forced with variant bit 512): every operand orientation,
+    ragged edges (clamped rows never stored), split K; bias + relu + beta into bf16 C and the fused
+    backward epilogue of the layer below (act'(y) * v, column sums) vs an fp32 reference."""
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(11)
+    A = torch.randn(M, K, device=gpu)
+    B = torch.randn(K, N, device=gpu)
+    Ab = bf(A) if a_k else bf(A.t().contiguous())
+    Bb = bf(B.t().contiguous()) if b_k else bf(B)
+    lda, ldb = (K if a_k else M), (K if b_k else N)
+    ref = bf(A).float() @ bf(B).float()
+    Kk.C().gemm_set_variant(512)
+    try:
+        C = torch.empty(M, N, device=gpu)
+        Kk.gemm(Ab, lda, a_k, Bb, ldb, b_k, C, N, M, N, K, ksplit=ks)
+        assert rel_err(C, ref) < 2e-3, "plain"
+        bias = torch.randn(N, device=gpu)
+        Cb = torch.randn(M, N, device=gpu).to(torch.bfloat16)
+        C0 = Cb.float().clone()
+        Kk.gemm(Ab, lda, a_k, Bb, ldb, b_k, Cb, N, M, N, K, bias=bias, act=11, beta=True, ksplit=ks)
+        assert rel_err(Cb, torch.relu(ref + bias) + C0) < 1e-2, "bias/relu/beta"
+        y = torch.relu(torch.randn(M, N, device=gpu)).to(torch.bfloat16)
+        cs = torch.zeros(N, device=gpu)
+        Cd = torch.empty(M, N, device=gpu)
+        Kk.gemm(Ab, lda, a_k, Bb, ldb, b_k, Cd, N, M, N, K, act_y=y, bwd_act=11, colsum=cs)
+        d = ref * (y.float() > 0)
+        assert rel_err(Cd, d) < 2e-3, "fused act-bwd"
+        assert rel_err(cs, d.sum(0)) < 2e-3, "colsum"
+    finally:
+        Kk.C().gemm_set_variant(0)
+
+
+@pytest.mark.parametrize("M,N,K", [(1024, 512, 8192), (256, 480, 8192), (130, 200, 1024)])
+def test_gemm_x1_dw_fused_sgd(gpu, M, N, K):
+    """dW GEMM (both operands MN-contiguous) on the big-tile kernel with the bias-gradient row sums
+    and the SGD update fused (unsplit: in the epilogue; split: in the reduce)."""
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(12)
+    dpre = bf(torch.randn(K, M, device=gpu))           # [K][M]
+    x = bf(torch.randn(K, N, device=gpu))              # [K][N]
+    g = dpre.float().t() @ x.float()
+    Kk.C().gemm_set_variant(512)
+    try:
+        dw = torch.empty(M, N, device=gpu)
+        rs = torch.zeros(M, device=gpu)
+        Kk.gemm(dpre, M, False, x, N, False, dw, N, M, N, K, rowsum_a=rs)
+        assert rel_err(dw, g) < 2e-3
+        assert rel_err(rs, dpre.float().sum(0)) < 1e-3
+        W = torch.randn(M, N, device=gpu)
+        W0 = W.clone()
+        Wc = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+        lr = torch.tensor([0.01], device=gpu)
+        db = torch.zeros(M, device=gpu)
+        upd = Kk.FusedSGD(W, Wc, None, lr, 0.0, 0.0, False)
+        assert Kk._dw_fused_sgd(dpre, x, None, db, upd)
+        Wn = W0 - 0.01 * g
+        assert rel_err(W, Wn) < 1e-4
+        assert rel_err(Wc, Wn) < 1e-2
+        assert rel_err(db, dpre.float().sum(0)) < 1e-3
+    finally:
+        Kk.C().gemm_set_variant(0)

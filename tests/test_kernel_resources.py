@@ -1,8 +1,9 @@
-"""Register-allocation guard for the hot fp32 GEMM kernel: the split-bf16 kernel
+"""Register-allocation guard for the hot GEMM kernels: the split-bf16 fp32 kernel
 (csrc/kernels/gemm_x3.hip) runs at one block of 8 waves per CU with ~220-240 VGPRs, so any change
 that pushes it over 256 spills to scratch and silently costs 2-3x (a timing knob with runtime
-branches did exactly that: 221 spilled VGPRs, 8192x1024x1024 dW 99 -> 262 us).  Compiles the file
-for gfx950 (no GPU needed) and checks hipcc's resource report for every instantiation."""
+branches did exactly that: 221 spilled VGPRs, 8192x1024x1024 dW 99 -> 262 us); the big-tile bf16
+kernel (gemm_x1.hip) sits at 128-170.  Compiles both files for gfx950 concurrently (no GPU needed)
+and checks hipcc's resource report for every instantiation."""
 import os
 import re
 import shutil
@@ -15,14 +16,22 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
-def test_split_gemm_kernels_do_not_spill(tmp_path):
-    src = os.path.join(ROOT, "csrc", "kernels", "gemm_x3.hip")
-    out = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-c", src, "-o", str(tmp_path / "x3.o"),
-                          "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True, timeout=900)
-    assert out.returncode == 0, out.stderr[-2000:]
-    names = re.findall(r"Function Name: (\S+)", out.stderr)
-    spills = [int(v) for v in re.findall(r"VGPRs Spill: (\d+)", out.stderr)]
-    scratch = [int(v) for v in re.findall(r"ScratchSize \[bytes/lane\]: (\d+)", out.stderr)]
-    assert names and len(spills) == len(names) == len(scratch)
-    bad = [(n, s, c) for n, s, c in zip(names, spills, scratch) if s or c]
-    assert not bad, bad
+def test_big_gemm_kernels_do_not_spill(tmp_path):
+    procs = {}
+    for name in ("gemm_x3", "gemm_x1"):
+        src = os.path.join(ROOT, "csrc", "kernels", name + ".hip")
+        procs[name] = subprocess.Popen([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-c", src, "-o",
+                                        str(tmp_path / (name + ".o")), "-Rpass-analysis=kernel-resource-usage"],
+                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    for name, p in procs.items():
+        _, err = p.communicate(timeout=900)
+        assert p.returncode == 0, err[-2000:]
+        names = re.findall(r"Function Name: (\S+)", err)
+        spills = [int(v) for v in re.findall(r"VGPRs Spill: (\d+)", err)]
+        scratch = [int(v) for v in re.findall(r"ScratchSize \[bytes/lane\]: (\d+)", err)]
+        assert names and len(spills) == len(names) == len(scratch), name
+        assert not [(n, s) for n, s in zip(names, spills) if s], (name, "VGPR spill")
+        # x3: no scratch at all; x1 shares gemm_common.h's epilogue, whose (never taken in these
+        # launches) in-launch split-K combine copies the parameter block to the stack: 12 B
+        lim = 0 if name == "gemm_x3" else 16
+        assert not [(n, c) for n, c in zip(names, scratch) if c > lim], (name, "scratch")

@@ -52,7 +52,8 @@ def main():
                         ref = out.float().clone()
                     else:
                         err = ((out.float() - ref).abs().max() / ref.abs().max().clamp_min(1e-30)).item()
-                        assert err < 1e-4, (name, v, err)
+                        # bf16 outputs: kernels with different summation orders round differently
+                        assert err < (1e-4 if out.dtype == torch.float32 else 1e-2), (name, v, err)
             setv(0)
             fl = 2.0 * B * k * n
             row = {"shape": f"{B}x{k}->{n}", "op": name}
