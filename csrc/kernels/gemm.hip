@@ -547,20 +547,24 @@ static int gemm_run(const void* A, long lda, long sA, int a_kcontig,
   bool vec = al(A) && al(B) && (lda % 8 == 0) && (ldb % 8 == 0) && (sA % 8 == 0) && (sB % 8 == 0);
   vec = vec && (a_kcontig ? (K % 8 == 0) : (M % 8 == 0)) && (b_kcontig ? (K % 8 == 0) : (N % 8 == 0));
   // big-tile kernel (gemm_x1.hip: 256x128 tiles of 8 64x64 waves, loads two steps ahead) for grids
-  // that fill the chip, K split to get there; FM_GEMM_X1=0 or variant bit 1024 disables, bit 512
-  // forces it wherever it applies; FM_GEMM_X1_MIN = blocks (tiles x splits) it needs (default 192)
+  // that fill the chip, K split to get there.  OPT-IN (FM_GEMM_X1=1; variant bit 512 forces it
+  // wherever it applies, bit 1024 disables it; FM_GEMM_X1_MIN = blocks (tiles x splits) it needs,
+  // default 192): measured slower than this file's 128x128 8-wave kernel on every DLRM shape --
+  // 8192x1024x1024 fwd / dX / dW 32.7 / 32.5 / 40.3 vs 29.8 / 27.5 / 39.5 us, bf16 step 0.733 vs
+  // 0.627 ms with its first 32-deep form (profiles/gemm_bf16_x1_ab_r5x.jsonl, bench_ab_x1_r5w.txt):
+  // one block of 8 waves per CU leaves too little MFMA work per barrier to hide the staging
   {
-    static const int x1_env = getenv("FM_GEMM_X1") ? atoi(getenv("FM_GEMM_X1")) : 1;
+    static const int x1_env = getenv("FM_GEMM_X1") ? atoi(getenv("FM_GEMM_X1")) : 0;
     static const long x1_min = getenv("FM_GEMM_X1_MIN") ? atol(getenv("FM_GEMM_X1_MIN")) : 192L;
     const bool force = (g_gemm_variant & 512) != 0;
-    const bool off = x1_env == 0 || (g_gemm_variant & 1024) != 0;
-    if (!off && vec && !atomic_ok && K > 0 && K % 32 == 0 && M >= 64 && N >= 64) {
+    const bool off = (x1_env == 0 && !force) || (g_gemm_variant & 1024) != 0;
+    if (!off && vec && !atomic_ok && K > 0 && K % 64 == 0 && M >= 64 && N >= 64) {
       const int bm = M >= 256 ? 256 : 128;
       GemmP q = p;
       q.tiles_m = (M + bm - 1) / bm;
       q.tiles_n = (N + 127) / 128;
       const long tiles = (long)q.tiles_m * q.tiles_n * batch;
-      const int ktiles = K / 32;
+      const int ktiles = K / 64;
       int ks = 1;
       if (ksplit_req > 0) ks = ksplit_req;
       else if (ws != nullptr) {

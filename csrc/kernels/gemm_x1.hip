@@ -9,9 +9,11 @@
 // fragments (256 B/clk) against 1024 MFMA cycles per SIMD: ~1.5x the MFMA time in LDS traffic
 // alone (26.5 us / 648 TF on 8192x1024x1024, profiles/gemm_variants_probe.txt).  Here:
 //   * 256x128 tile, 8 waves of 64x64 (4x4 16x16x32 tiles): 8 fragment reads per 16 MFMAs;
-//   * [row][32 k] images with 64-B rows and the 16-B chunk XOR-swizzled by (row >> 1) & 3 (the
-//     x3 layout: conflict-free ds_read_b128), two 24 KiB stages, two blocks per CU;
-//   * one barrier per 32-deep k step; the global loads run two steps ahead in two register sets
+//   * [row][64 k] images with 128-B rows and the 16-B chunk XOR-swizzled by (row >> 1) & 7
+//     (conflict-free ds_read_b128), two 48 KiB stages, one block per CU;
+//   * one barrier per 64-deep k step (two MFMA sub-steps; a 32-deep step measured slower than
+//     the register-staged kernel: 35 vs 30 us on 8192x1024x1024, gpurun_out r5w); the global
+//     loads run two steps ahead in two register sets
 //     and the two waves of a SIMD run the staging pass and the MFMAs in opposite order (x3v2
 //     schedule 3);
 //   * K-contiguous operands: one 16-B load per (row, k-octet) unit; MN-contiguous operands (dX's
@@ -26,22 +28,22 @@
 
 namespace {
 
-constexpr int X1K = 32;   // k per stage
+constexpr int X1K = 64;   // k per stage (two 32-deep MFMA sub-steps per barrier)
 
-FM_DEVICE int x1_off(int r, int c) { return r * 64 + 16 * (c ^ ((r >> 1) & 3)); }
+// byte offset of 16-B chunk c (8 bf16) of row r in a [row][64 k] image (128-B rows, chunk XOR (r>>1)&7)
+FM_DEVICE int x1_off(int r, int c) { return r * 128 + 16 * (c ^ ((r >> 1) & 7)); }
 
 template <bool KC, int R, int NTH>
 struct X1Stage {
-  static constexpr int UNITS = R * 4;
+  static constexpr int UNITS = R * (X1K / 8);
   static constexpr int PER_T = (UNITS + NTH - 1) / NTH;
-  static constexpr int NV = KC ? 1 : 8;
   // KC: the unit's 16 B; MN: eight k values (low half of each word), packed at store time
   unsigned v[PER_T][KC ? 4 : 8];
 
   FM_DEVICE static void unit(int ci, int& r, int& c) {
     if constexpr (KC) {
-      r = ci >> 2;
-      c = ci & 3;
+      r = ci / (X1K / 8);
+      c = ci % (X1K / 8);
     } else {
       r = ci % R;
       c = ci / R;
@@ -108,7 +110,7 @@ template <int BM, int BN, bool AK, bool BKC, bool SGD>
 __global__ void __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) fm_gemm_x1_kernel(GemmP p) {
   constexpr int WN = BN / 64, NTH = (BM / 64) * WN * 64;
   constexpr int MR = 4, NR = 4;
-  constexpr int PA_ = BM * 64, PB_ = BN * 64;          // bytes of one operand image
+  constexpr int PA_ = BM * X1K * 2, PB_ = BN * X1K * 2;   // bytes of one operand image
   constexpr int STG = PA_ + PB_;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -163,20 +165,24 @@ __global__ void __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) fm_gemm_x1_kern
     __syncthreads();                 // stage t&1 complete; stage (t+1)&1 no longer read
     const char* la = stage(t & 1);
     const char* lb = la + PA_;
-    bf16x8_t bf[NR];
-#pragma unroll
-    for (int j = 0; j < NR; ++j) bf[j] = *reinterpret_cast<const bf16x8_t*>(lb + x1_off(wn * 64 + 16 * j + q, g));
     if (!mfma_first && t + 1 < nst) {
       put_from((t + 1) & 1, SA, SB);
       if (t + 3 < nst) get_into(kt0 + t + 3, SA, SB);
     }
 #pragma unroll
-    for (int i = 0; i < MR; ++i) {
-      const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(la + x1_off(wm * 64 + 16 * i + q, g));
+    for (int ss = 0; ss < X1K / 32; ++ss) {
+      bf16x8_t bf[NR];
 #pragma unroll
       for (int j = 0; j < NR; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8v_t*>(&bf[j]),
-                                                            *reinterpret_cast<const bf16x8v_t*>(&af), acc[i][j], 0, 0, 0);
+        bf[j] = *reinterpret_cast<const bf16x8_t*>(lb + x1_off(wn * 64 + 16 * j + q, 4 * ss + g));
+#pragma unroll
+      for (int i = 0; i < MR; ++i) {
+        const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(la + x1_off(wm * 64 + 16 * i + q, 4 * ss + g));
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8v_t*>(&bf[j]),
+                                                              *reinterpret_cast<const bf16x8v_t*>(&af), acc[i][j], 0, 0, 0);
+      }
     }
     if (mfma_first && t + 1 < nst) {
       put_from((t + 1) & 1, SA, SB);
@@ -207,7 +213,7 @@ __global__ void __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) fm_gemm_x1_kern
 template <int BM, int BN, bool SGD>
 void launch_x1(const GemmP& p, bool ak, bool bk, hipStream_t s) {
   constexpr int NTH = (BM / 64) * (BN / 64) * 64;
-  constexpr int LDS = 2 * (BM + BN) * 64;
+  constexpr int LDS = 2 * (BM + BN) * X1K * 2;
   dim3 grid(p.tiles_m * p.tiles_n, p.batch, p.ksplit);
   if (ak && bk) hipLaunchKernelGGL((fm_gemm_x1_kernel<BM, BN, true, true, SGD>), grid, dim3(NTH), LDS, s, p);
   else if (ak) hipLaunchKernelGGL((fm_gemm_x1_kernel<BM, BN, true, false, SGD>), grid, dim3(NTH), LDS, s, p);
@@ -218,7 +224,7 @@ void launch_x1(const GemmP& p, bool ak, bool bk, hipStream_t s) {
 }  // namespace
 
 // Launch on a prepared parameter block (tiles_m / tiles_n / ksplit filled for the bm x 128 tile).
-// Caller guarantees: K % 32 == 0 (per split: whole steps); K-contiguous operands 16-B aligned
+// Caller guarantees: K % 64 == 0 (per split: whole steps); K-contiguous operands 16-B aligned
 // with ld % 8 == 0 (MN-contiguous: no constraint); no in-launch split-K combine (tile_cnt null).
 // sgd: the fused-SGD epilogue (unsplit tiles only).  Returns -1 for an unsupported tile.
 extern "C" int fm_gemm_x1_launch(const void* params, int bm, int a_kcontig, int b_kcontig, int sgd, hipStream_t s) {

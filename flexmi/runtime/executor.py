@@ -206,9 +206,11 @@ def Embedding_row_lo(ctx):
 
 
 # items after the embedding-group backward that touch nothing it writes when every group table is
-# trained by fused sparse SGD (no dense table gradient): the dense optimizer step and the split-K
-# stream join run on the main stream without waiting for the side stream, which is joined at the
-# segment end instead (FM_EMB_LATE_JOIN=0: join before them, as for dense-gradient tables)
+# trained by fused sparse SGD (no dense table gradient): with FM_EMB_LATE_JOIN=1 the dense optimizer
+# step and the split-K stream join run on the main stream without waiting for the side stream,
+# which is joined at the segment end instead.  OPT-IN: measured slower on the MLPerf fp32 step
+# (1.189 vs 1.178 ms, profiles/bench_ab_late_join_r5w.txt -- the optimizer sweep then contends
+# with the embedding backward instead of running alone after it)
 LATE_JOIN_OK = ("update", "gemm.join", "fused_sgd.disarm")
 
 
@@ -2493,7 +2495,7 @@ class Executor:
         s.wait_stream(torch.cuda.current_stream())
         ov = overlap_embeddings_enabled(self)
         side = torch.cuda.Stream() if ov else None
-        late = ov and os.environ.get("FM_EMB_LATE_JOIN", "1") != "0" and self._groups_sparse_only()
+        late = ov and os.environ.get("FM_EMB_LATE_JOIN", "0") == "1" and self._groups_sparse_only()
         runs = []
         graphs = []
         # thread_local capture: the RCCL process group's watchdog thread queries events while

@@ -436,7 +436,7 @@ def test_embedding_overlap_on_off_equivalent(gpu, monkeypatch):
     res = {}
     for mode in ("0", "1", "1-early-join"):
         monkeypatch.setattr(E, "OVERLAP_EMB", mode[0])
-        # late join (default): the dense update does not wait for the sparse-SGD table backward
+        # late join (opt-in): the dense update does not wait for the sparse-SGD table backward
         monkeypatch.setenv("FM_EMB_LATE_JOIN", "0" if mode == "1-early-join" else "1")
         ws, loss, ex = _dlrm_run("gpu", dcfg, 2048, 4, graph=True)
         assert E.overlap_embeddings_enabled(ex) == (mode[0] == "1")
