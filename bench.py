@@ -228,24 +228,39 @@ def run_once(a, dtype, comm, strategy=None):
         for _ in range(2):
             step_eager()
         torch.cuda.synchronize()
-        stage = []
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        for k in range(data.nb):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.stream(s):
-                with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+        gi = [0]
+        if os.environ.get("FM_BENCH_STAGE_GRAPH", "0") == "1":
+            # A/B: input staging as its own small graph per pooled batch, replayed before the step
+            stage = []
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            for k in range(data.nb):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.stream(s):
+                    with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+                        data.i = k
+                        data.next_batch()
+                stage.append(g)
+            torch.cuda.current_stream().wait_stream(s)
+            run_step = ex.capture_step()
+
+            def step():
+                stage[gi[0] % len(stage)].replay()
+                run_step()
+                gi[0] += 1
+        else:
+            # one step graph per pooled batch with that batch's input staging captured at its head
+            # (one multi-copy launch): no second graph launch and no gap between the two per step
+            def stage_fn(k):
+                def f():
                     data.i = k
                     data.next_batch()
-            stage.append(g)
-        torch.cuda.current_stream().wait_stream(s)
-        run_step = ex.capture_step()
-        gi = [0]
+                return f
+            runs = [ex.capture_step(pre=stage_fn(k)) for k in range(data.nb)]
 
-        def step():
-            stage[gi[0] % len(stage)].replay()
-            run_step()
-            gi[0] += 1
+            def step():
+                runs[gi[0] % len(runs)]()
+                gi[0] += 1
     else:
         step = step_eager
 

@@ -259,17 +259,17 @@ struct CopyDesc {
   long rows, cols, lds, ldd;
   int vec;   // 16-B units: pointers, row bytes and leading dims all multiples of 16 B
 };
-constexpr int MAXC = 16;
+constexpr int MAXC = 32;   // one launch stages a DLRM batch's 27 inputs
 struct CopyTab {
   CopyDesc d[MAXC];
   int n;
-  int add;  // bitmask: accumulate into dst
+  unsigned add;  // bitmask: accumulate into dst
 };
 
 template <typename T>
 __global__ void fm_multi_copy(CopyTab t) {
   const CopyDesc& d = t.d[blockIdx.y];
-  const int add = (t.add >> blockIdx.y) & 1;
+  const int add = (t.add >> blockIdx.y) & 1u;
   if (d.vec) {   // 16-B vector path: 8 bf16 / 4 fp32 per thread-iteration
     constexpr int E = 16 / sizeof(T);
     const long cu = d.cols / E, total = d.rows * cu;
@@ -482,7 +482,7 @@ extern "C" void fm_multi_copy2d(int n, const void* const* src, void* const* dst,
       maxe = std::max(maxe, rows[base + i] * cols[base + i] / (vec ? E : 1));
     }
     t.n = m;
-    t.add = (add_mask >> base) & ((1 << m) - 1);
+    t.add = base < 32 ? ((unsigned)add_mask >> base) & (m >= 32 ? 0xffffffffu : ((1u << m) - 1u)) : 0u;
     dim3 grid(fm_grid(maxe, 256, 1024), m);
     if (elem_bytes == 2) hipLaunchKernelGGL((fm_multi_copy<unsigned short>), grid, dim3(256), 0, s, t);
     else hipLaunchKernelGGL((fm_multi_copy<float>), grid, dim3(256), 0, s, t);

@@ -556,7 +556,19 @@ __global__ void __launch_bounds__(256) fm_dot_bwd_f32(PtrTabF Z, long ldz, const
 // per lane), stages the sample's Z (F <= 32 rows) in a per-wave LDS tile padded to D + 4 floats a
 // row (the row-per-lane ds_read_b128 of the MFMA operands is then bank-conflict free), and keeps
 // the NEXT sample's rows in flight in registers while this sample's MFMAs and stores run.
-template <int D, typename ZT = PtrTabF>
+// exact truncation split of two fp32 values into three packed bf16 pairs (as gemm_x3.hip split2)
+FM_DEVICE void dot_split2(float a, float b, unsigned& h, unsigned& m, unsigned& l) {
+  const unsigned ha = __float_as_uint(a) & 0xffff0000u, hb = __float_as_uint(b) & 0xffff0000u;
+  const float ra = a - __uint_as_float(ha), rb = b - __uint_as_float(hb);
+  const unsigned ma = __float_as_uint(ra) & 0xffff0000u, mb = __float_as_uint(rb) & 0xffff0000u;
+  const unsigned la = __float_as_uint(ra - __uint_as_float(ma)) & 0xffff0000u;
+  const unsigned lb = __float_as_uint(rb - __uint_as_float(mb)) & 0xffff0000u;
+  h = (ha >> 16) | hb;
+  m = (ma >> 16) | mb;
+  l = (la >> 16) | lb;
+}
+
+template <int D, typename ZT = PtrTabF, bool X3 = false>
 __global__ void __launch_bounds__(256, 2) fm_dot_fwd_f32s(ZT Z, long ldz, float* __restrict__ out, long ldo, long B,
                                                           int F, int W, int self) {
   constexpr int LPR = D / 4, RPI = 64 / LPR, NI = 32 / RPI, RS = D + 4;
@@ -590,11 +602,37 @@ __global__ void __launch_bounds__(256, 2) fm_dot_fwd_f32s(ZT Z, long ldz, float*
     f32x16_t acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    if constexpr (X3) {
+      // exact three-way bf16 split of every fp32 value (gemm_x3.hip): G = sum of the six products
+      // with plane indices summing to <= 2 on v_mfma_f32_32x32x16_bf16 (32 cycles per 16 k against
+      // 8 x 16 for 32x32x2f32); lane (r, h) holds Z[r][16 s + 8 h .. + 7] for both operands
 #pragma unroll
-    for (int v = 0; v < D / 8; ++v) {
-      const f32x4_t x = *reinterpret_cast<const f32x4_t*>(zs + r * RS + h * (D / 2) + 4 * v);
+      for (int st = 0; st < D / 16; ++st) {
+        const f32x4_t x0 = *reinterpret_cast<const f32x4_t*>(zs + r * RS + 16 * st + 8 * h);
+        const f32x4_t x1 = *reinterpret_cast<const f32x4_t*>(zs + r * RS + 16 * st + 8 * h + 4);
+        unsigned ph[4], pm[4], pl[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x[e], x[e], acc, 0, 0, 0);
+        for (int u = 0; u < 4; ++u) {
+          const float a = u < 2 ? x0[2 * u] : x1[2 * u - 4], b = u < 2 ? x0[2 * u + 1] : x1[2 * u - 3];
+          dot_split2(a, b, ph[u], pm[u], pl[u]);
+        }
+        const bf16x8v_t H = __builtin_bit_cast(bf16x8v_t, u32x4_t{ph[0], ph[1], ph[2], ph[3]});
+        const bf16x8v_t Mm = __builtin_bit_cast(bf16x8v_t, u32x4_t{pm[0], pm[1], pm[2], pm[3]});
+        const bf16x8v_t L = __builtin_bit_cast(bf16x8v_t, u32x4_t{pl[0], pl[1], pl[2], pl[3]});
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(L, H, acc, 0, 0, 0);    // small terms first
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(H, L, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Mm, Mm, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Mm, H, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(H, Mm, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(H, H, acc, 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int v = 0; v < D / 8; ++v) {
+        const f32x4_t x = *reinterpret_cast<const f32x4_t*>(zs + r * RS + h * (D / 2) + 4 * v);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x[e], x[e], acc, 0, 0, 0);
+      }
     }
     // output row: [ z_0 (D) | pairs | zero pad ]
     for (int c = 4 * lane; c < D; c += 256) *reinterpret_cast<f32x4_t*>(row + c) = *reinterpret_cast<const f32x4_t*>(zs + c);
@@ -781,12 +819,23 @@ extern "C" void fm_dot_interaction_fwd_f32(const float* const* z, int F, long ld
   static const bool staged = getenv("FM_DOT_FWD_STAGED") == nullptr || atoi(getenv("FM_DOT_FWD_STAGED")) != 0;
   if (staged && fast && D >= 32 && F <= 32 && (W & 3) == 0 && (ldo & 3) == 0 && W <= 1024 && al16(out)) {
     const size_t lds_s = (size_t)waves * (32 * (D + 4) + ((W + 3) & ~3)) * 4;
-    auto ks = D == 128 ? fm_dot_fwd_f32s<128> : D == 64 ? fm_dot_fwd_f32s<64> : fm_dot_fwd_f32s<32>;
+    // FM_DOT_FWD_X3=1: the Gram on the bf16 matrix cores through the exact three-way split
+    const char* x3e = getenv("FM_DOT_FWD_X3");   // read per call: tests flip it in-process
+    const bool x3 = x3e != nullptr && atoi(x3e) == 1;
+    auto ks = x3 ? (D == 128 ? fm_dot_fwd_f32s<128, PtrTabF, true> : D == 64 ? fm_dot_fwd_f32s<64, PtrTabF, true>
+                                                                            : fm_dot_fwd_f32s<32, PtrTabF, true>)
+                 : (D == 128 ? fm_dot_fwd_f32s<128> : D == 64 ? fm_dot_fwd_f32s<64> : fm_dot_fwd_f32s<32>);
     static bool attr = false;
     if (!attr) {
       (void)hipFuncSetAttribute((const void*)fm_dot_fwd_f32s<128>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10);
       (void)hipFuncSetAttribute((const void*)fm_dot_fwd_f32s<64>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10);
       (void)hipFuncSetAttribute((const void*)fm_dot_fwd_f32s<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10);
+      (void)hipFuncSetAttribute((const void*)fm_dot_fwd_f32s<128, PtrTabF, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                96 << 10);
+      (void)hipFuncSetAttribute((const void*)fm_dot_fwd_f32s<64, PtrTabF, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                96 << 10);
+      (void)hipFuncSetAttribute((const void*)fm_dot_fwd_f32s<32, PtrTabF, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                96 << 10);
       attr = true;
     }
     hipLaunchKernelGGL(ks, dim3((int)blocks), dim3(64 * waves), lds_s, s, t, ldz, out, ldo, B, F, W, self);

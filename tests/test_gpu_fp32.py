@@ -193,6 +193,35 @@ def test_dot_interaction_f32(gpu, F, D, selfi):
         assert rel_err(dz[i], exp) < TOL, i
 
 
+@pytest.mark.parametrize("F,D,selfi", [(27, 128, False), (9, 64, True), (32, 32, False), (28, 128, True)])
+def test_dot_interaction_f32_split_forward(gpu, monkeypatch, F, D, selfi):
+    """fp32 interaction forward with the Gram on the bf16 matrix cores through the exact
+    three-way split (FM_DOT_FWD_X3=1), incl. operands spanning many binades, vs float64."""
+    from flexmi.ops import _kernels as Kk
+    monkeypatch.setenv("FM_DOT_FWD_X3", "1")
+    torch.manual_seed(19)
+    B = 777
+    zs = [torch.randn(B, D, device=gpu) * torch.exp2(torch.randint(-12, 12, (B, D), device=gpu).float())
+          for _ in range(F)]
+    npairs = F * (F + 1) // 2 if selfi else F * (F - 1) // 2
+    W = (D + npairs + 15) // 16 * 16
+    y = torch.full((B, W), 7.0, device=gpu)
+    Kk.dot_interaction_forward(zs, y, selfi)
+    Z = torch.stack([z.double() for z in zs], 1)
+    G = Z @ Z.transpose(1, 2)
+    li, lj = zip(*[(i, j) for i in range(F) for j in range(i + (1 if selfi else 0))])
+    ref = torch.zeros(B, W, dtype=torch.float64, device=gpu)
+    ref[:, :D] = Z[:, 0]
+    ref[:, D:D + npairs] = G[:, li, lj]
+    # per-element error against the magnitude the fp32 product sums carry (|Z||Z|^T)
+    A = Z.abs() @ Z.abs().transpose(1, 2)
+    scale = torch.zeros_like(ref)
+    scale[:, :D] = Z[:, 0].abs()
+    scale[:, D:D + npairs] = A[:, li, lj]
+    err = ((y.double() - ref).abs() / scale.clamp_min(1e-30))[:, :D + npairs].max().item()
+    assert err < 1e-5, err
+
+
 @pytest.mark.parametrize("F,D,selfi", [(27, 128, False), (27, 64, False), (9, 24, True), (5, 128, True)])
 def test_dot_interaction_f32_act0(gpu, F, D, selfi):
     """act0: the bottom MLP's ReLU backward applied to feature 0's gradient inside the interaction
