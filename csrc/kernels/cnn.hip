@@ -455,7 +455,8 @@ __global__ void __launch_bounds__(256) fm_pool_bwd_max_scatter(const T* __restri
                                                                const unsigned char* __restrict__ code, T* __restrict__ dx,
                                                                int NC, int H, int W, int P, int Q, int kh, int kw, int sh,
                                                                int pt, int pl, int sw, int act, int acc, int HB, int nbands,
-                                                               int G, FastDiv dQ, FastDiv dPQ, FastDiv dkw, FastDiv dsh) {
+                                                               int G, FastDiv dQ, FastDiv dPQ, FastDiv dkw, FastDiv dsh,
+                                                               int pa, int qa, int nph) {
   extern __shared__ float sdx[];
   int nc0, band, planes;
   if (G > 1) {
@@ -476,23 +477,34 @@ __global__ void __launch_bounds__(256) fm_pool_bwd_max_scatter(const T* __restri
   const int phi = G > 1 ? P : min(P, (h1b - 1 + pt) >= 0 ? fdiv(h1b - 1 + pt, dsh) + 1 : 0);
   const int nwin1 = max(0, phi - plo) * Q;
   const int nwin = planes * nwin1;
-  for (int e = threadIdx.x; e < nwin; e += 256) {
-    int gi = 0, r = e;
-    if (G > 1) {
-      gi = fdiv(e, dPQ);
-      r = e - gi * nwin1;
+  // phases > 1 (FM_POOL_SCATTER_PHASES=1): windows p, p + pa (pa = ceil(kh / sh)) and q, q + qa never
+  // share an input, so the (p mod pa, q mod qa) classes run one after another with plain LDS
+  // read-add-writes instead of LDS float atomics
+  for (int ph = 0; ph < nph; ++ph) {
+    const int pph = ph / qa, qph = ph - pph * qa;
+    for (int e = threadIdx.x; e < nwin; e += 256) {
+      int gi = 0, r = e;
+      if (G > 1) {
+        gi = fdiv(e, dPQ);
+        r = e - gi * nwin1;
+      }
+      const int pr = fdiv(r, dQ), q = r - pr * Q;
+      const int p = plo + pr;
+      if (nph > 1 && (p % pa != pph || q % qa != qph)) continue;
+      const long oi = ((long)(nc0 + gi) * P + p) * Q + q;
+      const int cd = code[oi];
+      if (cd == 255) continue;
+      const int rr = fdiv(cd, dkw), cc = cd - rr * kw;
+      const int h = p * sh - pt + rr;
+      if (h < h0b || h >= h1b) continue;             // this window's max lies in another band
+      const int w = q * sw - pl + cc;
+      const float gd = tof(dy[oi]);
+      const float v = act == ACT_NONE ? gd : act_bwd(act, tof(y[oi]), gd);
+      float* t = &sdx[(gi * rows + h - h0b) * W + w];
+      if (nph > 1) *t += v;
+      else atomicAdd(t, v);
     }
-    const int pr = fdiv(r, dQ), q = r - pr * Q;
-    const int p = plo + pr;
-    const long oi = ((long)(nc0 + gi) * P + p) * Q + q;
-    const int cd = code[oi];
-    if (cd == 255) continue;
-    const int rr = fdiv(cd, dkw), cc = cd - rr * kw;
-    const int h = p * sh - pt + rr;
-    if (h < h0b || h >= h1b) continue;             // this window's max lies in another band
-    const int w = q * sw - pl + cc;
-    const float gd = tof(dy[oi]);
-    atomicAdd(&sdx[(gi * rows + h - h0b) * W + w], act == ACT_NONE ? gd : act_bwd(act, tof(y[oi]), gd));
+    if (nph > 1) __syncthreads();
   }
   __syncthreads();
   // (a 16-B vector-store form of this loop -- 8 bf16 per lane between scalar head / tail -- measured
@@ -842,10 +854,13 @@ static void fm_pool_bwd_t(const void* x, const void* y, const void* dy, void* dx
     const size_t lds = (size_t)G * maxprows * Q * 5;
     if (is_max) {                        // max pooling: scatter through the recorded argmax
       const int blocks = G > 1 ? (NC + G - 1) / G : NC * nbands;
+      const char* phe = getenv("FM_POOL_SCATTER_PHASES");
+      const bool phases = phe != nullptr && atoi(phe) == 1;
+      const int pa = (kh + sh - 1) / sh, qa = (kw + sw - 1) / sw;
       const size_t lds_s = (size_t)(G > 1 ? G * H : HB) * W * sizeof(float);
       hipLaunchKernelGGL(fm_pool_bwd_max_scatter<T>, dim3(blocks), dim3(256), lds_s, st, (const T*)y, (const T*)dy,
                          (const unsigned char*)code, (T*)dx, NC, H, W, P, Q, kh, kw, sh, pt, pl, sw, act, acc, HB, nbands, G,
-                         make_fastdiv(Q), make_fastdiv(P * Q), make_fastdiv(kw), make_fastdiv(sh));
+                         make_fastdiv(Q), make_fastdiv(P * Q), make_fastdiv(kw), make_fastdiv(sh), pa, qa, phases ? pa * qa : 1);
       return;
     }
     if (lds <= 48 * 1024) {

@@ -819,9 +819,11 @@ extern "C" void fm_dot_interaction_fwd_f32(const float* const* z, int F, long ld
   static const bool staged = getenv("FM_DOT_FWD_STAGED") == nullptr || atoi(getenv("FM_DOT_FWD_STAGED")) != 0;
   if (staged && fast && D >= 32 && F <= 32 && (W & 3) == 0 && (ldo & 3) == 0 && W <= 1024 && al16(out)) {
     const size_t lds_s = (size_t)waves * (32 * (D + 4) + ((W + 3) & ~3)) * 4;
-    // FM_DOT_FWD_X3=1: the Gram on the bf16 matrix cores through the exact three-way split
+    // the Gram on the bf16 matrix cores through the exact three-way split (default; FM_DOT_FWD_X3=0:
+    // the fp32 MFMA): 8192 x 27 x 128 forward 35.6 -> 29.4 us, MLPerf fp32 step -6 us
+    // (profiles/dot_fwd_x3_ab_r5y.txt)
     const char* x3e = getenv("FM_DOT_FWD_X3");   // read per call: tests flip it in-process
-    const bool x3 = x3e != nullptr && atoi(x3e) == 1;
+    const bool x3 = !(x3e != nullptr && atoi(x3e) == 0);
     auto ks = x3 ? (D == 128 ? fm_dot_fwd_f32s<128, PtrTabF, true> : D == 64 ? fm_dot_fwd_f32s<64, PtrTabF, true>
                                                                             : fm_dot_fwd_f32s<32, PtrTabF, true>)
                  : (D == 128 ? fm_dot_fwd_f32s<128> : D == 64 ? fm_dot_fwd_f32s<64> : fm_dot_fwd_f32s<32>);
