@@ -213,6 +213,10 @@ def Embedding_row_lo(ctx):
 # with the embedding backward instead of running alone after it)
 LATE_JOIN_OK = ("update", "gemm.join", "fused_sgd.disarm")
 
+# FM_EMB_FWD_DELAY=d: fork a hoisted embedding-group forward d items later than the earliest point
+# it may start (A/B: lets the first bottom-MLP layer run alone instead of beside the gather)
+EMB_FWD_DELAY = max(0, int(os.environ.get("FM_EMB_FWD_DELAY", "0")))
+
 
 def _run_overlapped(items, s, side, late_join=False):
     """Issue one graph segment's items with the embedding groups on ``side`` (fork/join by events,
@@ -230,6 +234,7 @@ def _run_overlapped(items, s, side, late_join=False):
             if prev.writes is None or prev.name.endswith(".group_fwd") or (prev.writes & reads):
                 break
             j -= 1
+        j = min(k, j + EMB_FWD_DELAY)
         if j < k:
             hoist.add(k)
             fork_at.setdefault(j, []).append(k)
