@@ -477,9 +477,11 @@ __global__ void __launch_bounds__(256) fm_pool_bwd_max_scatter(const T* __restri
   const int phi = G > 1 ? P : min(P, (h1b - 1 + pt) >= 0 ? fdiv(h1b - 1 + pt, dsh) + 1 : 0);
   const int nwin1 = max(0, phi - plo) * Q;
   const int nwin = planes * nwin1;
-  // phases > 1 (FM_POOL_SCATTER_PHASES=1): windows p, p + pa (pa = ceil(kh / sh)) and q, q + qa never
-  // share an input, so the (p mod pa, q mod qa) classes run one after another with plain LDS
-  // read-add-writes instead of LDS float atomics
+  // phases > 1 (FM_POOL_SCATTER_PHASES=1, opt-in): windows p, p + pa (pa = ceil(kh / sh)) and q,
+  // q + qa never share an input, so the (p mod pa, q mod qa) classes run one after another with plain
+  // LDS read-add-writes instead of LDS float atomics.  Measured slower on AlexNet b256 (82.5 k vs
+  // 84.1 k img/s, profiles/pool_scatter_phases_ab_r5z.txt): the extra window passes and barriers
+  // cost more than the few colliding atomics at stride 2
   for (int ph = 0; ph < nph; ++ph) {
     const int pph = ph / qa, qph = ph - pph * qa;
     for (int e = threadIdx.x; e < nwin; e += 256) {

@@ -214,7 +214,8 @@ def Embedding_row_lo(ctx):
 LATE_JOIN_OK = ("update", "gemm.join", "fused_sgd.disarm")
 
 # FM_EMB_FWD_DELAY=d: fork a hoisted embedding-group forward d items later than the earliest point
-# it may start (A/B: lets the first bottom-MLP layer run alone instead of beside the gather)
+# it may start (A/B: lets the first bottom-MLP layer run alone instead of beside the gather; measured
+# no better on the MLPerf fp32 step, profiles/bench_ab_emb_fwd_delay_r5za.txt)
 EMB_FWD_DELAY = max(0, int(os.environ.get("FM_EMB_FWD_DELAY", "0")))
 
 
