@@ -66,14 +66,46 @@ FM_DEVICE long ldi(const void* p, long i) {
 }
 
 template <typename OutT, bool I64>
-__global__ void __launch_bounds__(256) fm_emb_fwd_multi(TabSet s, long B) {
+__global__ void __launch_bounds__(256) fm_emb_fwd_multi(TabSet s, long B, int su) {
   const TabDesc& d = s.t[blockIdx.y];
   const int D4 = d.D >> 2;
   const int lpr = D4 < 64 ? D4 : 64;              // lanes per row (D <= 256)
   const int rpi = 256 / lpr;                       // rows per block-iteration
   const int sub = threadIdx.x / lpr, lc = threadIdx.x - sub * lpr;
   if (sub >= rpi) return;
-  for (long b = (long)blockIdx.x * rpi + sub; b < B; b += (long)gridDim.x * rpi) {
+  const long bstride = (long)gridDim.x * rpi;
+  if (su && d.bag == 1 && D4 <= 64) {
+    // one lookup per sample (the MLPerf tables): SU samples' index loads, then their row loads in
+    // flight per lane, so a small grid still streams at the HBM rate and leaves CU slots to the
+    // bottom-MLP GEMMs running beside it on the other stream
+    constexpr int SU = 4;
+    const int c = lc * 4;
+    for (long b0 = (long)blockIdx.x * rpi + sub; b0 < B; b0 += SU * bstride) {
+      long r[SU];
+      bool ok[SU];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) r[u] = local_row(ldi<I64>(d.idx, min(b0 + u * bstride, B - 1)), d.lo, d.rows, ok[u]);
+      f32x4_t v[SU];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) v[u] = *reinterpret_cast<const f32x4_t*>(d.W + r[u] * d.D + c);
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const long b = b0 + u * bstride;
+        if (b >= B) break;
+        f32x4_t acc = ok[u] ? v[u] * d.scale : f32x4_t{0.f, 0.f, 0.f, 0.f};
+        OutT* o = reinterpret_cast<OutT*>(d.act) + b * d.ld + c;
+        if constexpr (sizeof(OutT) == 4) {
+          *reinterpret_cast<f32x4_t*>(o) = acc;
+        } else {
+          bf16x4_t w;
+          w[0] = (short)f2bf(acc[0]); w[1] = (short)f2bf(acc[1]); w[2] = (short)f2bf(acc[2]); w[3] = (short)f2bf(acc[3]);
+          *reinterpret_cast<bf16x4_t*>(o) = w;
+        }
+      }
+    }
+    return;
+  }
+  for (long b = (long)blockIdx.x * rpi + sub; b < B; b += bstride) {
     for (int c4 = lc; c4 < D4; c4 += lpr) {
       const int c = c4 * 4;
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
@@ -373,9 +405,11 @@ void launch_fwd(const TabSet& s, int m, bool vec, bool out_bf16, long B, int D0,
   // at 2048 blocks per table, 1.164 at 256, 1.172 at 64 (profiles/bench_ab_x3_sched_embgrid_r5n.txt)
   static const long cap_env = getenv("FM_EMB_FWD_BLOCKS") ? std::max(1L, atol(getenv("FM_EMB_FWD_BLOCKS"))) : 256L;
   dim3 grid((unsigned)std::max<long>(1, std::min<long>((B + rpi - 1) / rpi, cap_env)), m);
+  // FM_EMB_FWD_SU=0: one sample per lane-group iteration for single-lookup bags (A/B)
+  static const int su = !(getenv("FM_EMB_FWD_SU") != nullptr && atoi(getenv("FM_EMB_FWD_SU")) == 0);
   if (vec) {
-    if (out_bf16) hipLaunchKernelGGL((fm_emb_fwd_multi<unsigned short, I64>), grid, dim3(256), 0, st, s, B);
-    else hipLaunchKernelGGL((fm_emb_fwd_multi<float, I64>), grid, dim3(256), 0, st, s, B);
+    if (out_bf16) hipLaunchKernelGGL((fm_emb_fwd_multi<unsigned short, I64>), grid, dim3(256), 0, st, s, B, su);
+    else hipLaunchKernelGGL((fm_emb_fwd_multi<float, I64>), grid, dim3(256), 0, st, s, B, su);
   } else {
     if (out_bf16) hipLaunchKernelGGL((fm_emb_fwd_multi_scalar<unsigned short, I64>), grid, dim3(256), 0, st, s, B);
     else hipLaunchKernelGGL((fm_emb_fwd_multi_scalar<float, I64>), grid, dim3(256), 0, st, s, B);
