@@ -2497,7 +2497,10 @@ class Executor:
                 segments.append(("comm", it))
         if cur:
             segments.append(("graph", cur))
-        s = torch.cuda.Stream()
+        # FM_STREAM_PRIO=1 (A/B): the main stream (MLP chain, the critical path) at high priority and
+        # the embedding side stream at the default (lowest) one
+        prio = os.environ.get("FM_STREAM_PRIO", "0") == "1"
+        s = torch.cuda.Stream(priority=-1) if prio else torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         ov = overlap_embeddings_enabled(self)
         side = torch.cuda.Stream() if ov else None
