@@ -2498,7 +2498,9 @@ class Executor:
         if cur:
             segments.append(("graph", cur))
         # FM_STREAM_PRIO=1 (A/B): the main stream (MLP chain, the critical path) at high priority and
-        # the embedding side stream at the default (lowest) one
+        # the embedding side stream at the default (lowest) one.  Measured much slower (2.08-2.19 vs
+        # 1.15 ms/step, profiles/bench_ab_stream_prio_r5p.txt): the captured graph then starts the
+        # MLP chain ~30 us late and idles 84 us per step between the two queues
         prio = os.environ.get("FM_STREAM_PRIO", "0") == "1"
         s = torch.cuda.Stream(priority=-1) if prio else torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
