@@ -229,8 +229,9 @@ def run_once(a, dtype, comm, strategy=None):
             step_eager()
         torch.cuda.synchronize()
         gi = [0]
-        if os.environ.get("FM_BENCH_STAGE_GRAPH", "0") == "1":
-            # A/B: input staging as its own small graph per pooled batch, replayed before the step
+        if world > 1 or os.environ.get("FM_BENCH_STAGE_GRAPH", "0") == "1":
+            # input staging as its own small graph per pooled batch, replayed before the step (N > 1:
+            # one segmented step capture instead of one per pooled batch; N = 1 A/B)
             stage = []
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
