@@ -19,6 +19,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -92,13 +93,13 @@ __global__ void __launch_bounds__(256) fm_smallk_fwd_f32(const float* __restrict
 // [c*G, (c+1)*G) (G groups of 4 output rows n); thread = (sub-row, group) with its rows' dpre
 // loads all in flight at once; x rows come from LDS.  The R = NT/G sub-rows of a group are summed
 // through LDS into ws[p][k][j][g] (n = 4g + j, k = K: the bias)
-template <int K>
+template <int K, int ROWS = SK_ROWS_DW>
 __global__ void __launch_bounds__(SK_DW_NT) fm_smallk_dw_part(const float* __restrict__ dpre, long ldd,
                                                              const float* __restrict__ x, long ldx,
                                                              float* __restrict__ ws, long M, int N, int G) {
   constexpr int NT = SK_DW_NT;
   constexpr int PER = 8;                          // rows per thread in flight
-  __shared__ __attribute__((aligned(16))) float xs[SK_ROWS_DW * K];
+  __shared__ __attribute__((aligned(16))) float xs[ROWS * K];
   constexpr int KCH = 17;                         // partial sums staged per LDS pass (k chunk)
   __shared__ float red[KCH * NT];
   const int R = NT / G;
@@ -106,8 +107,8 @@ __global__ void __launch_bounds__(SK_DW_NT) fm_smallk_dw_part(const float* __res
   const int sub = threadIdx.x / G, cg = threadIdx.x % G;
   const int g = blockIdx.y * G + cg;
   const bool live = sub < R && g < NG;
-  const long m0 = (long)blockIdx.x * SK_ROWS_DW;
-  stage_x<K, NT>(x, ldx, m0, M, SK_ROWS_DW, xs);
+  const long m0 = (long)blockIdx.x * ROWS;
+  stage_x<K, NT>(x, ldx, m0, M, ROWS, xs);
   __syncthreads();
   float acc[4][K + 1];
 #pragma unroll
@@ -115,7 +116,7 @@ __global__ void __launch_bounds__(SK_DW_NT) fm_smallk_dw_part(const float* __res
 #pragma unroll
     for (int k = 0; k <= K; ++k) acc[j][k] = 0.f;
   if (live) {
-    const int rows = (int)min((long)SK_ROWS_DW, M - m0);
+    const int rows = (int)min((long)ROWS, M - m0);
     for (int r0 = sub; r0 < rows; r0 += PER * R) {
       f32x4_t d[PER];
 #pragma unroll
@@ -247,13 +248,23 @@ extern "C" int fm_smallk_dw_f32_launch(const float* dpre, long ldd, const float*
     return -1;
   const int NG = N / 4;
   const int G = NG < 64 ? NG : 64;               // column groups per block
-  const long P = (M + SK_ROWS_DW - 1) / SK_ROWS_DW;
+  // FM_SK_DW_ROWS (64 / 128 / 256): rows per partial block -- fewer, longer blocks leave fewer
+  // partials for the deterministic reduce; 64 (default) measured best on the step (1.161-1.163 vs
+  // 1.164-1.170 ms, profiles/smallk_dw_rows_ab_r5sk.txt)
+  static const int rows_env = getenv("FM_SK_DW_ROWS") ? atoi(getenv("FM_SK_DW_ROWS")) : SK_ROWS_DW;
+  const int RW = rows_env == 128 || rows_env == 256 ? rows_env : SK_ROWS_DW;
+  const long P = (M + RW - 1) / RW;
   const long per = (long)(K + 1) * N;
   if (P * per * 4 > ws_bytes || P > (1L << 30)) return -1;
   const dim3 grid((unsigned)P, (unsigned)((NG + G - 1) / G));
-#define FM_SD(KK)                                                                                              \
-  case KK:                                                                                                     \
-    hipLaunchKernelGGL(fm_smallk_dw_part<KK>, grid, dim3(SK_DW_NT), 0, s, dpre, ldd, x, ldx, ws, M, N, G); \
+#define FM_SD(KK)                                                                                                   \
+  case KK:                                                                                                          \
+    if (RW == 256)                                                                                                  \
+      hipLaunchKernelGGL((fm_smallk_dw_part<KK, 256>), grid, dim3(SK_DW_NT), 0, s, dpre, ldd, x, ldx, ws, M, N, G); \
+    else if (RW == 128)                                                                                             \
+      hipLaunchKernelGGL((fm_smallk_dw_part<KK, 128>), grid, dim3(SK_DW_NT), 0, s, dpre, ldd, x, ldx, ws, M, N, G); \
+    else                                                                                                            \
+      hipLaunchKernelGGL((fm_smallk_dw_part<KK>), grid, dim3(SK_DW_NT), 0, s, dpre, ldd, x, ldx, ws, M, N, G);      \
     break;
   switch (K) {
     FM_SD(4) FM_SD(8) FM_SD(12) FM_SD(16) FM_SD(20) FM_SD(24) FM_SD(28) FM_SD(32)
