@@ -353,8 +353,11 @@ class Embedding(Op):
                     w.index_add_(0, st.rids[s][k][:n].long(), mlr * st.rg[s][k][:n * D].view(n, D))
 
     CLAIM = os.environ.get("FM_EMB_CLAIM", "1") != "0"
-    # owner-computes only when rows exceed CLAIM_RATIO x lookups per step (fewer duplicates)
-    CLAIM_RATIO = float(os.environ.get("FM_EMB_CLAIM_RATIO", "1"))
+    # owner-computes when rows exceed CLAIM_RATIO x lookups per step (few enough duplicates for the
+    # claim / dup / owner kernels to beat per-lookup atomics): 0.2 takes the 2208..7420-row MLPerf
+    # tables off the atomic kernel, 1.162-1.163 vs 1.171 ms/step at ratio 1
+    # (profiles/bench_ab_claim_ratio_r5cr.txt)
+    CLAIM_RATIO = float(os.environ.get("FM_EMB_CLAIM_RATIO", "0.2"))
     # FM_EMB_BWD=count: the count / update kernel pair (csrc/kernels/embedding.hip) for every table
     # above the tiny-table LDS kernel's 16 rows, on the same slot / flag buffers
     COUNT = os.environ.get("FM_EMB_BWD", "claim") == "count"
