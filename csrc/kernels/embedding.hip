@@ -606,6 +606,14 @@ void launch_bwd(const TabSet& s, int m, bool tiny, bool dy_bf16, const float* lr
     size_t lds = 0;
     for (int i = 0; i < m; ++i) lds = std::max(lds, (size_t)s.t[i].rows * s.t[i].D * 4 * 4);  // one copy per wave
     static const int env_chunk = getenv("FM_TINY_CHUNK") ? atoi(getenv("FM_TINY_CHUNK")) : 0;
+    static bool attr = false;
+    if (!attr) {   // > 64 KiB of dynamic LDS (FM_EMB_TINY_ROWS above 32 at D = 128) needs the opt-in
+      (void)hipFuncSetAttribute((const void*)fm_emb_bwd_tiny_multi<unsigned short, I64>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10);
+      (void)hipFuncSetAttribute((const void*)fm_emb_bwd_tiny_multi<float, I64>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10);
+      attr = true;
+    }
     // 64-sample chunks keep the per-wave chain to one round trip; at large B more blocks would
     // pile onto the same few addresses in the flush (tools/bench_embedding.py: B=8192 -> 64,
     // B=65536 -> 128..256)
@@ -1021,7 +1029,12 @@ extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const
     }
   }
   auto kind_of = [&](int k) {
-    if (rows[k] <= TINY_ROWS && D[k] <= 256 && B * (long)bag[k] >= 16L * rows[k]) return 0;
+    // FM_EMB_TINY_ROWS (A/B, default 16): the wave-private LDS kernel up to that many rows while
+    // its four copies fit the LDS (rows * D * 16 B)
+    static const int tiny_rows = getenv("FM_EMB_TINY_ROWS") ? atoi(getenv("FM_EMB_TINY_ROWS")) : TINY_ROWS;
+    if (rows[k] <= tiny_rows && (long)rows[k] * D[k] * 16 <= (160L << 10) && D[k] <= 256 &&
+        B * (long)bag[k] >= 16L * rows[k])
+      return 0;
     if (small_on && (long)rows[k] * D[k] * 4 <= SMALL_LDS && D[k] <= 256 && B * (long)bag[k] >= 8L * rows[k]) return 1;
     return 2;
   };
