@@ -1029,9 +1029,12 @@ extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const
     }
   }
   auto kind_of = [&](int k) {
-    // FM_EMB_TINY_ROWS (A/B, default 16): the wave-private LDS kernel up to that many rows while
-    // its four copies fit the LDS (rows * D * 16 B)
-    static const int tiny_rows = getenv("FM_EMB_TINY_ROWS") ? atoi(getenv("FM_EMB_TINY_ROWS")) : TINY_ROWS;
+    // FM_EMB_TINY_ROWS (default 64): the wave-private LDS kernel up to that many rows while its four
+    // copies fit the LDS (rows * D * 16 B).  64 takes the 36- and 63-row MLPerf tables off the
+    // same-address atomics: slower alone (35.5 vs 32.3 us for the eight <= 155-row tables) but less
+    // contention beside the bottom-MLP backward, step 1.145-1.164 vs 1.170-1.173 ms at 16
+    // (profiles/emb_tiny_rows_ab_r5tr.txt)
+    static const int tiny_rows = getenv("FM_EMB_TINY_ROWS") ? atoi(getenv("FM_EMB_TINY_ROWS")) : 64;
     if (rows[k] <= tiny_rows && (long)rows[k] * D[k] * 16 <= (160L << 10) && D[k] <= 256 &&
         B * (long)bag[k] >= 16L * rows[k])
       return 0;

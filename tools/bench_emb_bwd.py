@@ -51,7 +51,8 @@ def main():
         torch.cuda.synchronize()
         best = min(best, e0.elapsed_time(e1) * 1000 / reps)
     print(json.dumps({"rows": rows, "B": B, "us": round(best, 2),
-                      "rowblock": os.environ.get("FM_EMB_ROWBLOCK", "1")}), flush=True)
+                      "rowblock": os.environ.get("FM_EMB_ROWBLOCK", "0"),
+                      "tiny_rows": os.environ.get("FM_EMB_TINY_ROWS", "64")}), flush=True)
 
 
 if __name__ == "__main__":
