@@ -74,6 +74,9 @@ def parse():
                     help="N>1: skip the pure data-parallel comparison run (config.dp / config.soap_speedup_vs_dp)")
     ap.add_argument("--no-table", action="store_true",
                     help="N>1 with --strategy search: skip the hand-plan comparison run (config.table)")
+    ap.add_argument("--budget-s", type=float, default=1200.0,
+                    help="wall budget of the whole command: a comparison run whose estimated time no longer fits "
+                         "is skipped (config.<run>.skipped) instead of risking the already-measured headline")
     a = ap.parse_args()
     if a.strategy is None:
         a.strategy = "search" if a.gpus > 1 else "table"
@@ -115,33 +118,36 @@ def main():
     if torch.cuda.is_available():
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
     cuda = torch.cuda.is_available()
+    t_start = time.time()
+    # the headline first: everything after it is a comparison whose failure must not lose it
     head = run_once(a, a.dtype, comm)
-    second = None
+    runs = []
     if cuda and not a.no_secondary:
-        second = run_once(a, "bf16" if a.dtype == "fp32" else "fp32", comm)
-    table = None
+        other = "bf16" if a.dtype == "fp32" else "fp32"
+        runs.append((other, other, None))
     if world > 1 and a.strategy == "search" and not a.no_table:
         # the hand-written plan the search was seeded with (table-wise / column embeddings + DP MLPs)
-        table = run_once(a, a.dtype, comm, strategy="table")
-    dp = None
+        runs.append(("table", a.dtype, "table"))
     if world > 1 and a.strategy != "dp" and not a.no_dp:
         # the second half of the BASELINE metric: the same model, precision and batch under pure
         # data parallelism (replicated tables trained by touched-row all-gather, DP MLPs)
-        dp = run_once(a, a.dtype, comm, strategy="dp")
+        runs.append(("dp", a.dtype, "dp"))
+    extra = {name: guarded_run(a, comm, name, dt, strat, head, t_start) for name, dt, strat in runs}
     if rank == 0:
         rec = head["rec"]
-        if second is not None:
-            rec["config"][second["dtype"]] = {"value": second["rec"]["value"], "ms_per_step": second["rec"]["ms_per_step"],
-                                              "loss": second["rec"]["config"]["loss"]}
-        if table is not None:
-            rec["config"]["table"] = {"value": table["rec"]["value"], "ms_per_step": table["rec"]["ms_per_step"],
-                                      "loss": table["rec"]["config"]["loss"],
-                                      "parallelism": table["rec"]["config"]["parallelism"]}
-            rec["config"]["search_speedup_vs_table"] = round(rec["value"] / table["rec"]["value"], 3)
-        if dp is not None:
-            rec["config"]["dp"] = {"value": dp["rec"]["value"], "ms_per_step": dp["rec"]["ms_per_step"],
-                                   "loss": dp["rec"]["config"]["loss"], "parallelism": dp["rec"]["config"]["parallelism"]}
-            rec["config"]["soap_speedup_vs_dp"] = round(rec["value"] / dp["rec"]["value"], 3)
+        for name, r in extra.items():
+            if "rec" not in r:                      # skipped or failed: say why, keep the headline
+                rec["config"][name] = {k: v for k, v in r.items()}
+                continue
+            sub = {"value": r["rec"]["value"], "ms_per_step": r["rec"]["ms_per_step"], "loss": r["rec"]["config"]["loss"]}
+            if name in ("table", "dp"):
+                sub["parallelism"] = r["rec"]["config"]["parallelism"]
+            sub["hbm"] = r["rec"]["config"].get("hbm")
+            rec["config"][name] = sub
+        if "rec" in extra.get("table", {}):
+            rec["config"]["search_speedup_vs_table"] = round(rec["value"] / extra["table"]["rec"]["value"], 3)
+        if "rec" in extra.get("dp", {}):
+            rec["config"]["soap_speedup_vs_dp"] = round(rec["value"] / extra["dp"]["rec"]["value"], 3)
         elif world == 1:
             rec["config"]["soap_speedup_vs_dp"] = 1.0   # one GPU: the searched plan IS data parallel
         print(f"ELAPSED TIME = {head['el']:.4f}s, THROUGHPUT = {rec['value']:.2f} samples/s", file=sys.stderr)
@@ -160,10 +166,96 @@ def main():
             os._exit(0)
 
 
-def run_once(a, dtype, comm, strategy=None):
+class SkipRun(Exception):
+    """A comparison run every rank agreed not to start (HBM preflight or wall budget)."""
+
+
+def _agree(comm, ok: bool) -> bool:
+    """True iff ``ok`` on every rank (one tiny all-reduce; ranks that failed still take part, so a
+    failure on one rank becomes the same decision everywhere instead of a hang in the next
+    collective)."""
+    if comm.world == 1:
+        return ok
+    import torch
+    import torch.distributed as dist
+    dev = "cuda" if (torch.cuda.is_available() and comm.backend == "nccl") else "cpu"
+    t = torch.tensor([0.0 if ok else 1.0], dtype=torch.float32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item()) == 0.0
+
+
+def _min_over_ranks(comm, v: float) -> float:
+    if comm.world == 1:
+        return v
+    import torch
+    import torch.distributed as dist
+    dev = "cuda" if (torch.cuda.is_available() and comm.backend == "nccl") else "cpu"
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return float(t.item())
+
+
+def _free_bytes():
+    """Free device memory (HBM) on a GPU, available host memory on the CPU rehearsal."""
+    import torch
+    if torch.cuda.is_available():
+        return float(torch.cuda.mem_get_info()[0])
+    import psutil
+    return float(psutil.virtual_memory().available)
+
+
+def _hbm_need_bytes(model, strategies, world):
+    """Per-device memory of this plan from the simulator's memory model (csrc/sim/simulator.cc
+    Simulator::memory: activations + gradients, weights with their optimizer state, tables and
+    sparse-DP receive buffers); the max over devices."""
+    from flexmi.parallel.search import SimGraph
+    g = SimGraph(model, world, max_cands=4, extra=strategies)
+    return max(g.memory(g.assign_from(strategies)))
+
+
+def _fail_injected(name, rank):
+    """FM_BENCH_FAIL=<run>[@<rank>] (tests): raise inside the build phase of that run."""
+    spec = os.environ.get("FM_BENCH_FAIL", "")
+    for item in filter(None, spec.split(",")):
+        run, _, r = item.partition("@")
+        if run == name and (r == "" or int(r) == rank):
+            raise RuntimeError(f"injected failure in the {name} run on rank {rank} (FM_BENCH_FAIL)")
+
+
+def guarded_run(a, comm, name, dtype, strategy, head, t_start):
+    """One comparison run that cannot lose the headline: skipped (with the reason) when the wall
+    budget left cannot hold it (estimate: the headline run's wall time x 1.5 + 30 s, rank 0's
+    clock) or when its HBM preflight fails; an exception becomes ``{"error": ...}`` on every rank."""
+    est = head["wall_s"] * 1.5 + 30.0
+    left = a.budget_s - (time.time() - t_start)
+    if not _agree(comm, left >= est if comm.rank == 0 else True):
+        return {"skipped": f"wall budget: {left:.0f} s left of --budget-s {a.budget_s:.0f}, run estimated at {est:.0f} s"}
+    try:
+        return run_once(a, dtype, comm, strategy=strategy, name=name)
+    except SkipRun as e:
+        return {"skipped": str(e)}
+    except Exception as e:   # noqa: BLE001 -- reported in the record, the headline survives
+        import traceback
+        traceback.print_exc(file=sys.stderr)
+        _release_memory()
+        return {"error": f"{type(e).__name__}: {e}"[:400]}
+
+
+def _release_memory():
+    import gc
+    import torch
+    gc.collect()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+
+
+def run_once(a, dtype, comm, strategy=None, name="head"):
     """Build, warm up and time one DLRM training configuration in compute precision ``dtype``
     under ``strategy`` (default ``--strategy``); frees the model before returning (the tables of
-    two configurations never coexist)."""
+    two configurations never coexist).  The build phase (model, plan, compile, HBM preflight) ends
+    in an all-rank agreement: a failure or a failed preflight on any rank stops the run on every
+    rank before its first collective."""
     strategy = strategy or a.strategy
     import gc
     import torch
@@ -171,6 +263,41 @@ def run_once(a, dtype, comm, strategy=None):
     rank, world = comm.rank, comm.world
     from flexmi.core import FFConfig, FFModel, SGDOptimizer, LossType, MetricsType
     from flexmi.models.dlrm import DLRMConfig, build_dlrm, dlrm_strategy, SyntheticDLRMData
+
+    t_run = time.time()
+    err = None
+    try:
+        _fail_injected(name, rank)
+        model, cfg, dcfg, dense_in, sparse, strategies, search = _build(a, dtype, comm, strategy)
+        need = _hbm_need_bytes(model, strategies, world)
+    except Exception as e:   # noqa: BLE001 -- re-raised below, after every rank has heard of it
+        err = e
+    if not _agree(comm, err is None):
+        if err is not None:
+            raise err
+        raise RuntimeError(f"the {name} run failed to build on another rank")
+    free = _min_over_ranks(comm, _free_bytes())
+    hbm = {"need_gb": round(need / 1e9, 3), "free_gb": round(free / 1e9, 3)}
+    if need > 0.92 * free and name != "head":
+        model = None
+        _release_memory()
+        raise SkipRun(f"HBM preflight: the plan needs {hbm['need_gb']} GB per device, {hbm['free_gb']} GB free")
+    cuda = torch.cuda.is_available()
+    sync = torch.cuda.synchronize if cuda else (lambda: None)   # CPU (gloo) rehearsal runs too
+    t0 = time.time()
+    ex = model.init_layers()
+    sync()
+    t_init = time.time() - t0
+    return _timed(a, comm, model, cfg, dcfg, dense_in, sparse, strategy, search, ex, t_init, hbm, t_run)
+
+
+def _build(a, dtype, comm, strategy):
+    """The model, its plan and the compiled graph (no device memory beyond the model objects)."""
+    import torch
+    import torch.distributed as dist
+    rank, world = comm.rank, comm.world
+    from flexmi.core import FFConfig, FFModel, SGDOptimizer, LossType, MetricsType
+    from flexmi.models.dlrm import DLRMConfig, build_dlrm, dlrm_strategy
 
     dcfg = DLRMConfig.preset(a.config)
     if a.table_scale != 1.0:
@@ -206,12 +333,18 @@ def run_once(a, dtype, comm, strategy=None):
     loss = LossType.LOSS_BINARY_CROSSENTROPY if dcfg.loss == "bce" else LossType.LOSS_MEAN_SQUARED_ERROR_AVG_REDUCE
     model.compile(SGDOptimizer(model, 0.01), loss, [MetricsType.METRICS_ACCURACY, MetricsType.METRICS_MEAN_SQUARED_ERROR])
     model.strategies = strategies
+    return model, cfg, dcfg, dense_in, sparse, strategies, search
+
+
+def _timed(a, comm, model, cfg, dcfg, dense_in, sparse, strategy, search, ex, t_init, hbm, t_run):
+    """Warm-up and the timed K steps of a built model; returns the record and frees the model."""
+    import gc
+    import torch
+    import torch.distributed as dist
+    from flexmi.models.dlrm import SyntheticDLRMData
+    rank, world = comm.rank, comm.world
     cuda = torch.cuda.is_available()
-    sync = torch.cuda.synchronize if cuda else (lambda: None)   # CPU (gloo) rehearsal runs too
-    t0 = time.time()
-    ex = model.init_layers()
-    sync()
-    t_init = time.time() - t0
+    sync = torch.cuda.synchronize if cuda else (lambda: None)
     data = SyntheticDLRMData(model, dense_in, sparse, dcfg, num_batches=4, seed=rank)
 
     use_graph = (not a.no_graph) and torch.cuda.is_available() and not a.profile
@@ -318,6 +451,7 @@ def run_once(a, dtype, comm, strategy=None):
             "backend": comm.backend if world > 1 else "none",
             "rccl_world": dist.get_world_size() if (world > 1 and comm.backend == "nccl") else None,
             "process_world": world,
+            "hbm": hbm,
         },
     }
     if cuda and cfg.compute_dtype == "fp32":
@@ -331,7 +465,7 @@ def run_once(a, dtype, comm, strategy=None):
         rec["config"]["search"] = dict(search)
     if rank == 0 and a.profile:
         ex.timer.print_summary(file=sys.stderr)
-    out = {"rec": rec, "el": el, "dtype": cfg.compute_dtype}
+    out = {"rec": rec, "el": el, "dtype": cfg.compute_dtype, "wall_s": time.time() - t_run}
     # release this configuration's device memory before the next one is built
     ex.release()
     ex = model = data = step = run_step = stage = None

@@ -34,6 +34,16 @@ int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, const float* B
                 float* C, long ldc, long sC, const float* bias, int M, int N, int K, int batch, float alpha, int beta,
                 int act, float* ws, long ws_bytes, int ksplit_req, const float* act_y, long lday, int bwd_act,
                 float* colsum, float* rowsum_a, hipStream_t stream);
+int fm_gemm_f32_pl(const float* A, long lda, long sA, int a_kcontig, const float* B, long ldb, long sB, int b_kcontig,
+                   float* C, long ldc, long sC, const float* bias, int M, int N, int K, int batch, float alpha, int beta,
+                   int act, float* ws, long ws_bytes, int ksplit_req, const float* act_y, long lday, int bwd_act,
+                   float* colsum, float* rowsum_a, const unsigned short* Ap, long psa, const unsigned short* Bp, long psb,
+                   unsigned short* Cp, long psc, hipStream_t stream);
+int fm_gemm_f32_dw_sgd_pl(const float* A, long lda, const float* B, long ldb, float* W, long ldw, unsigned short* Wc,
+                          float* V, const float* lr, float wd, float mom, int nesterov, int M, int N, int K, float* ws,
+                          long ws_bytes, float* rowsum_a, const unsigned short* Ap, long psa, const unsigned short* Bp,
+                          long psb, hipStream_t stream);
+void fm_split3(const float* src, long rows, int cols, long lds, unsigned short* dst, long ldd, long ps, hipStream_t s);
 int fm_smallk_fwd_f32_launch(const float* x, long ldx, const float* w, const float* bias, float* y, long ldy, long M,
                              int K, int N, int act, hipStream_t s);
 int fm_smallk_dw_f32_launch(const float* dpre, long ldd, const float* x, long ldx, float* dw, float* db, long M, int K,
@@ -180,7 +190,8 @@ int gemm(torch::Tensor A, int64_t lda, int64_t sA, bool a_kcontig, torch::Tensor
          torch::Tensor C, int64_t ldc, int64_t sC, c10::optional<torch::Tensor> bias, int64_t M, int64_t N, int64_t K,
          int64_t batch, double alpha, bool beta, int64_t act, c10::optional<torch::Tensor> ws, int64_t ksplit,
          c10::optional<torch::Tensor> act_y, int64_t lday, int64_t bwd_act, c10::optional<torch::Tensor> colsum,
-         c10::optional<torch::Tensor> rowsum_a, bool async_reduce) {
+         c10::optional<torch::Tensor> rowsum_a, bool async_reduce, c10::optional<torch::Tensor> ap,
+         c10::optional<torch::Tensor> bp, c10::optional<torch::Tensor> cp) {
   check_cuda(A, "A");
   check_cuda(B, "B");
   check_cuda(C, "C");
@@ -224,11 +235,26 @@ int gemm(torch::Tensor A, int64_t lda, int64_t sA, bool a_kcontig, torch::Tensor
   // caller joins (gemm_join) before anything reads C
   fm_gemm_async_arm(async_reduce ? 1 : 0);
   int ks;
+  // exact bf16 planes (gemm_pl.hip): [3, rows, ld] bf16 with the fp32 tensor's storage extent
+  // (plane stride = numel / 3), element (r, c) of plane p at p * ps + the fp32 offset
+  auto plane = [&](const c10::optional<torch::Tensor>& t, const torch::Tensor& like, const char* name) -> long {
+    if (!(t.has_value() && t->defined())) return 0;
+    TORCH_CHECK(f32 && t->is_cuda() && t->scalar_type() == torch::kBFloat16 && t->is_contiguous() && t->numel() % 3 == 0 &&
+                    t->numel() / 3 >= like.numel() - like.storage_offset() + like.storage_offset(),
+                "gemm ", name, ": bf16 planes [3, ...] covering the fp32 operand");
+    return t->numel() / 3;
+  };
+  const long psa = plane(ap, A, "ap"), psb = plane(bp, B, "bp"), psc = plane(cp, C, "cp");
+  if (psa) TORCH_CHECK(lastA + (batch - 1) * sA < psa, "gemm ap: planes smaller than A");
+  if (psb) TORCH_CHECK(lastB + (batch - 1) * sB < psb, "gemm bp: planes smaller than B");
+  if (psc) TORCH_CHECK((M - 1) * ldc + (N - 1) + (batch - 1) * sC < psc, "gemm cp: planes smaller than C");
   if (f32)
-    ks = fm_gemm_f32(A.data_ptr<float>(), lda, sA, a_kcontig, B.data_ptr<float>(), ldb, sB, b_kcontig, C.data_ptr<float>(),
-                     ldc, sC, bias.has_value() && bias->defined() ? bias->data_ptr<float>() : nullptr, (int)M, (int)N,
-                     (int)K, (int)batch, (float)alpha, beta ? 1 : 0, (int)act, w, wsb, (int)ksplit,
-                     (const float*)cptr(act_y), lday, (int)bwd_act, (float*)mptr(colsum), (float*)mptr(rowsum_a), cur());
+    ks = fm_gemm_f32_pl(A.data_ptr<float>(), lda, sA, a_kcontig, B.data_ptr<float>(), ldb, sB, b_kcontig, C.data_ptr<float>(),
+                        ldc, sC, bias.has_value() && bias->defined() ? bias->data_ptr<float>() : nullptr, (int)M, (int)N,
+                        (int)K, (int)batch, (float)alpha, beta ? 1 : 0, (int)act, w, wsb, (int)ksplit,
+                        (const float*)cptr(act_y), lday, (int)bwd_act, (float*)mptr(colsum), (float*)mptr(rowsum_a),
+                        (const unsigned short*)cptr(ap), psa, (const unsigned short*)cptr(bp), psb,
+                        (unsigned short*)mptr(cp), psc, cur());
   else
     ks = fm_gemm(A.data_ptr(), lda, sA, a_kcontig, B.data_ptr(), ldb, sB, b_kcontig, C.data_ptr(), ldc, sC,
                  C.scalar_type() == torch::kFloat32, bias.has_value() && bias->defined() ? bias->data_ptr<float>() : nullptr,
@@ -239,6 +265,18 @@ int gemm(torch::Tensor A, int64_t lda, int64_t sA, bool a_kcontig, torch::Tensor
 }
 
 void gemm_join() { fm_gemm_join(cur()); }
+
+// exact three-way bf16 split of an fp32 matrix (rows x cols, leading dim src.stride(0)) into planes
+// [3, rows, ld] (ld = dst.size(2)); element (r, c) of plane p at p * rows * ld + r * ld + c
+void split_planes(torch::Tensor src, torch::Tensor dst) {
+  TORCH_CHECK(src.is_cuda() && src.scalar_type() == torch::kFloat32 && src.dim() == 2 && src.stride(1) == 1,
+              "split_planes: fp32 [rows, cols] with unit column stride");
+  TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == torch::kBFloat16 && dst.is_contiguous() && dst.dim() == 3 &&
+                  dst.size(0) == 3 && dst.size(1) >= src.size(0) && dst.size(2) >= src.size(1),
+              "split_planes: bf16 [3, >= rows, >= cols] destination");
+  fm_split3(src.data_ptr<float>(), src.size(0), (int)src.size(1), src.stride(0), (unsigned short*)dst.data_ptr(),
+            dst.size(2), dst.size(1) * dst.size(2), cur());
+}
 
 // fm_sgd over disjoint [off, off + len) ranges of one flat master / grad / state / mirror set
 void sgd_segs(torch::Tensor W, torch::Tensor G, c10::optional<torch::Tensor> V, c10::optional<torch::Tensor> Wc,
@@ -267,7 +305,8 @@ void sgd_segs(torch::Tensor W, torch::Tensor G, c10::optional<torch::Tensor> V, 
 // computes the gradient and runs the optimizer kernel itself).
 int gemm_dw_sgd(torch::Tensor dpre, torch::Tensor x, torch::Tensor W, c10::optional<torch::Tensor> Wc,
                 c10::optional<torch::Tensor> V, torch::Tensor lr, double wd, double mom, bool nesterov,
-                c10::optional<torch::Tensor> db, torch::Tensor ws) {
+                c10::optional<torch::Tensor> db, torch::Tensor ws, c10::optional<torch::Tensor> dp,
+                c10::optional<torch::Tensor> xp) {
   check_cuda(dpre, "dpre");
   check_cuda(x, "x");
   check_cuda(W, "W");
@@ -286,11 +325,26 @@ int gemm_dw_sgd(torch::Tensor dpre, torch::Tensor x, torch::Tensor W, c10::optio
   if (db.has_value() && db->defined())
     TORCH_CHECK(db->scalar_type() == torch::kFloat32 && db->numel() >= Nout, "gemm_dw_sgd: db fp32 [out]");
   TORCH_CHECK((B - 1) * dpre.stride(0) + Nout <= dpre.numel() && (B - 1) * x.stride(0) + Kin <= x.numel(), "gemm_dw_sgd: extents");
+  long psa = 0, psb = 0;
+  for (auto* t : {&dp, &xp}) {
+    if (t->has_value() && (*t)->defined())
+      TORCH_CHECK(f32 && (*t)->is_cuda() && (*t)->scalar_type() == torch::kBFloat16 && (*t)->is_contiguous() &&
+                      (*t)->numel() % 3 == 0, "gemm_dw_sgd: bf16 planes [3, ...]");
+  }
+  if (dp.has_value() && dp->defined()) {
+    psa = dp->numel() / 3;
+    TORCH_CHECK((B - 1) * dpre.stride(0) + Nout <= psa, "gemm_dw_sgd: dpre planes too small");
+  }
+  if (xp.has_value() && xp->defined()) {
+    psb = xp->numel() / 3;
+    TORCH_CHECK((B - 1) * x.stride(0) + Kin <= psb, "gemm_dw_sgd: x planes too small");
+  }
   if (f32)
-    return fm_gemm_f32_dw_sgd(dpre.data_ptr<float>(), dpre.stride(0), x.data_ptr<float>(), x.stride(0), W.data_ptr<float>(),
-                              Kin, (unsigned short*)mptr(Wc), (float*)mptr(V), lr.data_ptr<float>(), (float)wd,
-                              (float)mom, nesterov ? 1 : 0, (int)Nout, (int)Kin, (int)B, ws.data_ptr<float>(),
-                              ws.numel() * 4, (float*)mptr(db), cur());
+    return fm_gemm_f32_dw_sgd_pl(dpre.data_ptr<float>(), dpre.stride(0), x.data_ptr<float>(), x.stride(0),
+                                 W.data_ptr<float>(), Kin, (unsigned short*)mptr(Wc), (float*)mptr(V), lr.data_ptr<float>(),
+                                 (float)wd, (float)mom, nesterov ? 1 : 0, (int)Nout, (int)Kin, (int)B, ws.data_ptr<float>(),
+                                 ws.numel() * 4, (float*)mptr(db), (const unsigned short*)cptr(dp), psa,
+                                 (const unsigned short*)cptr(xp), psb, cur());
   return fm_gemm_dw_sgd(dpre.data_ptr(), dpre.stride(0), x.data_ptr(), x.stride(0), W.data_ptr<float>(), Kin,
                         (unsigned short*)mptr(Wc), (float*)mptr(V), lr.data_ptr<float>(), (float)wd, (float)mom,
                         nesterov ? 1 : 0, (int)Nout, (int)Kin, (int)B, ws.data_ptr<float>(), ws.numel() * 4,
@@ -1216,9 +1270,16 @@ void lstm_cell_bwd(torch::Tensor A, int64_t a_off, int64_t lda, torch::Tensor ct
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "flexmi HIP/CDNA4 kernels (gfx950)";
-  m.def("gemm", &gemm);
+  m.def("gemm", &gemm, py::arg("A"), py::arg("lda"), py::arg("sA"), py::arg("a_kcontig"), py::arg("B"), py::arg("ldb"),
+        py::arg("sB"), py::arg("b_kcontig"), py::arg("C"), py::arg("ldc"), py::arg("sC"), py::arg("bias"), py::arg("M"),
+        py::arg("N"), py::arg("K"), py::arg("batch"), py::arg("alpha"), py::arg("beta"), py::arg("act"), py::arg("ws"),
+        py::arg("ksplit"), py::arg("act_y"), py::arg("lday"), py::arg("bwd_act"), py::arg("colsum"), py::arg("rowsum_a"),
+        py::arg("async_reduce"), py::arg("ap") = py::none(), py::arg("bp") = py::none(), py::arg("cp") = py::none());
   m.def("gemm_join", &gemm_join);
-  m.def("gemm_dw_sgd", &gemm_dw_sgd);
+  m.def("split_planes", &split_planes);
+  m.def("gemm_dw_sgd", &gemm_dw_sgd, py::arg("dpre"), py::arg("x"), py::arg("W"), py::arg("Wc"), py::arg("V"),
+        py::arg("lr"), py::arg("wd"), py::arg("mom"), py::arg("nesterov"), py::arg("db"), py::arg("ws"),
+        py::arg("dp") = py::none(), py::arg("xp") = py::none());
   m.def("sgd_segs", &sgd_segs);
   m.def("gemm_set_variant", [](int v) { fm_gemm_set_variant(v); });
   m.def("gemm_f32_set_variant", [](int v) { fm_gemm_f32_set_variant(v); });

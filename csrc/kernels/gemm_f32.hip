@@ -195,6 +195,10 @@ __global__ void fm_gemm_f32_reduce(GemmF p, int v4) {
       for (int r = 0; r < 4; ++r) s[r] = act_fwd(p.act, s[r] * p.alpha + (p.bias ? p.bias[n + r] : 0.f));
       if (p.beta) s += *reinterpret_cast<const f32x4_t*>(d);
       *reinterpret_cast<f32x4_t*>(d) = s;
+      if (p.Cp) {
+        const float fo[4] = {s[0], s[1], s[2], s[3]};
+        store_planes4(p.Cp, p.psc, zb * p.sC + (long)m * p.ldc + n, fo);
+      }
     } else {
       float s = slab_sum1(src, MN, p.ksplit);
       if constexpr (SGD) {
@@ -203,6 +207,7 @@ __global__ void fm_gemm_f32_reduce(GemmF p, int v4) {
       }
       s = act_fwd(p.act, s * p.alpha + (p.bias ? p.bias[n] : 0.f));
       *d = s + (p.beta ? *d : 0.f);
+      if (p.Cp) store_planes1(p.Cp, p.psc, zb * p.sC + (long)m * p.ldc + n, *d);
     }
   }
 }
@@ -506,6 +511,7 @@ __global__ void __launch_bounds__(256) fm_gemm_f32_reduce_bwd(GemmF p, int RB) {
       if (p.ay) v = act_bwd(p.bact, p.ay[(long)m * p.lday + n + r], v);
       cs[r] += v;
       d[r] = v + (p.beta ? d[r] : 0.f);
+      if (p.Cp) store_planes1(p.Cp, p.psc, (long)m * p.ldc + n + r, d[r]);
     }
   }
   if (p.colsum) {
@@ -519,6 +525,8 @@ __global__ void __launch_bounds__(256) fm_gemm_f32_reduce_bwd(GemmF p, int RB) {
 
 // the split-bf16 kernel, second form (gemm_x3.hip)
 extern "C" int fm_gemm_x3v2_launch(const void* params, int bm, int a_kcontig, int b_kcontig, int sgd, hipStream_t s);
+// the pre-split plane kernel (gemm_pl.hip)
+extern "C" int fm_gemm_pl3_launch(const void* params, int bm, int a_kcontig, int b_kcontig, int sgd, hipStream_t s);
 // the ring-form kernel (gemm_f32_ring.hip)
 extern "C" int fm_gemm_f32_ring_cfg(int c, int* geo);
 extern "C" void fm_gemm_f32_ring_launch(const void* params, int c, int a_kcontig, int b_kcontig, int sgd,
@@ -1107,6 +1115,26 @@ void launch_x_cfg(int c, const GemmF& p, bool ak, bool bk, hipStream_t s) {
 
 }  // namespace
 
+// Tile and split-K depth of the plane kernel: 256x128 (8 waves) when those tiles cover >= 3/4 of the
+// 256 CUs, else 128x128 (4 waves, 3-stage ring); K split until the grid reaches one block per CU
+// (a fused backward epilogue needs the whole sum).  FM_PL_BM / FM_PL_KS force them (lab A/B).
+static void pl3_choose(int M, int N, int K, bool fused, int ksplit_req, const float* ws, long ws_bytes, int& bm, int& ks) {
+  static const int bm_env = getenv("FM_PL_BM") ? atoi(getenv("FM_PL_BM")) : 0;
+  static const int ks_env = getenv("FM_PL_KS") ? atoi(getenv("FM_PL_KS")) : 0;
+  const long t256 = (long)((M + 255) / 256) * ((N + 127) / 128);
+  bm = (bm_env == 128 || bm_env == 256) ? bm_env : (t256 >= 192 ? 256 : 128);
+  const long tiles = (long)((M + bm - 1) / bm) * ((N + 127) / 128);
+  const int ktiles = K / 32;
+  ks = 1;
+  if (ksplit_req > 0) ks = ksplit_req;
+  else if (ks_env > 0) ks = ks_env;
+  else if (ws != nullptr)
+    while (tiles * ks < 256 && ks * 2 <= ktiles / 4 && ks < 16) ks *= 2;
+  if (fused) ks = 1;
+  while (ks > 1 && (ws == nullptr || (long)ks * M * (long)N * 4 > ws_bytes)) ks /= 2;
+  if (ks > ktiles) ks = ktiles > 0 ? ktiles : 1;
+}
+
 static int g_f32_variant = getenv("FM_GEMM_F32_VARIANT") ? atoi(getenv("FM_GEMM_F32_VARIANT")) : 0;
 extern "C" void fm_gemm_f32_set_variant(int v) { g_f32_variant = v; }
 
@@ -1127,17 +1155,38 @@ struct SgdUpdF {
   float* w; unsigned short* wc; float* v; const float* lr; float wd, mom; int nest;
 };
 
+struct PlanesF {
+  const unsigned short* a; long psa;
+  const unsigned short* b; long psb;
+  unsigned short* c; long psc;
+};
+
 static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const float* B, long ldb, long sB,
                         int b_kcontig, float* C, long ldc, long sC, const float* bias, int M, int N, int K, int batch,
                         float alpha, int beta, int act, float* ws, long ws_bytes, int ksplit_req, const float* act_y,
-                        long lday, int bwd_act, float* colsum, float* rowsum_a, const SgdUpdF* upd, hipStream_t stream);
+                        long lday, int bwd_act, float* colsum, float* rowsum_a, const SgdUpdF* upd, const PlanesF* pl,
+                        hipStream_t stream);
 
 extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, const float* B, long ldb, long sB,
                            int b_kcontig, float* C, long ldc, long sC, const float* bias, int M, int N, int K, int batch,
                            float alpha, int beta, int act, float* ws, long ws_bytes, int ksplit_req, const float* act_y,
                            long lday, int bwd_act, float* colsum, float* rowsum_a, hipStream_t stream) {
   return gemm_f32_run(A, lda, sA, a_kcontig, B, ldb, sB, b_kcontig, C, ldc, sC, bias, M, N, K, batch, alpha, beta, act, ws,
-                      ws_bytes, ksplit_req, act_y, lday, bwd_act, colsum, rowsum_a, nullptr, stream);
+                      ws_bytes, ksplit_req, act_y, lday, bwd_act, colsum, rowsum_a, nullptr, nullptr, stream);
+}
+
+// fm_gemm_f32 with exact bf16 operand planes (gemm_pl.hip): Ap / Bp (or nullptr) are the planes of
+// A / B with A's / B's leading dims, plane p at base + p * ps; Cp (or nullptr) receives the planes
+// of the stored C (C's leading dim, plane stride psc).  With both operand planes the plane kernel
+// runs wherever its shape constraints hold (else the fp32 kernels, which still emit Cp).
+extern "C" int fm_gemm_f32_pl(const float* A, long lda, long sA, int a_kcontig, const float* B, long ldb, long sB,
+                              int b_kcontig, float* C, long ldc, long sC, const float* bias, int M, int N, int K, int batch,
+                              float alpha, int beta, int act, float* ws, long ws_bytes, int ksplit_req, const float* act_y,
+                              long lday, int bwd_act, float* colsum, float* rowsum_a, const unsigned short* Ap, long psa,
+                              const unsigned short* Bp, long psb, unsigned short* Cp, long psc, hipStream_t stream) {
+  PlanesF pl{Ap, psa, Bp, psb, Cp, psc};
+  return gemm_f32_run(A, lda, sA, a_kcontig, B, ldb, sB, b_kcontig, C, ldc, sC, bias, M, N, K, batch, alpha, beta, act, ws,
+                      ws_bytes, ksplit_req, act_y, lday, bwd_act, colsum, rowsum_a, nullptr, &pl, stream);
 }
 
 // fp32 weight-gradient GEMM with the SGD update fused in (same contract as gemm.hip fm_gemm_dw_sgd):
@@ -1149,13 +1198,26 @@ extern "C" int fm_gemm_f32_dw_sgd(const float* A, long lda, const float* B, long
                                   int M, int N, int K, float* ws, long ws_bytes, float* rowsum_a, hipStream_t stream) {
   SgdUpdF u{W, Wc, V, lr, wd, mom, nesterov};
   return gemm_f32_run(A, lda, 0, 0, B, ldb, 0, 0, W, ldw, 0, nullptr, M, N, K, 1, 1.f, 0, 10, ws, ws_bytes, 0, nullptr, 0,
-                      10, nullptr, rowsum_a, &u, stream);
+                      10, nullptr, rowsum_a, &u, nullptr, stream);
+}
+
+// fm_gemm_f32_dw_sgd with the operand planes of dpre (Ap) and x (Bp), see fm_gemm_f32_pl
+extern "C" int fm_gemm_f32_dw_sgd_pl(const float* A, long lda, const float* B, long ldb, float* W, long ldw,
+                                     unsigned short* Wc, float* V, const float* lr, float wd, float mom, int nesterov,
+                                     int M, int N, int K, float* ws, long ws_bytes, float* rowsum_a,
+                                     const unsigned short* Ap, long psa, const unsigned short* Bp, long psb,
+                                     hipStream_t stream) {
+  SgdUpdF u{W, Wc, V, lr, wd, mom, nesterov};
+  PlanesF pl{Ap, psa, Bp, psb, nullptr, 0};
+  return gemm_f32_run(A, lda, 0, 0, B, ldb, 0, 0, W, ldw, 0, nullptr, M, N, K, 1, 1.f, 0, 10, ws, ws_bytes, 0, nullptr, 0,
+                      10, nullptr, rowsum_a, &u, &pl, stream);
 }
 
 static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const float* B, long ldb, long sB,
                         int b_kcontig, float* C, long ldc, long sC, const float* bias, int M, int N, int K, int batch,
                         float alpha, int beta, int act, float* ws, long ws_bytes, int ksplit_req, const float* act_y,
-                        long lday, int bwd_act, float* colsum, float* rowsum_a, const SgdUpdF* upd, hipStream_t stream) {
+                        long lday, int bwd_act, float* colsum, float* rowsum_a, const SgdUpdF* upd, const PlanesF* pl,
+                        hipStream_t stream) {
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
   if (upd && (K <= 0 || ldc % 4 != 0 || (((uintptr_t)upd->w | (uintptr_t)(upd->v ? upd->v : upd->w)) & 15) ||
               (((uintptr_t)(upd->wc ? (void*)upd->wc : (void*)upd->w)) & 7)))
@@ -1177,7 +1239,36 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
   p.unest = upd ? upd->nest : 0;
   static const bool sgd_direct = getenv("FM_SGD_EPI_DIRECT") != nullptr && atoi(getenv("FM_SGD_EPI_DIRECT")) == 1;
   p.ulds = upd && !sgd_direct;
+  p.Ap = pl ? pl->a : nullptr;
+  p.psa = pl ? pl->psa : 0;
+  p.Bp = pl ? pl->b : nullptr;
+  p.psb = pl ? pl->psb : 0;
+  p.Cp = (pl && !upd) ? pl->c : nullptr;
+  p.psc = pl ? pl->psc : 0;
+  static const int pvar_env = getenv("FM_PL_VAR") ? atoi(getenv("FM_PL_VAR")) : 0;
+  p.pvar = pvar_env;
   auto al = [](const void* q) { return (((uintptr_t)q) & 15) == 0; };
+  // pre-split operands (gemm_pl.hip): the plane kernel whenever both operand planes are given and
+  // the shape fits it (FM_F32_PLANES=0 disables it for A/B)
+  static const bool planes_on = getenv("FM_F32_PLANES") == nullptr || atoi(getenv("FM_F32_PLANES")) != 0;
+  if (planes_on && p.Ap && p.Bp && batch == 1 && K > 0 && K % 32 == 0 && M >= 64 && N >= 64 && al(p.Ap) && al(p.Bp) &&
+      lda % 8 == 0 && ldb % 8 == 0 && p.psa % 8 == 0 && p.psb % 8 == 0 && (a_kcontig || M % 8 == 0) &&
+      (b_kcontig || N % 8 == 0)) {
+    int bm = 0, ks = 0;
+    pl3_choose(M, N, K, act_y != nullptr || colsum != nullptr, ksplit_req, ws, ws_bytes, bm, ks);
+    p.tiles_m = (M + bm - 1) / bm;
+    p.tiles_n = (N + 127) / 128;
+    p.ksplit = ks;
+    if (ks > 1) fm_gemm_join(stream);
+    if (fm_gemm_pl3_launch(&p, bm, a_kcontig, b_kcontig, upd != nullptr && ks == 1, stream) == 0) {
+      if (ks > 1) {
+        const int v4 = (N % 4 == 0) && (ldc % 4 == 0) && (sC % 4 == 0) && al(C);
+        const long total = (long)M * N * batch / (v4 ? 4 : 1);
+        launch_reduce_f32(p, v4, total, stream);
+      }
+      return ks;
+    }
+  }
   bool vec = al(A) && al(B) && (lda % 4 == 0) && (ldb % 4 == 0) && (sA % 4 == 0) && (sB % 4 == 0);
   vec = vec && (a_kcontig ? (K % 4 == 0) : (M % 4 == 0)) && (b_kcontig ? (K % 4 == 0) : (N % 4 == 0));
   // variant knob (tools/bench_gemm.py A/B): 1 = the LDS-DMA kernel where it applies, 2 = its

@@ -7,6 +7,7 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -21,6 +22,24 @@ constexpr uint32_t kReady = 0x464d4843u;   // "FMHC"
 constexpr auto kTimeout = std::chrono::seconds(60);
 
 void fail(const std::string& what) { throw std::runtime_error("host comm: " + what); }
+
+// Session token shared by every rank of one run and (almost surely) different between runs: FNV-1a
+// of FM_RUN_ID, else the torch.distributed launcher's TORCHELASTIC_RUN_ID + MASTER_PORT; 0 when
+// none is set (then only world / slot size / the unlink by rank 0 guard against a stale region).
+uint64_t session_token() {
+  std::string key;
+  for (const char* v : {"FM_RUN_ID", "TORCHELASTIC_RUN_ID", "MASTER_PORT"}) {
+    const char* e = std::getenv(v);
+    if (e) {
+      key += e;
+      key += '|';
+    }
+  }
+  if (key.empty()) return 0;
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : key) h = (h ^ c) * 1099511628211ull;
+  return h;
+}
 }  // namespace
 
 HostComm::HostComm(const std::string& dir, int rank, int world, size_t slot_bytes)
@@ -30,9 +49,12 @@ HostComm::HostComm(const std::string& dir, int rank, int world, size_t slot_byte
   if (slot_bytes_ == 0) slot_bytes_ = 256;
   path_ = dir + "/host_comm.shm";
   map_bytes_ = header_bytes_ + (size_t)world * slot_bytes_;
+  const uint64_t token = session_token();
   if (rank == 0) {
-    // initialise under a temporary name, then rename: peers never map a half-built region (or a
-    // stale one from an earlier run: that name is replaced atomically)
+    // a region left by a crashed run goes first, then initialise under a temporary name and
+    // rename: peers never map a half-built region; the session token in the header keeps a peer
+    // that raced ahead of this unlink from accepting a stale region of the same world / slot size
+    ::unlink(path_.c_str());
     const std::string tmp = path_ + ".tmp";
     fd_ = ::open(tmp.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0600);
     if (fd_ < 0) fail("create " + tmp);
@@ -45,6 +67,7 @@ HostComm::HostComm(const std::string& dir, int rank, int world, size_t slot_byte
     hdr_->generation.store(0);
     hdr_->world = (uint32_t)world;
     hdr_->slot_bytes = slot_bytes_;
+    hdr_->token = token;
     hdr_->ready.store(kReady, std::memory_order_release);
     if (::rename(tmp.c_str(), path_.c_str()) != 0) fail("publish " + path_);
   } else {
@@ -58,7 +81,7 @@ HostComm::HostComm(const std::string& dir, int rank, int world, size_t slot_byte
           if (p != MAP_FAILED) {
             auto* h = reinterpret_cast<Header*>(p);
             if (h->ready.load(std::memory_order_acquire) == kReady && h->world == (uint32_t)world &&
-                h->slot_bytes == slot_bytes_ && (size_t)st.st_size == map_bytes_) {
+                h->slot_bytes == slot_bytes_ && h->token == token && (size_t)st.st_size == map_bytes_) {
               base_ = static_cast<char*>(p);
               hdr_ = h;
               break;

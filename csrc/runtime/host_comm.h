@@ -43,6 +43,7 @@ class HostComm {
     std::atomic<uint32_t> generation;
     uint32_t world;
     uint64_t slot_bytes;
+    uint64_t token;      // per-run session token (session_token()): a stale region never matches
   };
   char* slot(int r) const { return base_ + header_bytes_ + (size_t)r * slot_bytes_; }
 

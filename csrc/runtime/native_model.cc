@@ -453,8 +453,19 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
     xs += xcount_send_[p];
     xr += xcount_recv_[p];
   }
-  // engine + buffers
-  const size_t slot = std::max<size_t>((size_t)std::max(xs, xr) * 4 + 4096, 4u << 20);
+  // engine + buffers.  The host communicator's slot size must be the SAME on every rank (rank 0
+  // publishes it, peers require an exact match, and the chunk strides of all_reduce_sum /
+  // all_to_all depend on it), so it is sized from global quantities every rank derives from the
+  // deterministic placement: the largest send total of any rank (world * Bl * the D of the tables
+  // it owns) and the receive total (Bl * the D of every table, the same for all ranks).
+  int64_t xmax = xr;
+  {
+    std::vector<int64_t> own(world_, 0);
+    for (const Emb& e : embs_)
+      if (e.owner >= 0 && e.owner < world_) own[e.owner] += (int64_t)world_ * Bl_ * e.D;
+    for (int64_t v : own) xmax = std::max(xmax, v);
+  }
+  const size_t slot = std::max<size_t>((size_t)std::max<int64_t>(xmax, std::max(xs, xr)) * 4 + 4096, 4u << 20);
   eng_ = device_ == 1 ? make_hip_engine(rank_, world_, rendezvous_) : make_cpu_engine(rank_, world_, rendezvous_, slot);
   params_ = (float*)eng_->alloc(wplan_.numel * 4);
   grads_ = (float*)eng_->alloc(wplan_.numel * 4);

@@ -61,15 +61,28 @@ GEMM_WS_BYTES = 64 << 20
 
 def gemm(A, lda, a_kcontig, B, ldb, b_kcontig, Cout, ldc, M, N, K, bias=None, act=10, beta=False, alpha=1.0,
          batch=1, sA=0, sB=0, sC=0, ksplit=0, use_ws=True, act_y=None, bwd_act=10, colsum=None, rowsum_a=None,
-         async_reduce=False):
+         async_reduce=False, ap=None, bp=None, cp=None):
     """C = epi(A·B).  Optional fused backward epilogue of the layer below (act_y/bwd_act/colsum):
     C = act'(act_y) * (A·B) and colsum += column sums of C (its bias gradient).  async_reduce: a
     split-K reduce may run on a side stream (csrc/kernels/gemm_async.hip) -- the caller must
-    gemm_join() before anything reads Cout."""
+    gemm_join() before anything reads Cout.  fp32 only: ap / bp = exact bf16 planes of A / B
+    (:func:`planes_like`; the pre-split kernel csrc/kernels/gemm_pl.hip), cp = planes to write for C."""
     ws = workspace(Cout.device, GEMM_WS_BYTES) if use_ws else None
     lday = act_y.stride(0) if act_y is not None else 0
     return C().gemm(A, lda, sA, a_kcontig, B, ldb, sB, b_kcontig, Cout, ldc, sC, bias, M, N, K, batch, alpha, beta, act,
-                    ws, ksplit, act_y, lday, bwd_act, colsum, rowsum_a, bool(async_reduce))
+                    ws, ksplit, act_y, lday, bwd_act, colsum, rowsum_a, bool(async_reduce), ap, bp, cp)
+
+
+def planes_like(t):
+    """bf16 [3, *t.shape] buffer for the exact three-way split of the fp32 tensor ``t`` (its plane p
+    holds element i at p * t.numel() + i, so a 2-D view's leading dim carries over)."""
+    return torch.empty((3,) + tuple(t.shape), dtype=torch.bfloat16, device=t.device)
+
+
+def split_planes(src2d, planes):
+    """planes = exact split of the fp32 matrix src2d (x = h + m + l, csrc/kernels/gemm_pl.hip)."""
+    rows = src2d.shape[0]
+    C().split_planes(src2d, planes.view(3, rows, -1))
 
 
 # FM_GEMM_ASYNC_REDUCE=1: the executor's dW GEMMs run their split-K reduce on a side stream.

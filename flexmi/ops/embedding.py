@@ -359,9 +359,11 @@ class Embedding(Op):
     # (profiles/bench_ab_claim_ratio_r5cr.txt)
     CLAIM_RATIO = float(os.environ.get("FM_EMB_CLAIM_RATIO", "0.2"))
     # FM_EMB_BWD=count: the count / update kernel pair (csrc/kernels/embedding.hip) for every table
-    # above the tiny-table LDS kernel's 16 rows, on the same slot / flag buffers
+    # above the tiny-table LDS kernel's rows, on the same slot / flag buffers
     COUNT = os.environ.get("FM_EMB_BWD", "claim") == "count"
-    TINY_ROWS = 16
+    # the wave-private LDS kernel's table-size limit: the SAME variable and default as the C++
+    # dispatcher (embedding.hip kind_of, FM_EMB_TINY_ROWS, default 64), so the two cannot drift
+    TINY_ROWS = int(os.environ.get("FM_EMB_TINY_ROWS", "64"))
 
     def _claim_buffers(self, ctx):
         """Owner-computes sparse SGD buffers for a mostly-unique table (rows > lookups per step):

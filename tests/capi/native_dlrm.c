@@ -24,7 +24,9 @@
 static const int64_t ROWS[NT] = {100, 50, 200, 30};
 #define D 16
 #define FEAT 13
-#define B 64
+/* batch: 64, or NATIVE_DLRM_B (the uneven-ownership host-communicator test uses a batch whose
+ * per-rank embedding exchange exceeds the 4 MiB staging-slot floor) */
+static int B = 64;
 
 #define CHECK(x)                                                                     \
   do {                                                                               \
@@ -142,6 +144,7 @@ int main(int argc, char** argv) {
     return 2;
   }
   const int device = strcmp(argv[1], "hip") == 0 ? 1 : 0;
+  if (getenv("NATIVE_DLRM_B")) B = atoi(getenv("NATIVE_DLRM_B"));
   const int steps = atoi(argv[3]), world = atoi(argv[4]);
   fflush(stdout);
   int rc = 0;

@@ -19,8 +19,8 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(cmd):
-    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", MASTER_ADDR="127.0.0.1")
+def _run(cmd, **extra_env):
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", MASTER_ADDR="127.0.0.1", **extra_env)
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-2000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
@@ -35,6 +35,10 @@ def _check(r, n):
     assert r["scaling"] == "weak" and r["data"] == "synthetic"
     assert r["config"]["global_batch"] == 64 * n
     assert r["config"]["loss"] == r["config"]["loss"]   # not NaN
+    # HBM preflight of the headline plan (simulator memory model vs the minimum free memory over
+    # ranks; host memory on this CPU rehearsal)
+    h = r["config"]["hbm"]
+    assert h["need_gb"] >= 0 and h["free_gb"] > 0 and h["need_gb"] <= h["free_gb"]
 
 
 def _check_three_plans(r, n):
@@ -106,3 +110,30 @@ def test_bench_eight_ranks_mlperf_plan(strategy):
         assert r["config"]["parallelism"] == "dp8" and "soap_speedup_vs_dp" not in r["config"]
     else:
         assert r["config"]["dp"]["parallelism"] == "dp8" and r["config"]["soap_speedup_vs_dp"] > 0
+
+
+@pytest.mark.multiproc
+def test_bench_comparison_failure_keeps_headline():
+    """A comparison run that fails on ONE rank of eight (FM_BENCH_FAIL=dp@3: an exception in its
+    build phase) becomes ``config.dp.error`` on every rank -- no hang in the next collective -- and
+    the already-measured headline (and the table comparison) still come out as one JSON line."""
+    r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+              "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "8",
+              "--steps", "2", "--warmup", "1", "--config", "tiny", "--batch-per-gpu", "64",
+              "--search-budget", "200"], FM_BENCH_FAIL="dp@3")
+    _check(r, 8)
+    c = r["config"]
+    assert c["parallelism"] == "soap-search8"
+    assert "error" in c["dp"] and "soap_speedup_vs_dp" not in c
+    assert c["table"]["value"] > 0 and c["table"]["hbm"]["need_gb"] >= 0
+
+
+def test_bench_wall_budget_skips_comparisons():
+    """With no wall budget left after the headline, the comparison runs are skipped with a reason
+    instead of being started (two gloo ranks)."""
+    r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+              "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+              "--steps", "2", "--warmup", "1", "--config", "tiny", "--batch-per-gpu", "64", "--budget-s", "1"])
+    _check(r, 2)
+    for name in ("table", "dp"):
+        assert "wall budget" in r["config"][name]["skipped"]

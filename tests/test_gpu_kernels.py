@@ -470,6 +470,41 @@ def test_embedding_owner_computes_sgd(gpu, idx_dtype):
 
 
 @pytest.mark.parametrize("dy_dtype", [torch.float32, torch.bfloat16])
+def test_embedding_owner_computes_duplicate_heavy(gpu, dy_dtype):
+    """the DEFAULT claim rule (Embedding.CLAIM_RATIO = 0.2) puts owner-computes on
+    tables with 0.2 x lookups < rows < lookups -- the 2208 / 7420-row MLPerf tables at B = 8192,
+    where most lookups are duplicates and the dup-atomic path does most of the work.  Two steps
+    against the dense reference, incl. the slot / duplicate-counter release."""
+    from flexmi.ops import _kernels as Kk
+    from flexmi.ops.embedding import Embedding
+    torch.manual_seed(11)
+    B = 8192
+    specs = [(2208, 1, 128), (7420, 1, 128), (3000, 2, 64)]   # rows, bag, D: all in (0.2, 1) x lookups
+    tables, idxs, claim, refs = [], [], [], []
+    for rows, bag, D in specs:
+        assert Embedding.CLAIM_RATIO * B * bag < rows < B * bag
+        W = torch.randn(rows, D, device=gpu)
+        tables.append(W)
+        refs.append(W.clone())
+        idxs.append(torch.randint(0, rows, (B, bag), device=gpu, dtype=torch.int64))
+        claim += [torch.full((rows,), -1, dtype=torch.int32, device=gpu),
+                  torch.empty(B * bag, dtype=torch.int32, device=gpu), torch.zeros(1, dtype=torch.int32, device=gpu)]
+    lr = torch.tensor([0.05], device=gpu)
+    for step in range(2):
+        dys = [torch.randn(B, D, device=gpu).to(dy_dtype) for _, _, D in specs]
+        Kk.C().embedding_bwd_multi(tables, idxs, dys, [d.stride(0) for d in dys], [1.0] * len(specs), lr, claim)
+        for k, ((rows, bag, D), W) in enumerate(zip(specs, refs)):
+            upd = torch.zeros_like(W)
+            upd.index_add_(0, idxs[k].reshape(-1).long(), dys[k].float().repeat_interleave(bag, 0))
+            W -= 0.05 * upd
+        torch.cuda.synchronize()
+        for k in range(len(specs)):
+            assert torch.allclose(tables[k], refs[k], atol=2e-4), (step, specs[k])
+        for k in range(0, len(claim), 3):
+            assert int((claim[k] != -1).sum()) == 0 and int(claim[k + 2].item()) == 0, "claims not released"
+
+
+@pytest.mark.parametrize("dy_dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("idx_dtype", [torch.int64, torch.int32])
 def test_embedding_count_update_sgd(gpu, idx_dtype, dy_dtype):
     """Count / update sparse SGD (FM_EMB_BWD=count: slot = lookups - 1, plain RMW for single-lookup

@@ -201,6 +201,26 @@ def _replay_dlrm(rec):
     return [p.get_weights(m).reshape(-1) for p in m.parameters]
 
 
+def test_native_c_dlrm_uneven_ownership_large_exchange(tmp_path):
+    """the host communicator's slot size must be the same on every rank.  Four tables
+    round-robin over THREE ranks (rank 0 owns two) at a batch whose embedding exchange is above the
+    4 MiB slot floor: each rank's own send total differs, the slot (sized from global quantities)
+    does not, and the run trains like the Python executor."""
+    exe = _build_dlrm_c(tmp_path)
+    rdv = tmp_path / "rdv"
+    rdv.mkdir()
+    prefix = str(tmp_path / "run")
+    env = dict(os.environ, NATIVE_DLRM_B="49152")
+    r = subprocess.run([exe, "cpu", prefix, "2", "3", str(rdv)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "native_dlrm ok: 3 ranks" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+    rec = _parse_dlrm(prefix, 3)
+    got = _replay_dlrm(rec)
+    for i, g in enumerate(got):
+        fin = [rk[0][i] for rk in rec["ranks"] if rk[0][i] is not None]
+        assert fin, i
+        np.testing.assert_allclose(fin[0], g, rtol=2e-3, atol=2e-5)
+
+
 @pytest.mark.parametrize("world", [1, 2])
 def test_native_c_dlrm_tablewise_trains_like_the_executor(tmp_path, world):
     """a C program trains a DLRM through libflexmi_native_c with no CPython --
