@@ -362,9 +362,9 @@ def _timed(a, comm, model, cfg, dcfg, dense_in, sparse, strategy, search, ex, t_
             step_eager()
         torch.cuda.synchronize()
         gi = [0]
-        if world > 1 or os.environ.get("FM_BENCH_STAGE_GRAPH", "0") == "1":
+        if world > 1:
             # input staging as its own small graph per pooled batch, replayed before the step (N > 1:
-            # one segmented step capture instead of one per pooled batch; N = 1 A/B)
+            # one segmented step capture instead of one per pooled batch)
             stage = []
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())

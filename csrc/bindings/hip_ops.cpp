@@ -12,10 +12,6 @@ void fm_sgd_update_segs(float* W, float* G, float* V, unsigned short* Wc, const 
                         const long* len, int nseg, float wd, float mom, int nesterov, int zero_g, hipStream_t s);
 void fm_image_normalize(const unsigned char* src, void* dst, long N, int H, int W, const float* mean, const float* stdv,
                         int bf16, hipStream_t s);
-void fm_gemm_set_variant(int v);
-void fm_gemm_f32_set_variant(int v);
-void fm_gemm_async_arm(int on);
-void fm_gemm_join(hipStream_t s);
 int fm_gemm_dw_sgd(const void* A, long lda, const void* B, long ldb, float* W, long ldw, unsigned short* Wc, float* V,
                    const float* lr, float wd, float mom, int nesterov, int M, int N, int K, float* ws, long ws_bytes,
                    float* rowsum_a, hipStream_t stream);
@@ -28,22 +24,11 @@ int fm_gemm(const void* A, long lda, long sA, int a_kcontig, const void* B, long
             float* colsum, float* rowsum_a, hipStream_t stream);
 void fm_gemm_f32_set_split(int on);
 void fm_embedding_set_bwd_mode(int count);
-void fm_embedding_set_rowblock(int on);
 int fm_gemm_f32_get_split();
 int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, const float* B, long ldb, long sB, int b_kcontig,
                 float* C, long ldc, long sC, const float* bias, int M, int N, int K, int batch, float alpha, int beta,
                 int act, float* ws, long ws_bytes, int ksplit_req, const float* act_y, long lday, int bwd_act,
                 float* colsum, float* rowsum_a, hipStream_t stream);
-int fm_gemm_f32_pl(const float* A, long lda, long sA, int a_kcontig, const float* B, long ldb, long sB, int b_kcontig,
-                   float* C, long ldc, long sC, const float* bias, int M, int N, int K, int batch, float alpha, int beta,
-                   int act, float* ws, long ws_bytes, int ksplit_req, const float* act_y, long lday, int bwd_act,
-                   float* colsum, float* rowsum_a, const unsigned short* Ap, long psa, const unsigned short* Bp, long psb,
-                   unsigned short* Cp, long psc, hipStream_t stream);
-int fm_gemm_f32_dw_sgd_pl(const float* A, long lda, const float* B, long ldb, float* W, long ldw, unsigned short* Wc,
-                          float* V, const float* lr, float wd, float mom, int nesterov, int M, int N, int K, float* ws,
-                          long ws_bytes, float* rowsum_a, const unsigned short* Ap, long psa, const unsigned short* Bp,
-                          long psb, hipStream_t stream);
-void fm_split3(const float* src, long rows, int cols, long lds, unsigned short* dst, long ldd, long ps, hipStream_t s);
 int fm_smallk_fwd_f32_launch(const float* x, long ldx, const float* w, const float* bias, float* y, long ldy, long M,
                              int K, int N, int act, hipStream_t s);
 int fm_smallk_dw_f32_launch(const float* dpre, long ldd, const float* x, long ldx, float* dw, float* db, long M, int K,
@@ -83,11 +68,6 @@ void fm_dot_interaction_fwd(const void* const* z, int F, long ldz, void* out, lo
                             hipStream_t s);
 void fm_dot_interaction_bwd(const void* const* z, int F, long ldz, const void* dout, long ldo, void* const* dz, long lddz,
                             unsigned acc_mask, long B, int D, int self, hipStream_t s);
-int fm_dot_interaction_fwd_f32g(const float* const* z, const void* const* ix, const long* ld, const long* rows, int i64,
-                                int F, float* out, long ldo, long B, int D, int W, int self, hipStream_t s);
-int fm_dot_interaction_bwd_f32g(const float* const* z, const void* const* ix, const long* ld, const long* rows, int i64,
-                                int F, const float* dout, long ldo, float* const* dz, long lddz, unsigned acc_mask, long B,
-                                int D, int self, hipStream_t s);
 void fm_dot_interaction_fwd_f32(const float* const* z, int F, long ldz, float* out, long ldo, long B, int D, int W, int self,
                                 hipStream_t s);
 void fm_dot_interaction_bwd_f32(const float* const* z, int F, long ldz, const float* dout, long ldo, float* const* dz,
@@ -190,8 +170,7 @@ int gemm(torch::Tensor A, int64_t lda, int64_t sA, bool a_kcontig, torch::Tensor
          torch::Tensor C, int64_t ldc, int64_t sC, c10::optional<torch::Tensor> bias, int64_t M, int64_t N, int64_t K,
          int64_t batch, double alpha, bool beta, int64_t act, c10::optional<torch::Tensor> ws, int64_t ksplit,
          c10::optional<torch::Tensor> act_y, int64_t lday, int64_t bwd_act, c10::optional<torch::Tensor> colsum,
-         c10::optional<torch::Tensor> rowsum_a, bool async_reduce, c10::optional<torch::Tensor> ap,
-         c10::optional<torch::Tensor> bp, c10::optional<torch::Tensor> cp) {
+         c10::optional<torch::Tensor> rowsum_a) {
   check_cuda(A, "A");
   check_cuda(B, "B");
   check_cuda(C, "C");
@@ -231,52 +210,20 @@ int gemm(torch::Tensor A, int64_t lda, int64_t sA, bool a_kcontig, torch::Tensor
     w = ws->data_ptr<float>();
     wsb = ws->numel() * 4;
   }
-  // async_reduce: the split-K reduce of THIS GEMM may run on a side stream (gemm_async.hip); the
-  // caller joins (gemm_join) before anything reads C
-  fm_gemm_async_arm(async_reduce ? 1 : 0);
   int ks;
-  // exact bf16 planes (gemm_pl.hip): [3, rows, ld] bf16 with the fp32 tensor's storage extent
-  // (plane stride = numel / 3), element (r, c) of plane p at p * ps + the fp32 offset
-  auto plane = [&](const c10::optional<torch::Tensor>& t, const torch::Tensor& like, const char* name) -> long {
-    if (!(t.has_value() && t->defined())) return 0;
-    TORCH_CHECK(f32 && t->is_cuda() && t->scalar_type() == torch::kBFloat16 && t->is_contiguous() && t->numel() % 3 == 0 &&
-                    t->numel() / 3 >= like.numel() - like.storage_offset() + like.storage_offset(),
-                "gemm ", name, ": bf16 planes [3, ...] covering the fp32 operand");
-    return t->numel() / 3;
-  };
-  const long psa = plane(ap, A, "ap"), psb = plane(bp, B, "bp"), psc = plane(cp, C, "cp");
-  if (psa) TORCH_CHECK(lastA + (batch - 1) * sA < psa, "gemm ap: planes smaller than A");
-  if (psb) TORCH_CHECK(lastB + (batch - 1) * sB < psb, "gemm bp: planes smaller than B");
-  if (psc) TORCH_CHECK((M - 1) * ldc + (N - 1) + (batch - 1) * sC < psc, "gemm cp: planes smaller than C");
   if (f32)
-    ks = fm_gemm_f32_pl(A.data_ptr<float>(), lda, sA, a_kcontig, B.data_ptr<float>(), ldb, sB, b_kcontig, C.data_ptr<float>(),
-                        ldc, sC, bias.has_value() && bias->defined() ? bias->data_ptr<float>() : nullptr, (int)M, (int)N,
-                        (int)K, (int)batch, (float)alpha, beta ? 1 : 0, (int)act, w, wsb, (int)ksplit,
-                        (const float*)cptr(act_y), lday, (int)bwd_act, (float*)mptr(colsum), (float*)mptr(rowsum_a),
-                        (const unsigned short*)cptr(ap), psa, (const unsigned short*)cptr(bp), psb,
-                        (unsigned short*)mptr(cp), psc, cur());
+    ks = fm_gemm_f32(A.data_ptr<float>(), lda, sA, a_kcontig, B.data_ptr<float>(), ldb, sB, b_kcontig, C.data_ptr<float>(),
+                     ldc, sC, bias.has_value() && bias->defined() ? bias->data_ptr<float>() : nullptr, (int)M, (int)N,
+                     (int)K, (int)batch, (float)alpha, beta ? 1 : 0, (int)act, w, wsb, (int)ksplit,
+                     (const float*)cptr(act_y), lday, (int)bwd_act, (float*)mptr(colsum), (float*)mptr(rowsum_a), cur());
   else
     ks = fm_gemm(A.data_ptr(), lda, sA, a_kcontig, B.data_ptr(), ldb, sB, b_kcontig, C.data_ptr(), ldc, sC,
                  C.scalar_type() == torch::kFloat32, bias.has_value() && bias->defined() ? bias->data_ptr<float>() : nullptr,
                  (int)M, (int)N, (int)K, (int)batch, (float)alpha, beta ? 1 : 0, (int)act, w, wsb, (int)ksplit,
                  cptr(act_y), lday, (int)bwd_act, (float*)mptr(colsum), (float*)mptr(rowsum_a), cur());
-  fm_gemm_async_arm(0);
   return ks;
 }
 
-void gemm_join() { fm_gemm_join(cur()); }
-
-// exact three-way bf16 split of an fp32 matrix (rows x cols, leading dim src.stride(0)) into planes
-// [3, rows, ld] (ld = dst.size(2)); element (r, c) of plane p at p * rows * ld + r * ld + c
-void split_planes(torch::Tensor src, torch::Tensor dst) {
-  TORCH_CHECK(src.is_cuda() && src.scalar_type() == torch::kFloat32 && src.dim() == 2 && src.stride(1) == 1,
-              "split_planes: fp32 [rows, cols] with unit column stride");
-  TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == torch::kBFloat16 && dst.is_contiguous() && dst.dim() == 3 &&
-                  dst.size(0) == 3 && dst.size(1) >= src.size(0) && dst.size(2) >= src.size(1),
-              "split_planes: bf16 [3, >= rows, >= cols] destination");
-  fm_split3(src.data_ptr<float>(), src.size(0), (int)src.size(1), src.stride(0), (unsigned short*)dst.data_ptr(),
-            dst.size(2), dst.size(1) * dst.size(2), cur());
-}
 
 // fm_sgd over disjoint [off, off + len) ranges of one flat master / grad / state / mirror set
 void sgd_segs(torch::Tensor W, torch::Tensor G, c10::optional<torch::Tensor> V, c10::optional<torch::Tensor> Wc,
@@ -305,8 +252,7 @@ void sgd_segs(torch::Tensor W, torch::Tensor G, c10::optional<torch::Tensor> V, 
 // computes the gradient and runs the optimizer kernel itself).
 int gemm_dw_sgd(torch::Tensor dpre, torch::Tensor x, torch::Tensor W, c10::optional<torch::Tensor> Wc,
                 c10::optional<torch::Tensor> V, torch::Tensor lr, double wd, double mom, bool nesterov,
-                c10::optional<torch::Tensor> db, torch::Tensor ws, c10::optional<torch::Tensor> dp,
-                c10::optional<torch::Tensor> xp) {
+                c10::optional<torch::Tensor> db, torch::Tensor ws) {
   check_cuda(dpre, "dpre");
   check_cuda(x, "x");
   check_cuda(W, "W");
@@ -325,26 +271,11 @@ int gemm_dw_sgd(torch::Tensor dpre, torch::Tensor x, torch::Tensor W, c10::optio
   if (db.has_value() && db->defined())
     TORCH_CHECK(db->scalar_type() == torch::kFloat32 && db->numel() >= Nout, "gemm_dw_sgd: db fp32 [out]");
   TORCH_CHECK((B - 1) * dpre.stride(0) + Nout <= dpre.numel() && (B - 1) * x.stride(0) + Kin <= x.numel(), "gemm_dw_sgd: extents");
-  long psa = 0, psb = 0;
-  for (auto* t : {&dp, &xp}) {
-    if (t->has_value() && (*t)->defined())
-      TORCH_CHECK(f32 && (*t)->is_cuda() && (*t)->scalar_type() == torch::kBFloat16 && (*t)->is_contiguous() &&
-                      (*t)->numel() % 3 == 0, "gemm_dw_sgd: bf16 planes [3, ...]");
-  }
-  if (dp.has_value() && dp->defined()) {
-    psa = dp->numel() / 3;
-    TORCH_CHECK((B - 1) * dpre.stride(0) + Nout <= psa, "gemm_dw_sgd: dpre planes too small");
-  }
-  if (xp.has_value() && xp->defined()) {
-    psb = xp->numel() / 3;
-    TORCH_CHECK((B - 1) * x.stride(0) + Kin <= psb, "gemm_dw_sgd: x planes too small");
-  }
   if (f32)
-    return fm_gemm_f32_dw_sgd_pl(dpre.data_ptr<float>(), dpre.stride(0), x.data_ptr<float>(), x.stride(0),
-                                 W.data_ptr<float>(), Kin, (unsigned short*)mptr(Wc), (float*)mptr(V), lr.data_ptr<float>(),
-                                 (float)wd, (float)mom, nesterov ? 1 : 0, (int)Nout, (int)Kin, (int)B, ws.data_ptr<float>(),
-                                 ws.numel() * 4, (float*)mptr(db), (const unsigned short*)cptr(dp), psa,
-                                 (const unsigned short*)cptr(xp), psb, cur());
+    return fm_gemm_f32_dw_sgd(dpre.data_ptr<float>(), dpre.stride(0), x.data_ptr<float>(), x.stride(0),
+                              W.data_ptr<float>(), Kin, (unsigned short*)mptr(Wc), (float*)mptr(V), lr.data_ptr<float>(),
+                              (float)wd, (float)mom, nesterov ? 1 : 0, (int)Nout, (int)Kin, (int)B, ws.data_ptr<float>(),
+                              ws.numel() * 4, (float*)mptr(db), cur());
   return fm_gemm_dw_sgd(dpre.data_ptr(), dpre.stride(0), x.data_ptr(), x.stride(0), W.data_ptr<float>(), Kin,
                         (unsigned short*)mptr(Wc), (float*)mptr(V), lr.data_ptr<float>(), (float)wd, (float)mom,
                         nesterov ? 1 : 0, (int)Nout, (int)Kin, (int)B, ws.data_ptr<float>(), ws.numel() * 4,
@@ -698,77 +629,6 @@ void dot_bwd(std::vector<torch::Tensor> zs, int64_t ldz, torch::Tensor dout, int
   TORCH_CHECK(D % 8 == 0 && D <= 256, "dot interaction backward: D % 8 == 0, D <= 256");
   fm_dot_interaction_bwd(p.data(), (int)p.size(), ldz, dout.data_ptr(), ldo, g.data(), lddz, (unsigned)acc_mask,
                          dout.size(0), (int)D, self ? 1 : 0, cur());
-}
-
-// Gathered-row (embedding-into-interaction) forms, fp32: zs[i] is feature i's [rows, D] source --
-// the bottom-MLP output (ixs[i] = None: row b) or an embedding TABLE (ixs[i] = the bag-1 lookup
-// indices [B] / [B, 1]: row ixs[i][b]).  Returns false when the fast kernels do not apply (nothing
-// launched; the caller falls back to materialised embedding outputs).
-static bool gather_args(const std::vector<torch::Tensor>& zs, const std::vector<c10::optional<torch::Tensor>>& ixs, long B,
-                        int64_t D, std::vector<const float*>& p, std::vector<const void*>& ix, std::vector<long>& ld,
-                        std::vector<long>& rows, int& i64) {
-  TORCH_CHECK(zs.size() >= 2 && zs.size() <= 32 && ixs.size() == zs.size(), "dot gather: 2..32 features");
-  i64 = -1;
-  for (size_t i = 0; i < zs.size(); ++i) {
-    const auto& z = zs[i];
-    check_cuda(z, "z");
-    if (z.scalar_type() != torch::kFloat32 || z.dim() != 2 || z.size(1) < D || z.stride(1) != 1) return false;
-    p.push_back(z.data_ptr<float>());
-    ld.push_back(z.stride(0));
-    rows.push_back(z.size(0));
-    if (ixs[i].has_value()) {
-      const auto& t = *ixs[i];
-      check_cuda(t, "ix");
-      if (t.numel() != B || !t.is_contiguous()) return false;
-      const int w = t.scalar_type() == torch::kInt64 ? 1 : t.scalar_type() == torch::kInt32 ? 0 : -1;
-      if (w < 0 || (i64 >= 0 && w != i64)) return false;
-      i64 = w;
-      ix.push_back(t.data_ptr());
-    } else {
-      if (z.size(0) < B) return false;
-      ix.push_back(nullptr);
-    }
-  }
-  if (i64 < 0) i64 = 1;
-  return true;
-}
-
-bool dot_fwd_gather(std::vector<torch::Tensor> zs, std::vector<c10::optional<torch::Tensor>> ixs, torch::Tensor out,
-                    int64_t ldo, int64_t D, int64_t W, bool self) {
-  const long B = out.size(0);
-  std::vector<const float*> p;
-  std::vector<const void*> ix;
-  std::vector<long> ld, rows;
-  int i64 = 1;
-  check_cuda(out, "out");
-  if (out.scalar_type() != torch::kFloat32 || !gather_args(zs, ixs, B, D, p, ix, ld, rows, i64)) return false;
-  TORCH_CHECK(out.numel() >= (B - 1) * ldo + W, "dot output too small");
-  return fm_dot_interaction_fwd_f32g(p.data(), ix.data(), ld.data(), rows.data(), i64, (int)zs.size(), out.data_ptr<float>(),
-                                     ldo, B, (int)D, (int)W, self ? 1 : 0, cur()) == 0;
-}
-
-bool dot_bwd_gather(std::vector<torch::Tensor> zs, std::vector<c10::optional<torch::Tensor>> ixs, torch::Tensor dout,
-                    int64_t ldo, std::vector<c10::optional<torch::Tensor>> dzs, int64_t lddz, int64_t acc_mask, int64_t D,
-                    bool self) {
-  const long B = dout.size(0);
-  const long F = (long)zs.size();
-  std::vector<const float*> p;
-  std::vector<const void*> ix;
-  std::vector<long> ld, rows;
-  int i64 = 1;
-  check_cuda(dout, "dout");
-  if (dout.scalar_type() != torch::kFloat32 || (long)dzs.size() != F || !gather_args(zs, ixs, B, D, p, ix, ld, rows, i64))
-    return false;
-  const long np = self ? F * (F + 1) / 2 : F * (F - 1) / 2;
-  TORCH_CHECK(ldo >= D + np && dout.numel() >= (B - 1) * ldo + D + np, "dot gather backward: dOut row too small");
-  std::vector<float*> g;
-  for (auto& d : dzs) {
-    g.push_back((float*)mptr(d));
-    if (d.has_value())
-      TORCH_CHECK(d->scalar_type() == torch::kFloat32 && d->numel() >= (B - 1) * lddz + D, "dot gather backward: fp32 grads");
-  }
-  return fm_dot_interaction_bwd_f32g(p.data(), ix.data(), ld.data(), rows.data(), i64, (int)F, dout.data_ptr<float>(), ldo,
-                                     g.data(), lddz, (unsigned)acc_mask, B, (int)D, self ? 1 : 0, cur()) == 0;
 }
 
 void sgd(torch::Tensor W, torch::Tensor G, c10::optional<torch::Tensor> V, c10::optional<torch::Tensor> Wc, torch::Tensor lr,
@@ -1273,16 +1133,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm", &gemm, py::arg("A"), py::arg("lda"), py::arg("sA"), py::arg("a_kcontig"), py::arg("B"), py::arg("ldb"),
         py::arg("sB"), py::arg("b_kcontig"), py::arg("C"), py::arg("ldc"), py::arg("sC"), py::arg("bias"), py::arg("M"),
         py::arg("N"), py::arg("K"), py::arg("batch"), py::arg("alpha"), py::arg("beta"), py::arg("act"), py::arg("ws"),
-        py::arg("ksplit"), py::arg("act_y"), py::arg("lday"), py::arg("bwd_act"), py::arg("colsum"), py::arg("rowsum_a"),
-        py::arg("async_reduce"), py::arg("ap") = py::none(), py::arg("bp") = py::none(), py::arg("cp") = py::none());
-  m.def("gemm_join", &gemm_join);
-  m.def("split_planes", &split_planes);
+        py::arg("ksplit"), py::arg("act_y"), py::arg("lday"), py::arg("bwd_act"), py::arg("colsum"), py::arg("rowsum_a"));
   m.def("gemm_dw_sgd", &gemm_dw_sgd, py::arg("dpre"), py::arg("x"), py::arg("W"), py::arg("Wc"), py::arg("V"),
-        py::arg("lr"), py::arg("wd"), py::arg("mom"), py::arg("nesterov"), py::arg("db"), py::arg("ws"),
-        py::arg("dp") = py::none(), py::arg("xp") = py::none());
+        py::arg("lr"), py::arg("wd"), py::arg("mom"), py::arg("nesterov"), py::arg("db"), py::arg("ws"));
   m.def("sgd_segs", &sgd_segs);
-  m.def("gemm_set_variant", [](int v) { fm_gemm_set_variant(v); });
-  m.def("gemm_f32_set_variant", [](int v) { fm_gemm_f32_set_variant(v); });
   m.def("init_fill", &init_fill);
   m.def("smallk_fwd", &smallk_fwd);
   m.def("smallk_dw", &smallk_dw);
@@ -1306,7 +1160,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_f32_get_split", []() { return fm_gemm_f32_get_split(); });
   // sparse-SGD kernels of tables with slot buffers: 1 = count / update, 0 = claim / dup / owner
   m.def("embedding_set_bwd_mode", [](bool count) { fm_embedding_set_bwd_mode(count ? 1 : 0); });
-  m.def("embedding_set_rowblock", [](bool on) { fm_embedding_set_rowblock(on ? 1 : 0); });
   m.def("conv_nhwc_dgrad_strided", &conv_nhwc_dgrad_strided);
   m.def("conv_nhwc_wgrad", &conv_nhwc_wgrad);
   m.def("conv_s2d", &conv_s2d);
@@ -1323,8 +1176,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("dot_fwd", &dot_fwd);
   m.def("dot_bwd", &dot_bwd, py::arg("zs"), py::arg("ldz"), py::arg("dout"), py::arg("ldo"), py::arg("dzs"),
         py::arg("lddz"), py::arg("acc_mask"), py::arg("D"), py::arg("self"), py::arg("act0") = 10);
-  m.def("dot_fwd_gather", &dot_fwd_gather);
-  m.def("dot_bwd_gather", &dot_bwd_gather);
   m.def("sgd", &sgd);
   m.def("adam", &adam);
   m.def("cast_bf16", &cast_bf16);

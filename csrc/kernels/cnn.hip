@@ -2,7 +2,7 @@
 // batch normalisation (replace the reference's cuDNN calls: src/ops/conv_2d.cu:405-565,
 // src/ops/pool_2d.cu:256-357, src/ops/batch_norm.cu:348-503).
 //
-// Convolution runs on the MFMA GEMM (gemm.hip / gemm_glds.hip):
+// Convolution runs on the MFMA GEMM (gemm.hip):
 //   forward   out[NPQ, K]   = col[NPQ, CRS] . W[K, CRS]^T   (+bias, activation in the epilogue)
 //   dW, db    dW[K, CRS]    = g[NPQ, K]^T . col               (db from the A-tile row sums)
 //   dX        dcol[NPQ, CRS] = g . W                          -> col2im gather
@@ -168,43 +168,6 @@ __global__ void __launch_bounds__(256) fm_pool_argmax_kernel(const T* __restrict
 // pooling backward, per input element (32-bit index math, one thread per element): sum the
 // gradients of the <= ceil(k/s)^2 windows that route to it (max: the window's argmax code is this
 // element; avg: 1 / clipped window size)
-template <typename T>
-__global__ void __launch_bounds__(256) fm_pool_bwd_kernel(const T* __restrict__ y, const T* __restrict__ dy,
-                                                          const unsigned char* __restrict__ code, T* __restrict__ dx,
-                                                          int total, FastDiv dW, FastDiv dH, FastDiv dsh, FastDiv dsw,
-                                                          int H, int W, int P, int Q, int kh, int kw, int sh, int sw,
-                                                          int pt, int pl, int is_max, int act, int acc) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= total) return;
-  const int t = fdiv(i, dW), w = i - t * W;
-  const int nc = fdiv(t, dH), h = t - nc * H;
-  float g = 0.f;
-  // windows (p, q) containing (h, w): p*sh - pt <= h < p*sh - pt + kh (divisions by magic numbers;
-  // arguments kept >= 0: pmin = ceil((h + pt - kh + 1) / sh) clipped at 0)
-  const int pmin = h + pt + 1 >= kh ? fdiv(h + pt - kh + sh, dsh) : 0;
-  const int pmax = h + pt >= 0 ? min(P - 1, fdiv(h + pt, dsh)) : -1;    // pads may be negative (superset boxes)
-  const int qmin = w + pl + 1 >= kw ? fdiv(w + pl - kw + sw, dsw) : 0;
-  const int qmax = w + pl >= 0 ? min(Q - 1, fdiv(w + pl, dsw)) : -1;
-  for (int p = pmin; p <= pmax; ++p) {
-    const int h0 = p * sh - pt;
-    if (h < h0 || h >= h0 + kh) continue;
-    for (int q = qmin; q <= qmax; ++q) {
-      const int w0 = q * sw - pl;
-      if (w < w0 || w >= w0 + kw) continue;
-      const int o = (nc * P + p) * Q + q;
-      if (is_max) {
-        if (code[o] == (unsigned char)((h - h0) * kw + (w - w0)))
-          g += act == ACT_NONE ? tof(dy[o]) : act_bwd(act, tof(y[o]), tof(dy[o]));
-      } else {
-        const int hs = max(h0, 0), he = min(h0 + kh, H), ws = max(w0, 0), we = min(w0 + kw, W);
-        const float go = act == ACT_NONE ? tof(dy[o]) : act_bwd(act, tof(y[o]), tof(dy[o]));
-        g += go / (float)((he - hs) * (we - ws));
-      }
-    }
-  }
-  if (acc) g += tof(dx[i]);
-  dx[i] = fromf<T>(g);
-}
 
 // pooling backward, row segments: one thread = VW consecutive input columns of one (n, c, h) row.
 // The windows that route to the segment are the same rows p for all VW columns and a short run of
@@ -455,8 +418,7 @@ __global__ void __launch_bounds__(256) fm_pool_bwd_max_scatter(const T* __restri
                                                                const unsigned char* __restrict__ code, T* __restrict__ dx,
                                                                int NC, int H, int W, int P, int Q, int kh, int kw, int sh,
                                                                int pt, int pl, int sw, int act, int acc, int HB, int nbands,
-                                                               int G, FastDiv dQ, FastDiv dPQ, FastDiv dkw, FastDiv dsh,
-                                                               int pa, int qa, int nph) {
+                                                               int G, FastDiv dQ, FastDiv dPQ, FastDiv dkw, FastDiv dsh) {
   extern __shared__ float sdx[];
   int nc0, band, planes;
   if (G > 1) {
@@ -477,36 +439,27 @@ __global__ void __launch_bounds__(256) fm_pool_bwd_max_scatter(const T* __restri
   const int phi = G > 1 ? P : min(P, (h1b - 1 + pt) >= 0 ? fdiv(h1b - 1 + pt, dsh) + 1 : 0);
   const int nwin1 = max(0, phi - plo) * Q;
   const int nwin = planes * nwin1;
-  // phases > 1 (FM_POOL_SCATTER_PHASES=1, opt-in): windows p, p + pa (pa = ceil(kh / sh)) and q,
-  // q + qa never share an input, so the (p mod pa, q mod qa) classes run one after another with plain
-  // LDS read-add-writes instead of LDS float atomics.  Measured slower on AlexNet b256 (82.5 k vs
-  // 84.1 k img/s, profiles/pool_scatter_phases_ab_r5z.txt): the extra window passes and barriers
-  // cost more than the few colliding atomics at stride 2
-  for (int ph = 0; ph < nph; ++ph) {
-    const int pph = ph / qa, qph = ph - pph * qa;
-    for (int e = threadIdx.x; e < nwin; e += 256) {
-      int gi = 0, r = e;
-      if (G > 1) {
-        gi = fdiv(e, dPQ);
-        r = e - gi * nwin1;
-      }
-      const int pr = fdiv(r, dQ), q = r - pr * Q;
-      const int p = plo + pr;
-      if (nph > 1 && (p % pa != pph || q % qa != qph)) continue;
-      const long oi = ((long)(nc0 + gi) * P + p) * Q + q;
-      const int cd = code[oi];
-      if (cd == 255) continue;
-      const int rr = fdiv(cd, dkw), cc = cd - rr * kw;
-      const int h = p * sh - pt + rr;
-      if (h < h0b || h >= h1b) continue;             // this window's max lies in another band
-      const int w = q * sw - pl + cc;
-      const float gd = tof(dy[oi]);
-      const float v = act == ACT_NONE ? gd : act_bwd(act, tof(y[oi]), gd);
-      float* t = &sdx[(gi * rows + h - h0b) * W + w];
-      if (nph > 1) *t += v;
-      else atomicAdd(t, v);
+  // (measured and deleted in r6: running the (p mod ceil(kh/sh), q mod ceil(kw/sw)) window classes one
+  // after another with plain LDS read-add-writes instead of LDS float atomics -- 82.5 k vs 84.1 k
+  // img/s on AlexNet b256, profiles/pool_scatter_phases_ab_r5z.txt)
+  for (int e = threadIdx.x; e < nwin; e += 256) {
+    int gi = 0, r = e;
+    if (G > 1) {
+      gi = fdiv(e, dPQ);
+      r = e - gi * nwin1;
     }
-    if (nph > 1) __syncthreads();
+    const int pr = fdiv(r, dQ), q = r - pr * Q;
+    const int p = plo + pr;
+    const long oi = ((long)(nc0 + gi) * P + p) * Q + q;
+    const int cd = code[oi];
+    if (cd == 255) continue;
+    const int rr = fdiv(cd, dkw), cc = cd - rr * kw;
+    const int h = p * sh - pt + rr;
+    if (h < h0b || h >= h1b) continue;             // this window's max lies in another band
+    const int w = q * sw - pl + cc;
+    const float gd = tof(dy[oi]);
+    const float v = act == ACT_NONE ? gd : act_bwd(act, tof(y[oi]), gd);
+    atomicAdd(&sdx[(gi * rows + h - h0b) * W + w], v);
   }
   __syncthreads();
   // (a 16-B vector-store form of this loop -- 8 bf16 per lane between scalar head / tail -- measured
@@ -521,98 +474,10 @@ __global__ void __launch_bounds__(256) fm_pool_bwd_max_scatter(const T* __restri
   }
 }
 
-// ---- pooling on whole planes (one block per (n, c) plane staged in LDS) -------------------
-// The plane's operands are read ONCE, contiguously (coalesced), into LDS; every output of the
-// forward and every input element of the backward is then computed from LDS and written
-// contiguously -- no per-element global re-reads of the overlapping windows.  Opt-in
-// (FM_POOL_PLANE=1, planes that fit PLANE_LDS bytes): measured slower than the row / element
-// kernels on AlexNet b256 (pool bwd 479 vs 286 us/step) and ResNet-50 b64 (fwd 335 vs 137) --
-// one block per plane leaves too few waves in flight to hide the HBM latency of the staging.
-constexpr int PLANE_LDS = 48 * 1024;
+// (Pooling on whole planes -- one block per (n, c) plane staged in LDS -- measured slower than the
+// row / band kernels: AlexNet b256 pool bwd 479 vs 286 us/step, ResNet-50 b64 fwd 335 vs 137;
+// one block per plane leaves too few waves in flight.  Deleted in r6.)
 
-template <typename T>
-__global__ void __launch_bounds__(256) fm_pool_fwd_plane(const T* __restrict__ x, T* __restrict__ y,
-                                                         unsigned char* __restrict__ code, int H, int W, int P, int Q,
-                                                         int kh, int kw, int sh, int sw, int pt, int pl, int is_max,
-                                                         int act) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  T* xs = reinterpret_cast<T*>(smem);
-  const long plane = blockIdx.x;
-  const int HW = H * W, PQ = P * Q;
-  const T* xp = x + plane * HW;
-  for (int i = threadIdx.x; i < HW; i += 256) xs[i] = xp[i];
-  __syncthreads();
-  T* yp = y + plane * PQ;
-  unsigned char* cp = code ? code + plane * PQ : nullptr;
-  for (int o = threadIdx.x; o < PQ; o += 256) {
-    const int p = o / Q, q = o - p * Q;
-    const int h0 = p * sh - pt, w0 = q * sw - pl;
-    float m = -INFINITY, sum = 0.f;
-    int cnt = 0, bc = 255;
-    for (int r = 0; r < kh; ++r) {
-      const int h = h0 + r;
-      if (h < 0 || h >= H) continue;
-      for (int c = 0; c < kw; ++c) {
-        const int w = w0 + c;
-        if (w < 0 || w >= W) continue;
-        const float v = tof(xs[h * W + w]);
-        if (v > m || bc == 255) bc = r * kw + c;
-        m = fmaxf(m, v);
-        sum += v;
-        ++cnt;
-      }
-    }
-    const float out = is_max ? m : (cnt ? sum / cnt : 0.f);
-    yp[o] = fromf<T>(act_fwd(act, out));
-    if (cp) cp[o] = (unsigned char)bc;
-  }
-}
-
-template <typename T>
-__global__ void __launch_bounds__(256) fm_pool_bwd_plane(const T* __restrict__ y, const T* __restrict__ dy,
-                                                         const unsigned char* __restrict__ code, T* __restrict__ dx, int H,
-                                                         int W, int P, int Q, int kh, int kw, int sh, int sw, int pt, int pl,
-                                                         int is_max, int act, int acc) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const long plane = blockIdx.x;
-  const int HW = H * W, PQ = P * Q;
-  float* gs = reinterpret_cast<float*>(smem);                       // [PQ] output gradients (act-bwd applied)
-  unsigned char* cs = reinterpret_cast<unsigned char*>(gs + PQ);    // [PQ] argmax codes
-  const T* dyp = dy + plane * PQ;
-  const T* ypp = y + plane * PQ;
-  for (int o = threadIdx.x; o < PQ; o += 256) {
-    const float g = tof(dyp[o]);
-    gs[o] = act == ACT_NONE ? g : act_bwd(act, tof(ypp[o]), g);
-    if (is_max) cs[o] = code[plane * PQ + o];
-  }
-  __syncthreads();
-  T* dxp = dx + plane * HW;
-  for (int e = threadIdx.x; e < HW; e += 256) {
-    const int h = e / W, w = e - h * W;
-    const int pmin = h + pt + 1 >= kh ? (h + pt - kh + sh) / sh : 0;
-    const int pmax = h + pt >= 0 ? min(P - 1, (h + pt) / sh) : -1;
-    const int qmin = w + pl + 1 >= kw ? (w + pl - kw + sw) / sw : 0;
-    const int qmax = w + pl >= 0 ? min(Q - 1, (w + pl) / sw) : -1;
-    float g = 0.f;
-    for (int p = pmin; p <= pmax; ++p) {
-      const int h0 = p * sh - pt;
-      if (h < h0 || h >= h0 + kh) continue;
-      for (int q = qmin; q <= qmax; ++q) {
-        const int w0 = q * sw - pl;
-        if (w < w0 || w >= w0 + kw) continue;
-        const int o = p * Q + q;
-        if (is_max) {
-          if (cs[o] == (unsigned char)((h - h0) * kw + (w - w0))) g += gs[o];
-        } else {
-          const int hs = max(h0, 0), he = min(h0 + kh, H), ws = max(w0, 0), we = min(w0 + kw, W);
-          g += gs[o] / (float)((he - hs) * (we - ws));
-        }
-      }
-    }
-    if (acc) g += tof(dxp[e]);
-    dxp[e] = fromf<T>(g);
-  }
-}
 
 // ---- generic 4-D strided copy (stride-phase convolutions) ----------------------------------
 // dst[o_d + sum i_k t_k] (+)= src[o_s + sum i_k s_k] over the box d0 x d1 x d2 x d3 (innermost
@@ -802,15 +667,7 @@ static void fm_pool_fwd_t(const void* x, void* y, unsigned char* code, int N, in
                           int sh, int sw, int pt, int pl, int is_max, int act, hipStream_t st) {
   const int total = N * C * P * Q;
   if (total <= 0) return;
-  static const bool no_plane = !(getenv("FM_POOL_PLANE") != nullptr && atoi(getenv("FM_POOL_PLANE")) == 1);   // opt-in: loses to the row kernels (profiles/prof_r3e_*)
-  if (!no_plane && (long)H * W * sizeof(T) <= PLANE_LDS) {
-    hipLaunchKernelGGL(fm_pool_fwd_plane<T>, dim3(N * C), dim3(256), (size_t)H * W * sizeof(T), st, (const T*)x, (T*)y,
-                       is_max ? code : nullptr, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act);
-    return;
-  }
-  // FM_POOL_BAND=0: the per-output kernel instead of the LDS row bands
-  static const bool band = !(getenv("FM_POOL_BAND") != nullptr && atoi(getenv("FM_POOL_BAND")) == 0);
-  if (band && (long)kh * W <= 4096) {
+  if ((long)kh * W <= 4096) {   // LDS row bands (the per-output kernel below past their limit)
     const int PB = std::max(1, std::min(P, ((4096 / W) - kh) / sh + 1));
     const int nbands = (P + PB - 1) / PB;
     const int NC = N * C;
@@ -838,15 +695,8 @@ static void fm_pool_bwd_t(const void* x, const void* y, const void* dy, void* dx
   if (is_max && !code_ready)
     hipLaunchKernelGGL(fm_pool_argmax_kernel<T>, dim3((outs + 255) / 256), dim3(256), 0, st, (const T*)x, code, outs, H, W,
                        P, Q, kh, kw, sh, sw, pt, pl);
-  static const bool per_elem = getenv("FM_POOL_BWD_ELEM") != nullptr;   // A/B: the per-element kernel
-  static const bool no_plane = !(getenv("FM_POOL_PLANE") != nullptr && atoi(getenv("FM_POOL_PLANE")) == 1);   // opt-in: loses to the row kernels (profiles/prof_r3e_*)
-  if (!per_elem && !no_plane && (long)P * Q * 5 <= PLANE_LDS) {
-    hipLaunchKernelGGL(fm_pool_bwd_plane<T>, dim3(N * C), dim3(256), (size_t)P * Q * 5, st, (const T*)y, (const T*)dy,
-                       (const unsigned char*)code, (T*)dx, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, acc);
-    return;
-  }
-  static const bool band = !(getenv("FM_POOL_BAND") != nullptr && atoi(getenv("FM_POOL_BAND")) == 0);
-  if (!per_elem && band) {
+  {   // input-row band kernels (the per-input gather below only past their LDS limits; a one-plane
+      // LDS kernel measured slower than these, profiles/prof_r3e_*, and was deleted in r6)
     // input-row band HB: ~4 K input elements; it needs <= (HB + kh - 1) / sh + 1 output rows staged
     const int HB = std::max(1, std::min(H, 4096 / W));
     const int nbands = (H + HB - 1) / HB;
@@ -856,13 +706,10 @@ static void fm_pool_bwd_t(const void* x, const void* y, const void* dy, void* dx
     const size_t lds = (size_t)G * maxprows * Q * 5;
     if (is_max) {                        // max pooling: scatter through the recorded argmax
       const int blocks = G > 1 ? (NC + G - 1) / G : NC * nbands;
-      const char* phe = getenv("FM_POOL_SCATTER_PHASES");
-      const bool phases = phe != nullptr && atoi(phe) == 1;
-      const int pa = (kh + sh - 1) / sh, qa = (kw + sw - 1) / sw;
       const size_t lds_s = (size_t)(G > 1 ? G * H : HB) * W * sizeof(float);
       hipLaunchKernelGGL(fm_pool_bwd_max_scatter<T>, dim3(blocks), dim3(256), lds_s, st, (const T*)y, (const T*)dy,
                          (const unsigned char*)code, (T*)dx, NC, H, W, P, Q, kh, kw, sh, pt, pl, sw, act, acc, HB, nbands, G,
-                         make_fastdiv(Q), make_fastdiv(P * Q), make_fastdiv(kw), make_fastdiv(sh), pa, qa, phases ? pa * qa : 1);
+                         make_fastdiv(Q), make_fastdiv(P * Q), make_fastdiv(kw), make_fastdiv(sh));
       return;
     }
     if (lds <= 48 * 1024) {
@@ -874,18 +721,14 @@ static void fm_pool_bwd_t(const void* x, const void* y, const void* dy, void* dx
       return;
     }
   }
-  if (!per_elem) {
+  {   // past the band kernels' LDS limits: 8-wide input row segments gather their windows
     constexpr int VW = 8;
     const int WS = (W + VW - 1) / VW;
     const int rows_total = N * C * H * WS;
     hipLaunchKernelGGL((fm_pool_bwd_rows<T, VW>), dim3((rows_total + 255) / 256), dim3(256), 0, st, (const T*)y,
                        (const T*)dy, (const unsigned char*)code, (T*)dx, rows_total, make_fastdiv(WS), make_fastdiv(H),
                        make_fastdiv(sh), make_fastdiv(sw), WS, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, acc);
-    return;
   }
-  hipLaunchKernelGGL(fm_pool_bwd_kernel<T>, dim3((total + 255) / 256), dim3(256), 0, st, (const T*)y, (const T*)dy,
-                     (const unsigned char*)code, (T*)dx, total, make_fastdiv(W), make_fastdiv(H), make_fastdiv(sh),
-                     make_fastdiv(sw), H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, acc);
 }
 
 // stats / meaninv: fp32 [2C] device buffers owned by the op

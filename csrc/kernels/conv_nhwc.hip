@@ -592,9 +592,9 @@ __global__ void __launch_bounds__(256) fm_nhwc_stage_flat(const unsigned short* 
 template <bool GRAD>
 void stage_launch(const void* src, const void* y, void* dst, int act, int N, int C, int H, int W, int Cp, int Hp, int Wp, int top,
                   int left, int dh, int dw, hipStream_t s) {
-  // FM_STAGE_FLAT_BELOW (A/B, default 128; 32 / 64 / 128 measured in profiles/ab_stage_wgrad_r3y.txt): image widths below it take the flattened-pixel kernel
-  static const int flat_below = getenv("FM_STAGE_FLAT_BELOW") ? atoi(getenv("FM_STAGE_FLAT_BELOW")) : 128;
-  if (Wp < flat_below) {
+  // image widths below 128 take the flattened-pixel kernel (32 / 64 / 128 measured,
+  // profiles/ab_stage_wgrad_r3y.txt)
+  if (Wp < 128) {
     const int bpi = (Hp * Wp + 63) / 64;
     hipLaunchKernelGGL(fm_nhwc_stage_flat<GRAD>, dim3(N * bpi, (Cp + 63) / 64), dim3(256), 0, s, (const unsigned short*)src,
                        (const unsigned short*)y, (unsigned short*)dst, act, C, H, W, Cp, Hp, Wp, top, left, dh, dw, bpi);
@@ -728,8 +728,8 @@ Plan make_plan(int mode, int M, int N, int K) {
   q.tiles_n = (N + bn - 1) / bn;
   const int ktiles = (K + BK - 1) / BK;
   int ks = 1;
-  // FM_CONV_WGRAD_BLOCKS (A/B, default 512): split-K target of the weight gradient in blocks
-  static const int wg_blocks = getenv("FM_CONV_WGRAD_BLOCKS") ? std::max(1, atoi(getenv("FM_CONV_WGRAD_BLOCKS"))) : 512;
+  // split-K target of the weight gradient: 512 blocks
+  constexpr int wg_blocks = 512;
   if (mode == CN_WGRAD) ks = std::max(1, std::min(wg_blocks / std::max(q.tiles_m * q.tiles_n, 1), ktiles / 8));
   q.kt_per = (ktiles + ks - 1) / ks;
   q.ksplit = (ktiles + q.kt_per - 1) / q.kt_per;
@@ -751,15 +751,12 @@ void go(ConvN& p, const Plan& q, hipStream_t s) {
   hipLaunchKernelGGL((fm_conv_nhwc<BM, BN, MODE, NTH>), dim3(p.tiles_m * p.tiles_n, 1, p.ksplit), dim3(NTH), lds, s, p);
 }
 
-// FM_CONV_NHWC_4WAVE=1 (A/B): the 128x128 tiles as 4-wave blocks (64x64 per wave, twice the MFMAs
-// per k-tile per wave) instead of 8 waves
-static const bool g_cn_4wave = getenv("FM_CONV_NHWC_4WAVE") != nullptr && atoi(getenv("FM_CONV_NHWC_4WAVE")) == 1;
-
+// 128x128 tiles as 8-wave blocks (a 4-wave form with 64x64 per wave measured slower,
+// profiles/ab_conv_nhwc_4wave_r3v.txt)
 template <int MODE>
 int dispatch(ConvN& p, hipStream_t s) {
   const Plan q = make_plan(MODE, p.M, p.N, p.K);
-  if (q.shape == 0 && g_cn_4wave) go<128, 128, MODE, 256>(p, q, s);
-  else if (q.shape == 0) go<128, 128, MODE, 512>(p, q, s);
+  if (q.shape == 0) go<128, 128, MODE, 512>(p, q, s);
   else if (q.shape == 1) go<64, 128, MODE, 256>(p, q, s);
   else go<64, 64, MODE, 256>(p, q, s);
   return q.ksplit;

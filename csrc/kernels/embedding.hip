@@ -15,9 +15,7 @@
 // Backward (fused sparse SGD: W[idx] -= lr*scale*dy; or dense-grad accumulate when lr == null):
 //   * regular tables: one wave-instruction = 64 consecutive fp32 atomic adds (256 contiguous bytes:
 //     the full gfx950 atomic rate, MI355X_MICROARCH "Global float atomics");
-//   * small tables (<= 128 KB of fp32 rows), opt-in: one block-shared LDS copy per block with LDS
-//     atomics, flushed with one global atomic per (row, col) (measured slower, see launch site);
-//   * tiny tables (<= 16 rows: 3, 4, 10, 14 rows in the MLPerf set): thousands of samples hit the
+//   * tiny tables (<= 64 rows: 3, 4, 10, 14, 36, 63 rows in the MLPerf set): thousands of samples hit the
 //     same few addresses, which L2 serialises; each wave accumulates into a PRIVATE LDS copy of the
 //     table gradient with plain read-add-write (row index wave-uniform, lane = column: 64 distinct
 //     banks, no atomics), the block sums its waves' copies and flushes one atomic per (row, col).
@@ -294,102 +292,18 @@ __global__ void __launch_bounds__(256) fm_emb_bwd_tiny_multi(TabSet s, const flo
   }
 }
 
-// Small tables (16 < rows, rows*D*4 <= SMALL_LDS: e.g. 36..155 rows x 128 in the MLPerf set):
-// 8192 lookups pile onto a few thousand addresses, so the per-lookup global atomics of the regular
-// path serialise in L2.  Each block accumulates a chunk of samples into ONE block-shared LDS copy
-// of the table gradient (ds_add_f32: lane = column, 64 distinct banks per wave-instruction) and
-// flushes it with one global atomic per (row, col); blocks per table are sized so the flush stays
-// well below the B*D atomics it replaces.
-constexpr long SMALL_LDS = 128L << 10;
-template <typename GT, bool I64>
-__global__ void __launch_bounds__(256) fm_emb_bwd_small_multi(TabSet s, const float* __restrict__ lr, long B, int chunk) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* acc = reinterpret_cast<float*>(smem);     // [rows][D]
-  const TabDesc& d = s.t[blockIdx.y];
-  const long b0 = (long)blockIdx.x * chunk;
-  if (b0 >= B) return;                             // block-uniform
-  const long b1 = min(B, b0 + chunk);
-  const int n = d.rows * d.D;
-  for (int i = threadIdx.x; i < n; i += 256) acc[i] = 0.f;
-  __syncthreads();
-  const int lpr = d.D < 256 ? d.D : 256;
-  const int rpi = 256 / lpr;
-  const int sub = threadIdx.x / lpr, lc = threadIdx.x - sub * lpr;
-  const GT* dy = reinterpret_cast<const GT*>(d.act);
-  if (sub < rpi) {
-    for (long bb = b0 + sub; bb < b1; bb += 4L * rpi) {
-      for (int c = lc; c < d.D; c += lpr) {
-        float g[4];
-        long r0[4];
-        bool ok0[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {                // loads first (clamped: unconditional)
-          const long b = min(bb + u * rpi, b1 - 1);
-          g[u] = ld<GT>(dy + b * d.ld + c);
-          r0[u] = local_row(ldi<I64>(d.idx, b * d.bag), d.lo, d.rows, ok0[u]);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const long b = bb + u * rpi;
-          if (b >= b1) break;
-          if (ok0[u]) atomicAdd(acc + r0[u] * d.D + c, g[u]);
-          for (int j = 1; j < d.bag; ++j) {
-            bool ok;
-            const long r = local_row(ldi<I64>(d.idx, b * d.bag + j), d.lo, d.rows, ok);
-            if (ok) atomicAdd(acc + r * d.D + c, g[u]);
-          }
-        }
-      }
-    }
-  }
-  __syncthreads();
-  const float mul = (lr ? -lr[0] : 1.f) * d.scale;
-  float* W = const_cast<float*>(d.W);
-  for (int i = threadIdx.x; i < n; i += 256) {
-    const float v = acc[i];
-    if (v != 0.f) atomicAdd(W + i, v * mul);
-  }
-}
-
-template <bool I64>
-void launch_small(const TabSet& s, int m, bool dy_bf16, const float* lr, long B, hipStream_t st) {
-  size_t lds = 0;
-  long maxrows = 1, maxbag = 1;
-  for (int i = 0; i < m; ++i) {
-    lds = std::max(lds, (size_t)s.t[i].rows * s.t[i].D * 4);
-    maxrows = std::max<long>(maxrows, s.t[i].rows);
-    maxbag = std::max<long>(maxbag, s.t[i].bag);
-  }
-  static bool attr = false;
-  if (!attr) {     // > 64 KiB of dynamic LDS needs the opt-in attribute
-    (void)hipFuncSetAttribute((const void*)fm_emb_bwd_small_multi<unsigned short, I64>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)SMALL_LDS);
-    (void)hipFuncSetAttribute((const void*)fm_emb_bwd_small_multi<float, I64>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)SMALL_LDS);
-    attr = true;
-  }
-  // ~4 lookups per table row per block: enough duplication that the flush (rows*D atomics per
-  // block) costs a fraction of the per-lookup atomics it replaces
-  const long blocks = std::max(4L, std::min(32L, B * maxbag / (4 * maxrows)));
-  const int chunk = (int)((B + blocks - 1) / blocks);
-  dim3 grid((unsigned)((B + chunk - 1) / chunk), m);
-  if (dy_bf16) hipLaunchKernelGGL((fm_emb_bwd_small_multi<unsigned short, I64>), grid, dim3(256), lds, st, s, lr, B, chunk);
-  else hipLaunchKernelGGL((fm_emb_bwd_small_multi<float, I64>), grid, dim3(256), lds, st, s, lr, B, chunk);
-}
-
 template <bool I64>
 void launch_fwd(const TabSet& s, int m, bool vec, bool out_bf16, long B, int D0, hipStream_t st) {
   const int rpi = std::max(1, 256 / std::min(64, std::max(1, D0 / 4)));
   // long bags with too few samples to fill the chip: split every bag over SP lane groups
-  // (FM_EMB_FWD_SPLIT=0 disables; measured on summit_large, profiles/README.md)
-  static const bool split_ok = !(getenv("FM_EMB_FWD_SPLIT") != nullptr && atoi(getenv("FM_EMB_FWD_SPLIT")) == 0);
+  // (measured on summit_large, profiles/README.md)
   int minbag = 1 << 30, maxD = 0, minD = 1 << 30;
   for (int i = 0; i < m; ++i) {
     minbag = std::min(minbag, s.t[i].bag);
     maxD = std::max(maxD, s.t[i].D);
     minD = std::min(minD, s.t[i].D);
   }
-  if (split_ok && vec && maxD == minD && maxD <= 256 && minbag >= 16 && (B + rpi - 1) / rpi * m < 1024) {
+  if (vec && maxD == minD && maxD <= 256 && minbag >= 16 && (B + rpi - 1) / rpi * m < 1024) {
     int sp = 1;
     while (sp * 2 <= rpi && sp * 2 <= minbag / 4 && (B * sp * 2 + rpi - 1) / rpi * m <= 2048) sp *= 2;
     if (sp > 1) {
@@ -400,13 +314,12 @@ void launch_fwd(const TabSet& s, int m, bool vec, bool out_bf16, long B, int D0,
       return;
     }
   }
-  // FM_EMB_FWD_BLOCKS: blocks per table (default 256).  The forward runs beside the bottom MLP on
-  // a second stream; fewer, longer-running blocks leave CUs to its GEMMs: MLPerf fp32 step 1.181 ms
-  // at 2048 blocks per table, 1.164 at 256, 1.172 at 64 (profiles/bench_ab_x3_sched_embgrid_r5n.txt)
-  static const long cap_env = getenv("FM_EMB_FWD_BLOCKS") ? std::max(1L, atol(getenv("FM_EMB_FWD_BLOCKS"))) : 256L;
-  dim3 grid((unsigned)std::max<long>(1, std::min<long>((B + rpi - 1) / rpi, cap_env)), m);
-  // FM_EMB_FWD_SU=0: one sample per lane-group iteration for single-lookup bags (A/B)
-  static const int su = !(getenv("FM_EMB_FWD_SU") != nullptr && atoi(getenv("FM_EMB_FWD_SU")) == 0);
+  // 256 blocks per table: the forward runs beside the bottom MLP on a second stream; fewer,
+  // longer-running blocks leave CUs to its GEMMs: MLPerf fp32 step 1.181 ms at 2048 blocks per
+  // table, 1.164 at 256, 1.172 at 64 (profiles/bench_ab_x3_sched_embgrid_r5n.txt).  Single-lookup
+  // bags take two samples per lane-group iteration (su; profiles/bench_ab_emb_fwd_su_r5zc.txt)
+  dim3 grid((unsigned)std::max<long>(1, std::min<long>((B + rpi - 1) / rpi, 256L)), m);
+  const int su = 1;
   if (vec) {
     if (out_bf16) hipLaunchKernelGGL((fm_emb_fwd_multi<unsigned short, I64>), grid, dim3(256), 0, st, s, B, su);
     else hipLaunchKernelGGL((fm_emb_fwd_multi<float, I64>), grid, dim3(256), 0, st, s, B, su);
@@ -577,12 +490,8 @@ void launch_count(const ClaimSet& s, int m, bool dy_bf16, const float* lr, long 
   else hipLaunchKernelGGL((fm_emb_update_multi<float, I64>), gu, dim3(256), 0, st, s, lr, B);
 }
 
-// FM_EMB_BWD_BLOCKS: cap on the blocks per table of the grid-stride backward kernels (claim / dup /
-// owner / atomic; 0 = uncapped).  They run beside the bottom-MLP backward GEMMs on a second stream.
-long emb_bwd_cap(long want) {
-  static const long cap = getenv("FM_EMB_BWD_BLOCKS") ? std::max(0L, atol(getenv("FM_EMB_BWD_BLOCKS"))) : 0L;
-  return cap > 0 ? std::min(want, cap) : want;
-}
+// blocks per table of the grid-stride backward kernels (claim / dup / owner / atomic): uncapped
+long emb_bwd_cap(long want) { return want; }
 
 template <bool I64>
 void launch_claim(const ClaimSet& s, int m, bool dy_bf16, const float* lr, long B, int maxbag, int minD4,
@@ -605,7 +514,6 @@ void launch_bwd(const TabSet& s, int m, bool tiny, bool dy_bf16, const float* lr
   if (tiny) {
     size_t lds = 0;
     for (int i = 0; i < m; ++i) lds = std::max(lds, (size_t)s.t[i].rows * s.t[i].D * 4 * 4);  // one copy per wave
-    static const int env_chunk = getenv("FM_TINY_CHUNK") ? atoi(getenv("FM_TINY_CHUNK")) : 0;
     static bool attr = false;
     if (!attr) {   // > 64 KiB of dynamic LDS (FM_EMB_TINY_ROWS above 32 at D = 128) needs the opt-in
       (void)hipFuncSetAttribute((const void*)fm_emb_bwd_tiny_multi<unsigned short, I64>,
@@ -617,7 +525,7 @@ void launch_bwd(const TabSet& s, int m, bool tiny, bool dy_bf16, const float* lr
     // 64-sample chunks keep the per-wave chain to one round trip; at large B more blocks would
     // pile onto the same few addresses in the flush (tools/bench_embedding.py: B=8192 -> 64,
     // B=65536 -> 128..256)
-    const int chunk = env_chunk > 0 ? env_chunk : (B <= 16384 ? 64 : B <= 32768 ? 128 : 256);
+    const int chunk = B <= 16384 ? 64 : B <= 32768 ? 128 : 256;
     dim3 grid((unsigned)((B + chunk - 1) / chunk), m);
     if (dy_bf16) hipLaunchKernelGGL((fm_emb_bwd_tiny_multi<unsigned short, I64>), grid, dim3(256), lds, st, s, lr, B, chunk);
     else hipLaunchKernelGGL((fm_emb_bwd_tiny_multi<float, I64>), grid, dim3(256), lds, st, s, lr, B, chunk);
@@ -626,176 +534,6 @@ void launch_bwd(const TabSet& s, int m, bool tiny, bool dy_bf16, const float* lr
     dim3 grid((unsigned)std::max<long>(1, emb_bwd_cap(std::min<long>((B + rpi - 1) / rpi, 2048))), m);
     if (dy_bf16) hipLaunchKernelGGL((fm_emb_bwd_atomic_multi<unsigned short, I64>), grid, dim3(256), 0, st, s, lr, B);
     else hipLaunchKernelGGL((fm_emb_bwd_atomic_multi<float, I64>), grid, dim3(256), 0, st, s, lr, B);
-  }
-}
-
-// ---- row-block ownership (tables of up to ~64 LDS blocks of rows: 3 .. 8192 rows x 128) --------
-// Every block OWNS a range of RR table rows (RR*D*4 <= 64 KiB) and one chunk of the lookups: it
-// scans the chunk's indices (L2-resident, read by every row block of the table), compacts the
-// lookups that hit its rows into an LDS list (wave ballot), adds their gradient rows into an LDS
-// copy of its rows (each wave owns a quarter of the rows: lane = column, plain read-add-write in
-// list order, 8 lookups' loads in flight) and applies the result once.  With one chunk the block is the rows' only
-// writer and the apply is a plain read-modify-write; tables with so few rows that one block would
-// serialise thousands of lookups (3 .. 155 rows) split the lookups over up to 32 chunks and flush
-// with one float atomic per (row, col, chunk).  Replaces both the per-lookup global atomics (which
-// pile onto the same addresses for 36 .. 8192-row tables and run at the L2 atomic rate) and the
-// tiny-table kernel: no global atomics at all for the mid-size tables.
-struct RbDesc {
-  float* W;
-  const void* idx;
-  const void* dy;
-  long ld;
-  long lo;
-  int rows, D, bag;
-  float scale;
-  int rr;       // rows per block
-  int chunks;   // lookup chunks per row block
-  int first;    // first blockIdx.x of this table
-};
-struct RbSet {
-  RbDesc t[MAXT];
-  int n;
-};
-constexpr int RB_LDS = 64 << 10;
-constexpr int RB_SCAN = 2048;   // lookups scanned per round (8 per thread, loads issued together)
-
-template <typename GT, bool I64, int NQ>
-__global__ void __launch_bounds__(256) fm_emb_bwd_rowblock(RbSet s, const float* __restrict__ lr, long B) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ int le[RB_SCAN];
-  __shared__ short lrow[RB_SCAN];
-  __shared__ int nlist;
-  int ti = 0;
-  for (int i = 1; i < s.n; ++i)
-    if ((int)blockIdx.x >= s.t[i].first) ti = i;
-  const RbDesc& d = s.t[ti];
-  const int local = (int)blockIdx.x - d.first;
-  const int rbi = local / d.chunks, ci = local - rbi * d.chunks;
-  const long r0 = (long)rbi * d.rr;
-  const int nr = (int)min((long)d.rr, (long)d.rows - r0);
-  if (nr <= 0) return;                                   // block-uniform
-  const int D = d.D, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  float* acc = reinterpret_cast<float*>(smem);           // [nr][D]
-  for (int i = tid; i < nr * D; i += 256) acc[i] = 0.f;
-  const long n = B * d.bag;
-  const long per = (n + d.chunks - 1) / d.chunks;
-  const long e0 = (long)ci * per, e1 = min(n, e0 + per);
-  const GT* dy = reinterpret_cast<const GT*>(d.dy);
-  constexpr int PT = RB_SCAN / 256;
-  constexpr int U = 8;
-  for (long base = e0; base < e1; base += RB_SCAN) {
-    if (tid == 0) nlist = 0;
-    __syncthreads();
-    long rv[PT];
-#pragma unroll
-    for (int u = 0; u < PT; ++u) rv[u] = ldi<I64>(d.idx, min(base + u * 256 + tid, e1 - 1));   // clamped
-#pragma unroll
-    for (int u = 0; u < PT; ++u) {
-      const long e = base + u * 256 + tid;
-      const long l = rv[u] - d.lo - r0;
-      const bool m = e < e1 && (unsigned long)l < (unsigned long)nr;
-      const unsigned long long mask = __ballot(m);
-      int wb = 0;
-      if (lane == 0 && mask) wb = atomicAdd(&nlist, __popcll(mask));
-      wb = __shfl(wb, 0);
-      if (m) {
-        const int pos = wb + __popcll(mask & ((1ull << lane) - 1ull));
-        le[pos] = (int)e;
-        lrow[pos] = (short)l;
-      }
-    }
-    __syncthreads();
-    const int nm = nlist;
-    // wave w owns the block's rows with lrow % 4 == w and applies its lookups with plain LDS
-    // read-add-writes in list order (no LDS float atomics: ds_add_f32 ran ~5x slower than the
-    // global-atomic kernel it replaced, gpurun_out r5t); U lookups' gradient loads in flight
-    for (int j0 = 0; j0 < nm; j0 += 64) {
-      const int jr = min(j0 + lane, nm - 1);
-      const int lrj = lrow[jr], lej = le[jr];
-      unsigned long long mine = __ballot(j0 + lane < nm && (lrj & 3) == wave);
-      while (mine) {                                     // wave-uniform
-        int rw[U];
-        float g[U][NQ];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int sl = mine ? __builtin_ctzll(mine) : 0;
-          rw[u] = mine ? __builtin_amdgcn_readlane(lrj, sl) : -1;
-          mine &= mine - 1;                              // 0 stays 0
-          const int e = __builtin_amdgcn_readlane(lej, sl);
-          const long b = d.bag == 1 ? (long)e : (long)(e / d.bag);
-#pragma unroll
-          for (int q = 0; q < NQ; ++q) g[u][q] = ld<GT>(dy + b * d.ld + min(lane + 64 * q, D - 1));
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (rw[u] < 0) break;                          // wave-uniform
-          float* a = acc + rw[u] * D;
-#pragma unroll
-          for (int q = 0; q < NQ; ++q)
-            if (lane + 64 * q < D) a[lane + 64 * q] += g[u][q];
-        }
-      }
-    }
-    __syncthreads();                                     // the list is rebuilt next round
-  }
-  const float mul = (lr ? -lr[0] : 1.f) * d.scale;
-  float* W = d.W + r0 * D;
-  if (d.chunks == 1) {                                   // sole writer of these rows
-    for (int i = tid; i < nr * D; i += 256) {
-      const float v = acc[i];
-      if (v != 0.f) W[i] += v * mul;
-    }
-  } else {
-    for (int i = tid; i < nr * D; i += 256) {
-      const float v = acc[i];
-      if (v != 0.f) atomicAdd(W + i, v * mul);
-    }
-  }
-}
-
-// rows per block and lookup chunks of a table on the row-block path (false: not eligible)
-bool rowblock_shape(int rows, int D, long n, int& rr, int& chunks) {
-  if (D <= 0 || D > 256 || rows <= 0 || n <= 0) return false;
-  rr = std::min(rows, std::min(RB_LDS / (D * 4), 32767));
-  const long rbn = (rows + rr - 1) / rr;
-  if (rbn > 64) return false;                            // every row block rescans all lookups
-  // ~256 lookups per block; a split chunk costs one flush atomic per (row, col)
-  chunks = (int)std::max(1L, std::min(32L, n / (rbn * 256)));
-  if (chunks > 1 && (long)chunks * rows * 4 > n) chunks = std::max(1L, n / (4L * rows));
-  return true;
-}
-
-template <bool I64>
-void launch_rowblock(RbSet& s, int m, bool dy_bf16, const float* lr, long B, hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)fm_emb_bwd_rowblock<unsigned short, I64, 2>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, RB_LDS);
-    (void)hipFuncSetAttribute((const void*)fm_emb_bwd_rowblock<float, I64, 2>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, RB_LDS);
-    (void)hipFuncSetAttribute((const void*)fm_emb_bwd_rowblock<unsigned short, I64, 4>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, RB_LDS);
-    (void)hipFuncSetAttribute((const void*)fm_emb_bwd_rowblock<float, I64, 4>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, RB_LDS);
-    attr = true;
-  }
-  int blocks = 0, maxD = 1;
-  size_t lds = 0;
-  for (int i = 0; i < m; ++i) {
-    s.t[i].first = blocks;
-    blocks += (s.t[i].rows + s.t[i].rr - 1) / s.t[i].rr * s.t[i].chunks;
-    lds = std::max(lds, (size_t)std::min(s.t[i].rr, s.t[i].rows) * s.t[i].D * 4);
-    maxD = std::max(maxD, s.t[i].D);
-  }
-  s.n = m;
-  if (blocks <= 0) return;
-  const dim3 grid(blocks);
-  if (maxD <= 128) {
-    if (dy_bf16) hipLaunchKernelGGL((fm_emb_bwd_rowblock<unsigned short, I64, 2>), grid, dim3(256), lds, st, s, lr, B);
-    else hipLaunchKernelGGL((fm_emb_bwd_rowblock<float, I64, 2>), grid, dim3(256), lds, st, s, lr, B);
-  } else {
-    if (dy_bf16) hipLaunchKernelGGL((fm_emb_bwd_rowblock<unsigned short, I64, 4>), grid, dim3(256), lds, st, s, lr, B);
-    else hipLaunchKernelGGL((fm_emb_bwd_rowblock<float, I64, 4>), grid, dim3(256), lds, st, s, lr, B);
   }
 }
 
@@ -949,8 +687,6 @@ extern "C" void fm_embedding_fwd_multi(int n, const float* const* W, const void*
 
 static int g_emb_count = -1;   // -1: from FM_EMB_BWD at the first call
 extern "C" void fm_embedding_set_bwd_mode(int count) { g_emb_count = count ? 1 : 0; }
-static int g_emb_rowblock = -1;  // -1: from FM_EMB_ROWBLOCK at the first call
-extern "C" void fm_embedding_set_rowblock(int on) { g_emb_rowblock = on ? 1 : 0; }
 
 // lr != nullptr: fused sparse SGD into W; lr == nullptr: W is a dense grad buffer (accumulate).
 extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const* idx, const int* idx64,
@@ -992,42 +728,9 @@ extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const
       }
     }
   }
-  // kind: 0 tiny (wave-private LDS copies), 1 small (block-shared LDS copy), 2 regular (atomics)
-  // small path OPT-IN (FM_EMB_SMALL=1): on the MLPerf step it measured 113 us for the four 36..155-row
-  // tables against 16.6 us of regular atomics (profiles/README.md): with 1 block/CU of LDS and ~13
-  // blocks per table the serial LDS atomics are latency-bound, and more blocks multiply the flush
-  static const bool small_on = getenv("FM_EMB_SMALL") != nullptr && atoi(getenv("FM_EMB_SMALL")) == 1;
-  // row-block ownership for the other tables small enough: OPT-IN (FM_EMB_ROWBLOCK=1).  Measured
-  // slower than the atomic / tiny kernels on the MLPerf set at B = 8192 (tools/bench_emb_bwd.py,
-  // profiles/emb_bwd_rowblock_r5u.jsonl: 76 vs 48 us for the 13 tables of <= 8192 rows; a 976-row
-  // table alone 47 vs 6 us): ~16 blocks per table leave each wave a serial chain of gradient-row
-  // loads and LDS read-add-writes, where the atomic kernel spreads 1 M fire-and-forget atomics over
-  // 2048 blocks.  (Its first form, LDS float atomics, ran 199 us: ds_add_f32 is slow.)
-  if (g_emb_rowblock < 0) g_emb_rowblock = getenv("FM_EMB_ROWBLOCK") != nullptr && atoi(getenv("FM_EMB_ROWBLOCK")) == 1;
-  const bool rb_on = g_emb_rowblock == 1;
-  std::vector<char> on_rb(n, 0);
-  if (rb_on) {
-    for (int wide = 0; wide < 2; ++wide) {
-      RbSet s;
-      int m = 0;
-      for (int k = 0; k < n; ++k) {
-        if (claimable(k) || (idx64[k] != 0) != (wide != 0)) continue;
-        int rr = 0, chunks = 0;
-        if (!rowblock_shape(rows[k], D[k], B * (long)bag[k], rr, chunks)) continue;
-        on_rb[k] = 1;
-        s.t[m++] = RbDesc{W[k], idx[k], dy[k], ldg[k], lo ? lo[k] : 0, rows[k], D[k], bag[k], scale[k], rr, chunks, 0};
-        if (m == MAXT) {
-          if (wide) launch_rowblock<true>(s, m, dy_bf16, lr, B, st);
-          else launch_rowblock<false>(s, m, dy_bf16, lr, B, st);
-          m = 0;
-        }
-      }
-      if (m > 0) {
-        if (wide) launch_rowblock<true>(s, m, dy_bf16, lr, B, st);
-        else launch_rowblock<false>(s, m, dy_bf16, lr, B, st);
-      }
-    }
-  }
+  // kind: 0 tiny (wave-private LDS copies), 2 regular (atomics).  Measured and deleted in r6: a
+  // block-shared LDS copy for 36..155-row tables (113 vs 16.6 us of regular atomics) and row-block
+  // ownership for <= 8192-row tables (76 vs 48 us; profiles/emb_bwd_rowblock_r5u.jsonl)
   auto kind_of = [&](int k) {
     // FM_EMB_TINY_ROWS (default 64): the wave-private LDS kernel up to that many rows while its four
     // copies fit the LDS (rows * D * 16 B).  64 takes the 36- and 63-row MLPerf tables off the
@@ -1038,15 +741,14 @@ extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const
     if (rows[k] <= tiny_rows && (long)rows[k] * D[k] * 16 <= (160L << 10) && D[k] <= 256 &&
         B * (long)bag[k] >= 16L * rows[k])
       return 0;
-    if (small_on && (long)rows[k] * D[k] * 4 <= SMALL_LDS && D[k] <= 256 && B * (long)bag[k] >= 8L * rows[k]) return 1;
     return 2;
   };
-  for (int pass = 0; pass < 6; ++pass) {
-    const int kind = pass >> 1;
+  for (int pass = 0; pass < 4; ++pass) {
+    const int kind = (pass >> 1) * 2;
     const bool tiny = kind == 0, wide = pass & 1;
     std::vector<int> sel;
     for (int k = 0; k < n; ++k) {
-      if (claimable(k) || on_rb[k]) continue;
+      if (claimable(k)) continue;
       if (kind_of(k) == kind && (idx64[k] != 0) == wide) sel.push_back(k);
     }
     for (size_t base = 0; base < sel.size(); base += MAXT) {
@@ -1059,10 +761,7 @@ extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const
         maxD = std::max(maxD, D[k]);
       }
       s.n = m;
-      if (kind == 1) {
-        if (wide) launch_small<true>(s, m, dy_bf16, lr, B, st);
-        else launch_small<false>(s, m, dy_bf16, lr, B, st);
-      } else if (wide) {
+      if (wide) {
         launch_bwd<true>(s, m, tiny, dy_bf16, lr, B, maxD, st);
       } else {
         launch_bwd<false>(s, m, tiny, dy_bf16, lr, B, maxD, st);

@@ -279,10 +279,6 @@ __global__ void fm_gemm_splitk_reduce4(GemmP p) {
 
 }  // namespace
 
-// split-K reduce off the critical path (gemm_async.hip)
-extern "C" void fm_gemm_join(hipStream_t s);
-extern "C" hipStream_t fm_gemm_async_fork(hipStream_t s);
-extern "C" void fm_gemm_async_forked(hipStream_t side);
 
 namespace {
 
@@ -290,15 +286,13 @@ void launch_splitk_reduce(const GemmP& p, hipStream_t stream) {
   const long total = (long)p.M * p.N * p.batch;
   const bool v4 = p.c_fp32 && (p.N % 4 == 0) && (p.ldc % 4 == 0) && (p.sC % 4 == 0) &&
                   ((((uintptr_t)p.C) & 15) == 0);
-  hipStream_t rs = fm_gemm_async_fork(stream);
   if (p.uw) {
-    if (v4) hipLaunchKernelGGL(fm_gemm_splitk_reduce4<true>, dim3(fm_grid(total / 4)), dim3(256), 0, rs, p);
-    else hipLaunchKernelGGL(fm_gemm_splitk_reduce<true>, dim3(fm_grid(total)), dim3(256), 0, rs, p);
+    if (v4) hipLaunchKernelGGL(fm_gemm_splitk_reduce4<true>, dim3(fm_grid(total / 4)), dim3(256), 0, stream, p);
+    else hipLaunchKernelGGL(fm_gemm_splitk_reduce<true>, dim3(fm_grid(total)), dim3(256), 0, stream, p);
   } else {
-    if (v4) hipLaunchKernelGGL(fm_gemm_splitk_reduce4<false>, dim3(fm_grid(total / 4)), dim3(256), 0, rs, p);
-    else hipLaunchKernelGGL(fm_gemm_splitk_reduce<false>, dim3(fm_grid(total)), dim3(256), 0, rs, p);
+    if (v4) hipLaunchKernelGGL(fm_gemm_splitk_reduce4<false>, dim3(fm_grid(total / 4)), dim3(256), 0, stream, p);
+    else hipLaunchKernelGGL(fm_gemm_splitk_reduce<false>, dim3(fm_grid(total)), dim3(256), 0, stream, p);
   }
-  if (rs != stream) fm_gemm_async_forked(rs);
 }
 
 template <bool SGD>
@@ -374,8 +368,6 @@ __global__ void __launch_bounds__(256) fm_gemm_splitk_reduce_bwd(GemmP p, int RB
   }
 }
 
-static int g_gemm_variant_early();
-
 template <int BM, int BN, bool AK, bool BKC, bool VEC>
 void launch_t(const GemmP& p, hipStream_t s) {
   constexpr int LDS = 2 * (BM + BN) * BK * 2;
@@ -383,23 +375,18 @@ void launch_t(const GemmP& p, hipStream_t s) {
   if constexpr (!AK && !BKC) {   // fused-SGD dW GEMMs (both operands MN-contiguous): own instantiation
     if (p.uw) {
       if constexpr (VEC && BM == 128) {
-        if (!(g_gemm_variant_early() & 256)) {
-          hipLaunchKernelGGL((fm_gemm_kernel<BM, BN, AK, BKC, VEC, 512, true>), grid, dim3(512), LDS, s, p);
-          return;
-        }
+        hipLaunchKernelGGL((fm_gemm_kernel<BM, BN, AK, BKC, VEC, 512, true>), grid, dim3(512), LDS, s, p);
+        return;
       }
       hipLaunchKernelGGL((fm_gemm_kernel<BM, BN, AK, BKC, VEC, NT, true>), grid, dim3(NT), LDS, s, p);
       return;
     }
   }
-  // default: the 8-wave form of the 128-row tiles (4 waves per SIMD hide the per-K-tile barrier and
-  // fragment latency: DLRM GEMMs -6 %, bf16 step 0.673 -> 0.626 ms, profiles/gemm_bf16_8wave_ab.jsonl);
-  // variant bit 256 = the 4-wave kernel
+  // the 8-wave form of the 128-row tiles (4 waves per SIMD hide the per-K-tile barrier and
+  // fragment latency: DLRM GEMMs -6 %, bf16 step 0.673 -> 0.626 ms, profiles/gemm_bf16_8wave_ab.jsonl)
   if constexpr (VEC && BM == 128) {
-    if (!(g_gemm_variant_early() & 256)) {
-      hipLaunchKernelGGL((fm_gemm_kernel<BM, BN, AK, BKC, VEC, 512>), grid, dim3(512), LDS, s, p);
-      return;
-    }
+    hipLaunchKernelGGL((fm_gemm_kernel<BM, BN, AK, BKC, VEC, 512>), grid, dim3(512), LDS, s, p);
+    return;
   }
   hipLaunchKernelGGL((fm_gemm_kernel<BM, BN, AK, BKC, VEC>), grid, dim3(NT), LDS, s, p);
 }
@@ -420,49 +407,6 @@ void launch_bm(const GemmP& p, bool ak, bool bk, bool vec, hipStream_t s) {
 }
 
 }  // namespace
-
-extern "C" void fm_gemm_glds_launch(const void* params, int bm, int bn, int a_kcontig, int b_kcontig, int prio,
-                                    int wide, hipStream_t stream);
-extern "C" int fm_gemm_x1_launch(const void* params, int bm, int a_kcontig, int b_kcontig, int sgd, hipStream_t s);
-
-// dispatch experiments (tools/gemm_probe.py): 1 = never glds, 2 = glds for every orientation and
-// grid size (K % 64 == 0), 4 = glds 128x128 tiles, 8 = s_setprio around the glds MFMA blocks,
-// 64 = 256x128 glds tile with 4 waves of 128x64, 128 = in-launch split-K combine (split_counters),
-// 256 = 4-wave register-staged kernel instead of the 8-wave default
-static int g_gemm_variant = getenv("FM_GEMM_VARIANT") ? atoi(getenv("FM_GEMM_VARIANT")) : 0;
-namespace {
-int g_gemm_variant_early() { return g_gemm_variant; }
-}
-
-// Per-device tile arrival counters of the in-launch split-K combine (gemm_common.h): zeroed once
-// at allocation; each tile's last arriver resets its own counter, so consecutive launches on the
-// stream reuse them (like the shared slab workspace, split-K GEMMs are stream-ordered).  Never
-// allocated inside a stream capture: a capture before any eager split-K launch keeps the reduce
-// kernel.  OPT-IN (variant bit 128 or FM_GEMM_FUSED_SPLITK=1): measured on the DLRM MLPerf step
-// it is SLOWER than the separate reduce launch (0.96 vs 0.755 ms/step, profiles/README.md): each
-// tile's last arriver pays the agent acquire and then reads the other slices' 32-64 KB sc1 slabs
-// serially at the cross-XCD rate, which costs more than the latency-bound reduce kernel it saves.
-static int* split_counters(hipStream_t s, long n, long slab_bytes) {
-  static const bool env_on = getenv("FM_GEMM_FUSED_SPLITK") != nullptr && atoi(getenv("FM_GEMM_FUSED_SPLITK")) == 1;
-  constexpr long CAP = 1L << 16;
-  static int* cnt[64] = {nullptr};
-  if (!(env_on || (g_gemm_variant & 128)) || n > CAP || slab_bytes >= (1L << 31)) return nullptr;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (cnt[dev] == nullptr) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-    int* q = nullptr;
-    if (hipMalloc(&q, CAP * sizeof(int)) != hipSuccess) return nullptr;
-    if (hipMemset(q, 0, CAP * sizeof(int)) != hipSuccess) {
-      (void)hipFree(q);
-      return nullptr;
-    }
-    cnt[dev] = q;
-  }
-  return cnt[dev];
-}
-extern "C" void fm_gemm_set_variant(int v) { g_gemm_variant = v; }
 
 // A_kcontig: A stored [M][K] (lda >= K) else [K][M] (lda >= M)
 // B_kcontig: B stored [N][K] (ldb >= K) else [K][N] (ldb >= N)
@@ -512,7 +456,6 @@ static int gemm_run(const void* A, long lda, long sA, int a_kcontig,
   if (upd && (K <= 0 || ldc % 4 != 0 || (((uintptr_t)upd->w | (uintptr_t)(upd->v ? upd->v : upd->w)) & 15) ||
               (((uintptr_t)(upd->wc ? (void*)upd->wc : (void*)upd->w)) & 7)))
     return -1;                         // the caller computes the gradient and runs the update itself
-  if (beta) fm_gemm_join(stream);      // C may be a gradient an async reduce is still writing
   GemmP p;
   p.A = (const unsigned short*)A; p.lda = lda; p.sA = sA;
   p.B = (const unsigned short*)B; p.ldb = ldb; p.sB = sB;
@@ -521,8 +464,6 @@ static int gemm_run(const void* A, long lda, long sA, int a_kcontig,
   p.alpha = alpha; p.batch = batch; p.ws = ws;
   p.ay = (const unsigned short*)act_y; p.lday = lday; p.bact = bwd_act; p.colsum = colsum; p.rowsum_a = rowsum_a;
   p.n_fast = M >= N;
-  p.atomic_c = 0;
-  p.tile_cnt = nullptr;
   p.uw = upd ? upd->w : nullptr;
   p.uwc = upd ? upd->wc : nullptr;
   p.uv = upd ? upd->v : nullptr;
@@ -530,96 +471,11 @@ static int gemm_run(const void* A, long lda, long sA, int a_kcontig,
   p.uwd = upd ? upd->wd : 0.f;
   p.umom = upd ? upd->mom : 0.f;
   p.unest = upd ? upd->nest : 0;
-  // A/B knob FM_SGD_EPI_DIRECT=1: the update straight from the accumulator layout (no LDS staging)
-  static const bool sgd_direct = getenv("FM_SGD_EPI_DIRECT") != nullptr && atoi(getenv("FM_SGD_EPI_DIRECT")) == 1;
-  p.ulds = upd && !sgd_direct;
-  // opt-in (FM_GEMM_ATOMIC_SPLIT=1): split-K partial tiles added straight into a small fp32
-  // accumulating C with float atomics, no slabs and no reduce launch.  Measured SLOWER on the
-  // DLRM dW GEMMs (profiles/README.md): the 16x16 accumulator layout issues 4-B atomics over 16
-  // rows per wave-instruction, far below the 256-contiguous-byte atomic rate.
-  static const long atomic_max = getenv("FM_GEMM_ATOMIC_SPLIT") ? (getenv("FM_GEMM_ATOMIC_MAX") ? atol(getenv("FM_GEMM_ATOMIC_MAX"))
-                                                                                                : (256L << 10))
-                                                                 : 0L;
-  const bool atomic_ok = !upd && c_fp32 && beta && bias == nullptr && act == 10 && act_y == nullptr && colsum == nullptr &&
-                         (long)M * N <= atomic_max;
+  p.ulds = upd != nullptr;   // the update staged through LDS (whole-row W accesses, gemm.hip sgd_epilogue_lds)
   // vector (16-B) loads need the contiguous extent and leading dims to be multiples of 8
   auto al = [](const void* q) { return (((uintptr_t)q) & 15) == 0; };
   bool vec = al(A) && al(B) && (lda % 8 == 0) && (ldb % 8 == 0) && (sA % 8 == 0) && (sB % 8 == 0);
   vec = vec && (a_kcontig ? (K % 8 == 0) : (M % 8 == 0)) && (b_kcontig ? (K % 8 == 0) : (N % 8 == 0));
-  // big-tile kernel (gemm_x1.hip: 256x128 tiles of 8 64x64 waves, loads two steps ahead) for grids
-  // that fill the chip, K split to get there.  OPT-IN (FM_GEMM_X1=1; variant bit 512 forces it
-  // wherever it applies, bit 1024 disables it; FM_GEMM_X1_MIN = blocks (tiles x splits) it needs,
-  // default 192): measured slower than this file's 128x128 8-wave kernel on every DLRM shape --
-  // 8192x1024x1024 fwd / dX / dW 32.7 / 32.5 / 40.3 vs 29.8 / 27.5 / 39.5 us, bf16 step 0.733 vs
-  // 0.627 ms with its first 32-deep form (profiles/gemm_bf16_x1_ab_r5x.jsonl, bench_ab_x1_r5w.txt):
-  // one block of 8 waves per CU leaves too little MFMA work per barrier to hide the staging
-  {
-    static const int x1_env = getenv("FM_GEMM_X1") ? atoi(getenv("FM_GEMM_X1")) : 0;
-    static const long x1_min = getenv("FM_GEMM_X1_MIN") ? atol(getenv("FM_GEMM_X1_MIN")) : 192L;
-    const bool force = (g_gemm_variant & 512) != 0;
-    const bool off = (x1_env == 0 && !force) || (g_gemm_variant & 1024) != 0;
-    if (!off && vec && !atomic_ok && K > 0 && K % 64 == 0 && M >= 64 && N >= 64) {
-      const int bm = M >= 256 ? 256 : 128;
-      GemmP q = p;
-      q.tiles_m = (M + bm - 1) / bm;
-      q.tiles_n = (N + 127) / 128;
-      const long tiles = (long)q.tiles_m * q.tiles_n * batch;
-      const int ktiles = K / 64;
-      int ks = 1;
-      if (ksplit_req > 0) ks = ksplit_req;
-      else if (ws != nullptr) {
-        while (tiles * ks < 256 && ks * 2 <= ktiles / 4 && ks < 16) ks *= 2;
-      }
-      if (act_y != nullptr || colsum != nullptr) ks = 1;       // fused epilogue needs the full sum
-      while (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks /= 2;
-      if (ks <= ktiles && (force || tiles * ks >= x1_min)) {
-        q.ksplit = ks;
-        q.atomic_c = 0;
-        q.tile_cnt = nullptr;
-        if (ks > 1) fm_gemm_join(stream);  // the slab workspace is shared
-        if (fm_gemm_x1_launch(&q, bm, a_kcontig, b_kcontig, upd != nullptr && ks == 1, stream) == 0) {
-          if (ks > 1) launch_splitk_reduce(q, stream);
-          return ks;
-        }
-      }
-    }
-  }
-  // LDS-DMA pipelined kernel (gemm_glds.hip) whenever K-tiles are whole
-  static const bool no_glds_env = getenv("FM_GEMM_NO_GLDS") != nullptr;
-  const bool no_glds = no_glds_env || (g_gemm_variant & 1);
-  const bool glds_any = (g_gemm_variant & 2) != 0;
-  // (measured, tools/bench_gemm.py in hipGraph mode: the pipelined kernel wins for K-contiguous
-  // operands once 256x128 tiles fill the chip; MN-contiguous (transposed-read) operands and small
-  // grids stay on the register-staged kernel's 128x64/128x128 tiles)
-  // (in the DLRM step, where the 1024-wide layers give exactly 256 such tiles, the register kernel's
-  // 512 blocks of 128x128 beat one wave of 256x128 glds blocks: 11.07 vs 10.86 M samples/s,
-  // profiles/README.md -- so glds starts at two waves of its tiles)
-  const long t256 = (long)((M + 255) / 256) * ((N + 127) / 128) * batch;
-  if (vec && !no_glds && !upd && K > 0 && K % BK == 0 && M >= 8 && N >= 8 &&
-      ((a_kcontig && b_kcontig && t256 >= 512) || glds_any)) {
-    const int bm = ((g_gemm_variant & 4) || t256 < 256) ? 128 : 256;
-    p.tiles_m = (M + bm - 1) / bm;
-    p.tiles_n = (N + 127) / 128;
-    const long tiles = (long)p.tiles_m * p.tiles_n * batch;
-    const int ktiles = K / BK;
-    int ks = 1;
-    if (ksplit_req > 0) ks = ksplit_req;
-    else if (ws != nullptr) {
-      while (tiles * ks < 200 && ks * 2 <= ktiles / 4 && ks < 16) ks *= 2;
-    }
-    if (act_y != nullptr || colsum != nullptr) ks = 1;
-    if (ks > 1 && !atomic_ok && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks = 1;
-    p.ksplit = ks;
-    p.atomic_c = ks > 1 && atomic_ok;
-    if (ks > 1) fm_gemm_join(stream);  // the slab workspace is shared
-    if (p.ksplit > 1 && !p.atomic_c) p.tile_cnt = split_counters(stream, tiles, (long)M * N * 4);
-    fm_gemm_glds_launch(&p, bm, 128, a_kcontig, b_kcontig, (g_gemm_variant & 8) ? 1 : 0, (g_gemm_variant & 64) ? 1 : 0,
-                        stream);
-    if (p.ksplit > 1 && !p.atomic_c && p.tile_cnt == nullptr) {
-      launch_splitk_reduce(p, stream);
-    }
-    return p.ksplit;
-  }
   // tile choice: 128x128 when it yields >= 2 waves of blocks on 256 CUs, else narrower N
   int BMv = 128, BNv = 128;
   long t128 = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;
@@ -628,47 +484,39 @@ static int gemm_run(const void* A, long lda, long sA, int a_kcontig,
       // resident per CU where 128x64 gives at most one wave of blocks; long-K GEMMs (dW, K =
       // batch) keep the bigger tile and split K instead
     long t12864 = (long)((M + 127) / 128) * ((N + 63) / 64) * batch;
-    if (BNv == 64 && t12864 <= 256 && K <= 1024 && !(g_gemm_variant & 16)) BMv = 64;
+    if (BNv == 64 && t12864 <= 256 && K <= 1024) BMv = 64;
   }
   // few 128x128 tiles and a short K (small-batch layers, e.g. DLRM run_random at 256 samples
   // per GPU): 64x64 tiles give 4x the blocks without split-K slabs (measured +26 % step rate)
-  if (t128 < 128 && K <= 2048 && !(g_gemm_variant & 16)) { BMv = 64; BNv = 64; }
+  if (t128 < 128 && K <= 2048) { BMv = 64; BNv = 64; }
   // a fused backward epilogue in the tile cannot split K: small grids with a long K split it and run
   // the epilogue in the reduce (fm_gemm_splitk_reduce_bwd), short ones take 64x64 tiles for 4x the
   // blocks (summit_large dX, 256 x 4096 x 4096)
   const bool fused_ep = act_y != nullptr || colsum != nullptr;
   const bool fused_split = fused_ep && t128 < 256 && K >= 1024 && ws != nullptr && batch == 1 && ksplit_req <= 0 &&
                            (long)M * N * 4 * 2 <= ws_bytes;
-  if (fused_ep && t128 < 256 && !fused_split && !(g_gemm_variant & 16)) { BMv = 64; BNv = 64; }
-  if (g_gemm_variant & 32) { BMv = 64; BNv = 64; }
+  if (fused_ep && t128 < 256 && !fused_split) { BMv = 64; BNv = 64; }
   p.tiles_m = (M + BMv - 1) / BMv;
   p.tiles_n = (N + BNv - 1) / BNv;
   long tiles = (long)p.tiles_m * p.tiles_n * batch;
   int ktiles = (K + BK - 1) / BK;
   int ks = 1;
   if (ksplit_req > 0) ks = ksplit_req;
-  else if (ws != nullptr || atomic_ok) {
+  else if (ws != nullptr) {
     // split until the grid reaches ~1.5 blocks per CU (measured on the DLRM step, 200-step runs:
-    // target 256 -> 11.05, 384 -> 11.32, 512 -> 11.27, 1024 -> 9.81 M samples/s; FM_GEMM_SPLIT_BLOCKS)
+    // target 256 -> 11.05, 384 -> 11.32, 512 -> 11.27, 1024 -> 9.81 M samples/s)
     // -- long-K (dW at large batch) only: short-K small-batch GEMMs keep 256 (DLRM run_random at
     // 256/GPU: 1.10 M samples/s at 256 vs 1.04 M at 384)
-    static const long env_target = getenv("FM_GEMM_SPLIT_BLOCKS") ? std::max(1L, atol(getenv("FM_GEMM_SPLIT_BLOCKS"))) : 0L;
-    const long target = env_target > 0 ? env_target : (K >= 4096 ? 384L : 256L);
-    static const int ks_max = getenv("FM_GEMM_KSPLIT_MAX") ? std::max(1, atoi(getenv("FM_GEMM_KSPLIT_MAX"))) : 16;
-    while (tiles * ks < target && ks * 2 <= ktiles / 2 && ks < ks_max) ks *= 2;
+    const long target = K >= 4096 ? 384L : 256L;
+    while (tiles * ks < target && ks * 2 <= ktiles / 2 && ks < 16) ks *= 2;
   }
   if (fused_ep && !fused_split) ks = 1;  // fused bwd epilogue in the tile needs the full K sum
-  if (ks > 1 && !atomic_ok) {
-    while (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks /= 2;
-  }
+  while (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks /= 2;
   p.ksplit = ks;
   if (K <= 0) {  // degenerate: C = epilogue(0)
     p.ksplit = 1;
   }
-  p.atomic_c = p.ksplit > 1 && atomic_ok;
-  if (p.ksplit > 1) fm_gemm_join(stream);
   const bool reduce_bwd = p.ksplit > 1 && fused_ep;
-  if (p.ksplit > 1 && !p.atomic_c && !reduce_bwd) p.tile_cnt = split_counters(stream, tiles, (long)M * N * 4);
   if (BNv == 128) launch_bm<128, 128>(p, a_kcontig, b_kcontig, vec, stream);
   else if (BMv == 128) launch_bm<128, 64>(p, a_kcontig, b_kcontig, vec, stream);
   else launch_bm<64, 64>(p, a_kcontig, b_kcontig, vec, stream);
@@ -677,7 +525,7 @@ static int gemm_run(const void* A, long lda, long sA, int a_kcontig,
     const int by = std::max(1, std::min(M, 1024 / bx));
     const int RB = (M + by - 1) / by;
     hipLaunchKernelGGL(fm_gemm_splitk_reduce_bwd, dim3(bx, (M + RB - 1) / RB), dim3(256), 0, stream, p, RB);
-  } else if (p.ksplit > 1 && !p.atomic_c && p.tile_cnt == nullptr) {
+  } else if (p.ksplit > 1) {
     launch_splitk_reduce(p, stream);
   }
   return p.ksplit;

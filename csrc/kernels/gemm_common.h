@@ -1,5 +1,5 @@
-// Shared pieces of flexmi's MFMA GEMM kernels (gemm.hip register-staged, gemm_glds.hip LDS-DMA
-// pipelined): LDS operand images + swizzles, MFMA fragment reads, the parameter block and the
+// Shared pieces of flexmi's MFMA GEMM kernels (gemm.hip register-staged bf16,
+// gemm_f32.hip / gemm_x3.hip fp32): LDS operand images + swizzles, MFMA fragment reads, the parameter block and the
 // fused epilogue (alpha, bias, activation, fused activation-backward of the layer below, beta
 // accumulate, bf16/fp32 output, split-K slabs).
 #pragma once
@@ -77,8 +77,6 @@ struct GemmP {
   float alpha;
   int tiles_m, tiles_n;
   int n_fast;   // tile order: column tiles fastest (A row-block reused by consecutive tiles on one XCD)
-  int atomic_c; // split-K into an accumulating fp32 C: every split adds its tile with float atomics
-  int* tile_cnt; // in-launch split-K combine: per-tile arrival counters (nullptr = separate reduce launch)
   // fused SGD (dW GEMMs whose gradient has no other consumer): instead of storing the gradient,
   // the epilogue updates the fp32 master W (same [M][ldc] layout as C), its momentum and bf16 mirror
   // exactly as fm_sgd_kernel would (optim.hip) -- the gradient never round-trips through HBM
@@ -197,28 +195,8 @@ FM_DEVICE void gemm_epilogue(const GemmP& p, const f32x4_t (&acc)[MR][NR], int z
                              int lane) {
   const int mrow = lane & 15;
   const int ncol = 4 * (lane >> 4);
-  if (p.ksplit > 1 && p.atomic_c) {
-    // C (+)= alpha * partial: the splits meet in C itself (no slabs, no reduce launch).  Each
-    // 16x16 accumulator tile is 16 rows x 64 B; used only for small outputs (dW of narrow
-    // layers), where the ~1.3 TB/s atomic rate beats a slab round trip + an extra kernel.
-    float* Cf = reinterpret_cast<float*>(p.C) + (long)zb * p.sC;
-#pragma unroll
-    for (int i = 0; i < MR; ++i)
-#pragma unroll
-      for (int j = 0; j < NR; ++j) {
-        const int m = mbase + 16 * i + mrow;
-        const int n = nbase + 16 * j + ncol;
-        if (m >= p.M) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (n + r < p.N) atomicAdd(Cf + (long)m * p.ldc + n + r, acc[i][j][r] * p.alpha);
-      }
-    return;
-  }
-  if (p.ksplit > 1) {
+  if (p.ksplit > 1) {   // split-K partial tile -> fp32 slab [batch][split][M][N] (reduce launch)
     float* ws = p.ws + ((long)zb * p.ksplit + split) * (long)p.M * p.N;
-    // with the in-launch combine the slabs are stored WRITE-THROUGH (sc1): no release fence needed
-    const auto wrs = __builtin_amdgcn_make_buffer_rsrc(ws, 0, (int)((long)p.M * p.N * 4), 0x00020000);
 #pragma unroll
     for (int i = 0; i < MR; ++i)
 #pragma unroll
@@ -228,69 +206,13 @@ FM_DEVICE void gemm_epilogue(const GemmP& p, const f32x4_t (&acc)[MR][NR], int z
         if (m >= p.M) continue;
         float* dst = ws + (long)m * p.N + n;
         if (n + 3 < p.N && (p.N & 3) == 0) {
-          if (p.tile_cnt)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[i][j]), wrs,
-                                                   (int)(((long)m * p.N + n) * 4), 0, 16);
-          else
-            *reinterpret_cast<f32x4_t*>(dst) = acc[i][j];
+          *reinterpret_cast<f32x4_t*>(dst) = acc[i][j];
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            if (n + r < p.N) {
-              if (p.tile_cnt) __hip_atomic_store(dst + r, acc[i][j][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              else dst[r] = acc[i][j][r];
-            }
+            if (n + r < p.N) dst[r] = acc[i][j][r];
         }
       }
-    if (p.tile_cnt == nullptr) return;
-    // In-launch split-K combine (cdna_hip_programming.md "In-launch split-K reduction", sc1 form):
-    // every wave drains its write-through slab stores, lane 0 draws a relaxed agent-scope ticket;
-    // the block drawing ksplit-1 acquires once (one buffer_inv sc1), sums the other slices' slabs
-    // into its own registers and runs the regular epilogue -- no reduce launch.  The "I am last"
-    // flag goes through the kernel's one dynamic LDS array (free after the K loop).
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    int* flag = reinterpret_cast<int*>(smem);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int* cnt = p.tile_cnt + (long)blockIdx.y * gridDim.x + blockIdx.x;
-      const int ticket = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = ticket == p.ksplit - 1;
-      if (last) {
-        __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // ready for the next launch
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      *flag = last;
-    }
-    __syncthreads();
-    if (*flag == 0) return;
-    const float* wsz = p.ws + (long)zb * p.ksplit * (long)p.M * p.N;
-    f32x4_t tot[MR][NR];
-#pragma unroll
-    for (int i = 0; i < MR; ++i)
-#pragma unroll
-      for (int j = 0; j < NR; ++j) {
-        tot[i][j] = acc[i][j];
-        const int m = mbase + 16 * i + mrow;
-        const int n = nbase + 16 * j + ncol;
-        if (m >= p.M) continue;
-        const bool v4 = n + 3 < p.N && (p.N & 3) == 0;
-        for (int k = 0; k < p.ksplit; ++k) {
-          if (k == split) continue;
-          const float* src = wsz + (long)k * p.M * p.N + (long)m * p.N + n;
-          if (v4) {
-            tot[i][j] += *reinterpret_cast<const f32x4_t*>(src);
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              if (n + r < p.N) tot[i][j][r] += src[r];
-          }
-        }
-      }
-    GemmP q = p;
-    q.ksplit = 1;
-    gemm_epilogue_store<MR, NR, SGD>(q, tot, zb, mbase, nbase, lane);
     return;
   }
   gemm_epilogue_store<MR, NR, SGD>(p, acc, zb, mbase, nbase, lane);

@@ -1,4 +1,4 @@
-// Shared pieces of flexmi's fp32 MFMA GEMMs (gemm_f32.hip, gemm_f32_ring.hip): the parameter block,
+// Shared pieces of flexmi's fp32 MFMA GEMMs (gemm_f32.hip, gemm_x3.hip): the parameter block,
 // LDS image helpers, fragment loads and the fused epilogues (bias / activation / activation-backward /
 // bias-gradient column sums / beta accumulate / split-K slabs / fused SGD).  Internal linkage: every
 // translation unit gets its own copy.
@@ -24,7 +24,6 @@ struct GemmF {
   int M, N, K, act, beta, ksplit, batch;
   float alpha;
   int tiles_m, tiles_n, n_fast;
-  int atomic;           // split-K partials float-atomically added into C (32x32 kernel, beta = 1)
   // fused SGD (fm_gemm_f32_dw_sgd; default register-staged kernel and its reduce only): the
   // epilogue updates W (same [M][ldc] layout as C) instead of storing the gradient
   float* uw;
@@ -34,51 +33,7 @@ struct GemmF {
   float uwd, umom;
   int unest;
   int ulds;             // unsplit tiles stage the update through LDS (sgd_epilogue_lds_f32)
-  // exact bf16 planes (x = h + m + l, gemm_pl.hip): operand planes read by the plane kernel instead
-  // of A / B (same leading dims, plane p at base + p * ps elements), and the planes of the stored C
-  // written beside it by every epilogue / reduce (nullptr: none)
-  const unsigned short* Ap; long psa;
-  const unsigned short* Bp; long psb;
-  unsigned short* Cp; long psc;
-  int pvar;             // plane kernel A/B knob (FM_PL_VAR): 1 = s_setprio 1 for waves 4-7, 2 = around MFMAs
 };
-
-// Exact three-way truncation split x = h + m + l of one fp32 value into bf16 bit patterns (high
-// halves of the returned words).  h keeps x's top 16 bits, r = x - h is exact (<= 16 significant
-// bits), m = r truncated, l = r - m (<= 8 significant bits: exactly a bf16).  Non-finite x: h
-// carries it (a NaN stays a NaN), m = l = 0.  A GEMM over split operands turns a non-finite
-// operand into NaN rather than +-inf (inf * 0 among the six partial products): documented
-// behaviour, pinned by tests/test_gpu_planes.py.
-FM_DEVICE void split3_bits(float x, unsigned& h, unsigned& m, unsigned& l) {
-  const unsigned b = __float_as_uint(x);
-  h = b & 0xffff0000u;
-  const float r = x - __uint_as_float(h);
-  m = __float_as_uint(r) & 0xffff0000u;
-  l = __float_as_uint(r - __uint_as_float(m)) & 0xffff0000u;
-  if ((b & 0x7f800000u) == 0x7f800000u) {
-    h |= (b & 0x007fffffu) ? 0x00400000u : 0u;
-    m = 0u;
-    l = 0u;
-  }
-}
-
-// planes of four consecutive values at element offset o (8-B aligned): one 8-B store per plane
-FM_DEVICE void store_planes4(unsigned short* cp, long ps, long o, const float (&v)[4]) {
-  unsigned h[4], m[4], l[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) split3_bits(v[e], h[e], m[e], l[e]);
-  typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
-  *reinterpret_cast<u32x2_t*>(cp + o) = u32x2_t{(h[0] >> 16) | h[1], (h[2] >> 16) | h[3]};
-  *reinterpret_cast<u32x2_t*>(cp + ps + o) = u32x2_t{(m[0] >> 16) | m[1], (m[2] >> 16) | m[3]};
-  *reinterpret_cast<u32x2_t*>(cp + 2 * ps + o) = u32x2_t{(l[0] >> 16) | l[1], (l[2] >> 16) | l[3]};
-}
-FM_DEVICE void store_planes1(unsigned short* cp, long ps, long o, float v) {
-  unsigned h, m, l;
-  split3_bits(v, h, m, l);
-  cp[o] = (unsigned short)(h >> 16);
-  cp[ps + o] = (unsigned short)(m >> 16);
-  cp[2 * ps + o] = (unsigned short)(l >> 16);
-}
 
 template <int N>
 using fvec = float __attribute__((ext_vector_type(N)));
@@ -278,18 +233,10 @@ FM_DEVICE void epilogue_f32(const GemmF& p, const f32x4_t (&acc)[MR][NR], int zb
         f32x4_t o = {v[0], v[1], v[2], v[3]};
         if (p.beta) o += *reinterpret_cast<const f32x4_t*>(dst);
         *reinterpret_cast<f32x4_t*>(dst) = o;
-        if (p.Cp) {
-          const float fo[4] = {o[0], o[1], o[2], o[3]};
-          store_planes4(p.Cp, p.psc, (long)zb * p.sC + (long)m * p.ldc + n0, fo);
-        }
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          if (n0 + e < p.N) {
-            const float fo = v[e] + (p.beta ? dst[e] : 0.f);
-            dst[e] = fo;
-            if (p.Cp) store_planes1(p.Cp, p.psc, (long)zb * p.sC + (long)m * p.ldc + n0 + e, fo);
-          }
+          if (n0 + e < p.N) dst[e] = v[e] + (p.beta ? dst[e] : 0.f);
       }
     }
   }

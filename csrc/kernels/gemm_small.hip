@@ -248,23 +248,16 @@ extern "C" int fm_smallk_dw_f32_launch(const float* dpre, long ldd, const float*
     return -1;
   const int NG = N / 4;
   const int G = NG < 64 ? NG : 64;               // column groups per block
-  // FM_SK_DW_ROWS (64 / 128 / 256): rows per partial block -- fewer, longer blocks leave fewer
-  // partials for the deterministic reduce; 64 (default) measured best on the step (1.161-1.163 vs
-  // 1.164-1.170 ms, profiles/smallk_dw_rows_ab_r5sk.txt)
-  static const int rows_env = getenv("FM_SK_DW_ROWS") ? atoi(getenv("FM_SK_DW_ROWS")) : SK_ROWS_DW;
-  const int RW = rows_env == 128 || rows_env == 256 ? rows_env : SK_ROWS_DW;
+  // 64 rows per partial block: fewer, longer blocks leave fewer partials for the deterministic
+  // reduce, 64 measured best on the step (1.161-1.163 vs 1.164-1.170 ms, profiles/smallk_dw_rows_ab_r5sk.txt)
+  constexpr int RW = SK_ROWS_DW;
   const long P = (M + RW - 1) / RW;
   const long per = (long)(K + 1) * N;
   if (P * per * 4 > ws_bytes || P > (1L << 30)) return -1;
   const dim3 grid((unsigned)P, (unsigned)((NG + G - 1) / G));
-#define FM_SD(KK)                                                                                                   \
-  case KK:                                                                                                          \
-    if (RW == 256)                                                                                                  \
-      hipLaunchKernelGGL((fm_smallk_dw_part<KK, 256>), grid, dim3(SK_DW_NT), 0, s, dpre, ldd, x, ldx, ws, M, N, G); \
-    else if (RW == 128)                                                                                             \
-      hipLaunchKernelGGL((fm_smallk_dw_part<KK, 128>), grid, dim3(SK_DW_NT), 0, s, dpre, ldd, x, ldx, ws, M, N, G); \
-    else                                                                                                            \
-      hipLaunchKernelGGL((fm_smallk_dw_part<KK>), grid, dim3(SK_DW_NT), 0, s, dpre, ldd, x, ldx, ws, M, N, G);      \
+#define FM_SD(KK)                                                                                            \
+  case KK:                                                                                                   \
+    hipLaunchKernelGGL((fm_smallk_dw_part<KK>), grid, dim3(SK_DW_NT), 0, s, dpre, ldd, x, ldx, ws, M, N, G); \
     break;
   switch (K) {
     FM_SD(4) FM_SD(8) FM_SD(12) FM_SD(16) FM_SD(20) FM_SD(24) FM_SD(28) FM_SD(32)

@@ -39,7 +39,8 @@ namespace {
 
 constexpr int XK = 32;   // k per stage
 
-// byte offset of 16-B chunk c (8 bf16) of row r in a [row][32 bf16] plane
+// byte offset of 16-B chunk c (8 bf16) of row r in a [row][32 bf16] plane; the chunk XOR
+// (r >> 1) & 3 makes the 16x16x32 fragment reads (lane = 16 rows x 4 chunks) conflict-free
 FM_DEVICE int x3_off(int r, int c) { return r * 64 + 16 * (c ^ ((r >> 1) & 3)); }
 
 // exact truncation split of one fp32 value: x = h + m + l, each a bf16 (returned as fp32 bits
@@ -264,47 +265,13 @@ __global__ void __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) fm_gemm_x3v2_ke
     for (int t = 0; t < nst; ++t) {
       __syncthreads();               // stage t&1 complete; stage (t+1)&1 no longer read
       const char* b = stage(t & 1);
-      const char* la = b;
       bf16x8_t bf[3][NR];
       load_b(b + 3 * PA_, bf);
-      if constexpr (SCHED == 1) {
-        // every fragment of the step first, then the staging pass (split + ds_write of step t+1,
-        // loads of step t+2), then the MFMAs: nothing orders the MFMAs behind the staging VALU /
-        // LDS writes, so the scheduler can interleave them
-        bf16x8_t af[MR][3];
-#pragma unroll
-        for (int i = 0; i < MR; ++i)
-#pragma unroll
-          for (int pl = 0; pl < 3; ++pl)
-            af[i][pl] = *reinterpret_cast<const bf16x8_t*>(la + pl * PA_ + x3_off(wm * 64 + 16 * i + q, g));
-        if (t + 1 < nst) {
-          put_from((t + 1) & 1, sa, sb);
-          if (t + 2 < nst) get_into(kt0 + t + 2, sa, sb);
-        }
-#pragma unroll
-        for (int i = 0; i < MR; ++i)
-#pragma unroll
-          for (int s = 0; s < 6; ++s)
-#pragma unroll
-            for (int j = 0; j < NR; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8v_t*>(&bf[TB[s]][j]),
-                                                                  *reinterpret_cast<bf16x8v_t*>(&af[i][TA[s]]),
-                                                                  acc[i][j], 0, 0, 0);
-      } else {
-        // SCHED 2: the two waves sharing a SIMD (w and w + 4) run the step's two phases in
-        // opposite order -- one splits / stores while the other issues MFMAs -- instead of both
-        // idling the MFMA pipe through the staging pass together
-        const bool mfma_first = SCHED == 2 && ((wave >> 2) & 1);
-        if (!mfma_first && t + 1 < nst) {
-          put_from((t + 1) & 1, sa, sb);
-          if (t + 2 < nst) get_into(kt0 + t + 2, sa, sb);
-        }
-        mfma_rows(la, bf);
-        if (mfma_first && t + 1 < nst) {
-          put_from((t + 1) & 1, sa, sb);
-          if (t + 2 < nst) get_into(kt0 + t + 2, sa, sb);
-        }
+      if (t + 1 < nst) {
+        put_from((t + 1) & 1, sa, sb);
+        if (t + 2 < nst) get_into(kt0 + t + 2, sa, sb);
       }
+      mfma_rows(b, bf);
     }
   }
   if constexpr (!AK) {
@@ -333,11 +300,11 @@ void launch_x3v2_s(const GemmF& p, bool ak, bool bk, hipStream_t s) {
   do {                                                                                                           \
     static bool attr = false;                                                                                    \
     if (!attr) {                                                                                                 \
-      (void)hipFuncSetAttribute((const void*)fm_gemm_x3v2_kernel<BM, BN, AKv, BKv, SGD, SCHED>,                        \
+      (void)hipFuncSetAttribute((const void*)fm_gemm_x3v2_kernel<BM, BN, AKv, BKv, SGD, SCHED>,                   \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS);                                \
       attr = true;                                                                                               \
     }                                                                                                            \
-    hipLaunchKernelGGL((fm_gemm_x3v2_kernel<BM, BN, AKv, BKv, SGD, SCHED>), grid, dim3(NTH), LDS, s, p);              \
+    hipLaunchKernelGGL((fm_gemm_x3v2_kernel<BM, BN, AKv, BKv, SGD, SCHED>), grid, dim3(NTH), LDS, s, p);         \
   } while (0)
   if (ak && bk) FM_X3V2(true, true);
   else if (ak) FM_X3V2(true, false);
@@ -346,18 +313,21 @@ void launch_x3v2_s(const GemmF& p, bool ak, bool bk, hipStream_t s) {
 #undef FM_X3V2
 }
 
-// FM_X3_SCHED (A/B): 1 = all fragment reads of a step ahead of its staging pass; 2 = the two waves
-// of a SIMD run staging and MFMAs in opposite order (8-wave tile only); 3 = 2 with the global loads
-// two steps ahead (a second staging register set)
+// Schedules: 256x128 tiles (8 waves, two per SIMD) run schedule 3 -- the two waves of a SIMD do
+// the staging split and the MFMAs of a step in opposite order, global loads two steps ahead
+// (972.6 vs 975.6 us for schedule 2 and more for the one-register-set forms over the DLRM lab
+// shapes, profiles/bench_ab_x3_sched_embgrid_r5n.txt; schedules 1 / 2 deleted in r6); 128x128
+// tiles (4 waves) the plain one-set schedule 0.  The same schedule on 32x32x16 MFMAs (each leaving
+// 24 of its 32 issue cycles to the staging split) measured slower: 1.236 vs 1.185 ms per DLRM fp32
+// step (profiles/gemm_x3_mfma_form_bench_r5p3.txt), deleted.
+
 template <int BM, int BN, bool SGD>
 void launch_x3v2(const GemmF& p, bool ak, bool bk, hipStream_t s) {
-  // default 3 (de-phased waves, loads two steps ahead): 972.6 vs 975.6 us (sched 2) over the DLRM
-  // lab shapes, step 1.181 vs 1.186 ms (profiles/bench_ab_x3_sched_embgrid_r5n.txt)
-  static const int sched = getenv("FM_X3_SCHED") ? atoi(getenv("FM_X3_SCHED")) : 3;
-  if (sched == 1) launch_x3v2_s<BM, BN, SGD, 1>(p, ak, bk, s);
-  else if (sched == 2 && BM == 256) launch_x3v2_s<BM, BN, SGD, 2>(p, ak, bk, s);
-  else if (sched == 3 && BM == 256) launch_x3v2_s<BM, BN, SGD, 3>(p, ak, bk, s);
-  else launch_x3v2_s<BM, BN, SGD, 0>(p, ak, bk, s);
+  if constexpr (BM == 256) {
+    launch_x3v2_s<BM, BN, SGD, 3>(p, ak, bk, s);
+  } else {
+    launch_x3v2_s<BM, BN, SGD, 0>(p, ak, bk, s);
+  }
 }
 
 }  // namespace

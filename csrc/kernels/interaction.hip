@@ -346,26 +346,7 @@ struct PtrTabF {
 struct MPtrTabF {
   float* p[MAXF];
 };
-// Embedding rows gathered in place (the embedding-into-interaction fusion): feature i's row of
-// sample b is p[i] + r * ld[i] with r = ix[i][b] (the bag-1 lookup index) or r = b (ix[i] null),
-// so the interaction reads table rows directly and the [B, D] embedding outputs are never written.
-struct GatherTabF {
-  const float* p[MAXF];
-  const void* ix[MAXF];
-  long ld[MAXF];
-  long rows[MAXF];   // table rows: an out-of-range index is clamped (never a wild read)
-  int i64;
-};
 FM_DEVICE const float* zrow(const PtrTabF& Z, long ldz, int i, long b) { return Z.p[i] + b * ldz; }
-FM_DEVICE const float* zrow(const GatherTabF& Z, long, int i, long b) {
-  const void* ix = Z.ix[i];
-  long r = b;
-  if (ix != nullptr) {
-    r = Z.i64 ? reinterpret_cast<const long*>(ix)[b] : (long)reinterpret_cast<const int*>(ix)[b];
-    r = min(max(r, 0L), Z.rows[i] - 1);
-  }
-  return Z.p[i] + r * Z.ld[i];
-}
 
 template <int DT>
 __global__ void __launch_bounds__(256) fm_dot_fwd_f32(PtrTabF Z, long ldz, float* __restrict__ out, long ldo, long B,
@@ -797,14 +778,8 @@ __global__ void __launch_bounds__(256, 2) fm_dot_bwd_f32r(ZT Z, long ldz, const 
 FM_HOST_DEVICE bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // persistent-grid size of the interaction kernels (4 waves per block; each wave loops over
-// samples with the next one prefetched).  FM_DOT_BLOCKS overrides (tuning runs).
-long dot_block_cap() {
-  static const long cap = [] {
-    const char* e = getenv("FM_DOT_BLOCKS");
-    return e ? std::max(1L, atol(e)) : 512L;
-  }();
-  return cap;
-}
+// samples with the next one prefetched)
+long dot_block_cap() { return 512L; }
 
 }  // namespace
 
@@ -816,22 +791,15 @@ extern "C" void fm_dot_interaction_fwd_f32(const float* const* z, int F, long ld
   const long blocks = std::min<long>((B + waves - 1) / waves, dot_block_cap());
   bool fast = (D == 16 || D == 32 || D == 64 || D == 128) && ldz % 4 == 0;
   for (int i = 0; i < F; ++i) fast = fast && al16(z[i]);
-  static const bool staged = getenv("FM_DOT_FWD_STAGED") == nullptr || atoi(getenv("FM_DOT_FWD_STAGED")) != 0;
-  if (staged && fast && D >= 32 && F <= 32 && (W & 3) == 0 && (ldo & 3) == 0 && W <= 1024 && al16(out)) {
+  // the staged kernel with the Gram on the bf16 matrix cores through the exact three-way split:
+  // 8192 x 27 x 128 forward 35.6 -> 29.4 us against the fp32 MFMA, MLPerf fp32 step -6 us
+  // (profiles/dot_fwd_x3_ab_r5y.txt; the fp32-MFMA and unstaged A/B forms deleted in r6)
+  if (fast && D >= 32 && F <= 32 && (W & 3) == 0 && (ldo & 3) == 0 && W <= 1024 && al16(out)) {
     const size_t lds_s = (size_t)waves * (32 * (D + 4) + ((W + 3) & ~3)) * 4;
-    // the Gram on the bf16 matrix cores through the exact three-way split (default; FM_DOT_FWD_X3=0:
-    // the fp32 MFMA): 8192 x 27 x 128 forward 35.6 -> 29.4 us, MLPerf fp32 step -6 us
-    // (profiles/dot_fwd_x3_ab_r5y.txt)
-    const char* x3e = getenv("FM_DOT_FWD_X3");   // read per call: tests flip it in-process
-    const bool x3 = !(x3e != nullptr && atoi(x3e) == 0);
-    auto ks = x3 ? (D == 128 ? fm_dot_fwd_f32s<128, PtrTabF, true> : D == 64 ? fm_dot_fwd_f32s<64, PtrTabF, true>
-                                                                            : fm_dot_fwd_f32s<32, PtrTabF, true>)
-                 : (D == 128 ? fm_dot_fwd_f32s<128> : D == 64 ? fm_dot_fwd_f32s<64> : fm_dot_fwd_f32s<32>);
+    auto ks = D == 128 ? fm_dot_fwd_f32s<128, PtrTabF, true> : D == 64 ? fm_dot_fwd_f32s<64, PtrTabF, true>
+                                                                       : fm_dot_fwd_f32s<32, PtrTabF, true>;
     static bool attr = false;
     if (!attr) {
-      (void)hipFuncSetAttribute((const void*)fm_dot_fwd_f32s<128>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10);
-      (void)hipFuncSetAttribute((const void*)fm_dot_fwd_f32s<64>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10);
-      (void)hipFuncSetAttribute((const void*)fm_dot_fwd_f32s<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10);
       (void)hipFuncSetAttribute((const void*)fm_dot_fwd_f32s<128, PtrTabF, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 96 << 10);
       (void)hipFuncSetAttribute((const void*)fm_dot_fwd_f32s<64, PtrTabF, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -890,73 +858,6 @@ extern "C" void fm_dot_interaction_bwd_f32(const float* const* z, int F, long ld
                                      : D == 32 ? fm_dot_bwd_f32<32> : fm_dot_bwd_f32<16>;
   hipLaunchKernelGGL(k, dim3((int)blocks), dim3(64 * waves), lds, s, t, ldz, dout, ldo, g, lddz, acc_mask, B, F, D, Wr,
                      self, act0);
-}
-
-// Gathered-row forms (GatherTabF): feature i reads p[i] + ix[i][b] * ld[i] (ix[i] null: row b).
-// Only the fast fp32 kernels take them; returns -1 (nothing launched) when the operands do not fit.
-static bool gather_tab(GatherTabF& t, const float* const* z, const void* const* ix, const long* ld, const long* rows,
-                       int i64, int F) {
-  if (F < 2 || F > MAXF) return false;
-  for (int i = 0; i < MAXF; ++i) {
-    t.p[i] = i < F ? z[i] : nullptr;
-    t.ix[i] = i < F ? ix[i] : nullptr;
-    t.ld[i] = i < F ? ld[i] : 0;
-    t.rows[i] = i < F ? rows[i] : 1;
-    if (i < F && ix[i] != nullptr && rows[i] < 1) return false;
-    if (i < F && (!al16(z[i]) || ld[i] % 4 != 0)) return false;
-  }
-  t.i64 = i64;
-  return true;
-}
-
-extern "C" int fm_dot_interaction_fwd_f32g(const float* const* z, const void* const* ix, const long* ld, const long* rows,
-                                           int i64, int F, float* out, long ldo, long B, int D, int W, int self, hipStream_t s) {
-  GatherTabF t;
-  if (!gather_tab(t, z, ix, ld, rows, i64, F) || !(D == 32 || D == 64 || D == 128) || F > 32 || (W & 3) || (ldo & 3) ||
-      W > 1024 || !al16(out))
-    return -1;
-  const int waves = 4;
-  const long blocks = std::min<long>((B + waves - 1) / waves, dot_block_cap());
-  const size_t lds_s = (size_t)waves * (32 * (D + 4) + ((W + 3) & ~3)) * 4;
-  auto ks = D == 128 ? fm_dot_fwd_f32s<128, GatherTabF> : D == 64 ? fm_dot_fwd_f32s<64, GatherTabF>
-                                                                  : fm_dot_fwd_f32s<32, GatherTabF>;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)fm_dot_fwd_f32s<128, GatherTabF>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10);
-    (void)hipFuncSetAttribute((const void*)fm_dot_fwd_f32s<64, GatherTabF>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10);
-    (void)hipFuncSetAttribute((const void*)fm_dot_fwd_f32s<32, GatherTabF>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10);
-    attr = true;
-  }
-  hipLaunchKernelGGL(ks, dim3((int)blocks), dim3(64 * waves), lds_s, s, t, 0L, out, ldo, B, F, W, self);
-  return 0;
-}
-
-extern "C" int fm_dot_interaction_bwd_f32g(const float* const* z, const void* const* ix, const long* ld, const long* rows,
-                                           int i64, int F, const float* dout, long ldo, float* const* dz, long lddz, unsigned acc_mask,
-                                           long B, int D, int self, hipStream_t s) {
-  GatherTabF t;
-  if (!gather_tab(t, z, ix, ld, rows, i64, F) || !(D == 32 || D == 64 || D == 128) || ldo % 4 || !al16(dout)) return -1;
-  const int npairs = self ? F * (F + 1) / 2 : F * (F - 1) / 2;
-  const int W = D + npairs;
-  const int E = D / 32;
-  if (W > 1024 || lddz % E) return -1;
-  MPtrTabF g;
-  for (int i = 0; i < MAXF; ++i) {
-    g.p[i] = i < F ? dz[i] : nullptr;
-    if (i < F && dz[i] != nullptr && ((uintptr_t)dz[i] & (4 * E - 1))) return -1;
-  }
-  const int waves = 4;
-  const long blocks = std::min<long>((B + waves - 1) / waves, dot_block_cap());
-  const int wpad = (W + 3) & ~3;
-  const bool acc = acc_mask != 0;
-  const bool k14 = E == 4 && (F + 1) / 2 == 14 && !acc;
-  auto k = k14 ? fm_dot_bwd_f32r<4, 14, false, GatherTabF>
-         : E == 4 ? (acc ? fm_dot_bwd_f32r<4, 16, true, GatherTabF> : fm_dot_bwd_f32r<4, 16, false, GatherTabF>)
-         : E == 2 ? (acc ? fm_dot_bwd_f32r<2, 16, true, GatherTabF> : fm_dot_bwd_f32r<2, 16, false, GatherTabF>)
-                  : (acc ? fm_dot_bwd_f32r<1, 16, true, GatherTabF> : fm_dot_bwd_f32r<1, 16, false, GatherTabF>);
-  hipLaunchKernelGGL(k, dim3((int)blocks), dim3(64 * waves), (size_t)waves * wpad * 4, s, t, 0L, dout, ldo, g, lddz,
-                     acc_mask, B, F, W, self, (int)ACT_NONE);
-  return 0;
 }
 
 extern "C" void fm_dot_interaction_fwd(const void* const* z, int F, long ldz, void* out, long ldo, long B, int D, int W,

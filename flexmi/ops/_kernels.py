@@ -48,7 +48,10 @@ _ws = {}
 
 
 def workspace(device, nbytes):
-    key = (str(device),)
+    """Grow-only split-K slab workspace of the CURRENT stream on ``device``: GEMMs issued on
+    different streams (the executor's dW stream beside the main one) never share slabs."""
+    stream = torch.cuda.current_stream(device).cuda_stream if torch.cuda.is_available() else 0
+    key = (str(device), stream)
     t = _ws.get(key)
     if t is None or t.numel() * 4 < nbytes:
         t = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=device)
@@ -60,41 +63,13 @@ GEMM_WS_BYTES = 64 << 20
 
 
 def gemm(A, lda, a_kcontig, B, ldb, b_kcontig, Cout, ldc, M, N, K, bias=None, act=10, beta=False, alpha=1.0,
-         batch=1, sA=0, sB=0, sC=0, ksplit=0, use_ws=True, act_y=None, bwd_act=10, colsum=None, rowsum_a=None,
-         async_reduce=False, ap=None, bp=None, cp=None):
+         batch=1, sA=0, sB=0, sC=0, ksplit=0, use_ws=True, act_y=None, bwd_act=10, colsum=None, rowsum_a=None):
     """C = epi(A·B).  Optional fused backward epilogue of the layer below (act_y/bwd_act/colsum):
-    C = act'(act_y) * (A·B) and colsum += column sums of C (its bias gradient).  async_reduce: a
-    split-K reduce may run on a side stream (csrc/kernels/gemm_async.hip) -- the caller must
-    gemm_join() before anything reads Cout.  fp32 only: ap / bp = exact bf16 planes of A / B
-    (:func:`planes_like`; the pre-split kernel csrc/kernels/gemm_pl.hip), cp = planes to write for C."""
+    C = act'(act_y) * (A·B) and colsum += column sums of C (its bias gradient)."""
     ws = workspace(Cout.device, GEMM_WS_BYTES) if use_ws else None
     lday = act_y.stride(0) if act_y is not None else 0
     return C().gemm(A, lda, sA, a_kcontig, B, ldb, sB, b_kcontig, Cout, ldc, sC, bias, M, N, K, batch, alpha, beta, act,
-                    ws, ksplit, act_y, lday, bwd_act, colsum, rowsum_a, bool(async_reduce), ap, bp, cp)
-
-
-def planes_like(t):
-    """bf16 [3, *t.shape] buffer for the exact three-way split of the fp32 tensor ``t`` (its plane p
-    holds element i at p * t.numel() + i, so a 2-D view's leading dim carries over)."""
-    return torch.empty((3,) + tuple(t.shape), dtype=torch.bfloat16, device=t.device)
-
-
-def split_planes(src2d, planes):
-    """planes = exact split of the fp32 matrix src2d (x = h + m + l, csrc/kernels/gemm_pl.hip)."""
-    rows = src2d.shape[0]
-    C().split_planes(src2d, planes.view(3, rows, -1))
-
-
-# FM_GEMM_ASYNC_REDUCE=1: the executor's dW GEMMs run their split-K reduce on a side stream.
-# OPT-IN: measured SLOWER on the DLRM MLPerf step (fp32 1.52-1.54 vs 1.47-1.48 ms, bf16 0.70-0.72
-# vs 0.63 ms, profiles/bench_ab_async_reduce_r3h.txt): in the captured graph the reduce still ran
-# before the next GEMM, and the cross-stream edges added gaps
-ASYNC_DW = os.environ.get("FM_GEMM_ASYNC_REDUCE", "0") == "1"
-
-
-def gemm_join():
-    """Current stream waits for a pending side-stream split-K reduce (no-op when none)."""
-    C().gemm_join()
+                    ws, ksplit, act_y, lday, bwd_act, colsum, rowsum_a)
 
 
 # ------------------------------------------------------------------ init
@@ -157,16 +132,10 @@ def _smallk(x2, K):
 def _dw_smallk(dpre, x2, dw, db, upd):
     """dW (+ db) of a thin-input layer on gemm_small.hip; with upd the SGD step is applied to the
     weight in the same launch pair.  False when the kernel does not apply."""
-    if ASYNC_DW:
-        gemm_join()                # the shared workspace may still feed an async split-K reduce
     ws = workspace(dpre.device, GEMM_WS_BYTES)
     if upd is None:
         return C().smallk_dw(dpre, x2, dw, db, ws, None, None, None, 0.0, 0.0, False)
     return C().smallk_dw(dpre, x2, upd.w, db, ws, upd.v, upd.wc, upd.lr, upd.wd, upd.mom, upd.nesterov)
-
-
-DX_LIB = os.environ.get("FM_DX_LIB", "0") == "1"
-DX_LIB_MIN = int(os.environ.get("FM_DX_LIB_MIN", str(1 << 32)))
 
 
 class FusedSGD:
@@ -195,12 +164,11 @@ def _dw_fused_sgd(dpre, x2, dw, db, upd):
 
 
 def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=False, fuse_below=None, phase="all",
-                    async_dw=False, upd=None):
+                    upd=None):
     """Weight/bias grads ACCUMULATE into dw/db (the executor zeroes the flat gradient buffer once
     per step).  grad_is_dpre: dy2 already holds act'(y)*dy (written by the consumer's fused dX
     epilogue).  fuse_below = (y_below, act_below): apply the activation backward of the layer
-    below in this layer's dX GEMM epilogue.  async_dw: the dW GEMM's split-K reduce may run on a
-    side stream, overlapping the dX GEMM (the caller joins with gemm_join() before dw is read).
+    below in this layer's dX GEMM epilogue.
     upd (FusedSGD): the weight is updated in place by this call (after its dX GEMM, which reads
     it) and dw stays zero; the bias gradient is still accumulated into db."""
     M, K = x2.shape
@@ -255,11 +223,9 @@ def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=F
     # dW[N,K] = dpre^T x (both operands MN-contiguous: transposing LDS reads); the bias gradient
     # db = column sums of dpre is accumulated from the staged A tiles of the same GEMM
     # dW ACCUMULATES (beta): the executor zeroes the flat gradient buffer once per step, so weights
-    # used by several ops sum their gradients, and split-K partials of small dW tiles can be added
-    # with atomics straight into dw (no slab / reduce launch)
+    # used by several ops sum their gradients
     if phase != "dx" and not lib and not (_smallk(x2, K) and _dw_smallk(dpre, x2, dw, db, None)):
-        gemm(dpre, dpre.stride(0), False, x2, x2.stride(0), False, dw, K, N, K, M, beta=True, rowsum_a=db,
-             async_reduce=async_dw and ASYNC_DW)
+        gemm(dpre, dpre.stride(0), False, x2, x2.stride(0), False, dw, K, N, K, M, beta=True, rowsum_a=db)
     if phase == "dw":
         return
     if dx2 is not None:
@@ -268,17 +234,6 @@ def linear_backward(x2, w, y2, dy2, act, dx2, dx_acc, dw, db, ws, grad_is_dpre=F
 
 def _linear_dx(dpre, w, dx2, dx_acc, fuse_below, M, N, K):
     # dX[M,K] = dpre W   (+ fused activation backward of the layer below)
-    if DX_LIB and M * K * N >= DX_LIB_MIN and dx2.is_contiguous():
-        # plain library GEMM (hipBLASLt) for the big dX products, activation backward of the layer
-        # below as a separate pass (FM_DX_LIB=1; A/B in profiles/README.md)
-        t = torch.matmul(dpre, w)
-        if fuse_below is not None:
-            C().act_bwd_bias(fuse_below[0].view(M, K), t, dx2, None, M, K, int(fuse_below[1]))
-        elif dx_acc:
-            dx2.add_(t)
-        else:
-            dx2.copy_(t)
-        return
     if dx2 is not None:
         if fuse_below is not None:
             yb, actb = fuse_below[0], fuse_below[1]
@@ -338,24 +293,6 @@ def dot_interaction_backward(inputs, dy, in_grads, accs, self_inter, act0=10):
     ld = next((g.stride(0) for g in in_grads if g is not None), D)
     C().dot_bwd(list(inputs), inputs[0].stride(0), dy, dy.stride(0), list(in_grads), ld, mask, D, bool(self_inter),
                 int(act0))
-
-
-def dot_interaction_forward_gather(srcs, ixs, y, self_inter):
-    """Embedding-into-interaction form (fp32): feature i's rows are srcs[i][ixs[i][b]] (an embedding
-    TABLE gathered by its bag-1 indices) or srcs[i][b] (ixs[i] None).  False: not launched."""
-    D = srcs[0].shape[-1]
-    return bool(C().dot_fwd_gather(list(srcs), list(ixs), y, y.stride(0), D, y.shape[1], bool(self_inter)))
-
-
-def dot_interaction_backward_gather(srcs, ixs, dy, in_grads, accs, self_inter):
-    D = srcs[0].shape[-1]
-    mask = 0
-    for i, a in enumerate(accs):
-        if a and in_grads[i] is not None:
-            mask |= 1 << i
-    ld = next((g.stride(0) for g in in_grads if g is not None), D)
-    return bool(C().dot_bwd_gather(list(srcs), list(ixs), dy, dy.stride(0), list(in_grads), ld, mask, D,
-                                   bool(self_inter)))
 
 
 # ------------------------------------------------------------------ optimizers / loss

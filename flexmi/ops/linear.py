@@ -127,7 +127,7 @@ class Linear(Op):
             K.linear_backward(x2, ctx.wcompute[0], y2, dy2, int(act), dx2,
                               bool(ctx.in_grad_accumulate[0]) if dx2 is not None else False, dw, db,
                               ctx.workspace, ctx.saved.get("grad_is_dpre", False), ctx.saved.get("fuse_below"), phase,
-                              ctx.saved.get("async_dw", False), upd=_armed_sgd(ctx))
+                              upd=_armed_sgd(ctx))
         else:
             dpre = act_backward_torch(dy2.float(), y2.float(), act)
             if phase != "dx":

@@ -186,38 +186,9 @@ class DotInteraction(Op):
                 lj.append(j)
         return li, lj
 
-    @staticmethod
-    def _gather_args(ctx):
-        """Executor embedding-into-interaction fusion (Executor._build_gather_fusion): per input,
-        (table, bag-1 indices) for a fused embedding, else (activation, None)."""
-        g = ctx.saved["gather"]
-        srcs = [ctx.inputs[i] if g[i] is None else g[i][0] for i in range(len(ctx.inputs))]
-        ixs = [None if g[i] is None else g[i][1] for i in range(len(ctx.inputs))]
-        return srcs, ixs
-
-    @staticmethod
-    def _ungather(ctx):
-        """The fused form did not launch: materialise the embedding outputs the usual way (their
-        group forward) and drop the fusion for good."""
-        g = ctx.saved.pop("gather")
-        done = set()
-        for e in g:
-            if e is None or id(e[2]) in done:
-                continue
-            grp, ctxs = e[2], e[3]
-            done.add(id(grp))
-            type(grp[0]).forward_group(grp, ctxs)
-            for c in ctxs:
-                c.saved.pop("gathered", None)
-
     def forward(self, ctx: OpCtx):
         y = ctx.outputs[0]
         if ctx.hip:
-            if "gather" in ctx.saved:
-                srcs, ixs = self._gather_args(ctx)
-                if K.dot_interaction_forward_gather(srcs, ixs, y, self.self_interaction):
-                    return
-                self._ungather(ctx)
             K.dot_interaction_forward(list(ctx.inputs), y, self.self_interaction)
             return
         Z = torch.stack([t.float() for t in ctx.inputs], dim=1)  # [B,F,d]
@@ -231,12 +202,6 @@ class DotInteraction(Op):
     def backward(self, ctx: OpCtx):
         dy = ctx.out_grads[0]
         if ctx.hip:
-            if "gather" in ctx.saved:
-                srcs, ixs = self._gather_args(ctx)
-                ok = K.dot_interaction_backward_gather(srcs, ixs, dy, list(ctx.in_grads), list(ctx.in_grad_accumulate),
-                                                       self.self_interaction)
-                assert ok, f"{self.name}: gathered interaction backward did not launch (forward did)"
-                return
             K.dot_interaction_backward(list(ctx.inputs), dy, list(ctx.in_grads),
                                        list(ctx.in_grad_accumulate), self.self_interaction,
                                        ctx.saved.get("act0", 10))

@@ -199,33 +199,31 @@ def overlap_embeddings_enabled(ex):
     return any(st[0] == "op" and type(st[1]).__name__ == "Embedding" and st[1].out_dim >= 128 for st in ex.fwd_steps)
 
 
-def Embedding_row_lo(ctx):
-    """First table row of this rank's embedding shard (0 for a whole table)."""
-    b = ctx.w_boxes[0] if ctx.w_boxes else None
-    return int(b[0][0]) if b is not None else 0
+# FM_DW_STREAM=N (default 1): inside captured segments, the weight-gradient GEMMs (".bwd_dw" items)
+# of the LAST N Linear ops of every backward chain of Linear ops (DLRM: the top MLP's first layer,
+# right before the interaction backward) run on a third HIP stream, forked where the chain ends on
+# the main stream and joined before the optimizer / the segment end: they overlap the memory-bound
+# interaction / embedding backward instead of delaying it.  Earlier layers keep dX + dW inline: every
+# Linear's dW on the side stream (forked right after its dX) ran BESIDE the next layers' dX GEMMs, and
+# two 1-block-per-CU GEMMs sharing the chip took 45 % longer than back to back (fp32 step 1.30 vs 1.18
+# ms, profiles/bench_ab_dw_stream_r6.txt).  The dW GEMMs use their own split-K workspace
+# (flexmi.ops._kernels.workspace is per stream).  0 = off.
+DW_STREAM = max(0, int(os.environ.get("FM_DW_STREAM", "1")))
 
-
-# items after the embedding-group backward that touch nothing it writes when every group table is
-# trained by fused sparse SGD (no dense table gradient): with FM_EMB_LATE_JOIN=1 the dense optimizer
-# step and the split-K stream join run on the main stream without waiting for the side stream,
-# which is joined at the segment end instead.  OPT-IN: measured slower on the MLPerf fp32 step
-# (1.189 vs 1.178 ms, profiles/bench_ab_late_join_r5w.txt -- the optimizer sweep then contends
-# with the embedding backward instead of running alone after it)
-LATE_JOIN_OK = ("update", "gemm.join", "fused_sgd.disarm")
-
-# FM_EMB_FWD_DELAY=d: fork a hoisted embedding-group forward d items later than the earliest point
-# it may start (A/B: lets the first bottom-MLP layer run alone instead of beside the gather; measured
-# no better on the MLPerf fp32 step, profiles/bench_ab_emb_fwd_delay_r5za.txt)
-EMB_FWD_DELAY = max(0, int(os.environ.get("FM_EMB_FWD_DELAY", "0")))
-
-
-def _run_overlapped(items, s, side, late_join=False):
-    """Issue one graph segment's items with the embedding groups on ``side`` (fork/join by events,
-    which stream capture records as graph edges).  A group forward is hoisted only across plain
+def _run_overlapped(items, s, side, dws=None):
+    """Issue one graph segment's items with the embedding groups on ``side`` and the Linear
+    weight-gradient items (".bwd_dw") on ``dws`` (fork/join by events, which stream capture records
+    as graph edges; either stream may be None).  A group forward is hoisted only across plain
     op forwards that declare what they write (``Item.writes``) and write none of the group's
     inputs (``Item.reads``): never across reshards, exchange unpacks or another group.
-    ``late_join``: the items named in LATE_JOIN_OK do not wait for a pending group backward."""
-    fwd = [k for k, it in enumerate(items) if it.name.endswith(".group_fwd")]
+    (Measured and dropped: forking the group forward later than its earliest point, and letting the
+    optimizer skip the join of a pending group backward -- profiles/bench_ab_emb_fwd_delay_r5za.txt,
+    bench_ab_late_join_r5w.txt.)  A dW item forks after everything issued before it on the main stream (the op's dX item, which
+    reads the weight a fused-SGD dW updates); the main stream joins the dW stream before every item
+    that is not itself a backward / dX item (the optimizer, gradient joins, fused-SGD disarm, ...)
+    and at the segment end."""
+    # without the side stream the embedding-group items run in place on the main stream
+    fwd = [k for k, it in enumerate(items) if it.name.endswith(".group_fwd")] if side is not None else []
     hoist, fork_at = set(), {}
     for k in fwd:
         j = k
@@ -235,12 +233,11 @@ def _run_overlapped(items, s, side, late_join=False):
             if prev.writes is None or prev.name.endswith(".group_fwd") or (prev.writes & reads):
                 break
             j -= 1
-        j = min(k, j + EMB_FWD_DELAY)
         if j < k:
             hoist.add(k)
             fork_at.setdefault(j, []).append(k)
     joined_fwd = set()
-    bwd_pending = False
+    bwd_pending = dw_pending = False
     for k, it in enumerate(items):
         if k in fork_at:
             side.wait_stream(s)
@@ -251,18 +248,29 @@ def _run_overlapped(items, s, side, late_join=False):
             s.wait_stream(side)      # join at the item's original position (before its consumer)
             joined_fwd.add(k)
             continue
-        if it.name.endswith(".group_bwd"):
+        if side is not None and it.name.endswith(".group_bwd"):
             side.wait_stream(s)
             with torch.cuda.stream(side):
                 it.fn()
             bwd_pending = True
             continue
-        if bwd_pending and not it.name.endswith((".bwd", ".bwd_dw", ".bwd_dx")) and not (
-                late_join and it.name in LATE_JOIN_OK):
+        if dws is not None and it.name.endswith(".bwd_dw"):
+            dws.wait_stream(s)
+            with torch.cuda.stream(dws):
+                it.fn()
+            dw_pending = True
+            continue
+        if bwd_pending and not it.name.endswith((".bwd", ".bwd_dw", ".bwd_dx")):
             s.wait_stream(side)
             bwd_pending = False
+        if dw_pending and not it.name.endswith((".bwd", ".bwd_dx", ".group_bwd")):
+            s.wait_stream(dws)
+            dw_pending = False
         it.fn()
-    s.wait_stream(side)
+    if side is not None:
+        s.wait_stream(side)
+    if dws is not None:
+        s.wait_stream(dws)
 
 
 class Item:
@@ -706,6 +714,9 @@ class Executor:
         self.strategies = strategies
         self.timer = OpTimer(self.cfg.profiling, self.backend == "hip")
         self.debug = bool(getattr(self.cfg, "debug", False))
+        # the last DW_STREAM Linear dW GEMMs of each backward Linear chain as items of their own at the
+        # chain end (any backend: eager runs them in order), on a third stream in captured HIP steps
+        self._dw_stream = DW_STREAM if not self.debug else 0
         self.watchdog = None
         if getattr(self.cfg, "watchdog_s", 0) > 0:
             from flexmi.runtime.health import Watchdog
@@ -918,16 +929,7 @@ class Executor:
         self._build_epilogue_fusion(ops)
         self._build_binary_relu_fusion(ops)
         self._build_conv_chain_fusion(ops)
-        self._build_gather_fusion(ops)
-        self._build_interaction_act_fusion(ops)    # after the gather fusion: not with gathered rows
-        if self.backend == "hip":
-            # dW split-K reduces on a side stream (csrc/kernels/gemm_async.hip), joined before
-            # every collective and at the end of the backward program (_with_gemm_joins)
-            from flexmi.core.types import OperatorType
-            for op in ops:
-                c = self.ctx.get(op.guid)
-                if c is not None and op.op_type == OperatorType.OP_LINEAR:
-                    c.saved["async_dw"] = True
+        self._build_interaction_act_fusion(ops)
         self.adam_state = torch.tensor([1.0, 1.0, 0.0], dtype=torch.float32, device=self.device)
         self._compile_program()
 
@@ -1004,7 +1006,7 @@ class Executor:
             dop, idx = cons[0]
             cd = self.ctx.get(dop.guid)
             if (type(dop).__name__ != "DotInteraction" or idx != 0 or cd is None or cd.in_grads[0] is None
-                    or "gather" in cd.saved or not self.need[(dop.guid, idx)].same_as(self.home[t.guid])):
+                    or not self.need[(dop.guid, idx)].same_as(self.home[t.guid])):
                 continue
             cd.saved["act0"] = int(op.activation)
             c1.saved["grad_is_dpre"] = True
@@ -1089,64 +1091,6 @@ class Executor:
             gs_a = torch.zeros((N, Hg, Wg, Kp), dtype=ya.dtype, device=dev)
             ca.saved["nhwc_gs"], ca.saved["nhwc_g_prestaged"] = gs_a, True
             cb.saved["nhwc_dgrad_out2"] = (gs_a, (Hg, Wg, Kp, gt, gl, dh, dw, 0))
-
-    def _build_gather_fusion(self, ops):
-        """Embedding group E -> DotInteraction D (every member's output consumed only by D, in
-        D's layout; bag-1 SUM lookups into a whole local fp32 table): D's kernels read the table
-        rows straight through the lookup indices, so E's forward never runs and its [B, d] outputs
-        are never written and re-read (DLRM MLPerf fp32: 26 x 8192 x 128 x 4 B = 109 MB each way
-        per step).  E's backward is unchanged: D's backward still writes E's output gradients,
-        reading the (not yet updated) table rows the same way.  Reference: the embedding writes
-        its output and the interaction/concat re-reads it (src/ops/embedding.cu:173-224,
-        src/ops/concat.cu:159-235).  OPT-IN (FM_EMB_GATHER=1): measured on the DLRM MLPerf fp32
-        step it LOSES 33 us (1.492 vs 1.459 ms/step, profiles/emb_gather_ab_r5c.txt) -- unfused,
-        the embedding forward runs on a side stream under the bottom MLP, fused the random row
-        gather sits on the critical path inside the interaction kernel.  Off under --debug and for
-        micro-batch-pipelined tails (XCHG_CHUNKS_LOCAL)."""
-        from flexmi.core.types import AggrMode, OperatorType
-        if (self.backend != "hip" or self.debug or XCHG_LOCAL or os.environ.get("FM_EMB_GATHER", "0") != "1"):
-            return
-        for d in ops:
-            if d.op_type != OperatorType.OP_DOT_INTERACTION:
-                continue
-            cd = self.ctx.get(d.guid)
-            if cd is None or cd.empty or d.guid in self.group_of or cd.outputs[0] is None:
-                continue
-            if cd.outputs[0].dtype != torch.float32 or d.d not in (32, 64, 128):
-                continue
-            spec = [None] * len(d.inputs)
-            for i, t in enumerate(d.inputs):
-                e = t.owner_op
-                if e is None or e.op_type != OperatorType.OP_EMBEDDING or getattr(e, "host_exec", False):
-                    continue
-                ce = self.ctx.get(e.guid)
-                cons = self.consumers.get(t.guid, [])
-                if ce is None or ce.empty or len(cons) != 1 or t is self.final:
-                    continue
-                idx, w = ce.inputs[0], ce.weights[0]
-                if (idx is None or w is None or idx.dim() != 2 or idx.shape[1] != 1 or not idx.is_contiguous()
-                        or w.dtype != torch.float32 or tuple(w.shape) != (e.num_entries, e.out_dim)
-                        or Embedding_row_lo(ce) != 0 or ce.outputs[0].dtype != torch.float32
-                        or not self.need[(d.guid, i)].same_as(self.home[t.guid])
-                        or idx.shape[0] != cd.outputs[0].shape[0]):
-                    continue
-                grp = self.group_of.get(e.guid, [e])
-                spec[i] = (w, idx, grp, [self.ctx[o.guid] for o in grp])
-            # a group is fused only when ALL its members feed this interaction through the gather
-            fused = {}
-            for s_ in spec:
-                if s_ is not None:
-                    fused.setdefault(id(s_[2]), [s_[2], 0])[1] += 1
-            for i, s_ in enumerate(spec):
-                if s_ is not None and fused[id(s_[2])][1] != len(s_[2]):
-                    spec[i] = None
-            if not any(s_ is not None for s_ in spec):
-                continue
-            cd.saved["gather"] = spec
-            for s_ in spec:
-                if s_ is not None:
-                    for c in s_[3]:
-                        c.saved["gathered"] = True
 
     def _build_groups(self, ops):
         """Fuse independent ops of the same kind and placement into one launch (embedding
@@ -1684,9 +1628,6 @@ class Executor:
             if any(g.zero for g in self.groups):
                 upd.append(Item("comm", self._zero_gather, "zero.allgather", native=("ag_sync",)))
                 C(upd, "zero.cast", self._zero_cast)
-        from flexmi.ops import _kernels as K
-        if self.backend == "hip" and K.ASYNC_DW:
-            bwd = self._with_gemm_joins(bwd)
         self.prog_fwd, self.prog_bwd, self.prog_upd = fwd, bwd, upd
         self._plan_fused_sgd()
 
@@ -1764,20 +1705,6 @@ class Executor:
         self.prog_upd_fused = [Item("compute", (lambda: self._optimizer_step(fused=True)), "update")
                                if it.name == "update" else it for it in self.prog_upd]
 
-    @staticmethod
-    def _with_gemm_joins(items):
-        """A side-stream split-K reduce (Linear dW) is joined into the compute stream before every
-        collective -- it may read the gradient, and a captured segment must join its forks -- and
-        at the end of the program."""
-        from flexmi.ops import _kernels as K
-        out = []
-        for it in items:
-            if it.kind == "comm":
-                out.append(Item("compute", K.gemm_join, "gemm.join"))
-            out.append(it)
-        out.append(Item("compute", K.gemm_join, "gemm.join"))
-        return out
-
     def _emit_exchange_start(self, lst, ex, name):
         name = getattr(ex, "tag", None) or name
         lst.append(Item("compute", ex.pack, name + ".pack"))
@@ -1792,8 +1719,6 @@ class Executor:
         c = self.ctx.get(op.guid)
         if c is None:
             return
-        if c.saved.get("gathered"):
-            return       # read in place by its interaction (Executor._build_gather_fusion)
         grp = self.group_of.get(op.guid)
         if grp is not None:
             if grp[0] is op:
@@ -1873,6 +1798,35 @@ class Executor:
                 bucket_done([dop])
             deferred.clear()
 
+        # DW_STREAM: runs of consecutive Linear backward steps; the last N of each run take the dW stream
+        dw_side, dw_flush = set(), set()
+        if self._dw_stream:
+            def lin(j):
+                st = steps[j]
+                if st[0] != "op" or st[1].op_type != OperatorType.OP_LINEAR or not st[1].weights:
+                    return False
+                op, c = st[1], self.ctx.get(st[1].guid)
+                return (c is not None and op.guid not in self.group_of and not getattr(op, "host_exec", False)
+                        and not getattr(op, "sparse_dp", None))
+            j = 0
+            while j < len(steps):
+                if not lin(j):
+                    j += 1
+                    continue
+                e = j
+                while e + 1 < len(steps) and lin(e + 1):
+                    e += 1
+                dw_side.update(range(max(j, e + 1 - self._dw_stream), e + 1))
+                dw_flush.add(e)
+                j = e + 1
+        chain_dw = []
+
+        def flush_chain():
+            for dop, dc in chain_dw:
+                C(bwd, dop.name + ".bwd_dw", (lambda op=dop, c=dc: op.backward(c, "dw")))
+                bucket_done([dop])
+            chain_dw.clear()
+
         pipe = getattr(self, "pipe", None)
         kb = pipe["kb"] if pipe is not None else None
         skip_to = -1
@@ -1910,6 +1864,11 @@ class Executor:
                         C(bwd, op.name + ".bwd_dx", (lambda op=op, c=c, flags=flags: self._bwd_op(op, c, flags, "dx")))
                         bwd[-1].check = (lambda op=op, c=c: self._check_op(op.name + ".bwd", c.in_grads, "input grad"))
                         deferred.append((op, c))
+                    elif k in dw_side:
+                        # dX now on the main stream; dW at the chain end (the dW stream of captured steps)
+                        C(bwd, op.name + ".bwd_dx", (lambda op=op, c=c, flags=flags: self._bwd_op(op, c, flags, "dx")))
+                        bwd[-1].check = (lambda op=op, c=c: self._check_op(op.name + ".bwd", c.in_grads, "input grad"))
+                        chain_dw.append((op, c))
                     else:
                         bwd.append(Item("comm" if getattr(op, "host_exec", False) else "compute",
                                         (lambda op=op, c=c, flags=flags: self._bwd_op(op, c, flags)), op.name + ".bwd"))
@@ -1924,7 +1883,11 @@ class Executor:
                 done_ops = [op] if grp is None else (list(grp) if grp[0] is op else [])
                 if deferred and deferred[-1][0] is op:
                     done_ops = []            # its dW (and bucket) come with the deferred items
+                if chain_dw and chain_dw[-1][0] is op:
+                    done_ops = []            # its dW (and bucket) come at the chain end
                 bucket_done(done_ops)
+                if k in dw_flush:
+                    flush_chain()
             else:
                 items, seen = [], set()
                 for op, i, g, rs in st[1]:
@@ -1944,6 +1907,7 @@ class Executor:
                     finish_before[nxt].append(ex)
                 for op, i, g, rs in st[1]:
                     written.add(self.gkey(g))
+        flush_chain()
         flush_deferred()
         for ex in finish_before.pop(len(steps), []):
             self._emit_exchange_finish(bwd, ex, "reshard.bwd")
@@ -2451,13 +2415,6 @@ class Executor:
             return self.prog_fwd + self.prog_bwd_fused + self.prog_upd_fused
         return self.prog_fwd + self.prog_bwd + self.prog_upd
 
-    def _groups_sparse_only(self):
-        """Every fused embedding group's tables are trained by fused sparse SGD on this rank (no
-        dense gradient, no sparse-DP collectives): their backward writes only the tables."""
-        ops = {id(op): op for grp in self.group_of.values() for op in grp}.values()
-        return bool(ops) and all(getattr(op, "sparse_sgd", False) and not getattr(op, "sparse_dp", None)
-                                 and not getattr(op, "host_exec", False) for op in ops)
-
     def capture_step(self, pre=None):
         """The training step as a replayable hipGraph program (see ``_capture_step``).  The
         per-step gradient memset is left out of the graph: the update kernels consume the
@@ -2497,16 +2454,19 @@ class Executor:
                 segments.append(("comm", it))
         if cur:
             segments.append(("graph", cur))
-        # FM_STREAM_PRIO=1 (A/B): the main stream (MLP chain, the critical path) at high priority and
-        # the embedding side stream at the default (lowest) one.  Measured much slower (2.08-2.19 vs
-        # 1.15 ms/step, profiles/bench_ab_stream_prio_r5p.txt): the captured graph then starts the
-        # MLP chain ~30 us late and idles 84 us per step between the two queues
-        prio = os.environ.get("FM_STREAM_PRIO", "0") == "1"
-        s = torch.cuda.Stream(priority=-1) if prio else torch.cuda.Stream()
+        # (a high-priority main stream measured much slower: 2.08-2.19 vs 1.15 ms/step,
+        # profiles/bench_ab_stream_prio_r5p.txt -- the graph started the MLP chain ~30 us late)
+        s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         ov = overlap_embeddings_enabled(self)
         side = torch.cuda.Stream() if ov else None
-        late = ov and os.environ.get("FM_EMB_LATE_JOIN", "0") == "1" and self._groups_sparse_only()
+        dws = None
+        if self._dw_stream and any(it.name.endswith(".bwd_dw") for it in prog):
+            dws = torch.cuda.Stream()
+            # the dW GEMMs' split-K workspace on their own stream, allocated outside the capture
+            from flexmi.ops import _kernels as K
+            with torch.cuda.stream(dws):
+                K.workspace(self.device, K.GEMM_WS_BYTES)
         runs = []
         graphs = []
         # thread_local capture: the RCCL process group's watchdog thread queries events while
@@ -2516,8 +2476,8 @@ class Executor:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.stream(s):
                     with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
-                        if ov:
-                            _run_overlapped(x, s, side, late)
+                        if ov or dws is not None:
+                            _run_overlapped(x, s, side, dws)
                         else:
                             for it in x:
                                 it.fn()

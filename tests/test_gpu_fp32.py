@@ -35,29 +35,6 @@ def test_gemm_f32_orientations(gpu, a_k, b_k, M, N, K):
     assert rel_err(C, ref) < TOL, (a_k, b_k, M, N, K, rel_err(C, ref))
 
 
-@pytest.mark.parametrize("variant", [1, 3])
-@pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, False)])
-@pytest.mark.parametrize("M,N,K", [(8192, 1024, 1024), (1024, 1024, 8192), (1000, 520, 512)])
-def test_gemm_f32_lds_dma_variant(gpu, variant, a_k, b_k, M, N, K):
-    """The opt-in LDS-DMA pipelined fp32 kernel (256x128 with 8 or 4 waves, 128x128, split-K)."""
-    from flexmi.ops import _kernels as Kk
-    torch.manual_seed(4)
-    A, B = torch.randn(M, K, device=gpu), torch.randn(K, N, device=gpu)
-    Ag = A if a_k else A.t().contiguous()
-    Bg = B.t().contiguous() if b_k else B
-    C = torch.empty(M, N, device=gpu)
-    db = torch.zeros(M, device=gpu)
-    Kk.C().gemm_f32_set_variant(variant)
-    try:
-        Kk.gemm(Ag, K if a_k else M, a_k, Bg, K if b_k else N, b_k, C, N, M, N, K,
-                rowsum_a=None if a_k else db)
-    finally:
-        Kk.C().gemm_f32_set_variant(0)
-    assert rel_err(C, A.double() @ B.double()) < TOL
-    if not a_k:
-        assert rel_err(db, A.double().sum(1)) < TOL
-
-
 def test_gemm_f32_epilogue_bias_act_beta(gpu):
     from flexmi.ops import _kernels as Kk
     torch.manual_seed(1)
@@ -89,19 +66,13 @@ def test_gemm_f32_splitk_and_batch(gpu, ks):
     Kk.bmm(X, O, Y.new_empty(bs, 72, 24), True, False, False)    # transposed A operand
 
 
-@pytest.mark.parametrize("M,K,N,variant", [(2048, 512, 256, 0), (8192, 1024, 1024, 0), (8192, 1024, 1024, 20),
-                                           (8192, 480, 1024, 0)])
-def test_gemm_f32_fused_backward_epilogue(gpu, M, K, N, variant):
+@pytest.mark.parametrize("M,K,N", [(2048, 512, 256), (8192, 1024, 1024), (8192, 480, 1024)])
+def test_gemm_f32_fused_backward_epilogue(gpu, M, K, N):
     """dX GEMM with the activation backward of the layer below (y fp32) and its bias-gradient
-    column sums fused; dW GEMM with the bias gradient as row sums of the staged MN-contiguous A.
-    The MLPerf shapes run the 8-wave 128x128 kernel (variant 20: the 4-wave one)."""
+    column sums fused; dW GEMM with the bias gradient as row sums of the staged MN-contiguous A."""
     from flexmi.ops import _kernels as Kk
     torch.manual_seed(3)
-    Kk.C().gemm_f32_set_variant(variant)
-    try:
-        _fused_backward_epilogue(Kk, gpu, M, K, N)
-    finally:
-        Kk.C().gemm_f32_set_variant(0)
+    _fused_backward_epilogue(Kk, gpu, M, K, N)
 
 
 def _fused_backward_epilogue(Kk, gpu, M, K, N):     # dpre [M,N], W [N,K] -> dX [M,K]
@@ -247,119 +218,6 @@ def test_dot_interaction_f32_act0(gpu, F, D, selfi):
         assert rel_err(dz[i], dZ[:, i]) < TOL, i
 
 
-@pytest.mark.parametrize("F,D,selfi,i64", [(27, 128, False, True), (9, 64, True, False), (5, 32, False, True)])
-def test_dot_interaction_gather_f32(gpu, F, D, selfi, i64):
-    """Embedding-into-interaction kernels: features 1.. are TABLE rows gathered by bag-1 indices
-    (incl. duplicates and an out-of-range index, clamped), forward and backward vs float64."""
-    from flexmi.ops import _kernels as Kk
-    torch.manual_seed(19)
-    B = 1000
-    x = torch.randn(B, D, device=gpu)
-    rows = [3, 70, 1000, 40000] * F
-    tabs = [torch.randn(rows[i], D, device=gpu) for i in range(F - 1)]
-    idt = torch.int64 if i64 else torch.int32
-    ixs = [torch.randint(0, t.shape[0], (B, 1), device=gpu, dtype=idt) for t in tabs]
-    ixs[0][5, 0] = tabs[0].shape[0] + 7          # out of range: clamped to the last row
-    cl = [ix.view(-1).long().clamp(0, t.shape[0] - 1) for ix, t in zip(ixs, tabs)]
-    zs = [x] + [t[c] for t, c in zip(tabs, cl)]  # the materialised rows (oracle)
-    npairs = F * (F + 1) // 2 if selfi else F * (F - 1) // 2
-    W = (D + npairs + 15) // 16 * 16
-    y = torch.full((B, W), 7.0, device=gpu)
-    assert Kk.dot_interaction_forward_gather([x] + tabs, [None] + ixs, y, selfi)
-    Z = torch.stack([z.double() for z in zs], 1)
-    G = Z @ Z.transpose(1, 2)
-    li, lj = zip(*[(i, j) for i in range(F) for j in range(i + (1 if selfi else 0))])
-    ref = torch.zeros(B, W, dtype=torch.float64, device=gpu)
-    ref[:, :D] = Z[:, 0]
-    ref[:, D:D + npairs] = G[:, li, lj]
-    assert rel_err(y, ref) < TOL
-    dy = torch.randn(B, W, device=gpu)
-    dz = [torch.randn(B, D, device=gpu) for _ in range(F)]
-    old = [g.double().clone() for g in dz]
-    accs = [i % 2 == 1 for i in range(F)]
-    assert Kk.dot_interaction_backward_gather([x] + tabs, [None] + ixs, dy, dz, accs, selfi)
-    dG = torch.zeros(B, F, F, dtype=torch.float64, device=gpu)
-    dG[:, li, lj] = dy[:, D:D + npairs].double()
-    dZ = (dG + dG.transpose(1, 2)) @ Z
-    dZ[:, 0] += dy[:, :D].double()
-    for i in range(F):
-        exp = dZ[:, i] + (old[i] if accs[i] else 0)
-        assert rel_err(dz[i], exp) < TOL, i
-
-
-def test_embedding_gather_fusion_on_off_equivalent(gpu, monkeypatch):
-    """The executor's embedding-into-interaction fusion (Executor._build_gather_fusion) trains a
-    DLRM exactly like materialised embedding outputs (FM_EMB_GATHER=0), and really engages."""
-    from flexmi.models.dlrm import DLRMConfig
-    dcfg = DLRMConfig(128, [5000, 300, 12, 70000, 40], [13, 256, 128], [256, 256, 1], 1, -1, -1, 0.0, "dot", "", -1,
-                      "bce", "gather")
-    res = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("FM_EMB_GATHER", mode)
-        ws, loss, ex = _dlrm_run("gpu", dcfg, 2048, 4, graph=True)
-        dots = [op for op in ex.model.layers if type(op).__name__ == "DotInteraction"]
-        fused = any("gather" in ex.ctx[op.guid].saved for op in dots)
-        assert fused == (mode == "1"), mode
-        res[mode] = (ws, loss)
-    _assert_params_close(res["0"][0], res["1"][0], 1e-5)
-    assert abs(res["0"][1] - res["1"][1]) < 1e-5
-
-
-# ---------------------------------------------------------------- whole models, fp32 GPU vs fp32 CPU
-def _dlrm_run(dev, dcfg, B, steps, seed=0, graph=False, lr=0.1):
-    from flexmi.core import FFConfig, FFModel, SGDOptimizer, LossType, MetricsType
-    from flexmi.models.dlrm import build_dlrm
-    rng = np.random.RandomState(seed)
-    cfg = FFConfig()
-    cfg.batchSize = B
-    cfg.device = dev
-    cfg.compute_dtype = "fp32"
-    cfg.seed = 5
-    m = FFModel(cfg)
-    d, s, p = build_dlrm(m, dcfg)
-    m.compile(SGDOptimizer(m, lr), LossType.LOSS_BINARY_CROSSENTROPY, [MetricsType.METRICS_ACCURACY])
-    ex = m.init_layers()
-    batches = []
-    for _ in range(steps):
-        dd = np.zeros((B, d.dims[1]), np.float32)
-        dd[:, :13] = rng.rand(B, 13)
-        # skewed indices: hot rows repeat (atomic / duplicate paths), tails stay mostly unique
-        sp = [np.minimum((rng.zipf(1.2, (B, dcfg.embedding_bag_size)) - 1), r - 1).astype(np.int64)
-              if r > 64 else rng.randint(0, r, (B, dcfg.embedding_bag_size)).astype(np.int64)
-              for r in dcfg.embedding_size]
-        lab = rng.randint(0, 2, (B, 1)).astype(np.float32)
-        batches.append((dd, sp, lab))
-
-    def feed(k):
-        dd, sp, lab = batches[k]
-        ex.scatter_from_host(d, dd)
-        for t, a in zip(s, sp):
-            ex.scatter_from_host(t, a)
-        ex.scatter_from_host(m.get_label_tensor(), lab)
-
-    if graph and dev == "gpu":
-        feed(0)
-        ex.train_step()
-        run = ex.capture_step()
-        for k in range(1, steps):
-            feed(k)          # host scatter into the captured input buffers, then replay
-            run()
-        torch.cuda.synchronize()
-    else:
-        for k in range(steps):
-            feed(k)
-            ex.train_step()
-    ws = [w.get_weights(m) for w in m.parameters]
-    ws[0] = ws[0][:, :13]   # the GPU pads the 13 dense features (zero input columns) for aligned loads
-    return ws, m.get_perf_metrics().get_loss(), ex
-
-
-def _assert_params_close(a_list, b_list, rtol):
-    for a, b in zip(a_list, b_list):
-        err = np.abs(a - b).max() / max(np.abs(a).max(), 1e-6)
-        assert err < rtol, (a.shape, err)
-
-
 def test_dlrm_tiny_fp32_gpu_matches_cpu(gpu):
     from flexmi.models.dlrm import DLRMConfig
     dcfg = DLRMConfig.preset("tiny")
@@ -456,24 +314,24 @@ def test_lstm_fp32_gpu_matches_cpu(gpu, state):
 
 
 def test_embedding_overlap_on_off_equivalent(gpu, monkeypatch):
-    """Captured steps with the fused embedding groups on a second HIP stream (OVERLAP_EMB=1) train
-    exactly like the single-stream schedule (=0): multi-table group, >= 128-wide tables, bottom MLP."""
+    """Captured steps with the fused embedding groups on a second HIP stream (OVERLAP_EMB=1) and the
+    Linear dW GEMMs on a third (DW_STREAM) train exactly like the single-stream schedule: multi-table
+    group, >= 128-wide tables, bottom MLP."""
     from flexmi.models.dlrm import DLRMConfig
     from flexmi.runtime import executor as E
     dcfg = DLRMConfig(128, [5000, 300, 12, 70000, 40], [13, 256, 128], [256, 256, 1], 1, -1, -1, 0.0, "dot", "", -1,
                       "bce", "overlap")
     res = {}
-    for mode in ("0", "1", "1-early-join"):
+    for mode in ("00", "10", "11", "01"):
         monkeypatch.setattr(E, "OVERLAP_EMB", mode[0])
-        # late join (opt-in): the dense update does not wait for the sparse-SGD table backward
-        monkeypatch.setenv("FM_EMB_LATE_JOIN", "0" if mode == "1-early-join" else "1")
+        monkeypatch.setattr(E, "DW_STREAM", mode[1] == "1")
         ws, loss, ex = _dlrm_run("gpu", dcfg, 2048, 4, graph=True)
         assert E.overlap_embeddings_enabled(ex) == (mode[0] == "1")
-        assert ex._groups_sparse_only()
+        assert any(it.name.endswith(".bwd_dw") for it in ex.step_program()) == (mode[1] == "1")
         res[mode] = (ws, loss)
-    for mode in ("1", "1-early-join"):
-        _assert_params_close(res["0"][0], res[mode][0], 1e-5)
-        assert abs(res["0"][1] - res[mode][1]) < 1e-5
+    for mode in ("10", "11", "01"):
+        _assert_params_close(res["00"][0], res[mode][0], 1e-5)
+        assert abs(res["00"][1] - res[mode][1]) < 1e-5
 
 
 # ---------------------------------------------------------------- CNN kernels (fp32)

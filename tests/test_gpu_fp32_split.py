@@ -1,8 +1,7 @@
-"""fp32 GEMM on the bf16 matrix cores by exact three-way operand splitting (csrc/kernels/gemm_f32.hip
-fm_gemm_x3_kernel, FM_F32_SPLIT=1, and its second form csrc/kernels/gemm_x3.hip, FM_F32_SPLIT=2 /
-gemm_f32_set_split(mode)): every orientation, tails, epilogues, fused SGD, the
-fused backward epilogue, row sums and split-K against a float64 oracle at the fp32 test tolerance,
-with its error compared to the native v_mfma_f32_16x16x4_f32 kernel's on the same inputs."""
+"""fp32 GEMM on the bf16 matrix cores by exact three-way operand splitting (csrc/kernels/gemm_x3.hip;
+gemm_f32_set_split(2) = every eligible GEMM, 3 = the default big-GEMM policy): every orientation, tails, epilogues, fused SGD, the fused
+backward epilogue, row sums and split-K against a float64 oracle at the fp32 test tolerance, with
+its error compared to the native v_mfma_f32_16x16x4_f32 kernel's on the same inputs."""
 import pytest
 import torch
 
@@ -11,7 +10,7 @@ from tests.test_gpu_fp32 import TOL, _fused_backward_epilogue, rel_err
 pytestmark = pytest.mark.gpu
 
 
-MODES = [1, 2]
+MODES = [2, 3]     # split mode
 
 
 @pytest.fixture(params=MODES)
@@ -44,7 +43,10 @@ def _gemm(Kk, A, B, a_k, b_k, M, N, K):
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 200, 130), (8192, 1024, 1024), (2048, 479, 512),
                                    (8192, 1024, 480), (1000, 1020, 8192), (256, 4096, 4096), (129, 67, 67),
-                                   (330, 194, 96), (8192, 512, 1024), (1024, 480, 8192)])
+                                   (330, 194, 96), (8192, 512, 1024), (1024, 480, 8192),
+                                   # the default policy's boundaries (mode 3: min(M, N) >= 480, K >= 480)
+                                   (480, 480, 480), (479, 1024, 1024), (1024, 479, 1024), (1024, 1024, 479),
+                                   (480, 512, 512)])
 def test_split_gemm_orientations_vs_native(gpu, mode, a_k, b_k, M, N, K):
     from flexmi.ops import _kernels as Kk
     torch.manual_seed(M + N + K)

@@ -66,63 +66,6 @@ def test_gemm_splitk_and_batch(gpu):
     assert rel_err(O, bf(X).float() @ bf(Y).float()) < 1e-2
 
 
-@pytest.mark.parametrize("ks", [2, 3, 4])
-@pytest.mark.parametrize("M,N,c_fp32,kc", [(1024, 1024, True, False), (200, 130, True, False), (256, 96, False, False),
-                                           (77, 50, False, False), (2048, 2048, True, True)])
-def test_gemm_splitk_inlaunch_combine(gpu, ks, M, N, c_fp32, kc):
-    """Split-K slices combined INSIDE the launch by each tile's last arriving block (write-through
-    slabs + agent-scope ticket): bias + relu + beta accumulate, fp32 and bf16 C, ragged N, the
-    register-staged and the LDS-DMA kernels; repeated launches reuse the self-resetting counters."""
-    from flexmi.ops import _kernels as Kk
-    torch.manual_seed(3)
-    K = 4096
-    A, B = torch.randn(K, M, device=gpu), torch.randn(K, N, device=gpu)
-    bias = torch.randn(N, device=gpu)
-    dt = torch.float32 if c_fp32 else torch.bfloat16
-    C = torch.randn(M, N, device=gpu).to(dt)
-    acc = C.float().clone()
-    ref = torch.relu(bf(A).float().t() @ bf(B).float() + bias)
-    if kc:
-        Ab, lda, Bb, ldb = bf(A.t().contiguous()), K, bf(B.t().contiguous()), K
-    else:
-        Ab, lda, Bb, ldb = bf(A), M, bf(B), N
-    Kk.C().gemm_set_variant(128)        # opt-in path (measured slower on DLRM; kept correct)
-    try:
-        for rep in range(3):
-            got = Kk.gemm(Ab, lda, kc, Bb, ldb, kc, C, N, M, N, K, bias=bias, act=11, beta=True, ksplit=ks)
-            assert got == ks
-            acc = acc + ref
-            assert rel_err(C, acc) < (2e-3 if c_fp32 else 2e-2), (rep, ks, M, N, kc)
-    finally:
-        Kk.C().gemm_set_variant(0)
-
-
-@pytest.mark.parametrize("rows,D,bag,i64", [(36, 128, 1, True), (155, 128, 1, True), (250, 128, 1, False),
-                                          (60, 96, 2, True), (40, 100, 1, True)])
-def test_embedding_small_table_lds_path(gpu, rows, D, bag, i64):
-    """Small tables (16 < rows, <= 128 KB): block-shared LDS accumulation + one flush atomic per
-    (row, col), for the fused sparse SGD and the dense gradient."""
-    import os
-    if os.environ.get("FM_EMB_SMALL") != "1":
-        pytest.skip("small-table LDS path is opt-in (FM_EMB_SMALL=1)")
-    from flexmi.ops import _kernels as Kk
-    torch.manual_seed(5)
-    B = 8192
-    W = torch.randn(rows, D, device=gpu)
-    idx = torch.randint(0, rows, (B, bag), device=gpu)
-    if not i64:
-        idx = idx.to(torch.int32)
-    dy = torch.randn(B, D, device=gpu).to(torch.bfloat16)
-    lr = torch.tensor([0.05], device=gpu)
-    upd = torch.zeros_like(W)
-    upd.index_add_(0, idx.long().reshape(-1), dy.float().repeat_interleave(bag, 0))
-    W2 = W.clone()
-    Kk.embedding_backward_sgd(idx, dy, W2, lr, 21, {})
-    assert torch.allclose(W2, W - 0.05 * upd, atol=2e-3, rtol=1e-4)
-    dW = torch.empty_like(W)
-    Kk.embedding_backward_dense(idx, dy, dW, 21)
-    assert torch.allclose(dW, upd, atol=2e-2, rtol=1e-4)
-
 
 @pytest.mark.parametrize("B,K,act,dx_acc", [(8192, 256, 12, False), (256, 64, 11, True), (1000, 128, 10, False),
                                             (37, 16, 12, True), (512, 4096, 11, False), (300, 2056, 12, True)])
@@ -550,21 +493,13 @@ def test_embedding_count_update_sgd(gpu, idx_dtype, dy_dtype):
         Kk.C().embedding_set_bwd_mode(False)
 
 
-@pytest.mark.parametrize("rowblock", [False, True])
 @pytest.mark.parametrize("dy_dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("idx_dtype", [torch.int64, torch.int32])
-def test_embedding_rowblock_tables(gpu, idx_dtype, dy_dtype, rowblock):
-    """The MLPerf set's non-claimed table sizes (3 .. 7420 rows at B = 8192) through the default
-    atomic / tiny kernels and through the opt-in row-block ownership kernel (embedding.hip
-    fm_emb_bwd_rowblock: one-chunk plain apply, multi-chunk atomic flush), plus D = 256 / 200 / 24
-    columns, a bag of 3 and a row shard, over two steps, for the fused sparse SGD and the dense
-    gradient, against a float64 oracle."""
-    from flexmi.ops import _kernels as Kk
-    Kk.C().embedding_set_rowblock(rowblock)
-    try:
-        _embedding_small_tables_case(gpu, idx_dtype, dy_dtype)
-    finally:
-        Kk.C().embedding_set_rowblock(False)
+def test_embedding_small_and_mid_tables(gpu, idx_dtype, dy_dtype):
+    """The MLPerf set's non-claimed table sizes (3 .. 7420 rows at B = 8192) through the atomic /
+    tiny kernels, plus D = 256 / 200 / 24 columns, a bag of 3 and a row shard, over two steps, for
+    the fused sparse SGD and the dense gradient, against a float64 oracle."""
+    _embedding_small_tables_case(gpu, idx_dtype, dy_dtype)
 
 
 def _embedding_small_tables_case(gpu, idx_dtype, dy_dtype):
@@ -664,68 +599,3 @@ def test_embedding_fwd_long_bag_split(gpu, B, bag, D, out_dt):
         assert rel_err(o, ref) < tol, (B, bag, D)
 
 
-@pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
-@pytest.mark.parametrize("M,N,K,ks", [(1024, 512, 256, 1), (300, 200, 96, 1), (8192, 256, 512, 0), (256, 1024, 4096, 4),
-                                      (77, 130, 64, 1)])
-def test_gemm_x1_bigtile(gpu, a_k, b_k, M, N, K, ks):
-    """Big-tile bf16 kernel (gemm_x1.hip, forced with variant bit 512): every operand orientation,
-    ragged edges (clamped rows never stored), split K; bias + relu + beta into bf16 C and the fused
-    backward epilogue of the layer below (act'(y) * v, column sums) vs an fp32 reference."""
-    from flexmi.ops import _kernels as Kk
-    torch.manual_seed(11)
-    A = torch.randn(M, K, device=gpu)
-    B = torch.randn(K, N, device=gpu)
-    Ab = bf(A) if a_k else bf(A.t().contiguous())
-    Bb = bf(B.t().contiguous()) if b_k else bf(B)
-    lda, ldb = (K if a_k else M), (K if b_k else N)
-    ref = bf(A).float() @ bf(B).float()
-    Kk.C().gemm_set_variant(512)
-    try:
-        C = torch.empty(M, N, device=gpu)
-        Kk.gemm(Ab, lda, a_k, Bb, ldb, b_k, C, N, M, N, K, ksplit=ks)
-        assert rel_err(C, ref) < 2e-3, "plain"
-        bias = torch.randn(N, device=gpu)
-        Cb = torch.randn(M, N, device=gpu).to(torch.bfloat16)
-        C0 = Cb.float().clone()
-        Kk.gemm(Ab, lda, a_k, Bb, ldb, b_k, Cb, N, M, N, K, bias=bias, act=11, beta=True, ksplit=ks)
-        assert rel_err(Cb, torch.relu(ref + bias) + C0) < 1e-2, "bias/relu/beta"
-        y = torch.relu(torch.randn(M, N, device=gpu)).to(torch.bfloat16)
-        cs = torch.zeros(N, device=gpu)
-        Cd = torch.empty(M, N, device=gpu)
-        Kk.gemm(Ab, lda, a_k, Bb, ldb, b_k, Cd, N, M, N, K, act_y=y, bwd_act=11, colsum=cs)
-        d = ref * (y.float() > 0)
-        assert rel_err(Cd, d) < 2e-3, "fused act-bwd"
-        assert rel_err(cs, d.sum(0)) < 2e-3, "colsum"
-    finally:
-        Kk.C().gemm_set_variant(0)
-
-
-@pytest.mark.parametrize("M,N,K", [(1024, 512, 8192), (256, 480, 8192), (130, 200, 1024)])
-def test_gemm_x1_dw_fused_sgd(gpu, M, N, K):
-    """dW GEMM (both operands MN-contiguous) on the big-tile kernel with the bias-gradient row sums
-    and the SGD update fused (unsplit: in the epilogue; split: in the reduce)."""
-    from flexmi.ops import _kernels as Kk
-    torch.manual_seed(12)
-    dpre = bf(torch.randn(K, M, device=gpu))           # [K][M]
-    x = bf(torch.randn(K, N, device=gpu))              # [K][N]
-    g = dpre.float().t() @ x.float()
-    Kk.C().gemm_set_variant(512)
-    try:
-        dw = torch.empty(M, N, device=gpu)
-        rs = torch.zeros(M, device=gpu)
-        Kk.gemm(dpre, M, False, x, N, False, dw, N, M, N, K, rowsum_a=rs)
-        assert rel_err(dw, g) < 2e-3
-        assert rel_err(rs, dpre.float().sum(0)) < 1e-3
-        W = torch.randn(M, N, device=gpu)
-        W0 = W.clone()
-        Wc = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
-        lr = torch.tensor([0.01], device=gpu)
-        db = torch.zeros(M, device=gpu)
-        upd = Kk.FusedSGD(W, Wc, None, lr, 0.0, 0.0, False)
-        assert Kk._dw_fused_sgd(dpre, x, None, db, upd)
-        Wn = W0 - 0.01 * g
-        assert rel_err(W, Wn) < 1e-4
-        assert rel_err(Wc, Wn) < 1e-2
-        assert rel_err(db, dpre.float().sum(0)) < 1e-3
-    finally:
-        Kk.C().gemm_set_variant(0)

@@ -26,18 +26,12 @@ def _ref_pool(x, k, s, pt, pl, P, Q, is_max):
     return (F.avg_pool2d(xp, k, s, divisor_override=1) / F.avg_pool2d(ones, k, s, divisor_override=1))[:, :, :P, :Q]
 
 
-@pytest.mark.parametrize("phases", ["0", "1"])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("is_max", [True, False])
 @pytest.mark.parametrize("H,W,k,s,pt,pl", [(13, 27, 3, 2, 1, 1), (16, 16, 3, 2, -1, -1), (12, 55, 3, 2, 0, -1),
                                             (9, 33, 2, 2, -1, 0), (11, 8, 3, 1, 1, 1), (55, 55, 3, 2, 0, 0),
                                             (27, 27, 3, 2, 0, 0)])
-def test_pool_rows_and_negative_pads(dt, is_max, H, W, k, s, pt, pl, phases, monkeypatch):
-    """phases = 1: the max-pool scatter in (p mod ceil(k/s), q mod ceil(k/s)) classes with plain LDS
-    read-add-writes instead of LDS float atomics (FM_POOL_SCATTER_PHASES)."""
-    if phases == "1" and not is_max:
-        pytest.skip("average pooling has no scatter")
-    monkeypatch.setenv("FM_POOL_SCATTER_PHASES", phases)
+def test_pool_rows_and_negative_pads(dt, is_max, H, W, k, s, pt, pl):
     from flexmi.ops import _kernels as Kk
     torch.manual_seed(H * W + k)
     dev = torch.device("cuda")

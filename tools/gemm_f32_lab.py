@@ -4,7 +4,8 @@ orientations, exactly as the executor issues them (fwd with bias+ReLU epilogue; 
 beta = 1 accumulation and the fused bias-gradient row sums), for a list of FM_GEMM_F32_VARIANT
 values, against hipBLASLt (torch.matmul, fp32).  Checks every variant against a float64 oracle
 and reports the best-of-rounds GPU time per call (hipGraph of 20 calls, interleaved rounds).
-usage: gemm_f32_lab.py v0,v1,... ["M,K,N;..."]   (negative v: split-bf16 form -v, FM_F32_SPLIT)"""
+usage: gemm_f32_lab.py v0,v1,... ["M,K,N;..."]   (v: 0 = native fp32 MFMA kernel, -2 = split-bf16
+kernel 16x16x32 form, -32 = split-bf16 kernel 32x32x16 form)"""
 import json
 import os
 import sys
@@ -27,8 +28,7 @@ def main():
         shapes = [tuple(int(v) for v in t.split(",")) for t in args[1].split(";")]
     torch.backends.cuda.matmul.allow_tf32 = False
     def setv(v):
-        K.C().gemm_f32_set_split(-v if v < 0 else 0)
-        K.C().gemm_f32_set_variant(v if v > 0 else 0)
+        K.C().gemm_f32_set_split(2 if v < 0 else 0)
 
     dev = torch.device("cuda")
     torch.manual_seed(0)

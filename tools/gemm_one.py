@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Run one flexmi GEMM shape repeatedly (for rocprofv3 --pmc): gemm_one.py M K N orient [iters] [bf16|fp32|planes]
+"""Run one flexmi GEMM shape repeatedly (for rocprofv3 --pmc): gemm_one.py M K N orient [iters] [bf16|fp32]
 orient: fwd (x[M,K] . W[N,K]^T), dx (dy[M,N] . W[N,K]), dw (dy^T . x)."""
 import sys
 import torch
@@ -10,7 +10,7 @@ B, k, n = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
 orient = sys.argv[4] if len(sys.argv) > 4 else "fwd"
 iters = int(sys.argv[5]) if len(sys.argv) > 5 else 50
 mode = sys.argv[6] if len(sys.argv) > 6 else "bf16"
-dt = torch.float32 if mode in ("fp32", "planes") else torch.bfloat16
+dt = torch.float32 if mode == "fp32" else torch.bfloat16
 dev = torch.device("cuda")
 x = torch.randn(B, k, device=dev).to(dt)
 w = torch.randn(n, k, device=dev).to(dt)
@@ -18,18 +18,12 @@ dy = torch.randn(B, n, device=dev).to(dt)
 y = torch.empty(B, n, device=dev, dtype=dt)
 dx = torch.empty(B, k, device=dev, dtype=dt)
 dw = torch.empty(n, k, device=dev)
-xp = wp = dyp = None
-if mode == "planes":   # fp32 values from pre-split bf16 planes (csrc/kernels/gemm_pl.hip)
-    xp, wp, dyp = K.planes_like(x), K.planes_like(w), K.planes_like(dy)
-    K.split_planes(x, xp)
-    K.split_planes(w, wp)
-    K.split_planes(dy, dyp)
 for _ in range(iters):
     if orient == "fwd":
-        K.gemm(x, k, True, w, k, True, y, n, B, n, k, act=11, ap=xp, bp=wp)
+        K.gemm(x, k, True, w, k, True, y, n, B, n, k, act=11)
     elif orient == "dx":
-        K.gemm(dy, n, True, w, k, False, dx, k, B, k, n, ap=dyp, bp=wp)
+        K.gemm(dy, n, True, w, k, False, dx, k, B, k, n)
     else:
-        K.gemm(dy, n, False, x, k, False, dw, k, n, k, B, ap=dyp, bp=xp)
+        K.gemm(dy, n, False, x, k, False, dw, k, n, k, B)
 torch.cuda.synchronize()
 print("ok")
