@@ -199,29 +199,15 @@ def overlap_embeddings_enabled(ex):
     return any(st[0] == "op" and type(st[1]).__name__ == "Embedding" and st[1].out_dim >= 128 for st in ex.fwd_steps)
 
 
-# FM_DW_STREAM=N (default 1): inside captured segments, the weight-gradient GEMMs (".bwd_dw" items)
-# of the LAST N Linear ops of every backward chain of Linear ops (DLRM: the top MLP's first layer,
-# right before the interaction backward) run on a third HIP stream, forked where the chain ends on
-# the main stream and joined before the optimizer / the segment end: they overlap the memory-bound
-# interaction / embedding backward instead of delaying it.  Earlier layers keep dX + dW inline: every
-# Linear's dW on the side stream (forked right after its dX) ran BESIDE the next layers' dX GEMMs, and
-# two 1-block-per-CU GEMMs sharing the chip took 45 % longer than back to back (fp32 step 1.30 vs 1.18
-# ms, profiles/bench_ab_dw_stream_r6.txt).  The dW GEMMs use their own split-K workspace
-# (flexmi.ops._kernels.workspace is per stream).  0 = off.
-DW_STREAM = max(0, int(os.environ.get("FM_DW_STREAM", "1")))
-
-def _run_overlapped(items, s, side, dws=None):
-    """Issue one graph segment's items with the embedding groups on ``side`` and the Linear
-    weight-gradient items (".bwd_dw") on ``dws`` (fork/join by events, which stream capture records
-    as graph edges; either stream may be None).  A group forward is hoisted only across plain
+def _run_overlapped(items, s, side):
+    """Issue one graph segment's items with the embedding groups on ``side`` (fork/join by events,
+    which stream capture records as graph edges).  A group forward is hoisted only across plain
     op forwards that declare what they write (``Item.writes``) and write none of the group's
     inputs (``Item.reads``): never across reshards, exchange unpacks or another group.
-    (Measured and dropped: forking the group forward later than its earliest point, and letting the
-    optimizer skip the join of a pending group backward -- profiles/bench_ab_emb_fwd_delay_r5za.txt,
-    bench_ab_late_join_r5w.txt.)  A dW item forks after everything issued before it on the main stream (the op's dX item, which
-    reads the weight a fused-SGD dW updates); the main stream joins the dW stream before every item
-    that is not itself a backward / dX item (the optimizer, gradient joins, fused-SGD disarm, ...)
-    and at the segment end."""
+    (Measured and dropped: forking the group forward later than its earliest point, letting the
+    optimizer skip the join of a pending group backward, and weight-gradient GEMMs on a third
+    stream -- profiles/bench_ab_emb_fwd_delay_r5za.txt, bench_ab_late_join_r5w.txt,
+    dw_stream_ab_r5p4.txt, dw_stream_chain_tail_ab_r6.txt.)"""
     # without the side stream the embedding-group items run in place on the main stream
     fwd = [k for k, it in enumerate(items) if it.name.endswith(".group_fwd")] if side is not None else []
     hoist, fork_at = set(), {}
@@ -237,7 +223,7 @@ def _run_overlapped(items, s, side, dws=None):
             hoist.add(k)
             fork_at.setdefault(j, []).append(k)
     joined_fwd = set()
-    bwd_pending = dw_pending = False
+    bwd_pending = False
     for k, it in enumerate(items):
         if k in fork_at:
             side.wait_stream(s)
@@ -254,23 +240,12 @@ def _run_overlapped(items, s, side, dws=None):
                 it.fn()
             bwd_pending = True
             continue
-        if dws is not None and it.name.endswith(".bwd_dw"):
-            dws.wait_stream(s)
-            with torch.cuda.stream(dws):
-                it.fn()
-            dw_pending = True
-            continue
         if bwd_pending and not it.name.endswith((".bwd", ".bwd_dw", ".bwd_dx")):
             s.wait_stream(side)
             bwd_pending = False
-        if dw_pending and not it.name.endswith((".bwd", ".bwd_dx", ".group_bwd")):
-            s.wait_stream(dws)
-            dw_pending = False
         it.fn()
     if side is not None:
         s.wait_stream(side)
-    if dws is not None:
-        s.wait_stream(dws)
 
 
 class Item:
@@ -714,9 +689,6 @@ class Executor:
         self.strategies = strategies
         self.timer = OpTimer(self.cfg.profiling, self.backend == "hip")
         self.debug = bool(getattr(self.cfg, "debug", False))
-        # the last DW_STREAM Linear dW GEMMs of each backward Linear chain as items of their own at the
-        # chain end (any backend: eager runs them in order), on a third stream in captured HIP steps
-        self._dw_stream = DW_STREAM if not self.debug else 0
         self.watchdog = None
         if getattr(self.cfg, "watchdog_s", 0) > 0:
             from flexmi.runtime.health import Watchdog
@@ -1798,35 +1770,6 @@ class Executor:
                 bucket_done([dop])
             deferred.clear()
 
-        # DW_STREAM: runs of consecutive Linear backward steps; the last N of each run take the dW stream
-        dw_side, dw_flush = set(), set()
-        if self._dw_stream:
-            def lin(j):
-                st = steps[j]
-                if st[0] != "op" or st[1].op_type != OperatorType.OP_LINEAR or not st[1].weights:
-                    return False
-                op, c = st[1], self.ctx.get(st[1].guid)
-                return (c is not None and op.guid not in self.group_of and not getattr(op, "host_exec", False)
-                        and not getattr(op, "sparse_dp", None))
-            j = 0
-            while j < len(steps):
-                if not lin(j):
-                    j += 1
-                    continue
-                e = j
-                while e + 1 < len(steps) and lin(e + 1):
-                    e += 1
-                dw_side.update(range(max(j, e + 1 - self._dw_stream), e + 1))
-                dw_flush.add(e)
-                j = e + 1
-        chain_dw = []
-
-        def flush_chain():
-            for dop, dc in chain_dw:
-                C(bwd, dop.name + ".bwd_dw", (lambda op=dop, c=dc: op.backward(c, "dw")))
-                bucket_done([dop])
-            chain_dw.clear()
-
         pipe = getattr(self, "pipe", None)
         kb = pipe["kb"] if pipe is not None else None
         skip_to = -1
@@ -1864,11 +1807,6 @@ class Executor:
                         C(bwd, op.name + ".bwd_dx", (lambda op=op, c=c, flags=flags: self._bwd_op(op, c, flags, "dx")))
                         bwd[-1].check = (lambda op=op, c=c: self._check_op(op.name + ".bwd", c.in_grads, "input grad"))
                         deferred.append((op, c))
-                    elif k in dw_side:
-                        # dX now on the main stream; dW at the chain end (the dW stream of captured steps)
-                        C(bwd, op.name + ".bwd_dx", (lambda op=op, c=c, flags=flags: self._bwd_op(op, c, flags, "dx")))
-                        bwd[-1].check = (lambda op=op, c=c: self._check_op(op.name + ".bwd", c.in_grads, "input grad"))
-                        chain_dw.append((op, c))
                     else:
                         bwd.append(Item("comm" if getattr(op, "host_exec", False) else "compute",
                                         (lambda op=op, c=c, flags=flags: self._bwd_op(op, c, flags)), op.name + ".bwd"))
@@ -1883,11 +1821,7 @@ class Executor:
                 done_ops = [op] if grp is None else (list(grp) if grp[0] is op else [])
                 if deferred and deferred[-1][0] is op:
                     done_ops = []            # its dW (and bucket) come with the deferred items
-                if chain_dw and chain_dw[-1][0] is op:
-                    done_ops = []            # its dW (and bucket) come at the chain end
                 bucket_done(done_ops)
-                if k in dw_flush:
-                    flush_chain()
             else:
                 items, seen = [], set()
                 for op, i, g, rs in st[1]:
@@ -1907,7 +1841,6 @@ class Executor:
                     finish_before[nxt].append(ex)
                 for op, i, g, rs in st[1]:
                     written.add(self.gkey(g))
-        flush_chain()
         flush_deferred()
         for ex in finish_before.pop(len(steps), []):
             self._emit_exchange_finish(bwd, ex, "reshard.bwd")
@@ -2460,13 +2393,6 @@ class Executor:
         s.wait_stream(torch.cuda.current_stream())
         ov = overlap_embeddings_enabled(self)
         side = torch.cuda.Stream() if ov else None
-        dws = None
-        if self._dw_stream and any(it.name.endswith(".bwd_dw") for it in prog):
-            dws = torch.cuda.Stream()
-            # the dW GEMMs' split-K workspace on their own stream, allocated outside the capture
-            from flexmi.ops import _kernels as K
-            with torch.cuda.stream(dws):
-                K.workspace(self.device, K.GEMM_WS_BYTES)
         runs = []
         graphs = []
         # thread_local capture: the RCCL process group's watchdog thread queries events while
@@ -2476,8 +2402,8 @@ class Executor:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.stream(s):
                     with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
-                        if ov or dws is not None:
-                            _run_overlapped(x, s, side, dws)
+                        if ov:
+                            _run_overlapped(x, s, side)
                         else:
                             for it in x:
                                 it.fn()
