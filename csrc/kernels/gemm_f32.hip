@@ -207,6 +207,51 @@ __global__ void fm_gemm_f32_reduce(GemmF p, int v4) {
   }
 }
 
+// split-K reduce for DEEP splits (ks >= 16, N % 4 == 0; the small-output dW GEMMs: 128 x 256 x 8192
+// runs 64-way): the one-thread-per-4-outputs reduce above leaves a 32-block grid with 64 dependent
+// slab reads per thread (21 us for 8 MB, profiles/prof_r5final_step_fp32.txt).  Here G = 8 threads
+// share each 4-output group -- thread g sums slabs g, g + 8, ... in order -- and the G partial sums are
+// added through LDS in g order (deterministic): 8x the blocks and the loads in flight.
+constexpr int RD_G = 8;
+template <bool SGD>
+__global__ void __launch_bounds__(256) fm_gemm_f32_reduce_deep(GemmF p) {
+  __shared__ f32x4_t part[RD_G][256 / RD_G];
+  constexpr int O = 256 / RD_G;
+  const long MN = (long)p.M * p.N;
+  const long total = MN * p.batch / 4;
+  const int o = threadIdx.x % O, g = threadIdx.x / O;
+  const long i = blockIdx.x * (long)O + o;
+  const long e0 = (i < total ? i : total - 1) * 4;
+  const long zb = e0 / MN, e = e0 % MN;
+  const float* src = p.ws + zb * p.ksplit * MN + e;
+  f32x4_t s = {0.f, 0.f, 0.f, 0.f};
+  int k = g;
+  for (; k + 3 * RD_G < p.ksplit; k += 4 * RD_G) {
+    f32x4_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const f32x4_t*>(src + (long)(k + u * RD_G) * MN);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s += v[u];
+  }
+  for (; k < p.ksplit; k += RD_G) s += *reinterpret_cast<const f32x4_t*>(src + (long)k * MN);
+  part[g][o] = s;
+  __syncthreads();
+  if (g != 0 || i >= total) return;
+  s = part[0][o];
+#pragma unroll
+  for (int t = 1; t < RD_G; ++t) s += part[t][o];
+  const int m = (int)(e / p.N), n = (int)(e % p.N);
+  if constexpr (SGD) {
+    sgd_apply4(p, (long)m * p.ldc + n, s * p.alpha);
+    return;
+  }
+  float* d = p.C + zb * p.sC + (long)m * p.ldc + n;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) s[r] = act_fwd(p.act, s[r] * p.alpha + (p.bias ? p.bias[n + r] : 0.f));
+  if (p.beta) s += *reinterpret_cast<const f32x4_t*>(d);
+  *reinterpret_cast<f32x4_t*>(d) = s;
+}
+
 // split-K reduce of a GEMM with the FUSED BACKWARD epilogue (dX of a layer whose input has an
 // activation): v = act_bwd(bact, ay, act(alpha * sum + bias)), colsum[n] += sum over rows of v.
 // Thread = 4 columns x RB rows: the column sums stay in registers, one atomic per (column, block),
@@ -258,6 +303,12 @@ extern "C" int fm_gemm_x3v2_launch(const void* params, int bm, int a_kcontig, in
 namespace {
 
 void launch_reduce_f32(const GemmF& p, int v4, long total, hipStream_t stream) {
+  if (v4 && p.ksplit >= 16) {
+    const dim3 grid((unsigned)((total + 256 / RD_G - 1) / (256 / RD_G)));
+    if (p.uw) hipLaunchKernelGGL(fm_gemm_f32_reduce_deep<true>, grid, dim3(256), 0, stream, p);
+    else hipLaunchKernelGGL(fm_gemm_f32_reduce_deep<false>, grid, dim3(256), 0, stream, p);
+    return;
+  }
   if (p.uw) hipLaunchKernelGGL(fm_gemm_f32_reduce<true>, dim3(fm_grid(total)), dim3(256), 0, stream, p, v4);
   else hipLaunchKernelGGL(fm_gemm_f32_reduce<false>, dim3(fm_grid(total)), dim3(256), 0, stream, p, v4);
 }
@@ -319,6 +370,10 @@ static int f32_split_mode() {
 }
 extern "C" int fm_gemm_f32_get_split() { return f32_split_mode(); }
 
+// the form (see gemm_f32_run) the last fp32 GEMM issued from this thread ran with (tuner check)
+static thread_local int g_last_form = 0;
+extern "C" int fm_gemm_f32_last_form() { return g_last_form; }
+
 struct SgdUpdF {
   float* w; unsigned short* wc; float* v; const float* lr; float wd, mom; int nest;
 };
@@ -343,10 +398,11 @@ extern "C" int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, con
 // split kernel (gemm_x3.hip) or the default register-staged kernel, the update in its epilogue.
 extern "C" int fm_gemm_f32_dw_sgd(const float* A, long lda, const float* B, long ldb, float* W, long ldw,
                                   unsigned short* Wc, float* V, const float* lr, float wd, float mom, int nesterov,
-                                  int M, int N, int K, float* ws, long ws_bytes, float* rowsum_a, hipStream_t stream) {
+                                  int M, int N, int K, float* ws, long ws_bytes, float* rowsum_a, int cfg,
+                                  hipStream_t stream) {
   SgdUpdF u{W, Wc, V, lr, wd, mom, nesterov};
-  return gemm_f32_run(A, lda, 0, 0, B, ldb, 0, 0, W, ldw, 0, nullptr, M, N, K, 1, 1.f, 0, 10, ws, ws_bytes, 0, nullptr, 0,
-                      10, nullptr, rowsum_a, &u, stream);
+  return gemm_f32_run(A, lda, 0, 0, B, ldb, 0, 0, W, ldw, 0, nullptr, M, N, K, 1, 1.f, 0, 10, ws, ws_bytes, cfg, nullptr,
+                      0, 10, nullptr, rowsum_a, &u, stream);
 }
 
 static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const float* B, long ldb, long sB,
@@ -376,6 +432,13 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
   auto al = [](const void* q) { return (((uintptr_t)q) & 15) == 0; };
   bool vec = al(A) && al(B) && (lda % 4 == 0) && (ldb % 4 == 0) && (sA % 4 == 0) && (sB % 4 == 0);
   vec = vec && (a_kcontig ? (K % 4 == 0) : (M % 4 == 0)) && (b_kcontig ? (K % 4 == 0) : (N % 4 == 0));
+  // ksplit_req = ks | form << 8: a measured configuration (flexmi/ops/gemm_tune.py) -- form 1/2/3 the
+  // native kernel with 128x128 / 128x64 / 64x64 tiles, 4/5 the split kernel with 256x128 / 128x128,
+  // ks the split-K depth (0: the heuristic's); form 0 = the heuristic tile.  A form that does not
+  // apply to the operands falls back to the heuristic.
+  int form = ksplit_req >> 8;
+  ksplit_req &= 255;
+  const bool fused_ok_split = ws != nullptr && batch == 1 && (long)M * N * 4 * 2 <= ws_bytes;
   // fp32 on the bf16 matrix cores (gemm_x3.hip: exact three-way operand split in the register
   // staging pass).  Split mode (FM_F32_SPLIT / fm_gemm_f32_set_split): 0 = the native fp32 MFMA
   // kernel only, 2 = the split kernel for every eligible GEMM, 3 (default) = only the big ones,
@@ -383,14 +446,15 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
   // profiles/gemm_f32_lab_r5i_*).  K-contiguous operands need 16-B rows; MN-contiguous ones are
   // read per element.
   const int split_mode = f32_split_mode();
-  const bool x3_pick = split_mode == 2 || (split_mode == 3 && std::min(M, N) >= 480 && K >= 480);
+  const bool x3_pick = form ? (form >= 4 && split_mode != 0)
+                            : split_mode == 2 || (split_mode == 3 && std::min(M, N) >= 480 && K >= 480);
   if (x3_pick && K > 0 && K % 32 == 0 && M >= 64 && N >= 64) {
     auto opnd_ok = [&](const float* X, long ld, long sX, bool kc) {
       return kc ? (al(X) && ld % 4 == 0 && sX % 4 == 0) : true;   // MN-contiguous: 4-B loads
     };
     if (opnd_ok(A, lda, sA, a_kcontig) && opnd_ok(B, ldb, sB, b_kcontig)) {
       // 256x128 (8 waves, 2 per SIMD) whenever M fills it, split-K for the grid
-      const int bm = M >= 256 ? 256 : 128;
+      const int bm = form == 4 ? 256 : form == 5 ? 128 : M >= 256 ? 256 : 128;
       p.tiles_m = (M + bm - 1) / bm;
       p.tiles_n = (N + 127) / 128;
       const long tiles = (long)p.tiles_m * p.tiles_n * batch;
@@ -401,8 +465,10 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
       else if (ws != nullptr && !fused)
         while (tiles * ks < 256 && ks * 2 <= ktiles / 4 && ks < 16) ks *= 2;
       if (fused) ks = 1;
+      ks = std::min(ks, std::max(1, ktiles));
       while (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks /= 2;
       p.ksplit = ks;
+      g_last_form = bm == 256 ? 4 : 5;
       if (fm_gemm_x3v2_launch(&p, bm, a_kcontig, b_kcontig, upd != nullptr && ks == 1, stream) == 0) {
         if (ks > 1) {
           const int v4 = (N % 4 == 0) && (ldc % 4 == 0) && (sC % 4 == 0) && al(C);
@@ -429,6 +495,10 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
   const bool fused_split = fused_ep && t128 < 256 && K >= 1024 && ws != nullptr && batch == 1 && ksplit_req <= 0 &&
                            (long)M * N * 4 * 2 <= ws_bytes;
   if (fused_ep && t128 < 256 && !fused_split) { BMv = 64; BNv = 64; }
+  if (form >= 4) form = 0;   // the split kernel did not apply
+  if (form == 1) { BMv = 128; BNv = 128; }
+  if (form == 2) { BMv = 128; BNv = 64; }
+  if (form == 3) { BMv = 64; BNv = 64; }
   p.tiles_m = (M + BMv - 1) / BMv;
   p.tiles_n = (N + BNv - 1) / BNv;
   const long tiles = (long)p.tiles_m * p.tiles_n * batch;
@@ -442,10 +512,13 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
     const int ks_max = tiles <= 8 ? 64 : 16;
     while (tiles * ks < target && ks * 2 <= ktiles / 4 && ks < ks_max) ks *= 2;
   }
-  if (fused_ep && !fused_split) ks = 1;   // fused bwd epilogue in the tile: needs the full K sum
+  // fused bwd epilogue in the tile needs the full K sum (split: the epilogue runs in the reduce)
+  if (fused_ep && !(form ? fused_ok_split : fused_split)) ks = 1;
+  ks = std::min(ks, std::max(1, ktiles));
   while (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks /= 2;
   if (K <= 0) ks = 1;
   p.ksplit = ks;
+  g_last_form = BNv == 128 ? 1 : BMv == 128 ? 2 : 3;
   if (BNv == 128) launch_fbm<128, 128>(p, a_kcontig, b_kcontig, vec, stream);
   else if (BMv == 128) launch_fbm<128, 64>(p, a_kcontig, b_kcontig, vec, stream);
   else launch_fbm<64, 64>(p, a_kcontig, b_kcontig, vec, stream);

@@ -48,7 +48,7 @@ def test_gemm_f32_epilogue_bias_act_beta(gpu):
         assert rel_err(C, ref) < TOL, act
 
 
-@pytest.mark.parametrize("ks", [2, 4, 8])
+@pytest.mark.parametrize("ks", [2, 4, 8, 16, 64])      # >= 16: the slab-parallel reduce
 def test_gemm_f32_splitk_and_batch(gpu, ks):
     from flexmi.ops import _kernels as Kk
     torch.manual_seed(2)
@@ -218,6 +218,60 @@ def test_dot_interaction_f32_act0(gpu, F, D, selfi):
         assert rel_err(dz[i], dZ[:, i]) < TOL, i
 
 
+def _dlrm_run(dev, dcfg, B, steps, seed=0, graph=False, lr=0.1):
+    from flexmi.core import FFConfig, FFModel, SGDOptimizer, LossType, MetricsType
+    from flexmi.models.dlrm import build_dlrm
+    rng = np.random.RandomState(seed)
+    cfg = FFConfig()
+    cfg.batchSize = B
+    cfg.device = dev
+    cfg.compute_dtype = "fp32"
+    cfg.seed = 5
+    m = FFModel(cfg)
+    d, s, p = build_dlrm(m, dcfg)
+    m.compile(SGDOptimizer(m, lr), LossType.LOSS_BINARY_CROSSENTROPY, [MetricsType.METRICS_ACCURACY])
+    ex = m.init_layers()
+    batches = []
+    for _ in range(steps):
+        dd = np.zeros((B, d.dims[1]), np.float32)
+        dd[:, :13] = rng.rand(B, 13)
+        # skewed indices: hot rows repeat (atomic / duplicate paths), tails stay mostly unique
+        sp = [np.minimum((rng.zipf(1.2, (B, dcfg.embedding_bag_size)) - 1), r - 1).astype(np.int64)
+              if r > 64 else rng.randint(0, r, (B, dcfg.embedding_bag_size)).astype(np.int64)
+              for r in dcfg.embedding_size]
+        lab = rng.randint(0, 2, (B, 1)).astype(np.float32)
+        batches.append((dd, sp, lab))
+
+    def feed(k):
+        dd, sp, lab = batches[k]
+        ex.scatter_from_host(d, dd)
+        for t, a in zip(s, sp):
+            ex.scatter_from_host(t, a)
+        ex.scatter_from_host(m.get_label_tensor(), lab)
+
+    if graph and dev == "gpu":
+        feed(0)
+        ex.train_step()
+        run = ex.capture_step()
+        for k in range(1, steps):
+            feed(k)          # host scatter into the captured input buffers, then replay
+            run()
+        torch.cuda.synchronize()
+    else:
+        for k in range(steps):
+            feed(k)
+            ex.train_step()
+    ws = [w.get_weights(m) for w in m.parameters]
+    ws[0] = ws[0][:, :13]   # the GPU pads the 13 dense features (zero input columns) for aligned loads
+    return ws, m.get_perf_metrics().get_loss(), ex
+
+
+def _assert_params_close(a_list, b_list, rtol):
+    for a, b in zip(a_list, b_list):
+        err = np.abs(a - b).max() / max(np.abs(a).max(), 1e-6)
+        assert err < rtol, (a.shape, err)
+
+
 def test_dlrm_tiny_fp32_gpu_matches_cpu(gpu):
     from flexmi.models.dlrm import DLRMConfig
     dcfg = DLRMConfig.preset("tiny")
@@ -314,24 +368,20 @@ def test_lstm_fp32_gpu_matches_cpu(gpu, state):
 
 
 def test_embedding_overlap_on_off_equivalent(gpu, monkeypatch):
-    """Captured steps with the fused embedding groups on a second HIP stream (OVERLAP_EMB=1) and the
-    Linear dW GEMMs on a third (DW_STREAM) train exactly like the single-stream schedule: multi-table
-    group, >= 128-wide tables, bottom MLP."""
+    """Captured steps with the fused embedding groups on a second HIP stream (OVERLAP_EMB=1) train
+    exactly like the single-stream schedule: multi-table group, >= 128-wide tables, bottom MLP."""
     from flexmi.models.dlrm import DLRMConfig
     from flexmi.runtime import executor as E
     dcfg = DLRMConfig(128, [5000, 300, 12, 70000, 40], [13, 256, 128], [256, 256, 1], 1, -1, -1, 0.0, "dot", "", -1,
                       "bce", "overlap")
     res = {}
-    for mode in ("00", "10", "11", "01"):
-        monkeypatch.setattr(E, "OVERLAP_EMB", mode[0])
-        monkeypatch.setattr(E, "DW_STREAM", mode[1] == "1")
+    for mode in ("0", "1"):
+        monkeypatch.setattr(E, "OVERLAP_EMB", mode)
         ws, loss, ex = _dlrm_run("gpu", dcfg, 2048, 4, graph=True)
-        assert E.overlap_embeddings_enabled(ex) == (mode[0] == "1")
-        assert any(it.name.endswith(".bwd_dw") for it in ex.step_program()) == (mode[1] == "1")
+        assert E.overlap_embeddings_enabled(ex) == (mode == "1")
         res[mode] = (ws, loss)
-    for mode in ("10", "11", "01"):
-        _assert_params_close(res["00"][0], res[mode][0], 1e-5)
-        assert abs(res["00"][1] - res[mode][1]) < 1e-5
+    _assert_params_close(res["0"][0], res["1"][0], 1e-5)
+    assert abs(res["0"][1] - res["1"][1]) < 1e-5
 
 
 # ---------------------------------------------------------------- CNN kernels (fp32)
