@@ -14,10 +14,10 @@ void fm_image_normalize(const unsigned char* src, void* dst, long N, int H, int 
                         int bf16, hipStream_t s);
 int fm_gemm_dw_sgd(const void* A, long lda, const void* B, long ldb, float* W, long ldw, unsigned short* Wc, float* V,
                    const float* lr, float wd, float mom, int nesterov, int M, int N, int K, float* ws, long ws_bytes,
-                   float* rowsum_a, hipStream_t stream);
+                   float* rowsum_a, int cfg, hipStream_t stream);
 int fm_gemm_f32_dw_sgd(const float* A, long lda, const float* B, long ldb, float* W, long ldw, unsigned short* Wc,
                        float* V, const float* lr, float wd, float mom, int nesterov, int M, int N, int K, float* ws,
-                       long ws_bytes, float* rowsum_a, hipStream_t stream);
+                       long ws_bytes, float* rowsum_a, int cfg, hipStream_t stream);
 int fm_gemm(const void* A, long lda, long sA, int a_kcontig, const void* B, long ldb, long sB, int b_kcontig, void* C,
             long ldc, long sC, int c_fp32, const float* bias, int M, int N, int K, int batch, float alpha, int beta,
             int act, float* ws, long ws_bytes, int ksplit_req, const void* act_y, long lday, int bwd_act,
@@ -25,6 +25,7 @@ int fm_gemm(const void* A, long lda, long sA, int a_kcontig, const void* B, long
 void fm_gemm_f32_set_split(int on);
 void fm_embedding_set_bwd_mode(int count);
 int fm_gemm_f32_get_split();
+int fm_gemm_f32_last_form();
 int fm_gemm_f32(const float* A, long lda, long sA, int a_kcontig, const float* B, long ldb, long sB, int b_kcontig,
                 float* C, long ldc, long sC, const float* bias, int M, int N, int K, int batch, float alpha, int beta,
                 int act, float* ws, long ws_bytes, int ksplit_req, const float* act_y, long lday, int bwd_act,
@@ -252,7 +253,7 @@ void sgd_segs(torch::Tensor W, torch::Tensor G, c10::optional<torch::Tensor> V, 
 // computes the gradient and runs the optimizer kernel itself).
 int gemm_dw_sgd(torch::Tensor dpre, torch::Tensor x, torch::Tensor W, c10::optional<torch::Tensor> Wc,
                 c10::optional<torch::Tensor> V, torch::Tensor lr, double wd, double mom, bool nesterov,
-                c10::optional<torch::Tensor> db, torch::Tensor ws) {
+                c10::optional<torch::Tensor> db, torch::Tensor ws, int64_t cfg) {
   check_cuda(dpre, "dpre");
   check_cuda(x, "x");
   check_cuda(W, "W");
@@ -275,11 +276,11 @@ int gemm_dw_sgd(torch::Tensor dpre, torch::Tensor x, torch::Tensor W, c10::optio
     return fm_gemm_f32_dw_sgd(dpre.data_ptr<float>(), dpre.stride(0), x.data_ptr<float>(), x.stride(0),
                               W.data_ptr<float>(), Kin, (unsigned short*)mptr(Wc), (float*)mptr(V), lr.data_ptr<float>(),
                               (float)wd, (float)mom, nesterov ? 1 : 0, (int)Nout, (int)Kin, (int)B, ws.data_ptr<float>(),
-                              ws.numel() * 4, (float*)mptr(db), cur());
+                              ws.numel() * 4, (float*)mptr(db), (int)cfg, cur());
   return fm_gemm_dw_sgd(dpre.data_ptr(), dpre.stride(0), x.data_ptr(), x.stride(0), W.data_ptr<float>(), Kin,
                         (unsigned short*)mptr(Wc), (float*)mptr(V), lr.data_ptr<float>(), (float)wd, (float)mom,
                         nesterov ? 1 : 0, (int)Nout, (int)Kin, (int)B, ws.data_ptr<float>(), ws.numel() * 4,
-                        (float*)mptr(db), cur());
+                        (float*)mptr(db), (int)cfg, cur());
 }
 
 // thin-input fp32 Linear (gemm_small.hip): y = act(x W^T + b) for in_features K <= 32, K % 4 == 0.
@@ -1135,7 +1136,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("N"), py::arg("K"), py::arg("batch"), py::arg("alpha"), py::arg("beta"), py::arg("act"), py::arg("ws"),
         py::arg("ksplit"), py::arg("act_y"), py::arg("lday"), py::arg("bwd_act"), py::arg("colsum"), py::arg("rowsum_a"));
   m.def("gemm_dw_sgd", &gemm_dw_sgd, py::arg("dpre"), py::arg("x"), py::arg("W"), py::arg("Wc"), py::arg("V"),
-        py::arg("lr"), py::arg("wd"), py::arg("mom"), py::arg("nesterov"), py::arg("db"), py::arg("ws"));
+        py::arg("lr"), py::arg("wd"), py::arg("mom"), py::arg("nesterov"), py::arg("db"), py::arg("ws"), py::arg("cfg") = 0);
+  m.def("gemm_f32_last_form", []() { return fm_gemm_f32_last_form(); });
   m.def("sgd_segs", &sgd_segs);
   m.def("init_fill", &init_fill);
   m.def("smallk_fwd", &smallk_fwd);

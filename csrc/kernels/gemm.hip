@@ -439,9 +439,10 @@ extern "C" int fm_gemm(const void* A, long lda, long sA, int a_kcontig,
 // the dW orientation), rowsum_a += column sums of dpre (the bias gradient).  Returns the split.
 extern "C" int fm_gemm_dw_sgd(const void* A, long lda, const void* B, long ldb, float* W, long ldw,
                               unsigned short* Wc, float* V, const float* lr, float wd, float mom, int nesterov,
-                              int M, int N, int K, float* ws, long ws_bytes, float* rowsum_a, hipStream_t stream) {
+                              int M, int N, int K, float* ws, long ws_bytes, float* rowsum_a, int cfg,
+                              hipStream_t stream) {
   SgdUpd u{W, Wc, V, lr, wd, mom, nesterov};
-  return gemm_run(A, lda, 0, 0, B, ldb, 0, 0, W, ldw, 0, 1, nullptr, M, N, K, 1, 1.f, 0, 10, ws, ws_bytes, 0, nullptr,
+  return gemm_run(A, lda, 0, 0, B, ldb, 0, 0, W, ldw, 0, 1, nullptr, M, N, K, 1, 1.f, 0, 10, ws, ws_bytes, cfg, nullptr,
                   0, 10, nullptr, rowsum_a, &u, stream);
 }
 
@@ -476,6 +477,11 @@ static int gemm_run(const void* A, long lda, long sA, int a_kcontig,
   auto al = [](const void* q) { return (((uintptr_t)q) & 15) == 0; };
   bool vec = al(A) && al(B) && (lda % 8 == 0) && (ldb % 8 == 0) && (sA % 8 == 0) && (sB % 8 == 0);
   vec = vec && (a_kcontig ? (K % 8 == 0) : (M % 8 == 0)) && (b_kcontig ? (K % 8 == 0) : (N % 8 == 0));
+  // ksplit_req = ks | form << 8: a measured configuration (flexmi/ops/gemm_tune.py), form 1/2/3 =
+  // 128x128 / 128x64 / 64x64 tiles, ks the split-K depth (0: the heuristic's); form 0: heuristic tile
+  const int form = ksplit_req >> 8;
+  ksplit_req &= 255;
+  const bool fused_ok_split = ws != nullptr && batch == 1 && (long)M * N * 4 * 2 <= ws_bytes;
   // tile choice: 128x128 when it yields >= 2 waves of blocks on 256 CUs, else narrower N
   int BMv = 128, BNv = 128;
   long t128 = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;
@@ -496,6 +502,9 @@ static int gemm_run(const void* A, long lda, long sA, int a_kcontig,
   const bool fused_split = fused_ep && t128 < 256 && K >= 1024 && ws != nullptr && batch == 1 && ksplit_req <= 0 &&
                            (long)M * N * 4 * 2 <= ws_bytes;
   if (fused_ep && t128 < 256 && !fused_split) { BMv = 64; BNv = 64; }
+  if (form == 1) { BMv = 128; BNv = 128; }
+  if (form == 2) { BMv = 128; BNv = 64; }
+  if (form == 3) { BMv = 64; BNv = 64; }
   p.tiles_m = (M + BMv - 1) / BMv;
   p.tiles_n = (N + BNv - 1) / BNv;
   long tiles = (long)p.tiles_m * p.tiles_n * batch;
@@ -510,7 +519,8 @@ static int gemm_run(const void* A, long lda, long sA, int a_kcontig,
     const long target = K >= 4096 ? 384L : 256L;
     while (tiles * ks < target && ks * 2 <= ktiles / 2 && ks < 16) ks *= 2;
   }
-  if (fused_ep && !fused_split) ks = 1;  // fused bwd epilogue in the tile needs the full K sum
+  if (fused_ep && !(form ? fused_ok_split : fused_split)) ks = 1;  // fused bwd epilogue needs the full K sum
+  ks = std::min(ks, std::max(1, ktiles));
   while (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks /= 2;
   p.ksplit = ks;
   if (K <= 0) {  // degenerate: C = epilogue(0)

@@ -61,6 +61,8 @@ def workspace(device, nbytes):
 
 GEMM_WS_BYTES = 64 << 20
 
+from flexmi.ops import gemm_tune as _tune  # noqa: E402
+
 
 def gemm(A, lda, a_kcontig, B, ldb, b_kcontig, Cout, ldc, M, N, K, bias=None, act=10, beta=False, alpha=1.0,
          batch=1, sA=0, sB=0, sC=0, ksplit=0, use_ws=True, act_y=None, bwd_act=10, colsum=None, rowsum_a=None):
@@ -68,6 +70,18 @@ def gemm(A, lda, a_kcontig, B, ldb, b_kcontig, Cout, ldc, M, N, K, bias=None, ac
     C = act'(act_y) * (A·B) and colsum += column sums of C (its bias gradient)."""
     ws = workspace(Cout.device, GEMM_WS_BYTES) if use_ws else None
     lday = act_y.stride(0) if act_y is not None else 0
+    if ksplit == 0 and use_ws:
+        # a configuration measured for this GEMM (flexmi/ops/gemm_tune.py), else the heuristic
+        dt = "fp32" if A.dtype == torch.float32 else "bf16"
+        k = _tune.key(dt, M, N, K, a_kcontig, b_kcontig, batch, act_y is not None, colsum is not None,
+                      rowsum_a is not None, False, Cout.dtype == torch.float32)
+        ksplit = _tune.lookup(k)
+        if _tune.RECORD is not None:
+            _tune.RECORD.append(dict(key=k, dtype=dt, M=M, N=N, K=K, a_k=bool(a_kcontig), b_k=bool(b_kcontig), lda=lda,
+                                     ldb=ldb, ldc=ldc, batch=batch, sA=sA, sB=sB, sC=sC, bias=bias is not None,
+                                     act=act, beta=bool(beta), act_y=act_y is not None, bwd_act=bwd_act,
+                                     colsum=colsum is not None, rowsum=rowsum_a is not None,
+                                     c_fp32=Cout.dtype == torch.float32, sgd=None))
     return C().gemm(A, lda, sA, a_kcontig, B, ldb, sB, b_kcontig, Cout, ldc, sC, bias, M, N, K, batch, alpha, beta, act,
                     ws, ksplit, act_y, lday, bwd_act, colsum, rowsum_a)
 
@@ -158,8 +172,16 @@ def _dw_fused_sgd(dpre, x2, dw, db, upd):
     """dW GEMM + SGD in one kernel (csrc/kernels/gemm.hip fm_gemm_dw_sgd, gemm_f32.hip
     fm_gemm_f32_dw_sgd); False when it does not apply (misaligned views, ldw % 4 != 0) and the
     caller must compute dW itself."""
+    dt = "fp32" if dpre.dtype == torch.float32 else "bf16"
+    B, Nout = dpre.shape
+    Kin = x2.shape[1]
+    k = _tune.key(dt, Nout, Kin, B, False, False, 1, False, False, db is not None, True, True)
+    if _tune.RECORD is not None:
+        _tune.RECORD.append(dict(key=k, dtype=dt, M=Nout, N=Kin, K=B, ldd=dpre.stride(0), ldx=x2.stride(0),
+                                 rowsum=db is not None, sgd=dict(mom=upd.mom, nesterov=upd.nesterov, wd=upd.wd,
+                                                                 mirror=upd.wc is not None)))
     ks = C().gemm_dw_sgd(dpre, x2, upd.w, upd.wc, upd.v, upd.lr, upd.wd, upd.mom, upd.nesterov, db,
-                         workspace(dpre.device, GEMM_WS_BYTES))
+                         workspace(dpre.device, GEMM_WS_BYTES), _tune.lookup(k))
     return ks >= 0
 
 

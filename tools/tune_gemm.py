@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""Measure the GEMM configuration table (flexmi/ops/gemm_tune.py) on the GPU.
+
+  python tools/tune_gemm.py [--configs mlperf:8192,summit:512] [--dtypes fp32,bf16] [--reps 20]
+                            [--out flexmi/ops/tuned/gemm_mi355x.json] [--merge]
+
+For each DLRM configuration and compute dtype: build the model (tables shrunk: the GEMM shapes do
+not depend on them), run one eager training step with the GEMM recorder on, then for every distinct
+GEMM key time the heuristic (cfg 0) and every candidate configuration on operands of the recorded
+shapes and strides (warm-up, then ``reps`` launches between two CUDA events; each launch includes
+its split-K reduce).  A candidate is kept only if it ran in the requested form and matches the
+heuristic's result.  The fastest configuration of each key is written when it beats the heuristic
+by more than 2 %.  Reference: per-layer algorithm search at init, src/ops/conv_2d.cu:216-243.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def record_specs(config, batch, dtype):
+    import torch
+    from flexmi.core import FFConfig, FFModel, LossType, MetricsType, SGDOptimizer
+    from flexmi.models.dlrm import DLRMConfig, build_dlrm
+    from flexmi.ops import gemm_tune as T
+    dcfg = DLRMConfig.preset(config)
+    dcfg.embedding_size = [max(2, min(r, 4096)) for r in dcfg.embedding_size]
+    cfg = FFConfig()
+    cfg.batchSize = batch
+    cfg.compute_dtype = dtype
+    m = FFModel(cfg)
+    d, s, _ = build_dlrm(m, dcfg)
+    loss = LossType.LOSS_BINARY_CROSSENTROPY if dcfg.loss == "bce" else LossType.LOSS_MEAN_SQUARED_ERROR_AVG_REDUCE
+    m.compile(SGDOptimizer(m, 0.01), loss, [MetricsType.METRICS_ACCURACY])
+    ex = m.init_layers()
+    rng = np.random.RandomState(0)
+    dd = np.zeros((batch, d.dims[1]), np.float32)
+    dd[:, :dcfg.mlp_bot[0]] = rng.rand(batch, dcfg.mlp_bot[0])
+    ex.scatter_from_host(d, dd)
+    for t, r in zip(s, dcfg.embedding_size):
+        ex.scatter_from_host(t, rng.randint(0, r, (batch, dcfg.embedding_bag_size)).astype(np.int64))
+    ex.scatter_from_host(m.get_label_tensor(), rng.randint(0, 2, (batch, 1)).astype(np.float32))
+    T.RECORD = []
+    try:
+        ex.train_step()
+        torch.cuda.synchronize()
+        specs = T.RECORD
+    finally:
+        T.RECORD = None
+    del ex, m
+    torch.cuda.empty_cache()
+    return specs
+
+
+def _flat(n, dt, dev, scale=1.0):
+    import torch
+    return (torch.randn(max(1, n), device=dev) * scale).to(dt)
+
+
+def make_runner(spec, dev):
+    """A callable run(cfg) issuing the recorded GEMM with configuration ``cfg`` and a function
+    returning its result tensor (for the cross-check)."""
+    import torch
+    from flexmi.ops import _kernels as K
+    dt = torch.float32 if spec["dtype"] == "fp32" else torch.bfloat16
+    M, N, Kd = spec["M"], spec["N"], spec["K"]
+    if spec.get("sgd") is not None:
+        ldd, ldx = spec["ldd"], spec["ldx"]
+        dpre = _flat((Kd - 1) * ldd + M, dt, dev, 0.1).as_strided((Kd, M), (ldd, 1))
+        x = _flat((Kd - 1) * ldx + N, dt, dev).as_strided((Kd, N), (ldx, 1))
+        sg = spec["sgd"]
+        w0 = torch.randn(M, N, device=dev) * 0.05
+        w = w0.clone()
+        v = torch.zeros(M, N, device=dev) if sg["mom"] > 0 else None
+        wc = torch.empty(M, N, device=dev, dtype=torch.bfloat16) if sg["mirror"] else None
+        db = torch.zeros(M, device=dev) if spec["rowsum"] else None
+        lr = torch.tensor([1e-3], device=dev)
+        ws = K.workspace(dev, K.GEMM_WS_BYTES)
+
+        def run(cfg):
+            return K.C().gemm_dw_sgd(dpre, x, w, wc, v, lr, sg["wd"], sg["mom"], sg["nesterov"], db, ws, cfg)
+
+        def result(cfg):
+            w.copy_(w0)
+            if v is not None:
+                v.zero_()
+            run(cfg)
+            return w.clone()
+        return run, result
+    a_k, b_k, batch = spec["a_k"], spec["b_k"], spec["batch"]
+    lda, ldb, ldc = spec["lda"], spec["ldb"], spec["ldc"]
+    sA, sB, sC = spec["sA"], spec["sB"], spec["sC"]
+    na = (batch - 1) * sA + ((M - 1) * lda + Kd if a_k else (Kd - 1) * lda + M)
+    nb = (batch - 1) * sB + ((N - 1) * ldb + Kd if b_k else (Kd - 1) * ldb + N)
+    nc = (batch - 1) * sC + (M - 1) * ldc + N
+    A = _flat(na, dt, dev)
+    B = _flat(nb, dt, dev, 0.05)
+    cdt = torch.float32 if spec["c_fp32"] else torch.bfloat16
+    Cout = torch.zeros(nc, device=dev, dtype=cdt)
+    bias = torch.randn(N, device=dev) if spec["bias"] else None
+    act_y = torch.randn(M, N, device=dev).to(dt) if spec["act_y"] else None
+    colsum = torch.zeros(N, device=dev) if spec["colsum"] else None
+    rowsum = torch.zeros(M, device=dev) if spec["rowsum"] else None
+
+    def run(cfg):
+        return K.gemm(A, lda, a_k, B, ldb, b_k, Cout, ldc, M, N, Kd, bias=bias, act=spec["act"], beta=spec["beta"],
+                      batch=batch, sA=sA, sB=sB, sC=sC, ksplit=cfg, act_y=act_y, bwd_act=spec["bwd_act"], colsum=colsum,
+                      rowsum_a=rowsum)
+
+    def result(cfg):
+        Cout.zero_()
+        run(cfg)
+        return Cout.float().clone()
+    return run, result
+
+
+def time_cfg(run, cfg, reps):
+    import torch
+    for _ in range(3):
+        run(cfg)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        run(cfg)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1000.0 / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="mlperf:8192")
+    ap.add_argument("--dtypes", default="fp32,bf16")
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--merge", action="store_true", help="keep entries of an existing table not re-measured")
+    ap.add_argument("--log", default=None, help="per-candidate timings (JSONL)")
+    args = ap.parse_args()
+    import torch
+    from flexmi.ops import _kernels as K
+    from flexmi.ops import gemm_tune as T
+    out = args.out or T.DEFAULT_PATH
+    T.set_table({})                     # heuristics only while recording and timing
+    dev = torch.device("cuda")
+    entries = {}
+    if args.merge and os.path.exists(out):
+        with open(out) as f:
+            entries = json.load(f).get("entries", {})
+    logf = open(args.log, "w") if args.log else None
+    t_start = time.time()
+    for item in args.configs.split(","):
+        config, batch = item.split(":")
+        for dtype in args.dtypes.split(","):
+            specs = record_specs(config, int(batch), dtype)
+            seen = {}
+            for sp in specs:
+                seen.setdefault(sp["key"], sp)
+            print(f"# {config} b{batch} {dtype}: {len(specs)} GEMM calls, {len(seen)} keys", flush=True)
+            for k, sp in seen.items():
+                torch.manual_seed(0)
+                run, result = make_runner(sp, dev)
+                ref = result(0)
+                base = time_cfg(run, 0, args.reps)
+                best, best_us = 0, base
+                fused = sp.get("act_y") or sp.get("colsum")
+                cands = T.candidates(sp["dtype"], sp["M"], sp["N"], sp["K"], fused=bool(fused), sgd=sp.get("sgd") is not None)
+                tried = {}
+                for cfg in cands:
+                    form, ks = T.decode(cfg)
+                    got = result(cfg)
+                    if sp["dtype"] == "fp32" and K.C().gemm_f32_last_form() != form:
+                        continue                    # fell back: the form does not apply here
+                    err = ((got - ref).abs().max() / (ref.abs().max() + 1e-12)).item()
+                    if not err < (1e-4 if sp["dtype"] == "fp32" else 2e-2):
+                        print(f"  ! {k} cfg {form}/{ks}: mismatch {err:.2e}", flush=True)
+                        continue
+                    us = time_cfg(run, cfg, args.reps)
+                    tried[f"{form}/{ks}"] = round(us, 2)
+                    if us < best_us:
+                        best, best_us = cfg, us
+                keep = best != 0 and best_us < 0.98 * base
+                form, ks = T.decode(best)
+                print(f"  {k}: heuristic {base:.1f} us, best {form}/{ks} {best_us:.1f} us"
+                      f"{'' if keep else ' (heuristic kept)'}", flush=True)
+                entries[k] = {"cfg": best if keep else 0, "us": round(best_us if keep else base, 2),
+                              "heuristic_us": round(base, 2), "config": f"{config}:{batch}"}
+                if logf:
+                    logf.write(json.dumps({"key": k, "heuristic_us": round(base, 2), "cands": tried}) + "\n")
+                    logf.flush()
+    meta = {"device": torch.cuda.get_device_name(0), "configs": args.configs, "dtypes": args.dtypes,
+            "reps": args.reps, "seconds": round(time.time() - t_start, 1)}
+    T.save(entries, out, meta)
+    print(f"# wrote {len(entries)} entries to {out}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
