@@ -594,6 +594,27 @@ int fmn_model_set_table_owner(fmn_model_t m, int table, int rank) {
       -1);
 }
 
+int fmn_model_set_table_columns(fmn_model_t m, int table, int n, const int* ranks) {
+  if (!m || n < 1 || !ranks) return fail("fmn_model_set_table_columns: null model / empty holder list");
+  return guarded(
+      [&] {
+        m->m->set_table_columns(table, std::vector<int>(ranks, ranks + n));
+        return 0;
+      },
+      -1);
+}
+
+int fmn_model_table_columns(fmn_model_t m, int table, int* ranks, int max) {
+  if (!m) return fail("fmn_model_table_columns: null model");
+  return guarded(
+      [&] {
+        const auto& h = m->m->table_holders(table);
+        for (int i = 0; i < (int)h.size() && i < max; ++i) ranks[i] = h[i];
+        return (int)h.size();
+      },
+      -1);
+}
+
 int fmn_model_table_owner(fmn_model_t m, int table) {
   if (!m) return fail("fmn_model_table_owner: null model");
   return guarded([&] { return m->m->table_owner(table); }, -1);

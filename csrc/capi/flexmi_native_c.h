@@ -165,6 +165,12 @@ int fmn_model_dot_interaction(fmn_model_t m, int bottom, int n, const int* embed
 /* place table t (embedding creation order) on `rank` (before compile; default: greedy by rows) */
 int fmn_model_set_table_owner(fmn_model_t m, int table, int rank);
 int fmn_model_table_owner(fmn_model_t m, int table);
+/* column split of a table over n holder ranks (dim % n == 0): holder j keeps columns [j*dim/n,
+ * (j+1)*dim/n); set/get_param of such a table move the FULL rows x dim host array (this rank's
+ * columns read / written).  fmn_model_table_columns returns the holder count (after compile: 1 for
+ * a table-wise table) and writes up to max holder ranks. */
+int fmn_model_set_table_columns(fmn_model_t m, int table, int n, const int* ranks);
+int fmn_model_table_columns(fmn_model_t m, int table, int* ranks, int max);
 /* loss: 51 sparse categorical CE (softmax of the last layer's logits, int32 labels), 52 MSE (avg),
  * 54 binary CE (sigmoid output); bucket_mb = gradient all-reduce bucket size */
 int fmn_model_compile(fmn_model_t m, int loss_type, float lr, double bucket_mb);

@@ -163,6 +163,10 @@ class HipEngine : public Engine {
   void copy(void* dst, const void* src, size_t bytes) override {
     HIPX(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st_));
   }
+  void copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows) override {
+    HIPX(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, hipMemcpyDeviceToDevice, st_));
+  }
+
   void emb_fwd(const float* W, int64_t rows, const int64_t* idx, int bag, float* out, int64_t B, int D) override {
     fm_embedding_fwd(idx, 1, W, out, 0, B, bag, (int)rows, D, D, 1.f, st_);
   }

@@ -152,6 +152,10 @@ class CpuEngine : public Engine {
   }
   void allreduce_wait() override {}
   void copy(void* dst, const void* src, size_t bytes) override { std::memcpy(dst, src, bytes); }
+  void copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows) override {
+    for (size_t r = 0; r < rows; ++r)
+      std::memcpy(static_cast<char*>(dst) + r * dpitch, static_cast<const char*>(src) + r * spitch, width);
+  }
   void emb_fwd(const float* W, int64_t rows, const int64_t* idx, int bag, float* out, int64_t B, int D) override {
     for (int64_t b = 0; b < B; ++b) {
       float* o = out + b * D;
@@ -372,6 +376,27 @@ void Model::set_table_owner(int table, int rank) {
   if (table < 0 || table >= (int)embs_.size() || rank < 0 || rank >= world_)
     throw std::invalid_argument("native model: table / rank");
   embs_[table].owner = rank;
+  embs_[table].holders.clear();
+}
+
+void Model::set_table_columns(int table, const std::vector<int>& ranks) {
+  if (compiled_) throw std::logic_error("native model: placement after compile");
+  if (table < 0 || table >= (int)embs_.size() || ranks.empty()) throw std::invalid_argument("native model: table / ranks");
+  Emb& e = embs_[table];
+  if (e.D % (int)ranks.size() != 0) throw std::invalid_argument("native model: columns not divisible by the holders");
+  for (size_t i = 0; i < ranks.size(); ++i) {
+    if (ranks[i] < 0 || ranks[i] >= world_) throw std::invalid_argument("native model: holder rank");
+    for (size_t j = 0; j < i; ++j)
+      if (ranks[j] == ranks[i]) throw std::invalid_argument("native model: holder listed twice");
+  }
+  e.holders = ranks;
+  e.owner = ranks[0];
+}
+
+int Model::slice_of(const Emb& e, int r) const {
+  for (size_t j = 0; j < e.holders.size(); ++j)
+    if (e.holders[j] == r) return (int)j;
+  return -1;
 }
 
 int Model::dense_out_node() const {
@@ -381,7 +406,7 @@ int Model::dense_out_node() const {
 
 bool Model::param_local(int i) const {
   const int t = entry_table_.at(i);
-  return t < 0 || embs_[t].owner == rank_;
+  return t < 0 || slice_of(embs_[t], rank_) >= 0;
 }
 
 void Model::compile(int loss_type, float lr, double bucket_mb) {
@@ -426,6 +451,10 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
       embs_[t].owner = r;
       load[r] += embs_[t].rows;
     }
+    for (Emb& e : embs_) {
+      if (e.holders.empty()) e.holders = {e.owner};
+      e.Dc = e.D / (int)e.holders.size();
+    }
   }
   // dense parameter entries in backward order -> one flat buffer, all-reduce buckets
   porder_.clear();
@@ -439,14 +468,15 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
   wplan_ = plan_weights(nums, cap);
   pofs_.assign(pnumel_.size(), 0);
   for (size_t j = 0; j < porder_.size(); ++j) pofs_[porder_[j]] = wplan_.offset[j];
-  // embedding exchange: every owner sends each peer its shard rows of every owned table (table
-  // order); each rank receives, per peer, that peer's tables (table order)
+  // embedding exchange: every holder sends each peer that peer's sample rows of its column slice
+  // of every held table (table order); each rank receives, per peer, the slices that peer holds
+  // (table order) and assembles the columns
   xcount_send_.assign(world_, 0);
   xcount_recv_.assign(world_, 0);
   for (const Emb& e : embs_)
     for (int p = 0; p < world_; ++p) {
-      if (e.owner == rank_) xcount_send_[p] += (int64_t)Bl_ * e.D;
-      if (e.owner == p) xcount_recv_[p] += (int64_t)Bl_ * e.D;
+      if (slice_of(e, rank_) >= 0) xcount_send_[p] += (int64_t)Bl_ * e.Dc;
+      if (slice_of(e, p) >= 0) xcount_recv_[p] += (int64_t)Bl_ * e.Dc;
     }
   int64_t xs = 0, xr = 0;
   for (int p = 0; p < world_; ++p) {
@@ -462,7 +492,7 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
   {
     std::vector<int64_t> own(world_, 0);
     for (const Emb& e : embs_)
-      if (e.owner >= 0 && e.owner < world_) own[e.owner] += (int64_t)world_ * Bl_ * e.D;
+      for (int h : e.holders) own[h] += (int64_t)world_ * Bl_ * e.Dc;
     for (int64_t v : own) xmax = std::max(xmax, v);
   }
   const size_t slot = std::max<size_t>((size_t)std::max<int64_t>(xmax, std::max(xs, xr)) * 4 + 4096, 4u << 20);
@@ -480,10 +510,10 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
   idx_.assign(embs_.size(), nullptr);
   for (size_t t = 0; t < embs_.size(); ++t) {
     const Emb& e = embs_[t];
-    if (e.owner != rank_) continue;
-    table_[t] = (float*)eng_->alloc((size_t)e.rows * e.D * 4);
+    if (slice_of(e, rank_) < 0) continue;
+    table_[t] = (float*)eng_->alloc((size_t)e.rows * e.Dc * 4);
     idx_[t] = (int64_t*)eng_->alloc((size_t)B_ * e.bag * 8);
-    if (world_ > 1) emb_full_[t] = (float*)eng_->alloc((size_t)B_ * e.D * 4);
+    if (world_ > 1) emb_full_[t] = (float*)eng_->alloc((size_t)B_ * e.Dc * 4);
   }
   if (world_ > 1 && !embs_.empty()) {
     xsend_ = (float*)eng_->alloc((size_t)std::max<int64_t>(xs, 1) * 4);
@@ -510,8 +540,8 @@ void Model::init_weights(uint64_t seed) {
     }
   }
   for (const Emb& e : embs_) {
-    if (e.owner != rank_) continue;
-    std::vector<float> w((size_t)e.rows * e.D);
+    if (slice_of(e, rank_) < 0) continue;
+    std::vector<float> w((size_t)e.rows * e.D);   // the whole table; this rank keeps its columns
     const float lim = std::sqrt(1.f / (float)e.rows);
     uint64_t s = seed * 1000003ULL + (uint64_t)e.w;
     for (auto& v : w) v = ((float)(splitmix(s) >> 40) / (float)(1ULL << 24) * 2.f - 1.f) * lim;
@@ -523,8 +553,17 @@ void Model::set_param(int i, const float* host) {
   if (!compiled_) throw std::logic_error("native model: set_param after compile");
   const int t = entry_table_.at(i);
   if (t >= 0) {
-    if (embs_[t].owner != rank_) throw std::invalid_argument("native model: table not on this rank");
-    eng_->h2d(table_[t], host, pnumel_[i] * 4);
+    const Emb& e = embs_[t];
+    const int j = slice_of(e, rank_);
+    if (j < 0) throw std::invalid_argument("native model: table not on this rank");
+    if (e.Dc == e.D) {
+      eng_->h2d(table_[t], host, pnumel_[i] * 4);
+    } else {
+      std::vector<float> sl((size_t)e.rows * e.Dc);
+      for (int64_t r = 0; r < e.rows; ++r)
+        std::memcpy(&sl[(size_t)r * e.Dc], host + r * e.D + (int64_t)j * e.Dc, (size_t)e.Dc * 4);
+      eng_->h2d(table_[t], sl.data(), sl.size() * 4);
+    }
   } else {
     eng_->h2d(params_ + pofs_.at(i), host, pnumel_.at(i) * 4);
   }
@@ -536,8 +575,17 @@ void Model::get_param(int i, float* host) const {
   eng_->sync();
   const int t = entry_table_.at(i);
   if (t >= 0) {
-    if (embs_[t].owner != rank_) throw std::invalid_argument("native model: table not on this rank");
-    eng_->d2h(host, table_[t], pnumel_[i] * 4);
+    const Emb& e = embs_[t];
+    const int j = slice_of(e, rank_);
+    if (j < 0) throw std::invalid_argument("native model: table not on this rank");
+    if (e.Dc == e.D) {
+      eng_->d2h(host, table_[t], pnumel_[i] * 4);
+    } else {
+      std::vector<float> sl((size_t)e.rows * e.Dc);
+      eng_->d2h(sl.data(), table_[t], sl.size() * 4);
+      for (int64_t r = 0; r < e.rows; ++r)
+        std::memcpy(host + r * e.D + (int64_t)j * e.Dc, &sl[(size_t)r * e.Dc], (size_t)e.Dc * 4);
+    }
   } else {
     eng_->d2h(host, params_ + pofs_.at(i), pnumel_.at(i) * 4);
   }
@@ -554,7 +602,7 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
   const size_t lab_row = loss_ == LOSS_SCCE ? 4 : (size_t)C * 4;
   eng_->h2d(labels_, static_cast<const char*>(labels) + r0 * lab_row, (size_t)Bl_ * lab_row);
   for (size_t t = 0; t < embs_.size(); ++t)
-    if (embs_[t].owner == rank_) eng_->h2d(idx_[t], sparse[embs_[t].sparse], (size_t)B_ * embs_[t].bag * 8);
+    if (slice_of(embs_[t], rank_) >= 0) eng_->h2d(idx_[t], sparse[embs_[t].sparse], (size_t)B_ * embs_[t].bag * 8);
   float zero[2] = {0.f, 0.f};
   eng_->h2d(stats_, zero, sizeof(zero));
 
@@ -563,27 +611,28 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
   auto emb_forward = [&]() {
     for (size_t t = 0; t < embs_.size(); ++t) {
       const Emb& e = embs_[t];
-      if (e.owner != rank_) continue;
-      eng_->emb_fwd(table_[t], e.rows, idx_[t], e.bag, world_ > 1 ? emb_full_[t] : act_[e.y], B_, e.D);
+      if (slice_of(e, rank_) < 0) continue;
+      eng_->emb_fwd(table_[t], e.rows, idx_[t], e.bag, world_ > 1 ? emb_full_[t] : act_[e.y], B_, e.Dc);
     }
     if (world_ == 1 || embs_.empty()) return;
-    // pack: per peer p, every owned table's rows [p*Bl, (p+1)*Bl)
+    // pack: per peer p, every held slice's rows [p*Bl, (p+1)*Bl)
     int64_t o = 0;
     for (int p = 0; p < world_; ++p)
       for (size_t t = 0; t < embs_.size(); ++t) {
         const Emb& e = embs_[t];
-        if (e.owner != rank_) continue;
-        eng_->copy(xsend_ + o, emb_full_[t] + (int64_t)p * Bl_ * e.D, (size_t)Bl_ * e.D * 4);
-        o += (int64_t)Bl_ * e.D;
+        if (slice_of(e, rank_) < 0) continue;
+        eng_->copy(xsend_ + o, emb_full_[t] + (int64_t)p * Bl_ * e.Dc, (size_t)Bl_ * e.Dc * 4);
+        o += (int64_t)Bl_ * e.Dc;
       }
     eng_->all_to_all(xsend_, xcount_send_.data(), xrecv_, xcount_recv_.data());
     o = 0;
     for (int p = 0; p < world_; ++p)
       for (size_t t = 0; t < embs_.size(); ++t) {
         const Emb& e = embs_[t];
-        if (e.owner != p) continue;
-        eng_->copy(act_[e.y], xrecv_ + o, (size_t)Bl_ * e.D * 4);
-        o += (int64_t)Bl_ * e.D;
+        const int j = slice_of(e, p);
+        if (j < 0) continue;
+        eng_->copy2d(act_[e.y] + (int64_t)j * e.Dc, (size_t)e.D * 4, xrecv_ + o, (size_t)e.Dc * 4, (size_t)e.Dc * 4, Bl_);
+        o += (int64_t)Bl_ * e.Dc;
       }
   };
   emb_forward();
@@ -649,24 +698,25 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
       for (int p = 0; p < world_; ++p)
         for (size_t t = 0; t < embs_.size(); ++t) {
           const Emb& e = embs_[t];
-          if (e.owner != p) continue;
-          eng_->copy(xrecv_ + o, grad_[e.y], (size_t)Bl_ * e.D * 4);
-          o += (int64_t)Bl_ * e.D;
+          const int j = slice_of(e, p);
+          if (j < 0) continue;
+          eng_->copy2d(xrecv_ + o, (size_t)e.Dc * 4, grad_[e.y] + (int64_t)j * e.Dc, (size_t)e.D * 4, (size_t)e.Dc * 4, Bl_);
+          o += (int64_t)Bl_ * e.Dc;
         }
       eng_->all_to_all(xrecv_, xcount_recv_.data(), xsend_, xcount_send_.data());
       o = 0;
       for (int p = 0; p < world_; ++p)
         for (size_t t = 0; t < embs_.size(); ++t) {
           const Emb& e = embs_[t];
-          if (e.owner != rank_) continue;
-          eng_->copy(emb_full_[t] + (int64_t)p * Bl_ * e.D, xsend_ + o, (size_t)Bl_ * e.D * 4);
-          o += (int64_t)Bl_ * e.D;
+          if (slice_of(e, rank_) < 0) continue;
+          eng_->copy(emb_full_[t] + (int64_t)p * Bl_ * e.Dc, xsend_ + o, (size_t)Bl_ * e.Dc * 4);
+          o += (int64_t)Bl_ * e.Dc;
         }
     }
     for (size_t t = 0; t < embs_.size(); ++t) {
       const Emb& e = embs_[t];
-      if (e.owner != rank_) continue;
-      eng_->emb_sgd(table_[t], e.rows, idx_[t], e.bag, world_ > 1 ? emb_full_[t] : grad_[e.y], B_, e.D, lr_);
+      if (slice_of(e, rank_) < 0) continue;
+      eng_->emb_sgd(table_[t], e.rows, idx_[t], e.bag, world_ > 1 ? emb_full_[t] : grad_[e.y], B_, e.Dc, lr_);
     }
   }
   if (world_ > 1) eng_->allreduce_wait();
@@ -693,8 +743,14 @@ std::string Model::describe() const {
         << (d.skip_act_grad ? " [sigmoid folded into BCE]" : "") << "\n";
     } else if (n.kind == K_EMB) {
       const Emb& e = embs_[n.idx];
-      o << "  embedding" << n.idx << ": " << e.rows << " x " << e.D << " bag " << e.bag << " on rank " << e.owner
-        << (e.owner == rank_ ? " (local: global-batch lookups, sparse SGD)" : "") << "\n";
+      if (e.holders.size() > 1) {
+        o << "  embedding" << n.idx << ": " << e.rows << " x " << e.D << " bag " << e.bag << " column-split over ranks";
+        for (int h : e.holders) o << " " << h;
+        o << " (" << e.Dc << " columns each" << (slice_of(e, rank_) >= 0 ? "; local slice" : "") << ")\n";
+      } else {
+        o << "  embedding" << n.idx << ": " << e.rows << " x " << e.D << " bag " << e.bag << " on rank " << e.owner
+          << (e.owner == rank_ ? " (local: global-batch lookups, sparse SGD)" : "") << "\n";
+      }
     } else {
       const Dot& d = dots_[n.idx];
       o << "  dot interaction: " << d.in.size() << " features x " << d.D << " -> " << d.W << "\n";

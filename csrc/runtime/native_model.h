@@ -62,7 +62,13 @@ struct Emb {
   int D = 0, bag = 1;
   int y = -1;                  // tensor id of the [local batch][D] output
   int w = -1;                  // parameter entry id (the table)
-  int owner = 0;               // rank holding the table (plan)
+  int owner = 0;               // rank holding the table (plan; the first holder of a split table)
+  // column split (the reference's attribute/parameter split of the embedding weight over its
+  // columns, ParallelConfig [c, 1] with c > 1; bench "table" plan for the ~40 M-row tables):
+  // holders[j] keeps columns [j*Dc, (j+1)*Dc) of every row, looks them up for the global batch
+  // and sends each rank its sample shard of that slice; table-wise = one holder, Dc = D
+  std::vector<int> holders;
+  int Dc = 0;
 };
 
 // DLRM dot interaction (src/ops/tests/test_harness.py:96-186 DotCompressor; caveat C3):
@@ -96,6 +102,9 @@ class Model {
   int dot_interaction(int bottom, const std::vector<int>& embs, int pad_to);
   // table placement before compile (default: greedy by rows over the ranks)
   void set_table_owner(int table, int rank);
+  // column split of a table over `ranks` (D % ranks.size() == 0); holder j keeps columns
+  // [j*D/n, (j+1)*D/n)
+  void set_table_columns(int table, const std::vector<int>& ranks);
   void compile(int loss_type, float lr, double bucket_mb);
   void init_weights(uint64_t seed);            // Glorot-uniform weights, zero biases, U(+-sqrt(1/rows)) tables
   int num_params() const { return (int)pnumel_.size(); }
@@ -103,6 +112,9 @@ class Model {
   // tables: only the owner holds the rows (param_local(i) == false elsewhere)
   bool param_local(int i) const;
   int table_owner(int table) const { return embs_.at(table).owner; }
+  const std::vector<int>& table_holders(int table) const { return embs_.at(table).holders; }
+  // parameters of a column-split table move as the FULL [rows][D] host array: set_param reads this
+  // rank's columns from it, get_param writes them into it (the other columns untouched)
   int num_tables() const { return (int)embs_.size(); }
   void set_param(int i, const float* host);
   void get_param(int i, float* host) const;
@@ -119,6 +131,7 @@ class Model {
     int kind, idx;
   };
   int dense_out_node() const;
+  int slice_of(const Emb& e, int r) const;    // this rank's column slice of e, -1: none
   void check_tensor(int t, const char* what) const;
 
   int B_, Bl_, device_, rank_, world_;
@@ -145,8 +158,8 @@ class Model {
   float* grads_ = nullptr;
   std::vector<float*> act_;                   // tensor id -> [Bl][cols]
   std::vector<float*> grad_;                  // tensor id -> [Bl][cols]
-  std::vector<float*> table_;                 // table id -> [rows][D] (owner only)
-  std::vector<float*> emb_full_;              // table id -> [B][D] owner-side lookups (world > 1)
+  std::vector<float*> table_;                 // table id -> [rows][Dc] (holders only)
+  std::vector<float*> emb_full_;              // table id -> [B][Dc] holder-side lookups (world > 1)
   std::vector<int64_t*> idx_;                 // table id -> [B][bag] indices (owner only)
   float* xsend_ = nullptr;                    // all-to-all staging (world > 1)
   float* xrecv_ = nullptr;
@@ -182,6 +195,8 @@ class Engine {
   virtual void allreduce_wait() = 0;
   // ---- embeddings / interaction / exchange (DLRM plans) ----
   virtual void copy(void* dst, const void* src, size_t bytes) = 0;   // device -> device
+  // rows x width_bytes from src (row pitch spitch bytes) to dst (pitch dpitch), device -> device
+  virtual void copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width_bytes, size_t rows) = 0;
   // out[b] = sum_j W[idx[b][j]]  (b < B; an index outside [0, rows) contributes nothing)
   virtual void emb_fwd(const float* W, int64_t rows, const int64_t* idx, int bag, float* out, int64_t B, int D) = 0;
   // W[idx[b][j]] -= lr * g[b]  (duplicates accumulate)

@@ -60,8 +60,18 @@ static int run_rank(int device, const char* prefix, int steps, int rank, int wor
   CHECK(t = fmn_model_dot_interaction(m, bottom, NT, emb, 16));
   CHECK(t = fmn_model_dense(m, t, 32, 11, 1));
   CHECK(t = fmn_model_dense(m, t, 1, 12, 1));
-  /* a fixed table-wise placement over the ranks (round robin) */
-  for (int i = 0; i < NT; ++i) CHECK(fmn_model_set_table_owner(m, i, i % world));
+  /* a fixed table-wise placement over the ranks (round robin); NATIVE_DLRM_PLAN=colsplit splits
+   * tables 0 and 2 by columns over every rank (the bench "table" plan's large tables) */
+  const int colsplit = getenv("NATIVE_DLRM_PLAN") && strcmp(getenv("NATIVE_DLRM_PLAN"), "colsplit") == 0;
+  for (int i = 0; i < NT; ++i) {
+    if (colsplit && (i == 0 || i == 2)) {
+      int ranks[16];
+      for (int r = 0; r < world; ++r) ranks[r] = r;
+      CHECK(fmn_model_set_table_columns(m, i, world, ranks));
+    } else {
+      CHECK(fmn_model_set_table_owner(m, i, i % world));
+    }
+  }
   CHECK(fmn_model_compile(m, 54, 0.1f, 0.0005));
   static char desc[8192];
   fmn_model_describe(m, desc, sizeof(desc));
@@ -125,7 +135,9 @@ static int run_rank(int device, const char* prefix, int steps, int rank, int wor
     const int32_t local = fmn_model_param_local(m, i) == 1;
     fwrite(&local, 4, 1, f);
     if (local) {
+      /* a column-split table fills only this rank's columns: the rest keep the initial values */
       float* w = (float*)malloc(numel[i] * sizeof(float));
+      memcpy(w, init[i], numel[i] * sizeof(float));
       CHECK(fmn_model_get_param(m, i, w));
       fwrite(w, 4, numel[i], f);
       free(w);

@@ -251,6 +251,39 @@ def test_native_c_dlrm_tablewise_trains_like_the_executor(tmp_path, world):
         assert all(rec["ranks"][1][0][i] is not None for i in (5, 7))
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_native_c_dlrm_column_split_trains_like_the_executor(tmp_path, world):
+    """the native plan compiler also compiles COLUMN-split tables (the bench's table
+    plan: the large tables split by columns over every rank): each holder looks up its column slice
+    for the global batch, the all-to-all assembles every sample shard's columns, the reverse
+    exchange returns each holder its slice of the row gradients.  Merged over the holders, the
+    tables end like the Python executor's."""
+    exe = _build_dlrm_c(tmp_path)
+    rdv = tmp_path / "rdv"
+    rdv.mkdir()
+    prefix = str(tmp_path / "run")
+    env = dict(os.environ, NATIVE_DLRM_PLAN="colsplit")
+    r = subprocess.run([exe, "cpu", prefix, "4", str(world), str(rdv)], capture_output=True, text=True, timeout=120,
+                       env=env)
+    assert r.returncode == 0 and "native_dlrm ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "column-split over ranks" in r.stdout
+    rec = _parse_dlrm(prefix, world)
+    got = _replay_dlrm(rec)
+    dc = 16 // world
+    for i, want in enumerate(got):
+        if i in (4, 6):                    # tables 0 and 2: every rank holds a column slice
+            w = np.empty_like(want).reshape(-1, 16)
+            for rk in range(world):
+                part = rec["ranks"][rk][0][i]
+                assert part is not None, (i, rk)
+                w[:, rk * dc:(rk + 1) * dc] = part.reshape(-1, 16)[:, rk * dc:(rk + 1) * dc]
+            np.testing.assert_allclose(w.reshape(-1), want, rtol=2e-5, atol=2e-6, err_msg=f"param {i}")
+            continue
+        holders = [f[i] for f, _ in rec["ranks"] if f[i] is not None]
+        assert holders, f"param {i} held by no rank"
+        np.testing.assert_allclose(holders[0], want, rtol=2e-5, atol=2e-6, err_msg=f"param {i}")
+
+
 @pytest.mark.gpu
 def test_native_c_dlrm_hip_engine_matches_cpu(tmp_path):
     """The same C program on the HIP engine (flexmi's embedding / interaction / GEMM kernels,
