@@ -171,6 +171,10 @@ int fmn_model_table_owner(fmn_model_t m, int table);
  * a table-wise table) and writes up to max holder ranks. */
 int fmn_model_set_table_columns(fmn_model_t m, int table, int n, const int* ranks);
 int fmn_model_table_columns(fmn_model_t m, int table, int* ranks, int max);
+/* row split of a table over n holder ranks: holder j keeps rows [j*rows/n, (j+1)*rows/n) of every
+ * column, looks up the global batch (lookups outside its rows add nothing) and each rank sums the
+ * holders' partial bag sums; set/get_param move the FULL host array (this rank's rows). */
+int fmn_model_set_table_rows(fmn_model_t m, int table, int n, const int* ranks);
 /* loss: 51 sparse categorical CE (softmax of the last layer's logits, int32 labels), 52 MSE (avg),
  * 54 binary CE (sigmoid output); bucket_mb = gradient all-reduce bucket size */
 int fmn_model_compile(fmn_model_t m, int loss_type, float lr, double bucket_mb);

@@ -44,6 +44,14 @@ void fm_loss_fwd_bwd(const void* logits, int logits_bf16, const void* labels, vo
                      int loss_type, float scale, float* acc, int mask, float clamp_t, hipStream_t s);
 void fm_sgd_update(float* W, float* G, float* V, unsigned short* Wc, const float* lr, long n, float wd, float mom, int nesterov,
                    int zero_g, hipStream_t s);
+void fm_embedding_fwd_multi(int n, const float* const* W, const void* const* idx, const int* idx64, void* const* out,
+                            const long* ldo, const long* lo, const int* rows, const int* D, const int* bag,
+                            const float* scale, int out_bf16, long B, hipStream_t st);
+void fm_embedding_bwd_multi(int n, float* const* W, const void* const* idx, const int* idx64, const void* const* dy,
+                            const long* ldg, const long* lo, const int* rows, const int* D, const int* bag,
+                            const float* scale, int dy_bf16, const float* lr, long B, int* const* owner,
+                            int* const* dups, int* const* ndup, hipStream_t st);
+void fm_binary_forward(int code, const void* a, const void* b, void* y, long n, int relu, int bf16, hipStream_t s);
 void fm_embedding_fwd(const void* idx, int idx64, const float* W, void* out, int out_bf16, long B, int bag, int rows, int D,
                       long ldo, float scale, hipStream_t s);
 void fm_embedding_bwd(const void* idx, int idx64, const void* dy, int dy_bf16, float* W, const float* lr, long B, int bag,
@@ -167,13 +175,26 @@ class HipEngine : public Engine {
     HIPX(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, hipMemcpyDeviceToDevice, st_));
   }
 
-  void emb_fwd(const float* W, int64_t rows, const int64_t* idx, int bag, float* out, int64_t B, int D) override {
-    fm_embedding_fwd(idx, 1, W, out, 0, B, bag, (int)rows, D, D, 1.f, st_);
+  void emb_fwd(const float* W, int64_t rows, const int64_t* idx, int bag, float* out, int64_t B, int D,
+               int64_t lo) override {
+    const void* ix = idx;
+    const int i64 = 1, r = (int)rows;
+    void* o = out;
+    const long ld = D, l0 = (long)lo;
+    const float sc = 1.f;
+    fm_embedding_fwd_multi(1, &W, &ix, &i64, &o, &ld, &l0, &r, &D, &bag, &sc, 0, B, st_);
   }
-  void emb_sgd(float* W, int64_t rows, const int64_t* idx, int bag, const float* g, int64_t B, int D, float lr) override {
+  void emb_sgd(float* W, int64_t rows, const int64_t* idx, int bag, const float* g, int64_t B, int D, float lr,
+               int64_t lo) override {
     set_lr(lr);
-    fm_embedding_bwd(idx, 1, g, 0, W, lr_, B, bag, (int)rows, D, D, 1.f, st_);
+    const void* ix = idx;
+    const void* dy = g;
+    const int i64 = 1, r = (int)rows;
+    const long ld = D, l0 = (long)lo;
+    const float sc = 1.f;
+    fm_embedding_bwd_multi(1, &W, &ix, &i64, &dy, &ld, &l0, &r, &D, &bag, &sc, 0, lr_, B, nullptr, nullptr, nullptr, st_);
   }
+  void add(float* dst, const float* src, int64_t n) override { fm_binary_forward(0, dst, src, dst, n, 0, 0, st_); }
   void dot_fwd(const float* const* z, int F, float* y, int M, int D, int W) override {
     fm_dot_interaction_fwd_f32(z, F, D, y, W, M, D, W, 0, st_);
   }

@@ -152,26 +152,31 @@ class CpuEngine : public Engine {
   }
   void allreduce_wait() override {}
   void copy(void* dst, const void* src, size_t bytes) override { std::memcpy(dst, src, bytes); }
+  void add(float* dst, const float* src, int64_t n) override {
+    for (int64_t i = 0; i < n; ++i) dst[i] += src[i];
+  }
   void copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows) override {
     for (size_t r = 0; r < rows; ++r)
       std::memcpy(static_cast<char*>(dst) + r * dpitch, static_cast<const char*>(src) + r * spitch, width);
   }
-  void emb_fwd(const float* W, int64_t rows, const int64_t* idx, int bag, float* out, int64_t B, int D) override {
+  void emb_fwd(const float* W, int64_t rows, const int64_t* idx, int bag, float* out, int64_t B, int D,
+               int64_t lo) override {
     for (int64_t b = 0; b < B; ++b) {
       float* o = out + b * D;
       for (int d = 0; d < D; ++d) o[d] = 0.f;
       for (int j = 0; j < bag; ++j) {
-        const int64_t r = idx[b * bag + j];
+        const int64_t r = idx[b * bag + j] - lo;
         if (r < 0 || r >= rows) continue;
         const float* w = W + r * D;
         for (int d = 0; d < D; ++d) o[d] += w[d];
       }
     }
   }
-  void emb_sgd(float* W, int64_t rows, const int64_t* idx, int bag, const float* g, int64_t B, int D, float lr) override {
+  void emb_sgd(float* W, int64_t rows, const int64_t* idx, int bag, const float* g, int64_t B, int D, float lr,
+               int64_t lo) override {
     for (int64_t b = 0; b < B; ++b)
       for (int j = 0; j < bag; ++j) {
-        const int64_t r = idx[b * bag + j];
+        const int64_t r = idx[b * bag + j] - lo;
         if (r < 0 || r >= rows) continue;
         float* w = W + r * D;
         const float* gr = g + b * D;
@@ -393,6 +398,19 @@ void Model::set_table_columns(int table, const std::vector<int>& ranks) {
   e.owner = ranks[0];
 }
 
+void Model::set_table_rows(int table, const std::vector<int>& ranks) {
+  set_table_columns(table, std::vector<int>{ranks.at(0)});   // validation of table / first rank
+  Emb& e = embs_[table];
+  for (size_t i = 0; i < ranks.size(); ++i) {
+    if (ranks[i] < 0 || ranks[i] >= world_) throw std::invalid_argument("native model: holder rank");
+    for (size_t j = 0; j < i; ++j)
+      if (ranks[j] == ranks[i]) throw std::invalid_argument("native model: holder listed twice");
+  }
+  if ((int64_t)ranks.size() > e.rows) throw std::invalid_argument("native model: more row blocks than rows");
+  e.holders = ranks;
+  e.rows_split = ranks.size() > 1;
+}
+
 int Model::slice_of(const Emb& e, int r) const {
   for (size_t j = 0; j < e.holders.size(); ++j)
     if (e.holders[j] == r) return (int)j;
@@ -453,7 +471,11 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
     }
     for (Emb& e : embs_) {
       if (e.holders.empty()) e.holders = {e.owner};
-      e.Dc = e.D / (int)e.holders.size();
+      const int n = (int)e.holders.size();
+      e.Dc = e.rows_split ? e.D : e.D / n;
+      const int j = slice_of(e, rank_);
+      e.lo = e.rows_split && j >= 0 ? e.rows * j / n : 0;
+      e.nrows = e.rows_split ? (j >= 0 ? e.rows * (j + 1) / n - e.lo : 0) : e.rows;
     }
   }
   // dense parameter entries in backward order -> one flat buffer, all-reduce buckets
@@ -511,7 +533,7 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
   for (size_t t = 0; t < embs_.size(); ++t) {
     const Emb& e = embs_[t];
     if (slice_of(e, rank_) < 0) continue;
-    table_[t] = (float*)eng_->alloc((size_t)e.rows * e.Dc * 4);
+    table_[t] = (float*)eng_->alloc((size_t)e.nrows * e.Dc * 4);
     idx_[t] = (int64_t*)eng_->alloc((size_t)B_ * e.bag * 8);
     if (world_ > 1) emb_full_[t] = (float*)eng_->alloc((size_t)B_ * e.Dc * 4);
   }
@@ -556,7 +578,9 @@ void Model::set_param(int i, const float* host) {
     const Emb& e = embs_[t];
     const int j = slice_of(e, rank_);
     if (j < 0) throw std::invalid_argument("native model: table not on this rank");
-    if (e.Dc == e.D) {
+    if (e.rows_split) {
+      eng_->h2d(table_[t], host + e.lo * e.D, (size_t)e.nrows * e.D * 4);
+    } else if (e.Dc == e.D) {
       eng_->h2d(table_[t], host, pnumel_[i] * 4);
     } else {
       std::vector<float> sl((size_t)e.rows * e.Dc);
@@ -578,7 +602,9 @@ void Model::get_param(int i, float* host) const {
     const Emb& e = embs_[t];
     const int j = slice_of(e, rank_);
     if (j < 0) throw std::invalid_argument("native model: table not on this rank");
-    if (e.Dc == e.D) {
+    if (e.rows_split) {
+      eng_->d2h(host + e.lo * e.D, table_[t], (size_t)e.nrows * e.D * 4);
+    } else if (e.Dc == e.D) {
       eng_->d2h(host, table_[t], pnumel_[i] * 4);
     } else {
       std::vector<float> sl((size_t)e.rows * e.Dc);
@@ -612,7 +638,7 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
     for (size_t t = 0; t < embs_.size(); ++t) {
       const Emb& e = embs_[t];
       if (slice_of(e, rank_) < 0) continue;
-      eng_->emb_fwd(table_[t], e.rows, idx_[t], e.bag, world_ > 1 ? emb_full_[t] : act_[e.y], B_, e.Dc);
+      eng_->emb_fwd(table_[t], e.nrows, idx_[t], e.bag, world_ > 1 ? emb_full_[t] : act_[e.y], B_, e.Dc, e.lo);
     }
     if (world_ == 1 || embs_.empty()) return;
     // pack: per peer p, every held slice's rows [p*Bl, (p+1)*Bl)
@@ -631,7 +657,10 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
         const Emb& e = embs_[t];
         const int j = slice_of(e, p);
         if (j < 0) continue;
-        eng_->copy2d(act_[e.y] + (int64_t)j * e.Dc, (size_t)e.D * 4, xrecv_ + o, (size_t)e.Dc * 4, (size_t)e.Dc * 4, Bl_);
+        if (e.rows_split && j > 0)       // row blocks: the holders' partial bag sums add up
+          eng_->add(act_[e.y], xrecv_ + o, (int64_t)Bl_ * e.D);
+        else
+          eng_->copy2d(act_[e.y] + (int64_t)j * e.Dc, (size_t)e.D * 4, xrecv_ + o, (size_t)e.Dc * 4, (size_t)e.Dc * 4, Bl_);
         o += (int64_t)Bl_ * e.Dc;
       }
   };
@@ -700,7 +729,9 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
           const Emb& e = embs_[t];
           const int j = slice_of(e, p);
           if (j < 0) continue;
-          eng_->copy2d(xrecv_ + o, (size_t)e.Dc * 4, grad_[e.y] + (int64_t)j * e.Dc, (size_t)e.D * 4, (size_t)e.Dc * 4, Bl_);
+          // (row blocks: every holder gets the whole gradient, j * Dc = 0 columns offset)
+          eng_->copy2d(xrecv_ + o, (size_t)e.Dc * 4, grad_[e.y] + (e.rows_split ? 0 : (int64_t)j * e.Dc), (size_t)e.D * 4,
+                       (size_t)e.Dc * 4, Bl_);
           o += (int64_t)Bl_ * e.Dc;
         }
       eng_->all_to_all(xrecv_, xcount_recv_.data(), xsend_, xcount_send_.data());
@@ -716,7 +747,7 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
     for (size_t t = 0; t < embs_.size(); ++t) {
       const Emb& e = embs_[t];
       if (slice_of(e, rank_) < 0) continue;
-      eng_->emb_sgd(table_[t], e.rows, idx_[t], e.bag, world_ > 1 ? emb_full_[t] : grad_[e.y], B_, e.Dc, lr_);
+      eng_->emb_sgd(table_[t], e.nrows, idx_[t], e.bag, world_ > 1 ? emb_full_[t] : grad_[e.y], B_, e.Dc, lr_, e.lo);
     }
   }
   if (world_ > 1) eng_->allreduce_wait();
@@ -743,7 +774,13 @@ std::string Model::describe() const {
         << (d.skip_act_grad ? " [sigmoid folded into BCE]" : "") << "\n";
     } else if (n.kind == K_EMB) {
       const Emb& e = embs_[n.idx];
-      if (e.holders.size() > 1) {
+      if (e.rows_split) {
+        o << "  embedding" << n.idx << ": " << e.rows << " x " << e.D << " bag " << e.bag << " row-split over ranks";
+        for (int h : e.holders) o << " " << h;
+        o << " (partial bag sums added" << (slice_of(e, rank_) >= 0 ? "; local rows " : "");
+        if (slice_of(e, rank_) >= 0) o << e.lo << ".." << e.lo + e.nrows;
+        o << ")\n";
+      } else if (e.holders.size() > 1) {
         o << "  embedding" << n.idx << ": " << e.rows << " x " << e.D << " bag " << e.bag << " column-split over ranks";
         for (int h : e.holders) o << " " << h;
         o << " (" << e.Dc << " columns each" << (slice_of(e, rank_) >= 0 ? "; local slice" : "") << ")\n";

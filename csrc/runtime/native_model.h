@@ -69,6 +69,12 @@ struct Emb {
   // and sends each rank its sample shard of that slice; table-wise = one holder, Dc = D
   std::vector<int> holders;
   int Dc = 0;
+  // row split (the flexmi [c, n, r] extension: r row blocks): holder j keeps rows [lo_j, lo_{j+1})
+  // of all D columns and looks up the global batch; lookups outside its rows add nothing, and each
+  // rank SUMS the holders' partial bag sums for its sample shard (gradients go to every holder,
+  // which updates the rows it keeps)
+  bool rows_split = false;
+  int64_t lo = 0, nrows = 0;   // this rank's row block (plan)
 };
 
 // DLRM dot interaction (src/ops/tests/test_harness.py:96-186 DotCompressor; caveat C3):
@@ -105,6 +111,9 @@ class Model {
   // column split of a table over `ranks` (D % ranks.size() == 0); holder j keeps columns
   // [j*D/n, (j+1)*D/n)
   void set_table_columns(int table, const std::vector<int>& ranks);
+  // row split of a table over `ranks`: holder j keeps rows [j*rows/n, (j+1)*rows/n); its parameters
+  // move as the FULL host array (this rank's rows read / written)
+  void set_table_rows(int table, const std::vector<int>& ranks);
   void compile(int loss_type, float lr, double bucket_mb);
   void init_weights(uint64_t seed);            // Glorot-uniform weights, zero biases, U(+-sqrt(1/rows)) tables
   int num_params() const { return (int)pnumel_.size(); }
@@ -197,10 +206,13 @@ class Engine {
   virtual void copy(void* dst, const void* src, size_t bytes) = 0;   // device -> device
   // rows x width_bytes from src (row pitch spitch bytes) to dst (pitch dpitch), device -> device
   virtual void copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width_bytes, size_t rows) = 0;
-  // out[b] = sum_j W[idx[b][j]]  (b < B; an index outside [0, rows) contributes nothing)
-  virtual void emb_fwd(const float* W, int64_t rows, const int64_t* idx, int bag, float* out, int64_t B, int D) = 0;
-  // W[idx[b][j]] -= lr * g[b]  (duplicates accumulate)
-  virtual void emb_sgd(float* W, int64_t rows, const int64_t* idx, int bag, const float* g, int64_t B, int D, float lr) = 0;
+  // out[b] = sum_j W[idx[b][j] - lo]  (b < B; an index outside [lo, lo + rows) contributes nothing)
+  virtual void emb_fwd(const float* W, int64_t rows, const int64_t* idx, int bag, float* out, int64_t B, int D,
+                       int64_t lo) = 0;
+  // W[idx[b][j] - lo] -= lr * g[b]  (duplicates accumulate; indices outside the rows skipped)
+  virtual void emb_sgd(float* W, int64_t rows, const int64_t* idx, int bag, const float* g, int64_t B, int D, float lr,
+                       int64_t lo) = 0;
+  virtual void add(float* dst, const float* src, int64_t n) = 0;   // dst += src (device)
   // y[M][W] = [z0 | lower(Z Z^T) | 0] ; dz[i] = (S Z)_i (+ dy[:, :D] for i = 0), S = dG + dG^T
   virtual void dot_fwd(const float* const* z, int F, float* y, int M, int D, int W) = 0;
   virtual void dot_bwd(const float* const* z, int F, const float* dy, float* const* dz, int M, int D, int W) = 0;

@@ -1,6 +1,7 @@
 /* Trains a small DLRM through the native C API alone (libflexmi_native_c: C++ plan compiler +
  * engine, no Python anywhere in the process): bottom MLP 13-32-16, four embedding tables
- * (100 / 50 / 200 / 30 rows x 16) placed TABLE-WISE over the ranks, dot interaction, top MLP
+ * (100 / 50 / 200 / 30 rows x 16) placed TABLE-WISE over the ranks (NATIVE_DLRM_PLAN: colsplit / rowsplit /
+ * mixed split some of them by columns or rows over every rank), dot interaction, top MLP
  * -32-1 with a sigmoid, binary cross-entropy, SGD.  With world > 1 the program forks one process
  * per rank; the ranks exchange embeddings (all-to-all) and dense gradients (all-reduce) through
  * the CPU engine's host communicator in the rendezvous directory (or RCCL on the HIP engine).
@@ -62,12 +63,16 @@ static int run_rank(int device, const char* prefix, int steps, int rank, int wor
   CHECK(t = fmn_model_dense(m, t, 1, 12, 1));
   /* a fixed table-wise placement over the ranks (round robin); NATIVE_DLRM_PLAN=colsplit splits
    * tables 0 and 2 by columns over every rank (the bench "table" plan's large tables) */
-  const int colsplit = getenv("NATIVE_DLRM_PLAN") && strcmp(getenv("NATIVE_DLRM_PLAN"), "colsplit") == 0;
+  const char* plan = getenv("NATIVE_DLRM_PLAN") ? getenv("NATIVE_DLRM_PLAN") : "table";
+  /* "mixed": table 0 split by columns, table 1 by rows over every rank, the others whole */
+  const int colsplit = strcmp(plan, "colsplit") == 0, rowsplit = strcmp(plan, "rowsplit") == 0, mixed = strcmp(plan, "mixed") == 0;
+  int all[16];
+  for (int r = 0; r < world; ++r) all[r] = r;
   for (int i = 0; i < NT; ++i) {
-    if (colsplit && (i == 0 || i == 2)) {
-      int ranks[16];
-      for (int r = 0; r < world; ++r) ranks[r] = r;
-      CHECK(fmn_model_set_table_columns(m, i, world, ranks));
+    if ((colsplit && (i == 0 || i == 2)) || (mixed && i == 0)) {
+      CHECK(fmn_model_set_table_columns(m, i, world, all));
+    } else if ((rowsplit && (i == 1 || i == 3)) || (mixed && i == 1)) {
+      CHECK(fmn_model_set_table_rows(m, i, world, all));
     } else {
       CHECK(fmn_model_set_table_owner(m, i, i % world));
     }

@@ -251,32 +251,46 @@ def test_native_c_dlrm_tablewise_trains_like_the_executor(tmp_path, world):
         assert all(rec["ranks"][1][0][i] is not None for i in (5, 7))
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_native_c_dlrm_column_split_trains_like_the_executor(tmp_path, world):
-    """the native plan compiler also compiles COLUMN-split tables (the bench's table
-    plan: the large tables split by columns over every rank): each holder looks up its column slice
-    for the global batch, the all-to-all assembles every sample shard's columns, the reverse
-    exchange returns each holder its slice of the row gradients.  Merged over the holders, the
-    tables end like the Python executor's."""
+@pytest.mark.parametrize("plan,world", [("colsplit", 2), ("colsplit", 4), ("rowsplit", 2), ("rowsplit", 4),
+                                        ("mixed", 4)])
+def test_native_c_dlrm_split_tables_train_like_the_executor(tmp_path, plan, world):
+    """the native plan compiler also compiles column- and row-split tables (the bench's
+    table plan splits the large tables by columns over every rank; row blocks are the [c, n, r]
+    extension): column holders look up their slice for the global batch and the all-to-all
+    assembles the columns; row holders look up the lookups in their rows and each rank sums the
+    partial bag sums; every holder updates its part.  Merged over the holders, the tables end like
+    the Python executor's."""
     exe = _build_dlrm_c(tmp_path)
     rdv = tmp_path / "rdv"
     rdv.mkdir()
     prefix = str(tmp_path / "run")
-    env = dict(os.environ, NATIVE_DLRM_PLAN="colsplit")
+    env = dict(os.environ, NATIVE_DLRM_PLAN=plan)
     r = subprocess.run([exe, "cpu", prefix, "4", str(world), str(rdv)], capture_output=True, text=True, timeout=120,
                        env=env)
     assert r.returncode == 0 and "native_dlrm ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
-    assert "column-split over ranks" in r.stdout
+    cols = {"colsplit": (0, 2), "rowsplit": (), "mixed": (0,)}[plan]
+    rows = {"colsplit": (), "rowsplit": (1, 3), "mixed": (1,)}[plan]
+    if cols:
+        assert "column-split over ranks" in r.stdout
+    if rows:
+        assert "row-split over ranks" in r.stdout
     rec = _parse_dlrm(prefix, world)
     got = _replay_dlrm(rec)
-    dc = 16 // world
     for i, want in enumerate(got):
-        if i in (4, 6):                    # tables 0 and 2: every rank holds a column slice
+        t = i - 4                           # parameters 4..7 are the tables
+        if t in cols or t in rows:
             w = np.empty_like(want).reshape(-1, 16)
+            n = w.shape[0]
             for rk in range(world):
                 part = rec["ranks"][rk][0][i]
                 assert part is not None, (i, rk)
-                w[:, rk * dc:(rk + 1) * dc] = part.reshape(-1, 16)[:, rk * dc:(rk + 1) * dc]
+                part = part.reshape(-1, 16)
+                if t in cols:
+                    dc = 16 // world
+                    w[:, rk * dc:(rk + 1) * dc] = part[:, rk * dc:(rk + 1) * dc]
+                else:
+                    lo, hi = n * rk // world, n * (rk + 1) // world
+                    w[lo:hi] = part[lo:hi]
             np.testing.assert_allclose(w.reshape(-1), want, rtol=2e-5, atol=2e-6, err_msg=f"param {i}")
             continue
         holders = [f[i] for f, _ in rec["ranks"] if f[i] is not None]
