@@ -133,14 +133,14 @@ def _dw_lib(M, N, K, dtype):
     return DW_LIB == "1" or (N >= 512 and K >= 480 and M >= 4096)
 
 
-# FM_SMALLK=1/0: thin-input fp32 Linear layers (in_features <= 32, the 13->512 bottom layer of
+# FM_SMALLK=1/0: thin-input Linear layers (fp32 or bf16; in_features <= 32, the 13->512 bottom layer of
 # DLRM) on the VALU kernels of gemm_small.hip instead of a 1-2 step K loop of MFMA tiles (forward)
 # and a split-K GEMM + reduce (dW)
 SMALLK = os.environ.get("FM_SMALLK", "1") == "1"
 
 
 def _smallk(x2, K):
-    return SMALLK and x2.dtype == torch.float32 and K <= 32 and K % 4 == 0 and x2.stride(0) % 4 == 0
+    return SMALLK and K <= 32 and K % 4 == 0 and x2.stride(0) % 4 == 0
 
 
 def _dw_smallk(dpre, x2, dw, db, upd):
@@ -315,6 +315,16 @@ def dot_interaction_backward(inputs, dy, in_grads, accs, self_inter, act0=10):
     ld = next((g.stride(0) for g in in_grads if g is not None), D)
     C().dot_bwd(list(inputs), inputs[0].stride(0), dy, dy.stride(0), list(in_grads), ld, mask, D, bool(self_inter),
                 int(act0))
+
+
+def dot_interaction_backward_upd(inputs, dy, in_grads, self_inter, act0, desc):
+    """fp32 interaction backward with the embedding sparse-SGD updates of the features described
+    by ``desc`` (C().dot_upd_desc) applied in the kernel; their dZ is not written.  False: not
+    launched (outside the fused kernel's domain)."""
+    D = inputs[0].shape[-1]
+    ld = next((g.stride(0) for g in in_grads if g is not None), D)
+    return bool(C().dot_bwd_upd(list(inputs), inputs[0].stride(0), dy, dy.stride(0), list(in_grads), ld, D,
+                                bool(self_inter), int(act0), desc))
 
 
 # ------------------------------------------------------------------ optimizers / loss
