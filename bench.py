@@ -459,8 +459,11 @@ def _timed(a, comm, model, cfg, dcfg, dense_in, sparse, strategy, search, ex, t_
         # exact in fp32, fp32 accumulation; float64-oracle tests at the native kernel's tolerance)
         # for the big layers, the native v_mfma_f32_16x16x4_f32 kernel for the rest
         from flexmi.ops import _kernels as _K
-        rec["config"]["fp32_gemm"] = {0: "native-f32-mfma", 1: "bf16x3-split-v1", 2: "bf16x3-split-all",
+        rec["config"]["fp32_gemm"] = {0: "native-f32-mfma", 2: "bf16x3-split-all",
                                       3: "bf16x3-split-big+native-f32-mfma"}.get(_K.C().gemm_f32_get_split(), "?")
+        # measured per-shape GEMM configurations in use (flexmi/ops/gemm_tune.py; FM_GEMM_TUNE=0: none)
+        from flexmi.ops import gemm_tune as _T
+        rec["config"]["gemm_tuned_entries"] = len(_T.table())
     if search is not None:
         rec["config"]["search"] = dict(search)
     if rank == 0 and a.profile:

@@ -3,7 +3,6 @@
 // only, no torch headers); this file only unpacks torch tensors into raw pointers and launches on
 // PyTorch's current HIP stream, so kernels compose with torch's caching allocator, RCCL streams
 // and hipGraph capture.
-#include "../kernels/dot_upd.h"
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include <cstring>
@@ -73,10 +72,6 @@ void fm_dot_interaction_bwd(const void* const* z, int F, long ldz, const void* d
                             unsigned acc_mask, long B, int D, int self, hipStream_t s);
 void fm_dot_interaction_fwd_f32(const float* const* z, int F, long ldz, float* out, long ldo, long B, int D, int W, int self,
                                 hipStream_t s);
-int fm_dot_interaction_bwd_f32_upd(const float* const* z, int F, long ldz, const float* dout, long ldo, float* const* dz,
-                                   long lddz, long B, int D, int self, int act0, const void* desc, hipStream_t s);
-void fm_embedding_count(int n, const void* const* idx, int i64, const long* lo, const int* rows, const int* bag,
-                        int* const* slot, int* const* own, long B, hipStream_t st);
 void fm_dot_interaction_bwd_f32(const float* const* z, int F, long ldz, const float* dout, long ldo, float* const* dz,
                                 long lddz, unsigned acc_mask, long B, int D, int self, int act0, hipStream_t s);
 void fm_sgd_update(float* W, float* G, float* V, unsigned short* Wc, const float* lr, long n, float wd, float mom,
@@ -611,101 +606,6 @@ void dot_fwd(std::vector<torch::Tensor> zs, int64_t ldz, torch::Tensor out, int6
 }
 
 // act0 (fp32 only): activation backward of feature 0's producer applied to dz[0] (10 = none)
-// Device descriptor of the embedding sparse-SGD update fused into the fp32 interaction backward
-// (csrc/kernels/dot_upd.h): per feature i either None (dZ[i] written as usual) or the table W[i]
-// [rows, 128] fp32, its bag-1 lookup indices, the count-pass slots / first-arrival flags (None:
-// atomics only), its first row lo[i] and scale[i]; lr the device learning rate.  Built once per plan.
-torch::Tensor dot_upd_desc(std::vector<c10::optional<torch::Tensor>> W, std::vector<c10::optional<torch::Tensor>> idx,
-                           std::vector<c10::optional<torch::Tensor>> slot, std::vector<c10::optional<torch::Tensor>> own,
-                           std::vector<int64_t> lo, std::vector<double> scale, torch::Tensor lr) {
-  const size_t F = W.size();
-  TORCH_CHECK(F <= DOT_UPD_MAXF && idx.size() == F && slot.size() == F && own.size() == F && lo.size() == F &&
-                  scale.size() == F, "dot_upd_desc: per-feature lists of one length <= 32");
-  TORCH_CHECK(lr.is_cuda() && lr.scalar_type() == torch::kFloat32, "dot_upd_desc: device fp32 lr");
-  DotUpd u{};
-  int i64 = -1;
-  for (size_t i = 0; i < F; ++i) {
-    if (!(W[i].has_value() && W[i]->defined())) continue;
-    const auto& w = *W[i];
-    TORCH_CHECK(w.is_cuda() && w.scalar_type() == torch::kFloat32 && w.is_contiguous() && w.dim() == 2 && w.size(1) == 128,
-                "dot_upd_desc: fp32 [rows, 128] tables");
-    TORCH_CHECK(idx[i].has_value() && idx[i]->is_contiguous() && idx[i]->numel() == idx[i]->size(0),
-                "dot_upd_desc: bag-1 indices");
-    const int w64 = idx[i]->scalar_type() == torch::kInt64 ? 1 : 0;
-    TORCH_CHECK(w64 || idx[i]->scalar_type() == torch::kInt32, "dot_upd_desc: int32/int64 indices");
-    TORCH_CHECK(i64 < 0 || i64 == w64, "dot_upd_desc: one index width");
-    i64 = w64;
-    u.W[i] = w.data_ptr<float>();
-    u.idx[i] = idx[i]->data_ptr();
-    u.rows[i] = (int)w.size(0);
-    u.lo[i] = (long)lo[i];
-    u.scale[i] = (float)scale[i];
-    if (slot[i].has_value() && slot[i]->defined()) {
-      TORCH_CHECK(slot[i]->scalar_type() == torch::kInt32 && slot[i]->numel() >= w.size(0) && own[i].has_value() &&
-                      own[i]->scalar_type() == torch::kInt32 && own[i]->numel() >= idx[i]->numel(),
-                  "dot_upd_desc: int32 slots [rows] and flags [B]");
-      u.slot[i] = slot[i]->data_ptr<int>();
-      u.own[i] = own[i]->data_ptr<int>();
-    }
-  }
-  u.lr = lr.data_ptr<float>();
-  u.i64 = i64 < 0 ? 1 : i64;
-  auto host = torch::empty({(long)sizeof(DotUpd)}, torch::kUInt8);
-  std::memcpy(host.data_ptr(), &u, sizeof(DotUpd));
-  return host.to(lr.device());
-}
-
-// the fp32 interaction backward with the fused embedding update (desc from dot_upd_desc); false:
-// outside the fused kernel's domain (nothing launched)
-bool dot_bwd_upd(std::vector<torch::Tensor> zs, int64_t ldz, torch::Tensor dout, int64_t ldo,
-                 std::vector<c10::optional<torch::Tensor>> dzs, int64_t lddz, int64_t D, bool self, int64_t act0,
-                 torch::Tensor desc) {
-  TORCH_CHECK(zs.size() >= 2 && zs.size() <= 32 && dzs.size() == zs.size(), "dot_bwd_upd: 2..32 features");
-  TORCH_CHECK(dout.scalar_type() == torch::kFloat32 && desc.is_cuda() && desc.numel() == (long)sizeof(DotUpd),
-              "dot_bwd_upd: fp32 dOut and a dot_upd_desc descriptor");
-  const long B = dout.size(0);
-  const long F = (long)zs.size();
-  const long np = self ? F * (F + 1) / 2 : F * (F - 1) / 2;
-  TORCH_CHECK(dout.numel() >= (B - 1) * ldo + D + np && ldo >= D + np, "dot_bwd_upd: dOut row too small");
-  std::vector<const float*> p;
-  std::vector<float*> g;
-  for (size_t i = 0; i < zs.size(); ++i) {
-    TORCH_CHECK(zs[i].scalar_type() == torch::kFloat32 && zs[i].numel() >= (B - 1) * ldz + D, "dot_bwd_upd: fp32 inputs");
-    p.push_back(zs[i].data_ptr<float>());
-    float* d = (float*)mptr(dzs[i]);
-    if (d) TORCH_CHECK(dzs[i]->scalar_type() == torch::kFloat32 && dzs[i]->numel() >= (B - 1) * lddz + D, "dot_bwd_upd: fp32 grads");
-    g.push_back(d);
-  }
-  return fm_dot_interaction_bwd_f32_upd(p.data(), (int)F, ldz, dout.data_ptr<float>(), ldo, g.data(), lddz, B, (int)D,
-                                        self ? 1 : 0, (int)act0, desc.data_ptr(), cur()) == 0;
-}
-
-// count pass of the fused-update tables (with the forward lookups)
-void embedding_count(std::vector<torch::Tensor> idx, std::vector<int64_t> lo, std::vector<int64_t> rows,
-                     std::vector<torch::Tensor> slot, std::vector<torch::Tensor> own) {
-  const size_t n = idx.size();
-  TORCH_CHECK(lo.size() == n && rows.size() == n && slot.size() == n && own.size() == n && n > 0, "embedding_count: lists");
-  std::vector<const void*> ix;
-  std::vector<long> l;
-  std::vector<int> r, bag;
-  std::vector<int*> sl, ow;
-  const long B = idx[0].size(0);
-  const int i64 = idx[0].scalar_type() == torch::kInt64 ? 1 : 0;
-  for (size_t i = 0; i < n; ++i) {
-    TORCH_CHECK(idx[i].is_cuda() && idx[i].is_contiguous() && idx[i].size(0) == B &&
-                    (idx[i].scalar_type() == torch::kInt64) == (i64 == 1), "embedding_count: [B, bag] indices, one width");
-    TORCH_CHECK(slot[i].scalar_type() == torch::kInt32 && slot[i].numel() >= rows[i] && own[i].scalar_type() == torch::kInt32 &&
-                    own[i].numel() >= idx[i].numel(), "embedding_count: int32 slots / flags");
-    ix.push_back(idx[i].data_ptr());
-    l.push_back((long)lo[i]);
-    r.push_back((int)rows[i]);
-    bag.push_back(idx[i].dim() > 1 ? (int)idx[i].size(1) : 1);
-    sl.push_back(slot[i].data_ptr<int>());
-    ow.push_back(own[i].data_ptr<int>());
-  }
-  fm_embedding_count((int)n, ix.data(), i64, l.data(), r.data(), bag.data(), sl.data(), ow.data(), B, cur());
-}
-
 void dot_bwd(std::vector<torch::Tensor> zs, int64_t ldz, torch::Tensor dout, int64_t ldo,
              std::vector<c10::optional<torch::Tensor>> dzs, int64_t lddz, int64_t acc_mask, int64_t D, bool self,
              int64_t act0) {
@@ -1279,9 +1179,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("sdp_coalesce", &sdp_coalesce);
   m.def("sdp_apply", &sdp_apply);
   m.def("dot_fwd", &dot_fwd);
-  m.def("dot_upd_desc", &dot_upd_desc);
-  m.def("dot_bwd_upd", &dot_bwd_upd);
-  m.def("embedding_count", &embedding_count);
   m.def("dot_bwd", &dot_bwd, py::arg("zs"), py::arg("ldz"), py::arg("dout"), py::arg("ldo"), py::arg("dzs"),
         py::arg("lddz"), py::arg("acc_mask"), py::arg("D"), py::arg("self"), py::arg("act0") = 10);
   m.def("sgd", &sgd);

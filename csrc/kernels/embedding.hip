@@ -771,29 +771,6 @@ extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const
 }
 
 // single-table conveniences
-// The count pass alone (fm_emb_count_multi) for tables whose sparse-SGD update the interaction
-// backward applies (csrc/kernels/interaction.hip fm_dot_interaction_bwd_f32_upd): slot[r] = lookups
-// of row r - 1 (from -1), own[e] = 1 for the first lookup of its row.  Runs with the forward lookups
-// (indices only), off the backward's critical path.
-extern "C" void fm_embedding_count(int n, const void* const* idx, int i64, const long* lo, const int* rows,
-                                   const int* bag, int* const* slot, int* const* own, long B, hipStream_t st) {
-  for (int t0 = 0; t0 < n; t0 += MAXT) {
-    ClaimSet s{};
-    const int m = std::min(MAXT, n - t0);
-    int maxbag = 1;
-    for (int i = 0; i < m; ++i) {
-      const int k = t0 + i;
-      s.t[i] = ClaimDesc{nullptr, idx[k], nullptr, 0, lo[k], rows[k], 0, bag[k], 1.f, slot[k], own[k], nullptr};
-      maxbag = std::max(maxbag, bag[k]);
-    }
-    s.n = m;
-    const long nl = B * maxbag;
-    dim3 gc((unsigned)std::max<long>(1, std::min<long>((nl + 255) / 256, 1024)), m);
-    if (i64) hipLaunchKernelGGL((fm_emb_count_multi<true>), gc, dim3(256), 0, st, s, B);
-    else hipLaunchKernelGGL((fm_emb_count_multi<false>), gc, dim3(256), 0, st, s, B);
-  }
-}
-
 extern "C" void fm_embedding_fwd(const void* idx, int idx64, const float* W, void* out, int out_bf16, long B, int bag,
                                  int rows, int D, long ldo, float scale, hipStream_t s) {
   fm_embedding_fwd_multi(1, &W, &idx, &idx64, &out, &ldo, nullptr, &rows, &D, &bag, &scale, out_bf16, B, s);

@@ -23,35 +23,58 @@
 
 namespace {
 
+// 4 consecutive operands -> fp32 (T = float or bf16 bits), and back
+template <typename T>
+FM_DEVICE f32x4_t ld4(const T* p) {
+  if constexpr (sizeof(T) == 4) {
+    return *reinterpret_cast<const f32x4_t*>(p);
+  } else {
+    const bf16x4_t v = *reinterpret_cast<const bf16x4_t*>(p);
+    return f32x4_t{bf2f((unsigned short)v[0]), bf2f((unsigned short)v[1]), bf2f((unsigned short)v[2]),
+                   bf2f((unsigned short)v[3])};
+  }
+}
+template <typename T>
+FM_DEVICE void st4(T* p, const f32x4_t& v) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<f32x4_t*>(p) = v;
+  } else {
+    bf16x4_t o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (short)f2bf(v[e]);
+    *reinterpret_cast<bf16x4_t*>(p) = o;
+  }
+}
+
 constexpr int SK_ROWS_FWD = 32;   // rows per forward block (x rows staged in LDS)
 constexpr int SK_ROWS_DW = 64;    // rows per dW partial block
 constexpr int SK_DW_NT = 512;     // dW partial block size
 
 // x rows [m0, m0 + rows) -> LDS (rows * K floats, 16-B chunks), zero past M
-template <int K, int NT>
-FM_DEVICE void stage_x(const float* __restrict__ x, long ldx, long m0, long M, int rows, float* xs) {
+template <int K, int NT, typename T>
+FM_DEVICE void stage_x(const T* __restrict__ x, long ldx, long m0, long M, int rows, float* xs) {
   constexpr int C = K / 4;
   for (int i = threadIdx.x; i < rows * C; i += NT) {
     const int r = i / C, c = i % C;
     const long m = m0 + r;
     f32x4_t v = {0.f, 0.f, 0.f, 0.f};
-    if (m < M) v = *reinterpret_cast<const f32x4_t*>(x + m * ldx + 4 * c);
+    if (m < M) v = ld4<T>(x + m * ldx + 4 * c);
     *reinterpret_cast<f32x4_t*>(xs + r * K + 4 * c) = v;
   }
 }
 
 // forward: block = SK_ROWS_FWD rows x (4 G) columns; thread = 4 columns (weight rows in registers)
 // x (sub-row, rows sub, sub + R, ...); x rows are LDS broadcast reads, y one 16-B store per row
-template <int K>
-__global__ void __launch_bounds__(256) fm_smallk_fwd_f32(const float* __restrict__ x, long ldx, const float* __restrict__ w,
-                                                        const float* __restrict__ bias, float* __restrict__ y, long ldy,
-                                                        long M, int N, int G, int act) {
+template <int K, typename T>
+__global__ void __launch_bounds__(256) fm_smallk_fwd(const T* __restrict__ x, long ldx, const T* __restrict__ w,
+                                                    const float* __restrict__ bias, T* __restrict__ y, long ldy, long M,
+                                                    int N, int G, int act) {
   __shared__ __attribute__((aligned(16))) float xs[SK_ROWS_FWD * K];
   const int R = 256 / G;
   const int sub = threadIdx.x / G, cg = threadIdx.x % G;
   const int g = blockIdx.y * G + cg;
   const long m0 = (long)blockIdx.x * SK_ROWS_FWD;
-  stage_x<K, 256>(x, ldx, m0, M, SK_ROWS_FWD, xs);
+  stage_x<K, 256, T>(x, ldx, m0, M, SK_ROWS_FWD, xs);
   __syncthreads();
   if (sub >= R || 4 * g >= N) return;
   const int n0 = 4 * g;
@@ -60,7 +83,7 @@ __global__ void __launch_bounds__(256) fm_smallk_fwd_f32(const float* __restrict
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int k = 0; k < K; k += 4) {
-      const f32x4_t v = *reinterpret_cast<const f32x4_t*>(w + (long)(n0 + j) * K + k);
+      const f32x4_t v = ld4<T>(w + (long)(n0 + j) * K + k);
 #pragma unroll
       for (int e = 0; e < 4; ++e) wr[j][k + e] = v[e];
     }
@@ -85,7 +108,7 @@ __global__ void __launch_bounds__(256) fm_smallk_fwd_f32(const float* __restrict
       for (int k = 0; k < K; ++k) acc = fmaf(xr[k], wr[j][k], acc);
       o[j] = act_fwd(act, acc);
     }
-    *reinterpret_cast<f32x4_t*>(y + (m0 + r) * ldy + n0) = o;
+    st4<T>(y + (m0 + r) * ldy + n0, o);
   }
 }
 
@@ -93,10 +116,9 @@ __global__ void __launch_bounds__(256) fm_smallk_fwd_f32(const float* __restrict
 // [c*G, (c+1)*G) (G groups of 4 output rows n); thread = (sub-row, group) with its rows' dpre
 // loads all in flight at once; x rows come from LDS.  The R = NT/G sub-rows of a group are summed
 // through LDS into ws[p][k][j][g] (n = 4g + j, k = K: the bias)
-template <int K, int ROWS = SK_ROWS_DW>
-__global__ void __launch_bounds__(SK_DW_NT) fm_smallk_dw_part(const float* __restrict__ dpre, long ldd,
-                                                             const float* __restrict__ x, long ldx,
-                                                             float* __restrict__ ws, long M, int N, int G) {
+template <int K, typename T, int ROWS = SK_ROWS_DW>
+__global__ void __launch_bounds__(SK_DW_NT) fm_smallk_dw_part(const T* __restrict__ dpre, long ldd, const T* __restrict__ x,
+                                                             long ldx, float* __restrict__ ws, long M, int N, int G) {
   constexpr int NT = SK_DW_NT;
   constexpr int PER = 8;                          // rows per thread in flight
   __shared__ __attribute__((aligned(16))) float xs[ROWS * K];
@@ -108,7 +130,7 @@ __global__ void __launch_bounds__(SK_DW_NT) fm_smallk_dw_part(const float* __res
   const int g = blockIdx.y * G + cg;
   const bool live = sub < R && g < NG;
   const long m0 = (long)blockIdx.x * ROWS;
-  stage_x<K, NT>(x, ldx, m0, M, ROWS, xs);
+  stage_x<K, NT, T>(x, ldx, m0, M, ROWS, xs);
   __syncthreads();
   float acc[4][K + 1];
 #pragma unroll
@@ -122,7 +144,7 @@ __global__ void __launch_bounds__(SK_DW_NT) fm_smallk_dw_part(const float* __res
 #pragma unroll
       for (int u = 0; u < PER; ++u) {              // clamped row: every load unconditional
         const int r = min(r0 + u * R, rows - 1);
-        d[u] = *reinterpret_cast<const f32x4_t*>(dpre + (m0 + r) * ldd + 4 * g);
+        d[u] = ld4<T>(dpre + (m0 + r) * ldd + 4 * g);
       }
 #pragma unroll
       for (int u = 0; u < PER; ++u) {
@@ -217,19 +239,27 @@ __global__ void __launch_bounds__(256) fm_smallk_dw_reduce(const float* __restri
 
 }  // namespace
 
-// y = act(x W^T + b) for K in {4, 8, ..., 32}, N % 4 == 0, 16-B aligned rows; returns -1 (nothing
-// launched) otherwise
-extern "C" int fm_smallk_fwd_f32_launch(const float* x, long ldx, const float* w, const float* bias, float* y, long ldy,
-                                        long M, int K, int N, int act, hipStream_t s) {
+// y = act(x W^T + b) for K in {4, 8, ..., 32}, N % 4 == 0, rows aligned to 4 elements (x, w, y
+// all fp32 or all bf16: bf16 = 1); returns -1 (nothing launched) otherwise
+extern "C" int fm_smallk_fwd_launch(const void* x, long ldx, const void* w, const float* bias, void* y, long ldy, long M,
+                                    int K, int N, int act, int bf16, hipStream_t s) {
   if (M <= 0) return 0;
+  const uintptr_t amask = bf16 ? 7 : 15;
   if (K % 4 || K < 4 || K > 32 || N % 4 || N < 4 || ldx % 4 || ldy % 4 ||
-      (((uintptr_t)x | (uintptr_t)w | (uintptr_t)y) & 15))
+      (((uintptr_t)x | (uintptr_t)w | (uintptr_t)y) & amask))
     return -1;
   const int NG = N / 4;
   const int G = NG < 64 ? NG : 64;
   const dim3 grid((unsigned)((M + SK_ROWS_FWD - 1) / SK_ROWS_FWD), (unsigned)((NG + G - 1) / G));
-#define FM_SK(KK) \
-  case KK: hipLaunchKernelGGL(fm_smallk_fwd_f32<KK>, grid, dim3(256), 0, s, x, ldx, w, bias, y, ldy, M, N, G, act); break;
+#define FM_SK(KK)                                                                                                 \
+  case KK:                                                                                                        \
+    if (bf16)                                                                                                     \
+      hipLaunchKernelGGL((fm_smallk_fwd<KK, unsigned short>), grid, dim3(256), 0, s, (const unsigned short*)x, ldx,  \
+                         (const unsigned short*)w, bias, (unsigned short*)y, ldy, M, N, G, act);                 \
+    else                                                                                                          \
+      hipLaunchKernelGGL((fm_smallk_fwd<KK, float>), grid, dim3(256), 0, s, (const float*)x, ldx, (const float*)w, bias, \
+                         (float*)y, ldy, M, N, G, act);                                                           \
+    break;
   switch (K) {
     FM_SK(4) FM_SK(8) FM_SK(12) FM_SK(16) FM_SK(20) FM_SK(24) FM_SK(28) FM_SK(32)
   }
@@ -240,11 +270,12 @@ extern "C" int fm_smallk_fwd_f32_launch(const float* x, long ldx, const float* w
 // dW[N][K] += dpre^T x, db[N] += colsum(dpre) (db may be null); with lr the SGD step is applied to
 // the weight dw = W instead (V / Wc optional).  ws: (K + 1) * N * ceil(M / 64) floats; returns -1
 // (nothing launched) outside the shape limits of the forward or with too small a workspace.
-extern "C" int fm_smallk_dw_f32_launch(const float* dpre, long ldd, const float* x, long ldx, float* dw, float* db, long M,
-                                       int K, int N, float* ws, long ws_bytes, float* V, unsigned short* Wc,
-                                       const float* lr, float wd, float mom, int nesterov, hipStream_t s) {
+extern "C" int fm_smallk_dw_launch(const void* dpre, long ldd, const void* x, long ldx, float* dw, float* db, long M, int K,
+                                   int N, float* ws, long ws_bytes, float* V, unsigned short* Wc, const float* lr, float wd,
+                                   float mom, int nesterov, int bf16, hipStream_t s) {
   if (M <= 0) return 0;
-  if (K % 4 || K < 4 || K > 32 || N % 4 || N < 4 || ldd % 4 || ldx % 4 || (((uintptr_t)dpre | (uintptr_t)x) & 15))
+  const uintptr_t amask = bf16 ? 7 : 15;
+  if (K % 4 || K < 4 || K > 32 || N % 4 || N < 4 || ldd % 4 || ldx % 4 || (((uintptr_t)dpre | (uintptr_t)x) & amask))
     return -1;
   const int NG = N / 4;
   const int G = NG < 64 ? NG : 64;               // column groups per block
@@ -255,9 +286,14 @@ extern "C" int fm_smallk_dw_f32_launch(const float* dpre, long ldd, const float*
   const long per = (long)(K + 1) * N;
   if (P * per * 4 > ws_bytes || P > (1L << 30)) return -1;
   const dim3 grid((unsigned)P, (unsigned)((NG + G - 1) / G));
-#define FM_SD(KK)                                                                                            \
-  case KK:                                                                                                   \
-    hipLaunchKernelGGL((fm_smallk_dw_part<KK>), grid, dim3(SK_DW_NT), 0, s, dpre, ldd, x, ldx, ws, M, N, G); \
+#define FM_SD(KK)                                                                                              \
+  case KK:                                                                                                     \
+    if (bf16)                                                                                                  \
+      hipLaunchKernelGGL((fm_smallk_dw_part<KK, unsigned short>), grid, dim3(SK_DW_NT), 0, s,                  \
+                         (const unsigned short*)dpre, ldd, (const unsigned short*)x, ldx, ws, M, N, G);         \
+    else                                                                                                       \
+      hipLaunchKernelGGL((fm_smallk_dw_part<KK, float>), grid, dim3(SK_DW_NT), 0, s, (const float*)dpre, ldd,  \
+                         (const float*)x, ldx, ws, M, N, G);                                                    \
     break;
   switch (K) {
     FM_SD(4) FM_SD(8) FM_SD(12) FM_SD(16) FM_SD(20) FM_SD(24) FM_SD(28) FM_SD(32)

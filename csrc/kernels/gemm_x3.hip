@@ -44,7 +44,10 @@ constexpr int XK = 32;   // k per stage
 FM_DEVICE int x3_off(int r, int c) { return r * 64 + 16 * (c ^ ((r >> 1) & 3)); }
 
 // exact truncation split of one fp32 value: x = h + m + l, each a bf16 (returned as fp32 bits
-// with zero low halves)
+// with zero low halves).  A non-finite x gives m = l = NaN (x - h is inf - inf or NaN), so a GEMM
+// with an inf operand returns NaN where the native fp32 kernel returns +-inf: documented, pinned by
+// tests/test_gpu_fp32_split.py::test_split_nonfinite_operand (no per-element select in the staging
+// pass, which is the kernel's VALU budget)
 FM_DEVICE void split1(float x, unsigned& h, unsigned& m, unsigned& l) {
   h = __float_as_uint(x) & 0xffff0000u;
   const float r = x - __uint_as_float(h);

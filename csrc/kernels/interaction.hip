@@ -11,7 +11,6 @@
 //   columns via the transposing ds_read_b64_tr_b16);
 //   dZ_0 += dOut[:, :D].  Inputs/grads are pointer tables, so it also reads/writes concat slices.
 #include "common.h"
-#include "dot_upd.h"
 
 #include <cstdlib>
 
@@ -642,29 +641,13 @@ __global__ void __launch_bounds__(256, 2) fm_dot_fwd_f32s(ZT Z, long ldz, float*
 // whole 32E-column rows.  No Z staging in LDS (only the dOut row, for the per-lane S gather),
 // so a wave keeps the NEXT sample's Z rows and dOut chunks in flight in registers while this
 // sample's (F+1)/2 x E MFMAs run.  Steps past F are skipped (uniform), not padded to 32.
-// Embedding sparse-SGD update fused into the interaction backward (UPD): for the features whose
-// producer is an embedding table looked up once per sample (bag 1) and trained with sparse SGD,
-// the kernel applies W[idx[b]] -= lr * scale * dZ[b] itself instead of writing dZ for the table's
-// backward kernels to read back (DLRM MLPerf fp32: 16 + 4 of 26 tables, 2 x 84 MB of dZ traffic
-// and the claim / dup / owner launches).  Rows that a count pass (csrc/kernels/embedding.hip
-// fm_emb_count_multi, run with the forward lookups) found hit once take a plain 16-B
-// read-modify-write, repeated rows float atomics; slot-less tables always use atomics.  The first
-// lookup of a repeated row frees its slot (-1), so the exclusive path never sees a repeated row.
-// Reference: the embedding's sparse update reads the concat/interaction gradient back from memory
-// (src/ops/embedding.cu:199-224, src/ops/concat.cu:263-317).
-typedef __attribute__((address_space(1))) const void* gptr_i;
-typedef __attribute__((address_space(3))) void* lptr_i;
-
-
-
 template <int E> struct VecF { using type = float __attribute__((ext_vector_type(E))); };
 template <> struct VecF<1> { using type = float; };
 
-// UPD runs one block per CU: the update's extra state does not fit the 256-VGPR budget of two
-template <int E, int NKS, bool ACC, typename ZT = PtrTabF, bool UPD = false>
-__global__ void __launch_bounds__(256, UPD ? 1 : 2) fm_dot_bwd_f32r(ZT Z, long ldz, const float* __restrict__ dout, long ldo,
+template <int E, int NKS, bool ACC, typename ZT = PtrTabF>
+__global__ void __launch_bounds__(256, 2) fm_dot_bwd_f32r(ZT Z, long ldz, const float* __restrict__ dout, long ldo,
                                                          MPtrTabF dZ, long lddz, unsigned acc_mask, long B, int F,
-                                                         int W, int self, int act0, const DotUpd* __restrict__ U) {
+                                                         int W, int self, int act0) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int D = 32 * E;
   constexpr int DCH = 4;                           // dOut float4 chunks per lane (W <= 1024)
@@ -672,8 +655,6 @@ __global__ void __launch_bounds__(256, UPD ? 1 : 2) fm_dot_bwd_f32r(ZT Z, long l
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wpad = (W + 3) & ~3;
   float* ds = reinterpret_cast<float*>(smem) + (long)wave * wpad;
-  // UPD: the wave's staged table rows, [F][D] floats after every wave's dOut row
-  float* wst = reinterpret_cast<float*>(smem) + (long)(blockDim.x >> 6) * wpad + (long)wave * MAXF * D;
   const int waves_total = gridDim.x * (blockDim.x >> 6);
   const int r = lane & 31, h = lane >> 5;
   // A operand positions: S[r][j = 2ks + h]; j >= F -> 0 (the B row loaded for it is row F-1)
@@ -712,21 +693,11 @@ __global__ void __launch_bounds__(256, UPD ? 1 : 2) fm_dot_bwd_f32r(ZT Z, long l
     }
   };
   const long b_first = blockIdx.x * (blockDim.x >> 6) + wave;
-  // UPD: lane j < F holds feature j's lookup index of the current sample (ix) and, loaded at the
-  // top of each sample, its row slot (sl) and first-arrival flag (ow)
-  const int fj = lane < F ? lane : 0;
-  const bool jupd = UPD && lane < F && U->W[fj] != nullptr;
-  auto load_ix = [&](long bb) -> long {
-    if (!jupd) return 0;
-    return U->i64 ? (long)reinterpret_cast<const long long*>(U->idx[fj])[bb] : (long)reinterpret_cast<const int*>(U->idx[fj])[bb];
-  };
-  long ix = 0;
   {
     const long b0 = min(b_first, B - 1);
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) load_row(b0, ks);
     load_dout(b0);
-    if constexpr (UPD) ix = load_ix(b0);
   }
   for (long b = b_first; b < B; b += waves_total) {
     const long bn = min(b + waves_total, B - 1);
@@ -737,43 +708,6 @@ __global__ void __launch_bounds__(256, UPD ? 1 : 2) fm_dot_bwd_f32r(ZT Z, long l
     }
     FM_WAVE_LDS_SYNC();
     load_dout(bn);
-    // UPD: this sample's slot / flag, and the table rows it updates staged into the wave's LDS
-    // rows by LDS-DMA (global_load_lds: no registers held while the MFMAs run), two 512-B rows
-    // per wave-instruction (D = 128): lanes 0-31 row 2p, lanes 32-63 row 2p + 1
-    int sl = -1, ow = 0;
-    long ixn = 0;
-    unsigned fmask = 0, xmask = 0;
-    float mulj = 0.f;
-    if constexpr (UPD) {
-      ixn = load_ix(bn);
-      if (jupd) {
-        const long rl = ix - U->lo[fj];
-        const bool in = (unsigned long)rl < (unsigned long)U->rows[fj];
-        if (U->slot[fj] != nullptr && in) {
-          sl = __hip_atomic_load(U->slot[fj] + rl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ow = U->own[fj][b];
-        }
-      }
-      static_assert(!UPD || D == 128, "the fused update stages 512-B rows");
-      // wave-uniform masks over the features: fused (updated here) and exclusive (hit once: plain
-      // store of the updated row); lane j's learning-rate multiplier for feature j
-      {
-        const long rl = ix - U->lo[fj];
-        const bool in = jupd && (unsigned long)rl < (unsigned long)U->rows[fj];
-        fmask = (unsigned)__ballot(jupd);
-        xmask = (unsigned)__ballot(in && U->slot[fj] != nullptr && sl == 0);
-        mulj = jupd ? -U->lr[0] * U->scale[fj] : 0.f;
-      }
-      for (int pr = 0; 2 * pr < F; ++pr) {
-        const int f = 2 * pr + h;
-        const int fc = f < F ? f : 0;
-        const long ri = __shfl(ix, fc, 64) - U->lo[fc];
-        const bool ok = f < F && U->W[fc] != nullptr && (unsigned long)ri < (unsigned long)U->rows[fc];
-        // rows not updated read a valid dummy address (dOut's row) so the DMA is unconditional
-        const float* src = ok ? U->W[fc] + ri * D + 4 * r : dout + 4 * r;
-        __builtin_amdgcn_global_load_lds((gptr_i)(const void*)src, (lptr_i)(void*)(wst + pr * 2 * D), 16, 0, 0);
-      }
-    }
     const float* dp = ds + D;
     float a[NKS];
 #pragma unroll
@@ -803,7 +737,6 @@ __global__ void __launch_bounds__(256, UPD ? 1 : 2) fm_dot_bwd_f32r(ZT Z, long l
       load_row(bn, ks);
       __builtin_amdgcn_sched_barrier(0);
     }
-    if constexpr (UPD) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the staged rows have landed
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
       const int i0 = (t & 3) + 8 * (t >> 2);
@@ -830,18 +763,6 @@ __global__ void __launch_bounds__(256, UPD ? 1 : 2) fm_dot_bwd_f32r(ZT Z, long l
           }
         }
       }
-      if constexpr (UPD) {
-        // fused rows go to the wave's LDS row: the new row value for a row hit once (its staged
-        // old value + mul * dZ), else mul * dZ for the atomics; written out after the loop
-        // every lane takes part in the shuffle (a lane reading an inactive lane gets garbage)
-        const float mul = __shfl(mulj, i & 31, 64);
-        if ((fmask >> (i & 31)) & 1u) {
-          vecE* lp = reinterpret_cast<vecE*>(wst + i * D + E * r);
-          if ((xmask >> i) & 1u) *lp = *lp + mul * v;
-          else *lp = mul * v;
-          continue;
-        }
-      }
       if (i < F && q != nullptr) {
         float* d = q + b * lddz + E * r;
         if constexpr (ACC) {
@@ -849,33 +770,6 @@ __global__ void __launch_bounds__(256, UPD ? 1 : 2) fm_dot_bwd_f32r(ZT Z, long l
         }
         *reinterpret_cast<vecE*>(d) = v;
       }
-    }
-    if constexpr (UPD) {
-      // write the fused rows out: one row per half-wave per iteration (lane r: its E columns)
-      __builtin_amdgcn_s_waitcnt(0x0F70);
-      FM_WAVE_LDS_SYNC();
-      for (int f0 = 0; f0 < F; f0 += 2) {
-        const int f = f0 + h < F ? f0 + h : f0;
-        // shuffles first, with every lane active (an inactive source lane reads as garbage)
-        const long ri = __shfl(ix, f, 64) - U->lo[f];
-        const int c = __shfl(sl, f, 64), o = __shfl(ow, f, 64);
-        if (f0 + h >= F || !((fmask >> f) & 1u)) continue;  // uniform across the half-wave
-        if ((unsigned long)ri >= (unsigned long)U->rows[f]) continue;
-        float* wp = U->W[f] + ri * D + E * r;
-        const vecE val = *reinterpret_cast<const vecE*>(wst + f * D + E * r);
-        if ((xmask >> f) & 1u) {
-          *reinterpret_cast<vecE*>(wp) = val;             // the row's only lookup: plain store
-        } else {                                          // repeated row / no slots: atomics
-          if constexpr (E == 1) atomicAdd(wp, val);
-          else {
-#pragma unroll
-            for (int e = 0; e < E; ++e) atomicAdd(wp + e, val[e]);
-          }
-        }
-        if (U->slot[f] != nullptr && r == 0 && (c == 0 || o))
-          __hip_atomic_store(U->slot[f] + ri, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      ix = ixn;
     }
     FM_WAVE_LDS_SYNC();
   }
@@ -954,7 +848,7 @@ extern "C" void fm_dot_interaction_bwd_f32(const float* const* z, int F, long ld
              : E == 2 ? (acc ? fm_dot_bwd_f32r<2, 16, true> : fm_dot_bwd_f32r<2, 16, false>)
                       : (acc ? fm_dot_bwd_f32r<1, 16, true> : fm_dot_bwd_f32r<1, 16, false>);
       hipLaunchKernelGGL(k, dim3((int)blocks), dim3(64 * waves), (size_t)waves * wpad * 4, s, t, ldz, dout, ldo, g, lddz,
-                         acc_mask, B, F, W, self, act0, nullptr);
+                         acc_mask, B, F, W, self, act0);
       return;
     }
   }
@@ -1009,41 +903,4 @@ extern "C" void fm_dot_interaction_bwd(const void* const* z, int F, long ldz, co
   size_t lds = waves * (32 * Dp * 2 + 32 * 32 * 2);
   hipLaunchKernelGGL(fm_dot_bwd, dim3((int)blocks), dim3(64 * waves), lds, s, t, ldz, (const unsigned short*)dout, ldo,
                      g, lddz, acc_mask, B, F, D, self);
-}
-
-// The fp32 interaction backward with the embedding sparse-SGD update fused (dot_upd.h DotUpd, in
-// device memory): W[i] / idx[i] / slot[i] / own[i] per feature (W[i] == nullptr: dZ[i] written as
-// usual), lr the device learning rate.  Returns -1 (nothing launched) outside the fused kernel's domain: D = 128, no
-// gradient accumulation, 16-B rows.
-extern "C" int fm_dot_interaction_bwd_f32_upd(const float* const* z, int F, long ldz, const float* dout, long ldo,
-                                              float* const* dz, long lddz, long B, int D, int self, int act0,
-                                              const void* desc, hipStream_t s) {
-  if (F > MAXF || F < 2 || D != 128 || desc == nullptr) return -1;
-  const int npairs = self ? F * (F + 1) / 2 : F * (F - 1) / 2;
-  const int W = D + npairs;
-  if (ldo % 4 || !al16(dout) || W > 1024 || ldz % 4 || lddz % 4) return -1;
-  PtrTabF t;
-  MPtrTabF g;
-  for (int i = 0; i < MAXF; ++i) {
-    t.p[i] = i < F ? z[i] : nullptr;
-    g.p[i] = i < F ? dz[i] : nullptr;
-  }
-  for (int i = 0; i < F; ++i)
-    if (!al16(z[i]) || (dz[i] != nullptr && !al16(dz[i]))) return -1;
-  const int waves = 4;
-  const long blocks = std::min<long>((B + waves - 1) / waves, 256L);   // one block per CU
-  const int wpad = (W + 3) & ~3;
-  auto k = (F + 1) / 2 == 14 ? fm_dot_bwd_f32r<4, 14, false, PtrTabF, true> : fm_dot_bwd_f32r<4, 16, false, PtrTabF, true>;
-  const size_t lds = (size_t)waves * (wpad + MAXF * D) * 4;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)fm_dot_bwd_f32r<4, 14, false, PtrTabF, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10);
-    (void)hipFuncSetAttribute((const void*)fm_dot_bwd_f32r<4, 16, false, PtrTabF, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10);
-    attr = true;
-  }
-  hipLaunchKernelGGL(k, dim3((int)blocks), dim3(64 * waves), lds, s, t, ldz, dout, ldo, g, lddz, 0u, B, F, W, self, act0,
-                     static_cast<const DotUpd*>(desc));
-  return 0;
 }

@@ -317,16 +317,6 @@ def dot_interaction_backward(inputs, dy, in_grads, accs, self_inter, act0=10):
                 int(act0))
 
 
-def dot_interaction_backward_upd(inputs, dy, in_grads, self_inter, act0, desc):
-    """fp32 interaction backward with the embedding sparse-SGD updates of the features described
-    by ``desc`` (C().dot_upd_desc) applied in the kernel; their dZ is not written.  False: not
-    launched (outside the fused kernel's domain)."""
-    D = inputs[0].shape[-1]
-    ld = next((g.stride(0) for g in in_grads if g is not None), D)
-    return bool(C().dot_bwd_upd(list(inputs), inputs[0].stride(0), dy, dy.stride(0), list(in_grads), ld, D,
-                                bool(self_inter), int(act0), desc))
-
-
 # ------------------------------------------------------------------ optimizers / loss
 def sgd_update(master, grad, v, compute, lr_tensor, wd, momentum, nesterov, zero_grad=False):
     """zero_grad: the kernel writes the consumed gradient back as zeros (no separate memset)."""

@@ -212,8 +212,6 @@ class Embedding(Op):
             out.copy_(r)
 
     def backward(self, ctx: OpCtx):
-        if ctx.saved.get("dot_upd"):
-            return            # updated by its interaction's backward (Executor._build_dot_update_fusion)
         idx = ctx.inputs[0]
         dy = ctx.out_grads[0]
         if self.sparse_sgd:
@@ -268,13 +266,6 @@ class Embedding(Op):
                                   [1.0 / c.inputs[0].shape[1] if op.aggr == AggrMode.AGGR_MODE_AVG else 1.0
                                    for op, c in zip(ops, ctxs)],
                                   [Embedding._row_lo(c) for c in ctxs])
-        # count pass of the tables whose update the interaction backward applies
-        # (Executor._build_dot_update_fusion): indices only, here beside the lookups
-        cnt = [(op, c) for op, c in zip(ops, ctxs) if c.saved.get("dot_upd") == "count"]
-        if cnt:
-            K.C().embedding_count([c.inputs[0] for _, c in cnt], [Embedding._row_lo(c) for _, c in cnt],
-                                  [c.weights[0].shape[0] for _, c in cnt],
-                                  [op._claim_buffers(c)[0] for op, c in cnt], [op._claim_buffers(c)[1] for op, c in cnt])
 
     @staticmethod
     def backward_group(ops, ctxs):
@@ -282,12 +273,6 @@ class Embedding(Op):
             for op, c in zip(ops, ctxs):
                 op.backward(c)
             return
-        # tables updated by their interaction's backward (Executor._build_dot_update_fusion)
-        keep = [k for k, c in enumerate(ctxs) if not c.saved.get("dot_upd")]
-        if not keep:
-            return
-        if len(keep) < len(ctxs):
-            ops, ctxs = [ops[k] for k in keep], [ctxs[k] for k in keep]
         scales = [1.0 / c.inputs[0].shape[1] if op.aggr == AggrMode.AGGR_MODE_AVG else 1.0 for op, c in zip(ops, ctxs)]
         if ops[0].sparse_sgd:
             tables = [c.weights[0] for c in ctxs]

@@ -202,13 +202,6 @@ class DotInteraction(Op):
     def backward(self, ctx: OpCtx):
         dy = ctx.out_grads[0]
         if ctx.hip:
-            desc = ctx.saved.get("upd_desc")
-            if desc is not None:
-                # the embedding tables' sparse SGD fused in (Executor._build_dot_update_fusion)
-                ok = K.dot_interaction_backward_upd(list(ctx.inputs), dy, list(ctx.in_grads), self.self_interaction,
-                                                    ctx.saved.get("act0", 10), desc)
-                assert ok, f"{self.name}: fused interaction backward + embedding update did not launch"
-                return
             K.dot_interaction_backward(list(ctx.inputs), dy, list(ctx.in_grads),
                                        list(ctx.in_grad_accumulate), self.self_interaction,
                                        ctx.saved.get("act0", 10))

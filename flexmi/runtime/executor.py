@@ -902,7 +902,6 @@ class Executor:
         self._build_binary_relu_fusion(ops)
         self._build_conv_chain_fusion(ops)
         self._build_interaction_act_fusion(ops)
-        self._build_dot_update_fusion(ops)
         self.adam_state = torch.tensor([1.0, 1.0, 0.0], dtype=torch.float32, device=self.device)
         self._compile_program()
 
@@ -983,62 +982,6 @@ class Executor:
                 continue
             cd.saved["act0"] = int(op.activation)
             c1.saved["grad_is_dpre"] = True
-
-    def _build_dot_update_fusion(self, ops):
-        """Embedding E -> DotInteraction D input i (bag-1 fp32 [rows, 128] table trained with sparse
-        SGD, E's output consumed only by D, in D's layout): D's backward applies E's update
-        W[idx] -= lr * dZ_i itself (csrc/kernels/interaction.hip fm_dot_interaction_bwd_f32_upd) and
-        never writes dZ_i; E's backward skips the table.  Tables with owner-computes buffers
-        (Embedding._claim_buffers) get their count pass with the forward lookups (rows hit once:
-        plain store, repeated rows: atomics), the other non-tiny tables take atomics; tiny tables
-        keep their LDS-privatised backward kernel.  Reference: the table update reads the
-        interaction/concat gradient back from memory (src/ops/embedding.cu:199-224).  Off with
-        FM_EMB_DOT_UPD=0, under --debug and for micro-batch-pipelined tails."""
-        from flexmi.core.types import AggrMode, OperatorType
-        from flexmi.ops.embedding import Embedding
-        if (self.backend != "hip" or self.debug or self.cfg.compute_dtype != "fp32" or XCHG_LOCAL
-                or getattr(self, "pipe", None) is not None or os.environ.get("FM_EMB_DOT_UPD", "1") == "0"):
-            return
-        for d in ops:
-            if d.op_type != OperatorType.OP_DOT_INTERACTION:
-                continue
-            cd = self.ctx.get(d.guid)
-            if cd is None or cd.empty or d.guid in self.group_of or cd.outputs[0] is None or d.d != 128:
-                continue
-            if cd.outputs[0].dtype != torch.float32 or len(d.inputs) > 32:
-                continue
-            spec = [None] * len(d.inputs)
-            for i, t in enumerate(d.inputs):
-                e = t.owner_op
-                if i == 0 or e is None or e.op_type != OperatorType.OP_EMBEDDING or not e.sparse_sgd:
-                    continue
-                if getattr(e, "host_exec", False) or getattr(e, "sparse_dp", None):
-                    continue
-                ce = self.ctx.get(e.guid)
-                cons = self.consumers.get(t.guid, [])
-                if ce is None or ce.empty or len(cons) != 1 or t is self.final or cd.inputs[i] is not ce.outputs[0]:
-                    continue
-                idx, w = ce.inputs[0], ce.weights[0]
-                if (idx is None or w is None or idx.dim() != 2 or idx.shape[1] != 1 or not idx.is_contiguous()
-                        or w.dtype != torch.float32 or w.dim() != 2 or w.shape[1] != 128 or not w.is_contiguous()
-                        or idx.shape[0] != cd.outputs[0].shape[0] or w.shape[0] <= Embedding.TINY_ROWS):
-                    continue
-                claim = e._claim_buffers(ce)
-                scale = 1.0 / idx.shape[1] if e.aggr == AggrMode.AGGR_MODE_AVG else 1.0
-                spec[i] = (e, ce, claim, scale)
-            if not any(spec):
-                continue
-            from flexmi.ops import _kernels as K
-            desc = K.C().dot_upd_desc([None if s_ is None else s_[1].weights[0] for s_ in spec],
-                                      [None if s_ is None else s_[1].inputs[0] for s_ in spec],
-                                      [None if s_ is None or s_[2] is None else s_[2][0] for s_ in spec],
-                                      [None if s_ is None or s_[2] is None else s_[2][1] for s_ in spec],
-                                      [0 if s_ is None else Embedding._row_lo(s_[1]) for s_ in spec],
-                                      [1.0 if s_ is None else s_[3] for s_ in spec], self.lr_tensor)
-            cd.saved["upd_desc"] = desc
-            for s_ in spec:
-                if s_ is not None:
-                    s_[1].saved["dot_upd"] = "count" if s_[2] is not None else "atomic"
 
     def _build_binary_relu_fusion(self, ops):
         """ElementBinary A -> ReLU B (A's output consumed only by B, same layout, B's input gradient

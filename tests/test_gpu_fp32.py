@@ -559,6 +559,27 @@ def test_smallk_dw(gpu, M, K, N):
     assert torch.equal(dw2, dw) and torch.equal(db2, db)          # fixed summation order
 
 
+@pytest.mark.parametrize("M,K,N", [(8192, 16, 512), (1000, 4, 12), (77, 8, 4)])
+def test_smallk_bf16(gpu, M, K, N):
+    """The bf16 forms (bf16 x / w / y and dpre, fp32 accumulate and dW): against float64 of the same
+    bf16 values."""
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(14)
+    x = torch.randn(M, K, device=gpu).bfloat16()
+    w = torch.randn(N, K, device=gpu).bfloat16()
+    b = torch.randn(N, device=gpu)
+    y = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    assert Kk.C().smallk_fwd(x, w, b, y, 11)
+    ref = (x.double() @ w.double().t() + b.double()).clamp_min(0)
+    assert rel_err(y, ref) < 1e-2
+    dpre = torch.randn(M, N, device=gpu).bfloat16()
+    dw, db = torch.zeros(N, K, device=gpu), torch.zeros(N, device=gpu)
+    ws = Kk.workspace(gpu, Kk.GEMM_WS_BYTES)
+    assert Kk.C().smallk_dw(dpre, x, dw, db, ws, None, None, None, 0.0, 0.0, False)
+    assert rel_err(dw, dpre.double().t() @ x.double()) < 1e-5
+    assert rel_err(db, dpre.double().sum(0)) < 1e-5
+
+
 @pytest.mark.parametrize("mom,nesterov,mirror", [(0.0, False, False), (0.9, False, True), (0.9, True, False)])
 def test_smallk_dw_fused_sgd(gpu, mom, nesterov, mirror):
     """The SGD step applied in the dW reduce == gradient + optim.hip SGD kernel."""

@@ -158,3 +158,25 @@ def test_split2_dw_fused_sgd(gpu, mom, nesterov, Nout, Kin):
     assert ks >= 1
     assert rel_err(w, w_ref) < TOL
     assert rel_err(db, dpre.double().sum(0)) < TOL
+
+
+def test_split_nonfinite_operand(gpu):
+    """Documented behaviour of the exact split (csrc/kernels/gemm_x3.hip split1): an inf operand turns
+    the rows / columns it reaches into NaN (the native fp32 kernel gives inf); finite entries are
+    unaffected."""
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(21)
+    M = N = K = 512
+    A, B = torch.randn(M, K, device=gpu), torch.randn(K, N, device=gpu)
+    A[3, 7] = float("inf")
+    C = torch.empty(M, N, device=gpu)
+    Kk.C().gemm_f32_set_split(2)
+    try:
+        Kk.gemm(A, K, True, B.t().contiguous(), K, True, C, N, M, N, K)
+    finally:
+        Kk.C().gemm_f32_set_split(3)
+    assert torch.isnan(C[3]).all()
+    mask = torch.ones(M, dtype=torch.bool, device=gpu)
+    mask[3] = False
+    ref = A[mask].double() @ B.double()
+    assert rel_err(C[mask], ref) < TOL
