@@ -21,6 +21,29 @@ FM_DEVICE unsigned short f2bf(float f) {
   return *reinterpret_cast<unsigned short*>(&b);
 }
 
+// Exact three-way bf16 split of two fp32 values x = h + m + l (truncation: h = x with the low 16
+// bits cleared, r = x - h exact, m = r truncated, l = r - m: <= 8 significant bits, already a bf16),
+// returned as one packed bf16 pair per plane (a in the low half).  9 VALU per pair: one v_perm_b32
+// per plane packs the high halves (truncation needs no mask there), each residual subtraction is
+// one v_pk_add_f32, only the fp32 images of h and m need masks.  The per-element form (mask every
+// term, shift/or packing) compiled to 26 VALU per pair with SDWA ors and moves into the ds_write
+// quads.  A non-finite x gives m = l = NaN (inf - inf): the split GEMMs document it.
+FM_DEVICE unsigned fm_hi_pair(unsigned a, unsigned b) { return __builtin_amdgcn_perm(b, a, 0x07060302u); }
+
+FM_DEVICE void fm_split3_pair(float a, float b, unsigned& h, unsigned& m, unsigned& l) {
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  const unsigned ua = __float_as_uint(a), ub = __float_as_uint(b);
+  h = fm_hi_pair(ua, ub);
+  const f2_t x = {a, b};
+  const f2_t hf = {__uint_as_float(ua & 0xffff0000u), __uint_as_float(ub & 0xffff0000u)};
+  const f2_t r = x - hf;
+  const unsigned ra = __float_as_uint(r.x), rb = __float_as_uint(r.y);
+  m = fm_hi_pair(ra, rb);
+  const f2_t mf = {__uint_as_float(ra & 0xffff0000u), __uint_as_float(rb & 0xffff0000u)};
+  const f2_t lf = r - mf;
+  l = fm_hi_pair(__float_as_uint(lf.x), __float_as_uint(lf.y));
+}
+
 // value conversion generic over float / bf16 storage (tof: storage -> f32, fromf<T>: f32 -> storage)
 FM_DEVICE float tof(float v) { return v; }
 FM_DEVICE float tof(unsigned short v) { return bf2f(v); }

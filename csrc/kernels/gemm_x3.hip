@@ -43,27 +43,12 @@ constexpr int XK = 32;   // k per stage
 // (r >> 1) & 3 makes the 16x16x32 fragment reads (lane = 16 rows x 4 chunks) conflict-free
 FM_DEVICE int x3_off(int r, int c) { return r * 64 + 16 * (c ^ ((r >> 1) & 3)); }
 
-// exact truncation split of one fp32 value: x = h + m + l, each a bf16 (returned as fp32 bits
-// with zero low halves).  A non-finite x gives m = l = NaN (x - h is inf - inf or NaN), so a GEMM
-// with an inf operand returns NaN where the native fp32 kernel returns +-inf: documented, pinned by
-// tests/test_gpu_fp32_split.py::test_split_nonfinite_operand (no per-element select in the staging
-// pass, which is the kernel's VALU budget)
-FM_DEVICE void split1(float x, unsigned& h, unsigned& m, unsigned& l) {
-  h = __float_as_uint(x) & 0xffff0000u;
-  const float r = x - __uint_as_float(h);
-  m = __float_as_uint(r) & 0xffff0000u;
-  l = __float_as_uint(r - __uint_as_float(m)) & 0xffff0000u;
-}
-
-// two fp32 -> one packed bf16 pair per plane (element a in the low half)
-FM_DEVICE void split2(float a, float b, unsigned& h, unsigned& m, unsigned& l) {
-  unsigned ha, ma, la, hb, mb, lb;
-  split1(a, ha, ma, la);
-  split1(b, hb, mb, lb);
-  h = (ha >> 16) | hb;
-  m = (ma >> 16) | mb;
-  l = (la >> 16) | lb;
-}
+// the exact split of fp32 pairs into three bf16 planes: fm_split3_pair (common.h).  A non-finite
+// operand gives m = l = NaN, so a GEMM with an inf operand returns NaN where the native fp32 kernel
+// returns +-inf: documented, pinned by tests/test_gpu_fp32_split.py::test_split_nonfinite_operand
+// (no per-element select in the staging pass, which is the kernel's VALU budget).  The 9-VALU
+// packed form cut the 256x128 main loop from 3.4 to 2.4 VALU per MFMA (static count, no register
+// moves left) and the DLRM step's split GEMMs 609.8 -> 599.9 us (profiles/x3_phase_lab_r6.txt).
 
 // One operand's k step (R rows x 32 k) staged through registers; unit = (row, k-octet): the 8 k
 // values of one row, split and written as one 16-B chunk per plane.  K-contiguous: two 16-B loads
@@ -128,7 +113,7 @@ struct X3Stage {
       for (int u = 0; u < 4; ++u) {
         const f32x4_t& v = u < 2 ? a[i] : b[i];
         unsigned hh, mm, ll;
-        split2(v[2 * (u & 1)], v[2 * (u & 1) + 1], hh, mm, ll);
+        fm_split3_pair(v[2 * (u & 1)], v[2 * (u & 1) + 1], hh, mm, ll);
         h[u] = hh;
         m[u] = mm;
         l[u] = ll;
@@ -213,7 +198,9 @@ __global__ void __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) fm_gemm_x3v2_ke
       for (int j = 0; j < NR; ++j)
         bf[pl][j] = *reinterpret_cast<const bf16x8_t*>(lb + pl * PB_ + x3_off(wn * 64 + 16 * j + q, g));
   };
-  // MFMAs of one step, A fragments read per tile row (NR independent accumulator chains per term)
+  // MFMAs of one step, A fragments read per tile row (NR independent accumulator chains per term);
+  // reading row i + 1 ahead of row i's MFMAs, or the fragments in first-use order, measured the same
+  // (profiles/x3_phase_lab_r6.txt)
   auto mfma_rows = [&](const char* la, const bf16x8_t (&bf)[3][NR]) {
 #pragma unroll
     for (int i = 0; i < MR; ++i) {

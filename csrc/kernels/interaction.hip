@@ -537,18 +537,6 @@ __global__ void __launch_bounds__(256) fm_dot_bwd_f32(PtrTabF Z, long ldz, const
 // per lane), stages the sample's Z (F <= 32 rows) in a per-wave LDS tile padded to D + 4 floats a
 // row (the row-per-lane ds_read_b128 of the MFMA operands is then bank-conflict free), and keeps
 // the NEXT sample's rows in flight in registers while this sample's MFMAs and stores run.
-// exact truncation split of two fp32 values into three packed bf16 pairs (as gemm_x3.hip split2)
-FM_DEVICE void dot_split2(float a, float b, unsigned& h, unsigned& m, unsigned& l) {
-  const unsigned ha = __float_as_uint(a) & 0xffff0000u, hb = __float_as_uint(b) & 0xffff0000u;
-  const float ra = a - __uint_as_float(ha), rb = b - __uint_as_float(hb);
-  const unsigned ma = __float_as_uint(ra) & 0xffff0000u, mb = __float_as_uint(rb) & 0xffff0000u;
-  const unsigned la = __float_as_uint(ra - __uint_as_float(ma)) & 0xffff0000u;
-  const unsigned lb = __float_as_uint(rb - __uint_as_float(mb)) & 0xffff0000u;
-  h = (ha >> 16) | hb;
-  m = (ma >> 16) | mb;
-  l = (la >> 16) | lb;
-}
-
 template <int D, typename ZT = PtrTabF, bool X3 = false>
 __global__ void __launch_bounds__(256, 2) fm_dot_fwd_f32s(ZT Z, long ldz, float* __restrict__ out, long ldo, long B,
                                                           int F, int W, int self) {
@@ -595,7 +583,7 @@ __global__ void __launch_bounds__(256, 2) fm_dot_fwd_f32s(ZT Z, long ldz, float*
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const float a = u < 2 ? x0[2 * u] : x1[2 * u - 4], b = u < 2 ? x0[2 * u + 1] : x1[2 * u - 3];
-          dot_split2(a, b, ph[u], pm[u], pl[u]);
+          fm_split3_pair(a, b, ph[u], pm[u], pl[u]);
         }
         const bf16x8v_t H = __builtin_bit_cast(bf16x8v_t, u32x4_t{ph[0], ph[1], ph[2], ph[3]});
         const bf16x8v_t Mm = __builtin_bit_cast(bf16x8v_t, u32x4_t{pm[0], pm[1], pm[2], pm[3]});
