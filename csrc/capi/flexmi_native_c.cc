@@ -614,6 +614,16 @@ int fmn_model_set_table_rows(fmn_model_t m, int table, int n, const int* ranks) 
       -1);
 }
 
+int fmn_model_set_dense_channels(fmn_model_t m, int layer, int n, const int* ranks) {
+  if (!m || n < 1 || !ranks) return fail("fmn_model_set_dense_channels: null model / empty holder list");
+  return guarded(
+      [&] {
+        m->m->set_dense_channels(layer, std::vector<int>(ranks, ranks + n));
+        return 0;
+      },
+      -1);
+}
+
 int fmn_model_table_columns(fmn_model_t m, int table, int* ranks, int max) {
   if (!m) return fail("fmn_model_table_columns: null model");
   return guarded(

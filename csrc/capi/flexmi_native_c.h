@@ -175,6 +175,11 @@ int fmn_model_table_columns(fmn_model_t m, int table, int* ranks, int max);
  * column, looks up the global batch (lookups outside its rows add nothing) and each rank sums the
  * holders' partial bag sums; set/get_param move the FULL host array (this rank's rows). */
 int fmn_model_set_table_rows(fmn_model_t m, int table, int n, const int* ranks);
+/* channel split of dense layer `layer` (creation order among the dense layers) over n holder ranks:
+ * holder j keeps output features [j*N/n, (j+1)*N/n) and computes them for the global batch (input
+ * gathered, outputs and input gradients exchanged by all-to-all, its slice updated without an
+ * all-reduce); set/get_param move the FULL W [N][K] / b [N] host arrays (this rank's slice). */
+int fmn_model_set_dense_channels(fmn_model_t m, int layer, int n, const int* ranks);
 /* loss: 51 sparse categorical CE (softmax of the last layer's logits, int32 labels), 52 MSE (avg),
  * 54 binary CE (sigmoid output); bucket_mb = gradient all-reduce bucket size */
 int fmn_model_compile(fmn_model_t m, int loss_type, float lr, double bucket_mb);

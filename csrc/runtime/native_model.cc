@@ -273,6 +273,10 @@ Model::~Model() {
   for (auto* p : table_) rel(p);
   for (auto* p : emb_full_) rel(p);
   for (auto* p : idx_) rel(p);
+  for (auto& c : chan_)
+    for (float* q : {c.x, c.y, c.dy, c.dx, c.w, c.b, c.gw, c.gb}) rel(q);
+  rel(csend_);
+  rel(crecv_);
   rel(xsend_);
   rel(xrecv_);
   rel(probs_);
@@ -311,10 +315,12 @@ int Model::dense(int x, int out_dim, int act, bool bias) {
   d.w = (int)pnumel_.size();
   pnumel_.push_back((int64_t)d.N * d.K);
   entry_table_.push_back(-1);
+  entry_dense_.push_back((int)ops_.size());
   if (bias) {
     d.b = (int)pnumel_.size();
     pnumel_.push_back(d.N);
     entry_table_.push_back(-1);
+    entry_dense_.push_back((int)ops_.size());
   }
   ops_.push_back(d);
   nodes_.push_back({K_DENSE, (int)ops_.size() - 1});
@@ -345,6 +351,7 @@ int Model::embedding(int sparse, int64_t rows, int dim) {
   e.w = (int)pnumel_.size();
   pnumel_.push_back(rows * dim);
   entry_table_.push_back((int)embs_.size());
+  entry_dense_.push_back(-1);
   e.owner = -1;
   embs_.push_back(e);
   nodes_.push_back({K_EMB, (int)embs_.size() - 1});
@@ -411,6 +418,19 @@ void Model::set_table_rows(int table, const std::vector<int>& ranks) {
   e.rows_split = ranks.size() > 1;
 }
 
+void Model::set_dense_channels(int layer, const std::vector<int>& ranks) {
+  if (compiled_) throw std::logic_error("native model: placement after compile");
+  if (layer < 0 || layer >= (int)ops_.size() || ranks.empty()) throw std::invalid_argument("native model: dense layer / ranks");
+  Dense& d = ops_[layer];
+  if (d.N % (int)ranks.size() != 0) throw std::invalid_argument("native model: output features not divisible by the holders");
+  for (size_t i = 0; i < ranks.size(); ++i) {
+    if (ranks[i] < 0 || ranks[i] >= world_) throw std::invalid_argument("native model: holder rank");
+    for (size_t k = 0; k < i; ++k)
+      if (ranks[k] == ranks[i]) throw std::invalid_argument("native model: holder listed twice");
+  }
+  d.holders = ranks;
+}
+
 int Model::slice_of(const Emb& e, int r) const {
   for (size_t j = 0; j < e.holders.size(); ++j)
     if (e.holders[j] == r) return (int)j;
@@ -424,7 +444,9 @@ int Model::dense_out_node() const {
 
 bool Model::param_local(int i) const {
   const int t = entry_table_.at(i);
-  return t < 0 || slice_of(embs_[t], rank_) >= 0;
+  if (t >= 0) return slice_of(embs_[t], rank_) >= 0;
+  const Dense& d = ops_[entry_dense_.at(i)];
+  return d.holders.empty() || std::find(d.holders.begin(), d.holders.end(), rank_) != d.holders.end();
 }
 
 void Model::compile(int loss_type, float lr, double bucket_mb) {
@@ -478,9 +500,20 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
       e.nrows = e.rows_split ? (j >= 0 ? e.rows * (j + 1) / n - e.lo : 0) : e.rows;
     }
   }
-  // dense parameter entries in backward order -> one flat buffer, all-reduce buckets
+  // channel-split dense layers: this rank's slice
+  for (Dense& d : ops_) {
+    d.j = -1;
+    d.Nc = d.N;
+    if (d.holders.empty()) continue;
+    d.Nc = d.N / (int)d.holders.size();
+    for (size_t k = 0; k < d.holders.size(); ++k)
+      if (d.holders[k] == rank_) d.j = (int)k;
+  }
+  // data-parallel dense parameter entries in backward order -> one flat buffer, all-reduce buckets
+  // (channel-split slices are updated by their holders, never reduced)
   porder_.clear();
   for (auto it = ops_.rbegin(); it != ops_.rend(); ++it) {
+    if (!it->holders.empty()) continue;
     porder_.push_back(it->w);
     if (it->b >= 0) porder_.push_back(it->b);
   }
@@ -517,6 +550,17 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
       for (int h : e.holders) own[h] += (int64_t)world_ * Bl_ * e.Dc;
     for (int64_t v : own) xmax = std::max(xmax, v);
   }
+  // channel-split exchanges (every quantity global): input gather (each rank sends n * Bl * K, a
+  // holder receives B * K), output slices (a holder sends B * Nc, each rank receives Bl * N), their
+  // gradients back, the partial input gradients (a holder sends B * K, each rank receives
+  // n * Bl * K)
+  int64_t cmax = 0;
+  for (const Dense& d : ops_) {
+    if (d.holders.empty()) continue;
+    const int64_t n = (int64_t)d.holders.size();
+    cmax = std::max({cmax, (int64_t)B_ * d.K, (int64_t)B_ * d.Nc, n * Bl_ * d.K, (int64_t)Bl_ * d.N});
+  }
+  xmax = std::max(xmax, cmax);
   const size_t slot = std::max<size_t>((size_t)std::max<int64_t>(xmax, std::max(xs, xr)) * 4 + 4096, 4u << 20);
   eng_ = device_ == 1 ? make_hip_engine(rank_, world_, rendezvous_) : make_cpu_engine(rank_, world_, rendezvous_, slot);
   params_ = (float*)eng_->alloc(wplan_.numel * 4);
@@ -541,6 +585,26 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
     xsend_ = (float*)eng_->alloc((size_t)std::max<int64_t>(xs, 1) * 4);
     xrecv_ = (float*)eng_->alloc((size_t)std::max<int64_t>(xr, 1) * 4);
   }
+  chan_.assign(ops_.size(), ChanBufs{});
+  for (size_t i = 0; i < ops_.size(); ++i) {
+    const Dense& d = ops_[i];
+    if (d.j < 0) continue;
+    ChanBufs& c = chan_[i];
+    c.x = (float*)eng_->alloc((size_t)B_ * d.K * 4);
+    c.y = (float*)eng_->alloc((size_t)B_ * d.Nc * 4);
+    c.dy = (float*)eng_->alloc((size_t)B_ * d.Nc * 4);
+    if (d.need_dx) c.dx = (float*)eng_->alloc((size_t)B_ * d.K * 4);
+    c.w = (float*)eng_->alloc((size_t)d.Nc * d.K * 4);
+    c.gw = (float*)eng_->alloc((size_t)d.Nc * d.K * 4);
+    if (d.b >= 0) {
+      c.b = (float*)eng_->alloc((size_t)d.Nc * 4);
+      c.gb = (float*)eng_->alloc((size_t)d.Nc * 4);
+    }
+  }
+  if (cmax > 0) {
+    csend_ = (float*)eng_->alloc((size_t)cmax * 4);
+    crecv_ = (float*)eng_->alloc((size_t)cmax * 4);
+  }
   const int C = last.N;
   if (loss_ == LOSS_SCCE) probs_ = (float*)eng_->alloc((size_t)Bl_ * C * 4);
   labels_ = eng_->alloc((size_t)Bl_ * C * 4);
@@ -555,6 +619,7 @@ void Model::init_weights(uint64_t seed) {
     const float lim = std::sqrt(6.f / (float)(d.K + d.N));
     uint64_t s = seed * 1000003ULL + (uint64_t)d.w;
     for (auto& v : w) v = ((float)(splitmix(s) >> 40) / (float)(1ULL << 24) * 2.f - 1.f) * lim;
+    if (!param_local(d.w)) continue;
     set_param(d.w, w.data());
     if (d.b >= 0) {
       std::vector<float> z(d.N, 0.f);
@@ -588,6 +653,12 @@ void Model::set_param(int i, const float* host) {
         std::memcpy(&sl[(size_t)r * e.Dc], host + r * e.D + (int64_t)j * e.Dc, (size_t)e.Dc * 4);
       eng_->h2d(table_[t], sl.data(), sl.size() * 4);
     }
+  } else if (!ops_[entry_dense_.at(i)].holders.empty()) {
+    const int di = entry_dense_[i];
+    const Dense& d = ops_[di];
+    if (d.j < 0) throw std::invalid_argument("native model: dense slice not on this rank");
+    if (i == d.w) eng_->h2d(chan_[di].w, host + (int64_t)d.j * d.Nc * d.K, (size_t)d.Nc * d.K * 4);
+    else eng_->h2d(chan_[di].b, host + (int64_t)d.j * d.Nc, (size_t)d.Nc * 4);
   } else {
     eng_->h2d(params_ + pofs_.at(i), host, pnumel_.at(i) * 4);
   }
@@ -612,8 +683,91 @@ void Model::get_param(int i, float* host) const {
       for (int64_t r = 0; r < e.rows; ++r)
         std::memcpy(host + r * e.D + (int64_t)j * e.Dc, &sl[(size_t)r * e.Dc], (size_t)e.Dc * 4);
     }
+  } else if (!ops_[entry_dense_.at(i)].holders.empty()) {
+    const int di = entry_dense_[i];
+    const Dense& d = ops_[di];
+    if (d.j < 0) throw std::invalid_argument("native model: dense slice not on this rank");
+    if (i == d.w) eng_->d2h(host + (int64_t)d.j * d.Nc * d.K, chan_[di].w, (size_t)d.Nc * d.K * 4);
+    else eng_->d2h(host + (int64_t)d.j * d.Nc, chan_[di].b, (size_t)d.Nc * 4);
   } else {
     eng_->d2h(host, params_ + pofs_.at(i), pnumel_.at(i) * 4);
+  }
+}
+
+// forward of a channel-split dense layer (every rank takes part in the exchanges)
+void Model::dense_split_fwd(const Dense& d, int di) {
+  const ChanBufs& c = chan_[di];
+  const int n = (int)d.holders.size();
+  if (world_ == 1) {   // one rank holds every slice
+    eng_->dense_fwd(act_[d.x], c.w, c.b, act_[d.y], Bl_, d.K, d.N, d.act);
+    return;
+  }
+  std::vector<int64_t> sc(world_, 0), rc(world_, 0);
+  // 1. gather the input shards on the holders (peer order = sample order)
+  int64_t o = 0;
+  for (int p = 0; p < world_; ++p)
+    if (std::find(d.holders.begin(), d.holders.end(), p) != d.holders.end()) {
+      eng_->copy(csend_ + o, act_[d.x], (size_t)Bl_ * d.K * 4);
+      sc[p] = (int64_t)Bl_ * d.K;
+      o += sc[p];
+    }
+  if (d.j >= 0) std::fill(rc.begin(), rc.end(), (int64_t)Bl_ * d.K);
+  eng_->all_to_all(csend_, sc.data(), d.j >= 0 ? c.x : crecv_, rc.data());
+  // 2. the slice for the global batch
+  if (d.j >= 0) eng_->dense_fwd(c.x, c.w, c.b, c.y, B_, d.K, d.Nc, d.act);
+  // 3. every rank gets its sample rows of every slice (the slice's rows are contiguous by peer)
+  std::fill(sc.begin(), sc.end(), d.j >= 0 ? (int64_t)Bl_ * d.Nc : 0);
+  std::fill(rc.begin(), rc.end(), 0);
+  for (int h : d.holders) rc[h] = (int64_t)Bl_ * d.Nc;
+  eng_->all_to_all(d.j >= 0 ? c.y : csend_, sc.data(), crecv_, rc.data());
+  o = 0;
+  for (int p = 0; p < world_; ++p) {
+    if (rc[p] == 0) continue;
+    const int jj = (int)(std::find(d.holders.begin(), d.holders.end(), p) - d.holders.begin());
+    eng_->copy2d(act_[d.y] + (int64_t)jj * d.Nc, (size_t)d.N * 4, crecv_ + o, (size_t)d.Nc * 4, (size_t)d.Nc * 4, Bl_);
+    o += rc[p];
+  }
+  (void)n;
+}
+
+// backward of a channel-split dense layer: output-gradient slices to the holders, the slice's
+// weight gradients for the global batch, the holders' partial input gradients summed per shard
+void Model::dense_split_bwd(const Dense& d, int di, const Dense* below, bool is_dpre) {
+  const ChanBufs& c = chan_[di];
+  if (world_ == 1) {
+    eng_->dense_bwd(act_[d.x], c.w, act_[d.y], grad_[d.y], d.need_dx ? grad_[d.x] : nullptr, c.gw, c.gb, Bl_, d.K, d.N,
+                    d.act, is_dpre, below ? act_[below->y] : nullptr, below ? below->act : ACT_NONE);
+    return;
+  }
+  std::vector<int64_t> sc(world_, 0), rc(world_, 0);
+  int64_t o = 0;
+  for (int p = 0; p < world_; ++p) {
+    const auto it = std::find(d.holders.begin(), d.holders.end(), p);
+    if (it == d.holders.end()) continue;
+    const int jj = (int)(it - d.holders.begin());
+    eng_->copy2d(csend_ + o, (size_t)d.Nc * 4, grad_[d.y] + (int64_t)jj * d.Nc, (size_t)d.N * 4, (size_t)d.Nc * 4, Bl_);
+    sc[p] = (int64_t)Bl_ * d.Nc;
+    o += sc[p];
+  }
+  if (d.j >= 0) std::fill(rc.begin(), rc.end(), (int64_t)Bl_ * d.Nc);
+  eng_->all_to_all(csend_, sc.data(), d.j >= 0 ? c.dy : crecv_, rc.data());
+  // the layer below's activation output for the global batch is this layer's gathered input
+  if (d.j >= 0)
+    eng_->dense_bwd(c.x, c.w, c.y, c.dy, d.need_dx ? c.dx : nullptr, c.gw, c.gb, B_, d.K, d.Nc, d.act, is_dpre,
+                    below ? c.x : nullptr, below ? below->act : ACT_NONE);
+  if (!d.need_dx) return;
+  std::fill(sc.begin(), sc.end(), d.j >= 0 ? (int64_t)Bl_ * d.K : 0);
+  std::fill(rc.begin(), rc.end(), 0);
+  for (int h : d.holders) rc[h] = (int64_t)Bl_ * d.K;
+  eng_->all_to_all(d.j >= 0 ? c.dx : csend_, sc.data(), crecv_, rc.data());
+  o = 0;
+  bool first = true;
+  for (int p = 0; p < world_; ++p) {
+    if (rc[p] == 0) continue;
+    if (first) eng_->copy(grad_[d.x], crecv_ + o, (size_t)Bl_ * d.K * 4);
+    else eng_->add(grad_[d.x], crecv_ + o, (int64_t)Bl_ * d.K);
+    first = false;
+    o += rc[p];
   }
 }
 
@@ -669,6 +823,10 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
   for (const Node& n : nodes_) {
     if (n.kind == K_DENSE) {
       const Dense& d = ops_[n.idx];
+      if (!d.holders.empty()) {
+        dense_split_fwd(d, n.idx);
+        continue;
+      }
       eng_->dense_fwd(act_[d.x], params_ + pofs_[d.w], d.b >= 0 ? params_ + pofs_[d.b] : nullptr, act_[d.y], Bl_, d.K,
                       d.N, d.act);
     } else if (n.kind == K_DOT) {
@@ -698,6 +856,10 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
       const Dense& d = ops_[n.idx];
       const Dense* below = d.fuse_below ? &ops_[d.below] : nullptr;
       const bool is_dpre = d.grad_is_dpre || d.skip_act_grad;
+      if (!d.holders.empty()) {
+        dense_split_bwd(d, n.idx, below, is_dpre);
+        continue;
+      }
       eng_->dense_bwd(act_[d.x], params_ + pofs_[d.w], act_[d.y], grad_[d.y], d.need_dx ? grad_[d.x] : nullptr,
                       grads_ + pofs_[d.w], d.b >= 0 ? grads_ + pofs_[d.b] : nullptr, Bl_, d.K, d.N, d.act, is_dpre,
                       below ? act_[below->y] : nullptr, below ? below->act : ACT_NONE);
@@ -752,6 +914,12 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
   }
   if (world_ > 1) eng_->allreduce_wait();
   eng_->sgd(params_, grads_, wplan_.numel, lr_);
+  for (size_t i = 0; i < ops_.size(); ++i) {
+    const Dense& d = ops_[i];
+    if (d.j < 0) continue;
+    eng_->sgd(chan_[i].w, chan_[i].gw, (int64_t)d.Nc * d.K, lr_);
+    if (chan_[i].b) eng_->sgd(chan_[i].b, chan_[i].gb, d.Nc, lr_);
+  }
   float st[2];
   eng_->sync();
   eng_->d2h(st, stats_, sizeof(st));
@@ -771,7 +939,13 @@ std::string Model::describe() const {
       const Dense& d = ops_[n.idx];
       o << "  dense" << n.idx << ": " << d.K << " -> " << d.N << " act " << d.act
         << (d.fuse_below ? " [dX epilogue: act' below]" : "") << (d.grad_is_dpre ? " [grad arrives as dpre]" : "")
-        << (d.skip_act_grad ? " [sigmoid folded into BCE]" : "") << "\n";
+        << (d.skip_act_grad ? " [sigmoid folded into BCE]" : "");
+      if (!d.holders.empty()) {
+        o << " channel-split over ranks";
+        for (int h : d.holders) o << " " << h;
+        o << " (" << d.Nc << " features each" << (d.j >= 0 ? "; local slice" : "") << ")";
+      }
+      o << "\n";
     } else if (n.kind == K_EMB) {
       const Emb& e = embs_[n.idx];
       if (e.rows_split) {

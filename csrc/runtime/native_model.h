@@ -1,7 +1,8 @@
 // flexmi native model: graph -> per-rank execution plan -> execution, entirely in C++ (no Python).
 // Graphs: dense (MLP) chains, embedding tables and the DLRM dot interaction (a DLRM-shaped DAG:
-// bottom MLP + tables -> interaction -> top MLP); tables are placed table-wise over the ranks,
-// MLPs are data parallel.
+// bottom MLP + tables -> interaction -> top MLP); tables are placed table-wise, column-split or
+// row-split over the ranks, dense layers are data parallel or channel-split (output features over a
+// set of ranks).
 //
 // Reference: FFModel::compile / init_layers / forward / backward / update
 // (src/runtime/model.cc:374-1180) build the per-op regions, the replica gradient regions and
@@ -49,6 +50,18 @@ struct Dense {
   int below = -1;              // dense node whose activation backward that is
   bool skip_act_grad = false;  // sigmoid folded into BCE
   bool need_dx = true;
+  // channel split (the reference's Linear partitioned over its output channels, ParallelConfig
+  // [1, c] on the channel dim; src/ops/linear.cu:188-293 with the input replicated): holders[j]
+  // keeps output features [j*Nc, (j+1)*Nc) of W and b and computes them for the GLOBAL batch.
+  // Forward: the ranks' input shards are gathered on every holder (all-to-all), each holder sends
+  // every rank its sample rows of its feature slice (the columns are assembled as for a
+  // column-split table).  Backward: every holder receives the output gradient of its slice for
+  // the global batch, updates its slice (no all-reduce), and the partial input gradients of the
+  // holders are summed on each rank's sample shard (reduce-scatter through the all-to-all).
+  // Empty holders: data parallel (replicated W, bucketed gradient all-reduce).
+  std::vector<int> holders;
+  int Nc = 0;
+  int j = -1;                  // this rank's slice (plan), -1: not a holder
 };
 
 // An embedding table (SUM bag lookups of one sparse input), placed WHOLE on one rank: table-wise
@@ -114,6 +127,11 @@ class Model {
   // row split of a table over `ranks`: holder j keeps rows [j*rows/n, (j+1)*rows/n); its parameters
   // move as the FULL host array (this rank's rows read / written)
   void set_table_rows(int table, const std::vector<int>& ranks);
+  // channel split of dense layer `layer` (creation order among the dense layers) over `ranks`
+  // (N % ranks.size() == 0): holder j keeps output features [j*N/n, (j+1)*N/n); W [N][K] and b [N]
+  // move as FULL host arrays (this rank's rows / entries read / written)
+  void set_dense_channels(int layer, const std::vector<int>& ranks);
+  int num_dense() const { return (int)ops_.size(); }
   void compile(int loss_type, float lr, double bucket_mb);
   void init_weights(uint64_t seed);            // Glorot-uniform weights, zero biases, U(+-sqrt(1/rows)) tables
   int num_params() const { return (int)pnumel_.size(); }
@@ -153,7 +171,8 @@ class Model {
   std::vector<Emb> embs_;
   std::vector<Dot> dots_;
   std::vector<int> sparse_bag_;
-  std::vector<int> entry_table_;              // parameter entry -> table id (-1: dense DP entry)
+  std::vector<int> entry_table_;              // parameter entry -> table id (-1: dense entry)
+  std::vector<int> entry_dense_;              // parameter entry -> dense op id (-1: table)
   std::vector<int64_t> pnumel_;               // parameter entries (model order)
   std::vector<int> porder_;                   // backward order of the dense entries
   WeightPlan wplan_;
@@ -170,6 +189,18 @@ class Model {
   std::vector<float*> table_;                 // table id -> [rows][Dc] (holders only)
   std::vector<float*> emb_full_;              // table id -> [B][Dc] holder-side lookups (world > 1)
   std::vector<int64_t*> idx_;                 // table id -> [B][bag] indices (owner only)
+  // channel-split dense layers (holders only; indexed by dense op id): the gathered global-batch
+  // input [B][K], this slice's output / output gradient [B][Nc], the partial input gradient [B][K],
+  // the slice's parameters and gradients
+  struct ChanBufs {
+    float *x = nullptr, *y = nullptr, *dy = nullptr, *dx = nullptr, *w = nullptr, *b = nullptr, *gw = nullptr,
+          *gb = nullptr;
+  };
+  std::vector<ChanBufs> chan_;
+  float* csend_ = nullptr;                    // channel-split exchange staging (world > 1)
+  float* crecv_ = nullptr;
+  void dense_split_fwd(const Dense& d, int di);
+  void dense_split_bwd(const Dense& d, int di, const Dense* below, bool is_dpre);
   float* xsend_ = nullptr;                    // all-to-all staging (world > 1)
   float* xrecv_ = nullptr;
   std::vector<int64_t> xcount_send_, xcount_recv_;

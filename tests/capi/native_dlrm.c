@@ -64,18 +64,30 @@ static int run_rank(int device, const char* prefix, int steps, int rank, int wor
   /* a fixed table-wise placement over the ranks (round robin); NATIVE_DLRM_PLAN=colsplit splits
    * tables 0 and 2 by columns over every rank (the bench "table" plan's large tables) */
   const char* plan = getenv("NATIVE_DLRM_PLAN") ? getenv("NATIVE_DLRM_PLAN") : "table";
-  /* "mixed": table 0 split by columns, table 1 by rows over every rank, the others whole */
+  /* "mixed": table 0 split by columns, table 1 by rows over every rank, the others whole;
+   * "chan": the first bottom layer (13 -> 32) and the first top layer (-> 32) channel-split over
+   * every rank, table 0 split by columns; "chanhalf": the top layer over ranks {1, 0} of a larger
+   * world (holders in reverse order, other ranks only exchange) */
   const int colsplit = strcmp(plan, "colsplit") == 0, rowsplit = strcmp(plan, "rowsplit") == 0, mixed = strcmp(plan, "mixed") == 0;
+  const int chan = strcmp(plan, "chan") == 0, chanhalf = strcmp(plan, "chanhalf") == 0;
   int all[16];
   for (int r = 0; r < world; ++r) all[r] = r;
   for (int i = 0; i < NT; ++i) {
-    if ((colsplit && (i == 0 || i == 2)) || (mixed && i == 0)) {
+    if ((colsplit && (i == 0 || i == 2)) || ((mixed || chan) && i == 0)) {
       CHECK(fmn_model_set_table_columns(m, i, world, all));
     } else if ((rowsplit && (i == 1 || i == 3)) || (mixed && i == 1)) {
       CHECK(fmn_model_set_table_rows(m, i, world, all));
     } else {
       CHECK(fmn_model_set_table_owner(m, i, i % world));
     }
+  }
+  if (chan) {
+    CHECK(fmn_model_set_dense_channels(m, 0, world, all));
+    CHECK(fmn_model_set_dense_channels(m, 2, world, all));
+  }
+  if (chanhalf) {
+    const int two[2] = {1, 0};
+    CHECK(fmn_model_set_dense_channels(m, 2, world > 1 ? 2 : 1, world > 1 ? two : all));
   }
   CHECK(fmn_model_compile(m, 54, 0.1f, 0.0005));
   static char desc[8192];

@@ -252,31 +252,55 @@ def test_native_c_dlrm_tablewise_trains_like_the_executor(tmp_path, world):
 
 
 @pytest.mark.parametrize("plan,world", [("colsplit", 2), ("colsplit", 4), ("rowsplit", 2), ("rowsplit", 4),
-                                        ("mixed", 4)])
+                                        ("mixed", 4), ("chan", 2), ("chan", 4), ("chanhalf", 3)])
 def test_native_c_dlrm_split_tables_train_like_the_executor(tmp_path, plan, world):
     """the native plan compiler also compiles column- and row-split tables (the bench's
     table plan splits the large tables by columns over every rank; row blocks are the [c, n, r]
     extension): column holders look up their slice for the global batch and the all-to-all
     assembles the columns; row holders look up the lookups in their rows and each rank sums the
-    partial bag sums; every holder updates its part.  Merged over the holders, the tables end like
-    the Python executor's."""
+    partial bag sums; every holder updates its part.  Channel-split dense layers ("chan": the first
+    bottom and top layers over every rank; "chanhalf": the top layer over ranks 1, 0 of three, the
+    third rank only exchanging): holders compute their output features for the gathered global
+    batch and update their slice, the partial input gradients are summed per shard.  Merged over
+    the holders, tables and layers end like the Python executor's."""
     exe = _build_dlrm_c(tmp_path)
     rdv = tmp_path / "rdv"
     rdv.mkdir()
     prefix = str(tmp_path / "run")
     env = dict(os.environ, NATIVE_DLRM_PLAN=plan)
+    if world == 3:
+        env["NATIVE_DLRM_B"] = "96"          # the batch must divide over the ranks
     r = subprocess.run([exe, "cpu", prefix, "4", str(world), str(rdv)], capture_output=True, text=True, timeout=120,
                        env=env)
     assert r.returncode == 0 and "native_dlrm ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
-    cols = {"colsplit": (0, 2), "rowsplit": (), "mixed": (0,)}[plan]
-    rows = {"colsplit": (), "rowsplit": (1, 3), "mixed": (1,)}[plan]
+    cols = {"colsplit": (0, 2), "rowsplit": (), "mixed": (0,), "chan": (0,), "chanhalf": ()}[plan]
+    rows = {"colsplit": (), "rowsplit": (1, 3), "mixed": (1,), "chan": (), "chanhalf": ()}[plan]
+    # channel-split dense layers: parameter ids of (W, b) -> holder ranks in slice order
+    chan = {"chan": {0: list(range(world)), 1: list(range(world)), 8: list(range(world)), 9: list(range(world))},
+            "chanhalf": {8: [1, 0], 9: [1, 0]}}.get(plan, {})
     if cols:
         assert "column-split over ranks" in r.stdout
     if rows:
         assert "row-split over ranks" in r.stdout
+    if chan:
+        assert "channel-split over ranks" in r.stdout
     rec = _parse_dlrm(prefix, world)
     got = _replay_dlrm(rec)
     for i, want in enumerate(got):
+        if i in chan:                       # W [N][K] rows / b [N] entries by holder slice
+            hs = chan[i]
+            w = np.full_like(want, np.nan).reshape(len(hs) if i in (1, 9) else 32, -1)
+            w = w.reshape(32, -1)
+            nc = 32 // len(hs)
+            for jj, rk in enumerate(hs):
+                part = rec["ranks"][rk][0][i]
+                assert part is not None, (i, rk)
+                w[jj * nc:(jj + 1) * nc] = part.reshape(32, -1)[jj * nc:(jj + 1) * nc]
+            for rk in range(world):
+                if rk not in hs:
+                    assert rec["ranks"][rk][0][i] is None, (i, rk)
+            np.testing.assert_allclose(w.reshape(-1), want, rtol=2e-5, atol=2e-6, err_msg=f"param {i}")
+            continue
         t = i - 4                           # parameters 4..7 are the tables
         if t in cols or t in rows:
             w = np.empty_like(want).reshape(-1, 16)
