@@ -624,6 +624,75 @@ int fmn_model_set_dense_channels(fmn_model_t m, int layer, int n, const int* ran
       -1);
 }
 
+int fmn_model_apply_strategy(fmn_model_t m, fmn_strategy_t s, int n_dense, const char* const* dense_names, int n_tables,
+                             const char* const* table_names) {
+  if (!m || !s) return fail("fmn_model_apply_strategy: null model / strategy");
+  return guarded(
+      [&] {
+        auto find = [&](const char* name) -> const flexmi::OpStrategy* {
+          if (!name) return nullptr;
+          for (const auto& o : s->ops)
+            if (o.name == name) return &o;
+          return nullptr;
+        };
+        auto distinct = [](const std::vector<int>& v) {
+          for (size_t i = 0; i < v.size(); ++i)
+            for (size_t k = 0; k < i; ++k)
+              if (v[k] == v[i]) return false;
+          return true;
+        };
+        int placed = 0;
+        for (int i = 0; i < n_dense && i < m->m->num_dense(); ++i) {
+          const flexmi::OpStrategy* o = find(dense_names ? dense_names[i] : nullptr);
+          if (!o || o->device_ids.empty()) continue;
+          const int c = o->dims.empty() ? 1 : o->dims[0];
+          std::vector<int> holders;
+          if (c > 1) {
+            for (int j = 0; j < c && j < (int)o->device_ids.size(); ++j) holders.push_back(o->device_ids[j]);
+          } else if (o->num_parts() == 1) {
+            holders.push_back(o->device_ids[0]);
+          }
+          if (holders.empty() || !distinct(holders)) continue;   // data parallel
+          try {
+            m->m->set_dense_channels(i, holders);
+            ++placed;
+          } catch (const std::invalid_argument&) {             // uneven channels: data parallel
+          }
+        }
+        for (int t = 0; t < n_tables && t < m->m->num_tables(); ++t) {
+          const flexmi::OpStrategy* o = find(table_names ? table_names[t] : nullptr);
+          if (!o || o->device_ids.empty()) continue;
+          std::vector<int> d = o->dims;
+          d.resize(3, 1);
+          const int c = d[0], n = d[1], r = d[2];
+          const auto& ids = o->device_ids;
+          auto dev = [&](int i, int j, int k) { return ids.at(j + c * (i + n * k)); };
+          std::vector<int> holders;
+          bool rows = false;
+          if (c > 1) {
+            for (int j = 0; j < c; ++j) holders.push_back(dev(0, j, 0));
+          } else if (r > 1) {
+            for (int k = 0; k < r; ++k) holders.push_back(dev(0, 0, k));
+            rows = true;
+          }
+          try {
+            if (!holders.empty() && distinct(holders)) {
+              if (rows) m->m->set_table_rows(t, holders);
+              else m->m->set_table_columns(t, holders);
+            } else {
+              m->m->set_table_owner(t, ids[0]);
+            }
+            ++placed;
+          } catch (const std::invalid_argument&) {
+            m->m->set_table_owner(t, ids[0]);
+            ++placed;
+          }
+        }
+        return placed;
+      },
+      -1);
+}
+
 int fmn_model_table_columns(fmn_model_t m, int table, int* ranks, int max) {
   if (!m) return fail("fmn_model_table_columns: null model");
   return guarded(

@@ -180,6 +180,16 @@ int fmn_model_set_table_rows(fmn_model_t m, int table, int n, const int* ranks);
  * gathered, outputs and input gradients exchanged by all-to-all, its slice updated without an
  * all-reduce); set/get_param move the FULL W [N][K] / b [N] host arrays (this rank's slice). */
 int fmn_model_set_dense_channels(fmn_model_t m, int layer, int n, const int* ranks);
+/* place the model's dense layers / tables by a strategy (e.g. the MCMC search's result saved as a
+ * .pb): dense layer i is op dense_names[i], table t is op table_names[t] (NULL names: skipped).
+ * Internal dims (reference order, dim 0 fastest in the device list): Linear [c, n] -> channel split
+ * over the devices of channel slices 0..c-1 (c = 1 and one part: the layer on that device; else
+ * data parallel); Embedding [c, n] or [c, n, r] -> column split over c devices, row split over r
+ * devices, or the table on device 0 of the list.  A config the native plan cannot express exactly
+ * (uneven channels, a device repeated) falls back to data parallel / table-wise, which computes the
+ * same values.  Returns the number of ops placed from the strategy. */
+int fmn_model_apply_strategy(fmn_model_t m, fmn_strategy_t s, int n_dense, const char* const* dense_names, int n_tables,
+                             const char* const* table_names);
 /* loss: 51 sparse categorical CE (softmax of the last layer's logits, int32 labels), 52 MSE (avg),
  * 54 binary CE (sigmoid output); bucket_mb = gradient all-reduce bucket size */
 int fmn_model_compile(fmn_model_t m, int loss_type, float lr, double bucket_mb);

@@ -89,6 +89,30 @@ static int run_rank(int device, const char* prefix, int steps, int rank, int wor
     const int two[2] = {1, 0};
     CHECK(fmn_model_set_dense_channels(m, 2, world > 1 ? 2 : 1, world > 1 ? two : all));
   }
+  /* NATIVE_DLRM_STRATEGY=<.pb> with NATIVE_DLRM_NAMES="dense0,..,dense3;table0,..,table3": the
+   * placement a strategy file gives (e.g. the MCMC search's result) */
+  if (getenv("NATIVE_DLRM_STRATEGY")) {
+    fmn_strategy_t st = fmn_strategy_load(getenv("NATIVE_DLRM_STRATEGY"));
+    if (!st) {
+      fprintf(stderr, "native_dlrm r%d: strategy: %s\n", rank, fmn_last_error());
+      return 1;
+    }
+    static char names[2048];
+    const char* dn[4] = {0, 0, 0, 0};
+    const char* tn[NT];
+    for (int i = 0; i < NT; ++i) tn[i] = 0;
+    strncpy(names, getenv("NATIVE_DLRM_NAMES") ? getenv("NATIVE_DLRM_NAMES") : "", sizeof(names) - 1);
+    int k = 0;
+    char* save = 0;
+    for (char* tok = strtok_r(names, ",;", &save); tok && k < 4 + NT; tok = strtok_r(0, ",;", &save), ++k) {
+      if (k < 4) dn[k] = tok;
+      else tn[k - 4] = tok;
+    }
+    int placed;
+    CHECK(placed = fmn_model_apply_strategy(m, st, 4, dn, NT, tn));
+    if (rank == 0) printf("strategy: %d ops placed\n", placed);
+    fmn_strategy_destroy(st);
+  }
   CHECK(fmn_model_compile(m, 54, 0.1f, 0.0005));
   static char desc[8192];
   fmn_model_describe(m, desc, sizeof(desc));

@@ -338,3 +338,71 @@ def test_native_c_dlrm_hip_engine_matches_cpu(tmp_path):
     for a, b in zip(recs["cpu"]["ranks"][0][0], recs["hip"]["ranks"][0][0]):
         np.testing.assert_allclose(b, a, rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(recs["hip"]["ranks"][0][1], recs["cpu"]["ranks"][0][1], rtol=1e-4)
+
+
+def _search_tiny_dlrm(B, world, seed, budget=3000):
+    """The test DLRM in the Python front end, searched by the MCMC optimizer over `world` devices:
+    (dense op names, table op names, strategies)."""
+    from flexmi.core import ActiMode, AggrMode, DataType, FFConfig, FFModel, LossType, MetricsType, SGDOptimizer
+    from flexmi.parallel.search import optimize
+    cfg = FFConfig()
+    cfg.batchSize, cfg.device, cfg.compute_dtype = B, "cpu", "fp32"
+    m = FFModel(cfg)
+    x = m.create_tensor([B, 13], name="dense")
+    h = m.dense(x, 32, ActiMode.AC_MODE_RELU)
+    h = m.dense(h, 16, ActiMode.AC_MODE_RELU)
+    sp = [m.create_tensor([B, 1], DataType.DT_INT64, name=f"sparse{i}") for i in range(4)]
+    embs = [m.embedding(s, r, 16, AggrMode.AGGR_MODE_SUM) for s, r in zip(sp, _DLRM_ROWS)]
+    z = m.dot_interaction(h, embs)
+    t = m.dense(z, 32, ActiMode.AC_MODE_RELU)
+    t = m.dense(t, 1, ActiMode.AC_MODE_SIGMOID)
+    m.compile(SGDOptimizer(m, 0.1), LossType.LOSS_BINARY_CROSSENTROPY, [MetricsType.METRICS_ACCURACY])
+    res = optimize(m, budget, num_devices=world, seed=seed, verbose=False)
+    dense = [op.name for op in m.layers if type(op).__name__ == "Linear"]
+    tables = [op.name for op in m.layers if type(op).__name__ == "Embedding"]
+    return dense, tables, res.best
+
+
+@pytest.mark.parametrize("seed", [1, 3])
+def test_native_c_dlrm_searched_plan_trains_like_the_executor(tmp_path, seed):
+    """the C program takes the placement the MCMC search emits for the DLRM graph
+    (written as a reference-format .pb, applied by fmn_model_apply_strategy): layers placed on one
+    device or channel-split, tables table-wise / column-split on the searched devices, the rest data
+    parallel.  Four rank processes train it; merged over the holders, every parameter ends like the
+    Python executor's."""
+    from flexmi.parallel.strategy import save_strategies_to_file
+    world = 4
+    dense, tables, best = _search_tiny_dlrm(64, world, seed)
+    pb = str(tmp_path / "searched.pb")
+    save_strategies_to_file(pb, best)
+    exe = _build_dlrm_c(tmp_path)
+    rdv = tmp_path / "rdv"
+    rdv.mkdir()
+    prefix = str(tmp_path / "run")
+    env = dict(os.environ, NATIVE_DLRM_STRATEGY=pb, NATIVE_DLRM_NAMES=",".join(dense) + ";" + ",".join(tables))
+    r = subprocess.run([exe, "cpu", prefix, "4", str(world), str(rdv)], capture_output=True, text=True, timeout=120,
+                       env=env)
+    assert r.returncode == 0 and "native_dlrm ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "strategy: 8 ops placed" in r.stdout or "strategy:" in r.stdout, r.stdout[-2000:]
+    # the searched placements really are in the plan
+    for name in tables:
+        pc = best[name]
+        if pc.dims[0] > 1:
+            assert "column-split over ranks" in r.stdout
+        elif pc.num_parts() == 1:
+            assert f"on rank {pc.device_ids[0]}" in r.stdout
+    if any(best[n].num_parts() == 1 or best[n].dims[0] > 1 for n in dense):
+        assert "channel-split over ranks" in r.stdout
+    rec = _parse_dlrm(prefix, world)
+    got = _replay_dlrm(rec)
+    for i, want in enumerate(got):
+        init = rec["init"][i]
+        parts = [f[i] for f, _ in rec["ranks"] if f[i] is not None]
+        assert parts, f"param {i} held by no rank"
+        # each holder wrote its part onto the initial values: merge the changed elements
+        merged = init.copy()
+        for p in parts:
+            ch = p != init
+            assert np.allclose(merged[ch & (merged != init)], p[ch & (merged != init)], rtol=1e-6, atol=1e-7), i
+            merged[ch] = p[ch]
+        np.testing.assert_allclose(merged, want, rtol=2e-5, atol=2e-6, err_msg=f"param {i}")
