@@ -95,6 +95,39 @@ struct Stage {
   }
 };
 
+typedef __attribute__((address_space(1))) const void* gptr_b;
+typedef __attribute__((address_space(3))) void* lptr_b;
+
+// ---- global -> LDS by LDS-DMA (global_load_lds: no VGPR round trip, no ds_write) ------------
+// One wave-instruction fills 1 KiB of the operand image: lane L's 16 B land at base + 16 L, so each
+// lane loads the global chunk that the image's swizzle puts there (the inverse of lds_off).  Full
+// tiles only (the caller guarantees M, N multiples of the tile, K of BK): no edge predication.
+template <bool KC, int R, int NTH>
+struct DmaStage {
+  static constexpr int BYTES = R * BK * 2;
+  static constexpr int PER_W = BYTES / 1024 / (NTH / 64);   // wave-instructions per wave
+  static_assert(PER_W >= 1 && BYTES % (1024 * (NTH / 64)) == 0, "whole 1-KiB pieces per wave");
+  FM_DEVICE static void issue(const unsigned short* __restrict__ p, long ld, int row0, int k0, char* lds, int wave,
+                              int lane) {
+#pragma unroll
+    for (int i = 0; i < PER_W; ++i) {
+      const int piece = wave * PER_W + i;
+      const int o = piece * 1024 + 16 * lane;
+      const unsigned short* src;
+      if constexpr (KC) {
+        const int row = o / (BK * 2), slot = (o % (BK * 2)) / 16;
+        const int c = slot ^ ((row >> 1) & 7);
+        src = p + (long)(row0 + row) * ld + k0 + 8 * c;
+      } else {
+        const int kr = o / (R * 2), slot = (o % (R * 2)) / 16;
+        const int c = slot ^ MNSwz<R>::f(kr);
+        src = p + (long)(k0 + kr) * ld + row0 + 8 * c;
+      }
+      __builtin_amdgcn_global_load_lds((gptr_b)(const void*)src, (lptr_b)(void*)(lds + piece * 1024), 16, 0, 0);
+    }
+  }
+};
+
 // NTH = 256: 4 waves (2x2, wave tile BM/2 x BN/2); 512: 8 waves (2x4 for BN >= 128, else 4x2).
 // Fused-SGD epilogue of an unsplit dW tile, staged through LDS: the accumulator layout gives each
 // lane 4 columns of one row, i.e. 64-B row pieces per 16x16 tile -- a scattered pattern that held the
@@ -138,7 +171,7 @@ FM_DEVICE void sgd_epilogue_lds(const GemmP& p, const f32x4_t (&acc)[MR][NR], ch
   }
 }
 
-template <int BM, int BN, bool AK, bool BKC, bool VEC, int NTH = NT, bool SGD = false>
+template <int BM, int BN, bool AK, bool BKC, bool VEC, int NTH = NT, bool SGD = false, bool DMA = false>
 __global__ void __launch_bounds__(NTH, 2) fm_gemm_kernel(GemmP p) {
   constexpr int A_BYTES = BM * BK * 2;
   constexpr int B_BYTES = BN * BK * 2;
@@ -181,14 +214,29 @@ __global__ void __launch_bounds__(NTH, 2) fm_gemm_kernel(GemmP p) {
 
   Stage<AK, BM, VEC, NTH> sa;
   Stage<BKC, BN, VEC, NTH> sb;
-  const bool rowsum = (!AK) && (p.rowsum_a != nullptr) && (tn == 0);
+  const bool rowsum = (!DMA) && (!AK) && (p.rowsum_a != nullptr) && (tn == 0);
   float rs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // DMA: LDS-DMA staging (full tiles, no row sums): step kt+1's 1-KiB pieces are issued into the
+  // free stage before step kt's MFMAs and waited for (vmcnt 0) before the barrier that publishes
+  // them -- no VGPR round trip, no ds_write (the register-staged form's 64 KiB of ds_write_b128 per
+  // CU and k-step run at ~79 B/clk beside 192 KiB of fragment reads: the LDS, not the MFMA, set
+  // its step time).  8192x1024x1024: fwd 30.7 -> 24.5, dX 31.9 -> 27.8, dW 35.3 -> 30.6 us
+  // (profiles/gemm_bf16_dma_ab_r6.txt).
+  auto stage_dma = [&](int kt, int b) {
+    DmaStage<AK, BM, NTH>::issue(A, p.lda, m0, kt * BK, LDS_A(b), wave, lane);
+    DmaStage<BKC, BN, NTH>::issue(B, p.ldb, n0, kt * BK, LDS_B(b), wave, lane);
+  };
   if (kt0 < kt1) {
-    sa.load(A, p.lda, m0, p.M, kt0 * BK, p.K, tid);
-    sb.load(B, p.ldb, n0, p.N, kt0 * BK, p.K, tid);
-    sa.store(LDS_A(0), tid);
-    sb.store(LDS_B(0), tid);
-    if (rowsum) sa.accumulate_rows(rs);
+    if constexpr (DMA) {
+      stage_dma(kt0, 0);
+      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+    } else {
+      sa.load(A, p.lda, m0, p.M, kt0 * BK, p.K, tid);
+      sb.load(B, p.ldb, n0, p.N, kt0 * BK, p.K, tid);
+      sa.store(LDS_A(0), tid);
+      sb.store(LDS_B(0), tid);
+      if (rowsum) sa.accumulate_rows(rs);
+    }
   }
   __syncthreads();
 
@@ -196,8 +244,12 @@ __global__ void __launch_bounds__(NTH, 2) fm_gemm_kernel(GemmP p) {
     const int cur = (kt - kt0) & 1;
     const bool more = kt + 1 < kt1;
     if (more) {
-      sa.load(A, p.lda, m0, p.M, (kt + 1) * BK, p.K, tid);
-      sb.load(B, p.ldb, n0, p.N, (kt + 1) * BK, p.K, tid);
+      if constexpr (DMA) {
+        stage_dma(kt + 1, cur ^ 1);
+      } else {
+        sa.load(A, p.lda, m0, p.M, (kt + 1) * BK, p.K, tid);
+        sb.load(B, p.ldb, n0, p.N, (kt + 1) * BK, p.K, tid);
+      }
     }
     const char* la = LDS_A(cur);
     const char* lb = LDS_B(cur);
@@ -216,7 +268,9 @@ __global__ void __launch_bounds__(NTH, 2) fm_gemm_kernel(GemmP p) {
                                                               *reinterpret_cast<bf16x8v_t*>(&af[i]),
                                                               acc[i][j], 0, 0, 0);
     }
-    if (more) {
+    if constexpr (DMA) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's pieces of step kt+1 landed
+    } else if (more) {
       sa.store(LDS_A(cur ^ 1), tid);
       sb.store(LDS_B(cur ^ 1), tid);
       if (rowsum) sa.accumulate_rows(rs);
@@ -375,7 +429,8 @@ void launch_t(const GemmP& p, hipStream_t s) {
   if constexpr (!AK && !BKC) {   // fused-SGD dW GEMMs (both operands MN-contiguous): own instantiation
     if (p.uw) {
       if constexpr (VEC && BM == 128) {
-        hipLaunchKernelGGL((fm_gemm_kernel<BM, BN, AK, BKC, VEC, 512, true>), grid, dim3(512), LDS, s, p);
+        if (p.dma) hipLaunchKernelGGL((fm_gemm_kernel<BM, BN, AK, BKC, VEC, 512, true, true>), grid, dim3(512), LDS, s, p);
+        else hipLaunchKernelGGL((fm_gemm_kernel<BM, BN, AK, BKC, VEC, 512, true>), grid, dim3(512), LDS, s, p);
         return;
       }
       hipLaunchKernelGGL((fm_gemm_kernel<BM, BN, AK, BKC, VEC, NT, true>), grid, dim3(NT), LDS, s, p);
@@ -385,8 +440,15 @@ void launch_t(const GemmP& p, hipStream_t s) {
   // the 8-wave form of the 128-row tiles (4 waves per SIMD hide the per-K-tile barrier and
   // fragment latency: DLRM GEMMs -6 %, bf16 step 0.673 -> 0.626 ms, profiles/gemm_bf16_8wave_ab.jsonl)
   if constexpr (VEC && BM == 128) {
-    hipLaunchKernelGGL((fm_gemm_kernel<BM, BN, AK, BKC, VEC, 512>), grid, dim3(512), LDS, s, p);
+    if (p.dma) hipLaunchKernelGGL((fm_gemm_kernel<BM, BN, AK, BKC, VEC, 512, false, true>), grid, dim3(512), LDS, s, p);
+    else hipLaunchKernelGGL((fm_gemm_kernel<BM, BN, AK, BKC, VEC, 512>), grid, dim3(512), LDS, s, p);
     return;
+  }
+  if constexpr (VEC) {
+    if (p.dma) {
+      hipLaunchKernelGGL((fm_gemm_kernel<BM, BN, AK, BKC, VEC, NT, false, true>), grid, dim3(NT), LDS, s, p);
+      return;
+    }
   }
   hipLaunchKernelGGL((fm_gemm_kernel<BM, BN, AK, BKC, VEC>), grid, dim3(NT), LDS, s, p);
 }
@@ -525,6 +587,10 @@ static int gemm_run(const void* A, long lda, long sA, int a_kcontig,
   p.ksplit = ks;
   if (K <= 0) {  // degenerate: C = epilogue(0)
     p.ksplit = 1;
+  }
+  {   // LDS-DMA staging for full tiles without row sums (FM_GEMM_DMA=0: register staging everywhere)
+    static const bool dma_on = !getenv("FM_GEMM_DMA") || atoi(getenv("FM_GEMM_DMA")) != 0;
+    p.dma = dma_on && vec && M % BMv == 0 && N % BNv == 0 && K % BK == 0 && K > 0 && rowsum_a == nullptr;
   }
   const bool reduce_bwd = p.ksplit > 1 && fused_ep;
   if (BNv == 128) launch_bm<128, 128>(p, a_kcontig, b_kcontig, vec, stream);

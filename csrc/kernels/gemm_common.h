@@ -87,6 +87,7 @@ struct GemmP {
   float uwd, umom;
   int unest;
   int ulds;              // unsplit tiles stage the update through LDS (gemm.hip sgd_epilogue_lds)
+  int dma;   // operands staged by LDS-DMA (gemm.hip: full tiles, no row sums)
 };
 
 // W -= lr * (g + wd W) (momentum / Nesterov as fm_sgd_kernel), one element at offset o of W
