@@ -24,6 +24,8 @@ int fm_gemm(const void* A, long lda, long sA, int a_kcontig, const void* B, long
             int act, float* ws, long ws_bytes, int ksplit_req, const void* act_y, long lday, int bwd_act,
             float* colsum, float* rowsum_a, hipStream_t stream);
 void fm_gemm_f32_set_split(int on);
+void fm_gemm_set_dma(int on);
+int fm_gemm_dma_enabled();
 void fm_embedding_set_bwd_mode(int count);
 int fm_gemm_f32_get_split();
 int fm_gemm_f32_last_form();
@@ -1162,6 +1164,8 @@ PYBIND11_MODULE(_C, m) {
   // 0 = native fp32 MFMA, 1 = split-bf16 kernel (gemm_f32.hip x3), 2 = its second form (gemm_x3.hip);
   // bools map to 0 / 1 for the older callers
   m.def("gemm_f32_set_split", [](int mode) { fm_gemm_f32_set_split(mode); });
+  m.def("gemm_set_dma", [](int on) { fm_gemm_set_dma(on); });
+  m.def("gemm_dma_enabled", []() { return fm_gemm_dma_enabled(); });
   m.def("gemm_f32_get_split", []() { return fm_gemm_f32_get_split(); });
   // sparse-SGD kernels of tables with slot buffers: 1 = count / update, 0 = claim / dup / owner
   m.def("embedding_set_bwd_mode", [](bool count) { fm_embedding_set_bwd_mode(count ? 1 : 0); });

@@ -34,6 +34,8 @@
 #include <cstdlib>
 #include <type_traits>
 
+extern "C" int fm_gemm_dma_enabled();   // gemm_f32.hip
+
 namespace {
 
 constexpr unsigned OOBN = 0x80000000u;   // buffer offset past num_records: the load returns 0
@@ -153,6 +155,50 @@ struct LoadKC {
   }
 };
 
+// K-contiguous rows staged by LDS-DMA (buffer_load_dwordx4 ... lds: no VGPR round trip, no
+// ds_write): one wave-instruction fills 1 KiB of the image (8 rows x 128 B), lane L's 16 B landing at
+// base + 16 L, so lane L loads the (row, k-chunk) the image's swizzle puts at its slot; out-of-range
+// rows / chunks / halo taps read at OOBN, which the buffer unit returns as zeros.
+template <int R, int NTH, bool GATHER>
+struct LoadKCDma {
+  static constexpr int PER_W = R * BK * 2 / 1024 / (NTH / 64);
+  static_assert(PER_W >= 1 && (R * BK * 2) % (1024 * (NTH / 64)) == 0, "whole 1-KiB pieces per wave");
+  int org[PER_W], ch[PER_W];
+  bool rok[PER_W];
+
+  FM_DEVICE void init(const ConvN& p, int row0, int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < PER_W; ++i) {
+      const int o = (wave * PER_W + i) * 1024 + 16 * lane;
+      const int r = o / (BK * 2);
+      ch[i] = ((o % (BK * 2)) / 16) ^ ((r >> 1) & 7);
+      const int row = row0 + r;
+      if constexpr (GATHER) {
+        rok[i] = row < p.N;
+        int n, pp, q;
+        pix_nqp(p.gb, rok[i] ? row : 0, n, pp, q);
+        org[i] = pix_org(p.gb, n, pp, q);
+      } else {
+        rok[i] = row < p.M;
+        org[i] = (rok[i] ? row : 0) * p.K;
+      }
+    }
+  }
+
+  FM_DEVICE void issue(const ConvN& p, __amdgpu_buffer_rsrc_t rs, int kt, char* lds, int wave) const {
+#pragma unroll
+    for (int i = 0; i < PER_W; ++i) {
+      const int j = kt * 8 + ch[i];
+      const bool ok = rok[i] && j * 8 < p.K;
+      int t;
+      if constexpr (GATHER) t = tap_off(p.tb, ok ? j : 0);
+      else t = 8 * j;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds + (wave * PER_W + i) * 1024),
+                                               16, ok ? (unsigned)(org[i] + t) * 2u : OOBN, 0, 0, 0);
+    }
+  }
+};
+
 // MN-contiguous (wgrad): k-row = pixel, chunks of 8 channels / taps along the R rows of the tile.
 // Chunk ci = tid + NTH*i: k-row ci / (R/8), chunk ci % (R/8) (fixed per thread).  The window
 // origins of a k-tile's pixels come from the per-pass origin table (fm_pix_table: {orgA, orgB} per
@@ -232,7 +278,7 @@ __global__ void __launch_bounds__(256) fm_pix_table(int* __restrict__ tab, int n
 }
 
 // ---- the kernel -------------------------------------------------------------------------------
-template <int BM, int BN, int MODE, int NTH>
+template <int BM, int BN, int MODE, int NTH, bool DMA = false>
 __global__ void __launch_bounds__(NTH, 2) fm_conv_nhwc(ConvN p) {
   constexpr bool KCM = MODE != CN_WGRAD;     // both operands K-contiguous (fwd / dgrad)
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
@@ -284,6 +330,46 @@ __global__ void __launch_bounds__(NTH, 2) fm_conv_nhwc(ConvN p) {
   float dbs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   bool dbrow = false;
   if constexpr (!KCM) dbrow = p.db != nullptr && tn == 0;
+  if constexpr (KCM && DMA) {
+    // fwd / dgrad with LDS-DMA staging: k-tile kt+1 issued into the free stage before k-tile kt's
+    // MFMAs, vmcnt(0) before the barrier that publishes it (profiles/conv_dma_ab_r6.txt)
+    LoadKCDma<BM, NTH, false> da;
+    LoadKCDma<BN, NTH, true> db;
+    da.init(p, m0, wave, lane);
+    db.init(p, n0, wave, lane);
+    if (kt0 < kt1) {
+      da.issue(p, rsa, kt0, smem, wave);
+      db.issue(p, rsb, kt0, smem + A_BYTES, wave);
+      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+    }
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int cur = (kt - kt0) & 1;
+      if (kt + 1 < kt1) {
+        char* nx = smem + (cur ^ 1) * (A_BYTES + B_BYTES);
+        da.issue(p, rsa, kt + 1, nx, wave);
+        db.issue(p, rsb, kt + 1, nx + A_BYTES, wave);
+      }
+      const char* sa = smem + cur * (A_BYTES + B_BYTES);
+      const char* sb = sa + A_BYTES;
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        bf16x8_t af[MR], bfr[NR];
+#pragma unroll
+        for (int i = 0; i < MR; ++i) af[i] = frag<KCM, BM>(sa, wm * TM + 16 * i, kk, lane);
+#pragma unroll
+        for (int j = 0; j < NR; ++j) bfr[j] = frag<KCM, BN>(sb, wn * TN + 16 * j, kk, lane);
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+#pragma unroll
+          for (int j = 0; j < NR; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8v_t*>(&bfr[j]),
+                                                                *reinterpret_cast<bf16x8v_t*>(&af[i]), acc[i][j], 0, 0, 0);
+      }
+      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's pieces of k-tile kt+1 landed
+      __syncthreads();
+    }
+  } else {
   if (kt0 < kt1) {
     FM_CN_LOAD(kt0);
     if constexpr (!KCM) {
@@ -322,6 +408,7 @@ __global__ void __launch_bounds__(NTH, 2) fm_conv_nhwc(ConvN p) {
       lb.store(nx + A_BYTES, tid);
     }
     __syncthreads();
+  }
   }
 #undef FM_CN_LOAD
   if constexpr (!KCM) {
@@ -743,12 +830,19 @@ void go(ConvN& p, const Plan& q, hipStream_t s) {
   p.ksplit = q.ksplit;
   p.kt_per = q.kt_per;
   const int lds = 2 * (BM + BN) * BK * 2;
+  // fwd / dgrad stage their operands by LDS-DMA (FM_GEMM_DMA=0: register staging, for A/B)
+  const bool dma = MODE != CN_WGRAD && fm_gemm_dma_enabled();
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)fm_conv_nhwc<BM, BN, MODE, NTH>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    (void)hipFuncSetAttribute((const void*)fm_conv_nhwc<BM, BN, MODE, NTH, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              lds);
     attr = true;
   }
-  hipLaunchKernelGGL((fm_conv_nhwc<BM, BN, MODE, NTH>), dim3(p.tiles_m * p.tiles_n, 1, p.ksplit), dim3(NTH), lds, s, p);
+  if (dma)
+    hipLaunchKernelGGL((fm_conv_nhwc<BM, BN, MODE, NTH, true>), dim3(p.tiles_m * p.tiles_n, 1, p.ksplit), dim3(NTH), lds, s, p);
+  else
+    hipLaunchKernelGGL((fm_conv_nhwc<BM, BN, MODE, NTH>), dim3(p.tiles_m * p.tiles_n, 1, p.ksplit), dim3(NTH), lds, s, p);
 }
 
 // 128x128 tiles as 8-wave blocks (a 4-wave form with 64x64 per wave measured slower,

@@ -23,6 +23,8 @@
 #include <algorithm>
 #include <cstdlib>
 
+extern "C" int fm_gemm_dma_enabled();   // gemm_f32.hip
+
 namespace {
 
 constexpr int NT = 256;
@@ -589,8 +591,7 @@ static int gemm_run(const void* A, long lda, long sA, int a_kcontig,
     p.ksplit = 1;
   }
   {   // LDS-DMA staging for full tiles without row sums (FM_GEMM_DMA=0: register staging everywhere)
-    static const bool dma_on = !getenv("FM_GEMM_DMA") || atoi(getenv("FM_GEMM_DMA")) != 0;
-    p.dma = dma_on && vec && M % BMv == 0 && N % BNv == 0 && K % BK == 0 && K > 0 && rowsum_a == nullptr;
+    p.dma = fm_gemm_dma_enabled() && vec && M % BMv == 0 && N % BNv == 0 && K % BK == 0 && K > 0 && rowsum_a == nullptr;
   }
   const bool reduce_bwd = p.ksplit > 1 && fused_ep;
   if (BNv == 128) launch_bm<128, 128>(p, a_kcontig, b_kcontig, vec, stream);

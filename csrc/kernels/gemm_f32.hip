@@ -71,26 +71,42 @@ __global__ void __launch_bounds__(NT, MINB) fm_gemm_f32_kernel(GemmF p) {
 #pragma unroll
     for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+  // OPT & 4: LDS-DMA staging (full tiles, no row sums; as gemm.hip): step kt+1's pieces issued into
+  // the free stage before step kt's MFMAs, vmcnt(0) before the barrier that publishes them
+  constexpr bool DMA = (OPT & 4) != 0;
   StageF<AK, BM, VEC, NT> sa;
   StageF<BKC, BN, VEC, NT> sb;
-  const bool rowsum = (!AK) && (p.rowsum_a != nullptr) && (tn == 0);
+  const bool rowsum = (!DMA) && (!AK) && (p.rowsum_a != nullptr) && (tn == 0);
   float rs[4] = {0.f, 0.f, 0.f, 0.f};
 #define LDSF_A(b) (smem + (b) * (A_BYTES + B_BYTES))
 #define LDSF_B(b) (smem + (b) * (A_BYTES + B_BYTES) + A_BYTES)
+  auto stage_dma = [&](int kt, int b) {
+    DmaStageF<AK, BM, NT>::issue(A, p.lda, m0, kt * BKF, LDSF_A(b), wave, lane);
+    DmaStageF<BKC, BN, NT>::issue(B, p.ldb, n0, kt * BKF, LDSF_B(b), wave, lane);
+  };
   if (kt0 < kt1) {
-    sa.load(A, p.lda, m0, p.M, kt0 * BKF, p.K, tid);
-    sb.load(B, p.ldb, n0, p.N, kt0 * BKF, p.K, tid);
-    sa.store(LDSF_A(0), tid);
-    sb.store(LDSF_B(0), tid);
-    if (rowsum) sa.accumulate_rows(rs);
+    if constexpr (DMA) {
+      stage_dma(kt0, 0);
+      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+    } else {
+      sa.load(A, p.lda, m0, p.M, kt0 * BKF, p.K, tid);
+      sb.load(B, p.ldb, n0, p.N, kt0 * BKF, p.K, tid);
+      sa.store(LDSF_A(0), tid);
+      sb.store(LDSF_B(0), tid);
+      if (rowsum) sa.accumulate_rows(rs);
+    }
   }
   __syncthreads();
   for (int kt = kt0; kt < kt1; ++kt) {
     const int cur = (kt - kt0) & 1;
     const bool more = kt + 1 < kt1;
     if (more) {
-      sa.load(A, p.lda, m0, p.M, (kt + 1) * BKF, p.K, tid);
-      sb.load(B, p.ldb, n0, p.N, (kt + 1) * BKF, p.K, tid);
+      if constexpr (DMA) {
+        stage_dma(kt + 1, cur ^ 1);
+      } else {
+        sa.load(A, p.lda, m0, p.M, (kt + 1) * BKF, p.K, tid);
+        sb.load(B, p.ldb, n0, p.N, (kt + 1) * BKF, p.K, tid);
+      }
     }
     if constexpr ((OPT & 2) != 0) {
       float af0[MR][4], bf0[NR][4], af1[MR][4], bf1[NR][4];
@@ -139,7 +155,9 @@ __global__ void __launch_bounds__(NT, MINB) fm_gemm_f32_kernel(GemmF p) {
       if constexpr ((OPT & 1) != 0) __builtin_amdgcn_s_setprio(0);
     }
     }
-    if (more) {
+    if constexpr (DMA) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's pieces of step kt+1 landed
+    } else if (more) {
       sa.store(LDSF_A(cur ^ 1), tid);
       sb.store(LDSF_B(cur ^ 1), tid);
       if (rowsum) sa.accumulate_rows(rs);
@@ -320,7 +338,8 @@ void launch_f(const GemmF& p, hipStream_t s) {
   if constexpr (!AK && !BKC && BM <= 128) {   // fused-SGD dW GEMMs: own instantiation of the default forms
     if (p.uw) {
       if constexpr (VEC && BM == 128) {
-        hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 2, 512, 2, true>), grid, dim3(512), LDS, s, p);
+        if (p.dma) hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 6, 512, 2, true>), grid, dim3(512), LDS, s, p);
+        else hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 2, 512, 2, true>), grid, dim3(512), LDS, s, p);
       } else {
         hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 0, NTF, 2, true>), grid, dim3(NTF), LDS, s, p);
       }
@@ -332,8 +351,15 @@ void launch_f(const GemmF& p, hipStream_t s) {
     // first-fragment latency (DLRM fp32 GEMMs -3.7 %, the 1024-wide layers -5..8 %, the 512/256-wide
     // layers' dX/dW -5..14 % against the 4-wave kernel: profiles/gemm_f32_variants_ab.jsonl,
     // gemm_f32_8wave_ab.jsonl; the 4-wave / s_setprio / 256x128 A/B variants deleted in r6)
-    hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 2, 512>), grid, dim3(512), LDS, s, p);
+    if (p.dma) hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 6, 512>), grid, dim3(512), LDS, s, p);
+    else hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 2, 512>), grid, dim3(512), LDS, s, p);
     return;
+  }
+  if constexpr (VEC) {
+    if (p.dma) {
+      hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC, 4>), grid, dim3(NTF), LDS, s, p);
+      return;
+    }
   }
   hipLaunchKernelGGL((fm_gemm_f32_kernel<BM, BN, AK, BKC, VEC>), grid, dim3(NTF), LDS, s, p);
 }
@@ -360,6 +386,15 @@ void launch_fbm(const GemmF& p, bool ak, bool bk, bool vec, hipStream_t s) {
 //   B_kcontig: B stored [N][K] (ldb >= K) else [K][N] (ldb >= N)
 static int g_f32_split = -1;   // -1: from FM_F32_SPLIT at the first call
 extern "C" void fm_gemm_f32_set_split(int on) { g_f32_split = on < 0 ? 0 : on; }
+
+// LDS-DMA operand staging of the GEMM / convolution kernels for eligible shapes (full tiles, no row
+// sums): FM_GEMM_DMA (default 1) or fm_gemm_set_dma; 0 = register staging everywhere (A/B, tests)
+static int g_gemm_dma = -1;
+extern "C" void fm_gemm_set_dma(int on) { g_gemm_dma = on ? 1 : 0; }
+extern "C" int fm_gemm_dma_enabled() {
+  if (g_gemm_dma < 0) g_gemm_dma = !getenv("FM_GEMM_DMA") || atoi(getenv("FM_GEMM_DMA")) != 0;
+  return g_gemm_dma;
+}
 // default 3: the split kernel (gemm_x3.hip) for the big GEMMs, where it beat both the native
 // fp32 MFMA kernel and hipBLASLt on every DLRM shape and orientation (profiles/gemm_f32_lab_r5i_*);
 // 1 (the first split kernel, deleted in r6) reads as 2
@@ -429,6 +464,7 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
   p.umom = upd ? upd->mom : 0.f;
   p.unest = upd ? upd->nest : 0;
   p.ulds = upd != nullptr;   // the update staged through LDS (whole-row W accesses)
+  p.dma = 0;
   auto al = [](const void* q) { return (((uintptr_t)q) & 15) == 0; };
   bool vec = al(A) && al(B) && (lda % 4 == 0) && (ldb % 4 == 0) && (sA % 4 == 0) && (sB % 4 == 0);
   vec = vec && (a_kcontig ? (K % 4 == 0) : (M % 4 == 0)) && (b_kcontig ? (K % 4 == 0) : (N % 4 == 0));
@@ -518,6 +554,9 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
   while (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks /= 2;
   if (K <= 0) ks = 1;
   p.ksplit = ks;
+  {   // LDS-DMA operand staging for full tiles without row sums (FM_GEMM_DMA=0: register staging)
+    p.dma = fm_gemm_dma_enabled() && vec && M % BMv == 0 && N % BNv == 0 && K % BKF == 0 && K > 0 && rowsum_a == nullptr;
+  }
   g_last_form = BNv == 128 ? 1 : BMv == 128 ? 2 : 3;
   if (BNv == 128) launch_fbm<128, 128>(p, a_kcontig, b_kcontig, vec, stream);
   else if (BMv == 128) launch_fbm<128, 64>(p, a_kcontig, b_kcontig, vec, stream);

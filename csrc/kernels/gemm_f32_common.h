@@ -33,6 +33,7 @@ struct GemmF {
   float uwd, umom;
   int unest;
   int ulds;             // unsplit tiles stage the update through LDS (sgd_epilogue_lds_f32)
+  int dma;              // operands staged by LDS-DMA (gemm_f32.hip: full tiles, no row sums)
 };
 
 template <int N>
@@ -103,6 +104,35 @@ struct StageF {
     for (int i = 0; i < PER_T; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) s[j] += v[i][j];
+  }
+};
+
+typedef __attribute__((address_space(1))) const void* gptr_s;
+typedef __attribute__((address_space(3))) void* lptr_s;
+
+// global -> LDS by LDS-DMA (global_load_lds_dwordx4: 1 KiB per wave-instruction, lane L's 16 B at
+// base + 16 L): each lane loads the chunk the image layout (kc_off swizzle / linear MN rows) puts at
+// its slot.  Full tiles only (the caller guarantees M, N multiples of the tile and K of BKF).
+template <bool KC, int R, int NT>
+struct DmaStageF {
+  static constexpr int BYTES = R * BKF * 4;
+  static constexpr int PER_W = BYTES / 1024 / (NT / 64);
+  static_assert(PER_W >= 1 && BYTES % (1024 * (NT / 64)) == 0, "whole 1-KiB pieces per wave");
+  FM_DEVICE static void issue(const float* __restrict__ p, long ld, int row0, int k0, char* lds, int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < PER_W; ++i) {
+      const int piece = wave * PER_W + i;
+      const int o = piece * 1024 + 16 * lane;
+      const float* src;
+      if constexpr (KC) {
+        const int row = o / (BKF * 4), slot = (o % (BKF * 4)) / 16;
+        src = p + (long)(row0 + row) * ld + k0 + 4 * (slot ^ ((row >> 1) & 7));
+      } else {
+        const int kr = o / (R * 4), ch = (o % (R * 4)) / 16;
+        src = p + (long)(k0 + kr) * ld + row0 + 4 * ch;
+      }
+      __builtin_amdgcn_global_load_lds((gptr_s)(const void*)src, (lptr_s)(void*)(lds + piece * 1024), 16, 0, 0);
+    }
   }
 };
 

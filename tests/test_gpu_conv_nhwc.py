@@ -1,7 +1,8 @@
 """NHWC-staged bf16 convolution (csrc/kernels/conv_nhwc.hip via flexmi/ops/_kernels.py
 _nhwc_forward / _nhwc_backward) against a float64 torch oracle: forward (+bias +ReLU), data
 gradient (overwrite / accumulate; strided layers through the stride-dilated staged G), weight
-gradient (split-K float atomics + fold into [K,C,R,S]) and bias gradient.  Geometries: ResNet /
+gradient (split-K float atomics + fold into [K,C,R,S]) and bias gradient, with the forward / data
+gradient operands staged by LDS-DMA and by registers.  Geometries: ResNet /
 Inception / AlexNet widths, channel counts off the 8-channel staging grain (C, K = 20, 36),
 tile tails, 1x7 / 7x1, strides 2 and 3, negative (superset-box) pads, and the saved-forward vs
 restaged backward."""
@@ -28,6 +29,17 @@ CASES = [
     (1, 16, 12, 13, 16, 3, 3, 1, (0, -1, 1, 0)),      # asymmetric halo-shard pads
     (1, 136, 6, 5, 136, 3, 3, 1, (1, 1, 1, 1)),       # M, N tails off the 128 / 64 tiles
 ]
+
+
+@pytest.fixture(params=[1, 0], ids=["dma", "regstage"], autouse=True)
+def staging(request):
+    """Every case with the LDS-DMA operand staging (default for fwd / dgrad) and with register
+    staging (fm_gemm_set_dma(0))."""
+    from flexmi.ops import _kernels as Kk
+    prev = Kk.C().gemm_dma_enabled()
+    Kk.C().gemm_set_dma(request.param)
+    yield request.param
+    Kk.C().gemm_set_dma(prev)
 
 
 def _oracle(x, w, b, st, pads):
