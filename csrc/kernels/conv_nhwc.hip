@@ -267,6 +267,54 @@ struct LoadMN {
   }
 };
 
+// MN-contiguous (wgrad) operand staged by LDS-DMA: a 1-KiB piece is 1024 / (R*2) pixel k-rows of the
+// [pixel][R] image; lane L loads the 8 channels / taps the MN swizzle puts at its slot, from the
+// pixel's window origin (per-pass table, read one k-tile ahead into registers).
+template <int R, int NTH, bool IS_A>
+struct LoadMNDma {
+  static constexpr int PER_W = R * BK * 2 / 1024 / (NTH / 64);
+  static_assert(PER_W >= 1 && (R * BK * 2) % (1024 * (NTH / 64)) == 0, "whole 1-KiB pieces per wave");
+  int org[PER_W], kr[PER_W], coff[PER_W];
+  bool cok[PER_W];
+
+  FM_DEVICE void table(const ConvN& p, __amdgpu_buffer_rsrc_t rtab, int kt) {
+#pragma unroll
+    for (int i = 0; i < PER_W; ++i) {
+      const int pix = kt * 64 + kr[i];
+      org[i] = __builtin_amdgcn_raw_buffer_load_b32(rtab, pix < p.npix ? (unsigned)(2 * pix + (IS_A ? 0 : 1)) * 4u : OOBN,
+                                                    0, 0);
+    }
+  }
+
+  FM_DEVICE void init(const ConvN& p, __amdgpu_buffer_rsrc_t rtab, int col0, int wave, int lane, int kt0) {
+#pragma unroll
+    for (int i = 0; i < PER_W; ++i) {
+      const int o = (wave * PER_W + i) * 1024 + 16 * lane;
+      kr[i] = o / (R * 2);
+      const int c = col0 + 8 * (((o % (R * 2)) / 16) ^ MNSwz<R>::f(kr[i]));
+      if constexpr (IS_A) {
+        cok[i] = c < p.Mp;
+        coff[i] = c;
+      } else {
+        cok[i] = c < p.N;
+        coff[i] = tap_off(p.tb, cok[i] ? c / 8 : 0);
+      }
+    }
+    table(p, rtab, kt0);
+  }
+
+  // k-tile kt into lds (origins in registers), then the origins of k-tile kt+1
+  FM_DEVICE void issue(const ConvN& p, __amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t rtab, int kt, char* lds, int wave) {
+#pragma unroll
+    for (int i = 0; i < PER_W; ++i) {
+      const bool ok = cok[i] && kt * 64 + kr[i] < p.npix;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds + (wave * PER_W + i) * 1024),
+                                               16, ok ? (unsigned)(org[i] + coff[i]) * 2u : OOBN, 0, 0, 0);
+    }
+    table(p, rtab, kt + 1);
+  }
+};
+
 // {orgA, orgB} window origins of every pixel of a wgrad pass (both operands share the pixel space)
 __global__ void __launch_bounds__(256) fm_pix_table(int* __restrict__ tab, int npix, PixG ga, PixG gb) {
   for (int pix = blockIdx.x * 256 + threadIdx.x; pix < npix; pix += gridDim.x * 256) {
@@ -303,10 +351,10 @@ __global__ void __launch_bounds__(NTH, 2) fm_conv_nhwc(ConvN p) {
   LA la;
   LB lb;
   const auto rst = rsrc_n(p.ptab, KCM ? 0 : (long)p.npix * 8);
-  if constexpr (KCM) {
+  if constexpr (KCM && !DMA) {
     la.init(p, m0, tid);
     lb.init(p, n0, tid);
-  } else {
+  } else if constexpr (!DMA) {
     la.init(p, m0, tid, kt0);
     lb.init(p, n0, tid, kt0);
   }
@@ -330,26 +378,38 @@ __global__ void __launch_bounds__(NTH, 2) fm_conv_nhwc(ConvN p) {
   float dbs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   bool dbrow = false;
   if constexpr (!KCM) dbrow = p.db != nullptr && tn == 0;
-  if constexpr (KCM && DMA) {
-    // fwd / dgrad with LDS-DMA staging: k-tile kt+1 issued into the free stage before k-tile kt's
-    // MFMAs, vmcnt(0) before the barrier that publishes it (profiles/conv_dma_ab_r6.txt)
-    LoadKCDma<BM, NTH, false> da;
-    LoadKCDma<BN, NTH, true> db;
-    da.init(p, m0, wave, lane);
-    db.init(p, n0, wave, lane);
+  if constexpr (DMA) {
+    // LDS-DMA staging: k-tile kt+1 issued into the free stage before k-tile kt's MFMAs, vmcnt(0)
+    // before the barrier that publishes it (profiles/conv_dma_ab_r6.txt); wgrad reads its bias
+    // gradient back from the staged G image
+    using DA = typename std::conditional<KCM, LoadKCDma<BM, NTH, false>, LoadMNDma<BM, NTH, true>>::type;
+    using DB = typename std::conditional<KCM, LoadKCDma<BN, NTH, true>, LoadMNDma<BN, NTH, false>>::type;
+    DA da;
+    DB db;
+    auto issue = [&](int kt, char* st) {
+      if constexpr (KCM) {
+        da.issue(p, rsa, kt, st, wave);
+        db.issue(p, rsb, kt, st + A_BYTES, wave);
+      } else {
+        da.issue(p, rsa, rst, kt, st, wave);
+        db.issue(p, rsb, rst, kt, st + A_BYTES, wave);
+      }
+    };
+    if constexpr (KCM) {
+      da.init(p, m0, wave, lane);
+      db.init(p, n0, wave, lane);
+    } else {
+      da.init(p, rst, m0, wave, lane, kt0);
+      db.init(p, rst, n0, wave, lane, kt0);
+    }
     if (kt0 < kt1) {
-      da.issue(p, rsa, kt0, smem, wave);
-      db.issue(p, rsb, kt0, smem + A_BYTES, wave);
+      issue(kt0, smem);
       __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
     }
     __syncthreads();
     for (int kt = kt0; kt < kt1; ++kt) {
       const int cur = (kt - kt0) & 1;
-      if (kt + 1 < kt1) {
-        char* nx = smem + (cur ^ 1) * (A_BYTES + B_BYTES);
-        da.issue(p, rsa, kt + 1, nx, wave);
-        db.issue(p, rsb, kt + 1, nx + A_BYTES, wave);
-      }
+      if (kt + 1 < kt1) issue(kt + 1, smem + (cur ^ 1) * (A_BYTES + B_BYTES));
       const char* sa = smem + cur * (A_BYTES + B_BYTES);
       const char* sb = sa + A_BYTES;
 #pragma unroll
@@ -365,6 +425,21 @@ __global__ void __launch_bounds__(NTH, 2) fm_conv_nhwc(ConvN p) {
           for (int j = 0; j < NR; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8v_t*>(&bfr[j]),
                                                                 *reinterpret_cast<bf16x8v_t*>(&af[i]), acc[i][j], 0, 0, 0);
+      }
+      if constexpr (!KCM) {   // bias gradient: the register form's chunks, read back from the staged G
+        if (dbrow) {
+          constexpr int CPR = BM / 8, PER_T = BM * 8 / NTH;
+#pragma unroll
+          for (int i = 0; i < PER_T; ++i) {
+            const int ci = tid + NTH * i;
+            const u32x4_t w = *reinterpret_cast<const u32x4_t*>(sa + lds_off<false, BM>(ci / CPR, ci % CPR));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              dbs[2 * j] += bf2f((unsigned short)(w[j] & 0xFFFF));
+              dbs[2 * j + 1] += bf2f((unsigned short)(w[j] >> 16));
+            }
+          }
+        }
       }
       __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's pieces of k-tile kt+1 landed
       __syncthreads();
@@ -830,8 +905,8 @@ void go(ConvN& p, const Plan& q, hipStream_t s) {
   p.ksplit = q.ksplit;
   p.kt_per = q.kt_per;
   const int lds = 2 * (BM + BN) * BK * 2;
-  // fwd / dgrad stage their operands by LDS-DMA (FM_GEMM_DMA=0: register staging, for A/B)
-  const bool dma = MODE != CN_WGRAD && fm_gemm_dma_enabled();
+  // operands staged by LDS-DMA (FM_GEMM_DMA=0: register staging, for A/B)
+  const bool dma = fm_gemm_dma_enabled();
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)fm_conv_nhwc<BM, BN, MODE, NTH>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);

@@ -216,9 +216,9 @@ __global__ void __launch_bounds__(NTH, 2) fm_gemm_kernel(GemmP p) {
 
   Stage<AK, BM, VEC, NTH> sa;
   Stage<BKC, BN, VEC, NTH> sb;
-  const bool rowsum = (!DMA) && (!AK) && (p.rowsum_a != nullptr) && (tn == 0);
+  const bool rowsum = (!AK) && (p.rowsum_a != nullptr) && (tn == 0);
   float rs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  // DMA: LDS-DMA staging (full tiles, no row sums): step kt+1's 1-KiB pieces are issued into the
+  // DMA: LDS-DMA staging (full tiles; row sums read back from the image): step kt+1's 1-KiB pieces are issued into the
   // free stage before step kt's MFMAs and waited for (vmcnt 0) before the barrier that publishes
   // them -- no VGPR round trip, no ds_write (the register-staged form's 64 KiB of ds_write_b128 per
   // CU and k-step run at ~79 B/clk beside 192 KiB of fragment reads: the LDS, not the MFMA, set
@@ -271,6 +271,20 @@ __global__ void __launch_bounds__(NTH, 2) fm_gemm_kernel(GemmP p) {
                                                               acc[i][j], 0, 0, 0);
     }
     if constexpr (DMA) {
+      if constexpr (!AK) {   // bias-gradient row sums from the DMA-staged image (the register form's chunks)
+        if (rowsum) {
+#pragma unroll
+          for (int i = 0; i < Stage<AK, BM, VEC, NTH>::PER_T; ++i) {
+            const int ci = tid + NTH * i;
+            const u32x4_t w = *reinterpret_cast<const u32x4_t*>(la + lds_off<false, BM>(ci / (BM / 8), ci % (BM / 8)));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              rs[2 * j] += bf2f((unsigned short)(w[j] & 0xFFFF));
+              rs[2 * j + 1] += bf2f((unsigned short)(w[j] >> 16));
+            }
+          }
+        }
+      }
       __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's pieces of step kt+1 landed
     } else if (more) {
       sa.store(LDS_A(cur ^ 1), tid);
@@ -591,7 +605,7 @@ static int gemm_run(const void* A, long lda, long sA, int a_kcontig,
     p.ksplit = 1;
   }
   {   // LDS-DMA staging for full tiles without row sums (FM_GEMM_DMA=0: register staging everywhere)
-    p.dma = fm_gemm_dma_enabled() && vec && M % BMv == 0 && N % BNv == 0 && K % BK == 0 && K > 0 && rowsum_a == nullptr;
+    p.dma = fm_gemm_dma_enabled() && vec && M % BMv == 0 && N % BNv == 0 && K % BK == 0 && K > 0;
   }
   const bool reduce_bwd = p.ksplit > 1 && fused_ep;
   if (BNv == 128) launch_bm<128, 128>(p, a_kcontig, b_kcontig, vec, stream);

@@ -71,12 +71,12 @@ __global__ void __launch_bounds__(NT, MINB) fm_gemm_f32_kernel(GemmF p) {
 #pragma unroll
     for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  // OPT & 4: LDS-DMA staging (full tiles, no row sums; as gemm.hip): step kt+1's pieces issued into
+  // OPT & 4: LDS-DMA staging (full tiles, row sums read back from the image; as gemm.hip): step kt+1's pieces issued into
   // the free stage before step kt's MFMAs, vmcnt(0) before the barrier that publishes them
   constexpr bool DMA = (OPT & 4) != 0;
   StageF<AK, BM, VEC, NT> sa;
   StageF<BKC, BN, VEC, NT> sb;
-  const bool rowsum = (!DMA) && (!AK) && (p.rowsum_a != nullptr) && (tn == 0);
+  const bool rowsum = (!AK) && (p.rowsum_a != nullptr) && (tn == 0);
   float rs[4] = {0.f, 0.f, 0.f, 0.f};
 #define LDSF_A(b) (smem + (b) * (A_BYTES + B_BYTES))
 #define LDSF_B(b) (smem + (b) * (A_BYTES + B_BYTES) + A_BYTES)
@@ -156,6 +156,17 @@ __global__ void __launch_bounds__(NT, MINB) fm_gemm_f32_kernel(GemmF p) {
     }
     }
     if constexpr (DMA) {
+      if constexpr (!AK) {   // bias-gradient row sums from the DMA-staged image (the register form's chunks)
+        if (rowsum) {
+#pragma unroll
+          for (int i = 0; i < StageF<AK, BM, VEC, NT>::PER_T; ++i) {
+            const int ci = tid + NT * i;
+            const f32x4_t v = *reinterpret_cast<const f32x4_t*>(LDSF_A(cur) + (ci / (BM / 4)) * (BM * 4) + 16 * (ci % (BM / 4)));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) rs[j] += v[j];
+          }
+        }
+      }
       __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's pieces of step kt+1 landed
     } else if (more) {
       sa.store(LDSF_A(cur ^ 1), tid);
@@ -555,7 +566,7 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
   if (K <= 0) ks = 1;
   p.ksplit = ks;
   {   // LDS-DMA operand staging for full tiles without row sums (FM_GEMM_DMA=0: register staging)
-    p.dma = fm_gemm_dma_enabled() && vec && M % BMv == 0 && N % BNv == 0 && K % BKF == 0 && K > 0 && rowsum_a == nullptr;
+    p.dma = fm_gemm_dma_enabled() && vec && M % BMv == 0 && N % BNv == 0 && K % BKF == 0 && K > 0;
   }
   g_last_form = BNv == 128 ? 1 : BMv == 128 ? 2 : 3;
   if (BNv == 128) launch_fbm<128, 128>(p, a_kcontig, b_kcontig, vec, stream);
