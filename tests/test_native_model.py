@@ -406,3 +406,44 @@ def test_native_c_dlrm_searched_plan_trains_like_the_executor(tmp_path, seed):
             assert np.allclose(merged[ch & (merged != init)], p[ch & (merged != init)], rtol=1e-6, atol=1e-7), i
             merged[ch] = p[ch]
         np.testing.assert_allclose(merged, want, rtol=2e-5, atol=2e-6, err_msg=f"param {i}")
+
+
+def test_native_c_dlrm_strategy_mapping_rules(tmp_path):
+    """fmn_model_apply_strategy's mapping of reference-format configs: a Linear on one device -> the
+    layer placed on that rank; a channel split that does not divide the features -> data parallel
+    (same values); an Embedding [c, n, r] with r > 1 -> row split over the r devices; [c, n] with
+    c > 1 -> column split.  The four-rank run still trains like the Python executor."""
+    from flexmi.parallel.layout import ParallelConfig
+    from flexmi.parallel.strategy import save_strategies_to_file
+    world = 4
+    dense, tables, best = _search_tiny_dlrm(64, world, 1, budget=10)
+    st = {n: ParallelConfig([1, world], list(range(world))) for n in dense}
+    st[dense[1]] = ParallelConfig([1, 1], [1])                    # 32 -> 16 layer on rank 1
+    st[dense[2]] = ParallelConfig([3, 1], [0, 1, 2])              # 32 features over 3: not exact -> DP
+    st[tables[0]] = ParallelConfig([1, 1, 2], [2, 3])             # row split over ranks 2, 3
+    st[tables[1]] = ParallelConfig([2, 1], [3, 1])                # column split over ranks 3, 1
+    st[tables[2]] = ParallelConfig([1, 1], [0])
+    st[tables[3]] = ParallelConfig([1, 1], [2])
+    pb = str(tmp_path / "handmade.pb")
+    save_strategies_to_file(pb, st)
+    exe = _build_dlrm_c(tmp_path)
+    rdv = tmp_path / "rdv"
+    rdv.mkdir()
+    prefix = str(tmp_path / "run")
+    env = dict(os.environ, NATIVE_DLRM_STRATEGY=pb, NATIVE_DLRM_NAMES=",".join(dense) + ";" + ",".join(tables))
+    r = subprocess.run([exe, "cpu", prefix, "3", str(world), str(rdv)], capture_output=True, text=True, timeout=120,
+                       env=env)
+    assert r.returncode == 0 and "native_dlrm ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+    out = r.stdout
+    assert "channel-split over ranks 1 (16 features each" in out, out[-3000:]
+    assert "row-split over ranks 2 3" in out and "column-split over ranks 3 1" in out, out[-3000:]
+    assert out.count("channel-split") == 1                         # the 32-over-3 layer fell back to DP
+    rec = _parse_dlrm(prefix, world)
+    got = _replay_dlrm(rec)
+    for i, want in enumerate(got):
+        init = rec["init"][i]
+        merged = init.copy()
+        for p in [f[i] for f, _ in rec["ranks"] if f[i] is not None]:
+            ch = p != init
+            merged[ch] = p[ch]
+        np.testing.assert_allclose(merged, want, rtol=2e-5, atol=2e-6, err_msg=f"param {i}")
