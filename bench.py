@@ -464,6 +464,8 @@ def _timed(a, comm, model, cfg, dcfg, dense_in, sparse, strategy, search, ex, t_
         # measured per-shape GEMM configurations in use (flexmi/ops/gemm_tune.py; FM_GEMM_TUNE=0: none)
         from flexmi.ops import gemm_tune as _T
         rec["config"]["gemm_tuned_entries"] = len(_T.table())
+        # operand staging of full GEMM / conv tiles: LDS-DMA (FM_GEMM_DMA=0: register staging)
+        rec["config"]["gemm_staging"] = "lds-dma" if _K.C().gemm_dma_enabled() else "registers"
     if search is not None:
         rec["config"]["search"] = dict(search)
     if rank == 0 and a.profile:
