@@ -604,7 +604,7 @@ static int gemm_run(const void* A, long lda, long sA, int a_kcontig,
   if (K <= 0) {  // degenerate: C = epilogue(0)
     p.ksplit = 1;
   }
-  {   // LDS-DMA staging for full tiles without row sums (FM_GEMM_DMA=0: register staging everywhere)
+  {   // LDS-DMA staging for full tiles (FM_GEMM_DMA=0: register staging everywhere)
     p.dma = fm_gemm_dma_enabled() && vec && M % BMv == 0 && N % BNv == 0 && K % BK == 0 && K > 0;
   }
   const bool reduce_bwd = p.ksplit > 1 && fused_ep;

@@ -398,8 +398,8 @@ void launch_fbm(const GemmF& p, bool ak, bool bk, bool vec, hipStream_t s) {
 static int g_f32_split = -1;   // -1: from FM_F32_SPLIT at the first call
 extern "C" void fm_gemm_f32_set_split(int on) { g_f32_split = on < 0 ? 0 : on; }
 
-// LDS-DMA operand staging of the GEMM / convolution kernels for eligible shapes (full tiles, no row
-// sums): FM_GEMM_DMA (default 1) or fm_gemm_set_dma; 0 = register staging everywhere (A/B, tests)
+// LDS-DMA operand staging of the GEMM / convolution kernels for eligible shapes (full tiles; dW row
+// sums read back from the image): FM_GEMM_DMA (default 1) or fm_gemm_set_dma; 0 = register staging (A/B, tests)
 static int g_gemm_dma = -1;
 extern "C" void fm_gemm_set_dma(int on) { g_gemm_dma = on ? 1 : 0; }
 extern "C" int fm_gemm_dma_enabled() {
@@ -565,7 +565,7 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
   while (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks /= 2;
   if (K <= 0) ks = 1;
   p.ksplit = ks;
-  {   // LDS-DMA operand staging for full tiles without row sums (FM_GEMM_DMA=0: register staging)
+  {   // LDS-DMA operand staging for full tiles (FM_GEMM_DMA=0: register staging)
     p.dma = fm_gemm_dma_enabled() && vec && M % BMv == 0 && N % BNv == 0 && K % BKF == 0 && K > 0;
   }
   g_last_form = BNv == 128 ? 1 : BMv == 128 ? 2 : 3;

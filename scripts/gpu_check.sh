@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU session after a change: GPU test suite, smoke, then an A/B of one environment knob on the
 # default bench (two runs per arm, alternating), each step under its own time limit.
-# usage: scripts/gpu_check.sh TAG [KNOB "v1 v2"]   e.g. scripts/gpu_check.sh p5 FM_DW_STREAM "0 1"
+# usage: scripts/gpu_check.sh TAG [KNOB "v1 v2"]   e.g. scripts/gpu_check.sh p5 FM_GEMM_DMA "0 1"
 set -o pipefail
 TAG=$1
 KNOB=$2
