@@ -389,6 +389,7 @@ void Model::set_table_owner(int table, int rank) {
     throw std::invalid_argument("native model: table / rank");
   embs_[table].owner = rank;
   embs_[table].holders.clear();
+  embs_[table].rows_split = false;
 }
 
 void Model::set_table_columns(int table, const std::vector<int>& ranks) {
@@ -403,10 +404,13 @@ void Model::set_table_columns(int table, const std::vector<int>& ranks) {
   }
   e.holders = ranks;
   e.owner = ranks[0];
+  e.rows_split = false;
 }
 
 void Model::set_table_rows(int table, const std::vector<int>& ranks) {
-  set_table_columns(table, std::vector<int>{ranks.at(0)});   // validation of table / first rank
+  // every check before any field changes: a rejected call leaves the table's placement as it was
+  if (compiled_) throw std::logic_error("native model: placement after compile");
+  if (table < 0 || table >= (int)embs_.size() || ranks.empty()) throw std::invalid_argument("native model: table / ranks");
   Emb& e = embs_[table];
   for (size_t i = 0; i < ranks.size(); ++i) {
     if (ranks[i] < 0 || ranks[i] >= world_) throw std::invalid_argument("native model: holder rank");
@@ -415,6 +419,7 @@ void Model::set_table_rows(int table, const std::vector<int>& ranks) {
   }
   if ((int64_t)ranks.size() > e.rows) throw std::invalid_argument("native model: more row blocks than rows");
   e.holders = ranks;
+  e.owner = ranks[0];
   e.rows_split = ranks.size() > 1;
 }
 
@@ -806,15 +811,20 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
       }
     eng_->all_to_all(xsend_, xcount_send_.data(), xrecv_, xcount_recv_.data());
     o = 0;
+    // row blocks: the holders' partial bag sums add up -- the FIRST block received (peer order, which
+    // need not be slice order: holders {3, 1}) initialises the output, later ones add to it
+    std::vector<char> first(embs_.size(), 1);
     for (int p = 0; p < world_; ++p)
       for (size_t t = 0; t < embs_.size(); ++t) {
         const Emb& e = embs_[t];
         const int j = slice_of(e, p);
         if (j < 0) continue;
-        if (e.rows_split && j > 0)       // row blocks: the holders' partial bag sums add up
+        if (e.rows_split && !first[t])
           eng_->add(act_[e.y], xrecv_ + o, (int64_t)Bl_ * e.D);
         else
-          eng_->copy2d(act_[e.y] + (int64_t)j * e.Dc, (size_t)e.D * 4, xrecv_ + o, (size_t)e.Dc * 4, (size_t)e.Dc * 4, Bl_);
+          eng_->copy2d(act_[e.y] + (e.rows_split ? 0 : (int64_t)j * e.Dc), (size_t)e.D * 4, xrecv_ + o, (size_t)e.Dc * 4,
+                       (size_t)e.Dc * 4, Bl_);
+        first[t] = 0;
         o += (int64_t)Bl_ * e.Dc;
       }
   };

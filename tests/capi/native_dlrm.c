@@ -70,13 +70,18 @@ static int run_rank(int device, const char* prefix, int steps, int rank, int wor
    * world (holders in reverse order, other ranks only exchange) */
   const int colsplit = strcmp(plan, "colsplit") == 0, rowsplit = strcmp(plan, "rowsplit") == 0, mixed = strcmp(plan, "mixed") == 0;
   const int chan = strcmp(plan, "chan") == 0, chanhalf = strcmp(plan, "chanhalf") == 0;
-  int all[16];
-  for (int r = 0; r < world; ++r) all[r] = r;
+  /* "rowsplitrev": tables 1 and 3 split by rows over every rank in DESCENDING rank order (slice j on
+   * rank world-1-j: the partial sums arrive in an order other than slice order) */
+  const int rowsplitrev = strcmp(plan, "rowsplitrev") == 0;
+  int all[16], rev[16];
+  for (int r = 0; r < world; ++r) all[r] = r, rev[r] = world - 1 - r;
   for (int i = 0; i < NT; ++i) {
     if ((colsplit && (i == 0 || i == 2)) || ((mixed || chan) && i == 0)) {
       CHECK(fmn_model_set_table_columns(m, i, world, all));
     } else if ((rowsplit && (i == 1 || i == 3)) || (mixed && i == 1)) {
       CHECK(fmn_model_set_table_rows(m, i, world, all));
+    } else if (rowsplitrev && (i == 1 || i == 3)) {
+      CHECK(fmn_model_set_table_rows(m, i, world, rev));
     } else {
       CHECK(fmn_model_set_table_owner(m, i, i % world));
     }

@@ -252,7 +252,8 @@ def test_native_c_dlrm_tablewise_trains_like_the_executor(tmp_path, world):
 
 
 @pytest.mark.parametrize("plan,world", [("colsplit", 2), ("colsplit", 4), ("rowsplit", 2), ("rowsplit", 4),
-                                        ("mixed", 4), ("chan", 2), ("chan", 4), ("chanhalf", 3)])
+                                        ("rowsplitrev", 2), ("rowsplitrev", 3), ("mixed", 4), ("chan", 2), ("chan", 4),
+                                        ("chanhalf", 3)])
 def test_native_c_dlrm_split_tables_train_like_the_executor(tmp_path, plan, world):
     """the native plan compiler also compiles column- and row-split tables (the bench's
     table plan splits the large tables by columns over every rank; row blocks are the [c, n, r]
@@ -262,7 +263,8 @@ def test_native_c_dlrm_split_tables_train_like_the_executor(tmp_path, plan, worl
     bottom and top layers over every rank; "chanhalf": the top layer over ranks 1, 0 of three, the
     third rank only exchanging): holders compute their output features for the gathered global
     batch and update their slice, the partial input gradients are summed per shard.  Merged over
-    the holders, tables and layers end like the Python executor's."""
+    the holders, tables and layers end like the Python executor's.  "rowsplitrev" lists the row
+    holders in descending rank order (the partial sums then arrive out of slice order)."""
     exe = _build_dlrm_c(tmp_path)
     rdv = tmp_path / "rdv"
     rdv.mkdir()
@@ -270,6 +272,11 @@ def test_native_c_dlrm_split_tables_train_like_the_executor(tmp_path, plan, worl
     env = dict(os.environ, NATIVE_DLRM_PLAN=plan)
     if world == 3:
         env["NATIVE_DLRM_B"] = "96"          # the batch must divide over the ranks
+    rev = plan == "rowsplitrev"
+    if rev:
+        plan = "rowsplit"                    # same tables, holders reversed
+    if rev:
+        env["NATIVE_DLRM_PLAN"] = "rowsplitrev"
     r = subprocess.run([exe, "cpu", prefix, "4", str(world), str(rdv)], capture_output=True, text=True, timeout=120,
                        env=env)
     assert r.returncode == 0 and "native_dlrm ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
@@ -313,7 +320,8 @@ def test_native_c_dlrm_split_tables_train_like_the_executor(tmp_path, plan, worl
                     dc = 16 // world
                     w[:, rk * dc:(rk + 1) * dc] = part[:, rk * dc:(rk + 1) * dc]
                 else:
-                    lo, hi = n * rk // world, n * (rk + 1) // world
+                    j = world - 1 - rk if rev else rk       # the slice this rank holds
+                    lo, hi = n * j // world, n * (j + 1) // world
                     w[lo:hi] = part[lo:hi]
             np.testing.assert_allclose(w.reshape(-1), want, rtol=2e-5, atol=2e-6, err_msg=f"param {i}")
             continue
