@@ -65,6 +65,9 @@ def parse():
                          "table-wise embedding placement + DP MLPs (the hand plan, dlrm_strategy); dp: pure data "
                          "parallel")
     ap.add_argument("--search-budget", type=int, default=10000)
+    ap.add_argument("--robust-threshold", type=float, default=0.10,
+                    help="N>1 search: fall back to the table plan when the searched plan simulates more than this "
+                         "fraction slower than it on any machine corner (xGMI / all-reduce constants at 0.5x and 2x)")
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--table-scale", type=float, default=1.0, help="debug only: shrink tables (invalid for reporting)")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
@@ -170,6 +173,10 @@ class SkipRun(Exception):
     """A comparison run every rank agreed not to start (HBM preflight or wall budget)."""
 
 
+class StepFailure(Exception):
+    """An exception inside a run's training steps (after every agreement point)."""
+
+
 def _agree(comm, ok: bool) -> bool:
     """True iff ``ok`` on every rank (one tiny all-reduce; ranks that failed still take part, so a
     failure on one rank becomes the same decision everywhere instead of a hang in the next
@@ -213,19 +220,24 @@ def _hbm_need_bytes(model, strategies, world):
     return max(g.memory(g.assign_from(strategies)))
 
 
-def _fail_injected(name, rank):
-    """FM_BENCH_FAIL=<run>[@<rank>] (tests): raise inside the build phase of that run."""
+def _fail_injected(name, rank, phase="build"):
+    """FM_BENCH_FAIL=<run>[@<rank>][:<phase>] (tests): raise in that phase of that run -- build
+    (default), init (device allocation and weight init, after the build agreement) or step (the
+    first warm-up step, which runs collectives)."""
     spec = os.environ.get("FM_BENCH_FAIL", "")
     for item in filter(None, spec.split(",")):
+        item, _, ph = item.partition(":")
         run, _, r = item.partition("@")
-        if run == name and (r == "" or int(r) == rank):
-            raise RuntimeError(f"injected failure in the {name} run on rank {rank} (FM_BENCH_FAIL)")
+        if run == name and (r == "" or int(r) == rank) and (ph or "build") == phase:
+            raise RuntimeError(f"injected failure in the {name} run ({phase}) on rank {rank} (FM_BENCH_FAIL)")
 
 
 def guarded_run(a, comm, name, dtype, strategy, head, t_start):
     """One comparison run that cannot lose the headline: skipped (with the reason) when the wall
     budget left cannot hold it (estimate: the headline run's wall time x 1.5 + 30 s, rank 0's
-    clock) or when its HBM preflight fails; an exception becomes ``{"error": ...}`` on every rank."""
+    clock) or when its HBM preflight fails.  An exception in the build or init phase becomes
+    ``{"error": ...}`` on every rank (both phases end in an all-rank agreement); one inside the steps
+    ends the job on every rank (StepFailure: the other ranks may be blocked in a collective)."""
     est = head["wall_s"] * 1.5 + 30.0
     left = a.budget_s - (time.time() - t_start)
     if not _agree(comm, left >= est if comm.rank == 0 else True):
@@ -234,6 +246,18 @@ def guarded_run(a, comm, name, dtype, strategy, head, t_start):
         return run_once(a, dtype, comm, strategy=strategy, name=name)
     except SkipRun as e:
         return {"skipped": str(e)}
+    except StepFailure as e:
+        # a failure inside the steps, whose collectives the other ranks may already be blocked in: no
+        # agreement can reach them, so this rank ends the job (torch.distributed.run then stops every
+        # rank) instead of leaving them hung -- non-zero exit, no record
+        import traceback
+        traceback.print_exc(file=sys.stderr)
+        print(f"[bench] rank {comm.rank}: the {name} run failed inside its steps; aborting the job", file=sys.stderr,
+              flush=True)
+        if comm.world > 1:
+            os._exit(17)
+        _release_memory()
+        return {"error": f"{type(e).__name__}: {e}"[:400]}
     except Exception as e:   # noqa: BLE001 -- reported in the record, the headline survives
         import traceback
         traceback.print_exc(file=sys.stderr)
@@ -284,11 +308,28 @@ def run_once(a, dtype, comm, strategy=None, name="head"):
         raise SkipRun(f"HBM preflight: the plan needs {hbm['need_gb']} GB per device, {hbm['free_gb']} GB free")
     cuda = torch.cuda.is_available()
     sync = torch.cuda.synchronize if cuda else (lambda: None)   # CPU (gloo) rehearsal runs too
+    # device allocation and weight init (no collectives: every rank initialises its shards from the
+    # seeds) end in a second agreement -- an OOM on one rank stops the run everywhere before the
+    # first step's collectives
     t0 = time.time()
-    ex = model.init_layers()
-    sync()
+    ex = None
+    try:
+        _fail_injected(name, rank, "init")
+        ex = model.init_layers()
+        sync()
+    except Exception as e:   # noqa: BLE001 -- re-raised below, after every rank has heard of it
+        err = e
+    if not _agree(comm, err is None):
+        ex = model = None
+        _release_memory()
+        if err is not None:
+            raise err
+        raise RuntimeError(f"the {name} run failed to initialise on another rank")
     t_init = time.time() - t0
-    return _timed(a, comm, model, cfg, dcfg, dense_in, sparse, strategy, search, ex, t_init, hbm, t_run)
+    try:
+        return _timed(a, comm, model, cfg, dcfg, dense_in, sparse, strategy, search, ex, t_init, hbm, t_run, name)
+    except Exception as e:   # noqa: BLE001
+        raise StepFailure(f"{type(e).__name__}: {e}") from e
 
 
 def _build(a, dtype, comm, strategy):
@@ -324,7 +365,22 @@ def _build(a, dtype, comm, strategy):
                 res = optimize(model, a.search_budget, 1.0, num_devices=world, init=strategies, seed=0, verbose=True)
                 summ = {k: round(v, 4) for k, v in res.summary().items()}
                 summ["budget"] = a.search_budget
-                plan = [dict(res.best), summ]
+                best = dict(res.best)
+                # sensitivity pass: the pick re-simulated against the table plan with every xGMI /
+                # all-reduce constant at 0.5x and 2x; a pick that loses > robust_threshold to the
+                # table plan in any corner is replaced by the table plan (the constants are spec-based
+                # until an 8-GPU node calibrates them)
+                from flexmi.parallel.search import sensitivity
+                rows, worst = sensitivity(model, best, strategies, world)
+                wc = max(rows, key=lambda r: r[3])
+                fallback = worst > 1.0 + a.robust_threshold
+                summ["sensitivity"] = {"worst_ratio_vs_table": round(worst, 4), "worst_corner": wc[0],
+                                       "threshold": a.robust_threshold, "fallback_to_table": fallback}
+                print(f"[bench] search sensitivity: worst pick/table {worst:.3f} at {wc[0]}"
+                      f"{' -> table plan' if fallback else ''}", file=sys.stderr)
+                if fallback:
+                    best = dict(strategies)
+                plan = [best, summ]
             dist.broadcast_object_list(plan, src=0)
             a._search_plan = cached = (plan[0], plan[1])
         strategies = dict(cached[0])
@@ -336,7 +392,7 @@ def _build(a, dtype, comm, strategy):
     return model, cfg, dcfg, dense_in, sparse, strategies, search
 
 
-def _timed(a, comm, model, cfg, dcfg, dense_in, sparse, strategy, search, ex, t_init, hbm, t_run):
+def _timed(a, comm, model, cfg, dcfg, dense_in, sparse, strategy, search, ex, t_init, hbm, t_run, name="head"):
     """Warm-up and the timed K steps of a built model; returns the record and frees the model."""
     import gc
     import torch
@@ -350,7 +406,12 @@ def _timed(a, comm, model, cfg, dcfg, dense_in, sparse, strategy, search, ex, t_
     use_graph = (not a.no_graph) and torch.cuda.is_available() and not a.profile
     run_step = stage = None
 
+    first = [True]
+
     def step_eager():
+        if first[0]:
+            first[0] = False
+            _fail_injected(name, rank, "step")
         data.next_batch()
         ex.train_step()
 
@@ -438,7 +499,9 @@ def _timed(a, comm, model, cfg, dcfg, dense_in, sparse, strategy, search, ex, t_
             "global_batch": gb,
             "seq_len": 1,
             "parallelism": (f"dp{world}" if world == 1 or strategy == "dp" else
-                            f"soap-search{world}" if strategy == "search" else f"table+column-emb{world}+dp{world}-mlp"),
+                            (f"soap-search{world}" + ("-robust-table" if (search or {}).get("sensitivity", {}).get(
+                                "fallback_to_table") else "")) if strategy == "search" else
+                            f"table+column-emb{world}+dp{world}-mlp"),
             "tables_rows": sum(dcfg.embedding_size),
             "embedding_dim": dcfg.sparse_feature_size,
             "mlp_bot": dcfg.mlp_bot,
@@ -455,12 +518,17 @@ def _timed(a, comm, model, cfg, dcfg, dense_in, sparse, strategy, search, ex, t_
         },
     }
     if cuda and cfg.compute_dtype == "fp32":
-        # how the fp32 GEMMs run: 3 = the exact three-way bf16 split kernel (gemm_x3.hip, products
-        # exact in fp32, fp32 accumulation; float64-oracle tests at the native kernel's tolerance)
-        # for the big layers, the native v_mfma_f32_16x16x4_f32 kernel for the rest
+        # how the fp32 GEMMs run (split mode, gemm_f32.hip): 3 = the exact three-way bf16 split kernel
+        # (gemm_x3.hip, six bf16 products exact in fp32, fp32 accumulation) for the big layers, the
+        # native v_mfma_f32_16x16x4_f32 kernel for the rest; 4 = as 3 with the scaled fp16 two-plane
+        # split (three fp16 products, per-row / per-column power-of-two scales) on the forward and dX
+        # GEMMs.  Both are float64-oracle tested at the native kernel's tolerance
+        # (tests/test_gpu_fp32_split.py)
         from flexmi.ops import _kernels as _K
         rec["config"]["fp32_gemm"] = {0: "native-f32-mfma", 2: "bf16x3-split-all",
-                                      3: "bf16x3-split-big+native-f32-mfma"}.get(_K.C().gemm_f32_get_split(), "?")
+                                      3: "bf16x3-split-big+native-f32-mfma",
+                                      4: "f16x2-scaled-split-fwd-dx+bf16x3-split-dw+native-f32-mfma",
+                                      5: "f16x2-scaled-split-all"}.get(_K.C().gemm_f32_get_split(), "?")
         # measured per-shape GEMM configurations in use (flexmi/ops/gemm_tune.py; FM_GEMM_TUNE=0: none)
         from flexmi.ops import gemm_tune as _T
         rec["config"]["gemm_tuned_entries"] = len(_T.table())

@@ -326,7 +326,8 @@ __global__ void __launch_bounds__(256) fm_gemm_f32_reduce_bwd(GemmF p, int RB) {
 }  // namespace
 
 // the split-bf16 kernel, second form (gemm_x3.hip)
-extern "C" int fm_gemm_x3v2_launch(const void* params, int bm, int a_kcontig, int b_kcontig, int sgd, hipStream_t s);
+extern "C" int fm_gemm_x3v2_launch(const void* params, int bm, int bn, int a_kcontig, int b_kcontig, int sgd,
+                                   hipStream_t s);
 
 
 namespace {
@@ -392,6 +393,96 @@ void launch_fbm(const GemmF& p, bool ak, bool bk, bool vec, hipStream_t s) {
 
 }  // namespace
 
+// ---- per-row / per-column max |x| (the F16 split form's operand scales) ----------------------------
+// max |x| as a bit pattern (non-negative floats order like their bits).  One launch serves both
+// operands of a GEMM (two jobs; blocks [0, nb0) job 0, the rest job 1).  A job reduces either along
+// the rows of a [R][C] array (ROWS: one wave per row, out[r]) or down its columns (COLS: a block covers
+// 256 columns x rpb rows, folded through LDS, one PARTIAL per block row: out[by * C + c], by < np --
+// no atomics, no zeroing; the consumer takes the max over the np partials).
+struct AmaxJob {
+  const float* X;
+  long ld;
+  int R, C, cols, rpb, nbx;   // cols: 0 = ROWS, 1 = COLS (nbx column blocks)
+  unsigned* out;
+};
+
+__global__ void __launch_bounds__(256) fm_f32_amax2(AmaxJob j0, AmaxJob j1, int nb0) {
+  __shared__ unsigned red[4][256];
+  const bool second = (int)blockIdx.x >= nb0;
+  const AmaxJob& j = second ? j1 : j0;
+  const int b = second ? blockIdx.x - nb0 : blockIdx.x;
+  const int nb = second ? gridDim.x - nb0 : nb0;
+  const bool vec = (j.ld % 4 == 0) && ((((uintptr_t)j.X) & 15) == 0);
+  if (!j.cols) {
+    const int lane = threadIdx.x & 63;
+    for (long r = b * 4L + (threadIdx.x >> 6); r < j.R; r += nb * 4L) {
+      const float* x = j.X + r * j.ld;
+      unsigned m = 0;
+      if (vec && j.C % 4 == 0) {
+        for (int c = lane * 4; c < j.C; c += 256) {
+          const u32x4_t v = *reinterpret_cast<const u32x4_t*>(x + c);
+          m = max(max(m, max(v[0] & 0x7fffffffu, v[1] & 0x7fffffffu)), max(v[2] & 0x7fffffffu, v[3] & 0x7fffffffu));
+        }
+      } else {
+        for (int c = lane; c < j.C; c += 64) m = max(m, __float_as_uint(x[c]) & 0x7fffffffu);
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o, 64));
+      if (lane == 0) j.out[r] = m;
+    }
+    return;
+  }
+  const int bx = b % j.nbx, by = b / j.nbx;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = bx * 256 + tx * 4;
+  const int r0 = by * j.rpb, r1 = min(j.R, r0 + j.rpb);
+  const bool v4 = vec && c + 3 < j.C;
+  unsigned m[4] = {0u, 0u, 0u, 0u};
+  if (c < j.C) {
+    for (int r = r0 + ty; r < r1; r += 4) {
+      const float* x = j.X + (long)r * j.ld + c;
+      if (v4) {
+        const u32x4_t v = *reinterpret_cast<const u32x4_t*>(x);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) m[e] = max(m[e], v[e] & 0x7fffffffu);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (c + e < j.C) m[e] = max(m[e], __float_as_uint(x[e]) & 0x7fffffffu);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) red[ty][tx * 4 + e] = m[e];
+  __syncthreads();
+  if (ty == 0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (c + e < j.C)
+        j.out[(long)by * j.C + c + e] =
+            max(max(red[0][tx * 4 + e], red[1][tx * 4 + e]), max(red[2][tx * 4 + e], red[3][tx * 4 + e]));
+  }
+}
+
+// the job computing the max |x| of every M row of A / N column of B over K; np = partial count
+static AmaxJob amax_job(const float* X, long ld, bool kcontig, int rows_mn, int K, unsigned* out, int& nblocks, int& np) {
+  AmaxJob j{X, ld, 0, 0, 0, 0, 1, out};
+  if (kcontig) {   // [rows_mn][K]: a row reduction
+    j.R = rows_mn; j.C = K; j.cols = 0;
+    nblocks = (int)std::min<long>((rows_mn + 3) / 4, 1024);
+    np = 1;
+  } else {         // [K][rows_mn]: partial column reductions, <= 16 partials of >= 64 rows
+    j.R = K; j.C = rows_mn; j.cols = 1;
+    j.nbx = (rows_mn + 255) / 256;
+    int by = std::max(1, std::min(16, (K + 63) / 64));
+    j.rpb = (K + by - 1) / by;
+    by = (K + j.rpb - 1) / j.rpb;
+    nblocks = j.nbx * by;
+    np = by;
+  }
+  return j;
+}
+
 // Same contract as fm_gemm (gemm.hip) with fp32 operands and output:
 //   A_kcontig: A stored [M][K] (lda >= K) else [K][M] (lda >= M)
 //   B_kcontig: B stored [N][K] (ldb >= K) else [K][N] (ldb >= N)
@@ -408,7 +499,8 @@ extern "C" int fm_gemm_dma_enabled() {
 }
 // default 3: the split kernel (gemm_x3.hip) for the big GEMMs, where it beat both the native
 // fp32 MFMA kernel and hipBLASLt on every DLRM shape and orientation (profiles/gemm_f32_lab_r5i_*);
-// 1 (the first split kernel, deleted in r6) reads as 2
+// 1 (the first split kernel, deleted in r6) reads as 2.  4 / 5: as 3 / 2 with the F16 form of the
+// split kernel (two scaled fp16 planes, three products instead of six bf16 ones)
 static int f32_split_mode() {
   if (g_f32_split < 0) g_f32_split = getenv("FM_F32_SPLIT") != nullptr ? std::max(0, atoi(getenv("FM_F32_SPLIT"))) : 3;
   if (g_f32_split == 1) g_f32_split = 2;
@@ -476,11 +568,14 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
   p.unest = upd ? upd->nest : 0;
   p.ulds = upd != nullptr;   // the update staged through LDS (whole-row W accesses)
   p.dma = 0;
+  p.amax_a = p.amax_b = nullptr;
+  p.amax_na = p.amax_nb = 1;
   auto al = [](const void* q) { return (((uintptr_t)q) & 15) == 0; };
   bool vec = al(A) && al(B) && (lda % 4 == 0) && (ldb % 4 == 0) && (sA % 4 == 0) && (sB % 4 == 0);
   vec = vec && (a_kcontig ? (K % 4 == 0) : (M % 4 == 0)) && (b_kcontig ? (K % 4 == 0) : (N % 4 == 0));
   // ksplit_req = ks | form << 8: a measured configuration (flexmi/ops/gemm_tune.py) -- form 1/2/3 the
-  // native kernel with 128x128 / 128x64 / 64x64 tiles, 4/5 the split kernel with 256x128 / 128x128,
+  // native kernel with 128x128 / 128x64 / 64x64 tiles, 4/5/6 the split kernel with 256x128 / 128x128 /
+  // 128x64,
   // ks the split-K depth (0: the heuristic's); form 0 = the heuristic tile.  A form that does not
   // apply to the operands falls back to the heuristic.
   int form = ksplit_req >> 8;
@@ -493,17 +588,20 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
   // profiles/gemm_f32_lab_r5i_*).  K-contiguous operands need 16-B rows; MN-contiguous ones are
   // read per element.
   const int split_mode = f32_split_mode();
+  const bool big = std::min(M, N) >= 480 && K >= 480;
   const bool x3_pick = form ? (form >= 4 && split_mode != 0)
-                            : split_mode == 2 || (split_mode == 3 && std::min(M, N) >= 480 && K >= 480);
+                            : split_mode == 2 || split_mode == 5 || ((split_mode == 3 || split_mode == 4) && big);
+  const bool f16_form = split_mode >= 4 && batch == 1;
   if (x3_pick && K > 0 && K % 32 == 0 && M >= 64 && N >= 64) {
     auto opnd_ok = [&](const float* X, long ld, long sX, bool kc) {
       return kc ? (al(X) && ld % 4 == 0 && sX % 4 == 0) : true;   // MN-contiguous: 4-B loads
     };
     if (opnd_ok(A, lda, sA, a_kcontig) && opnd_ok(B, ldb, sB, b_kcontig)) {
       // 256x128 (8 waves, 2 per SIMD) whenever M fills it, split-K for the grid
-      const int bm = form == 4 ? 256 : form == 5 ? 128 : M >= 256 ? 256 : 128;
+      const int bm = form == 4 ? 256 : (form == 5 || form == 6) ? 128 : M >= 256 ? 256 : 128;
+      const int bn = form == 6 ? 64 : 128;
       p.tiles_m = (M + bm - 1) / bm;
-      p.tiles_n = (N + 127) / 128;
+      p.tiles_n = (N + bn - 1) / bn;
       const long tiles = (long)p.tiles_m * p.tiles_n * batch;
       const int ktiles = K / 32;
       const bool fused = act_y != nullptr || colsum != nullptr;
@@ -515,8 +613,28 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
       ks = std::min(ks, std::max(1, ktiles));
       while (ks > 1 && (ws == nullptr || (long)batch * ks * M * (long)N * 4 > ws_bytes)) ks /= 2;
       p.ksplit = ks;
-      g_last_form = bm == 256 ? 4 : 5;
-      if (fm_gemm_x3v2_launch(&p, bm, a_kcontig, b_kcontig, upd != nullptr && ks == 1, stream) == 0) {
+      p.amax_a = p.amax_b = nullptr;
+      // F16 form for the GEMMs with a K-contiguous A (forward, dX): measured faster than the bf16
+      // six-product split there, slower on the dW orientation whose two column scans read both
+      // batch-long operands (profiles/f16_split_ab_r7.txt)
+      if (f16_form && ws != nullptr && (a_kcontig || split_mode == 5)) {
+        // per-row / per-column scales from the tail of the workspace (the slabs use the front)
+        const long abytes = (((long)M + N) * 16 * 4 + 255) & ~255L;
+        const long slab = (long)batch * ks * M * (long)N * 4;
+        if (slab + abytes <= ws_bytes) {
+          unsigned* am = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(ws) + ws_bytes - abytes);
+          int nba, nbb, npa, npb;
+          const AmaxJob ja = amax_job(A, lda, a_kcontig, M, K, am, nba, npa);
+          const AmaxJob jb = amax_job(B, ldb, b_kcontig, N, K, am + (long)M * 16, nbb, npb);
+          hipLaunchKernelGGL(fm_f32_amax2, dim3(nba + nbb), dim3(256), 0, stream, ja, jb, nba);
+          p.amax_a = am;
+          p.amax_b = am + (long)M * 16;
+          p.amax_na = npa;
+          p.amax_nb = npb;
+        }
+      }
+      g_last_form = bm == 256 ? 4 : bn == 64 ? 6 : 5;
+      if (fm_gemm_x3v2_launch(&p, bm, bn, a_kcontig, b_kcontig, upd != nullptr && ks == 1, stream) == 0) {
         if (ks > 1) {
           const int v4 = (N % 4 == 0) && (ldc % 4 == 0) && (sC % 4 == 0) && al(C);
           const long total = (long)M * N * batch / (v4 ? 4 : 1);

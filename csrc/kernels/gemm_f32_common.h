@@ -34,7 +34,32 @@ struct GemmF {
   int unest;
   int ulds;             // unsplit tiles stage the update through LDS (sgd_epilogue_lds_f32)
   int dma;              // operands staged by LDS-DMA (gemm_f32.hip: full tiles, no row sums)
+  // fp16 two-plane split (gemm_x3.hip F16 form): max |x| bit patterns of every A row (M index) and
+  // every B column (N index) over K, from fm_f32_amax (the per-row / per-column power-of-two scales)
+  const unsigned* amax_a;
+  const unsigned* amax_b;
+  int amax_na, amax_nb;   // partials per index (strides M / N): the scale takes their max
 };
+
+// the max over the np partials of index i (stride n)
+FM_DEVICE unsigned amax_of(const unsigned* a, int np, int n, int i) {
+  unsigned v = a[i];
+  for (int k = 1; k < np; ++k) v = max(v, a[(long)k * n + i]);
+  return v;
+}
+
+// power-of-two scale of a row / column whose max |x| has bit pattern mb: 2^sig with
+// max * 2^sig in [2^14, 2^15) (an fp16 holds it with 11 significant bits and no overflow; a subnormal
+// max counts by its leading bit); an all-zero row takes sig 0.  sig is clamped to the normal fp32
+// exponent range, so rows below 2^-112 keep fp16 subnormal precision only (as fp32 itself does there).
+FM_DEVICE int f16_sig(unsigned mb) {
+  if (mb == 0) return 0;
+  const int e = (int)(mb >> 23);
+  const int eu = e ? e - 127 : (31 - __clz(mb)) - 149;
+  const int sg = 14 - eu;
+  return sg > 126 ? 126 : (sg < -126 ? -126 : sg);
+}
+FM_DEVICE float pow2f(int e) { return __uint_as_float((unsigned)(e + 127) << 23); }   // e in [-126, 127]
 
 template <int N>
 using fvec = float __attribute__((ext_vector_type(N)));

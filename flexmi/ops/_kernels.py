@@ -128,7 +128,7 @@ DW_LIB = os.environ.get("FM_DW_LIB", "auto")
 def _dw_lib(M, N, K, dtype):
     if DW_LIB == "0" or dtype != torch.float32:
         return False
-    if DW_LIB == "auto" and C().gemm_f32_get_split() in (2, 3):
+    if DW_LIB == "auto" and C().gemm_f32_get_split() in (2, 3, 4, 5):
         return False               # the split-bf16 kernel (gemm_x3.hip) takes the big fp32 dW GEMMs
     return DW_LIB == "1" or (N >= 512 and K >= 480 and M >= 4096)
 

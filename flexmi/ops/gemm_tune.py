@@ -20,7 +20,8 @@ import os
 _DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")
 DEFAULT_PATH = os.path.join(_DIR, "gemm_mi355x.json")
 
-FORMS_F32 = {1: "native128x128", 2: "native128x64", 3: "native64x64", 4: "x3_256x128", 5: "x3_128x128"}
+FORMS_F32 = {1: "native128x128", 2: "native128x64", 3: "native64x64", 4: "x3_256x128", 5: "x3_128x128",
+             6: "x3_128x64"}
 FORMS_BF16 = {1: "128x128", 2: "128x64", 3: "64x64"}
 KS_CHOICES = (1, 2, 4, 8, 16, 32, 64)
 
@@ -80,9 +81,11 @@ def candidates(dtype, M, N, K, fused=False, sgd=False):
     forms = list(FORMS_F32) if dtype == "fp32" else list(FORMS_BF16)
     for f in forms:
         x3 = dtype == "fp32" and f >= 4
-        if x3 and (K % 32 or M < 64 or N < 64 or fused):
+        if x3 and (K % 32 or M < 64 or N < 64):
             continue
         for ks in KS_CHOICES:
+            if x3 and fused and ks > 1:
+                break               # the split kernel carries a fused epilogue unsplit only
             if ks > 1 and ks * 4 > ktiles:
                 break
             out.append(encode(f, ks))

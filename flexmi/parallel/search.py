@@ -318,3 +318,47 @@ def optimize(model, budget, alpha=1.0, num_devices=None, machine=None, cost_db=N
         print(f"[search] {n} devices, {budget} iters in {res.seconds:.1f}s: best {best_us / 1e3:.3f} ms/iter "
               f"(data parallel {dp_us / 1e3:.3f} ms, predicted speedup {res.speedup_vs_dp:.2f}x)", file=sys.stderr)
     return res
+
+
+# machine corners of the sensitivity pass: every communication constant of the (spec-derived,
+# uncalibrated above one GPU) MI355X model at half and at twice its value, one at a time, plus the
+# all-pessimistic and all-optimistic combinations.  Reference: the simulator's fixed machine
+# constants, src/runtime/simulator.cu:21-76.
+SENS_KEYS = ("link_GBps", "link_lat_us", "ar_busbw_GBps", "ar_lat_us")
+
+
+def machine_corners(base: MachineModel):
+    corners = [("nominal", base)]
+    for k in SENS_KEYS:
+        for f in (0.5, 2.0):
+            m = MachineModel(**{**base.__dict__})
+            setattr(m, k, getattr(base, k) * f)
+            corners.append((f"{k}x{f:g}", m))
+    slow = MachineModel(**{**base.__dict__})
+    fast = MachineModel(**{**base.__dict__})
+    for k in SENS_KEYS:
+        bw = k.endswith("GBps")
+        setattr(slow, k, getattr(base, k) * (0.5 if bw else 2.0))
+        setattr(fast, k, getattr(base, k) * (2.0 if bw else 0.5))
+    corners += [("all_slow", slow), ("all_fast", fast)]
+    return corners
+
+
+def sensitivity(model, pick: Dict[str, ParallelConfig], base: Dict[str, ParallelConfig], num_devices, machine=None,
+                cost_db=None):
+    """Re-simulate the searched plan ``pick`` and a reference plan ``base`` (the hand-written table
+    plan it was seeded with) on every machine corner.  Returns (rows, worst) with rows =
+    [(corner, pick_us, base_us, pick_us / base_us)] and worst = the largest ratio: > 1.10 means
+    the search's choice loses more than 10 % to the robust plan if a constant is off by 2x."""
+    n = num_devices
+    machine = machine or MachineModel.mi355x(n)
+    rows = []
+    for name, m in machine_corners(machine):
+        m.ndev = n
+        cost = CostModel(m, cost_db, dtype_bytes=2 if model.config.compute_dtype == "bf16" else 4)
+        us = []
+        for plan in (pick, base):
+            g = SimGraph(model, n, m, cost, extra=plan)
+            us.append(g.simulate(g.assign_from(plan)))
+        rows.append((name, us[0], us[1], us[0] / us[1]))
+    return rows, max(r[3] for r in rows)

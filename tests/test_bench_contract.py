@@ -110,6 +110,27 @@ def test_bench_eight_ranks_mlperf_plan(strategy):
         assert r["config"]["parallelism"] == "dp8" and "soap_speedup_vs_dp" not in r["config"]
     else:
         assert r["config"]["dp"]["parallelism"] == "dp8" and r["config"]["soap_speedup_vs_dp"] > 0
+    if strategy == "search":
+        sens = r["config"]["search"]["sensitivity"]
+        assert sens["worst_ratio_vs_table"] > 0 and sens["threshold"] == 0.10 and sens["worst_corner"]
+        assert r["config"]["parallelism"] == "soap-search8" + ("-robust-table" if sens["fallback_to_table"] else "")
+
+
+@pytest.mark.multiproc
+def test_bench_search_falls_back_to_the_robust_plan():
+    """when the searched plan is not robust to the spec-based machine constants (here
+    forced: --robust-threshold -1 rejects any pick), the 8-rank MLPerf headline runs the table plan
+    the search was seeded with, labelled as such, with the corner table's worst case recorded."""
+    r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+              "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "8",
+              "--steps", "2", "--warmup", "1", "--config", "mlperf", "--table-scale", "1e-4",
+              "--batch-per-gpu", "64", "--search-budget", "200", "--robust-threshold", "-1", "--no-dp"])
+    _check(r, 8)
+    c = r["config"]
+    assert c["parallelism"] == "soap-search8-robust-table"
+    assert c["search"]["sensitivity"]["fallback_to_table"] is True
+    # the headline ran the table plan: same plan as the table comparison run, so their step times agree
+    assert 0.5 < c["search_speedup_vs_table"] < 2.0
 
 
 @pytest.mark.multiproc
@@ -137,3 +158,31 @@ def test_bench_wall_budget_skips_comparisons():
     _check(r, 2)
     for name in ("table", "dp"):
         assert "wall budget" in r["config"][name]["skipped"]
+
+
+def test_bench_init_failure_keeps_headline():
+    """a comparison run that fails on one rank AFTER the build agreement (FM_BENCH_FAIL
+    dp@1:init -- device allocation / weight init) is agreed on by both ranks: ``config.dp.error``,
+    the headline kept, no hang."""
+    r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+              "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+              "--steps", "2", "--warmup", "1", "--config", "tiny", "--batch-per-gpu", "64",
+              "--search-budget", "200"], FM_BENCH_FAIL="dp@1:init")
+    _check(r, 2)
+    assert "init" in r["config"]["dp"]["error"]      # rank 0 reports the other rank's init failure
+    assert r["config"]["table"]["value"] > 0
+
+
+def test_bench_step_failure_ends_the_job():
+    """A failure inside a comparison run's steps (dp@1:step: the other rank may already wait in the
+    step's collectives) ends the whole job with a non-zero exit within seconds instead of hanging."""
+    import time
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", MASTER_ADDR="127.0.0.1", FM_BENCH_FAIL="dp@1:step")
+    t0 = time.time()
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+                        "--steps", "2", "--warmup", "1", "--config", "tiny", "--batch-per-gpu", "64",
+                        "--search-budget", "200"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode != 0, p.stdout[-2000:]
+    assert "failed inside its steps" in p.stderr
+    assert time.time() - t0 < 200

@@ -1,5 +1,6 @@
-"""fp32 GEMM on the bf16 matrix cores by exact three-way operand splitting (csrc/kernels/gemm_x3.hip;
-gemm_f32_set_split(2) = every eligible GEMM, 3 = the default big-GEMM policy): every orientation, tails, epilogues, fused SGD, the fused
+"""fp32 GEMM on the 16-bit matrix cores by operand splitting (csrc/kernels/gemm_x3.hip): the exact bf16
+three-way split (gemm_f32_set_split(2) = every eligible GEMM, 3 = the big-GEMM policy) and the scaled
+fp16 two-plane split (4 / 5: the same policies): every orientation, tails, epilogues, fused SGD, the fused
 backward epilogue, row sums and split-K against a float64 oracle at the fp32 test tolerance, with
 its error compared to the native v_mfma_f32_16x16x4_f32 kernel's on the same inputs."""
 import pytest
@@ -10,7 +11,7 @@ from tests.test_gpu_fp32 import TOL, _fused_backward_epilogue, rel_err
 pytestmark = pytest.mark.gpu
 
 
-MODES = [2, 3]     # split mode
+MODES = [2, 3, 4, 5]     # split mode (4 / 5: the fp16 two-plane scaled form)
 
 
 @pytest.fixture(params=MODES)
@@ -180,3 +181,32 @@ def test_split_nonfinite_operand(gpu):
     mask[3] = False
     ref = A[mask].double() @ B.double()
     assert rel_err(C[mask], ref) < TOL
+
+
+@pytest.mark.parametrize("mode", [4, 5])
+@pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, False)])
+def test_f16_split_row_scales(gpu, mode, a_k, b_k):
+    """The fp16 form scales every A row and B column by its own power of two: rows and columns whose
+    magnitudes span twelve decades, an all-zero row and column, subnormal-size and 1e30-size rows all
+    come out at fp32 accuracy relative to EACH row's own magnitude (not only the global max)."""
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(7)
+    M, N, K = 1024, 640, 1024
+    A = torch.randn(M, K, device=gpu) * torch.pow(10.0, -12 * torch.rand(M, 1, device=gpu))
+    B = torch.randn(K, N, device=gpu) * torch.pow(10.0, -6 * torch.rand(1, N, device=gpu))
+    A[3] = 0.0
+    B[:, 5] = 0.0
+    A[7] *= 1e-30
+    A[9] *= 1e30
+    ref = A.double() @ B.double()
+    Kk.C().gemm_f32_set_split(0)
+    Cn = _gemm(Kk, A, B, a_k, b_k, M, N, K)
+    Kk.C().gemm_f32_set_split(mode)
+    Cs = _gemm(Kk, A, B, a_k, b_k, M, N, K)
+    for C, name in ((Cs, "split"), (Cn, "native")):
+        assert torch.isfinite(C).all(), name
+    assert (Cs[3] == 0).all() and (Cs[:, 5] == 0).all()
+    rowmax = ref.abs().amax(1, keepdim=True) + 1e-300
+    e_split = ((Cs.double() - ref).abs() / rowmax).max().item()
+    e_native = ((Cn.double() - ref).abs() / rowmax).max().item()
+    assert e_split < 4 * e_native + 1e-6, (e_split, e_native)

@@ -149,6 +149,27 @@ def test_embedding_fwd_bwd(gpu, bag, D, rows):
     assert torch.allclose(dW, upd, atol=1e-3)
 
 
+@pytest.mark.parametrize("dy_dtype", [torch.float32, torch.bfloat16])
+def test_embedding_small_tables_lds_atomics(gpu, dy_dtype):
+    """The small-table backward (<= 160 rows: block-shared LDS copy, LDS float atomics, one global
+    atomic per touched element and block) at the MLPerf batch on the 3 / 63 / 108 / 155-row sizes
+    (and a bag of 2 with a row shard), fused SGD against a float64 index_add oracle."""
+    from flexmi.ops import _kernels as Kk
+    torch.manual_seed(11)
+    B = 8192
+    for rows, bag, D in [(3, 1, 128), (63, 1, 128), (108, 1, 128), (155, 1, 128), (40, 2, 64)]:
+        W = torch.randn(rows, D, device=gpu)
+        idx = torch.randint(0, rows, (B, bag), device=gpu)
+        dy = (torch.randn(B, D, device=gpu) * 1e-2).to(dy_dtype)
+        lr = torch.tensor([0.05], device=gpu)
+        W2 = W.clone()
+        Kk.embedding_backward_sgd(idx, dy, W2, lr, 21, {})
+        upd = torch.zeros(rows, D, dtype=torch.float64, device=gpu)
+        upd.index_add_(0, idx.reshape(-1), dy.double().repeat_interleave(bag, 0))
+        ref = W.double() - 0.05 * upd
+        assert (W2.double() - ref).abs().max().item() < 2e-5 * (1 + ref.abs().max().item()), (rows, bag, D)
+
+
 @pytest.mark.parametrize("F,D,self_i", [(27, 128, False), (9, 64, True), (4, 32, False)])
 def test_dot_interaction(gpu, F, D, self_i):
     from flexmi.ops import _kernels as Kk
