@@ -414,10 +414,10 @@ void launch_x3v2_s(const GemmF& p, bool ak, bool bk, hipStream_t s) {
 template <int BM, int BN, bool SGD>
 void launch_x3v2(const GemmF& p, bool ak, bool bk, hipStream_t s) {
   const bool f16 = p.amax_a != nullptr;
-  static const int f16s = getenv("FM_X3_F16_SCHED") ? atoi(getenv("FM_X3_F16_SCHED")) : 3;   // LAB (temporary)
   if constexpr (BM == 256) {
-    if (f16 && f16s == 0) launch_x3v2_s<BM, BN, SGD, 0, true>(p, ak, bk, s);
-    else if (f16) launch_x3v2_s<BM, BN, SGD, 3, true>(p, ak, bk, s);
+    // the F16 form takes the one-register-set schedule: two staging sets plus its second
+    // accumulator set spill at 256 VGPRs (the dX orientation)
+    if (f16) launch_x3v2_s<BM, BN, SGD, 0, true>(p, ak, bk, s);
     else launch_x3v2_s<BM, BN, SGD, 3>(p, ak, bk, s);
   } else {
     if (f16) launch_x3v2_s<BM, BN, SGD, 0, true>(p, ak, bk, s);
