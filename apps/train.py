@@ -102,6 +102,11 @@ def main(argv=None):
         print(f"[{a.model}] batch {cfg.batchSize} x {a.iterations} iterations on {comm.world} device(s), "
               f"loss {m.get_loss():.4f} accuracy {m.get_accuracy():.2f}%", file=sys.stderr)
         print(f"ELAPSED TIME = {el:.4f}s, THROUGHPUT = {samples / el:.2f} samples/s", flush=True)
+        from flexmi.ops import _kernels as K
+        for d, key, times, pick in K.CONV_TUNE_LOG:   # per-layer measured convolution forms
+            print(f"[conv-tune] {d} x{list(key[0])} w{list(key[1])} s{key[2][0]}: " +
+                  " ".join(f"{f}={t:.1f}us" for f, t in sorted(times.items(), key=lambda kv: kv[1])) + f" -> {pick}",
+                  file=sys.stderr)
     if cfg.metrics_log:
         from flexmi.utils.log import MetricsLogger
         mlog = MetricsLogger(cfg.metrics_log, cfg)

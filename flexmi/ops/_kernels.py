@@ -503,23 +503,103 @@ def _s2d_operands(x, w, plan, pads, saved):
     return xs, ws
 
 
-def conv2d_forward(x, w, b, y, stride, pads, act, groups, saved=None):
-    """Implicit-GEMM convolution on MFMA straight from NCHW (csrc/kernels/conv_igemm.hip): the
-    image operand is gathered into LDS per tile, bias + activation fused into the NCHW store.
-    pads = (top, bottom, left, right) of this shard (bottom / right are implied by y's extent).
-    Strided stems on few channels go through space-to-depth onto the stride-1 pixel-vector path."""
-    assert groups == 1, "grouped convolution is not supported on the HIP path"
-    w = w.contiguous()
+# ---- per-layer measured convolution algorithms ---------------------------------------------------
+# The reference times cuDNN's candidate algorithms per conv layer at init and keeps the fastest for the
+# forward, filter-gradient and data-gradient passes (src/ops/conv_2d.cu:216-243, :332-347, :872-930:
+# cudnnFind*AlgorithmEx).  flexmi does the same over its own MFMA convolution forms: the first eager
+# call of a layer's forward / backward times every applicable form on the layer's real operands
+# (CUDA events, outputs into scratch, accumulating gradients untouched) and records the fastest in the
+# op's context; later calls (and the hipGraph capture) run the recorded form.  Forms:
+#   nhwc      NHWC-staged implicit GEMM (conv_nhwc.hip; >= 16 input channels, bf16)
+#   igemm     NCHW implicit GEMM (conv_igemm.hip; any shape) -- strided 1x1 forward and strided
+#             backward through the stride-phase decomposition when phase=True
+#   s2d       space-to-depth of a strided few-channel stem onto the stride-1 NCHW kernels
+#   s2d_nhwc  the same re-laid stem on the NHWC kernels (the space-to-depth input has s*s*Cin channels)
+# FM_CONV_TUNE=0: no timing, the fixed heuristic order (nhwc > s2d > igemm).  Layers whose NHWC images
+# are shared with a neighbour (the executor's conv chain fusion) keep the nhwc form.
+CONV_TUNE = os.environ.get("FM_CONV_TUNE", "1") != "0"
+CONV_TUNE_LOG = []      # (direction, key, {form: us}, chosen): what the tuner measured (tests, reports)
+
+
+def _chained(saved):
+    return saved is not None and any(k in saved for k in ("nhwc_out2", "nhwc_x_prestaged", "nhwc_dgrad_out2",
+                                                          "nhwc_g_prestaged"))
+
+
+def conv_forms(x, w, y, stride, groups, direction="fwd"):
+    """Applicable convolution forms of one layer, in the heuristic's preference order."""
+    out = []
     if _nhwc_ok(x, w, groups):
-        _nhwc_forward(x, w, b, y, stride, pads, act, saved)
-        return
+        out.append("nhwc")
     plan = _s2d_plan(x, w, y, stride)
     if plan is not None:
+        out.append("s2d")
+        if NHWC_CONV and w.shape[1] * plan[0] * plan[0] >= 16:
+            out.append("s2d_nhwc")
+    out.append("igemm")
+    return out
+
+
+def _time_us(fn, reps=3):
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / reps
+
+
+def _conv_choose(saved, direction, forms, run, key):
+    """The form recorded for this layer and direction, measuring the candidates on first use."""
+    name = "conv_form_" + direction
+    if saved is not None and saved.get(name) in forms:
+        return saved[name]
+    pick = forms[0]
+    if (CONV_TUNE and len(forms) > 1 and saved is not None and not _chained(saved) and torch.cuda.is_available()
+            and not torch.cuda.is_current_stream_capturing()):
+        times = {f: _time_us(lambda f=f: run(f)) for f in forms}
+        pick = min(times, key=times.get)
+        CONV_TUNE_LOG.append((direction, key, times, pick))
+    if saved is not None:
+        saved[name] = pick
+    return pick
+
+
+def conv2d_forward(x, w, b, y, stride, pads, act, groups, saved=None, form=None):
+    """Implicit-GEMM convolution on MFMA: the form measured fastest for this layer (see
+    conv_forms / _conv_choose; ``form`` forces one).  pads = (top, bottom, left, right) of this
+    shard (bottom / right are implied by y's extent)."""
+    assert groups == 1, "grouped convolution is not supported on the HIP path"
+    w = w.contiguous()
+    forms = conv_forms(x, w, y, stride, groups)
+    if form is None:
+        if _chained(saved) or len(forms) == 1:
+            form = forms[0]
+        else:
+            # candidates write a scratch output and keep no staged state for the backward
+            ys = scratch(y.device, "conv_tune_y", y.numel(), y.dtype).view(y.shape)
+            key = (tuple(x.shape), tuple(w.shape), tuple(stride), tuple(pads), str(x.dtype))
+            form = _conv_choose(saved, "fwd", forms, lambda f: _conv_fwd_run(f, x, w, b, ys, stride, pads, act, None), key)
+    _conv_fwd_run(form, x, w, b, y, stride, pads, act, saved)
+
+
+def _conv_fwd_run(form, x, w, b, y, stride, pads, act, saved):
+    if form == "nhwc":
+        _nhwc_forward(x, w, b, y, stride, pads, act, saved)
+        return
+    if form in ("s2d", "s2d_nhwc"):
+        plan = _s2d_plan(x, w, y, stride)
         xs, ws = _s2d_operands(x, w, plan, pads, saved)
         C().conv_s2d(x, xs, plan[0], pads[0], pads[2], False, False)
         C().conv_w_s2d(w, ws, ws, ws, plan[0], False)
         if saved is not None:
             saved["s2d_ready"] = True
+        if form == "s2d_nhwc":
+            # the re-laid stem's NHWC staging is not kept (its geometry is the s2d image's, not x's)
+            _nhwc_forward(xs, ws, b, y, (1, 1), (0, 0, 0, 0), act, None)
+            return
         x, w, stride, pads = xs, ws, (1, 1), (0, 0, 0, 0)
     Kout, Cg, R, S = w.shape
     if (PHASE_CONV and R == 1 and S == 1 and stride[0] == stride[1] and stride[0] > 1 and x.dtype == torch.bfloat16):
@@ -537,18 +617,54 @@ def conv2d_forward(x, w, b, y, stride, pads, act, groups, saved=None):
     C().conv_fwd(x, w, wpad, b, y, stride[0], stride[1], pads[0], pads[2], int(act))
 
 
-def conv2d_backward(x, w, y, dy, dx, dw, db, stride, pads, act, groups, acc, saved=None):
-    """G = act'(y) * dY with db = sum G (one pass; skipped for a linear conv without bias), then
-    dW += G (x) X and dX (+)= Wt (x) G as implicit GEMMs -- no columns, no transposes."""
+def conv2d_backward(x, w, y, dy, dx, dw, db, stride, pads, act, groups, acc, saved=None, form=None):
+    """G = act'(y) * dY with db = sum G, then dW += G (x) X and dX (+)= Wt (x) G, in the form measured
+    fastest for this layer's backward (candidates run on scratch gradients: dW / db / an accumulated
+    dX are touched only by the chosen form)."""
     assert groups == 1, "grouped convolution is not supported on the HIP path"
     w = w.contiguous()
-    if _nhwc_ok(x, w, groups) and _nhwc_backward(x, w, y, dy, int(act), db, dx, dw, stride, pads, acc, saved):
-        return
+    forms = conv_forms(x, w, y, stride, groups, "bwd")
+    if form is None:
+        if _chained(saved) or len(forms) == 1:
+            form = forms[0]
+        else:
+            dws = scratch(x.device, "conv_tune_dw", dw.numel(), dw.dtype).view(dw.shape)
+            dbs = scratch(x.device, "conv_tune_db", db.numel(), db.dtype).view(db.shape) if db is not None else None
+            dxs = scratch(x.device, "conv_tune_dx", dx.numel(), dx.dtype).view(dx.shape) if dx is not None else None
+            key = (tuple(x.shape), tuple(w.shape), tuple(stride), tuple(pads), str(x.dtype), dx is not None)
+            form = _conv_choose(saved, "bwd", forms,
+                                lambda f: _conv_bwd_run(f, x, w, y, dy, dxs, dws, dbs, stride, pads, act, False, None),
+                                key)
+    if not _conv_bwd_run(form, x, w, y, dy, dx, dw, db, stride, pads, act, acc, saved):
+        _conv_bwd_run("igemm", x, w, y, dy, dx, dw, db, stride, pads, act, acc, saved)
+
+
+def _conv_bwd_run(form, x, w, y, dy, dx, dw, db, stride, pads, act, acc, saved):
+    """One backward form; False when it does not apply to this layout (the caller falls back)."""
+    if form == "nhwc":
+        return _nhwc_backward(x, w, y, dy, int(act), db, dx, dw, stride, pads, acc, saved)
+    plan = _s2d_plan(x, w, y, stride) if form in ("s2d", "s2d_nhwc") else None
+    if plan is not None and form == "s2d_nhwc":
+        s_, Hs, Ws, Rs, Ss = plan
+        xs, ws = _s2d_operands(x, w, plan, pads, saved)
+        if not (saved is not None and saved.get("s2d_ready")):
+            C().conv_s2d(x, xs, s_, pads[0], pads[2], False, False)
+        C().conv_w_s2d(w, ws, ws, ws, s_, False)
+        dws = scratch(x.device, "conv_s2d_dw", ws.numel(), torch.float32).view(ws.shape)
+        dws.zero_()
+        dxs = scratch(x.device, "conv_s2d_dx", xs.numel(), xs.dtype).view(xs.shape) if dx is not None else None
+        if not _nhwc_backward(xs, ws, y, dy, int(act), db, dxs, dws, (1, 1), (0, 0, 0, 0), False, None):
+            return False
+        C().conv_w_s2d(w, ws, dws.view(-1), dw.view(-1), s_, True)
+        if dx is not None:
+            if not acc:
+                dx.zero_()
+            C().conv_s2d(dx, dxs, s_, pads[0], pads[2], True, True)
+        return True
     g = dy
     if int(act) != 10 or db is not None:
         g = scratch(x.device, "conv_g", dy.numel(), dy.dtype).view(dy.shape) if int(act) != 10 else dy
         C().conv_act_bwd(dy, y, g, db, int(act))
-    plan = _s2d_plan(x, w, y, stride)
     if plan is not None:
         s_, Hs, Ws, Rs, Ss = plan
         xs, ws = _s2d_operands(x, w, plan, pads, saved)
@@ -566,16 +682,17 @@ def conv2d_backward(x, w, y, dy, dx, dw, db, stride, pads, act, groups, acc, sav
             if not acc:
                 dx.zero_()
             C().conv_s2d(dx, dxs, s_, pads[0], pads[2], True, True)
-        return
+        return True
     Kout, Cg, R, S = w.shape
     if PHASE_CONV and stride[0] == stride[1] and stride[0] > 1 and x.dtype == torch.bfloat16:
         _conv_backward_phases(x, w, g, dx, dw, stride[0], pads, acc)
-        return
+        return True
     # dW / db ACCUMULATE into the per-step zeroed gradient buffer (tied weights sum their grads)
     C().conv_wgrad(g, x, dw.view(-1), R, S, stride[0], stride[1], pads[0], pads[2])
     if dx is not None:
         wt = scratch(x.device, "conv_wt", C().conv_scratch(Cg, Kout * R * S), w.dtype)
         C().conv_dgrad(g, w, wt, dx, stride[0], stride[1], pads[0], pads[2], bool(acc))
+    return True
 
 
 # Stride-phase decomposition of a strided convolution's backward (FM_CONV_PHASE=0: the strided

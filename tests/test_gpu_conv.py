@@ -10,6 +10,13 @@ import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _no_conv_tune(monkeypatch):
+    """These tests target specific convolution paths: the heuristic form, no per-layer timing."""
+    from flexmi.ops import _kernels as Kk
+    monkeypatch.setattr(Kk, "CONV_TUNE", False)
+
 CASES = [
     # N, C, H, W, K, R, S, sh, sw, pads(t,b,l,r)
     (2, 3, 67, 67, 64, 11, 11, 4, 4, (2, 2, 2, 2)),     # AlexNet stem (small image)

@@ -12,6 +12,13 @@ import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _no_conv_tune(monkeypatch):
+    """These tests target specific convolution paths: the heuristic form, no per-layer timing."""
+    from flexmi.ops import _kernels as Kk
+    monkeypatch.setattr(Kk, "CONV_TUNE", False)
+
 CASES = [
     # N, C, H, W, K, R, S, stride, pads (t, b, l, r)
     (2, 64, 14, 14, 64, 3, 3, 1, (1, 1, 1, 1)),       # ResNet 3x3

@@ -9,6 +9,13 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _no_conv_tune(monkeypatch):
+    """These tests target specific convolution paths: the heuristic form, no per-layer timing."""
+    from flexmi.ops import _kernels as Kk
+    monkeypatch.setattr(Kk, "CONV_TUNE", False)
+
+
 @pytest.mark.parametrize("N,C,H,W,K,R,S,s,pt,pl", [
     (2, 16, 14, 14, 32, 3, 3, 2, 1, 1),     # ResNet downsampling 3x3/2
     (2, 32, 14, 14, 16, 1, 1, 2, 0, 0),     # ResNet 1x1/2 shortcut
