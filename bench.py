@@ -14,18 +14,26 @@ bucketed all-reduce).
     python bench.py --gpus N --steps K --warmup W          (N>1 under torch.distributed.run)
 
 Precision: the headline ``value`` is the REFERENCE precision, fp32 end to end (the reference is
-fp32 everywhere: cublasSgemm / cuDNN FLOAT) -- fp32 activations, fp32 weights,
-GEMMs on the exact f32-input MFMA (v_mfma_f32_16x16x4_f32).  The bf16 fast mode (bf16
-activations / MFMA operands, fp32 master weights and accumulation) is measured afterwards in the
-same process and reported as a secondary field ``config.bf16`` (``--dtype bf16`` makes it the
-headline, ``--no-secondary`` skips it).
+fp32 everywhere: cublasSgemm / cuDNN FLOAT) -- fp32 activations, fp32 weights, fp32
+tables.  The big Linear GEMMs run the exact three-way split on the bf16 matrix cores (every fp32
+operand split into three bf16 planes, the six products that matter, each exact in fp32, fp32
+accumulation: csrc/kernels/gemm_x3.hip), the small ones the f32-input MFMA
+(v_mfma_f32_16x16x4_f32); both are tested against float64 at the native fp32 kernel's accuracy
+and the record names the engine in ``config.fp32_gemm``.  The bf16 fast mode (bf16 activations /
+MFMA operands, fp32 master weights and accumulation) is measured afterwards in the same process
+and reported as a secondary field ``config.bf16`` (``--dtype bf16`` makes it the headline,
+``--no-secondary`` skips it).
 
 Plans (N > 1): the headline is the SOAP-SEARCHED plan (``--strategy search``, the default): rank 0
 runs the MCMC search over the MI355X execution simulator (budget ``--search-budget``, seeded with the
 hand plan; the reference's FFModel::optimize, src/runtime/model.cc:1093-1144) and every rank trains
 with that plan; ``config.search`` carries the simulated speedup, budget and wall seconds.  The hand
 plan the search was seeded with (table-wise / column-split embeddings + DP MLPs, dlrm_strategy) is
-then timed as ``config.table`` (``config.search_speedup_vs_table``).
+then timed as ``config.table`` (``config.search_speedup_vs_table``).  Before training, the pick is
+re-simulated against the table plan with every xGMI / all-reduce constant of the (spec-based)
+machine model at 0.5x and 2x; if it loses more than ``--robust-threshold`` (10 %) in any corner the
+headline runs the table plan instead (``config.search.sensitivity``, parallelism
+``soap-searchN-robust-table``; profiles/search_sensitivity_mlperf.txt).
 
 SOAP vs DP (N > 1): after the headline plan, the same model / precision / batch is built and timed
 under pure data parallelism -- every table replicated on every GPU and trained by touched-row

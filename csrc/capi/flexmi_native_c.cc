@@ -569,6 +569,27 @@ int fmn_model_dense(fmn_model_t m, int input_tensor, int out_dim, int activation
   return guarded([&] { return m->m->dense(input_tensor, out_dim, activation, use_bias != 0); }, -1);
 }
 
+int fmn_model_input_image(fmn_model_t m, int channels, int height, int width) {
+  if (!m) return fail("fmn_model_input_image: null model");
+  return guarded([&] { return m->m->input_image(channels, height, width); }, -1);
+}
+
+int fmn_model_conv2d(fmn_model_t m, int input_tensor, int out_channels, int kernel_h, int kernel_w, int stride_h,
+                     int stride_w, int pad_h, int pad_w, int activation, int use_bias) {
+  if (!m) return fail("fmn_model_conv2d: null model");
+  return guarded([&] {
+    return m->m->conv2d(input_tensor, out_channels, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, activation,
+                        use_bias != 0);
+  }, -1);
+}
+
+int fmn_model_pool2d(fmn_model_t m, int input_tensor, int kernel_h, int kernel_w, int stride_h, int stride_w, int pad_h,
+                     int pad_w, int is_max) {
+  if (!m) return fail("fmn_model_pool2d: null model");
+  return guarded([&] { return m->m->pool2d(input_tensor, kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, is_max != 0); },
+                 -1);
+}
+
 int fmn_model_sparse_input(fmn_model_t m, int bag) {
   if (!m) return fail("fmn_model_sparse_input: null model");
   return guarded([&] { return m->m->sparse_input(bag); }, -1);

@@ -155,6 +155,16 @@ void fmn_model_destroy(fmn_model_t m);
  * 11 relu, 12 sigmoid, 13 tanh) */
 int fmn_model_input(fmn_model_t m, int features);
 int fmn_model_dense(fmn_model_t m, int input_tensor, int out_dim, int activation, int use_bias);
+/* CNN graphs (data parallel): an image input [B][C][H][W] (NCHW, train_step takes the global batch
+ * of C*H*W features per sample), 2-D convolutions (out channels, kernel, stride, symmetric zero
+ * padding, fused bias + activation) and poolings (is_max 1: max, 0: average excluding the
+ * padding) -> their [B][C'][P][Q] tensor ids; dense layers take them flattened.  Reference:
+ * FFModel::conv2d / pool2d (include/model.h, src/ops/conv_2d.cu, src/ops/pool_2d.cu). */
+int fmn_model_input_image(fmn_model_t m, int channels, int height, int width);
+int fmn_model_conv2d(fmn_model_t m, int input_tensor, int out_channels, int kernel_h, int kernel_w, int stride_h,
+                     int stride_w, int pad_h, int pad_w, int activation, int use_bias);
+int fmn_model_pool2d(fmn_model_t m, int input_tensor, int kernel_h, int kernel_w, int stride_h, int stride_w, int pad_h,
+                     int pad_w, int is_max);
 /* DLRM graphs: a sparse input (int64 [B][bag] lookup indices of the GLOBAL batch) -> its id; an
  * embedding table rows x dim over a sparse input (SUM bag) -> its [B][dim] tensor id; the dot
  * interaction of a bottom tensor and n embedding tensors -> its [B][W] tensor id (W = dim +

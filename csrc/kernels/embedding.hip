@@ -415,7 +415,7 @@ __global__ void __launch_bounds__(256) fm_emb_owner_multi(ClaimSet s, const floa
   if (blockIdx.x == 0 && threadIdx.x == 0) *d.ndup = 0;   // the dup kernel has finished reading it
 }
 
-// ---- count-based sparse SGD (FM_EMB_BWD=count): two launches for every non-tiny table ---------
+// ---- count-based sparse SGD (fm_embedding_set_bwd_mode(1)): two launches for every non-tiny table ---
 // count: every in-shard lookup e adds one to its row's slot (slot = lookups - 1; -1 = untouched)
 // and records in own[e] (the dups array) whether it arrived first.  update: a lookup whose row was
 // hit exactly once (slot == 0) applies a plain 16-B read-modify-write and frees the slot; rows hit
@@ -515,7 +515,7 @@ void launch_bwd(const TabSet& s, int m, bool tiny, bool dy_bf16, const float* lr
     size_t lds = 0;
     for (int i = 0; i < m; ++i) lds = std::max(lds, (size_t)s.t[i].rows * s.t[i].D * 4 * 4);  // one copy per wave
     static bool attr = false;
-    if (!attr) {   // > 64 KiB of dynamic LDS (FM_EMB_TINY_ROWS above 32 at D = 128) needs the opt-in
+    if (!attr) {   // > 64 KiB of dynamic LDS (above 32 rows at D = 128) needs the opt-in
       (void)hipFuncSetAttribute((const void*)fm_emb_bwd_tiny_multi<unsigned short, I64>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10);
       (void)hipFuncSetAttribute((const void*)fm_emb_bwd_tiny_multi<float, I64>,
@@ -685,7 +685,7 @@ extern "C" void fm_embedding_fwd_multi(int n, const float* const* W, const void*
   }
 }
 
-static int g_emb_count = -1;   // -1: from FM_EMB_BWD at the first call
+static int g_emb_count = 0;    // fm_embedding_set_bwd_mode: 1 = the count / update pair
 extern "C" void fm_embedding_set_bwd_mode(int count) { g_emb_count = count ? 1 : 0; }
 
 // lr != nullptr: fused sparse SGD into W; lr == nullptr: W is a dense grad buffer (accumulate).
@@ -694,9 +694,8 @@ extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const
                                        const int* bag, const float* scale, int dy_bf16, const float* lr, long B,
                                        int* const* owner, int* const* dups, int* const* ndup, hipStream_t st) {
   if (B <= 0) return;
-  // owner-computes path: fused SGD, claim buffers given, 16-B rows; FM_EMB_BWD=count: the
-  // count / update pair instead of claim / dup / owner (the buffers are the same)
-  if (g_emb_count < 0) g_emb_count = getenv("FM_EMB_BWD") != nullptr && strcmp(getenv("FM_EMB_BWD"), "count") == 0;
+  // owner-computes path: fused SGD, claim buffers given, 16-B rows; count mode: the count / update
+  // pair instead of claim / dup / owner (the buffers are the same)
   const bool count_mode = g_emb_count == 1;
   auto claimable = [&](int k) {
     return lr != nullptr && owner != nullptr && owner[k] != nullptr && D[k] % 4 == 0 && ldg[k] % 4 == 0 &&
@@ -732,12 +731,12 @@ extern "C" void fm_embedding_bwd_multi(int n, float* const* W, const void* const
   // block-shared LDS copy for 36..155-row tables (113 vs 16.6 us of regular atomics) and row-block
   // ownership for <= 8192-row tables (76 vs 48 us; profiles/emb_bwd_rowblock_r5u.jsonl)
   auto kind_of = [&](int k) {
-    // FM_EMB_TINY_ROWS (default 64): the wave-private LDS kernel up to that many rows while its four
-    // copies fit the LDS (rows * D * 16 B).  64 takes the 36- and 63-row MLPerf tables off the
-    // same-address atomics: slower alone (35.5 vs 32.3 us for the eight <= 155-row tables) but less
-    // contention beside the bottom-MLP backward, step 1.145-1.164 vs 1.170-1.173 ms at 16
-    // (profiles/emb_tiny_rows_ab_r5tr.txt)
-    static const int tiny_rows = getenv("FM_EMB_TINY_ROWS") ? atoi(getenv("FM_EMB_TINY_ROWS")) : 64;
+    // the wave-private LDS kernel up to TINY_ROWS rows while its four copies fit the LDS (rows * D *
+    // 16 B).  64 takes the 36- and 63-row MLPerf tables off the same-address atomics: slower alone
+    // (35.5 vs 32.3 us for the eight <= 155-row tables) but less contention beside the bottom-MLP
+    // backward, step 1.145-1.164 vs 1.170-1.173 ms at 16 (profiles/emb_tiny_rows_ab_r5tr.txt).  A
+    // block-shared copy with LDS float atomics for <= 160 rows measured 93.5 vs 30.5 us (r7, removed).
+    constexpr int tiny_rows = 64;
     if (rows[k] <= tiny_rows && (long)rows[k] * D[k] * 16 <= (160L << 10) && D[k] <= 256 &&
         B * (long)bag[k] >= 16L * rows[k])
       return 0;

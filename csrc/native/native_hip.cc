@@ -10,6 +10,8 @@
 //   embeddings     fm_embedding_fwd (global-batch lookups on the owner), fm_embedding_bwd with a
 //                  device lr (fused sparse SGD of the touched rows); fm_dot_interaction_{fwd,bwd}_f32
 //                  (v_mfma_f32_32x32x2_f32); the exchange = RCCL grouped send / recv per peer
+//   convolutions   fm_conv_fwd / fm_conv_act_bwd / fm_conv_wgrad / fm_conv_dgrad (fp32 implicit GEMM
+//                  on MFMA), fm_pool_fwd / fm_pool_bwd -- the Python executor's Conv2D / Pool2D kernels
 //   communication  one RCCL communicator per model (unique id handed over through a file in the
 //                  rendezvous directory); bucket all-reduces on a second HIP stream, started as
 //                  soon as the bucket's last gradient kernel is enqueued (event dependency) and
@@ -60,6 +62,20 @@ void fm_dot_interaction_fwd_f32(const float* const* z, int F, long ldz, float* o
                                 hipStream_t s);
 void fm_dot_interaction_bwd_f32(const float* const* z, int F, long ldz, const float* dout, long ldo, float* const* dz,
                                 long lddz, unsigned acc_mask, long B, int D, int self, int act0, hipStream_t s);
+int fm_conv_lda(int cols);
+int fm_conv_fwd(const void* x, const void* w, void* wpad, const float* bias, void* y, int bf16, int N, int C, int H, int W,
+                int K, int R, int S, int P, int Q, int sh, int sw, int pt, int pl, int act, hipStream_t s);
+int fm_conv_dgrad(const void* g, const void* w, void* wt, void* dx, int accum, int bf16, int N, int C, int H, int W, int K,
+                  int R, int S, int P, int Q, int sh, int sw, int pt, int pl, hipStream_t s);
+int fm_conv_wgrad(const void* g, const void* x, float* dw, int bf16, int N, int C, int H, int W, int K, int R, int S, int P,
+                  int Q, int sh, int sw, int pt, int pl, hipStream_t s);
+void fm_conv_act_bwd(const void* dy, const void* y, void* g, float* db, int bf16, int N, int K, int PQ, int act,
+                     hipStream_t s);
+void fm_pool_fwd(const void* x, void* y, unsigned char* code, int N, int C, int H, int W, int P, int Q, int kh, int kw,
+                 int sh, int sw, int pt, int pl, int is_max, int act, int bf16, hipStream_t st);
+void fm_pool_bwd(const void* x, const void* y, const void* dy, void* dx, unsigned char* code, int code_ready, int N, int C,
+                 int H, int W, int P, int Q, int kh, int kw, int sh, int sw, int pt, int pl, int is_max, int act, int acc,
+                 int bf16, hipStream_t st);
 }
 
 namespace flexmi {
@@ -100,6 +116,8 @@ class HipEngine : public Engine {
     for (auto e : events_) hipEventDestroy(e);
     if (comm_) ncclCommDestroy(comm_);
     hipFree(ws_);
+    for (float* b : bufs_)
+      if (b) hipFree(b);
     hipFree(slots_);
     hipFree(lr_);
     hipStreamDestroy(comm_st_);
@@ -217,6 +235,37 @@ class HipEngine : public Engine {
     NCCLX(ncclGroupEnd());
   }
 
+  // convolutions on flexmi's implicit-GEMM MFMA kernels (conv_igemm.hip, fp32 operands), pooling on
+  // cnn.hip -- the kernels the Python executor's Conv2D / Pool2D ops run
+  void conv_fwd(const float* x, const float* W, const float* b, float* y, int N, const Conv& c) override {
+    float* wpad = buf(1, (size_t)c.K * fm_conv_lda(c.C * c.R * c.S));
+    if (fm_conv_fwd(x, W, wpad, b, y, 0, N, c.C, c.H, c.W, c.K, c.R, c.S, c.P, c.Q, c.sh, c.sw, c.ph, c.pw, c.act, st_) != 0)
+      throw std::runtime_error("native hip engine: conv forward");
+  }
+  void conv_bwd(const float* x, const float* W, const float* y, const float* dy, float* dx, float* dW, float* db, int N,
+                const Conv& c) override {
+    const float* g = dy;
+    if (c.act != ACT_NONE || db) {
+      float* t = c.act != ACT_NONE ? buf(0, (size_t)N * c.K * c.P * c.Q) : nullptr;
+      fm_conv_act_bwd(dy, y, t ? t : const_cast<float*>(dy), db, 0, N, c.K, c.P * c.Q, c.act, st_);
+      if (t) g = t;
+    }
+    if (fm_conv_wgrad(g, x, dW, 0, N, c.C, c.H, c.W, c.K, c.R, c.S, c.P, c.Q, c.sh, c.sw, c.ph, c.pw, st_) != 0)
+      throw std::runtime_error("native hip engine: conv weight gradient");
+    if (!dx) return;
+    float* wt = buf(2, (size_t)c.C * fm_conv_lda(c.K * c.R * c.S));
+    if (fm_conv_dgrad(g, W, wt, dx, 0, 0, N, c.C, c.H, c.W, c.K, c.R, c.S, c.P, c.Q, c.sh, c.sw, c.ph, c.pw, st_) != 0)
+      throw std::runtime_error("native hip engine: conv data gradient");
+  }
+  void pool_fwd(const float* x, float* y, unsigned char* code, int N, const Pool& p) override {
+    fm_pool_fwd(x, y, code, N, p.C, p.H, p.W, p.P, p.Q, p.kh, p.kw, p.sh, p.sw, p.ph, p.pw, p.max ? 1 : 0, ACT_NONE, 0, st_);
+  }
+  void pool_bwd(const float* x, const float* y, const float* dy, float* dx, const unsigned char* code, int N,
+                const Pool& p) override {
+    fm_pool_bwd(x, y, dy, dx, const_cast<unsigned char*>(code), 1, N, p.C, p.H, p.W, p.P, p.Q, p.kh, p.kw, p.sh, p.sw, p.ph,
+                p.pw, p.max ? 1 : 0, ACT_NONE, 0, 0, st_);
+  }
+
   void allreduce_start(float* buf, int64_t n) override {
     if (!comm_) return;
     hipEvent_t ready = event();
@@ -249,6 +298,18 @@ class HipEngine : public Engine {
       events_.push_back(e);
     }
     return events_[ev_next_++];
+  }
+  // grow-only scratch slots (0: conv act' gradient, 1 / 2: repacked conv kernels)
+  float* buf(int k, size_t n) {
+    if (n > bufn_[k]) {
+      if (bufs_[k]) {
+        HIPX(hipStreamSynchronize(st_));
+        hipFree(bufs_[k]);
+      }
+      HIPX(hipMalloc(&bufs_[k], n * sizeof(float)));
+      bufn_[k] = n;
+    }
+    return bufs_[k];
   }
   float* scratch(size_t n) {
     if (n > scratch_n_) {
@@ -297,6 +358,8 @@ class HipEngine : public Engine {
   float lr_host_ = -1.f;
   float* scratch_ = nullptr;
   size_t scratch_n_ = 0;
+  float* bufs_[3] = {nullptr, nullptr, nullptr};
+  size_t bufn_[3] = {0, 0, 0};
   std::vector<hipEvent_t> events_;
   size_t ev_next_ = 0;
   bool pending_ = false;

@@ -229,6 +229,140 @@ class CpuEngine : public Engine {
     }
     std::memcpy(recv, send, (size_t)send_counts[0] * sizeof(float));
   }
+  // direct convolution loops (double accumulation: the reference result the executor's torch
+  // convolution is compared against)
+  void conv_fwd(const float* x, const float* W, const float* b, float* y, int N, const Conv& c) override {
+    for (int n = 0; n < N; ++n)
+      for (int k = 0; k < c.K; ++k)
+        for (int p = 0; p < c.P; ++p)
+          for (int q = 0; q < c.Q; ++q) {
+            double s = b ? b[k] : 0.0;
+            for (int ch = 0; ch < c.C; ++ch)
+              for (int r = 0; r < c.R; ++r) {
+                const int h = p * c.sh - c.ph + r;
+                if (h < 0 || h >= c.H) continue;
+                for (int t = 0; t < c.S; ++t) {
+                  const int w = q * c.sw - c.pw + t;
+                  if (w < 0 || w >= c.W) continue;
+                  s += (double)x[(((int64_t)n * c.C + ch) * c.H + h) * c.W + w] *
+                       W[(((int64_t)k * c.C + ch) * c.R + r) * c.S + t];
+                }
+              }
+            y[(((int64_t)n * c.K + k) * c.P + p) * c.Q + q] = act_f(c.act, (float)s);
+          }
+  }
+  void conv_bwd(const float* x, const float* W, const float* y, const float* dy, float* dx, float* dW, float* db, int N,
+                const Conv& c) override {
+    const int64_t ny = (int64_t)N * c.K * c.P * c.Q;
+    std::vector<float> g(ny);
+    for (int64_t i = 0; i < ny; ++i) g[i] = act_b(c.act, y[i], dy[i]);
+    auto G = [&](int n, int k, int p, int q) { return g[(((int64_t)n * c.K + k) * c.P + p) * c.Q + q]; };
+    for (int k = 0; k < c.K; ++k) {
+      if (db) {
+        double s = 0.0;
+        for (int n = 0; n < N; ++n)
+          for (int p = 0; p < c.P; ++p)
+            for (int q = 0; q < c.Q; ++q) s += G(n, k, p, q);
+        db[k] += (float)s;
+      }
+      for (int ch = 0; ch < c.C; ++ch)
+        for (int r = 0; r < c.R; ++r)
+          for (int t = 0; t < c.S; ++t) {
+            double s = 0.0;
+            for (int n = 0; n < N; ++n)
+              for (int p = 0; p < c.P; ++p) {
+                const int h = p * c.sh - c.ph + r;
+                if (h < 0 || h >= c.H) continue;
+                for (int q = 0; q < c.Q; ++q) {
+                  const int w = q * c.sw - c.pw + t;
+                  if (w < 0 || w >= c.W) continue;
+                  s += (double)G(n, k, p, q) * x[(((int64_t)n * c.C + ch) * c.H + h) * c.W + w];
+                }
+              }
+            dW[(((int64_t)k * c.C + ch) * c.R + r) * c.S + t] += (float)s;
+          }
+    }
+    if (!dx) return;
+    std::vector<double> acc((size_t)N * c.C * c.H * c.W, 0.0);
+    for (int n = 0; n < N; ++n)
+      for (int k = 0; k < c.K; ++k)
+        for (int p = 0; p < c.P; ++p)
+          for (int q = 0; q < c.Q; ++q) {
+            const double gv = G(n, k, p, q);
+            if (gv == 0.0) continue;
+            for (int ch = 0; ch < c.C; ++ch)
+              for (int r = 0; r < c.R; ++r) {
+                const int h = p * c.sh - c.ph + r;
+                if (h < 0 || h >= c.H) continue;
+                for (int t = 0; t < c.S; ++t) {
+                  const int w = q * c.sw - c.pw + t;
+                  if (w < 0 || w >= c.W) continue;
+                  acc[(((size_t)n * c.C + ch) * c.H + h) * c.W + w] += gv * W[(((int64_t)k * c.C + ch) * c.R + r) * c.S + t];
+                }
+              }
+          }
+    for (size_t i = 0; i < acc.size(); ++i) dx[i] = (float)acc[i];
+  }
+  void pool_fwd(const float* x, float* y, unsigned char* code, int N, const Pool& pl) override {
+    for (int n = 0; n < N; ++n)
+      for (int ch = 0; ch < pl.C; ++ch) {
+        const float* xc = x + ((int64_t)n * pl.C + ch) * pl.H * pl.W;
+        for (int p = 0; p < pl.P; ++p)
+          for (int q = 0; q < pl.Q; ++q) {
+            float best = -INFINITY;
+            int arg = 0, cnt = 0;
+            double sum = 0.0;
+            for (int r = 0; r < pl.kh; ++r) {
+              const int h = p * pl.sh - pl.ph + r;
+              if (h < 0 || h >= pl.H) continue;
+              for (int t = 0; t < pl.kw; ++t) {
+                const int w = q * pl.sw - pl.pw + t;
+                if (w < 0 || w >= pl.W) continue;
+                const float v = xc[(int64_t)h * pl.W + w];
+                if (v > best) {
+                  best = v;
+                  arg = r * pl.kw + t;
+                }
+                sum += v;
+                ++cnt;
+              }
+            }
+            const int64_t o = (((int64_t)n * pl.C + ch) * pl.P + p) * pl.Q + q;
+            y[o] = pl.max ? best : (float)(sum / std::max(cnt, 1));
+            if (code) code[o] = (unsigned char)arg;
+          }
+      }
+  }
+  void pool_bwd(const float* x, const float* y, const float* dy, float* dx, const unsigned char* code, int N,
+                const Pool& pl) override {
+    (void)x;
+    (void)y;
+    std::fill(dx, dx + (int64_t)N * pl.C * pl.H * pl.W, 0.f);
+    for (int n = 0; n < N; ++n)
+      for (int ch = 0; ch < pl.C; ++ch) {
+        float* dc = dx + ((int64_t)n * pl.C + ch) * pl.H * pl.W;
+        for (int p = 0; p < pl.P; ++p)
+          for (int q = 0; q < pl.Q; ++q) {
+            const int64_t o = (((int64_t)n * pl.C + ch) * pl.P + p) * pl.Q + q;
+            if (pl.max) {
+              const int r = code[o] / pl.kw, t = code[o] % pl.kw;
+              dc[(int64_t)(p * pl.sh - pl.ph + r) * pl.W + (q * pl.sw - pl.pw + t)] += dy[o];
+              continue;
+            }
+            int cnt = 0;
+            for (int r = 0; r < pl.kh; ++r)
+              for (int t = 0; t < pl.kw; ++t) {
+                const int h = p * pl.sh - pl.ph + r, w = q * pl.sw - pl.pw + t;
+                cnt += h >= 0 && h < pl.H && w >= 0 && w < pl.W;
+              }
+            for (int r = 0; r < pl.kh; ++r)
+              for (int t = 0; t < pl.kw; ++t) {
+                const int h = p * pl.sh - pl.ph + r, w = q * pl.sw - pl.pw + t;
+                if (h >= 0 && h < pl.H && w >= 0 && w < pl.W) dc[(int64_t)h * pl.W + w] += dy[o] / (float)std::max(cnt, 1);
+              }
+          }
+      }
+  }
 
  private:
   std::unique_ptr<HostComm> comm_;
@@ -282,6 +416,7 @@ Model::~Model() {
   rel(probs_);
   rel(labels_);
   rel(stats_);
+  for (auto* p : pool_code_) rel(p);
 }
 
 void Model::check_tensor(int t, const char* what) const {
@@ -289,12 +424,97 @@ void Model::check_tensor(int t, const char* what) const {
   if (consumers_[t] > 0) throw std::invalid_argument(std::string("native model: tensor consumed twice (") + what + ")");
 }
 
+int Model::new_tensor(const std::vector<int>& shape) {
+  int64_t n = 1;
+  for (int v : shape) n *= v;
+  if (n <= 0 || n > (1LL << 30)) throw std::invalid_argument("native model: tensor shape");
+  cols_.push_back((int)n);
+  shape_.push_back(shape);
+  consumers_.push_back(0);
+  return (int)cols_.size() - 1;
+}
+
 int Model::input(int features) {
   if (compiled_ || input_ >= 0) throw std::logic_error("native model: one input, before compile");
-  cols_.push_back(features);
-  consumers_.push_back(0);
-  input_ = (int)cols_.size() - 1;
+  input_ = new_tensor({features});
   return input_;
+}
+
+int Model::input_image(int channels, int height, int width) {
+  if (compiled_ || input_ >= 0) throw std::logic_error("native model: one input, before compile");
+  if (channels <= 0 || height <= 0 || width <= 0) throw std::invalid_argument("native model: image shape");
+  input_ = new_tensor({channels, height, width});
+  return input_;
+}
+
+int Model::conv2d(int x, int out_channels, int kh, int kw, int sh, int sw, int ph, int pw, int act, bool bias) {
+  if (compiled_) throw std::logic_error("native model: conv2d after compile");
+  check_tensor(x, "conv2d");
+  if (shape_[x].size() != 3) throw std::invalid_argument("native model: conv2d needs an image tensor [C][H][W]");
+  if (act != ACT_NONE && act != ACT_RELU && act != ACT_SIGMOID && act != ACT_TANH)
+    throw std::invalid_argument("native model: activation");
+  Conv c;
+  c.x = x;
+  c.C = shape_[x][0];
+  c.H = shape_[x][1];
+  c.W = shape_[x][2];
+  c.K = out_channels;
+  c.R = kh;
+  c.S = kw;
+  c.sh = sh;
+  c.sw = sw;
+  c.ph = ph;
+  c.pw = pw;
+  c.act = act;
+  c.bias = bias;
+  if (out_channels <= 0 || kh <= 0 || kw <= 0 || sh <= 0 || sw <= 0 || ph < 0 || pw < 0)
+    throw std::invalid_argument("native model: conv2d geometry");
+  c.P = (c.H + 2 * ph - kh) / sh + 1;
+  c.Q = (c.W + 2 * pw - kw) / sw + 1;
+  if (c.P <= 0 || c.Q <= 0) throw std::invalid_argument("native model: conv2d output is empty");
+  consumers_[x]++;
+  c.y = new_tensor({c.K, c.P, c.Q});
+  c.w = (int)pnumel_.size();
+  pnumel_.push_back((int64_t)c.K * c.C * c.R * c.S);
+  entry_table_.push_back(-1);
+  entry_dense_.push_back(-1);
+  if (bias) {
+    c.b = (int)pnumel_.size();
+    pnumel_.push_back(c.K);
+    entry_table_.push_back(-1);
+    entry_dense_.push_back(-1);
+  }
+  convs_.push_back(c);
+  nodes_.push_back({K_CONV, (int)convs_.size() - 1});
+  return c.y;
+}
+
+int Model::pool2d(int x, int kh, int kw, int sh, int sw, int ph, int pw, bool max) {
+  if (compiled_) throw std::logic_error("native model: pool2d after compile");
+  check_tensor(x, "pool2d");
+  if (shape_[x].size() != 3) throw std::invalid_argument("native model: pool2d needs an image tensor [C][H][W]");
+  if (kh <= 0 || kw <= 0 || sh <= 0 || sw <= 0 || ph < 0 || pw < 0 || ph >= kh || pw >= kw || kh * kw > 255)
+    throw std::invalid_argument("native model: pool2d geometry");
+  Pool pl;
+  pl.x = x;
+  pl.C = shape_[x][0];
+  pl.H = shape_[x][1];
+  pl.W = shape_[x][2];
+  pl.kh = kh;
+  pl.kw = kw;
+  pl.sh = sh;
+  pl.sw = sw;
+  pl.ph = ph;
+  pl.pw = pw;
+  pl.max = max;
+  pl.P = (pl.H + 2 * ph - kh) / sh + 1;
+  pl.Q = (pl.W + 2 * pw - kw) / sw + 1;
+  if (pl.P <= 0 || pl.Q <= 0) throw std::invalid_argument("native model: pool2d output is empty");
+  consumers_[x]++;
+  pl.y = new_tensor({pl.C, pl.P, pl.Q});
+  pools_.push_back(pl);
+  nodes_.push_back({K_POOL, (int)pools_.size() - 1});
+  return pl.y;
 }
 
 int Model::dense(int x, int out_dim, int act, bool bias) {
@@ -309,9 +529,7 @@ int Model::dense(int x, int out_dim, int act, bool bias) {
   d.act = act;
   d.bias = bias;
   consumers_[x]++;
-  cols_.push_back(out_dim);
-  consumers_.push_back(0);
-  d.y = (int)cols_.size() - 1;
+  d.y = new_tensor({out_dim});
   d.w = (int)pnumel_.size();
   pnumel_.push_back((int64_t)d.N * d.K);
   entry_table_.push_back(-1);
@@ -345,9 +563,7 @@ int Model::embedding(int sparse, int64_t rows, int dim) {
   e.rows = rows;
   e.D = dim;
   e.bag = sparse_bag_[sparse];
-  cols_.push_back(dim);
-  consumers_.push_back(0);
-  e.y = (int)cols_.size() - 1;
+  e.y = new_tensor({dim});
   e.w = (int)pnumel_.size();
   pnumel_.push_back(rows * dim);
   entry_table_.push_back((int)embs_.size());
@@ -375,9 +591,7 @@ int Model::dot_interaction(int bottom, const std::vector<int>& embs, int pad_to)
   d.npairs = F * (F - 1) / 2;
   const int p = std::max(1, pad_to);
   d.W = (d.D + d.npairs + p - 1) / p * p;
-  cols_.push_back(d.W);
-  consumers_.push_back(0);
-  d.y = (int)cols_.size() - 1;
+  d.y = new_tensor({d.W});
   dots_.push_back(d);
   nodes_.push_back({K_DOT, (int)dots_.size() - 1});
   return d.y;
@@ -470,6 +684,8 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
   std::vector<int> dense_of(cols_.size(), -1);
   for (size_t i = 0; i < ops_.size(); ++i) dense_of[ops_[i].y] = (int)i;
   for (Dense& d : ops_) d.need_dx = d.x != input_;
+  for (Conv& c : convs_) c.need_dx = c.x != input_;
+  for (Pool& pl : pools_) pl.need_dx = pl.x != input_;
   // fused epilogues: a dense layer whose input is another dense layer's output applies that
   // layer's activation backward in its dX GEMM (the producer then reads its gradient as dpre)
   for (Dense& hi : ops_) {
@@ -517,10 +733,21 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
   // data-parallel dense parameter entries in backward order -> one flat buffer, all-reduce buckets
   // (channel-split slices are updated by their holders, never reduced)
   porder_.clear();
-  for (auto it = ops_.rbegin(); it != ops_.rend(); ++it) {
-    if (!it->holders.empty()) continue;
-    porder_.push_back(it->w);
-    if (it->b >= 0) porder_.push_back(it->b);
+  for (auto it = nodes_.rbegin(); it != nodes_.rend(); ++it) {   // backward (reverse creation) order
+    int w = -1, b = -1;
+    if (it->kind == K_DENSE) {
+      const Dense& d = ops_[it->idx];
+      if (!d.holders.empty()) continue;
+      w = d.w;
+      b = d.b;
+    } else if (it->kind == K_CONV) {
+      w = convs_[it->idx].w;
+      b = convs_[it->idx].b;
+    } else {
+      continue;
+    }
+    porder_.push_back(w);
+    if (b >= 0) porder_.push_back(b);
   }
   std::vector<int64_t> nums;
   for (int e : porder_) nums.push_back(pnumel_[e]);
@@ -610,6 +837,9 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
     csend_ = (float*)eng_->alloc((size_t)cmax * 4);
     crecv_ = (float*)eng_->alloc((size_t)cmax * 4);
   }
+  pool_code_.assign(pools_.size(), nullptr);
+  for (size_t i = 0; i < pools_.size(); ++i)
+    pool_code_[i] = (unsigned char*)eng_->alloc((size_t)Bl_ * pools_[i].C * pools_[i].P * pools_[i].Q);
   const int C = last.N;
   if (loss_ == LOSS_SCCE) probs_ = (float*)eng_->alloc((size_t)Bl_ * C * 4);
   labels_ = eng_->alloc((size_t)Bl_ * C * 4);
@@ -629,6 +859,17 @@ void Model::init_weights(uint64_t seed) {
     if (d.b >= 0) {
       std::vector<float> z(d.N, 0.f);
       set_param(d.b, z.data());
+    }
+  }
+  for (const Conv& c : convs_) {   // Glorot-uniform over fan-in C*R*S and fan-out K*R*S, zero bias
+    std::vector<float> w((size_t)c.K * c.C * c.R * c.S);
+    const float lim = std::sqrt(6.f / (float)((c.C + c.K) * c.R * c.S));
+    uint64_t s = seed * 1000003ULL + (uint64_t)c.w;
+    for (auto& v : w) v = ((float)(splitmix(s) >> 40) / (float)(1ULL << 24) * 2.f - 1.f) * lim;
+    set_param(c.w, w.data());
+    if (c.b >= 0) {
+      std::vector<float> z(c.K, 0.f);
+      set_param(c.b, z.data());
     }
   }
   for (const Emb& e : embs_) {
@@ -658,7 +899,7 @@ void Model::set_param(int i, const float* host) {
         std::memcpy(&sl[(size_t)r * e.Dc], host + r * e.D + (int64_t)j * e.Dc, (size_t)e.Dc * 4);
       eng_->h2d(table_[t], sl.data(), sl.size() * 4);
     }
-  } else if (!ops_[entry_dense_.at(i)].holders.empty()) {
+  } else if (entry_dense_.at(i) >= 0 && !ops_[entry_dense_[i]].holders.empty()) {
     const int di = entry_dense_[i];
     const Dense& d = ops_[di];
     if (d.j < 0) throw std::invalid_argument("native model: dense slice not on this rank");
@@ -688,7 +929,7 @@ void Model::get_param(int i, float* host) const {
       for (int64_t r = 0; r < e.rows; ++r)
         std::memcpy(host + r * e.D + (int64_t)j * e.Dc, &sl[(size_t)r * e.Dc], (size_t)e.Dc * 4);
     }
-  } else if (!ops_[entry_dense_.at(i)].holders.empty()) {
+  } else if (entry_dense_.at(i) >= 0 && !ops_[entry_dense_[i]].holders.empty()) {
     const int di = entry_dense_[i];
     const Dense& d = ops_[di];
     if (d.j < 0) throw std::invalid_argument("native model: dense slice not on this rank");
@@ -844,6 +1085,12 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
       std::vector<const float*> z;
       for (int t : d.in) z.push_back(act_[t]);
       eng_->dot_fwd(z.data(), (int)z.size(), act_[d.y], Bl_, d.D, d.W);
+    } else if (n.kind == K_CONV) {
+      const Conv& c = convs_[n.idx];
+      eng_->conv_fwd(act_[c.x], params_ + pofs_[c.w], c.b >= 0 ? params_ + pofs_[c.b] : nullptr, act_[c.y], Bl_, c);
+    } else if (n.kind == K_POOL) {
+      const Pool& pl = pools_[n.idx];
+      eng_->pool_fwd(act_[pl.x], act_[pl.y], pool_code_[n.idx], Bl_, pl);
     }
   }
   // loss: gradient scaled by 1 / global batch (the reference's convention), so summing the
@@ -881,6 +1128,21 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
             eng_->allreduce_start(grads_ + wplan_.buckets[bi][0], wplan_.buckets[bi][1] - wplan_.buckets[bi][0]);
         }
       }
+    } else if (n.kind == K_CONV) {
+      const Conv& c = convs_[n.idx];
+      eng_->conv_bwd(act_[c.x], params_ + pofs_[c.w], act_[c.y], grad_[c.y], c.need_dx ? grad_[c.x] : nullptr,
+                     grads_ + pofs_[c.w], c.b >= 0 ? grads_ + pofs_[c.b] : nullptr, Bl_, c);
+      if (world_ > 1) {
+        for (int e : {c.w, c.b}) {
+          if (e < 0) continue;
+          const int bi = bucket_of[e];
+          if (--left[bi] == 0)
+            eng_->allreduce_start(grads_ + wplan_.buckets[bi][0], wplan_.buckets[bi][1] - wplan_.buckets[bi][0]);
+        }
+      }
+    } else if (n.kind == K_POOL) {
+      const Pool& pl = pools_[n.idx];
+      if (pl.need_dx) eng_->pool_bwd(act_[pl.x], act_[pl.y], grad_[pl.y], grad_[pl.x], pool_code_[n.idx], Bl_, pl);
     } else if (n.kind == K_DOT) {
       const Dot& d = dots_[n.idx];
       std::vector<const float*> z;
@@ -972,6 +1234,15 @@ std::string Model::describe() const {
         o << "  embedding" << n.idx << ": " << e.rows << " x " << e.D << " bag " << e.bag << " on rank " << e.owner
           << (e.owner == rank_ ? " (local: global-batch lookups, sparse SGD)" : "") << "\n";
       }
+    } else if (n.kind == K_CONV) {
+      const Conv& c = convs_[n.idx];
+      o << "  conv" << n.idx << ": " << c.C << "x" << c.H << "x" << c.W << " -> " << c.K << "x" << c.P << "x" << c.Q << " kernel "
+        << c.R << "x" << c.S << " stride " << c.sh << "x" << c.sw << " pad " << c.ph << "x" << c.pw << " act " << c.act
+        << " (data parallel)\n";
+    } else if (n.kind == K_POOL) {
+      const Pool& pl = pools_[n.idx];
+      o << "  pool" << n.idx << " " << (pl.max ? "max" : "avg") << ": " << pl.C << "x" << pl.H << "x" << pl.W << " -> " << pl.C
+        << "x" << pl.P << "x" << pl.Q << " window " << pl.kh << "x" << pl.kw << " stride " << pl.sh << "x" << pl.sw << "\n";
     } else {
       const Dot& d = dots_[n.idx];
       o << "  dot interaction: " << d.in.size() << " features x " << d.D << " -> " << d.W << "\n";

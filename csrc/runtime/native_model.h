@@ -1,8 +1,9 @@
 // flexmi native model: graph -> per-rank execution plan -> execution, entirely in C++ (no Python).
 // Graphs: dense (MLP) chains, embedding tables and the DLRM dot interaction (a DLRM-shaped DAG:
-// bottom MLP + tables -> interaction -> top MLP); tables are placed table-wise, column-split or
-// row-split over the ranks, dense layers are data parallel or channel-split (output features over a
-// set of ranks).
+// bottom MLP + tables -> interaction -> top MLP), and CNN chains (image input -> convolutions /
+// poolings -> dense layers on the flattened features, AlexNet-shaped); tables are placed
+// table-wise, column-split or row-split over the ranks, dense layers are data parallel or
+// channel-split (output features over a set of ranks), convolutions data parallel.
 //
 // Reference: FFModel::compile / init_layers / forward / backward / update
 // (src/runtime/model.cc:374-1180) build the per-op regions, the replica gradient regions and
@@ -97,6 +98,28 @@ struct Dot {
   int y = -1, D = 0, W = 0, npairs = 0;
 };
 
+// 2-D convolution (the reference's Conv2D, src/ops/conv_2d.cu): x [B][C][H][W] (NCHW, a sample's
+// C*H*W features contiguous) -> y [B][K][P][Q], kernel [K][C][R][S], symmetric zero padding, bias +
+// activation fused; data parallel (replicated kernel in the flat buffer, bucketed all-reduce).
+struct Conv {
+  int x = -1, y = -1;
+  int C = 0, H = 0, W = 0, K = 0, R = 0, S = 0, P = 0, Q = 0;
+  int sh = 1, sw = 1, ph = 0, pw = 0;
+  int act = ACT_NONE;
+  bool bias = true;
+  int w = -1, b = -1;          // parameter entry ids
+  bool need_dx = true;
+};
+
+// 2-D pooling (src/ops/pool_2d.cu): max (padding never wins) or average excluding the padding
+struct Pool {
+  int x = -1, y = -1;
+  int C = 0, H = 0, W = 0, P = 0, Q = 0;
+  int kh = 1, kw = 1, sh = 1, sw = 1, ph = 0, pw = 0;
+  bool max = true;
+  bool need_dx = true;
+};
+
 struct StepStat {
   double loss = 0.0;
   int64_t samples = 0;
@@ -110,7 +133,13 @@ class Model {
   Model(int global_batch, int device, int rank, int world, const std::string& rendezvous);
   ~Model();
   int input(int features);
+  // image input [B][C][H][W] (its C*H*W features per sample, NCHW)
+  int input_image(int channels, int height, int width);
   int dense(int x, int out_dim, int act, bool bias);
+  // convolution of an image tensor; returns the [B][K][P][Q] output tensor id (dense layers take it
+  // flattened)
+  int conv2d(int x, int out_channels, int kh, int kw, int sh, int sw, int ph, int pw, int act, bool bias);
+  int pool2d(int x, int kh, int kw, int sh, int sw, int ph, int pw, bool max);
   // sparse index input [B][bag] (int64, the GLOBAL batch on every rank); returns its id
   int sparse_input(int bag);
   // embedding table rows x dim looked up by sparse input `sparse` (SUM over the bag); returns the
@@ -153,7 +182,7 @@ class Model {
   const WeightPlan& weight_plan() const { return wplan_; }
 
  private:
-  enum Kind { K_DENSE = 0, K_EMB = 1, K_DOT = 2 };
+  enum Kind { K_DENSE = 0, K_EMB = 1, K_DOT = 2, K_CONV = 3, K_POOL = 4 };
   struct Node {
     int kind, idx;
   };
@@ -164,6 +193,11 @@ class Model {
   int B_, Bl_, device_, rank_, world_;
   std::string rendezvous_;
   std::vector<int> cols_;                     // tensor id -> features
+  std::vector<std::vector<int>> shape_;       // tensor id -> per-sample shape ({C, H, W} or {features})
+  std::vector<Conv> convs_;
+  std::vector<Pool> pools_;
+  std::vector<unsigned char*> pool_code_;     // pool id -> max-pool argmax codes (engine scratch)
+  int new_tensor(const std::vector<int>& shape);
   std::vector<int> consumers_;                // tensor id -> number of consumers
   int input_ = -1;
   std::vector<Node> nodes_;                   // creation (= topological) order
@@ -249,6 +283,16 @@ class Engine {
   virtual void dot_bwd(const float* const* z, int F, const float* dy, float* const* dz, int M, int D, int W) = 0;
   // per-peer float counts; send / recv contiguous by peer
   virtual void all_to_all(const float* send, const int64_t* send_counts, float* recv, const int64_t* recv_counts) = 0;
+  // ---- convolution / pooling (CNN plans), NCHW fp32 ----
+  // y = act(conv(x, W) + b)
+  virtual void conv_fwd(const float* x, const float* W, const float* b, float* y, int N, const Conv& c) = 0;
+  // g = act'(y) dy; dW += g (x) x, db += sum g, dx = W^T (x) g (overwritten; skipped when null)
+  virtual void conv_bwd(const float* x, const float* W, const float* y, const float* dy, float* dx, float* dW, float* db,
+                        int N, const Conv& c) = 0;
+  // code: one byte per output (the argmax offset inside the max window), written by the forward
+  virtual void pool_fwd(const float* x, float* y, unsigned char* code, int N, const Pool& p) = 0;
+  virtual void pool_bwd(const float* x, const float* y, const float* dy, float* dx, const unsigned char* code, int N,
+                        const Pool& p) = 0;
 };
 
 // CPU engine; world > 1 ranks (one process each) exchange through a HostComm in `rendezvous`

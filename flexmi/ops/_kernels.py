@@ -48,10 +48,11 @@ _ws = {}
 
 
 def workspace(device, nbytes):
-    """Grow-only split-K slab workspace of the CURRENT stream on ``device``: GEMMs issued on
-    different streams (the executor's dW stream beside the main one) never share slabs."""
-    stream = torch.cuda.current_stream(device).cuda_stream if torch.cuda.is_available() else 0
-    key = (str(device), stream)
+    """Grow-only split-K slab workspace of ``device``.  The GEMMs of a step never run concurrently
+    (the executor's second stream carries only the embedding-group kernels), so one workspace per
+    device serves them all; keyed by device, not by stream handle -- a hipGraph capture creates
+    fresh streams and must not leave a 64 MiB workspace behind per stream."""
+    key = str(device)
     t = _ws.get(key)
     if t is None or t.numel() * 4 < nbytes:
         t = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=device)
@@ -695,8 +696,8 @@ def _conv_bwd_run(form, x, w, y, dy, dx, dw, db, stride, pads, act, acc, saved):
     return True
 
 
-# Stride-phase decomposition of a strided convolution's backward (FM_CONV_PHASE=0: the strided
-# element-gather kernels instead).  For input phase (a, b) -- rows h = a + s*h', columns
+# Stride-phase decomposition of a strided convolution's backward (PHASE_CONV; tests switch it off to
+# compare with the strided element-gather kernels).  For input phase (a, b) -- rows h = a + s*h', columns
 # w = b + s*w' -- only the taps r = r0 + s*i (r0 = (a + pt) mod s) and t = t0 + s*j reach it, and
 #   dX[:, :, a::s, b::s] = dgrad_stride1(G, W[:, :, r0::s, t0::s], pads (oa, ob))
 #   dW[:, :, r0::s, t0::s] += wgrad_stride1(G, X[:, :, a::s, b::s], pads (oa, ob))
@@ -704,7 +705,7 @@ def _conv_bwd_run(form, x, w, y, dy, dx, dw, db, stride, pads, act, acc, saved):
 # exactly the convolution's useful MACs (the strided element path computes every tap of every
 # output position and keeps a quarter: 567 us per ResNet-50 b64 downsampling dgrad,
 # profiles/prof_r3_resnet50_b64_bf16_kernels.txt).
-PHASE_CONV = os.environ.get("FM_CONV_PHASE", "1") != "0"
+PHASE_CONV = True
 
 
 def _strided(src, dst, d, ss, ts, so, to, acc):
@@ -761,9 +762,9 @@ def _conv_backward_phases(x, w, g, dx, dw, s_, pads, acc):
 # per-element gather math, no halo masks).  The forward's staged input is kept in ``saved`` for
 # the weight gradient.  Stems on few channels keep the NCHW kernels (space-to-depth).
 NHWC_CONV = os.environ.get("FM_CONV_NHWC", "1") != "0"
-# FM_CONV_PHASE_DGRAD=0 (A/B): strided data gradients as one GEMM over the stride-dilated G (s*s the
-# MACs) instead of one GEMM per stride phase
-STRIDE_PHASE_DGRAD = os.environ.get("FM_CONV_PHASE_DGRAD", "1") != "0"
+# STRIDE_PHASE_DGRAD (tests compare both): strided NHWC data gradients as one GEMM per stride phase
+# instead of one GEMM over the stride-dilated G (s*s the MACs)
+STRIDE_PHASE_DGRAD = True
 
 
 def _r8(v):

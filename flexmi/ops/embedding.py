@@ -352,18 +352,19 @@ class Embedding(Op):
                     D = w.shape[1]
                     w.index_add_(0, st.rids[s][k][:n].long(), mlr * st.rg[s][k][:n * D].view(n, D))
 
-    CLAIM = os.environ.get("FM_EMB_CLAIM", "1") != "0"
+    CLAIM = True                 # owner-computes path for mostly-unique tables (tests may switch it)
     # owner-computes when rows exceed CLAIM_RATIO x lookups per step (few enough duplicates for the
     # claim / dup / owner kernels to beat per-lookup atomics): 0.2 takes the 2208..7420-row MLPerf
     # tables off the atomic kernel, 1.162-1.163 vs 1.171 ms/step at ratio 1
     # (profiles/bench_ab_claim_ratio_r5cr.txt)
-    CLAIM_RATIO = float(os.environ.get("FM_EMB_CLAIM_RATIO", "0.2"))
-    # FM_EMB_BWD=count: the count / update kernel pair (csrc/kernels/embedding.hip) for every table
-    # above the tiny-table LDS kernel's rows, on the same slot / flag buffers
-    COUNT = os.environ.get("FM_EMB_BWD", "claim") == "count"
-    # the wave-private LDS kernel's table-size limit: the SAME variable and default as the C++
-    # dispatcher (embedding.hip kind_of, FM_EMB_TINY_ROWS, default 64), so the two cannot drift
-    TINY_ROWS = int(os.environ.get("FM_EMB_TINY_ROWS", "64"))
+    CLAIM_RATIO = 0.2
+    # the count / update kernel pair (csrc/kernels/embedding.hip, fm_embedding_set_bwd_mode(1)) for
+    # every table above the tiny-table LDS kernel's rows, on the same slot / flag buffers: an
+    # alternative form kept tested (tests/test_gpu_kernels.py), off by default
+    COUNT = False
+    # the wave-private LDS kernel's table-size limit: the same constant as the C++ dispatcher
+    # (embedding.hip kind_of TINY_ROWS)
+    TINY_ROWS = 64
 
     def _claim_buffers(self, ctx):
         """Owner-computes sparse SGD buffers for a mostly-unique table (rows > lookups per step):

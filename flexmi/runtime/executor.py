@@ -180,8 +180,10 @@ P2P_MODE = os.environ.get("FM_P2P", "auto")
 # every embedding output in one exchange (src/runtime/dlrm_strategy.cc:252-263).
 XCHG_CHUNKS = os.environ.get("FLEXMI_XCHG_CHUNKS", "auto")
 # test hook: chunk the row-wise tail at world 1 too (no exchange; exercises the chunked kernels)
-XCHG_LOCAL = os.environ.get("FLEXMI_XCHG_CHUNKS_LOCAL") == "1"
+XCHG_LOCAL = False
 PIPE_ROW_ALIGN = 8          # chunk boundaries on 8-row multiples: 16-B aligned rows for the kernels
+# smallest weight (elements) whose SGD is fused into its dW GEMM (FM_FUSED_SGD); tests lower it
+FUSED_SGD_MIN = 1 << 21
 
 
 def chunk_bounds(n, k):
@@ -965,7 +967,7 @@ class Executor:
         the gradient it writes (interaction.hip act0), so L skips its separate act-bwd / bias-grad
         pass and sums its bias gradient in its dW GEMM."""
         from flexmi.core.types import OperatorType
-        if self.backend != "hip" or self.cfg.compute_dtype != "fp32" or os.environ.get("FM_DOT_ACT0", "1") == "0":
+        if self.backend != "hip" or self.cfg.compute_dtype != "fp32":
             return
         for op in ops:
             if op.op_type != OperatorType.OP_LINEAR or getattr(op, "skip_act_grad", False):
@@ -1628,7 +1630,7 @@ class Executor:
         # only weights big enough for the saved gradient round trip to matter: on the MLPerf DLRM
         # (<= 1 M-element candidates) fusing measured 0.3-0.9 % slower, on summit_large
         # (16-42 M-element layers) 1.61 -> 1.17 ms bf16 (profiles/fused_sgd_ab_r4i.txt)
-        min_numel = int(os.environ.get("FM_FUSED_SGD_MIN", str(1 << 21)))
+        min_numel = FUSED_SGD_MIN
         uses = defaultdict(int)
         for st in self.bwd_steps:
             if st[0] == "op":

@@ -18,7 +18,7 @@ def test_key_distinguishes_what_changes_the_configuration():
 
 
 def test_encoding_round_trips_and_fits_the_ksplit_argument():
-    for form in range(6):
+    for form in range(7):
         for ks in T.KS_CHOICES:
             c = T.encode(form, ks)
             assert T.decode(c) == (form, ks)
@@ -28,11 +28,13 @@ def test_encoding_round_trips_and_fits_the_ksplit_argument():
 def test_candidates_respect_form_and_split_limits():
     c = T.candidates("fp32", 8192, 1024, 1024)
     forms = {T.decode(x)[0] for x in c}
-    assert forms == {1, 2, 3, 4, 5}
+    assert forms == {1, 2, 3, 4, 5, 6}
     for x in c:          # every split keeps >= 4 k-steps of 32
         assert T.decode(x)[1] * 4 <= 1024 // 32 or T.decode(x)[1] == 1
-    # fused backward epilogue: the split kernel cannot carry it
-    assert {T.decode(x)[0] for x in T.candidates("fp32", 8192, 1024, 1024, fused=True)} == {1, 2, 3}
+    # fused backward epilogue: the x3 split-K kernels (forms 4-6) carry it unsplit only
+    fused = {T.decode(x) for x in T.candidates("fp32", 8192, 1024, 1024, fused=True)}
+    assert {f for f, _ in fused} == {1, 2, 3, 4, 5, 6}
+    assert all(ks == 1 for f, ks in fused if f >= 4)
     # tiny operands: no split kernel
     assert {T.decode(x)[0] for x in T.candidates("fp32", 8192, 32, 16)} == {1, 2, 3}
     assert {T.decode(x)[0] for x in T.candidates("bf16", 8192, 1024, 1024)} == {1, 2, 3}

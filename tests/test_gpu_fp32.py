@@ -167,9 +167,8 @@ def test_dot_interaction_f32(gpu, F, D, selfi):
 @pytest.mark.parametrize("F,D,selfi", [(27, 128, False), (9, 64, True), (32, 32, False), (28, 128, True)])
 def test_dot_interaction_f32_split_forward(gpu, monkeypatch, F, D, selfi):
     """fp32 interaction forward with the Gram on the bf16 matrix cores through the exact
-    three-way split (FM_DOT_FWD_X3=1, the default), incl. operands spanning many binades, vs float64."""
+    three-way split (the only fp32 forward form), incl. operands spanning many binades, vs float64."""
     from flexmi.ops import _kernels as Kk
-    monkeypatch.setenv("FM_DOT_FWD_X3", "1")
     torch.manual_seed(19)
     B = 777
     zs = [torch.randn(B, D, device=gpu) * torch.exp2(torch.randint(-12, 12, (B, D), device=gpu).float())

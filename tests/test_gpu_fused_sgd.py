@@ -63,7 +63,8 @@ def _train(monkeypatch, fused, graph, momentum, dtype="bf16"):
     from flexmi.core import FFConfig, FFModel, SGDOptimizer, LossType, MetricsType
     from flexmi.models.dlrm import DLRMConfig, build_dlrm, SyntheticDLRMData
     monkeypatch.setenv("FM_FUSED_SGD", "1" if fused else "0")
-    monkeypatch.setenv("FM_FUSED_SGD_MIN", "0")      # the tiny model's layers are below the default size
+    from flexmi.runtime import executor as _E
+    monkeypatch.setattr(_E, "FUSED_SGD_MIN", 0)      # the tiny model's layers are below the default size
     cfg = FFConfig()
     cfg.batchSize = 512
     cfg.seed = 5
@@ -116,7 +117,8 @@ def test_separate_backward_update_keeps_gradients(gpu, monkeypatch):
     from flexmi.core import FFConfig, FFModel, SGDOptimizer, LossType, MetricsType
     from flexmi.models.dlrm import DLRMConfig, build_dlrm, SyntheticDLRMData
     monkeypatch.setenv("FM_FUSED_SGD", "1")
-    monkeypatch.setenv("FM_FUSED_SGD_MIN", "0")
+    from flexmi.runtime import executor as _E
+    monkeypatch.setattr(_E, "FUSED_SGD_MIN", 0)
     cfg = FFConfig()
     cfg.batchSize = 256
     m = FFModel(cfg)

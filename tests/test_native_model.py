@@ -455,3 +455,114 @@ def test_native_c_dlrm_strategy_mapping_rules(tmp_path):
             ch = p != init
             merged[ch] = p[ch]
         np.testing.assert_allclose(merged, want, rtol=2e-5, atol=2e-6, err_msg=f"param {i}")
+
+
+# ---------------------------------------------------------------------- native CNN (data parallel)
+def _build_cnn_c(tmp_path):
+    if not os.path.exists(LIB):
+        pytest.skip("libflexmi_native_c.so not built")
+    exe = str(tmp_path / "native_cnn")
+    subprocess.run(["gcc", "-O2", "-I" + os.path.join(ROOT, "csrc", "capi"), os.path.join(ROOT, "tests", "capi", "native_cnn.c"),
+                    "-L" + os.path.join(ROOT, "flexmi"), "-Wl,-rpath," + os.path.join(ROOT, "flexmi"), "-lflexmi_native_c",
+                    "-o", exe], check=True)
+    ldd = subprocess.run(["ldd", exe], capture_output=True, text=True).stdout
+    assert "libpython" not in ldd and "libtorch" not in ldd, ldd
+    return exe
+
+
+def _parse_cnn(prefix, world):
+    b = open(prefix + ".init.bin", "rb").read()
+    o = 0
+
+    def take(buf, fmt, n=1):
+        nonlocal o
+        v = np.frombuffer(buf, dtype=np.dtype(fmt), count=n, offset=o)
+        o += np.dtype(fmt).itemsize * n
+        return v
+    B, steps, npar = (int(v) for v in take(b, "<i4", 3))
+    init = []
+    for _ in range(npar):
+        n = int(take(b, "<i8")[0])
+        init.append(take(b, "<f4", n).copy())
+    batches = [(take(b, "<f4", B * 3 * 20 * 20).reshape(B, 3, 20, 20).copy(), take(b, "<i4", B).copy())
+               for _ in range(steps)]
+    ranks = []
+    for r in range(world):
+        rb = open(f"{prefix}.r{r}.bin", "rb").read()
+        o = 0
+        rk, n = (int(v) for v in take(rb, "<i4", 2))
+        assert rk == r and n == npar
+        final = [take(rb, "<f4", len(init[i])).copy() for i in range(npar)]
+        ranks.append((final, take(rb, "<f8", steps).copy()))
+    return dict(B=B, steps=steps, init=init, batches=batches, ranks=ranks)
+
+
+def _replay_cnn(rec):
+    """The same CNN, weights and batches through flexmi's Python executor (CPU, fp32, world 1)."""
+    from flexmi.core import ActiMode, FFConfig, FFModel, LossType, MetricsType, PoolType, SGDOptimizer
+    B = rec["B"]
+    cfg = FFConfig()
+    cfg.batchSize, cfg.device, cfg.compute_dtype = B, "cpu", "fp32"
+    m = FFModel(cfg)
+    x = m.create_tensor([B, 3, 20, 20], name="image")
+    t = m.conv2d(x, 8, 5, 5, 1, 1, 2, 2, ActiMode.AC_MODE_RELU)
+    t = m.pool2d(t, 3, 3, 2, 2, 0, 0, PoolType.POOL_MAX)
+    t = m.conv2d(t, 16, 3, 3, 1, 1, 1, 1, ActiMode.AC_MODE_RELU)
+    t = m.pool2d(t, 2, 2, 2, 2, 1, 1, PoolType.POOL_AVG)
+    t = m.flat(t)
+    t = m.dense(t, 32, ActiMode.AC_MODE_RELU)
+    t = m.dense(t, 10)
+    t = m.softmax(t)
+    m.compile(SGDOptimizer(m, 0.05), LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, [MetricsType.METRICS_ACCURACY])
+    ex = m.init_layers()
+    assert len(m.parameters) == len(rec["init"])
+    for p, w in zip(m.parameters, rec["init"]):
+        p.set_weights(m, w.reshape(p.dims))
+    for xb, yb in rec["batches"]:
+        ex.scatter_from_host(x, xb)
+        lab = m.get_label_tensor()
+        ex.scatter_from_host(lab, yb.reshape(lab.dims))
+        ex.train_step()
+    return [p.get_weights(m).reshape(-1) for p in m.parameters]
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_native_c_cnn_trains_like_the_executor(tmp_path, world):
+    """VERDICT r5 #5 (first step): the native plan compiler also compiles CNN graphs -- image input,
+    convolutions (bias + ReLU fused), max / average pooling, dense layers on the flattened features --
+    data parallel over `world` rank processes with bucketed gradient all-reduces; a C program trains
+    an AlexNet-shaped network through libflexmi_native_c alone and ends with the Python executor's
+    parameters."""
+    exe = _build_cnn_c(tmp_path)
+    rdv = tmp_path / "rdv"
+    rdv.mkdir()
+    prefix = str(tmp_path / "run")
+    r = subprocess.run([exe, "cpu", prefix, "4", str(world), str(rdv)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "native_cnn ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "conv0: 3x20x20 -> 8x20x20" in r.stdout and "pool0 max" in r.stdout and "pool1 avg" in r.stdout
+    rec = _parse_cnn(prefix, world)
+    got = _replay_cnn(rec)
+    for i, want in enumerate(got):
+        reps = [rk[0][i] for rk in rec["ranks"]]
+        for h in reps[1:]:                      # DP replicas end identical
+            np.testing.assert_array_equal(h, reps[0])
+        np.testing.assert_allclose(reps[0], want, rtol=1e-4, atol=1e-5, err_msg=f"param {i}")
+    assert np.all(np.isfinite(rec["ranks"][0][1]))
+
+
+@pytest.mark.gpu
+def test_native_c_cnn_hip_engine_matches_cpu(tmp_path):
+    """The same C CNN program on the HIP engine (flexmi's fp32 implicit-GEMM convolution and pooling
+    kernels) against the CPU engine."""
+    exe = _build_cnn_c(tmp_path)
+    recs = {}
+    for dev in ("cpu", "hip"):
+        rdv = tmp_path / f"rdv_{dev}"
+        rdv.mkdir()
+        r = subprocess.run([exe, dev, str(tmp_path / dev), "4", "1", str(rdv)], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0 and "native_cnn ok" in r.stdout, (dev, r.stdout[-2000:] + r.stderr[-2000:])
+        recs[dev] = _parse_cnn(str(tmp_path / dev), 1)
+    c, h = recs["cpu"], recs["hip"]
+    for a, b in zip(c["ranks"][0][0], h["ranks"][0][0]):
+        np.testing.assert_allclose(b, a, rtol=1e-3, atol=1e-4)
+    np.testing.assert_allclose(h["ranks"][0][1], c["ranks"][0][1], rtol=1e-3)
