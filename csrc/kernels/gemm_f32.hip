@@ -598,7 +598,10 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
     };
     if (opnd_ok(A, lda, sA, a_kcontig) && opnd_ok(B, ldb, sB, b_kcontig)) {
       // 256x128 (8 waves, 2 per SIMD) whenever M fills it, split-K for the grid
-      const int bm = form == 4 ? 256 : (form == 5 || form == 6) ? 128 : M >= 256 ? 256 : 128;
+      // the F16 form runs on 128-row tiles (4 or 2 waves per block: room for its second accumulator set)
+      const bool f16_pick = f16_form && ws != nullptr && (a_kcontig || split_mode == 5);
+      const int bm = (form == 4 && !f16_pick) ? 256 : (form == 4 || form == 5 || form == 6) ? 128
+                                                     : (M >= 256 && !f16_pick) ? 256 : 128;
       const int bn = form == 6 ? 64 : 128;
       p.tiles_m = (M + bm - 1) / bm;
       p.tiles_n = (N + bn - 1) / bn;
@@ -617,7 +620,7 @@ static int gemm_f32_run(const float* A, long lda, long sA, int a_kcontig, const 
       // F16 form for the GEMMs with a K-contiguous A (forward, dX): measured faster than the bf16
       // six-product split there, slower on the dW orientation whose two column scans read both
       // batch-long operands (profiles/f16_split_ab_r7.txt)
-      if (f16_form && ws != nullptr && (a_kcontig || split_mode == 5)) {
+      if (f16_pick) {
         // per-row / per-column scales from the tail of the workspace (the slabs use the front)
         const long abytes = (((long)M + N) * 16 * 4 + 255) & ~255L;
         const long slab = (long)batch * ks * M * (long)N * 4;

@@ -415,10 +415,10 @@ template <int BM, int BN, bool SGD>
 void launch_x3v2(const GemmF& p, bool ak, bool bk, hipStream_t s) {
   const bool f16 = p.amax_a != nullptr;
   if constexpr (BM == 256) {
-    // the F16 form takes the one-register-set schedule: two staging sets plus its second
-    // accumulator set spill at 256 VGPRs (the dX orientation)
-    if (f16) launch_x3v2_s<BM, BN, SGD, 0, true>(p, ak, bk, s);
-    else launch_x3v2_s<BM, BN, SGD, 3>(p, ak, bk, s);
+    // no F16 form at 256x128: its second accumulator set spills at the 256 VGPRs of two waves per
+    // SIMD in either schedule (tests/test_kernel_resources.py); the caller takes 128-row tiles for it
+    (void)f16;
+    launch_x3v2_s<BM, BN, SGD, 3>(p, ak, bk, s);
   } else {
     if (f16) launch_x3v2_s<BM, BN, SGD, 0, true>(p, ak, bk, s);
     else launch_x3v2_s<BM, BN, SGD, 0>(p, ak, bk, s);
