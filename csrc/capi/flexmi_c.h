@@ -1,4 +1,7 @@
-/* flexmi C API (C-API parity with the reference's python/flexflow_c.h:49-749).
+/* flexmi C API -- the CPython-EMBEDDING model API (C-API parity with the reference's
+ * python/flexflow_c.h:49-749).  For C programs that must not load Python at all, use the native
+ * API in flexmi_native_c.h (libflexmi_native_c.so: the C++ runtime, plan compiler for DLRM and
+ * CNN graphs, simulator / search, loaders -- no interpreter).
  *
  * Opaque handles over the flexmi runtime.  The library embeds CPython when the host program is
  * not Python (a C/C++ application calls flexmi_init first) and works from inside a Python

@@ -1,9 +1,12 @@
-/* flexmi native C API: flexmi's C++ runtime from C without any Python.
+/* flexmi NATIVE C API: flexmi's C++ runtime from C without any Python.
  *
- * flexmi_c.h is the full model API (it drives the Python front end through an embedded
- * interpreter, like the reference's cffi layer drives its C++ core).  This header is the
+ * flexmi_c.h is the CPython-embedding model API (it drives the Python front end through an
+ * embedded interpreter, like the reference's cffi layer drives its C++ core).  This header is the
  * CPython-free layer over the native runtime itself (libflexmi_native_c.so links only the C++
- * runtime): strategy files in the reference's protobuf format, the sharding algebra of the plan
+ * runtime): the native plan compiler and trainer (fmn_model_*: dense / embedding / dot-interaction
+ * DLRM graphs and convolution / pooling CNN graphs under data, table-, column-, row- and
+ * channel-parallel plans, CPU and HIP engines), strategy files in the reference's protobuf format,
+ * the sharding algebra of the plan
  * compiler (partitions, boxes, reshard transfer lists), the MI355X execution simulator and MCMC
  * SOAP search, the HDF5 dataset reader, the prefetching batch loader ring and the CPU
  * embedding-bag kernels.  Reference counterparts: src/runtime/strategy.cc (.pb files),
