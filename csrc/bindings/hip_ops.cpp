@@ -128,6 +128,13 @@ void fm_conv_s2d_run(const void* x, void* xs, int bf16, int N, int C, int H, int
 void fm_conv_w_s2d_run(const void* w, void* ws, const float* dws, float* dw, int bf16, int K, int C, int R, int S, int s,
                        int Rs, int Ss, int inv, hipStream_t st);
 void fm_pad_rows(const void* src, void* dst, int K, int n, int ldp, int bf16, hipStream_t st);
+int fm_stem_supported(int C, int K, int R, int S, int sh, int sw);
+long fm_stem_wgrad_ws(int C, int K, int R, int S, int s);
+long fm_stem_wf_elems(int C, int K, int R, int S, int s);
+int fm_stem_fwd_run(const void* x, const void* w, void* wf, const float* bias, void* y, int N, int C, int H, int W, int R, int S,
+                    int P, int Q, int s, int pt, int pl, int act, hipStream_t st);
+int fm_stem_wgrad_run(const void* x, const void* y, const void* dy, float* dw, float* db, float* ws, int N, int C, int H,
+                      int W, int R, int S, int P, int Q, int s, int pt, int pl, int act, hipStream_t st);
 void fm_nhwc_stage_run(const void* src, void* dst, int N, int C, int H, int W, int Cp, int Hp, int Wp, int top, int left,
                        int dh, int dw, hipStream_t s);
 void fm_nhwc_stage_grad_run(const void* dy, const void* y, void* dst, int act, int N, int C, int H, int W, int Cp, int Hp,
@@ -787,6 +794,8 @@ static void conv_chk(const torch::Tensor& x, const torch::Tensor& w, const torch
   TORCH_CHECK(((uintptr_t)x.data_ptr() & 15) == 0 && ((uintptr_t)w.data_ptr() & 15) == 0 && ((uintptr_t)y.data_ptr() & 15) == 0,
               n, ": 16-B aligned operands");
 }
+#define CONV_GEOM_NO_K(x, w, y) (int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)w.size(2), \
+                                (int)w.size(3), (int)y.size(2), (int)y.size(3)
 #define CONV_GEOM(x, w, y) (int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)w.size(0), (int)w.size(2), \
                            (int)w.size(3), (int)y.size(2), (int)y.size(3)
 int64_t conv_scratch(int64_t rows, int64_t cols) { return rows * fm_conv_lda((int)cols); }
@@ -827,6 +836,59 @@ void conv_wgrad(torch::Tensor g, torch::Tensor x, torch::Tensor dw, int64_t R, i
               "conv_wgrad: operands under 2 GiB");
   fm_conv_wgrad(g.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), is_bf16(x), (int)x.size(0), (int)x.size(1), (int)x.size(2),
                 (int)x.size(3), (int)g.size(1), (int)R, (int)S, (int)g.size(2), (int)g.size(3), sh, sw, pt, pl, cur());
+}
+// stem convolutions (csrc/kernels/conv_stem.hip): bf16, 64 filters, few channels, stride 4 / 2
+bool stem_supported(int64_t C, int64_t K, int64_t R, int64_t S, int64_t sh, int64_t sw) {
+  return fm_stem_supported((int)C, (int)K, (int)R, (int)S, (int)sh, (int)sw) != 0;
+}
+int64_t stem_wgrad_ws(int64_t C, int64_t K, int64_t R, int64_t S, int64_t s) {
+  return fm_stem_wgrad_ws((int)C, (int)K, (int)R, (int)S, (int)s);
+}
+int64_t stem_wf_elems(int64_t C, int64_t K, int64_t R, int64_t S, int64_t s) {
+  return fm_stem_wf_elems((int)C, (int)K, (int)R, (int)S, (int)s);
+}
+void stem_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor wf, c10::optional<torch::Tensor> bias, torch::Tensor y,
+              int64_t s, int64_t pt, int64_t pl, int64_t act) {
+  conv_chk(x, w, y, "stem_fwd");
+  TORCH_CHECK(is_bf16(x), "stem_fwd: bf16 operands");
+  TORCH_CHECK(stem_supported(x.size(1), w.size(0), w.size(2), w.size(3), s, s), "stem_fwd: unsupported geometry");
+  const float* b = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == torch::kFloat32 && bias->numel() == w.size(0) && bias->is_contiguous(),
+                "stem_fwd: fp32 bias[K]");
+    b = bias->data_ptr<float>();
+  }
+  check_cuda(wf, "wf");
+  TORCH_CHECK(wf.element_size() == 2 && wf.numel() >= stem_wf_elems(x.size(1), w.size(0), w.size(2), w.size(3), s) &&
+                  ((uintptr_t)wf.data_ptr() & 15) == 0, "stem_fwd: 16-bit weight-fragment scratch of stem_wf_elems");
+  TORCH_CHECK(fm_stem_fwd_run(x.data_ptr(), w.data_ptr(), wf.data_ptr(), b, y.data_ptr(), CONV_GEOM_NO_K(x, w, y), (int)s, (int)pt,
+                              (int)pl, (int)act, cur()) == 0, "stem_fwd: launch");
+}
+void stem_wgrad(torch::Tensor x, torch::Tensor y, torch::Tensor dy, torch::Tensor dw, c10::optional<torch::Tensor> db,
+                torch::Tensor ws, int64_t R, int64_t S, int64_t s, int64_t pt, int64_t pl, int64_t act) {
+  chk4(x, "stem_wgrad x");
+  chk4(y, "stem_wgrad y");
+  chk4(dy, "stem_wgrad dy");
+  TORCH_CHECK(is_bf16(x) && is_bf16(y) && is_bf16(dy), "stem_wgrad: bf16 x / y / dy");
+  TORCH_CHECK(x.dim() == 4 && y.sizes() == dy.sizes() && y.size(0) == x.size(0), "stem_wgrad: x [N,C,H,W], y = dy [N,K,P,Q]");
+  TORCH_CHECK(stem_supported(x.size(1), y.size(1), R, S, s, s), "stem_wgrad: unsupported geometry");
+  TORCH_CHECK(x.numel() < (1L << 30) && y.numel() < (1L << 30), "stem_wgrad: operands under 2 GiB");
+  TORCH_CHECK(((uintptr_t)dy.data_ptr() & 15) == 0 && ((uintptr_t)y.data_ptr() & 15) == 0, "stem_wgrad: 16-B aligned y / dy");
+  check_cuda(dw, "dw");
+  TORCH_CHECK(dw.scalar_type() == torch::kFloat32 && dw.is_contiguous() && dw.numel() == y.size(1) * x.size(1) * R * S,
+              "stem_wgrad: contiguous fp32 dw[K*C*R*S]");
+  float* dbp = nullptr;
+  if (db.has_value() && db->defined()) {
+    TORCH_CHECK(db->scalar_type() == torch::kFloat32 && db->is_contiguous() && db->numel() == y.size(1), "stem_wgrad: fp32 db[K]");
+    dbp = db->data_ptr<float>();
+  }
+  check_cuda(ws, "ws");
+  TORCH_CHECK(ws.scalar_type() == torch::kFloat32 && ws.numel() >= stem_wgrad_ws(x.size(1), y.size(1), R, S, s),
+              "stem_wgrad: fp32 workspace of stem_wgrad_ws elements");
+  TORCH_CHECK(fm_stem_wgrad_run(x.data_ptr(), y.data_ptr(), dy.data_ptr(), dw.data_ptr<float>(), dbp, ws.data_ptr<float>(),
+                                (int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)R, (int)S, (int)y.size(2),
+                                (int)y.size(3), (int)s, (int)pt, (int)pl, (int)act, cur()) == 0,
+              "stem_wgrad: launch");
 }
 // space-to-depth: x [N,C,H,W] <-> xs [N, C*s*s, Hs, Ws] (inv scatters xs back into x, acc adds)
 void conv_s2d(torch::Tensor x, torch::Tensor xs, int64_t s, int64_t pt, int64_t pl, bool inv, bool acc) {
@@ -1172,6 +1234,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_nhwc_dgrad_strided", &conv_nhwc_dgrad_strided);
   m.def("conv_nhwc_wgrad", &conv_nhwc_wgrad);
   m.def("conv_s2d", &conv_s2d);
+  m.def("stem_supported", &stem_supported);
+  m.def("stem_wgrad_ws", &stem_wgrad_ws);
+  m.def("stem_wf_elems", &stem_wf_elems);
+  m.def("stem_fwd", &stem_fwd);
+  m.def("stem_wgrad", &stem_wgrad);
   m.def("conv_w_s2d", &conv_w_s2d);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);

@@ -516,6 +516,8 @@ def _s2d_operands(x, w, plan, pads, saved):
 #             backward through the stride-phase decomposition when phase=True
 #   s2d       space-to-depth of a strided few-channel stem onto the stride-1 NCHW kernels
 #   s2d_nhwc  the same re-laid stem on the NHWC kernels (the space-to-depth input has s*s*Cin channels)
+#   stem      the dedicated stem kernels: the input tile staged into LDS in space-to-depth NHWC order
+#             by the convolution kernel itself (no re-laid image in HBM), 64 filters, few channels
 # FM_CONV_TUNE=0: no timing, the fixed heuristic order (nhwc > s2d > igemm).  Layers whose NHWC images
 # are shared with a neighbour (the executor's conv chain fusion) keep the nhwc form.
 CONV_TUNE = os.environ.get("FM_CONV_TUNE", "1") != "0"
@@ -527,9 +529,22 @@ def _chained(saved):
                                                           "nhwc_g_prestaged"))
 
 
-def conv_forms(x, w, y, stride, groups, direction="fwd"):
-    """Applicable convolution forms of one layer, in the heuristic's preference order."""
+# the dedicated stem kernels (csrc/kernels/conv_stem.hip) for strided few-channel first layers
+# (tests switch them off to compare with the generic forms)
+STEM_CONV = True
+
+
+def _stem_ok(x, w, stride, groups):
+    return (STEM_CONV and x.dtype == torch.bfloat16 and groups == 1 and stride[0] == stride[1]
+            and C().stem_supported(x.shape[1], w.shape[0], w.shape[2], w.shape[3], stride[0], stride[1]))
+
+
+def conv_forms(x, w, y, stride, groups, direction="fwd", need_dx=False):
+    """Applicable convolution forms of one layer, in the heuristic's preference order (the stem
+    kernels compute no input gradient: backward candidates only for a layer on the network input)."""
     out = []
+    if _stem_ok(x, w, stride, groups) and not (direction == "bwd" and need_dx):
+        out.append("stem")
     if _nhwc_ok(x, w, groups):
         out.append("nhwc")
     plan = _s2d_plan(x, w, y, stride)
@@ -587,6 +602,11 @@ def conv2d_forward(x, w, b, y, stride, pads, act, groups, saved=None, form=None)
 
 
 def _conv_fwd_run(form, x, w, b, y, stride, pads, act, saved):
+    if form == "stem":
+        Kout, Cin, R, S = w.shape
+        wf = scratch(x.device, "stem_wf", C().stem_wf_elems(Cin, Kout, R, S, stride[0]), torch.bfloat16)
+        C().stem_fwd(x, w, wf, b, y, stride[0], pads[0], pads[2], int(act))
+        return
     if form == "nhwc":
         _nhwc_forward(x, w, b, y, stride, pads, act, saved)
         return
@@ -624,7 +644,7 @@ def conv2d_backward(x, w, y, dy, dx, dw, db, stride, pads, act, groups, acc, sav
     dX are touched only by the chosen form)."""
     assert groups == 1, "grouped convolution is not supported on the HIP path"
     w = w.contiguous()
-    forms = conv_forms(x, w, y, stride, groups, "bwd")
+    forms = conv_forms(x, w, y, stride, groups, "bwd", need_dx=dx is not None)
     if form is None:
         if _chained(saved) or len(forms) == 1:
             form = forms[0]
@@ -642,6 +662,13 @@ def conv2d_backward(x, w, y, dy, dx, dw, db, stride, pads, act, groups, acc, sav
 
 def _conv_bwd_run(form, x, w, y, dy, dx, dw, db, stride, pads, act, acc, saved):
     """One backward form; False when it does not apply to this layout (the caller falls back)."""
+    if form == "stem":
+        if dx is not None:
+            return False
+        Kout, Cin, R, S = w.shape
+        ws = scratch(x.device, "stem_ws", C().stem_wgrad_ws(Cin, Kout, R, S, stride[0]), torch.float32)
+        C().stem_wgrad(x, y, dy, dw.view(-1), db, ws, R, S, stride[0], pads[0], pads[2], int(act))
+        return True
     if form == "nhwc":
         return _nhwc_backward(x, w, y, dy, int(act), db, dx, dw, stride, pads, acc, saved)
     plan = _s2d_plan(x, w, y, stride) if form in ("s2d", "s2d_nhwc") else None
