@@ -75,6 +75,9 @@ FM_DEVICE void tile_of(const StemP& p, int tile, int& n, int& p0, int& q0) {
 // instruction, 60 % TA-busy -- the kernel's bound.)  Positions outside the image are written as zeros
 // every tile.  Split into a register prefetch (load) and the LDS write (store), so the forward can
 // keep the next tile's loads in flight under this tile's MFMAs; row tasks bounded for C <= 3.
+constexpr int ST_RAWN = 256;                            // elements of one raw row buffer (32 lanes x 8)
+constexpr int ST_RAW_BYTES = 4 * 2 * ST_RAWN * 2;       // per block: 4 waves x 2 row tasks
+
 template <int CP, int RS, int SS, int S_, int NR = (3 * S_ * (STP + RS - 1) + 7) / 8>
 struct StemLoader {
   using G = StemGeo<CP, RS, SS>;
@@ -104,10 +107,12 @@ struct StemLoader {
       bool rok;
       row_of(p, min(r, nrow - 1), n, p0, q0, yr, ch, rok, g0);
       const int base = g0 - (g0 & 7) + 8 * j;
-      if (r < nrow && rok && base >= 0 && base + 8 <= total) {
+      if (r >= nrow || !rok) {
+        v[u] = u32x4_t{0u, 0u, 0u, 0u};                  // a row outside the image: no loads
+      } else if (base >= 0 && base + 8 <= total) {
         v[u] = *reinterpret_cast<const u32x4_t*>(p.x + base);
       } else {
-        // a row outside the image (zeros) or a chunk overhanging the tensor: element loads
+        // a chunk overhanging the tensor (its first / last row): element loads
         unsigned e16[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -121,27 +126,43 @@ struct StemLoader {
     }
   }
 
-  FM_DEVICE void store(const StemP& p, unsigned short* xs, int n, int p0, int q0, int ub = 0) const {
+  // raw: this wave's 2 x ST_RAWN-element row buffers.  The 16-B chunks go to the raw row first
+  // (ds_write_b128, lanes contiguous: conflict-free); each lane then gathers whole s2d pixels (S_
+  // phases) from it and writes them with one 8- / 4-B store.  (Scattering the 8 elements of a chunk
+  // with 2-B stores directly -- lanes 8 elements apart, so two pixels = 56 dwords apart -- conflicted
+  // 8-16 ways and was the forward's LDS bound.)
+  FM_DEVICE void store(const StemP& p, unsigned short* xs, unsigned short* raw, int n, int p0, int q0, int ub = 0) const {
     const int nrow = p.C * S_ * G::XH;
     const int lane = threadIdx.x & 63, j = lane & 31;
+    unsigned short* rw = raw + (lane >> 5) * ST_RAWN;
     const int xx0 = q0 * S_ - p.pl;
 #pragma unroll
     for (int u = 0; u < NR; ++u) {
       const int r = ((int)threadIdx.x >> 5) + 8 * (ub + u);
-      if (r >= nrow) break;
       int yr, ch, g0;
       bool rok;
-      row_of(p, r, n, p0, q0, yr, ch, rok, g0);
-      const int c0 = 8 * j - (g0 & 7);                   // row position of this lane's first element
-      unsigned short* row = xs + yr * G::XWA * G::CPS + ch;
+      row_of(p, min(r, nrow - 1), n, p0, q0, yr, ch, rok, g0);
+      *reinterpret_cast<u32x4_t*>(rw + 8 * j) = v[u];
+      FM_WAVE_LDS_SYNC();
+      const int rot = g0 & 7;                            // raw index of row position 0
+      unsigned short* drow = xs + yr * G::XWA * G::CPS + ch;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int col = c0 + e;
-        if (col < 0 || col >= XWS) continue;
-        const int xx = xx0 + col;
-        const unsigned short val = (unsigned short)(v[u][e >> 1] >> (16 * (e & 1)));
-        row[(col / S_) * G::CPS + col % S_] = (rok && xx >= 0 && xx < p.W) ? val : (unsigned short)0;
+      for (int kk = 0; kk < (G::XW + 31) / 32; ++kk) {
+        const int k = j + 32 * kk;                       // s2d pixel of this row task
+        if (r < nrow && k < G::XW) {
+          unsigned e16[S_];
+#pragma unroll
+          for (int e = 0; e < S_; ++e) {
+            const int xx = xx0 + k * S_ + e;
+            e16[e] = (rok && xx >= 0 && xx < p.W) ? (unsigned)rw[k * S_ + e + rot] : 0u;
+          }
+          if constexpr (S_ == 4)
+            *reinterpret_cast<uint2*>(drow + k * G::CPS) = uint2{e16[0] | (e16[1] << 16), e16[2] | (e16[3] << 16)};
+          else
+            *reinterpret_cast<unsigned*>(drow + k * G::CPS) = e16[0] | (e16[1] << 16);
+        }
       }
+      FM_WAVE_LDS_SYNC();                                // the gathers read the raw row before it is reused
     }
   }
 };
@@ -207,6 +228,7 @@ __global__ void __launch_bounds__(STT, 2) fm_stem_fwd(StemP p) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) bias2[j] = p.bias ? p.bias[(2 * h + j) * 16 + l16] : 0.f;
   const int lbase = (rw * G::XWA + l16) * G::CPS;
+  unsigned short* raw = xs + 2 * G::LDS_ELEMS + wave * 2 * ST_RAWN;
   StemLoader<CP, RS, SS, S_> ld;
   int buf = 0;
   if ((int)blockIdx.x < p.ntiles) {
@@ -214,7 +236,7 @@ __global__ void __launch_bounds__(STT, 2) fm_stem_fwd(StemP p) {
     tile_of(p, blockIdx.x, n, p0, q0);
     __syncthreads();                                    // the zero fill is done
     ld.load(p, n, p0, q0);
-    ld.store(p, xs, n, p0, q0);
+    ld.store(p, xs, raw, n, p0, q0);
   }
   __syncthreads();
   for (int tile = blockIdx.x; tile < p.ntiles; tile += gridDim.x) {
@@ -280,7 +302,7 @@ __global__ void __launch_bounds__(STT, 2) fm_stem_fwd(StemP p) {
     if (next < p.ntiles) {
       int n1, p1, q1;
       tile_of(p, next, n1, p1, q1);
-      ld.store(p, xs + (buf ^ 1) * G::LDS_ELEMS, n1, p1, q1);
+      ld.store(p, xs + (buf ^ 1) * G::LDS_ELEMS, raw, n1, p1, q1);
     }
     __syncthreads();
     buf ^= 1;
@@ -301,6 +323,7 @@ __global__ void __launch_bounds__(STT, 2) fm_stem_wgrad(StemP p) {
   constexpr int NTW = (NT + 3) / 4;                     // per wave
   extern __shared__ __attribute__((aligned(16))) unsigned short xs[];
   unsigned short* gs = xs + G::LDS_ELEMS;               // [64][ST_GROW]
+  unsigned short* raw = gs + STK * ST_GROW + ((int)threadIdx.x >> 6) * 2 * ST_RAWN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, kg = lane >> 4;
   const int tq4 = l16 >> 2, tp4 = l16 & 3;             // transposed read: block row tq4, columns 4tp4 ..
@@ -326,7 +349,10 @@ __global__ void __launch_bounds__(STT, 2) fm_stem_wgrad(StemP p) {
       const int qend = min(p.Q, q0 + STQ);             // this tile's columns
       const long o = (((long)n * STK + f) * p.P + min(pp, p.P - 1)) * p.Q;
       float gv[8];
-      if (vec && pp < p.P && q + 8 <= qend) {
+      if (pp >= p.P || q >= qend) {                     // outside the tile: zeros, no loads
+#pragma unroll
+        for (int e = 0; e < 8; ++e) gv[e] = 0.f;
+      } else if (vec && q + 8 <= qend) {
         const bf16x8_t d = *reinterpret_cast<const bf16x8_t*>(p.dy + o + q);
         bf16x8_t yv = d;
         if constexpr (ACT != ACT_NONE) yv = *reinterpret_cast<const bf16x8_t*>(p.y + o + q);
@@ -360,7 +386,7 @@ __global__ void __launch_bounds__(STT, 2) fm_stem_wgrad(StemP p) {
 #pragma unroll
       for (int ub = 0; ub < L::NRT; ub += 2) {
         ld.load(p, n, p0, q0, ub);
-        ld.store(p, xs, n, p0, q0, ub);
+        ld.store(p, xs, raw, n, p0, q0, ub);
       }
     }
     __syncthreads();
@@ -461,7 +487,7 @@ void stem_launch(StemP& p, int mode, float* dw, float* db, int grid, hipStream_t
   using G = StemGeo<CP, RS, SS>;
   const int lds = G::LDS_ELEMS * 2;
   if (mode == 0) {
-    const int lds2 = 2 * lds;                           // double-buffered image
+    const int lds2 = 2 * lds + ST_RAW_BYTES;            // double-buffered image + raw rows
     static bool attr = false;
     if (!attr) {
       (void)hipFuncSetAttribute((const void*)fm_stem_fwd<CP, RS, SS, S_, ACT>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -471,7 +497,7 @@ void stem_launch(StemP& p, int mode, float* dw, float* db, int grid, hipStream_t
     hipLaunchKernelGGL((fm_stem_fwd<CP, RS, SS, S_, ACT>), dim3(grid), dim3(STT), lds2, st, p);
     return;
   }
-  const int lds_w = lds + STK * ST_GROW * 2;             // the image + the g tile
+  const int lds_w = lds + STK * ST_GROW * 2 + ST_RAW_BYTES;   // the image + the g tile + raw rows
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)fm_stem_wgrad<CP, RS, SS, S_, ACT>, hipFuncAttributeMaxDynamicSharedMemorySize,
