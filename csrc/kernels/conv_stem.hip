@@ -136,6 +136,19 @@ struct StemLoader {
     const int lane = threadIdx.x & 63, j = lane & 31;
     unsigned short* rw = raw + (lane >> 5) * ST_RAWN;
     const int xx0 = q0 * S_ - p.pl;
+    constexpr int KK = (G::XW + 31) / 32;
+    // the image columns of this lane's pixels (the same for every row task of the tile): bit e of
+    // cm[kk] = source column xx0 + k*S_ + e inside the image
+    unsigned cm[KK];
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      cm[kk] = 0;
+#pragma unroll
+      for (int e = 0; e < S_; ++e) {
+        const int xx = xx0 + (j + 32 * kk) * S_ + e;
+        cm[kk] |= (xx >= 0 && xx < p.W) ? (1u << e) : 0u;
+      }
+    }
 #pragma unroll
     for (int u = 0; u < NR; ++u) {
       const int r = ((int)threadIdx.x >> 5) + 8 * (ub + u);
@@ -147,14 +160,21 @@ struct StemLoader {
       const int rot = g0 & 7;                            // raw index of row position 0
       unsigned short* drow = xs + yr * G::XWA * G::CPS + ch;
 #pragma unroll
-      for (int kk = 0; kk < (G::XW + 31) / 32; ++kk) {
+      for (int kk = 0; kk < KK; ++kk) {
         const int k = j + 32 * kk;                       // s2d pixel of this row task
         if (r < nrow && k < G::XW) {
+          const unsigned m = rok ? cm[kk] : 0u;
           unsigned e16[S_];
+          if ((rot & 1) == 0) {                          // 4-B aligned pairs
 #pragma unroll
-          for (int e = 0; e < S_; ++e) {
-            const int xx = xx0 + k * S_ + e;
-            e16[e] = (rok && xx >= 0 && xx < p.W) ? (unsigned)rw[k * S_ + e + rot] : 0u;
+            for (int e = 0; e < S_; e += 2) {
+              const unsigned d = *reinterpret_cast<const unsigned*>(rw + k * S_ + e + rot);
+              e16[e] = (m >> e) & 1 ? (d & 0xffffu) : 0u;
+              e16[e + 1] = (m >> (e + 1)) & 1 ? (d >> 16) : 0u;
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < S_; ++e) e16[e] = (m >> e) & 1 ? (unsigned)rw[k * S_ + e + rot] : 0u;
           }
           if constexpr (S_ == 4)
             *reinterpret_cast<uint2*>(drow + k * G::CPS) = uint2{e16[0] | (e16[1] << 16), e16[2] | (e16[3] << 16)};
