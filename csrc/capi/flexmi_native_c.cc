@@ -590,6 +590,11 @@ int fmn_model_pool2d(fmn_model_t m, int input_tensor, int kernel_h, int kernel_w
                  -1);
 }
 
+int fmn_model_batch_norm(fmn_model_t m, int input_tensor, int relu) {
+  if (!m) return fail("fmn_model_batch_norm: null model");
+  return guarded([&] { return m->m->batch_norm(input_tensor, relu != 0); }, -1);
+}
+
 int fmn_model_sparse_input(fmn_model_t m, int bag) {
   if (!m) return fail("fmn_model_sparse_input: null model");
   return guarded([&] { return m->m->sparse_input(bag); }, -1);

@@ -168,6 +168,9 @@ int fmn_model_conv2d(fmn_model_t m, int input_tensor, int out_channels, int kern
                      int stride_w, int pad_h, int pad_w, int activation, int use_bias);
 int fmn_model_pool2d(fmn_model_t m, int input_tensor, int kernel_h, int kernel_w, int stride_h, int stride_w, int pad_h,
                      int pad_w, int is_max);
+/* batch norm of an image tensor (training-mode statistics over this rank's samples, scale 1 / bias 0
+ * at init, optional fused ReLU); returns the output tensor id */
+int fmn_model_batch_norm(fmn_model_t m, int input_tensor, int relu);
 /* DLRM graphs: a sparse input (int64 [B][bag] lookup indices of the GLOBAL batch) -> its id; an
  * embedding table rows x dim over a sparse input (SUM bag) -> its [B][dim] tensor id; the dot
  * interaction of a bottom tensor and n embedding tensors -> its [B][W] tensor id (W = dim +

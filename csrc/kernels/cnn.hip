@@ -317,6 +317,88 @@ __global__ void __launch_bounds__(256) fm_pool_fwd_band(const T* __restrict__ x,
   }
 }
 
+// bf16 form of fm_pool_fwd_band: the block's input chunk is staged with 16-B loads aligned down from
+// its first element (all of a thread's loads in flight at once) into a bf16 LDS image that starts at
+// that aligned element; the windows read it with 2-B LDS loads.  (The 2-B staging loads of the band
+// kernel needed two or more dependent load rounds per block.)
+__global__ void __launch_bounds__(256) fm_pool_fwd_band_v8(const unsigned short* __restrict__ x, unsigned short* __restrict__ y,
+                                                           unsigned char* __restrict__ code, int NC, int H, int W, int P, int Q,
+                                                           int kh, int kw, int sh, int sw, int pt, int pl, int is_max, int act,
+                                                           int PB, int nbands, int G, FastDiv dQ, FastDiv dPQ, long total) {
+  extern __shared__ __attribute__((aligned(16))) unsigned short sxb[];
+  int nc0, band, planes;
+  if (G > 1) {
+    nc0 = blockIdx.x * G;
+    band = 0;
+    planes = min(G, NC - nc0);
+  } else {
+    nc0 = blockIdx.x / nbands;
+    band = blockIdx.x - nc0 * nbands;
+    planes = 1;
+  }
+  const int p0 = band * PB, p1 = min(P, p0 + PB);
+  const int hlo = G > 1 ? 0 : max(0, p0 * sh - pt);
+  const int hhi = G > 1 ? H : min(H, (p1 - 1) * sh - pt + kh);
+  const int rows = max(0, hhi - hlo);
+  const long start = ((long)nc0 * H + hlo) * W;
+  const long a0 = start & ~7L;
+  const int off = (int)(start - a0);
+  const int nst = planes * rows * W;
+  const int nvec = (off + nst + 7) >> 3;
+  for (int v0 = 0; v0 < nvec; v0 += 256 * 4) {
+    u32x4_t vv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int v = min(v0 + u * 256 + (int)threadIdx.x, nvec - 1);
+      const long g = a0 + 8L * v;
+      if (g + 8 <= total) {
+        vv[u] = *reinterpret_cast<const u32x4_t*>(x + g);
+      } else {                                         // the tensor's last partial vector
+        unsigned e16[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) e16[e] = g + e < total ? x[g + e] : 0u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) vv[u][i] = e16[2 * i] | (e16[2 * i + 1] << 16);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int v = v0 + u * 256 + (int)threadIdx.x;
+      if (v < nvec) *reinterpret_cast<u32x4_t*>(sxb + 8 * v) = vv[u];
+    }
+  }
+  __syncthreads();
+  const int nout1 = (p1 - p0) * Q;
+  const int nout = planes * nout1;
+  for (int o = threadIdx.x; o < nout; o += 256) {
+    int gi = 0, r = o;
+    if (G > 1) {
+      gi = fdiv(o, dPQ);
+      r = o - gi * nout1;
+    }
+    const int pr = fdiv(r, dQ), q = r - pr * Q;
+    const int p = p0 + pr;
+    const int h0 = p * sh - pt, w0 = q * sw - pl;
+    const int r0 = max(0, -h0), r1 = min(kh, H - h0), c0 = max(0, -w0), c1 = min(kw, W - w0);
+    const unsigned short* plane = sxb + off + gi * rows * W;
+    float m = -INFINITY, sacc = 0.f;
+    int bc = 255;
+    for (int rr = r0; rr < r1; ++rr) {
+      const unsigned short* row = plane + (h0 + rr - hlo) * W + w0;
+      for (int c = c0; c < c1; ++c) {
+        const float v = bf2f(row[c]);
+        if (v > m || bc == 255) bc = rr * kw + c;
+        m = fmaxf(m, v);
+        sacc += v;
+      }
+    }
+    const int cnt = max(0, r1 - r0) * max(0, c1 - c0);
+    const long oi = ((long)(nc0 + gi) * P + p) * Q + q;
+    y[oi] = f2bf(act_fwd(act, is_max ? m : (cnt ? sacc / cnt : 0.f)));
+    if (code) code[oi] = (unsigned char)bc;
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) fm_pool_bwd_band(const T* __restrict__ y, const T* __restrict__ dy,
                                                         const unsigned char* __restrict__ code, T* __restrict__ dx, int NC,
@@ -442,24 +524,44 @@ __global__ void __launch_bounds__(256) fm_pool_bwd_max_scatter(const T* __restri
   // (measured and deleted in r6: running the (p mod ceil(kh/sh), q mod ceil(kw/sw)) window classes one
   // after another with plain LDS read-add-writes instead of LDS float atomics -- 82.5 k vs 84.1 k
   // img/s on AlexNet b256, profiles/pool_scatter_phases_ab_r5z.txt)
-  for (int e = threadIdx.x; e < nwin; e += 256) {
-    int gi = 0, r = e;
-    if (G > 1) {
-      gi = fdiv(e, dPQ);
-      r = e - gi * nwin1;
+  // 4 windows per thread per pass with every (code, dy, y) load issued up front: the code -> dy
+  // dependency was a second memory round trip per window
+  for (int e0 = 0; e0 < nwin; e0 += 256 * 4) {
+    long oi[4];
+    int cdv[4];
+    float gdv[4], yvv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = min(e0 + u * 256 + (int)threadIdx.x, nwin - 1);
+      int gi = 0, r = e;
+      if (G > 1) {
+        gi = fdiv(e, dPQ);
+        r = e - gi * nwin1;
+      }
+      const int pr = fdiv(r, dQ), q = r - pr * Q;
+      oi[u] = ((long)(nc0 + gi) * P + plo + pr) * Q + q;
+      cdv[u] = code[oi[u]];
+      gdv[u] = tof(dy[oi[u]]);
+      yvv[u] = act == ACT_NONE ? 0.f : tof(y[oi[u]]);
     }
-    const int pr = fdiv(r, dQ), q = r - pr * Q;
-    const int p = plo + pr;
-    const long oi = ((long)(nc0 + gi) * P + p) * Q + q;
-    const int cd = code[oi];
-    if (cd == 255) continue;
-    const int rr = fdiv(cd, dkw), cc = cd - rr * kw;
-    const int h = p * sh - pt + rr;
-    if (h < h0b || h >= h1b) continue;             // this window's max lies in another band
-    const int w = q * sw - pl + cc;
-    const float gd = tof(dy[oi]);
-    const float v = act == ACT_NONE ? gd : act_bwd(act, tof(y[oi]), gd);
-    atomicAdd(&sdx[(gi * rows + h - h0b) * W + w], v);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * 256 + (int)threadIdx.x;
+      if (e >= nwin || cdv[u] == 255) continue;
+      int gi = 0, r = e;
+      if (G > 1) {
+        gi = fdiv(e, dPQ);
+        r = e - gi * nwin1;
+      }
+      const int pr = fdiv(r, dQ), q = r - pr * Q;
+      const int p = plo + pr;
+      const int rr = fdiv(cdv[u], dkw), cc = cdv[u] - rr * kw;
+      const int h = p * sh - pt + rr;
+      if (h < h0b || h >= h1b) continue;           // this window's max lies in another band
+      const int w = q * sw - pl + cc;
+      const float v = act == ACT_NONE ? gdv[u] : act_bwd(act, yvv[u], gdv[u]);
+      atomicAdd(&sdx[(gi * rows + h - h0b) * W + w], v);
+    }
   }
   __syncthreads();
   // (a 16-B vector-store form of this loop -- 8 bf16 per lane between scalar head / tail -- measured
@@ -662,6 +764,9 @@ static void fm_transpose_batched_t(const void* in, const void* yin, void* out, i
                      (T*)out, A, B, act, mode);
 }
 
+// the 16-B staged bf16 forward (fm_pool_fwd_band_v8) for bf16; the 2-B staging band kernel for fp32
+constexpr bool POOL_FWD_V8 = true;
+
 template <typename T>
 static void fm_pool_fwd_t(const void* x, void* y, unsigned char* code, int N, int C, int H, int W, int P, int Q, int kh, int kw,
                           int sh, int sw, int pt, int pl, int is_max, int act, hipStream_t st) {
@@ -675,6 +780,15 @@ static void fm_pool_fwd_t(const void* x, void* y, unsigned char* code, int N, in
     const int G = (nbands == 1 && (long)H * W <= 2048) ? std::max(1, std::min(NC, 4096 / (H * W))) : 1;
     const int rows = G > 1 ? H : std::min(H, (PB - 1) * sh + kh);
     const int blocks = G > 1 ? (NC + G - 1) / G : NC * nbands;
+    if constexpr (sizeof(T) == 2) {
+      if (POOL_FWD_V8) {
+        const size_t lds = ((size_t)G * rows * W + 16) * 2;
+        hipLaunchKernelGGL(fm_pool_fwd_band_v8, dim3(blocks), dim3(256), lds, st, (const unsigned short*)x, (unsigned short*)y,
+                           is_max ? code : nullptr, NC, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, PB, nbands, G,
+                           make_fastdiv(Q), make_fastdiv(P * Q), (long)NC * H * W);
+        return;
+      }
+    }
     hipLaunchKernelGGL(fm_pool_fwd_band<T>, dim3(blocks), dim3(256), (size_t)G * rows * W * sizeof(float), st, (const T*)x,
                        (T*)y, is_max ? code : nullptr, NC, H, W, P, Q, kh, kw, sh, sw, pt, pl, is_max, act, PB, nbands, G,
                        make_fastdiv(Q), make_fastdiv(P * Q));

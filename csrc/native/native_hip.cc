@@ -11,7 +11,8 @@
 //                  device lr (fused sparse SGD of the touched rows); fm_dot_interaction_{fwd,bwd}_f32
 //                  (v_mfma_f32_32x32x2_f32); the exchange = RCCL grouped send / recv per peer
 //   convolutions   fm_conv_fwd / fm_conv_act_bwd / fm_conv_wgrad / fm_conv_dgrad (fp32 implicit GEMM
-//                  on MFMA), fm_pool_fwd / fm_pool_bwd -- the Python executor's Conv2D / Pool2D kernels
+//                  on MFMA), fm_pool_fwd / fm_pool_bwd, fm_bn_fwd / fm_bn_bwd -- the Python executor's Conv2D /
+//                  Pool2D / BatchNorm kernels
 //   communication  one RCCL communicator per model (unique id handed over through a file in the
 //                  rendezvous directory); bucket all-reduces on a second HIP stream, started as
 //                  soon as the bucket's last gradient kernel is enqueued (event dependency) and
@@ -76,6 +77,10 @@ void fm_pool_fwd(const void* x, void* y, unsigned char* code, int N, int C, int 
 void fm_pool_bwd(const void* x, const void* y, const void* dy, void* dx, unsigned char* code, int code_ready, int N, int C,
                  int H, int W, int P, int Q, int kh, int kw, int sh, int sw, int pt, int pl, int is_max, int act, int acc,
                  int bf16, hipStream_t st);
+void fm_bn_fwd(const void* x, void* y, const float* gamma, const float* beta, float* stats, float* meaninv, int N, int C,
+               int HW, float eps, int relu, int bf16, hipStream_t st);
+void fm_bn_bwd(const void* x, const void* y, const void* dy, const float* meaninv, const float* gamma, float* gsum,
+               float* dgamma, float* dbeta, void* dx, int N, int C, int HW, int relu, int acc, int bf16, hipStream_t st);
 }
 
 namespace flexmi {
@@ -264,6 +269,14 @@ class HipEngine : public Engine {
                 const Pool& p) override {
     fm_pool_bwd(x, y, dy, dx, const_cast<unsigned char*>(code), 1, N, p.C, p.H, p.W, p.P, p.Q, p.kh, p.kw, p.sh, p.sw, p.ph,
                 p.pw, p.max ? 1 : 0, ACT_NONE, 0, 0, st_);
+  }
+  // batch norm on the executor's kernels (cnn.hip): buf = stats [2C] | mean, 1/std [2C] | sums [2C]
+  void bn_fwd(const float* x, float* y, const float* gamma, const float* beta, float* buf, int N, const BNorm& b) override {
+    fm_bn_fwd(x, y, gamma, beta, buf, buf + 2 * b.C, N, b.C, b.H * b.W, (float)kBnEps, b.relu ? 1 : 0, 0, st_);
+  }
+  void bn_bwd(const float* x, const float* y, const float* dy, const float* gamma, float* buf, float* dgamma, float* dbeta,
+              float* dx, int N, const BNorm& b) override {
+    fm_bn_bwd(x, y, dy, buf + 2 * b.C, gamma, buf + 4 * b.C, dgamma, dbeta, dx, N, b.C, b.H * b.W, b.relu ? 1 : 0, 0, 0, st_);
   }
 
   void allreduce_start(float* buf, int64_t n) override {

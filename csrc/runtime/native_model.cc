@@ -363,6 +363,60 @@ class CpuEngine : public Engine {
           }
       }
   }
+  // batch norm in double: buf[0..C) mean, buf[C..2C) 1/sqrt(var + eps)
+  void bn_fwd(const float* x, float* y, const float* gamma, const float* beta, float* buf, int N, const BNorm& b) override {
+    const int64_t HW = (int64_t)b.H * b.W, m = (int64_t)N * HW;
+    for (int c = 0; c < b.C; ++c) {
+      double s = 0.0, s2 = 0.0;
+      for (int n = 0; n < N; ++n) {
+        const float* xc = x + ((int64_t)n * b.C + c) * HW;
+        for (int64_t i = 0; i < HW; ++i) s += xc[i];
+      }
+      const double mean = s / (double)m;
+      for (int n = 0; n < N; ++n) {
+        const float* xc = x + ((int64_t)n * b.C + c) * HW;
+        for (int64_t i = 0; i < HW; ++i) s2 += ((double)xc[i] - mean) * ((double)xc[i] - mean);
+      }
+      const double inv = 1.0 / std::sqrt(s2 / (double)m + kBnEps);
+      buf[c] = (float)mean;
+      buf[b.C + c] = (float)inv;
+      for (int n = 0; n < N; ++n) {
+        const float* xc = x + ((int64_t)n * b.C + c) * HW;
+        float* yc = y + ((int64_t)n * b.C + c) * HW;
+        for (int64_t i = 0; i < HW; ++i) {
+          const float v = (float)(((double)xc[i] - mean) * inv) * gamma[c] + beta[c];
+          yc[i] = b.relu ? std::max(v, 0.f) : v;
+        }
+      }
+    }
+  }
+  void bn_bwd(const float* x, const float* y, const float* dy, const float* gamma, float* buf, float* dgamma, float* dbeta,
+              float* dx, int N, const BNorm& b) override {
+    const int64_t HW = (int64_t)b.H * b.W, m = (int64_t)N * HW;
+    for (int c = 0; c < b.C; ++c) {
+      const double mean = buf[c], inv = buf[b.C + c];
+      double sg = 0.0, sgx = 0.0;
+      auto G = [&](int n, int64_t i) {
+        const int64_t o = ((int64_t)n * b.C + c) * HW + i;
+        return (double)(b.relu && !(y[o] > 0.f) ? 0.f : dy[o]);
+      };
+      for (int n = 0; n < N; ++n)
+        for (int64_t i = 0; i < HW; ++i) {
+          const double g = G(n, i);
+          sg += g;
+          sgx += g * ((double)x[((int64_t)n * b.C + c) * HW + i] - mean) * inv;
+        }
+      dbeta[c] = (float)sg;
+      dgamma[c] = (float)sgx;
+      if (!dx) continue;
+      for (int n = 0; n < N; ++n)
+        for (int64_t i = 0; i < HW; ++i) {
+          const int64_t o = ((int64_t)n * b.C + c) * HW + i;
+          const double xh = ((double)x[o] - mean) * inv;
+          dx[o] = (float)(gamma[c] * inv / (double)m * ((double)m * G(n, i) - sg - xh * sgx));
+        }
+    }
+  }
 
  private:
   std::unique_ptr<HostComm> comm_;
@@ -417,6 +471,7 @@ Model::~Model() {
   rel(labels_);
   rel(stats_);
   for (auto* p : pool_code_) rel(p);
+  for (auto* p : bn_buf_) rel(p);
 }
 
 void Model::check_tensor(int t, const char* what) const {
@@ -515,6 +570,29 @@ int Model::pool2d(int x, int kh, int kw, int sh, int sw, int ph, int pw, bool ma
   pools_.push_back(pl);
   nodes_.push_back({K_POOL, (int)pools_.size() - 1});
   return pl.y;
+}
+
+int Model::batch_norm(int x, bool relu) {
+  if (compiled_) throw std::logic_error("native model: batch_norm after compile");
+  check_tensor(x, "batch_norm");
+  if (shape_[x].size() != 3) throw std::invalid_argument("native model: batch_norm needs an image tensor [C][H][W]");
+  BNorm b;
+  b.x = x;
+  b.C = shape_[x][0];
+  b.H = shape_[x][1];
+  b.W = shape_[x][2];
+  b.relu = relu;
+  consumers_[x]++;
+  b.y = new_tensor({b.C, b.H, b.W});
+  for (int* e : {&b.g, &b.b}) {
+    *e = (int)pnumel_.size();
+    pnumel_.push_back(b.C);
+    entry_table_.push_back(-1);
+    entry_dense_.push_back(-1);
+  }
+  bns_.push_back(b);
+  nodes_.push_back({K_BN, (int)bns_.size() - 1});
+  return b.y;
 }
 
 int Model::dense(int x, int out_dim, int act, bool bias) {
@@ -686,6 +764,7 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
   for (Dense& d : ops_) d.need_dx = d.x != input_;
   for (Conv& c : convs_) c.need_dx = c.x != input_;
   for (Pool& pl : pools_) pl.need_dx = pl.x != input_;
+  for (BNorm& b : bns_) b.need_dx = b.x != input_;
   // fused epilogues: a dense layer whose input is another dense layer's output applies that
   // layer's activation backward in its dX GEMM (the producer then reads its gradient as dpre)
   for (Dense& hi : ops_) {
@@ -743,6 +822,9 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
     } else if (it->kind == K_CONV) {
       w = convs_[it->idx].w;
       b = convs_[it->idx].b;
+    } else if (it->kind == K_BN) {
+      w = bns_[it->idx].g;
+      b = bns_[it->idx].b;
     } else {
       continue;
     }
@@ -840,6 +922,8 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
   pool_code_.assign(pools_.size(), nullptr);
   for (size_t i = 0; i < pools_.size(); ++i)
     pool_code_[i] = (unsigned char*)eng_->alloc((size_t)Bl_ * pools_[i].C * pools_[i].P * pools_[i].Q);
+  bn_buf_.assign(bns_.size(), nullptr);
+  for (size_t i = 0; i < bns_.size(); ++i) bn_buf_[i] = (float*)eng_->alloc((size_t)6 * bns_[i].C * 4);
   const int C = last.N;
   if (loss_ == LOSS_SCCE) probs_ = (float*)eng_->alloc((size_t)Bl_ * C * 4);
   labels_ = eng_->alloc((size_t)Bl_ * C * 4);
@@ -871,6 +955,11 @@ void Model::init_weights(uint64_t seed) {
       std::vector<float> z(c.K, 0.f);
       set_param(c.b, z.data());
     }
+  }
+  for (const BNorm& b : bns_) {    // scale 1, bias 0
+    std::vector<float> one(b.C, 1.f), zero(b.C, 0.f);
+    set_param(b.g, one.data());
+    set_param(b.b, zero.data());
   }
   for (const Emb& e : embs_) {
     if (slice_of(e, rank_) < 0) continue;
@@ -1091,6 +1180,9 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
     } else if (n.kind == K_POOL) {
       const Pool& pl = pools_[n.idx];
       eng_->pool_fwd(act_[pl.x], act_[pl.y], pool_code_[n.idx], Bl_, pl);
+    } else if (n.kind == K_BN) {
+      const BNorm& b = bns_[n.idx];
+      eng_->bn_fwd(act_[b.x], act_[b.y], params_ + pofs_[b.g], params_ + pofs_[b.b], bn_buf_[n.idx], Bl_, b);
     }
   }
   // loss: gradient scaled by 1 / global batch (the reference's convention), so summing the
@@ -1143,6 +1235,17 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
     } else if (n.kind == K_POOL) {
       const Pool& pl = pools_[n.idx];
       if (pl.need_dx) eng_->pool_bwd(act_[pl.x], act_[pl.y], grad_[pl.y], grad_[pl.x], pool_code_[n.idx], Bl_, pl);
+    } else if (n.kind == K_BN) {
+      const BNorm& b = bns_[n.idx];
+      eng_->bn_bwd(act_[b.x], act_[b.y], grad_[b.y], params_ + pofs_[b.g], bn_buf_[n.idx], grads_ + pofs_[b.g],
+                   grads_ + pofs_[b.b], b.need_dx ? grad_[b.x] : nullptr, Bl_, b);
+      if (world_ > 1) {
+        for (int e : {b.g, b.b}) {
+          const int bi = bucket_of[e];
+          if (--left[bi] == 0)
+            eng_->allreduce_start(grads_ + wplan_.buckets[bi][0], wplan_.buckets[bi][1] - wplan_.buckets[bi][0]);
+        }
+      }
     } else if (n.kind == K_DOT) {
       const Dot& d = dots_[n.idx];
       std::vector<const float*> z;
@@ -1239,6 +1342,10 @@ std::string Model::describe() const {
       o << "  conv" << n.idx << ": " << c.C << "x" << c.H << "x" << c.W << " -> " << c.K << "x" << c.P << "x" << c.Q << " kernel "
         << c.R << "x" << c.S << " stride " << c.sh << "x" << c.sw << " pad " << c.ph << "x" << c.pw << " act " << c.act
         << " (data parallel)\n";
+    } else if (n.kind == K_BN) {
+      const BNorm& b = bns_[n.idx];
+      o << "  batchnorm" << n.idx << ": " << b.C << "x" << b.H << "x" << b.W << (b.relu ? " relu" : "")
+        << " (local-shard statistics, data parallel)\n";
     } else if (n.kind == K_POOL) {
       const Pool& pl = pools_[n.idx];
       o << "  pool" << n.idx << " " << (pl.max ? "max" : "avg") << ": " << pl.C << "x" << pl.H << "x" << pl.W << " -> " << pl.C

@@ -37,6 +37,7 @@ WeightPlan plan_weights(const std::vector<int64_t>& numels, int64_t cap_elems);
 namespace nm {
 
 enum Act { ACT_NONE = 10, ACT_RELU = 11, ACT_SIGMOID = 12, ACT_TANH = 13 };
+constexpr double kBnEps = 1e-5;   // batch-norm epsilon (flexmi.ops.conv.BatchNorm.eps)
 enum Loss { LOSS_SCCE = 51, LOSS_MSE_AVG = 52, LOSS_BCE = 54 };
 
 struct Dense {
@@ -120,6 +121,16 @@ struct Pool {
   bool need_dx = true;
 };
 
+// spatial batch normalisation (src/ops/batch_norm.cu:348-503): training-mode statistics over the
+// local shard's samples and pixels per channel, y = act(gamma * xhat + beta), optional ReLU
+struct BNorm {
+  int x = -1, y = -1;
+  int C = 0, H = 0, W = 0;
+  bool relu = true;
+  int g = -1, b = -1;          // parameter entry ids (scale, bias)
+  bool need_dx = true;
+};
+
 struct StepStat {
   double loss = 0.0;
   int64_t samples = 0;
@@ -140,6 +151,8 @@ class Model {
   // flattened)
   int conv2d(int x, int out_channels, int kh, int kw, int sh, int sw, int ph, int pw, int act, bool bias);
   int pool2d(int x, int kh, int kw, int sh, int sw, int ph, int pw, bool max);
+  // batch norm of an image tensor (scale 1, bias 0 at init); returns the normalised tensor id
+  int batch_norm(int x, bool relu);
   // sparse index input [B][bag] (int64, the GLOBAL batch on every rank); returns its id
   int sparse_input(int bag);
   // embedding table rows x dim looked up by sparse input `sparse` (SUM over the bag); returns the
@@ -182,7 +195,7 @@ class Model {
   const WeightPlan& weight_plan() const { return wplan_; }
 
  private:
-  enum Kind { K_DENSE = 0, K_EMB = 1, K_DOT = 2, K_CONV = 3, K_POOL = 4 };
+  enum Kind { K_DENSE = 0, K_EMB = 1, K_DOT = 2, K_CONV = 3, K_POOL = 4, K_BN = 5 };
   struct Node {
     int kind, idx;
   };
@@ -197,6 +210,8 @@ class Model {
   std::vector<Conv> convs_;
   std::vector<Pool> pools_;
   std::vector<unsigned char*> pool_code_;     // pool id -> max-pool argmax codes (engine scratch)
+  std::vector<BNorm> bns_;
+  std::vector<float*> bn_buf_;                // bn id -> [6C] engine scratch (statistics, mean / 1/std, sums)
   int new_tensor(const std::vector<int>& shape);
   std::vector<int> consumers_;                // tensor id -> number of consumers
   int input_ = -1;
@@ -293,6 +308,11 @@ class Engine {
   virtual void pool_fwd(const float* x, float* y, unsigned char* code, int N, const Pool& p) = 0;
   virtual void pool_bwd(const float* x, const float* y, const float* dy, float* dx, const unsigned char* code, int N,
                         const Pool& p) = 0;
+  // batch norm: buf [6C] floats of engine scratch kept from the forward to the backward; the
+  // backward writes dgamma / dbeta and overwrites dx (skipped when null)
+  virtual void bn_fwd(const float* x, float* y, const float* gamma, const float* beta, float* buf, int N, const BNorm& b) = 0;
+  virtual void bn_bwd(const float* x, const float* y, const float* dy, const float* gamma, float* buf, float* dgamma,
+                      float* dbeta, float* dx, int N, const BNorm& b) = 0;
 };
 
 // CPU engine; world > 1 ranks (one process each) exchange through a HostComm in `rendezvous`

@@ -4,7 +4,10 @@
  * softmax cross-entropy, SGD, data parallel over `world` rank processes (bucketed all-reduce through
  * the CPU engine's host communicator, or RCCL on the HIP engine).
  *
- *   native_cnn <cpu|hip> <out prefix> <steps> <world> <rendezvous dir>
+ *   native_cnn <cpu|hip> <out prefix> <steps> <world> <rendezvous dir> [bn]
+ *
+ * bn: the first convolution has no activation and feeds a batch norm with a fused ReLU (statistics
+ * over each rank's samples).
  *
  * <prefix>.init.bin (rank 0): int32 B, int32 steps, int32 nparams; per param int64 numel + float
  *   init[numel]; per step float x[B*3*20*20], int32 labels[B].
@@ -32,6 +35,7 @@
   } while (0)
 
 static uint32_t rng = 4242u;
+static int g_bn = 0;
 static float frand(void) {
   rng = rng * 1664525u + 1013904223u;
   return (float)(rng >> 8) / (float)(1u << 24);
@@ -45,7 +49,12 @@ static int run_rank(int device, const char* prefix, int steps, int rank, int wor
   }
   int t;
   CHECK(t = fmn_model_input_image(m, CIN, HW, HW));
-  CHECK(t = fmn_model_conv2d(m, t, 8, 5, 5, 1, 1, 2, 2, 11, 1));
+  if (g_bn) {
+    CHECK(t = fmn_model_conv2d(m, t, 8, 5, 5, 1, 1, 2, 2, 10, 1));
+    CHECK(t = fmn_model_batch_norm(m, t, 1));
+  } else {
+    CHECK(t = fmn_model_conv2d(m, t, 8, 5, 5, 1, 1, 2, 2, 11, 1));
+  }
   CHECK(t = fmn_model_pool2d(m, t, 3, 3, 2, 2, 0, 0, 1));
   CHECK(t = fmn_model_conv2d(m, t, 16, 3, 3, 1, 1, 1, 1, 11, 1));
   CHECK(t = fmn_model_pool2d(m, t, 2, 2, 2, 2, 1, 1, 0));
@@ -114,9 +123,10 @@ static int run_rank(int device, const char* prefix, int steps, int rank, int wor
 
 int main(int argc, char** argv) {
   if (argc < 6) {
-    fprintf(stderr, "usage: native_cnn <cpu|hip> <out prefix> <steps> <world> <rendezvous dir>\n");
+    fprintf(stderr, "usage: native_cnn <cpu|hip> <out prefix> <steps> <world> <rendezvous dir> [bn]\n");
     return 2;
   }
+  g_bn = argc > 6 && strcmp(argv[6], "bn") == 0;
   const int device = strcmp(argv[1], "hip") == 0 ? 1 : 0;
   const int steps = atoi(argv[3]), world = atoi(argv[4]);
   if (world < 1 || world > 16 || B % world) return 2;

@@ -497,7 +497,7 @@ def _parse_cnn(prefix, world):
     return dict(B=B, steps=steps, init=init, batches=batches, ranks=ranks)
 
 
-def _replay_cnn(rec):
+def _replay_cnn(rec, bn=False):
     """The same CNN, weights and batches through flexmi's Python executor (CPU, fp32, world 1)."""
     from flexmi.core import ActiMode, FFConfig, FFModel, LossType, MetricsType, PoolType, SGDOptimizer
     B = rec["B"]
@@ -505,7 +505,11 @@ def _replay_cnn(rec):
     cfg.batchSize, cfg.device, cfg.compute_dtype = B, "cpu", "fp32"
     m = FFModel(cfg)
     x = m.create_tensor([B, 3, 20, 20], name="image")
-    t = m.conv2d(x, 8, 5, 5, 1, 1, 2, 2, ActiMode.AC_MODE_RELU)
+    if bn:
+        t = m.conv2d(x, 8, 5, 5, 1, 1, 2, 2, ActiMode.AC_MODE_NONE)
+        t = m.batch_norm(t, relu=True)
+    else:
+        t = m.conv2d(x, 8, 5, 5, 1, 1, 2, 2, ActiMode.AC_MODE_RELU)
     t = m.pool2d(t, 3, 3, 2, 2, 0, 0, PoolType.POOL_MAX)
     t = m.conv2d(t, 16, 3, 3, 1, 1, 1, 1, ActiMode.AC_MODE_RELU)
     t = m.pool2d(t, 2, 2, 2, 2, 1, 1, PoolType.POOL_AVG)
@@ -550,19 +554,45 @@ def test_native_c_cnn_trains_like_the_executor(tmp_path, world):
     assert np.all(np.isfinite(rec["ranks"][0][1]))
 
 
+def test_native_c_cnn_batch_norm(tmp_path):
+    """Batch norm in the native compiler: at world 1 the C program ends with the executor's parameters;
+    at world 2 each rank normalises with its own samples' statistics (the executor's and the reference's
+    data-parallel semantics), the gradients are all-reduced and the replicas stay identical."""
+    exe = _build_cnn_c(tmp_path)
+    for world in (1, 2):
+        rdv = tmp_path / f"rdv{world}"
+        rdv.mkdir()
+        prefix = str(tmp_path / f"bn{world}")
+        r = subprocess.run([exe, "cpu", prefix, "4", str(world), str(rdv), "bn"], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0 and "native_cnn ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+        assert "batchnorm0: 8x20x20 relu" in r.stdout
+        rec = _parse_cnn(prefix, world)
+        for i in range(len(rec["init"])):
+            for rk in rec["ranks"][1:]:
+                np.testing.assert_array_equal(rk[0][i], rec["ranks"][0][0][i])
+        assert np.all(np.isfinite(rec["ranks"][0][1]))
+        if world == 1:
+            got = _replay_cnn(rec, bn=True)
+            for i, want in enumerate(got):
+                np.testing.assert_allclose(rec["ranks"][0][0][i], want, rtol=1e-4, atol=1e-5, err_msg=f"param {i}")
+
+
 @pytest.mark.gpu
 def test_native_c_cnn_hip_engine_matches_cpu(tmp_path):
     """The same C CNN program on the HIP engine (flexmi's fp32 implicit-GEMM convolution and pooling
     kernels) against the CPU engine."""
     exe = _build_cnn_c(tmp_path)
-    recs = {}
-    for dev in ("cpu", "hip"):
-        rdv = tmp_path / f"rdv_{dev}"
-        rdv.mkdir()
-        r = subprocess.run([exe, dev, str(tmp_path / dev), "4", "1", str(rdv)], capture_output=True, text=True, timeout=120)
-        assert r.returncode == 0 and "native_cnn ok" in r.stdout, (dev, r.stdout[-2000:] + r.stderr[-2000:])
-        recs[dev] = _parse_cnn(str(tmp_path / dev), 1)
-    c, h = recs["cpu"], recs["hip"]
-    for a, b in zip(c["ranks"][0][0], h["ranks"][0][0]):
-        np.testing.assert_allclose(b, a, rtol=1e-3, atol=1e-4)
-    np.testing.assert_allclose(h["ranks"][0][1], c["ranks"][0][1], rtol=1e-3)
+    for variant in ("", "bn"):
+        recs = {}
+        for dev in ("cpu", "hip"):
+            rdv = tmp_path / f"rdv_{dev}{variant}"
+            rdv.mkdir()
+            prefix = str(tmp_path / (dev + variant))
+            r = subprocess.run([exe, dev, prefix, "4", "1", str(rdv)] + ([variant] if variant else []), capture_output=True,
+                               text=True, timeout=120)
+            assert r.returncode == 0 and "native_cnn ok" in r.stdout, (dev, r.stdout[-2000:] + r.stderr[-2000:])
+            recs[dev] = _parse_cnn(prefix, 1)
+        c, h = recs["cpu"], recs["hip"]
+        for a, b in zip(c["ranks"][0][0], h["ranks"][0][0]):
+            np.testing.assert_allclose(b, a, rtol=1e-3, atol=1e-4, err_msg=variant)
+        np.testing.assert_allclose(h["ranks"][0][1], c["ranks"][0][1], rtol=1e-3, err_msg=variant)
