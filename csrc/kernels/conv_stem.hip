@@ -231,7 +231,7 @@ template <int CP, int RS, int SS, int S_, int ACT>
 __global__ void __launch_bounds__(STT, 2) fm_stem_fwd(StemP p) {
   using G = StemGeo<CP, RS, SS>;
   extern __shared__ __attribute__((aligned(16))) unsigned short xs[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int rw = wave >> 1, h = wave & 1;              // output row rw of the tile; filters 32h .. 32h+31
   const int l16 = lane & 15, kg = lane >> 4;
   // B fragments for the block's lifetime (fm_stem_wprep's [ks][nt][lane][8] layout): 16-B loads
@@ -344,7 +344,7 @@ __global__ void __launch_bounds__(STT, 2) fm_stem_wgrad(StemP p) {
   extern __shared__ __attribute__((aligned(16))) unsigned short xs[];
   unsigned short* gs = xs + G::LDS_ELEMS;               // [64][ST_GROW]
   unsigned short* raw = gs + STK * ST_GROW + ((int)threadIdx.x >> 6) * 2 * ST_RAWN;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l16 = lane & 15, kg = lane >> 4;
   const int tq4 = l16 >> 2, tp4 = l16 & 3;             // transposed read: block row tq4, columns 4tp4 ..
   for (int e = tid * 8; e < G::LDS_ELEMS; e += STT * 8)
