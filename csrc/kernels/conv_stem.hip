@@ -78,12 +78,13 @@ FM_DEVICE void tile_of(const StemP& p, int tile, int& n, int& p0, int& q0) {
 constexpr int ST_RAWN = 256;                            // elements of one raw row buffer (32 lanes x 8)
 constexpr int ST_RAW_BYTES = 4 * 2 * ST_RAWN * 2;       // per block: 4 waves x 2 row tasks
 
-template <int CP, int RS, int SS, int S_, int NR = (3 * S_ * (STP + RS - 1) + 7) / 8>
+template <int CP, int RS, int SS, int S_, int NR = (3 * S_ * (STP + RS - 1) + 7) / 8, int NTH = STT>
 struct StemLoader {
   using G = StemGeo<CP, RS, SS>;
   static constexpr int XWS = G::XW * S_;
   static_assert(XWS + 7 <= 256, "a row task spans at most 32 lanes x 8 elements");
-  static constexpr int NRT = (3 * S_ * G::XH + 7) / 8;   // rounds of 8 row tasks per block
+  static constexpr int RPR = NTH / 32;                   // row tasks per round (one per half-wave)
+  static constexpr int NRT = (3 * S_ * G::XH + RPR - 1) / RPR;   // rounds per tile
   u32x4_t v[NR];                                        // rounds ub .. ub + NR - 1
 
   FM_DEVICE static void row_of(const StemP& p, int r, int n, int p0, int q0, int& yr, int& ch, bool& rok, int& g0) {
@@ -102,7 +103,7 @@ struct StemLoader {
     const int total = p.N * p.C * p.H * p.W;
 #pragma unroll
     for (int u = 0; u < NR; ++u) {
-      const int r = ((int)threadIdx.x >> 5) + 8 * (ub + u);
+      const int r = ((int)threadIdx.x >> 5) + RPR * (ub + u);
       int yr, ch, g0;
       bool rok;
       row_of(p, min(r, nrow - 1), n, p0, q0, yr, ch, rok, g0);
@@ -151,7 +152,7 @@ struct StemLoader {
     }
 #pragma unroll
     for (int u = 0; u < NR; ++u) {
-      const int r = ((int)threadIdx.x >> 5) + 8 * (ub + u);
+      const int r = ((int)threadIdx.x >> 5) + RPR * (ub + u);
       int yr, ch, g0;
       bool rok;
       row_of(p, min(r, nrow - 1), n, p0, q0, yr, ch, rok, g0);
@@ -462,6 +463,169 @@ __global__ void __launch_bounds__(STT, 2) fm_stem_wgrad(StemP p) {
   }
 }
 
+// Pipelined weight gradient (the form the launcher uses): 8 waves per block, one block per CU; wave
+// w owns filters 32*(w&1) .. +31 and the k column blocks 7*(w>>1) .. +6 (NT/4 of them), so the
+// accumulators take 56 registers and the NEXT tile's image and g loads (28 registers) stay in
+// flight under this tile's MFMAs; images and g tiles double-buffered in LDS, one barrier per tile.
+// (The 4-wave form above staged synchronously: 67 % of its wave cycles waiting on memory.)
+constexpr int SW_NTH = 512;
+
+template <int CP, int RS, int SS, int S_>
+struct StemGLoader {                                   // the g tile of one block tile: 2 chunks per thread
+  u32x4_t d[2], y[2];
+  FM_DEVICE void load(const StemP& p, int n, int p0, int q0, bool need_y) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = (int)threadIdx.x + SW_NTH * i;
+      const int f = c >> 4, r = (c >> 3) & 1, c8 = (c & 7) * 8;
+      const int pp = p0 + r, q = q0 + c8;
+      const int qend = min(p.Q, q0 + STQ);
+      const long o = (((long)n * STK + f) * p.P + min(pp, p.P - 1)) * p.Q;
+      d[i] = u32x4_t{0u, 0u, 0u, 0u};
+      y[i] = u32x4_t{0u, 0u, 0u, 0u};
+      if (pp >= p.P || q >= qend) continue;            // outside the tile: zeros
+      if ((p.Q & 7) == 0 && q + 8 <= qend) {
+        d[i] = *reinterpret_cast<const u32x4_t*>(p.dy + o + q);
+        if (need_y) y[i] = *reinterpret_cast<const u32x4_t*>(p.y + o + q);
+      } else {
+        unsigned dv[8], yv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const bool ok = q + e < qend;
+          const long oi = o + (ok ? q + e : 0);
+          dv[e] = ok ? (unsigned)p.dy[oi] : 0u;
+          yv[e] = ok && need_y ? (unsigned)p.y[oi] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          d[i][k] = dv[2 * k] | (dv[2 * k + 1] << 16);
+          y[i][k] = yv[2 * k] | (yv[2 * k + 1] << 16);
+        }
+      }
+    }
+  }
+  template <int ACT>
+  FM_DEVICE void store(const StemP& p, unsigned short* gs, float (&dbs)[2]) const {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = (int)threadIdx.x + SW_NTH * i;
+      const int f = c >> 4, r = (c >> 3) & 1, c8 = (c & 7) * 8;
+      u32x4_t o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float g2[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float dd = bf2f((unsigned short)(d[i][k] >> (16 * h)));
+          const float yy = bf2f((unsigned short)(y[i][k] >> (16 * h)));
+          g2[h] = stem_act_bwd<ACT>(p.act, yy, dd);
+          dbs[i] += g2[h];
+        }
+        o[k] = (unsigned)f2bf(g2[0]) | ((unsigned)f2bf(g2[1]) << 16);
+      }
+      *reinterpret_cast<u32x4_t*>(gs + f * ST_GROW + r * 64 + c8) = o;
+    }
+  }
+};
+
+template <int CP, int RS, int SS, int S_, int ACT>
+__global__ void __launch_bounds__(SW_NTH, 1) fm_stem_wgrad2(StemP p) {
+  using G = StemGeo<CP, RS, SS>;
+  constexpr int NT = G::KP / 16;                        // k column blocks of 16
+  constexpr int NTW = (NT + 3) / 4;                     // per wave (four k quarters)
+  constexpr int BUF = G::LDS_ELEMS + STK * ST_GROW;     // one image + one g tile (elements)
+  using L = StemLoader<CP, RS, SS, S_, (3 * S_ * (STP + RS - 1) + SW_NTH / 32 - 1) / (SW_NTH / 32), SW_NTH>;
+  extern __shared__ __attribute__((aligned(16))) unsigned short xs[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l16 = lane & 15, kg = lane >> 4;
+  const int tq4 = l16 >> 2, tp4 = l16 & 3;
+  const int mh = wave & 1, kq = wave >> 1;
+  unsigned short* raw = xs + 2 * BUF + wave * 2 * ST_RAWN;
+  for (int e = tid * 8; e < 2 * BUF; e += SW_NTH * 8)
+    *reinterpret_cast<u32x4_t*>(xs + e) = u32x4_t{0u, 0u, 0u, 0u};
+  f32x4_t acc[2][NTW];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc[m][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float dbs[2] = {0.f, 0.f};                           // filters tid/16 and tid/16 + 32
+  L ld;
+  StemGLoader<CP, RS, SS, S_> gl;
+  int buf = 0;
+  if ((int)blockIdx.x < p.ntiles) {
+    int n, p0, q0;
+    tile_of(p, blockIdx.x, n, p0, q0);
+    __syncthreads();                                    // the zero fill is done
+    ld.load(p, n, p0, q0);
+    gl.load(p, n, p0, q0, ACT != ACT_NONE);
+    ld.store(p, xs, raw, n, p0, q0);
+    gl.template store<ACT>(p, xs + G::LDS_ELEMS, dbs);
+  }
+  __syncthreads();
+  for (int tile = blockIdx.x; tile < p.ntiles; tile += gridDim.x) {
+    const int next = tile + gridDim.x;
+    int n1 = 0, p1 = 0, q1 = 0;
+    if (next < p.ntiles) {                              // the next tile's loads fly under this tile's MFMAs
+      tile_of(p, next, n1, p1, q1);
+      ld.load(p, n1, p1, q1);
+      gl.load(p, n1, p1, q1, ACT != ACT_NONE);
+    }
+    const unsigned short* xb = xs + buf * BUF;
+    const unsigned short* gsb = xb + G::LDS_ELEMS;
+#pragma unroll
+    for (int r = 0; r < STP; ++r)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        u32x4_t ga[2];
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+          ga[m] = *reinterpret_cast<const u32x4_t*>(gsb + ((2 * mh + m) * 16 + l16) * ST_GROW + r * 64 + hh * 32 + kg * 8);
+        const int pix = (r * G::XWA + hh * 32 + kg * 8 + tq4) * G::CPS;
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+          const int nt = min(kq * NTW + j, NT - 1);
+          const int t = min(nt * 16 / CP, G::NTAP - 1), cp = nt * 16 - (nt * 16 / CP) * CP;
+          const int boff = ((t / SS) * G::XWA + t % SS) * G::CPS + cp + 4 * tp4;
+          const bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((st_lds_v4_t*)(xb + pix + boff));
+          const bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((st_lds_v4_t*)(xb + pix + 4 * G::CPS + boff));
+          bf16x8_t bx;
+          bx.lo = lo;
+          bx.hi = hi;
+#pragma unroll
+          for (int m = 0; m < 2; ++m)
+            acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8v_t, ga[m]),
+                                                                __builtin_bit_cast(bf16x8v_t, bx), acc[m][j], 0, 0, 0);
+        }
+      }
+    if (next < p.ntiles) {
+      unsigned short* nb = xs + (buf ^ 1) * BUF;
+      ld.store(p, nb, raw, n1, p1, q1);
+      gl.template store<ACT>(p, nb + G::LDS_ELEMS, dbs);
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+  float* part = p.part + (long)blockIdx.x * STK * (G::KP + 4);
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) {
+    const int nt = kq * NTW + j;
+    if (nt >= NT) break;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) part[((2 * mh + m) * 16 + 4 * kg + i) * (G::KP + 4) + nt * 16 + l16] = acc[m][j][i];
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    float v = dbs[i];
+    v += __shfl_xor(v, 1);
+    v += __shfl_xor(v, 2);
+    v += __shfl_xor(v, 4);
+    v += __shfl_xor(v, 8);
+    if ((tid & 15) == 0) part[((tid >> 4) + 32 * i) * (G::KP + 4) + G::KP] = v;
+  }
+}
+
 // dW[f][c][r][s] += sum over blocks of part[.][f][k(c, r, s)]; db[f] += sum of part[.][f][KP].  A block
 // takes 32 consecutive partial columns x 8 block slices (8 loads in flight per thread), then folds the
 // 8 slice sums in a fixed order (deterministic).
@@ -502,8 +666,11 @@ __global__ void __launch_bounds__(256) fm_stem_wgrad_reduce(const float* __restr
   }
 }
 
+// wgrad form: the pipelined 8-wave kernel for the 48-channel (stride-4) stems -- AlexNet 245 -> 135
+// us; the 4-wave kernel for the 16-channel (stride-2) ones, where the pipelined form measured
+// slower (ResNet-50 b64 142 vs 208 us, profiles/stem_forms_r7.txt)
 template <int CP, int RS, int SS, int S_, int ACT>
-void stem_launch(StemP& p, int mode, float* dw, float* db, int grid, hipStream_t st) {
+void stem_launch(StemP& p, int mode, float* dw, float* db, int grid, bool pipelined, hipStream_t st) {
   using G = StemGeo<CP, RS, SS>;
   const int lds = G::LDS_ELEMS * 2;
   if (mode == 0) {
@@ -517,14 +684,26 @@ void stem_launch(StemP& p, int mode, float* dw, float* db, int grid, hipStream_t
     hipLaunchKernelGGL((fm_stem_fwd<CP, RS, SS, S_, ACT>), dim3(grid), dim3(STT), lds2, st, p);
     return;
   }
-  const int lds_w = lds + STK * ST_GROW * 2 + ST_RAW_BYTES;   // the image + the g tile + raw rows
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)fm_stem_wgrad<CP, RS, SS, S_, ACT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              lds_w);
-    attr = true;
+  if (pipelined) {
+    // two (image + g tile) buffers + 8 waves' raw rows
+    const int lds_w = 2 * (lds + STK * ST_GROW * 2) + 8 * 2 * ST_RAWN * 2;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)fm_stem_wgrad2<CP, RS, SS, S_, ACT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                lds_w);
+      attr = true;
+    }
+    hipLaunchKernelGGL((fm_stem_wgrad2<CP, RS, SS, S_, ACT>), dim3(grid), dim3(SW_NTH), lds_w, st, p);
+  } else {
+    const int lds_w = lds + STK * ST_GROW * 2 + ST_RAW_BYTES;   // the image + the g tile + raw rows
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)fm_stem_wgrad<CP, RS, SS, S_, ACT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                lds_w);
+      attr = true;
+    }
+    hipLaunchKernelGGL((fm_stem_wgrad<CP, RS, SS, S_, ACT>), dim3(grid), dim3(STT), lds_w, st, p);
   }
-  hipLaunchKernelGGL((fm_stem_wgrad<CP, RS, SS, S_, ACT>), dim3(grid), dim3(STT), lds_w, st, p);
   const int tot = STK * (G::KP + 4);
   hipLaunchKernelGGL((fm_stem_wgrad_reduce<CP, RS, SS, S_>), dim3((tot + 31) / 32), dim3(256), 0, st, p.part, grid, dw, db,
                      p.C, p.R, p.S);
@@ -536,7 +715,9 @@ int stem_run(StemP& p, int mode, float* dw, float* db, int nsm, hipStream_t st) 
   p.tiles_q = (p.Q + STQ - 1) / STQ;
   p.tiles_p = (p.P + STP - 1) / STP;
   p.ntiles = p.N * p.tiles_p * p.tiles_q;
-  const int grid = std::max(1, std::min(p.ntiles, 2 * nsm));
+  const bool pipelined = CP == 48;                      // see stem_launch
+  // 4-wave kernels: two blocks per CU; the pipelined wgrad: one 8-wave block per CU
+  const int grid = std::max(1, std::min(p.ntiles, (mode == 1 && pipelined ? 1 : 2) * nsm));
   if (mode == 0) {
     // the caller's raw weights -> fragments in the scratch (p.part as 16-bit storage)
     unsigned short* wf = reinterpret_cast<unsigned short*>(p.part);
@@ -544,9 +725,9 @@ int stem_run(StemP& p, int mode, float* dw, float* db, int nsm, hipStream_t st) 
                        p.R, p.S);
     p.w = wf;
   }
-  if (p.act == ACT_RELU) stem_launch<CP, RS, SS, S_, ACT_RELU>(p, mode, dw, db, grid, st);
-  else if (p.act == ACT_NONE) stem_launch<CP, RS, SS, S_, ACT_NONE>(p, mode, dw, db, grid, st);
-  else stem_launch<CP, RS, SS, S_, -1>(p, mode, dw, db, grid, st);
+  if (p.act == ACT_RELU) stem_launch<CP, RS, SS, S_, ACT_RELU>(p, mode, dw, db, grid, pipelined, st);
+  else if (p.act == ACT_NONE) stem_launch<CP, RS, SS, S_, ACT_NONE>(p, mode, dw, db, grid, pipelined, st);
+  else stem_launch<CP, RS, SS, S_, -1>(p, mode, dw, db, grid, pipelined, st);
   return 0;
 }
 
