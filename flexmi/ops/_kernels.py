@@ -592,7 +592,8 @@ def conv2d_forward(x, w, b, y, stride, pads, act, groups, saved=None, form=None)
     forms = conv_forms(x, w, y, stride, groups)
     if form is None:
         if _chained(saved) or len(forms) == 1:
-            form = forms[0]
+            # a layer whose NHWC images are shared with a neighbour keeps the NHWC form
+            form = "nhwc" if "nhwc" in forms else forms[0]
         else:
             # candidates write a scratch output and keep no staged state for the backward
             ys = scratch(y.device, "conv_tune_y", y.numel(), y.dtype).view(y.shape)
@@ -647,7 +648,8 @@ def conv2d_backward(x, w, y, dy, dx, dw, db, stride, pads, act, groups, acc, sav
     forms = conv_forms(x, w, y, stride, groups, "bwd", need_dx=dx is not None)
     if form is None:
         if _chained(saved) or len(forms) == 1:
-            form = forms[0]
+            # a layer whose NHWC images are shared with a neighbour keeps the NHWC form
+            form = "nhwc" if "nhwc" in forms else forms[0]
         else:
             dws = scratch(x.device, "conv_tune_dw", dw.numel(), dw.dtype).view(dw.shape)
             dbs = scratch(x.device, "conv_tune_db", db.numel(), db.dtype).view(db.shape) if db is not None else None
