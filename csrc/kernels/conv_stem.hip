@@ -228,6 +228,15 @@ FM_DEVICE float stem_act_bwd(int act, float y, float dy) {
   else return act_bwd(act, y, dy);
 }
 
+// image offset of GEMM k run k0 (8 channels of one tap; the tap clamped: padding k meet zero weights)
+template <int CP, int RS, int SS>
+constexpr int stem_koff(int k0) {
+  using G = StemGeo<CP, RS, SS>;
+  const int t = k0 / CP < G::NTAP - 1 ? k0 / CP : G::NTAP - 1;
+  return ((t / SS) * G::XWA + t % SS) * G::CPS + k0 % CP;
+}
+FM_DEVICE int sel4(int i, int a, int b, int c, int d) { return i < 2 ? (i == 0 ? a : b) : (i == 2 ? c : d); }
+
 template <int CP, int RS, int SS, int S_, int ACT>
 __global__ void __launch_bounds__(STT, 2) fm_stem_fwd(StemP p) {
   using G = StemGeo<CP, RS, SS>;
@@ -278,10 +287,10 @@ __global__ void __launch_bounds__(STT, 2) fm_stem_fwd(StemP p) {
 #pragma unroll
     for (int ks = 0; ks < G::KS; ++ks) {
       // this lane's k run: tap t (clamped: padding k meet zero weights), channels cp .. cp+7
-      const int k0 = ks * 32 + kg * 8;
-      const int t = min(k0 / CP, G::NTAP - 1), cp = k0 - (k0 / CP) * CP;
-      const int ra = t / SS, sa = t - ra * SS;
-      const int koff = lbase + (ra * G::XWA + sa) * G::CPS + cp;
+      // the lane's k run k0 = 32 ks + 8 kg: its image offset is one of four compile-time constants
+      // (selected by kg) instead of a run-time division per k step
+      const int koff = lbase + sel4(kg, stem_koff<CP, RS, SS>(ks * 32), stem_koff<CP, RS, SS>(ks * 32 + 8),
+                                    stem_koff<CP, RS, SS>(ks * 32 + 16), stem_koff<CP, RS, SS>(ks * 32 + 24));
       if ((ks & 1) == 0) __builtin_amdgcn_sched_barrier(0);    // bound the A reads in flight
       u32x4_t af[4];
 #pragma unroll
