@@ -144,6 +144,7 @@ void fm_conv_nhwc_dgrad_strided(const void* gs, long gs_bytes, const void* w, vo
                                 void* out2, int H2, int W2, int C2, int t2, int l2, int d2h, int d2w, int write_nchw,
                                 hipStream_t s);
 long fm_conv_nhwc_wgrad_ws(int N, int K, int P, int Q, int R, int S, int Cp);
+void fm_conv_nhwc_set_shape(int mode, int shape);
 void fm_cnhwc_wprep_run(const void* w, void* out, void* out2, const float* g2, float* dw, int K, int C, int R, int S, int Cp,
                         int Kp, int mode, int nsplit, hipStream_t s);
 void fm_conv_nhwc_fwd(const void* xs, long xs_bytes, const void* wf, const float* bias, void* y, int N, int K, int P, int Q,
@@ -1220,6 +1221,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("nhwc_stage", &nhwc_stage);
   m.def("nhwc_stage_grad", &nhwc_stage_grad);
   m.def("conv_nhwc_wgrad_ws", &conv_nhwc_wgrad_ws);
+  m.def("conv_nhwc_set_shape", [](int64_t mode, int64_t shape) { fm_conv_nhwc_set_shape((int)mode, (int)shape); });
   m.def("cnhwc_wprep", &cnhwc_wprep);
   m.def("conv_nhwc_fwd", &conv_nhwc_fwd);
   m.def("conv_nhwc_dgrad", &conv_nhwc_dgrad);

@@ -878,10 +878,15 @@ struct Plan {
   int shape, tiles_m, tiles_n, ksplit, kt_per;
 };
 
+// per-pass tile-shape override (-1: the heuristic below), set by the per-layer measured selection
+// around one layer's launches (fm_conv_nhwc_set_shape); the split-K workspace size follows it
+int g_cn_shape[3] = {-1, -1, -1};
+
 Plan make_plan(int mode, int M, int N, int K) {
   auto tiles = [&](int bm, int bn) { return (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
   Plan q;
-  if (mode == CN_WGRAD) q.shape = N <= 64 ? 2 : M > 64 ? 0 : 1;
+  if (g_cn_shape[mode] >= 0) q.shape = g_cn_shape[mode];
+  else if (mode == CN_WGRAD) q.shape = N <= 64 ? 2 : M > 64 ? 0 : 1;
   else if (M > 64 && tiles(128, 128) >= 256) q.shape = 0;
   else if (tiles(64, 128) >= 256) q.shape = 1;
   else q.shape = 2;
@@ -932,6 +937,12 @@ int dispatch(ConvN& p, hipStream_t s) {
 }
 
 }  // namespace
+
+// tile shape of pass mode (0 fwd, 1 dgrad, 2 wgrad) for the launches that follow: 0 = 128x128 (8
+// waves), 1 = 64x128, 2 = 64x64 (4 waves), -1 = the size heuristic
+extern "C" void fm_conv_nhwc_set_shape(int mode, int shape) {
+  if (mode >= 0 && mode < 3) g_cn_shape[mode] = shape >= 0 && shape < 3 ? shape : -1;
+}
 
 // stage src [N][C][H][W] (bf16) into dst [N][Hp][Wp][Cp] at (top, left), zeros elsewhere
 extern "C" void fm_nhwc_stage_run(const void* src, void* dst, int N, int C, int H, int W, int Cp, int Hp, int Wp, int top,

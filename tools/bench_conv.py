@@ -31,12 +31,16 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="", help="fwd / dgrad / wgrad")
     ap.add_argument("--layer", default="", help="one layer name (e.g. conv2)")
+    ap.add_argument("--shape", type=int, default=-1,
+                    help="NHWC conv tile shape for every pass (0 128x128, 1 64x128, 2 64x64; -1 heuristic)")
     ap.add_argument("--path", default="raw", choices=["raw", "op"],
                     help="raw: the NCHW kernels (fwd / dgrad / wgrad); op: the framework's conv2d_forward / "
                          "conv2d_backward as dispatched (NHWC staging included; bwd = dgrad + wgrad + act/bias)")
     a = ap.parse_args()
     import torch
     from flexmi.ops import _kernels as K
+    for mode in range(3):
+        K.C().conv_nhwc_set_shape(mode, a.shape)
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     layers = sum((NETS[n] for n in (NETS if a.net == "all" else [a.net])), [])
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0, "bwd": 0.0}
@@ -66,9 +70,11 @@ def main():
         else:
             saved = {}
             db = torch.zeros(Ko, device="cuda")
+            fm = "nhwc" if C >= 16 else None
             runs = {
-                "fwd": lambda: K.conv2d_forward(x, w, b, y, (st, st), pads, 11, 1, saved),
-                "bwd": lambda: K.conv2d_backward(x, w, y, dy, dx, dw, db, (st, st), pads, 11, 1, False, saved),
+                "fwd": lambda: K.conv2d_forward(x, w, b, y, (st, st), pads, 11, 1, saved, form=fm),
+                "bwd": lambda: K.conv2d_backward(x, w, y, dy, dx, dw, db, (st, st), pads, 11, 1, False, saved,
+                                                 form=fm),
             }
         line = f"{name:8s} N{N} C{C} {H}x{W} K{Ko} {R}x{S}/{st}:"
         for k, fn in runs.items():
