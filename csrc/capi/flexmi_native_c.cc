@@ -753,6 +753,35 @@ int fmn_model_train_step_sparse(fmn_model_t m, const float* x, const int64_t* co
       -1);
 }
 
+int fmn_model_set_optimizer(fmn_model_t m, int type, float momentum, int nesterov, float weight_decay, float beta1,
+                            float beta2, float epsilon) {
+  if (!m) return fail("fmn_model_set_optimizer: null model");
+  return guarded(
+      [&] {
+        flexmi::nm::OptConfig o;
+        o.type = type;
+        o.momentum = momentum;
+        o.nesterov = nesterov != 0;
+        o.weight_decay = weight_decay;
+        o.beta1 = beta1;
+        o.beta2 = beta2;
+        o.eps = epsilon;
+        m->m->set_optimizer(o);
+        return 0;
+      },
+      -1);
+}
+
+int fmn_model_set_zero(fmn_model_t m, int stage) {
+  if (!m) return fail("fmn_model_set_zero: null model");
+  return guarded(
+      [&] {
+        m->m->set_zero(stage);
+        return 0;
+      },
+      -1);
+}
+
 int fmn_model_compile(fmn_model_t m, int loss_type, float lr, double bucket_mb) {
   if (!m) return fail("fmn_model_compile: null model");
   return guarded(

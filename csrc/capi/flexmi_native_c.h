@@ -206,6 +206,16 @@ int fmn_model_set_dense_channels(fmn_model_t m, int layer, int n, const int* ran
  * same values.  Returns the number of ops placed from the strategy. */
 int fmn_model_apply_strategy(fmn_model_t m, fmn_strategy_t s, int n_dense, const char* const* dense_names, int n_tables,
                              const char* const* table_names);
+/* optimizer of the dense parameters (before compile; default plain SGD): type 0 SGD at compile's lr
+ * with momentum / Nesterov / weight decay, 1 Adam with alpha = compile's lr (beta1, beta2, epsilon,
+ * weight decay).  A model with embedding tables needs plain SGD (its tables take sparse in-place
+ * updates).  Reference: SGDOptimizer / AdamOptimizer (include/optimizer.h, src/runtime/optimizer.cc). */
+int fmn_model_set_optimizer(fmn_model_t m, int type, float momentum, int nesterov, float weight_decay, float beta1,
+                            float beta2, float epsilon);
+/* ZeRO stage 1 (before compile; world > 1): gradient buckets reduce-scattered, the optimizer state of
+ * the data-parallel parameters kept for this rank's 1/world slice of each bucket, the updated slices
+ * all-gathered.  0 turns it off. */
+int fmn_model_set_zero(fmn_model_t m, int stage);
 /* loss: 51 sparse categorical CE (softmax of the last layer's logits, int32 labels), 52 MSE (avg),
  * 54 binary CE (sigmoid output); bucket_mb = gradient all-reduce bucket size */
 int fmn_model_compile(fmn_model_t m, int loss_type, float lr, double bucket_mb);

@@ -47,6 +47,8 @@ void fm_loss_fwd_bwd(const void* logits, int logits_bf16, const void* labels, vo
                      int loss_type, float scale, float* acc, int mask, float clamp_t, hipStream_t s);
 void fm_sgd_update(float* W, float* G, float* V, unsigned short* Wc, const float* lr, long n, float wd, float mom, int nesterov,
                    int zero_g, hipStream_t s);
+void fm_adam_update(float* W, float* G, float* M, float* V, unsigned short* Wc, long n, const float* alpha_t, float b1, float b2,
+                    float wd, float eps, int zero_g, hipStream_t s);
 void fm_embedding_fwd_multi(int n, const float* const* W, const void* const* idx, const int* idx64, void* const* out,
                             const long* ldo, const long* lo, const int* rows, const int* D, const int* bag,
                             const float* scale, int out_bf16, long B, hipStream_t st);
@@ -189,6 +191,39 @@ class HipEngine : public Engine {
   void sgd(float* w, float* g, int64_t n, float lr) override {
     set_lr(lr);
     fm_sgd_update(w, g, nullptr, nullptr, lr_, n, 0.f, 0.f, 0, 1, st_);
+  }
+
+  // the executor's optimizer kernels (optim.hip): SGD with momentum / Nesterov / weight decay, Adam
+  // with the device-side alpha_t; both consume the gradient
+  void opt_update(float* w, float* g, float* s1, float* s2, int64_t n, const OptStep& o) override {
+    set_lr(o.lr);
+    const OptConfig& c = o.c;
+    if (c.type == OPT_ADAM)
+      fm_adam_update(w, g, s1, s2, nullptr, n, lr_, c.beta1, c.beta2, c.weight_decay, c.eps, 1, st_);
+    else
+      fm_sgd_update(w, g, c.momentum > 0.f ? s1 : nullptr, nullptr, lr_, n, c.weight_decay, c.momentum, c.nesterov ? 1 : 0,
+                    1, st_);
+  }
+  void zero(void* p, size_t bytes) override { HIPX(hipMemsetAsync(p, 0, bytes, st_)); }
+  // ZeRO-1 collectives on RCCL: the reduce-scatter runs on the communication stream like the bucket
+  // all-reduces (overlapping the rest of the backward), the all-gather in order on the compute stream
+  void reduce_scatter_start(const float* buf, int64_t n, float* out) override {
+    if (!comm_) {
+      HIPX(hipMemcpyAsync(out, buf, (size_t)n * sizeof(float), hipMemcpyDeviceToDevice, st_));
+      return;
+    }
+    hipEvent_t ready = event();
+    HIPX(hipEventRecord(ready, st_));
+    HIPX(hipStreamWaitEvent(comm_st_, ready, 0));
+    NCCLX(ncclReduceScatter(buf, out, (size_t)(n / world_), ncclFloat32, ncclSum, comm_, comm_st_));
+    pending_ = true;
+  }
+  void all_gather(const float* in, int64_t n, float* buf) override {
+    if (!comm_) {
+      HIPX(hipMemcpyAsync(buf, in, (size_t)n * sizeof(float), hipMemcpyDeviceToDevice, st_));
+      return;
+    }
+    NCCLX(ncclAllGather(in, buf, (size_t)n, ncclFloat32, comm_, st_));
   }
 
   void copy(void* dst, const void* src, size_t bytes) override {

@@ -8,6 +8,7 @@
 #include <cstring>
 #include <sstream>
 #include <stdexcept>
+#include <vector>
 
 namespace flexmi {
 
@@ -60,7 +61,7 @@ inline float act_b(int act, float y, float g) {
 // the collectives between rank processes
 class CpuEngine : public Engine {
  public:
-  CpuEngine(int rank, int world, const std::string& dir, size_t slot_bytes) {
+  CpuEngine(int rank, int world, const std::string& dir, size_t slot_bytes) : rank_(rank), world_(world) {
     if (world > 1) comm_ = std::make_unique<HostComm>(dir, rank, world, slot_bytes);
   }
   void* alloc(size_t bytes) override { return std::calloc(std::max<size_t>(bytes, 16), 1); }
@@ -147,8 +148,49 @@ class CpuEngine : public Engine {
       g[i] = 0.f;
     }
   }
+  void opt_update(float* w, float* g, float* s1, float* s2, int64_t n, const OptStep& o) override {
+    const OptConfig& c = o.c;
+    for (int64_t i = 0; i < n; ++i) {
+      float gt = g[i] + c.weight_decay * w[i];
+      if (c.type == OPT_ADAM) {
+        s1[i] = s1[i] * c.beta1 + (1.f - c.beta1) * gt;
+        s2[i] = s2[i] * c.beta2 + (1.f - c.beta2) * gt * gt;
+        w[i] -= o.lr * s1[i] / (std::sqrt(s2[i]) + c.eps);
+      } else {
+        if (c.momentum > 0.f) {
+          s1[i] = s1[i] * c.momentum + gt;
+          gt = c.nesterov ? gt + c.momentum * s1[i] : s1[i];
+        }
+        w[i] -= o.lr * gt;
+      }
+      g[i] = 0.f;
+    }
+  }
+  void zero(void* p, size_t bytes) override { std::memset(p, 0, bytes); }
   void allreduce_start(float* buf, int64_t n) override {
     if (comm_) comm_->all_reduce_sum(buf, n);   // host collectives complete in place
+  }
+  // the host communicator has no reduce-scatter / all-gather: the sum-in-rank-order all-reduce, then
+  // this rank's slice (the same fp32 sums); the gather as an all-reduce of a buffer that is zero
+  // outside this rank's slice (x + 0 is exact)
+  void reduce_scatter_start(const float* buf, int64_t n, float* out) override {
+    const int64_t k = n / world_;
+    if (!comm_) {
+      std::memcpy(out, buf, (size_t)k * 4);
+      return;
+    }
+    std::vector<float> t(buf, buf + n);
+    comm_->all_reduce_sum(t.data(), n);
+    std::memcpy(out, t.data() + (int64_t)rank_ * k, (size_t)k * 4);
+  }
+  void all_gather(const float* in, int64_t n, float* buf) override {
+    if (!comm_) {
+      std::memcpy(buf, in, (size_t)n * 4);
+      return;
+    }
+    std::memset(buf, 0, (size_t)n * world_ * 4);
+    std::memcpy(buf + (int64_t)rank_ * n, in, (size_t)n * 4);
+    comm_->all_reduce_sum(buf, n * world_);
   }
   void allreduce_wait() override {}
   void copy(void* dst, const void* src, size_t bytes) override { std::memcpy(dst, src, bytes); }
@@ -419,6 +461,7 @@ class CpuEngine : public Engine {
   }
 
  private:
+  int rank_, world_;
   std::unique_ptr<HostComm> comm_;
 };
 
@@ -472,6 +515,11 @@ Model::~Model() {
   rel(stats_);
   for (auto* p : pool_code_) rel(p);
   for (auto* p : bn_buf_) rel(p);
+  rel(zmaster_);
+  rel(zgrad_);
+  for (auto* p : ostate_) rel(p);
+  for (auto& a : chan_state_)
+    for (float* q : a) rel(q);
 }
 
 void Model::check_tensor(int t, const char* what) const {
@@ -746,8 +794,39 @@ bool Model::param_local(int i) const {
   return d.holders.empty() || std::find(d.holders.begin(), d.holders.end(), rank_) != d.holders.end();
 }
 
+void Model::set_optimizer(const OptConfig& o) {
+  if (compiled_) throw std::logic_error("native model: set_optimizer after compile");
+  if (o.type != OPT_SGD && o.type != OPT_ADAM) throw std::invalid_argument("native model: optimizer type");
+  if (o.momentum < 0.f || o.weight_decay < 0.f || o.beta1 < 0.f || o.beta1 >= 1.f || o.beta2 < 0.f || o.beta2 >= 1.f ||
+      o.eps <= 0.f)
+    throw std::invalid_argument("native model: optimizer hyper-parameters");
+  opt_ = o;
+}
+
+void Model::set_zero(int stage) {
+  if (compiled_) throw std::logic_error("native model: set_zero after compile");
+  if (stage < 0 || stage > 1) throw std::invalid_argument("native model: ZeRO stage (0 or 1)");
+  zero_ = stage;
+}
+
+OptStep Model::next_step() {
+  OptStep s;
+  s.c = opt_;
+  s.lr = lr_;
+  if (opt_.type == OPT_ADAM) {   // AdamOptimizer::next (src/runtime/optimizer.cc:167-173), fp32 counters
+    b1t_ *= opt_.beta1;
+    b2t_ *= opt_.beta2;
+    s.lr = lr_ * std::sqrt(1.f - b2t_) / (1.f - b1t_);
+  }
+  return s;
+}
+
 void Model::compile(int loss_type, float lr, double bucket_mb) {
   if (ops_.empty()) throw std::logic_error("native model: no layers");
+  if (!embs_.empty() && !opt_.plain())
+    throw std::invalid_argument(
+        "native model: embedding tables train with the sparse in-place SGD; momentum / weight decay / Adam "
+        "need dense table gradients (not planned natively)");
   if (loss_type != LOSS_SCCE && loss_type != LOSS_MSE_AVG && loss_type != LOSS_BCE)
     throw std::invalid_argument("native model: loss type");
   loss_ = loss_type;
@@ -834,7 +913,41 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
   std::vector<int64_t> nums;
   for (int e : porder_) nums.push_back(pnumel_[e]);
   const int64_t cap = std::max<int64_t>(1, (int64_t)(bucket_mb * (1 << 20) / 4));
-  wplan_ = plan_weights(nums, cap);
+  if (zero_on()) {
+    // ZeRO-1 layout (flexmi.runtime.executor._zero_layout): 64-float aligned entries, every bucket
+    // padded to a multiple of world x 64 floats so each rank owns an equal 256-B aligned slice
+    const int64_t quant = (int64_t)world_ * 64;
+    WeightPlan p;
+    p.offset.resize(nums.size());
+    int64_t off = 0, start = 0;
+    std::vector<int64_t> ids;
+    auto close = [&] {
+      const int64_t end = start + (off - start + quant - 1) / quant * quant;
+      std::vector<int64_t> b{start, end};
+      b.insert(b.end(), ids.begin(), ids.end());
+      p.buckets.push_back(std::move(b));
+      start = off = end;
+      ids.clear();
+    };
+    for (size_t e = 0; e < nums.size(); ++e) {
+      const int64_t sz = (nums[e] + 63) / 64 * 64;
+      if (!ids.empty() && off + sz - start > cap) close();
+      p.offset[e] = off;
+      off += sz;
+      ids.push_back((int64_t)e);
+    }
+    if (!ids.empty()) close();
+    p.numel = off;
+    wplan_ = std::move(p);
+    zshard_off_.clear();
+    zshard_n_ = 0;
+    for (auto& b : wplan_.buckets) {
+      zshard_off_.push_back(zshard_n_);
+      zshard_n_ += (b[1] - b[0]) / world_;
+    }
+  } else {
+    wplan_ = plan_weights(nums, cap);
+  }
   pofs_.assign(pnumel_.size(), 0);
   for (size_t j = 0; j < porder_.size(); ++j) pofs_[porder_[j]] = wplan_.offset[j];
   // embedding exchange: every holder sends each peer that peer's sample rows of its column slice
@@ -928,6 +1041,25 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
   if (loss_ == LOSS_SCCE) probs_ = (float*)eng_->alloc((size_t)Bl_ * C * 4);
   labels_ = eng_->alloc((size_t)Bl_ * C * 4);
   stats_ = (float*)eng_->alloc(64);
+  // optimizer state (momentum v / Adam m, v) for the flat buffer -- or, under ZeRO-1, for this
+  // rank's slices only -- and for the channel-split slices this rank holds
+  const int64_t on = zero_on() ? zshard_n_ : wplan_.numel;
+  for (int k = 0; k < opt_.states(); ++k) ostate_[k] = (float*)eng_->alloc((size_t)std::max<int64_t>(on, 1) * 4);
+  if (zero_on()) {
+    zmaster_ = (float*)eng_->alloc((size_t)std::max<int64_t>(zshard_n_, 1) * 4);
+    zgrad_ = (float*)eng_->alloc((size_t)std::max<int64_t>(zshard_n_, 1) * 4);
+  }
+  chan_state_.assign(ops_.size(), {nullptr, nullptr, nullptr, nullptr});
+  for (size_t i = 0; i < ops_.size(); ++i) {
+    const Dense& d = ops_[i];
+    if (d.j < 0) continue;
+    for (int k = 0; k < opt_.states(); ++k) {
+      chan_state_[i][k] = (float*)eng_->alloc((size_t)d.Nc * d.K * 4);
+      if (d.b >= 0) chan_state_[i][2 + k] = (float*)eng_->alloc((size_t)d.Nc * 4);
+    }
+  }
+  b1t_ = b2t_ = 1.f;
+  zdirty_ = true;
   compiled_ = true;
 }
 
@@ -996,6 +1128,7 @@ void Model::set_param(int i, const float* host) {
     else eng_->h2d(chan_[di].b, host + (int64_t)d.j * d.Nc, (size_t)d.Nc * 4);
   } else {
     eng_->h2d(params_ + pofs_.at(i), host, pnumel_.at(i) * 4);
+    zdirty_ = true;   // the ZeRO master slices are refreshed from params_ before the next update
   }
   eng_->sync();
 }
@@ -1199,6 +1332,12 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
   std::vector<int> bucket_of(pnumel_.size(), -1);
   for (size_t bi = 0; bi < wplan_.buckets.size(); ++bi)
     for (size_t k = 2; k < wplan_.buckets[bi].size(); ++k) bucket_of[porder_[wplan_.buckets[bi][k]]] = (int)bi;
+  // a final bucket: all-reduced, or under ZeRO-1 reduce-scattered into this rank's gradient slice
+  auto bucket_done = [&](int bi) {
+    const int64_t b0 = wplan_.buckets[bi][0], n = wplan_.buckets[bi][1] - b0;
+    if (zero_on()) eng_->reduce_scatter_start(grads_ + b0, n, zgrad_ + zshard_off_[bi]);
+    else eng_->allreduce_start(grads_ + b0, n);
+  };
   for (int ni = (int)nodes_.size() - 1; ni >= 0; --ni) {
     const Node& n = nodes_[ni];
     if (n.kind == K_DENSE) {
@@ -1217,7 +1356,7 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
           if (e < 0) continue;
           const int bi = bucket_of[e];
           if (--left[bi] == 0)
-            eng_->allreduce_start(grads_ + wplan_.buckets[bi][0], wplan_.buckets[bi][1] - wplan_.buckets[bi][0]);
+            bucket_done(bi);
         }
       }
     } else if (n.kind == K_CONV) {
@@ -1229,7 +1368,7 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
           if (e < 0) continue;
           const int bi = bucket_of[e];
           if (--left[bi] == 0)
-            eng_->allreduce_start(grads_ + wplan_.buckets[bi][0], wplan_.buckets[bi][1] - wplan_.buckets[bi][0]);
+            bucket_done(bi);
         }
       }
     } else if (n.kind == K_POOL) {
@@ -1243,7 +1382,7 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
         for (int e : {b.g, b.b}) {
           const int bi = bucket_of[e];
           if (--left[bi] == 0)
-            eng_->allreduce_start(grads_ + wplan_.buckets[bi][0], wplan_.buckets[bi][1] - wplan_.buckets[bi][0]);
+            bucket_done(bi);
         }
       }
     } else if (n.kind == K_DOT) {
@@ -1288,12 +1427,38 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
     }
   }
   if (world_ > 1) eng_->allreduce_wait();
-  eng_->sgd(params_, grads_, wplan_.numel, lr_);
+  const OptStep os = next_step();
+  if (zero_on()) {
+    // ZeRO-1: update this rank's fp32 slices with their state, then all-gather the fresh slices
+    if (zdirty_) {
+      for (size_t bi = 0; bi < wplan_.buckets.size(); ++bi) {
+        const int64_t b0 = wplan_.buckets[bi][0], k = (wplan_.buckets[bi][1] - b0) / world_;
+        eng_->copy(zmaster_ + zshard_off_[bi], params_ + b0 + (int64_t)rank_ * k, (size_t)k * 4);
+      }
+      zdirty_ = false;
+    }
+    eng_->zero(grads_, (size_t)wplan_.numel * 4);   // the reduce-scatter consumed the gradients
+    eng_->opt_update(zmaster_, zgrad_, ostate_[0], ostate_[1], zshard_n_, os);
+    for (size_t bi = 0; bi < wplan_.buckets.size(); ++bi) {
+      const int64_t b0 = wplan_.buckets[bi][0], k = (wplan_.buckets[bi][1] - b0) / world_;
+      eng_->all_gather(zmaster_ + zshard_off_[bi], k, params_ + b0);
+    }
+  } else if (opt_.plain()) {
+    eng_->sgd(params_, grads_, wplan_.numel, lr_);
+  } else {
+    eng_->opt_update(params_, grads_, ostate_[0], ostate_[1], wplan_.numel, os);
+  }
   for (size_t i = 0; i < ops_.size(); ++i) {
     const Dense& d = ops_[i];
     if (d.j < 0) continue;
-    eng_->sgd(chan_[i].w, chan_[i].gw, (int64_t)d.Nc * d.K, lr_);
-    if (chan_[i].b) eng_->sgd(chan_[i].b, chan_[i].gb, d.Nc, lr_);
+    const auto& cs = chan_state_[i];
+    if (opt_.plain()) {
+      eng_->sgd(chan_[i].w, chan_[i].gw, (int64_t)d.Nc * d.K, lr_);
+      if (chan_[i].b) eng_->sgd(chan_[i].b, chan_[i].gb, d.Nc, lr_);
+    } else {
+      eng_->opt_update(chan_[i].w, chan_[i].gw, cs[0], cs[1], (int64_t)d.Nc * d.K, os);
+      if (chan_[i].b) eng_->opt_update(chan_[i].b, chan_[i].gb, cs[2], cs[3], d.Nc, os);
+    }
   }
   float st[2];
   eng_->sync();
@@ -1362,7 +1527,17 @@ std::string Model::describe() const {
     for (auto c : xcount_recv_) o << " " << c;
     o << "\n";
   }
-  o << "  flat parameters " << wplan_.numel << " floats, " << wplan_.buckets.size() << " all-reduce bucket(s)\n";
+  if (opt_.type == OPT_ADAM)
+    o << "  optimizer: adam alpha " << lr_ << " beta1 " << opt_.beta1 << " beta2 " << opt_.beta2 << " eps " << opt_.eps
+      << " weight decay " << opt_.weight_decay << "\n";
+  else
+    o << "  optimizer: sgd lr " << lr_ << " momentum " << opt_.momentum << (opt_.nesterov ? " nesterov" : "")
+      << " weight decay " << opt_.weight_decay << "\n";
+  if (zero_on())
+    o << "  ZeRO-1: buckets reduce-scattered, optimizer state for this rank's " << zshard_n_ << " of " << wplan_.numel
+      << " floats, slices all-gathered after the update\n";
+  o << "  flat parameters " << wplan_.numel << " floats, " << wplan_.buckets.size()
+    << (zero_on() ? " reduce-scatter bucket(s)\n" : " all-reduce bucket(s)\n");
   for (auto& b : wplan_.buckets) {
     o << "    [" << b[0] << ", " << b[1] << ") entries";
     for (size_t k = 2; k < b.size(); ++k) o << " " << porder_[b[k]];

@@ -17,6 +17,7 @@
 // native_hip.cc).  plan_weights() is the same bucket planner the Python executor uses.
 #pragma once
 
+#include <array>
 #include <cstdint>
 #include <memory>
 #include <string>
@@ -39,6 +40,27 @@ namespace nm {
 enum Act { ACT_NONE = 10, ACT_RELU = 11, ACT_SIGMOID = 12, ACT_TANH = 13 };
 constexpr double kBnEps = 1e-5;   // batch-norm epsilon (flexmi.ops.conv.BatchNorm.eps)
 enum Loss { LOSS_SCCE = 51, LOSS_MSE_AVG = 52, LOSS_BCE = 54 };
+
+// optimizer of the dense parameters (reference: SGDOptimizer / AdamOptimizer, src/runtime/optimizer.cc
+// and optimizer_kernel.cu).  SGD: gt = g + wd w; v = momentum v + gt; gt = nesterov ? gt + momentum v
+// : v (momentum > 0); w -= lr gt.  Adam: gt = g + wd w; m = b1 m + (1-b1) gt; v = b2 v + (1-b2) gt^2;
+// w -= alpha_t m / (sqrt(v) + eps) with alpha_t = alpha sqrt(1 - b2^t) / (1 - b1^t) (the host keeps
+// b1^t, b2^t in fp32 as AdamOptimizer::next does)
+enum OptType { OPT_SGD = 0, OPT_ADAM = 1 };
+struct OptConfig {
+  int type = OPT_SGD;
+  float momentum = 0.f;
+  bool nesterov = false;
+  float weight_decay = 0.f;
+  float beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f;
+  int states() const { return type == OPT_ADAM ? 2 : momentum > 0.f ? 1 : 0; }
+  bool plain() const { return type == OPT_SGD && momentum == 0.f && weight_decay == 0.f; }
+};
+// one update: lr = the SGD learning rate or Adam's alpha_t of this step
+struct OptStep {
+  OptConfig c;
+  float lr = 0.f;
+};
 
 struct Dense {
   int x = -1, y = -1;          // tensor ids
@@ -174,6 +196,14 @@ class Model {
   // move as FULL host arrays (this rank's rows / entries read / written)
   void set_dense_channels(int layer, const std::vector<int>& ranks);
   int num_dense() const { return (int)ops_.size(); }
+  // optimizer (before compile; default plain SGD at compile's lr).  Embedding tables train with the
+  // sparse in-place SGD, so a model with tables needs plain SGD (no momentum / weight decay / Adam).
+  void set_optimizer(const OptConfig& o);
+  // ZeRO stage 1 (before compile): data-parallel dense parameters keep optimizer state for this rank's
+  // 1/world slice of every gradient bucket only -- buckets are reduce-scattered instead of
+  // all-reduced, each rank updates its fp32 slice, the fresh slices are all-gathered (the reference
+  // has no ZeRO; SURVEY P13, flexmi.runtime.executor._zero_layout)
+  void set_zero(int stage);
   void compile(int loss_type, float lr, double bucket_mb);
   void init_weights(uint64_t seed);            // Glorot-uniform weights, zero biases, U(+-sqrt(1/rows)) tables
   int num_params() const { return (int)pnumel_.size(); }
@@ -228,6 +258,18 @@ class Model {
   std::vector<int64_t> pofs_;                 // dense entry -> flat offset
   int loss_ = LOSS_MSE_AVG;
   float lr_ = 0.01f;
+  OptConfig opt_;
+  float b1t_ = 1.f, b2t_ = 1.f;               // Adam: beta1^t, beta2^t
+  OptStep next_step();
+  int zero_ = 0;                              // ZeRO stage (1: sharded optimizer state, world > 1)
+  bool zero_on() const { return zero_ >= 1 && world_ > 1; }
+  std::vector<int64_t> zshard_off_;           // bucket -> offset of this rank's slice in the shard buffers
+  int64_t zshard_n_ = 0;
+  float* zmaster_ = nullptr;                  // [zshard_n_] fp32 master slices (ZeRO)
+  float* zgrad_ = nullptr;                    // [zshard_n_] reduce-scattered gradient slices
+  bool zdirty_ = true;                        // params_ changed on the host side: refresh zmaster_
+  float* ostate_[2] = {nullptr, nullptr};     // optimizer state of the flat (or shard) buffer
+  std::vector<std::array<float*, 4>> chan_state_;   // channel-split slices: w state x2, b state x2
   bool compiled_ = false;
   std::unique_ptr<Engine> eng_;
   // device buffers
@@ -278,6 +320,14 @@ class Engine {
   virtual void loss(int type, const float* p, const void* labels, float* grad, int M, int C, float scale,
                     float* stats) = 0;
   virtual void sgd(float* w, float* g, int64_t n, float lr) = 0;   // w -= lr g; g = 0
+  // one optimizer update of n parameters (OptConfig); s1 / s2: its state (momentum v, or Adam m / v);
+  // consumes g (left zeroed)
+  virtual void opt_update(float* w, float* g, float* s1, float* s2, int64_t n, const OptStep& o) = 0;
+  virtual void zero(void* p, size_t bytes) = 0;
+  // ZeRO: out[n / world] = this rank's slice of sum-over-ranks(buf[n]) (asynchronous like
+  // allreduce_start, completed by allreduce_wait); all_gather: buf[world * n] = every rank's in[n]
+  virtual void reduce_scatter_start(const float* buf, int64_t n, float* out) = 0;
+  virtual void all_gather(const float* in, int64_t n, float* buf) = 0;
   // gradient bucket reduction (sum over ranks): start after the bucket's last gradient, wait
   // before the update
   virtual void allreduce_start(float* buf, int64_t n) = 0;

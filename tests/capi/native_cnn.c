@@ -4,10 +4,11 @@
  * softmax cross-entropy, SGD, data parallel over `world` rank processes (bucketed all-reduce through
  * the CPU engine's host communicator, or RCCL on the HIP engine).
  *
- *   native_cnn <cpu|hip> <out prefix> <steps> <world> <rendezvous dir> [bn]
+ *   native_cnn <cpu|hip> <out prefix> <steps> <world> <rendezvous dir> [options]
  *
- * bn: the first convolution has no activation and feeds a batch norm with a fused ReLU (statistics
- * over each rank's samples).
+ * options (comma-separated): bn -- the first convolution has no activation and feeds a batch norm with
+ * a fused ReLU (statistics over each rank's samples); mom / nag -- SGD with momentum 0.9 (Nesterov);
+ * adam -- Adam (alpha 0.01); wd -- weight decay 0.01; zero -- ZeRO-1 sharded optimizer state.
  *
  * <prefix>.init.bin (rank 0): int32 B, int32 steps, int32 nparams; per param int64 numel + float
  *   init[numel]; per step float x[B*3*20*20], int32 labels[B].
@@ -36,6 +37,7 @@
 
 static uint32_t rng = 4242u;
 static int g_bn = 0;
+static const char* g_opts = "";
 static float frand(void) {
   rng = rng * 1664525u + 1013904223u;
   return (float)(rng >> 8) / (float)(1u << 24);
@@ -60,7 +62,11 @@ static int run_rank(int device, const char* prefix, int steps, int rank, int wor
   CHECK(t = fmn_model_pool2d(m, t, 2, 2, 2, 2, 1, 1, 0));
   CHECK(t = fmn_model_dense(m, t, 32, 11, 1));
   CHECK(t = fmn_model_dense(m, t, NCLS, 10, 1));
-  CHECK(fmn_model_compile(m, 51, 0.05f, 0.002));
+  const int adam = strstr(g_opts, "adam") != NULL, nag = strstr(g_opts, "nag") != NULL;
+  const float mom = (strstr(g_opts, "mom") != NULL || nag) ? 0.9f : 0.f, wd = strstr(g_opts, "wd") ? 0.01f : 0.f;
+  if (adam || mom > 0.f || wd > 0.f) CHECK(fmn_model_set_optimizer(m, adam, mom, nag, wd, 0.9f, 0.999f, 1e-8f));
+  if (strstr(g_opts, "zero")) CHECK(fmn_model_set_zero(m, 1));
+  CHECK(fmn_model_compile(m, 51, adam ? 0.01f : 0.05f, 0.002));
   static char desc[8192];
   fmn_model_describe(m, desc, sizeof(desc));
   if (rank == 0) printf("%s", desc);
@@ -123,10 +129,11 @@ static int run_rank(int device, const char* prefix, int steps, int rank, int wor
 
 int main(int argc, char** argv) {
   if (argc < 6) {
-    fprintf(stderr, "usage: native_cnn <cpu|hip> <out prefix> <steps> <world> <rendezvous dir> [bn]\n");
+    fprintf(stderr, "usage: native_cnn <cpu|hip> <out prefix> <steps> <world> <rendezvous dir> [options]\n");
     return 2;
   }
-  g_bn = argc > 6 && strcmp(argv[6], "bn") == 0;
+  g_opts = argc > 6 ? argv[6] : "";
+  g_bn = strstr(g_opts, "bn") != NULL;
   const int device = strcmp(argv[1], "hip") == 0 ? 1 : 0;
   const int steps = atoi(argv[3]), world = atoi(argv[4]);
   if (world < 1 || world > 16 || B % world) return 2;

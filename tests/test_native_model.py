@@ -497,9 +497,10 @@ def _parse_cnn(prefix, world):
     return dict(B=B, steps=steps, init=init, batches=batches, ranks=ranks)
 
 
-def _replay_cnn(rec, bn=False):
-    """The same CNN, weights and batches through flexmi's Python executor (CPU, fp32, world 1)."""
-    from flexmi.core import ActiMode, FFConfig, FFModel, LossType, MetricsType, PoolType, SGDOptimizer
+def _replay_cnn(rec, bn=False, opts=""):
+    """The same CNN, weights and batches through flexmi's Python executor (CPU, fp32, world 1); opts: the
+    C program's optimizer options (mom / nag / adam / wd)."""
+    from flexmi.core import ActiMode, AdamOptimizer, FFConfig, FFModel, LossType, MetricsType, PoolType, SGDOptimizer
     B = rec["B"]
     cfg = FFConfig()
     cfg.batchSize, cfg.device, cfg.compute_dtype = B, "cpu", "fp32"
@@ -517,7 +518,13 @@ def _replay_cnn(rec, bn=False):
     t = m.dense(t, 32, ActiMode.AC_MODE_RELU)
     t = m.dense(t, 10)
     t = m.softmax(t)
-    m.compile(SGDOptimizer(m, 0.05), LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, [MetricsType.METRICS_ACCURACY])
+    wd = 0.01 if "wd" in opts else 0.0
+    if "adam" in opts:
+        opt = AdamOptimizer(m, alpha=0.01, weight_decay=wd)
+    else:
+        nag = "nag" in opts
+        opt = SGDOptimizer(m, 0.05, momentum=0.9 if ("mom" in opts or nag) else 0.0, nesterov=nag, weight_decay=wd)
+    m.compile(opt, LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, [MetricsType.METRICS_ACCURACY])
     ex = m.init_layers()
     assert len(m.parameters) == len(rec["init"])
     for p, w in zip(m.parameters, rec["init"]):
@@ -577,12 +584,69 @@ def test_native_c_cnn_batch_norm(tmp_path):
                 np.testing.assert_allclose(rec["ranks"][0][0][i], want, rtol=1e-4, atol=1e-5, err_msg=f"param {i}")
 
 
+@pytest.mark.parametrize("opts,world", [("mom", 1), ("nag,wd", 2), ("adam", 1), ("adam,wd,zero", 2), ("mom,zero", 4),
+                                         ("bn,adam,zero", 2)])
+def test_native_c_cnn_optimizers_and_zero(tmp_path, opts, world):
+    """The native compiler's optimizers -- SGD with momentum / Nesterov / weight decay and Adam (the
+    reference's SGDOptimizer / AdamOptimizer) -- and ZeRO-1 (gradient buckets reduce-scattered, optimizer
+    state for this rank's slice only, the updated slices all-gathered): the C program ends with the
+    Python executor's parameters at world 1..4 and the replicas stay identical."""
+    exe = _build_cnn_c(tmp_path)
+    rdv = tmp_path / "rdv"
+    rdv.mkdir()
+    prefix = str(tmp_path / "run")
+    r = subprocess.run([exe, "cpu", prefix, "4", str(world), str(rdv), opts], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "native_cnn ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+    assert ("optimizer: adam" if "adam" in opts else "momentum 0.9") in r.stdout
+    assert ("ZeRO-1" in r.stdout) == ("zero" in opts and world > 1)
+    rec = _parse_cnn(prefix, world)
+    got = _replay_cnn(rec, bn="bn" in opts, opts=opts)
+    for i, want in enumerate(got):
+        reps = [rk[0][i] for rk in rec["ranks"]]
+        for h in reps[1:]:
+            np.testing.assert_array_equal(h, reps[0])
+        if "bn" in opts and world > 1:
+            continue    # local-shard batch statistics: the world-1 executor normalises differently
+        np.testing.assert_allclose(reps[0], want, rtol=2e-4, atol=2e-5, err_msg=f"param {i}")
+    assert np.all(np.isfinite(rec["ranks"][0][1]))
+
+
+def test_native_model_rejects_stateful_optimizer_with_tables(tmp_path):
+    """Tables take sparse in-place SGD updates: momentum / weight decay / Adam with embedding tables is
+    refused at compile with a message, not silently trained differently."""
+    import ctypes
+    if not os.path.exists(LIB):
+        pytest.skip("libflexmi_native_c.so not built")
+    L = ctypes.CDLL(LIB)
+    L.fmn_model_create.restype = ctypes.c_void_p
+    L.fmn_model_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]
+    L.fmn_last_error.restype = ctypes.c_char_p
+    for fn in ("fmn_model_input", "fmn_model_sparse_input"):
+        getattr(L, fn).argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.fmn_model_embedding.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int]
+    L.fmn_model_dense.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    L.fmn_model_set_optimizer.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_int, ctypes.c_float,
+                                          ctypes.c_float, ctypes.c_float, ctypes.c_float]
+    L.fmn_model_compile.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_double]
+    L.fmn_model_destroy.argtypes = [ctypes.c_void_p]
+    m = L.fmn_model_create(8, 0, 0, 1, b"")
+    assert m
+    x = L.fmn_model_input(m, 4)
+    s = L.fmn_model_sparse_input(m, 1)
+    assert L.fmn_model_embedding(m, s, 10, 4) >= 0
+    assert L.fmn_model_dense(m, x, 2, 10, 1) >= 0
+    assert L.fmn_model_set_optimizer(m, 1, 0.0, 0, 0.0, 0.9, 0.999, 1e-8) == 0
+    assert L.fmn_model_compile(m, 52, 0.01, 1.0) < 0
+    assert b"sparse in-place SGD" in L.fmn_last_error()
+    L.fmn_model_destroy(m)
+
+
 @pytest.mark.gpu
 def test_native_c_cnn_hip_engine_matches_cpu(tmp_path):
     """The same C CNN program on the HIP engine (flexmi's fp32 implicit-GEMM convolution and pooling
     kernels) against the CPU engine."""
     exe = _build_cnn_c(tmp_path)
-    for variant in ("", "bn"):
+    for variant in ("", "bn", "nag,wd"):
         recs = {}
         for dev in ("cpu", "hip"):
             rdv = tmp_path / f"rdv_{dev}{variant}"
