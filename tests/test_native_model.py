@@ -4,6 +4,7 @@ flexmi's Python executor: same initial weights, same batches, same final weights
 runs the same C program on the HIP engine (flexmi's gfx950 kernels + RCCL communicator) and
 compares with the CPU engine."""
 import os
+import json
 import subprocess
 
 import numpy as np
@@ -660,3 +661,21 @@ def test_native_c_cnn_hip_engine_matches_cpu(tmp_path):
         for a, b in zip(c["ranks"][0][0], h["ranks"][0][0]):
             np.testing.assert_allclose(b, a, rtol=1e-3, atol=1e-4, err_msg=variant)
         np.testing.assert_allclose(h["ranks"][0][1], c["ranks"][0][1], rtol=1e-3, err_msg=variant)
+
+
+def test_native_dlrm_mlperf_bench_program_runs_on_cpu(tmp_path):
+    """apps/c/dlrm_native_bench.c: the BASELINE DLRM configuration (26 MLPerf tables, 13-512-256-128
+    bottom, 479-1024-1024-512-256-1 top) compiled and trained by the native engine alone; here with
+    tables capped at 100 k rows and a 64-sample batch on the CPU engine (the HIP run is the box's)."""
+    if not os.path.exists(LIB):
+        pytest.skip("libflexmi_native_c.so not built")
+    exe = str(tmp_path / "dlrm_native_bench")
+    subprocess.run(["gcc", "-O2", "-I" + os.path.join(ROOT, "csrc", "capi"), os.path.join(ROOT, "apps", "c", "dlrm_native_bench.c"),
+                    "-L" + os.path.join(ROOT, "flexmi"), "-Wl,-rpath," + os.path.join(ROOT, "flexmi"), "-lflexmi_native_c",
+                    "-o", exe], check=True)
+    r = subprocess.run([exe, "cpu", "2", "1", "64", "small"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "dot interaction: 27 features x 128 -> 479" in r.stdout
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rec["engine"] == "native-cpu" and rec["batch"] == 64 and rec["ms_per_step"] > 0
+    assert np.isfinite(rec["loss"])
