@@ -962,6 +962,7 @@ void cnhwc_wprep(torch::Tensor w, torch::Tensor out, torch::Tensor out2, torch::
   const long K = w.size(0), C = w.size(1), RS = w.size(2) * w.size(3);
   TORCH_CHECK(Cp % 8 == 0 && Cp >= C && Kp % 8 == 0 && Kp >= K, "cnhwc_wprep: padded channel counts");
   if (mode != 2) {
+    TORCH_CHECK(K * RS * Cp + C * RS * Kp + 256L * 1024 < (1L << 31), "cnhwc_wprep: weight too large for 32-bit indexing");
     nhwc_chk(w, K * C * RS, "cnhwc_wprep w");
     if (mode == 0 || mode == 3) nhwc_chk(out, K * RS * Cp, "cnhwc_wprep out (fwd matrix)");
     if (mode == 1) nhwc_chk(out, C * RS * Kp, "cnhwc_wprep out (dgrad matrix)");
