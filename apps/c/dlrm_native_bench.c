@@ -79,7 +79,9 @@ int main(int argc, char** argv) {
     CHECK(sp = fmn_model_sparse_input(m, 1));
     CHECK(emb[i] = fmn_model_embedding(m, sp, rows[i], D));
   }
-  CHECK(t = fmn_model_dot_interaction(m, bottom, NT, emb, 1));
+  /* 479 interaction features padded to 480 (a zero column, as the executor pads): 16-B rows for the
+   * staged interaction kernels and the top GEMM */
+  CHECK(t = fmn_model_dot_interaction(m, bottom, NT, emb, 8));
   const int top[5] = {1024, 1024, 512, 256, 1};
   for (int i = 0; i < 5; ++i) CHECK(t = fmn_model_dense(m, t, top[i], i == 4 ? 12 : 11, 1));
   CHECK(fmn_model_compile(m, 54, 0.01f, 64.0));

@@ -1,7 +1,8 @@
 // HIP engine of the native model (native_model.h): flexmi's gfx950 kernels (linked from
 // libflexmi_kernels.so, no PyTorch) and flexmi's own RCCL communicator.
 //
-//   dense forward  fm_gemm_f32 (v_mfma_f32_16x16x4_f32, bias + activation in the epilogue) or
+//   dense forward  fm_gemm_f32 (the exact three-way bf16 split or v_mfma_f32_16x16x4_f32, bias +
+//                  activation in the epilogue; the executor's measured GEMM table picks the form) or
 //                  the skinny N = 1 kernel
 //   dense backward fm_act_bwd_bias (act'), fm_gemm_f32 dW (+= , bias gradient as the staged A
 //                  tiles' row sums) and dX (activation backward of the layer below fused into
@@ -20,13 +21,18 @@
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
+#include <dlfcn.h>
+
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <fstream>
+#include <sstream>
 #include <stdexcept>
 #include <string>
 #include <thread>
 #include <unistd.h>
+#include <unordered_map>
 #include <vector>
 
 #include "native_model.h"
@@ -103,6 +109,93 @@ namespace {
 
 constexpr long WS_BYTES = 64L << 20;   // split-K slabs of the dW GEMMs
 
+// The measured GEMM configuration table the Python executor uses (flexmi/ops/gemm_tune.py: key ->
+// cfg = split depth | form << 8), read from flexmi/ops/tuned/gemm_mi355x.json next to this library
+// (FM_GEMM_TUNE: 0 = off, or another table's path).  Keys as gemm_tune.key: dtype|MxNxK|orientations
+// |batch|fused epilogues|C dtype.  A missing table or key means the kernels' own heuristic.
+class TuneTable {
+ public:
+  static const TuneTable& get() {
+    static const TuneTable t;
+    return t;
+  }
+  int cfg(int M, int N, int K, bool a_k, bool b_k, bool act_y, bool rowsum) const {
+    if (m_.empty()) return 0;
+    char k[160];
+    std::snprintf(k, sizeof(k), "fp32|%dx%dx%d|%c%c|b1|%s|c32", M, N, K, a_k ? 'k' : 'm', b_k ? 'k' : 'm',
+                  act_y ? "y" : rowsum ? "r" : "-");
+    auto it = m_.find(k);
+    return it == m_.end() ? 0 : it->second;
+  }
+
+ private:
+  TuneTable() {
+    const char* env = std::getenv("FM_GEMM_TUNE");
+    std::string path;
+    if (env && std::string(env) == "0") return;
+    if (env && *env && std::string(env) != "1") {
+      path = env;
+    } else {
+      Dl_info info;
+      if (!dladdr(reinterpret_cast<void*>(&TuneTable::get), &info) || !info.dli_fname) return;
+      const std::string lib = info.dli_fname;
+      const size_t slash = lib.rfind('/');
+      path = (slash == std::string::npos ? std::string(".") : lib.substr(0, slash)) + "/ops/tuned/gemm_mi355x.json";
+    }
+    std::ifstream f(path);
+    if (!f) return;
+    std::stringstream ss;
+    ss << f.rdbuf();
+    const std::string j = ss.str();
+    // entries: "<key with '|'>": { ... "cfg": <int>, ... }
+    size_t pos = 0;
+    while ((pos = j.find('"', pos)) != std::string::npos) {
+      const size_t end = j.find('"', pos + 1);
+      if (end == std::string::npos) break;
+      const std::string key = j.substr(pos + 1, end - pos - 1);
+      pos = end + 1;
+      if (key.find('|') == std::string::npos) continue;
+      const size_t open = j.find('{', pos), close = j.find('}', pos);
+      if (open == std::string::npos || close == std::string::npos || open > close) continue;
+      const size_t c = j.find("\"cfg\"", open);
+      if (c == std::string::npos || c > close) continue;
+      const size_t colon = j.find(':', c);
+      const int v = std::atoi(j.c_str() + colon + 1);
+      if (v > 0) m_[key] = v;
+      pos = close + 1;
+    }
+  }
+  std::unordered_map<std::string, int> m_;
+};
+
+// the multi-table embedding launchers' parallel arrays
+struct EmbArrays {
+  explicit EmbArrays(const std::vector<Engine::EmbJob>& jobs) : n((int)jobs.size()) {
+    for (const Engine::EmbJob& j : jobs) {
+      W.push_back(j.W);
+      Wc.push_back(j.W);
+      ix.push_back(j.idx);
+      i64.push_back(1);
+      o.push_back(j.io);
+      ld.push_back(j.D);
+      l0.push_back((long)j.lo);
+      r.push_back((int)j.rows);
+      D.push_back(j.D);
+      bag.push_back(j.bag);
+      sc.push_back(1.f);
+    }
+  }
+  int n;
+  std::vector<float*> W;
+  std::vector<const float*> Wc;
+  std::vector<const void*> ix;
+  std::vector<int> i64;
+  std::vector<void*> o;
+  std::vector<long> ld, l0;
+  std::vector<int> r, D, bag;
+  std::vector<float> sc;
+};
+
 class HipEngine : public Engine {
  public:
   HipEngine(int rank, int world, const std::string& rendezvous) : rank_(rank), world_(world) {
@@ -112,6 +205,8 @@ class HipEngine : public Engine {
     HIPX(hipSetDevice(rank % ndev));
     HIPX(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     HIPX(hipStreamCreateWithFlags(&comm_st_, hipStreamNonBlocking));
+    HIPX(hipStreamCreateWithFlags(&side_st_, hipStreamNonBlocking));
+    main_st_ = st_;
     HIPX(hipMalloc(&ws_, WS_BYTES));
     HIPX(hipMalloc(&slots_, 16 * sizeof(float)));
     HIPX(hipMalloc(&lr_, sizeof(float)));
@@ -120,6 +215,7 @@ class HipEngine : public Engine {
   ~HipEngine() override {
     hipStreamSynchronize(st_);
     hipStreamSynchronize(comm_st_);
+    hipStreamSynchronize(side_st_);
     for (auto e : events_) hipEventDestroy(e);
     if (comm_) ncclCommDestroy(comm_);
     hipFree(ws_);
@@ -128,6 +224,7 @@ class HipEngine : public Engine {
     hipFree(slots_);
     hipFree(lr_);
     hipStreamDestroy(comm_st_);
+    hipStreamDestroy(side_st_);
     hipStreamDestroy(st_);
   }
 
@@ -146,14 +243,39 @@ class HipEngine : public Engine {
     HIPX(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st_));
     HIPX(hipStreamSynchronize(st_));
   }
-  void sync() override { HIPX(hipStreamSynchronize(st_)); }
+  void sync() override {
+    HIPX(hipStreamSynchronize(main_st_));
+    HIPX(hipStreamSynchronize(side_st_));
+    if (!pending_) ev_next_ = 0;   // every recorded event has completed: the pool is reusable
+  }
+  // the side queue: every kernel launch goes to st_, which points at the main or the side stream
+  void side_begin() override {
+    if (st_ == side_st_) return;
+    hipEvent_t e = event();
+    HIPX(hipEventRecord(e, main_st_));
+    HIPX(hipStreamWaitEvent(side_st_, e, 0));
+    st_ = side_st_;
+  }
+  void side_end() override {
+    if (st_ != side_st_) return;
+    st_ = main_st_;
+    side_pending_ = true;
+  }
+  void side_join() override {
+    if (!side_pending_) return;
+    hipEvent_t e = event();
+    HIPX(hipEventRecord(e, side_st_));
+    HIPX(hipStreamWaitEvent(main_st_, e, 0));
+    side_pending_ = false;
+  }
 
   void dense_fwd(const float* x, const float* W, const float* b, float* y, int M, int K, int N, int act) override {
     if (N == 1) {
       fm_skinny_fwd_f32_launch(x, K, W, b, y, 1, M, K, act, st_);
       return;
     }
-    fm_gemm_f32(x, K, 0, 1, W, K, 0, 1, y, N, 0, b, M, N, K, 1, 1.f, 0, act, ws_, WS_BYTES, 0, nullptr, 0, ACT_NONE, nullptr,
+    const int cfg = TuneTable::get().cfg(M, N, K, true, true, false, false);
+    fm_gemm_f32(x, K, 0, 1, W, K, 0, 1, y, N, 0, b, M, N, K, 1, 1.f, 0, act, ws_, WS_BYTES, cfg, nullptr, 0, ACT_NONE, nullptr,
                 nullptr, st_);
   }
 
@@ -170,12 +292,13 @@ class HipEngine : public Engine {
       dpre = t;
     }
     // dW[N][K] += dpre^T x (both operands MN-contiguous), db += column sums of dpre
-    fm_gemm_f32(dpre, N, 0, 0, x, K, 0, 0, dW, K, 0, nullptr, N, K, M, 1, 1.f, 1, ACT_NONE, ws_, WS_BYTES, 0, nullptr, 0,
-                ACT_NONE, nullptr, db, st_);
+    fm_gemm_f32(dpre, N, 0, 0, x, K, 0, 0, dW, K, 0, nullptr, N, K, M, 1, 1.f, 1, ACT_NONE, ws_, WS_BYTES,
+                TuneTable::get().cfg(N, K, M, false, false, false, db != nullptr), nullptr, 0, ACT_NONE, nullptr, db, st_);
     if (!dx) return;
     // dX[M][K] = dpre W (+ act' of the layer below)
-    fm_gemm_f32(dpre, N, 0, 1, W, K, 0, 0, dx, K, 0, nullptr, M, K, N, 1, 1.f, 0, ACT_NONE, ws_, WS_BYTES, 0, y_below,
-                y_below ? K : 0, y_below ? act_below : ACT_NONE, nullptr, nullptr, st_);
+    fm_gemm_f32(dpre, N, 0, 1, W, K, 0, 0, dx, K, 0, nullptr, M, K, N, 1, 1.f, 0, ACT_NONE, ws_, WS_BYTES,
+                TuneTable::get().cfg(M, K, N, true, false, y_below != nullptr, false), y_below, y_below ? K : 0,
+                y_below ? act_below : ACT_NONE, nullptr, nullptr, st_);
   }
 
   void softmax(const float* x, float* y, int M, int C) override { fm_softmax_fwd(x, y, M, C, 0, st_); }
@@ -251,6 +374,21 @@ class HipEngine : public Engine {
     const long ld = D, l0 = (long)lo;
     const float sc = 1.f;
     fm_embedding_bwd_multi(1, &W, &ix, &i64, &dy, &ld, &l0, &r, &D, &bag, &sc, 0, lr_, B, nullptr, nullptr, nullptr, st_);
+  }
+  void emb_fwd_multi(const std::vector<EmbJob>& jobs, int64_t B) override {
+    EmbArrays a(jobs);
+    fm_embedding_fwd_multi(a.n, a.Wc.data(), a.ix.data(), a.i64.data(), a.o.data(), a.ld.data(), a.l0.data(), a.r.data(),
+                           a.D.data(), a.bag.data(), a.sc.data(), 0, B, st_);
+  }
+  void emb_sgd_multi(const std::vector<EmbJob>& jobs, int64_t B, float lr) override {
+    set_lr(lr);
+    EmbArrays a(jobs);
+    std::vector<const void*> dy(a.o.begin(), a.o.end());
+    fm_embedding_bwd_multi(a.n, a.W.data(), a.ix.data(), a.i64.data(), dy.data(), a.ld.data(), a.l0.data(), a.r.data(),
+                           a.D.data(), a.bag.data(), a.sc.data(), 0, lr_, B, nullptr, nullptr, nullptr, st_);
+  }
+  void h2d_nosync(void* dst, const void* src, size_t bytes) override {
+    HIPX(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st_));
   }
   void add(float* dst, const float* src, int64_t n) override { fm_binary_forward(0, dst, src, dst, n, 0, 0, st_); }
   void dot_fwd(const float* const* z, int F, float* y, int M, int D, int W) override {
@@ -398,7 +536,8 @@ class HipEngine : public Engine {
   }
 
   int rank_, world_;
-  hipStream_t st_ = nullptr, comm_st_ = nullptr;
+  hipStream_t st_ = nullptr, comm_st_ = nullptr, main_st_ = nullptr, side_st_ = nullptr;
+  bool side_pending_ = false;
   ncclComm_t comm_ = nullptr;
   float* ws_ = nullptr;
   float* slots_ = nullptr;

@@ -1246,22 +1246,26 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
   const int C = last.N;
   // this rank's sample shard of the global batch; the owned tables' GLOBAL indices
   const int64_t r0 = (int64_t)rank_ * Bl_;
-  eng_->h2d(act_[input_], x + r0 * cols_[input_], (size_t)Bl_ * cols_[input_] * 4);
+  // the batch uploads are issued back to back with ONE sync (the caller's host arrays may change after
+  // train_step returns)
+  eng_->h2d_nosync(act_[input_], x + r0 * cols_[input_], (size_t)Bl_ * cols_[input_] * 4);
   const size_t lab_row = loss_ == LOSS_SCCE ? 4 : (size_t)C * 4;
-  eng_->h2d(labels_, static_cast<const char*>(labels) + r0 * lab_row, (size_t)Bl_ * lab_row);
+  eng_->h2d_nosync(labels_, static_cast<const char*>(labels) + r0 * lab_row, (size_t)Bl_ * lab_row);
   for (size_t t = 0; t < embs_.size(); ++t)
-    if (slice_of(embs_[t], rank_) >= 0) eng_->h2d(idx_[t], sparse[embs_[t].sparse], (size_t)B_ * embs_[t].bag * 8);
-  float zero[2] = {0.f, 0.f};
-  eng_->h2d(stats_, zero, sizeof(zero));
+    if (slice_of(embs_[t], rank_) >= 0) eng_->h2d_nosync(idx_[t], sparse[embs_[t].sparse], (size_t)B_ * embs_[t].bag * 8);
+  eng_->sync();
+  eng_->zero(stats_, 2 * sizeof(float));
 
   // embedding lookups (owners, global batch) and the exchange to the sample shards, issued ahead
   // of the first consumer
   auto emb_forward = [&]() {
+    std::vector<Engine::EmbJob> jobs;
     for (size_t t = 0; t < embs_.size(); ++t) {
       const Emb& e = embs_[t];
       if (slice_of(e, rank_) < 0) continue;
-      eng_->emb_fwd(table_[t], e.nrows, idx_[t], e.bag, world_ > 1 ? emb_full_[t] : act_[e.y], B_, e.Dc, e.lo);
+      jobs.push_back({table_[t], e.nrows, idx_[t], e.bag, world_ > 1 ? emb_full_[t] : act_[e.y], e.Dc, e.lo});
     }
+    if (!jobs.empty()) eng_->emb_fwd_multi(jobs, B_);
     if (world_ == 1 || embs_.empty()) return;
     // pack: per peer p, every held slice's rows [p*Bl, (p+1)*Bl)
     int64_t o = 0;
@@ -1291,7 +1295,12 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
         o += (int64_t)Bl_ * e.Dc;
       }
   };
+  // one rank: the lookups run on the engine's side queue beside the bottom MLP, joined before the
+  // interaction (with ranks, the exchange's RCCL calls stay in program order on one stream)
+  const bool side = world_ == 1 && !embs_.empty();
+  if (side) eng_->side_begin();
   emb_forward();
+  if (side) eng_->side_end();
   // forward in creation order
   for (const Node& n : nodes_) {
     if (n.kind == K_DENSE) {
@@ -1306,6 +1315,7 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
       const Dot& d = dots_[n.idx];
       std::vector<const float*> z;
       for (int t : d.in) z.push_back(act_[t]);
+      eng_->side_join();
       eng_->dot_fwd(z.data(), (int)z.size(), act_[d.y], Bl_, d.D, d.W);
     } else if (n.kind == K_CONV) {
       const Conv& c = convs_[n.idx];
@@ -1337,6 +1347,42 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
     const int64_t b0 = wplan_.buckets[bi][0], n = wplan_.buckets[bi][1] - b0;
     if (zero_on()) eng_->reduce_scatter_start(grads_ + b0, n, zgrad_ + zshard_off_[bi]);
     else eng_->allreduce_start(grads_ + b0, n);
+  };
+  // embedding gradients back to the owners (reverse exchange), then sparse SGD of the touched rows;
+  // with one rank issued on the side queue right after the interaction backward (beside the bottom
+  // MLP's backward), else after the dense backward
+  bool emb_bwd_done = embs_.empty();
+  auto emb_backward = [&]() {
+    if (world_ > 1) {
+      int64_t o = 0;
+      for (int p = 0; p < world_; ++p)
+        for (size_t t = 0; t < embs_.size(); ++t) {
+          const Emb& e = embs_[t];
+          const int j = slice_of(e, p);
+          if (j < 0) continue;
+          // (row blocks: every holder gets the whole gradient, j * Dc = 0 columns offset)
+          eng_->copy2d(xrecv_ + o, (size_t)e.Dc * 4, grad_[e.y] + (e.rows_split ? 0 : (int64_t)j * e.Dc), (size_t)e.D * 4,
+                       (size_t)e.Dc * 4, Bl_);
+          o += (int64_t)Bl_ * e.Dc;
+        }
+      eng_->all_to_all(xrecv_, xcount_recv_.data(), xsend_, xcount_send_.data());
+      o = 0;
+      for (int p = 0; p < world_; ++p)
+        for (size_t t = 0; t < embs_.size(); ++t) {
+          const Emb& e = embs_[t];
+          if (slice_of(e, rank_) < 0) continue;
+          eng_->copy(emb_full_[t] + (int64_t)p * Bl_ * e.Dc, xsend_ + o, (size_t)Bl_ * e.Dc * 4);
+          o += (int64_t)Bl_ * e.Dc;
+        }
+    }
+    std::vector<Engine::EmbJob> jobs;
+    for (size_t t = 0; t < embs_.size(); ++t) {
+      const Emb& e = embs_[t];
+      if (slice_of(e, rank_) < 0) continue;
+      jobs.push_back({table_[t], e.nrows, idx_[t], e.bag, world_ > 1 ? emb_full_[t] : grad_[e.y], e.Dc, e.lo});
+    }
+    if (!jobs.empty()) eng_->emb_sgd_multi(jobs, B_, lr_);
+    emb_bwd_done = true;
   };
   for (int ni = (int)nodes_.size() - 1; ni >= 0; --ni) {
     const Node& n = nodes_[ni];
@@ -1394,38 +1440,15 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
         dz.push_back(grad_[t]);
       }
       eng_->dot_bwd(z.data(), (int)z.size(), grad_[d.y], dz.data(), Bl_, d.D, d.W);
+      if (side && !emb_bwd_done) {
+        eng_->side_begin();
+        emb_backward();
+        eng_->side_end();
+      }
     }
   }
-  // embedding gradients back to the owners (reverse exchange), then sparse SGD of the touched rows
-  if (!embs_.empty()) {
-    if (world_ > 1) {
-      int64_t o = 0;
-      for (int p = 0; p < world_; ++p)
-        for (size_t t = 0; t < embs_.size(); ++t) {
-          const Emb& e = embs_[t];
-          const int j = slice_of(e, p);
-          if (j < 0) continue;
-          // (row blocks: every holder gets the whole gradient, j * Dc = 0 columns offset)
-          eng_->copy2d(xrecv_ + o, (size_t)e.Dc * 4, grad_[e.y] + (e.rows_split ? 0 : (int64_t)j * e.Dc), (size_t)e.D * 4,
-                       (size_t)e.Dc * 4, Bl_);
-          o += (int64_t)Bl_ * e.Dc;
-        }
-      eng_->all_to_all(xrecv_, xcount_recv_.data(), xsend_, xcount_send_.data());
-      o = 0;
-      for (int p = 0; p < world_; ++p)
-        for (size_t t = 0; t < embs_.size(); ++t) {
-          const Emb& e = embs_[t];
-          if (slice_of(e, rank_) < 0) continue;
-          eng_->copy(emb_full_[t] + (int64_t)p * Bl_ * e.Dc, xsend_ + o, (size_t)Bl_ * e.Dc * 4);
-          o += (int64_t)Bl_ * e.Dc;
-        }
-    }
-    for (size_t t = 0; t < embs_.size(); ++t) {
-      const Emb& e = embs_[t];
-      if (slice_of(e, rank_) < 0) continue;
-      eng_->emb_sgd(table_[t], e.nrows, idx_[t], e.bag, world_ > 1 ? emb_full_[t] : grad_[e.y], B_, e.Dc, lr_, e.lo);
-    }
-  }
+  if (!emb_bwd_done) emb_backward();
+  eng_->side_join();
   if (world_ > 1) eng_->allreduce_wait();
   const OptStep os = next_step();
   if (zero_on()) {

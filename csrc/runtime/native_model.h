@@ -342,6 +342,32 @@ class Engine {
   // W[idx[b][j] - lo] -= lr * g[b]  (duplicates accumulate; indices outside the rows skipped)
   virtual void emb_sgd(float* W, int64_t rows, const int64_t* idx, int bag, const float* g, int64_t B, int D, float lr,
                        int64_t lo) = 0;
+  // every local table in one call (default: one emb_fwd / emb_sgd each; the HIP engine batches them
+  // into one multi-table launch, as the executor's fused embedding groups do)
+  struct EmbJob {
+    float* W;
+    int64_t rows;
+    const int64_t* idx;
+    int bag;
+    float* io;       // forward: the output rows; backward: the gradient rows
+    int D;
+    int64_t lo;
+  };
+  virtual void emb_fwd_multi(const std::vector<EmbJob>& jobs, int64_t B) {
+    for (const EmbJob& j : jobs) emb_fwd(j.W, j.rows, j.idx, j.bag, j.io, B, j.D, j.lo);
+  }
+  virtual void emb_sgd_multi(const std::vector<EmbJob>& jobs, int64_t B, float lr) {
+    for (const EmbJob& j : jobs) emb_sgd(j.W, j.rows, j.idx, j.bag, j.io, B, j.D, lr, j.lo);
+  }
+  // a second in-order queue for independent work (the embedding lookups beside the bottom MLP, the
+  // table updates beside its backward): side_begin -> later work runs after everything issued so
+  // far but beside what follows side_end; side_join -> later work waits for the side work.  No-ops
+  // on engines with one queue.
+  virtual void side_begin() {}
+  virtual void side_end() {}
+  virtual void side_join() {}
+  // host -> device without the per-copy sync (the caller syncs before the host buffers change)
+  virtual void h2d_nosync(void* dst, const void* src, size_t bytes) { h2d(dst, src, bytes); }
   virtual void add(float* dst, const float* src, int64_t n) = 0;   // dst += src (device)
   // y[M][W] = [z0 | lower(Z Z^T) | 0] ; dz[i] = (S Z)_i (+ dy[:, :D] for i = 0), S = dG + dG^T
   virtual void dot_fwd(const float* const* z, int F, float* y, int M, int D, int W) = 0;

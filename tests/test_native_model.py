@@ -675,7 +675,7 @@ def test_native_dlrm_mlperf_bench_program_runs_on_cpu(tmp_path):
                     "-o", exe], check=True)
     r = subprocess.run([exe, "cpu", "2", "1", "64", "small"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-    assert "dot interaction: 27 features x 128 -> 479" in r.stdout
+    assert "dot interaction: 27 features x 128 -> 480" in r.stdout
     rec = json.loads(r.stdout.strip().splitlines()[-1])
     assert rec["engine"] == "native-cpu" and rec["batch"] == 64 and rec["ms_per_step"] > 0
     assert np.isfinite(rec["loss"])

@@ -175,7 +175,7 @@ def write_ninja(only=None):
         nc = os.path.join(ROOT, "flexmi", "libflexmi_native_c.so")
         lines.append(f"build {nc}: cxxlink {' '.join(nobjs)} | {klib}")
         lines.append(f"  ldflags = -pthread -L{ROOT}/flexmi -Wl,-rpath,'$$ORIGIN' -lflexmi_kernels "
-                     f"-L{ROCM}/lib -Wl,-rpath,{ROCM}/lib -lamdhip64 -lrccl")
+                     f"-L{ROCM}/lib -Wl,-rpath,{ROCM}/lib -lamdhip64 -lrccl -ldl")
         targets.append(nc)
         # C API (csrc/capi): embeds CPython, so it links libpython
         capi_src = os.path.join(ROOT, "csrc", "capi", "flexmi_c.cc")
