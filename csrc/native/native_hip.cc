@@ -225,6 +225,7 @@ class HipEngine : public Engine {
     hipFree(lr_);
     hipStreamDestroy(comm_st_);
     hipStreamDestroy(side_st_);
+    if (pinned_) hipHostFree(pinned_);
     hipStreamDestroy(st_);
   }
 
@@ -387,6 +388,17 @@ class HipEngine : public Engine {
     fm_embedding_bwd_multi(a.n, a.W.data(), a.ix.data(), a.i64.data(), dy.data(), a.ld.data(), a.l0.data(), a.r.data(),
                            a.D.data(), a.bag.data(), a.sc.data(), 0, lr_, B, nullptr, nullptr, nullptr, st_);
   }
+  void* pinned(size_t bytes) override {
+    if (bytes > pinned_n_) {
+      if (pinned_) {
+        HIPX(hipStreamSynchronize(main_st_));
+        HIPX(hipHostFree(pinned_));
+      }
+      HIPX(hipHostMalloc(&pinned_, bytes, hipHostMallocDefault));
+      pinned_n_ = bytes;
+    }
+    return pinned_;
+  }
   void h2d_nosync(void* dst, const void* src, size_t bytes) override {
     HIPX(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st_));
   }
@@ -538,6 +550,8 @@ class HipEngine : public Engine {
   int rank_, world_;
   hipStream_t st_ = nullptr, comm_st_ = nullptr, main_st_ = nullptr, side_st_ = nullptr;
   bool side_pending_ = false;
+  void* pinned_ = nullptr;
+  size_t pinned_n_ = 0;
   ncclComm_t comm_ = nullptr;
   float* ws_ = nullptr;
   float* slots_ = nullptr;

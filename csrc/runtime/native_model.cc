@@ -499,11 +499,12 @@ Model::~Model() {
   };
   rel(params_);
   rel(grads_);
+  if (input_ >= 0 && input_ < (int)act_.size()) act_[input_] = nullptr;   // carved from in_arena_
   for (auto* p : act_) rel(p);
   for (auto* p : grad_) rel(p);
   for (auto* p : table_) rel(p);
   for (auto* p : emb_full_) rel(p);
-  for (auto* p : idx_) rel(p);
+  rel(in_arena_);   // idx_ and labels_ are views into it
   for (auto& c : chan_)
     for (float* q : {c.x, c.y, c.dy, c.dx, c.w, c.b, c.gw, c.gb}) rel(q);
   rel(csend_);
@@ -511,7 +512,6 @@ Model::~Model() {
   rel(xsend_);
   rel(xrecv_);
   rel(probs_);
-  rel(labels_);
   rel(stats_);
   for (auto* p : pool_code_) rel(p);
   for (auto* p : bn_buf_) rel(p);
@@ -994,18 +994,38 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
   grads_ = (float*)eng_->alloc(wplan_.numel * 4);
   act_.assign(cols_.size(), nullptr);
   grad_.assign(cols_.size(), nullptr);
+  // input arena: [dense input shard | labels | indices of every owned table], 256-B aligned parts
+  {
+    const Dense& lastd = ops_[dense_out_node()];
+    auto part = [&](size_t bytes) {
+      in_parts_.push_back({in_bytes_, bytes});
+      in_bytes_ += (bytes + 255) / 256 * 256;
+    };
+    in_parts_.clear();
+    in_bytes_ = 0;
+    part((size_t)Bl_ * cols_[input_] * 4);
+    part((size_t)Bl_ * (loss_ == LOSS_SCCE ? 4 : (size_t)lastd.N * 4));   // int32 class ids / float targets
+    for (const Emb& e : embs_)
+      if (slice_of(e, rank_) >= 0) part((size_t)B_ * e.bag * 8);
+    in_arena_ = (char*)eng_->alloc(in_bytes_);
+  }
   for (size_t t = 0; t < cols_.size(); ++t) {
+    if ((int)t == input_) {
+      act_[t] = reinterpret_cast<float*>(in_arena_ + in_parts_[0].first);
+      continue;
+    }
     act_[t] = (float*)eng_->alloc((size_t)Bl_ * cols_[t] * 4);
     if ((int)t != input_) grad_[t] = (float*)eng_->alloc((size_t)Bl_ * cols_[t] * 4);
   }
   table_.assign(embs_.size(), nullptr);
   emb_full_.assign(embs_.size(), nullptr);
   idx_.assign(embs_.size(), nullptr);
+  int next_in_part = 0;
   for (size_t t = 0; t < embs_.size(); ++t) {
     const Emb& e = embs_[t];
     if (slice_of(e, rank_) < 0) continue;
     table_[t] = (float*)eng_->alloc((size_t)e.nrows * e.Dc * 4);
-    idx_[t] = (int64_t*)eng_->alloc((size_t)B_ * e.bag * 8);
+    idx_[t] = reinterpret_cast<int64_t*>(in_arena_ + in_parts_[2 + (next_in_part++)].first);
     if (world_ > 1) emb_full_[t] = (float*)eng_->alloc((size_t)B_ * e.Dc * 4);
   }
   if (world_ > 1 && !embs_.empty()) {
@@ -1039,7 +1059,7 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
   for (size_t i = 0; i < bns_.size(); ++i) bn_buf_[i] = (float*)eng_->alloc((size_t)6 * bns_[i].C * 4);
   const int C = last.N;
   if (loss_ == LOSS_SCCE) probs_ = (float*)eng_->alloc((size_t)Bl_ * C * 4);
-  labels_ = eng_->alloc((size_t)Bl_ * C * 4);
+  labels_ = in_arena_ + in_parts_[1].first;
   stats_ = (float*)eng_->alloc(64);
   // optimizer state (momentum v / Adam m, v) for the flat buffer -- or, under ZeRO-1, for this
   // rank's slices only -- and for the channel-split slices this rank holds
@@ -1248,12 +1268,19 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
   const int64_t r0 = (int64_t)rank_ * Bl_;
   // the batch uploads are issued back to back with ONE sync (the caller's host arrays may change after
   // train_step returns)
-  eng_->h2d_nosync(act_[input_], x + r0 * cols_[input_], (size_t)Bl_ * cols_[input_] * 4);
   const size_t lab_row = loss_ == LOSS_SCCE ? 4 : (size_t)C * 4;
-  eng_->h2d_nosync(labels_, static_cast<const char*>(labels) + r0 * lab_row, (size_t)Bl_ * lab_row);
+  std::vector<const void*> srcs{x + r0 * cols_[input_], static_cast<const char*>(labels) + r0 * lab_row};
   for (size_t t = 0; t < embs_.size(); ++t)
-    if (slice_of(embs_[t], rank_) >= 0) eng_->h2d_nosync(idx_[t], sparse[embs_[t].sparse], (size_t)B_ * embs_[t].bag * 8);
-  eng_->sync();
+    if (slice_of(embs_[t], rank_) >= 0) srcs.push_back(sparse[embs_[t].sparse]);
+  if (char* pin = static_cast<char*>(eng_->pinned(in_bytes_))) {
+    // packed into page-locked memory, one asynchronous upload (the previous step's final sync has
+    // released the staging buffer)
+    for (size_t k = 0; k < srcs.size(); ++k) std::memcpy(pin + in_parts_[k].first, srcs[k], in_parts_[k].second);
+    eng_->h2d_nosync(in_arena_, pin, in_bytes_);
+  } else {
+    for (size_t k = 0; k < srcs.size(); ++k) eng_->h2d_nosync(in_arena_ + in_parts_[k].first, srcs[k], in_parts_[k].second);
+    eng_->sync();
+  }
   eng_->zero(stats_, 2 * sizeof(float));
 
   // embedding lookups (owners, global batch) and the exchange to the sample shards, issued ahead

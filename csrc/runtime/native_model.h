@@ -298,6 +298,11 @@ class Model {
   float* probs_ = nullptr;                    // SCCE: softmax of the logits
   void* labels_ = nullptr;
   float* stats_ = nullptr;                    // [loss, correct] accumulators
+  // the per-step inputs (dense shard, labels, owned tables' indices) carved from ONE device arena in
+  // the order of a host-side packing, so a pinned engine uploads a batch with one copy
+  char* in_arena_ = nullptr;
+  std::vector<std::pair<size_t, size_t>> in_parts_;   // (offset, bytes): input, labels, idx of each owned table
+  size_t in_bytes_ = 0;
 };
 
 // ---- execution engines ----------------------------------------------------------------------
@@ -366,6 +371,12 @@ class Engine {
   virtual void side_begin() {}
   virtual void side_end() {}
   virtual void side_join() {}
+  // page-locked host memory (grow-only, owned by the engine; nullptr: the engine has none) -- the batch
+  // is packed there and uploaded by ONE asynchronous copy
+  virtual void* pinned(size_t bytes) {
+    (void)bytes;
+    return nullptr;
+  }
   // host -> device without the per-copy sync (the caller syncs before the host buffers change)
   virtual void h2d_nosync(void* dst, const void* src, size_t bytes) { h2d(dst, src, bytes); }
   virtual void add(float* dst, const float* src, int64_t n) = 0;   // dst += src (device)
