@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Measure the GEMM configuration table (flexmi/ops/gemm_tune.py) on the GPU.
 
-  python tools/tune_gemm.py [--configs mlperf:8192,summit:512] [--dtypes fp32,bf16] [--reps 20]
+  python tools/tune_gemm.py [--configs mlperf:8192,summit:512,alexnet:256] [--dtypes fp32,bf16] [--reps 20]
                             [--out flexmi/ops/tuned/gemm_mi355x.json] [--merge]
 
 For each DLRM configuration and compute dtype: build the model (tables shrunk: the GEMM shapes do
@@ -45,6 +45,44 @@ def record_specs(config, batch, dtype):
     for t, r in zip(s, dcfg.embedding_size):
         ex.scatter_from_host(t, rng.randint(0, r, (batch, dcfg.embedding_bag_size)).astype(np.int64))
     ex.scatter_from_host(m.get_label_tensor(), rng.randint(0, 2, (batch, 1)).astype(np.float32))
+    T.RECORD = []
+    try:
+        ex.train_step()
+        torch.cuda.synchronize()
+        specs = T.RECORD
+    finally:
+        T.RECORD = None
+    del ex, m
+    torch.cuda.empty_cache()
+    return specs
+
+
+def record_specs_zoo(name, batch, dtype):
+    """The GEMMs of one training step of a model-zoo network (CNN classifiers: the fully connected
+    layers' forward / dX / dW-with-SGD GEMMs; the convolutions run their own kernels)."""
+    import torch
+    from flexmi.core import DataType, FFConfig, FFModel, SGDOptimizer
+    from flexmi.models import zoo
+    from flexmi.ops import gemm_tune as T
+    cfg = FFConfig()
+    cfg.batchSize = batch
+    cfg.compute_dtype = dtype
+    m = FFModel(cfg)
+    built = zoo.build(name, m)
+    m.compile(SGDOptimizer(m, built.lr), built.loss, built.metrics)
+    ex = m.init_layers()
+    rng = np.random.RandomState(0)
+    for t in built.inputs.values():
+        if t.data_type in (DataType.DT_INT32, DataType.DT_INT64):
+            ex.scatter_from_host(t, rng.randint(0, built.extra.get("int_range", 2), t.dims).astype(np.int32))
+        else:
+            ex.scatter_from_host(t, rng.rand(*t.dims).astype(np.float32))
+    lab = m.get_label_tensor()
+    if lab.data_type == DataType.DT_INT32:
+        ex.scatter_from_host(lab, rng.randint(0, built.output.dims[-1], lab.dims).astype(np.int32))
+    else:
+        ex.scatter_from_host(lab, rng.rand(*lab.dims).astype(np.float32))
+    ex.train_step()                      # first step: conv forms measured, buffers settled
     T.RECORD = []
     try:
         ex.train_step()
@@ -156,7 +194,13 @@ def main():
     for item in args.configs.split(","):
         config, batch = item.split(":")
         for dtype in args.dtypes.split(","):
-            specs = record_specs(config, int(batch), dtype)
+            from flexmi.models.dlrm import DLRMConfig
+            try:
+                DLRMConfig.preset(config)
+                zoo_model = False
+            except Exception:
+                zoo_model = True            # a model-zoo network (alexnet, resnet50, ...)
+            specs = record_specs_zoo(config, int(batch), dtype) if zoo_model else record_specs(config, int(batch), dtype)
             seen = {}
             for sp in specs:
                 seen.setdefault(sp["key"], sp)
