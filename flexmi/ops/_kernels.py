@@ -575,8 +575,12 @@ def _conv_choose(saved, direction, forms, run, key):
     pick = forms[0]
     if (CONV_TUNE and len(forms) > 1 and saved is not None and not _chained(saved) and torch.cuda.is_available()
             and not torch.cuda.is_current_stream_capturing()):
-        times = {f: _time_us(lambda f=f: run(f)) for f in forms}
-        pick = min(times, key=times.get)
+        times = {}
+        for f in forms:
+            if run(f) is False:     # the form does not apply to this layout (a backward fell through)
+                continue
+            times[f] = _time_us(lambda f=f: run(f))
+        pick = min(times, key=times.get) if times else forms[0]
         CONV_TUNE_LOG.append((direction, key, times, pick))
     if saved is not None:
         saved[name] = pick

@@ -20,6 +20,7 @@ CASES = [
     (2, 32, 14, 14, 48, 3, 3, 1, (1, 1, 1, 1)),
     (2, 64, 14, 14, 32, 1, 1, 2, (0, 0, 0, 0)),       # strided 1x1 shortcut (phase forward)
     (2, 48, 17, 17, 64, 3, 3, 2, (1, 1, 1, 1)),       # strided 3x3 (phase backward)
+    (2, 32, 15, 15, 48, 1, 1, 2, (0, 0, 0, 0)),       # strided 1x1, odd extent
 ]
 
 
@@ -95,3 +96,22 @@ def test_tuner_picks_and_records_a_form(gpu, case, monkeypatch):
     # later calls reuse the recorded forms without timing again
     Kk.conv2d_forward(x, w, b, y, (s, s), pads, 11, 1, saved)
     assert len(Kk.CONV_TUNE_LOG) == n0 + len(log)
+
+
+
+def test_tuner_skips_a_form_that_does_not_apply(gpu, monkeypatch):
+    """A backward candidate that falls through (returns False: the form does not apply to the layout)
+    is not timed -- an early return once measured 1.5 us and was picked, and the step then ran the
+    slow fallback."""
+    from flexmi.ops import _kernels as Kk
+    monkeypatch.setattr(Kk, "CONV_TUNE", True)
+    x = torch.zeros(64, 64, device=gpu)
+
+    def run(f):
+        if f == "nope":
+            return False
+        x.add_(1.0)
+        return True
+    saved = {}
+    assert Kk._conv_choose(saved, "bwd", ["nope", "works"], run, ("k",)) == "works"
+    assert saved["conv_form_bwd"] == "works"
