@@ -145,6 +145,8 @@ void fm_conv_nhwc_dgrad_strided(const void* gs, long gs_bytes, const void* w, vo
                                 hipStream_t s);
 long fm_conv_nhwc_wgrad_ws(int N, int K, int P, int Q, int R, int S, int Cp);
 void fm_conv_nhwc_set_shape(int mode, int shape);
+void fm_cnhwc_wprep_multi_run(int n, const void* const* w, void* const* out, void* const* out2, const int* K, const int* C,
+                              const int* R, const int* S, const int* Cp, const int* Kp, hipStream_t s);
 void fm_cnhwc_wprep_run(const void* w, void* out, void* out2, const float* g2, float* dw, int K, int C, int R, int S, int Cp,
                         int Kp, int mode, int nsplit, hipStream_t s);
 void fm_conv_nhwc_fwd(const void* xs, long xs_bytes, const void* wf, const float* bias, void* y, int N, int K, int P, int Q,
@@ -979,6 +981,38 @@ void cnhwc_wprep(torch::Tensor w, torch::Tensor out, torch::Tensor out2, torch::
                      mode == 2 ? g2.data_ptr<float>() : nullptr, mode == 2 ? dw.data_ptr<float>() : nullptr, (int)K, (int)C,
                      (int)w.size(2), (int)w.size(3), (int)Cp, (int)Kp, (int)mode, (int)nsplit, cur());
 }
+// cnhwc_wprep mode 3 of several layers in one launch: w[i] [K,C,R,S] bf16 -> out[i] (fwd matrix
+// [K][R*S*Cp[i]]) and out2[i] (dgrad matrix [C][R*S*Kp[i]])
+void cnhwc_wprep_multi(std::vector<torch::Tensor> w, std::vector<torch::Tensor> out, std::vector<torch::Tensor> out2,
+                       std::vector<int64_t> Cp, std::vector<int64_t> Kp) {
+  const size_t n = w.size();
+  TORCH_CHECK(out.size() == n && out2.size() == n && Cp.size() == n && Kp.size() == n, "cnhwc_wprep_multi: list sizes");
+  std::vector<const void*> wp(n);
+  std::vector<void*> op(n), o2(n);
+  std::vector<int> K(n), C(n), R(n), S(n), cp(n), kp(n);
+  for (size_t i = 0; i < n; ++i) {
+    TORCH_CHECK(w[i].dim() == 4, "cnhwc_wprep_multi: w [K,C,R,S]");
+    K[i] = (int)w[i].size(0);
+    C[i] = (int)w[i].size(1);
+    R[i] = (int)w[i].size(2);
+    S[i] = (int)w[i].size(3);
+    cp[i] = (int)Cp[i];
+    kp[i] = (int)Kp[i];
+    const long RS = (long)R[i] * S[i];
+    TORCH_CHECK(cp[i] % 8 == 0 && cp[i] >= C[i] && kp[i] % 8 == 0 && kp[i] >= K[i], "cnhwc_wprep_multi: padded channel counts");
+    TORCH_CHECK((long)K[i] * RS * cp[i] + (long)C[i] * RS * kp[i] + 256L * 1024 < (1L << 31),
+                "cnhwc_wprep_multi: weight too large for 32-bit indexing");
+    nhwc_chk(w[i], (long)K[i] * C[i] * RS, "cnhwc_wprep_multi w");
+    nhwc_chk(out[i], (long)K[i] * RS * cp[i], "cnhwc_wprep_multi out (fwd matrix)");
+    nhwc_chk(out2[i], (long)C[i] * RS * kp[i], "cnhwc_wprep_multi out2 (dgrad matrix)");
+    wp[i] = w[i].data_ptr();
+    op[i] = out[i].data_ptr();
+    o2[i] = out2[i].data_ptr();
+  }
+  if (n) fm_cnhwc_wprep_multi_run((int)n, wp.data(), op.data(), o2.data(), K.data(), C.data(), R.data(), S.data(), cp.data(),
+                                  kp.data(), cur());
+}
+
 // second output of a conv GEMM: a consumer's staged operand [N][H2][W2][C2] (o2 = {H2, W2, C2, t2, l2,
 // d2h, d2w, write_nchw}); every position the epilogue can address lies inside it
 static void* out2_chk(const c10::optional<torch::Tensor>& out2, const std::vector<int64_t>& o2, long N, long M, long OH,
@@ -1222,6 +1256,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("nhwc_stage", &nhwc_stage);
   m.def("nhwc_stage_grad", &nhwc_stage_grad);
   m.def("conv_nhwc_wgrad_ws", &conv_nhwc_wgrad_ws);
+  m.def("cnhwc_wprep_multi", &cnhwc_wprep_multi);
   m.def("conv_nhwc_set_shape", [](int64_t mode, int64_t shape) { fm_conv_nhwc_set_shape((int)mode, (int)shape); });
   m.def("cnhwc_wprep", &cnhwc_wprep);
   m.def("conv_nhwc_fwd", &conv_nhwc_fwd);

@@ -852,22 +852,53 @@ def nhwc_g_geometry(x_shape, w_shape, y_shape, stride, pads, need_dx):
     return (N, P, Q, _r8(Kout), 0, 0, 1, 1)
 
 
+def _nhwc_wbufs(saved, w):
+    """This layer's forward matrix [K][R*S*Cp] and dgrad matrix [C][R*S*Kp] (kept in ``saved``)."""
+    Kout, Cin, R, S = w.shape
+    nwf, nwd = Kout * R * S * _r8(Cin), Cin * R * S * _r8(Kout)
+    wf, wd = saved.get("nhwc_wf"), saved.get("nhwc_wd")
+    if wf is None or wf.numel() != nwf or wf.device != w.device:
+        wf = saved["nhwc_wf"] = torch.empty(nwf, dtype=w.dtype, device=w.device)
+    if wd is None or wd.numel() != nwd or wd.device != w.device:
+        wd = saved["nhwc_wd"] = torch.empty(nwd, dtype=w.dtype, device=w.device)
+    return wf, wd
+
+
+def conv_wprep_all(layers):
+    """The weight re-layouts of every convolution whose last forward ran the NHWC form, in ONE launch
+    at the start of the step's forward (weights change only at the update): ``layers`` = [(w,
+    saved)].  Each such layer's next _nhwc_forward finds ``saved["nhwc_wf_ready"]`` and skips its own
+    re-layout launch (ResNet-50: 53 launches of ~7 us per step -> 1)."""
+    ws, wfs, wds, cps, kps, marks = [], [], [], [], [], []
+    for w, saved in layers:
+        if saved is None or not saved.get("nhwc_fwd_used") or w.dtype != torch.bfloat16 or not w.is_contiguous():
+            continue
+        wf, wd = _nhwc_wbufs(saved, w)
+        ws.append(w)
+        wfs.append(wf)
+        wds.append(wd)
+        cps.append(_r8(w.shape[1]))
+        kps.append(_r8(w.shape[0]))
+        marks.append(saved)
+    if ws:
+        C().cnhwc_wprep_multi(ws, wfs, wds, cps, kps)
+    for sv in marks:
+        sv["nhwc_wf_ready"] = True
+
+
 def _nhwc_forward(x, w, b, y, stride, pads, act, saved):
     Kout, Cin, R, S = w.shape
     xs, Cp, Hp, Wp = _nhwc_stage_x(x, w, y, stride, pads, saved)
     if saved is not None:
         saved["nhwc_x_ready"] = True
-    wf = scratch(x.device, "cn_wf", Kout * R * S * Cp, w.dtype)
-    if saved is not None:
+        saved["nhwc_fwd_used"] = True
         # the backward's flipped / transposed matrix comes out of the same launch (weights do not
-        # change between an op's forward and backward)
-        nwd = Cin * R * S * _r8(Kout)
-        wd = saved.get("nhwc_wd")
-        if wd is None or wd.numel() != nwd or wd.device != w.device:
-            wd = torch.empty(nwd, dtype=w.dtype, device=w.device)
-            saved["nhwc_wd"] = wd
-        C().cnhwc_wprep(w, wf, wd, w, w, Cp, _r8(Kout), 3, 1)
+        # change between an op's forward and backward), or both came from this step's conv_wprep_all
+        wf, wd = _nhwc_wbufs(saved, w)
+        if not saved.pop("nhwc_wf_ready", False):
+            C().cnhwc_wprep(w, wf, wd, w, w, Cp, _r8(Kout), 3, 1)
     else:
+        wf = scratch(x.device, "cn_wf", Kout * R * S * Cp, w.dtype)
         C().cnhwc_wprep(w, wf, w, w, w, Cp, _r8(Kout), 0, 1)
     o2 = saved.get("nhwc_out2") if saved is not None else None   # conv chain fusion: the consumer's staged input
     C().conv_nhwc_fwd(xs, wf, b, y, R, S, Cp, Hp, Wp, stride[0], stride[1], int(act), o2[0] if o2 else None,

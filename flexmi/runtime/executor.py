@@ -182,6 +182,9 @@ XCHG_CHUNKS = os.environ.get("FLEXMI_XCHG_CHUNKS", "auto")
 # test hook: chunk the row-wise tail at world 1 too (no exchange; exercises the chunked kernels)
 XCHG_LOCAL = False
 PIPE_ROW_ALIGN = 8          # chunk boundaries on 8-row multiples: 16-B aligned rows for the kernels
+# the NHWC convolutions' weight re-layouts as one launch per step (conv_wprep_all): ResNet-50 b64
+# 6.62 -> 6.69 k img/s, AlexNet b256 within noise (profiles/conv_wprep_all_ab_r7.txt); tests flip it
+CONV_WPREP_ALL = True
 # smallest weight (elements) whose SGD is fused into its dW GEMM (FM_FUSED_SGD); tests lower it
 FUSED_SGD_MIN = 1 << 21
 
@@ -1542,6 +1545,21 @@ class Executor:
 
         def C(lst, name, fn):
             lst.append(Item("compute", fn, name))
+
+        # the NHWC convolutions' weight re-layouts of the step in one launch before the forward
+        # (flexmi/ops/_kernels.py conv_wprep_all; layers join after their first NHWC forward)
+        from flexmi.core.types import OperatorType as _OT
+        convs = [st[1] for st in self.fwd_steps if st[0] == "op" and st[1].op_type == _OT.OP_CONV2D]
+        if self.backend == "hip" and convs and CONV_WPREP_ALL:
+            def wprep_all(convs=convs):
+                from flexmi.ops import _kernels as K
+                layers = []
+                for op in convs:
+                    c = self.ctx.get(op.guid)
+                    if c is not None and not c.empty and c.wcompute and c.wcompute[0] is not None:
+                        layers.append((c.wcompute[0], c.saved))
+                K.conv_wprep_all(layers)
+            C(fwd, "conv.wprep_all", wprep_all)
 
         # ---------------- forward
         # cross-device reshards are split: pack + asynchronous all_to_all right after the last
