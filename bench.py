@@ -41,6 +41,10 @@ exchange (each replica coalesces its lookups, one all-gather of (row, gradient) 
 replica applies them in rank order; no table-sized gradient) -- and reported as ``config.dp``
 with ``config.soap_speedup_vs_dp`` = value / dp.value (``--no-dp`` skips it).
 
+Native engine (N = 1, fp32): the same model, batch, steps and warm-up trained by the C++ plan compiler and
+HIP engine alone (apps/c/dlrm_native_bench.c through libflexmi_native_c, a child process with no
+Python), reported as ``config.native_engine`` (``--no-native`` skips it).
+
 Timed region: W untimed steps, then EXACTLY K full training steps (forward, backward, all
 collectives, SGD update of every parameter incl. the sparse embedding rows) bracketed by a
 barrier + device synchronize on both sides; the max over ranks is reported.  Prints ONE JSON line.
@@ -81,6 +85,9 @@ def parse():
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
                     help="headline compute precision (fp32 = the reference's precision)")
     ap.add_argument("--no-secondary", action="store_true", help="skip the secondary run in the other precision")
+    ap.add_argument("--no-native", action="store_true",
+                    help="N=1: skip the native-engine comparison (config.native_engine: the same model trained by the "
+                         "C++ plan compiler + HIP engine alone, apps/c/dlrm_native_bench.c)")
     ap.add_argument("--no-dp", action="store_true",
                     help="N>1: skip the pure data-parallel comparison run (config.dp / config.soap_speedup_vs_dp)")
     ap.add_argument("--no-table", action="store_true",
@@ -144,6 +151,9 @@ def main():
         # data parallelism (replicated tables trained by touched-row all-gather, DP MLPs)
         runs.append(("dp", a.dtype, "dp"))
     extra = {name: guarded_run(a, comm, name, dt, strat, head, t_start) for name, dt, strat in runs}
+    native = None
+    if cuda and world == 1 and not a.no_native and a.dtype == "fp32" and a.table_scale == 1.0:
+        native = native_run(a, t_start)
     if rank == 0:
         rec = head["rec"]
         for name, r in extra.items():
@@ -155,6 +165,8 @@ def main():
                 sub["parallelism"] = r["rec"]["config"]["parallelism"]
             sub["hbm"] = r["rec"]["config"].get("hbm")
             rec["config"][name] = sub
+        if native is not None:
+            rec["config"]["native_engine"] = native
         if "rec" in extra.get("table", {}):
             rec["config"]["search_speedup_vs_table"] = round(rec["value"] / extra["table"]["rec"]["value"], 3)
         if "rec" in extra.get("dp", {}):
@@ -271,6 +283,42 @@ def guarded_run(a, comm, name, dtype, strategy, head, t_start):
         traceback.print_exc(file=sys.stderr)
         _release_memory()
         return {"error": f"{type(e).__name__}: {e}"[:400]}
+
+
+def native_run(a, t_start, timeout_s=300.0):
+    """The headline configuration trained by the native engine alone: apps/c/dlrm_native_bench.c (the C
+    API's plan compiler + HIP engine, no Python in that process; same model, batch, fp32, steps and
+    warm-up; its tables stay zero-initialised) built with gcc and run as a child process after this
+    process released its models.  A comparison only: any failure is reported, never raised."""
+    import json as _json
+    import shutil
+    import subprocess
+    import tempfile
+    root = os.path.dirname(os.path.abspath(__file__))
+    lib_dir = os.path.join(root, "flexmi")
+    src = os.path.join(root, "apps", "c", "dlrm_native_bench.c")
+    if not os.path.exists(os.path.join(lib_dir, "libflexmi_native_c.so")) or not os.path.exists(src):
+        return {"skipped": "libflexmi_native_c.so or apps/c/dlrm_native_bench.c missing"}
+    if shutil.which("gcc") is None:
+        return {"skipped": "no gcc to build apps/c/dlrm_native_bench.c"}
+    left = a.budget_s - (time.time() - t_start)
+    if left < timeout_s + 30:
+        return {"skipped": f"wall budget: {left:.0f} s left of --budget-s {a.budget_s:.0f}"}
+    _release_memory()
+    try:
+        exe = os.path.join(tempfile.mkdtemp(prefix="flexmi_native_"), "dlrm_native_bench")
+        subprocess.run(["gcc", "-O2", src, "-I" + os.path.join(root, "csrc", "capi"), "-L" + lib_dir,
+                        "-Wl,-rpath," + lib_dir, "-lflexmi_native_c", "-o", exe], check=True, capture_output=True,
+                       timeout=120)
+        r = subprocess.run([exe, "hip", str(a.steps), str(a.warmup), str(a.batch_per_gpu)], capture_output=True,
+                           text=True, timeout=timeout_s)
+        if r.returncode != 0:
+            return {"error": f"exit {r.returncode}: {r.stderr.strip()[-300:]}"}
+        out = _json.loads(r.stdout.strip().splitlines()[-1])
+        return {"engine": out["engine"], "value": out["samples_per_s"], "ms_per_step": out["ms_per_step"],
+                "loss": out["loss"], "program": "apps/c/dlrm_native_bench.c"}
+    except Exception as e:   # noqa: BLE001 -- reported in the record
+        return {"error": f"{type(e).__name__}: {e}"[:300]}
 
 
 def _release_memory():
