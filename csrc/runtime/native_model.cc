@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <sstream>
 #include <stdexcept>
 #include <vector>
@@ -1272,11 +1273,16 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
   std::vector<const void*> srcs{x + r0 * cols_[input_], static_cast<const char*>(labels) + r0 * lab_row};
   for (size_t t = 0; t < embs_.size(); ++t)
     if (slice_of(embs_[t], rank_) >= 0) srcs.push_back(sparse[embs_[t].sparse]);
+  std::function<void()> idx_upload;
   if (char* pin = static_cast<char*>(eng_->pinned(in_bytes_))) {
     // packed into page-locked memory, one asynchronous upload (the previous step's final sync has
     // released the staging buffer)
     for (size_t k = 0; k < srcs.size(); ++k) std::memcpy(pin + in_parts_[k].first, srcs[k], in_parts_[k].second);
-    eng_->h2d_nosync(in_arena_, pin, in_bytes_);
+    // the dense input and labels on the compute stream; the table indices (most of the bytes) go up
+    // with the lookups (on the side queue at one rank), so the bottom MLP starts after the small copy
+    const size_t head = srcs.size() > 2 ? in_parts_[2].first : in_bytes_;
+    eng_->h2d_nosync(in_arena_, pin, head);
+    if (head < in_bytes_) idx_upload = [this, pin, head]() { eng_->h2d_nosync(in_arena_ + head, pin + head, in_bytes_ - head); };
   } else {
     for (size_t k = 0; k < srcs.size(); ++k) eng_->h2d_nosync(in_arena_ + in_parts_[k].first, srcs[k], in_parts_[k].second);
     eng_->sync();
@@ -1326,6 +1332,7 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
   // interaction (with ranks, the exchange's RCCL calls stay in program order on one stream)
   const bool side = world_ == 1 && !embs_.empty();
   if (side) eng_->side_begin();
+  if (idx_upload) idx_upload();
   emb_forward();
   if (side) eng_->side_end();
   // forward in creation order
