@@ -305,12 +305,10 @@ class HipEngine : public Engine {
   void softmax(const float* x, float* y, int M, int C) override { fm_softmax_fwd(x, y, M, C, 0, st_); }
 
   void loss(int type, const float* p, const void* labels, float* grad, int M, int C, float scale, float* stats) override {
-    HIPX(hipMemsetAsync(slots_, 0, 16 * sizeof(float), st_));
-    fm_loss_fwd_bwd(p, 0, labels, grad, 0, M, C, type, scale, slots_, 1, 0.f, st_);
-    // metric slots: [1] correct, [7] loss sum
-    HIPX(hipMemcpyAsync(stats, slots_ + 7, sizeof(float), hipMemcpyDeviceToDevice, st_));
-    HIPX(hipMemcpyAsync(stats + 1, slots_ + 1, sizeof(float), hipMemcpyDeviceToDevice, st_));
+    // the kernel's metric slots ARE the model's stats buffer ([1] correct, [7] loss sum): no copies
+    fm_loss_fwd_bwd(p, 0, labels, grad, 0, M, C, type, scale, stats, 1, 0.f, st_);
   }
+  int stat_slot(int which) const override { return which == 0 ? 7 : 1; }
 
   void sgd(float* w, float* g, int64_t n, float lr) override {
     set_lr(lr);

@@ -1287,7 +1287,7 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
     for (size_t k = 0; k < srcs.size(); ++k) eng_->h2d_nosync(in_arena_ + in_parts_[k].first, srcs[k], in_parts_[k].second);
     eng_->sync();
   }
-  eng_->zero(stats_, 2 * sizeof(float));
+  eng_->zero(stats_, 16 * sizeof(float));
 
   // embedding lookups (owners, global batch) and the exchange to the sample shards, issued ahead
   // of the first consumer
@@ -1517,12 +1517,12 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
       if (chan_[i].b) eng_->opt_update(chan_[i].b, chan_[i].gb, cs[2], cs[3], d.Nc, os);
     }
   }
-  float st[2];
+  float st[16];
   eng_->sync();
   eng_->d2h(st, stats_, sizeof(st));
   StepStat s;
-  s.loss = st[0] / Bl_;
-  s.correct = (int64_t)st[1];
+  s.loss = st[eng_->stat_slot(0)] / Bl_;
+  s.correct = (int64_t)st[eng_->stat_slot(1)];
   s.samples = Bl_;
   return s;
 }

@@ -321,9 +321,11 @@ class Engine {
   virtual void dense_bwd(const float* x, const float* W, const float* y, const float* dy, float* dx, float* dW, float* db,
                          int M, int K, int N, int act, bool grad_is_dpre, const float* y_below, int act_below) = 0;
   virtual void softmax(const float* x, float* y, int M, int C) = 0;
-  // grad = (p - target) * scale; stats[0] += loss sum, stats[1] += correct predictions
+  // grad = (p - target) * scale; stats (16 floats, zeroed by the caller each step): loss sum at
+  // stats[stat_slot(0)], correct predictions at stats[stat_slot(1)]
   virtual void loss(int type, const float* p, const void* labels, float* grad, int M, int C, float scale,
                     float* stats) = 0;
+  virtual int stat_slot(int which) const { return which; }
   virtual void sgd(float* w, float* g, int64_t n, float lr) = 0;   // w -= lr g; g = 0
   // one optimizer update of n parameters (OptConfig); s1 / s2: its state (momentum v, or Adam m / v);
   // consumes g (left zeroed)
