@@ -23,6 +23,7 @@
 #define NT 26
 #define D 128
 #define FEAT 13
+#define FEAT_PAD 16   /* the dense input zero-padded to 16 features (as the executor pads it): 16-B rows */
 static const int64_t MLPERF_ROWS[NT] = {39884406, 39043,    17289,    7420,     20263,   3,     7120,  1543,   63,
                                         38532951, 2953546,  403346,   10,       2208,    11938, 155,   4,      976,
                                         14,       39979771, 25641295, 39664984, 585935,  12972, 108,   36};
@@ -68,7 +69,7 @@ int main(int argc, char** argv) {
   }
   int x, t, emb[NT];
   int64_t rows[NT];
-  CHECK(x = fmn_model_input(m, FEAT));
+  CHECK(x = fmn_model_input(m, FEAT_PAD));
   CHECK(t = fmn_model_dense(m, x, 512, 11, 1));
   CHECK(t = fmn_model_dense(m, t, 256, 11, 1));
   CHECK(t = fmn_model_dense(m, t, D, 11, 1));
@@ -100,10 +101,11 @@ int main(int argc, char** argv) {
     CHECK(fmn_model_set_param(m, i, w));
     free(w);
   }
-  float* dense = (float*)malloc(sizeof(float) * (size_t)B * FEAT);
+  float* dense = (float*)calloc((size_t)B * FEAT_PAD, sizeof(float));
   float* lab = (float*)malloc(sizeof(float) * (size_t)B);
   int64_t* idx[NT];
-  for (int k = 0; k < B * FEAT; ++k) dense[k] = frand();
+  for (int b = 0; b < B; ++b)
+    for (int k = 0; k < FEAT; ++k) dense[(size_t)b * FEAT_PAD + k] = frand();
   for (int b = 0; b < B; ++b) lab[b] = (float)(next_u64() & 1);
   for (int i = 0; i < NT; ++i) {
     idx[i] = (int64_t*)malloc(sizeof(int64_t) * (size_t)B);

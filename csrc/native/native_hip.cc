@@ -53,6 +53,11 @@ void fm_loss_fwd_bwd(const void* logits, int logits_bf16, const void* labels, vo
                      int loss_type, float scale, float* acc, int mask, float clamp_t, hipStream_t s);
 void fm_sgd_update(float* W, float* G, float* V, unsigned short* Wc, const float* lr, long n, float wd, float mom, int nesterov,
                    int zero_g, hipStream_t s);
+int fm_smallk_fwd_launch(const void* x, long ldx, const void* w, const float* bias, void* y, long ldy, long M, int K, int N,
+                         int act, int bf16, hipStream_t s);
+int fm_smallk_dw_launch(const void* dpre, long ldd, const void* x, long ldx, float* dw, float* db, long M, int K, int N,
+                        float* ws, long ws_bytes, float* V, unsigned short* Wc, const float* lr, float wd, float mom,
+                        int nesterov, int bf16, hipStream_t s);
 void fm_adam_update(float* W, float* G, float* M, float* V, unsigned short* Wc, long n, const float* alpha_t, float b1, float b2,
                     float wd, float eps, int zero_g, hipStream_t s);
 void fm_embedding_fwd_multi(int n, const float* const* W, const void* const* idx, const int* idx64, void* const* out,
@@ -271,6 +276,9 @@ class HipEngine : public Engine {
   }
 
   void dense_fwd(const float* x, const float* W, const float* b, float* y, int M, int K, int N, int act) override {
+    // thin inputs (K <= 32, K % 4 == 0: the DLRM bottom layer on its padded 16 features) on the
+    // executor's gemm_small kernel
+    if (K <= 32 && fm_smallk_fwd_launch(x, K, W, b, y, N, M, K, N, act, 0, st_) == 0) return;
     if (N == 1) {
       fm_skinny_fwd_f32_launch(x, K, W, b, y, 1, M, K, act, st_);
       return;
@@ -292,9 +300,13 @@ class HipEngine : public Engine {
       fm_act_bwd_bias(y, dy, t, nullptr, M, N, act, 0, st_);
       dpre = t;
     }
-    // dW[N][K] += dpre^T x (both operands MN-contiguous), db += column sums of dpre
-    fm_gemm_f32(dpre, N, 0, 0, x, K, 0, 0, dW, K, 0, nullptr, N, K, M, 1, 1.f, 1, ACT_NONE, ws_, WS_BYTES,
-                TuneTable::get().cfg(N, K, M, false, false, false, db != nullptr), nullptr, 0, ACT_NONE, nullptr, db, st_);
+    // dW[N][K] += dpre^T x (both operands MN-contiguous), db += column sums of dpre (thin inputs:
+    // gemm_small's partial / reduce pair)
+    const bool thin = K <= 32 && fm_smallk_dw_launch(dpre, N, x, K, dW, db, M, K, N, ws_, WS_BYTES, nullptr, nullptr, nullptr,
+                                                     0.f, 0.f, 0, 0, st_) == 0;
+    if (!thin)
+      fm_gemm_f32(dpre, N, 0, 0, x, K, 0, 0, dW, K, 0, nullptr, N, K, M, 1, 1.f, 1, ACT_NONE, ws_, WS_BYTES,
+                  TuneTable::get().cfg(N, K, M, false, false, false, db != nullptr), nullptr, 0, ACT_NONE, nullptr, db, st_);
     if (!dx) return;
     // dX[M][K] = dpre W (+ act' of the layer below)
     fm_gemm_f32(dpre, N, 0, 1, W, K, 0, 0, dx, K, 0, nullptr, M, K, N, 1, 1.f, 0, ACT_NONE, ws_, WS_BYTES,
