@@ -416,8 +416,8 @@ class HipEngine : public Engine {
   void dot_fwd(const float* const* z, int F, float* y, int M, int D, int W) override {
     fm_dot_interaction_fwd_f32(z, F, D, y, W, M, D, W, 0, st_);
   }
-  void dot_bwd(const float* const* z, int F, const float* dy, float* const* dz, int M, int D, int W) override {
-    fm_dot_interaction_bwd_f32(z, F, D, dy, W, dz, D, 0u, M, D, 0, ACT_NONE, st_);
+  void dot_bwd(const float* const* z, int F, const float* dy, float* const* dz, int M, int D, int W, int act0) override {
+    fm_dot_interaction_bwd_f32(z, F, D, dy, W, dz, D, 0u, M, D, 0, act0, st_);
   }
   void all_to_all(const float* send, const int64_t* send_counts, float* recv, const int64_t* recv_counts) override {
     if (!comm_) {

@@ -242,7 +242,7 @@ class CpuEngine : public Engine {
         }
     }
   }
-  void dot_bwd(const float* const* z, int F, const float* dy, float* const* dz, int M, int D, int W) override {
+  void dot_bwd(const float* const* z, int F, const float* dy, float* const* dz, int M, int D, int W, int act0) override {
     std::vector<float> S((size_t)F * F);
     for (int m = 0; m < M; ++m) {
       const float* g = dy + (int64_t)m * W;
@@ -260,7 +260,7 @@ class CpuEngine : public Engine {
         for (int d = 0; d < D; ++d) {
           float s = i == 0 ? g[d] : 0.f;
           for (int j = 0; j < F; ++j) s += S[(size_t)i * F + j] * z[j][(int64_t)m * D + d];
-          o[d] = s;
+          o[d] = i == 0 ? act_b(act0, z[0][(int64_t)m * D + d], s) : s;
         }
       }
     }
@@ -855,6 +855,17 @@ void Model::compile(int loss_type, float lr, double bucket_mb) {
       hi.fuse_below = true;
       hi.below = lo_i;
       lo.grad_is_dpre = true;
+    }
+  }
+  // the dot interaction's backward applies the bottom layer's activation derivative to the gradient it
+  // writes (flexmi/runtime/executor.py _build_interaction_act_fusion): that layer reads it as dpre
+  for (Dot& d : dots_) {
+    const int li = dense_of[d.in[0]];
+    if (li < 0) continue;
+    Dense& L = ops_[li];
+    if (L.holders.empty() && L.act != ACT_NONE && L.N > 1 && !L.grad_is_dpre && !L.skip_act_grad) {
+      d.act0 = L.act;
+      L.grad_is_dpre = true;
     }
   }
   // table-wise placement: unplaced tables go to the rank with the fewest rows (largest first)
@@ -1473,7 +1484,7 @@ StepStat Model::train_step(const float* x, const int64_t* const* sparse, const v
         z.push_back(act_[t]);
         dz.push_back(grad_[t]);
       }
-      eng_->dot_bwd(z.data(), (int)z.size(), grad_[d.y], dz.data(), Bl_, d.D, d.W);
+      eng_->dot_bwd(z.data(), (int)z.size(), grad_[d.y], dz.data(), Bl_, d.D, d.W, d.act0);
       if (side && !emb_bwd_done) {
         eng_->side_begin();
         emb_backward();
@@ -1574,7 +1585,8 @@ std::string Model::describe() const {
         << "x" << pl.P << "x" << pl.Q << " window " << pl.kh << "x" << pl.kw << " stride " << pl.sh << "x" << pl.sw << "\n";
     } else {
       const Dot& d = dots_[n.idx];
-      o << "  dot interaction: " << d.in.size() << " features x " << d.D << " -> " << d.W << "\n";
+      o << "  dot interaction: " << d.in.size() << " features x " << d.D << " -> " << d.W
+        << (d.act0 != ACT_NONE ? " [backward applies the bottom layer's act']" : "") << "\n";
     }
   }
   if (!embs_.empty() && world_ > 1) {

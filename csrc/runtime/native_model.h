@@ -119,6 +119,7 @@ struct Emb {
 struct Dot {
   std::vector<int> in;         // tensor ids: bottom output first, then the embeddings
   int y = -1, D = 0, W = 0, npairs = 0;
+  int act0 = ACT_NONE;         // the bottom layer's activation, applied by the dot backward to its gradient
 };
 
 // 2-D convolution (the reference's Conv2D, src/ops/conv_2d.cu): x [B][C][H][W] (NCHW, a sample's
@@ -384,7 +385,8 @@ class Engine {
   virtual void add(float* dst, const float* src, int64_t n) = 0;   // dst += src (device)
   // y[M][W] = [z0 | lower(Z Z^T) | 0] ; dz[i] = (S Z)_i (+ dy[:, :D] for i = 0), S = dG + dG^T
   virtual void dot_fwd(const float* const* z, int F, float* y, int M, int D, int W) = 0;
-  virtual void dot_bwd(const float* const* z, int F, const float* dy, float* const* dz, int M, int D, int W) = 0;
+  // act0 != ACT_NONE: dz[0] leaves as act0'(z[0]) * dz[0] (the bottom layer's pre-activation gradient)
+  virtual void dot_bwd(const float* const* z, int F, const float* dy, float* const* dz, int M, int D, int W, int act0) = 0;
   // per-peer float counts; send / recv contiguous by peer
   virtual void all_to_all(const float* send, const int64_t* send_counts, float* recv, const int64_t* recv_counts) = 0;
   // ---- convolution / pooling (CNN plans), NCHW fp32 ----
