@@ -231,6 +231,11 @@ class HipEngine : public Engine {
     hipStreamDestroy(comm_st_);
     hipStreamDestroy(side_st_);
     if (pinned_) hipHostFree(pinned_);
+    for (auto& kv : claim_) {
+      hipFree(kv.second.owner);
+      hipFree(kv.second.dups);
+      hipFree(kv.second.ndup);
+    }
     hipStreamDestroy(st_);
   }
 
@@ -391,12 +396,34 @@ class HipEngine : public Engine {
     fm_embedding_fwd_multi(a.n, a.Wc.data(), a.ix.data(), a.i64.data(), a.o.data(), a.ld.data(), a.l0.data(), a.r.data(),
                            a.D.data(), a.bag.data(), a.sc.data(), 0, B, st_);
   }
+  // the executor's owner-computes sparse SGD for mostly-unique tables (rows > 0.2 x lookups per step,
+  // flexmi.ops.embedding CLAIM_RATIO): a per-row claim slot (-1 = free, restored by the owner kernel),
+  // the duplicate list and its counter per table, allocated on the table's first update; the other
+  // tables keep the atomic / LDS kernels
   void emb_sgd_multi(const std::vector<EmbJob>& jobs, int64_t B, float lr) override {
     set_lr(lr);
     EmbArrays a(jobs);
     std::vector<const void*> dy(a.o.begin(), a.o.end());
+    std::vector<int*> owner(a.n, nullptr), dups(a.n, nullptr), ndup(a.n, nullptr);
+    for (int i = 0; i < a.n; ++i) {
+      const EmbJob& j = jobs[i];
+      const int64_t lookups = B * j.bag;
+      if ((double)j.rows <= 0.2 * (double)lookups || j.D % 4 != 0) continue;
+      ClaimBufs& c = claim_[j.W];
+      if (!c.owner) {
+        HIPX(hipMalloc(&c.owner, (size_t)j.rows * sizeof(int)));
+        HIPX(hipMemsetAsync(c.owner, 0xff, (size_t)j.rows * sizeof(int), st_));   // -1: free
+        HIPX(hipMalloc(&c.dups, (size_t)std::max<int64_t>(lookups, 1) * sizeof(int)));
+        HIPX(hipMalloc(&c.ndup, sizeof(int)));
+        HIPX(hipMemsetAsync(c.ndup, 0, sizeof(int), st_));
+        HIPX(hipStreamSynchronize(st_));
+      }
+      owner[i] = c.owner;
+      dups[i] = c.dups;
+      ndup[i] = c.ndup;
+    }
     fm_embedding_bwd_multi(a.n, a.W.data(), a.ix.data(), a.i64.data(), dy.data(), a.ld.data(), a.l0.data(), a.r.data(),
-                           a.D.data(), a.bag.data(), a.sc.data(), 0, lr_, B, nullptr, nullptr, nullptr, st_);
+                           a.D.data(), a.bag.data(), a.sc.data(), 0, lr_, B, owner.data(), dups.data(), ndup.data(), st_);
   }
   void* pinned(size_t bytes) override {
     if (bytes > pinned_n_) {
@@ -562,6 +589,10 @@ class HipEngine : public Engine {
   bool side_pending_ = false;
   void* pinned_ = nullptr;
   size_t pinned_n_ = 0;
+  struct ClaimBufs {
+    int *owner = nullptr, *dups = nullptr, *ndup = nullptr;
+  };
+  std::unordered_map<const float*, ClaimBufs> claim_;   // table -> owner-computes buffers
   ncclComm_t comm_ = nullptr;
   float* ws_ = nullptr;
   float* slots_ = nullptr;
