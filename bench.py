@@ -305,8 +305,9 @@ def native_run(a, t_start, timeout_s=300.0):
     if left < timeout_s + 30:
         return {"skipped": f"wall budget: {left:.0f} s left of --budget-s {a.budget_s:.0f}"}
     _release_memory()
+    tmp = tempfile.mkdtemp(prefix="flexmi_native_")
     try:
-        exe = os.path.join(tempfile.mkdtemp(prefix="flexmi_native_"), "dlrm_native_bench")
+        exe = os.path.join(tmp, "dlrm_native_bench")
         subprocess.run(["gcc", "-O2", src, "-I" + os.path.join(root, "csrc", "capi"), "-L" + lib_dir,
                         "-Wl,-rpath," + lib_dir, "-lflexmi_native_c", "-o", exe], check=True, capture_output=True,
                        timeout=120)
@@ -319,6 +320,8 @@ def native_run(a, t_start, timeout_s=300.0):
                 "loss": out["loss"], "program": "apps/c/dlrm_native_bench.c"}
     except Exception as e:   # noqa: BLE001 -- reported in the record
         return {"error": f"{type(e).__name__}: {e}"[:300]}
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def _release_memory():
